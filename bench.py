@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""Headline benchmark: KawPow MH/s (+ Equihash(200,9) Sol/s), whole node, N MI355X.
+
+BASELINE.json config 2/4: KawPow miner on a synthetic regtest header with a
+4 GiB DAG (epoch 384), nonce-range data parallelism over N GPUs (one process
+per GPU, RCCL over xGMI): the work packet (header hash, target, height) is
+broadcast from rank 0, every rank searches its own disjoint nonce window per
+step, and the per-rank share rings are all-gathered on the GPU stream after
+every search kernel — the full mining step, nothing skipped.
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+
+One step = one search window of --batch nonces per GPU (weak scaling).
+Timing: W untimed steps, barrier + synchronize, K timed steps, synchronize +
+barrier, max elapsed over ranks. Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import struct
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_MHS = None  # filled from BASELINE.json "published" if present
+
+
+def _baseline() -> float | None:
+    try:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            pub = json.load(f).get("published") or {}
+        v = pub.get("kawpow_mhs")
+        return float(v) if v else None
+    except (OSError, ValueError):
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--epoch", type=int, default=384, help="384 -> 4 GiB DAG (BASELINE config)")
+    ap.add_argument("--batch", type=int, default=1 << 23, help="nonces per GPU per step")
+    ap.add_argument("--equihash", type=int, default=0, help="also time N Equihash(200,9) solves")
+    ap.add_argument("--quiet", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    from nodexa_chain_core_amd import _build
+
+    _build.build_all()
+    from nodexa_chain_core_amd import _core
+    from nodexa_chain_core_amd.chain.header import BlockHeader
+    from nodexa_chain_core_amd.ops import jit
+    from nodexa_chain_core_amd.ops.ethash import DeviceEpoch
+    from nodexa_chain_core_amd.ops.kawpow import KawpowSearcher
+    from nodexa_chain_core_amd.parallel import dag as pdag
+    from nodexa_chain_core_amd.parallel import world as W
+    from nodexa_chain_core_amd.parallel.shares import ShareGather
+
+    world = W.init(use_gpu=True)
+    rank, ws = world.rank, world.world_size
+    log = (lambda *a: print(*a, file=sys.stderr, flush=True)) if (rank == 0 and not args.quiet) else (lambda *a: None)
+
+    height = args.epoch * _core.EPOCH_LENGTH + 123
+    period = height // 3
+    # Compile the period kernel before touching the DAG (child-process compile).
+    jit.get(period) if rank == 0 else None
+    W.barrier()
+
+    # Synthetic regtest header (KawPow layout; time after activation).
+    hdr = BlockHeader(version=0x20000000, prev=_core.sha256d(b"nodexa-bench-prev"),
+                      merkle_root=_core.sha256d(b"nodexa-bench-merkle"), time=1_700_000_000,
+                      bits=0x1b00ffff, height=height)
+    work = struct.pack("<32sQII", hdr.progpow_header_hash(), 0, height, 0)
+    work = W.broadcast_bytes(work if rank == 0 else None, len(work))
+    header_hash, _, height, _ = struct.unpack("<32sQII", work)
+    # Target: ~1 share per 2^22 nonces, so the share path is exercised every step.
+    target64 = (1 << 64) // (1 << 22)
+
+    t0 = time.time()
+    ctx = _core.get_epoch_context(args.epoch)
+    log(f"[bench] light cache epoch {args.epoch}: {ctx.light_bytes/2**20:.0f} MiB in {time.time()-t0:.1f}s")
+    ep = DeviceEpoch(args.epoch, ctx=ctx, world_size=ws)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    pdag.build_dag(ep)
+    torch.cuda.synchronize()
+    dag_s = time.time() - t0
+    log(f"[bench] DAG {ep.dag_bytes/2**30:.2f} GiB built in {dag_s:.2f}s over {ws} GPU(s)")
+    if not ep.l1_matches():
+        raise SystemExit("DAG L1 mismatch vs host golden model")
+
+    searcher = KawpowSearcher(ep, height)
+    gather = ShareGather(searcher)
+    nonce_base = 0x5EED_0000_0000_0000
+    batch = args.batch
+
+    def step(i: int) -> None:
+        start = nonce_base + (i * ws + rank) * batch
+        searcher.launch(header_hash, start, batch, target64)
+        gather.enqueue()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    W.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    W.barrier()
+    elapsed = time.perf_counter() - t_start
+    elapsed = W.all_reduce_max(elapsed)
+
+    # Validate the last step's gathered shares bit-exactly on the host.
+    shares = gather.collect()
+    bad = [s for s in shares if not s.verify_host(height, header_hash)]
+    if bad:
+        raise SystemExit(f"{len(bad)} invalid shares from the GPU")
+    total = batch * ws * args.steps
+    mhs = total / elapsed / 1e6
+
+    eq_sols = None
+    if args.equihash:
+        from nodexa_chain_core_amd.models import equihash as eqm
+
+        eq_sols = eqm.bench_device(args.equihash)
+
+    if rank == 0:
+        base = _baseline()
+        out = {
+            "metric": "KawPow MH/s + Equihash(200,9) Sol/s, whole node at 1/2/4/8 MI355X",
+            "value": round(mhs, 3),
+            "unit": "MH/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(mhs / base, 3) if base else None,
+            "dtype": "u32",
+            "data": "synthetic regtest header, random-init epoch DAG (no chain data)",
+            "config": {
+                "model": f"KawPow (ProgPoW 0.9.4, RAVENCOINKAWPOW) epoch {args.epoch}, "
+                         f"{ep.dag_bytes/2**30:.2f} GiB DAG, height {height}",
+                "global_batch": batch * ws,
+                "seq_len": None,
+                "parallelism": f"dp{ws}",
+            },
+            "shares_last_step": len(shares),
+            "dag_build_s": round(dag_s, 3),
+            "equihash_sol_per_s": eq_sols,
+        }
+        print(json.dumps(out), flush=True)
+    W.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,175 @@
+"""In-tree native build for nodexa_chain_core_amd.
+
+Produces (all inside the package directory, so they travel with a gpurun
+snapshot and are what the GPU tests load):
+
+  _core.<abi>.so      CPU consensus/PoW core (g++, pybind11)           csrc/**
+  _hip.<abi>.so       HIP host runtime (g++ against torch's libamdhip64) hip/runtime/**
+  kernels/*.hsaco     gfx950 code objects for the static kernels      hip/kernels/*.hip
+  bin/nodexad         native daemon (JSON-RPC server + miner)          csrc/** + tools
+
+The HIP runtime links the *same* libamdhip64.so that torch ships (no SONAME,
+resolved through an rpath into torch/lib): one HIP runtime per process, so
+device pointers from torch tensors, torch streams and RCCL communicators are
+valid in our kernels. Device code is never linked into the host .so; every
+kernel is a code object loaded with hipModuleLoadData, which also serves the
+per-period KawPow kernels that are generated at run time (see ops/jit.py).
+
+Usage: python -m nodexa_chain_core_amd._build [--force] [--jobs N] [core|hip|kernels|bin]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+HIPDIR = os.path.join(PKG, "hip")
+BUILD = os.path.join(PKG, "..", "build", "obj")
+ARCH = os.environ.get("NODEXA_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-march=x86-64-v3",
+            "-fvisibility=hidden"]
+
+
+def _pybind_includes() -> list[str]:
+    import pybind11
+
+    return ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
+
+
+def _torch_lib() -> str:
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        raise RuntimeError("torch (ROCm build) is required to link the HIP runtime")
+    return os.path.join(list(spec.submodule_search_locations)[0], "lib")
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _headers(root: str) -> list[str]:
+    return glob.glob(os.path.join(root, "**", "*.h*"), recursive=True)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+
+
+def _compile_all(srcs: list[str], flags: list[str], objdir: str, jobs: int, force: bool,
+                 compiler: str = "g++") -> list[str]:
+    os.makedirs(objdir, exist_ok=True)
+    hdrs = _headers(CSRC) + _headers(HIPDIR)
+    todo, objs = [], []
+    for s in srcs:
+        rel = os.path.relpath(s, PKG).replace(os.sep, "_")
+        o = os.path.join(objdir, rel + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            todo.append((s, o))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = [ex.submit(_run, [compiler, *flags, "-c", s, "-o", o]) for s, o in todo]
+        for f in futs:
+            f.result()
+    return objs
+
+
+def core_sources() -> list[str]:
+    srcs = glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)
+    return sorted(s for s in srcs if os.sep + "daemon" + os.sep not in s)
+
+
+def build_core(force: bool = False, jobs: int = 8) -> str:
+    out = os.path.join(PKG, "_core" + EXT)
+    objs = _compile_all(core_sources(), CXXFLAGS + _pybind_includes(), os.path.join(BUILD, "core"), jobs, force)
+    if force or _newer(out, objs):
+        _run(["g++", "-shared", "-o", out, *objs, "-pthread"])
+    return out
+
+
+def build_hip_runtime(force: bool = False, jobs: int = 8) -> str:
+    out = os.path.join(PKG, "_hip" + EXT)
+    tlib = _torch_lib()
+    srcs = sorted(glob.glob(os.path.join(HIPDIR, "runtime", "*.cpp")))
+    # The runtime takes host data (light cache, generated program) from _core by
+    # pointer/bytes, so it links no core objects: one epoch-context cache per process.
+    flags = CXXFLAGS + _pybind_includes() + ["-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include")]
+    objs = _compile_all(srcs, flags, os.path.join(BUILD, "hip"), jobs, force)
+    if force or _newer(out, objs):
+        _run(["g++", "-shared", "-o", out, *objs, "-L" + tlib, "-lamdhip64",
+              "-Wl,-rpath," + tlib, "-pthread"])
+    return out
+
+
+def hipcc_genco(src: str, out: str, defines: list[str] | None = None, includes: list[str] | None = None) -> None:
+    cmd = [os.path.join(ROCM, "bin", "hipcc"), "--genco", "--offload-arch=" + ARCH, "-O3", "-std=c++17",
+           "-mcode-object-version=5", "-ffp-contract=fast", "-I" + os.path.join(HIPDIR, "kernels")]
+    for d in defines or []:
+        cmd.append("-D" + d)
+    for i in includes or []:
+        cmd.append("-I" + i)
+    _run(cmd + [src, "-o", out])
+
+
+def build_kernels(force: bool = False, jobs: int = 8) -> list[str]:
+    """Static gfx950 code objects (every .hip that is not a per-period template)."""
+    kdir = os.path.join(PKG, "kernels")
+    os.makedirs(kdir, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(HIPDIR, "kernels", "*.hip")))
+    hdrs = _headers(os.path.join(HIPDIR, "kernels"))
+    outs, todo = [], []
+    for s in srcs:
+        name = os.path.splitext(os.path.basename(s))[0]
+        if name.startswith("kawpow_search"):
+            continue  # per-period template, compiled by ops/jit.py
+        o = os.path.join(kdir, name + ".hsaco")
+        outs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            todo.append((s, o))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for f in [ex.submit(hipcc_genco, s, o) for s, o in todo]:
+            f.result()
+    return outs
+
+
+def build_all(force: bool = False, jobs: int = 8, with_hip: bool = True) -> None:
+    build_core(force, jobs)
+    if with_hip:
+        build_hip_runtime(force, jobs)
+        build_kernels(force, jobs)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("what", nargs="*", default=["all"])
+    a = ap.parse_args()
+    for w in a.what:
+        if w in ("all", "core"):
+            print(build_core(a.force, a.jobs))
+        if w in ("all", "hip"):
+            print(build_hip_runtime(a.force, a.jobs))
+        if w in ("all", "kernels"):
+            for k in build_kernels(a.force, a.jobs):
+                print(k)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

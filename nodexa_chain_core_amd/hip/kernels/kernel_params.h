@@ -1,0 +1,65 @@
+// Kernel parameter blocks shared by the gfx950 kernels (device side) and the
+// HIP host runtime (hip/runtime/*.cpp). Every kernel takes exactly one of these
+// structs by value; the host passes it through hipModuleLaunchKernel's
+// HIP_LAUNCH_PARAM_BUFFER_POINTER, so the layout here is the ABI.
+#pragma once
+#include <stdint.h>
+
+#define NODEXA_KAWPOW_MAX_SHARES 64
+#define NODEXA_KAWPOW_BLOCK 256
+
+// Fast u32 modulo by a runtime constant d (round-up multiply-shift, valid for
+// every 32-bit numerator): q = (mulhi(x, m) + ((x - mulhi(x, m)) >> 1)) >> (s - 1).
+struct FastMod32 {
+    uint32_t d;
+    uint32_t m;
+    uint32_t s;  // ceil(log2 d), >= 1
+    uint32_t pad;
+};
+
+struct EthashDagParams {
+    const void* light;     // light cache, light_items x 64 B
+    void* dag;             // output, 512-bit items
+    uint64_t first_item;   // first 512-bit item to compute
+    uint64_t num_items;    // number of 512-bit items in this launch
+    uint32_t light_items;  // light cache items (prime)
+    uint32_t pad;
+};
+
+struct KawpowShare {
+    uint64_t nonce;
+    uint32_t mix[8];    // mix digest words (storage order)
+    uint32_t final_[8]; // final hash words (storage order)
+};
+
+struct KawpowResults {
+    uint32_t count;     // number of shares appended (may exceed MAX; extra dropped)
+    uint32_t pad[3];
+    struct KawpowShare shares[NODEXA_KAWPOW_MAX_SHARES];
+};
+
+struct KawpowSearchParams {
+    const void* dag;           // 2048-bit items (16 x uint4 each)
+    struct KawpowResults* results;
+    uint64_t start_nonce;
+    uint64_t target;           // share if bswap64(final[0..1]) <= target (upper 64 bits, BE)
+    uint32_t header[8];        // header hash words (storage order)
+    struct FastMod32 items;    // modulo by number of 2048-bit items (full_items / 2)
+};
+
+// Light-mode / full-DAG batch verification of (header, nonce) pairs.
+struct KawpowVerifyJob {
+    uint32_t header[8];
+    uint64_t nonce;
+    uint32_t block_number;
+    uint32_t pad;
+};
+
+struct KawpowHashParams {
+    const void* dag;                  // full DAG (2048-bit items)
+    const struct KawpowVerifyJob* jobs;
+    uint32_t* out;                    // per job: mix[8] then final[8]
+    uint32_t num_jobs;
+    uint32_t pad;
+    struct FastMod32 items;
+};

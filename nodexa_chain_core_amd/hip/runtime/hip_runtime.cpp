@@ -1,0 +1,230 @@
+// HIP host runtime for the gfx950 kernels (pybind11 module `_hip`).
+//
+// * Code objects (static .hsaco from _build.py, or per-period KawPow objects
+//   from ops/jit.py) are loaded with hipModuleLoadData and launched with
+//   hipModuleLaunchKernel; each kernel takes one parameter struct from
+//   hip/kernels/kernel_params.h, so host and device share the ABI header.
+// * Device memory and streams belong to torch (its caching allocator, its
+//   streams, its RCCL communicators): every entry point takes raw device
+//   pointers and a hipStream_t as integers. This module links the very same
+//   libamdhip64.so torch loaded, so those handles are valid here.
+// * Launches never synchronise and never allocate, so callers may capture
+//   them into hipGraphs.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
+#include "../kernels/kernel_params.h"
+
+namespace py = pybind11;
+
+namespace {
+
+void check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+FastMod32 make_fastmod(uint32_t d) {
+    if (d < 2) throw std::invalid_argument("fastmod divisor must be >= 2");
+    uint32_t s = 0;
+    while ((uint64_t(1) << s) < d) ++s;  // s = ceil(log2 d)
+    const uint64_t m = ((uint64_t(1) << 32) * ((uint64_t(1) << s) - d)) / d + 1;
+    FastMod32 f{};
+    f.d = d;
+    f.m = uint32_t(m);
+    f.s = s;
+    return f;
+}
+
+struct Kernel {
+    hipFunction_t fn = nullptr;
+    std::string name;
+    int device = -1;
+
+    void launch_bytes(dim3 grid, dim3 block, unsigned shmem, hipStream_t stream, const void* params,
+                      size_t size) const {
+        int cur = -1;
+        check(hipGetDevice(&cur), "hipGetDevice");
+        if (cur != device)
+            throw std::runtime_error("kernel " + name + " belongs to device " + std::to_string(device) +
+                                     " but current device is " + std::to_string(cur));
+        void* config[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, const_cast<void*>(params), HIP_LAUNCH_PARAM_BUFFER_SIZE,
+                          &size, HIP_LAUNCH_PARAM_END};
+        check(hipModuleLaunchKernel(fn, grid.x, grid.y, grid.z, block.x, block.y, block.z, shmem, stream, nullptr,
+                                    config),
+              ("hipModuleLaunchKernel(" + name + ")").c_str());
+    }
+};
+
+struct CodeObject {
+    hipModule_t mod = nullptr;
+    int device = -1;
+    std::string image;  // kept alive for the module's lifetime
+    std::mutex mu;
+    std::unordered_map<std::string, std::shared_ptr<Kernel>> fns;
+
+    explicit CodeObject(std::string img) : image(std::move(img)) {
+        check(hipGetDevice(&device), "hipGetDevice");
+        check(hipModuleLoadData(&mod, image.data()), "hipModuleLoadData");
+    }
+    ~CodeObject() {
+        if (mod) (void)hipModuleUnload(mod);
+    }
+    std::shared_ptr<Kernel> function(const std::string& name) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = fns.find(name);
+        if (it != fns.end()) return it->second;
+        auto k = std::make_shared<Kernel>();
+        check(hipModuleGetFunction(&k->fn, mod, name.c_str()), ("hipModuleGetFunction(" + name + ")").c_str());
+        k->name = name;
+        k->device = device;
+        fns[name] = k;
+        return k;
+    }
+};
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Two 32-byte hashes as 8 LE words.
+void load_words(const std::string& b, uint32_t out[8]) {
+    if (b.size() != 32) throw std::invalid_argument("expected 32-byte header hash");
+    std::memcpy(out, b.data(), 32);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+    m.doc() = "nodexa HIP host runtime: gfx950 code-object loading and typed kernel launchers";
+
+    m.def("device_count", [] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+        return n;
+    });
+    m.def("set_device", [](int d) { check(hipSetDevice(d), "hipSetDevice"); });
+    m.def("get_device", [] {
+        int d = -1;
+        check(hipGetDevice(&d), "hipGetDevice");
+        return d;
+    });
+    m.def("synchronize", [] { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); },
+          py::call_guard<py::gil_scoped_release>());
+    m.def("stream_synchronize", [](uintptr_t s) { check(hipStreamSynchronize(as_stream(s)), "hipStreamSynchronize"); },
+          py::call_guard<py::gil_scoped_release>());
+    m.def("device_name", [](int d) {
+        hipDeviceProp_t p;
+        check(hipGetDeviceProperties(&p, d), "hipGetDeviceProperties");
+        return std::string(p.gcnArchName);
+    });
+    m.def("device_props", [](int d) {
+        hipDeviceProp_t p;
+        check(hipGetDeviceProperties(&p, d), "hipGetDeviceProperties");
+        py::dict r;
+        r["name"] = std::string(p.name);
+        r["arch"] = std::string(p.gcnArchName);
+        r["cus"] = p.multiProcessorCount;
+        r["total_mem"] = p.totalGlobalMem;
+        r["l2_bytes"] = p.l2CacheSize;
+        r["lds_per_block"] = p.sharedMemPerBlock;
+        r["clock_khz"] = p.clockRate;
+        r["mem_clock_khz"] = p.memoryClockRate;
+        r["mem_bus_width"] = p.memoryBusWidth;
+        return r;
+    });
+    m.def("memcpy_htod", [](uintptr_t dst, uintptr_t src, size_t n) {
+        check(hipMemcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyHostToDevice),
+              "hipMemcpy(HtoD)");
+    }, py::call_guard<py::gil_scoped_release>());
+    m.def("memcpy_dtoh", [](uintptr_t dst, uintptr_t src, size_t n) {
+        check(hipMemcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyDeviceToHost),
+              "hipMemcpy(DtoH)");
+    }, py::call_guard<py::gil_scoped_release>());
+    m.def("fastmod32", [](uint32_t d) {
+        FastMod32 f = make_fastmod(d);
+        return py::make_tuple(f.d, f.m, f.s);
+    });
+    m.def("fastmod32_eval", [](uint32_t x, uint32_t d) {
+        FastMod32 f = make_fastmod(d);
+        const uint32_t t = uint32_t((uint64_t(x) * f.m) >> 32);
+        const uint32_t q = (t + ((x - t) >> 1)) >> (f.s - 1);
+        return x - q * f.d;
+    }, "host model of the device FastMod32 (tests compare it with x % d)");
+    m.def("sizeof_results", [] { return sizeof(KawpowResults); });
+    m.def("sizeof_share", [] { return sizeof(KawpowShare); });
+    m.attr("KAWPOW_MAX_SHARES") = NODEXA_KAWPOW_MAX_SHARES;
+    m.attr("KAWPOW_BLOCK") = NODEXA_KAWPOW_BLOCK;
+
+    py::class_<Kernel, std::shared_ptr<Kernel>>(m, "Kernel")
+        .def_readonly("name", &Kernel::name)
+        .def_readonly("device", &Kernel::device)
+        .def("launch", [](const Kernel& k, std::tuple<unsigned, unsigned, unsigned> g,
+                          std::tuple<unsigned, unsigned, unsigned> b, unsigned shmem, uintptr_t stream,
+                          const py::bytes& params) {
+            std::string p = params;
+            k.launch_bytes(dim3(std::get<0>(g), std::get<1>(g), std::get<2>(g)),
+                           dim3(std::get<0>(b), std::get<1>(b), std::get<2>(b)), shmem, as_stream(stream),
+                           p.data(), p.size());
+        }, "generic launch with a packed parameter struct");
+
+    py::class_<CodeObject, std::shared_ptr<CodeObject>>(m, "CodeObject")
+        .def(py::init([](const py::bytes& img) { return std::make_shared<CodeObject>(std::string(img)); }))
+        .def_readonly("device", &CodeObject::device)
+        .def("function", &CodeObject::function);
+
+    // ---- typed launchers (layout from kernel_params.h) ----
+    m.def("launch_ethash_dag_build", [](const Kernel& k, uintptr_t light, uint32_t light_items, uintptr_t dag,
+                                        uint64_t first_item, uint64_t num_items, uintptr_t stream) {
+        struct {
+            EthashDagParams p;
+            FastMod32 lmod;
+        } args{};
+        args.p.light = reinterpret_cast<const void*>(light);
+        args.p.dag = reinterpret_cast<void*>(dag);
+        args.p.first_item = first_item;
+        args.p.num_items = num_items;
+        args.p.light_items = light_items;
+        args.lmod = make_fastmod(light_items);
+        const unsigned block = 256;
+        const uint64_t grid = (num_items + block - 1) / block;
+        if (grid == 0) return;
+        if (grid > 0x7fffffffULL) throw std::invalid_argument("dag build launch too large; split it");
+        k.launch_bytes(dim3(unsigned(grid)), dim3(block), 0, as_stream(stream), &args, sizeof(args));
+    });
+
+    m.def("launch_kawpow_search", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t results,
+                                     const py::bytes& header, uint64_t start_nonce, uint64_t target,
+                                     uint64_t num_nonces, uintptr_t stream) {
+        if (num_nonces % NODEXA_KAWPOW_BLOCK)
+            throw std::invalid_argument("num_nonces must be a multiple of the block size");
+        KawpowSearchParams p{};
+        p.dag = reinterpret_cast<const void*>(dag);
+        p.results = reinterpret_cast<KawpowResults*>(results);
+        p.start_nonce = start_nonce;
+        p.target = target;
+        load_words(header, p.header);
+        p.items = make_fastmod(dag_items2048);
+        const uint64_t grid = num_nonces / NODEXA_KAWPOW_BLOCK;
+        if (grid == 0 || grid > 0x7fffffffULL) throw std::invalid_argument("bad search grid");
+        k.launch_bytes(dim3(unsigned(grid)), dim3(NODEXA_KAWPOW_BLOCK), 0, as_stream(stream), &p, sizeof(p));
+    });
+
+    m.def("launch_kawpow_hash_batch", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t jobs,
+                                         uint32_t num_jobs, uintptr_t out, uintptr_t stream) {
+        KawpowHashParams p{};
+        p.dag = reinterpret_cast<const void*>(dag);
+        p.jobs = reinterpret_cast<const KawpowVerifyJob*>(jobs);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        p.num_jobs = num_jobs;
+        p.items = make_fastmod(dag_items2048);
+        const unsigned grid = (num_jobs + NODEXA_KAWPOW_BLOCK - 1) / NODEXA_KAWPOW_BLOCK;
+        if (grid == 0) return;
+        k.launch_bytes(dim3(grid), dim3(NODEXA_KAWPOW_BLOCK), 0, as_stream(stream), &p, sizeof(p));
+    });
+    m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
+}

@@ -1,0 +1,90 @@
+"""Ethash epoch state resident on one MI355X: light cache + full DAG.
+
+The light cache is built on the host (inherently serial keccak chain,
+SURVEY K5) by `_core` and uploaded once; the DAG is generated on the GPU by
+`ethash_dag_build` (hip/kernels/ethash_dag.hip) straight into a torch-owned
+buffer. A 4 GiB DAG is 1.4 % of one GPU's 288 GB HBM3E, so several epochs can
+stay resident (next-epoch prebuild, cross-epoch batch verification).
+
+For multi-GPU nodes `build(shard=(rank, world))` computes only this rank's
+contiguous slice in place; parallel/dag.py then all-gathers the slices over
+RCCL ("DAG sharding").
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _core
+from . import runtime
+
+# 512-bit items per launch: keeps a single dispatch well under a second even
+# at epoch 384 while still giving >> 256 CUs x 8 waves of work.
+_DAG_CHUNK = 1 << 22
+
+
+class DeviceEpoch:
+    def __init__(self, epoch: int, device: int | torch.device | None = None, ctx=None, world_size: int = 1):
+        runtime.require_gpu()
+        self.epoch = int(epoch)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   (device.index if isinstance(device, torch.device) else int(device)))
+        self.ctx = ctx if ctx is not None else _core.get_epoch_context(self.epoch)
+        self.full_items = int(self.ctx.full_items)          # 1024-bit items
+        self.items512 = 2 * self.full_items
+        self.items2048 = self.full_items // 2
+        self.dag_bytes = self.items512 * 64
+        with torch.cuda.device(self.device):
+            self.light = torch.empty(int(self.ctx.light_bytes), dtype=torch.uint8, device=self.device)
+            runtime.hip().memcpy_htod(self.light.data_ptr(), self.ctx.light_cache_ptr(), int(self.ctx.light_bytes))
+            # padded to a whole number of equal shards so RCCL can all-gather in place
+            self._storage = torch.empty(self.shard_bytes(world_size) * world_size, dtype=torch.uint8,
+                                        device=self.device)
+            self.dag = self._storage[:self.dag_bytes]
+        self.built = False
+
+    # ------------------------------------------------------------------
+    def shard_items(self, world: int) -> int:
+        return (self.items512 + world - 1) // world
+
+    def shard_bytes(self, world: int) -> int:
+        return self.shard_items(world) * 64
+
+    def dag_padded(self, world: int) -> torch.Tensor:
+        n = self.shard_bytes(world) * world
+        if n > self._storage.numel():
+            raise ValueError("DeviceEpoch was allocated for a smaller world size")
+        return self._storage[:n]
+
+    def shard_range(self, rank: int, world: int) -> tuple[int, int]:
+        """[first, first+count) 512-bit items owned by `rank` (equal contiguous slices)."""
+        per = self.shard_items(world)
+        first = min(rank * per, self.items512)
+        return first, min(per, self.items512 - first)
+
+    def build(self, shard: tuple[int, int] | None = None, stream: int | None = None) -> None:
+        h = runtime.hip()
+        with torch.cuda.device(self.device):
+            k = runtime.static_kernel("ethash_dag", "ethash_dag_build")
+            s = runtime.current_stream_handle() if stream is None else stream
+            first, count = (0, self.items512) if shard is None else self.shard_range(*shard)
+            end = first + count
+            pos = first
+            while pos < end:
+                n = min(_DAG_CHUNK, end - pos)
+                h.launch_ethash_dag_build(k, self.light.data_ptr(), int(self.ctx.light_items), self.dag.data_ptr(),
+                                          pos, n, s)
+                pos += n
+        if shard is None:
+            self.built = True
+
+    def mark_built(self) -> None:
+        self.built = True
+
+    def l1_matches(self) -> bool:
+        """The first 16 KiB of the device DAG equals the host-computed KawPow L1."""
+        dev = self.dag[:16384].cpu().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        ref = torch.tensor(self.ctx.l1, dtype=torch.int64)
+        return bool(torch.equal(dev, ref))
+
+    def item512(self, index: int) -> bytes:
+        return bytes(self.dag[index * 64:(index + 1) * 64].cpu().numpy().tobytes())

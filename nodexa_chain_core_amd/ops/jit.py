@@ -1,0 +1,91 @@
+"""Per-period KawPow kernel compilation (the hipRTC-style JIT of SURVEY §7.3).
+
+A ProgPoW period lasts 3 blocks. For each period the C++ generator
+(`_core.kawpow_codegen_hip`, csrc/pow/kawpow_codegen.cpp) emits the period's
+straight-line program; it is compiled together with
+hip/kernels/kawpow_search.hip into a gfx950 code object by the offline
+compiler (`hipcc --genco`, run as a child process — never exec'd in place of
+a GPU process). Objects are cached on disk keyed by (period, arch, template
+hash), so a restart or the next run of the same height reuses them, and
+`prefetch()` compiles the next period on a worker thread while the current one
+is mining.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import tempfile
+import threading
+
+from .. import _build, _core
+
+TEMPLATE = os.path.join(_build.HIPDIR, "kernels", "kawpow_search.hip")
+CACHE_DIR = os.environ.get("NODEXA_KERNEL_CACHE", os.path.join(_build.PKG, "..", ".kernel_cache"))
+_pool = cf.ThreadPoolExecutor(max_workers=2, thread_name_prefix="kawpow-jit")
+_lock = threading.Lock()
+_inflight: dict[int, cf.Future] = {}
+
+
+def _template_digest() -> str:
+    h = hashlib.sha256()
+    kdir = os.path.join(_build.HIPDIR, "kernels")
+    for name in ("kawpow_search.hip", "kernel_params.h", "keccak_device.hpp"):
+        with open(os.path.join(kdir, name), "rb") as f:
+            h.update(f.read())
+    h.update(_build.ARCH.encode())
+    return h.hexdigest()[:16]
+
+
+def object_path(period: int) -> str:
+    return os.path.join(os.path.abspath(CACHE_DIR), f"kawpow_p{period}_{_build.ARCH}_{_template_digest()}.hsaco")
+
+
+def program_source(period: int) -> str:
+    return _core.kawpow_codegen_hip(period)
+
+
+def compile_period(period: int) -> str:
+    """Compile (or reuse) the code object for `period`; returns its path."""
+    out = object_path(period)
+    if os.path.exists(out):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with tempfile.TemporaryDirectory(prefix="kawpow_jit_") as tmp:
+        inc = os.path.join(tmp, f"kawpow_program_p{period}.inc")
+        with open(inc, "w") as f:
+            f.write(program_source(period))
+        tmp_out = os.path.join(tmp, "k.hsaco")
+        _build.hipcc_genco(TEMPLATE, tmp_out, defines=[f'KAWPOW_PROGRAM_HEADER="{inc}"'])
+        _atomic_copy(tmp_out, out)
+    return out
+
+
+def _atomic_copy(src: str, dst: str) -> None:
+    tmp = dst + f".tmp{os.getpid()}"
+    with open(src, "rb") as a, open(tmp, "wb") as b:
+        b.write(a.read())
+    os.replace(tmp, dst)
+
+
+def prefetch(period: int) -> cf.Future:
+    """Start compiling `period` in the background (idempotent)."""
+    with _lock:
+        fut = _inflight.get(period)
+        if fut is None:
+            fut = _pool.submit(compile_period, period)
+            _inflight[period] = fut
+        return fut
+
+
+def get(period: int) -> str:
+    return prefetch(period).result()
+
+
+def hipcc_available() -> bool:
+    try:
+        subprocess.run([os.path.join(_build.ROCM, "bin", "hipcc"), "--version"], capture_output=True, check=True)
+        return True
+    except (OSError, subprocess.CalledProcessError):
+        return False

@@ -1,0 +1,33 @@
+"""Sharded DAG generation + RCCL all-gather (SURVEY §5 "DAG sharding").
+
+Every GPU needs the whole DAG (each hash does 64 random 256-byte gathers, far
+too fine-grained to serve over xGMI), but generating it is embarrassingly
+parallel: rank r computes the r-th contiguous 1/world slice in place, then
+one in-place `all_gather_into_tensor` replicates the slices. For a 4 GiB DAG
+on 8 GPUs each rank ships 512 MiB, which RCCL moves over the xGMI mesh in tens
+of milliseconds — small next to the generation it saves (8x less per GPU).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..ops.ethash import DeviceEpoch
+from . import world as W
+
+
+def build_dag(epoch_dev: DeviceEpoch) -> None:
+    w = W.get()
+    if not w.distributed:
+        epoch_dev.build()
+        return
+    epoch_dev.build(shard=(w.rank, w.world_size))
+    per = epoch_dev.shard_bytes(w.world_size)
+    full = epoch_dev.dag_padded(w.world_size)
+    mine = full[w.rank * per:(w.rank + 1) * per]
+    if w.backend == "nccl":
+        dist.all_gather_into_tensor(full, mine)
+    else:  # gloo has no in-place all_gather_into_tensor: go through a list
+        parts = list(full.view(w.world_size, per).unbind(0))
+        dist.all_gather(parts, mine.clone())
+    epoch_dev.mark_built()  # later kernels on this stream are ordered after the gather

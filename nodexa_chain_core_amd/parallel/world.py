@@ -1,0 +1,116 @@
+"""Process-group bring-up: one process per GPU, torch.distributed over RCCL.
+
+On ROCm the "nccl" backend *is* RCCL; on the 8 MI355X of a node its
+collectives run over the point-to-point xGMI mesh (7 links per GPU). CPU-only
+runs (tests, rehearsals) use "gloo" with the same code paths.
+
+Rendezvous always uses 127.0.0.1 (the container hostname may not resolve).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class World:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+_WORLD: World | None = None
+
+
+def init(use_gpu: bool | None = None, timeout_s: int = 600) -> World:
+    """Initialise from RANK/WORLD_SIZE/LOCAL_RANK (torchrun) or single-process."""
+    global _WORLD
+    if _WORLD is not None:
+        return _WORLD
+    rank = int(os.environ.get("RANK", "0"))
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+        device = torch.device("cuda", torch.cuda.current_device())
+    else:
+        device = torch.device("cpu")
+    backend = "none"
+    if world_size > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        backend = "nccl" if use_gpu else "gloo"
+        kw = {}
+        if use_gpu:
+            kw["device_id"] = device
+        dist.init_process_group(backend=backend, rank=rank, world_size=world_size,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    _WORLD = World(rank, world_size, local_rank, backend, device)
+    return _WORLD
+
+
+def get() -> World:
+    return _WORLD if _WORLD is not None else init()
+
+
+def shutdown() -> None:
+    global _WORLD
+    if _WORLD is not None and _WORLD.distributed and dist.is_initialized():
+        dist.destroy_process_group()
+    _WORLD = None
+
+
+def barrier() -> None:
+    w = get()
+    if w.distributed:
+        if w.backend == "nccl":
+            dist.barrier(device_ids=[w.device.index])
+        else:
+            dist.barrier()
+
+
+def broadcast_bytes(payload: bytes | None, size: int, src: int = 0) -> bytes:
+    """Broadcast a fixed-size packet (e.g. the 96-byte work packet) from `src`."""
+    w = get()
+    t = torch.zeros(size, dtype=torch.uint8, device=w.device)
+    if w.rank == src and payload is not None:
+        if len(payload) != size:
+            raise ValueError("payload size mismatch")
+        t.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
+    if w.distributed:
+        dist.broadcast(t, src=src)
+    return bytes(t.cpu().numpy().tobytes())
+
+
+def all_reduce_max(x: float) -> float:
+    w = get()
+    if not w.distributed:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=w.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_sum_int(x: int) -> int:
+    w = get()
+    if not w.distributed:
+        return x
+    t = torch.tensor([x], dtype=torch.int64, device=w.device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
