@@ -28,6 +28,25 @@
 #endif
 #include KAWPOW_PROGRAM_HEADER
 
+// Tuning knobs (compile-time; ops/jit.py passes them as -D variants):
+//   KP_MIN_WAVES  minimum waves per SIMD for __launch_bounds__ (caps VGPRs)
+//   KP_NT_DAG     non-temporal DAG loads (the 4 GiB DAG has no L2 reuse)
+#ifdef KP_MIN_WAVES
+#define KP_BOUNDS __launch_bounds__(NODEXA_KAWPOW_BLOCK, KP_MIN_WAVES)
+#else
+#define KP_BOUNDS __launch_bounds__(NODEXA_KAWPOW_BLOCK)
+#endif
+typedef uint32_t kp_u32x4 __attribute__((ext_vector_type(4)));
+NX_DEV uint4 kp_dag_load(const uint4* p) {
+#ifdef KP_NT_DAG
+    const kp_u32x4 v = __builtin_nontemporal_load((const kp_u32x4*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+#define KP_DAG_LOAD(p) kp_dag_load(p)
+
 #define KP_REGS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) \
     X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
 
@@ -112,7 +131,7 @@ NX_DEV uint32_t kp_hash_lane(const uint4* __restrict__ dag, const FastMod32& ite
     for (uint32_t r = 0; r < 64; ++r) {
         const uint32_t src = __shfl(m0, (int)(r & 15), 16);
         const uint32_t index = kp_fastmod(src, items);
-        const uint4 d = dag[(size_t)index * 16 + ((lane ^ r) & 15)];
+        const uint4 d = KP_DAG_LOAD(dag + (size_t)index * 16 + ((lane ^ r) & 15));
         KAWPOW_PROGRAM(l1);
         KAWPOW_DAG_MERGE(d);
     }
@@ -123,7 +142,7 @@ NX_DEV uint32_t kp_hash_lane(const uint4* __restrict__ dag, const FastMod32& ite
     return h;
 }
 
-extern "C" __global__ __launch_bounds__(NODEXA_KAWPOW_BLOCK) void kawpow_search(KawpowSearchParams p) {
+extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     __shared__ uint32_t l1[4096];
     {
         const uint4* src = (const uint4*)p.dag;
@@ -172,7 +191,7 @@ extern "C" __global__ __launch_bounds__(NODEXA_KAWPOW_BLOCK) void kawpow_search(
 
 // Batch hash (no target): for verification of (header, nonce, height) jobs that
 // all share this period and epoch. One job per thread, grouped as in search.
-extern "C" __global__ __launch_bounds__(NODEXA_KAWPOW_BLOCK) void kawpow_hash_batch(KawpowHashParams p) {
+extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     __shared__ uint32_t l1[4096];
     {
         const uint4* src = (const uint4*)p.dag;

