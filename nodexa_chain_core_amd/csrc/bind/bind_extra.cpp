@@ -1,3 +1,272 @@
+// Bindings for the consensus layer (chain/*), X16R and Equihash.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../chain/headerchain.hpp"
+#include "../chain/script.hpp"
+#include "../pow/equihash.hpp"
+#include "../pow/x16r.hpp"
+
 namespace py = pybind11;
-void bind_extra(py::module_& m) { (void)m; }
+using namespace nodexa;
+
+namespace {
+
+Uint256 u256(const py::bytes& b) {
+    std::string s = b;
+    if (s.size() != 32) throw std::invalid_argument("expected 32 bytes");
+    return Uint256::from_bytes(reinterpret_cast<const u8*>(s.data()));
+}
+py::bytes pyb(const Uint256& u) { return py::bytes(reinterpret_cast<const char*>(u.data), 32); }
+py::bytes pyb(const Bytes& b) { return py::bytes(reinterpret_cast<const char*>(b.data()), b.size()); }
+Bytes bytes_of(const py::bytes& b) { std::string s = b; return Bytes(s.begin(), s.end()); }
+
+py::int_ arith_to_int(const ArithU256& a) {
+    return py::int_(py::reinterpret_steal<py::object>(
+        PyLong_FromString(const_cast<char*>(a.hex().c_str()), nullptr, 16)));
+}
+ArithU256 int_to_arith(const py::int_& v) {
+    py::object mask = py::int_(1).attr("__lshift__")(256).attr("__sub__")(1);
+    py::int_ x = v.attr("__and__")(mask);
+    std::string hex = py::str(py::module_::import("builtins").attr("format")(x, "064x"));
+    return ArithU256::from_uint256(Uint256::from_hex(hex));
+}
+
+}  // namespace
+
+void bind_extra(py::module_& m) {
+    // ------------------------------------------------ uint256 / arith
+    m.def("u256_hex", [](const py::bytes& b) { return u256(b).hex(); }, "uint256::GetHex of storage bytes");
+    m.def("u256_from_hex", [](const std::string& s) { return pyb(Uint256::from_hex(s)); }, "uint256S");
+    m.def("set_compact", [](u32 c) {
+        bool neg = false, ovf = false;
+        ArithU256 a;
+        a.set_compact(c, &neg, &ovf);
+        return py::make_tuple(arith_to_int(a), neg, ovf);
+    });
+    m.def("get_compact", [](const py::int_& v, bool negative) { return int_to_arith(v).get_compact(negative); },
+          py::arg("value"), py::arg("negative") = false);
+    m.def("arith_div", [](const py::int_& a, const py::int_& b) { return arith_to_int(int_to_arith(a) / int_to_arith(b)); });
+    m.def("arith_mul", [](const py::int_& a, const py::int_& b) { return arith_to_int(int_to_arith(a) * int_to_arith(b)); });
+
+    // ------------------------------------------------ X16R
+    m.def("x16r", [](const py::bytes& data, const py::bytes& prev) {
+        std::string s = data;
+        Uint256 p = u256(prev), out;
+        x16r_hash(reinterpret_cast<const u8*>(s.data()), s.size(), p.data, false, out.data);
+        return pyb(out);
+    });
+    m.def("x16rv2", [](const py::bytes& data, const py::bytes& prev) {
+        std::string s = data;
+        Uint256 p = u256(prev), out;
+        x16r_hash(reinterpret_cast<const u8*>(s.data()), s.size(), p.data, true, out.data);
+        return pyb(out);
+    });
+    m.def("x16r_algo", [](int algo, const py::bytes& data) {
+        std::string s = data;
+        Hash512 h = x16r_single(algo, reinterpret_cast<const u8*>(s.data()), s.size());
+        return py::bytes(reinterpret_cast<const char*>(h.bytes), 64);
+    });
+    m.def("x16r_slot_available", &x16r_slot_available);
+    m.def("x16r_selection", [](const py::bytes& prev, int i) { return x16r_selection(u256(prev).data, i); });
+
+    // ------------------------------------------------ script / addresses
+    m.def("base58check_encode", [](const py::bytes& p) { return base58check_encode(bytes_of(p)); });
+    m.def("base58check_decode", [](const std::string& s) -> py::object {
+        Bytes out;
+        if (!base58check_decode(s, out)) return py::none();
+        return pyb(out);
+    });
+    m.def("address_to_script", [](const std::string& a, u8 pkh, u8 sh) -> py::object {
+        Bytes s;
+        if (!address_to_script(a, pkh, sh, s)) return py::none();
+        return pyb(s);
+    });
+    m.def("script_to_address", [](const py::bytes& s, u8 pkh, u8 sh) { return script_to_address(bytes_of(s), pkh, sh); });
+    m.def("script_push_int", [](int64_t v) { return pyb(ScriptBuilder().push_int(v).s); });
+    m.def("script_push_data", [](const py::bytes& d) { return pyb(ScriptBuilder().push_data(bytes_of(d)).s); });
+    m.def("scriptnum", [](int64_t v) { return pyb(ScriptBuilder::scriptnum(v)); });
+    m.def("ripemd160", [](const py::bytes& d) { Bytes b = bytes_of(d); u8 o[20]; ripemd160(b.data(), b.size(), o); return py::bytes((char*)o, 20); });
+    m.def("hash160", [](const py::bytes& d) { Bytes b = bytes_of(d); u8 o[20]; hash160(b.data(), b.size(), o); return py::bytes((char*)o, 20); });
+
+    // ------------------------------------------------ transactions / blocks
+    py::class_<OutPoint>(m, "OutPoint")
+        .def(py::init<>())
+        .def_property("hash", [](const OutPoint& o) { return pyb(o.hash); }, [](OutPoint& o, const py::bytes& b) { o.hash = u256(b); })
+        .def_readwrite("n", &OutPoint::n)
+        .def("is_null", &OutPoint::is_null);
+    py::class_<TxIn>(m, "TxIn")
+        .def(py::init<>())
+        .def_readwrite("prevout", &TxIn::prevout)
+        .def_property("script_sig", [](const TxIn& t) { return pyb(t.script_sig); }, [](TxIn& t, const py::bytes& b) { t.script_sig = bytes_of(b); })
+        .def_readwrite("sequence", &TxIn::sequence)
+        .def_property("witness", [](const TxIn& t) { py::list l; for (auto& w : t.witness) l.append(pyb(w)); return l; },
+                      [](TxIn& t, const std::vector<py::bytes>& w) { t.witness.clear(); for (auto& x : w) t.witness.push_back(bytes_of(x)); });
+    py::class_<TxOut>(m, "TxOut")
+        .def(py::init<>())
+        .def(py::init([](Amount v, const py::bytes& s) { TxOut o; o.value = v; o.script_pubkey = bytes_of(s); return o; }))
+        .def_readwrite("value", &TxOut::value)
+        .def_property("script_pubkey", [](const TxOut& t) { return pyb(t.script_pubkey); }, [](TxOut& t, const py::bytes& b) { t.script_pubkey = bytes_of(b); });
+    py::class_<Transaction>(m, "Transaction")
+        .def(py::init<>())
+        .def_readwrite("version", &Transaction::version)
+        .def_readwrite("vin", &Transaction::vin)
+        .def_readwrite("vout", &Transaction::vout)
+        .def_readwrite("lock_time", &Transaction::lock_time)
+        .def("serialize", [](const Transaction& t, bool w) { return pyb(t.bytes(w)); }, py::arg("with_witness") = true)
+        .def_static("deserialize", [](const py::bytes& b) {
+            Bytes d = bytes_of(b);
+            Reader r(d);
+            Transaction t = Transaction::deserialize(r);
+            if (!r.empty()) throw std::runtime_error("trailing bytes after transaction");
+            return t;
+        })
+        .def("txid", [](const Transaction& t) { return pyb(t.txid()); })
+        .def("wtxid", [](const Transaction& t) { return pyb(t.wtxid()); })
+        .def("is_coinbase", &Transaction::is_coinbase)
+        .def("has_witness", &Transaction::has_witness)
+        .def("value_out", &Transaction::value_out);
+    py::class_<BlockHeader>(m, "BlockHeader")
+        .def(py::init<>())
+        .def_readwrite("version", &BlockHeader::version)
+        .def_property("prev", [](const BlockHeader& h) { return pyb(h.prev); }, [](BlockHeader& h, const py::bytes& b) { h.prev = u256(b); })
+        .def_property("merkle_root", [](const BlockHeader& h) { return pyb(h.merkle_root); }, [](BlockHeader& h, const py::bytes& b) { h.merkle_root = u256(b); })
+        .def_readwrite("time", &BlockHeader::time)
+        .def_readwrite("bits", &BlockHeader::bits)
+        .def_readwrite("nonce", &BlockHeader::nonce)
+        .def_readwrite("height", &BlockHeader::height)
+        .def_readwrite("nonce64", &BlockHeader::nonce64)
+        .def_property("mix_hash", [](const BlockHeader& h) { return pyb(h.mix_hash); }, [](BlockHeader& h, const py::bytes& b) { h.mix_hash = u256(b); })
+        .def("serialize", [](const BlockHeader& h, u32 act) { return pyb(h.bytes(act)); })
+        .def_static("deserialize", [](const py::bytes& b, u32 act) { Bytes d = bytes_of(b); Reader r(d); return BlockHeader::deserialize(r, act); })
+        .def("kawpow_header_hash", [](const BlockHeader& h) { return pyb(h.kawpow_header_hash()); })
+        .def("legacy80", [](const BlockHeader& h) { return pyb(h.legacy80()); });
+    py::class_<Block>(m, "Block")
+        .def(py::init<>())
+        .def_readwrite("header", &Block::header)
+        .def_readwrite("vtx", &Block::vtx)
+        .def("serialize", [](const Block& b, u32 act, bool w) { return pyb(b.bytes(act, w)); }, py::arg("act"), py::arg("with_witness") = true)
+        .def_static("deserialize", [](const py::bytes& b, u32 act) {
+            Bytes d = bytes_of(b);
+            Reader r(d);
+            Block blk = Block::deserialize(r, act);
+            if (!r.empty()) throw std::runtime_error("trailing bytes after block");
+            return blk;
+        })
+        .def("merkle_root", [](const Block& b) { bool mut = false; Uint256 r = block_merkle_root(b, &mut); return py::make_tuple(pyb(r), mut); })
+        .def("witness_merkle_root", [](const Block& b) { return pyb(block_witness_merkle_root(b)); })
+        .def("witness_commitment_index", [](const Block& b) { return witness_commitment_index(b); })
+        .def("weight", &Block::weight)
+        .def("total_size", &Block::total_size)
+        .def("stripped_size", &Block::stripped_size);
+    m.def("compute_merkle_root", [](const std::vector<py::bytes>& leaves) {
+        std::vector<Uint256> l;
+        for (auto& x : leaves) l.push_back(u256(x));
+        bool mut = false;
+        Uint256 r = compute_merkle_root(l, &mut);
+        return py::make_tuple(pyb(r), mut);
+    });
+
+    // ------------------------------------------------ params / rules
+    py::class_<ChainParams>(m, "ChainParams")
+        .def_readonly("network_id", &ChainParams::network_id)
+        .def_property_readonly("message_start", [](const ChainParams& p) { return py::bytes((const char*)p.message_start, 4); })
+        .def_readonly("default_port", &ChainParams::default_port)
+        .def_readonly("default_rpc_port", &ChainParams::default_rpc_port)
+        .def_readonly("pubkey_prefix", &ChainParams::pubkey_prefix)
+        .def_readonly("script_prefix", &ChainParams::script_prefix)
+        .def_readwrite("genesis", &ChainParams::genesis)
+        .def_property_readonly("genesis_hash", [](const ChainParams& p) { return pyb(p.consensus.genesis_hash); })
+        .def_property_readonly("pow_limit", [](const ChainParams& p) { return pyb(p.consensus.pow_limit); })
+        .def_property_readonly("kawpow_limit", [](const ChainParams& p) { return pyb(p.consensus.kawpow_limit); })
+        .def_property_readonly("pow_target_spacing", [](const ChainParams& p) { return p.consensus.pow_target_spacing; })
+        .def_property_readonly("pow_allow_min_difficulty_blocks", [](const ChainParams& p) { return p.consensus.pow_allow_min_difficulty_blocks; })
+        .def_property_readonly("checkpoints", [](const ChainParams& p) { py::dict d; for (auto& kv : p.checkpoints) d[py::int_(kv.first)] = pyb(kv.second); return d; })
+        .def_readwrite("community_autonomous_pct", &ChainParams::community_autonomous_pct)
+        .def_readwrite("community_autonomous_address", &ChainParams::community_autonomous_address)
+        .def_readwrite("dgw_activation_block", &ChainParams::dgw_activation_block)
+        .def_readwrite("kawpow_activation_time", &ChainParams::kawpow_activation_time)
+        .def_readwrite("x16rv2_activation_time", &ChainParams::x16rv2_activation_time)
+        .def_readwrite("equihash_activation_time", &ChainParams::equihash_activation_time)
+        .def_readwrite("max_reorg_depth", &ChainParams::max_reorg_depth)
+        .def_readonly("mine_blocks_on_demand", &ChainParams::mine_blocks_on_demand)
+        .def_readonly("mining_requires_peers", &ChainParams::mining_requires_peers);
+    m.def("make_chain_params", &make_chain_params);
+    m.def("check_proof_of_work", [](const py::bytes& h, u32 bits, const ChainParams& p) { return check_proof_of_work(u256(h), bits, p); });
+    m.def("block_proof", [](u32 bits) { return arith_to_int(block_proof(bits)); });
+    m.def("block_subsidy", &block_subsidy);
+    m.def("difficulty_from_bits", &difficulty_from_bits);
+
+    py::class_<HeaderIndex>(m, "HeaderIndex")
+        .def_property_readonly("hash", [](const HeaderIndex& i) { return pyb(i.hash); })
+        .def_readonly("height", &HeaderIndex::height)
+        .def_readonly("time", &HeaderIndex::time)
+        .def_readonly("bits", &HeaderIndex::bits)
+        .def_readonly("header", &HeaderIndex::header)
+        .def_property_readonly("chain_work", [](const HeaderIndex& i) { return arith_to_int(i.chain_work); })
+        .def_property_readonly("prev_hash", [](const HeaderIndex& i) { return i.prev ? pyb(i.prev->hash) : pyb(Uint256()); })
+        .def("median_time_past", &HeaderIndex::median_time_past);
+
+    py::class_<AcceptResult>(m, "AcceptResult")
+        .def_readonly("ok", &AcceptResult::ok)
+        .def_readonly("duplicate", &AcceptResult::duplicate)
+        .def_readonly("reject", &AcceptResult::reject)
+        .def_readonly("dos", &AcceptResult::dos)
+        .def_property_readonly("index", [](const AcceptResult& r) { return r.index; }, py::return_value_policy::reference);
+
+    py::class_<HeaderChain, std::shared_ptr<HeaderChain>>(m, "HeaderChain")
+        .def(py::init([](const ChainParams& p) { return std::make_shared<HeaderChain>(p, std::make_shared<CpuPowVerifier>()); }))
+        .def_property_readonly("params", &HeaderChain::params, py::return_value_policy::reference_internal)
+        .def("set_kawpow_activation_time", [](HeaderChain& c, u32 t) { c.mutable_params().kawpow_activation_time = t; })
+        .def_readwrite("strict_kawpow_height", &HeaderChain::strict_kawpow_height)
+        .def("check_header", &HeaderChain::check_header, py::call_guard<py::gil_scoped_release>())
+        .def("accept_header", &HeaderChain::accept_header, py::arg("header"), py::arg("adjusted_time"), py::arg("check_pow") = true,
+             py::call_guard<py::gil_scoped_release>())
+        .def("accept_headers", &HeaderChain::accept_headers, py::arg("headers"), py::arg("adjusted_time"), py::arg("check_pow") = true,
+             py::call_guard<py::gil_scoped_release>())
+        .def("tip", &HeaderChain::tip, py::return_value_policy::reference_internal)
+        .def("genesis", &HeaderChain::genesis, py::return_value_policy::reference_internal)
+        .def("at_height", &HeaderChain::at_height, py::return_value_policy::reference_internal)
+        .def("find", [](const HeaderChain& c, const py::bytes& h) { return c.find(u256(h)); }, py::return_value_policy::reference_internal)
+        .def("in_active_chain", &HeaderChain::in_active_chain)
+        .def("height", &HeaderChain::height)
+        .def("size", &HeaderChain::size)
+        .def("next_bits", &HeaderChain::next_bits)
+        .def("invalidate", [](HeaderChain& c, const py::bytes& h) { c.invalidate(u256(h)); })
+        .def("reconsider", [](HeaderChain& c, const py::bytes& h) { c.reconsider(u256(h)); })
+        .def("block_hash", [](const HeaderChain& c, const BlockHeader& h) { return pyb(c.verifier().block_hash(h, c.params())); })
+        .def("block_hash_full", [](const HeaderChain& c, const BlockHeader& h) {
+            Uint256 mix;
+            Uint256 pow;
+            {
+                py::gil_scoped_release rel;
+                pow = c.verifier().block_hash_full(h, c.params(), mix);
+            }
+            return py::make_tuple(pyb(pow), pyb(mix));
+        })
+        .def("dgw", [](const HeaderChain& c, const BlockHeader& next) { return dark_gravity_wave(c.tip(), next, c.params()); });
+
+    py::class_<BlockStore::Pos>(m, "BlockPos")
+        .def(py::init<>())
+        .def_readwrite("file", &BlockStore::Pos::file)
+        .def_readwrite("offset", &BlockStore::Pos::offset)
+        .def_readwrite("size", &BlockStore::Pos::size)
+        .def(py::pickle([](const BlockStore::Pos& p) { return py::make_tuple(p.file, p.offset, p.size); },
+                        [](py::tuple t) { BlockStore::Pos p; p.file = t[0].cast<int>(); p.offset = t[1].cast<u32>(); p.size = t[2].cast<u32>(); return p; }));
+    py::class_<BlockStore, std::shared_ptr<BlockStore>>(m, "BlockStore")
+        .def(py::init([](const std::string& dir, const py::bytes& magic, u32 act) {
+            std::string mg = magic;
+            if (mg.size() != 4) throw std::invalid_argument("magic must be 4 bytes");
+            return std::make_shared<BlockStore>(dir, reinterpret_cast<const u8*>(mg.data()), act);
+        }))
+        .def("write", &BlockStore::write)
+        .def("write_raw", [](BlockStore& s, const py::bytes& b) { return s.write_raw(bytes_of(b)); })
+        .def("read_raw", [](const BlockStore& s, const BlockStore::Pos& p) { return pyb(s.read_raw(p)); })
+        .def("read", &BlockStore::read)
+        .def("scan", [](const BlockStore& s) { py::list l; for (auto& kv : s.scan()) l.append(py::make_tuple(kv.first, pyb(kv.second))); return l; })
+        .def("path", &BlockStore::path)
+        .def("current_file", &BlockStore::current_file);
+
+    // ------------------------------------------------ Equihash (CPU reference)
+    bind_equihash_cpu(m);
+}

@@ -1,0 +1,346 @@
+#include "headerchain.hpp"
+
+#include <cstdio>
+#include <sys/stat.h>
+
+#include "../pow/kawpow.hpp"
+#include "../pow/x16r.hpp"
+
+namespace nodexa {
+
+// ---------------------------------------------------------------- verifier
+Uint256 CpuPowVerifier::block_hash(const BlockHeader& h, const ChainParams& p) const {
+    switch (p.algo_for(h.time)) {
+        case PowAlgo::KAWPOW: {
+            const Hash256 fin = kawpow_hash_no_verify(int(h.height), h.kawpow_header_hash().to_progpow(),
+                                                      h.mix_hash.to_progpow(), h.nonce64);
+            return Uint256::from_progpow(fin);
+        }
+        case PowAlgo::X16RV2:
+        case PowAlgo::X16R: {
+            const Bytes d = h.legacy80();
+            Uint256 out;
+            x16r_hash(d.data(), d.size(), h.prev.data, p.algo_for(h.time) == PowAlgo::X16RV2, out.data);
+            return out;
+        }
+    }
+    return Uint256();
+}
+
+Uint256 CpuPowVerifier::block_hash_full(const BlockHeader& h, const ChainParams& p, Uint256& mix) const {
+    if (p.algo_for(h.time) != PowAlgo::KAWPOW) {
+        mix = Uint256();
+        return block_hash(h, p);
+    }
+    auto ctx = get_epoch_context(epoch_of_block(int(h.height)));
+    const KawpowResult r = kawpow_hash(*ctx, int(h.height), h.kawpow_header_hash().to_progpow(), h.nonce64);
+    mix = Uint256::from_progpow(r.mix_hash);
+    return Uint256::from_progpow(r.final_hash);
+}
+
+// ---------------------------------------------------------------- chain
+HeaderChain::HeaderChain(ChainParams params, std::shared_ptr<const PowVerifier> verifier)
+    : params_(std::move(params)), verifier_(std::move(verifier)) {
+    const BlockHeader& g = params_.genesis.header;
+    Uint256 gh = params_.consensus.genesis_hash;
+    if (gh.is_null()) gh = verifier_->block_hash(g, params_);
+    params_.consensus.genesis_hash = gh;
+    genesis_ = add_to_index(g, gh, nullptr);
+    update_active_chain();
+}
+
+const HeaderIndex* HeaderChain::add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev) {
+    storage_.emplace_back();
+    HeaderIndex& idx = storage_.back();
+    idx.hash = hash;
+    idx.prev = prev;
+    idx.height = prev ? prev->height + 1 : 0;
+    idx.time = h.time;
+    idx.bits = h.bits;
+    idx.header = h;
+    idx.chain_work = (prev ? prev->chain_work : ArithU256()) + block_proof(h.bits);
+    if (prev) {
+        // skip pointer: GetSkipHeight (src/chain.cpp)
+        auto invert_low = [](int n) { return n & (n - 1); };
+        const int hgt = idx.height;
+        const int skip_h = hgt < 2 ? 0 : ((hgt & 1) ? invert_low(invert_low(hgt - 1)) + 1 : invert_low(hgt));
+        idx.skip = prev->ancestor(skip_h);
+    }
+    index_[hash] = &idx;
+    return &idx;
+}
+
+AcceptResult HeaderChain::check_header(const BlockHeader& h, bool check_pow) const {
+    AcceptResult r;
+    if (!check_pow) {
+        r.ok = true;
+        return r;
+    }
+    const bool kawpow = h.time >= params_.kawpow_activation_time;
+    if (kawpow) {
+        const int cp = params_.last_checkpoint_height();
+        if (cp >= 0 && int64_t(h.height) <= cp) {
+            if (!check_proof_of_work(verifier_->block_hash(h, params_), h.bits, params_)) {
+                r.reject = "high-hash";
+                r.dos = 50;
+                return r;
+            }
+            r.ok = true;
+            return r;
+        }
+    }
+    Uint256 mix;
+    const Uint256 pow = verifier_->block_hash_full(h, params_, mix);
+    if (!check_proof_of_work(pow, h.bits, params_)) {
+        r.reject = "high-hash";
+        r.dos = 50;
+        return r;
+    }
+    if (kawpow && mix != h.mix_hash) {
+        r.reject = "invalid-mix-hash";
+        r.dos = 50;
+        return r;
+    }
+    r.ok = true;
+    return r;
+}
+
+u32 HeaderChain::next_bits(const BlockHeader& candidate) const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    return next_work_required(tip(), candidate, params_);
+}
+
+AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_time, bool check_pow) {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    AcceptResult r;
+    const Uint256 hash = verifier_->block_hash(h, params_);
+    if (hash == params_.consensus.genesis_hash) {
+        r.ok = true;
+        r.duplicate = true;
+        r.index = genesis_;
+        return r;
+    }
+    auto self = index_.find(hash);
+    if (self != index_.end()) {
+        r.index = self->second;
+        r.duplicate = true;
+        if (failed_.count(self->second)) {
+            r.reject = "duplicate";
+            return r;
+        }
+        r.ok = true;
+        return r;
+    }
+    r = check_header(h, check_pow);
+    if (!r.ok) return r;
+    r.ok = false;
+    auto pit = index_.find(h.prev);
+    if (pit == index_.end()) {
+        r.reject = "prev-blk-not-found";
+        r.dos = 10;
+        return r;
+    }
+    const HeaderIndex* prev = pit->second;
+    if (failed_.count(prev)) {
+        r.reject = "bad-prevblk";
+        r.dos = 100;
+        return r;
+    }
+    // ContextualCheckBlockHeader
+    const int height = prev->height + 1;
+    if (h.bits != next_work_required(prev, h, params_)) {
+        r.reject = "bad-diffbits";
+        r.dos = 100;
+        return r;
+    }
+    const int cp = params_.last_checkpoint_height();
+    if (cp >= 0 && height < cp && at_height(cp) != nullptr) {
+        r.reject = "bad-fork-prior-to-checkpoint";
+        r.dos = 100;
+        return r;
+    }
+    auto cpit = params_.checkpoints.find(height);
+    if (cpit != params_.checkpoints.end() && cpit->second != hash) {
+        r.reject = "checkpoint mismatch";
+        r.dos = 100;
+        return r;
+    }
+    if (int64_t(h.time) <= prev->median_time_past()) {
+        r.reject = "time-too-old";
+        return r;
+    }
+    const int64_t max_future = (height >= params_.dgw_activation_block) ? kMaxFutureBlockTimeDgw : kMaxFutureBlockTime;
+    if (int64_t(h.time) > adjusted_time + max_future) {
+        r.reject = "time-too-new";
+        return r;
+    }
+    if (h.version < kVersionBitsTopBitsAssets) {
+        char buf[48];
+        std::snprintf(buf, sizeof(buf), "bad-version(0x%08x)", unsigned(h.version));
+        r.reject = buf;
+        return r;
+    }
+    // The reference never checks that a KawPow header's nHeight equals its index
+    // height (the epoch/period therefore follow the claimed height). Off by
+    // default for consensus compatibility; -strictheight turns it on as policy.
+    if (strict_kawpow_height && params_.algo_for(h.time) == PowAlgo::KAWPOW && int(h.height) != height) {
+        r.reject = "bad-height";
+        r.dos = 100;
+        return r;
+    }
+    r.index = add_to_index(h, hash, prev);
+    r.ok = true;
+    update_active_chain();
+    return r;
+}
+
+std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHeader>& hs, int64_t adjusted_time,
+                                                      bool check_pow) {
+    std::vector<AcceptResult> out;
+    out.reserve(hs.size());
+    for (auto& h : hs) {
+        out.push_back(accept_header(h, adjusted_time, check_pow));
+        if (!out.back().ok) break;
+    }
+    return out;
+}
+
+void HeaderChain::update_active_chain() {
+    const HeaderIndex* best = genesis_;
+    for (auto& kv : index_) {
+        const HeaderIndex* c = kv.second;
+        bool bad = false;
+        for (const HeaderIndex* p = c; p && !bad; p = p->prev) bad = failed_.count(p) > 0;
+        if (bad) continue;
+        if (c->chain_work > best->chain_work) best = c;
+    }
+    active_.assign(size_t(best->height) + 1, nullptr);
+    for (const HeaderIndex* p = best; p; p = p->prev) active_[size_t(p->height)] = p;
+}
+
+const HeaderIndex* HeaderChain::tip() const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    return active_.empty() ? nullptr : active_.back();
+}
+
+const HeaderIndex* HeaderChain::at_height(int h) const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    if (h < 0 || size_t(h) >= active_.size()) return nullptr;
+    return active_[size_t(h)];
+}
+
+const HeaderIndex* HeaderChain::find(const Uint256& hash) const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    auto it = index_.find(hash);
+    return it == index_.end() ? nullptr : it->second;
+}
+
+void HeaderChain::invalidate(const Uint256& hash) {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    auto it = index_.find(hash);
+    if (it == index_.end() || it->second == genesis_) return;
+    failed_[it->second] = true;
+    update_active_chain();
+}
+
+void HeaderChain::reconsider(const Uint256& hash) {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    auto it = index_.find(hash);
+    if (it == index_.end()) return;
+    failed_.erase(it->second);
+    update_active_chain();
+}
+
+// ---------------------------------------------------------------- block files
+BlockStore::BlockStore(std::string dir, const u8 magic[4], u32 act) : dir_(std::move(dir)), act_(act) {
+    std::memcpy(magic_, magic, 4);
+    ::mkdir(dir_.c_str(), 0755);
+    // continue after the last existing file
+    for (;;) {
+        struct stat st;
+        if (::stat(path(file_).c_str(), &st) != 0) break;
+        if (::stat(path(file_ + 1).c_str(), &st) != 0) {
+            file_size_ = u32(st.st_size);
+            break;
+        }
+        ++file_;
+    }
+    if (file_ > 0 || file_size_ > 0) {
+        struct stat st;
+        if (::stat(path(file_).c_str(), &st) == 0) file_size_ = u32(st.st_size);
+    }
+}
+
+std::string BlockStore::path(int file) const {
+    char name[32];
+    std::snprintf(name, sizeof(name), "/blk%05d.dat", file);
+    return dir_ + name;
+}
+
+BlockStore::Pos BlockStore::write(const Block& b) { return write_raw(b.bytes(act_, true)); }
+
+BlockStore::Pos BlockStore::write_raw(const Bytes& data) {
+    std::lock_guard<std::mutex> g(mu_);
+    const u32 rec = u32(data.size()) + 8;
+    if (file_size_ > 0 && file_size_ + rec > kMaxBlockfileSize) {
+        ++file_;
+        file_size_ = 0;
+    }
+    FILE* f = std::fopen(path(file_).c_str(), "ab");
+    if (!f) throw std::runtime_error("cannot open " + path(file_));
+    u8 hdr[8];
+    std::memcpy(hdr, magic_, 4);
+    store_le32(hdr + 4, u32(data.size()));
+    const bool ok = std::fwrite(hdr, 1, 8, f) == 8 && std::fwrite(data.data(), 1, data.size(), f) == data.size();
+    std::fflush(f);
+    std::fclose(f);
+    if (!ok) throw std::runtime_error("short write to " + path(file_));
+    Pos p;
+    p.file = file_;
+    p.offset = file_size_ + 8;
+    p.size = u32(data.size());
+    file_size_ += rec;
+    return p;
+}
+
+Bytes BlockStore::read_raw(const Pos& pos) const {
+    FILE* f = std::fopen(path(pos.file).c_str(), "rb");
+    if (!f) throw std::runtime_error("cannot open " + path(pos.file));
+    Bytes hdr(8), data(pos.size);
+    bool ok = std::fseek(f, long(pos.offset) - 8, SEEK_SET) == 0 && std::fread(hdr.data(), 1, 8, f) == 8;
+    ok = ok && std::memcmp(hdr.data(), magic_, 4) == 0 && load_le32(hdr.data() + 4) == pos.size;
+    ok = ok && std::fread(data.data(), 1, data.size(), f) == data.size();
+    std::fclose(f);
+    if (!ok) throw std::runtime_error("ReadBlockFromDisk: bad record");
+    return data;
+}
+
+Block BlockStore::read(const Pos& pos) const {
+    Bytes d = read_raw(pos);
+    Reader r(d);
+    return Block::deserialize(r, act_);
+}
+
+std::vector<std::pair<BlockStore::Pos, Bytes>> BlockStore::scan() const {
+    std::vector<std::pair<Pos, Bytes>> out;
+    for (int file = 0;; ++file) {
+        FILE* f = std::fopen(path(file).c_str(), "rb");
+        if (!f) break;
+        u32 off = 0;
+        for (;;) {
+            u8 hdr[8];
+            if (std::fread(hdr, 1, 8, f) != 8) break;
+            if (std::memcmp(hdr, magic_, 4) != 0) break;
+            const u32 size = load_le32(hdr + 4);
+            Bytes d(size);
+            if (std::fread(d.data(), 1, size, f) != size) break;
+            Pos p{file, off + 8, size};
+            out.emplace_back(p, std::move(d));
+            off += 8 + size;
+        }
+        std::fclose(f);
+    }
+    return out;
+}
+
+}  // namespace nodexa

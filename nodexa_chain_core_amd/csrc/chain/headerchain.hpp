@@ -1,0 +1,117 @@
+// Header chain (block index + active chain) and blk?????.dat block files.
+//
+// Parity: CBlockIndex / CChain (src/chain.h:172,465), AcceptBlockHeader /
+// ProcessNewBlockHeaders (src/validation.cpp:11957-12035), CheckBlockHeader
+// (:11638-11665, checkpoint-gated mix-only vs full KawPow), ContextualCheck-
+// BlockHeader (:11811-11875: bad-diffbits, checkpoint forks, time-too-old
+// (MTP), time-too-new (2 h, 12 min once DGW is active), asset block version),
+// WriteBlockToDisk / ReadBlockFromDisk framing (src/validation.cpp:1275-1328,
+// sizes src/validation.h:89-93).
+//
+// Design: the PoW check is a pluggable verifier so the same pipeline runs
+// with the CPU golden model, with GPU batch verification (headers pre-checked
+// in bulk, then accepted with `check_pow=false`), or the mix-only fast path.
+#pragma once
+
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <unordered_map>
+
+#include "pow_rules.hpp"
+
+namespace nodexa {
+
+constexpr int64_t kMaxFutureBlockTime = 2 * 60 * 60;
+constexpr int64_t kMaxFutureBlockTimeDgw = kMaxFutureBlockTime / 10;
+constexpr int32_t kVersionBitsTopBitsAssets = 0x30000000;
+constexpr u32 kMaxBlockfileSize = 0x8000000;  // 128 MiB
+
+struct PowVerifier {
+    virtual ~PowVerifier() = default;
+    // CBlockHeader::GetHash (X16R / X16RV2 / KawPow mix-only).
+    virtual Uint256 block_hash(const BlockHeader& h, const ChainParams& p) const = 0;
+    // CBlockHeader::GetHashFull: (pow hash, computed mix_hash).
+    virtual Uint256 block_hash_full(const BlockHeader& h, const ChainParams& p, Uint256& mix) const = 0;
+};
+
+// CPU golden verifier (KawPow light mode via cached epoch contexts, X16R CPU).
+struct CpuPowVerifier : PowVerifier {
+    Uint256 block_hash(const BlockHeader& h, const ChainParams& p) const override;
+    Uint256 block_hash_full(const BlockHeader& h, const ChainParams& p, Uint256& mix) const override;
+};
+
+struct AcceptResult {
+    bool ok = false;
+    bool duplicate = false;
+    std::string reject;  // reference reject reason ("high-hash", "bad-diffbits", ...)
+    int dos = 0;
+    const HeaderIndex* index = nullptr;
+};
+
+class HeaderChain {
+public:
+    HeaderChain(ChainParams params, std::shared_ptr<const PowVerifier> verifier);
+
+    const ChainParams& params() const { return params_; }
+    ChainParams& mutable_params() { return params_; }
+    const PowVerifier& verifier() const { return *verifier_; }
+
+    // CheckBlockHeader (context-free PoW check).
+    AcceptResult check_header(const BlockHeader& h, bool check_pow) const;
+    AcceptResult accept_header(const BlockHeader& h, int64_t adjusted_time, bool check_pow = true);
+    // Accepts headers in order; stops at the first failure (ProcessNewBlockHeaders).
+    std::vector<AcceptResult> accept_headers(const std::vector<BlockHeader>& hs, int64_t adjusted_time,
+                                             bool check_pow = true);
+
+    const HeaderIndex* tip() const;
+    const HeaderIndex* genesis() const { return genesis_; }
+    const HeaderIndex* at_height(int h) const;
+    const HeaderIndex* find(const Uint256& hash) const;
+    int height() const { const HeaderIndex* t = tip(); return t ? t->height : -1; }
+    bool in_active_chain(const HeaderIndex* idx) const { return idx && at_height(idx->height) == idx; }
+    size_t size() const { return index_.size(); }
+    // Marks a block (and descendants) invalid and re-selects the tip (invalidateblock).
+    void invalidate(const Uint256& hash);
+    void reconsider(const Uint256& hash);
+    u32 next_bits(const BlockHeader& candidate) const;  // GetNextWorkRequired on the tip
+    bool strict_kawpow_height = false;  // policy: header nHeight must equal index height
+
+private:
+    const HeaderIndex* add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev);
+    void update_active_chain();
+
+    ChainParams params_;
+    std::shared_ptr<const PowVerifier> verifier_;
+    mutable std::recursive_mutex mu_;
+    std::deque<HeaderIndex> storage_;
+    std::unordered_map<Uint256, HeaderIndex*, Uint256Hasher> index_;
+    std::unordered_map<const HeaderIndex*, bool> failed_;
+    std::vector<const HeaderIndex*> active_;
+    const HeaderIndex* genesis_ = nullptr;
+};
+
+// blk?????.dat files: [magic 4][u32 size][block] records, 128 MiB per file.
+class BlockStore {
+public:
+    BlockStore(std::string dir, const u8 magic[4], u32 kawpow_activation_time);
+    struct Pos { int file = -1; u32 offset = 0; u32 size = 0; };
+    Pos write(const Block& b);
+    Pos write_raw(const Bytes& serialized_block);
+    Bytes read_raw(const Pos& pos) const;
+    Block read(const Pos& pos) const;
+    // Scan every record of every blk file (reindex / -loadblock). Stops on a bad magic.
+    std::vector<std::pair<Pos, Bytes>> scan() const;
+    std::string path(int file) const;
+    int current_file() const { return file_; }
+
+private:
+    std::string dir_;
+    u8 magic_[4];
+    u32 act_;
+    int file_ = 0;
+    u32 file_size_ = 0;
+    mutable std::mutex mu_;
+};
+
+}  // namespace nodexa

@@ -1,0 +1,140 @@
+#include "pow_rules.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace nodexa {
+
+int64_t HeaderIndex::median_time_past() const {
+    int64_t times[11];
+    int n = 0;
+    for (const HeaderIndex* p = this; p && n < 11; p = p->prev) times[n++] = p->time;
+    std::sort(times, times + n);
+    return times[n / 2];
+}
+
+const HeaderIndex* HeaderIndex::ancestor(int h) const {
+    if (h > height || h < 0) return nullptr;
+    const HeaderIndex* p = this;
+    while (p && p->height > h) p = (p->skip && p->skip->height >= h) ? p->skip : p->prev;
+    return p;
+}
+
+u32 dark_gravity_wave(const HeaderIndex* last, const BlockHeader& next, const ChainParams& params) {
+    const ConsensusParams& c = params.consensus;
+    const ArithU256 pow_limit = ArithU256::from_uint256(c.pow_limit);
+    const u32 pow_limit_compact = pow_limit.get_compact();
+    const int64_t past_blocks = 180;
+    if (!last || last->height < past_blocks) return pow_limit_compact;
+
+    if (c.pow_allow_min_difficulty_blocks && c.pow_no_retargeting) {
+        if (int64_t(next.time) > int64_t(last->time) + c.pow_target_spacing * 2) return pow_limit_compact;
+        const HeaderIndex* p = last;
+        while (p->prev && p->height % c.difficulty_adjustment_interval() != 0 && p->bits == pow_limit_compact)
+            p = p->prev;
+        return p->bits;
+    }
+
+    const HeaderIndex* p = last;
+    ArithU256 avg;
+    int kawpow_blocks = 0;
+    for (u32 count = 1; count <= u32(past_blocks); ++count) {
+        ArithU256 target;
+        target.set_compact(p->bits);
+        if (count == 1) avg = target;
+        else avg = (avg * count + target) / ArithU256(count + 1);  // "not really an average" (src/pow.cpp:57)
+        if (p->time >= params.kawpow_activation_time) ++kawpow_blocks;
+        if (count != u32(past_blocks)) {
+            if (!p->prev) throw std::logic_error("DGW walked past genesis");
+            p = p->prev;
+        }
+    }
+    if (next.time >= params.kawpow_activation_time && kawpow_blocks != past_blocks)
+        return ArithU256::from_uint256(c.kawpow_limit).get_compact();
+
+    ArithU256 bn = avg;
+    int64_t actual = int64_t(last->time) - int64_t(p->time);
+    const int64_t target_timespan = past_blocks * c.pow_target_spacing;
+    if (actual < target_timespan / 3) actual = target_timespan / 3;
+    if (actual > target_timespan * 3) actual = target_timespan * 3;
+    bn *= u32(actual);                        // operator*=(uint32_t) in the reference
+    bn /= ArithU256(u64(target_timespan));    // operator/=(base_uint(uint64))
+    if (bn > pow_limit) bn = pow_limit;
+    return bn.get_compact();
+}
+
+u32 calculate_next_work_required(const HeaderIndex* last, int64_t first_block_time, const ChainParams& params) {
+    const ConsensusParams& c = params.consensus;
+    if (c.pow_no_retargeting) return last->bits;
+    int64_t actual = int64_t(last->time) - first_block_time;
+    if (actual < c.pow_target_timespan / 4) actual = c.pow_target_timespan / 4;
+    if (actual > c.pow_target_timespan * 4) actual = c.pow_target_timespan * 4;
+    const ArithU256 pow_limit = ArithU256::from_uint256(c.pow_limit);
+    ArithU256 bn;
+    bn.set_compact(last->bits);
+    bn *= u32(actual);
+    bn /= ArithU256(u64(c.pow_target_timespan));
+    if (bn > pow_limit) bn = pow_limit;
+    return bn.get_compact();
+}
+
+u32 next_work_required_btc(const HeaderIndex* last, const BlockHeader& next, const ChainParams& params) {
+    const ConsensusParams& c = params.consensus;
+    const u32 pow_limit_compact = ArithU256::from_uint256(c.pow_limit).get_compact();
+    const int64_t interval = c.difficulty_adjustment_interval();
+    if ((last->height + 1) % interval != 0) {
+        if (c.pow_allow_min_difficulty_blocks) {
+            if (int64_t(next.time) > int64_t(last->time) + c.pow_target_spacing * 2) return pow_limit_compact;
+            const HeaderIndex* p = last;
+            while (p->prev && p->height % interval != 0 && p->bits == pow_limit_compact) p = p->prev;
+            return p->bits;
+        }
+        return last->bits;
+    }
+    const int first_height = last->height - int(interval - 1);
+    const HeaderIndex* first = last->ancestor(first_height);
+    if (!first) throw std::logic_error("BTC retarget: missing ancestor");
+    return calculate_next_work_required(last, first->time, params);
+}
+
+u32 next_work_required(const HeaderIndex* last, const BlockHeader& next, const ChainParams& params) {
+    // IsDGWActive(nHeight) = nHeight >= nDGWActivationBlock
+    if (last->height + 1 >= params.dgw_activation_block) return dark_gravity_wave(last, next, params);
+    return next_work_required_btc(last, next, params);
+}
+
+bool check_proof_of_work(const Uint256& hash, u32 bits, const ChainParams& params) {
+    bool negative = false, overflow = false;
+    ArithU256 target;
+    target.set_compact(bits, &negative, &overflow);
+    if (negative || target.is_zero() || overflow || target > ArithU256::from_uint256(params.consensus.pow_limit))
+        return false;
+    return !(ArithU256::from_uint256(hash) > target);
+}
+
+ArithU256 block_proof(u32 bits) {
+    bool negative = false, overflow = false;
+    ArithU256 target;
+    target.set_compact(bits, &negative, &overflow);
+    if (negative || overflow || target.is_zero()) return ArithU256();
+    // 2**256 / (target+1) == ~target / (target+1) + 1
+    return (~target / (target + ArithU256(1))) + ArithU256(1);
+}
+
+Amount block_subsidy(int height) {
+    // Linux/glibc branch of the reference (the Windows branch patches libm
+    // differences with a lookup table of these same values).
+    const Amount s = Amount(54193019856 * std::pow(1 - 0.00000041686938347033551682078457954749861613663597381673753261566162109375,
+                                                   height));
+    return s;
+}
+
+double difficulty_from_bits(u32 bits) {
+    int shift = (bits >> 24) & 0xff;
+    double diff = double(0x0000ffff) / double(bits & 0x00ffffff);
+    while (shift < 29) { diff *= 256.0; ++shift; }
+    while (shift > 29) { diff /= 256.0; --shift; }
+    return diff;
+}
+
+}  // namespace nodexa
