@@ -48,7 +48,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epoch", type=int, default=384, help="384 -> 4 GiB DAG (BASELINE config)")
     ap.add_argument("--batch", type=int, default=1 << 23, help="nonces per GPU per step")
-    ap.add_argument("--equihash", type=int, default=0, help="also time N Equihash(200,9) solves")
+    ap.add_argument("--equihash", type=int, default=4,
+                    help="Equihash(200,9): batches of 8 solves per GPU to time (0 = skip)")
     ap.add_argument("--quiet", action="store_true")
     args = ap.parse_args()
 
@@ -132,9 +133,26 @@ def main() -> int:
 
     eq_sols = None
     if args.equihash:
-        from nodexa_chain_core_amd.models import equihash as eqm
+        # Equihash(200,9): every rank solves its own nonces (weak scaling);
+        # node Sol/s = all solutions / slowest rank's time.
+        from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
-        eq_sols = eqm.bench_device(args.equihash)
+        solver = EquihashSolver(num_inst=8)
+        mk = lambda i, j: hdr.kawpow_input() + struct.pack("<QQQQ", rank, i, j, 0xE9)  # noqa: E731
+        solver.solve([mk(-1 & 0xFFFF, j) for j in range(8)])  # warm-up
+        torch.cuda.synchronize()
+        W.barrier()
+        t0 = time.perf_counter()
+        found = 0
+        for i in range(args.equihash):
+            inputs = [mk(i, j) for j in range(8)]
+            solver.launch(inputs)
+            found += sum(len(s) for s in solver.collect(inputs))
+        torch.cuda.synchronize()
+        eq_dt = W.all_reduce_max(time.perf_counter() - t0)
+        eq_sols = round(W.all_reduce_sum_int(found) / eq_dt, 2)
+        del solver
+        log(f"[bench] Equihash(200,9): {eq_sols} Sol/s ({args.equihash} x 8 solves per rank)")
 
     if rank == 0:
         base = _baseline()
@@ -162,7 +180,10 @@ def main() -> int:
             "dag_build_s": round(dag_s, 3),
             "equihash_sol_per_s": eq_sols,
         }
-        print(json.dumps(out), flush=True)
+        for k, v in list(out.items()) + [("config." + a, b) for a, b in out["config"].items()]:
+            if isinstance(v, (bytes, bytearray)):
+                print(f"[bench] warning: field {k} is bytes", file=sys.stderr)
+        print(json.dumps(out, default=lambda o: o.hex() if isinstance(o, (bytes, bytearray)) else str(o)), flush=True)
     W.shutdown()
     return 0
 

@@ -1,0 +1,386 @@
+// Equihash(200,9) Wagner solver for gfx950 (new; the reference has no
+// Equihash — SURVEY §0.4 / Appendix D). CPU golden model: csrc/pow/equihash.cpp.
+//
+// Data layout (per solver instance = one header/nonce; blockIdx.y = instance):
+//   digit d_j = bits [20j, 20j+20) of the 200-bit leaf string (big-endian),
+//   a row of level r has d_0..d_{r-1} == 0 and lives in bucket  d_r >> 8
+//   (4096 buckets x EQ_CAP slots); the low 8 bits of d_r select the
+//   collision sub-bucket inside the workgroup.
+//   hash table  [2][inst][4096][EQ_CAP][8] u32: word 0 unused, words 1..7 =
+//               the 224-bit big-endian row (double-buffered across levels);
+//   refs        [inst][9][4096][EQ_CAP] u32: level 0 = leaf index, level r>0 =
+//               (parent bucket << 20 | slot a << 10 | slot b) into level r-1;
+//   counts      [inst][10][4096] u32 bucket fill (atomics), memset per solve.
+//
+// Round kernel (one 256-thread workgroup per bucket, 4096 x instances
+// workgroups — many times the 256 CUs): the bucket's rows are staged in LDS,
+// chained by their 8-bit sub-digit with LDS atomics, every pair inside a
+// chain is XORed in registers, rows whose remaining bits vanish are dropped
+// (they only produce duplicate indices), and survivors are appended to their
+// next-level bucket with one global atomic each. A level is ~2.1M rows x 32 B
+// (67 MB), so one solver instance's live set sits in the 256 MiB Infinity Cache.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernel_params.h"  // EquihashDev + EQ_* geometry (shared with the host runtime)
+
+#define EQ_BLOCK 256
+#define EQ_MAX_CHAIN 24
+
+#define NX_DEV __device__ __forceinline__
+
+NX_DEV size_t eq_hidx(const EquihashDev& p, int buf, uint32_t inst, uint32_t bucket, uint32_t slot) {
+    return ((((size_t)buf * p.num_inst + inst) * EQ_BUCKETS + bucket) * EQ_CAP + slot) * EQ_WORDS;
+}
+NX_DEV size_t eq_ridx(const EquihashDev& p, uint32_t inst, int level, uint32_t bucket, uint32_t slot) {
+    return (((size_t)inst * EQ_LEVELS + level) * EQ_BUCKETS + bucket) * EQ_CAP + slot;
+}
+NX_DEV uint32_t* eq_count(const EquihashDev& p, uint32_t inst, int level) {
+    return p.counts + ((size_t)inst * (EQ_LEVELS + 1) + level) * EQ_BUCKETS * EQ_MAX_BANKS;
+}
+
+// Append one row to bucket `nb`: bank = blockIdx.x % banks owns slots
+// [bank*per, (bank+1)*per). Returns the slot index or EQ_CAP when full.
+NX_DEV uint32_t eq_alloc_slot(const EquihashDev& p, uint32_t* cnt, uint32_t nb) {
+    const uint32_t bank = blockIdx.x & (p.banks - 1);
+    const uint32_t per = EQ_CAP / p.banks;
+    const uint32_t local = atomicAdd(&cnt[nb * EQ_MAX_BANKS + bank], 1u);
+    return local < per ? bank * per + local : EQ_CAP;
+}
+
+// Gather the rows of (level, bucket) from every bank into LDS order 0..n-1;
+// sid[i] = the row's slot index inside the bucket (what refs encode).
+// Ends with a __syncthreads(); returns n.
+template <bool ROWS>
+NX_DEV uint32_t eq_stage(const EquihashDev& p, uint32_t inst, int level, int buf, uint32_t bucket, uint32_t* rows,
+                         short* sid, uint32_t* bstart) {
+    const uint32_t per = EQ_CAP / p.banks;
+    if (threadIdx.x == 0) {
+        const uint32_t* c = eq_count(p, inst, level) + (size_t)bucket * EQ_MAX_BANKS;
+        uint32_t tot = 0;
+        for (uint32_t k = 0; k < p.banks; ++k) {
+            bstart[k] = tot;
+            tot += min(c[k], per);
+        }
+        bstart[EQ_MAX_BANKS] = tot;
+    }
+    __syncthreads();
+    const uint32_t n = bstart[EQ_MAX_BANKS];
+    for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
+        uint32_t k = 0;
+        while (k + 1 < p.banks && i >= bstart[k + 1]) ++k;
+        const uint32_t slot = k * per + (i - bstart[k]);
+        sid[i] = (short)slot;
+        if (ROWS) {
+            const uint4* src = (const uint4*)(p.hashes + eq_hidx(p, buf, inst, bucket, slot));
+            ((uint4*)rows)[2 * i] = src[0];
+            ((uint4*)rows)[2 * i + 1] = src[1];
+        }
+    }
+    __syncthreads();
+    return n;
+}
+
+// digit j (20 bits) of a row held as words w[1..7] (w[1] = bits 0..31).
+template <int J>
+NX_DEV uint32_t eq_digit(const uint32_t* w) {
+    constexpr int off = 20 * J;
+    constexpr int q = off / 32 + 1;
+    constexpr int o = off % 32;
+    if constexpr (o + 20 <= 32) {
+        return (w[q] >> (32 - o - 20)) & 0xFFFFFu;
+    } else {
+        return ((w[q] << (o + 20 - 32)) | (w[q + 1] >> (64 - o - 20))) & 0xFFFFFu;
+    }
+}
+
+// true if bits [20*J, 200) of the row are all zero
+template <int J>
+NX_DEV bool eq_zero_from(const uint32_t* w) {
+    constexpr int off = 20 * J;
+    constexpr int q = off / 32 + 1;
+    constexpr int o = off % 32;
+    uint32_t acc = o ? (w[q] & (0xFFFFFFFFu >> o)) : w[q];
+#pragma unroll
+    for (int i = q + 1; i <= 7; ++i) acc |= w[i];
+    return acc == 0;
+}
+
+// ------------------------------------------------------------------ BLAKE2b
+__constant__ static const uint8_t eq_sigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+NX_DEV uint64_t eq_rotr(uint64_t x, int n) { return __builtin_rotateright64(x, n); }
+
+#define EQ_G(a, b, c, d, x, y)                       \
+    do {                                             \
+        v[a] = v[a] + v[b] + (x); v[d] = eq_rotr(v[d] ^ v[a], 32); \
+        v[c] = v[c] + v[d];       v[b] = eq_rotr(v[b] ^ v[c], 24); \
+        v[a] = v[a] + v[b] + (y); v[d] = eq_rotr(v[d] ^ v[a], 16); \
+        v[c] = v[c] + v[d];       v[b] = eq_rotr(v[b] ^ v[c], 63); \
+    } while (0)
+
+NX_DEV void eq_blake2b_final(const uint64_t h0[8], const uint64_t m[16], uint64_t t0, uint64_t out[8]) {
+    const uint64_t iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                            0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+    uint64_t v[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { v[i] = h0[i]; v[i + 8] = iv[i]; }
+    v[12] ^= t0;
+    v[14] = ~v[14];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) {
+        EQ_G(0, 4, 8, 12, m[eq_sigma[r][0]], m[eq_sigma[r][1]]);
+        EQ_G(1, 5, 9, 13, m[eq_sigma[r][2]], m[eq_sigma[r][3]]);
+        EQ_G(2, 6, 10, 14, m[eq_sigma[r][4]], m[eq_sigma[r][5]]);
+        EQ_G(3, 7, 11, 15, m[eq_sigma[r][6]], m[eq_sigma[r][7]]);
+        EQ_G(0, 5, 10, 15, m[eq_sigma[r][8]], m[eq_sigma[r][9]]);
+        EQ_G(1, 6, 11, 12, m[eq_sigma[r][10]], m[eq_sigma[r][11]]);
+        EQ_G(2, 7, 8, 13, m[eq_sigma[r][12]], m[eq_sigma[r][13]]);
+        EQ_G(3, 4, 9, 14, m[eq_sigma[r][14]], m[eq_sigma[r][15]]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = h0[i] ^ v[i] ^ v[i + 8];
+}
+
+NX_DEV uint32_t eq_bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// Round 0: one BLAKE2b per thread -> 2 leaves -> level-0 buckets.
+extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_gen(EquihashDev p) {
+    const uint32_t inst = blockIdx.y;
+    const uint32_t g = blockIdx.x * EQ_BLOCK + threadIdx.x;  // digest index, < 2^20
+    uint64_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = p.msgs[(size_t)inst * 16 + i];
+    // append le32(g) at byte offset input_len (input_len % 8 == 0 or 4 handled generically)
+    {
+        const uint32_t off = p.input_len;
+        const uint32_t wi = off >> 3, sh = (off & 7) * 8;
+        // word-aligned in practice (112 = 14*8); generic path for off % 8 == 4
+        uint64_t add = (uint64_t)g << sh;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((uint32_t)i == wi) m[i] |= add;
+        if (sh > 32) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if ((uint32_t)i == wi + 1) m[i] |= (uint64_t)g >> (64 - sh);
+        }
+    }
+    uint64_t out[8];
+    eq_blake2b_final(p.h0, m, (uint64_t)p.input_len + 4, out);
+    // 50 digest bytes -> two 25-byte leaves, as big-endian 32-bit words
+    uint8_t b[56];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[8 * i + k] = (uint8_t)(out[i] >> (8 * k));
+    }
+    uint32_t* cnt = eq_count(p, inst, 0);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        uint32_t w[8];
+        w[0] = 0;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+            const int base = half * 25 + 4 * i;
+            const uint32_t b0 = b[base];
+            const uint32_t b1 = (4 * i + 1 < 25) ? b[base + 1] : 0;
+            const uint32_t b2 = (4 * i + 2 < 25) ? b[base + 2] : 0;
+            const uint32_t b3 = (4 * i + 3 < 25) ? b[base + 3] : 0;
+            w[i + 1] = (4 * i < 25) ? ((b0 << 24) | (b1 << 16) | (b2 << 8) | b3) : 0;
+        }
+        const uint32_t bucket = eq_digit<0>(w) >> 8;
+        const uint32_t slot = eq_alloc_slot(p, cnt, bucket);
+        if (slot < EQ_CAP) {
+            uint4* dst = (uint4*)(p.hashes + eq_hidx(p, 0, inst, bucket, slot));
+            dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+            dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+            p.refs[eq_ridx(p, inst, 0, bucket, slot)] = 2 * g + half;
+        }
+    }
+}
+
+// Round R (1..8): collide level R-1 on digit R-1, write level R.
+template <int R>
+NX_DEV void eq_round_impl(const EquihashDev& p) {
+    __shared__ __attribute__((aligned(16))) uint32_t rows[EQ_CAP * EQ_WORDS];
+    __shared__ int head[256];
+    __shared__ short nxt[EQ_CAP];
+    __shared__ short sid[EQ_CAP];
+    __shared__ uint32_t bstart[EQ_MAX_BANKS + 1];
+    const uint32_t inst = blockIdx.y;
+    const uint32_t bucket = blockIdx.x;
+    for (int i = threadIdx.x; i < 256; i += EQ_BLOCK) head[i] = -1;
+    const uint32_t n = eq_stage<true>(p, inst, R - 1, (R - 1) & 1, bucket, rows, sid, bstart);
+    for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
+        const uint32_t sub = eq_digit<R - 1>(&rows[i * EQ_WORDS]) & 0xFFu;
+        nxt[i] = (short)atomicExch(&head[sub], (int)i);
+    }
+    __syncthreads();
+    uint32_t* cnt = eq_count(p, inst, R);
+    for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
+        const uint32_t* a = &rows[i * EQ_WORDS];
+        int j = nxt[i];
+        for (int steps = 0; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
+            const uint32_t* b = &rows[(uint32_t)j * EQ_WORDS];
+            uint32_t x[8];
+            x[0] = 0;
+#pragma unroll
+            for (int k = 1; k < 8; ++k) x[k] = a[k] ^ b[k];
+            if (eq_zero_from<R>(x)) continue;  // identical remainder -> only duplicate indices
+            const uint32_t nb = eq_digit<R>(x) >> 8;
+            const uint32_t slot = eq_alloc_slot(p, cnt, nb);
+            if (slot < EQ_CAP) {
+                uint4* dst = (uint4*)(p.hashes + eq_hidx(p, R & 1, inst, nb, slot));
+                dst[0] = make_uint4(0, x[1], x[2], x[3]);
+                dst[1] = make_uint4(x[4], x[5], x[6], x[7]);
+                p.refs[eq_ridx(p, inst, R, nb, slot)] =
+                    (bucket << 20) | ((uint32_t)sid[i] << 10) | (uint32_t)sid[j];
+            }
+        }
+    }
+}
+
+#define EQ_ROUND_KERNEL(R) \
+    extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_round##R(EquihashDev p) { eq_round_impl<R>(p); }
+EQ_ROUND_KERNEL(1)
+EQ_ROUND_KERNEL(2)
+EQ_ROUND_KERNEL(3)
+EQ_ROUND_KERNEL(4)
+EQ_ROUND_KERNEL(5)
+EQ_ROUND_KERNEL(6)
+EQ_ROUND_KERNEL(7)
+EQ_ROUND_KERNEL(8)
+
+// Final round: level-8 rows colliding on d_8 and d_9 (40 bits) are candidates.
+extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_final(EquihashDev p) {
+    __shared__ uint32_t d9[EQ_CAP];
+    __shared__ int head[256];
+    __shared__ short nxt[EQ_CAP];
+    __shared__ short sid[EQ_CAP];
+    __shared__ uint32_t bstart[EQ_MAX_BANKS + 1];
+    const uint32_t inst = blockIdx.y;
+    const uint32_t bucket = blockIdx.x;
+    for (int i = threadIdx.x; i < 256; i += EQ_BLOCK) head[i] = -1;
+    const uint32_t n = eq_stage<false>(p, inst, 8, 0, bucket, nullptr, sid, bstart);
+    for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
+        // level 8 lives in buffer 8 & 1 = 0
+        const uint32_t* w = p.hashes + eq_hidx(p, 0, inst, bucket, (uint32_t)sid[i]);
+        const uint32_t d8 = eq_digit<8>(w), dd = eq_digit<9>(w);
+        d9[i] = dd;
+        nxt[i] = (short)atomicExch(&head[d8 & 0xFFu], (int)i);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
+        for (int j = nxt[i], steps = 0; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
+            if (d9[i] != d9[(uint32_t)j]) continue;
+            uint32_t* c = p.cands + (size_t)inst * (1 + 2 * EQ_MAX_CAND);
+            const uint32_t k = atomicAdd(&c[0], 1u);
+            if (k < EQ_MAX_CAND) {
+                c[1 + 2 * k] = bucket * EQ_CAP + (uint32_t)sid[i];
+                c[2 + 2 * k] = bucket * EQ_CAP + (uint32_t)sid[j];
+            }
+        }
+    }
+}
+
+// Reconstruct the 512 leaf indices of every candidate, reject duplicate trees
+// early (most final-round collisions reuse a row: they are caught while the
+// tree is still <= 64 wide), canonicalise the order, and append valid
+// solutions. EQ_RECON_GROUPS workgroups per instance stride over candidates.
+extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_reconstruct(EquihashDev p) {
+    __shared__ uint32_t cur[512];
+    __shared__ uint32_t tmp[512];
+    __shared__ int bad;
+    __shared__ uint32_t slot;
+    const uint32_t inst = blockIdx.y;
+    const uint32_t* c = p.cands + (size_t)inst * (1 + 2 * EQ_MAX_CAND);
+    const uint32_t ncand = min(c[0], (uint32_t)EQ_MAX_CAND);
+    uint32_t* sb = p.sols + (size_t)inst * (1 + EQ_MAX_SOL * 512);
+    for (uint32_t cand = blockIdx.x; cand < ncand; cand += gridDim.x) {
+        __syncthreads();  // previous iteration done with the LDS arrays
+        if (threadIdx.x == 0) {
+            cur[0] = c[1 + 2 * cand];
+            cur[1] = c[2 + 2 * cand];
+            bad = 0;
+        }
+        __syncthreads();
+        uint32_t width = 2;
+        for (int level = 8; level >= 1; --level) {
+            for (uint32_t t = threadIdx.x; t < width; t += EQ_BLOCK) {
+                const uint32_t s = cur[t];
+                const uint32_t ref = p.refs[eq_ridx(p, inst, level, s / EQ_CAP, s % EQ_CAP)];
+                const uint32_t pb = ref >> 20;
+                tmp[2 * t] = pb * EQ_CAP + ((ref >> 10) & 1023u);
+                tmp[2 * t + 1] = pb * EQ_CAP + (ref & 1023u);
+            }
+            __syncthreads();
+            width *= 2;
+            for (uint32_t t = threadIdx.x; t < width; t += EQ_BLOCK) cur[t] = tmp[t];
+            __syncthreads();
+            if (width <= 64) {  // a repeated row at any level means repeated leaves
+                const uint32_t npairs = width * (width - 1) / 2;
+                for (uint32_t q = threadIdx.x; q < npairs; q += EQ_BLOCK) {
+                    uint32_t a = 0, rem = q;
+                    while (rem >= width - 1 - a) { rem -= width - 1 - a; ++a; }
+                    if (cur[a] == cur[a + 1 + rem]) bad = 1;
+                }
+                __syncthreads();
+                if (bad) break;
+            }
+        }
+        if (bad) continue;
+        for (uint32_t t = threadIdx.x; t < 512; t += EQ_BLOCK) {
+            const uint32_t s = cur[t];
+            cur[t] = p.refs[eq_ridx(p, inst, 0, s / EQ_CAP, s % EQ_CAP)];
+        }
+        __syncthreads();
+        // canonical order: every node's left subtree starts with the smaller index
+        for (uint32_t sz = 1; sz < 512; sz *= 2) {
+            for (uint32_t node = threadIdx.x; node < 512 / (2 * sz); node += EQ_BLOCK) {
+                const uint32_t l = node * 2 * sz, r = l + sz;
+                if (cur[l] > cur[r]) {
+                    for (uint32_t k = 0; k < sz; ++k) {
+                        const uint32_t x = cur[l + k];
+                        cur[l + k] = cur[r + k];
+                        cur[r + k] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // full duplicate check on a bitonic-sorted copy
+        for (uint32_t t = threadIdx.x; t < 512; t += EQ_BLOCK) tmp[t] = cur[t];
+        __syncthreads();
+        for (uint32_t k = 2; k <= 512; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t t = threadIdx.x; t < 512; t += EQ_BLOCK) {
+                    const uint32_t ixj = t ^ j;
+                    if (ixj > t) {
+                        const bool up = (t & k) == 0;
+                        const uint32_t a = tmp[t], b = tmp[ixj];
+                        if ((a > b) == up) {
+                            tmp[t] = b;
+                            tmp[ixj] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t t = threadIdx.x; t < 511; t += EQ_BLOCK)
+            if (tmp[t] == tmp[t + 1]) bad = 1;
+        __syncthreads();
+        if (bad) continue;
+        if (threadIdx.x == 0) slot = atomicAdd(&sb[0], 1u);
+        __syncthreads();
+        if (slot < EQ_MAX_SOL)
+            for (uint32_t t = threadIdx.x; t < 512; t += EQ_BLOCK) sb[1 + slot * 512 + t] = cur[t];
+    }
+}

@@ -55,6 +55,31 @@ struct KawpowVerifyJob {
     uint32_t pad;
 };
 
+// ---------------------------------------------------------------- Equihash(200,9)
+#define EQ_BUCKET_BITS 12
+#define EQ_BUCKETS (1 << EQ_BUCKET_BITS)
+#define EQ_CAP 768  // mean fill 512..537 rows/bucket, max observed 647 over 4096 buckets
+#define EQ_WORDS 8
+#define EQ_LEVELS 9
+#define EQ_MAX_CAND 4096  // ~500-1100 final-round collisions per nonce, almost all duplicate trees
+#define EQ_RECON_GROUPS 128  // reconstruct workgroups per instance (grid-stride over candidates)
+#define EQ_MAX_BANKS 8
+#define EQ_MAX_SOL 16
+
+struct EquihashDev {
+    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (input bytes, LE); the index is OR-ed in-kernel
+    uint64_t h0[8];         // BLAKE2b state after the parameter block (digest 50, "ZcashPoW" personal)
+    uint32_t input_len;     // bytes of input (<= 124: one compression per digest)
+    uint32_t num_inst;
+    uint32_t banks;         // slot-counter banks per bucket (1,2,4,8): spreads the append atomics
+    uint32_t pad;
+    uint32_t* hashes;       // [2][inst][BUCKETS][CAP][WORDS]
+    uint32_t* refs;         // [inst][LEVELS][BUCKETS][CAP]
+    uint32_t* counts;       // [inst][LEVELS+1][BUCKETS][EQ_MAX_BANKS]
+    uint32_t* cands;        // [inst][1 + 2*MAX_CAND]: count, then (slot_a, slot_b) global slot ids at level 8
+    uint32_t* sols;         // [inst][1 + MAX_SOL*512]: count, then solutions
+};
+
 struct KawpowHashParams {
     const void* dag;                  // full DAG (2048-bit items)
     const struct KawpowVerifyJob* jobs;

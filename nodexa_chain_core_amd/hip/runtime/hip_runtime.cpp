@@ -227,4 +227,43 @@ PYBIND11_MODULE(_hip, m) {
         k.launch_bytes(dim3(grid), dim3(NODEXA_KAWPOW_BLOCK), 0, as_stream(stream), &p, sizeof(p));
     });
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
+
+    // ---- Equihash(200,9): one full Wagner solve for `num_inst` inputs, enqueued on `stream`
+    m.attr("EQ_BUCKETS") = EQ_BUCKETS;
+    m.attr("EQ_CAP") = EQ_CAP;
+    m.attr("EQ_WORDS") = EQ_WORDS;
+    m.attr("EQ_LEVELS") = EQ_LEVELS;
+    m.attr("EQ_MAX_CAND") = EQ_MAX_CAND;
+    m.attr("EQ_MAX_SOL") = EQ_MAX_SOL;
+    m.attr("EQ_MAX_BANKS") = EQ_MAX_BANKS;
+    m.def("launch_equihash_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
+                                      uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
+                                      uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols,
+                                      uintptr_t stream, uint32_t banks) {
+        if (banks == 0 || banks > EQ_MAX_BANKS || (banks & (banks - 1)) || EQ_CAP % banks)
+            throw std::invalid_argument("banks must be a power of two <= EQ_MAX_BANKS dividing EQ_CAP");
+        // ks = [eq_gen, eq_round1..eq_round8, eq_final, eq_reconstruct]
+        if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash kernels");
+        if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
+        if (input_len > 124 || num_inst == 0) throw std::invalid_argument("bad equihash geometry");
+        EquihashDev p{};
+        p.msgs = reinterpret_cast<const uint64_t*>(msgs);
+        for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
+        p.input_len = input_len;
+        p.num_inst = num_inst;
+        p.banks = banks;
+        p.hashes = reinterpret_cast<uint32_t*>(hashes);
+        p.refs = reinterpret_cast<uint32_t*>(refs);
+        p.counts = reinterpret_cast<uint32_t*>(counts);
+        p.cands = reinterpret_cast<uint32_t*>(cands);
+        p.sols = reinterpret_cast<uint32_t*>(sols);
+        hipStream_t s = as_stream(stream);
+        check(hipMemsetAsync(p.counts, 0, size_t(num_inst) * (EQ_LEVELS + 1) * EQ_BUCKETS * EQ_MAX_BANKS * 4, s), "memset counts");
+        check(hipMemsetAsync(p.cands, 0, size_t(num_inst) * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
+        check(hipMemsetAsync(p.sols, 0, size_t(num_inst) * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
+        ks[0]->launch_bytes(dim3((1u << 20) / 256, num_inst), dim3(256), 0, s, &p, sizeof(p));
+        for (int r = 1; r <= 8; ++r) ks[size_t(r)]->launch_bytes(dim3(EQ_BUCKETS, num_inst), dim3(256), 0, s, &p, sizeof(p));
+        ks[9]->launch_bytes(dim3(EQ_BUCKETS, num_inst), dim3(256), 0, s, &p, sizeof(p));
+        ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
+    });
 }
