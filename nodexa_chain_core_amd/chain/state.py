@@ -1,0 +1,247 @@
+"""Chain state: header chain + block files + the ProcessNewBlock pipeline.
+
+Parity (behaviour): ProcessNewBlock -> CheckBlock -> AcceptBlock ->
+ActivateBestChain (src/validation.cpp:12131-12162, 12038, 11272) restricted to
+what the PoW engine owns: header PoW + contextual checks (C++ HeaderChain),
+structural block checks, the CLORE coinbase / community-fund rules
+(C++ validation.cpp), block storage in reference-format blk?????.dat files, tip
+selection by chain work, and the validation-interface signal bus
+(CValidationInterface, src/validationinterface.h:37-86). UTXO/script
+validation is DEFERred: non-coinbase transactions are carried
+opaquely and their fees are taken as declared by the template builder.
+
+On start-up the block index is rebuilt by scanning the blk files
+(`-reindex` semantics; SURVEY S5: COMPAT-read optional).
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+
+from .. import core
+from ..utils import log
+
+_core = core()
+
+REGTEST_NODEXA_KAWPOW_ACTIVATION = 1524179366 + 1  # genesis + 1: every mined regtest block is KawPow
+
+
+@dataclass
+class ValidationState:
+    ok: bool = True
+    reject: str = ""
+    dos: int = 0
+
+    @classmethod
+    def invalid(cls, reason: str, dos: int = 0) -> "ValidationState":
+        return cls(False, reason, dos)
+
+
+class ValidationInterface:
+    """Subscriber interface (CValidationInterface). Override what you need."""
+
+    def updated_block_tip(self, tip, fork, initial_download: bool) -> None: ...
+
+    def block_connected(self, block, index) -> None: ...
+
+    def block_checked(self, block, state: ValidationState) -> None: ...
+
+    def block_found(self, block_hash: bytes) -> None: ...
+
+
+def make_params(network: str, kawpow_activation_time: int | None = None,
+                equihash_activation_time: int | None = None):
+    p = _core.make_chain_params(network)
+    if kawpow_activation_time is not None:
+        p.kawpow_activation_time = int(kawpow_activation_time)
+    elif network == "regtest":
+        p.kawpow_activation_time = REGTEST_NODEXA_KAWPOW_ACTIVATION
+    if equihash_activation_time is not None:
+        p.equihash_activation_time = int(equihash_activation_time)
+    return p
+
+
+@dataclass
+class MempoolEntry:
+    tx: object
+    fee: int
+    time: float = field(default_factory=time.time)
+
+
+class ChainState:
+    def __init__(self, params, datadir: str | None = None, strict_height: bool = False):
+        self.params = params
+        self.chain = _core.HeaderChain(params)
+        self.chain.strict_kawpow_height = strict_height
+        self.lock = threading.RLock()
+        self.cv_tip = threading.Condition(self.lock)
+        self.listeners: list[ValidationInterface] = []
+        self.block_pos: dict[bytes, object] = {}
+        self.mempool: dict[bytes, MempoolEntry] = {}
+        self.transactions_updated = 0
+        self.datadir = datadir
+        self.store = None
+        self.start_time = time.time()
+        if datadir is not None:
+            bdir = os.path.join(datadir, "blocks")
+            os.makedirs(bdir, exist_ok=True)
+            self.store = _core.BlockStore(bdir, params.message_start, params.kawpow_activation_time)
+            self._load_block_files()
+        gh = self.chain.genesis().hash
+        if self.store is not None and gh not in self.block_pos:
+            self.block_pos[gh] = self.store.write(params.genesis)
+
+    # ------------------------------------------------------------------ load / reindex
+    def _load_block_files(self) -> None:
+        act = self.params.kawpow_activation_time
+        n = 0
+        for pos, raw in self.store.scan():
+            blk = _core.Block.deserialize(raw, act)
+            h = self.chain.block_hash(blk.header)
+            if h == self.chain.genesis().hash:
+                self.block_pos[h] = pos
+                continue
+            # blocks in our files were fully validated before they were written
+            r = self.chain.accept_header(blk.header, 2**62, False)
+            if r.ok:
+                self.block_pos[h] = pos
+                n += 1
+        if n:
+            log.log_printf(f"loaded {n} blocks from block files, tip height {self.chain.height()}")
+
+    # ------------------------------------------------------------------ signals
+    def register(self, l: ValidationInterface) -> None:
+        with self.lock:
+            self.listeners.append(l)
+
+    def unregister(self, l: ValidationInterface) -> None:
+        with self.lock:
+            if l in self.listeners:
+                self.listeners.remove(l)
+
+    def _emit(self, name: str, *a) -> None:
+        for l in list(self.listeners):
+            try:
+                getattr(l, name)(*a)
+            except Exception as e:  # a subscriber must never break validation
+                log.log_printf(f"validation listener {type(l).__name__}.{name} failed: {e}")
+
+    # ------------------------------------------------------------------ queries
+    def tip(self):
+        return self.chain.tip()
+
+    def height(self) -> int:
+        return self.chain.height()
+
+    def block_hash(self, header) -> bytes:
+        return self.chain.block_hash(header)
+
+    def get_block(self, h: bytes):
+        pos = self.block_pos.get(h)
+        if pos is None or self.store is None:
+            return None
+        return self.store.read(pos)
+
+    def get_block_raw(self, h: bytes) -> bytes | None:
+        pos = self.block_pos.get(h)
+        if pos is None or self.store is None:
+            return None
+        return self.store.read_raw(pos)
+
+    def adjusted_time(self) -> int:
+        return int(time.time())
+
+    # ------------------------------------------------------------------ mempool-lite
+    def add_to_mempool(self, tx, fee: int) -> bytes:
+        txid = tx.txid()
+        with self.lock:
+            self.mempool[txid] = MempoolEntry(tx, int(fee))
+            self.transactions_updated += 1
+        return txid
+
+    # ------------------------------------------------------------------ ProcessNewBlock
+    def check_block_header(self, header) -> ValidationState:
+        r = self.chain.check_header(header, True)
+        return ValidationState(r.ok, r.reject, r.dos)
+
+    def process_new_block(self, block, check_pow: bool = True, fees_known: bool | None = None) -> ValidationState:
+        """Validate + store + activate. Returns the BIP22-style state."""
+        with self.lock:
+            h = self.chain.block_hash(block.header)
+            existing = self.chain.find(h)
+            if existing is not None and h in self.block_pos:
+                st = ValidationState.invalid("duplicate")
+                self._emit("block_checked", block, st)
+                return st
+            ok, reason, dos = _core.check_block(block, self.params, True)
+            if not ok:
+                st = ValidationState.invalid(reason, dos)
+                self._emit("block_checked", block, st)
+                return st
+            prev = self.chain.find(block.header.prev)
+            if prev is None:
+                st = ValidationState.invalid("prev-blk-not-found", 10)
+                self._emit("block_checked", block, st)
+                return st
+            height = prev.height + 1
+            ok, reason, dos = _core.contextual_check_block(block, self.params, height)
+            if ok:
+                fees = sum(self.mempool[tx.txid()].fee for tx in block.vtx[1:] if tx.txid() in self.mempool)
+                known = (len(block.vtx) == 1) if fees_known is None else fees_known
+                if not known:
+                    known = all(tx.txid() in self.mempool for tx in block.vtx[1:])
+                ok, reason, dos = _core.check_coinbase_rewards(block, self.params, height, fees, known)
+            if not ok:
+                st = ValidationState.invalid(reason, dos)
+                self._emit("block_checked", block, st)
+                return st
+            old_tip = self.chain.tip()
+            r = self.chain.accept_header(block.header, self.adjusted_time(), check_pow)
+            if not r.ok:
+                st = ValidationState.invalid(r.reject, r.dos)
+                self._emit("block_checked", block, st)
+                return st
+            if self.store is not None:
+                self.block_pos[h] = self.store.write(block)
+            else:
+                self.block_pos[h] = None
+            st = ValidationState()
+            self._emit("block_checked", block, st)
+            for tx in block.vtx[1:]:
+                self.mempool.pop(tx.txid(), None)
+            new_tip = self.chain.tip()
+            if new_tip.hash != old_tip.hash:
+                self._emit("block_connected", block, r.index)
+                self._emit("updated_block_tip", new_tip, old_tip, False)
+                self.cv_tip.notify_all()
+                log.log_print("validation", f"new tip {_core.u256_hex(new_tip.hash)} height {new_tip.height}")
+            return st
+
+    def wait_for_tip_change(self, old_hash: bytes, timeout: float) -> bool:
+        with self.cv_tip:
+            return self.cv_tip.wait_for(lambda: self.chain.tip().hash != old_hash, timeout=timeout)
+
+    # ------------------------------------------------------------------ stats
+    def network_hashps(self, lookup: int = 120, height: int = -1) -> float:
+        """GetNetworkHashPS (src/rpc/mining.cpp:58-93)."""
+        tip = self.chain.tip()
+        pb = tip
+        if 0 <= height < tip.height:
+            pb = self.chain.at_height(height)
+        if pb is None or pb.height == 0:
+            return 0.0
+        interval = 2016
+        if lookup <= 0:
+            lookup = pb.height % interval + 1
+        lookup = min(lookup, pb.height)
+        min_t = max_t = pb.time
+        pb0 = pb
+        for _ in range(lookup):
+            pb0 = self.chain.at_height(pb0.height - 1) if self.chain.in_active_chain(pb0) else self.chain.find(pb0.prev_hash)
+            min_t = min(min_t, pb0.time)
+            max_t = max(max_t, pb0.time)
+        if min_t == max_t:
+            return 0.0
+        return float(pb.chain_work - pb0.chain_work) / (max_t - min_t)

@@ -4,6 +4,7 @@
 
 #include "../chain/headerchain.hpp"
 #include "../chain/script.hpp"
+#include "../chain/validation.hpp"
 #include "../pow/equihash.hpp"
 #include "../pow/x16r.hpp"
 
@@ -266,6 +267,16 @@ void bind_extra(py::module_& m) {
         .def("scan", [](const BlockStore& s) { py::list l; for (auto& kv : s.scan()) l.append(py::make_tuple(kv.first, pyb(kv.second))); return l; })
         .def("path", &BlockStore::path)
         .def("current_file", &BlockStore::current_file);
+
+    // ------------------------------------------------ block validation
+    auto bc = [](const BlockCheck& c) { return py::make_tuple(c.ok, c.reject, c.dos); };
+    m.def("check_block", [bc](const Block& b, const ChainParams& p, bool merkle) { return bc(check_block(b, p, merkle)); },
+          py::arg("block"), py::arg("params"), py::arg("check_merkle") = true);
+    m.def("contextual_check_block", [bc](const Block& b, const ChainParams& p, int h) { return bc(contextual_check_block(b, p, h)); });
+    m.def("check_coinbase_rewards", [bc](const Block& b, const ChainParams& p, int h, Amount fees, bool known) {
+        return bc(check_coinbase_rewards(b, p, h, fees, known));
+    });
+    m.def("coinbase_height_prefix", [](int h) { return pyb(coinbase_height_prefix(h)); });
 
     // ------------------------------------------------ Equihash (CPU reference)
     bind_equihash_cpu(m);

@@ -109,6 +109,7 @@ PYBIND11_MODULE(_core, m) {
         });
     m.def("make_kawpow_program", &make_kawpow_program);
     m.def("kawpow_codegen_hip", [](u64 period) { return kawpow_codegen_hip(make_kawpow_program(period)); });
+    m.def("kawpow_program_words", [](u64 period) { return kawpow_program_words(make_kawpow_program(period)); });
     m.def("kawpow_hash", [](const EpochContext& c, int block, const py::bytes& h, u64 nonce) {
         KawpowResult r;
         Hash256 hh = to_h256(h);

@@ -116,5 +116,8 @@ double kawpow_cpu_hashrate(HostDag& dag, int block_number, u64 nonces, int threa
 
 // gfx950 HIP source for one period (see hip/kernels/kawpow_search.hip).
 std::string kawpow_codegen_hip(const KawpowProgram& prog);
+// 64-word data encoding of a period's program for the batch-verify kernel
+// (hip/kernels/kawpow_verify.hip, layout documented there).
+std::vector<u32> kawpow_program_words(const KawpowProgram& prog);
 
 }  // namespace nodexa

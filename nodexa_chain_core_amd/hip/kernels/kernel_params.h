@@ -80,6 +80,19 @@ struct EquihashDev {
     uint32_t* sols;         // [inst][1 + MAX_SOL*512]: count, then solutions
 };
 
+// Batch verification with the period program as data (kawpow_verify.hip).
+#define KV_PROG_WORDS 64
+struct KawpowVerifyParams {
+    const void* dag;                    // full DAG of the batch's epoch (2048-bit items)
+    const struct KawpowVerifyJob* jobs; // sorted by period, padded so each 64-job slab is one period
+    const uint32_t* programs;           // [num_programs][KV_PROG_WORDS]
+    const uint32_t* job_program;        // per 64-job slab: program index
+    uint32_t* out;                      // per job: mix[8], final[8]
+    uint32_t num_jobs;
+    uint32_t pad;
+    struct FastMod32 items;
+};
+
 struct KawpowHashParams {
     const void* dag;                  // full DAG (2048-bit items)
     const struct KawpowVerifyJob* jobs;

@@ -227,6 +227,23 @@ PYBIND11_MODULE(_hip, m) {
         k.launch_bytes(dim3(grid), dim3(NODEXA_KAWPOW_BLOCK), 0, as_stream(stream), &p, sizeof(p));
     });
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
+    m.attr("KV_PROG_WORDS") = KV_PROG_WORDS;
+    m.def("launch_kawpow_verify_batch", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t jobs,
+                                           uintptr_t programs, uintptr_t job_program, uint32_t num_jobs, uintptr_t out,
+                                           uintptr_t stream) {
+        if (num_jobs % 64) throw std::invalid_argument("verify batch must be padded to 64-job slabs");
+        KawpowVerifyParams p{};
+        p.dag = reinterpret_cast<const void*>(dag);
+        p.jobs = reinterpret_cast<const KawpowVerifyJob*>(jobs);
+        p.programs = reinterpret_cast<const uint32_t*>(programs);
+        p.job_program = reinterpret_cast<const uint32_t*>(job_program);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        p.num_jobs = num_jobs;
+        p.items = make_fastmod(dag_items2048);
+        const unsigned grid = (num_jobs + 255) / 256;
+        if (grid == 0) return;
+        k.launch_bytes(dim3(grid), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
 
     // ---- Equihash(200,9): one full Wagner solve for `num_inst` inputs, enqueued on `stream`
     m.attr("EQ_BUCKETS") = EQ_BUCKETS;

@@ -1,0 +1,137 @@
+"""Block templates: BlockAssembler::CreateNewBlock + IncrementExtraNonce.
+
+Parity: CreateNewBlock (src/miner.cpp:123-256): coinbase vout[0] = fees +
+(100-pct)% of the subsidy to the miner script, vout[1] = subsidy*pct/100 to
+the community-autonomous address, scriptSig = <height> OP_0, witness
+commitment output (GenerateCoinbaseCommitment, src/validation.cpp:11779-11806)
+with the 32-byte witness nonce; header: version = 0x30000000 (assets
+deployed), time = max(MTP+1, now), bits = GetNextWorkRequired, nNonce = 0,
+nNonce64 = 0, nHeight = tip+1. IncrementExtraNonce (src/miner.cpp:508-525):
+scriptSig = <height> <extranonce>, merkle root recomputed.
+
+Mempool selection (addPackageTxs) is out of scope: templates carry the
+transactions of the engine's mempool-lite in arrival order, capped by weight.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+
+from .. import core
+from ..chain.state import ChainState
+
+_core = core()
+
+BLOCK_VERSION_ASSETS = 0x30000000
+WITNESS_COMMITMENT_HEADER = bytes([0x6a, 0x24, 0xaa, 0x21, 0xa9, 0xed])
+
+
+@dataclass
+class BlockTemplate:
+    block: object          # _core.Block
+    height: int
+    fees: int
+    coinbase_value: int
+    community_value: int
+    witness_commitment: bytes
+    target: int
+    created: float
+
+
+def script_for_address(params, address: str) -> bytes:
+    spk = _core.address_to_script(address, params.pubkey_prefix, params.script_prefix)
+    if spk is None:
+        raise ValueError(f"invalid address for {params.network_id}: {address}")
+    return spk
+
+
+class BlockAssembler:
+    def __init__(self, state: ChainState, max_weight: int = 7_999_000):
+        self.state = state
+        self.params = state.params
+        self.max_weight = max_weight
+
+    def create_new_block(self, script_pubkey: bytes, now: int | None = None) -> BlockTemplate:
+        st = self.state
+        with st.lock:
+            prev = st.tip()
+            height = prev.height + 1
+            txs, fees, weight = [], 0, 4000
+            for e in list(st.mempool.values()):
+                w = len(e.tx.serialize(False)) * 3 + len(e.tx.serialize(True))
+                if weight + w > self.max_weight:
+                    break
+                txs.append(e.tx)
+                fees += e.fee
+                weight += w
+            subsidy = _core.block_subsidy(height)
+            pct = self.params.community_autonomous_pct
+            cb = _core.Transaction()
+            cb.version = 1
+            vin = _core.TxIn()
+            vin.script_sig = _core.script_push_int(height) + b"\x00"  # CScript() << nHeight << OP_0
+            cb.vin = [vin]
+            miner = _core.TxOut(fees + (100 - pct) * subsidy // 100, script_pubkey)
+            community = _core.TxOut(subsidy * pct // 100, script_for_address(self.params, self.params.community_autonomous_address))
+            cb.vout = [miner, community]
+            blk = _core.Block()
+            blk.vtx = [cb] + txs
+            commitment = self._add_witness_commitment(blk)
+            hdr = _core.BlockHeader()
+            hdr.version = BLOCK_VERSION_ASSETS
+            hdr.prev = prev.hash
+            t = int(time.time()) if now is None else int(now)
+            hdr.time = max(prev.median_time_past() + 1, t)
+            hdr.height = height
+            hdr.nonce = 0
+            hdr.nonce64 = 0
+            hdr.bits = st.chain.next_bits(hdr)
+            blk.header = hdr
+            root, _ = blk.merkle_root()
+            hdr.merkle_root = root
+            blk.header = hdr
+            target, _, _ = _core.set_compact(hdr.bits)
+            return BlockTemplate(blk, height, fees, miner.value, community.value, commitment, target, time.time())
+
+    def _add_witness_commitment(self, blk) -> bytes:
+        # segwit is enabled on every network (nSegwitEnabled = true in all three params)
+        cb = blk.vtx[0]
+        vin = cb.vin[0]
+        vin.witness = [bytes(32)]  # witness reserved value (UpdateUncommittedBlockStructures)
+        cb.vin = [vin]
+        vtx = [cb] + list(blk.vtx[1:])
+        blk.vtx = vtx
+        wroot = blk.witness_merkle_root()
+        commit = _core.sha256d(wroot + bytes(32))
+        spk = WITNESS_COMMITMENT_HEADER + commit
+        cb.vout = list(cb.vout) + [_core.TxOut(0, spk)]
+        blk.vtx = [cb] + vtx[1:]
+        return spk
+
+
+class ExtraNonce:
+    """IncrementExtraNonce state (one per miner thread / GPU)."""
+
+    def __init__(self):
+        self.prev = None
+        self.n = 0
+
+    def increment(self, blk, height: int) -> int:
+        if self.prev != blk.header.prev:
+            self.n = 0
+            self.prev = blk.header.prev
+        self.n += 1
+        vtx = list(blk.vtx)
+        cb = vtx[0]
+        vin = cb.vin[0]
+        vin.script_sig = _core.script_push_int(height) + _core.script_push_data(_core.scriptnum(self.n))
+        if len(vin.script_sig) > 100:
+            raise ValueError("coinbase scriptSig too long")
+        cb.vin = [vin]
+        vtx[0] = cb
+        blk.vtx = vtx
+        hdr = blk.header
+        root, _ = blk.merkle_root()
+        hdr.merkle_root = root
+        blk.header = hdr
+        return self.n

@@ -1,0 +1,265 @@
+"""nodexad — the engine daemon (AppInit / AppInitMain / Shutdown equivalent).
+
+Parity: main -> AppInit (src/clore_blockchaind.cpp:66-198) -> AppInitMain
+(src/init.cpp:1322-1966): parse args + config file, select network, lock the
+data directory, load the block index (here: rebuild from blk files), start the
+RPC server (warm-up until the chain is loaded), start the miner when -gen,
+wait for shutdown; Interrupt/Shutdown (src/init.cpp:172,355).
+
+MI355X specifics: `-gpus=0,1,...` selects the devices the miner and the batch
+verifier use (one DAG per device, built on the GPU); `-kawpowactivationtime`
+overrides the activation (regtest default: genesis+1, so regtest blocks are
+KawPow — the reference's 2083 default would mine X16RV2); `-equihash=<time>`
+enables the Equihash(200,9) extension from that time (off by default).
+
+    python -m nodexa_chain_core_amd.node -regtest -rpcport=19443 -miningaddress=<addr> [-gpus=0]
+"""
+from __future__ import annotations
+
+import fcntl
+import os
+import signal
+import sys
+import threading
+import time
+
+from . import core
+from .chain.state import ChainState, make_params
+from .miner.assembler import BlockAssembler, ExtraNonce
+from .miner.kawpow_miner import CpuKawpowBackend, GpuKawpowBackend, MinerController
+from .rpc import methods
+from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
+from .utils import log
+from .utils.config import ArgsManager, gpu_list
+
+_core = core()
+
+
+class Node:
+    def __init__(self, args: ArgsManager):
+        self.args = args
+        self.network = args.network
+        act = args.get("kawpowactivationtime")
+        eq = args.get("equihash")
+        self.params = make_params(self.network, int(act) if act is not None else None,
+                                  int(eq) if eq not in (None, "", "1") else None)
+        self.datadir = args.data_dir() if args.get("datadir") is not None or not args.get_bool("nodatadir") else None
+        self._lock_file = None
+        self._shutdown = threading.Event()
+        self.last_block_tx = 0
+        self.last_block_weight = 0
+        self.pprpc_templates: dict[str, object] = {}
+        self._last_pprpc: tuple[str, float] | None = None
+        self.gpus = gpu_list(args)
+        self.state: ChainState | None = None
+        self.miner: MinerController | None = None
+        self.rpc: RPCServer | None = None
+        self.table = RPCTable()
+        addr = args.get("miningaddress")
+        self.mining_script = None
+        if addr:
+            self.mining_script = _core.address_to_script(addr, self.params.pubkey_prefix, self.params.script_prefix)
+            if self.mining_script is None:
+                raise SystemExit(f"Error: invalid -miningaddress {addr} for {self.network}")
+
+    # ------------------------------------------------------------------ lifecycle
+    def lock_datadir(self) -> None:
+        if self.datadir is None:
+            return
+        path = os.path.join(self.datadir, ".lock")
+        self._lock_file = open(path, "a+")
+        try:
+            fcntl.flock(self._lock_file, fcntl.LOCK_EX | fcntl.LOCK_NB)
+        except OSError:
+            raise SystemExit(f"Cannot obtain a lock on data directory {self.datadir}. Nodexa is probably already running.")
+
+    def start(self) -> None:
+        a = self.args
+        log.configure(a.get_list("debug"), a.get_list("debugexclude"),
+                      os.path.join(self.datadir, "debug.log") if self.datadir else None,
+                      console=a.get_bool("printtoconsole", True))
+        self.lock_datadir()
+        # RPC comes up first in warm-up mode (AppInitServers)
+        self.table.warmup = "Loading block index..."
+        methods.register(self.table, self)
+        if a.get_bool("server", True):
+            self._start_rpc()
+        self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False))
+        backends = []
+        for d in self.gpus:
+            backends.append(GpuKawpowBackend(d, a.get_int("gpuintensity", 1 << 22)))
+        if not backends:
+            backends.append(CpuKawpowBackend(a.get_int("genproclimit", 1)))
+        self.miner = MinerController(self.state, backends)
+        self.table.warmup = None
+        log.log_printf(f"nodexad started: network={self.network} height={self.state.height()} "
+                       f"kawpow_activation={self.params.kawpow_activation_time} gpus={self.gpus or 'none'}")
+        if a.get_bool("gen", False) and self.network != "regtest":
+            self.miner.set_generate(True, self.mining_script)
+
+    def _start_rpc(self) -> None:
+        a = self.args
+        creds = []
+        user, pw = a.get("rpcuser"), a.get("rpcpassword")
+        if user and pw:
+            creds.append(f"{user}:{pw}")
+        elif self.datadir is not None:
+            creds.append(make_cookie(self.datadir))
+        port = a.get_int("rpcport", self.params.default_rpc_port)
+        host = a.get("rpcbind", "127.0.0.1")
+        self.rpc = RPCServer(self.table, host, port, creds, a.get_int("rpcworkqueue", 16), rest=self.rest)
+        self.rpc.start()
+        log.log_printf(f"RPC listening on {host}:{self.rpc.port}")
+
+    def request_shutdown(self) -> None:
+        self._shutdown.set()
+
+    def shutdown_requested(self) -> bool:
+        return self._shutdown.is_set()
+
+    def wait(self) -> None:
+        while not self._shutdown.wait(0.5):
+            pass
+
+    def stop(self) -> None:
+        if getattr(self, "_stopped", False):
+            return
+        self._stopped = True
+        if self.miner is not None:
+            self.miner.stop()
+        if self.rpc is not None:
+            self.rpc.stop()
+        if self.datadir is not None:
+            delete_cookie(self.datadir)
+        if self._lock_file is not None:
+            fcntl.flock(self._lock_file, fcntl.LOCK_UN)
+            self._lock_file.close()
+            self._lock_file = None
+        log.log_printf("Shutdown: done")
+
+    # ------------------------------------------------------------------ helpers used by RPCs
+    def peer_count(self) -> int:
+        return 0  # P2P networking is out of the engine's scope (DEFER)
+
+    def blocks_size_on_disk(self) -> int:
+        if self.datadir is None:
+            return 0
+        bdir = os.path.join(self.datadir, "blocks")
+        return sum(os.path.getsize(os.path.join(bdir, f)) for f in os.listdir(bdir)) if os.path.isdir(bdir) else 0
+
+    def template_for_gbt(self):
+        script = self.mining_script or bytes([0x51])  # OP_TRUE when no -miningaddress (src/rpc/mining.cpp:550-563)
+        tpl = BlockAssembler(self.state).create_new_block(script)
+        ExtraNonce().increment(tpl.block, tpl.height)
+        return tpl
+
+    def register_pprpc_template(self, tpl) -> str:
+        """mapHVNKAWBlockTemplates: reuse the last header for 30 s (src/rpc/mining.cpp:722-739)."""
+        if self._last_pprpc is not None:
+            hh, t0 = self._last_pprpc
+            old = self.pprpc_templates.get(hh)
+            if old is not None and old.block.header.prev == tpl.block.header.prev and tpl.block.header.time - 30 < old.block.header.time:
+                return hh
+        hh = _core.u256_hex(tpl.block.header.kawpow_header_hash())
+        self.pprpc_templates[hh] = tpl
+        self._last_pprpc = (hh, time.time())
+        if len(self.pprpc_templates) > 64:
+            for k in list(self.pprpc_templates)[:-64]:
+                self.pprpc_templates.pop(k, None)
+        return hh
+
+    def gpu_info(self) -> list[dict]:
+        out = []
+        for be in (self.miner.backends if self.miner else []):
+            if getattr(be, "name", "") != "gpu":
+                continue
+            info = {"device": be.device, "epochs_resident": sorted(be.epochs.keys()), "intensity": be.intensity}
+            try:
+                from .ops import runtime
+
+                info.update(runtime.hip().device_props(be.device))
+            except Exception as e:  # pragma: no cover
+                info["error"] = str(e)
+            out.append(info)
+        return out
+
+    def gpu_memory_info(self) -> list[dict]:
+        out = []
+        if not self.gpus:
+            return out
+        import torch
+
+        for d in self.gpus:
+            free, total = torch.cuda.mem_get_info(d)
+            out.append({"device": d, "free": free, "total": total})
+        return out
+
+    def verify_headers(self, headers) -> list[dict]:
+        """Full PoW verification of a header batch (models/verify.py picks GPU or CPU)."""
+        from .models import verify
+
+        return verify.verify_headers(self.params, headers, gpus=self.gpus)
+
+    def equihash_solve(self, inp: bytes) -> list[list[int]]:
+        if self.gpus:
+            from .ops.equihash import EquihashSolver
+
+            import torch
+
+            with torch.cuda.device(self.gpus[0]):
+                s = EquihashSolver(num_inst=1, device=self.gpus[0])
+                return s.solve([inp])[0]
+        from .models.equihash import solve_cpu
+
+        return solve_cpu(inp)
+
+    def rest(self, path: str):
+        """REST subset: /rest/chaininfo.json, /rest/block/<hash>.{hex,bin}, /rest/headers/<n>/<hash>.hex."""
+        import json
+
+        parts = path.split("?")[0].split("/")[2:]
+        if parts == ["chaininfo.json"]:
+            tip = self.state.tip()
+            body = json.dumps({"chain": self.network, "blocks": tip.height, "bestblockhash": _core.u256_hex(tip.hash)})
+            return 200, "application/json", body.encode()
+        if len(parts) == 2 and parts[0] == "block":
+            h, _, fmt = parts[1].partition(".")
+            raw = self.state.get_block_raw(_core.u256_from_hex(h))
+            if raw is None:
+                return 404, "text/plain", b"block not found"
+            return (200, "application/octet-stream", raw) if fmt == "bin" else (200, "text/plain", raw.hex().encode())
+        if len(parts) == 3 and parts[0] == "headers":
+            n = int(parts[1])
+            h, _, fmt = parts[2].partition(".")
+            idx = self.state.chain.find(_core.u256_from_hex(h))
+            out = b""
+            while idx is not None and n > 0:
+                out += idx.header.serialize(self.params.kawpow_activation_time)
+                idx = self.state.chain.at_height(idx.height + 1)
+                n -= 1
+            return (200, "application/octet-stream", out) if fmt == "bin" else (200, "text/plain", out.hex().encode())
+        return 404, "text/plain", b"unknown REST path"
+
+
+def main(argv: list[str] | None = None) -> int:
+    args = ArgsManager()
+    rest = args.parse_parameters(sys.argv[1:] if argv is None else argv)
+    if rest:
+        print(f"Error: unexpected arguments {rest}", file=sys.stderr)
+        return 1
+    conf = args.get("conf", "nodexa.conf")
+    if args.get("datadir"):
+        args.read_config_file(os.path.join(os.path.expanduser(args.get("datadir")), conf))
+    node = Node(args)
+    signal.signal(signal.SIGTERM, lambda *_: node.request_shutdown())
+    signal.signal(signal.SIGINT, lambda *_: node.request_shutdown())
+    node.start()
+    try:
+        node.wait()
+    finally:
+        node.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

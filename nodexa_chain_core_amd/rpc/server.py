@@ -1,0 +1,222 @@
+"""HTTP/1.1 JSON-RPC server with the reference's request semantics.
+
+Parity:
+  * HTTP front-end with a bounded work queue and N worker threads
+    (src/httpserver.cpp:68-460, -rpcworkqueue / -rpcthreads, 503 "Work queue
+    depth exceeded" when full), persistent connections.
+  * Basic auth against -rpcuser/-rpcpassword or the `.cookie` file
+    (src/httprpc.cpp:128, RPCAuthorized; GenerateAuthCookie).
+  * Single and batch requests (JSONRPCExecBatch, src/rpc/server.cpp:501),
+    error -> HTTP status mapping (JSONErrorReply), warm-up gate (RPC_IN_WARMUP).
+  * CRPCTable: category/name/handler/arg names, `help`, positional and named
+    parameters (src/rpc/server.cpp:379-560).
+The daemon runs this in-process next to the chain state and the GPU miner.
+"""
+from __future__ import annotations
+
+import base64
+import hmac
+import http.server
+import json
+import os
+import queue
+import secrets
+import socketserver
+import threading
+import time
+from dataclasses import dataclass
+from typing import Callable
+
+from ..utils import log
+from .protocol import (RPC_IN_WARMUP, RPC_INTERNAL_ERROR, RPC_INVALID_PARAMETER, RPC_INVALID_REQUEST,
+                       RPC_METHOD_NOT_FOUND, RPC_PARSE_ERROR, RPCError, http_status_for, reply)
+
+
+@dataclass
+class RPCCommand:
+    category: str
+    name: str
+    handler: Callable
+    arg_names: tuple[str, ...]
+    help: str = ""
+
+
+class RPCTable:
+    def __init__(self) -> None:
+        self.commands: dict[str, RPCCommand] = {}
+        self.warmup: str | None = None
+        self.started = time.time()
+        self.active: dict[int, tuple[str, float]] = {}
+        self._lock = threading.Lock()
+
+    def append(self, category: str, name: str, handler: Callable, arg_names=(), help: str = "") -> None:
+        if name in self.commands:
+            raise ValueError(f"duplicate RPC {name}")
+        self.commands[name] = RPCCommand(category, name, handler, tuple(arg_names), help or (handler.__doc__ or ""))
+
+    def help(self, name: str | None = None) -> str:
+        if name:
+            c = self.commands.get(name)
+            if c is None:
+                return f"help: unknown command: {name}"
+            args = " ".join(f'"{a}"' for a in c.arg_names)
+            return f"{c.name} {args}\n\n{c.help.strip()}"
+        out, cat = [], None
+        for c in sorted(self.commands.values(), key=lambda c: (c.category, c.name)):
+            if c.category != cat:
+                cat = c.category
+                out.append(f"\n== {cat[0].upper() + cat[1:]} ==")
+            out.append(f"{c.name} " + " ".join(f'"{a}"' for a in c.arg_names))
+        return "\n".join(out).strip()
+
+    def execute(self, method: str, params) -> object:
+        if self.warmup is not None:
+            raise RPCError(RPC_IN_WARMUP, self.warmup)
+        cmd = self.commands.get(method)
+        if cmd is None:
+            raise RPCError(RPC_METHOD_NOT_FOUND, "Method not found")
+        if isinstance(params, dict):  # named arguments
+            unknown = set(params) - set(cmd.arg_names)
+            if unknown:
+                raise RPCError(RPC_INVALID_PARAMETER, f"Unknown named parameter {sorted(unknown)[0]}")
+            last = max((cmd.arg_names.index(k) for k in params), default=-1)
+            params = [params.get(a) for a in cmd.arg_names[:last + 1]]
+        elif params is None:
+            params = []
+        elif not isinstance(params, list):
+            raise RPCError(RPC_INVALID_REQUEST, "Params must be an array or object")
+        tid = threading.get_ident()
+        with self._lock:
+            self.active[tid] = (method, time.time())
+        try:
+            return cmd.handler(params)
+        finally:
+            with self._lock:
+                self.active.pop(tid, None)
+
+    def exec_request(self, req: dict) -> dict:
+        id_ = req.get("id") if isinstance(req, dict) else None
+        try:
+            if not isinstance(req, dict):
+                raise RPCError(RPC_INVALID_REQUEST, "Invalid Request object")
+            method = req.get("method")
+            if not isinstance(method, str):
+                raise RPCError(RPC_INVALID_REQUEST, "Method must be a string")
+            log.log_print("rpc", f"ThreadRPCServer method={method}")
+            return reply(self.execute(method, req.get("params")), None, id_)
+        except RPCError as e:
+            return reply(None, e.to_json(), id_)
+        except Exception as e:  # handler bug or runtime error -> RPC_MISC style
+            return reply(None, {"code": -1, "message": str(e)}, id_)
+
+
+class _Handler(http.server.BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+    server_version = "nodexa-json-rpc/0.1"
+
+    def log_message(self, fmt, *args):  # route to category logging
+        log.log_print("http", fmt % args)
+
+    def _send(self, status: int, body: bytes, ctype: str = "application/json") -> None:
+        self.send_response(status)
+        self.send_header("Content-Type", ctype)
+        self.send_header("Content-Length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+
+    def _authorized(self) -> bool:
+        auth = self.headers.get("Authorization", "")
+        if not auth.startswith("Basic "):
+            return False
+        try:
+            userpass = base64.b64decode(auth[6:].strip()).decode()
+        except Exception:
+            return False
+        return any(hmac.compare_digest(userpass, c) for c in self.server.credentials)
+
+    def do_POST(self):  # noqa: N802
+        srv: RPCHTTPServer = self.server
+        if srv.credentials and not self._authorized():
+            log.log_printf(f"ThreadRPCServer incorrect password attempt from {self.client_address[0]}")
+            time.sleep(0.25)
+            self.send_response(401)
+            self.send_header("WWW-Authenticate", 'Basic realm="jsonrpc"')
+            self.send_header("Content-Length", "0")
+            self.end_headers()
+            return
+        if not srv.slots.acquire(blocking=False):
+            self._send(503, b"Work queue depth exceeded", "text/plain")
+            return
+        try:
+            length = int(self.headers.get("Content-Length", "0"))
+            raw = self.rfile.read(length)
+            try:
+                req = json.loads(raw)
+            except ValueError:
+                body = json.dumps(reply(None, {"code": RPC_PARSE_ERROR, "message": "Parse error"}, None))
+                self._send(500, body.encode())
+                return
+            if isinstance(req, list):
+                body = json.dumps([srv.table.exec_request(r) for r in req])
+                self._send(200, body.encode())
+                return
+            rep = srv.table.exec_request(req)
+            status = 200 if rep["error"] is None else http_status_for(rep["error"]["code"])
+            self._send(status, json.dumps(rep).encode())
+        finally:
+            srv.slots.release()
+
+    def do_GET(self):  # noqa: N802
+        # REST subset (src/rest.cpp:569-580): /rest/chaininfo.json
+        if self.path.startswith("/rest/") and self.server.rest is not None:
+            try:
+                status, ctype, body = self.server.rest(self.path)
+            except Exception as e:
+                status, ctype, body = 400, "text/plain", str(e).encode()
+            self._send(status, body, ctype)
+            return
+        self._send(405, b"JSONRPC server handles only POST requests", "text/plain")
+
+
+class RPCHTTPServer(socketserver.ThreadingMixIn, http.server.HTTPServer):
+    daemon_threads = True
+    allow_reuse_address = True
+
+    def __init__(self, addr, table: RPCTable, credentials: list[str], work_queue: int, rest=None):
+        super().__init__(addr, _Handler)
+        self.table = table
+        self.credentials = credentials
+        self.slots = threading.BoundedSemaphore(max(1, work_queue))
+        self.rest = rest
+
+
+def make_cookie(datadir: str) -> str:
+    """GenerateAuthCookie: `__cookie__:<64 hex>` in <datadir>/.cookie (0600)."""
+    token = "__cookie__:" + secrets.token_hex(32)
+    path = os.path.join(datadir, ".cookie")
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    with os.fdopen(fd, "w") as f:
+        f.write(token)
+    return token
+
+
+def delete_cookie(datadir: str) -> None:
+    try:
+        os.unlink(os.path.join(datadir, ".cookie"))
+    except OSError:
+        pass
+
+
+class RPCServer:
+    def __init__(self, table: RPCTable, host: str, port: int, credentials: list[str], work_queue: int = 16,
+                 rest=None):
+        self.httpd = RPCHTTPServer((host, port), table, credentials, work_queue, rest)
+        self.port = self.httpd.server_address[1]
+        self.thread = threading.Thread(target=self.httpd.serve_forever, name="http", daemon=True)
+
+    def start(self) -> None:
+        self.thread.start()
+
+    def stop(self) -> None:
+        self.httpd.shutdown()
+        self.httpd.server_close()

@@ -1,0 +1,166 @@
+"""End-to-end node on regtest (CPU PoW backend): JSON-RPC server + client,
+KawPow mining through generate / getblocktemplate+pprpcsb / submitblock,
+blk-file persistence and reload. Mirrors the reference's functional tests
+(test/functional: mining_basic, mining_getblocktemplate_longpoll, rpc_*)."""
+import json
+import os
+import struct
+import threading
+
+import pytest
+
+
+@pytest.fixture()
+def node_factory(core, tmp_path):
+    from nodexa_chain_core_amd.node import Node
+    from nodexa_chain_core_amd.utils.config import ArgsManager
+
+    nodes = []
+
+    def make(extra=()):
+        addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
+        args = ArgsManager()
+        args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+                               f"-miningaddress={addr}", "-printtoconsole=0", *extra])
+        n = Node(args)
+        n.start()
+        nodes.append(n)
+        return n, addr
+
+    yield make
+    for n in nodes:
+        n.stop()
+
+
+def client(node):
+    from nodexa_chain_core_amd.rpc.client import RPCClient
+
+    return RPCClient("127.0.0.1", node.rpc.port, "u", "p")
+
+
+def test_generate_and_query(core, node_factory):
+    node, addr = node_factory()
+    c = client(node)
+    assert c.getblockcount() == 0
+    hashes = c.generatetoaddress(3, addr)
+    assert len(hashes) == 3 and c.getblockcount() == 3
+    assert c.getbestblockhash() == hashes[-1]
+    assert c.getblockhash(3) == hashes[-1]
+    blk = c.getblock(hashes[0])
+    assert blk["height"] == 1 and blk["nTx"] == 1 and blk["confirmations"] == 3
+    assert {"headerhash", "mixhash", "nonce64"} <= set(blk)  # KawPow fields (src/rpc/blockchain.cpp:254-256)
+    hdr = c.getblockheader(hashes[1])
+    assert hdr["previousblockhash"] == hashes[0] and hdr["nextblockhash"] == hashes[2]
+    raw = bytes.fromhex(c.getblock(hashes[0], 0))
+    p = node.params
+    b = core.Block.deserialize(raw, p.kawpow_activation_time)
+    # coinbase: miner + community-autonomous output + witness commitment
+    cb = b.vtx[0]
+    sub = core.block_subsidy(1)
+    assert cb.vout[1].value == sub * p.community_autonomous_pct // 100
+    assert core.script_to_address(cb.vout[1].script_pubkey, p.pubkey_prefix, p.script_prefix) == \
+        p.community_autonomous_address
+    # getkawpowhash agrees with the stored header
+    res = c.getkawpowhash(blk["headerhash"], blk["mixhash"], "%016x" % blk["nonce64"], 1, "7f" + "ff" * 31)
+    assert res["result"] == "true" and res["meets_target"] == "true" and res["digest"] == hashes[0]
+    info = c.getmininginfo()
+    assert info["blocks"] == 3 and info["chain"] == "regtest"
+    assert c.submitblock(raw.hex()) == "duplicate"
+    assert c.call("verifychain", 4, 3) is True
+
+
+def test_gbt_pprpcsb_roundtrip(core, node_factory):
+    node, addr = node_factory()
+    c = client(node)
+    tpl = c.getblocktemplate({"rules": ["segwit"]})
+    for k in ("previousblockhash", "coinbasevalue", "CommunityAutonomousAddress", "CommunityAutonomousValue", "target",
+              "bits", "height", "pprpcheader", "pprpcepoch", "default_witness_commitment", "longpollid"):
+        assert k in tpl, k
+    # an external miner: search nNonce64 for the template's KawPow header hash
+    header_hash = bytes.fromhex(tpl["pprpcheader"])
+    boundary = bytes.fromhex(tpl["target"])
+    ctx = core.get_epoch_context(tpl["pprpcepoch"])
+    ok, nonce, fin, mix = core.kawpow_search_light(ctx, tpl["height"], header_hash, boundary, 0, 1000)
+    assert ok
+    assert c.pprpcsb(tpl["pprpcheader"], mix.hex(), "%016x" % nonce) is True
+    assert c.getblockcount() == 1
+    with pytest.raises(RuntimeError, match="not found"):
+        c.pprpcsb("00" * 32, mix.hex(), "%016x" % nonce)
+
+
+def test_submitblock_rejects(core, node_factory):
+    node, addr = node_factory()
+    c = client(node)
+    from nodexa_chain_core_amd.miner.assembler import BlockAssembler
+
+    tpl = BlockAssembler(node.state).create_new_block(node.mining_script)
+    blk = tpl.block
+    act = node.params.kawpow_activation_time
+    # wrong community amount -> bad-cb-community-autonomous-amount
+    bad = core.Block.deserialize(blk.serialize(act), act)
+    cb = bad.vtx[0]
+    outs = list(cb.vout)
+    outs[1] = core.TxOut(outs[1].value + 1, outs[1].script_pubkey)
+    cb.vout = outs
+    bad.vtx = [cb]
+    h = bad.header
+    h.merkle_root = bad.merkle_root()[0]
+    bad.header = h
+    assert c.submitblock(bad.serialize(act).hex()) == "bad-cb-community-autonomous-amount"
+    # merkle mismatch
+    bad2 = core.Block.deserialize(blk.serialize(act), act)
+    h = bad2.header
+    h.merkle_root = bytes(32)
+    bad2.header = h
+    assert c.submitblock(bad2.serialize(act).hex()) == "bad-txnmrklroot"
+    # unsolved header -> high-hash (regtest target is 2^255: pick a failing nonce)
+    ctx = core.get_epoch_context(0)
+    h = blk.header
+    for n in range(64):
+        h.nonce64 = n
+        fin, mix = core.kawpow_hash(ctx, h.height, h.kawpow_header_hash()[::-1], n)
+        if fin[0] >= 0x80:
+            h.mix_hash = mix[::-1]
+            break
+    blk.header = h
+    assert c.submitblock(blk.serialize(act).hex()) == "high-hash"
+
+
+def test_restart_reloads_blocks(core, node_factory, tmp_path):
+    node, addr = node_factory()
+    c = client(node)
+    hashes = c.generatetoaddress(2, addr)
+    node.stop()
+    # blk file framing: magic, size, block (src/validation.cpp:1275-1294)
+    raw = open(os.path.join(str(tmp_path), "regtest", "blocks", "blk00000.dat"), "rb").read()
+    assert raw[:4] == b"DROW"
+    n2, _ = node_factory()
+    c2 = client(n2)
+    assert c2.getblockcount() == 2 and c2.getbestblockhash() == hashes[-1]
+
+
+def test_rpc_protocol_errors(node_factory):
+    node, _ = node_factory()
+    c = client(node)
+    status, rep = c.call_raw({"method": "nosuchmethod", "params": [], "id": 7})
+    assert status == 404 and rep["error"]["code"] == -32601 and rep["id"] == 7
+    rep = c.batch([("getblockcount", []), ("getblockhash", [99])])
+    assert rep[0]["result"] == 0 and rep[1]["error"]["code"] == -8
+    from nodexa_chain_core_amd.rpc.client import RPCClient
+
+    bad = RPCClient("127.0.0.1", node.rpc.port, "u", "wrong")
+    with pytest.raises(PermissionError):
+        bad.getblockcount()
+    assert "getblocktemplate" in c.help()
+    # named parameters
+    status, rep = c.call_raw({"method": "getblockhash", "params": {"height": 0}, "id": 1})
+    assert rep["result"] == c.getbestblockhash()
+
+
+def test_cli_main(node_factory, capsys, tmp_path):
+    node, _ = node_factory()
+    from nodexa_chain_core_amd.rpc.client import main
+
+    rc = main(["-regtest", f"-datadir={tmp_path}", f"-rpcport={node.rpc.port}", "-rpcuser=u", "-rpcpassword=p",
+               "getblockcount"])
+    assert rc == 0 and capsys.readouterr().out.strip() == "0"
