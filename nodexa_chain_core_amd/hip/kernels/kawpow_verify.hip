@@ -83,6 +83,9 @@ extern "C" __global__ __launch_bounds__(256) void kawpow_verify_batch(KawpowVeri
     const uint32_t lane = threadIdx.x & 15;
     const uint32_t job = blockIdx.x * 256 + threadIdx.x;
     const uint32_t slab = __builtin_amdgcn_readfirstlane(job >> 6);
+    // num_jobs is a multiple of 64, so this exit is wave-uniform; waves past the
+    // last slab must not index job_program (it has num_jobs / 64 entries).
+    if (slab >= (p.num_jobs >> 6)) return;
     const uint32_t* prog = p.programs + (size_t)p.job_program[slab] * KV_PROG_WORDS;
     const bool valid = job < p.num_jobs;
     const KawpowVerifyJob j = p.jobs[valid ? job : 0];

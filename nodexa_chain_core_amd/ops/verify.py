@@ -57,6 +57,8 @@ def gpu_full_hash(block_numbers: list[int], header_hashes: list[bytes], nonces: 
                 padded = members + [-1] * ((-len(members)) % 64)
                 order.extend(padded)
                 slab_prog.extend([pi] * (len(padded) // 64))
+            # the kernel indexes job_program[slot // 64] and programs[job_program * 64]
+            assert len(slab_prog) * 64 == len(order) and max(slab_prog) < len(programs) // 64
             buf = bytearray(JOB.size * len(order))
             for slot, i in enumerate(order):
                 if i >= 0:

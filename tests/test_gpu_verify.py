@@ -1,0 +1,63 @@
+"""GPU batch verification (program-as-data kernel) and the node's GPU miner."""
+import random
+
+import pytest
+
+from kawpow_vectors import VECTORS
+
+pytestmark = pytest.mark.gpu
+
+
+def test_verify_batch_multi_period_vs_cpu(core, gpu):
+    from nodexa_chain_core_amd.ops.verify import gpu_full_hash
+
+    rng = random.Random(5)
+    blocks = [rng.randrange(0, 7500) for _ in range(150)] + [7, 8, 9]  # many periods, epoch 0
+    headers = [rng.randbytes(32) for _ in blocks]
+    nonces = [rng.getrandbits(64) for _ in blocks]
+    res = gpu_full_hash(blocks, headers, nonces, device=0)
+    ctx = core.get_epoch_context(0)
+    for i in range(0, len(blocks), 7):
+        assert res[i] == core.kawpow_hash(ctx, blocks[i], headers[i], nonces[i]), i
+
+
+def test_verify_batch_reference_vectors(core, gpu):
+    from nodexa_chain_core_amd.ops.verify import gpu_full_hash
+
+    vecs = [v for v in VECTORS if v[0] < 7500]
+    res = gpu_full_hash([v[0] for v in vecs], [bytes.fromhex(v[1]) for v in vecs], [int(v[2], 16) for v in vecs],
+                        device=0)
+    for (block, _, _, mix, final), (f, m) in zip(vecs, res):
+        assert (m.hex(), f.hex()) == (mix, final), block
+
+
+def test_node_gpu_mining_and_batch_verify(core, gpu, tmp_path):
+    from nodexa_chain_core_amd.models.verify import verify_headers
+    from nodexa_chain_core_amd.node import Node
+    from nodexa_chain_core_amd.rpc.client import RPCClient
+    from nodexa_chain_core_amd.utils.config import ArgsManager
+
+    addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
+    args = ArgsManager()
+    args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+                           f"-miningaddress={addr}", "-printtoconsole=0", "-gpus=0", "-gpuintensity=65536"])
+    node = Node(args)
+    node.start()
+    try:
+        c = RPCClient("127.0.0.1", node.rpc.port, "u", "p")
+        hashes = c.generatetoaddress(5, addr)
+        assert c.getblockcount() == 5
+        info = c.getgpuinfo()
+        assert info and info[0]["device"] == 0 and 0 in info[0]["epochs_resident"]
+        hdrs = [node.state.chain.at_height(h).header for h in range(1, 6)]
+        gpu_res = verify_headers(node.params, hdrs, gpus=[0])
+        cpu_res = verify_headers(node.params, hdrs, gpus=None)
+        assert all(r["valid"] for r in gpu_res) and gpu_res == cpu_res
+        assert [r["hash"] for r in gpu_res] == hashes
+        bad = core.BlockHeader.deserialize(hdrs[0].serialize(node.params.kawpow_activation_time),
+                                           node.params.kawpow_activation_time)
+        bad.nonce64 ^= 1
+        r = verify_headers(node.params, [bad], gpus=[0])[0]
+        assert not r["valid"]
+    finally:
+        node.stop()
