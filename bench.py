@@ -28,17 +28,22 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-BASELINE_MHS = None  # filled from BASELINE.json "published" if present
-
-
-def _baseline() -> float | None:
+def _baseline() -> tuple[float | None, str | None]:
+    """The reference publishes no KawPow number. Use a published one if
+    BASELINE.json ever gains it, else the reference's own progpow::search measured on
+    this container's 8-core host (tools/ref_cpu_baseline.sh -> profiles/ref_cpu_baseline/)."""
     try:
         with open(os.path.join(ROOT, "BASELINE.json")) as f:
-            pub = json.load(f).get("published") or {}
-        v = pub.get("kawpow_mhs")
-        return float(v) if v else None
+            v = (json.load(f).get("published") or {}).get("kawpow_mhs")
+        if v:
+            return float(v), "BASELINE.json published.kawpow_mhs"
     except (OSError, ValueError):
-        return None
+        pass
+    try:
+        with open(os.path.join(ROOT, "profiles", "ref_cpu_baseline", "epoch384.json")) as f:
+            return float(json.load(f)["mhs"]), "reference progpow::search, 8-core host, epoch 384 (BASELINE.md)"
+    except (OSError, ValueError, KeyError):
+        return None, None
 
 
 def main() -> int:
@@ -155,7 +160,7 @@ def main() -> int:
         log(f"[bench] Equihash(200,9): {eq_sols} Sol/s ({args.equihash} x 8 solves per rank)")
 
     if rank == 0:
-        base = _baseline()
+        base, base_src = _baseline()
         out = {
             "metric": "KawPow MH/s + Equihash(200,9) Sol/s, whole node at 1/2/4/8 MI355X",
             "value": round(mhs, 3),
@@ -168,7 +173,8 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(mhs / base, 3) if base else None,
             "dtype": "u32",
-            "data": "synthetic regtest header, random-init epoch DAG (no chain data)",
+            "data": "synthetic regtest header + sequential nonces; the real epoch DAG generated on the GPU "
+                    "(no chain data)",
             "config": {
                 "model": f"KawPow (ProgPoW 0.9.4, RAVENCOINKAWPOW) epoch {args.epoch}, "
                          f"{ep.dag_bytes/2**30:.2f} GiB DAG, height {height}",
@@ -179,6 +185,8 @@ def main() -> int:
             "shares_last_step": len(shares),
             "dag_build_s": round(dag_s, 3),
             "equihash_sol_per_s": eq_sols,
+            "baseline_mhs": base,
+            "baseline_source": base_src,
         }
         for k, v in list(out.items()) + [("config." + a, b) for a, b in out["config"].items()]:
             if isinstance(v, (bytes, bytearray)):

@@ -8,18 +8,27 @@
 //
 // CDNA4 mapping
 //   * one ProgPoW lane per thread; a 16-thread group is one hash; a wave64 runs
-//     4 hashes side by side. Each thread owns one nonce: it computes that
-//     nonce's keccak-f800 seed, then its group walks the group's 16 nonces one
-//     after another (the keccak cost is paid once per nonce, not 16x).
-//   * the 32 mix registers are named scalars (m0..m31): with the program baked
-//     in, every index is a literal and the state never leaves VGPRs.
+//     4 groups side by side. Each thread owns one nonce: it computes that
+//     nonce's keccak-f800 seed, then its group walks the group's 16 nonces
+//     (the keccak cost is paid once per nonce, not 16x).
+//   * the hash is a chain of 64 dependent DAG gathers (round r+1's address
+//     depends on round r's DAG merge into mix[0]), so throughput is set by how
+//     many gathers are in flight per SIMD (Little's law on HBM latency), not by
+//     ALU. A group therefore interleaves KP_HASHES independent hashes of its 16
+//     (KP_HASHES x 32 mix VGPRs): KP_HASHES gathers are issued back to back at
+//     round start and the KP_HASHES programs give the scheduler independent
+//     chains to fill the latency with.
+//   * the mix registers are arrays subscripted only by literals (the emitted
+//     program bakes every index in), so they are scalarised into VGPRs.
+//   * everything not needed inside the round loop leaves the VGPR file: the 8
+//     digest words go to LDS as each hash finishes, and the keccak state words
+//     2..7 are recomputed for the final absorb instead of being held live.
 //   * the 16 KiB L1 (first 64 DAG items) sits in LDS; cache ops are
 //     ds_read_b32 with a 12-bit masked address.
 //   * each round's 256-byte DAG item is one coalesced 16 B/lane load by the
-//     group (lane l takes words ((l^r)%16)*4..+3), issued at round start and
-//     consumed at round end, so the 29 cache/math ops hide its HBM latency.
-//   * the round's item index is broadcast from lane r%16 with ds_bpermute
-//     (__shfl, width 16) and reduced with a FastMod32 multiply-shift.
+//     group (lane l takes words ((l^r)%16)*4..+3); the item index is broadcast
+//     from lane r%16 with ds_bpermute (__shfl, width 16) and reduced with a
+//     FastMod32 multiply-shift.
 #include "kernel_params.h"
 #include "keccak_device.hpp"
 
@@ -29,8 +38,15 @@
 #include KAWPOW_PROGRAM_HEADER
 
 // Tuning knobs (compile-time; ops/jit.py passes them as -D variants):
+//   KP_HASHES     hashes interleaved per 16-lane group (1, 2, 4 or 8)
 //   KP_MIN_WAVES  minimum waves per SIMD for __launch_bounds__ (caps VGPRs)
 //   KP_NT_DAG     non-temporal DAG loads (the 4 GiB DAG has no L2 reuse)
+#ifndef KP_HASHES
+#define KP_HASHES 2
+#endif
+#if (16 % KP_HASHES) != 0
+#error "KP_HASHES must divide 16"
+#endif
 #ifdef KP_MIN_WAVES
 #define KP_BOUNDS __launch_bounds__(NODEXA_KAWPOW_BLOCK, KP_MIN_WAVES)
 #else
@@ -45,10 +61,19 @@ NX_DEV uint4 kp_dag_load(const uint4* p) {
     return *p;
 #endif
 }
-#define KP_DAG_LOAD(p) kp_dag_load(p)
 
-#define KP_REGS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) \
-    X(15) X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
+// x*33 for the merge ops. Left to itself the compiler folds `a*33 + b` into
+// v_mad_u64_u32 (a multi-cycle integer MAD); KP_MUL33_SHIFT pins it to one
+// full-rate v_lshl_add_u32 (a<<5)+a, leaving the +b as a plain add.
+#ifdef KP_MUL33_SHIFT
+NX_DEV uint32_t kp_mul33(uint32_t a) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 5, %1" : "=v"(r) : "v"(a));
+    return r;
+}
+#else
+NX_DEV uint32_t kp_mul33(uint32_t a) { return a * 33u; }
+#endif
 
 NX_DEV uint32_t kp_clz(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : 32u; }
 NX_DEV uint32_t kp_fnv1a(uint32_t h, uint32_t d) { return (h ^ d) * 0x01000193u; }
@@ -115,35 +140,54 @@ NX_DEV void kp_final(const uint32_t st2[8], const uint32_t digest[8], uint32_t o
     for (int i = 0; i < 8; ++i) out[i] = s[i];
 }
 
-// Mix of one hash for the calling lane; returns this lane's FNV lane-hash.
-// `seed0/seed1` are the hash's keccak seed words, identical across the group.
-NX_DEV uint32_t kp_hash_lane(const uint4* __restrict__ dag, const FastMod32& items, const uint32_t* l1,
-                             uint32_t seed0, uint32_t seed1, uint32_t lane) {
-    const uint32_t z = kp_fnv1a(0x811c9dc5u, seed0);
-    const uint32_t w = kp_fnv1a(z, seed1);
-    const uint32_t jsr = kp_fnv1a(w, lane);
-    KpKiss rng{z, w, jsr, kp_fnv1a(jsr, lane)};
-#define KP_DECL(i) uint32_t m##i = rng.next();
-    KP_REGS(KP_DECL)
-#undef KP_DECL
-
+// The group's 16 hashes, KP_HASHES at a time. `st0/st1` are this thread's own
+// nonce seed words (hash h's seed lives in lane h). Each finished hash's 8
+// digest words are written to dig[h * 8 + k] (LDS, this group's 128 words).
+NX_DEV void kp_group_hashes(const uint4* __restrict__ dag, const FastMod32& items, const uint32_t* l1,
+                            uint32_t st0, uint32_t st1, uint32_t lane, uint32_t* dig) {
 #pragma unroll 1
-    for (uint32_t r = 0; r < 64; ++r) {
-        const uint32_t src = __shfl(m0, (int)(r & 15), 16);
-        const uint32_t index = kp_fastmod(src, items);
-        const uint4 d = KP_DAG_LOAD(dag + (size_t)index * 16 + ((lane ^ r) & 15));
-        KAWPOW_PROGRAM(l1);
-        KAWPOW_DAG_MERGE(d);
+    for (uint32_t h0 = 0; h0 < 16; h0 += KP_HASHES) {
+        uint32_t mx[KP_HASHES][32];
+#pragma unroll
+        for (int k = 0; k < KP_HASHES; ++k) {
+            const uint32_t s0 = __shfl(st0, (int)(h0 + k), 16);
+            const uint32_t s1 = __shfl(st1, (int)(h0 + k), 16);
+            const uint32_t z = kp_fnv1a(0x811c9dc5u, s0);
+            const uint32_t w = kp_fnv1a(z, s1);
+            const uint32_t jsr = kp_fnv1a(w, lane);
+            KpKiss rng{z, w, jsr, kp_fnv1a(jsr, lane)};
+#pragma unroll
+            for (int i = 0; i < 32; ++i) mx[k][i] = rng.next();
+        }
+#pragma unroll 1
+        for (uint32_t r = 0; r < 64; ++r) {
+            uint4 d[KP_HASHES];
+            const uint32_t part = (lane ^ r) & 15;
+#pragma unroll
+            for (int k = 0; k < KP_HASHES; ++k) {
+                const uint32_t index = kp_fastmod(__shfl(mx[k][0], (int)(r & 15), 16), items);
+                d[k] = kp_dag_load(dag + (size_t)index * 16 + part);
+            }
+#pragma unroll
+            for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM(l1, mx[k]);
+#pragma unroll
+            for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < KP_HASHES; ++k) {
+            uint32_t lh = 0x811c9dc5u;
+#pragma unroll
+            for (int i = 0; i < 32; ++i) lh = kp_fnv1a(lh, mx[k][i]);
+            // digest[j] = fnv1a(fnv1a(basis, lane_hash[j]), lane_hash[j + 8]); lanes 0..7 own j
+            const uint32_t hi = __shfl(lh, (int)(lane + 8), 16);
+            if (lane < 8) dig[(h0 + k) * 8 + lane] = kp_fnv1a(kp_fnv1a(0x811c9dc5u, lh), hi);
+        }
     }
-    uint32_t h = 0x811c9dc5u;
-#define KP_RED(i) h = kp_fnv1a(h, m##i);
-    KP_REGS(KP_RED)
-#undef KP_RED
-    return h;
 }
 
 extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     __shared__ uint32_t l1[4096];
+    __shared__ uint32_t digs[NODEXA_KAWPOW_BLOCK * 8];
     {
         const uint4* src = (const uint4*)p.dag;
         uint4* dst = (uint4*)l1;
@@ -154,25 +198,17 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
 
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t nonce = p.start_nonce + (uint64_t)blockIdx.x * NODEXA_KAWPOW_BLOCK + threadIdx.x;
-    uint32_t st2[8];
-    kp_seed(p.header, nonce, st2);
-
-    uint32_t digest[8];
-#pragma unroll 1
-    for (uint32_t h = 0; h < 16; ++h) {
-        const uint32_t s0 = __shfl(st2[0], (int)h, 16);
-        const uint32_t s1 = __shfl(st2[1], (int)h, 16);
-        const uint32_t lh = kp_hash_lane((const uint4*)p.dag, p.items, l1, s0, s1, lane);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t a = __shfl(lh, k, 16);
-            const uint32_t b = __shfl(lh, k + 8, 16);
-            const uint32_t v = kp_fnv1a(kp_fnv1a(0x811c9dc5u, a), b);
-            if (h == lane) digest[k] = v;
-        }
+    uint32_t* dig = digs + (threadIdx.x & ~15u) * 8;
+    {
+        uint32_t st2[8];
+        kp_seed(p.header, nonce, st2);
+        kp_group_hashes((const uint4*)p.dag, p.items, l1, st2[0], st2[1], lane, dig);
     }
-
-    uint32_t fin[8];
+    __syncthreads();
+    uint32_t st2[8], digest[8], fin[8];
+    kp_seed(p.header, nonce, st2);  // recomputed: cheaper than 6 VGPRs held across the mix loop
+#pragma unroll
+    for (int k = 0; k < 8; ++k) digest[k] = dig[lane * 8 + k];
     kp_final(st2, digest, fin);
     const uint64_t head = ((uint64_t)__builtin_bswap32(fin[0]) << 32) | __builtin_bswap32(fin[1]);
     if (head <= p.target) {
@@ -193,6 +229,7 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
 // all share this period and epoch. One job per thread, grouped as in search.
 extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     __shared__ uint32_t l1[4096];
+    __shared__ uint32_t digs[NODEXA_KAWPOW_BLOCK * 8];
     {
         const uint4* src = (const uint4*)p.dag;
         uint4* dst = (uint4*)l1;
@@ -203,23 +240,14 @@ extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     const uint32_t job = blockIdx.x * NODEXA_KAWPOW_BLOCK + threadIdx.x;
     const bool valid = job < p.num_jobs;
     const KawpowVerifyJob j = p.jobs[valid ? job : 0];
+    uint32_t* dig = digs + (threadIdx.x & ~15u) * 8;
     uint32_t st2[8];
     kp_seed(j.header, j.nonce, st2);
-    uint32_t digest[8];
-#pragma unroll 1
-    for (uint32_t h = 0; h < 16; ++h) {
-        const uint32_t s0 = __shfl(st2[0], (int)h, 16);
-        const uint32_t s1 = __shfl(st2[1], (int)h, 16);
-        const uint32_t lh = kp_hash_lane((const uint4*)p.dag, p.items, l1, s0, s1, lane);
+    kp_group_hashes((const uint4*)p.dag, p.items, l1, st2[0], st2[1], lane, dig);
+    __syncthreads();
+    uint32_t digest[8], fin[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t a = __shfl(lh, k, 16);
-            const uint32_t b = __shfl(lh, k + 8, 16);
-            const uint32_t v = kp_fnv1a(kp_fnv1a(0x811c9dc5u, a), b);
-            if (h == lane) digest[k] = v;
-        }
-    }
-    uint32_t fin[8];
+    for (int k = 0; k < 8; ++k) digest[k] = dig[lane * 8 + k];
     kp_final(st2, digest, fin);
     if (valid) {
         uint32_t* o = p.out + (size_t)job * 16;

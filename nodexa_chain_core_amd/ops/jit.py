@@ -45,8 +45,10 @@ def _variant_tag(defines: tuple[str, ...]) -> str:
 
 
 def object_path(period: int, defines: tuple[str, ...] = ()) -> str:
+    # the key covers the template, the generated program text (codegen changes) and the variant
+    prog = hashlib.sha256(program_source(period).encode()).hexdigest()[:8]
     return os.path.join(os.path.abspath(CACHE_DIR),
-                        f"kawpow_p{period}_{_build.ARCH}_{_template_digest()}{_variant_tag(defines)}.hsaco")
+                        f"kawpow_p{period}_{_build.ARCH}_{_template_digest()}{prog}{_variant_tag(defines)}.hsaco")
 
 
 def program_source(period: int) -> str:

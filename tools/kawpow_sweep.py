@@ -52,6 +52,24 @@ def main() -> int:
         h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header, start, 0,
                                a.batch, stream)
 
+    # bit-exactness: every variant, target = all-pass, first shares re-hashed on the CPU
+    import struct
+
+    ctx = _core.get_epoch_context(a.epoch)
+    hh = bytes(header)
+    bad = 0
+    for v in variants:
+        res.zero_()
+        h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header, 1000, (1 << 64) - 1,
+                               4096, stream)
+        raw = res.cpu().numpy().tobytes()
+        n = min(struct.unpack_from("<I", raw, 0)[0], 64)
+        for i in range(min(n, 3)):
+            vals = struct.unpack_from("<Q8I8I", raw, 16 + i * 72)
+            fin, mix = _core.kawpow_hash(ctx, height, hh, vals[0])
+            ok = struct.pack("<8I", *vals[1:9]) == mix and struct.pack("<8I", *vals[9:17]) == fin
+            bad += not ok
+        print(json.dumps({"variant": ",".join(v) or "base", "shares": n, "bitexact": bad == 0}), flush=True)
     for v in variants:  # warm
         run(v, 0)
     torch.cuda.synchronize()
