@@ -11,24 +11,26 @@
 //     4 groups side by side. Each thread owns one nonce: it computes that
 //     nonce's keccak-f800 seed, then its group walks the group's 16 nonces
 //     (the keccak cost is paid once per nonce, not 16x).
-//   * the hash is a chain of 64 dependent DAG gathers (round r+1's address
-//     depends on round r's DAG merge into mix[0]), so throughput is set by how
-//     many gathers are in flight per SIMD (Little's law on HBM latency), not by
-//     ALU. A group therefore interleaves KP_HASHES independent hashes of its 16
-//     (KP_HASHES x 32 mix VGPRs): KP_HASHES gathers are issued back to back at
-//     round start and the KP_HASHES programs give the scheduler independent
-//     chains to fill the latency with.
+//   * measured (profiles/README.md): the kernel is VALU-issue bound, not HBM
+//     bound — ~2k wave64 integer VALU instructions per hash at 4 cycles each
+//     saturate the SIMDs at ~270 MH/s while the 16 KiB/hash of DAG gathers
+//     runs at ~4.4 TB/s. Doubling gathers in flight (KP_HASHES=2/4) did not
+//     help; every VALU op removed from the round did. So the tuned variant
+//     (ops/jit.py TUNED_DEFINES) spends its effort on instruction count:
+//       - rounds unrolled by 16 so the item-index broadcast from lane r%16 is
+//         one DPP row_newbcast (no ds_bpermute / address math),
+//       - a 5-op Barrett modulo for the item index,
+//       - raw-buffer DAG loads with a 32-bit byte offset,
+//       - the L1 replicated 4x in LDS so each of the 11 cache lookups needs a
+//         single v_lshlrev_b16 for its address (512-thread workgroups keep 4
+//         waves/SIMD within the 160 KiB LDS).
 //   * the mix registers are arrays subscripted only by literals (the emitted
 //     program bakes every index in), so they are scalarised into VGPRs.
 //   * everything not needed inside the round loop leaves the VGPR file: the 8
 //     digest words go to LDS as each hash finishes, and the keccak state words
 //     2..7 are recomputed for the final absorb instead of being held live.
-//   * the 16 KiB L1 (first 64 DAG items) sits in LDS; cache ops are
-//     ds_read_b32 with a 12-bit masked address.
 //   * each round's 256-byte DAG item is one coalesced 16 B/lane load by the
-//     group (lane l takes words ((l^r)%16)*4..+3); the item index is broadcast
-//     from lane r%16 with ds_bpermute (__shfl, width 16) and reduced with a
-//     FastMod32 multiply-shift.
+//     group (lane l takes words ((l^r)%16)*4..+3).
 #include "kernel_params.h"
 #include "keccak_device.hpp"
 
@@ -47,11 +49,44 @@
 #if (16 % KP_HASHES) != 0
 #error "KP_HASHES must divide 16"
 #endif
-#ifdef KP_MIN_WAVES
-#define KP_BOUNDS __launch_bounds__(NODEXA_KAWPOW_BLOCK, KP_MIN_WAVES)
-#else
-#define KP_BOUNDS __launch_bounds__(NODEXA_KAWPOW_BLOCK)
+//   KP_BLOCK      threads per workgroup (the host launcher reads it back from
+//                 the kernel's max-threads attribute)
+//   KP_DPP        rounds unrolled by 16; item index broadcast by DPP row_newbcast
+//   KP_BARRETT    5-op Barrett modulo for the item index
+//   KP_BUFFER     raw-buffer DAG loads with a 32-bit offset (DAG < 4 GiB only)
+//   KP_L1X4       L1 replicated 4x in LDS (64 KiB) so an L1 address is one
+//                 16-bit shift: ((x << 2) & 0xffff) reads l1[x % 4096]
+#ifndef KP_BLOCK
+#define KP_BLOCK NODEXA_KAWPOW_BLOCK
 #endif
+#ifdef KP_MIN_WAVES
+#define KP_BOUNDS __launch_bounds__(KP_BLOCK, KP_MIN_WAVES)
+#else
+#define KP_BOUNDS __launch_bounds__(KP_BLOCK)
+#endif
+
+#ifdef KP_L1X4
+#define KP_L1_WORDS 16384
+// v_lshlrev_b16 writes the low half and zeroes the high half of the VGPR, so
+// the shifted value is directly a byte offset < 64 KiB into the 4 copies.
+NX_DEV uint32_t kp_l1_read(const uint32_t* l1, uint32_t x) {
+    uint32_t off;
+    asm("v_lshlrev_b16 %0, 2, %1" : "=v"(off) : "v"(x));
+    return *(const uint32_t*)((const char*)l1 + off);
+}
+#define KP_L1(l1, x) kp_l1_read((l1), (x))
+#else
+#define KP_L1_WORDS 4096
+#define KP_L1(l1, x) (l1)[(x) & 4095u]
+#endif
+
+// LDS copy of the L1 (first 16 KiB of the DAG), KP_L1_WORDS / 4096 times.
+NX_DEV void kp_fill_l1(uint32_t* l1, const void* dag) {
+    const uint4* src = (const uint4*)dag;
+    uint4* dst = (uint4*)l1;
+#pragma unroll
+    for (int i = threadIdx.x; i < KP_L1_WORDS / 4; i += KP_BLOCK) dst[i] = src[i & 1023];
+}
 typedef uint32_t kp_u32x4 __attribute__((ext_vector_type(4)));
 NX_DEV uint4 kp_dag_load(const uint4* p) {
 #ifdef KP_NT_DAG
@@ -78,9 +113,50 @@ NX_DEV uint32_t kp_mul33(uint32_t a) { return a * 33u; }
 NX_DEV uint32_t kp_clz(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : 32u; }
 NX_DEV uint32_t kp_fnv1a(uint32_t h, uint32_t d) { return (h ^ d) * 0x01000193u; }
 NX_DEV uint32_t kp_fastmod(uint32_t x, const FastMod32& f) {
+#ifdef KP_BARRETT
+    // q' = floor(x * floor(2^32/d) / 2^32) is q or q-1, so r' < 2d and one
+    // unsigned min(r', r'-d) finishes it (r'-d wraps high when r' < d).
+    const uint32_t r = x - __umulhi(x, f.mb) * f.d;
+    return min(r, r - f.d);
+#else
     const uint32_t t = __umulhi(x, f.m);
     const uint32_t q = (t + ((x - t) >> 1)) >> (f.s - 1);
     return x - q * f.d;
+#endif
+}
+
+// DAG item access. KP_BUFFER addresses the (< 4 GiB) DAG through a raw buffer
+// resource with a 32-bit byte offset (one v_lshl_add) instead of 64-bit
+// pointer arithmetic.
+#ifdef KP_BUFFER
+typedef __amdgpu_buffer_rsrc_t kp_dag_t;
+NX_DEV kp_dag_t kp_dag_handle(const void* dag) {
+    // num_records 0xffffffff: no range clamp; the host only selects KP_BUFFER for DAGs < 4 GiB
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(dag), (short)0, -1, 0x00020000);
+}
+NX_DEV uint4 kp_dag_item(kp_dag_t dag, uint32_t index, uint32_t part) {
+#ifdef KP_NT_DAG
+    const int aux = 2;
+#else
+    const int aux = 0;
+#endif
+    const kp_u32x4 v = __builtin_bit_cast(kp_u32x4,
+        __builtin_amdgcn_raw_buffer_load_b128(dag, (index << 8) + (part << 4), 0, aux));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+#else
+typedef const uint4* kp_dag_t;
+NX_DEV kp_dag_t kp_dag_handle(const void* dag) { return (const uint4*)dag; }
+NX_DEV uint4 kp_dag_item(kp_dag_t dag, uint32_t index, uint32_t part) {
+    return kp_dag_load(dag + (size_t)index * 16 + part);
+}
+#endif
+
+// Broadcast lane j of each 16-lane row: DPP row_newbcast (one VALU op, no LDS
+// round trip) when the round index is a compile-time constant.
+template <int J>
+NX_DEV uint32_t kp_bcast(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + J, 0xf, 0xf, false);
 }
 
 struct KpKiss {
@@ -143,7 +219,22 @@ NX_DEV void kp_final(const uint32_t st2[8], const uint32_t digest[8], uint32_t o
 // The group's 16 hashes, KP_HASHES at a time. `st0/st1` are this thread's own
 // nonce seed words (hash h's seed lives in lane h). Each finished hash's 8
 // digest words are written to dig[h * 8 + k] (LDS, this group's 128 words).
-NX_DEV void kp_group_hashes(const uint4* __restrict__ dag, const FastMod32& items, const uint32_t* l1,
+// One ProgPoW round with the round index known mod 16 (J): the item index comes
+// from lane J of the row via DPP and the lane's 16-byte slice is lane ^ J.
+template <int J>
+NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
+                       uint32_t lane) {
+    uint4 d[KP_HASHES];
+    const uint32_t part = lane ^ (uint32_t)J;
+#pragma unroll
+    for (int k = 0; k < KP_HASHES; ++k) d[k] = kp_dag_item(dag, kp_fastmod(kp_bcast<J>(mx[k][0]), items), part);
+#pragma unroll
+    for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM(l1, mx[k]);
+#pragma unroll
+    for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
+}
+
+NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
                             uint32_t st0, uint32_t st1, uint32_t lane, uint32_t* dig) {
 #pragma unroll 1
     for (uint32_t h0 = 0; h0 < 16; h0 += KP_HASHES) {
@@ -159,20 +250,33 @@ NX_DEV void kp_group_hashes(const uint4* __restrict__ dag, const FastMod32& item
 #pragma unroll
             for (int i = 0; i < 32; ++i) mx[k][i] = rng.next();
         }
+#ifdef KP_DPP
+        // 64 rounds = 4 x 16 with the round index mod 16 baked into each copy
+#pragma unroll 1
+        for (uint32_t rr = 0; rr < 64; rr += 16) {
+            kp_round_c<0>(mx, dag, items, l1, lane);   kp_round_c<1>(mx, dag, items, l1, lane);
+            kp_round_c<2>(mx, dag, items, l1, lane);   kp_round_c<3>(mx, dag, items, l1, lane);
+            kp_round_c<4>(mx, dag, items, l1, lane);   kp_round_c<5>(mx, dag, items, l1, lane);
+            kp_round_c<6>(mx, dag, items, l1, lane);   kp_round_c<7>(mx, dag, items, l1, lane);
+            kp_round_c<8>(mx, dag, items, l1, lane);   kp_round_c<9>(mx, dag, items, l1, lane);
+            kp_round_c<10>(mx, dag, items, l1, lane);  kp_round_c<11>(mx, dag, items, l1, lane);
+            kp_round_c<12>(mx, dag, items, l1, lane);  kp_round_c<13>(mx, dag, items, l1, lane);
+            kp_round_c<14>(mx, dag, items, l1, lane);  kp_round_c<15>(mx, dag, items, l1, lane);
+        }
+#else
 #pragma unroll 1
         for (uint32_t r = 0; r < 64; ++r) {
             uint4 d[KP_HASHES];
             const uint32_t part = (lane ^ r) & 15;
 #pragma unroll
-            for (int k = 0; k < KP_HASHES; ++k) {
-                const uint32_t index = kp_fastmod(__shfl(mx[k][0], (int)(r & 15), 16), items);
-                d[k] = kp_dag_load(dag + (size_t)index * 16 + part);
-            }
+            for (int k = 0; k < KP_HASHES; ++k)
+                d[k] = kp_dag_item(dag, kp_fastmod(__shfl(mx[k][0], (int)(r & 15), 16), items), part);
 #pragma unroll
             for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM(l1, mx[k]);
 #pragma unroll
             for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
         }
+#endif
 #pragma unroll
         for (int k = 0; k < KP_HASHES; ++k) {
             uint32_t lh = 0x811c9dc5u;
@@ -186,24 +290,27 @@ NX_DEV void kp_group_hashes(const uint4* __restrict__ dag, const FastMod32& item
 }
 
 extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
-    __shared__ uint32_t l1[4096];
-    __shared__ uint32_t digs[NODEXA_KAWPOW_BLOCK * 8];
-    {
-        const uint4* src = (const uint4*)p.dag;
-        uint4* dst = (uint4*)l1;
-#pragma unroll
-        for (int i = threadIdx.x; i < 1024; i += NODEXA_KAWPOW_BLOCK) dst[i] = src[i];
-    }
+    __shared__ uint32_t l1[KP_L1_WORDS];
+#ifdef KP_DIGEST_GLOBAL
+    // digests parked in HBM (32 B per nonce, <0.2% of the DAG traffic) so the
+    // 64 KiB L1X4 table leaves LDS room for 2 workgroups of KP_BLOCK per CU
+    uint32_t* digs = p.scratch + (size_t)blockIdx.x * KP_BLOCK * 8;
+#else
+    __shared__ uint32_t digs[KP_BLOCK * 8];
+#endif
+    if (blockDim.x != KP_BLOCK) return;  // launched with the wrong block: no shares rather than bad ones
+    kp_fill_l1(l1, p.dag);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 15;
-    const uint64_t nonce = p.start_nonce + (uint64_t)blockIdx.x * NODEXA_KAWPOW_BLOCK + threadIdx.x;
+    const uint64_t nonce = p.start_nonce + (uint64_t)blockIdx.x * KP_BLOCK + threadIdx.x;
     uint32_t* dig = digs + (threadIdx.x & ~15u) * 8;
     {
         uint32_t st2[8];
         kp_seed(p.header, nonce, st2);
-        kp_group_hashes((const uint4*)p.dag, p.items, l1, st2[0], st2[1], lane, dig);
+        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig);
     }
+    __threadfence_block();  // digest words written by lanes 0..7 are read by lane h below
     __syncthreads();
     uint32_t st2[8], digest[8], fin[8];
     kp_seed(p.header, nonce, st2);  // recomputed: cheaper than 6 VGPRs held across the mix loop
@@ -228,22 +335,19 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
 // Batch hash (no target): for verification of (header, nonce, height) jobs that
 // all share this period and epoch. One job per thread, grouped as in search.
 extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
-    __shared__ uint32_t l1[4096];
-    __shared__ uint32_t digs[NODEXA_KAWPOW_BLOCK * 8];
-    {
-        const uint4* src = (const uint4*)p.dag;
-        uint4* dst = (uint4*)l1;
-        for (int i = threadIdx.x; i < 1024; i += NODEXA_KAWPOW_BLOCK) dst[i] = src[i];
-    }
+    __shared__ uint32_t l1[KP_L1_WORDS];
+    __shared__ uint32_t digs[KP_BLOCK * 8];
+    if (blockDim.x != KP_BLOCK) return;
+    kp_fill_l1(l1, p.dag);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 15;
-    const uint32_t job = blockIdx.x * NODEXA_KAWPOW_BLOCK + threadIdx.x;
+    const uint32_t job = blockIdx.x * KP_BLOCK + threadIdx.x;
     const bool valid = job < p.num_jobs;
     const KawpowVerifyJob j = p.jobs[valid ? job : 0];
     uint32_t* dig = digs + (threadIdx.x & ~15u) * 8;
     uint32_t st2[8];
     kp_seed(j.header, j.nonce, st2);
-    kp_group_hashes((const uint4*)p.dag, p.items, l1, st2[0], st2[1], lane, dig);
+    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig);
     __syncthreads();
     uint32_t digest[8], fin[8];
 #pragma unroll

@@ -14,7 +14,7 @@ struct FastMod32 {
     uint32_t d;
     uint32_t m;
     uint32_t s;  // ceil(log2 d), >= 1
-    uint32_t pad;
+    uint32_t mb; // floor(2^32 / d): Barrett estimate, off by at most one d (one min() fixes it)
 };
 
 struct EthashDagParams {
@@ -45,6 +45,7 @@ struct KawpowSearchParams {
     uint64_t target;           // share if bswap64(final[0..1]) <= target (upper 64 bits, BE)
     uint32_t header[8];        // header hash words (storage order)
     struct FastMod32 items;    // modulo by number of 2048-bit items (full_items / 2)
+    uint32_t* scratch;         // >= 8 words per nonce of the launch (variants that park digests in HBM)
 };
 
 // Light-mode / full-DAG batch verification of (header, nonce) pairs.

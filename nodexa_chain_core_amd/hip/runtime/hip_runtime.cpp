@@ -39,6 +39,7 @@ FastMod32 make_fastmod(uint32_t d) {
     f.d = d;
     f.m = uint32_t(m);
     f.s = s;
+    f.mb = uint32_t((uint64_t(1) << 32) / d);
     return f;
 }
 
@@ -46,6 +47,7 @@ struct Kernel {
     hipFunction_t fn = nullptr;
     std::string name;
     int device = -1;
+    int max_threads = 0;  // __launch_bounds__ of the kernel = the block size its launcher uses
 
     void launch_bytes(dim3 grid, dim3 block, unsigned shmem, hipStream_t stream, const void* params,
                       size_t size) const {
@@ -84,6 +86,8 @@ struct CodeObject {
         check(hipModuleGetFunction(&k->fn, mod, name.c_str()), ("hipModuleGetFunction(" + name + ")").c_str());
         k->name = name;
         k->device = device;
+        check(hipFuncGetAttribute(&k->max_threads, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, k->fn),
+              "hipFuncGetAttribute(MAX_THREADS_PER_BLOCK)");
         fns[name] = k;
         return k;
     }
@@ -163,6 +167,7 @@ PYBIND11_MODULE(_hip, m) {
     py::class_<Kernel, std::shared_ptr<Kernel>>(m, "Kernel")
         .def_readonly("name", &Kernel::name)
         .def_readonly("device", &Kernel::device)
+        .def_readonly("max_threads", &Kernel::max_threads)
         .def("launch", [](const Kernel& k, std::tuple<unsigned, unsigned, unsigned> g,
                           std::tuple<unsigned, unsigned, unsigned> b, unsigned shmem, uintptr_t stream,
                           const py::bytes& params) {
@@ -199,19 +204,27 @@ PYBIND11_MODULE(_hip, m) {
 
     m.def("launch_kawpow_search", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t results,
                                      const py::bytes& header, uint64_t start_nonce, uint64_t target,
-                                     uint64_t num_nonces, uintptr_t stream) {
-        if (num_nonces % NODEXA_KAWPOW_BLOCK)
-            throw std::invalid_argument("num_nonces must be a multiple of the block size");
+                                     uint64_t num_nonces, uintptr_t stream, uintptr_t scratch,
+                                     uint64_t scratch_bytes) {
+        // search variants are compiled for different block sizes (KP_BLOCK); their
+        // __launch_bounds__ is the block, one nonce per thread
+        const unsigned block = unsigned(k.max_threads);
+        if (block == 0 || num_nonces % block)
+            throw std::invalid_argument("num_nonces must be a multiple of the kernel's block size");
+        // variants that park digests in HBM write 32 B per nonce of the launch
+        if (scratch == 0 || scratch_bytes < num_nonces * 32)
+            throw std::invalid_argument("search scratch must hold 32 bytes per nonce");
         KawpowSearchParams p{};
+        p.scratch = reinterpret_cast<uint32_t*>(scratch);
         p.dag = reinterpret_cast<const void*>(dag);
         p.results = reinterpret_cast<KawpowResults*>(results);
         p.start_nonce = start_nonce;
         p.target = target;
         load_words(header, p.header);
         p.items = make_fastmod(dag_items2048);
-        const uint64_t grid = num_nonces / NODEXA_KAWPOW_BLOCK;
+        const uint64_t grid = num_nonces / block;
         if (grid == 0 || grid > 0x7fffffffULL) throw std::invalid_argument("bad search grid");
-        k.launch_bytes(dim3(unsigned(grid)), dim3(NODEXA_KAWPOW_BLOCK), 0, as_stream(stream), &p, sizeof(p));
+        k.launch_bytes(dim3(unsigned(grid)), dim3(block), 0, as_stream(stream), &p, sizeof(p));
     });
 
     m.def("launch_kawpow_hash_batch", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t jobs,
@@ -222,9 +235,10 @@ PYBIND11_MODULE(_hip, m) {
         p.out = reinterpret_cast<uint32_t*>(out);
         p.num_jobs = num_jobs;
         p.items = make_fastmod(dag_items2048);
-        const unsigned grid = (num_jobs + NODEXA_KAWPOW_BLOCK - 1) / NODEXA_KAWPOW_BLOCK;
+        const unsigned block = unsigned(k.max_threads);
+        const unsigned grid = (num_jobs + block - 1) / block;
         if (grid == 0) return;
-        k.launch_bytes(dim3(grid), dim3(NODEXA_KAWPOW_BLOCK), 0, as_stream(stream), &p, sizeof(p));
+        k.launch_bytes(dim3(grid), dim3(block), 0, as_stream(stream), &p, sizeof(p));
     });
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
     m.attr("KV_PROG_WORDS") = KV_PROG_WORDS;

@@ -91,7 +91,8 @@ class GpuKawpowBackend:
         s = self.searcher(block_number)
         pos, end = start, start + count
         while pos < end:
-            n = min(self.intensity, max(256, (end - pos + 255) // 256 * 256))
+            b = s.block
+            n = max(b, min(self.intensity, end - pos + b - 1) // b * b)
             shares = s.search(header_hash, pos, n, boundary)
             shares = [x for x in shares if x.nonce < end]
             if shares:

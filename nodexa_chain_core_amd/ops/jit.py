@@ -80,8 +80,21 @@ def _atomic_copy(src: str, dst: str) -> None:
     os.replace(tmp, dst)
 
 
-DEFAULT_DEFINES: tuple[str, ...] = tuple(
-    d for d in os.environ.get("NODEXA_KAWPOW_DEFINES", "").split(",") if d)
+# Tuned variant of the search template (profiles/README.md has the sweep that
+# picked it); NODEXA_KAWPOW_DEFINES="A,B=1" overrides it ("none" = plain template).
+TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_BUFFER", "KP_L1X4", "KP_BLOCK=512")
+_env = os.environ.get("NODEXA_KAWPOW_DEFINES")
+DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
+    d for d in _env.split(",") if d and d != "none")
+
+
+def defines_for(dag_bytes: int, defines: tuple[str, ...] | None = None) -> tuple[str, ...]:
+    """The variant to compile for a DAG of `dag_bytes`: KP_BUFFER addresses the DAG with a
+    32-bit byte offset, so it is dropped for DAGs of 4 GiB or more (epochs >= ~385)."""
+    d = DEFAULT_DEFINES if defines is None else tuple(defines)
+    if dag_bytes >= 1 << 32:
+        d = tuple(x for x in d if x != "KP_BUFFER")
+    return d
 
 
 def prefetch(period: int, defines: tuple[str, ...] | None = None) -> cf.Future:

@@ -57,6 +57,7 @@ class KawpowSearcher:
         self.period = -1
         self.kernel = None
         self.hash_kernel = None
+        self._scratch: torch.Tensor | None = None
         nbytes = self.h.sizeof_results()
         with torch.cuda.device(self.device):
             self.results = torch.zeros(nbytes // 4, dtype=torch.int32, device=self.device)
@@ -68,26 +69,43 @@ class KawpowSearcher:
             raise ValueError(f"block {block_number} is not in epoch {self.epoch_dev.epoch}")
         period = block_number // 3
         if period != self.period:
+            defines = jit.defines_for(self.epoch_dev.dag_bytes)
             with torch.cuda.device(self.device):
-                co = runtime.load_code_object(jit.get(period), key=f"kawpow_p{period}")
+                path = jit.get(period, defines)
+                co = runtime.load_code_object(path, key=path)
                 self.kernel = co.function("kawpow_search")
                 self.hash_kernel = co.function("kawpow_hash_batch")
             self.period = period
             if self.prefetch_next:
-                jit.prefetch(period + 1)  # next period compiles while this one mines
+                jit.prefetch(period + 1, defines)  # next period compiles while this one mines
         self.block_number = block_number
+
+    @property
+    def block(self) -> int:
+        """Threads per workgroup of the loaded variant = the nonce granularity of a launch."""
+        return int(self.kernel.max_threads)
 
     # ------------------------------------------------------------------
     def launch(self, header_hash: bytes, start_nonce: int, num_nonces: int, target64: int,
                stream: int | None = None) -> None:
         """Queue one search window on `stream` (no host sync)."""
-        if num_nonces % self.h.KAWPOW_BLOCK:
-            raise ValueError(f"num_nonces must be a multiple of {self.h.KAWPOW_BLOCK}")
+        if num_nonces % self.block:
+            raise ValueError(f"num_nonces must be a multiple of {self.block}")
         with torch.cuda.device(self.device):
             s = runtime.current_stream_handle() if stream is None else stream
+            scratch = self.scratch(num_nonces)
             self.results[:4].zero_()
             self.h.launch_kawpow_search(self.kernel, self.epoch_dev.dag.data_ptr(), self.epoch_dev.items2048,
-                                        self.results.data_ptr(), header_hash, start_nonce, target64, num_nonces, s)
+                                        self.results.data_ptr(), header_hash, start_nonce, target64, num_nonces, s,
+                                        scratch.data_ptr(), scratch.numel() * 4)
+
+    def scratch(self, num_nonces: int) -> torch.Tensor:
+        """Per-nonce digest parking space (8 words/nonce) for the launch; grown on demand.
+        Reused across launches: kernels on one stream are ordered."""
+        need = num_nonces * 8
+        if self._scratch is None or self._scratch.numel() < need:
+            self._scratch = torch.empty(need, dtype=torch.int32, device=self.device)
+        return self._scratch
 
     def collect(self) -> list[Share]:
         """Copy the share ring back (synchronises the current stream)."""
@@ -105,13 +123,12 @@ class KawpowSearcher:
         return shares
 
     def search(self, header_hash: bytes, start_nonce: int, num_nonces: int, boundary: bytes) -> list[Share]:
-        """All shares in [start, start+num) with final <= boundary (bit-exact, host-checked)."""
-        self.launch(header_hash, start_nonce, num_nonces, target_prefix(boundary))
-        out = []
-        for s in self.collect():
-            if _core.hash_le(s.final_hash, boundary):
-                out.append(s)
-        return out
+        """All shares in [start, start+num) with final <= boundary (bit-exact, host-checked).
+        The launch is rounded up to whole workgroups; shares past the window are dropped."""
+        padded = -(-num_nonces // self.block) * self.block
+        self.launch(header_hash, start_nonce, padded, target_prefix(boundary))
+        end = start_nonce + num_nonces
+        return [s for s in self.collect() if s.nonce < end and _core.hash_le(s.final_hash, boundary)]
 
     def hash_batch(self, header_hashes: list[bytes], nonces: list[int]) -> list[tuple[bytes, bytes]]:
         """(final, mix) for each (header, nonce) at this searcher's block height."""

@@ -12,22 +12,30 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from ..ops.ethash import DeviceEpoch
 from . import world as W
 
 
-def build_dag(epoch_dev: DeviceEpoch) -> None:
+def allgather_shards(full: torch.Tensor, per: int) -> None:
+    """In place: rank r's bytes [r*per, (r+1)*per) of `full` are replicated to every rank."""
+    w = W.get()
+    if not w.distributed:
+        return
+    if full.numel() != per * w.world_size:
+        raise ValueError("buffer must hold exactly world_size shards")
+    mine = full[w.rank * per:(w.rank + 1) * per]
+    if w.backend == "nccl":
+        dist.all_gather_into_tensor(full, mine)
+    else:  # gloo: no in-place all_gather_into_tensor, go through views of the same buffer
+        parts = list(full.view(w.world_size, per).unbind(0))
+        dist.all_gather(parts, mine.clone())
+
+
+def build_dag(epoch_dev) -> None:
+    """Build `epoch_dev` (ops.ethash.DeviceEpoch): 1/world per rank, then all-gather."""
     w = W.get()
     if not w.distributed:
         epoch_dev.build()
         return
     epoch_dev.build(shard=(w.rank, w.world_size))
-    per = epoch_dev.shard_bytes(w.world_size)
-    full = epoch_dev.dag_padded(w.world_size)
-    mine = full[w.rank * per:(w.rank + 1) * per]
-    if w.backend == "nccl":
-        dist.all_gather_into_tensor(full, mine)
-    else:  # gloo has no in-place all_gather_into_tensor: go through a list
-        parts = list(full.view(w.world_size, per).unbind(0))
-        dist.all_gather(parts, mine.clone())
+    allgather_shards(epoch_dev.dag_padded(w.world_size), epoch_dev.shard_bytes(w.world_size))
     epoch_dev.mark_built()  # later kernels on this stream are ordered after the gather

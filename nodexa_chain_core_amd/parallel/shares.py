@@ -13,34 +13,54 @@ import struct
 import torch
 import torch.distributed as dist
 
-from ..ops.kawpow import SHARE_FMT, SHARE_SIZE, KawpowSearcher, Share
 from . import world as W
+
+# KawpowResults layout (hip/kernels/kernel_params.h): u32 count, 3 pad, then
+# shares of {u64 nonce, u32 mix[8], u32 final[8]}.
+SHARE_FMT = "<Q8I8I"
+SHARE_SIZE = struct.calcsize(SHARE_FMT)
+RING_HEADER = 16
+
+
+def parse_ring(raw: bytes, max_shares: int, base: int = 0) -> list[tuple[int, bytes, bytes]]:
+    """(nonce, mix, final) entries of one result ring (count clamped to the ring size)."""
+    count = struct.unpack_from("<I", raw, base)[0]
+    out = []
+    for i in range(min(count, max_shares)):
+        vals = struct.unpack_from(SHARE_FMT, raw, base + RING_HEADER + i * SHARE_SIZE)
+        out.append((vals[0], struct.pack("<8I", *vals[1:9]), struct.pack("<8I", *vals[9:17])))
+    return out
 
 
 class ShareGather:
-    def __init__(self, searcher: KawpowSearcher):
-        self.s = searcher
+    """All-gather of every rank's share ring into one [world x ring] device tensor.
+
+    `ShareGather(searcher)` for an ops.kawpow.KawpowSearcher, or
+    `ShareGather(results=tensor, max_shares=n)` for any ring-shaped int32 tensor."""
+
+    def __init__(self, searcher=None, *, results: torch.Tensor | None = None, max_shares: int | None = None):
+        self.results = searcher.results if searcher is not None else results
+        self.max_shares = searcher.h.KAWPOW_MAX_SHARES if searcher is not None else int(max_shares)
         self.w = W.get()
-        n = searcher.results.numel()
-        self.gathered = torch.zeros(self.w.world_size * n, dtype=torch.int32, device=searcher.device)
+        n = self.results.numel()
+        self.gathered = torch.zeros(self.w.world_size * n, dtype=self.results.dtype, device=self.results.device)
+        self._views = list(self.gathered.view(self.w.world_size, n).unbind(0))
 
     def enqueue(self) -> None:
-        """Queue the gather after the last search launch (no host sync)."""
-        if self.w.distributed:
-            dist.all_gather_into_tensor(self.gathered, self.s.results)
+        """Queue the gather after the last search launch (no host sync on RCCL)."""
+        if not self.w.distributed:
+            self.gathered.copy_(self.results, non_blocking=True)
+        elif self.w.backend == "nccl":
+            dist.all_gather_into_tensor(self.gathered, self.results)
         else:
-            self.gathered.copy_(self.s.results, non_blocking=True)
+            dist.all_gather(self._views, self.results)
 
-    def collect(self) -> list[Share]:
+    def collect(self):
+        from ..ops.kawpow import Share
+
         raw = self.gathered.cpu().numpy().tobytes()
-        per = self.s.results.numel() * 4
-        max_shares = self.s.h.KAWPOW_MAX_SHARES
-        out: list[Share] = []
-        for r in range(self.w.world_size):
-            base = r * per
-            count = struct.unpack_from("<I", raw, base)[0]
-            for i in range(min(count, max_shares)):
-                vals = struct.unpack_from(SHARE_FMT, raw, base + 16 + i * SHARE_SIZE)
-                out.append(Share(vals[0], struct.pack("<8I", *vals[1:9]), struct.pack("<8I", *vals[9:17])))
+        per = self.results.numel() * self.results.element_size()
+        out = [Share(n, mix, fin) for r in range(self.w.world_size)
+               for n, mix, fin in parse_ring(raw, self.max_shares, r * per)]
         out.sort(key=lambda s: s.nonce)
         return out

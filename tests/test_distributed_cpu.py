@@ -1,0 +1,90 @@
+"""Multi-process (gloo, world_size 2, CPU) rehearsal of the RCCL paths in parallel/:
+work-packet broadcast, max/sum reductions, in-place DAG shard all-gather (slices
+filled with golden ethash items), share-ring all-gather, and the disjoint nonce
+partition bench.py and the miner use. Same code as the GPU path, gloo backend."""
+import os
+import socket
+import struct
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
+        import torch
+
+        from nodexa_chain_core_amd import _core
+        from nodexa_chain_core_amd.parallel import dag as pdag
+        from nodexa_chain_core_amd.parallel import world as W
+        from nodexa_chain_core_amd.parallel.shares import RING_HEADER, SHARE_SIZE, ShareGather
+
+        w = W.init(use_gpu=False)
+        assert w.backend == "gloo" and w.world_size == world
+        # 1. work packet broadcast from rank 0
+        pkt = struct.pack("<32sQII", bytes(range(32)), 7, 1234, 0)
+        got = W.broadcast_bytes(pkt if rank == 0 else None, len(pkt))
+        assert got == pkt
+        # 2. reductions
+        assert W.all_reduce_max(float(rank) + 0.5) == world - 0.5
+        assert W.all_reduce_sum_int(rank + 1) == world * (world + 1) // 2
+        # 3. DAG shard all-gather: each rank fills its slice with golden 2048-bit items
+        ctx = _core.get_epoch_context(0)
+        per_items = 8
+        full = torch.zeros(world * per_items * 256, dtype=torch.uint8)
+        for i in range(per_items):
+            item = rank * per_items + i
+            full[(item * 256):(item + 1) * 256] = torch.frombuffer(bytearray(_core.dataset_item_2048(ctx, item)),
+                                                                   dtype=torch.uint8)
+        pdag.allgather_shards(full, per_items * 256)
+        raw = full.numpy().tobytes()
+        for item in range(world * per_items):
+            assert raw[item * 256:(item + 1) * 256] == _core.dataset_item_2048(ctx, item), item
+        # 4. share-ring all-gather: rank r reports r+1 shares with nonces r*1000+i
+        max_shares = 4
+        ring = bytearray(RING_HEADER + max_shares * SHARE_SIZE)
+        struct.pack_into("<I", ring, 0, rank + 1)
+        for i in range(rank + 1):
+            struct.pack_into("<Q8I8I", ring, RING_HEADER + i * SHARE_SIZE, rank * 1000 + i, *([rank] * 8), *([i] * 8))
+        g = ShareGather(results=torch.frombuffer(ring, dtype=torch.int32).clone(), max_shares=max_shares)
+        g.enqueue()
+        shares = g.collect()
+        assert [s.nonce for s in shares] == sorted(r * 1000 + i for r in range(world) for i in range(r + 1))
+        # 5. nonce partition of bench.py: disjoint windows across ranks and steps
+        batch, base = 1 << 20, 0x5EED_0000_0000_0000
+        windows = [(base + (i * world + r) * batch, batch) for i in range(3) for r in range(world)]
+        ends = sorted(windows)
+        assert all(a[0] + a[1] <= b[0] for a, b in zip(ends, ends[1:]))
+        W.barrier()
+        W.shutdown()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc() or repr(e)))
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_collectives():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=280) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert results == {0: "ok", 1: "ok"}, results

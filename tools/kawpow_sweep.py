@@ -23,7 +23,7 @@ def main() -> int:
     ap.add_argument("--epoch", type=int, default=384)
     ap.add_argument("--batch", type=int, default=1 << 23)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", nargs="*", default=[""])
+    ap.add_argument("--variants", nargs="*", default=["tuned"])
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
@@ -35,7 +35,8 @@ def main() -> int:
 
     height = a.epoch * 7500 + 123
     period = height // 3
-    variants = [tuple(x for x in v.split(",") if x) for v in a.variants]
+    # "tuned" = the production variant (ops/jit.py TUNED_DEFINES); "" = the plain template
+    variants = [jit.TUNED_DEFINES if v == "tuned" else tuple(x for x in v.split(",") if x) for v in a.variants]
     paths = {v: jit.get(period, v) for v in variants}
     torch.cuda.set_device(0)
     ep = DeviceEpoch(a.epoch, device=0)
@@ -43,14 +44,18 @@ def main() -> int:
     torch.cuda.synchronize()
     h = runtime.hip()
     res = torch.zeros(h.sizeof_results() // 4, dtype=torch.int32, device="cuda")
+    scratch = torch.empty(a.batch * 8, dtype=torch.int32, device="cuda")
+    sargs = (scratch.data_ptr(), scratch.numel() * 4)
     kern = {v: runtime.load_code_object(p, key=p).function("kawpow_search") for v, p in paths.items()}
     header = _core.sha256d(b"sweep")
     stream = runtime.current_stream_handle()
 
+    nb = {v: a.batch // k.max_threads * k.max_threads for v, k in kern.items()}  # whole workgroups
+
     def run(v, start):
         res[:4].zero_()
         h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header, start, 0,
-                               a.batch, stream)
+                               nb[v], stream, *sargs)
 
     # bit-exactness: every variant, target = all-pass, first shares re-hashed on the CPU
     import struct
@@ -61,7 +66,7 @@ def main() -> int:
     for v in variants:
         res.zero_()
         h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header, 1000, (1 << 64) - 1,
-                               4096, stream)
+                               5120, stream, *sargs)
         raw = res.cpu().numpy().tobytes()
         n = min(struct.unpack_from("<I", raw, 0)[0], 64)
         for i in range(min(n, 3)):
@@ -84,7 +89,7 @@ def main() -> int:
             times[v].append(e0.elapsed_time(e1) / 1e3)
     rows = []
     for v in variants:
-        mhs = [a.batch / t / 1e6 for t in times[v]]
+        mhs = [nb[v] / t / 1e6 for t in times[v]]
         rows.append({"variant": ",".join(v) or "base", "median_mhs": round(statistics.median(mhs), 2),
                      "max_mhs": round(max(mhs), 2), "min_mhs": round(min(mhs), 2)})
         print(json.dumps(rows[-1]), flush=True)
