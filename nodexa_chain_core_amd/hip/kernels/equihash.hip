@@ -51,7 +51,7 @@ NX_DEV uint32_t eq_alloc_slot(const EquihashDev& p, uint32_t* cnt, uint32_t nb) 
 // Gather the rows of (level, bucket) from every bank into LDS order 0..n-1;
 // sid[i] = the row's slot index inside the bucket (what refs encode).
 // Ends with a __syncthreads(); returns n.
-template <bool ROWS>
+template <bool ROWS, bool HALF = false>
 NX_DEV uint32_t eq_stage(const EquihashDev& p, uint32_t inst, int level, int buf, uint32_t bucket, uint32_t* rows,
                          short* sid, uint32_t* bstart) {
     const uint32_t per = EQ_CAP / p.banks;
@@ -73,7 +73,7 @@ NX_DEV uint32_t eq_stage(const EquihashDev& p, uint32_t inst, int level, int buf
         sid[i] = (short)slot;
         if (ROWS) {
             const uint4* src = (const uint4*)(p.hashes + eq_hidx(p, buf, inst, bucket, slot));
-            ((uint4*)rows)[2 * i] = src[0];
+            if (!HALF) ((uint4*)rows)[2 * i] = src[0];  // HALF: words 0..3 are never read
             ((uint4*)rows)[2 * i + 1] = src[1];
         }
     }
@@ -206,7 +206,42 @@ extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_gen(EquihashDev p) {
     }
 }
 
+// First word (of w[1..7]) that still carries bits at level L: bits [20L, 200).
+// From level 5 on that is word >= 4, so only the second 16-byte half of a
+// 32-byte row slot is read or written (levels 5..8: half the row traffic).
+constexpr int eq_first_word(int level) { return (20 * level) / 32 + 1; }
+#ifdef EQ_NO_HALF
+constexpr bool eq_half_row(int) { return false; }
+#else
+constexpr bool eq_half_row(int level) { return eq_first_word(level) >= 4; }
+#endif
+
+// XOR of two staged rows of level L-1 into the level-L row x (words of
+// levels < first meaningful word are zero / never read).
+template <int L>
+NX_DEV void eq_xor_rows(const uint32_t* a, const uint32_t* b, uint32_t x[8]) {
+    constexpr int k0 = eq_half_row(L - 1) ? 4 : 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = (k >= k0) ? (a[k] ^ b[k]) : 0u;
+}
+
+template <int L>
+NX_DEV void eq_store_row(const EquihashDev& p, uint32_t inst, uint32_t nb, uint32_t slot, const uint32_t x[8],
+                         uint32_t ref) {
+    uint4* dst = (uint4*)(p.hashes + eq_hidx(p, L & 1, inst, nb, slot));
+    if (!eq_half_row(L)) dst[0] = make_uint4(0, x[1], x[2], x[3]);
+    dst[1] = make_uint4(x[4], x[5], x[6], x[7]);
+    p.refs[eq_ridx(p, inst, L, nb, slot)] = ref;
+}
+
 // Round R (1..8): collide level R-1 on digit R-1, write level R.
+// Phase 1 stages the bucket and chains rows by their 8-bit sub-digit (LDS
+// atomics); each thread then walks its chain and appends every surviving pair
+// to its next-level bucket (one slot atomic + one row store each).
+// EQ_PAIRLIST instead lists the pairs in LDS first and emits them two per
+// thread with both slot atomics in flight — measured 16 % SLOWER per solve
+// (profiles/r1c_equihash), so it stays a tuning variant.
+#define EQ_PAIR_MAX 992  // keeps the round's LDS under 32 KiB: 5 workgroups per CU
 template <int R>
 NX_DEV void eq_round_impl(const EquihashDev& p) {
     __shared__ __attribute__((aligned(16))) uint32_t rows[EQ_CAP * EQ_WORDS];
@@ -214,10 +249,13 @@ NX_DEV void eq_round_impl(const EquihashDev& p) {
     __shared__ short nxt[EQ_CAP];
     __shared__ short sid[EQ_CAP];
     __shared__ uint32_t bstart[EQ_MAX_BANKS + 1];
+    __shared__ uint32_t pairs[EQ_PAIR_MAX];
+    __shared__ uint32_t npairs;
     const uint32_t inst = blockIdx.y;
     const uint32_t bucket = blockIdx.x;
     for (int i = threadIdx.x; i < 256; i += EQ_BLOCK) head[i] = -1;
-    const uint32_t n = eq_stage<true>(p, inst, R - 1, (R - 1) & 1, bucket, rows, sid, bstart);
+    if (threadIdx.x == 0) npairs = 0;
+    const uint32_t n = eq_stage<true, eq_half_row(R - 1)>(p, inst, R - 1, (R - 1) & 1, bucket, rows, sid, bstart);
     for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
         const uint32_t sub = eq_digit<R - 1>(&rows[i * EQ_WORDS]) & 0xFFu;
         nxt[i] = (short)atomicExch(&head[sub], (int)i);
@@ -228,22 +266,42 @@ NX_DEV void eq_round_impl(const EquihashDev& p) {
         const uint32_t* a = &rows[i * EQ_WORDS];
         int j = nxt[i];
         for (int steps = 0; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
-            const uint32_t* b = &rows[(uint32_t)j * EQ_WORDS];
             uint32_t x[8];
-            x[0] = 0;
-#pragma unroll
-            for (int k = 1; k < 8; ++k) x[k] = a[k] ^ b[k];
+            eq_xor_rows<R>(a, &rows[(uint32_t)j * EQ_WORDS], x);
             if (eq_zero_from<R>(x)) continue;  // identical remainder -> only duplicate indices
-            const uint32_t nb = eq_digit<R>(x) >> 8;
-            const uint32_t slot = eq_alloc_slot(p, cnt, nb);
-            if (slot < EQ_CAP) {
-                uint4* dst = (uint4*)(p.hashes + eq_hidx(p, R & 1, inst, nb, slot));
-                dst[0] = make_uint4(0, x[1], x[2], x[3]);
-                dst[1] = make_uint4(x[4], x[5], x[6], x[7]);
-                p.refs[eq_ridx(p, inst, R, nb, slot)] =
-                    (bucket << 20) | ((uint32_t)sid[i] << 10) | (uint32_t)sid[j];
+#ifdef EQ_PAIRLIST
+            const uint32_t k = atomicAdd(&npairs, 1u);
+#else
+            const uint32_t k = EQ_PAIR_MAX;  // default: emit in place (measured faster)
+#endif
+            if (k < EQ_PAIR_MAX) {
+                pairs[k] = (i << 16) | (uint32_t)j;
+            } else {  // list full (rare): emit directly
+                const uint32_t nb = eq_digit<R>(x) >> 8;
+                const uint32_t slot = eq_alloc_slot(p, cnt, nb);
+                if (slot < EQ_CAP)
+                    eq_store_row<R>(p, inst, nb, slot, x, (bucket << 20) | ((uint32_t)sid[i] << 10) | (uint32_t)sid[j]);
             }
         }
+    }
+    __syncthreads();
+    const uint32_t np = min(npairs, (uint32_t)EQ_PAIR_MAX);
+    for (uint32_t k = threadIdx.x; k < np; k += 2 * EQ_BLOCK) {
+        const uint32_t k2 = k + EQ_BLOCK;
+        const bool two = k2 < np;
+        const uint32_t pa = pairs[k], pb = two ? pairs[k2] : pairs[k];
+        uint32_t xa[8], xb[8];
+        eq_xor_rows<R>(&rows[(pa >> 16) * EQ_WORDS], &rows[(pa & 0xFFFFu) * EQ_WORDS], xa);
+        eq_xor_rows<R>(&rows[(pb >> 16) * EQ_WORDS], &rows[(pb & 0xFFFFu) * EQ_WORDS], xb);
+        const uint32_t nba = eq_digit<R>(xa) >> 8, nbb = eq_digit<R>(xb) >> 8;
+        const uint32_t sa = eq_alloc_slot(p, cnt, nba);
+        const uint32_t sb = two ? eq_alloc_slot(p, cnt, nbb) : EQ_CAP;
+        if (sa < EQ_CAP)
+            eq_store_row<R>(p, inst, nba, sa, xa,
+                            (bucket << 20) | ((uint32_t)sid[pa >> 16] << 10) | (uint32_t)sid[pa & 0xFFFFu]);
+        if (sb < EQ_CAP)
+            eq_store_row<R>(p, inst, nbb, sb, xb,
+                            (bucket << 20) | ((uint32_t)sid[pb >> 16] << 10) | (uint32_t)sid[pb & 0xFFFFu]);
     }
 }
 

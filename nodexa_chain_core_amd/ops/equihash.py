@@ -38,7 +38,9 @@ def blake2b_h0(n: int = 200, k: int = 9) -> list[int]:
 
 
 class EquihashSolver:
-    def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 4):
+    def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 8,
+                 code_object: str | None = None):
+        """`code_object`: path of an alternative build of equihash.hip (tuning sweeps)."""
         self.banks = int(banks)
         runtime.require_gpu()
         self.h = runtime.hip()
@@ -48,13 +50,24 @@ class EquihashSolver:
         B, C, W, L = self.h.EQ_BUCKETS, self.h.EQ_CAP, self.h.EQ_WORDS, self.h.EQ_LEVELS
         ni = self.num_inst
         with torch.cuda.device(self.device):
-            self.kernels = [runtime.static_kernel("equihash", k) for k in KERNELS]
+            if code_object is None:
+                self.kernels = [runtime.static_kernel("equihash", k) for k in KERNELS]
+            else:
+                co = runtime.load_code_object(code_object)
+                self.kernels = [co.function(k) for k in KERNELS]
             self.hashes = torch.empty(2 * ni * B * C * W, dtype=torch.int32, device=self.device)
             self.refs = torch.empty(ni * L * B * C, dtype=torch.int32, device=self.device)
             self.counts = torch.empty(ni * (L + 1) * B * self.h.EQ_MAX_BANKS, dtype=torch.int32, device=self.device)
             self.cands = torch.empty(ni * (1 + 2 * self.h.EQ_MAX_CAND), dtype=torch.int32, device=self.device)
             self.sols = torch.empty(ni * (1 + self.h.EQ_MAX_SOL * 512), dtype=torch.int32, device=self.device)
             self.msgs = torch.zeros(ni * 16, dtype=torch.int64, device=self.device)
+            # two pinned landing buffers: the solutions of launch i are copied
+            # back on the stream right after its kernels, so launch i+1 can be
+            # queued before the host verifies launch i (GPU and CPU overlap)
+            self._landing = [torch.empty(self.sols.numel(), dtype=torch.int32).pin_memory() for _ in range(2)]
+            self._stage = [torch.empty(ni * 16, dtype=torch.int64).pin_memory() for _ in range(2)]
+        self._pending: list[tuple[list[bytes], torch.Tensor, torch.cuda.Event]] = []
+        self._next = 0
         self.h0 = blake2b_h0()
         self.input_len = None
 
@@ -65,19 +78,39 @@ class EquihashSolver:
         if len(lens) != 1 or next(iter(lens)) > 124 or next(iter(lens)) % 4:
             raise ValueError("inputs must share one length <= 124 bytes, multiple of 4")
         self.input_len = next(iter(lens))
+        if len(self._pending) >= len(self._landing):
+            raise RuntimeError("collect() the oldest launch before queueing another")
         buf = bytearray(self.num_inst * 128)
         for i, x in enumerate(inputs):
             buf[i * 128:i * 128 + len(x)] = x
         with torch.cuda.device(self.device):
-            self.msgs.copy_(torch.frombuffer(buf, dtype=torch.int64))
+            # staged through pinned memory so the upload is stream-ordered and the
+            # host does not wait for the previous launch (slot reuse is safe: its
+            # previous copy completed before that launch's landing event)
+            stage = self._stage[self._next]
+            stage.copy_(torch.frombuffer(buf, dtype=torch.int64))
+            self.msgs.copy_(stage, non_blocking=True)
             s = runtime.current_stream_handle() if stream is None else stream
             self.h.launch_equihash_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst,
                                          self.hashes.data_ptr(), self.refs.data_ptr(), self.counts.data_ptr(),
                                          self.cands.data_ptr(), self.sols.data_ptr(), s, self.banks)
+            land = self._landing[self._next]
+            self._next = (self._next + 1) % len(self._landing)
+            land.copy_(self.sols, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        self._pending.append((list(inputs), land, ev))
 
-    def collect(self, inputs: list[bytes], verify: bool = True) -> list[list[list[int]]]:
-        with torch.cuda.device(self.device):
-            raw = self.sols.cpu().numpy()
+    def collect(self, inputs: list[bytes] | None = None, verify: bool = True) -> list[list[list[int]]]:
+        """Solutions of the oldest queued launch (waits only for that launch)."""
+        if not self._pending:
+            raise RuntimeError("nothing launched")
+        launched, land, ev = self._pending.pop(0)
+        if inputs is not None and list(inputs) != launched:
+            raise ValueError("collect() inputs differ from the oldest launch")
+        inputs = launched
+        ev.synchronize()
+        raw = land.numpy()
         per = 1 + self.h.EQ_MAX_SOL * 512
         out = []
         for i in range(self.num_inst):

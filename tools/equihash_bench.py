@@ -1,53 +1,86 @@
 #!/usr/bin/env python3
 """Equihash(200,9) GPU solver timing: device-only time per batch (hip events),
-solutions per solve, host verification cost — for several counter-bank
-settings, interleaved in one process."""
+solutions per solve and host verification cost, for several counter-bank
+settings and compile-time variants of equihash.hip, interleaved in one process.
+
+    python tools/equihash_bench.py --banks 8 --variants "" EQ_NO_HALF EQ_DIRECT
+    python tools/equihash_bench.py --compile-only --variants EQ_NO_HALF   # on the build host
+
+Variants are built to .kernel_cache/equihash_<tag>.hsaco (hipcc --genco).
+"""
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def variant_object(defines: tuple[str, ...]) -> str | None:
+    if not defines:
+        return None
+    from nodexa_chain_core_amd import _build
+
+    src = os.path.join(_build.HIPDIR, "kernels", "equihash.hip")
+    h = hashlib.sha256("|".join(defines).encode())
+    for name in ("equihash.hip", "kernel_params.h"):
+        with open(os.path.join(_build.HIPDIR, "kernels", name), "rb") as f:
+            h.update(f.read())
+    out = os.path.join(ROOT, ".kernel_cache", f"equihash_{h.hexdigest()[:12]}.hsaco")
+    if not os.path.exists(out):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        _build.hipcc_genco(src, out, defines=list(defines))
+    return out
 
 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--inst", type=int, default=8)
     ap.add_argument("--batches", type=int, default=5)
-    ap.add_argument("--banks", type=int, nargs="*", default=[4])
+    ap.add_argument("--banks", type=int, nargs="*", default=[8])
+    ap.add_argument("--variants", nargs="*", default=[""])
+    ap.add_argument("--compile-only", action="store_true")
     a = ap.parse_args()
+    variants = [tuple(x for x in v.split(",") if x) for v in a.variants]
+    objs = {v: variant_object(v) for v in variants}
+    if a.compile_only:
+        print(json.dumps({",".join(v) or "base": o for v, o in objs.items()}))
+        return 0
     import torch
 
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
-    solvers = {b: EquihashSolver(num_inst=a.inst, device=0, banks=b) for b in a.banks}
+    cfgs = [(b, v) for v in variants for b in a.banks]
+    solvers = {c: EquihashSolver(num_inst=a.inst, device=0, banks=c[0], code_object=objs[c[1]]) for c in cfgs}
     batches = [[os.urandom(112) for _ in range(a.inst)] for _ in range(a.batches + 1)]
     for s in solvers.values():
         s.solve(batches[0])
     torch.cuda.synchronize()
-    res = {b: {"dev_ms": [], "sols": 0, "verify_s": 0.0} for b in a.banks}
+    res = {c: {"dev_ms": [], "sols": 0, "verify_s": 0.0} for c in cfgs}
     for bt in batches[1:]:
-        for b, s in solvers.items():
+        for c, s in solvers.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             s.launch(bt)
             e1.record()
             e1.synchronize()
-            res[b]["dev_ms"].append(e0.elapsed_time(e1))
+            res[c]["dev_ms"].append(e0.elapsed_time(e1))
             t = time.perf_counter()
-            res[b]["sols"] += sum(len(x) for x in s.collect(bt))
-            res[b]["verify_s"] += time.perf_counter() - t
-    for b, r in res.items():
+            res[c]["sols"] += sum(len(x) for x in s.collect(bt))
+            res[c]["verify_s"] += time.perf_counter() - t
+    for (b, v), r in res.items():
         per_batch = sum(r["dev_ms"]) / len(r["dev_ms"])
-        out = {"banks": b, "inst_per_batch": a.inst, "device_ms_per_batch": round(per_batch, 3),
-               "device_ms_per_solve": round(per_batch / a.inst, 3),
+        out = {"variant": ",".join(v) or "base", "banks": b, "inst_per_batch": a.inst,
+               "device_ms_per_batch": round(per_batch, 3), "device_ms_per_solve": round(per_batch / a.inst, 3),
                "sols_per_solve": round(r["sols"] / (a.batches * a.inst), 3),
                "device_sol_per_s": round(r["sols"] / (sum(r["dev_ms"]) / 1e3), 1),
                "host_collect_verify_s_per_batch": round(r["verify_s"] / a.batches, 4),
-               "stats": solvers[b].stats()}
+               "stats": solvers[(b, v)].stats()}
         print(json.dumps(out), flush=True)
     return 0
 
