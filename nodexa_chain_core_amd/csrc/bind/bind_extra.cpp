@@ -36,6 +36,7 @@ ArithU256 int_to_arith(const py::int_& v) {
 }  // namespace
 
 void bind_extra(py::module_& m) {
+    m.attr("EQUIHASH_VERSION_BIT") = kEquihashVersionBit;
     // ------------------------------------------------ uint256 / arith
     m.def("u256_hex", [](const py::bytes& b) { return u256(b).hex(); }, "uint256::GetHex of storage bytes");
     m.def("u256_from_hex", [](const std::string& s) { return pyb(Uint256::from_hex(s)); }, "uint256S");
@@ -138,10 +139,25 @@ void bind_extra(py::module_& m) {
         .def_readwrite("height", &BlockHeader::height)
         .def_readwrite("nonce64", &BlockHeader::nonce64)
         .def_property("mix_hash", [](const BlockHeader& h) { return pyb(h.mix_hash); }, [](BlockHeader& h, const py::bytes& b) { h.mix_hash = u256(b); })
+        .def_property("nonce256", [](const BlockHeader& h) { return pyb(h.nonce256); }, [](BlockHeader& h, const py::bytes& b) { h.nonce256 = u256(b); })
+        .def_property("solution", [](const BlockHeader& h) { return py::bytes(reinterpret_cast<const char*>(h.solution.data()), h.solution.size()); },
+                      [](BlockHeader& h, const py::bytes& b) { h.solution = bytes_of(b); })
+        .def("is_equihash", &BlockHeader::is_equihash)
+        .def("equihash_input", [](const BlockHeader& h) { Bytes b = h.equihash_input(); return py::bytes(reinterpret_cast<const char*>(b.data()), b.size()); })
+        .def("equihash_hash", [](const BlockHeader& h, u32 act) { return pyb(h.equihash_hash(act)); })
+        .def("kawpow_input", [](const BlockHeader& h) { Bytes b = h.kawpow_input(); return py::bytes(reinterpret_cast<const char*>(b.data()), b.size()); })
         .def("serialize", [](const BlockHeader& h, u32 act) { return pyb(h.bytes(act)); })
         .def_static("deserialize", [](const py::bytes& b, u32 act) { Bytes d = bytes_of(b); Reader r(d); return BlockHeader::deserialize(r, act); })
         .def("kawpow_header_hash", [](const BlockHeader& h) { return pyb(h.kawpow_header_hash()); })
         .def("legacy80", [](const BlockHeader& h) { return pyb(h.legacy80()); });
+    m.def("deserialize_headers", [](const py::bytes& b, u32 act) {
+        // concatenated headers of mixed formats (80 / 120 / Equihash-extended)
+        Bytes d = bytes_of(b);
+        Reader r(d);
+        std::vector<BlockHeader> out;
+        while (!r.empty()) out.push_back(BlockHeader::deserialize(r, act));
+        return out;
+    });
     py::class_<Block>(m, "Block")
         .def(py::init<>())
         .def_readwrite("header", &Block::header)
@@ -171,6 +187,8 @@ void bind_extra(py::module_& m) {
     // ------------------------------------------------ params / rules
     py::class_<ChainParams>(m, "ChainParams")
         .def_readonly("network_id", &ChainParams::network_id)
+        .def_readonly("equihash_n", &ChainParams::equihash_n)
+        .def_readonly("equihash_k", &ChainParams::equihash_k)
         .def_property_readonly("message_start", [](const ChainParams& p) { return py::bytes((const char*)p.message_start, 4); })
         .def_readonly("default_port", &ChainParams::default_port)
         .def_readonly("default_rpc_port", &ChainParams::default_rpc_port)
@@ -180,6 +198,8 @@ void bind_extra(py::module_& m) {
         .def_property_readonly("genesis_hash", [](const ChainParams& p) { return pyb(p.consensus.genesis_hash); })
         .def_property_readonly("pow_limit", [](const ChainParams& p) { return pyb(p.consensus.pow_limit); })
         .def_property_readonly("kawpow_limit", [](const ChainParams& p) { return pyb(p.consensus.kawpow_limit); })
+        .def_property("equihash_limit", [](const ChainParams& p) { return pyb(p.consensus.equihash_limit); },
+                      [](ChainParams& p, const py::bytes& b) { p.consensus.equihash_limit = u256(b); })
         .def_property_readonly("pow_target_spacing", [](const ChainParams& p) { return p.consensus.pow_target_spacing; })
         .def_property_readonly("pow_allow_min_difficulty_blocks", [](const ChainParams& p) { return p.consensus.pow_allow_min_difficulty_blocks; })
         .def_property_readonly("checkpoints", [](const ChainParams& p) { py::dict d; for (auto& kv : p.checkpoints) d[py::int_(kv.first)] = pyb(kv.second); return d; })

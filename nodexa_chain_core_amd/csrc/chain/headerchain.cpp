@@ -3,6 +3,7 @@
 #include <cstdio>
 #include <sys/stat.h>
 
+#include "../pow/equihash.hpp"
 #include "../pow/kawpow.hpp"
 #include "../pow/x16r.hpp"
 
@@ -10,6 +11,7 @@ namespace nodexa {
 
 // ---------------------------------------------------------------- verifier
 Uint256 CpuPowVerifier::block_hash(const BlockHeader& h, const ChainParams& p) const {
+    if (h.is_equihash()) return h.equihash_hash(p.kawpow_activation_time);  // SHA256d(header) (extension)
     switch (p.algo_for(h.time)) {
         case PowAlgo::KAWPOW: {
             const Hash256 fin = kawpow_hash_no_verify(int(h.height), h.kawpow_header_hash().to_progpow(),
@@ -28,7 +30,7 @@ Uint256 CpuPowVerifier::block_hash(const BlockHeader& h, const ChainParams& p) c
 }
 
 Uint256 CpuPowVerifier::block_hash_full(const BlockHeader& h, const ChainParams& p, Uint256& mix) const {
-    if (p.algo_for(h.time) != PowAlgo::KAWPOW) {
+    if (h.is_equihash() || p.algo_for(h.time) != PowAlgo::KAWPOW) {
         mix = Uint256();
         return block_hash(h, p);
     }
@@ -73,6 +75,25 @@ const HeaderIndex* HeaderChain::add_to_index(const BlockHeader& h, const Uint256
 AcceptResult HeaderChain::check_header(const BlockHeader& h, bool check_pow) const {
     AcceptResult r;
     if (!check_pow) {
+        r.ok = true;
+        return r;
+    }
+    if (h.is_equihash()) {
+        // extension: valid (n,k) solution for kawpow_input || nonce256, then
+        // SHA256d(header) <= target
+        const EquihashParams ep{params_.equihash_n, params_.equihash_k};
+        const Bytes in = h.equihash_input();
+        if (int(h.solution.size()) != ep.solution_bytes() ||
+            !equihash_verify(ep, in.data(), in.size(), equihash_unpack_indices(ep, h.solution))) {
+            r.reject = "invalid-solution";
+            r.dos = 100;
+            return r;
+        }
+        if (!check_proof_of_work(verifier_->block_hash(h, params_), h.bits, params_)) {
+            r.reject = "high-hash";
+            r.dos = 50;
+            return r;
+        }
         r.ok = true;
         return r;
     }
@@ -178,6 +199,20 @@ AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_t
         char buf[48];
         std::snprintf(buf, sizeof(buf), "bad-version(0x%08x)", unsigned(h.version));
         r.reject = buf;
+        return r;
+    }
+    // Equihash extension era (new): the flag bit is required from the activation
+    // time on and forbidden before it (so reference-network headers never parse
+    // as extended ones), and the extended header commits to its height.
+    const bool eq_era = h.time >= params_.equihash_activation_time;
+    if (eq_era != h.is_equihash()) {
+        r.reject = eq_era ? "bad-version(equihash-required)" : "bad-version(equihash-not-active)";
+        r.dos = 100;
+        return r;
+    }
+    if (h.is_equihash() && int(h.height) != height) {
+        r.reject = "bad-height";
+        r.dos = 100;
         return r;
     }
     // The reference never checks that a KawPow header's nHeight equals its index

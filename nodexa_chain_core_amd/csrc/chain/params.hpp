@@ -22,6 +22,9 @@ struct ConsensusParams {
     int subsidy_halving_interval = 2100000;
     Uint256 pow_limit;
     Uint256 kawpow_limit;
+    // Equihash-era bootstrap target (DGW returns it until 180 Equihash blocks
+    // fill the window, mirroring the KawPow switch rule); null = pow_limit.
+    Uint256 equihash_limit;
     int64_t pow_target_spacing = 60;
     int64_t pow_target_timespan = 2016 * 60;
     bool pow_allow_min_difficulty_blocks = false;

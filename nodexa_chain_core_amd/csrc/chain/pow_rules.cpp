@@ -37,18 +37,22 @@ u32 dark_gravity_wave(const HeaderIndex* last, const BlockHeader& next, const Ch
 
     const HeaderIndex* p = last;
     ArithU256 avg;
-    int kawpow_blocks = 0;
+    int kawpow_blocks = 0, equihash_blocks = 0;
     for (u32 count = 1; count <= u32(past_blocks); ++count) {
         ArithU256 target;
         target.set_compact(p->bits);
         if (count == 1) avg = target;
         else avg = (avg * count + target) / ArithU256(count + 1);  // "not really an average" (src/pow.cpp:57)
         if (p->time >= params.kawpow_activation_time) ++kawpow_blocks;
+        if (p->time >= params.equihash_activation_time) ++equihash_blocks;
         if (count != u32(past_blocks)) {
             if (!p->prev) throw std::logic_error("DGW walked past genesis");
             p = p->prev;
         }
     }
+    // Equihash extension (new): same bootstrap as the KawPow switch below
+    if (next.time >= params.equihash_activation_time && equihash_blocks != past_blocks)
+        return ArithU256::from_uint256(c.equihash_limit.is_null() ? c.pow_limit : c.equihash_limit).get_compact();
     if (next.time >= params.kawpow_activation_time && kawpow_blocks != past_blocks)
         return ArithU256::from_uint256(c.kawpow_limit).get_compact();
 

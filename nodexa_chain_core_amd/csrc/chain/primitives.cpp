@@ -95,7 +95,11 @@ void BlockHeader::serialize(Writer& w, u32 act) const {
     w.u256(merkle_root);
     w.u32_(time);
     w.u32_(bits);
-    if (time < act) {
+    if (is_equihash()) {
+        w.u32_(height);
+        w.u256(nonce256);
+        w.var_bytes(solution);
+    } else if (time < act) {
         w.u32_(nonce);
     } else {
         w.u32_(height);
@@ -104,6 +108,14 @@ void BlockHeader::serialize(Writer& w, u32 act) const {
     }
 }
 
+Bytes BlockHeader::equihash_input() const {
+    Bytes b = kawpow_input();
+    b.insert(b.end(), nonce256.data, nonce256.data + 32);
+    return b;
+}
+
+Uint256 BlockHeader::equihash_hash(u32 act) const { return sha256d_u(bytes(act)); }
+
 BlockHeader BlockHeader::deserialize(Reader& r, u32 act) {
     BlockHeader h;
     h.version = r.i32_();
@@ -111,7 +123,12 @@ BlockHeader BlockHeader::deserialize(Reader& r, u32 act) {
     h.merkle_root = r.u256();
     h.time = r.u32_();
     h.bits = r.u32_();
-    if (h.time < act) {
+    if (h.is_equihash()) {
+        h.height = r.u32_();
+        h.nonce256 = r.u256();
+        h.solution = r.var_bytes();
+        if (h.solution.size() > 4096) throw std::runtime_error("equihash solution too large");
+    } else if (h.time < act) {
         h.nonce = r.u32_();
     } else {
         h.height = r.u32_();

@@ -61,6 +61,18 @@ struct Transaction {
 
 enum class PowAlgo { X16R, X16RV2, KAWPOW };
 
+// Equihash(200,9) header extension (new). The
+// reference has no Equihash, so the extension must leave every reference
+// header byte-identical: it is flagged by a version bit no reference network
+// sets, and consensus only allows it from ChainParams::equihash_activation_time
+// (never set on main/test/regtest by default). An extended header is
+//   version|prev|merkle|time|bits|height | nonce256 | CompactSize(1344) solution
+// i.e. the KawPow 80-byte CKAWPOWInput prefix followed by a 32-byte nonce and
+// the 512 x 21-bit packed index solution; the Equihash input is those
+// 80 + 32 bytes, and the block hash (the PoW hash compared to nBits) is the
+// SHA256d of the whole serialized header, as in Zcash.
+constexpr int32_t kEquihashVersionBit = 1 << 26;
+
 struct BlockHeader {
     int32_t version = 0;
     Uint256 prev;
@@ -72,8 +84,14 @@ struct BlockHeader {
     u32 height = 0;
     u64 nonce64 = 0;
     Uint256 mix_hash;
+    // Equihash extension fields (serialized iff version & kEquihashVersionBit)
+    Uint256 nonce256;
+    Bytes solution;
 
     bool is_kawpow(u32 kawpow_activation_time) const { return time >= kawpow_activation_time; }
+    bool is_equihash() const { return (version & kEquihashVersionBit) != 0; }
+    Bytes equihash_input() const;  // kawpow_input() || nonce256 (112 bytes)
+    Uint256 equihash_hash(u32 kawpow_activation_time) const;  // SHA256d(serialized header)
     void serialize(Writer& w, u32 kawpow_activation_time) const;
     static BlockHeader deserialize(Reader& r, u32 kawpow_activation_time);
     Bytes bytes(u32 kawpow_activation_time) const { Writer w; serialize(w, kawpow_activation_time); return w.buf; }

@@ -442,3 +442,107 @@ extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_reconstruct(EquihashDe
             for (uint32_t t = threadIdx.x; t < 512; t += EQ_BLOCK) sb[1 + slot * 512 + t] = cur[t];
     }
 }
+
+// ------------------------------------------------------------------ batch verify
+// One 256-thread workgroup per packed solution (the extension's header check,
+// models/verify.py; SURVEY K10 `eqh_verify_batch`). The 512 leaves are
+// regenerated (BLAKE2b of input || le32(index / 2), half index % 2), then the
+// tree is folded level by level in LDS: at level l every node's children must
+// XOR to a string whose first 20*l bits are zero (all 200 at the root), the
+// left subtree's first index must be smaller than the right one's, and the
+// sorted index list must have no repeats — the rules of the CPU verifier
+// (csrc/pow/equihash.cpp).
+NX_DEV void eq_leaf(const EquihashVerifyParams& p, uint32_t s, uint32_t index, uint32_t w[8]) {
+    uint64_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = p.msgs[(size_t)s * 16 + i];
+    const uint32_t g = index >> 1;
+    const uint32_t off = p.input_len, wi = off >> 3, sh = (off & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if ((uint32_t)i == wi) m[i] |= (uint64_t)g << sh;
+        if (sh > 32 && (uint32_t)i == wi + 1) m[i] |= (uint64_t)g >> (64 - sh);
+    }
+    uint64_t out[8];
+    eq_blake2b_final(p.h0, m, (uint64_t)p.input_len + 4, out);
+    const int base = (index & 1) * 25;
+    w[0] = 0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int pos = base + 4 * i + k;
+            const uint32_t byte = (4 * i + k < 25) ? (uint32_t)((out[pos >> 3] >> (8 * (pos & 7))) & 0xFF) : 0u;
+            v = (v << 8) | byte;
+        }
+        w[i + 1] = v;
+    }
+}
+
+// first `bits` bits of the row w[1..7] (big-endian) are zero
+NX_DEV bool eq_prefix_zero(const uint32_t* w, int bits) {
+    for (int i = 1; i <= 7 && bits > 0; ++i, bits -= 32) {
+        const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> bits);
+        if (w[i] & mask) return false;
+    }
+    return true;
+}
+
+extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_verify(EquihashVerifyParams p) {
+    __shared__ uint32_t idx[512];
+    __shared__ uint32_t srt[512];
+    __shared__ uint32_t nodes[2][512 * 8];
+    __shared__ uint32_t verdict;
+    const uint32_t s = blockIdx.x;
+    if (threadIdx.x == 0) verdict = EQ_V_OK;
+    const uint8_t* sb = (const uint8_t*)(p.sols + (size_t)s * EQ_SOL_WORDS);
+    for (uint32_t i = threadIdx.x; i < 512; i += EQ_BLOCK) {
+        const uint32_t bit = 21u * i, byte = bit >> 3, sh = bit & 7;
+        const uint32_t v = ((uint32_t)sb[byte] << 24) | ((uint32_t)sb[byte + 1] << 16) | ((uint32_t)sb[byte + 2] << 8) |
+                           (byte + 3 < 1344 ? (uint32_t)sb[byte + 3] : 0u);
+        const uint32_t x = (v >> (32 - sh - 21)) & 0x1FFFFFu;
+        idx[i] = x;
+        srt[i] = x;
+        uint32_t w[8];
+        eq_leaf(p, s, x, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nodes[0][i * 8 + k] = w[k];
+    }
+    __syncthreads();
+    for (int l = 1; l <= 9; ++l) {
+        const uint32_t* src = nodes[(l - 1) & 1];
+        uint32_t* dst = nodes[l & 1];
+        const uint32_t n = 512u >> l;
+        for (uint32_t j = threadIdx.x; j < n; j += EQ_BLOCK) {
+            uint32_t x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = src[(2 * j) * 8 + k] ^ src[(2 * j + 1) * 8 + k];
+            if (!eq_prefix_zero(x, l == 9 ? 200 : 20 * l)) atomicMax(&verdict, l == 9 ? EQ_V_NONZERO : EQ_V_COLLISION);
+            if (idx[(2 * j) << (l - 1)] >= idx[(2 * j + 1) << (l - 1)]) atomicMax(&verdict, EQ_V_ORDER);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dst[j * 8 + k] = x[k];
+        }
+        __syncthreads();
+    }
+    // distinct indices: bitonic sort of the copy, then adjacent compare
+    for (uint32_t k = 2; k <= 512; k <<= 1) {
+        for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+            for (uint32_t t = threadIdx.x; t < 512; t += EQ_BLOCK) {
+                const uint32_t o = t ^ jj;
+                if (o > t) {
+                    const uint32_t a = srt[t], b = srt[o];
+                    if ((a > b) == ((t & k) == 0)) {
+                        srt[t] = b;
+                        srt[o] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t t = threadIdx.x; t < 511; t += EQ_BLOCK)
+        if (srt[t] == srt[t + 1]) atomicMax(&verdict, EQ_V_DUPLICATE);
+    __syncthreads();
+    if (threadIdx.x == 0) p.out[s] = verdict;
+}

@@ -1,0 +1,240 @@
+// KawPow light-mode batch verification for gfx950 (SURVEY K3,
+// `kawpow_verify_light_batch`; BASELINE config 5).
+//
+// Reference behaviour: progpow::hash / verify on a light epoch context
+// (src/crypto/ethash/lib/ethash/progpow.cpp:298-355, 431-495), which is what
+// CheckBlockHeader pays per header (~5 ms of one CPU core at epoch 384). The
+// DAG items a hash touches (64 rounds x one 2048-bit item = 4 x 512-bit items,
+// each 512 dependent light-cache parents, ethash.cpp:180-251) are recomputed
+// on the fly instead of reading a 4 GiB DAG — for fewer than ~10^5 headers per
+// epoch that is far cheaper than generating the whole DAG.
+//
+// CDNA4 mapping
+//   * one job (header, nonce, height) per 16-lane group, 16 jobs per 256-thread
+//     workgroup; every job of a batch is independent, so a 10k-header batch is
+//     ~2.5k waves — enough to cover the light-cache latency chain.
+//   * per round the group needs 4 x 512-bit items; lane quad q computes item
+//     4*index+q cooperatively: each lane owns 4 of the 16 mix words, the
+//     parent index word mix[j%16] is broadcast inside the quad with a DPP
+//     quad_perm (j%16 is a literal after unrolling by 16), and each lane
+//     gathers its 16 bytes of the 64-byte parent (the light cache is <= 64 MiB
+//     and stays in the 256 MiB Infinity Cache).
+//   * a lane then fetches its 4 words of the 256-byte item ((l^r)%16 selects
+//     the slice, owned by lane (l^r)%16) with four 16-wide shuffles.
+//   * the ProgPoW program is data (64 words per period, kawpow_program_words)
+//     staged per group in LDS, so jobs of any period share a launch; the
+//     32-word mix of each lane lives in LDS ([group][reg][lane], conflict-free
+//     for a group's uniform register index).
+#include "kernel_params.h"
+#include "keccak_device.hpp"
+
+#define KL_BLOCK 256
+#define KL_GROUPS (KL_BLOCK / 16)
+
+NX_DEV uint32_t kl_fnv1(uint32_t u, uint32_t v) { return (u * 0x01000193u) ^ v; }
+NX_DEV uint32_t kl_fnv1a(uint32_t h, uint32_t d) { return (h ^ d) * 0x01000193u; }
+NX_DEV uint32_t kl_mod(uint32_t x, const FastMod32& f) {
+    const uint32_t r = x - __umulhi(x, f.mb) * f.d;  // Barrett estimate, one correction (kernel_params.h)
+    return min(r, r - f.d);
+}
+NX_DEV uint32_t kl_clz(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : 32u; }
+
+NX_DEV uint32_t kl_merge(uint32_t a, uint32_t b, uint32_t kind, uint32_t rot) {
+    switch (kind) {
+        case 0: return a * 33u + b;
+        case 1: return (a ^ b) * 33u;
+        case 2: return __builtin_rotateleft32(a, rot) ^ b;
+        default: return __builtin_rotateright32(a, rot) ^ b;
+    }
+}
+
+NX_DEV uint32_t kl_math(uint32_t a, uint32_t b, uint32_t kind) {
+    switch (kind) {
+        case 0: return a + b;
+        case 1: return a * b;
+        case 2: return __umulhi(a, b);
+        case 3: return min(a, b);
+        case 4: return __builtin_rotateleft32(a, b);
+        case 5: return __builtin_rotateright32(a, b);
+        case 6: return a & b;
+        case 7: return a | b;
+        case 8: return a ^ b;
+        case 9: return kl_clz(a) + kl_clz(b);
+        default: return (uint32_t)(__builtin_popcount(a) + __builtin_popcount(b));
+    }
+}
+
+// Broadcast the value of lane C of each aligned quad (DPP quad_perm).
+template <int C>
+NX_DEV uint32_t kl_quad_bcast(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, C * 0x55, 0xf, 0xf, false);
+}
+
+// Words [4s, 4s+4) of 512-bit DAG item `index`, computed by the 4 lanes of a
+// quad together (s = this lane's position in the quad).
+NX_DEV uint4 kl_item512(const uint4* __restrict__ light, const FastMod32& lmod, uint32_t index, uint32_t s) {
+    uint32_t m[4];
+    {
+        // every quad lane runs the 64-byte keccak512 seed itself (cheap next to 512 parents)
+        const uint32_t li = kl_mod(index, lmod);
+        uint64_t in[8], out[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = light[(size_t)li * 4 + k];
+            in[2 * k] = ((uint64_t)v.y << 32) | v.x;
+            in[2 * k + 1] = ((uint64_t)v.w << 32) | v.z;
+        }
+        in[0] ^= index;
+        keccak512_64(in, out);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t w = (s & 2) ? ((s & 1) ? out[6 + (k >> 1)] : out[4 + (k >> 1)])
+                                       : ((s & 1) ? out[2 + (k >> 1)] : out[k >> 1]);
+            m[k] = (k & 1) ? (uint32_t)(w >> 32) : (uint32_t)w;
+        }
+    }
+#pragma unroll 1
+    for (uint32_t j = 0; j < 512; j += 16) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            // mix[k] lives in quad lane k/4, word k%4
+            uint32_t own = m[k & 3];
+            uint32_t mk;
+            switch (k >> 2) {
+                case 0: mk = kl_quad_bcast<0>(own); break;
+                case 1: mk = kl_quad_bcast<1>(own); break;
+                case 2: mk = kl_quad_bcast<2>(own); break;
+                default: mk = kl_quad_bcast<3>(own); break;
+            }
+            const uint32_t parent = kl_mod(kl_fnv1(index ^ (j + (uint32_t)k), mk), lmod);
+            const uint4 v = light[(size_t)parent * 4 + s];
+            m[0] = kl_fnv1(m[0], v.x);
+            m[1] = kl_fnv1(m[1], v.y);
+            m[2] = kl_fnv1(m[2], v.z);
+            m[3] = kl_fnv1(m[3], v.w);
+        }
+    }
+    // final keccak512 over the whole 16-word mix: gather it from the quad
+    uint32_t all[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        all[k] = kl_quad_bcast<0>(m[k]);
+        all[4 + k] = kl_quad_bcast<1>(m[k]);
+        all[8 + k] = kl_quad_bcast<2>(m[k]);
+        all[12 + k] = kl_quad_bcast<3>(m[k]);
+    }
+    uint64_t in[8], out[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) in[k] = ((uint64_t)all[2 * k + 1] << 32) | all[2 * k];
+    keccak512_64(in, out);
+    const uint64_t lo = (s & 2) ? ((s & 1) ? out[6] : out[4]) : ((s & 1) ? out[2] : out[0]);
+    const uint64_t hi = (s & 2) ? ((s & 1) ? out[7] : out[5]) : ((s & 1) ? out[3] : out[1]);
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+#define KL_MIX(r) mixs[(g * 32 + (r)) * 16 + lane]
+
+extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_light(KawpowLightParams p) {
+    __shared__ uint32_t l1[4096];
+    __shared__ uint32_t mixs[KL_GROUPS * 32 * 16];
+    __shared__ uint32_t progs[KL_GROUPS * KV_PROG_WORDS];
+    for (int i = threadIdx.x; i < 4096; i += KL_BLOCK) l1[i] = p.l1[i];
+    const uint32_t g = threadIdx.x >> 4;
+    const uint32_t lane = threadIdx.x & 15;
+    const uint32_t job = blockIdx.x * KL_GROUPS + g;
+    const bool valid = job < p.num_jobs;
+    const uint32_t jj = valid ? job : 0;
+    {
+        uint32_t pi = p.job_program[jj];
+        pi = pi < p.num_programs ? pi : 0;  // host validates; never index past the table
+#pragma unroll
+        for (int k = 0; k < 4; ++k) progs[g * KV_PROG_WORDS + lane * 4 + k] = p.programs[(size_t)pi * KV_PROG_WORDS + lane * 4 + k];
+    }
+    __syncthreads();
+    const uint32_t* prog = &progs[g * KV_PROG_WORDS];
+    const KawpowVerifyJob j = p.jobs[jj];
+    const uint4* light = (const uint4*)p.light;
+
+    uint32_t st2[8];
+    {
+        uint32_t s[25];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[i] = j.header[i];
+        s[8] = (uint32_t)j.nonce;
+        s[9] = (uint32_t)(j.nonce >> 32);
+        const uint32_t pad[15] = {0x72, 0x41, 0x56, 0x45, 0x4E, 0x43, 0x4F, 0x49, 0x4E, 0x4B, 0x41, 0x57, 0x50, 0x4F, 0x57};
+#pragma unroll
+        for (int i = 0; i < 15; ++i) s[10 + i] = pad[i];
+        keccak_f800(s);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st2[i] = s[i];
+    }
+    {
+        const uint32_t z0 = kl_fnv1a(0x811c9dc5u, st2[0]);
+        const uint32_t w0 = kl_fnv1a(z0, st2[1]);
+        const uint32_t jsr0 = kl_fnv1a(w0, lane);
+        uint32_t kz = z0, kw = w0, kj = jsr0, kc = kl_fnv1a(jsr0, lane);
+        for (int r = 0; r < 32; ++r) {
+            kz = 36969u * (kz & 0xffffu) + (kz >> 16);
+            kw = 18000u * (kw & 0xffffu) + (kw >> 16);
+            kc = 69069u * kc + 1234567u;
+            kj ^= (kj << 17);
+            kj ^= (kj >> 13);
+            kj ^= (kj << 5);
+            KL_MIX(r) = (((kz << 16) + kw) ^ kc) + kj;
+        }
+    }
+    const uint32_t q = lane >> 2, s = lane & 3;
+    for (uint32_t r = 0; r < 64; ++r) {
+        const uint32_t index = kl_mod(__shfl(KL_MIX(0), (int)(r & 15), 16), p.items);
+        const uint4 mine = kl_item512(light, p.light_items, index * 4 + q, s);
+        // lane l merges words ((l^r)%16)*4..+3 of the 2048-bit item: owned by lane (l^r)%16
+        const int src = (int)((lane ^ r) & 15);
+        const uint32_t dw[4] = {(uint32_t)__shfl((int)mine.x, src, 16), (uint32_t)__shfl((int)mine.y, src, 16),
+                                (uint32_t)__shfl((int)mine.z, src, 16), (uint32_t)__shfl((int)mine.w, src, 16)};
+        for (int i = 0; i < 18; ++i) {
+            if (i < 11) {
+                const uint32_t op = prog[i];
+                const uint32_t a = KL_MIX(op & 31);
+                uint32_t& dst = KL_MIX((op >> 8) & 31);
+                dst = kl_merge(dst, l1[a & 4095u], (op >> 16) & 3, op >> 24);
+            }
+            const uint32_t op = prog[11 + i];
+            const uint32_t mg = prog[29 + i];
+            const uint32_t v = kl_math(KL_MIX(op & 31), KL_MIX((op >> 8) & 31), (op >> 16) & 15);
+            uint32_t& dst = KL_MIX(op >> 24);
+            dst = kl_merge(dst, v, mg & 3, mg >> 8);
+        }
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t op = prog[47 + i];
+            uint32_t& dst = KL_MIX(op & 31);
+            dst = kl_merge(dst, dw[i], (op >> 8) & 3, op >> 16);
+        }
+    }
+    uint32_t lh = 0x811c9dc5u;
+    for (int r = 0; r < 32; ++r) lh = kl_fnv1a(lh, KL_MIX(r));
+    uint32_t digest[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t a = __shfl(lh, k, 16);
+        const uint32_t b = __shfl(lh, k + 8, 16);
+        digest[k] = kl_fnv1a(kl_fnv1a(0x811c9dc5u, a), b);
+    }
+    uint32_t st[25];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = st2[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[8 + i] = digest[i];
+    const uint32_t pad[9] = {0x72, 0x41, 0x56, 0x45, 0x4E, 0x43, 0x4F, 0x49, 0x4E};
+#pragma unroll
+    for (int i = 0; i < 9; ++i) st[16 + i] = pad[i];
+    keccak_f800(st);
+    if (valid && lane == 0) {
+        uint32_t* o = p.out + (size_t)job * 16;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            o[k] = digest[k];
+            o[8 + k] = st[k];
+        }
+    }
+}

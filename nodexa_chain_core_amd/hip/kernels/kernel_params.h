@@ -81,6 +81,22 @@ struct EquihashDev {
     uint32_t* sols;         // [inst][1 + MAX_SOL*512]: count, then solutions
 };
 
+// Batch verification of packed Equihash(200,9) solutions (equihash.hip eq_verify).
+#define EQ_SOL_WORDS 336  // 1344 bytes = 512 x 21-bit big-endian indices
+struct EquihashVerifyParams {
+    const uint64_t* msgs;   // [num][16] BLAKE2b message words of each input (as EquihashDev)
+    uint64_t h0[8];
+    uint32_t input_len;
+    uint32_t num;
+    const uint32_t* sols;   // [num][EQ_SOL_WORDS] packed solutions
+    uint32_t* out;          // [num] 0 = valid, else the failing rule (EQ_V_*)
+};
+#define EQ_V_OK 0
+#define EQ_V_COLLISION 1
+#define EQ_V_ORDER 2
+#define EQ_V_DUPLICATE 3
+#define EQ_V_NONZERO 4
+
 // Batch verification with the period program as data (kawpow_verify.hip).
 #define KV_PROG_WORDS 64
 struct KawpowVerifyParams {
@@ -92,6 +108,22 @@ struct KawpowVerifyParams {
     uint32_t num_jobs;
     uint32_t pad;
     struct FastMod32 items;
+};
+
+// Light-mode batch verification (kawpow_verify_light.hip): no DAG, every DAG
+// item a round touches is recomputed from the light cache. One job per 16-lane
+// group; jobs may mix periods freely (each group loads its own program).
+struct KawpowLightParams {
+    const void* light;                  // light cache of the batch's epoch (512-bit items)
+    const uint32_t* l1;                 // 4096-word L1 (first 16 KiB of the DAG, host-computed)
+    const struct KawpowVerifyJob* jobs;
+    const uint32_t* programs;           // [num_programs][KV_PROG_WORDS]
+    const uint32_t* job_program;        // per job: program index
+    uint32_t* out;                      // per job: mix[8], final[8]
+    uint32_t num_jobs;
+    uint32_t num_programs;
+    struct FastMod32 light_items;       // modulo by the number of 512-bit light items
+    struct FastMod32 items;             // modulo by the number of 2048-bit DAG items
 };
 
 struct KawpowHashParams {

@@ -242,6 +242,27 @@ PYBIND11_MODULE(_hip, m) {
     });
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
     m.attr("KV_PROG_WORDS") = KV_PROG_WORDS;
+    m.def("launch_kawpow_verify_light", [](const Kernel& k, uintptr_t light, uint32_t light_items, uintptr_t l1,
+                                           uint32_t dag_items2048, uintptr_t jobs, uintptr_t programs,
+                                           uint32_t num_programs, uintptr_t job_program, uint32_t num_jobs,
+                                           uintptr_t out, uintptr_t stream) {
+        if (num_programs == 0) throw std::invalid_argument("no programs");
+        KawpowLightParams p{};
+        p.light = reinterpret_cast<const void*>(light);
+        p.l1 = reinterpret_cast<const uint32_t*>(l1);
+        p.jobs = reinterpret_cast<const KawpowVerifyJob*>(jobs);
+        p.programs = reinterpret_cast<const uint32_t*>(programs);
+        p.job_program = reinterpret_cast<const uint32_t*>(job_program);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        p.num_jobs = num_jobs;
+        p.num_programs = num_programs;
+        p.light_items = make_fastmod(light_items);
+        p.items = make_fastmod(dag_items2048);
+        const unsigned groups = 256 / 16;  // one job per 16-lane group (KL_BLOCK / 16)
+        const unsigned grid = (num_jobs + groups - 1) / groups;
+        if (grid == 0) return;
+        k.launch_bytes(dim3(grid), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("launch_kawpow_verify_batch", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t jobs,
                                            uintptr_t programs, uintptr_t job_program, uint32_t num_jobs, uintptr_t out,
                                            uintptr_t stream) {
@@ -267,6 +288,21 @@ PYBIND11_MODULE(_hip, m) {
     m.attr("EQ_MAX_CAND") = EQ_MAX_CAND;
     m.attr("EQ_MAX_SOL") = EQ_MAX_SOL;
     m.attr("EQ_MAX_BANKS") = EQ_MAX_BANKS;
+    m.attr("EQ_SOL_WORDS") = EQ_SOL_WORDS;
+    m.def("launch_equihash_verify", [](const Kernel& k, std::vector<uint64_t> h0, uintptr_t msgs, uint32_t input_len,
+                                       uint32_t num, uintptr_t sols, uintptr_t out, uintptr_t stream) {
+        if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
+        if (input_len > 124) throw std::invalid_argument("equihash input must be <= 124 bytes");
+        if (num == 0) return;
+        EquihashVerifyParams p{};
+        p.msgs = reinterpret_cast<const uint64_t*>(msgs);
+        for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
+        p.input_len = input_len;
+        p.num = num;
+        p.sols = reinterpret_cast<const uint32_t*>(sols);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        k.launch_bytes(dim3(num), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("launch_equihash_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
                                       uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
                                       uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols,

@@ -1,0 +1,192 @@
+"""Synthetic header chains with real proof of work and real retargeting.
+
+BASELINE config 5 verifies "10k synthetic KawPow+Equihash headers + DarkGravityWave";
+there is no chain data in this environment, so this module mines one:
+  * testnet rules (DGW from block 1, 180-block window, pow limit 2^248 — ~256
+    hashes per header) with the KawPow activation moved to genesis+1, so every
+    header is a 120-byte KawPow header;
+  * optionally an Equihash(200,9) era after `n_kawpow` headers (the new header
+    extension, csrc/chain/primitives.hpp): extended headers with a 32-byte nonce
+    and a 1344-byte solution, DGW bootstrapping the era from the Equihash limit;
+  * block times jittered around the 60 s target so DGW actually retargets.
+Each header's proof of work is found by search:
+  * backend "cpu": the golden models (`_core.kawpow_search_full` over a lazily
+    filled host DAG; `_core.equihash_solve_cpu`) — small chains for tests;
+  * backend "gpu": the DAG-resident batch kernel (ops/verify.py) as a
+    period-agnostic KawPow searcher, and the gfx950 Equihash solver.
+The chain is accepted header by header into a C++ HeaderChain (contextual
+checks + DGW) while it is built, so every header in the output is valid.
+Files: concatenated serialized headers + `<file>.json` with the parameters.
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+
+from .. import core
+from ..chain.header import from_progpow, to_progpow
+from ..chain.state import make_params
+
+_core = core()
+
+
+def synthetic_params(network: str = "test", equihash_activation_time: int | None = None):
+    g = _core.make_chain_params(network)
+    return make_params(network, kawpow_activation_time=int(g.genesis.header.time) + 1,
+                       equihash_activation_time=equihash_activation_time)
+
+
+def _boundary(bits: int) -> bytes:
+    target, neg, ovf = _core.set_compact(bits)
+    return target.to_bytes(32, "big") if not (neg or ovf) else bytes(32)
+
+
+def _target(bits: int) -> int:
+    target, neg, ovf = _core.set_compact(bits)
+    return 0 if (neg or ovf) else target
+
+
+class _CpuKawpow:
+    def __init__(self, threads: int = 0):
+        self.threads = threads or (os.cpu_count() or 4)
+        self.dags: dict[int, object] = {}
+
+    def __call__(self, height: int, header_hash: bytes, boundary: bytes, start: int):
+        epoch = height // _core.EPOCH_LENGTH
+        dag = self.dags.get(epoch)
+        if dag is None:
+            dag = self.dags[epoch] = _core.HostDag(_core.get_epoch_context(epoch))
+        ok, nonce, fin, mix = _core.kawpow_search_full(dag, height, header_hash, boundary, start, 512, self.threads)
+        return ((nonce, fin, mix) if ok else None), 512
+
+
+class _GpuKawpow:
+    def __init__(self, device: int = 0, width: int = 2048):
+        from ..ops import verify
+
+        self.verify, self.device, self.width = verify, device, width
+
+    def __call__(self, height: int, header_hash: bytes, boundary: bytes, start: int):
+        nonces = list(range(start, start + self.width))
+        res = self.verify.gpu_full_hash([height] * self.width, [header_hash] * self.width, nonces,
+                                        device=self.device, mode="dag")
+        for n, (fin, mix) in zip(nonces, res):
+            if _core.hash_le(fin, boundary):
+                return (n, fin, mix), self.width
+        return None, self.width
+
+
+class _CpuEquihash:
+    batch = 1
+
+    def solve(self, inputs: list[bytes]) -> list[list[list[int]]]:
+        p = _core.EquihashParams(200, 9)
+        return [_core.equihash_solve_cpu(p, x, 16, 0)[0] for x in inputs]  # (solutions, stats)
+
+
+class _GpuEquihash:
+    batch = 8
+
+    def __init__(self, device: int = 0):
+        from ..ops.equihash import EquihashSolver
+
+        self.solver = EquihashSolver(num_inst=8, device=device)
+
+    def solve(self, inputs: list[bytes]) -> list[list[list[int]]]:
+        return self.solver.solve(inputs)
+
+
+def _solve_equihash_header(h, params, solver, rng) -> None:
+    """Search nonce256 values until a solution's SHA256d(header) meets nBits."""
+    p = _core.EquihashParams(params.equihash_n, params.equihash_k)
+    target = _target(h.bits)
+    act = params.kawpow_activation_time
+    while True:
+        nonces = [rng.getrandbits(256).to_bytes(32, "little") for _ in range(solver.batch)]
+        inputs = []
+        for nn in nonces:
+            h.nonce256 = nn
+            inputs.append(h.equihash_input())
+        for nn, sols in zip(nonces, solver.solve(inputs)):
+            for sol in sols:
+                h.nonce256 = nn
+                h.solution = _core.equihash_pack(p, sol)
+                if int.from_bytes(h.equihash_hash(act), "little") <= target:
+                    return
+
+
+def build_chain(n_kawpow: int, n_equihash: int = 0, network: str = "test", backend: str = "cpu", seed: int = 1,
+                device: int = 0, spacing: tuple[int, int] = (20, 100), progress=None):
+    """Mine `n_kawpow` KawPow headers then `n_equihash` Equihash-extension headers on
+    top of `network`'s genesis. Returns (params, headers)."""
+    rng = random.Random(seed)
+    base = synthetic_params(network)
+    times, t = [], int(base.genesis.header.time)
+    for _ in range(n_kawpow + n_equihash):
+        t += rng.randint(*spacing)
+        times.append(t)
+    eq_act = times[n_kawpow] if n_equihash else None
+    params = synthetic_params(network, eq_act)
+    chain = _core.HeaderChain(params)
+    kp = _GpuKawpow(device) if backend == "gpu" else _CpuKawpow()
+    eq = (_GpuEquihash(device) if backend == "gpu" else _CpuEquihash()) if n_equihash else None
+    out = []
+    for i in range(1, n_kawpow + n_equihash + 1):
+        h = _core.BlockHeader()
+        h.version = 0x30000000 | (_core.EQUIHASH_VERSION_BIT if i > n_kawpow else 0)
+        h.prev = chain.tip().hash
+        h.merkle_root = _core.sha256d(b"nodexa-synthetic-%d-%d" % (seed, i))
+        h.time = times[i - 1]
+        h.height = i
+        h.bits = chain.next_bits(h)
+        if i <= n_kawpow:
+            hh = to_progpow(h.kawpow_header_hash())
+            boundary = _boundary(h.bits)
+            start = rng.getrandbits(40) << 16
+            found = None
+            while found is None:
+                found, tried = kp(i, hh, boundary, start)
+                start += tried
+            nonce, fin, mix = found
+            h.nonce64 = nonce
+            h.mix_hash = from_progpow(mix)
+        else:
+            _solve_equihash_header(h, params, eq, rng)
+        r = chain.accept_header(h, h.time + 7200, i > n_kawpow)  # Equihash era: full check while mining
+        if not r.ok:
+            raise RuntimeError(f"synthetic header {i} rejected: {r.reject}")
+        out.append(h)
+        if progress and i % 500 == 0:
+            progress(i)
+    return params, out
+
+
+def build_kawpow_chain(n: int, network: str = "test", backend: str = "cpu", seed: int = 1, device: int = 0,
+                       spacing: tuple[int, int] = (20, 100), progress=None):
+    return build_chain(n, 0, network, backend, seed, device, spacing, progress)
+
+
+def save(path: str, params, headers) -> None:
+    act = params.kawpow_activation_time
+    with open(path, "wb") as f:
+        for h in headers:
+            f.write(h.serialize(act))
+    meta = {"network": params.network_id, "kawpow_activation_time": int(params.kawpow_activation_time),
+            "equihash_activation_time": int(params.equihash_activation_time), "headers": len(headers),
+            "equihash_headers": sum(1 for h in headers if h.is_equihash())}
+    with open(path + ".json", "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+def load(path: str):
+    with open(path + ".json") as f:
+        meta = json.load(f)
+    eq = meta["equihash_activation_time"]
+    params = make_params(meta["network"], kawpow_activation_time=meta["kawpow_activation_time"],
+                         equihash_activation_time=None if eq == 0xFFFFFFFF else eq)
+    with open(path, "rb") as f:
+        headers = _core.deserialize_headers(f.read(), params.kawpow_activation_time)
+    if len(headers) != meta["headers"]:
+        raise ValueError("header count mismatch")
+    return params, headers

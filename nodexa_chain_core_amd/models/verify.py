@@ -31,11 +31,20 @@ def _job(params, h):
             target.to_bytes(32, "big") if not (neg or ovf) else bytes(32))
 
 
-def verify_headers(params, headers, gpus: list[int] | None = None, threads: int = 0) -> list[dict]:
+def verify_headers(params, headers, gpus: list[int] | None = None, threads: int = 0,
+                   mode: str = "auto") -> list[dict]:
+    """Full PoW check of every header: {"valid", "hash", "reason"?} per header.
+
+    gpus: device ids (one host thread per GPU, the batch split in contiguous
+    chunks); None/[] = all host cores with the CPU golden model. mode: GPU
+    kernel choice, see ops/verify.py."""
     jobs = [_job(params, h) for h in headers]
     out: list[dict] = [{} for _ in jobs]
-    todo = []
+    todo, eq_todo = [], []
     for i, (bn, hh, nonce, mix, boundary) in enumerate(jobs):
+        if headers[i].is_equihash():
+            eq_todo.append(i)
+            continue
         if headers[i].time < params.kawpow_activation_time:
             out[i] = {"valid": False, "reason": "pre-kawpow header (X16R) not handled by the batch verifier"}
             continue
@@ -44,13 +53,20 @@ def verify_headers(params, headers, gpus: list[int] | None = None, threads: int 
             out[i] = {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(from_progpow(fin))}
             continue
         todo.append(i)
-    if gpus:
+    if gpus and todo:
         from ..ops.verify import gpu_full_hash
 
-        res = gpu_full_hash([jobs[i][0] for i in todo], [jobs[i][1] for i in todo], [jobs[i][2] for i in todo],
-                            device=gpus[0])
-        for i, (fin, mix) in zip(todo, res):
-            out[i] = _finish(jobs[i], fin, mix)
+        def run(dev: int, part: list[int]):
+            return part, gpu_full_hash([jobs[i][0] for i in part], [jobs[i][1] for i in part],
+                                       [jobs[i][2] for i in part], device=dev, mode=mode)
+
+        k = len(gpus)
+        step = -(-len(todo) // k)
+        parts = [(d, todo[j * step:(j + 1) * step]) for j, d in enumerate(gpus) if todo[j * step:(j + 1) * step]]
+        with cf.ThreadPoolExecutor(max_workers=len(parts)) as ex:
+            for part, res in ex.map(lambda a: run(*a), parts):
+                for i, (fin, mix) in zip(part, res):
+                    out[i] = _finish(jobs[i], fin, mix)
     else:
         threads = threads or (os.cpu_count() or 4)
 
@@ -62,7 +78,42 @@ def verify_headers(params, headers, gpus: list[int] | None = None, threads: int 
         with cf.ThreadPoolExecutor(max_workers=threads) as ex:
             for i, (fin, mix) in zip(todo, ex.map(one, todo)):
                 out[i] = _finish(jobs[i], fin, mix)
+    if eq_todo:
+        _verify_equihash(params, headers, eq_todo, out, gpus, threads)
     return out
+
+
+def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, threads: int) -> None:
+    """Equihash-extension headers: solution validity (GPU batch kernel when GPUs are given,
+    else the C++ verifier on all cores) and SHA256d(header) <= nBits."""
+    act = params.kawpow_activation_time
+    ok: dict[int, bool]
+    if gpus:
+        from ..ops.equihash import verify_solutions
+
+        res = verify_solutions([headers[i].equihash_input() for i in idxs], [headers[i].solution for i in idxs],
+                               device=gpus[0])
+        ok = dict(zip(idxs, res))
+    else:
+        p = _core.EquihashParams(params.equihash_n, params.equihash_k)
+
+        def one(i):
+            h = headers[i]
+            if len(h.solution) != p.solution_bytes:
+                return False
+            return bool(_core.equihash_verify(p, h.equihash_input(), _core.equihash_unpack(p, h.solution))[0])
+
+        with cf.ThreadPoolExecutor(max_workers=threads or (os.cpu_count() or 4)) as ex:
+            ok = dict(zip(idxs, ex.map(one, idxs)))
+    for i in idxs:
+        h = headers[i]
+        hsh = h.equihash_hash(act)
+        if not ok[i]:
+            out[i] = {"valid": False, "reason": "invalid-solution", "hash": _core.u256_hex(hsh)}
+        elif not _core.check_proof_of_work(hsh, h.bits, params):
+            out[i] = {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(hsh)}
+        else:
+            out[i] = {"valid": True, "hash": _core.u256_hex(hsh)}
 
 
 def _finish(job, fin: bytes, mix: bytes) -> dict:
@@ -72,3 +123,27 @@ def _finish(job, fin: bytes, mix: bytes) -> dict:
     if not _core.hash_le(fin, boundary):
         return {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(from_progpow(fin))}
     return {"valid": True, "hash": _core.u256_hex(from_progpow(fin))}
+
+
+def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None = None, mode: str = "auto") -> dict:
+    """ProcessNewBlockHeaders for a batch (src/validation.cpp:12017-12035): PoW of the whole
+    batch in bulk (GPU or all cores), then the contextual rules — nBits == DarkGravityWave,
+    MTP, future time, version — header by header on the host chain. Like the reference it
+    stops at the first invalid header. Returns counts, the first rejection and stage times."""
+    import time
+
+    t0 = time.perf_counter()
+    pow_res = verify_headers(chain.params, headers, gpus=gpus, mode=mode)
+    t1 = time.perf_counter()
+    accepted, reject = 0, None
+    for i, (h, r) in enumerate(zip(headers, pow_res)):
+        if not r["valid"]:
+            reject = {"index": i, "reason": r.get("reason", "high-hash")}
+            break
+        ar = chain.accept_header(h, adjusted_time, False)
+        if not ar.ok:
+            reject = {"index": i, "reason": ar.reject}
+            break
+        accepted += 1
+    t2 = time.perf_counter()
+    return {"accepted": accepted, "reject": reject, "pow_s": t1 - t0, "context_s": t2 - t1}

@@ -37,6 +37,40 @@ def blake2b_h0(n: int = 200, k: int = 9) -> list[int]:
     return [a ^ b for a, b in zip(iv, words)]
 
 
+def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | None = None) -> list[bool]:
+    """GPU batch check of packed (n=200, k=9) solutions (hip/kernels/equihash.hip eq_verify):
+    one workgroup per solution. `inputs` are the 112-byte header inputs."""
+    if len(inputs) != len(solutions):
+        raise ValueError("inputs and solutions differ in length")
+    runtime.require_gpu()
+    h = runtime.hip()
+    n = len(inputs)
+    out_ok = [False] * n
+    good = [i for i in range(n) if len(solutions[i]) == 4 * h.EQ_SOL_WORDS and len(inputs[i]) <= 124]
+    if not good:
+        return out_ok
+    lens = {len(inputs[i]) for i in good}
+    if len(lens) != 1:
+        raise ValueError("one input length per batch")
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
+    msgs = bytearray(len(good) * 128)
+    sols = bytearray(len(good) * 4 * h.EQ_SOL_WORDS)
+    for k, i in enumerate(good):
+        msgs[k * 128:k * 128 + len(inputs[i])] = inputs[i]
+        sols[k * 4 * h.EQ_SOL_WORDS:(k + 1) * 4 * h.EQ_SOL_WORDS] = solutions[i]
+    with torch.cuda.device(dev):
+        kern = runtime.static_kernel("equihash", "eq_verify")
+        dm = torch.frombuffer(msgs, dtype=torch.int64).to(dev)
+        ds = torch.frombuffer(sols, dtype=torch.int32).to(dev)
+        res = torch.full((len(good),), -1, dtype=torch.int32, device=dev)
+        h.launch_equihash_verify(kern, blake2b_h0(), dm.data_ptr(), lens.pop(), len(good), ds.data_ptr(),
+                                 res.data_ptr(), runtime.current_stream_handle())
+        verdicts = res.cpu().tolist()
+    for k, i in enumerate(good):
+        out_ok[i] = verdicts[k] == 0
+    return out_ok
+
+
 class EquihashSolver:
     def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 8,
                  code_object: str | None = None):

@@ -23,7 +23,10 @@ _DAG_CHUNK = 1 << 22
 
 
 class DeviceEpoch:
-    def __init__(self, epoch: int, device: int | torch.device | None = None, ctx=None, world_size: int = 1):
+    def __init__(self, epoch: int, device: int | torch.device | None = None, ctx=None, world_size: int = 1,
+                 light_only: bool = False):
+        """`light_only`: keep just the light cache and the 16 KiB L1 on the device (light-mode
+        batch verification, ops/verify.py) — no DAG allocation."""
         runtime.require_gpu()
         self.epoch = int(epoch)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
@@ -36,10 +39,15 @@ class DeviceEpoch:
         with torch.cuda.device(self.device):
             self.light = torch.empty(int(self.ctx.light_bytes), dtype=torch.uint8, device=self.device)
             runtime.hip().memcpy_htod(self.light.data_ptr(), self.ctx.light_cache_ptr(), int(self.ctx.light_bytes))
-            # padded to a whole number of equal shards so RCCL can all-gather in place
-            self._storage = torch.empty(self.shard_bytes(world_size) * world_size, dtype=torch.uint8,
-                                        device=self.device)
-            self.dag = self._storage[:self.dag_bytes]
+            self.l1 = torch.tensor(self.ctx.l1, dtype=torch.int64).to(torch.int32).to(self.device)
+            if light_only:
+                self._storage = None
+                self.dag = None
+            else:
+                # padded to a whole number of equal shards so RCCL can all-gather in place
+                self._storage = torch.empty(self.shard_bytes(world_size) * world_size, dtype=torch.uint8,
+                                            device=self.device)
+                self.dag = self._storage[:self.dag_bytes]
         self.built = False
 
     # ------------------------------------------------------------------
@@ -62,6 +70,8 @@ class DeviceEpoch:
         return first, min(per, self.items512 - first)
 
     def build(self, shard: tuple[int, int] | None = None, stream: int | None = None) -> None:
+        if self.dag is None:
+            raise ValueError("light-only DeviceEpoch has no DAG to build")
         h = runtime.hip()
         with torch.cuda.device(self.device):
             k = runtime.static_kernel("ethash_dag", "ethash_dag_build")

@@ -36,6 +36,29 @@ def test_gpu_solutions_valid_and_match_cpu(core, solver):
     assert total_gpu >= total_cpu - 1  # bucket-capacity drops may lose at most a rare solution
 
 
+def test_gpu_batch_verify_matches_cpu(core, solver):
+    from nodexa_chain_core_amd.ops.equihash import verify_solutions
+
+    p = core.EquihashParams(200, 9)
+    inputs = [bytes([3]) * 80 + i.to_bytes(32, "little") for i in range(4)]
+    sols = solver.solve(inputs)
+    batch_in, batch_sol, expect = [], [], []
+    for inp, ss in zip(inputs, sols):
+        for s in ss:
+            packed = core.equihash_pack(p, s)
+            batch_in.append(inp)
+            batch_sol.append(packed)
+            expect.append(True)
+            # corruptions the CPU verifier rejects: a flipped leaf index, swapped subtrees, a repeat
+            for mut in (lambda x: x[:1] + [x[1] ^ 1] + x[2:], lambda x: x[256:] + x[:256], lambda x: x[:511] + x[:1]):
+                bad = mut(list(s))
+                batch_in.append(inp)
+                batch_sol.append(core.equihash_pack(p, bad))
+                expect.append(bool(core.equihash_verify(p, inp, bad)[0]))
+    assert any(expect) and not all(expect)
+    assert verify_solutions(batch_in, batch_sol, device=0) == expect
+
+
 def test_gpu_repeatable(solver):
     inputs = [bytes([7]) * 112 for _ in range(4)]
     a = solver.solve(inputs)

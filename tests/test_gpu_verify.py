@@ -8,27 +8,48 @@ from kawpow_vectors import VECTORS
 pytestmark = pytest.mark.gpu
 
 
-def test_verify_batch_multi_period_vs_cpu(core, gpu):
+@pytest.mark.parametrize("mode", ["dag", "light"])
+def test_verify_batch_multi_period_vs_cpu(core, gpu, mode):
     from nodexa_chain_core_amd.ops.verify import gpu_full_hash
 
     rng = random.Random(5)
     blocks = [rng.randrange(0, 7500) for _ in range(150)] + [7, 8, 9]  # many periods, epoch 0
     headers = [rng.randbytes(32) for _ in blocks]
     nonces = [rng.getrandbits(64) for _ in blocks]
-    res = gpu_full_hash(blocks, headers, nonces, device=0)
+    res = gpu_full_hash(blocks, headers, nonces, device=0, mode=mode)
     ctx = core.get_epoch_context(0)
     for i in range(0, len(blocks), 7):
         assert res[i] == core.kawpow_hash(ctx, blocks[i], headers[i], nonces[i]), i
 
 
-def test_verify_batch_reference_vectors(core, gpu):
+@pytest.mark.parametrize("mode", ["dag", "light"])
+def test_verify_batch_reference_vectors(core, gpu, mode):
     from nodexa_chain_core_amd.ops.verify import gpu_full_hash
 
     vecs = [v for v in VECTORS if v[0] < 7500]
     res = gpu_full_hash([v[0] for v in vecs], [bytes.fromhex(v[1]) for v in vecs], [int(v[2], 16) for v in vecs],
-                        device=0)
+                        device=0, mode=mode)
     for (block, _, _, mix, final), (f, m) in zip(vecs, res):
         assert (m.hex(), f.hex()) == (mix, final), block
+
+
+def test_verify_light_other_epoch_and_mixed_batch(core, gpu):
+    """Light mode at epoch 4 (reference vector) in one call with epoch-0 jobs."""
+    from kawpow_vectors import HASH_30000
+
+    from nodexa_chain_core_amd.ops.verify import gpu_full_hash
+
+    block, header, nonce, mix, final = HASH_30000
+    rng = random.Random(9)
+    blocks = [block] + [rng.randrange(0, 7500) for _ in range(20)] + [block + 5]
+    headers = [bytes.fromhex(header)] + [rng.randbytes(32) for _ in range(21)]
+    nonces = [nonce] + [rng.getrandbits(64) for _ in range(21)]
+    res = gpu_full_hash(blocks, headers, nonces, device=0, mode="light")
+    assert (res[0][1].hex(), res[0][0].hex()) == (mix, final)
+    ctx0, ctx4 = core.get_epoch_context(0), core.get_epoch_context(4)
+    for i in (1, 10, 20):
+        assert res[i] == core.kawpow_hash(ctx0, blocks[i], headers[i], nonces[i])
+    assert res[-1] == core.kawpow_hash(ctx4, blocks[-1], headers[-1], nonces[-1])
 
 
 def test_node_gpu_mining_and_batch_verify(core, gpu, tmp_path):

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: batch block-header verification + DarkGravityWave retarget.
+
+Loads a mined synthetic testnet KawPow chain (tests/data/testnet_kawpow_10k.hdr,
+models/synthetic.py; built on the GPU when missing) and times
+ProcessNewBlockHeaders-style acceptance of the whole batch into a fresh header
+chain: full KawPow PoW of every header in bulk (GPU light mode, GPU DAG mode, or
+all host cores), then nBits == DGW / MTP / time / version per header.
+The reference path (CheckBlockHeader -> GetHashFull, light epoch context, one
+header at a time under cs_main) is timed on a sample on one host core.
+
+    python tools/verify_bench.py [--gpus N] [--modes light dag] [--cpu-sample 40]
+Prints one JSON line per measured path.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+FIXTURE = os.path.join(ROOT, "tests", "data", "testnet_kawpow_10k.hdr")
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--modes", nargs="*", default=["light", "dag"])
+    ap.add_argument("--cpu-sample", type=int, default=40, help="headers timed on the serial reference path")
+    ap.add_argument("--cpu-threads", action="store_true", help="also time all-host-core verification of the batch")
+    ap.add_argument("--file", default=FIXTURE)
+    a = ap.parse_args()
+
+    from nodexa_chain_core_amd import _core
+    from nodexa_chain_core_amd.models import synthetic
+    from nodexa_chain_core_amd.models.verify import process_headers
+
+    if os.path.exists(a.file):
+        params, headers = synthetic.load(a.file)
+    else:
+        params, headers = synthetic.build_kawpow_chain(10000, backend="gpu")
+    adjusted = headers[-1].time + 3600
+    n = len(headers)
+    bits = {h.bits for h in headers}
+    base = {"config": "batch block-verify + DGW (BASELINE config 5)", "headers": n,
+            "distinct_nbits": len(bits), "epochs": sorted({h.height // _core.EPOCH_LENGTH for h in headers})}
+
+    # reference path: serial full check per header (CpuPowVerifier == GetHashFull light) + DGW
+    chain = _core.HeaderChain(params)
+    t = time.perf_counter()
+    for h in headers[:a.cpu_sample]:
+        r = chain.accept_header(h, adjusted, True)
+        assert r.ok, r.reject
+    dt = time.perf_counter() - t
+    ref = dict(base, path="reference-equivalent serial CPU (1 core, light KawPow + DGW)",
+               headers_timed=a.cpu_sample, headers_per_s=round(a.cpu_sample / dt, 2), ms_per_header=round(dt / a.cpu_sample * 1e3, 3))
+    print(json.dumps(ref), flush=True)
+
+    if a.cpu_threads:
+        chain = _core.HeaderChain(params)
+        r = process_headers(chain, headers, adjusted, gpus=None)
+        tot = r["pow_s"] + r["context_s"]
+        print(json.dumps(dict(base, path=f"all host cores ({os.cpu_count()})", accepted=r["accepted"],
+                              reject=r["reject"], pow_s=round(r["pow_s"], 3), context_s=round(r["context_s"], 3),
+                              headers_per_s=round(n / tot, 1))), flush=True)
+
+    if a.gpus > 0:
+        import torch
+
+        gpus = list(range(min(a.gpus, torch.cuda.device_count())))
+        for mode in a.modes:
+            # warm-up (epoch contexts, code objects, light caches / DAGs)
+            process_headers(_core.HeaderChain(params), headers[:64], adjusted, gpus=gpus, mode=mode)
+            chain = _core.HeaderChain(params)
+            torch.cuda.synchronize()
+            r = process_headers(chain, headers, adjusted, gpus=gpus, mode=mode)
+            tot = r["pow_s"] + r["context_s"]
+            out = dict(base, path=f"GPU {mode} x{len(gpus)}", accepted=r["accepted"], reject=r["reject"],
+                       pow_s=round(r["pow_s"], 4), context_s=round(r["context_s"], 4),
+                       headers_per_s=round(n / tot, 1), vs_reference_serial=round(n / tot / ref["headers_per_s"], 1))
+            print(json.dumps(out), flush=True)
+            if r["accepted"] != n:
+                return 1
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
