@@ -1,4 +1,5 @@
 #include "x16r.hpp"
+#include "x16r_prims.hpp"
 
 #include <stdexcept>
 
@@ -145,15 +146,28 @@ int x16r_selection(const u8 prev_le[32], int index) {
     return (i % 2 == 1) ? (prev_le[i / 2] >> 4) : (prev_le[i / 2] & 0x0F);
 }
 
-bool x16r_slot_available(int algo) { return algo == 0 || algo == 4 || algo == 15; }
+bool x16r_slot_available(int algo) { return algo >= 0 && algo <= 16; }
 
 Hash512 x16r_single(int algo, const u8* data, size_t n) {
     switch (algo) {
         case 0: return blake512(data, n);
+        case 1: return bmw512(data, n);
+        case 2: return groestl512(data, n);
+        case 3: return jh512(data, n);
         case 4: return keccak512(data, n);
+        case 5: return skein512(data, n);
+        case 6: return luffa512(data, n);
+        case 7: return cubehash512(data, n);
+        case 8: return shavite512(data, n);
+        case 9: return simd512(data, n);
+        case 10: return echo512(data, n);
+        case 11: return hamsi512(data, n);
+        case 12: return fugue512(data, n);
+        case 13: return shabal512(data, n);
+        case 14: return whirlpool512(data, n);
         case 15: return sha512_hash(data, n);
-        default:
-            throw std::runtime_error("X16R slot " + std::to_string(algo) + " is not available in this build");
+        case 16: return tiger192_padded(data, n);
+        default: throw std::invalid_argument("X16R slot out of range: " + std::to_string(algo));
     }
 }
 

@@ -21,9 +21,6 @@ Hash512 x16r_single(int algo, const u8* data, size_t n);
 bool x16r_slot_available(int algo);
 int x16r_selection(const u8 prev_le[32], int index);
 
-// Individual primitives (x16r_*.cpp).
-Hash512 blake512(const u8* data, size_t n);
-Hash512 sha512_hash(const u8* data, size_t n);
-Hash512 tiger192_padded(const u8* data, size_t n);
+// Individual primitives: x16r_prims.hpp.
 
 }  // namespace nodexa

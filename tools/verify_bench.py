@@ -41,7 +41,10 @@ def main() -> int:
     if os.path.exists(a.file):
         params, headers = synthetic.load(a.file)
     else:
-        params, headers = synthetic.build_kawpow_chain(10000, backend="gpu")
+        t0 = time.time()
+        params, headers = synthetic.build_kawpow_chain(
+            10000, backend="gpu", progress=lambda i: print(f"[verify_bench] mined {i} headers, {time.time() - t0:.0f}s",
+                                                          file=sys.stderr, flush=True))
     adjusted = headers[-1].time + 3600
     n = len(headers)
     bits = {h.bits for h in headers}
