@@ -193,7 +193,212 @@ Hash512 echo512(const u8* data, size_t n) {
     return out;
 }
 
-Hash512 shavite512(const u8*, size_t) { throw std::runtime_error("shavite512: not implemented"); }
-Hash512 fugue512(const u8*, size_t) { throw std::runtime_error("fugue512: not implemented"); }
+// ================================================================ SHAvite-3-512
+// HAIFA compression C512: 512-bit chaining value as four 128-bit blocks, 1024-bit
+// message expanded into 448 round-key words (AES rounds + linear steps, the
+// 128-bit bit counter injected at four fixed positions), 14 Feistel-like rounds
+// of four keyless AES rounds per branch.
+namespace {
+
+u32 le_word(const u8* p) { return load_le32(p); }
+
+void aes_words(u32 x[4]) {  // one keyless AES round on four little-endian column words
+    u8 b[16];
+    for (int i = 0; i < 4; ++i) store_le32(b + 4 * i, x[i]);
+    aes_round(b, nullptr);
+    for (int i = 0; i < 4; ++i) x[i] = le_word(b + 4 * i);
+}
+
+void shavite_c512(u32 h[16], const u8 msg[128], const u32 cnt[4]) {
+    u32 rk[448];
+    for (int i = 0; i < 32; ++i) rk[i] = le_word(msg + 4 * i);
+    // counter words xored into the expansion, with the fourth complemented
+    auto inject = [&](int u, int a, int b, int c, int d) {
+        rk[u] ^= cnt[a]; rk[u + 1] ^= cnt[b]; rk[u + 2] ^= cnt[c]; rk[u + 3] ^= ~cnt[d];
+    };
+    int u = 32;
+    for (;;) {
+        for (int s = 0; s < 8; ++s) {  // nonlinear expansion: AES of the rotated 4 words 32 back
+            u32 x[4] = {rk[u - 31], rk[u - 30], rk[u - 29], rk[u - 32]};
+            aes_words(x);
+            for (int k = 0; k < 4; ++k) rk[u + k] = x[k] ^ rk[u - 4 + k];
+            if (u == 32) inject(32, 0, 1, 2, 3);
+            else if (u == 164) inject(164, 3, 2, 1, 0);
+            else if (u == 316) inject(316, 2, 3, 0, 1);
+            else if (u == 440) inject(440, 1, 0, 3, 2);
+            u += 4;
+        }
+        if (u == 448) break;
+        for (int s = 0; s < 8; ++s, u += 4)  // linear expansion
+            for (int k = 0; k < 4; ++k) rk[u + k] = rk[u - 32 + k] ^ rk[u - 7 + k];
+    }
+    u32 P[4][4];
+    for (int b = 0; b < 4; ++b)
+        for (int k = 0; k < 4; ++k) P[b][k] = h[4 * b + k];
+    int r_idx = 0;
+    auto F = [&](u32 (&L)[4], const u32 (&R)[4]) {
+        u32 x[4];
+        for (int k = 0; k < 4; ++k) x[k] = R[k] ^ rk[r_idx++];
+        aes_words(x);
+        for (int j = 0; j < 3; ++j) {
+            for (int k = 0; k < 4; ++k) x[k] ^= rk[r_idx++];
+            aes_words(x);
+        }
+        for (int k = 0; k < 4; ++k) L[k] ^= x[k];
+    };
+    for (int r = 0; r < 14; ++r) {
+        F(P[0], P[1]);
+        F(P[2], P[3]);
+        u32 t[4];
+        std::memcpy(t, P[3], sizeof t);
+        std::memcpy(P[3], P[2], sizeof t);
+        std::memcpy(P[2], P[1], sizeof t);
+        std::memcpy(P[1], P[0], sizeof t);
+        std::memcpy(P[0], t, sizeof t);
+    }
+    for (int b = 0; b < 4; ++b)
+        for (int k = 0; k < 4; ++k) h[4 * b + k] ^= P[b][k];
+}
+
+}  // namespace
+
+Hash512 shavite512(const u8* data, size_t n) {
+    static const u32 kIV[16] = {0x72FCCDD8, 0x79CA4727, 0x128A077B, 0x40D55AEC, 0xD1901A06, 0x430AE307,
+                                0xB29F5CD1, 0xDF07FBFC, 0x8E45D73D, 0x681AB538, 0xBDE86578, 0xDD577E47,
+                                0xE275EADE, 0x502D9FCD, 0xB9357178, 0x022A4B9A};
+    u32 h[16];
+    std::memcpy(h, kIV, sizeof h);
+    const u64 bits = u64(n) * 8;
+    u64 done = 0;
+    for (; n >= 128; n -= 128, data += 128) {
+        done += 1024;
+        const u32 cnt[4] = {u32(done), u32(done >> 32), 0, 0};
+        shavite_c512(h, data, cnt);
+    }
+    // 0x80, zeros, 128-bit bit count (LE) at 110, digest size 512 (16-bit LE) at 126
+    u8 buf[128] = {0};
+    std::memcpy(buf, data, n);
+    const u32 total[4] = {u32(bits), u32(bits >> 32), 0, 0};
+    const u32 zero[4] = {0, 0, 0, 0};
+    const u32* last_cnt = total;
+    if (n == 0) {
+        buf[0] = 0x80;
+        last_cnt = zero;  // a block with no message bits is compressed with counter 0
+    } else if (n < 110) {
+        buf[n] = 0x80;
+    } else {
+        buf[n] = 0x80;
+        shavite_c512(h, buf, total);
+        std::memset(buf, 0, 110);
+        last_cnt = zero;
+    }
+    for (int i = 0; i < 4; ++i) store_le32(buf + 110 + 4 * i, total[i]);
+    buf[126] = 0x00;
+    buf[127] = 0x02;
+    shavite_c512(h, buf, last_cnt);
+    Hash512 out;
+    for (int i = 0; i < 16; ++i) store_le32(out.bytes + 4 * i, h[i]);
+    return out;
+}
+
+// ================================================================ Fugue-512
+// 36-column state (u32 per column, row 0 in the most significant byte). Each input
+// word: TIX, then four sub-rounds of ROR3 / CMIX / SMIX; SMIX = AES S-box on the
+// 4x4 byte block followed by the Super-Mix matrix, evaluated through the
+// column tables (S, S, 7S, 4S) and their byte rotations. The final stage G runs
+// 32 extra ROR3/CMIX/SMIX rounds then 13 rounds of four ROR9/ROR8 + SMIX steps.
+namespace {
+
+struct FugueTables {
+    u32 mt[4][256];
+    FugueTables() {
+        const u8* S = aes_sbox();
+        for (int x = 0; x < 256; ++x) {
+            const u8 s = S[x];
+            const u32 v = (u32(s) << 24) | (u32(s) << 16) | (u32(gmul(s, 7)) << 8) | u32(gmul(s, 4));
+            for (int k = 0; k < 4; ++k) mt[k][x] = k ? rotr32(v, 8 * k) : v;
+        }
+    }
+};
+
+void fugue_smix(const FugueTables& T, u32& x0, u32& x1, u32& x2, u32& x3) {
+    u32 x[4] = {x0, x1, x2, x3}, c[4] = {0, 0, 0, 0}, r[4] = {0, 0, 0, 0};
+    for (int j = 0; j < 4; ++j)
+        for (int k = 0; k < 4; ++k) {
+            const u32 t = T.mt[k][(x[j] >> (24 - 8 * k)) & 0xFF];
+            c[j] ^= t;
+            if (k != j) r[k] ^= t;
+        }
+    x0 = ((c[0] ^ r[0]) & 0xFF000000u) | ((c[1] ^ r[1]) & 0x00FF0000u) | ((c[2] ^ r[2]) & 0x0000FF00u) |
+         ((c[3] ^ r[3]) & 0x000000FFu);
+    x1 = ((c[1] ^ (r[0] << 8)) & 0xFF000000u) | ((c[2] ^ (r[1] << 8)) & 0x00FF0000u) |
+         ((c[3] ^ (r[2] << 8)) & 0x0000FF00u) | ((c[0] ^ (r[3] >> 24)) & 0x000000FFu);
+    x2 = ((c[2] ^ (r[0] << 16)) & 0xFF000000u) | ((c[3] ^ (r[1] << 16)) & 0x00FF0000u) |
+         ((c[0] ^ (r[2] >> 16)) & 0x0000FF00u) | ((c[1] ^ (r[3] >> 16)) & 0x000000FFu);
+    x3 = ((c[3] ^ (r[0] << 24)) & 0xFF000000u) | ((c[0] ^ (r[1] >> 8)) & 0x00FF0000u) |
+         ((c[1] ^ (r[2] >> 8)) & 0x0000FF00u) | ((c[2] ^ (r[3] >> 8)) & 0x000000FFu);
+}
+
+struct Fugue {
+    u32 S[36];
+    const FugueTables& T;
+    explicit Fugue(const FugueTables& t) : T(t) {}
+    void ror(int n) {
+        u32 t[36];
+        for (int i = 0; i < 36; ++i) t[(i + n) % 36] = S[i];
+        std::memcpy(S, t, sizeof S);
+    }
+    void smix() { fugue_smix(T, S[0], S[1], S[2], S[3]); }
+    void cmix_sub() {
+        ror(3);
+        S[0] ^= S[4]; S[1] ^= S[5]; S[2] ^= S[6];
+        S[18] ^= S[4]; S[19] ^= S[5]; S[20] ^= S[6];
+        smix();
+    }
+    void word(u32 I) {
+        S[22] ^= S[0];
+        S[0] = I;
+        S[8] ^= S[0];
+        S[1] ^= S[24];
+        S[4] ^= S[27];
+        S[7] ^= S[30];
+        for (int k = 0; k < 4; ++k) cmix_sub();
+    }
+};
+
+}  // namespace
+
+Hash512 fugue512(const u8* data, size_t n) {
+    static const FugueTables T;
+    static const u32 kIV[16] = {0x8807a57e, 0xe616af75, 0xc5d3e4db, 0xac9ab027, 0xd915f117, 0xb6eecc54,
+                                0x06e8020b, 0x4a92efd1, 0xaac6e2c9, 0xddb21398, 0xcae65838, 0x437f203f,
+                                0x25ea78e7, 0x951fddd6, 0xda6ed11d, 0xe13e3567};
+    Fugue f(T);
+    std::memset(f.S, 0, sizeof f.S);
+    std::memcpy(f.S + 20, kIV, sizeof kIV);
+    const u64 bits = u64(n) * 8;
+    for (; n >= 4; n -= 4, data += 4) f.word(load_be32(data));
+    if (n) {
+        u8 w[4] = {0};
+        std::memcpy(w, data, n);
+        f.word(load_be32(w));
+    }
+    f.word(u32(bits >> 32));
+    f.word(u32(bits));
+    u32* S = f.S;
+    for (int i = 0; i < 32; ++i) f.cmix_sub();
+    static const int kG[4][4] = {{4, 9, 18, 27}, {4, 10, 18, 27}, {4, 10, 19, 27}, {4, 10, 19, 28}};
+    for (int i = 0; i < 13; ++i)
+        for (int k = 0; k < 4; ++k) {
+            for (int j = 0; j < 4; ++j) S[kG[k][j]] ^= S[0];
+            f.ror(k == 3 ? 8 : 9);
+            f.smix();
+        }
+    for (int j = 0; j < 4; ++j) S[kG[0][j]] ^= S[0];
+    static const int kOut[16] = {1, 2, 3, 4, 9, 10, 11, 12, 18, 19, 20, 21, 27, 28, 29, 30};
+    Hash512 out;
+    for (int i = 0; i < 16; ++i) store_be32(out.bytes + 4 * i, S[kOut[i]]);
+    return out;
+}
 
 }  // namespace nodexa

@@ -210,6 +210,106 @@ Hash512 shabal512(const u8* data, size_t n) {
     return out;
 }
 
-Hash512 bmw512(const u8*, size_t) { throw std::runtime_error("bmw512: not implemented"); }
+// ================================================================ BMW-512 (Blue Midnight Wish)
+// Double-pipe 16 x u64: f0 (bijective transform of M^H into Q[0..15]), f1 (two
+// expansion functions for Q[16..31]), f2 (folding into the new pipe). Final step
+// compresses the last pipe as a message under the constant pipe 0xaa..a0+j.
+namespace {
+
+// f0: W_i = sum of five (M^H)_j with signs; (index, sign) pairs, sign -1 = subtract.
+struct WTerm { int idx[5]; int sgn[5]; };
+const WTerm kBmwW[16] = {
+    {{5, 7, 10, 13, 14}, {1, -1, 1, 1, 1}},  {{6, 8, 11, 14, 15}, {1, -1, 1, 1, -1}},
+    {{0, 7, 9, 12, 15}, {1, 1, 1, -1, 1}},   {{0, 1, 8, 10, 13}, {1, -1, 1, -1, 1}},
+    {{1, 2, 9, 11, 14}, {1, 1, 1, -1, -1}},  {{3, 2, 10, 12, 15}, {1, -1, 1, -1, 1}},
+    {{4, 0, 3, 11, 13}, {1, -1, -1, -1, 1}}, {{1, 4, 5, 12, 14}, {1, -1, -1, -1, -1}},
+    {{2, 5, 6, 13, 15}, {1, -1, -1, 1, -1}}, {{0, 3, 6, 7, 14}, {1, -1, 1, -1, 1}},
+    {{8, 1, 4, 7, 15}, {1, -1, -1, -1, 1}},  {{8, 0, 2, 5, 9}, {1, -1, -1, -1, 1}},
+    {{1, 3, 6, 9, 10}, {1, 1, -1, -1, 1}},   {{2, 4, 7, 10, 11}, {1, 1, 1, 1, 1}},
+    {{3, 5, 8, 11, 12}, {1, -1, 1, -1, -1}}, {{12, 4, 6, 9, 13}, {1, -1, -1, -1, 1}}};
+
+inline u64 bmw_s(int k, u64 x) {
+    switch (k) {
+        case 0: return (x >> 1) ^ (x << 3) ^ rotl64(x, 4) ^ rotl64(x, 37);
+        case 1: return (x >> 1) ^ (x << 2) ^ rotl64(x, 13) ^ rotl64(x, 43);
+        case 2: return (x >> 2) ^ (x << 1) ^ rotl64(x, 19) ^ rotl64(x, 53);
+        case 3: return (x >> 2) ^ (x << 2) ^ rotl64(x, 28) ^ rotl64(x, 59);
+        case 4: return (x >> 1) ^ x;
+        default: return (x >> 2) ^ x;
+    }
+}
+
+void bmw_compress(const u64 M[16], const u64 H[16], u64 out[16]) {
+    u64 Q[32];
+    for (int i = 0; i < 16; ++i) {
+        u64 w = 0;
+        for (int t = 0; t < 5; ++t) {
+            const int j = kBmwW[i].idx[t];
+            const u64 v = M[j] ^ H[j];
+            w = (kBmwW[i].sgn[t] > 0) ? w + v : w - v;
+        }
+        Q[i] = bmw_s(i % 5, w) + H[(i + 1) & 15];
+    }
+    static const int kRot[7] = {5, 11, 27, 32, 37, 43, 53};
+    for (int i = 16; i < 32; ++i) {
+        const int j = i - 16;
+        auto rm = [&](int o) { const int k = (j + o) & 15; return rotl64(M[k], k + 1); };
+        const u64 add = ((rm(0) + rm(3) - rm(10) + u64(i) * 0x0555555555555555ULL) ^ H[(j + 7) & 15]);
+        u64 s = add;
+        if (i < 18) {  // expand1
+            for (int k = 0; k < 16; ++k) s += bmw_s((k + 1) & 3, Q[j + k]);
+        } else {  // expand2
+            for (int k = 0; k < 14; ++k) s += (k & 1) ? rotl64(Q[j + k], kRot[k >> 1]) : Q[j + k];
+            s += bmw_s(4, Q[i - 2]) + bmw_s(5, Q[i - 1]);
+        }
+        Q[i] = s;
+    }
+    u64 xl = 0, xh;
+    for (int i = 16; i < 24; ++i) xl ^= Q[i];
+    xh = xl;
+    for (int i = 24; i < 32; ++i) xh ^= Q[i];
+    // f2: shift amounts per output word (positive = left)
+    static const int kXh[8] = {5, -7, -5, -1, -3, 6, -4, -11};
+    static const int kQ[8] = {-5, 8, 5, 5, 0, -6, 6, 2};
+    static const int kXl[8] = {8, -6, 6, 4, -3, -4, -7, -2};
+    auto sh = [](u64 x, int s) { return s >= 0 ? x << s : x >> -s; };
+    for (int i = 0; i < 8; ++i)
+        out[i] = (sh(xh, kXh[i]) ^ sh(Q[16 + i], kQ[i]) ^ M[i]) + (xl ^ Q[24 + i] ^ Q[i]);
+    for (int i = 8; i < 16; ++i)
+        out[i] = rotl64(out[(i - 4) & 7], i + 1) + (xh ^ Q[16 + i] ^ M[i]) + (sh(xl, kXl[i - 8]) ^ (i == 8 ? Q[23] : Q[i + 7]) ^ Q[i]);
+}
+
+}  // namespace
+
+Hash512 bmw512(const u8* data, size_t n) {
+    u64 H[16], M[16], T[16];
+    for (int i = 0; i < 16; ++i) {
+        u64 v = 0;
+        for (int b = 0; b < 8; ++b) v |= u64(0x80 + 8 * i + b) << (56 - 8 * b);
+        H[i] = v;
+    }
+    const u64 bits = u64(n) * 8;
+    for (; n >= 128; n -= 128, data += 128) {
+        for (int i = 0; i < 16; ++i) M[i] = load_le64(data + 8 * i);
+        bmw_compress(M, H, T);
+        std::memcpy(H, T, sizeof H);
+    }
+    u8 buf[256] = {0};
+    std::memcpy(buf, data, n);
+    buf[n] = 0x80;
+    const size_t len = n + 1 > 120 ? 256 : 128;
+    store_le64(buf + len - 8, bits);
+    for (size_t off = 0; off < len; off += 128) {
+        for (int i = 0; i < 16; ++i) M[i] = load_le64(buf + off + 8 * i);
+        bmw_compress(M, H, T);
+        std::memcpy(H, T, sizeof H);
+    }
+    u64 F[16];
+    for (int i = 0; i < 16; ++i) F[i] = 0xaaaaaaaaaaaaaaa0ULL + u64(i);
+    bmw_compress(H, F, T);
+    Hash512 out;
+    for (int i = 0; i < 8; ++i) store_le64(out.bytes + 8 * i, T[8 + i]);
+    return out;
+}
 
 }  // namespace nodexa

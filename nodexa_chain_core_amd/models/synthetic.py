@@ -63,18 +63,12 @@ class _CpuKawpow:
 
 class _GpuKawpow:
     def __init__(self, device: int = 0, width: int = 2048):
-        from ..ops import verify
+        from ..ops.verify import DagNonceScanner
 
-        self.verify, self.device, self.width = verify, device, width
+        self.scan = DagNonceScanner(device, width)
 
     def __call__(self, height: int, header_hash: bytes, boundary: bytes, start: int):
-        nonces = list(range(start, start + self.width))
-        res = self.verify.gpu_full_hash([height] * self.width, [header_hash] * self.width, nonces,
-                                        device=self.device, mode="dag")
-        for n, (fin, mix) in zip(nonces, res):
-            if _core.hash_le(fin, boundary):
-                return (n, fin, mix), self.width
-        return None, self.width
+        return self.scan(height, header_hash, boundary, start)
 
 
 class _CpuEquihash:

