@@ -55,13 +55,19 @@ void bind_extra(py::module_& m) {
     m.def("x16r", [](const py::bytes& data, const py::bytes& prev) {
         std::string s = data;
         Uint256 p = u256(prev), out;
-        x16r_hash(reinterpret_cast<const u8*>(s.data()), s.size(), p.data, false, out.data);
+        {
+            py::gil_scoped_release nogil;
+            x16r_hash(reinterpret_cast<const u8*>(s.data()), s.size(), p.data, false, out.data);
+        }
         return pyb(out);
     });
     m.def("x16rv2", [](const py::bytes& data, const py::bytes& prev) {
         std::string s = data;
         Uint256 p = u256(prev), out;
-        x16r_hash(reinterpret_cast<const u8*>(s.data()), s.size(), p.data, true, out.data);
+        {
+            py::gil_scoped_release nogil;
+            x16r_hash(reinterpret_cast<const u8*>(s.data()), s.size(), p.data, true, out.data);
+        }
         return pyb(out);
     });
     m.def("x16r_algo", [](int algo, const py::bytes& data) {
@@ -70,6 +76,21 @@ void bind_extra(py::module_& m) {
         return py::bytes(reinterpret_cast<const char*>(h.bytes), 64);
     });
     m.def("x16r_slot_available", &x16r_slot_available);
+    m.def("x16r_search", [](const py::bytes& header80, bool v2, const py::bytes& target, u32 start, u64 count,
+                            int threads) -> py::object {
+        std::string h = header80;
+        if (h.size() != 80) throw std::invalid_argument("x16r_search needs the 80-byte legacy header");
+        Uint256 t = u256(target);
+        X16rSearchResult r;
+        {
+            py::gil_scoped_release nogil;
+            r = x16r_search(reinterpret_cast<const u8*>(h.data()), v2, t.data, start, count, threads);
+        }
+        if (!r.found) return py::make_tuple(py::none(), r.hashes);
+        return py::make_tuple(py::make_tuple(r.nonce, py::bytes(reinterpret_cast<const char*>(r.hash), 32)), r.hashes);
+    }, py::arg("header80"), py::arg("v2"), py::arg("target"), py::arg("start"), py::arg("count"),
+       py::arg("threads") = 0,
+       "lowest nNonce in [start, start+count) with X16R(V2) hash <= target (storage order) -> ((nonce, hash)|None, hashes)");
     m.def("x16r_selection", [](const py::bytes& prev, int i) { return x16r_selection(u256(prev).data, i); });
 
     // ------------------------------------------------ script / addresses

@@ -1,7 +1,10 @@
 #include "x16r.hpp"
 #include "x16r_prims.hpp"
 
+#include <atomic>
 #include <stdexcept>
+#include <thread>
+#include <vector>
 
 namespace nodexa {
 
@@ -187,6 +190,55 @@ void x16r_hash(const u8* data, size_t n, const u8 prev_le[32], bool v2, u8 out[3
         len = 64;
     }
     std::memcpy(out, h.bytes, 32);
+}
+
+X16rSearchResult x16r_search(const u8 header80[80], bool v2, const u8 target_le[32], u32 start, u64 count,
+                             int threads) {
+    // generateBlocks' legacy loop (src/rpc/mining.cpp:141-149: ++nNonce until
+    // CheckProofOfWork) split over host threads in interleaved nonce order; the
+    // lowest qualifying nonce of the window wins, so the result is deterministic.
+    if (threads <= 0) threads = int(std::max(1u, std::thread::hardware_concurrency()));
+    const u8* prev = header80 + 4;
+    std::atomic<u64> best{~u64(0)};
+    std::atomic<u64> done{0};
+    auto le_cmp = [](const u8* a, const u8* b) {  // a <= b as little-endian 256-bit
+        for (int i = 31; i >= 0; --i)
+            if (a[i] != b[i]) return a[i] < b[i];
+        return true;
+    };
+    auto worker = [&](int t) {
+        u8 hdr[80];
+        std::memcpy(hdr, header80, 80);
+        u64 local = 0;
+        for (u64 k = u64(t); k < count; k += u64(threads)) {
+            if (k > best.load(std::memory_order_relaxed)) break;
+            store_le32(hdr + 76, u32(start + k));
+            u8 out[32];
+            x16r_hash(hdr, 80, prev, v2, out);
+            ++local;
+            if (le_cmp(out, target_le)) {
+                u64 cur = best.load();
+                while (k < cur && !best.compare_exchange_weak(cur, k)) {
+                }
+                break;
+            }
+        }
+        done += local;
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t) pool.emplace_back(worker, t);
+    for (auto& th : pool) th.join();
+    X16rSearchResult r;
+    r.hashes = done.load();
+    if (best.load() != ~u64(0)) {
+        r.found = true;
+        r.nonce = u32(start + best.load());
+        u8 hdr[80];
+        std::memcpy(hdr, header80, 80);
+        store_le32(hdr + 76, r.nonce);
+        x16r_hash(hdr, 80, prev, v2, r.hash);
+    }
+    return r;
 }
 
 }  // namespace nodexa

@@ -21,6 +21,18 @@ Hash512 x16r_single(int algo, const u8* data, size_t n);
 bool x16r_slot_available(int algo);
 int x16r_selection(const u8 prev_le[32], int index);
 
+// Legacy-header nonce search (32-bit nNonce at byte 76 of the 80-byte header;
+// hashPrevBlock at bytes 4..35 drives the algorithm order). Lowest nonce in
+// [start, start + count) whose hash <= target (little-endian uint256 storage).
+struct X16rSearchResult {
+    bool found = false;
+    u32 nonce = 0;
+    u64 hashes = 0;
+    u8 hash[32] = {0};
+};
+X16rSearchResult x16r_search(const u8 header80[80], bool v2, const u8 target_le[32], u32 start, u64 count,
+                             int threads);
+
 // Individual primitives: x16r_prims.hpp.
 
 }  // namespace nodexa

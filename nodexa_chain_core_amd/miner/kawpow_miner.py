@@ -135,7 +135,7 @@ class MinerController:
         extranonce.increment(blk, tpl.height)
         hdr = blk.header
         if hdr.time < self.state.params.kawpow_activation_time:
-            raise RuntimeError("template is pre-KawPow: set -kawpowactivationtime (X16R mining is not supported)")
+            return self._mine_legacy(blk, tpl, max_tries, nonce_start, stop)
         header_hash = to_progpow(hdr.kawpow_header_hash())
         boundary = tpl.target.to_bytes(32, "big")
         chunk = 1 << 16
@@ -153,6 +153,30 @@ class MinerController:
             hdr.mix_hash = from_progpow(mix)
             blk.header = hdr
             return blk, tried + (nonce - nonce_start - tried) + 1
+        return None, tried
+
+    def _mine_legacy(self, blk, tpl, max_tries: int, nonce_start: int, stop):
+        """Pre-KawPow template (X16R / X16RV2 by nTime, src/primitives/block.cpp:38-55):
+        the reference's generateBlocks bumps the 32-bit nNonce (src/rpc/mining.cpp:141-149).
+        Native multi-threaded search (csrc/pow/x16r.cpp) in 64k-nonce windows."""
+        hdr = blk.header
+        v2 = hdr.time >= self.state.params.x16rv2_activation_time
+        target = tpl.target.to_bytes(32, "little")
+        tried = 0
+        start = nonce_start & 0xFFFFFFFF
+        while tried < max_tries and not (stop and stop.is_set()):
+            n = min(1 << 16, max_tries - tried, (1 << 32) - start)
+            hdr.nonce = 0
+            res, hashes = _core.x16r_search(hdr.legacy80(), v2, target, start, n)
+            self._account(hashes)
+            if res is not None:
+                hdr.nonce = res[0]
+                blk.header = hdr
+                return blk, tried + (res[0] - start) + 1
+            tried += n
+            start += n
+            if start >= 1 << 32:
+                break
         return None, tried
 
     def generate(self, script_pubkey: bytes, nblocks: int, max_tries: int = 1_000_000) -> list[str]:

@@ -62,7 +62,10 @@ class _CpuKawpow:
 
 
 class _GpuKawpow:
-    def __init__(self, device: int = 0, width: int = 2048):
+    # One scanner launch costs ~5.6 ms at 2048 nonces and is latency-bound (each
+    # 16-lane group hashes its 16 jobs serially), so a 32k window costs about the
+    # same and covers the post-bootstrap DGW difficulty in one call.
+    def __init__(self, device: int = 0, width: int = 32768):
         from ..ops.verify import DagNonceScanner
 
         self.scan = DagNonceScanner(device, width)

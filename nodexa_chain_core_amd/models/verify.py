@@ -40,13 +40,13 @@ def verify_headers(params, headers, gpus: list[int] | None = None, threads: int 
     kernel choice, see ops/verify.py."""
     jobs = [_job(params, h) for h in headers]
     out: list[dict] = [{} for _ in jobs]
-    todo, eq_todo = [], []
+    todo, eq_todo, legacy = [], [], []
     for i, (bn, hh, nonce, mix, boundary) in enumerate(jobs):
         if headers[i].is_equihash():
             eq_todo.append(i)
             continue
         if headers[i].time < params.kawpow_activation_time:
-            out[i] = {"valid": False, "reason": "pre-kawpow header (X16R) not handled by the batch verifier"}
+            legacy.append(i)
             continue
         fin = _core.kawpow_hash_no_verify(bn, hh, mix, nonce)
         if not _core.hash_le(fin, boundary):
@@ -80,7 +80,24 @@ def verify_headers(params, headers, gpus: list[int] | None = None, threads: int 
                 out[i] = _finish(jobs[i], fin, mix)
     if eq_todo:
         _verify_equihash(params, headers, eq_todo, out, gpus, threads)
+    if legacy:
+        _verify_x16r(params, headers, legacy, out, threads)
     return out
+
+
+def _verify_x16r(params, headers, idxs: list[int], out: list[dict], threads: int) -> None:
+    """Pre-KawPow headers: X16R / X16RV2 by nTime (src/primitives/block.cpp:38-55) on the
+    host cores (the native hash releases the GIL), then CheckProofOfWork."""
+    def one(i):
+        h = headers[i]
+        fn = _core.x16rv2 if h.time >= params.x16rv2_activation_time else _core.x16r
+        return fn(h.legacy80(), h.prev)
+
+    with cf.ThreadPoolExecutor(max_workers=threads or (os.cpu_count() or 4)) as ex:
+        for i, hsh in zip(idxs, ex.map(one, idxs)):
+            ok = _core.check_proof_of_work(hsh, headers[i].bits, params)
+            out[i] = {"valid": bool(ok), "hash": _core.u256_hex(hsh)} if ok else \
+                {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(hsh)}
 
 
 def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, threads: int) -> None:

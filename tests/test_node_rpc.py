@@ -164,3 +164,35 @@ def test_cli_main(node_factory, capsys, tmp_path):
     rc = main(["-regtest", f"-datadir={tmp_path}", f"-rpcport={node.rpc.port}", "-rpcuser=u", "-rpcpassword=p",
                "getblockcount"])
     assert rc == 0 and capsys.readouterr().out.strip() == "0"
+
+
+def test_generate_x16rv2_reference_default(core, node_factory):
+    """BASELINE config 1 with the reference's own regtest params: KawPow activation in
+    2083 (src/chainparams.cpp:566-570), so `generate` hashes 80-byte X16RV2 headers and
+    bumps the 32-bit nNonce (src/rpc/mining.cpp:117-173)."""
+    node, addr = node_factory(["-kawpowactivationtime=3582830167"])
+    c = client(node)
+    hashes = c.generatetoaddress(2, addr)
+    assert c.getblockcount() == 2
+    p = node.params
+    raw = bytes.fromhex(c.getblock(hashes[1], 0))
+    b = core.Block.deserialize(raw, p.kawpow_activation_time)
+    h = b.header
+    assert h.time < p.kawpow_activation_time and h.time >= p.x16rv2_activation_time
+    assert len(h.legacy80()) == 80
+    got = core.x16rv2(h.legacy80(), h.prev)
+    assert core.u256_hex(got) == hashes[1]
+    target, _, _ = core.set_compact(h.bits)
+    assert int.from_bytes(got, "little") <= target
+    # batch verifier handles legacy headers too (CPU X16RV2), and rejects a bumped nonce
+    from nodexa_chain_core_amd.models.verify import verify_headers
+
+    hdrs = [core.Block.deserialize(bytes.fromhex(c.getblock(x, 0)), p.kawpow_activation_time).header for x in hashes]
+    res = verify_headers(p, hdrs)
+    assert all(r["valid"] for r in res) and [r["hash"] for r in res] == hashes
+    bad = hdrs[0]
+    for k in range(1, 64):  # find a nonce that misses the regtest target (~1/2 of nonces do)
+        bad.nonce = (bad.nonce + 1) & 0xFFFFFFFF
+        if not verify_headers(p, [bad])[0]["valid"]:
+            break
+    assert verify_headers(p, [bad])[0]["reason"] == "high-hash"
