@@ -68,6 +68,10 @@ PYBIND11_MODULE(_core, m) {
             return py::bytes(reinterpret_cast<const char*>(c.light.data()), c.light.size() * 64);
         }, "raw light cache (light_items x 64 bytes)")
         .def("light_cache_ptr", [](const EpochContext& c) { return reinterpret_cast<uintptr_t>(c.light.data()); });
+    m.def("set_light_cache_dir", &set_light_cache_dir, "-dagcache: on-disk light-cache cache directory ('' = off)");
+    m.def("light_cache_dir", &light_cache_dir);
+    m.def("create_epoch_context", [](int e) { return std::const_pointer_cast<EpochContext>(create_epoch_context(e)); },
+          py::call_guard<py::gil_scoped_release>(), "uncached build (tests); honours the on-disk cache");
     m.def("get_epoch_context", [](int e) { return std::const_pointer_cast<EpochContext>(get_epoch_context(e)); },
           py::call_guard<py::gil_scoped_release>());
     m.def("dataset_item_512", [](const EpochContext& c, u64 i) { return from_h512(dataset_item_512(c, i)); });

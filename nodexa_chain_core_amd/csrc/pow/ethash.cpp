@@ -1,7 +1,11 @@
 #include "ethash.hpp"
 
+#include <cstdio>
 #include <list>
+#include <mutex>
+#include <string>
 #include <thread>
+#include <unistd.h>
 
 namespace nodexa {
 
@@ -102,6 +106,66 @@ void dataset_item_2048(const EpochContext& ctx, u32 index, Hash512 out[4]) {
     out[3] = d.final();
 }
 
+// ---------------------------------------------------------------- on-disk light-cache cache
+// `-dagcache=<dir>` (SURVEY §5 checkpoint/resume): the serial light-cache build
+// (2.3 s at epoch 384) is skipped on restart. File = 8-byte magic, the epoch
+// seed, the item count, the payload and keccak256(payload); written to a temp
+// file and renamed, so a crash never leaves a torn cache that would be trusted.
+namespace {
+std::mutex g_cache_mu;
+std::string g_cache_dir;
+constexpr char kCacheMagic[8] = {'N', 'X', 'L', 'I', 'G', 'H', 'T', '1'};
+
+std::string cache_path(const EpochContext& ctx, const Hash256& seed) {
+    return g_cache_dir + "/light-" + std::to_string(ctx.epoch) + "-" + hex_encode(seed.bytes, 8) + ".bin";
+}
+}  // namespace
+
+void set_light_cache_dir(const std::string& dir) {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    g_cache_dir = dir;
+}
+
+std::string light_cache_dir() {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    return g_cache_dir;
+}
+
+bool load_cached_light(EpochContext& ctx, const Hash256& seed) {
+    const std::string dir = light_cache_dir();
+    if (dir.empty()) return false;
+    FILE* f = std::fopen(cache_path(ctx, seed).c_str(), "rb");
+    if (!f) return false;
+    char magic[8];
+    Hash256 fseed, sum;
+    u32 items = 0;
+    const size_t payload = ctx.light.size() * sizeof(Hash512);
+    bool ok = std::fread(magic, 8, 1, f) == 1 && std::memcmp(magic, kCacheMagic, 8) == 0 &&
+              std::fread(fseed.bytes, 32, 1, f) == 1 && std::memcmp(fseed.bytes, seed.bytes, 32) == 0 &&
+              std::fread(&items, 4, 1, f) == 1 && int(items) == ctx.light_items &&
+              std::fread(ctx.light.data(), payload, 1, f) == 1 && std::fread(sum.bytes, 32, 1, f) == 1;
+    std::fclose(f);
+    if (ok) ok = keccak256(reinterpret_cast<const u8*>(ctx.light.data()), payload) == sum;
+    return ok;
+}
+
+void store_cached_light(const EpochContext& ctx, const Hash256& seed) {
+    const std::string dir = light_cache_dir();
+    if (dir.empty()) return;
+    const std::string path = cache_path(ctx, seed);
+    const std::string tmp = path + ".tmp" + std::to_string(::getpid());
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const size_t payload = ctx.light.size() * sizeof(Hash512);
+    const u32 items = u32(ctx.light_items);
+    const Hash256 sum = keccak256(reinterpret_cast<const u8*>(ctx.light.data()), payload);
+    bool ok = std::fwrite(kCacheMagic, 8, 1, f) == 1 && std::fwrite(seed.bytes, 32, 1, f) == 1 &&
+              std::fwrite(&items, 4, 1, f) == 1 && std::fwrite(ctx.light.data(), payload, 1, f) == 1 &&
+              std::fwrite(sum.bytes, 32, 1, f) == 1;
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+}
+
 std::shared_ptr<const EpochContext> create_epoch_context(int epoch) {
     if (epoch < 0 || epoch > 30000) throw std::invalid_argument("epoch out of range");
     auto ctx = std::make_shared<EpochContext>();
@@ -109,7 +173,11 @@ std::shared_ptr<const EpochContext> create_epoch_context(int epoch) {
     ctx->light_items = light_cache_num_items(epoch);
     ctx->full_items = full_dataset_num_items(epoch);
     ctx->light.resize(size_t(ctx->light_items));
-    build_light_cache(ctx->light.data(), ctx->light_items, epoch_seed(epoch));
+    const Hash256 seed = epoch_seed(epoch);
+    if (!load_cached_light(*ctx, seed)) {
+        build_light_cache(ctx->light.data(), ctx->light_items, seed);
+        store_cached_light(*ctx, seed);
+    }
     // L1 = first 16 KiB of the dataset = 2048-bit items 0..63.
     Hash512 item[4];
     for (u32 i = 0; i < kL1CacheWords / 64; ++i) {

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <memory>
 #include <mutex>
+#include <string>
 
 #include "../crypto/keccak.hpp"
 
@@ -54,6 +55,11 @@ struct EpochContext {
 
 void build_light_cache(Hash512* cache, int num_items, const Hash256& seed);
 std::shared_ptr<const EpochContext> create_epoch_context(int epoch);
+// Optional on-disk cache of light caches (empty dir = off). Loads verify a keccak256 checksum.
+void set_light_cache_dir(const std::string& dir);
+std::string light_cache_dir();
+bool load_cached_light(EpochContext& ctx, const Hash256& seed);
+void store_cached_light(const EpochContext& ctx, const Hash256& seed);
 // Process-wide cache of recently used contexts (thread-safe, LRU of 4).
 std::shared_ptr<const EpochContext> get_epoch_context(int epoch);
 

@@ -26,10 +26,10 @@ import time
 from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
-from .miner.kawpow_miner import CpuKawpowBackend, GpuKawpowBackend, MinerController
+from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, GpuKawpowBackend, MinerController
 from .rpc import methods
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
-from .utils import log
+from .utils import log, metrics
 from .utils.config import ArgsManager, gpu_list
 
 _core = core()
@@ -84,13 +84,31 @@ class Node:
         methods.register(self.table, self)
         if a.get_bool("server", True):
             self._start_rpc()
+        dagcache = a.get("dagcache")
+        if dagcache:  # on-disk light caches keyed by epoch seed (SURVEY §5 checkpoint/resume)
+            if dagcache == "1":
+                dagcache = os.path.join(self.datadir or ".", "dagcache")
+            os.makedirs(dagcache, exist_ok=True)
+            _core.set_light_cache_dir(dagcache)
         self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False))
         backends = []
         for d in self.gpus:
             backends.append(GpuKawpowBackend(d, a.get_int("gpuintensity", 1 << 22)))
         if not backends:
             backends.append(CpuKawpowBackend(a.get_int("genproclimit", 1)))
-        self.miner = MinerController(self.state, backends)
+        fail, drop = float(a.get("gpufailrate", "0") or 0), float(a.get("dropshare", "0") or 0)
+        if fail or drop:  # fault injection for failure-handling tests (never on by default)
+            backends = [FaultInjector(b, fail, drop, seed=i) for i, b in enumerate(backends)]
+        self.miner = MinerController(
+            self.state, backends, max_failures=a.get_int("minermaxfailures", 3),
+            watchdog_s=float(a.get("minerwatchdog", "120")),
+            state_path=os.path.join(self.datadir, "miner_state.json") if self.datadir else None)
+        self.metrics_writer = None
+        if a.get("metricslog"):
+            path = a.get("metricslog")
+            if not os.path.isabs(path) and self.datadir:
+                path = os.path.join(self.datadir, path)
+            self.metrics_writer = metrics.JsonlWriter(path, float(a.get("metricsinterval", "10"))).start()
         self.table.warmup = None
         log.log_printf(f"nodexad started: network={self.network} height={self.state.height()} "
                        f"kawpow_activation={self.params.kawpow_activation_time} gpus={self.gpus or 'none'}")
@@ -127,6 +145,8 @@ class Node:
         self._stopped = True
         if self.miner is not None:
             self.miner.stop()
+        if getattr(self, "metrics_writer", None) is not None:
+            self.metrics_writer.stop()
         if self.rpc is not None:
             self.rpc.stop()
         if self.datadir is not None:
@@ -218,6 +238,8 @@ class Node:
         import json
 
         parts = path.split("?")[0].split("/")[2:]
+        if parts == ["metrics"]:  # Prometheus text exposition of utils/metrics.REGISTRY
+            return 200, "text/plain; version=0.0.4", metrics.REGISTRY.prometheus().encode()
         if parts == ["chaininfo.json"]:
             tip = self.state.tip()
             body = json.dumps({"chain": self.network, "blocks": tip.height, "bestblockhash": _core.u256_hex(tip.hash)})

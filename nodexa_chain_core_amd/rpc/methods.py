@@ -278,7 +278,8 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         return {"blocks": tip.height, "currentblockweight": node.last_block_weight, "currentblocktx": node.last_block_tx,
                 "difficulty": _core.difficulty_from_bits(tip.bits), "networkhashps": st.network_hashps(120, -1),
                 "hashespersec": int(node.miner.hashrate), "pooledtx": len(st.mempool), "chain": params.network_id,
-                "warnings": "", "gpus": node.gpu_info()}
+                "warnings": "", "gpus": node.gpu_info(),
+                "workers": [h.as_dict() for h in node.miner.health]}
 
     def rpc_getnetworkhashps(p):
         """getnetworkhashps ( nblocks height )"""

@@ -93,3 +93,24 @@ def test_ethash_classic_roundtrip(core, ctx0):
     f, m = core.ethash_hash(ctx0, bytes(32), 7)
     assert core.ethash_verify(ctx0, bytes(32), m, 7, f)
     assert not core.ethash_verify(ctx0, bytes(32), bytes(32), 7, f)
+
+
+def test_light_cache_disk_cache(core, tmp_path):
+    """-dagcache: a light cache written to disk reloads bit-identically; a corrupted file
+    is detected by its checksum and rebuilt (SURVEY §5 checkpoint/resume)."""
+    import glob
+
+    core.set_light_cache_dir(str(tmp_path))
+    try:
+        a = core.create_epoch_context(1)
+        files = glob.glob(str(tmp_path / "light-1-*.bin"))
+        assert len(files) == 1
+        b = core.create_epoch_context(1)  # loaded from disk
+        assert a.light_cache() == b.light_cache() and a.l1 == b.l1
+        with open(files[0], "r+b") as f:
+            f.seek(100)
+            f.write(b"\xff\xff")
+        c = core.create_epoch_context(1)  # checksum mismatch -> rebuilt
+        assert c.light_cache() == a.light_cache()
+    finally:
+        core.set_light_cache_dir("")
