@@ -15,7 +15,7 @@ valid in our kernels. Device code is never linked into the host .so; every
 kernel is a code object loaded with hipModuleLoadData, which also serves the
 per-period KawPow kernels that are generated at run time (see ops/jit.py).
 
-Usage: python -m nodexa_chain_core_amd._build [--force] [--jobs N] [core|hip|kernels|bin]
+Usage: python -m nodexa_chain_core_amd._build [--force] [--jobs N] [core|bench|hip|kernels]
 """
 from __future__ import annotations
 
@@ -92,7 +92,7 @@ def _compile_all(srcs: list[str], flags: list[str], objdir: str, jobs: int, forc
 
 def core_sources() -> list[str]:
     srcs = glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)
-    return sorted(s for s in srcs if os.sep + "daemon" + os.sep not in s)
+    return sorted(s for s in srcs if os.sep + "daemon" + os.sep not in s and os.sep + "bench" + os.sep not in s)
 
 
 def build_core(force: bool = False, jobs: int = 8) -> str:
@@ -100,6 +100,22 @@ def build_core(force: bool = False, jobs: int = 8) -> str:
     objs = _compile_all(core_sources(), CXXFLAGS + _pybind_includes(), os.path.join(BUILD, "core"), jobs, force)
     if force or _newer(out, objs):
         _run(["g++", "-shared", "-o", out, *objs, "-pthread"])
+    return out
+
+
+def build_bench(force: bool = False, jobs: int = 8) -> str:
+    """bin/bench_nodexa: the host micro-benchmarks (csrc/bench) linked with the core objects
+    (everything but the pybind11 bindings)."""
+    out_dir = os.path.join(PKG, "bin")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "bench_nodexa")
+    core_objs = _compile_all(core_sources(), CXXFLAGS + _pybind_includes(), os.path.join(BUILD, "core"), jobs, force)
+    core_objs = [o for o in core_objs if "_bind_" not in os.path.basename(o)]
+    bench_srcs = sorted(glob.glob(os.path.join(CSRC, "bench", "*.cpp")))
+    bench_objs = _compile_all(bench_srcs, CXXFLAGS, os.path.join(BUILD, "bench"), jobs, force)
+    objs = core_objs + bench_objs
+    if force or _newer(out, objs):
+        _run(["g++", "-o", out, *objs, "-pthread"])
     return out
 
 
@@ -150,6 +166,7 @@ def build_kernels(force: bool = False, jobs: int = 8) -> list[str]:
 
 def build_all(force: bool = False, jobs: int = 8, with_hip: bool = True) -> None:
     build_core(force, jobs)
+    build_bench(force, jobs)
     if with_hip:
         build_hip_runtime(force, jobs)
         build_kernels(force, jobs)
@@ -164,6 +181,8 @@ def main() -> None:
     for w in a.what:
         if w in ("all", "core"):
             print(build_core(a.force, a.jobs))
+        if w in ("all", "bench"):
+            print(build_bench(a.force, a.jobs))
         if w in ("all", "hip"):
             print(build_hip_runtime(a.force, a.jobs))
         if w in ("all", "kernels"):

@@ -6,7 +6,9 @@
 #include "../chain/script.hpp"
 #include "../chain/validation.hpp"
 #include "../pow/equihash.hpp"
+#include "../crypto/hashes.hpp"
 #include "../pow/x16r.hpp"
+#include "../pow/x16r_prims.hpp"
 
 namespace py = pybind11;
 using namespace nodexa;
@@ -50,6 +52,43 @@ void bind_extra(py::module_& m) {
           py::arg("value"), py::arg("negative") = false);
     m.def("arith_div", [](const py::int_& a, const py::int_& b) { return arith_to_int(int_to_arith(a) / int_to_arith(b)); });
     m.def("arith_mul", [](const py::int_& a, const py::int_& b) { return arith_to_int(int_to_arith(a) * int_to_arith(b)); });
+
+    // ------------------------------------------------ auxiliary hashes (P20)
+    m.def("sha1", [](const py::bytes& d) {
+        std::string s = d;
+        u8 o[20];
+        sha1(reinterpret_cast<const u8*>(s.data()), s.size(), o);
+        return py::bytes(reinterpret_cast<const char*>(o), 20);
+    });
+    m.def("hmac_sha256", [](const py::bytes& k, const py::bytes& d) {
+        std::string ks = k, s = d;
+        u8 o[32];
+        hmac_sha256(reinterpret_cast<const u8*>(ks.data()), ks.size(), reinterpret_cast<const u8*>(s.data()), s.size(), o);
+        return py::bytes(reinterpret_cast<const char*>(o), 32);
+    });
+    m.def("hmac_sha512", [](const py::bytes& k, const py::bytes& d) {
+        std::string ks = k, s = d;
+        u8 o[64];
+        hmac_sha512(reinterpret_cast<const u8*>(ks.data()), ks.size(), reinterpret_cast<const u8*>(s.data()), s.size(), o);
+        return py::bytes(reinterpret_cast<const char*>(o), 64);
+    });
+    m.def("siphash24", [](u64 k0, u64 k1, const py::bytes& d) {
+        std::string s = d;
+        return siphash24(k0, k1, reinterpret_cast<const u8*>(s.data()), s.size());
+    });
+    m.def("siphash_uint256", [](u64 k0, u64 k1, const py::bytes& v) { return siphash_uint256(k0, k1, u256(v).data); });
+    m.def("siphash_uint256_extra", [](u64 k0, u64 k1, const py::bytes& v, u32 e) {
+        return siphash_uint256_extra(k0, k1, u256(v).data, e);
+    });
+    m.def("murmur3_32", [](u32 seed, const py::bytes& d) {
+        std::string s = d;
+        return murmur3_32(seed, reinterpret_cast<const u8*>(s.data()), s.size());
+    });
+    m.def("sha512", [](const py::bytes& d) {
+        std::string s = d;
+        Hash512 h = sha512_hash(reinterpret_cast<const u8*>(s.data()), s.size());
+        return py::bytes(reinterpret_cast<const char*>(h.bytes), 64);
+    });
 
     // ------------------------------------------------ X16R
     m.def("x16r", [](const py::bytes& data, const py::bytes& prev) {

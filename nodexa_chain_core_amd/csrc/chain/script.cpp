@@ -1,5 +1,7 @@
 #include "script.hpp"
 
+#include <utility>
+
 #include "../crypto/sha256.hpp"
 
 namespace nodexa {
@@ -149,7 +151,7 @@ std::string script_to_address(const Bytes& s, u8 pkh, u8 sh) {
 
 // ---------------- RIPEMD-160 (Dobbertin, Bosselaers, Preneel 1996) ----------------
 namespace {
-inline u32 rf(int j, u32 x, u32 y, u32 z) {
+constexpr inline u32 rf(int j, u32 x, u32 y, u32 z) {
     switch (j / 16) {
         case 0: return x ^ y ^ z;
         case 1: return (x & y) | (~x & z);
@@ -158,39 +160,49 @@ inline u32 rf(int j, u32 x, u32 y, u32 z) {
         default: return x ^ (y | ~z);
     }
 }
-const u32 KL[5] = {0x00000000, 0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xA953FD4E};
-const u32 KR[5] = {0x50A28BE6, 0x5C4DD124, 0x6D703EF3, 0x7A6D76E9, 0x00000000};
-const int RL[80] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 7, 4, 13, 1, 10, 6, 15, 3, 12, 0, 9,
+constexpr u32 KL[5] = {0x00000000, 0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xA953FD4E};
+constexpr u32 KR[5] = {0x50A28BE6, 0x5C4DD124, 0x6D703EF3, 0x7A6D76E9, 0x00000000};
+constexpr int RL[80] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 7, 4, 13, 1, 10, 6, 15, 3, 12, 0, 9,
                     5, 2, 14, 11, 8, 3, 10, 14, 4, 9, 15, 8, 1, 2, 7, 0, 6, 13, 11, 5, 12, 1, 9, 11, 10, 0, 8,
                     12, 4, 13, 3, 7, 15, 14, 5, 6, 2, 4, 0, 5, 9, 7, 12, 2, 10, 14, 1, 3, 8, 11, 6, 15, 13};
-const int RR[80] = {5, 14, 7, 0, 9, 2, 11, 4, 13, 6, 15, 8, 1, 10, 3, 12, 6, 11, 3, 7, 0, 13, 5, 10, 14, 15, 8,
+constexpr int RR[80] = {5, 14, 7, 0, 9, 2, 11, 4, 13, 6, 15, 8, 1, 10, 3, 12, 6, 11, 3, 7, 0, 13, 5, 10, 14, 15, 8,
                     12, 4, 9, 1, 2, 15, 5, 1, 3, 7, 14, 6, 9, 11, 8, 12, 2, 10, 0, 4, 13, 8, 6, 4, 1, 3, 11,
                     15, 0, 5, 12, 2, 13, 9, 7, 10, 14, 12, 15, 10, 4, 1, 5, 8, 7, 6, 2, 13, 14, 0, 3, 9, 11};
-const int SL[80] = {11, 14, 15, 12, 5, 8, 7, 9, 11, 13, 14, 15, 6, 7, 9, 8, 7, 6, 8, 13, 11, 9, 7, 15, 7, 12, 15,
+constexpr int SL[80] = {11, 14, 15, 12, 5, 8, 7, 9, 11, 13, 14, 15, 6, 7, 9, 8, 7, 6, 8, 13, 11, 9, 7, 15, 7, 12, 15,
                     9, 11, 7, 13, 12, 11, 13, 6, 7, 14, 9, 13, 15, 14, 8, 13, 6, 5, 12, 7, 5, 11, 12, 14, 15,
                     14, 15, 9, 8, 9, 14, 5, 6, 8, 6, 5, 12, 9, 15, 5, 11, 6, 8, 13, 12, 5, 12, 13, 14, 11, 8,
                     5, 6};
-const int SR[80] = {8, 9, 9, 11, 13, 15, 15, 5, 7, 7, 8, 11, 14, 14, 12, 6, 9, 13, 15, 7, 12, 8, 9, 11, 7, 7, 12,
+constexpr int SR[80] = {8, 9, 9, 11, 13, 15, 15, 5, 7, 7, 8, 11, 14, 14, 12, 6, 9, 13, 15, 7, 12, 8, 9, 11, 7, 7, 12,
                     7, 6, 15, 13, 11, 9, 7, 15, 11, 8, 6, 6, 14, 12, 13, 5, 14, 13, 13, 7, 5, 15, 5, 8, 11, 14,
                     14, 6, 14, 6, 9, 12, 9, 12, 5, 15, 8, 8, 5, 12, 9, 12, 5, 14, 6, 8, 13, 6, 5, 15, 13, 11,
                     11};
 
+// Both lines fully unrolled at compile time (the step index J is a template argument,
+// so the boolean function, message word and rotation fold to constants).
+template <int J>
+inline void rmd_step(u32 (&l)[5], u32 (&r)[5], const u32 (&X)[16]) {
+    u32 t = rotl32(l[0] + rf(J, l[1], l[2], l[3]) + X[RL[J]] + KL[J / 16], SL[J]) + l[4];
+    l[0] = l[4]; l[4] = l[3]; l[3] = rotl32(l[2], 10); l[2] = l[1]; l[1] = t;
+    t = rotl32(r[0] + rf(79 - J, r[1], r[2], r[3]) + X[RR[J]] + KR[J / 16], SR[J]) + r[4];
+    r[0] = r[4]; r[4] = r[3]; r[3] = rotl32(r[2], 10); r[2] = r[1]; r[1] = t;
+}
+
+template <int... J>
+inline void rmd_steps(std::integer_sequence<int, J...>, u32 (&l)[5], u32 (&r)[5], const u32 (&X)[16]) {
+    (rmd_step<J>(l, r, X), ...);
+}
+
 void rmd_compress(u32 h[5], const u8* block) {
     u32 X[16];
     for (int i = 0; i < 16; ++i) X[i] = load_le32(block + 4 * i);
-    u32 al = h[0], bl = h[1], cl = h[2], dl = h[3], el = h[4];
-    u32 ar = al, br = bl, cr = cl, dr = dl, er = el;
-    for (int j = 0; j < 80; ++j) {
-        u32 t = rotl32(al + rf(j, bl, cl, dl) + X[RL[j]] + KL[j / 16], SL[j]) + el;
-        al = el; el = dl; dl = rotl32(cl, 10); cl = bl; bl = t;
-        t = rotl32(ar + rf(79 - j, br, cr, dr) + X[RR[j]] + KR[j / 16], SR[j]) + er;
-        ar = er; er = dr; dr = rotl32(cr, 10); cr = br; br = t;
-    }
-    const u32 t = h[1] + cl + dr;
-    h[1] = h[2] + dl + er;
-    h[2] = h[3] + el + ar;
-    h[3] = h[4] + al + br;
-    h[4] = h[0] + bl + cr;
+    u32 l[5] = {h[0], h[1], h[2], h[3], h[4]};
+    u32 r[5] = {h[0], h[1], h[2], h[3], h[4]};
+    rmd_steps(std::make_integer_sequence<int, 80>{}, l, r, X);
+    const u32 t = h[1] + l[2] + r[3];
+    h[1] = h[2] + l[3] + r[4];
+    h[2] = h[3] + l[4] + r[0];
+    h[3] = h[4] + l[0] + r[1];
+    h[4] = h[0] + l[1] + r[2];
     h[0] = t;
 }
 }  // namespace

@@ -1,5 +1,7 @@
 #include "sha256.hpp"
 
+#include <immintrin.h>
+
 namespace nodexa {
 
 namespace {
@@ -15,6 +17,53 @@ constexpr u32 K[64] = {
 constexpr u32 H0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                        0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
 }  // namespace
+
+// x86 SHA extensions path (runtime-dispatched; the reference picks its SSE4 transform
+// the same way, src/crypto/sha256.cpp:187-189).
+__attribute__((target("sha,sse4.1"))) static void compress_shani(u32 st[8], const u8* data, size_t blocks) {
+    const __m128i mask = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    __m128i tmp = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(st)), 0xB1);
+    __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(st + 4)), 0x1B);
+    __m128i s0 = _mm_alignr_epi8(tmp, s1, 8);  // ABEF
+    s1 = _mm_blend_epi16(s1, tmp, 0xF0);      // CDGH
+    for (; blocks; --blocks, data += 64) {
+        const __m128i abef = s0, cdgh = s1;
+        __m128i m[4];
+        for (int g = 0; g < 16; ++g) {
+            if (g < 4) {
+                m[g] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(data + 16 * g)), mask);
+            } else {  // W[4g..4g+3] from groups g-4 .. g-1 held in m[g&3], m[(g+1)&3], m[(g+2)&3], m[(g+3)&3]
+                const __m128i t = _mm_add_epi32(_mm_sha256msg1_epu32(m[g & 3], m[(g + 1) & 3]),
+                                                _mm_alignr_epi8(m[(g + 3) & 3], m[(g + 2) & 3], 4));
+                m[g & 3] = _mm_sha256msg2_epu32(t, m[(g + 3) & 3]);
+            }
+            const __m128i wk = _mm_add_epi32(m[g & 3], _mm_loadu_si128(reinterpret_cast<const __m128i*>(K + 4 * g)));
+            s1 = _mm_sha256rnds2_epu32(s1, s0, wk);
+            s0 = _mm_sha256rnds2_epu32(s0, s1, _mm_shuffle_epi32(wk, 0x0E));
+        }
+        s0 = _mm_add_epi32(s0, abef);
+        s1 = _mm_add_epi32(s1, cdgh);
+    }
+    tmp = _mm_shuffle_epi32(s0, 0x1B);     // FEBA
+    s1 = _mm_shuffle_epi32(s1, 0xB1);      // DCHG
+    s0 = _mm_blend_epi16(tmp, s1, 0xF0);   // DCBA
+    s1 = _mm_alignr_epi8(s1, tmp, 8);      // HGFE
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(st), s0);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(st + 4), s1);
+}
+
+static bool have_shani() {
+    static const bool ok = __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1");
+    return ok;
+}
+
+void Sha256::compress_blocks(u32 s[8], const u8* data, size_t blocks) {
+    if (have_shani()) {
+        compress_shani(s, data, blocks);
+        return;
+    }
+    for (; blocks; --blocks, data += 64) compress(s, data);
+}
 
 void Sha256::compress(u32 s[8], const u8 block[64]) {
     u32 w[64];
@@ -52,12 +101,12 @@ Sha256& Sha256::write(const u8* data, size_t n) {
         data += take;
         n -= take;
         if (fill + take < 64) return *this;
-        compress(s_, buf_);
+        compress_blocks(s_, buf_, 1);
     }
-    while (n >= 64) {
-        compress(s_, data);
-        data += 64;
-        n -= 64;
+    if (n >= 64) {
+        compress_blocks(s_, data, n / 64);
+        data += n / 64 * 64;
+        n %= 64;
     }
     std::memcpy(buf_, data, n);
     return *this;

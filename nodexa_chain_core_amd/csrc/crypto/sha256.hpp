@@ -16,7 +16,8 @@ public:
     Sha256& write(const u8* data, size_t n);
     void finalize(u8 out[32]);
 
-    static void compress(u32 state[8], const u8 block[64]);
+    static void compress(u32 state[8], const u8 block[64]);                   // portable
+    static void compress_blocks(u32 state[8], const u8* data, size_t blocks);  // SHA-NI when present
 
 private:
     u32 s_[8];

@@ -4,6 +4,7 @@
 #include <atomic>
 #include <stdexcept>
 #include <thread>
+#include <utility>
 #include <vector>
 
 namespace nodexa {
@@ -83,7 +84,7 @@ Hash512 blake512(const u8* data, size_t n) {
 
 // ------------------------------------------------------------------ SHA-512 (FIPS 180-4)
 namespace {
-const u64 kSha512K[80] = {
+constexpr u64 kSha512K[80] = {
     0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL, 0x3956c25bf348b538ULL,
     0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL, 0xd807aa98a3030242ULL, 0x12835b0145706fbeULL,
     0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL, 0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL,
@@ -101,23 +102,33 @@ const u64 kSha512K[80] = {
     0x113f9804bef90daeULL, 0x1b710b35131c471bULL, 0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL,
     0x431d67c49c100d4cULL, 0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
+// Rounds unrolled at compile time over a rolling 16-word schedule.
+template <int I>
+inline void sha512_round(u64 (&v)[8], u64 (&w)[16]) {
+    if constexpr (I >= 16) {
+        const u64 a = w[(I - 15) & 15], b = w[(I - 2) & 15];
+        w[I & 15] += (rotr64(a, 1) ^ rotr64(a, 8) ^ (a >> 7)) + w[(I - 7) & 15] +
+                     (rotr64(b, 19) ^ rotr64(b, 61) ^ (b >> 6));
+    }
+    u64 &A = v[(80 - I) & 7], &B = v[(81 - I) & 7], &C = v[(82 - I) & 7], &D = v[(83 - I) & 7];
+    u64 &E = v[(84 - I) & 7], &F = v[(85 - I) & 7], &G = v[(86 - I) & 7], &H = v[(87 - I) & 7];
+    const u64 t1 = H + (rotr64(E, 14) ^ rotr64(E, 18) ^ rotr64(E, 41)) + ((E & F) ^ (~E & G)) + kSha512K[I] + w[I & 15];
+    const u64 t2 = (rotr64(A, 28) ^ rotr64(A, 34) ^ rotr64(A, 39)) + ((A & B) ^ (A & C) ^ (B & C));
+    D += t1;
+    H = t1 + t2;
+}
+
+template <int... I>
+inline void sha512_rounds(std::integer_sequence<int, I...>, u64 (&v)[8], u64 (&w)[16]) {
+    (sha512_round<I>(v, w), ...);
+}
+
 void sha512_compress(u64 s[8], const u8* block) {
-    u64 w[80];
+    u64 w[16], v[8];
     for (int i = 0; i < 16; ++i) w[i] = load_be64(block + 8 * i);
-    for (int i = 16; i < 80; ++i) {
-        const u64 s0 = rotr64(w[i - 15], 1) ^ rotr64(w[i - 15], 8) ^ (w[i - 15] >> 7);
-        const u64 s1 = rotr64(w[i - 2], 19) ^ rotr64(w[i - 2], 61) ^ (w[i - 2] >> 6);
-        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
-    }
-    u64 a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
-    for (int i = 0; i < 80; ++i) {
-        const u64 S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-        const u64 t1 = h + S1 + ((e & f) ^ (~e & g)) + kSha512K[i] + w[i];
-        const u64 S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-        const u64 t2 = S0 + ((a & b) ^ (a & c) ^ (b & c));
-        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
-    }
-    s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+    for (int i = 0; i < 8; ++i) v[i] = s[i];
+    sha512_rounds(std::make_integer_sequence<int, 80>{}, v, w);
+    for (int i = 0; i < 8; ++i) s[i] += v[i];
 }
 }  // namespace
 

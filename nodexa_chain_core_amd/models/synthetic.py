@@ -8,7 +8,9 @@ there is no chain data in this environment, so this module mines one:
   * optionally an Equihash(200,9) era after `n_kawpow` headers (the new header
     extension, csrc/chain/primitives.hpp): extended headers with a 32-byte nonce
     and a 1344-byte solution, DGW bootstrapping the era from the Equihash limit;
-  * block times jittered around the 60 s target so DGW actually retargets.
+  * block times jittered around the 60 s target so DGW actually retargets; the mean
+    spacing is 61 s because DGW measures 179 intervals against a 180-interval
+    timespan, so an exact 60 s mean would ratchet the difficulty up block after block.
 Each header's proof of work is found by search:
   * backend "cpu": the golden models (`_core.kawpow_search_full` over a lazily
     filled host DAG; `_core.equihash_solve_cpu`) — small chains for tests;
@@ -114,7 +116,7 @@ def _solve_equihash_header(h, params, solver, rng) -> None:
 
 
 def build_chain(n_kawpow: int, n_equihash: int = 0, network: str = "test", backend: str = "cpu", seed: int = 1,
-                device: int = 0, spacing: tuple[int, int] = (20, 100), progress=None):
+                device: int = 0, spacing: tuple[int, int] = (21, 101), progress=None):
     """Mine `n_kawpow` KawPow headers then `n_equihash` Equihash-extension headers on
     top of `network`'s genesis. Returns (params, headers)."""
     rng = random.Random(seed)
@@ -160,7 +162,7 @@ def build_chain(n_kawpow: int, n_equihash: int = 0, network: str = "test", backe
 
 
 def build_kawpow_chain(n: int, network: str = "test", backend: str = "cpu", seed: int = 1, device: int = 0,
-                       spacing: tuple[int, int] = (20, 100), progress=None):
+                       spacing: tuple[int, int] = (21, 101), progress=None):
     return build_chain(n, 0, network, backend, seed, device, spacing, progress)
 
 
