@@ -1,7 +1,10 @@
 #include "headerchain.hpp"
 
-#include <cstdio>
 #include <sys/stat.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <unordered_set>
 
 #include "../pow/equihash.hpp"
 #include "../pow/kawpow.hpp"
@@ -225,7 +228,7 @@ AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_t
     }
     r.index = add_to_index(h, hash, prev);
     r.ok = true;
-    update_active_chain();
+    consider_new_header(r.index);
     return r;
 }
 
@@ -240,17 +243,44 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
     return out;
 }
 
+// Full recompute (after invalidate / reconsider): one pass in height order marks every
+// descendant of a failed header bad, then the most-work good header becomes the tip. O(n).
 void HeaderChain::update_active_chain() {
+    std::vector<const HeaderIndex*> nodes;
+    nodes.reserve(index_.size());
+    for (auto& kv : index_) nodes.push_back(kv.second);
+    std::sort(nodes.begin(), nodes.end(),
+              [](const HeaderIndex* a, const HeaderIndex* b) { return a->height < b->height; });
+    std::unordered_set<const HeaderIndex*> bad;
     const HeaderIndex* best = genesis_;
-    for (auto& kv : index_) {
-        const HeaderIndex* c = kv.second;
-        bool bad = false;
-        for (const HeaderIndex* p = c; p && !bad; p = p->prev) bad = failed_.count(p) > 0;
-        if (bad) continue;
+    for (const HeaderIndex* c : nodes) {
+        if (failed_.count(c) || (c->prev && bad.count(c->prev))) {
+            bad.insert(c);
+            continue;
+        }
         if (c->chain_work > best->chain_work) best = c;
     }
-    active_.assign(size_t(best->height) + 1, nullptr);
-    for (const HeaderIndex* p = best; p; p = p->prev) active_[size_t(p->height)] = p;
+    set_active_tip(best);
+}
+
+// Re-point the active chain at `best`: only the entries from the fork point up change.
+void HeaderChain::set_active_tip(const HeaderIndex* best) {
+    active_.resize(size_t(best->height) + 1, nullptr);
+    for (const HeaderIndex* p = best; p && active_[size_t(p->height)] != p; p = p->prev)
+        active_[size_t(p->height)] = p;
+}
+
+// Incremental tip update after adding `idx` (ActivateBestChain for headers): a header with
+// more work than the tip becomes the tip unless a header between it and the active chain
+// failed. Costs the fork depth, not the chain length.
+void HeaderChain::consider_new_header(const HeaderIndex* idx) {
+    const HeaderIndex* t = active_.empty() ? genesis_ : active_.back();
+    if (!(idx->chain_work > t->chain_work)) return;
+    for (const HeaderIndex* p = idx; p; p = p->prev) {
+        if (size_t(p->height) < active_.size() && active_[size_t(p->height)] == p) break;  // fork point
+        if (failed_.count(p)) return;
+    }
+    set_active_tip(idx);
 }
 
 const HeaderIndex* HeaderChain::tip() const {

@@ -80,6 +80,8 @@ public:
 private:
     const HeaderIndex* add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev);
     void update_active_chain();
+    void set_active_tip(const HeaderIndex* best);
+    void consider_new_header(const HeaderIndex* idx);
 
     ChainParams params_;
     std::shared_ptr<const PowVerifier> verifier_;

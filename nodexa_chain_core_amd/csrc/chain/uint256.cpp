@@ -80,6 +80,18 @@ ArithU256& ArithU256::operator>>=(unsigned shift) {
 }
 
 ArithU256& ArithU256::operator/=(const ArithU256& b) {
+    bool small = true;  // divisor < 2^32 (DGW's n+1 and timespan): exact short division
+    for (int i = 1; i < W; ++i) small = small && b.pn[i] == 0;
+    if (small && b.pn[0] != 0) {
+        const u64 d = b.pn[0];
+        u64 rem = 0;
+        for (int i = W - 1; i >= 0; --i) {
+            const u64 cur = (rem << 32) | pn[i];
+            pn[i] = u32(cur / d);
+            rem = cur % d;
+        }
+        return *this;
+    }
     ArithU256 div = b, num = *this;
     *this = ArithU256();
     const int num_bits = int(num.bits()), div_bits = int(div.bits());

@@ -210,3 +210,60 @@ def test_blockstore_roundtrip(core, tmp_path):
     st2 = core.BlockStore(str(tmp_path / "blocks"), p.message_start, p.kawpow_activation_time)
     pos3 = st2.write(g)
     assert pos3.offset == pos2.offset + pos2.size + 8
+
+
+def _fake_header(core, chain, prev, h, t, salt=0):
+    hdr = core.BlockHeader()
+    hdr.version = 0x30000000
+    hdr.prev = prev.hash
+    hdr.merkle_root = core.sha256d(struct.pack("<II", h, salt))
+    hdr.time = t
+    hdr.height = h
+    hdr.bits = chain.next_bits(hdr) if prev.hash == chain.tip().hash else 0
+    return hdr
+
+
+def test_header_acceptance_scales_linearly(core):
+    """ProcessNewBlockHeaders over 20k headers (PoW skipped): the active-chain update is
+    incremental (fork depth), not a rescan of the whole index per header."""
+    import time
+
+    p = core.make_chain_params("test")
+    chain = core.HeaderChain(p)
+    chain.set_kawpow_activation_time(p.genesis.header.time)
+    prev, t = chain.tip(), p.genesis.header.time
+    t0 = time.perf_counter()
+    for h in range(1, 20001):
+        t += 61
+        r = chain.accept_header(_fake_header(core, chain, prev, h, t), t + 10, False)
+        assert r.ok, (h, r.reject)
+        prev = r.index
+    assert chain.height() == 20000
+    assert time.perf_counter() - t0 < 10.0
+
+
+def test_reorg_invalidate_reconsider(core):
+    """A heavier side branch takes over; invalidating its first block falls back to the
+    main branch (descendants excluded too); reconsider restores it."""
+    p = core.make_chain_params("regtest")
+    chain = core.HeaderChain(p)
+    chain.set_kawpow_activation_time(p.genesis.header.time)
+    g, t = chain.tip(), p.genesis.header.time
+    main = [g]
+    for h in range(1, 6):
+        hdr = _fake_header(core, chain, main[-1], h, t + 60 * h)
+        main.append(chain.accept_header(hdr, hdr.time + 10, False).index)
+    # side branch from height 2, one block longer (same bits on regtest -> more work)
+    side = [main[2]]
+    for h in range(3, 8):
+        hdr = _fake_header(core, chain, side[-1], h, t + 60 * h + 1, salt=1)
+        hdr.bits = main[1].bits
+        r = chain.accept_header(hdr, hdr.time + 10, False)
+        assert r.ok, r.reject
+        side.append(r.index)
+    assert chain.tip().hash == side[-1].hash and chain.height() == 7
+    assert chain.at_height(3).hash == side[1].hash
+    chain.invalidate(side[1].hash)
+    assert chain.tip().hash == main[-1].hash and chain.height() == 5
+    chain.reconsider(side[1].hash)
+    assert chain.tip().hash == side[-1].hash
