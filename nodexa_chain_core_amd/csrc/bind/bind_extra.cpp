@@ -218,6 +218,30 @@ void bind_extra(py::module_& m) {
         while (!r.empty()) out.push_back(BlockHeader::deserialize(r, act));
         return out;
     });
+    // P2P `headers` message payload: compact-size count, then header || compact-size(0)
+    // per entry (src/net_processing.cpp:2166-2187; <= MAX_HEADERS_RESULTS = 2000).
+    m.def("headers_msg_decode", [](const py::bytes& b, u32 act) {
+        Bytes d = bytes_of(b);
+        Reader r(d);
+        const u64 n = r.compact_size();
+        if (n > 2000) throw std::invalid_argument("headers message with more than 2000 headers");
+        std::vector<BlockHeader> out;
+        out.reserve(size_t(n));
+        for (u64 i = 0; i < n; ++i) {
+            out.push_back(BlockHeader::deserialize(r, act));
+            if (r.compact_size() != 0) throw std::invalid_argument("headers message: non-zero tx count");
+        }
+        return out;
+    });
+    m.def("headers_msg_encode", [](const std::vector<BlockHeader>& hs, u32 act) {
+        Writer w;
+        w.compact_size(hs.size());
+        for (auto& h : hs) {
+            w.raw(h.bytes(act));
+            w.compact_size(0);
+        }
+        return pyb(w.buf);
+    });
     py::class_<Block>(m, "Block")
         .def(py::init<>())
         .def_readwrite("header", &Block::header)

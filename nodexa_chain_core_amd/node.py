@@ -109,11 +109,43 @@ class Node:
             if not os.path.isabs(path) and self.datadir:
                 path = os.path.join(self.datadir, path)
             self.metrics_writer = metrics.JsonlWriter(path, float(a.get("metricsinterval", "10"))).start()
+        self.connman = None
+        self._start_p2p()
         self.table.warmup = None
         log.log_printf(f"nodexad started: network={self.network} height={self.state.height()} "
                        f"kawpow_activation={self.params.kawpow_activation_time} gpus={self.gpus or 'none'}")
         if a.get_bool("gen", False) and self.network != "regtest":
             self.miner.set_generate(True, self.mining_script)
+
+    def _start_p2p(self) -> None:
+        """-listen / -port / -bind / -connect (CConnman subset, net/p2p.py). Listening is opt-in
+        (-listen or -port) so tests and benches never fight over the default port."""
+        from .chain.state import ValidationInterface
+        from .net.p2p import ConnectionManager
+
+        a = self.args
+        listen = None
+        if a.get_bool("listen", False) or a.is_set("port"):
+            listen = (a.get("bind", "127.0.0.1"), a.get_int("port", self.params.default_port))
+        connect = a.get_list("connect")
+        if listen is None and not connect:
+            return
+        self.connman = ConnectionManager(self.state, self.params, gpus=self.gpus, listen=listen,
+                                         verify_mode=a.get("p2pverifymode", "auto"))
+        self.connman.start()
+        cm = self.connman
+
+        class _Relay(ValidationInterface):
+            def updated_block_tip(self, tip, fork, initial_download: bool) -> None:
+                cm.announce_block(tip.header)
+
+        self.state.register(_Relay())
+        for c in connect:
+            host, _, port = c.rpartition(":")
+            try:
+                cm.connect(host or "127.0.0.1", int(port))
+            except OSError as e:
+                log.log_printf(f"connect to {c} failed: {e}")
 
     def _start_rpc(self) -> None:
         a = self.args
@@ -145,6 +177,8 @@ class Node:
         self._stopped = True
         if self.miner is not None:
             self.miner.stop()
+        if getattr(self, "connman", None) is not None:
+            self.connman.stop()
         if getattr(self, "metrics_writer", None) is not None:
             self.metrics_writer.stop()
         if self.rpc is not None:
@@ -159,7 +193,7 @@ class Node:
 
     # ------------------------------------------------------------------ helpers used by RPCs
     def peer_count(self) -> int:
-        return 0  # P2P networking is out of the engine's scope (DEFER)
+        return self.connman.peer_count() if getattr(self, "connman", None) is not None else 0
 
     def blocks_size_on_disk(self) -> int:
         if self.datadir is None:

@@ -10,6 +10,7 @@ Engine additions are in the "gpu" category (getgpuinfo, equihash*, verifyheaders
 """
 from __future__ import annotations
 
+import struct
 import time
 
 from .. import core
@@ -536,3 +537,53 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
                            ("equihashsolve", rpc_equihashsolve, ("input",)),
                            ("equihashverify", rpc_equihashverify, ("input", "solution"))]:
         table.append("gpu", name, fn, args)
+
+    # ------------------------------------------------------------------ network (src/rpc/net.cpp subset)
+    def _cm():
+        return getattr(node, "connman", None)
+
+    def rpc_getconnectioncount(p):
+        """getconnectioncount — number of connected peers."""
+        return node.peer_count()
+
+    def rpc_getpeerinfo(p):
+        """getpeerinfo — data about each connected peer."""
+        cm = _cm()
+        return [x.as_dict() for x in list(cm.peers)] if cm else []
+
+    def rpc_getnetworkinfo(p):
+        """getnetworkinfo — P2P state."""
+        from ..net import protocol as P
+
+        cm = _cm()
+        return {"version": 40404, "subversion": P.USER_AGENT, "protocolversion": P.PROTOCOL_VERSION,
+                "localservices": "%016x" % (P.NODE_NETWORK | P.NODE_WITNESS), "localrelay": True,
+                "timeoffset": 0, "networkactive": cm is not None, "connections": node.peer_count(),
+                "networks": [], "relayfee": 0.00001, "incrementalfee": 0.00001,
+                "localaddresses": ([{"address": cm.listen_addr[0], "port": cm.port, "score": 1}]
+                                   if cm is not None and cm.port else []), "warnings": ""}
+
+    def rpc_addnode(p):
+        """addnode "node" "add|remove|onetry" — only onetry/add connect immediately here."""
+        _need(p, 2, 'addnode "node" "add|remove|onetry"')
+        cm = _cm()
+        if cm is None:
+            raise RPCError(-9, "P2P networking is disabled (start with -listen, -port or -connect)")
+        if p[1] not in ("add", "onetry", "remove"):
+            raise RPCError(-8, "Error: Node could not be added")
+        if p[1] != "remove":
+            host, _, port = str(p[0]).rpartition(":")
+            cm.connect(host or "127.0.0.1", int(port or params.default_port))
+        return None
+
+    def rpc_ping(p):
+        """ping — request a pong from every peer."""
+        cm = _cm()
+        for x in list(cm.peers) if cm else []:
+            x.send("ping", struct.pack("<Q", int(time.time() * 1e6)))
+        return None
+
+    for name, fn, args in [("getconnectioncount", rpc_getconnectioncount, ()), ("getpeerinfo", rpc_getpeerinfo, ()),
+                           ("getnetworkinfo", rpc_getnetworkinfo, ()), ("addnode", rpc_addnode, ("node", "command")),
+                           ("ping", rpc_ping, ())]:
+        table.append("network", name, fn, args)
