@@ -111,6 +111,13 @@ class Node:
             self.metrics_writer = metrics.JsonlWriter(path, float(a.get("metricsinterval", "10"))).start()
         self.connman = None
         self._start_p2p()
+        self.zmq = None
+        zmq_eps = {t: a.get("zmqpub" + t) for t in ("hashblock", "hashtx", "rawblock", "rawtx") if a.get("zmqpub" + t)}
+        if zmq_eps:
+            from .net.zmq_pub import ZmqNotifier
+
+            self.zmq = ZmqNotifier(self.state, zmq_eps)
+            self.state.register(self.zmq)
         self.table.warmup = None
         log.log_printf(f"nodexad started: network={self.network} height={self.state.height()} "
                        f"kawpow_activation={self.params.kawpow_activation_time} gpus={self.gpus or 'none'}")
@@ -179,6 +186,8 @@ class Node:
             self.miner.stop()
         if getattr(self, "connman", None) is not None:
             self.connman.stop()
+        if getattr(self, "zmq", None) is not None:
+            self.zmq.stop()
         if getattr(self, "metrics_writer", None) is not None:
             self.metrics_writer.stop()
         if self.rpc is not None:

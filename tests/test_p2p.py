@@ -132,3 +132,37 @@ def test_peer_sending_bad_headers_is_disconnected(core, tmp_path):
         sock.close()
     finally:
         a.stop()
+
+
+def test_zmq_hashblock_rawblock(core, tmp_path):
+    """-zmqpubhashblock / -zmqpubrawblock: a ZMTP 3.0 SUB client receives
+    [topic][payload][u32 seq] for every connected block (src/zmq/zmqpublishnotifier.cpp)."""
+    from nodexa_chain_core_amd.net import zmq_pub as Z
+
+    a = _node(core, tmp_path, "z", ["-zmqpubhashblock=tcp://127.0.0.1:0", "-zmqpubrawblock=tcp://127.0.0.1:0"])
+    try:
+        pubs = {t: p.port for t, p in a.zmq.pubs.items()}
+        sock = socket.create_connection(("127.0.0.1", pubs["hashblock"]))
+        sock.sendall(Z.greeting(as_server=False))
+        got = b""
+        while len(got) < 64:
+            got += sock.recv(64 - len(got))
+        assert got[0] == 0xFF and got[10] == 3
+        sock.sendall(Z.ready_command("SUB"))
+        flags, body = Z.read_frame(sock)
+        assert flags & 4 and body.startswith(b"\x05READY")
+        sock.sendall(Z.frame(b"\x01hashblock"))
+        time.sleep(0.2)
+        hashes = a.miner.generate(a.mining_script, 2)
+        for i, h in enumerate(hashes):
+            parts = []
+            while True:
+                flags, body = Z.read_frame(sock)
+                parts.append(body)
+                if not flags & 1:
+                    break
+            assert parts[0] == b"hashblock" and parts[1].hex() == h
+            assert struct.unpack("<I", parts[2])[0] == i
+        sock.close()
+    finally:
+        a.stop()
