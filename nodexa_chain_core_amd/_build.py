@@ -15,7 +15,7 @@ valid in our kernels. Device code is never linked into the host .so; every
 kernel is a code object loaded with hipModuleLoadData, which also serves the
 per-period KawPow kernels that are generated at run time (see ops/jit.py).
 
-Usage: python -m nodexa_chain_core_amd._build [--force] [--jobs N] [core|bench|hip|kernels]
+Usage: python -m nodexa_chain_core_amd._build [--force] [--jobs N] [core|bench|hip|kernels|tsan|asan]
 """
 from __future__ import annotations
 
@@ -92,7 +92,8 @@ def _compile_all(srcs: list[str], flags: list[str], objdir: str, jobs: int, forc
 
 def core_sources() -> list[str]:
     srcs = glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)
-    return sorted(s for s in srcs if os.sep + "daemon" + os.sep not in s and os.sep + "bench" + os.sep not in s)
+    skip = (os.sep + "daemon" + os.sep, os.sep + "bench" + os.sep, os.sep + "stress" + os.sep)
+    return sorted(s for s in srcs if not any(k in s for k in skip))
 
 
 def build_core(force: bool = False, jobs: int = 8) -> str:
@@ -116,6 +117,25 @@ def build_bench(force: bool = False, jobs: int = 8) -> str:
     objs = core_objs + bench_objs
     if force or _newer(out, objs):
         _run(["g++", "-o", out, *objs, "-pthread"])
+    return out
+
+
+SANITIZERS = {"tsan": ["-fsanitize=thread"], "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]}
+
+
+def build_sanitized(kind: str, force: bool = False, jobs: int = 8) -> str:
+    """bin/stress_<kind>: csrc/stress + every core source (no bindings) under ThreadSanitizer
+    ("tsan") or AddressSanitizer+UBSan ("asan"); host code only (SURVEY §5 race detection)."""
+    san = SANITIZERS[kind]
+    flags = ["-O1", "-g", "-std=c++17", "-fno-omit-frame-pointer", "-Wall", "-Wno-unused-function", *san]
+    srcs = [s for s in core_sources() if os.sep + "bind" + os.sep not in s]
+    srcs += sorted(glob.glob(os.path.join(CSRC, "stress", "*.cpp")))
+    objs = _compile_all(srcs, flags, os.path.join(BUILD, kind), jobs, force)
+    out_dir = os.path.join(PKG, "bin")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "stress_" + kind)
+    if force or _newer(out, objs):
+        _run(["g++", *san, "-o", out, *objs, "-pthread"])
     return out
 
 
@@ -183,6 +203,8 @@ def main() -> None:
             print(build_core(a.force, a.jobs))
         if w in ("all", "bench"):
             print(build_bench(a.force, a.jobs))
+        if w in ("tsan", "asan"):
+            print(build_sanitized(w, a.force, a.jobs))
         if w in ("all", "hip"):
             print(build_hip_runtime(a.force, a.jobs))
         if w in ("all", "kernels"):

@@ -153,7 +153,8 @@ void store_cached_light(const EpochContext& ctx, const Hash256& seed) {
     const std::string dir = light_cache_dir();
     if (dir.empty()) return;
     const std::string path = cache_path(ctx, seed);
-    const std::string tmp = path + ".tmp" + std::to_string(::getpid());
+    static std::atomic<u64> seq{0};  // unique per writer: several threads may store the same epoch
+    const std::string tmp = path + ".tmp" + std::to_string(::getpid()) + "." + std::to_string(seq.fetch_add(1));
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) return;
     const size_t payload = ctx.light.size() * sizeof(Hash512);
