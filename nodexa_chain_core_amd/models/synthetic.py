@@ -156,7 +156,7 @@ def build_chain(n_kawpow: int, n_equihash: int = 0, network: str = "test", backe
         if not r.ok:
             raise RuntimeError(f"synthetic header {i} rejected: {r.reject}")
         out.append(h)
-        if progress and i % 250 == 0:
+        if progress and (i % 250 == 0 or (i > n_kawpow and i % 10 == 0)):  # Equihash headers are ~100x slower
             progress(i)
     return params, out
 
