@@ -21,7 +21,7 @@ import time
 from dataclasses import dataclass, field
 
 from .. import core
-from ..utils import log
+from ..utils import log, sync
 
 _core = core()
 
@@ -75,7 +75,7 @@ class ChainState:
         self.params = params
         self.chain = _core.HeaderChain(params)
         self.chain.strict_kawpow_height = strict_height
-        self.lock = threading.RLock()
+        self.lock = sync.make_lock("cs_main")
         self.cv_tip = threading.Condition(self.lock)
         self.listeners: list[ValidationInterface] = []
         self.block_pos: dict[bytes, object] = {}

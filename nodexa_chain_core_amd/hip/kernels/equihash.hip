@@ -51,7 +51,10 @@ NX_DEV uint32_t eq_alloc_slot(const EquihashDev& p, uint32_t* cnt, uint32_t nb) 
 // Gather the rows of (level, bucket) from every bank into LDS order 0..n-1;
 // sid[i] = the row's slot index inside the bucket (what refs encode).
 // Ends with a __syncthreads(); returns n.
-template <bool ROWS, bool HALF = false>
+// LDS row layout: K0 = first stored word, STRIDE = words per staged row. (0, 8) keeps
+// the 32-byte global slot image (two b128 LDS writes); compact layouts (1, 7) / (4, 4)
+// store only the words a level can still read, so more workgroups fit per CU.
+template <bool ROWS, bool HALF = false, int K0 = 0, int STRIDE = EQ_WORDS>
 NX_DEV uint32_t eq_stage(const EquihashDev& p, uint32_t inst, int level, int buf, uint32_t bucket, uint32_t* rows,
                          short* sid, uint32_t* bstart) {
     const uint32_t per = EQ_CAP / p.banks;
@@ -73,8 +76,20 @@ NX_DEV uint32_t eq_stage(const EquihashDev& p, uint32_t inst, int level, int buf
         sid[i] = (short)slot;
         if (ROWS) {
             const uint4* src = (const uint4*)(p.hashes + eq_hidx(p, buf, inst, bucket, slot));
-            if (!HALF) ((uint4*)rows)[2 * i] = src[0];  // HALF: words 0..3 are never read
-            ((uint4*)rows)[2 * i + 1] = src[1];
+            if constexpr (K0 == 0) {
+                if (!HALF) ((uint4*)rows)[2 * i] = src[0];  // HALF: words 0..3 are never read
+                ((uint4*)rows)[2 * i + 1] = src[1];
+            } else {
+                uint32_t w[8];
+                const uint4 hi = src[1];
+                w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
+                if constexpr (K0 < 4) {
+                    const uint4 lo = src[0];
+                    w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
+                }
+#pragma unroll
+                for (int k = K0; k < 8; ++k) rows[i * STRIDE + (k - K0)] = w[k];
+            }
         }
     }
     __syncthreads();
@@ -242,67 +257,104 @@ NX_DEV void eq_store_row(const EquihashDev& p, uint32_t inst, uint32_t nb, uint3
 // thread with both slot atomics in flight — measured 16 % SLOWER per solve
 // (profiles/r1c_equihash), so it stays a tuning variant.
 #define EQ_PAIR_MAX 992  // keeps the round's LDS under 32 KiB: 5 workgroups per CU
+#ifndef EQ_EMIT_BATCH
+#define EQ_EMIT_BATCH 1  // pairs whose slot atomics a thread keeps in flight together
+#endif
+#ifdef EQ_COMPACT_LDS
+template <int R> constexpr int eq_lds_k0() { return eq_half_row(R - 1) ? 4 : 1; }
+#else
+template <int R> constexpr int eq_lds_k0() { return 0; }
+#endif
+template <int R> constexpr int eq_lds_stride() { return eq_lds_k0<R>() ? 8 - eq_lds_k0<R>() : EQ_WORDS; }
+
+template <int R>
+NX_DEV void eq_emit(const EquihashDev& p, uint32_t inst, uint32_t bucket, uint32_t* cnt, const uint32_t* rows,
+                    const short* sid, const uint32_t* pr, int np) {
+    constexpr int K0 = eq_lds_k0<R>(), ST = eq_lds_stride<R>();
+    uint32_t slot[EQ_EMIT_BATCH], nb[EQ_EMIT_BATCH];
+#pragma unroll
+    for (int k = 0; k < EQ_EMIT_BATCH; ++k) {  // all slot atomics first: their latencies overlap
+        if (k < np) {
+            uint32_t x[8];
+            eq_xor_rows<R>(rows + (pr[k] >> 16) * ST - K0, rows + (pr[k] & 0xFFFFu) * ST - K0, x);
+            nb[k] = eq_digit<R>(x) >> 8;
+            slot[k] = eq_alloc_slot(p, cnt, nb[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < EQ_EMIT_BATCH; ++k) {
+        if (k < np && slot[k] < EQ_CAP) {
+            uint32_t x[8];
+            const uint32_t i = pr[k] >> 16, j = pr[k] & 0xFFFFu;
+            eq_xor_rows<R>(rows + i * ST - K0, rows + j * ST - K0, x);
+            eq_store_row<R>(p, inst, nb[k], slot[k], x, (bucket << 20) | ((uint32_t)sid[i] << 10) | (uint32_t)sid[j]);
+        }
+    }
+}
+
+// Round R (1..8): collide level R-1 on digit R-1, write level R.
+// Phase 1 stages the bucket and chains rows by their 8-bit sub-digit (LDS
+// atomics); each thread then walks its chain and appends every surviving pair
+// to its next-level bucket (one slot atomic + one row store each), EQ_EMIT_BATCH
+// pairs at a time. EQ_PAIRLIST instead lists the pairs in LDS first and emits
+// them two per thread — measured 16 % SLOWER per solve (profiles/r1c_equihash).
 template <int R>
 NX_DEV void eq_round_impl(const EquihashDev& p) {
-    __shared__ __attribute__((aligned(16))) uint32_t rows[EQ_CAP * EQ_WORDS];
+    constexpr int K0 = eq_lds_k0<R>(), ST = eq_lds_stride<R>();
+    __shared__ __attribute__((aligned(16))) uint32_t rows[EQ_CAP * ST];
     __shared__ int head[256];
     __shared__ short nxt[EQ_CAP];
     __shared__ short sid[EQ_CAP];
     __shared__ uint32_t bstart[EQ_MAX_BANKS + 1];
+#ifdef EQ_PAIRLIST
     __shared__ uint32_t pairs[EQ_PAIR_MAX];
     __shared__ uint32_t npairs;
+#endif
     const uint32_t inst = blockIdx.y;
     const uint32_t bucket = blockIdx.x;
     for (int i = threadIdx.x; i < 256; i += EQ_BLOCK) head[i] = -1;
+#ifdef EQ_PAIRLIST
     if (threadIdx.x == 0) npairs = 0;
-    const uint32_t n = eq_stage<true, eq_half_row(R - 1)>(p, inst, R - 1, (R - 1) & 1, bucket, rows, sid, bstart);
+#endif
+    const uint32_t n = eq_stage<true, eq_half_row(R - 1), K0, ST>(p, inst, R - 1, (R - 1) & 1, bucket, rows, sid, bstart);
     for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
-        const uint32_t sub = eq_digit<R - 1>(&rows[i * EQ_WORDS]) & 0xFFu;
+        const uint32_t sub = eq_digit<R - 1>(rows + i * ST - K0) & 0xFFu;
         nxt[i] = (short)atomicExch(&head[sub], (int)i);
     }
     __syncthreads();
     uint32_t* cnt = eq_count(p, inst, R);
+    uint32_t pr[EQ_EMIT_BATCH];
+    int np = 0;
     for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
-        const uint32_t* a = &rows[i * EQ_WORDS];
+        const uint32_t* a = rows + i * ST - K0;
         int j = nxt[i];
         for (int steps = 0; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
             uint32_t x[8];
-            eq_xor_rows<R>(a, &rows[(uint32_t)j * EQ_WORDS], x);
+            eq_xor_rows<R>(a, rows + (uint32_t)j * ST - K0, x);
             if (eq_zero_from<R>(x)) continue;  // identical remainder -> only duplicate indices
 #ifdef EQ_PAIRLIST
             const uint32_t k = atomicAdd(&npairs, 1u);
-#else
-            const uint32_t k = EQ_PAIR_MAX;  // default: emit in place (measured faster)
-#endif
             if (k < EQ_PAIR_MAX) {
                 pairs[k] = (i << 16) | (uint32_t)j;
-            } else {  // list full (rare): emit directly
-                const uint32_t nb = eq_digit<R>(x) >> 8;
-                const uint32_t slot = eq_alloc_slot(p, cnt, nb);
-                if (slot < EQ_CAP)
-                    eq_store_row<R>(p, inst, nb, slot, x, (bucket << 20) | ((uint32_t)sid[i] << 10) | (uint32_t)sid[j]);
+                continue;
+            }
+#endif
+            pr[np++] = (i << 16) | (uint32_t)j;
+            if (np == EQ_EMIT_BATCH) {
+                eq_emit<R>(p, inst, bucket, cnt, rows, sid, pr, np);
+                np = 0;
             }
         }
     }
+    if (np) eq_emit<R>(p, inst, bucket, cnt, rows, sid, pr, np);
+#ifdef EQ_PAIRLIST
     __syncthreads();
-    const uint32_t np = min(npairs, (uint32_t)EQ_PAIR_MAX);
-    for (uint32_t k = threadIdx.x; k < np; k += 2 * EQ_BLOCK) {
-        const uint32_t k2 = k + EQ_BLOCK;
-        const bool two = k2 < np;
-        const uint32_t pa = pairs[k], pb = two ? pairs[k2] : pairs[k];
-        uint32_t xa[8], xb[8];
-        eq_xor_rows<R>(&rows[(pa >> 16) * EQ_WORDS], &rows[(pa & 0xFFFFu) * EQ_WORDS], xa);
-        eq_xor_rows<R>(&rows[(pb >> 16) * EQ_WORDS], &rows[(pb & 0xFFFFu) * EQ_WORDS], xb);
-        const uint32_t nba = eq_digit<R>(xa) >> 8, nbb = eq_digit<R>(xb) >> 8;
-        const uint32_t sa = eq_alloc_slot(p, cnt, nba);
-        const uint32_t sb = two ? eq_alloc_slot(p, cnt, nbb) : EQ_CAP;
-        if (sa < EQ_CAP)
-            eq_store_row<R>(p, inst, nba, sa, xa,
-                            (bucket << 20) | ((uint32_t)sid[pa >> 16] << 10) | (uint32_t)sid[pa & 0xFFFFu]);
-        if (sb < EQ_CAP)
-            eq_store_row<R>(p, inst, nbb, sb, xb,
-                            (bucket << 20) | ((uint32_t)sid[pb >> 16] << 10) | (uint32_t)sid[pb & 0xFFFFu]);
+    const uint32_t npl = min(npairs, (uint32_t)EQ_PAIR_MAX);
+    for (uint32_t k = threadIdx.x; k < npl; k += 2 * EQ_BLOCK) {
+        uint32_t pp[2] = {pairs[k], k + EQ_BLOCK < npl ? pairs[k + EQ_BLOCK] : 0u};
+        for (int q = 0; q < (k + EQ_BLOCK < npl ? 2 : 1); ++q) eq_emit<R>(p, inst, bucket, cnt, rows, sid, &pp[q], 1);
     }
+#endif
 }
 
 #define EQ_ROUND_KERNEL(R) \

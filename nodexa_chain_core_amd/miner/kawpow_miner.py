@@ -23,7 +23,7 @@ import time
 from .. import core
 from ..chain.header import from_progpow, to_progpow
 from ..chain.state import ChainState
-from ..utils import log
+from ..utils import log, sync
 from .assembler import BlockAssembler, ExtraNonce
 
 _core = core()
@@ -192,7 +192,7 @@ class MinerController:
         self._rate_t0 = time.time()
         self._threads: list[threading.Thread] = []
         self._stop = threading.Event()
-        self._lock = threading.Lock()
+        self._lock = sync.make_lock("cs_miner")
         self._cursors: dict[int, dict] = self._load_state()
         self.generating = False
 

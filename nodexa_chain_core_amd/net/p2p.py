@@ -23,7 +23,7 @@ import threading
 import time
 
 from .. import core
-from ..utils import log
+from ..utils import log, sync
 from ..utils.metrics import REGISTRY
 from . import protocol as P
 
@@ -112,12 +112,12 @@ class ConnectionManager:
         self.listen_addr = listen
         self.local_nonce = int.from_bytes(struct.pack("<d", time.time()), "little") ^ id(self)
         self.peers: list[Peer] = []
-        self._lock = threading.Lock()
+        self._lock = sync.make_lock("cs_vNodes")
         self._id = 0
         self._server: socket.socket | None = None
         self._stop = threading.Event()
         self.port: int | None = None
-        self.sync_lock = threading.Lock()  # one headers batch is processed at a time
+        self.sync_lock = sync.make_lock("cs_headers")  # one headers batch is processed at a time
 
     # ---------------------------------------------------------------- lifecycle
     def next_id(self) -> int:

@@ -90,6 +90,10 @@ class Node:
                 dagcache = os.path.join(self.datadir or ".", "dagcache")
             os.makedirs(dagcache, exist_ok=True)
             _core.set_light_cache_dir(dagcache)
+        if a.get_bool("debuglockorder", False):  # DEBUG_LOCKORDER (src/sync.cpp) for the Python-side locks
+            from .utils import sync
+
+            sync.enable(True)
         self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False))
         backends = []
         for d in self.gpus:
