@@ -51,7 +51,7 @@ static void stress_epoch_and_kawpow(int epochs) {
 static void stress_light_cache_dir(const std::string& dir, int writers) {
     set_light_cache_dir(dir);
     std::vector<std::thread> ts;
-    std::vector<std::shared_ptr<const EpochContext>> ctx(size_t(writers));
+    std::vector<std::shared_ptr<const EpochContext>> ctx(static_cast<size_t>(writers));
     for (int t = 0; t < writers; ++t) ts.emplace_back([t, &ctx] { ctx[size_t(t)] = create_epoch_context(0); });
     for (auto& th : ts) th.join();
     auto again = create_epoch_context(0);  // must load a complete, checksummed file
