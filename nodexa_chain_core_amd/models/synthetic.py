@@ -8,6 +8,10 @@ there is no chain data in this environment, so this module mines one:
   * optionally an Equihash(200,9) era after `n_kawpow` headers (the new header
     extension, csrc/chain/primitives.hpp): extended headers with a 32-byte nonce
     and a 1344-byte solution, DGW bootstrapping the era from the Equihash limit;
+  * note: DGW multiplies a 256-bit average target by the timespan without overflow
+    protection (src/pow.cpp:93-94, reproduced bit-exactly), so with testnet's 2^248
+    limit the first post-bootstrap retarget wraps and the difficulty jumps; an
+    Equihash era is therefore kept inside its 180-block bootstrap window;
   * block times jittered around the 60 s target so DGW actually retargets; the mean
     spacing is 61 s because DGW measures 179 intervals against a 180-interval
     timespan, so an exact 60 s mean would ratchet the difficulty up block after block.
