@@ -44,6 +44,10 @@ class CpuKawpowBackend:
 class GpuKawpowBackend:
     name = "gpu"
 
+    # Start building epoch e+1's DAG this many blocks before the boundary (SURVEY P9:
+    # double-buffered next-epoch prebuild). Two 4 GiB DAGs are ~3 % of 288 GB HBM3E.
+    PREBUILD_WINDOW = 120
+
     def __init__(self, device: int = 0, intensity: int = 1 << 22):
         from ..ops.ethash import DeviceEpoch  # noqa: F401  (imports torch + _hip)
 
@@ -52,6 +56,44 @@ class GpuKawpowBackend:
         self.epochs: dict[int, object] = {}
         self.searchers: dict[int, object] = {}
         self.lock = threading.Lock()
+        self._prebuild: threading.Thread | None = None
+        self.prebuilt_epochs: list[int] = []
+
+    def maybe_prebuild(self, block_number: int) -> threading.Thread | None:
+        """Near an epoch boundary, build the next epoch's DAG on a side HIP stream in a
+        background thread, so the switch costs no search time."""
+        nxt = block_number // _core.EPOCH_LENGTH + 1
+        if block_number % _core.EPOCH_LENGTH < _core.EPOCH_LENGTH - self.PREBUILD_WINDOW:
+            return None
+        with self.lock:
+            if nxt in self.epochs or (self._prebuild is not None and self._prebuild.is_alive()):
+                return None
+            t = threading.Thread(target=self._build_side, args=(nxt,), name=f"dag-prebuild-{nxt}", daemon=True)
+            self._prebuild = t
+        t.start()
+        return t
+
+    def _build_side(self, epoch: int) -> None:
+        import torch
+
+        from ..ops.ethash import DeviceEpoch
+        from ..utils.metrics import REGISTRY
+
+        t0 = time.time()
+        with torch.cuda.device(self.device):
+            side = torch.cuda.Stream(device=self.device)
+            with torch.cuda.stream(side):  # current stream is per thread: the DAG kernels go to `side`
+                e = DeviceEpoch(epoch, device=self.device)
+                e.build()
+            side.synchronize()
+            if not e.l1_matches():
+                log.log_printf(f"gpu{self.device}: prebuilt epoch {epoch} DAG failed its L1 self-check")
+                return
+        REGISTRY.set("dag_build_seconds", time.time() - t0, device=f"gpu{self.device}", epoch=epoch)
+        with self.lock:
+            self.epochs.setdefault(epoch, e)
+            self.prebuilt_epochs.append(epoch)
+        log.log_print("gpu", f"device {self.device}: epoch {epoch} DAG prebuilt in {time.time() - t0:.2f}s")
 
     def _epoch(self, epoch: int):
         import torch
@@ -82,6 +124,7 @@ class GpuKawpowBackend:
         from ..ops.kawpow import KawpowSearcher
 
         epoch = block_number // _core.EPOCH_LENGTH
+        self.maybe_prebuild(block_number)
         with self.lock:
             ep = self._epoch(epoch)
             s = self.searchers.get(epoch)

@@ -91,3 +91,24 @@ def test_vectors_other_epochs(core, gpu):
             assert (m.hex(), f.hex()) == (mix, final), block
         del e
         torch.cuda.empty_cache()
+
+
+def test_next_epoch_dag_prebuild(core, gpu):
+    """Within PREBUILD_WINDOW blocks of an epoch boundary the backend builds the next
+    epoch's DAG on a side stream; the first block of the new epoch then finds it resident
+    and a search there is bit-exact against the golden model."""
+    from nodexa_chain_core_amd.miner.kawpow_miner import GpuKawpowBackend
+
+    be = GpuKawpowBackend(0, intensity=1 << 16)
+    last = core.EPOCH_LENGTH - 5  # block 7495, epoch 0
+    t = be.maybe_prebuild(last)
+    assert t is not None
+    t.join(120)
+    assert 1 in be.epochs and be.prebuilt_epochs == [1]
+    assert be.maybe_prebuild(last) is None  # already resident
+    hh = core.sha256d(b"prebuild")
+    res = be.search(core.EPOCH_LENGTH, hh, bytes.fromhex("0f" + "ff" * 31), 0, 1 << 12)
+    assert res is not None
+    nonce, mix, fin = res
+    ctx = core.get_epoch_context(1)
+    assert core.kawpow_hash(ctx, core.EPOCH_LENGTH, hh, nonce) == (fin, mix)
