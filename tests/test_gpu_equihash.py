@@ -63,5 +63,8 @@ def test_gpu_repeatable(solver):
     inputs = [bytes([7]) * 112 for _ in range(4)]
     a = solver.solve(inputs)
     b = solver.solve(inputs)
-    assert [sorted(map(tuple, x)) for x in a] == [sorted(map(tuple, x)) for x in b]
-    assert all(x == a[0] for x in a)
+    canon = [sorted(map(tuple, x)) for x in a]
+    assert canon == [sorted(map(tuple, x)) for x in b]
+    # identical inputs in one batch: the same solution set (the order in which the
+    # reconstruct workgroups append them is not fixed)
+    assert all(x == canon[0] for x in canon)
