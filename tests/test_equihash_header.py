@@ -98,3 +98,26 @@ def test_batch_verify_cpu(core, mixed_chain):
     sol[7] ^= 1
     bad.solution = bytes(sol)
     assert verify_headers(params, [bad], gpus=None)[0]["reason"] == "invalid-solution"
+
+
+@pytest.mark.parametrize("name", ["testnet_kawpow_10k.hdr", "testnet_mixed_10k.hdr"])
+def test_synthetic_fixture_chain(core, name):
+    """The committed BASELINE config-5 fixtures (GPU-mined): every header passes the
+    contextual rules and DGW in a fresh header chain; PoW is checked on CPU for a sample
+    of KawPow headers and for every Equihash-extension header."""
+    import os
+
+    from nodexa_chain_core_amd.models import synthetic
+    from nodexa_chain_core_amd.models.verify import verify_headers
+
+    params, headers = synthetic.load(os.path.join(os.path.dirname(__file__), "data", name))
+    assert len(headers) == 10000
+    chain = core.HeaderChain(params)
+    for h in headers:
+        r = chain.accept_header(h, headers[-1].time + 3600, False)
+        assert r.ok, r.reject
+    eq = [h for h in headers if h.is_equihash()]
+    assert len(eq) == (170 if "mixed" in name else 0)
+    sample = headers[:40] + headers[7490:7510] + eq
+    res = verify_headers(params, sample)
+    assert all(r["valid"] for r in res), [r for r in res if not r["valid"]][:3]

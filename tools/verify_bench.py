@@ -22,7 +22,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-FIXTURE = os.path.join(ROOT, "tests", "data", "testnet_kawpow_10k.hdr")
+FIXTURE = os.path.join(ROOT, "tests", "data", "testnet_mixed_10k.hdr")  # 9830 KawPow + 170 Equihash
 
 
 def main() -> int:
