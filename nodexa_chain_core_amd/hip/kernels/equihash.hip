@@ -6,8 +6,9 @@
 //   a row of level r has d_0..d_{r-1} == 0 and lives in bucket  d_r >> 8
 //   (4096 buckets x EQ_CAP slots); the low 8 bits of d_r select the
 //   collision sub-bucket inside the workgroup.
-//   hash table  [2][inst][4096][EQ_CAP][8] u32: word 0 unused, words 1..7 =
-//               the 224-bit big-endian row (double-buffered across levels);
+//   hash table  [2][inst][4096][EQ_CAP][8] u32: word 0 = the row's ref (copied to
+//               `refs` when the next round stages it), words 1..7 = the 224-bit
+//               big-endian row (double-buffered across levels);
 //   refs        [inst][9][4096][EQ_CAP] u32: level 0 = leaf index, level r>0 =
 //               (parent bucket << 20 | slot a << 10 | slot b) into level r-1;
 //   counts      [inst][10][4096] u32 bucket fill (atomics), memset per solve.
@@ -76,15 +77,25 @@ NX_DEV uint32_t eq_stage(const EquihashDev& p, uint32_t inst, int level, int buf
         sid[i] = (short)slot;
         if (ROWS) {
             const uint4* src = (const uint4*)(p.hashes + eq_hidx(p, buf, inst, bucket, slot));
+#ifndef EQ_SEPARATE_REFS
+            const uint4 lo = src[0];
+            p.refs[eq_ridx(p, inst, level, bucket, slot)] = lo.x;  // bucket-contiguous: coalesced
+#endif
             if constexpr (K0 == 0) {
+#ifdef EQ_SEPARATE_REFS
                 if (!HALF) ((uint4*)rows)[2 * i] = src[0];  // HALF: words 0..3 are never read
+#else
+                if (!HALF) ((uint4*)rows)[2 * i] = lo;
+#endif
                 ((uint4*)rows)[2 * i + 1] = src[1];
             } else {
                 uint32_t w[8];
                 const uint4 hi = src[1];
                 w[4] = hi.x; w[5] = hi.y; w[6] = hi.z; w[7] = hi.w;
                 if constexpr (K0 < 4) {
+#ifdef EQ_SEPARATE_REFS
                     const uint4 lo = src[0];
+#endif
                     w[1] = lo.y; w[2] = lo.z; w[3] = lo.w;
                 }
 #pragma unroll
@@ -214,9 +225,13 @@ extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_gen(EquihashDev p) {
         const uint32_t slot = eq_alloc_slot(p, cnt, bucket);
         if (slot < EQ_CAP) {
             uint4* dst = (uint4*)(p.hashes + eq_hidx(p, 0, inst, bucket, slot));
+#ifdef EQ_SEPARATE_REFS
             dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
-            dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
             p.refs[eq_ridx(p, inst, 0, bucket, slot)] = 2 * g + half;
+#else
+            dst[0] = make_uint4(2 * g + half, w[1], w[2], w[3]);  // word 0 carries the ref (eq_store_row)
+#endif
+            dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
         }
     }
 }
@@ -244,9 +259,19 @@ template <int L>
 NX_DEV void eq_store_row(const EquihashDev& p, uint32_t inst, uint32_t nb, uint32_t slot, const uint32_t x[8],
                          uint32_t ref) {
     uint4* dst = (uint4*)(p.hashes + eq_hidx(p, L & 1, inst, nb, slot));
+#ifdef EQ_SEPARATE_REFS
     if (!eq_half_row(L)) dst[0] = make_uint4(0, x[1], x[2], x[3]);
     dst[1] = make_uint4(x[4], x[5], x[6], x[7]);
     p.refs[eq_ridx(p, inst, L, nb, slot)] = ref;
+#else
+    // One 32-byte write per row: word 0 (never part of the string) carries the
+    // back-pointer, so row and ref share one scattered memory request. The next
+    // round copies the refs of the rows it stages out to `refs` bucket by bucket,
+    // i.e. as coalesced writes (profiles/r1j: the scattered write requests, not
+    // bytes, bound the round kernels).
+    dst[0] = make_uint4(ref, x[1], x[2], x[3]);
+    dst[1] = make_uint4(x[4], x[5], x[6], x[7]);
+#endif
 }
 
 // Round R (1..8): collide level R-1 on digit R-1, write level R.
@@ -382,6 +407,9 @@ extern "C" __global__ __launch_bounds__(EQ_BLOCK) void eq_final(EquihashDev p) {
     for (uint32_t i = threadIdx.x; i < n; i += EQ_BLOCK) {
         // level 8 lives in buffer 8 & 1 = 0
         const uint32_t* w = p.hashes + eq_hidx(p, 0, inst, bucket, (uint32_t)sid[i]);
+#ifndef EQ_SEPARATE_REFS
+        p.refs[eq_ridx(p, inst, 8, bucket, (uint32_t)sid[i])] = w[0];
+#endif
         const uint32_t d8 = eq_digit<8>(w), dd = eq_digit<9>(w);
         d9[i] = dd;
         nxt[i] = (short)atomicExch(&head[d8 & 0xFFu], (int)i);
