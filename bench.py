@@ -53,7 +53,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epoch", type=int, default=384, help="384 -> 4 GiB DAG (BASELINE config)")
     ap.add_argument("--batch", type=int, default=1 << 23, help="nonces per GPU per step")
-    ap.add_argument("--equihash", type=int, default=4,
+    ap.add_argument("--equihash", type=int, default=12,
                     help="Equihash(200,9): batches of 8 solves per GPU to time (0 = skip)")
     ap.add_argument("--quiet", action="store_true")
     args = ap.parse_args()

@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world_size 2, CPU) rehearsal of the RCCL paths in parallel/:
+"""Multi-process (gloo, world_size 2 and 4, CPU) rehearsal of the RCCL paths in parallel/:
 work-packet broadcast, max/sum reductions, in-place DAG shard all-gather (slices
 filled with golden ethash items), share-ring all-gather, and the disjoint nonce
 partition bench.py and the miner use. Same code as the GPU path, gloo backend."""
@@ -77,14 +77,15 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_gloo_world2_collectives():
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_collectives(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     results = dict(q.get(timeout=280) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert results == {0: "ok", 1: "ok"}, results
+    assert results == {r: "ok" for r in range(world)}, results
