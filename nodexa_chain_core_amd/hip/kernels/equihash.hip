@@ -285,6 +285,11 @@ NX_DEV void eq_store_row(const EquihashDev& p, uint32_t inst, uint32_t nb, uint3
 #ifndef EQ_EMIT_BATCH
 #define EQ_EMIT_BATCH 1  // pairs whose slot atomics a thread keeps in flight together
 #endif
+// Compact LDS rows are the default (profiles/r1h_equihash: -4 % time per solve with the
+// ref-in-slot layout); EQ_FULL_LDS restores the 32-byte staged image for A/B runs.
+#ifndef EQ_FULL_LDS
+#define EQ_COMPACT_LDS
+#endif
 #ifdef EQ_COMPACT_LDS
 template <int R> constexpr int eq_lds_k0() { return eq_half_row(R - 1) ? 4 : 1; }
 #else
