@@ -141,14 +141,26 @@ __constant__ static const uint8_t eq_sigma[12][16] = {
     {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
     {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
 
-NX_DEV uint64_t eq_rotr(uint64_t x, int n) { return __builtin_rotateright64(x, n); }
+// 64-bit rotate as two v_alignbit_b32 on the halves (the generic lowering is four
+// shifts + two ORs); N is a literal at every call site.
+template <int N>
+NX_DEV uint64_t eq_rotr(uint64_t x) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if constexpr (N == 32) {
+        return ((uint64_t)lo << 32) | hi;
+    } else if constexpr (N < 32) {
+        return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, N) << 32) | __builtin_amdgcn_alignbit(hi, lo, N);
+    } else {
+        return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, N - 32) << 32) | __builtin_amdgcn_alignbit(lo, hi, N - 32);
+    }
+}
 
 #define EQ_G(a, b, c, d, x, y)                       \
     do {                                             \
-        v[a] = v[a] + v[b] + (x); v[d] = eq_rotr(v[d] ^ v[a], 32); \
-        v[c] = v[c] + v[d];       v[b] = eq_rotr(v[b] ^ v[c], 24); \
-        v[a] = v[a] + v[b] + (y); v[d] = eq_rotr(v[d] ^ v[a], 16); \
-        v[c] = v[c] + v[d];       v[b] = eq_rotr(v[b] ^ v[c], 63); \
+        v[a] = v[a] + v[b] + (x); v[d] = eq_rotr<32>(v[d] ^ v[a]); \
+        v[c] = v[c] + v[d];       v[b] = eq_rotr<24>(v[b] ^ v[c]); \
+        v[a] = v[a] + v[b] + (y); v[d] = eq_rotr<16>(v[d] ^ v[a]); \
+        v[c] = v[c] + v[d];       v[b] = eq_rotr<63>(v[b] ^ v[c]); \
     } while (0)
 
 NX_DEV void eq_blake2b_final(const uint64_t h0[8], const uint64_t m[16], uint64_t t0, uint64_t out[8]) {
@@ -295,7 +307,13 @@ template <int R> constexpr int eq_lds_k0() { return eq_half_row(R - 1) ? 4 : 1; 
 #else
 template <int R> constexpr int eq_lds_k0() { return 0; }
 #endif
+// Words per staged row. Half rows (4 live words) are padded to a stride of 5 under
+// EQ_LDS_PAD5 so that 64 consecutive rows hit 64 different LDS banks (stride 4: 4-way).
+#ifdef EQ_LDS_PAD5
+template <int R> constexpr int eq_lds_stride() { return eq_lds_k0<R>() == 4 ? 5 : (eq_lds_k0<R>() ? 8 - eq_lds_k0<R>() : EQ_WORDS); }
+#else
 template <int R> constexpr int eq_lds_stride() { return eq_lds_k0<R>() ? 8 - eq_lds_k0<R>() : EQ_WORDS; }
+#endif
 
 template <int R>
 NX_DEV void eq_emit(const EquihashDev& p, uint32_t inst, uint32_t bucket, uint32_t* cnt, const uint32_t* rows,
