@@ -281,12 +281,30 @@ class Node:
         return solve_cpu(inp)
 
     def rest(self, path: str):
-        """REST subset: /rest/chaininfo.json, /rest/block/<hash>.{hex,bin}, /rest/headers/<n>/<hash>.hex."""
+        """REST subset (src/rest.cpp:569-580): /rest/chaininfo.json, /rest/block/<hash>.{hex,bin},
+        /rest/headers/<n>/<hash>.{hex,bin}, /rest/mempool/{info,contents}.json,
+        /rest/blockhashbyheight/<h>.{json,hex,bin}, /rest/metrics (Prometheus)."""
         import json
 
         parts = path.split("?")[0].split("/")[2:]
         if parts == ["metrics"]:  # Prometheus text exposition of utils/metrics.REGISTRY
             return 200, "text/plain; version=0.0.4", metrics.REGISTRY.prometheus().encode()
+        if parts in (["mempool", "info.json"], ["mempool", "contents.json"]):  # src/rest.cpp rest_mempool_*
+            mp = self.state.mempool
+            if parts[1] == "info.json":
+                body = {"size": len(mp), "bytes": sum(len(e.tx.serialize(True)) for e in mp.values())}
+            else:
+                body = {_core.u256_hex(k): {"fee": e.fee / 1e8, "time": int(e.time)} for k, e in mp.items()}
+            return 200, "application/json", json.dumps(body).encode()
+        if len(parts) == 2 and parts[0] == "blockhashbyheight":
+            h, _, fmt = parts[1].partition(".")
+            idx = self.state.chain.at_height(int(h))
+            if idx is None:
+                return 404, "text/plain", b"Block height out of range"
+            if fmt == "json":
+                return 200, "application/json", json.dumps({"blockhash": _core.u256_hex(idx.hash)}).encode()
+            return (200, "application/octet-stream", bytes(idx.hash)) if fmt == "bin" else \
+                (200, "text/plain", _core.u256_hex(idx.hash).encode())
         if parts == ["chaininfo.json"]:
             tip = self.state.tip()
             body = json.dumps({"chain": self.network, "blocks": tip.height, "bestblockhash": _core.u256_hex(tip.hash)})

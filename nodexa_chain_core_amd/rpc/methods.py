@@ -492,6 +492,38 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             return {_hex(k): {"fee": e.fee / 1e8, "time": int(e.time)} for k, e in st.mempool.items()}
         return [_hex(k) for k in st.mempool]
 
+    def rpc_getmempoolinfo(p):
+        """getmempoolinfo — size / bytes of the template mempool."""
+        sizes = [len(e.tx.serialize(True)) for e in st.mempool.values()]
+        return {"size": len(sizes), "bytes": sum(sizes), "usage": sum(sizes), "maxmempool": 300_000_000,
+                "mempoolminfee": 0.00001, "minrelaytxfee": 0.00001}
+
+    def rpc_getrawtransaction(p):
+        """getrawtransaction "txid" ( verbose "blockhash" ) — mempool, or the given block (no -txindex)."""
+        _need(p, 1, 'getrawtransaction "txid" ( verbose "blockhash" )')
+        txid = _parse_hash(p[0])
+        tx, in_block = None, None
+        e = st.mempool.get(txid)
+        if e is not None:
+            tx = e.tx
+        elif _arg(p, 2) is not None:
+            bh = _parse_hash(p[2])
+            blk = st.get_block(bh)
+            if blk is None:
+                raise RPCError(RPC_INVALID_ADDRESS_OR_KEY, "Block hash not found")
+            for t in blk.vtx:
+                if t.txid() == txid:
+                    tx, in_block = t, bh
+                    break
+        if tx is None:
+            raise RPCError(RPC_INVALID_ADDRESS_OR_KEY, "No such mempool transaction. Use -txindex or provide a block hash")
+        if not _arg(p, 1, False):
+            return tx.serialize(True).hex()
+        out = tx_json(tx)
+        if in_block is not None:
+            out["blockhash"] = _hex(in_block)
+        return out
+
     def rpc_validateaddress(p):
         """validateaddress "address" """
         _need(p, 1, 'validateaddress "address"')
@@ -504,6 +536,8 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         ("rawtransactions", "decoderawtransaction", rpc_decoderawtransaction, ("hexstring",)),
         ("rawtransactions", "sendrawtransaction", rpc_sendrawtransaction, ("hexstring", "fee")),
         ("blockchain", "getrawmempool", rpc_getrawmempool, ("verbose",)),
+        ("blockchain", "getmempoolinfo", rpc_getmempoolinfo, ()),
+        ("rawtransactions", "getrawtransaction", rpc_getrawtransaction, ("txid", "verbose", "blockhash")),
         ("util", "validateaddress", rpc_validateaddress, ("address",)),
     ]:
         table.append(cat, name, fn, args)

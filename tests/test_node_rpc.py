@@ -196,3 +196,20 @@ def test_generate_x16rv2_reference_default(core, node_factory):
         if not verify_headers(p, [bad])[0]["valid"]:
             break
     assert verify_headers(p, [bad])[0]["reason"] == "high-hash"
+
+
+def test_mempool_rpcs_and_rest(core, node_factory):
+    node, addr = node_factory()
+    c = client(node)
+    hashes = c.generatetoaddress(2, addr)
+    assert c.getmempoolinfo()["size"] == 0
+    code, _, body = node.rest("/rest/mempool/info.json")
+    assert code == 200 and json.loads(body)["size"] == 0
+    code, _, body = node.rest("/rest/blockhashbyheight/2.json")
+    assert code == 200 and json.loads(body)["blockhash"] == hashes[1]
+    assert node.rest("/rest/blockhashbyheight/99.json")[0] == 404
+    blk = c.getblock(hashes[0])
+    cb = blk["tx"][0]
+    raw = c.getrawtransaction(cb, False, hashes[0])
+    assert c.decoderawtransaction(raw)["txid"] == cb
+    assert c.getrawtransaction(cb, True, hashes[0])["blockhash"] == hashes[0]
