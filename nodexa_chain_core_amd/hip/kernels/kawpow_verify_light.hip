@@ -134,7 +134,13 @@ NX_DEV uint4 kl_item512(const uint4* __restrict__ light, const FastMod32& lmod, 
 
 #define KL_MIX(r) mixs[(g * 32 + (r)) * 16 + lane]
 
-extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_light(KawpowLightParams p) {
+// DAG = false: items recomputed from the light cache (kawpow_verify_light).
+// DAG = true : items read from the resident DAG (kawpow_verify_dag) — the same
+// one-job-per-group layout, so a batch whose headers span thousands of periods
+// (3 headers each) needs no per-period padding, unlike kawpow_verify_batch's
+// wave-uniform 64-job slabs.
+template <bool DAG>
+NX_DEV void kl_verify(const KawpowLightParams& p) {
     __shared__ uint32_t l1[4096];
     __shared__ uint32_t mixs[KL_GROUPS * 32 * 16];
     __shared__ uint32_t progs[KL_GROUPS * KV_PROG_WORDS];
@@ -187,7 +193,13 @@ extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_light(Kawpo
     const uint32_t q = lane >> 2, s = lane & 3;
     for (uint32_t r = 0; r < 64; ++r) {
         const uint32_t index = kl_mod(__shfl(KL_MIX(0), (int)(r & 15), 16), p.items);
-        const uint4 mine = kl_item512(light, p.light_items, index * 4 + q, s);
+        uint4 mine;
+        if constexpr (DAG) {
+            // lane l = 4q+s holds words 4l..4l+3 of the 2048-bit item: one coalesced 256 B load per group
+            mine = ((const uint4*)p.dag)[(size_t)index * 16 + lane];
+        } else {
+            mine = kl_item512(light, p.light_items, index * 4 + q, s);
+        }
         // lane l merges words ((l^r)%16)*4..+3 of the 2048-bit item: owned by lane (l^r)%16
         const int src = (int)((lane ^ r) & 15);
         const uint32_t dw[4] = {(uint32_t)__shfl((int)mine.x, src, 16), (uint32_t)__shfl((int)mine.y, src, 16),
@@ -238,3 +250,6 @@ extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_light(Kawpo
         }
     }
 }
+
+extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_light(KawpowLightParams p) { kl_verify<false>(p); }
+extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_dag(KawpowLightParams p) { kl_verify<true>(p); }

@@ -124,6 +124,7 @@ struct KawpowLightParams {
     uint32_t num_programs;
     struct FastMod32 light_items;       // modulo by the number of 512-bit light items
     struct FastMod32 items;             // modulo by the number of 2048-bit DAG items
+    const void* dag;                    // kawpow_verify_dag: resident DAG (2048-bit items); else null
 };
 
 struct KawpowHashParams {

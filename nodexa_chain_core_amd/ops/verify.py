@@ -72,6 +72,31 @@ def _pack_jobs(order: list[int], header_hashes, nonces, block_numbers) -> bytear
 
 
 def _run_dag(ep: DeviceEpoch, idxs, block_numbers, header_hashes, nonces, out) -> None:
+    """Resident-DAG batch: one job per 16-lane group with its period's program staged in LDS
+    (kawpow_verify_dag), so headers of thousands of different periods share one dense launch."""
+    h = runtime.hip()
+    kern = runtime.static_kernel("kawpow_verify_light", "kawpow_verify_dag")
+    periods = sorted({block_numbers[i] // 3 for i in idxs})
+    pidx = {p: k for k, p in enumerate(periods)}
+    programs = [w for p in periods for w in _core.kawpow_program_words(p)]
+    job_prog = [pidx[block_numbers[i] // 3] for i in idxs]
+    assert max(job_prog) < len(periods) and len(programs) == 64 * len(periods)
+    jobs = torch.frombuffer(_pack_jobs(list(idxs), header_hashes, nonces, block_numbers),
+                            dtype=torch.uint8).to(ep.device)
+    progs = torch.tensor(programs, dtype=torch.int64).to(torch.int32).to(ep.device)
+    jp = torch.tensor(job_prog, dtype=torch.int32, device=ep.device)
+    res = torch.empty(len(idxs) * 16, dtype=torch.int32, device=ep.device)
+    h.launch_kawpow_verify_dag(kern, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(), jobs.data_ptr(),
+                               progs.data_ptr(), len(periods), jp.data_ptr(), len(idxs), res.data_ptr(),
+                               runtime.current_stream_handle())
+    raw = res.cpu().numpy().tobytes()
+    for slot, i in enumerate(idxs):
+        out[i] = (raw[slot * 64 + 32: slot * 64 + 64], raw[slot * 64: slot * 64 + 32])
+
+
+def _run_dag_slabs(ep: DeviceEpoch, idxs, block_numbers, header_hashes, nonces, out) -> None:
+    """Wave-uniform variant (kawpow_verify_batch): jobs padded into 64-job single-period
+    slabs. Efficient when each period has many jobs (nonce scans); kept as mode "dag-slab"."""
     h = runtime.hip()
     kern = runtime.static_kernel("kawpow_verify", "kawpow_verify_batch")
     by_period: dict[int, list[int]] = defaultdict(list)
@@ -124,7 +149,7 @@ def gpu_full_hash(block_numbers: list[int], header_hashes: list[bytes], nonces: 
 
     mode: "dag" (build/reuse the epoch DAG), "light" (recompute items from the light
     cache) or "auto"."""
-    if mode not in ("auto", "dag", "light"):
+    if mode not in ("auto", "dag", "dag-slab", "light"):
         raise ValueError(f"unknown verify mode {mode}")
     out: list[tuple[bytes, bytes] | None] = [None] * len(nonces)
     by_epoch: dict[int, list[int]] = defaultdict(list)
@@ -137,6 +162,8 @@ def gpu_full_hash(block_numbers: list[int], header_hashes: list[bytes], nonces: 
         with torch.cuda.device(device):
             if m == "dag":
                 _run_dag(_device_epoch(epoch, device), idxs, block_numbers, header_hashes, nonces, out)
+            elif m == "dag-slab":
+                _run_dag_slabs(_device_epoch(epoch, device), idxs, block_numbers, header_hashes, nonces, out)
             else:
                 _run_light(_light_epoch(epoch, device), idxs, block_numbers, header_hashes, nonces, out)
     return out  # type: ignore[return-value]

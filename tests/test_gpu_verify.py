@@ -8,7 +8,7 @@ from kawpow_vectors import VECTORS
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("mode", ["dag", "light"])
+@pytest.mark.parametrize("mode", ["dag", "dag-slab", "light"])
 def test_verify_batch_multi_period_vs_cpu(core, gpu, mode):
     from nodexa_chain_core_amd.ops.verify import gpu_full_hash
 
@@ -22,7 +22,7 @@ def test_verify_batch_multi_period_vs_cpu(core, gpu, mode):
         assert res[i] == core.kawpow_hash(ctx, blocks[i], headers[i], nonces[i]), i
 
 
-@pytest.mark.parametrize("mode", ["dag", "light"])
+@pytest.mark.parametrize("mode", ["dag", "dag-slab", "light"])
 def test_verify_batch_reference_vectors(core, gpu, mode):
     from nodexa_chain_core_amd.ops.verify import gpu_full_hash
 

@@ -28,7 +28,7 @@ FIXTURE = os.path.join(ROOT, "tests", "data", "testnet_mixed_10k.hdr")  # 9830 K
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--modes", nargs="*", default=["light", "dag"])
+    ap.add_argument("--modes", nargs="*", default=["light", "dag", "dag-slab"])
     ap.add_argument("--cpu-sample", type=int, default=40, help="headers timed on the serial reference path")
     ap.add_argument("--cpu-threads", action="store_true", help="also time all-host-core verification of the batch")
     ap.add_argument("--file", default=FIXTURE)
