@@ -9,6 +9,7 @@
 #include "../crypto/hashes.hpp"
 #include "../pow/x16r.hpp"
 #include "../pow/x16r_prims.hpp"
+#include "../pow/kawpow.hpp"
 
 namespace py = pybind11;
 using namespace nodexa;
@@ -39,6 +40,57 @@ ArithU256 int_to_arith(const py::int_& v) {
 
 void bind_extra(py::module_& m) {
     m.attr("EQUIHASH_VERSION_BIT") = kEquihashVersionBit;
+
+    // ------------------------------------------------ batch header verification (models/verify.py)
+    // One pass over a header batch: for every KawPow header the 48-byte job record the GPU
+    // verify kernels read (header hash progpow order, nonce64, height), its claimed mix and
+    // nBits boundary (progpow / big-endian order) and the mix-only final hash that lets a
+    // header whose claimed mix cannot meet nBits be rejected before any DAG access
+    // (kawpow::verify's first check). kind: 0 = needs the full hash, 1 = high-hash already,
+    // 2 = Equihash header, 3 = pre-KawPow (X16R) header.
+    m.def("kawpow_batch_prepare", [](const py::list& headers, u32 kawpow_activation_time) {
+        const size_t n = headers.size();
+        std::vector<const BlockHeader*> hs(n);
+        for (size_t i = 0; i < n; ++i) hs[i] = &headers[i].cast<const BlockHeader&>();
+        std::string kinds(n, '\0'), jobs(n * 48, '\0'), mix(n * 32, '\0'), bound(n * 32, '\0'), pre(n * 32, '\0');
+        {
+            py::gil_scoped_release rel;
+            for (size_t i = 0; i < n; ++i) {
+                const BlockHeader& h = *hs[i];
+                if (h.is_equihash()) { kinds[i] = 2; continue; }
+                if (!h.is_kawpow(kawpow_activation_time)) { kinds[i] = 3; continue; }
+                const Hash256 hh = h.kawpow_header_hash().to_progpow();
+                const Hash256 mx = h.mix_hash.to_progpow();
+                bool neg = false, ovf = false;
+                ArithU256 t;
+                t.set_compact(h.bits, &neg, &ovf);
+                Hash256 b;  // zero boundary (nothing passes) for a negative / overflowing nBits
+                if (!neg && !ovf) b = t.to_uint256().to_progpow();
+                const Hash256 fin = kawpow_hash_no_verify(int(h.height), hh, mx, h.nonce64);
+                kinds[i] = hash_le(fin, b) ? 0 : 1;
+                char* j = jobs.data() + 48 * i;
+                std::memcpy(j, hh.bytes, 32);
+                store_le64(reinterpret_cast<u8*>(j + 32), h.nonce64);
+                store_le32(reinterpret_cast<u8*>(j + 40), h.height);
+                std::memcpy(mix.data() + 32 * i, mx.bytes, 32);
+                std::memcpy(bound.data() + 32 * i, b.bytes, 32);
+                std::memcpy(pre.data() + 32 * i, fin.bytes, 32);
+            }
+        }
+        return py::make_tuple(py::bytes(kinds), py::bytes(jobs), py::bytes(mix), py::bytes(bound), py::bytes(pre));
+    }, py::arg("headers"), py::arg("kawpow_activation_time"));
+    m.def("kawpow_programs_bytes", [](const std::vector<u64>& periods) {
+        std::string out(periods.size() * 256, '\0');
+        {
+            py::gil_scoped_release rel;
+            for (size_t k = 0; k < periods.size(); ++k) {
+                const std::vector<u32> w = kawpow_program_words(make_kawpow_program(periods[k]));
+                if (w.size() != 64) throw std::runtime_error("unexpected program size");
+                std::memcpy(out.data() + 256 * k, w.data(), 256);
+            }
+        }
+        return py::bytes(out);
+    }, "64 little-endian u32 program words per period, concatenated (kawpow_program_words)");
     // ------------------------------------------------ uint256 / arith
     m.def("u256_hex", [](const py::bytes& b) { return u256(b).hex(); }, "uint256::GetHex of storage bytes");
     m.def("u256_from_hex", [](const std::string& s) { return pyb(Uint256::from_hex(s)); }, "uint256S");

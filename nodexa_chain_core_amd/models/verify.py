@@ -18,17 +18,11 @@ from __future__ import annotations
 import concurrent.futures as cf
 import os
 
+import numpy as np
+
 from .. import core
-from ..chain.header import from_progpow, to_progpow
 
 _core = core()
-
-
-def _job(params, h):
-    """(block_number, header_hash progpow-order, nonce, claimed mix progpow-order, boundary BE)."""
-    target, neg, ovf = _core.set_compact(h.bits)
-    return (int(h.height), to_progpow(h.kawpow_header_hash()), int(h.nonce64), to_progpow(h.mix_hash),
-            target.to_bytes(32, "big") if not (neg or ovf) else bytes(32))
 
 
 def verify_headers(params, headers, gpus: list[int] | None = None, threads: int = 0,
@@ -38,51 +32,80 @@ def verify_headers(params, headers, gpus: list[int] | None = None, threads: int 
     gpus: device ids (one host thread per GPU, the batch split in contiguous
     chunks); None/[] = all host cores with the CPU golden model. mode: GPU
     kernel choice, see ops/verify.py."""
-    jobs = [_job(params, h) for h in headers]
-    out: list[dict] = [{} for _ in jobs]
-    todo, eq_todo, legacy = [], [], []
-    for i, (bn, hh, nonce, mix, boundary) in enumerate(jobs):
-        if headers[i].is_equihash():
-            eq_todo.append(i)
-            continue
-        if headers[i].time < params.kawpow_activation_time:
-            legacy.append(i)
-            continue
-        fin = _core.kawpow_hash_no_verify(bn, hh, mix, nonce)
-        if not _core.hash_le(fin, boundary):
-            out[i] = {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(from_progpow(fin))}
-            continue
-        todo.append(i)
-    if gpus and todo:
-        from ..ops.verify import gpu_full_hash
+    act = params.kawpow_activation_time
+    hs = [h if isinstance(h, _core.BlockHeader) else _core.BlockHeader.deserialize(h.serialize(act), act)
+          for h in headers]
+    return _verify_native(params, hs, gpus, threads, mode)
 
-        def run(dev: int, part: list[int]):
-            return part, gpu_full_hash([jobs[i][0] for i in part], [jobs[i][1] for i in part],
-                                       [jobs[i][2] for i in part], device=dev, mode=mode)
 
-        k = len(gpus)
-        step = -(-len(todo) // k)
-        parts = [(d, todo[j * step:(j + 1) * step]) for j, d in enumerate(gpus) if todo[j * step:(j + 1) * step]]
-        with cf.ThreadPoolExecutor(max_workers=len(parts)) as ex:
-            for part, res in ex.map(lambda a: run(*a), parts):
-                for i, (fin, mix) in zip(part, res):
-                    out[i] = _finish(jobs[i], fin, mix)
-    else:
-        threads = threads or (os.cpu_count() or 4)
+def _rows_le(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Row-wise big-endian a <= b over (m, 32) uint8 arrays (ethash is_less_or_equal)."""
+    diff = a != b
+    first = diff.argmax(axis=1)
+    r = np.arange(len(a))
+    return ~diff.any(axis=1) | (a[r, first] < b[r, first])
 
-        def one(i):
-            bn, hh, nonce, _, _ = jobs[i]
-            ctx = _core.get_epoch_context(bn // _core.EPOCH_LENGTH)
-            return _core.kawpow_hash(ctx, bn, hh, nonce)
 
-        with cf.ThreadPoolExecutor(max_workers=threads) as ex:
-            for i, (fin, mix) in zip(todo, ex.map(one, todo)):
-                out[i] = _finish(jobs[i], fin, mix)
-    if eq_todo:
-        _verify_equihash(params, headers, eq_todo, out, gpus, threads)
+def _verify_native(params, headers, gpus, threads: int, mode: str) -> list[dict]:
+    """verify_headers for C++ BlockHeader batches: job records, boundaries and the
+    mix-only prefilter come from one native pass (kawpow_batch_prepare), the GPU result
+    rows are checked with numpy, so host time per header stays ~1-2 us."""
+    n = len(headers)
+    kinds_b, jobs_b, mix_b, bound_b, pre_b = _core.kawpow_batch_prepare(list(headers), params.kawpow_activation_time)
+    kinds = np.frombuffer(kinds_b, dtype=np.uint8)
+    out: list[dict] = [{} for _ in range(n)]
+    pre = np.frombuffer(pre_b, dtype=np.uint8).reshape(n, 32)
+    for i in np.flatnonzero(kinds == 1).tolist():
+        out[i] = {"valid": False, "reason": "high-hash", "hash": pre[i].tobytes().hex()}
+    cand = np.flatnonzero(kinds == 0)
+    if len(cand):
+        jobs = np.frombuffer(jobs_b, dtype=np.uint8).reshape(n, 48)[cand]
+        res = _gpu_rows(jobs, gpus, mode) if gpus else _cpu_rows(jobs, threads)
+        mix_ok = (res[:, :32] == np.frombuffer(mix_b, dtype=np.uint8).reshape(n, 32)[cand]).all(axis=1)
+        fin = np.ascontiguousarray(res[:, 32:])
+        le = _rows_le(fin, np.frombuffer(bound_b, dtype=np.uint8).reshape(n, 32)[cand])
+        hexes = fin.tobytes().hex()
+        for k, i in enumerate(cand.tolist()):
+            hx = hexes[64 * k: 64 * k + 64]
+            if not mix_ok[k]:
+                out[i] = {"valid": False, "reason": "invalid-mix-hash", "hash": hx}
+            elif not le[k]:
+                out[i] = {"valid": False, "reason": "high-hash", "hash": hx}
+            else:
+                out[i] = {"valid": True, "hash": hx}
+    eq = np.flatnonzero(kinds == 2).tolist()
+    if eq:
+        _verify_equihash(params, headers, eq, out, gpus, threads)
+    legacy = np.flatnonzero(kinds == 3).tolist()
     if legacy:
         _verify_x16r(params, headers, legacy, out, threads)
     return out
+
+
+def _gpu_rows(jobs: np.ndarray, gpus: list[int], mode: str) -> np.ndarray:
+    """(m, 64) mix||final rows, the batch split in contiguous chunks, one host thread per GPU."""
+    from ..ops.verify import gpu_hash_jobs
+
+    if len(gpus) == 1:
+        return gpu_hash_jobs(jobs, device=gpus[0], mode=mode)
+    chunks = [c for c in np.array_split(np.arange(len(jobs)), len(gpus)) if len(c)]
+    with cf.ThreadPoolExecutor(max_workers=len(chunks)) as ex:
+        parts = list(ex.map(lambda a: gpu_hash_jobs(jobs[a[1]], device=a[0], mode=mode), zip(gpus, chunks)))
+    return np.concatenate(parts)
+
+
+def _cpu_rows(jobs: np.ndarray, threads: int) -> np.ndarray:
+    """Same rows from the C++ golden model (light epoch contexts) on all host cores."""
+    def one(k):
+        j = jobs[k]
+        bn = int.from_bytes(j[40:44].tobytes(), "little")
+        ctx = _core.get_epoch_context(bn // _core.EPOCH_LENGTH)
+        fin, mix = _core.kawpow_hash(ctx, bn, j[:32].tobytes(), int.from_bytes(j[32:40].tobytes(), "little"))
+        return mix + fin
+
+    with cf.ThreadPoolExecutor(max_workers=threads or (os.cpu_count() or 4)) as ex:
+        rows = list(ex.map(one, range(len(jobs))))
+    return np.frombuffer(b"".join(rows), dtype=np.uint8).reshape(len(jobs), 64)
 
 
 def _verify_x16r(params, headers, idxs: list[int], out: list[dict], threads: int) -> None:
@@ -133,15 +156,6 @@ def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, th
             out[i] = {"valid": True, "hash": _core.u256_hex(hsh)}
 
 
-def _finish(job, fin: bytes, mix: bytes) -> dict:
-    _, _, _, claimed_mix, boundary = job
-    if mix != claimed_mix:
-        return {"valid": False, "reason": "invalid-mix-hash", "hash": _core.u256_hex(from_progpow(fin))}
-    if not _core.hash_le(fin, boundary):
-        return {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(from_progpow(fin))}
-    return {"valid": True, "hash": _core.u256_hex(from_progpow(fin))}
-
-
 def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None = None, mode: str = "auto") -> dict:
     """ProcessNewBlockHeaders for a batch (src/validation.cpp:12017-12035): PoW of the whole
     batch in bulk (GPU or all cores), then the contextual rules — nBits == DarkGravityWave,
@@ -152,15 +166,15 @@ def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None =
     t0 = time.perf_counter()
     pow_res = verify_headers(chain.params, headers, gpus=gpus, mode=mode)
     t1 = time.perf_counter()
+    first_bad = next((i for i, r in enumerate(pow_res) if not r["valid"]), len(headers))
     accepted, reject = 0, None
-    for i, (h, r) in enumerate(zip(headers, pow_res)):
-        if not r["valid"]:
-            reject = {"index": i, "reason": r.get("reason", "high-hash")}
-            break
-        ar = chain.accept_header(h, adjusted_time, False)
+    # contextual checks of the PoW-valid prefix in one native call (GIL released)
+    for ar in chain.accept_headers(list(headers[:first_bad]), adjusted_time, False):
         if not ar.ok:
-            reject = {"index": i, "reason": ar.reject}
+            reject = {"index": accepted, "reason": ar.reject}
             break
         accepted += 1
+    if reject is None and first_bad < len(headers):
+        reject = {"index": first_bad, "reason": pow_res[first_bad].get("reason", "high-hash")}
     t2 = time.perf_counter()
     return {"accepted": accepted, "reject": reject, "pow_s": t1 - t0, "context_s": t2 - t1}

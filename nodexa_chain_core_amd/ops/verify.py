@@ -1,11 +1,14 @@
 """GPU batch KawPow hashing for header verification (BASELINE config 5).
 
-Two kernels, chosen per epoch group of the batch:
-  * "dag"   (hip/kernels/kawpow_verify.hip): the epoch DAG is resident in HBM
-    (generated on the GPU, 0.15-0.6 s per epoch); jobs are sorted by period and
-    padded into 64-job slabs so each wave64 runs one period's program with
-    wave-uniform op fields. Best when the DAG is already resident (a mining
-    node's current epoch) or for very large batches.
+Three kernels, chosen per epoch group of the batch:
+  * "dag"   (kawpow_verify_dag in hip/kernels/kawpow_verify_light.hip): the epoch
+    DAG is resident in HBM (generated on the GPU, 0.15-0.6 s per epoch); one job per
+    16-lane group with its period's program staged in LDS, so a batch spanning
+    thousands of periods is one dense launch. Best when the DAG is already resident
+    (a mining node's current epoch) or for very large batches.
+  * "dag-slab" (kawpow_verify_batch in hip/kernels/kawpow_verify.hip): DAG-resident,
+    jobs sorted by period and padded into 64-job slabs so each wave64 runs one
+    period's program with wave-uniform op fields (nonce scans of one header).
   * "light" (hip/kernels/kawpow_verify_light.hip): no DAG; every 2048-bit item a
     hash touches is recomputed from the light cache (4 x 512 parents), one job
     per 16-lane group, any mix of periods per launch. Work per header is
@@ -17,8 +20,8 @@ below LIGHT_MAX_JOBS jobs per epoch.
 from __future__ import annotations
 
 import struct
-from collections import defaultdict
 
+import numpy as np
 import torch
 
 from .. import _core
@@ -28,6 +31,7 @@ from .ethash import DeviceEpoch
 _epochs: dict[tuple[int, int], DeviceEpoch] = {}        # (device, epoch) -> DAG-resident epochs
 _light: dict[tuple[int, int], DeviceEpoch] = {}         # (device, epoch) -> light-only epochs
 JOB = struct.Struct("<8IQII")
+JOB_DT = np.dtype([("hh", "<u4", 8), ("nonce", "<u8"), ("bn", "<u4"), ("pad", "<u4")])
 LIGHT_MAX_JOBS = 50_000
 
 
@@ -63,110 +67,121 @@ def register_resident(epoch_dev: DeviceEpoch) -> None:
         _epochs[(epoch_dev.device.index, epoch_dev.epoch)] = epoch_dev
 
 
-def _pack_jobs(order: list[int], header_hashes, nonces, block_numbers) -> bytearray:
-    buf = bytearray(JOB.size * len(order))
-    for slot, i in enumerate(order):
-        if i >= 0:
-            JOB.pack_into(buf, slot * JOB.size, *struct.unpack("<8I", header_hashes[i]), nonces[i], block_numbers[i], 0)
-    return buf
+def _pack_jobs(block_numbers, header_hashes, nonces) -> np.ndarray:
+    """(m, 48) uint8 job records (JOB) from per-job lists."""
+    jobs = np.zeros(len(nonces), dtype=JOB_DT)
+    if len(nonces):
+        jobs["hh"] = np.frombuffer(b"".join(header_hashes), dtype="<u4").reshape(-1, 8)
+        jobs["nonce"] = np.asarray(nonces, dtype=np.uint64)
+        jobs["bn"] = np.asarray(block_numbers, dtype=np.uint32)
+    return jobs.view(np.uint8).reshape(-1, JOB.size)
 
 
-def _run_dag(ep: DeviceEpoch, idxs, block_numbers, header_hashes, nonces, out) -> None:
+def _block_numbers(jobs: np.ndarray) -> np.ndarray:
+    return np.ascontiguousarray(jobs[:, 40:44]).view("<u4").ravel()
+
+
+def _programs(periods, device) -> torch.Tensor:
+    raw = _core.kawpow_programs_bytes([int(p) for p in periods])
+    assert len(raw) == 256 * len(periods)
+    return torch.frombuffer(bytearray(raw), dtype=torch.int32).to(device)
+
+
+def _grouped(jobs: np.ndarray, device):
+    """Device job records, the program of every distinct period in the batch and each
+    job's index into that program table (the kernels' job_program operand)."""
+    periods, job_prog = np.unique(_block_numbers(jobs) // 3, return_inverse=True)
+    dj = torch.from_numpy(np.ascontiguousarray(jobs)).to(device)
+    jp = torch.from_numpy(job_prog.astype(np.int32).ravel()).to(device)
+    return dj, _programs(periods, device), len(periods), jp
+
+
+def _run_dag(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
     """Resident-DAG batch: one job per 16-lane group with its period's program staged in LDS
     (kawpow_verify_dag), so headers of thousands of different periods share one dense launch."""
-    h = runtime.hip()
-    kern = runtime.static_kernel("kawpow_verify_light", "kawpow_verify_dag")
-    periods = sorted({block_numbers[i] // 3 for i in idxs})
-    pidx = {p: k for k, p in enumerate(periods)}
-    programs = [w for p in periods for w in _core.kawpow_program_words(p)]
-    job_prog = [pidx[block_numbers[i] // 3] for i in idxs]
-    assert max(job_prog) < len(periods) and len(programs) == 64 * len(periods)
-    jobs = torch.frombuffer(_pack_jobs(list(idxs), header_hashes, nonces, block_numbers),
-                            dtype=torch.uint8).to(ep.device)
-    progs = torch.tensor(programs, dtype=torch.int64).to(torch.int32).to(ep.device)
-    jp = torch.tensor(job_prog, dtype=torch.int32, device=ep.device)
-    res = torch.empty(len(idxs) * 16, dtype=torch.int32, device=ep.device)
-    h.launch_kawpow_verify_dag(kern, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(), jobs.data_ptr(),
-                               progs.data_ptr(), len(periods), jp.data_ptr(), len(idxs), res.data_ptr(),
-                               runtime.current_stream_handle())
-    raw = res.cpu().numpy().tobytes()
-    for slot, i in enumerate(idxs):
-        out[i] = (raw[slot * 64 + 32: slot * 64 + 64], raw[slot * 64: slot * 64 + 32])
+    m = len(jobs)
+    dj, progs, nprog, jp = _grouped(jobs, ep.device)
+    res = torch.empty(m * 16, dtype=torch.int32, device=ep.device)
+    runtime.hip().launch_kawpow_verify_dag(
+        runtime.static_kernel("kawpow_verify_light", "kawpow_verify_dag"), ep.dag.data_ptr(), ep.items2048,
+        ep.l1.data_ptr(), dj.data_ptr(), progs.data_ptr(), nprog, jp.data_ptr(), m, res.data_ptr(),
+        runtime.current_stream_handle())
+    return res.cpu().numpy().view(np.uint8).reshape(m, 64)
 
 
-def _run_dag_slabs(ep: DeviceEpoch, idxs, block_numbers, header_hashes, nonces, out) -> None:
+def _run_dag_slabs(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
     """Wave-uniform variant (kawpow_verify_batch): jobs padded into 64-job single-period
     slabs. Efficient when each period has many jobs (nonce scans); kept as mode "dag-slab"."""
-    h = runtime.hip()
-    kern = runtime.static_kernel("kawpow_verify", "kawpow_verify_batch")
-    by_period: dict[int, list[int]] = defaultdict(list)
-    for i in idxs:
-        by_period[block_numbers[i] // 3].append(i)
-    programs, slab_prog, order = [], [], []
-    for pi, (period, members) in enumerate(sorted(by_period.items())):
-        programs.extend(_core.kawpow_program_words(period))
-        padded = members + [-1] * ((-len(members)) % 64)
-        order.extend(padded)
-        slab_prog.extend([pi] * (len(padded) // 64))
+    per = _block_numbers(jobs) // 3
+    srt = np.argsort(per, kind="stable")
+    _, first, counts = np.unique(per[srt], return_index=True, return_counts=True)
+    parts, slab_prog = [], []
+    for k, (f, c) in enumerate(zip(first.tolist(), counts.tolist())):
+        pad = (-c) % 64
+        parts += [srt[f:f + c], np.full(pad, -1, dtype=np.int64)]
+        slab_prog += [k] * ((c + pad) // 64)
+    order = np.concatenate(parts)
+    valid = order >= 0
+    padded = np.zeros((len(order), JOB.size), dtype=np.uint8)
+    padded[valid] = jobs[order[valid]]
     # the kernel indexes job_program[slot // 64] and programs[job_program * 64]
-    assert len(slab_prog) * 64 == len(order) and max(slab_prog) < len(programs) // 64
-    jobs = torch.frombuffer(_pack_jobs(order, header_hashes, nonces, block_numbers), dtype=torch.uint8).to(ep.device)
-    progs = torch.tensor(programs, dtype=torch.int64).to(torch.int32).to(ep.device)
+    assert len(slab_prog) * 64 == len(order) and max(slab_prog) < len(first)
+    dj = torch.from_numpy(padded).to(ep.device)
+    progs = _programs(np.unique(per), ep.device)
     slabs = torch.tensor(slab_prog, dtype=torch.int32, device=ep.device)
     res = torch.empty(len(order) * 16, dtype=torch.int32, device=ep.device)
-    h.launch_kawpow_verify_batch(kern, ep.dag.data_ptr(), ep.items2048, jobs.data_ptr(), progs.data_ptr(),
-                                 slabs.data_ptr(), len(order), res.data_ptr(), runtime.current_stream_handle())
-    raw = res.cpu().numpy().tobytes()
-    for slot, i in enumerate(order):
-        if i >= 0:
-            out[i] = (raw[slot * 64 + 32: slot * 64 + 64], raw[slot * 64: slot * 64 + 32])
+    runtime.hip().launch_kawpow_verify_batch(
+        runtime.static_kernel("kawpow_verify", "kawpow_verify_batch"), ep.dag.data_ptr(), ep.items2048,
+        dj.data_ptr(), progs.data_ptr(), slabs.data_ptr(), len(order), res.data_ptr(),
+        runtime.current_stream_handle())
+    raw = res.cpu().numpy().view(np.uint8).reshape(len(order), 64)
+    out = np.empty((len(jobs), 64), dtype=np.uint8)
+    out[order[valid]] = raw[valid]
+    return out
 
 
-def _run_light(ep: DeviceEpoch, idxs, block_numbers, header_hashes, nonces, out) -> None:
-    h = runtime.hip()
-    kern = runtime.static_kernel("kawpow_verify_light", "kawpow_verify_light")
-    periods = sorted({block_numbers[i] // 3 for i in idxs})
-    pidx = {p: k for k, p in enumerate(periods)}
-    programs = [w for p in periods for w in _core.kawpow_program_words(p)]
-    job_prog = [pidx[block_numbers[i] // 3] for i in idxs]
-    assert max(job_prog) < len(periods) and len(programs) == 64 * len(periods)
-    jobs = torch.frombuffer(_pack_jobs(list(idxs), header_hashes, nonces, block_numbers),
-                            dtype=torch.uint8).to(ep.device)
-    progs = torch.tensor(programs, dtype=torch.int64).to(torch.int32).to(ep.device)
-    jp = torch.tensor(job_prog, dtype=torch.int32, device=ep.device)
-    res = torch.empty(len(idxs) * 16, dtype=torch.int32, device=ep.device)
-    h.launch_kawpow_verify_light(kern, ep.light.data_ptr(), int(ep.ctx.light_items), ep.l1.data_ptr(), ep.items2048,
-                                 jobs.data_ptr(), progs.data_ptr(), len(periods), jp.data_ptr(), len(idxs),
-                                 res.data_ptr(), runtime.current_stream_handle())
-    raw = res.cpu().numpy().tobytes()
-    for slot, i in enumerate(idxs):
-        out[i] = (raw[slot * 64 + 32: slot * 64 + 64], raw[slot * 64: slot * 64 + 32])
+def _run_light(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
+    m = len(jobs)
+    dj, progs, nprog, jp = _grouped(jobs, ep.device)
+    res = torch.empty(m * 16, dtype=torch.int32, device=ep.device)
+    runtime.hip().launch_kawpow_verify_light(
+        runtime.static_kernel("kawpow_verify_light", "kawpow_verify_light"), ep.light.data_ptr(),
+        int(ep.ctx.light_items), ep.l1.data_ptr(), ep.items2048, dj.data_ptr(), progs.data_ptr(), nprog,
+        jp.data_ptr(), m, res.data_ptr(), runtime.current_stream_handle())
+    return res.cpu().numpy().view(np.uint8).reshape(m, 64)
+
+
+def gpu_hash_jobs(jobs: np.ndarray, device: int = 0, mode: str = "auto") -> np.ndarray:
+    """Full ProgPoW of (m, 48) uint8 job records on one GPU -> (m, 64) uint8 rows:
+    mix (bytes 0..31) then final (32..63), ethash storage order.
+
+    mode: "dag" (build/reuse the epoch DAG, dense kernel), "dag-slab" (DAG, per-period
+    slabs), "light" (recompute items from the light cache) or "auto"."""
+    if mode not in ("auto", "dag", "dag-slab", "light"):
+        raise ValueError(f"unknown verify mode {mode}")
+    jobs = np.asarray(jobs, dtype=np.uint8).reshape(-1, JOB.size)
+    out = np.empty((len(jobs), 64), dtype=np.uint8)
+    epochs = _block_numbers(jobs) // _core.EPOCH_LENGTH
+    for epoch in np.unique(epochs).tolist():
+        idx = np.flatnonzero(epochs == epoch)
+        m = mode
+        if m == "auto":
+            m = "dag" if (device, epoch) in _epochs or len(idx) > LIGHT_MAX_JOBS else "light"
+        with torch.cuda.device(device):
+            if m == "dag":
+                out[idx] = _run_dag(_device_epoch(epoch, device), jobs[idx])
+            elif m == "dag-slab":
+                out[idx] = _run_dag_slabs(_device_epoch(epoch, device), jobs[idx])
+            else:
+                out[idx] = _run_light(_light_epoch(epoch, device), jobs[idx])
+    return out
 
 
 def gpu_full_hash(block_numbers: list[int], header_hashes: list[bytes], nonces: list[int],
                   device: int = 0, mode: str = "auto") -> list[tuple[bytes, bytes]]:
-    """(final, mix) in ethash storage order for every job (full ProgPoW on the GPU).
-
-    mode: "dag" (build/reuse the epoch DAG), "light" (recompute items from the light
-    cache) or "auto"."""
-    if mode not in ("auto", "dag", "dag-slab", "light"):
-        raise ValueError(f"unknown verify mode {mode}")
-    out: list[tuple[bytes, bytes] | None] = [None] * len(nonces)
-    by_epoch: dict[int, list[int]] = defaultdict(list)
-    for i, bn in enumerate(block_numbers):
-        by_epoch[bn // _core.EPOCH_LENGTH].append(i)
-    for epoch, idxs in sorted(by_epoch.items()):
-        m = mode
-        if m == "auto":
-            m = "dag" if (device, epoch) in _epochs or len(idxs) > LIGHT_MAX_JOBS else "light"
-        with torch.cuda.device(device):
-            if m == "dag":
-                _run_dag(_device_epoch(epoch, device), idxs, block_numbers, header_hashes, nonces, out)
-            elif m == "dag-slab":
-                _run_dag_slabs(_device_epoch(epoch, device), idxs, block_numbers, header_hashes, nonces, out)
-            else:
-                _run_light(_light_epoch(epoch, device), idxs, block_numbers, header_hashes, nonces, out)
-    return out  # type: ignore[return-value]
+    """(final, mix) in ethash storage order for every job (list form of gpu_hash_jobs)."""
+    raw = gpu_hash_jobs(_pack_jobs(block_numbers, header_hashes, nonces), device=device, mode=mode)
+    return [(r[32:].tobytes(), r[:32].tobytes()) for r in raw]
 
 
 class DagNonceScanner:
