@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <thread>
 #include <unordered_set>
 
 #include "../pow/equihash.hpp"
@@ -135,9 +136,14 @@ u32 HeaderChain::next_bits(const BlockHeader& candidate) const {
 }
 
 AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_time, bool check_pow) {
+    return accept_header_impl(h, nullptr, adjusted_time, check_pow, nullptr, nullptr);
+}
+
+AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256* known_hash, int64_t adjusted_time,
+                                             bool check_pow, const u32* expected_bits, const AcceptResult* precheck) {
     std::lock_guard<std::recursive_mutex> g(mu_);
     AcceptResult r;
-    const Uint256 hash = verifier_->block_hash(h, params_);
+    const Uint256 hash = known_hash ? *known_hash : verifier_->block_hash(h, params_);
     if (hash == params_.consensus.genesis_hash) {
         r.ok = true;
         r.duplicate = true;
@@ -155,7 +161,7 @@ AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_t
         r.ok = true;
         return r;
     }
-    r = check_header(h, check_pow);
+    r = precheck ? *precheck : check_header(h, check_pow);
     if (!r.ok) return r;
     r.ok = false;
     auto pit = index_.find(h.prev);
@@ -172,7 +178,7 @@ AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_t
     }
     // ContextualCheckBlockHeader
     const int height = prev->height + 1;
-    if (h.bits != next_work_required(prev, h, params_)) {
+    if (h.bits != (expected_bits ? *expected_bits : next_work_required(prev, h, params_))) {
         r.reject = "bad-diffbits";
         r.dos = 100;
         return r;
@@ -232,12 +238,83 @@ AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_t
     return r;
 }
 
+namespace {
+
+template <class F>
+void parallel_for(size_t n, F&& fn) {
+    const size_t threads = std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+    if (threads <= 1 || n < 2 * threads) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const size_t step = (n + threads - 1) / threads;
+    for (size_t t = 0; t < threads; ++t) {
+        const size_t lo = t * step, hi = std::min(n, lo + step);
+        if (lo >= hi) break;
+        pool.emplace_back([&fn, lo, hi] { for (size_t i = lo; i < hi; ++i) fn(i); });
+    }
+    for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+// ProcessNewBlockHeaders. For a batch that extends a known header linearly (the shape of
+// every P2P `headers` message) the block hashes and the expected nBits of all headers
+// are computed up front on all host cores: DarkGravityWave only reads the 180 previous
+// (nTime, nBits) pairs, which the batch itself supplies, so header i's retarget does not
+// wait for header i-1 to be indexed. The serial pass then does the index updates and
+// the remaining contextual checks. Results are identical to accepting one by one.
 std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHeader>& hs, int64_t adjusted_time,
                                                       bool check_pow) {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    const size_t n = hs.size();
     std::vector<AcceptResult> out;
-    out.reserve(hs.size());
-    for (auto& h : hs) {
-        out.push_back(accept_header(h, adjusted_time, check_pow));
+    out.reserve(n);
+    std::vector<Uint256> hashes;
+    std::vector<u32> expected;
+    std::vector<u8> have(n, 0);
+    std::vector<AcceptResult> pre;
+    if (n >= kParallelAcceptMin && check_pow) {  // CheckBlockHeader (full PoW) is context-free
+        pre.resize(n);
+        parallel_for(n, [&](size_t i) { pre[i] = check_header(hs[i], true); });
+    }
+    if (n >= kParallelAcceptMin) {
+        hashes.resize(n);
+        parallel_for(n, [&](size_t i) { hashes[i] = verifier_->block_hash(hs[i], params_); });
+        auto pit = index_.find(hs[0].prev);
+        bool linear = pit != index_.end();
+        for (size_t i = 1; linear && i < n; ++i) linear = hs[i].prev == hashes[i - 1];
+        const ConsensusParams& c = params_.consensus;
+        if (linear && !(c.pow_allow_min_difficulty_blocks && c.pow_no_retargeting)) {
+            const HeaderIndex* base = pit->second;
+            std::vector<const HeaderIndex*> anc;  // base and up to 179 ancestors, newest first
+            for (const HeaderIndex* p = base; p && anc.size() < size_t(kDgwPastBlocks); p = p->prev) anc.push_back(p);
+            const size_t a = anc.size();
+            std::vector<u32> times(a + n), bits(a + n);
+            for (size_t k = 0; k < a; ++k) {
+                times[k] = anc[a - 1 - k]->time;
+                bits[k] = anc[a - 1 - k]->bits;
+            }
+            for (size_t i = 0; i < n; ++i) {
+                times[a + i] = hs[i].time;
+                bits[a + i] = hs[i].bits;
+            }
+            const u32 limit_compact = ArithU256::from_uint256(c.pow_limit).get_compact();
+            expected.resize(n);
+            parallel_for(n, [&](size_t i) {
+                const int last_height = base->height + int(i);  // height of header i's parent
+                if (last_height + 1 < params_.dgw_activation_block) return;  // BTC retarget: serial path
+                expected[i] = last_height < kDgwPastBlocks
+                                  ? limit_compact
+                                  : dgw_average(times.data(), bits.data(), int64_t(a) - 1 + int64_t(i), hs[i].time, params_);
+                have[i] = 1;
+            });
+        }
+    }
+    for (size_t i = 0; i < n; ++i) {
+        out.push_back(accept_header_impl(hs[i], hashes.empty() ? nullptr : &hashes[i], adjusted_time, check_pow,
+                                         have[i] ? &expected[i] : nullptr, pre.empty() ? nullptr : &pre[i]));
         if (!out.back().ok) break;
     }
     return out;

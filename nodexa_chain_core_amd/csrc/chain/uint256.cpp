@@ -92,20 +92,44 @@ ArithU256& ArithU256::operator/=(const ArithU256& b) {
         }
         return *this;
     }
-    ArithU256 div = b, num = *this;
-    *this = ArithU256();
-    const int num_bits = int(num.bits()), div_bits = int(div.bits());
+    const int num_bits = int(bits()), div_bits = int(b.bits());
     if (div_bits == 0) throw std::domain_error("division by zero");
-    if (div_bits > num_bits) return *this;
+    if (div_bits > num_bits) return *this = ArithU256();
+    // binary long division on 64-bit limbs in registers: one compare / subtract / shift
+    // per quotient bit (num_bits - div_bits + 1 of them; ~70 for a mainnet GetBlockProof)
+    u64 n[4], d[4], q[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 4; ++i) {
+        n[i] = u64(pn[2 * i]) | (u64(pn[2 * i + 1]) << 32);
+        d[i] = u64(b.pn[2 * i]) | (u64(b.pn[2 * i + 1]) << 32);
+    }
     int shift = num_bits - div_bits;
-    div <<= unsigned(shift);
-    while (shift >= 0) {
-        if (num >= div) {
-            num -= div;
-            pn[shift / 32] |= (1u << (shift & 31));
+    {  // d <<= shift
+        const int k = shift / 64, r = shift % 64;
+        for (int i = 3; i >= 0; --i) {
+            const u64 hi = i - k >= 0 ? d[i - k] : 0, lo = i - k - 1 >= 0 ? d[i - k - 1] : 0;
+            d[i] = r ? (hi << r) | (lo >> (64 - r)) : hi;
         }
-        div >>= 1;
-        --shift;
+    }
+    for (; shift >= 0; --shift) {
+        bool ge = true;
+        for (int i = 3; i >= 0; --i) {
+            if (n[i] != d[i]) { ge = n[i] > d[i]; break; }
+        }
+        if (ge) {
+            u64 borrow = 0;
+            for (int i = 0; i < 4; ++i) {
+                const unsigned __int128 t = (unsigned __int128)n[i] - d[i] - borrow;
+                n[i] = u64(t);
+                borrow = u64(t >> 64) & 1;
+            }
+            q[shift / 64] |= u64(1) << (shift % 64);
+        }
+        for (int i = 0; i < 3; ++i) d[i] = (d[i] >> 1) | (d[i + 1] << 63);
+        d[3] >>= 1;
+    }
+    for (int i = 0; i < 4; ++i) {
+        pn[2 * i] = u32(q[i]);
+        pn[2 * i + 1] = u32(q[i] >> 32);
     }
     return *this;
 }

@@ -87,3 +87,40 @@ def test_process_headers_stops_at_first_invalid(chain_fixture):
     batch = [_copy(h, act) for h in headers[:5] + headers[6:9]]
     r = process_headers(chain, batch, headers[-1].time + 3600)
     assert r["accepted"] == 5 and r["reject"]["index"] == 5 and chain.height() == 5
+
+
+def test_arith_div_matches_python_ints():
+    import random
+
+    rng = random.Random(7)
+    for _ in range(5000):
+        a = rng.getrandbits(rng.randint(1, 256))
+        b = rng.getrandbits(rng.randint(1, 256)) or 1
+        assert _core.arith_div(a, b) == a // b
+
+
+@pytest.mark.parametrize("fixture", ["testnet_kawpow_10k.hdr", "testnet_mixed_10k.hdr"])
+def test_accept_headers_batch_equals_serial(fixture):
+    """accept_headers precomputes hashes + DGW for a linear batch on all cores; results,
+    tip and chain work must equal header-by-header acceptance (incl. the Equihash
+    bootstrap and DGW overflow eras of the mixed fixture)."""
+    params, headers = synthetic.load(os.path.join(os.path.dirname(__file__), "data", fixture))
+    act = params.kawpow_activation_time
+    adj = headers[-1].time + 3600
+    a = _core.HeaderChain(params)
+    ra = a.accept_headers(list(headers), adj, False)
+    b = _core.HeaderChain(params)
+    rb = [b.accept_header(h, adj, False) for h in headers]
+    assert [r.ok for r in ra] == [r.ok for r in rb] == [True] * len(headers)
+    assert a.tip().hash == b.tip().hash and a.tip().chain_work == b.tip().chain_work
+    # a wrong nBits in the middle: same reject at the same index, earlier headers kept
+    bad = list(headers)
+    h = _copy(headers[5000], act)
+    h.bits ^= 1
+    bad[5000] = h
+    c = _core.HeaderChain(params)
+    rc = c.accept_headers(bad, adj, False)
+    assert len(rc) == 5001 and rc[-1].reject == "bad-diffbits" and c.height() == headers[4999].height
+    # full PoW checked in parallel (check_pow=True) accepts the valid prefix
+    d = _core.HeaderChain(params)
+    assert all(r.ok for r in d.accept_headers(list(headers[:96]), adj, True))
