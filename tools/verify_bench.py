@@ -36,7 +36,7 @@ def main() -> int:
 
     from nodexa_chain_core_amd import _core
     from nodexa_chain_core_amd.models import synthetic
-    from nodexa_chain_core_amd.models.verify import process_headers
+    from nodexa_chain_core_amd.models.verify import LAST_TIMING, process_headers
 
     if os.path.exists(a.file):
         params, headers = synthetic.load(a.file)
@@ -83,7 +83,8 @@ def main() -> int:
             tot = r["pow_s"] + r["context_s"]
             out = dict(base, path=f"GPU {mode} x{len(gpus)}", accepted=r["accepted"], reject=r["reject"],
                        pow_s=round(r["pow_s"], 4), context_s=round(r["context_s"], 4),
-                       headers_per_s=round(n / tot, 1), vs_reference_serial=round(n / tot / ref["headers_per_s"], 1))
+                       headers_per_s=round(n / tot, 1), vs_reference_serial=round(n / tot / ref["headers_per_s"], 1),
+                       pow_stages_ms={k: round(v * 1e3, 2) for k, v in LAST_TIMING.items()})
             print(json.dumps(out), flush=True)
             if r["accepted"] != n:
                 return 1
