@@ -2,6 +2,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <thread>
+
 #include "../chain/headerchain.hpp"
 #include "../chain/script.hpp"
 #include "../chain/validation.hpp"
@@ -55,10 +57,10 @@ void bind_extra(py::module_& m) {
         std::string kinds(n, '\0'), jobs(n * 48, '\0'), mix(n * 32, '\0'), bound(n * 32, '\0'), pre(n * 32, '\0');
         {
             py::gil_scoped_release rel;
-            for (size_t i = 0; i < n; ++i) {
+            auto one = [&](size_t i) {
                 const BlockHeader& h = *hs[i];
-                if (h.is_equihash()) { kinds[i] = 2; continue; }
-                if (!h.is_kawpow(kawpow_activation_time)) { kinds[i] = 3; continue; }
+                if (h.is_equihash()) { kinds[i] = 2; return; }
+                if (!h.is_kawpow(kawpow_activation_time)) { kinds[i] = 3; return; }
                 const Hash256 hh = h.kawpow_header_hash().to_progpow();
                 const Hash256 mx = h.mix_hash.to_progpow();
                 bool neg = false, ovf = false;
@@ -75,7 +77,14 @@ void bind_extra(py::module_& m) {
                 std::memcpy(mix.data() + 32 * i, mx.bytes, 32);
                 std::memcpy(bound.data() + 32 * i, b.bytes, 32);
                 std::memcpy(pre.data() + 32 * i, fin.bytes, 32);
-            }
+            };
+            const size_t threads = n >= 1024 ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
+            std::vector<std::thread> pool;
+            const size_t step = (n + threads - 1) / threads;
+            for (size_t t = 1; t < threads; ++t)
+                pool.emplace_back([&, t] { for (size_t i = t * step; i < std::min(n, (t + 1) * step); ++i) one(i); });
+            for (size_t i = 0; i < std::min(n, step); ++i) one(i);
+            for (auto& th : pool) th.join();
         }
         return py::make_tuple(py::bytes(kinds), py::bytes(jobs), py::bytes(mix), py::bytes(bound), py::bytes(pre));
     }, py::arg("headers"), py::arg("kawpow_activation_time"));
