@@ -33,19 +33,23 @@ _light: dict[tuple[int, int], DeviceEpoch] = {}         # (device, epoch) -> lig
 JOB = struct.Struct("<8IQII")
 JOB_DT = np.dtype([("hh", "<u4", 8), ("nonce", "<u8"), ("bn", "<u4"), ("pad", "<u4")])
 LIGHT_MAX_JOBS = 50_000
+MAX_RESIDENT_DAGS = 4  # per device: <= 4 x ~5 GiB of the 288 GiB HBM
 
 
 def _device_epoch(epoch: int, device: int) -> DeviceEpoch:
     key = (device, epoch)
     e = _epochs.get(key)
     if e is None:
-        for k in [k for k in _epochs if k[0] == device]:  # keep one resident verify DAG per device
+        mine = [k for k in _epochs if k[0] == device]  # LRU: a header batch often spans 2 epochs
+        for k in mine[:max(0, len(mine) - MAX_RESIDENT_DAGS + 1)]:
             _epochs.pop(k)
         with torch.cuda.device(device):
             e = DeviceEpoch(epoch, device=device)
             e.build()
             torch.cuda.synchronize()
         _epochs[key] = e
+    else:
+        _epochs[key] = _epochs.pop(key)  # most recently used last
     return e
 
 

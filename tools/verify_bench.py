@@ -83,6 +83,9 @@ def main() -> int:
             for e in sorted({h.height // _core.EPOCH_LENGTH for h in headers}):
                 first = next(h for h in headers if h.height // _core.EPOCH_LENGTH == e)
                 verify_headers(params, [first], gpus=gpus, mode=mode)
+            eq = [h for h in headers if h.is_equihash()][:1]
+            if eq:
+                verify_headers(params, eq, gpus=gpus, mode=mode)
             setup = time.perf_counter() - tw
             chain = _core.HeaderChain(params)
             torch.cuda.synchronize()
