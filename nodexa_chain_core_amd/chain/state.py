@@ -16,6 +16,7 @@ On start-up the block index is rebuilt by scanning the blk files
 from __future__ import annotations
 
 import os
+import struct
 import threading
 import time
 from dataclasses import dataclass, field
@@ -68,6 +69,37 @@ class MempoolEntry:
     tx: object
     fee: int
     time: float = field(default_factory=time.time)
+    height: int = 0          # tip height when the tx entered the pool
+    fee_delta: int = 0       # prioritisetransaction adjustment (included in `fee`)
+    size: int = 0            # serialized size with witness
+
+    def vsize(self) -> int:
+        base = len(self.tx.serialize(False))
+        return (base * 3 + self.size + 3) // 4
+
+
+MEMPOOL_DUMP_VERSION = 1
+
+
+def _compact_size(n: int) -> bytes:
+    if n < 0xFD:
+        return bytes([n])
+    if n <= 0xFFFF:
+        return b"\xfd" + struct.pack("<H", n)
+    if n <= 0xFFFFFFFF:
+        return b"\xfe" + struct.pack("<I", n)
+    return b"\xff" + struct.pack("<Q", n)
+
+
+def _read_compact_size(b: bytes, off: int) -> tuple[int, int]:
+    v = b[off]
+    if v < 0xFD:
+        return v, off + 1
+    if v == 0xFD:
+        return struct.unpack_from("<H", b, off + 1)[0], off + 3
+    if v == 0xFE:
+        return struct.unpack_from("<I", b, off + 1)[0], off + 5
+    return struct.unpack_from("<Q", b, off + 1)[0], off + 9
 
 
 class ChainState:
@@ -80,6 +112,9 @@ class ChainState:
         self.listeners: list[ValidationInterface] = []
         self.block_pos: dict[bytes, object] = {}
         self.mempool: dict[bytes, MempoolEntry] = {}
+        self.ntx: dict[bytes, int] = {}      # transactions per stored block (CBlockIndex::nTx)
+        self.fee_stats: list[tuple[float, int]] = []  # (sat/vB, blocks to confirm) of mined pool txs
+        self.mocktime = 0                     # setmocktime (0 = wall clock)
         self.transactions_updated = 0
         self.datadir = datadir
         self.store = None
@@ -90,6 +125,7 @@ class ChainState:
             self.store = _core.BlockStore(bdir, params.message_start, params.kawpow_activation_time)
             self._load_block_files()
         gh = self.chain.genesis().hash
+        self.ntx[gh] = len(params.genesis.vtx)
         if self.store is not None and gh not in self.block_pos:
             self.block_pos[gh] = self.store.write(params.genesis)
 
@@ -107,6 +143,7 @@ class ChainState:
             r = self.chain.accept_header(blk.header, 2**62, False)
             if r.ok:
                 self.block_pos[h] = pos
+                self.ntx[h] = len(blk.vtx)
                 n += 1
         if n:
             log.log_printf(f"loaded {n} blocks from block files, tip height {self.chain.height()}")
@@ -151,15 +188,113 @@ class ChainState:
         return self.store.read_raw(pos)
 
     def adjusted_time(self) -> int:
-        return int(time.time())
+        return int(self.mocktime or time.time())
+
+    def chain_tx_count(self, idx) -> int:
+        """CBlockIndex::nChainTx: transactions in the chain up to and including idx."""
+        n = 0
+        while idx is not None:
+            n += self.ntx.get(idx.hash, 0)
+            idx = self.chain.find(idx.prev_hash) if idx.height > 0 else None
+        return n
 
     # ------------------------------------------------------------------ mempool-lite
-    def add_to_mempool(self, tx, fee: int) -> bytes:
+    def add_to_mempool(self, tx, fee: int, entry_time: float | None = None, fee_delta: int = 0) -> bytes:
         txid = tx.txid()
         with self.lock:
-            self.mempool[txid] = MempoolEntry(tx, int(fee))
+            self.mempool[txid] = MempoolEntry(tx, int(fee) + int(fee_delta), entry_time or time.time(),
+                                              self.chain.height(), int(fee_delta), len(tx.serialize(True)))
             self.transactions_updated += 1
         return txid
+
+    def clear_mempool(self) -> int:
+        with self.lock:
+            n = len(self.mempool)
+            self.mempool.clear()
+            self.transactions_updated += 1
+        return n
+
+    def mempool_parents(self, txid: bytes) -> set[bytes]:
+        e = self.mempool.get(txid)
+        return {i.prevout.hash for i in e.tx.vin if i.prevout.hash in self.mempool} if e else set()
+
+    def mempool_ancestors(self, txid: bytes) -> set[bytes]:
+        """CalculateMemPoolAncestors over in-pool parents (txmempool.cpp)."""
+        out, todo = set(), list(self.mempool_parents(txid))
+        while todo:
+            t = todo.pop()
+            if t not in out:
+                out.add(t)
+                todo.extend(self.mempool_parents(t))
+        return out
+
+    def mempool_descendants(self, txid: bytes) -> set[bytes]:
+        children: dict[bytes, set[bytes]] = {}
+        for t in self.mempool:
+            for p in self.mempool_parents(t):
+                children.setdefault(p, set()).add(t)
+        out, todo = set(), list(children.get(txid, ()))
+        while todo:
+            t = todo.pop()
+            if t not in out:
+                out.add(t)
+                todo.extend(children.get(t, ()))
+        return out
+
+    def save_mempool(self, path: str) -> int:
+        """DumpMempool (src/validation.cpp): version, count, then per tx the witness
+        serialization, entry time and fee delta, then the (empty) map of deltas for txs not
+        in the pool. Written to path.new and renamed."""
+        with self.lock:
+            entries = list(self.mempool.values())
+        out = bytearray(struct.pack("<QQ", MEMPOOL_DUMP_VERSION, len(entries)))
+        for e in entries:
+            out += e.tx.serialize(True)
+            out += struct.pack("<qq", int(e.time), int(e.fee_delta))
+        out += _compact_size(0)
+        tmp = path + ".new"
+        with open(tmp, "wb") as f:
+            f.write(out)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+        return len(entries)
+
+    def load_mempool(self, path: str) -> int:
+        """LoadMempool: re-adds every dumped tx (fees as the fee delta: no UTXO lookup)."""
+        if not os.path.exists(path):
+            return 0
+        with open(path, "rb") as f:
+            b = f.read()
+        version, count = struct.unpack_from("<QQ", b, 0)
+        if version != MEMPOOL_DUMP_VERSION:
+            return 0
+        off, n = 16, 0
+        for _ in range(count):
+            tx, used = _core.Transaction.deserialize_prefix(b, off)
+            off += used
+            t, delta = struct.unpack_from("<qq", b, off)
+            off += 16
+            self.add_to_mempool(tx, 0, float(t), delta)
+            n += 1
+        return n
+
+    def record_confirmations(self, block, height: int) -> None:
+        """Fee-estimator input (CBlockPolicyEstimator::processBlock, simplified): the feerate of
+        every pool tx the block confirms and how many blocks it waited."""
+        for tx in block.vtx[1:]:
+            e = self.mempool.get(tx.txid())
+            if e is not None:
+                self.fee_stats.append((e.fee / max(1, e.vsize()), max(1, height - e.height)))
+        del self.fee_stats[:-10000]
+
+    def estimate_fee(self, target: int) -> float | None:
+        """Median feerate (sat/vB) of recently mined pool txs confirmed within `target`
+        blocks, or None with fewer than 10 samples (the reference's 'insufficient data')."""
+        xs = sorted(f for f, waited in self.fee_stats if waited <= target)
+        if len(xs) < 10:
+            return None
+        return xs[len(xs) // 2]
 
     # ------------------------------------------------------------------ ProcessNewBlock
     def check_block_header(self, header) -> ValidationState:
@@ -208,7 +343,9 @@ class ChainState:
             else:
                 self.block_pos[h] = None
             st = ValidationState()
+            self.ntx[h] = len(block.vtx)
             self._emit("block_checked", block, st)
+            self.record_confirmations(block, height)
             for tx in block.vtx[1:]:
                 self.mempool.pop(tx.txid(), None)
             new_tip = self.chain.tip()
@@ -245,3 +382,4 @@ class ChainState:
         if min_t == max_t:
             return 0.0
         return float(pb.chain_work - pb0.chain_work) / (max_t - min_t)
+

@@ -244,6 +244,13 @@ void bind_extra(py::module_& m) {
             if (!r.empty()) throw std::runtime_error("trailing bytes after transaction");
             return t;
         })
+        .def_static("deserialize_prefix", [](const py::bytes& b, size_t offset) {
+            Bytes d = bytes_of(b);
+            if (offset > d.size()) throw std::out_of_range("offset past the end");
+            Reader r(d.data() + offset, d.size() - offset);
+            Transaction t = Transaction::deserialize(r);
+            return py::make_tuple(t, r.pos());
+        }, py::arg("data"), py::arg("offset") = 0, "(tx, bytes consumed) for a transaction at data[offset:]")
         .def("txid", [](const Transaction& t) { return pyb(t.txid()); })
         .def("wtxid", [](const Transaction& t) { return pyb(t.wtxid()); })
         .def("is_coinbase", &Transaction::is_coinbase)

@@ -28,6 +28,7 @@ from ..utils.metrics import REGISTRY
 from . import protocol as P
 
 _core = core()
+DEFAULT_MISBEHAVING_BANTIME = 60 * 60 * 24  # -bantime (src/net.h)
 
 
 class Peer:
@@ -51,6 +52,7 @@ class Peer:
         with self._send_lock:
             self.sock.sendall(msg)
         self.bytes_sent += len(msg)
+        self.mgr.total_sent += len(msg)
         self.last_send = time.time()
         REGISTRY.inc("p2p_bytes_sent_total", len(msg), command=cmd)
 
@@ -63,6 +65,7 @@ class Peer:
         self.misbehavior += score
         log.log_print("net", f"peer {self.id} misbehaving +{score} ({why}), total {self.misbehavior}")
         if self.misbehavior >= 100:
+            self.mgr.ban(self.addr[0], DEFAULT_MISBEHAVING_BANTIME)
             self.close()
 
     def close(self) -> None:
@@ -81,6 +84,7 @@ class Peer:
             while not self.closed.is_set():
                 cmd, payload = P.read_message(self.sock, self.mgr.magic)
                 self.bytes_recv += P.HEADER_SIZE + len(payload)
+                self.mgr.total_recv += P.HEADER_SIZE + len(payload)
                 self.last_recv = time.time()
                 REGISTRY.inc("p2p_bytes_recv_total", P.HEADER_SIZE + len(payload), command=cmd)
                 self.mgr.handle(self, cmd, payload)
@@ -118,6 +122,11 @@ class ConnectionManager:
         self._stop = threading.Event()
         self.port: int | None = None
         self.sync_lock = sync.make_lock("cs_headers")  # one headers batch is processed at a time
+        self.total_sent = self.total_recv = 0
+        self.started = time.time()
+        self.network_active = True
+        self.banned: dict[str, dict] = {}   # address -> {"banned_until", "ban_created", "ban_reason"}
+        self.added_nodes: list[str] = []    # addnode "add" list (getaddednodeinfo)
 
     # ---------------------------------------------------------------- lifecycle
     def next_id(self) -> int:
@@ -142,9 +151,14 @@ class ConnectionManager:
                 sock, addr = self._server.accept()
             except OSError:
                 break
+            if not self.network_active or self.is_banned(addr[0]):
+                sock.close()  # CConnman::AcceptConnection drops banned / inactive-network peers
+                continue
             self._add(sock, addr, inbound=True)
 
     def connect(self, host: str, port: int, timeout: float = 10.0) -> Peer:
+        if not self.network_active:
+            raise ConnectionError("network is disabled (setnetworkactive false)")
         sock = socket.create_connection((host, port), timeout=timeout)
         sock.settimeout(None)
         return self._add(sock, (host, port), inbound=False)
@@ -172,6 +186,44 @@ class ConnectionManager:
     def peer_count(self) -> int:
         with self._lock:
             return sum(1 for p in self.peers if p.verack)
+
+    # ---------------------------------------------------------------- bans / control (src/rpc/net.cpp)
+    def ban(self, address: str, seconds: int, absolute: bool = False, reason: str = "node misbehaving") -> None:
+        now = int(time.time())
+        until = int(seconds) if absolute else now + int(seconds or DEFAULT_MISBEHAVING_BANTIME)
+        self.banned[address] = {"address": address, "banned_until": until, "ban_created": now, "ban_reason": reason}
+        for p in list(self.peers):
+            if p.addr[0] == address:
+                p.close()
+
+    def unban(self, address: str) -> bool:
+        return self.banned.pop(address, None) is not None
+
+    def is_banned(self, address: str) -> bool:
+        e = self.banned.get(address)
+        if e is not None and e["banned_until"] < time.time():
+            self.banned.pop(address, None)
+            return False
+        return e is not None
+
+    def list_banned(self) -> list[dict]:
+        for a in list(self.banned):
+            self.is_banned(a)  # sweep expired entries
+        return list(self.banned.values())
+
+    def disconnect(self, address: str | None = None, node_id: int | None = None) -> bool:
+        for p in list(self.peers):
+            host, port = p.addr[:2]
+            if (node_id is not None and p.id == node_id) or (address is not None and address in (f"{host}:{port}", host)):
+                p.close()
+                return True
+        return False
+
+    def set_network_active(self, active: bool) -> None:
+        self.network_active = bool(active)
+        if not active:
+            for p in list(self.peers):
+                p.close()
 
     # ---------------------------------------------------------------- relay
     def announce_block(self, header) -> None:

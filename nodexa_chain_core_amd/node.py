@@ -27,7 +27,7 @@ from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
 from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, GpuKawpowBackend, MinerController
-from .rpc import methods
+from .rpc import methods, methods_ext
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
 from .utils import log, metrics
 from .utils.config import ArgsManager, gpu_list
@@ -82,6 +82,7 @@ class Node:
         # RPC comes up first in warm-up mode (AppInitServers)
         self.table.warmup = "Loading block index..."
         methods.register(self.table, self)
+        methods_ext.register(self.table, self)
         if a.get_bool("server", True):
             self._start_rpc()
         dagcache = a.get("dagcache")
@@ -95,6 +96,10 @@ class Node:
 
             sync.enable(True)
         self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False))
+        if self.datadir is not None and a.get_bool("persistmempool", True):  # -persistmempool (LoadMempool)
+            n = self.state.load_mempool(os.path.join(self.datadir, "mempool.dat"))
+            if n:
+                log.log_printf(f"Imported mempool transactions from disk: {n} succeeded")
         backends = []
         for d in self.gpus:
             backends.append(GpuKawpowBackend(d, a.get_int("gpuintensity", 1 << 22)))
@@ -188,6 +193,11 @@ class Node:
         self._stopped = True
         if self.miner is not None:
             self.miner.stop()
+        if self.state is not None and self.datadir is not None and self.args.get_bool("persistmempool", True):
+            try:
+                self.state.save_mempool(os.path.join(self.datadir, "mempool.dat"))  # DumpMempool on shutdown
+            except OSError as e:
+                log.log_printf(f"Failed to dump mempool: {e}")
         if getattr(self, "connman", None) is not None:
             self.connman.stop()
         if getattr(self, "zmq", None) is not None:

@@ -451,6 +451,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         e = st.mempool.get(_parse_hash(p[0]))
         if e is not None:
             e.fee += int(p[2])
+            e.fee_delta += int(p[2])
         return True
 
     for name, fn, args in [
@@ -605,9 +606,17 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             raise RPCError(-9, "P2P networking is disabled (start with -listen, -port or -connect)")
         if p[1] not in ("add", "onetry", "remove"):
             raise RPCError(-8, "Error: Node could not be added")
-        if p[1] != "remove":
-            host, _, port = str(p[0]).rpartition(":")
-            cm.connect(host or "127.0.0.1", int(port or params.default_port))
+        if p[1] == "remove":
+            if p[0] not in cm.added_nodes:
+                raise RPCError(-24, "Error: Node has not been added.")
+            cm.added_nodes.remove(p[0])
+            return None
+        if p[1] == "add":
+            if p[0] in cm.added_nodes:
+                raise RPCError(-23, "Error: Node already added")
+            cm.added_nodes.append(p[0])
+        host, _, port = str(p[0]).rpartition(":")
+        cm.connect(host or "127.0.0.1", int(port or params.default_port))
         return None
 
     def rpc_ping(p):
