@@ -23,6 +23,7 @@ from dataclasses import dataclass, field
 
 from .. import core
 from ..utils import log, sync
+from .blockindex import BlockIndexLog, scan_blk_tail
 
 _core = core()
 
@@ -103,10 +104,11 @@ def _read_compact_size(b: bytes, off: int) -> tuple[int, int]:
 
 
 class ChainState:
-    def __init__(self, params, datadir: str | None = None, strict_height: bool = False):
+    def __init__(self, params, datadir: str | None = None, strict_height: bool = False, reindex: bool = False):
         self.params = params
         self.chain = _core.HeaderChain(params)
         self.chain.strict_kawpow_height = strict_height
+        self.strict_height = strict_height
         self.lock = sync.make_lock("cs_main")
         self.cv_tip = threading.Condition(self.lock)
         self.listeners: list[ValidationInterface] = []
@@ -119,34 +121,88 @@ class ChainState:
         self.datadir = datadir
         self.store = None
         self.start_time = time.time()
+        self.index_log: BlockIndexLog | None = None
         if datadir is not None:
             bdir = os.path.join(datadir, "blocks")
             os.makedirs(bdir, exist_ok=True)
             self.store = _core.BlockStore(bdir, params.message_start, params.kawpow_activation_time)
-            self._load_block_files()
+            self.index_log = BlockIndexLog(os.path.join(bdir, "index.log"))
+            if reindex or not self._load_index(bdir):
+                self._load_block_files()
         gh = self.chain.genesis().hash
         self.ntx[gh] = len(params.genesis.vtx)
         if self.store is not None and gh not in self.block_pos:
             self.block_pos[gh] = self.store.write(params.genesis)
+            self.index_log.append(params.genesis.header.serialize(params.kawpow_activation_time),
+                                  self.block_pos[gh], len(params.genesis.vtx))
 
     # ------------------------------------------------------------------ load / reindex
     def _load_block_files(self) -> None:
+        """-reindex: rebuild the index from every record of the blk files, then rewrite
+        blocks/index.log from the result."""
         act = self.params.kawpow_activation_time
-        n = 0
+        n, records = 0, []
         for pos, raw in self.store.scan():
             blk = _core.Block.deserialize(raw, act)
             h = self.chain.block_hash(blk.header)
             if h == self.chain.genesis().hash:
                 self.block_pos[h] = pos
+                records.append((blk.header.serialize(act), pos, len(blk.vtx)))
                 continue
             # blocks in our files were fully validated before they were written
             r = self.chain.accept_header(blk.header, 2**62, False)
             if r.ok:
                 self.block_pos[h] = pos
                 self.ntx[h] = len(blk.vtx)
+                records.append((blk.header.serialize(act), pos, len(blk.vtx)))
                 n += 1
+        self.index_log.rewrite(records)
         if n:
-            log.log_printf(f"loaded {n} blocks from block files, tip height {self.chain.height()}")
+            log.log_printf(f"reindexed {n} blocks from block files, tip height {self.chain.height()}")
+
+    def _load_index(self, bdir: str) -> bool:
+        """LoadBlockIndex from blocks/index.log: headers accepted in one batch (no blk reads),
+        then any blocks written after the last good record are recovered from the blk-file
+        tail. False = no usable index (caller reindexes)."""
+        act = self.params.kawpow_activation_time
+        recs = self.index_log.load()
+        if not recs:
+            return not os.path.exists(os.path.join(bdir, "blk00000.dat"))
+        hdrs = [_core.BlockHeader.deserialize(hb, act) for hb, _, _ in recs]
+        res = self.chain.accept_headers(hdrs, 2**62, False)
+        if len(res) != len(recs) or not all(r.ok for r in res):
+            log.log_printf("block index log inconsistent with the header rules; reindexing")
+            self.chain = _core.HeaderChain(self.params)
+            self.chain.strict_kawpow_height = self.strict_height
+            self.block_pos.clear()
+            self.ntx.clear()
+            return False
+        last = (0, 0, 0)
+        for (_, (fi, fo, fs), ntx), r in zip(recs, res):
+            pos = _core.BlockPos()
+            pos.file, pos.offset, pos.size = fi, fo, fs
+            self.block_pos[r.index.hash] = pos
+            self.ntx[r.index.hash] = ntx
+            last = max(last, (fi, fo, fs))
+        n = 0
+        for fi, fo, raw in scan_blk_tail(bdir, bytes(self.params.message_start), last[0], last[1] + last[2]):
+            blk = _core.Block.deserialize(raw, act)
+            r = self.chain.accept_header(blk.header, 2**62, False)
+            if not r.ok:
+                break
+            pos = _core.BlockPos()
+            pos.file, pos.offset, pos.size = fi, fo, len(raw)
+            self.block_pos[r.index.hash] = pos
+            self.ntx[r.index.hash] = len(blk.vtx)
+            self.index_log.append(blk.header.serialize(act), pos, len(blk.vtx))
+            n += 1
+        log.log_printf(f"loaded block index: {len(recs)} records (+{n} recovered from blk files), "
+                       f"tip height {self.chain.height()}")
+        return True
+
+    def close(self) -> None:
+        if self.index_log is not None:
+            self.index_log.close()
 
     # ------------------------------------------------------------------ signals
     def register(self, l: ValidationInterface) -> None:
@@ -340,6 +396,8 @@ class ChainState:
                 return st
             if self.store is not None:
                 self.block_pos[h] = self.store.write(block)
+                self.index_log.append(block.header.serialize(self.params.kawpow_activation_time), self.block_pos[h],
+                                      len(block.vtx))
             else:
                 self.block_pos[h] = None
             st = ValidationState()

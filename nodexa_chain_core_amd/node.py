@@ -95,7 +95,8 @@ class Node:
             from .utils import sync
 
             sync.enable(True)
-        self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False))
+        self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False),
+                                reindex=a.get_bool("reindex", False))
         if self.datadir is not None and a.get_bool("persistmempool", True):  # -persistmempool (LoadMempool)
             n = self.state.load_mempool(os.path.join(self.datadir, "mempool.dat"))
             if n:
@@ -200,6 +201,8 @@ class Node:
                 log.log_printf(f"Failed to dump mempool: {e}")
         if getattr(self, "connman", None) is not None:
             self.connman.stop()
+        if self.state is not None:
+            self.state.close()
         if getattr(self, "zmq", None) is not None:
             self.zmq.stop()
         if getattr(self, "metrics_writer", None) is not None:
