@@ -294,9 +294,11 @@ class Node:
         return solve_cpu(inp)
 
     def rest(self, path: str):
-        """REST subset (src/rest.cpp:569-580): /rest/chaininfo.json, /rest/block/<hash>.{hex,bin},
-        /rest/headers/<n>/<hash>.{hex,bin}, /rest/mempool/{info,contents}.json,
-        /rest/blockhashbyheight/<h>.{json,hex,bin}, /rest/metrics (Prometheus)."""
+        """REST (src/rest.cpp:569-580): /rest/chaininfo.json, /rest/block/<hash>.{bin,hex,json},
+        /rest/block/notxdetails/<hash>.{bin,hex,json}, /rest/headers/<n>/<hash>.{bin,hex,json},
+        /rest/tx/<txid>.{bin,hex,json} (mempool), /rest/mempool/{info,contents}.json,
+        /rest/blockhashbyheight/<h>.{json,hex,bin}, /rest/metrics (Prometheus). /rest/getutxos
+        needs the UTXO set (DEFER)."""
         import json
 
         parts = path.split("?")[0].split("/")[2:]
@@ -322,22 +324,39 @@ class Node:
             tip = self.state.tip()
             body = json.dumps({"chain": self.network, "blocks": tip.height, "bestblockhash": _core.u256_hex(tip.hash)})
             return 200, "application/json", body.encode()
-        if len(parts) == 2 and parts[0] == "block":
-            h, _, fmt = parts[1].partition(".")
+        rpc = lambda name, *a: self.table.commands[name].handler(list(a))  # noqa: E731 — JSON forms reuse the RPCs
+        if parts[:1] == ["block"] and len(parts) in (2, 3) and (len(parts) == 2 or parts[1] == "notxdetails"):
+            h, _, fmt = parts[-1].partition(".")
             raw = self.state.get_block_raw(_core.u256_from_hex(h))
             if raw is None:
-                return 404, "text/plain", b"block not found"
+                return 404, "text/plain", f"{h} not found".encode()
+            if fmt == "json":  # rest_block_extended / rest_block_notxdetails
+                return 200, "application/json", json.dumps(rpc("getblock", h, 1 if len(parts) == 3 else 2)).encode()
             return (200, "application/octet-stream", raw) if fmt == "bin" else (200, "text/plain", raw.hex().encode())
         if len(parts) == 3 and parts[0] == "headers":
             n = int(parts[1])
+            if n < 1 or n > 2000:
+                return 400, "text/plain", f"Header count out of range: {n}".encode()
             h, _, fmt = parts[2].partition(".")
             idx = self.state.chain.find(_core.u256_from_hex(h))
-            out = b""
-            while idx is not None and n > 0:
+            out, found = b"", []
+            while idx is not None and n > 0 and self.state.chain.in_active_chain(idx):
                 out += idx.header.serialize(self.params.kawpow_activation_time)
+                found.append(idx)
                 idx = self.state.chain.at_height(idx.height + 1)
                 n -= 1
+            if fmt == "json":
+                return 200, "application/json", json.dumps([rpc("getblockheader", _core.u256_hex(i.hash)) for i in found]).encode()
             return (200, "application/octet-stream", out) if fmt == "bin" else (200, "text/plain", out.hex().encode())
+        if len(parts) == 2 and parts[0] == "tx":  # rest_tx: mempool (no -txindex in this engine)
+            h, _, fmt = parts[1].partition(".")
+            e = self.state.mempool.get(_core.u256_from_hex(h))
+            if e is None:
+                return 404, "text/plain", f"{h} not found".encode()
+            raw = e.tx.serialize(True)
+            if fmt == "json":
+                return 200, "application/json", json.dumps(rpc("getrawtransaction", h, True)).encode()
+            return (200, "application/octet-stream", raw) if fmt == "bin" else (200, "text/plain", raw.hex().encode())
         return 404, "text/plain", b"unknown REST path"
 
 

@@ -129,3 +129,26 @@ def test_network_rpcs(core, node_factory):  # noqa: F811
     assert "-29" in _rpc_error(c2.disconnectnode, "127.0.0.1:1")
     assert c2.setnetworkactive(False) is False
     assert c2.setnetworkactive(True) is True
+
+
+def test_rest_block_tx_headers(core, node_factory):  # noqa: F811
+    import json
+
+    node, addr = node_factory()
+    c = client(node)
+    hashes = c.generatetoaddress(3, addr)
+    code, _, body = node.rest(f"/rest/block/{hashes[1]}.json")
+    blk = json.loads(body)
+    assert code == 200 and blk["hash"] == hashes[1] and isinstance(blk["tx"][0], dict)
+    code, _, body = node.rest(f"/rest/block/notxdetails/{hashes[1]}.json")
+    assert code == 200 and isinstance(json.loads(body)["tx"][0], str)
+    code, _, body = node.rest(f"/rest/block/notxdetails/{hashes[1]}.hex")
+    assert body.decode() == c.getblock(hashes[1], 0)
+    code, _, body = node.rest(f"/rest/headers/2/{hashes[0]}.json")
+    assert [h["hash"] for h in json.loads(body)] == hashes[:2]
+    assert node.rest(f"/rest/headers/0/{hashes[0]}.json")[0] == 400
+    txid = c.sendrawtransaction(_tx(c, addr, "44" * 32))
+    code, _, body = node.rest(f"/rest/tx/{txid}.json")
+    assert code == 200 and json.loads(body)["txid"] == txid
+    assert node.rest(f"/rest/tx/{txid}.hex")[2].decode() == c.getrawtransaction(txid)
+    assert node.rest(f"/rest/tx/{'55' * 32}.json")[0] == 404
