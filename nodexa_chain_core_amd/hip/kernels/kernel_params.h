@@ -135,3 +135,14 @@ struct KawpowHashParams {
     uint32_t pad;
     struct FastMod32 items;
 };
+
+// Batch SHA-256d (sha256d.hip). sha256d_batch: n messages of len bytes, stride bytes apart.
+// sha256d_merkle_level: n output nodes from len 32-byte input nodes (stride unused).
+struct Sha256dParams {
+    const uint8_t* in;
+    uint8_t* out;      // n x 32 bytes
+    uint32_t len;
+    uint32_t stride;
+    uint32_t n;
+    uint32_t pad;
+};

@@ -1,0 +1,134 @@
+// Batch SHA-256d on gfx950 ("CPU + HIP device SHA256d for batch header hashing").
+//
+// sha256d_batch: one lane per fixed-length message (block headers: 80-byte KawPow inputs,
+// 1459-byte Equihash-extended headers), digest = SHA256(SHA256(msg)) in the byte order of
+// the reference's CHash256 / SerializeHash (src/hash.h:49,274).
+// sha256d_merkle_level: one level of ComputeMerkleRoot (src/consensus/merkle.cpp): out[i] =
+// SHA256d(in[2i] || in[2i+1]), the last node paired with itself on odd levels.
+// Both are integer-ALU kernels (64 rounds of 32-bit rotates/adds per 64-byte block) with
+// the message schedule in a 16-word register ring; SHA-256 has no MFMA shape.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernel_params.h"
+
+__constant__ uint32_t SHA256_K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u
+};
+
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+__device__ __forceinline__ void sha256_init(uint32_t s[8]) {
+    const uint32_t h0[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au, 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = h0[i];
+}
+
+__device__ __forceinline__ void sha256_compress(uint32_t s[8], uint32_t w[16]) {
+    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = w[i];
+        } else {
+            const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+            const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+            const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+            wi = w[i & 15] = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+        }
+        const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+        const uint32_t ch = (e & f) ^ (~e & g);
+        const uint32_t t1 = h + S1 + ch + SHA256_K[i] + wi;
+        const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+        const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+    s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+}
+
+// SHA-256 of len bytes at m (any alignment), padding generated on the fly.
+__device__ void sha256_bytes(const uint8_t* m, uint32_t len, uint32_t s[8]) {
+    sha256_init(s);
+    const uint32_t nblocks = (len + 9 + 63) / 64;
+    for (uint32_t b = 0; b < nblocks; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t idx = b * 64 + uint32_t(j) * 4 + uint32_t(k);
+                const uint32_t byte = idx < len ? m[idx] : (idx == len ? 0x80u : 0u);
+                word = (word << 8) | byte;
+            }
+            w[j] = word;
+        }
+        if (b == nblocks - 1) {
+            w[14] = len >> 29;
+            w[15] = len << 3;
+        }
+        sha256_compress(s, w);
+    }
+}
+
+// Second pass of SHA256d: SHA-256 of the 32-byte digest held as 8 big-endian words.
+__device__ __forceinline__ void sha256_of_digest(const uint32_t d[8], uint32_t s[8]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = d[i];
+    w[8] = 0x80000000u;
+#pragma unroll
+    for (int i = 9; i < 15; ++i) w[i] = 0;
+    w[15] = 256;
+    sha256_init(s);
+    sha256_compress(s, w);
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* o, const uint32_t s[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        o[4 * i + 0] = uint8_t(s[i] >> 24);
+        o[4 * i + 1] = uint8_t(s[i] >> 16);
+        o[4 * i + 2] = uint8_t(s[i] >> 8);
+        o[4 * i + 3] = uint8_t(s[i]);
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void sha256d_batch(Sha256dParams p) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    uint32_t s1[8], s2[8];
+    sha256_bytes(p.in + size_t(i) * p.stride, p.len, s1);
+    sha256_of_digest(s1, s2);
+    store_digest(p.out + size_t(i) * 32, s2);
+}
+
+extern "C" __global__ __launch_bounds__(256) void sha256d_merkle_level(Sha256dParams p) {
+    // p.n = output nodes, p.len = input nodes (32 bytes each)
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    const uint32_t l = 2 * i, r = (2 * i + 1 < p.len) ? 2 * i + 1 : 2 * i;
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint8_t* a = p.in + size_t(l) * 32 + 4 * j;
+        const uint8_t* b = p.in + size_t(r) * 32 + 4 * j;
+        w[j] = (uint32_t(a[0]) << 24) | (uint32_t(a[1]) << 16) | (uint32_t(a[2]) << 8) | a[3];
+        w[8 + j] = (uint32_t(b[0]) << 24) | (uint32_t(b[1]) << 16) | (uint32_t(b[2]) << 8) | b[3];
+    }
+    uint32_t s1[8], s2[8];
+    sha256_init(s1);
+    sha256_compress(s1, w);
+    uint32_t pad[16] = {0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512};
+    sha256_compress(s1, pad);
+    sha256_of_digest(s1, s2);
+    store_digest(p.out + size_t(i) * 32, s2);
+}

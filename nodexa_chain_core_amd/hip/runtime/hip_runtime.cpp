@@ -309,6 +309,21 @@ PYBIND11_MODULE(_hip, m) {
     m.attr("EQ_MAX_SOL") = EQ_MAX_SOL;
     m.attr("EQ_MAX_BANKS") = EQ_MAX_BANKS;
     m.attr("EQ_SOL_WORDS") = EQ_SOL_WORDS;
+    // Batch SHA-256d (sha256d.hip): messages of `len` bytes at `stride`, or (merkle=true) one
+    // ComputeMerkleRoot level of `len` 32-byte nodes into (len + 1) / 2 nodes.
+    m.def("launch_sha256d", [](const Kernel& k, uintptr_t in, uint32_t len, uint32_t stride, uint32_t n, uintptr_t out,
+                               bool merkle, uintptr_t stream) {
+        if (n == 0) return;
+        if (merkle ? (n != (len + 1) / 2) : (len > stride || len > (1u << 24)))
+            throw std::invalid_argument("bad sha256d geometry");
+        Sha256dParams p{};
+        p.in = reinterpret_cast<const uint8_t*>(in);
+        p.out = reinterpret_cast<uint8_t*>(out);
+        p.len = len;
+        p.stride = stride;
+        p.n = n;
+        k.launch_bytes(dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("launch_equihash_verify", [](const Kernel& k, std::vector<uint64_t> h0, uintptr_t msgs, uint32_t input_len,
                                        uint32_t num, uintptr_t sols, uintptr_t out, uintptr_t stream) {
         if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");

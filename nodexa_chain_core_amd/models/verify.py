@@ -133,8 +133,8 @@ def _verify_x16r(params, headers, idxs: list[int], out: list[dict], threads: int
 
 
 def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, threads: int) -> None:
-    """Equihash-extension headers: solution validity (GPU batch kernel when GPUs are given,
-    else the C++ verifier on all cores) and SHA256d(header) <= nBits."""
+    """Equihash-extension headers: solution validity and SHA256d(header) <= nBits — on the GPU
+    (eq_verify + sha256d_batch) when GPUs are given, else the C++ verifier on all cores."""
     act = params.kawpow_activation_time
     ok: dict[int, bool]
     if gpus:
@@ -154,9 +154,16 @@ def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, th
 
         with cf.ThreadPoolExecutor(max_workers=threads or (os.cpu_count() or 4)) as ex:
             ok = dict(zip(idxs, ex.map(one, idxs)))
+    hashes = {}
+    if gpus:  # block hash = SHA256d(serialized header) on the device (ops/sha256.py)
+        from ..ops.sha256 import sha256d_batch
+
+        ser = [headers[i].serialize(act) for i in idxs]
+        if len({len(x) for x in ser}) == 1:
+            hashes = dict(zip(idxs, (r.tobytes() for r in sha256d_batch(ser, device=gpus[0]))))
     for i in idxs:
         h = headers[i]
-        hsh = h.equihash_hash(act)
+        hsh = hashes.get(i) or h.equihash_hash(act)
         if not ok[i]:
             out[i] = {"valid": False, "reason": "invalid-solution", "hash": _core.u256_hex(hsh)}
         elif not _core.check_proof_of_work(hsh, h.bits, params):
