@@ -48,7 +48,7 @@ def _rows_le(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     return ~diff.any(axis=1) | (a[r, first] < b[r, first])
 
 
-def _verify_native(params, headers, gpus, threads: int, mode: str) -> list[dict]:
+def _verify_native(params, headers, gpus, threads: int, mode: str, rows_fn=None) -> list[dict]:
     """verify_headers for C++ BlockHeader batches: job records, boundaries and the
     mix-only prefilter come from one native pass (kawpow_batch_prepare), the GPU result
     rows are checked with numpy, so host time per header stays ~1-2 us."""
@@ -64,7 +64,10 @@ def _verify_native(params, headers, gpus, threads: int, mode: str) -> list[dict]
     t1 = t2 = time.perf_counter()
     if len(cand):
         jobs = np.frombuffer(jobs_b, dtype=np.uint8).reshape(n, 48)[cand]
-        res = _gpu_rows(jobs, gpus, mode) if gpus else _cpu_rows(jobs, threads)
+        if rows_fn is not None:
+            res = rows_fn(jobs)
+        else:
+            res = _gpu_rows(jobs, gpus, mode) if gpus else _cpu_rows(jobs, threads)
         t2 = time.perf_counter()
         mix_ok = (res[:, :32] == np.frombuffer(mix_b, dtype=np.uint8).reshape(n, 32)[cand]).all(axis=1)
         fin = np.ascontiguousarray(res[:, 32:])
@@ -172,14 +175,17 @@ def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, th
             out[i] = {"valid": True, "hash": _core.u256_hex(hsh)}
 
 
-def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None = None, mode: str = "auto") -> dict:
+def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None = None, mode: str = "auto",
+                    verify_fn=None) -> dict:
     """ProcessNewBlockHeaders for a batch (src/validation.cpp:12017-12035): PoW of the whole
     batch in bulk (GPU or all cores), then the contextual rules — nBits == DarkGravityWave,
     MTP, future time, version — header by header on the host chain. Like the reference it
-    stops at the first invalid header. Returns counts, the first rejection and stage times."""
+    stops at the first invalid header. Returns counts, the first rejection and stage times.
+    verify_fn(params, headers) replaces the PoW stage (parallel/verify.py: across ranks)."""
 
     t0 = time.perf_counter()
-    pow_res = verify_headers(chain.params, headers, gpus=gpus, mode=mode)
+    pow_res = verify_fn(chain.params, headers) if verify_fn is not None else \
+        verify_headers(chain.params, headers, gpus=gpus, mode=mode)
     t1 = time.perf_counter()
     first_bad = next((i for i, r in enumerate(pow_res) if not r["valid"]), len(headers))
     accepted, reject = 0, None

@@ -10,7 +10,9 @@ The reference path (CheckBlockHeader -> GetHashFull, light epoch context, one
 header at a time under cs_main) is timed on a sample on one host core.
 
     python tools/verify_bench.py [--gpus N] [--modes light dag] [--cpu-sample 40]
-Prints one JSON line per measured path.
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/verify_bench.py --modes dag
+Prints one JSON line per measured path (the torchrun form splits the full-hash work over
+ranks and all-gathers the rows over RCCL: parallel/verify.py).
 """
 from __future__ import annotations
 
@@ -60,7 +62,8 @@ def main() -> int:
     dt = time.perf_counter() - t
     ref = dict(base, path="reference-equivalent serial CPU (1 core, light KawPow + DGW)",
                headers_timed=a.cpu_sample, headers_per_s=round(a.cpu_sample / dt, 2), ms_per_header=round(dt / a.cpu_sample * 1e3, 3))
-    print(json.dumps(ref), flush=True)
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps(ref), flush=True)
 
     if a.cpu_threads:
         chain = _core.HeaderChain(params)
@@ -69,6 +72,9 @@ def main() -> int:
         print(json.dumps(dict(base, path=f"all host cores ({os.cpu_count()})", accepted=r["accepted"],
                               reject=r["reject"], pow_s=round(r["pow_s"], 3), context_s=round(r["context_s"], 3),
                               headers_per_s=round(n / tot, 1))), flush=True)
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # torchrun: one process per GPU, rows all-gathered over RCCL
+        return _distributed(a, params, headers, adjusted, base, ref)
 
     if a.gpus > 0:
         import torch
@@ -100,6 +106,40 @@ def main() -> int:
             if r["accepted"] != n:
                 return 1
     return 0
+
+
+def _distributed(a, params, headers, adjusted, base, ref) -> int:
+    import functools
+
+    import torch
+
+    from nodexa_chain_core_amd import _core
+    from nodexa_chain_core_amd.models.verify import LAST_TIMING, process_headers
+    from nodexa_chain_core_amd.parallel import world as W
+    from nodexa_chain_core_amd.parallel.verify import verify_headers_distributed
+
+    w = W.init()
+    n = len(headers)
+    rc = 0
+    for mode in a.modes:
+        fn = functools.partial(verify_headers_distributed, mode=mode)
+        process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn)  # warm: every epoch + code objects
+        W.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn)
+        torch.cuda.synchronize()
+        W.barrier()
+        dt = W.all_reduce_max(time.perf_counter() - t0)
+        if w.is_main:
+            print(json.dumps(dict(base, path=f"GPU {mode} over {w.world_size} ranks (RCCL all-gather)",
+                                  accepted=r["accepted"], reject=r["reject"], pow_s=round(r["pow_s"], 4),
+                                  context_s=round(r["context_s"], 4), headers_per_s=round(n / dt, 1),
+                                  vs_reference_serial=round(n / dt / ref["headers_per_s"], 1),
+                                  pow_stages_ms={k: round(v * 1e3, 2) for k, v in LAST_TIMING.items()})), flush=True)
+        rc |= int(r["accepted"] != n)
+    W.shutdown()
+    return rc
 
 
 if __name__ == "__main__":
