@@ -52,6 +52,8 @@ class ValidationInterface:
 
     def block_found(self, block_hash: bytes) -> None: ...
 
+    def transaction_added_to_mempool(self, tx) -> None: ...
+
 
 def make_params(network: str, kawpow_activation_time: int | None = None,
                 equihash_activation_time: int | None = None):
@@ -258,9 +260,12 @@ class ChainState:
     def add_to_mempool(self, tx, fee: int, entry_time: float | None = None, fee_delta: int = 0) -> bytes:
         txid = tx.txid()
         with self.lock:
+            new = txid not in self.mempool
             self.mempool[txid] = MempoolEntry(tx, int(fee) + int(fee_delta), entry_time or time.time(),
                                               self.chain.height(), int(fee_delta), len(tx.serialize(True)))
             self.transactions_updated += 1
+        if new:
+            self._emit("transaction_added_to_mempool", tx)  # TransactionAddedToMempool: P2P relay, ZMQ
         return txid
 
     def clear_mempool(self) -> int:

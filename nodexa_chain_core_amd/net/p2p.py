@@ -41,6 +41,8 @@ class Peer:
         self.send_headers = False
         self.misbehavior = 0
         self.bytes_sent = self.bytes_recv = 0
+        self.known_txs: set[bytes] = set()  # filterInventoryKnown
+        self.fee_filter = 0
         self.connected_at = time.time()
         self.last_recv = self.last_send = 0.0
         self._send_lock = threading.Lock()
@@ -94,6 +96,10 @@ class Peer:
         finally:
             self.close()
             self.mgr.remove(self)
+
+    @property
+    def relay_txs(self) -> bool:
+        return bool(self.info.get("relay", True))
 
     def as_dict(self) -> dict:
         host, port = self.addr[:2]
@@ -241,6 +247,17 @@ class ConnectionManager:
             except OSError:
                 p.close()
 
+    def announce_tx(self, txid: bytes, skip: "Peer | None" = None) -> None:
+        """RelayTransaction: `inv` MSG_TX to every peer that has not sent us this tx."""
+        for p in list(self.peers):
+            if p is skip or not p.verack or not p.relay_txs or txid in p.known_txs:
+                continue
+            p.known_txs.add(txid)
+            try:
+                p.send("inv", P.inv_payload([(P.MSG_TX, txid)]))
+            except OSError:
+                p.close()
+
     # ---------------------------------------------------------------- message handling
     def handle(self, peer: Peer, cmd: str, p: bytes) -> None:
         fn = getattr(self, "on_" + cmd, None)
@@ -330,8 +347,39 @@ class ConnectionManager:
 
     def on_inv(self, peer: Peer, p: bytes) -> None:
         items = P.parse_inv(p)
+        if len(items) > P.MAX_INV_SZ:
+            peer.misbehaving(20, "oversized inv")
+            return
         if any(t & ~P.MSG_WITNESS_FLAG == P.MSG_BLOCK and self.state.chain.find(h) is None for t, h in items):
             self.request_headers(peer)
+        want = []
+        for t, h in items:
+            if t & ~P.MSG_WITNESS_FLAG == P.MSG_TX:
+                peer.known_txs.add(h)
+                if h not in self.state.mempool:
+                    want.append((P.MSG_TX | P.MSG_WITNESS_FLAG, h))
+        if want:
+            peer.send("getdata", P.inv_payload(want))
+
+    def on_tx(self, peer: Peer, p: bytes) -> None:
+        """AcceptToMemoryPool for a relayed tx (context-free checks; no UTXO set), then relay."""
+        tx = _core.Transaction.deserialize(p)
+        txid = tx.txid()
+        peer.known_txs.add(txid)
+        REGISTRY.inc("p2p_tx_received_total", 1)
+        if txid in self.state.mempool or tx.is_coinbase() or not tx.vin or not tx.vout:
+            return
+        self.state.add_to_mempool(tx, 0)  # the mempool signal relays it to the other peers
+
+    def on_mempool(self, peer: Peer, p: bytes) -> None:
+        """BIP35: inv of every pool txid (in MAX_INV_SZ chunks)."""
+        ids = list(self.state.mempool)
+        peer.known_txs.update(ids)
+        for k in range(0, len(ids), P.MAX_INV_SZ):
+            peer.send("inv", P.inv_payload([(P.MSG_TX, h) for h in ids[k:k + P.MAX_INV_SZ]]))
+
+    def on_feefilter(self, peer: Peer, p: bytes) -> None:
+        (peer.fee_filter,) = struct.unpack_from("<q", p, 0)
 
     def on_getdata(self, peer: Peer, p: bytes) -> None:
         missing = []
@@ -342,6 +390,8 @@ class ConnectionManager:
                     missing.append((t, h))
                 else:
                     peer.send("block", raw)
+            elif t & ~P.MSG_WITNESS_FLAG == P.MSG_TX and h in self.state.mempool:
+                peer.send("tx", self.state.mempool[h].tx.serialize(bool(t & P.MSG_WITNESS_FLAG)))
             else:
                 missing.append((t, h))
         if missing:

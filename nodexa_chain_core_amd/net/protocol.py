@@ -30,6 +30,7 @@ NODE_WITNESS = 1 << 3
 MAX_HEADERS_RESULTS = 2000
 MAX_MESSAGE_SIZE = 32 * 1024 * 1024  # MAX_PROTOCOL_MESSAGE_LENGTH after the HIP2 block-size change
 MSG_TX, MSG_BLOCK = 1, 2
+MAX_INV_SZ = 50000  # src/net_processing.h
 MSG_WITNESS_FLAG = 1 << 30
 HEADER_SIZE = 24
 USER_AGENT = "/nodexa-mi355x:0.1.0/"

@@ -178,6 +178,12 @@ class ZmqNotifier:
                 self.pubs["rawtx"].publish("rawtx", tx.serialize(True))
 
     # the other ValidationInterface hooks are not used
+    def transaction_added_to_mempool(self, tx) -> None:  # CZMQNotificationInterface::TransactionAddedToMempool
+        if "hashtx" in self.pubs:
+            self.pubs["hashtx"].publish("hashtx", bytes(tx.txid())[::-1])
+        if "rawtx" in self.pubs:
+            self.pubs["rawtx"].publish("rawtx", tx.serialize(True))
+
     def updated_block_tip(self, *a) -> None: ...
 
     def block_checked(self, *a) -> None: ...

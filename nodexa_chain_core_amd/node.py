@@ -153,6 +153,9 @@ class Node:
         cm = self.connman
 
         class _Relay(ValidationInterface):
+            def transaction_added_to_mempool(self, tx) -> None:
+                cm.announce_tx(tx.txid())
+
             def updated_block_tip(self, tip, fork, initial_download: bool) -> None:
                 cm.announce_block(tip.header)
 

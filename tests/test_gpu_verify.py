@@ -95,3 +95,23 @@ def test_synthetic_chain_gpu_mixed(core, gpu):
         r = chain.accept_header(h, h.time + 7200, True)
         assert r.ok, r.reject
     assert sum(1 for h in headers if h.is_equihash()) == 8
+
+
+def test_distributed_verify_single_rank_gpu():
+    """parallel/verify.py on the GPU with one rank: same rows as the single-process path."""
+    import os
+
+    from nodexa_chain_core_amd.models import synthetic
+    from nodexa_chain_core_amd.models.verify import verify_headers
+    from nodexa_chain_core_amd.parallel import world as W
+    from nodexa_chain_core_amd.parallel.verify import verify_headers_distributed
+
+    params, headers = synthetic.load(os.path.join(os.path.dirname(__file__), "data", "testnet_mixed_10k.hdr"))
+    batch = headers[:300] + headers[-50:]
+    W.init()
+    try:
+        got = verify_headers_distributed(params, batch, mode="light")
+    finally:
+        W.shutdown()
+    assert got == verify_headers(params, batch, gpus=[0], mode="light")
+    assert all(r["valid"] for r in got)

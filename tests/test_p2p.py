@@ -166,3 +166,35 @@ def test_zmq_hashblock_rawblock(core, tmp_path):
         sock.close()
     finally:
         a.stop()
+
+
+def test_tx_relay_and_mempool_message(core, tmp_path):
+    """inv(MSG_TX) -> getdata -> tx -> mempool on the peer -> relayed on; BIP35 `mempool`
+    (src/net_processing.cpp RelayTransaction / ProcessGetData / NetMsgType::MEMPOOL)."""
+    a = _node(core, tmp_path, "a", ["-listen", "-port=0"])
+    b = c = None
+    try:
+        b = _node(core, tmp_path, "b", ["-listen", "-port=0", f"-connect=127.0.0.1:{a.connman.port}"])
+        assert _wait(lambda: a.peer_count() == 1 and b.peer_count() == 1)
+        tx = core.Transaction()
+        i, o, op = core.TxIn(), core.TxOut(), core.OutPoint()
+        op.hash, op.n = bytes([7]) * 32, 0
+        i.prevout = op
+        o.value, o.script_pubkey = 5000, b"\x51"
+        tx.vin, tx.vout = [i], [o]
+        txid = a.table.execute("sendrawtransaction", [tx.serialize(True).hex()])
+        h = core.u256_from_hex(txid)
+        assert _wait(lambda: h in b.state.mempool)
+        # a third node joining b asks for its mempool and gets the tx too
+        c = _node(core, tmp_path, "c", [f"-connect=127.0.0.1:{b.connman.port}"])
+        assert _wait(lambda: c.peer_count() == 1)
+        c.connman.peers[0].send("mempool")
+        assert _wait(lambda: h in c.state.mempool)
+        # mined on a: removed from a's pool; b learns the block and drops it too
+        a.miner.generate(a.mining_script, 1)
+        assert h not in a.state.mempool
+        assert _wait(lambda: b.state.height() == 1 and h not in b.state.mempool)
+    finally:
+        for n in (c, b, a):
+            if n is not None:
+                n.stop()
