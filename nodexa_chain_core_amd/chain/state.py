@@ -24,6 +24,7 @@ from dataclasses import dataclass, field
 from .. import core
 from ..utils import log, sync
 from .blockindex import BlockIndexLog, scan_blk_tail
+from .versionbits import VersionBits
 
 _core = core()
 
@@ -119,6 +120,7 @@ class ChainState:
         self.ntx: dict[bytes, int] = {}      # transactions per stored block (CBlockIndex::nTx)
         self.fee_stats: list[tuple[float, int]] = []  # (sat/vB, blocks to confirm) of mined pool txs
         self.mocktime = 0                     # setmocktime (0 = wall clock)
+        self.block_version_override: int | None = None  # -blockversion (regtest only)
         self.transactions_updated = 0
         self.datadir = datadir
         self.store = None
@@ -131,6 +133,7 @@ class ChainState:
             self.index_log = BlockIndexLog(os.path.join(bdir, "index.log"))
             if reindex or not self._load_index(bdir):
                 self._load_block_files()
+        self.versionbits = VersionBits(self.chain, params.network_id)
         gh = self.chain.genesis().hash
         self.ntx[gh] = len(params.genesis.vtx)
         if self.store is not None and gh not in self.block_pos:

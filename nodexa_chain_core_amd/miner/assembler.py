@@ -4,8 +4,9 @@ Parity: CreateNewBlock (src/miner.cpp:123-256): coinbase vout[0] = fees +
 (100-pct)% of the subsidy to the miner script, vout[1] = subsidy*pct/100 to
 the community-autonomous address, scriptSig = <height> OP_0, witness
 commitment output (GenerateCoinbaseCommitment, src/validation.cpp:11779-11806)
-with the 32-byte witness nonce; header: version = 0x30000000 (assets
-deployed), time = max(MTP+1, now), bits = GetNextWorkRequired, nNonce = 0,
+with the 32-byte witness nonce; header: version = ComputeBlockVersion
+(0x30000000 top bits | the bits of STARTED / LOCKED_IN deployments, chain/versionbits.py;
+-blockversion overrides it on regtest), time = max(MTP+1, now), bits = GetNextWorkRequired, nNonce = 0,
 nNonce64 = 0, nHeight = tip+1. IncrementExtraNonce (src/miner.cpp:508-525):
 scriptSig = <height> <extranonce>, merkle root recomputed.
 
@@ -78,7 +79,8 @@ class BlockAssembler:
             blk.vtx = [cb] + txs
             commitment = self._add_witness_commitment(blk)
             hdr = _core.BlockHeader()
-            hdr.version = BLOCK_VERSION_ASSETS
+            hdr.version = st.block_version_override if st.block_version_override is not None else \
+                st.versionbits.block_version(prev)  # ComputeBlockVersion (BIP9 signalling)
             hdr.prev = prev.hash
             t = int(time.time()) if now is None else int(now)
             hdr.time = max(prev.median_time_past() + 1, t)

@@ -97,6 +97,8 @@ class Node:
             sync.enable(True)
         self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False),
                                 reindex=a.get_bool("reindex", False))
+        if self.network == "regtest" and a.is_set("blockversion"):  # -blockversion (src/miner.cpp:146-149)
+            self.state.block_version_override = a.get_int("blockversion", 0)
         if self.datadir is not None and a.get_bool("persistmempool", True):  # -persistmempool (LoadMempool)
             n = self.state.load_mempool(os.path.join(self.datadir, "mempool.dat"))
             if n:

@@ -218,6 +218,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
                 "mediantime": tip.median_time_past(), "verificationprogress": 1.0,
                 "chainwork": "%064x" % tip.chain_work, "size_on_disk": node.blocks_size_on_disk(),
                 "pruned": False, "warnings": "",
+                "bip9_softforks": st.versionbits.bip9_softforks(tip),
                 "kawpow_activation_time": params.kawpow_activation_time,
                 "equihash_activation_time": params.equihash_activation_time}
 
@@ -321,9 +322,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         res = {
             "capabilities": ["proposal"],
             "version": hdr.version,
-            "rules": ["csv", "segwit"],
-            "vbavailable": {},
-            "vbrequired": 0,
+            **st.versionbits.gbt_fields(st.tip()),
             "previousblockhash": _hex(hdr.prev),
             "transactions": txs,
             "coinbaseaux": {"flags": ""},

@@ -152,3 +152,26 @@ def test_rest_block_tx_headers(core, node_factory):  # noqa: F811
     assert code == 200 and json.loads(body)["txid"] == txid
     assert node.rest(f"/rest/tx/{txid}.hex")[2].decode() == c.getrawtransaction(txid)
     assert node.rest(f"/rest/tx/{'55' * 32}.json")[0] == 404
+
+
+def test_bip9_versionbits_regtest(core, node_factory):  # noqa: F811
+    """BIP9 on regtest (window 144 / threshold 108; transfer_script 288 / 208; coinbase 500 / 400):
+    deployments start after the first period, lock in after a signalling period and activate one
+    period later (feature_versionbits / rpc_blockchain bip9_softforks in the reference)."""
+    node, addr = node_factory()
+    c = client(node)
+    c.generatetoaddress(433, addr)
+    forks = c.getblockchaininfo()["bip9_softforks"]
+    assert forks["assets"]["status"] == "active" and forks["assets"]["since"] == 432
+    assert forks["testdummy"]["status"] == "active"
+    ts = forks["transfer_script"]
+    assert ts["status"] == "started" and ts["since"] == 288 and ts["bit"] == 8
+    assert ts["statistics"]["period"] == 288 and ts["statistics"]["elapsed"] == 433 - 287
+    assert ts["statistics"]["count"] == ts["statistics"]["elapsed"] and ts["statistics"]["possible"]
+    assert forks["coinbase"]["status"] == "defined"
+    blk = c.getblock(c.getblockhash(200))
+    assert blk["version"] & 0xE0000000 == 0x20000000 and blk["version"] & (1 << 6)  # signalled assets
+    tpl = c.getblocktemplate()
+    assert set(tpl["rules"]) == {"testdummy", "assets", "messaging_restricted", "enforce_value"}
+    assert tpl["vbavailable"] == {"transfer_script": 8} and tpl["vbrequired"] == 0
+    assert tpl["version"] == 0x30000000 | (1 << 8)
