@@ -54,6 +54,7 @@
 //   KP_DPP        rounds unrolled by 16; item index broadcast by DPP row_newbcast
 //   KP_BARRETT    5-op Barrett modulo for the item index
 //   KP_BUFFER     raw-buffer DAG loads with a 32-bit offset (DAG < 4 GiB only)
+//   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride): any DAG size
 //   KP_L1X4       L1 replicated 4x in LDS (64 KiB) so an L1 address is one
 //                 16-bit shift: ((x << 2) & 0xffff) reads l1[x % 4096]
 #ifndef KP_BLOCK
@@ -128,7 +129,35 @@ NX_DEV uint32_t kp_fastmod(uint32_t x, const FastMod32& f) {
 // DAG item access. KP_BUFFER addresses the (< 4 GiB) DAG through a raw buffer
 // resource with a 32-bit byte offset (one v_lshl_add) instead of 64-bit
 // pointer arithmetic.
-#ifdef KP_BUFFER
+#if defined(KP_SBUFFER)
+// Structured-buffer addressing: vindex = item, stride 256 B in the V#, voffset = the lane's
+// 16-byte slice. One buffer_load_dwordx4 idxen offen per round with no address VALU, and the
+// item index is 32-bit, so this covers DAGs of any epoch (> 4 GiB included). clang has no
+// struct-buffer builtin, so the LLVM intrinsic is bound by name (the compiler still tracks
+// its vmcnt like any other load).
+typedef int32_t kp_i32x4 __attribute__((ext_vector_type(4)));
+__device__ kp_i32x4 kp_struct_load(kp_i32x4 rsrc, int vindex, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.struct.buffer.load.v4i32");
+typedef kp_i32x4 kp_dag_t;
+NX_DEV kp_dag_t kp_dag_handle(const void* dag) {
+    const uint64_t base = (uint64_t)dag;
+    kp_i32x4 r;
+    r.x = (int32_t)(uint32_t)base;
+    r.y = (int32_t)(((uint32_t)(base >> 32) & 0xffffu) | (256u << 16));  // stride 256 B
+    r.z = -1;                                                             // num_records: no clamp
+    r.w = 0x00020000;                                                     // DATA_FORMAT 32 (as KP_BUFFER)
+    return r;
+}
+NX_DEV uint4 kp_dag_item(kp_dag_t dag, uint32_t index, uint32_t part) {
+#ifdef KP_NT_DAG
+    const int aux = 2;
+#else
+    const int aux = 0;
+#endif
+    const kp_i32x4 v = kp_struct_load(dag, (int)index, (int)(part << 4), 0, aux);
+    return make_uint4((uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w);
+}
+#elif defined(KP_BUFFER)
 typedef __amdgpu_buffer_rsrc_t kp_dag_t;
 NX_DEV kp_dag_t kp_dag_handle(const void* dag) {
     // num_records 0xffffffff: no range clamp; the host only selects KP_BUFFER for DAGs < 4 GiB

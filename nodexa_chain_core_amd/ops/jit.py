@@ -90,10 +90,11 @@ DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
 
 def defines_for(dag_bytes: int, defines: tuple[str, ...] | None = None) -> tuple[str, ...]:
     """The variant to compile for a DAG of `dag_bytes`: KP_BUFFER addresses the DAG with a
-    32-bit byte offset, so it is dropped for DAGs of 4 GiB or more (epochs >= ~385)."""
+    32-bit byte offset, so DAGs of 4 GiB or more (epochs >= 385) switch to KP_SBUFFER
+    (item-indexed structured-buffer loads)."""
     d = DEFAULT_DEFINES if defines is None else tuple(defines)
-    if dag_bytes >= 1 << 32:
-        d = tuple(x for x in d if x != "KP_BUFFER")
+    if dag_bytes >= 1 << 32 and "KP_BUFFER" in d:  # the structured-buffer form has no 4 GiB limit
+        d = tuple("KP_SBUFFER" if x == "KP_BUFFER" else x for x in d)
     return d
 
 
