@@ -54,7 +54,7 @@
 //   KP_DPP        rounds unrolled by 16; item index broadcast by DPP row_newbcast
 //   KP_BARRETT    5-op Barrett modulo for the item index
 //   KP_BUFFER     raw-buffer DAG loads with a 32-bit offset (DAG < 4 GiB only)
-//   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride): any DAG size
+//   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride), DAG < 4 GiB only
 //   KP_L1X4       L1 replicated 4x in LDS (64 KiB) so an L1 address is one
 //                 16-bit shift: ((x << 2) & 0xffff) reads l1[x % 4096]
 #ifndef KP_BLOCK
@@ -131,10 +131,11 @@ NX_DEV uint32_t kp_fastmod(uint32_t x, const FastMod32& f) {
 // pointer arithmetic.
 #if defined(KP_SBUFFER)
 // Structured-buffer addressing: vindex = item, stride 256 B in the V#, voffset = the lane's
-// 16-byte slice. One buffer_load_dwordx4 idxen offen per round with no address VALU, and the
-// item index is 32-bit, so this covers DAGs of any epoch (> 4 GiB included). clang has no
-// struct-buffer builtin, so the LLVM intrinsic is bound by name (the compiler still tracks
-// its vmcnt like any other load).
+// 16-byte slice: one buffer_load_dwordx4 idxen offen per round and no address VALU at all
+// (KP_BUFFER still needs one v_lshl_add): +1.1 % at epoch 384 (profiles/r1s_kawpow). The
+// hardware forms index*stride+offset in 32 bits, so like KP_BUFFER it is for DAGs < 4 GiB
+// (measured: not bit-exact at epoch 390). clang has no struct-buffer builtin, so the LLVM
+// intrinsic is bound by name (the compiler still tracks its vmcnt like any other load).
 typedef int32_t kp_i32x4 __attribute__((ext_vector_type(4)));
 __device__ kp_i32x4 kp_struct_load(kp_i32x4 rsrc, int vindex, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.struct.buffer.load.v4i32");

@@ -82,19 +82,19 @@ def _atomic_copy(src: str, dst: str) -> None:
 
 # Tuned variant of the search template (profiles/README.md has the sweep that
 # picked it); NODEXA_KAWPOW_DEFINES="A,B=1" overrides it ("none" = plain template).
-TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_BUFFER", "KP_L1X4", "KP_BLOCK=512")
+TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_SBUFFER", "KP_L1X4", "KP_BLOCK=512")
 _env = os.environ.get("NODEXA_KAWPOW_DEFINES")
 DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
     d for d in _env.split(",") if d and d != "none")
 
 
 def defines_for(dag_bytes: int, defines: tuple[str, ...] | None = None) -> tuple[str, ...]:
-    """The variant to compile for a DAG of `dag_bytes`: KP_BUFFER addresses the DAG with a
-    32-bit byte offset, so DAGs of 4 GiB or more (epochs >= 385) switch to KP_SBUFFER
-    (item-indexed structured-buffer loads)."""
+    """The variant to compile for a DAG of `dag_bytes`: KP_SBUFFER / KP_BUFFER address the DAG
+    with 32-bit buffer offsets, so they are dropped for DAGs of 4 GiB or more (epochs >= 385;
+    measured there: the structured form is not bit-exact, the pointer form is)."""
     d = DEFAULT_DEFINES if defines is None else tuple(defines)
-    if dag_bytes >= 1 << 32 and "KP_BUFFER" in d:  # the structured-buffer form has no 4 GiB limit
-        d = tuple("KP_SBUFFER" if x == "KP_BUFFER" else x for x in d)
+    if dag_bytes >= 1 << 32:  # 32-bit buffer offsets: 64-bit pointers for DAGs of 4 GiB or more
+        d = tuple(x for x in d if x not in ("KP_BUFFER", "KP_SBUFFER"))
     return d
 
 
