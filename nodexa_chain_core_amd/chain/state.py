@@ -251,6 +251,15 @@ class ChainState:
     def adjusted_time(self) -> int:
         return int(self.mocktime or time.time())
 
+    def arm_reorg_guard(self, peer_count: int) -> bool:
+        """-maxreorg / -minreorgpeers / -minreorgage (ContextualCheckBlockHeader,
+        src/validation.cpp:11815-11827): forks deeper than max_reorg_depth are rejected while the
+        node has enough peers and its tip is recent. Re-armed before every P2P batch."""
+        p = self.params
+        armed = peer_count >= p.min_reorg_peers and (time.time() - self.tip().time) <= p.min_reorg_age
+        self.chain.max_reorg_depth = p.max_reorg_depth if armed else 0
+        return armed
+
     def chain_tx_count(self, idx) -> int:
         """CBlockIndex::nChainTx: transactions in the chain up to and including idx."""
         n = 0

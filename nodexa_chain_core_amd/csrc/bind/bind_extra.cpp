@@ -362,6 +362,8 @@ void bind_extra(py::module_& m) {
         .def_readwrite("x16rv2_activation_time", &ChainParams::x16rv2_activation_time)
         .def_readwrite("equihash_activation_time", &ChainParams::equihash_activation_time)
         .def_readwrite("max_reorg_depth", &ChainParams::max_reorg_depth)
+        .def_readwrite("min_reorg_peers", &ChainParams::min_reorg_peers)
+        .def_readwrite("min_reorg_age", &ChainParams::min_reorg_age)
         .def_readonly("mine_blocks_on_demand", &ChainParams::mine_blocks_on_demand)
         .def_readonly("mining_requires_peers", &ChainParams::mining_requires_peers);
     m.def("make_chain_params", &make_chain_params);
@@ -392,6 +394,7 @@ void bind_extra(py::module_& m) {
         .def_property_readonly("params", &HeaderChain::params, py::return_value_policy::reference_internal)
         .def("set_kawpow_activation_time", [](HeaderChain& c, u32 t) { c.mutable_params().kawpow_activation_time = t; })
         .def_readwrite("strict_kawpow_height", &HeaderChain::strict_kawpow_height)
+        .def_readwrite("max_reorg_depth", &HeaderChain::max_reorg_depth)
         .def("check_header", &HeaderChain::check_header, py::call_guard<py::gil_scoped_release>())
         .def("accept_header", &HeaderChain::accept_header, py::arg("header"), py::arg("adjusted_time"), py::arg("check_pow") = true,
              py::call_guard<py::gil_scoped_release>())

@@ -178,6 +178,11 @@ AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256
     }
     // ContextualCheckBlockHeader
     const int height = prev->height + 1;
+    if (max_reorg_depth > 0 && this->height() - (height - 1) >= max_reorg_depth) {
+        r.reject = "bad-fork-prior-to-maxreorgdepth";
+        r.dos = 10;
+        return r;
+    }
     if (h.bits != (expected_bits ? *expected_bits : next_work_required(prev, h, params_))) {
         r.reject = "bad-diffbits";
         r.dos = 100;

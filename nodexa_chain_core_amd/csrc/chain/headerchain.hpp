@@ -76,6 +76,10 @@ public:
     void reconsider(const Uint256& hash);
     u32 next_bits(const BlockHeader& candidate) const;  // GetNextWorkRequired on the tip
     bool strict_kawpow_height = false;  // policy: header nHeight must equal index height
+    // -maxreorg guard (ContextualCheckBlockHeader, src/validation.cpp:11815-11827): > 0 rejects a
+    // header whose parent is this many or more blocks below the active tip. The node arms it
+    // only while it has >= -minreorgpeers peers and a tip younger than -minreorgage.
+    int max_reorg_depth = 0;
 
     static constexpr size_t kParallelAcceptMin = 64;  // batch size from which accept_headers precomputes
 

@@ -20,6 +20,7 @@ from dataclasses import dataclass
 
 from .. import core
 from ..chain.state import ChainState
+from ..utils.trace import traced
 
 _core = core()
 
@@ -52,6 +53,7 @@ class BlockAssembler:
         self.params = state.params
         self.max_weight = max_weight
 
+    @traced("miner.create_new_block")
     def create_new_block(self, script_pubkey: bytes, now: int | None = None) -> BlockTemplate:
         st = self.state
         with st.lock:

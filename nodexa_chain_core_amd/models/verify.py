@@ -22,11 +22,13 @@ import time
 import numpy as np
 
 from .. import core
+from ..utils.trace import traced
 
 _core = core()
 LAST_TIMING: dict[str, float] = {}  # stage times of the last verify_headers call
 
 
+@traced("verify.headers_pow")
 def verify_headers(params, headers, gpus: list[int] | None = None, threads: int = 0,
                    mode: str = "auto") -> list[dict]:
     """Full PoW check of every header: {"valid", "hash", "reason"?} per header.
@@ -175,6 +177,7 @@ def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, th
             out[i] = {"valid": True, "hash": _core.u256_hex(hsh)}
 
 
+@traced("verify.process_headers")
 def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None = None, mode: str = "auto",
                     verify_fn=None) -> dict:
     """ProcessNewBlockHeaders for a batch (src/validation.cpp:12017-12035): PoW of the whole

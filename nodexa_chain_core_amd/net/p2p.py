@@ -328,6 +328,7 @@ class ConnectionManager:
             if chain.find(headers[0].prev) is None:  # unconnecting headers: ask from our locator
                 self.request_headers(peer)
                 return
+            self.state.arm_reorg_guard(self.peer_count())
             t0 = time.perf_counter()
             res = process_headers(chain, headers, self.state.adjusted_time(), gpus=self.gpus, mode=self.verify_mode)
             REGISTRY.inc("p2p_headers_accepted_total", res["accepted"])
@@ -399,6 +400,7 @@ class ConnectionManager:
 
     def on_block(self, peer: Peer, p: bytes) -> None:
         blk = _core.Block.deserialize(p, self.params.kawpow_activation_time)
+        self.state.arm_reorg_guard(self.peer_count())
         st = self.state.process_new_block(blk)
         REGISTRY.inc("p2p_blocks_received_total", 1, ok=st.ok)
         if not st.ok and st.reject != "duplicate":

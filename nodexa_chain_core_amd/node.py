@@ -97,6 +97,10 @@ class Node:
             sync.enable(True)
         self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False),
                                 reindex=a.get_bool("reindex", False))
+        for flag, attr in (("maxreorg", "max_reorg_depth"), ("minreorgpeers", "min_reorg_peers"),
+                           ("minreorgage", "min_reorg_age")):  # reorg guard knobs (src/init.cpp)
+            if a.is_set(flag):
+                setattr(self.params, attr, a.get_int(flag, getattr(self.params, attr)))
         if self.network == "regtest" and a.is_set("blockversion"):  # -blockversion (src/miner.cpp:146-149)
             self.state.block_version_override = a.get_int("blockversion", 0)
         if self.datadir is not None and a.get_bool("persistmempool", True):  # -persistmempool (LoadMempool)
@@ -130,6 +134,19 @@ class Node:
 
             self.zmq = ZmqNotifier(self.state, zmq_eps)
             self.state.register(self.zmq)
+        stop_at = a.get_int("stopatheight", 0)
+        if stop_at > 0:  # -stopatheight (src/validation.cpp:11280): shut down once the tip reaches it
+            from .chain.state import ValidationInterface
+
+            node = self
+
+            class _StopAt(ValidationInterface):
+                def updated_block_tip(self, tip, fork, initial_download: bool) -> None:
+                    if tip.height >= stop_at:
+                        log.log_printf(f"-stopatheight {stop_at} reached")
+                        node.request_shutdown()
+
+            self.state.register(_StopAt())
         self.table.warmup = None
         log.log_printf(f"nodexad started: network={self.network} height={self.state.height()} "
                        f"kawpow_activation={self.params.kawpow_activation_time} gpus={self.gpus or 'none'}")

@@ -17,6 +17,7 @@ import struct
 import torch
 
 from .. import _core
+from ..utils.trace import traced
 from . import runtime
 
 KERNELS = ["eq_gen"] + [f"eq_round{r}" for r in range(1, 9)] + ["eq_final", "eq_reconstruct"]
@@ -37,6 +38,7 @@ def blake2b_h0(n: int = 200, k: int = 9) -> list[int]:
     return [a ^ b for a, b in zip(iv, words)]
 
 
+@traced("equihash.verify")
 def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | None = None) -> list[bool]:
     """GPU batch check of packed (n=200, k=9) solutions (hip/kernels/equihash.hip eq_verify):
     one workgroup per solution. `inputs` are the 112-byte header inputs."""
@@ -160,6 +162,7 @@ class EquihashSolver:
             out.append(sols)
         return out
 
+    @traced("equihash.solve")
     def solve(self, inputs: list[bytes]) -> list[list[list[int]]]:
         self.launch(inputs)
         return self.collect(inputs)

@@ -16,6 +16,7 @@ import torch
 
 from .. import _core
 from . import runtime
+from ..utils.trace import traced
 
 # 512-bit items per launch: keeps a single dispatch well under a second even
 # at epoch 384 while still giving >> 256 CUs x 8 waves of work.
@@ -69,6 +70,7 @@ class DeviceEpoch:
         first = min(rank * per, self.items512)
         return first, min(per, self.items512 - first)
 
+    @traced("ethash.dag_build")
     def build(self, shard: tuple[int, int] | None = None, stream: int | None = None) -> None:
         if self.dag is None:
             raise ValueError("light-only DeviceEpoch has no DAG to build")

@@ -19,6 +19,7 @@ import torch
 
 from .. import _core
 from . import jit, runtime
+from ..utils.trace import traced
 from .ethash import DeviceEpoch
 
 SHARE_FMT = "<Q8I8I"
@@ -122,6 +123,7 @@ class KawpowSearcher:
         shares.sort(key=lambda s: s.nonce)
         return shares
 
+    @traced("kawpow.search")
     def search(self, header_hash: bytes, start_nonce: int, num_nonces: int, boundary: bytes) -> list[Share]:
         """All shares in [start, start+num) with final <= boundary (bit-exact, host-checked).
         The launch is rounded up to whole workgroups; shares past the window are dropped."""

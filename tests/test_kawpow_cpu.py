@@ -114,3 +114,17 @@ def test_light_cache_disk_cache(core, tmp_path):
         assert c.light_cache() == a.light_cache()
     finally:
         core.set_light_cache_dir("")
+
+
+def test_search_variant_selection_by_dag_size(core):
+    """ops/jit.defines_for: the 32-bit buffer-offset DAG loads (KP_SBUFFER / KP_BUFFER) are used
+    below 4 GiB only (epoch 384 is 4294962304 bytes; epoch 385 is above 2^32)."""
+    from nodexa_chain_core_amd.ops import jit
+
+    below = core.full_dataset_num_items(384) * 128
+    above = core.full_dataset_num_items(385) * 128
+    assert below < 1 << 32 <= above
+    assert "KP_SBUFFER" in jit.defines_for(below, jit.TUNED_DEFINES)
+    big = jit.defines_for(above, jit.TUNED_DEFINES)
+    assert "KP_SBUFFER" not in big and "KP_BUFFER" not in big and "KP_DPP" in big
+    assert "KP_BUFFER" not in jit.defines_for(above, ("KP_BUFFER", "KP_DPP"))

@@ -175,3 +175,16 @@ def test_bip9_versionbits_regtest(core, node_factory):  # noqa: F811
     assert set(tpl["rules"]) == {"testdummy", "assets", "messaging_restricted", "enforce_value"}
     assert tpl["vbavailable"] == {"transfer_script": 8} and tpl["vbrequired"] == 0
     assert tpl["version"] == 0x30000000 | (1 << 8)
+
+
+def test_stopatheight_and_reorg_flags(core, node_factory):  # noqa: F811
+    node, addr = node_factory(("-stopatheight=3", "-maxreorg=7", "-minreorgpeers=1"))
+    c = client(node)
+    assert node.params.max_reorg_depth == 7 and node.params.min_reorg_peers == 1
+    c.generatetoaddress(2, addr)
+    assert not node.shutdown_requested()
+    c.generatetoaddress(1, addr)
+    assert node.shutdown_requested()
+    # armed only with enough peers and a fresh tip
+    assert node.state.arm_reorg_guard(1) and node.state.chain.max_reorg_depth == 7
+    assert not node.state.arm_reorg_guard(0) and node.state.chain.max_reorg_depth == 0

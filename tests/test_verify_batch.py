@@ -124,3 +124,26 @@ def test_accept_headers_batch_equals_serial(fixture):
     # full PoW checked in parallel (check_pow=True) accepts the valid prefix
     d = _core.HeaderChain(params)
     assert all(r.ok for r in d.accept_headers(list(headers[:96]), adj, True))
+
+
+def test_max_reorg_depth_guard(chain_fixture):
+    """-maxreorg (ContextualCheckBlockHeader): with the guard armed a fork from >= 60 blocks
+    below the tip is rejected with DoS 10; disarmed it is stored as a side branch."""
+    params, headers = chain_fixture
+    act = params.kawpow_activation_time
+    adj = headers[-1].time + 3600
+    chain = _core.HeaderChain(params)
+    assert all(r.ok for r in chain.accept_headers(list(headers[:100]), adj, False))
+    tip = chain.tip().hash
+    fork = _copy(headers[20], act)  # same parent (height 20), different nonce: a new branch
+    fork.nonce64 ^= 1
+    deep = chain.height() - headers[19].height
+    assert deep >= params.max_reorg_depth == 60
+    chain.max_reorg_depth = params.max_reorg_depth
+    r = chain.accept_header(fork, adj, False)
+    assert not r.ok and r.reject == "bad-fork-prior-to-maxreorgdepth" and r.dos == 10
+    shallow = _copy(headers[95], act)  # 5 below the tip: allowed even when armed
+    shallow.nonce64 ^= 1
+    assert chain.accept_header(shallow, adj, False).ok
+    chain.max_reorg_depth = 0
+    assert chain.accept_header(fork, adj, False).ok and chain.tip().hash == tip
