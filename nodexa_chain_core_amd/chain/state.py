@@ -118,6 +118,7 @@ class ChainState:
         self.block_pos: dict[bytes, object] = {}
         self.mempool: dict[bytes, MempoolEntry] = {}
         self.ntx: dict[bytes, int] = {}      # transactions per stored block (CBlockIndex::nTx)
+        self._chain_tx: dict[bytes, int] = {}  # memo of chain_tx_count
         self.fee_stats: list[tuple[float, int]] = []  # (sat/vB, blocks to confirm) of mined pool txs
         self.mocktime = 0                     # setmocktime (0 = wall clock)
         self.block_version_override: int | None = None  # -blockversion (regtest only)
@@ -261,11 +262,20 @@ class ChainState:
         return armed
 
     def chain_tx_count(self, idx) -> int:
-        """CBlockIndex::nChainTx: transactions in the chain up to and including idx."""
-        n = 0
-        while idx is not None:
-            n += self.ntx.get(idx.hash, 0)
+        """CBlockIndex::nChainTx: transactions in the chain up to and including idx. Memoised per
+        block hash (a stored block's count never changes), so a tip query walks back only to
+        the last block already counted."""
+        path = []
+        while idx is not None and idx.hash not in self._chain_tx:
+            path.append(idx)
             idx = self.chain.find(idx.prev_hash) if idx.height > 0 else None
+        n = self._chain_tx[idx.hash] if idx is not None else 0
+        complete = True  # cache only counts whose every ancestor has its data (like nChainTx != 0)
+        for i in reversed(path):
+            n += self.ntx.get(i.hash, 0)
+            complete = complete and i.hash in self.ntx
+            if complete:
+                self._chain_tx[i.hash] = n
         return n
 
     # ------------------------------------------------------------------ mempool-lite
