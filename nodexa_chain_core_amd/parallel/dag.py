@@ -24,10 +24,10 @@ def allgather_shards(full: torch.Tensor, per: int) -> None:
         raise ValueError("buffer must hold exactly world_size shards")
     mine = full[w.rank * per:(w.rank + 1) * per]
     if w.backend == "nccl":
-        dist.all_gather_into_tensor(full, mine)
+        dist.all_gather_into_tensor(full, mine, group=w.group)
     else:  # gloo: no in-place all_gather_into_tensor, go through views of the same buffer
         parts = list(full.view(w.world_size, per).unbind(0))
-        dist.all_gather(parts, mine.clone())
+        dist.all_gather(parts, mine.clone(), group=w.group)
 
 
 def build_dag(epoch_dev) -> None:

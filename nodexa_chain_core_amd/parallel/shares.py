@@ -51,9 +51,9 @@ class ShareGather:
         if not self.w.distributed:
             self.gathered.copy_(self.results, non_blocking=True)
         elif self.w.backend == "nccl":
-            dist.all_gather_into_tensor(self.gathered, self.results)
+            dist.all_gather_into_tensor(self.gathered, self.results, group=self.w.group)
         else:
-            dist.all_gather(self._views, self.results)
+            dist.all_gather(self._views, self.results, group=self.w.group)
 
     def collect(self):
         from ..ops.kawpow import Share

@@ -38,7 +38,7 @@ def _sharded_rows(jobs: np.ndarray, mode: str) -> np.ndarray:
     if not w.distributed:
         return buf.cpu().numpy()[:m]
     out = torch.empty((per * w.world_size, 64), dtype=torch.uint8, device=w.device)
-    dist.all_gather_into_tensor(out, buf)
+    dist.all_gather_into_tensor(out, buf, group=w.group)
     return out.cpu().numpy()[:m]
 
 

@@ -23,6 +23,11 @@ class World:
     local_rank: int = 0
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    group: object = None            # process group of the collectives (None = the default group)
+    ranks: tuple[int, ...] = ()     # global ranks of the group members, index = rank in the group
+
+    def global_rank(self, r: int) -> int:
+        return self.ranks[r] if self.ranks else r
 
     @property
     def distributed(self) -> bool:
@@ -61,7 +66,27 @@ def init(use_gpu: bool | None = None, timeout_s: int = 600) -> World:
             kw["device_id"] = device
         dist.init_process_group(backend=backend, rank=rank, world_size=world_size,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    _WORLD = World(rank, world_size, local_rank, backend, device)
+    _WORLD = World(rank, world_size, local_rank, backend, device, None, tuple(range(world_size)))
+    return _WORLD
+
+
+def shrink(survivors: list[int], timeout_s: int = 120) -> World:
+    """Elastic world size: rebuild the communicator over the surviving ranks after a
+    rank is lost, and make it the group every collective here uses. Only the survivors call
+    this (local synchronisation: a dead rank never joins). Ranks are renumbered 0..n-1 in the
+    order of `survivors`' global ranks, so the nonce partition (rank, world_size) and shard
+    ownership simply re-derive from the new World."""
+    global _WORLD
+    w = get()
+    members = sorted(set(int(r) for r in survivors))
+    g = w.global_rank(w.rank)
+    if g not in members:
+        raise RuntimeError(f"rank {g} is not among the survivors {members}")
+    if len(members) == len(w.ranks or range(w.world_size)):
+        return w
+    grp = dist.new_group(ranks=members, timeout=datetime.timedelta(seconds=timeout_s),
+                         use_local_synchronization=True)
+    _WORLD = World(members.index(g), len(members), w.local_rank, w.backend, w.device, grp, tuple(members))
     return _WORLD
 
 
@@ -80,9 +105,9 @@ def barrier() -> None:
     w = get()
     if w.distributed:
         if w.backend == "nccl":
-            dist.barrier(device_ids=[w.device.index])
+            dist.barrier(group=w.group, device_ids=[w.device.index])
         else:
-            dist.barrier()
+            dist.barrier(group=w.group)
 
 
 def broadcast_bytes(payload: bytes | None, size: int, src: int = 0) -> bytes:
@@ -94,7 +119,7 @@ def broadcast_bytes(payload: bytes | None, size: int, src: int = 0) -> bytes:
             raise ValueError("payload size mismatch")
         t.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
     if w.distributed:
-        dist.broadcast(t, src=src)
+        dist.broadcast(t, src=w.global_rank(src), group=w.group)
     return bytes(t.cpu().numpy().tobytes())
 
 
@@ -103,7 +128,7 @@ def all_reduce_max(x: float) -> float:
     if not w.distributed:
         return x
     t = torch.tensor([x], dtype=torch.float64, device=w.device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=w.group)
     return float(t.item())
 
 
@@ -112,5 +137,5 @@ def all_reduce_sum_int(x: int) -> int:
     if not w.distributed:
         return x
     t = torch.tensor([x], dtype=torch.int64, device=w.device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=w.group)
     return int(t.item())

@@ -142,3 +142,60 @@ def test_distributed_verify_matches_single_process(world):
     assert not want[20][0] and all(v for v, _, _ in want[:20])
     for r in range(world):
         assert results[r] == want, results[r] if isinstance(results[r], str) else r
+
+
+def _elastic_worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
+        import torch
+
+        from nodexa_chain_core_amd.parallel import dag as pdag
+        from nodexa_chain_core_amd.parallel import world as W
+
+        W.init(use_gpu=False)
+        assert W.all_reduce_sum_int(1) == world
+        if rank == world - 1:  # this rank "dies": it leaves without another collective
+            q.put((rank, "left"))
+            return
+        w = W.shrink(list(range(world - 1)))
+        assert w.world_size == world - 1 and w.rank == rank
+        assert W.all_reduce_sum_int(rank + 1) == (world - 1) * world // 2
+        pkt = bytes(range(96))
+        assert W.broadcast_bytes(pkt if w.rank == 0 else None, 96) == pkt
+        per = 16
+        full = torch.zeros(w.world_size * per, dtype=torch.uint8)
+        full[w.rank * per:(w.rank + 1) * per] = w.rank + 1
+        pdag.allgather_shards(full, per)
+        assert full.tolist() == [r + 1 for r in range(w.world_size) for _ in range(per)]
+        # the nonce partition re-derives from the new (rank, world_size): disjoint, gap-free
+        batch, base = 1 << 10, 7 << 40
+        mine = [(base + (i * w.world_size + w.rank) * batch) for i in range(3)]
+        q.put((rank, mine))
+        W.barrier()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc() or repr(e)))
+
+
+@pytest.mark.timeout(300)
+def test_elastic_shrink_after_rank_loss():
+    """parallel/world.shrink: after rank 2 of 3 is lost the survivors rebuild the communicator
+    (new_group with local synchronisation) and every collective and the nonce partition carry on
+    over 2 ranks (SURVEY §5 elastic world size)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_elastic_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=280) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert results[2] == "left", results
+    starts = sorted(results[0] + results[1])
+    assert all(isinstance(results[r], list) for r in (0, 1)), results
+    assert [b - a for a, b in zip(starts, starts[1:])] == [1 << 10] * 5
