@@ -103,6 +103,53 @@ void load_words(const std::string& b, uint32_t out[8]) {
 
 }  // namespace
 
+
+// ---------------------------------------------------------------- Equihash solve sequence
+EquihashDev make_equihash_params(const std::vector<std::shared_ptr<Kernel>>& ks, const std::vector<uint64_t>& h0,
+                                 uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
+                                 uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols, uint32_t banks) {
+    if (banks == 0 || banks > EQ_MAX_BANKS || (banks & (banks - 1)) || EQ_CAP % banks)
+        throw std::invalid_argument("banks must be a power of two <= EQ_MAX_BANKS dividing EQ_CAP");
+    // ks = [eq_gen, eq_round1..eq_round8, eq_final, eq_reconstruct]
+    if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash kernels");
+    if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
+    if (input_len > 124 || num_inst == 0) throw std::invalid_argument("bad equihash geometry");
+    EquihashDev p{};
+    p.msgs = reinterpret_cast<const uint64_t*>(msgs);
+    for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
+    p.input_len = input_len;
+    p.num_inst = num_inst;
+    p.banks = banks;
+    p.hashes = reinterpret_cast<uint32_t*>(hashes);
+    p.refs = reinterpret_cast<uint32_t*>(refs);
+    p.counts = reinterpret_cast<uint32_t*>(counts);
+    p.cands = reinterpret_cast<uint32_t*>(cands);
+    p.sols = reinterpret_cast<uint32_t*>(sols);
+    return p;
+}
+
+void issue_equihash_solve(const std::vector<std::shared_ptr<Kernel>>& ks, const EquihashDev& p, hipStream_t s) {
+    const uint32_t n = p.num_inst;
+    check(hipMemsetAsync(p.counts, 0, size_t(n) * (EQ_LEVELS + 1) * EQ_BUCKETS * EQ_MAX_BANKS * 4, s), "memset counts");
+    check(hipMemsetAsync(p.cands, 0, size_t(n) * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
+    check(hipMemsetAsync(p.sols, 0, size_t(n) * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
+    ks[0]->launch_bytes(dim3((1u << 20) / 256, n), dim3(256), 0, s, &p, sizeof(p));
+    for (int r = 1; r <= 8; ++r) ks[size_t(r)]->launch_bytes(dim3(EQ_BUCKETS, n), dim3(256), 0, s, &p, sizeof(p));
+    ks[9]->launch_bytes(dim3(EQ_BUCKETS, n), dim3(256), 0, s, &p, sizeof(p));
+    ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, n), dim3(256), 0, s, &p, sizeof(p));
+}
+
+struct LaunchGraph {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    size_t num_nodes = 0;
+    EquihashDev params{};  // the launches' parameter block lives as long as the graph
+    ~LaunchGraph() {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        if (graph) (void)hipGraphDestroy(graph);
+    }
+};
+
 PYBIND11_MODULE(_hip, m) {
     m.doc() = "nodexa HIP host runtime: gfx950 code-object loading and typed kernel launchers";
 
@@ -342,30 +389,40 @@ PYBIND11_MODULE(_hip, m) {
                                       uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
                                       uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols,
                                       uintptr_t stream, uint32_t banks) {
-        if (banks == 0 || banks > EQ_MAX_BANKS || (banks & (banks - 1)) || EQ_CAP % banks)
-            throw std::invalid_argument("banks must be a power of two <= EQ_MAX_BANKS dividing EQ_CAP");
-        // ks = [eq_gen, eq_round1..eq_round8, eq_final, eq_reconstruct]
-        if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash kernels");
-        if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
-        if (input_len > 124 || num_inst == 0) throw std::invalid_argument("bad equihash geometry");
-        EquihashDev p{};
-        p.msgs = reinterpret_cast<const uint64_t*>(msgs);
-        for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
-        p.input_len = input_len;
-        p.num_inst = num_inst;
-        p.banks = banks;
-        p.hashes = reinterpret_cast<uint32_t*>(hashes);
-        p.refs = reinterpret_cast<uint32_t*>(refs);
-        p.counts = reinterpret_cast<uint32_t*>(counts);
-        p.cands = reinterpret_cast<uint32_t*>(cands);
-        p.sols = reinterpret_cast<uint32_t*>(sols);
-        hipStream_t s = as_stream(stream);
-        check(hipMemsetAsync(p.counts, 0, size_t(num_inst) * (EQ_LEVELS + 1) * EQ_BUCKETS * EQ_MAX_BANKS * 4, s), "memset counts");
-        check(hipMemsetAsync(p.cands, 0, size_t(num_inst) * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
-        check(hipMemsetAsync(p.sols, 0, size_t(num_inst) * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
-        ks[0]->launch_bytes(dim3((1u << 20) / 256, num_inst), dim3(256), 0, s, &p, sizeof(p));
-        for (int r = 1; r <= 8; ++r) ks[size_t(r)]->launch_bytes(dim3(EQ_BUCKETS, num_inst), dim3(256), 0, s, &p, sizeof(p));
-        ks[9]->launch_bytes(dim3(EQ_BUCKETS, num_inst), dim3(256), 0, s, &p, sizeof(p));
-        ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
+        const EquihashDev p = make_equihash_params(ks, h0, msgs, input_len, num_inst, hashes, refs, counts, cands,
+                                                   sols, banks);
+        issue_equihash_solve(ks, p, as_stream(stream));
+    });
+    // The same 3 memsets + 11 launches captured once into a hipGraph (fixed device buffers, so
+    // the graph stays valid across batches; only the message words change, in place). One
+    // hipGraphLaunch per batch replaces 14 stream operations.
+    py::class_<LaunchGraph, std::shared_ptr<LaunchGraph>>(m, "LaunchGraph")
+        .def("launch", [](LaunchGraph& g, uintptr_t stream) {
+            check(hipGraphLaunch(g.exec, as_stream(stream)), "hipGraphLaunch");
+        })
+        .def_readonly("num_nodes", &LaunchGraph::num_nodes);
+    m.def("capture_equihash_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
+                                       uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
+                                       uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols,
+                                       uint32_t banks) {
+        auto g = std::make_shared<LaunchGraph>();
+        g->params = make_equihash_params(ks, h0, msgs, input_len, num_inst, hashes, refs, counts, cands, sols, banks);
+        hipStream_t cs = nullptr;
+        check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate");
+        check(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+        try {
+            issue_equihash_solve(ks, g->params, cs);
+        } catch (...) {
+            hipGraph_t broken = nullptr;
+            (void)hipStreamEndCapture(cs, &broken);
+            if (broken) (void)hipGraphDestroy(broken);
+            (void)hipStreamDestroy(cs);
+            throw;
+        }
+        check(hipStreamEndCapture(cs, &g->graph), "hipStreamEndCapture");
+        (void)hipStreamDestroy(cs);
+        check(hipGraphGetNodes(g->graph, nullptr, &g->num_nodes), "hipGraphGetNodes");
+        check(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0), "hipGraphInstantiate");
+        return g;
     });
 }

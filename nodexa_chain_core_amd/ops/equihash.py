@@ -12,6 +12,7 @@ instance's live level (~67 MB) fits the 256 MiB Infinity Cache.
 """
 from __future__ import annotations
 
+import os
 import struct
 
 import torch
@@ -105,6 +106,10 @@ class EquihashSolver:
         self._pending: list[tuple[list[bytes], torch.Tensor, torch.cuda.Event]] = []
         self._next = 0
         self.h0 = blake2b_h0()
+        # hipGraph of the 14-operation solve sequence (captured on first launch; NODEXA_EQ_GRAPH=0
+        # launches the kernels one by one)
+        self.use_graph = os.environ.get("NODEXA_EQ_GRAPH", "1") != "0"
+        self._graph = None
         self.input_len = None
 
     def launch(self, inputs: list[bytes], stream: int | None = None) -> None:
@@ -127,9 +132,17 @@ class EquihashSolver:
             stage.copy_(torch.frombuffer(buf, dtype=torch.int64))
             self.msgs.copy_(stage, non_blocking=True)
             s = runtime.current_stream_handle() if stream is None else stream
-            self.h.launch_equihash_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst,
-                                         self.hashes.data_ptr(), self.refs.data_ptr(), self.counts.data_ptr(),
-                                         self.cands.data_ptr(), self.sols.data_ptr(), s, self.banks)
+            args = (self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst, self.hashes.data_ptr(),
+                    self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(), self.sols.data_ptr())
+            if self.use_graph and self._graph is None:
+                try:
+                    self._graph = self.h.capture_equihash_solve(*args, self.banks)
+                except RuntimeError:
+                    self.use_graph = False  # capture unsupported here: plain launches
+            if self._graph is not None:
+                self._graph.launch(s)
+            else:
+                self.h.launch_equihash_solve(*args, s, self.banks)
             land = self._landing[self._next]
             self._next = (self._next + 1) % len(self._landing)
             land.copy_(self.sols, non_blocking=True)
