@@ -106,9 +106,10 @@ class EquihashSolver:
         self._pending: list[tuple[list[bytes], torch.Tensor, torch.cuda.Event]] = []
         self._next = 0
         self.h0 = blake2b_h0()
-        # hipGraph of the 14-operation solve sequence (captured on first launch; NODEXA_EQ_GRAPH=0
-        # launches the kernels one by one)
-        self.use_graph = os.environ.get("NODEXA_EQ_GRAPH", "1") != "0"
+        # hipGraph of the 14-operation solve sequence (captured on first launch). Opt-in
+        # (NODEXA_EQ_GRAPH=1): the first capture, whose kernel nodes were built from
+        # HIP_LAUNCH_PARAM_BUFFER_POINTER launches, faulted on replay (profiles/README r1u)
+        self.use_graph = os.environ.get("NODEXA_EQ_GRAPH", "0") == "1"
         self._graph = None
         self.input_len = None
 
