@@ -62,6 +62,13 @@ struct Kernel {
                                     config),
               ("hipModuleLaunchKernel(" + name + ")").c_str());
     }
+    // kernelParams form (argv[i] = pointer to argument i). Used under stream capture with argv and
+    // the argument storage owned by the graph, so no node can refer to a dead stack frame.
+    void launch_args(dim3 grid, dim3 block, unsigned shmem, hipStream_t stream, void** argv) const {
+        check(hipModuleLaunchKernel(fn, grid.x, grid.y, grid.z, block.x, block.y, block.z, shmem, stream, argv,
+                                    nullptr),
+              ("hipModuleLaunchKernel(" + name + ")").c_str());
+    }
 };
 
 struct CodeObject {
@@ -128,15 +135,23 @@ EquihashDev make_equihash_params(const std::vector<std::shared_ptr<Kernel>>& ks,
     return p;
 }
 
-void issue_equihash_solve(const std::vector<std::shared_ptr<Kernel>>& ks, const EquihashDev& p, hipStream_t s) {
+// argv == nullptr: HIP_LAUNCH_PARAM_BUFFER_POINTER launches of &p (direct use). Under stream
+// capture pass argv = {&p} with p owned by the graph: the kernel nodes then take the
+// argument through kernelParams and nothing points into this function's stack.
+void issue_equihash_solve(const std::vector<std::shared_ptr<Kernel>>& ks, const EquihashDev& p, hipStream_t s,
+                          void** argv = nullptr) {
     const uint32_t n = p.num_inst;
     check(hipMemsetAsync(p.counts, 0, size_t(n) * (EQ_LEVELS + 1) * EQ_BUCKETS * EQ_MAX_BANKS * 4, s), "memset counts");
     check(hipMemsetAsync(p.cands, 0, size_t(n) * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
     check(hipMemsetAsync(p.sols, 0, size_t(n) * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
-    ks[0]->launch_bytes(dim3((1u << 20) / 256, n), dim3(256), 0, s, &p, sizeof(p));
-    for (int r = 1; r <= 8; ++r) ks[size_t(r)]->launch_bytes(dim3(EQ_BUCKETS, n), dim3(256), 0, s, &p, sizeof(p));
-    ks[9]->launch_bytes(dim3(EQ_BUCKETS, n), dim3(256), 0, s, &p, sizeof(p));
-    ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, n), dim3(256), 0, s, &p, sizeof(p));
+    auto launch = [&](size_t k, dim3 grid) {
+        if (argv) ks[k]->launch_args(grid, dim3(256), 0, s, argv);
+        else ks[k]->launch_bytes(grid, dim3(256), 0, s, &p, sizeof(p));
+    };
+    launch(0, dim3((1u << 20) / 256, n));
+    for (size_t r = 1; r <= 8; ++r) launch(r, dim3(EQ_BUCKETS, n));
+    launch(9, dim3(EQ_BUCKETS, n));
+    launch(10, dim3(EQ_RECON_GROUPS, n));
 }
 
 struct LaunchGraph {
@@ -144,6 +159,7 @@ struct LaunchGraph {
     hipGraphExec_t exec = nullptr;
     size_t num_nodes = 0;
     EquihashDev params{};  // the launches' parameter block lives as long as the graph
+    void* argv[1] = {&params};
     ~LaunchGraph() {
         if (exec) (void)hipGraphExecDestroy(exec);
         if (graph) (void)hipGraphDestroy(graph);
@@ -411,7 +427,7 @@ PYBIND11_MODULE(_hip, m) {
         check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate");
         check(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
         try {
-            issue_equihash_solve(ks, g->params, cs);
+            issue_equihash_solve(ks, g->params, cs, g->argv);
         } catch (...) {
             hipGraph_t broken = nullptr;
             (void)hipStreamEndCapture(cs, &broken);
