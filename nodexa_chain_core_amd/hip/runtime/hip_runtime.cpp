@@ -138,12 +138,17 @@ EquihashDev make_equihash_params(const std::vector<std::shared_ptr<Kernel>>& ks,
 // argv == nullptr: HIP_LAUNCH_PARAM_BUFFER_POINTER launches of &p (direct use). Under stream
 // capture pass argv = {&p} with p owned by the graph: the kernel nodes then take the
 // argument through kernelParams and nothing points into this function's stack.
-void issue_equihash_solve(const std::vector<std::shared_ptr<Kernel>>& ks, const EquihashDev& p, hipStream_t s,
-                          void** argv = nullptr) {
+void clear_equihash_state(const EquihashDev& p, hipStream_t s) {
     const uint32_t n = p.num_inst;
     check(hipMemsetAsync(p.counts, 0, size_t(n) * (EQ_LEVELS + 1) * EQ_BUCKETS * EQ_MAX_BANKS * 4, s), "memset counts");
     check(hipMemsetAsync(p.cands, 0, size_t(n) * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
     check(hipMemsetAsync(p.sols, 0, size_t(n) * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
+}
+
+void issue_equihash_solve(const std::vector<std::shared_ptr<Kernel>>& ks, const EquihashDev& p, hipStream_t s,
+                          void** argv = nullptr) {
+    const uint32_t n = p.num_inst;
+    if (!argv) clear_equihash_state(p, s);  // captured graphs hold the kernels only (see LaunchGraph)
     auto launch = [&](size_t k, dim3 grid) {
         if (argv) ks[k]->launch_args(grid, dim3(256), 0, s, argv);
         else ks[k]->launch_bytes(grid, dim3(256), 0, s, &p, sizeof(p));
@@ -409,11 +414,14 @@ PYBIND11_MODULE(_hip, m) {
                                                    sols, banks);
         issue_equihash_solve(ks, p, as_stream(stream));
     });
-    // The same 3 memsets + 11 launches captured once into a hipGraph (fixed device buffers, so
-    // the graph stays valid across batches; only the message words change, in place). One
-    // hipGraphLaunch per batch replaces 14 stream operations.
+    // The 11 kernel launches captured once into a hipGraph (fixed device buffers, so the graph
+    // stays valid across batches; only the message words change, in place). Per batch: 3
+    // memsets + one hipGraphLaunch instead of 14 stream operations.
     py::class_<LaunchGraph, std::shared_ptr<LaunchGraph>>(m, "LaunchGraph")
         .def("launch", [](LaunchGraph& g, uintptr_t stream) {
+            // the counter / candidate / solution clears stay plain stream memsets: captured as
+            // graph memset nodes they did not re-run on replay here (stale counts, invalid rows)
+            clear_equihash_state(g.params, as_stream(stream));
             check(hipGraphLaunch(g.exec, as_stream(stream)), "hipGraphLaunch");
         })
         .def_readonly("num_nodes", &LaunchGraph::num_nodes);

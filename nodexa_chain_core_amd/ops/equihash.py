@@ -106,9 +106,8 @@ class EquihashSolver:
         self._pending: list[tuple[list[bytes], torch.Tensor, torch.cuda.Event]] = []
         self._next = 0
         self.h0 = blake2b_h0()
-        # hipGraph of the 14-operation solve sequence (captured on first launch). Opt-in
-        # (NODEXA_EQ_GRAPH=1): the first capture, whose kernel nodes were built from
-        # HIP_LAUNCH_PARAM_BUFFER_POINTER launches, faulted on replay (profiles/README r1u)
+        # hipGraph of the 11 solve kernels (captured on first launch; the 3 state clears stay
+        # stream memsets). Opt-in (NODEXA_EQ_GRAPH=1) until measured: see profiles/README r1u
         self.use_graph = os.environ.get("NODEXA_EQ_GRAPH", "0") == "1"
         self._graph = None
         self.input_len = None
