@@ -1,7 +1,8 @@
 #!/bin/bash
-# hipGraph Equihash: agreement test, then graph vs direct launches in the bench.
+# hipGraph Equihash (kernels captured, clears as memsets): Equihash throughput graph vs direct, interleaved.
 set -o pipefail
 mkdir -p gpurun_out/r1u
-timeout -k 10 300 python -u -m pytest tests/test_gpu_equihash.py -x -v --timeout 180 --timeout-method thread > gpurun_out/r1u/pytest_eq.log 2>&1 &&
-timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 > gpurun_out/r1u/bench_graph.log 2>&1 &&
-NODEXA_EQ_GRAPH=0 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 > gpurun_out/r1u/bench_direct.log 2>&1
+for i in 1 2; do
+  NODEXA_EQ_GRAPH=1 timeout -k 10 200 python -u tools/equihash_bench.py --inst 8 --batches 20 > gpurun_out/r1u/eq_graph_$i.log 2>&1 &&
+  NODEXA_EQ_GRAPH=0 timeout -k 10 200 python -u tools/equihash_bench.py --inst 8 --batches 20 > gpurun_out/r1u/eq_direct_$i.log 2>&1 || exit $?
+done
