@@ -53,6 +53,7 @@
 //                 the kernel's max-threads attribute)
 //   KP_DPP        rounds unrolled by 16; item index broadcast by DPP row_newbcast
 //   KP_BARRETT    5-op Barrett modulo for the item index
+//   KP_FASTMOD24  the same with 24-bit (full-rate) multiplies, items < 2^24 (DAG < 4 GiB)
 //   KP_BUFFER     raw-buffer DAG loads with a 32-bit offset (DAG < 4 GiB only)
 //   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride), DAG < 4 GiB only
 //   KP_L1X4       L1 replicated 4x in LDS (64 KiB) so an L1 address is one
@@ -113,8 +114,20 @@ NX_DEV uint32_t kp_mul33(uint32_t a) { return a * 33u; }
 
 NX_DEV uint32_t kp_clz(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : 32u; }
 NX_DEV uint32_t kp_fnv1a(uint32_t h, uint32_t d) { return (h ^ d) * 0x01000193u; }
+#ifdef KP_FASTMOD24
+// 24-bit Barrett for 2^16 < d < 2^24 (DAGs < 4 GiB, with KP_SBUFFER): q' = mulhi24(x >> 8,
+// floor(2^40/d)) is q or q-1 (the dropped low byte and the floor of m24 move the estimate by
+// < 2^-7), then r = x - mul24(q', d) and one min(). Every op is a full-rate VALU op, where the
+// 32-bit v_mul_hi_u32 / v_mul_lo_u32 of KP_BARRETT issue at a quarter of that rate.
+__device__ uint32_t kp_mulhi_u24(uint32_t a, uint32_t b) __asm("llvm.amdgcn.mulhi.u24");
+__device__ uint32_t kp_mul_u24(uint32_t a, uint32_t b) __asm("llvm.amdgcn.mul.u24");
+#endif
 NX_DEV uint32_t kp_fastmod(uint32_t x, const FastMod32& f) {
-#ifdef KP_BARRETT
+#if defined(KP_FASTMOD24)
+    const uint32_t q = kp_mulhi_u24(x >> 8, f.m24);
+    const uint32_t r = x - kp_mul_u24(q, f.d);
+    return min(r, r - f.d);
+#elif defined(KP_BARRETT)
     // q' = floor(x * floor(2^32/d) / 2^32) is q or q-1, so r' < 2d and one
     // unsigned min(r', r'-d) finishes it (r'-d wraps high when r' < d).
     const uint32_t r = x - __umulhi(x, f.mb) * f.d;

@@ -15,6 +15,8 @@ struct FastMod32 {
     uint32_t m;
     uint32_t s;  // ceil(log2 d), >= 1
     uint32_t mb; // floor(2^32 / d): Barrett estimate, off by at most one d (one min() fixes it)
+    uint32_t m24; // floor(2^40 / d) for 2^16 < d < 2^24 (else 0; 2^40/2^16 needs 25 bits): 24-bit Barrett, see kawpow_search.hip
+    uint32_t pad;
 };
 
 struct EthashDagParams {

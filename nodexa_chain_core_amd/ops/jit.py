@@ -94,7 +94,7 @@ def defines_for(dag_bytes: int, defines: tuple[str, ...] | None = None) -> tuple
     measured there: the structured form is not bit-exact, the pointer form is)."""
     d = DEFAULT_DEFINES if defines is None else tuple(defines)
     if dag_bytes >= 1 << 32:  # 32-bit buffer offsets: 64-bit pointers for DAGs of 4 GiB or more
-        d = tuple(x for x in d if x not in ("KP_BUFFER", "KP_SBUFFER"))
+        d = tuple(x for x in d if x not in ("KP_BUFFER", "KP_SBUFFER", "KP_FASTMOD24"))
     return d
 
 
