@@ -82,7 +82,7 @@ def _atomic_copy(src: str, dst: str) -> None:
 
 # Tuned variant of the search template (profiles/README.md has the sweep that
 # picked it); NODEXA_KAWPOW_DEFINES="A,B=1" overrides it ("none" = plain template).
-TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_SBUFFER", "KP_L1X4", "KP_BLOCK=512")
+TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_SBUFFER", "KP_L1X4", "KP_BLOCK=512", "KP_NT_DAG")
 _env = os.environ.get("NODEXA_KAWPOW_DEFINES")
 DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
     d for d in _env.split(",") if d and d != "none")
