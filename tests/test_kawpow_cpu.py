@@ -129,6 +129,11 @@ def test_search_variant_selection_by_dag_size(core):
     assert "KP_SBUFFER" not in big and "KP_BUFFER" not in big and "KP_DPP" in big
     assert "KP_BUFFER" not in jit.defines_for(above, ("KP_BUFFER", "KP_DPP"))
     assert "KP_FASTMOD24" not in jit.defines_for(above, ("KP_FASTMOD24", "KP_SBUFFER"))
+    # the 24-bit Barrett is exact only for 2^16 < items: small DAGs fall back to KP_BARRETT
+    assert "KP_FASTMOD24" in jit.defines_for(below, ("KP_FASTMOD24", "KP_BARRETT"))
+    tiny = (1 << 16) * 256
+    assert "KP_FASTMOD24" not in jit.defines_for(tiny, ("KP_FASTMOD24", "KP_BARRETT"))
+    assert "KP_FASTMOD24" in jit.defines_for(tiny + 256, ("KP_FASTMOD24", "KP_BARRETT"))
 
 
 def test_fastmod24_model_matches_modulo():

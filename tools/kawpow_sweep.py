@@ -25,6 +25,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", nargs="*", default=["tuned"])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--check-windows", type=int, default=4, help="nonce windows re-hashed per variant")
     a = ap.parse_args()
 
     import torch
@@ -36,7 +37,24 @@ def main() -> int:
     height = a.epoch * 7500 + 123
     period = height // 3
     # "tuned" = the production variant (ops/jit.py TUNED_DEFINES); "" = the plain template
-    variants = [jit.TUNED_DEFINES if v == "tuned" else tuple(x for x in v.split(",") if x) for v in a.variants]
+    # "tuned-X+Y" = the production variant without X and with Y. Every variant goes through
+    # jit.defines_for, so at epochs with a DAG of 4 GiB or more the 32-bit buffer forms become
+    # pointer loads.
+    import re
+
+    def parse(v):
+        if v.startswith("tuned"):
+            d = list(jit.TUNED_DEFINES)
+            for op, x in re.findall(r"([+-])([^+-]+)", v[len("tuned"):]):
+                if op == "-":
+                    d = [y for y in d if y != x]
+                elif x not in d:
+                    d.append(x)
+            return tuple(d)
+        return tuple(x for x in v.split(",") if x)
+
+    dag_bytes = _core.full_dataset_num_items(a.epoch) * 128
+    variants = list(dict.fromkeys(jit.defines_for(dag_bytes, parse(v)) for v in a.variants))
     paths = {v: jit.get(period, v) for v in variants}
     torch.cuda.set_device(0)
     ep = DeviceEpoch(a.epoch, device=0)
@@ -57,30 +75,37 @@ def main() -> int:
         h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header, start, 0,
                                nb[v], stream, *sargs)
 
-    # bit-exactness: every variant, target = all-pass, first shares re-hashed on the CPU
+    # bit-exactness: every variant, target = all-pass, EVERY returned share (up to the 64-slot
+    # ring) of several nonce windows re-hashed on the CPU golden model
     import struct
 
     ctx = _core.get_epoch_context(a.epoch)
     hh = bytes(header)
-    bad = 0
     for v in variants:
-        res.zero_()
-        h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header, 1000, (1 << 64) - 1,
-                               5120, stream, *sargs)
-        raw = res.cpu().numpy().tobytes()
-        n = min(struct.unpack_from("<I", raw, 0)[0], 64)
-        for i in range(min(n, 3)):
-            vals = struct.unpack_from("<Q8I8I", raw, 16 + i * 72)
-            fin, mix = _core.kawpow_hash(ctx, height, hh, vals[0])
-            ok = struct.pack("<8I", *vals[1:9]) == mix and struct.pack("<8I", *vals[9:17]) == fin
-            bad += not ok
-        print(json.dumps({"variant": ",".join(v) or "base", "shares": n, "bitexact": bad == 0}), flush=True)
+        bad = checked = 0
+        for w in range(a.check_windows):
+            res.zero_()
+            h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header,
+                                   1000 + w * 7919 * 5120, (1 << 64) - 1, 5120, stream, *sargs)
+            raw = res.cpu().numpy().tobytes()
+            n = min(struct.unpack_from("<I", raw, 0)[0], 64)
+            for i in range(n):
+                vals = struct.unpack_from("<Q8I8I", raw, 16 + i * 72)
+                fin, mix = _core.kawpow_hash(ctx, height, hh, vals[0])
+                ok = struct.pack("<8I", *vals[1:9]) == mix and struct.pack("<8I", *vals[9:17]) == fin
+                bad += not ok
+                checked += 1
+        print(json.dumps({"variant": ",".join(v) or "base", "shares_checked": checked, "mismatches": bad,
+                          "bitexact": bad == 0 and checked > 0}), flush=True)
     for v in variants:  # warm
         run(v, 0)
     torch.cuda.synchronize()
     times = {v: [] for v in variants}
+    nv = len(variants)
     for r in range(a.rounds):
-        for v in variants:
+        # rotate the order every round so position effects (clock drift, L2 state left by the
+        # previous variant) are spread evenly over the variants
+        for v in variants[r % nv:] + variants[:r % nv]:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             run(v, (r + 1) * a.batch)
