@@ -83,6 +83,31 @@ struct EquihashDev {
     uint32_t* sols;         // [inst][1 + MAX_SOL*512]: count, then solutions
 };
 
+// Private-slot Equihash(200,9) solver (equihash_ps.hip). Each round runs `groups` (P)
+// workgroups per instance; workgroup w owns a `seg`-row (C) segment of every bucket of the
+// level it writes and allocates its slots with LDS atomics, so no global atomic is issued per
+// row (the global-slot solver's per-row atomics execute at the memory side and bound its
+// rounds: profiles/README r2c). P * C = EQP_SLOTS rows of address space per bucket.
+#define EQP_SLOTS 2048
+#define EQP_STAGE 768      // rows of one bucket staged in LDS (mean 512, sd ~23)
+#define EQP_REF_STRIDE 1024  // refs per bucket: a 10-bit staged index
+#define EQP_STATS 16
+#define EQP_FINAL_GROUPS 1024  // final-round workgroups per instance (it writes no level)
+struct EquihashPsDev {
+    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashDev)
+    uint64_t h0[8];
+    uint32_t input_len;
+    uint32_t num_inst;
+    uint32_t groups;        // P: workgroups per instance per round (a power of two <= 256)
+    uint32_t seg;           // C: rows per (bucket, workgroup) segment, EQP_SLOTS / P
+    uint32_t* hashes;       // [2][inst][BUCKETS][P][C][WORDS]: word 0 = back-pointer, 1..7 = row
+    uint32_t* refs;         // [inst][LEVELS][BUCKETS][EQP_REF_STRIDE] in staged (compact) order
+    uint8_t* counts;        // [inst][LEVELS][P][BUCKETS] rows per segment (clamped to C)
+    uint32_t* cands;        // [inst][1 + 2*MAX_CAND]: count, then (bucket << 10 | index) pairs at level 8
+    uint32_t* sols;         // [inst][1 + MAX_SOL*512]
+    uint32_t* stats;        // [inst][EQP_STATS]: rows dropped per level (segment or staging overflow)
+};
+
 // Batch verification of packed Equihash(200,9) solutions (equihash.hip eq_verify).
 #define EQ_SOL_WORDS 336  // 1344 bytes = 512 x 21-bit big-endian indices
 struct EquihashVerifyParams {

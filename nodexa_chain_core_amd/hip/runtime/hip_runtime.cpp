@@ -423,6 +423,46 @@ PYBIND11_MODULE(_hip, m) {
                                                    sols, banks);
         issue_equihash_solve(ks, p, as_stream(stream));
     });
+    // Private-slot solver (equihash_ps.hip): ks = [eqp_gen, eqp_round1..8, eqp_final,
+    // eqp_reconstruct]; `groups` workgroups per instance per round, EQP_SLOTS / groups rows per
+    // segment. Buffers as documented on EquihashPsDev.
+    m.attr("EQP_SLOTS") = EQP_SLOTS;
+    m.attr("EQP_STAGE") = EQP_STAGE;
+    m.attr("EQP_REF_STRIDE") = EQP_REF_STRIDE;
+    m.attr("EQP_STATS") = EQP_STATS;
+    m.def("launch_equihash_ps_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
+                                         uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uint32_t groups,
+                                         uintptr_t hashes, uintptr_t refs, uintptr_t counts, uintptr_t cands,
+                                         uintptr_t sols, uintptr_t stats, uintptr_t stream) {
+        if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash_ps kernels");
+        if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
+        if (input_len > 124 || num_inst == 0 || num_inst > 65535) throw std::invalid_argument("bad equihash geometry");
+        // P a power of two in [16, 256]: C = EQP_SLOTS / P fits the u8 counts and P the one-wave scan
+        if (groups < 16 || groups > 256 || (groups & (groups - 1))) throw std::invalid_argument("groups: 16..256, 2^k");
+        EquihashPsDev p{};
+        p.msgs = reinterpret_cast<const uint64_t*>(msgs);
+        for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
+        p.input_len = input_len;
+        p.num_inst = num_inst;
+        p.groups = groups;
+        p.seg = EQP_SLOTS / groups;
+        p.hashes = reinterpret_cast<uint32_t*>(hashes);
+        p.refs = reinterpret_cast<uint32_t*>(refs);
+        p.counts = reinterpret_cast<uint8_t*>(counts);
+        p.cands = reinterpret_cast<uint32_t*>(cands);
+        p.sols = reinterpret_cast<uint32_t*>(sols);
+        p.stats = reinterpret_cast<uint32_t*>(stats);
+        hipStream_t s = as_stream(stream);
+        const size_t n = num_inst;
+        check(hipMemsetAsync(p.cands, 0, n * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
+        check(hipMemsetAsync(p.sols, 0, n * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
+        check(hipMemsetAsync(p.stats, 0, n * EQP_STATS * 4, s), "memset stats");
+        // counts need no clear: every workgroup writes its whole row of every level
+        const dim3 grid(groups, num_inst);
+        for (size_t k = 0; k < 9; ++k) ks[k]->launch_bytes(grid, dim3(512), 0, s, &p, sizeof(p));
+        ks[9]->launch_bytes(dim3(EQP_FINAL_GROUPS, num_inst), dim3(512), 0, s, &p, sizeof(p));
+        ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
+    });
     // The 11 kernel launches captured once into a hipGraph (fixed device buffers, so the graph
     // stays valid across batches; only the message words change, in place). Per batch: 3
     // memsets + one hipGraphLaunch instead of 14 stream operations.

@@ -6,9 +6,10 @@ launch sequence — 1 BLAKE2b generation kernel, 8 collision rounds, the final
 host synchronisation in between. Every solution the GPU returns is re-verified
 by the CPU golden verifier (`_core.equihash_verify`) before it is reported.
 
-Memory per instance: 2 x 4096 x 640 x 32 B row buffers (168 MB) + 9 levels of
-index refs (94 MB) — 8 instances use ~2.1 GB of the 288 GB HBM3E, and one
-instance's live level (~67 MB) fits the 256 MiB Infinity Cache.
+Memory per instance, private-slot engine (default): 2 x 4096 x 2048 x 32 B row
+buffers (537 MB of address space, ~67 MB written per level) + 9 levels of
+index refs (151 MB) — 8 instances use ~5.5 GB of the 288 GB HBM3E. The
+global-slot engine needs 2 x 4096 x 768 x 32 B (201 MB) + 113 MB of refs.
 """
 from __future__ import annotations
 
@@ -22,6 +23,11 @@ from ..utils.trace import traced
 from . import runtime
 
 KERNELS = ["eq_gen"] + [f"eq_round{r}" for r in range(1, 9)] + ["eq_final", "eq_reconstruct"]
+PS_KERNELS = ["eqp_gen"] + [f"eqp_round{r}" for r in range(1, 9)] + ["eqp_final", "eqp_reconstruct"]
+# "ps": private slot segments per workgroup, pipelined rounds, 16-byte rows from level 5
+# (equihash_ps.hip; 5.64 ms per 8 solves, profiles/README r2d); "global": one global slot atomic
+# per row (equihash.hip; 6.54 ms). NODEXA_EQ_ENGINE overrides the default.
+DEFAULT_ENGINE = os.environ.get("NODEXA_EQ_ENGINE", "ps")
 
 
 def blake2b_h0(n: int = 200, k: int = 9) -> list[int]:
@@ -76,9 +82,15 @@ def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | 
 
 class EquihashSolver:
     def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 8,
-                 code_object: str | None = None):
-        """`code_object`: path of an alternative build of equihash.hip (tuning sweeps)."""
+                 code_object: str | None = None, engine: str | None = None, groups: int = 64):
+        """`code_object`: path of an alternative build of the engine's .hip (tuning sweeps).
+        `engine`: "ps" (private slot segments, `groups` workgroups per instance per round) or
+        "global" (global slot atomics, `banks` counters per bucket)."""
+        self.engine = DEFAULT_ENGINE if engine is None else engine
+        if self.engine not in ("ps", "global"):
+            raise ValueError(f"unknown Equihash engine {self.engine!r}")
         self.banks = int(banks)
+        self.groups = int(groups)
         runtime.require_gpu()
         self.h = runtime.hip()
         self.num_inst = int(num_inst)
@@ -86,15 +98,25 @@ class EquihashSolver:
         self.params = _core.EquihashParams(200, 9)
         B, C, W, L = self.h.EQ_BUCKETS, self.h.EQ_CAP, self.h.EQ_WORDS, self.h.EQ_LEVELS
         ni = self.num_inst
+        ps = self.engine == "ps"
+        module, names = ("equihash_ps", PS_KERNELS) if ps else ("equihash", KERNELS)
         with torch.cuda.device(self.device):
             if code_object is None:
-                self.kernels = [runtime.static_kernel("equihash", k) for k in KERNELS]
+                self.kernels = [runtime.static_kernel(module, k) for k in names]
             else:
                 co = runtime.load_code_object(code_object)
-                self.kernels = [co.function(k) for k in KERNELS]
-            self.hashes = torch.empty(2 * ni * B * C * W, dtype=torch.int32, device=self.device)
-            self.refs = torch.empty(ni * L * B * C, dtype=torch.int32, device=self.device)
-            self.counts = torch.empty(ni * (L + 1) * B * self.h.EQ_MAX_BANKS, dtype=torch.int32, device=self.device)
+                self.kernels = [co.function(k) for k in names]
+            if ps:
+                S, R = self.h.EQP_SLOTS, self.h.EQP_REF_STRIDE
+                self.hashes = torch.empty(2 * ni * B * S * W, dtype=torch.int32, device=self.device)
+                self.refs = torch.empty(ni * L * B * R, dtype=torch.int32, device=self.device)
+                self.counts = torch.empty(ni * L * self.groups * B, dtype=torch.uint8, device=self.device)
+                self.stats_buf = torch.zeros(ni * self.h.EQP_STATS, dtype=torch.int32, device=self.device)
+            else:
+                self.hashes = torch.empty(2 * ni * B * C * W, dtype=torch.int32, device=self.device)
+                self.refs = torch.empty(ni * L * B * C, dtype=torch.int32, device=self.device)
+                self.counts = torch.empty(ni * (L + 1) * B * self.h.EQ_MAX_BANKS, dtype=torch.int32,
+                                          device=self.device)
             self.cands = torch.empty(ni * (1 + 2 * self.h.EQ_MAX_CAND), dtype=torch.int32, device=self.device)
             self.sols = torch.empty(ni * (1 + self.h.EQ_MAX_SOL * 512), dtype=torch.int32, device=self.device)
             self.msgs = torch.zeros(ni * 16, dtype=torch.int64, device=self.device)
@@ -107,8 +129,9 @@ class EquihashSolver:
         self._next = 0
         self.h0 = blake2b_h0()
         # hipGraph of the 11 solve kernels (captured on first launch; the 3 state clears stay
-        # stream memsets). Opt-in (NODEXA_EQ_GRAPH=1) until measured: see profiles/README r1u
-        self.use_graph = os.environ.get("NODEXA_EQ_GRAPH", "0") == "1"
+        # stream memsets). Opt-in (NODEXA_EQ_GRAPH=1, global engine) until measured: see
+        # profiles/README r1u
+        self.use_graph = os.environ.get("NODEXA_EQ_GRAPH", "0") == "1" and not ps
         self._graph = None
         self.input_len = None
 
@@ -132,23 +155,32 @@ class EquihashSolver:
             stage.copy_(torch.frombuffer(buf, dtype=torch.int64))
             self.msgs.copy_(stage, non_blocking=True)
             s = runtime.current_stream_handle() if stream is None else stream
-            args = (self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst, self.hashes.data_ptr(),
-                    self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(), self.sols.data_ptr())
-            if self.use_graph and self._graph is None:
-                try:
-                    self._graph = self.h.capture_equihash_solve(*args, self.banks)
-                except RuntimeError:
-                    self.use_graph = False  # capture unsupported here: plain launches
-            if self._graph is not None:
-                self._graph.launch(s)
+            if self.engine == "ps":
+                self.h.launch_equihash_ps_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
+                                                self.num_inst, self.groups, self.hashes.data_ptr(),
+                                                self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
+                                                self.sols.data_ptr(), self.stats_buf.data_ptr(), s)
             else:
-                self.h.launch_equihash_solve(*args, s, self.banks)
+                self._issue_global(s)
             land = self._landing[self._next]
             self._next = (self._next + 1) % len(self._landing)
             land.copy_(self.sols, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
         self._pending.append((list(inputs), land, ev))
+
+    def _issue_global(self, s: int) -> None:
+        args = (self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst, self.hashes.data_ptr(),
+                self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(), self.sols.data_ptr())
+        if self.use_graph and self._graph is None:
+            try:
+                self._graph = self.h.capture_equihash_solve(*args, self.banks)
+            except RuntimeError:
+                self.use_graph = False  # capture unsupported here: plain launches
+        if self._graph is not None:
+            self._graph.launch(s)
+        else:
+            self.h.launch_equihash_solve(*args, s, self.banks)
 
     def collect(self, inputs: list[bytes] | None = None, verify: bool = True) -> list[list[list[int]]]:
         """Solutions of the oldest queued launch (waits only for that launch)."""
@@ -181,8 +213,13 @@ class EquihashSolver:
         return self.collect(inputs)
 
     def stats(self) -> dict:
-        """Per-level bucket fill of the last solve (instance 0) — overflow diagnostics."""
+        """Per-level fill of the last solve (instance 0) — overflow diagnostics."""
         B, L = self.h.EQ_BUCKETS, self.h.EQ_LEVELS
+        if self.engine == "ps":
+            c = self.counts[: L * self.groups * B].view(L, self.groups, B).to(torch.int32).sum(1).cpu()
+            dropped = self.stats_buf[: self.h.EQP_STATS].cpu().tolist()
+            return {"rows_per_level": [int(x) for x in c.sum(1)], "max_fill": [int(x) for x in c.max(1).values],
+                    "cap": self.h.EQP_STAGE, "dropped_per_level": dropped[:L], "candidates": int(self.cands[0].item())}
         nb = self.h.EQ_MAX_BANKS
         per = self.h.EQ_CAP // self.banks
         c = self.counts[: (L + 1) * B * nb].view(L + 1, B, nb)[:, :, :self.banks].cpu()

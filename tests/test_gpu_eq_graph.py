@@ -1,5 +1,6 @@
-"""Equihash solve sequence replayed from a hipGraph (ops/equihash.py, capture_equihash_solve):
-same solutions as direct launches, across several replays with new inputs in between."""
+"""Equihash solve sequence replayed from a hipGraph (ops/equihash.py, capture_equihash_solve; the
+global-slot engine): same solutions as direct launches, across several replays with new inputs in
+between."""
 import os
 
 import pytest
@@ -14,10 +15,10 @@ def test_graph_replays_match_direct_launches():
 
     os.environ["NODEXA_EQ_GRAPH"] = "1"
     try:
-        g = EquihashSolver(num_inst=4, device=0)
+        g = EquihashSolver(num_inst=4, device=0, engine="global")
     finally:
         del os.environ["NODEXA_EQ_GRAPH"]
-    d = EquihashSolver(num_inst=4, device=0)
+    d = EquihashSolver(num_inst=4, device=0, engine="global")
     assert g.use_graph and not d.use_graph
     key = lambda sols: [sorted(map(tuple, s)) for s in sols]  # noqa: E731
     for rep in range(4):

@@ -4,11 +4,17 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def solver(gpu):
+@pytest.fixture(scope="module", params=["global", "ps"])
+def solver(gpu, request):
+    """Both engines: global slot atomics (equihash.hip) and private slot segments (equihash_ps.hip)."""
+    import torch
+
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
-    return EquihashSolver(num_inst=4, device=0)
+    s = EquihashSolver(num_inst=4, device=0, engine=request.param)
+    yield s
+    del s
+    torch.cuda.empty_cache()
 
 
 def test_blake2b_h0_matches_cpu(core):
@@ -25,6 +31,9 @@ def test_gpu_solutions_valid_and_match_cpu(core, solver):
     gpu = solver.solve(inputs)  # every solution already CPU-verified inside collect()
     st = solver.stats()
     assert max(st["max_fill"]) <= st["cap"], st
+    if solver.engine == "ps":
+        assert sum(st["dropped_per_level"]) < 64, st  # segment / staging overflow stays rare
+        assert min(st["rows_per_level"]) > 1_900_000, st
     total_gpu = sum(len(s) for s in gpu)
     total_cpu = 0
     for inp, g in zip(inputs, gpu):

@@ -45,6 +45,7 @@ def main() -> int:
     ap.add_argument("--banks", type=int, nargs="*", default=[8])
     ap.add_argument("--variants", nargs="*", default=[""])
     ap.add_argument("--compile-only", action="store_true")
+    ap.add_argument("--engines", nargs="*", default=["global"], help="global and/or ps[:groups]")
     a = ap.parse_args()
     variants = [tuple(x for x in v.split(",") if x) for v in a.variants]
     objs = {v: variant_object(v) for v in variants}
@@ -55,8 +56,20 @@ def main() -> int:
 
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
-    cfgs = [(b, v) for v in variants for b in a.banks]
-    solvers = {c: EquihashSolver(num_inst=a.inst, device=0, banks=c[0], code_object=objs[c[1]]) for c in cfgs}
+    cfgs = []
+    for e in a.engines:
+        if e == "global":
+            cfgs += [(b, v) for v in variants for b in a.banks]
+        else:  # "ps" or "ps:<groups>": the private-slot engine (its own .hip, no variants)
+            cfgs.append((e, ()))
+
+    def make(c):
+        if isinstance(c[0], str):
+            g = int(c[0].split(":")[1]) if ":" in c[0] else 64
+            return EquihashSolver(num_inst=a.inst, device=0, engine="ps", groups=g)
+        return EquihashSolver(num_inst=a.inst, device=0, engine="global", banks=c[0], code_object=objs[c[1]])
+
+    solvers = {c: make(c) for c in cfgs}
     batches = [[os.urandom(112) for _ in range(a.inst)] for _ in range(a.batches + 1)]
     for s in solvers.values():
         s.solve(batches[0])
