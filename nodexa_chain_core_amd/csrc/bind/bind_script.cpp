@@ -1,0 +1,188 @@
+// Bindings for secp256k1 (crypto/secp256k1.*) and the script interpreter (chain/interpreter.*).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../chain/interpreter.hpp"
+#include "../crypto/secp256k1.hpp"
+
+namespace py = pybind11;
+using namespace nodexa;
+
+namespace {
+
+Bytes bytes_of(const py::bytes& b) {
+    std::string s = b;
+    return Bytes(s.begin(), s.end());
+}
+py::bytes pyb(const u8* p, size_t n) { return py::bytes(reinterpret_cast<const char*>(p), n); }
+py::bytes pyb(const Bytes& b) { return pyb(b.data(), b.size()); }
+
+void need32(const std::string& s, const char* what) {
+    if (s.size() != 32) throw std::invalid_argument(std::string(what) + " must be 32 bytes");
+}
+
+Transaction tx_of(const py::bytes& raw) {
+    const Bytes b = bytes_of(raw);
+    Reader r(b);
+    Transaction tx = Transaction::deserialize(r, true);
+    if (!r.empty()) throw std::invalid_argument("trailing bytes after transaction");
+    return tx;
+}
+
+std::vector<Bytes> stack_of(const std::vector<py::bytes>& v) {
+    std::vector<Bytes> out;
+    out.reserve(v.size());
+    for (auto& x : v) out.push_back(bytes_of(x));
+    return out;
+}
+
+}  // namespace
+
+void bind_script(py::module_& m) {
+    // ---------------------------------------------------------------- secp256k1
+    m.def("secp_pubkey_create", [](const py::bytes& key, bool compressed) -> py::object {
+        const std::string k = key;
+        need32(k, "key");
+        secp::Ge p;
+        if (!secp::pubkey_create(reinterpret_cast<const u8*>(k.data()), p)) return py::none();
+        u8 out[65];
+        return pyb(out, secp::pubkey_serialize(p, compressed, out));
+    }, py::arg("key"), py::arg("compressed") = true, "public key of a 32-byte secret (None if invalid)");
+    m.def("secp_pubkey_normalize", [](const py::bytes& pub, bool compressed) -> py::object {
+        const std::string s = pub;
+        secp::Ge p;
+        if (!secp::pubkey_parse(reinterpret_cast<const u8*>(s.data()), s.size(), p)) return py::none();
+        u8 out[65];
+        return pyb(out, secp::pubkey_serialize(p, compressed, out));
+    }, py::arg("pubkey"), py::arg("compressed") = true, "parse (02/03/04/06/07) and re-serialize, None if invalid");
+    m.def("secp_sign", [](const py::bytes& msg, const py::bytes& key) -> py::object {
+        const std::string m32 = msg, k = key;
+        need32(m32, "msg");
+        need32(k, "key");
+        secp::Scalar r, s;
+        if (!secp::ecdsa_sign(reinterpret_cast<const u8*>(m32.data()), reinterpret_cast<const u8*>(k.data()), r, s))
+            return py::none();
+        u8 der[72];
+        return pyb(der, secp::sig_serialize_der(r, s, der));
+    }, "RFC 6979 low-S DER signature (CKey::Sign with test_case 0)");
+    m.def("secp_verify", [](const py::bytes& pub, const py::bytes& sig, const py::bytes& msg) {
+        const std::string p = pub, sg = sig, m32 = msg;
+        need32(m32, "msg");
+        return secp::verify_der(reinterpret_cast<const u8*>(p.data()), p.size(), reinterpret_cast<const u8*>(sg.data()),
+                                sg.size(), reinterpret_cast<const u8*>(m32.data()));
+    }, "CPubKey::Verify: lax DER, S normalised");
+    m.def("secp_sign_compact", [](const py::bytes& msg, const py::bytes& key, bool compressed) -> py::object {
+        const std::string m32 = msg, k = key;
+        need32(m32, "msg");
+        need32(k, "key");
+        u8 out[65];
+        if (!secp::sign_compact(reinterpret_cast<const u8*>(m32.data()), reinterpret_cast<const u8*>(k.data()),
+                                compressed, out))
+            return py::none();
+        return pyb(out, 65);
+    });
+    m.def("secp_recover_compact", [](const py::bytes& msg, const py::bytes& sig) -> py::object {
+        const std::string m32 = msg, s = sig;
+        need32(m32, "msg");
+        if (s.size() != 65) return py::none();
+        secp::Ge p;
+        bool compressed = false;
+        if (!secp::recover_compact(reinterpret_cast<const u8*>(m32.data()), reinterpret_cast<const u8*>(s.data()), p,
+                                   compressed))
+            return py::none();
+        u8 out[65];
+        return pyb(out, secp::pubkey_serialize(p, compressed, out));
+    });
+    m.def("secp_seckey_tweak_add", [](const py::bytes& key, const py::bytes& tweak) -> py::object {
+        std::string k = key;
+        const std::string t = tweak;
+        need32(k, "key");
+        need32(t, "tweak");
+        if (!secp::seckey_tweak_add(reinterpret_cast<u8*>(k.data()), reinterpret_cast<const u8*>(t.data())))
+            return py::none();
+        return py::bytes(k);
+    });
+    m.def("secp_pubkey_tweak_add", [](const py::bytes& pub, const py::bytes& tweak) -> py::object {
+        const std::string p = pub, t = tweak;
+        need32(t, "tweak");
+        secp::Ge g;
+        if (!secp::pubkey_parse(reinterpret_cast<const u8*>(p.data()), p.size(), g)) return py::none();
+        if (!secp::pubkey_tweak_add(g, reinterpret_cast<const u8*>(t.data()))) return py::none();
+        u8 out[65];
+        return pyb(out, secp::pubkey_serialize(g, p.size() == 33, out));
+    });
+    m.def("secp_seckey_valid", [](const py::bytes& key) {
+        const std::string k = key;
+        return k.size() == 32 && secp::seckey_valid(reinterpret_cast<const u8*>(k.data()));
+    });
+    // DER signature normalisation helpers used by policy and the GPU batch packer
+    m.def("secp_der_to_rs", [](const py::bytes& sig) -> py::object {
+        const std::string s = sig;
+        secp::Scalar r, sv;
+        if (!secp::sig_parse_der_lax(reinterpret_cast<const u8*>(s.data()), s.size(), r, sv)) return py::none();
+        if (secp::sc_is_high(sv)) sv = secp::sc_neg(sv);
+        u8 out[64];
+        secp::sc_to_be(r, out);
+        secp::sc_to_be(sv, out + 32);
+        return pyb(out, 64);
+    }, "lax-DER signature -> r || low-S s (32+32 bytes big-endian), None on a structural error");
+
+    // ---------------------------------------------------------------- interpreter
+    m.attr("SCRIPT_VERIFY_P2SH") = u32(SCRIPT_VERIFY_P2SH);
+    m.attr("STANDARD_SCRIPT_VERIFY_FLAGS") = kStandardScriptFlags;
+    m.attr("MANDATORY_SCRIPT_VERIFY_FLAGS") = kMandatoryScriptFlags;
+    m.def("script_flag_bits", [] {
+        py::dict d;
+        const std::pair<const char*, u32> f[] = {
+            {"NONE", SCRIPT_VERIFY_NONE}, {"P2SH", SCRIPT_VERIFY_P2SH}, {"STRICTENC", SCRIPT_VERIFY_STRICTENC},
+            {"DERSIG", SCRIPT_VERIFY_DERSIG}, {"LOW_S", SCRIPT_VERIFY_LOW_S}, {"NULLDUMMY", SCRIPT_VERIFY_NULLDUMMY},
+            {"SIGPUSHONLY", SCRIPT_VERIFY_SIGPUSHONLY}, {"MINIMALDATA", SCRIPT_VERIFY_MINIMALDATA},
+            {"DISCOURAGE_UPGRADABLE_NOPS", SCRIPT_VERIFY_DISCOURAGE_UPGRADABLE_NOPS},
+            {"CLEANSTACK", SCRIPT_VERIFY_CLEANSTACK}, {"CHECKLOCKTIMEVERIFY", SCRIPT_VERIFY_CHECKLOCKTIMEVERIFY},
+            {"CHECKSEQUENCEVERIFY", SCRIPT_VERIFY_CHECKSEQUENCEVERIFY}, {"WITNESS", SCRIPT_VERIFY_WITNESS},
+            {"DISCOURAGE_UPGRADABLE_WITNESS_PROGRAM", SCRIPT_VERIFY_DISCOURAGE_UPGRADABLE_WITNESS_PROGRAM},
+            {"MINIMALIF", SCRIPT_VERIFY_MINIMALIF}, {"NULLFAIL", SCRIPT_VERIFY_NULLFAIL},
+            {"WITNESS_PUBKEYTYPE", SCRIPT_VERIFY_WITNESS_PUBKEYTYPE}};
+        for (auto& [k, v] : f) d[k] = v;
+        return d;
+    }, "the reference's flag names (src/test/transaction_tests.cpp mapFlagNames)");
+    m.def("verify_script", [](const py::bytes& script_sig, const py::bytes& script_pubkey,
+                              const std::vector<py::bytes>& witness, u32 flags, const py::bytes& tx_raw, unsigned n_in,
+                              int64_t amount) {
+        const Transaction tx = tx_of(tx_raw);
+        if (n_in >= tx.vin.size()) throw std::invalid_argument("input index out of range");
+        const PrecomputedTx cache(tx);
+        const TxSigChecker checker(&tx, n_in, amount, &cache);
+        const std::vector<Bytes> wit = stack_of(witness);
+        ScriptError err = ScriptError::UNKNOWN_ERROR;
+        py::gil_scoped_release rel;
+        const bool ok = verify_script(bytes_of(script_sig), bytes_of(script_pubkey), &wit, flags, checker, &err);
+        py::gil_scoped_acquire acq;
+        return py::make_tuple(ok, script_error_name(err));
+    }, py::arg("script_sig"), py::arg("script_pubkey"), py::arg("witness"), py::arg("flags"), py::arg("tx"),
+       py::arg("n_in"), py::arg("amount"),
+       "VerifyScript of input n_in of the serialized tx -> (ok, error name)");
+    m.def("eval_script", [](const std::vector<py::bytes>& stack, const py::bytes& script, u32 flags) {
+        std::vector<Bytes> st = stack_of(stack);
+        ScriptError err = ScriptError::UNKNOWN_ERROR;
+        const bool ok = eval_script(st, bytes_of(script), flags, SigChecker(), SigVersion::BASE, &err);
+        py::list out;
+        for (auto& e : st) out.append(pyb(e));
+        return py::make_tuple(ok, script_error_name(err), out);
+    }, "EvalScript with no transaction context (signature checks fail)");
+    m.def("signature_hash", [](const py::bytes& script_code, const py::bytes& tx_raw, unsigned n_in, int hash_type,
+                               int64_t amount, int sigversion) {
+        const Transaction tx = tx_of(tx_raw);
+        const Uint256 h = signature_hash(bytes_of(script_code), tx, n_in, hash_type, amount,
+                                         sigversion ? SigVersion::WITNESS_V0 : SigVersion::BASE);
+        return pyb(h.data, 32);
+    }, py::arg("script_code"), py::arg("tx"), py::arg("n_in"), py::arg("hash_type"), py::arg("amount") = 0,
+       py::arg("sigversion") = 0, "SignatureHash (uint256 storage order)");
+    m.def("check_transaction", [](const py::bytes& tx_raw) { return check_transaction(tx_of(tx_raw)); },
+          "CheckTransaction reject reason, '' when valid");
+    m.def("script_sigop_count", [](const py::bytes& s, bool accurate) {
+        return script_sigop_count(bytes_of(s), accurate);
+    }, py::arg("script"), py::arg("accurate") = false);
+    m.def("script_is_push_only", [](const py::bytes& s) { return script_is_push_only(bytes_of(s)); });
+    m.def("is_valid_signature_encoding", [](const py::bytes& s) { return is_valid_signature_encoding(bytes_of(s)); });
+}

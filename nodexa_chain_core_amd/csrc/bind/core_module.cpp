@@ -27,6 +27,7 @@ std::string as_str(const py::bytes& b) { return std::string(b); }
 }  // namespace
 
 void bind_extra(py::module_& m);  // bind_extra.cpp: chain, X16R, Equihash
+void bind_script(py::module_& m);  // bind_script.cpp: secp256k1, script interpreter
 
 PYBIND11_MODULE(_core, m) {
     m.doc() = "nodexa native CPU core: crypto, ethash/KawPow golden model, Equihash, consensus";
@@ -167,4 +168,5 @@ PYBIND11_MODULE(_core, m) {
     m.def("kawpow_cpu_hashrate", &kawpow_cpu_hashrate, py::call_guard<py::gil_scoped_release>());
 
     bind_extra(m);
+    bind_script(m);
 }
