@@ -4,6 +4,7 @@
 
 #include "../chain/interpreter.hpp"
 #include "../crypto/secp256k1.hpp"
+#include "../crypto/secp256k1_model32.hpp"
 
 namespace py = pybind11;
 using namespace nodexa;
@@ -126,6 +127,36 @@ void bind_script(py::module_& m) {
         secp::sc_to_be(sv, out + 32);
         return pyb(out, 64);
     }, "lax-DER signature -> r || low-S s (32+32 bytes big-endian), None on a structural error");
+
+    // ---------------------------------------------------------------- GPU batch verification
+    m.attr("SECP_JOB_BYTES") = sizeof(SecpVerifyJob);
+    m.def("secp_pack_jobs", [](const py::list& items) {
+        // items: [(pubkey, der_sig_without_hashtype, msg32)] -> SecpVerifyJob array
+        std::string out(items.size() * sizeof(SecpVerifyJob), '\0');
+        auto* jobs = reinterpret_cast<SecpVerifyJob*>(&out[0]);
+        size_t k = 0;
+        for (auto it : items) {
+            auto t = it.cast<py::tuple>();
+            const std::string pub = t[0].cast<py::bytes>(), sig = t[1].cast<py::bytes>(),
+                              msg = t[2].cast<py::bytes>();
+            need32(msg, "msg");
+            secp::pack_verify_job(reinterpret_cast<const u8*>(pub.data()), pub.size(),
+                                  reinterpret_cast<const u8*>(sig.data()), sig.size(),
+                                  reinterpret_cast<const u8*>(msg.data()), jobs[k++]);
+        }
+        return py::bytes(out);
+    }, "pack (pubkey, DER signature, message) triples as gfx950 verify jobs");
+    m.def("secp_gen_table32", [] {
+        return py::bytes(reinterpret_cast<const char*>(secp::gen_table32()), 64 * 16 * 16 * 4);
+    }, "the device comb table of G (64 KiB)");
+    m.def("secp_verify_model32", [](const py::bytes& pub, const py::bytes& sig, const py::bytes& msg) {
+        const std::string p = pub, sg = sig, m32 = msg;
+        need32(m32, "msg");
+        SecpVerifyJob job;
+        secp::pack_verify_job(reinterpret_cast<const u8*>(p.data()), p.size(), reinterpret_cast<const u8*>(sg.data()),
+                              sg.size(), reinterpret_cast<const u8*>(m32.data()), job);
+        return secp::verify_job_model32(job);
+    }, "the GPU verifier's 32-bit-limb arithmetic run on the host: 1 valid, 0 invalid, 2 degenerate");
 
     // ---------------------------------------------------------------- interpreter
     m.attr("SCRIPT_VERIFY_P2SH") = u32(SCRIPT_VERIFY_P2SH);

@@ -108,6 +108,26 @@ struct EquihashPsDev {
     uint32_t* stats;        // [inst][EQP_STATS]: rows dropped per level (segment or staging overflow)
 };
 
+// Batch ECDSA verification (secp256k1_verify.hip): one job per signature, limbs little-endian.
+#define SECP_KIND_UNCOMPRESSED 0u  // y given, checked on the curve
+#define SECP_KIND_EVEN 2u          // compressed, y recovered with even parity
+#define SECP_KIND_ODD 3u           // compressed, odd parity
+#define SECP_KIND_INVALID 0xffu    // host parsing already failed: result 0
+struct SecpVerifyJob {
+    uint32_t x[8], y[8];  // public key
+    uint32_t r[8], s[8];  // signature, s normalised to low-S, both in [0, n)
+    uint32_t z[8];        // message hash as a 256-bit big-endian integer (reduced mod n in-kernel)
+    uint32_t kind;
+    uint32_t pad[3];
+};
+struct SecpVerifyParams {
+    const struct SecpVerifyJob* jobs;
+    const uint32_t* gtab;  // 64 x 16 affine points j * 16^i * G, 16 limbs (x then y) each
+    uint32_t* out;         // per job: 1 valid, 0 invalid, 2 degenerate case (re-check on the host)
+    uint32_t n;
+    uint32_t pad;
+};
+
 // Batch verification of packed Equihash(200,9) solutions (equihash.hip eq_verify).
 #define EQ_SOL_WORDS 336  // 1344 bytes = 512 x 21-bit big-endian indices
 struct EquihashVerifyParams {

@@ -377,6 +377,19 @@ PYBIND11_MODULE(_hip, m) {
         k.launch_bytes(dim3(grid), dim3(256), 0, as_stream(stream), &p, sizeof(p));
     });
 
+    // ---- batch ECDSA verification (secp256k1_verify.hip): n SecpVerifyJob records -> n u32 verdicts
+    m.attr("SECP_JOB_BYTES") = sizeof(SecpVerifyJob);
+    m.def("launch_secp_verify", [](const Kernel& k, uintptr_t jobs, uint32_t n, uintptr_t gtab, uintptr_t out,
+                                   uintptr_t stream) {
+        if (n == 0) return;
+        SecpVerifyParams p{};
+        p.jobs = reinterpret_cast<const SecpVerifyJob*>(jobs);
+        p.gtab = reinterpret_cast<const uint32_t*>(gtab);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        p.n = n;
+        k.launch_bytes(dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
+
     // ---- Equihash(200,9): one full Wagner solve for `num_inst` inputs, enqueued on `stream`
     m.attr("EQ_BUCKETS") = EQ_BUCKETS;
     m.attr("EQ_CAP") = EQ_CAP;
