@@ -1,17 +1,26 @@
-"""Chain state: header chain + block files + the ProcessNewBlock pipeline.
+"""Chain state: header chain, block and undo files, the UTXO set and the ProcessNewBlock pipeline.
 
-Parity (behaviour): ProcessNewBlock -> CheckBlock -> AcceptBlock ->
-ActivateBestChain (src/validation.cpp:12131-12162, 12038, 11272) restricted to
-what the PoW engine owns: header PoW + contextual checks (C++ HeaderChain),
-structural block checks, the CLORE coinbase / community-fund rules
-(C++ validation.cpp), block storage in reference-format blk?????.dat files, tip
-selection by chain work, and the validation-interface signal bus
-(CValidationInterface, src/validationinterface.h:37-86). UTXO/script
-validation is DEFERred: non-coinbase transactions are carried
-opaquely and their fees are taken as declared by the template builder.
+Parity (behaviour): ProcessNewBlock -> CheckBlock -> AcceptBlock -> ActivateBestChain ->
+ConnectTip / DisconnectTip -> ConnectBlock / DisconnectBlock (src/validation.cpp:12131-12162,
+12038, 11272, 10958, 10052, 9479): header PoW + contextual checks (C++ HeaderChain), structural
+block checks, block storage in reference-format blk?????.dat files, tip selection by chain work,
+then the UTXO set (C++ CoinsView, chain/coins.hpp) follows the best header chain: every block is
+connected with its inputs, sequence locks, sigop cost and scripts checked, the CLORE coinbase /
+community-fund rules applied to the real fees, and undo data written to rev?????.dat
+(chain/undo.py) so a reorg can disconnect. AcceptToMemoryPool checks transactions against the
+same UTXO set. The validation-interface signal bus is CValidationInterface
+(src/validationinterface.h:37-86).
 
-On start-up the block index is rebuilt by scanning the blk files
-(`-reindex` semantics; SURVEY S5: COMPAT-read optional).
+Signatures in blocks are verified in one GPU batch per block when a GPU is present
+(ops/secp.verify_batch; the reference spreads them over its CCheckQueue CPU threads). The batch
+result is only trusted where it cannot differ from the reference: any input whose signature the
+batch rejects is re-run on the host, and a block whose deferred run fails is re-connected with
+host checks (`_connect_one`).
+
+The UTXO snapshot is chainstate/coins.dat (no LevelDB in this environment: SURVEY S6), flushed
+every `flush_interval` connected blocks and at shutdown; on start-up blocks stored past the
+snapshot are reconnected (ReplayBlocks-lite), and a snapshot whose best block is unknown is
+rebuilt from genesis.
 """
 from __future__ import annotations
 
@@ -24,6 +33,7 @@ from dataclasses import dataclass, field
 from .. import core
 from ..utils import log, sync
 from .blockindex import BlockIndexLog, scan_blk_tail
+from .undo import UndoStore
 from .versionbits import VersionBits
 
 _core = core()
@@ -83,6 +93,10 @@ class MempoolEntry:
 
 
 MEMPOOL_DUMP_VERSION = 1
+DEFAULT_MIN_RELAY_TX_FEE = 1_000_000   # sat per kvB (src/validation.h:69)
+MAX_STANDARD_TX_WEIGHT = 400_000       # src/policy/policy.h:28
+MAX_STANDARD_SCRIPTSIG_SIZE = 1650
+GPU_SIG_BATCH_MIN = 16                 # below this many signatures a block is checked on the host
 
 
 def _compact_size(n: int) -> bytes:
@@ -127,6 +141,12 @@ class ChainState:
         self.store = None
         self.start_time = time.time()
         self.index_log: BlockIndexLog | None = None
+        self._mem_blocks: dict[bytes, object] = {}  # block data when there is no datadir
+        self.min_relay_fee = DEFAULT_MIN_RELAY_TX_FEE
+        self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
+        self.flush_interval = 1000
+        self._since_flush = 0
+        self.sig_stats = {"gpu_batches": 0, "gpu_sigs": 0, "host_rechecks": 0}
         if datadir is not None:
             bdir = os.path.join(datadir, "blocks")
             os.makedirs(bdir, exist_ok=True)
@@ -141,6 +161,10 @@ class ChainState:
             self.block_pos[gh] = self.store.write(params.genesis)
             self.index_log.append(params.genesis.header.serialize(params.kawpow_activation_time),
                                   self.block_pos[gh], len(params.genesis.vtx))
+        self.undo = UndoStore(os.path.join(datadir, "blocks") if datadir else None, bytes(params.message_start))
+        self.coins_path = os.path.join(datadir, "chainstate", "coins.dat") if datadir else None
+        self.coins = _core.CoinsView()
+        self._init_coins()
 
     # ------------------------------------------------------------------ load / reindex
     def _load_block_files(self) -> None:
@@ -207,8 +231,10 @@ class ChainState:
         return True
 
     def close(self) -> None:
+        self.flush()
         if self.index_log is not None:
             self.index_log.close()
+        self.undo.close()
 
     # ------------------------------------------------------------------ signals
     def register(self, l: ValidationInterface) -> None:
@@ -238,14 +264,19 @@ class ChainState:
         return self.chain.block_hash(header)
 
     def get_block(self, h: bytes):
+        if self.store is None:
+            return self._mem_blocks.get(h)
         pos = self.block_pos.get(h)
-        if pos is None or self.store is None:
+        if pos is None:
             return None
         return self.store.read(pos)
 
     def get_block_raw(self, h: bytes) -> bytes | None:
+        if self.store is None:
+            blk = self._mem_blocks.get(h)
+            return None if blk is None else blk.serialize(self.params.kawpow_activation_time)
         pos = self.block_pos.get(h)
-        if pos is None or self.store is None:
+        if pos is None:
             return None
         return self.store.read_raw(pos)
 
@@ -344,7 +375,8 @@ class ChainState:
         return len(entries)
 
     def load_mempool(self, path: str) -> int:
-        """LoadMempool: re-adds every dumped tx (fees as the fee delta: no UTXO lookup)."""
+        """LoadMempool: every dumped tx goes through AcceptToMemoryPool again (its fee delta
+        restored); transactions no longer valid are dropped."""
         if not os.path.exists(path):
             return 0
         with open(path, "rb") as f:
@@ -358,8 +390,10 @@ class ChainState:
             off += used
             t, delta = struct.unpack_from("<qq", b, off)
             off += 16
-            self.add_to_mempool(tx, 0, float(t), delta)
-            n += 1
+            ok, _, fee = self.accept_to_mempool(tx, test_only=True)
+            if ok:
+                self.add_to_mempool(tx, fee, float(t), delta)
+                n += 1
         return n
 
     def record_confirmations(self, block, height: int) -> None:
@@ -384,12 +418,14 @@ class ChainState:
         r = self.chain.check_header(header, True)
         return ValidationState(r.ok, r.reject, r.dos)
 
-    def process_new_block(self, block, check_pow: bool = True, fees_known: bool | None = None) -> ValidationState:
-        """Validate + store + activate. Returns the BIP22-style state."""
+    def process_new_block(self, block, check_pow: bool = True) -> ValidationState:
+        """Validate + store + activate (ProcessNewBlock). Returns the BIP22-style state of this
+        block: invalid if it fails a context-free, contextual, header or connection rule. A
+        valid block on a lighter fork is stored (and connected later if its fork wins)."""
         with self.lock:
             h = self.chain.block_hash(block.header)
             existing = self.chain.find(h)
-            if existing is not None and h in self.block_pos:
+            if existing is not None and (h in self.block_pos or h in self._mem_blocks):
                 st = ValidationState.invalid("duplicate")
                 self._emit("block_checked", block, st)
                 return st
@@ -405,17 +441,10 @@ class ChainState:
                 return st
             height = prev.height + 1
             ok, reason, dos = _core.contextual_check_block(block, self.params, height)
-            if ok:
-                fees = sum(self.mempool[tx.txid()].fee for tx in block.vtx[1:] if tx.txid() in self.mempool)
-                known = (len(block.vtx) == 1) if fees_known is None else fees_known
-                if not known:
-                    known = all(tx.txid() in self.mempool for tx in block.vtx[1:])
-                ok, reason, dos = _core.check_coinbase_rewards(block, self.params, height, fees, known)
             if not ok:
                 st = ValidationState.invalid(reason, dos)
                 self._emit("block_checked", block, st)
                 return st
-            old_tip = self.chain.tip()
             r = self.chain.accept_header(block.header, self.adjusted_time(), check_pow)
             if not r.ok:
                 st = ValidationState.invalid(r.reject, r.dos)
@@ -427,19 +456,274 @@ class ChainState:
                                       len(block.vtx))
             else:
                 self.block_pos[h] = None
-            st = ValidationState()
+                self._mem_blocks[h] = block
             self.ntx[h] = len(block.vtx)
+            failed = self._activate()
+            st = failed.get(h, ValidationState())
             self._emit("block_checked", block, st)
-            self.record_confirmations(block, height)
-            for tx in block.vtx[1:]:
-                self.mempool.pop(tx.txid(), None)
-            new_tip = self.chain.tip()
+            return st
+
+    # ------------------------------------------------------------------ UTXO set / ActivateBestChain
+    def _init_coins(self) -> None:
+        """Load the UTXO snapshot and bring it to the best stored chain (ReplayBlocks-lite)."""
+        gh = self.chain.genesis().hash
+        loaded = self.coins_path is not None and self.coins.load(self.coins_path)
+        if not loaded or self.chain.find(self.coins.best_block) is None:
+            if loaded:
+                log.log_printf("UTXO snapshot's best block is unknown; rebuilding the UTXO set from genesis")
+            self.coins = _core.CoinsView()
+            self.coins.best_block = gh  # the genesis coinbase is unspendable: never added
+        with self.lock:
+            self._activate()
+
+    def coins_tip(self):
+        return self.chain.find(self.coins.best_block)
+
+    def invalidate_block(self, h: bytes) -> None:
+        """InvalidateBlock: mark the block (and its descendants) invalid and move the UTXO set to
+        the best remaining chain; the disconnected transactions go back to the mempool."""
+        with self.lock:
+            self.chain.invalidate(h)
+            self._activate()
+
+    def reconsider_block(self, h: bytes) -> None:
+        """ReconsiderBlock: clear the invalid flags and re-activate the best chain."""
+        with self.lock:
+            self.chain.reconsider(h)
+            self._activate()
+
+    def _fork_point(self, a, b):
+        while a.height > b.height:
+            a = self.chain.find(a.prev_hash)
+        while b.height > a.height:
+            b = self.chain.find(b.prev_hash)
+        while a.hash != b.hash:
+            a, b = self.chain.find(a.prev_hash), self.chain.find(b.prev_hash)
+        return a
+
+    def _activate(self) -> dict[bytes, ValidationState]:
+        """ActivateBestChain: move the UTXO set from its tip to the header chain's best tip,
+        disconnecting to the fork point and connecting every block whose data is stored. A block
+        that fails is marked invalid in the header chain (which re-selects its tip) and the walk
+        restarts. Returns the failed blocks' states."""
+        failed: dict[bytes, ValidationState] = {}
+        old_tip = self.coins_tip()
+        disconnected = []
+        connected = []
+        while True:
+            target = self.chain.tip()
+            cur = self.coins_tip()
+            if cur.hash == target.hash:
+                break
+            fork = self._fork_point(cur, target)
+            while cur.hash != fork.hash:
+                blk = self.get_block(cur.hash)
+                undo = self.undo.read(cur.hash, cur.prev_hash)
+                if blk is None or undo is None:
+                    raise RuntimeError(f"cannot disconnect {_core.u256_hex(cur.hash)}: block or undo data missing")
+                if not _core.disconnect_block(blk, undo, self.coins):
+                    log.log_printf(f"disconnect of {_core.u256_hex(cur.hash)} found an inconsistent UTXO set")
+                self.coins.best_block = cur.prev_hash
+                disconnected.append(blk)
+                cur = self.chain.find(cur.prev_hash)
+            path, x = [], target
+            while x.hash != fork.hash:
+                path.append(x)
+                x = self.chain.find(x.prev_hash)
+            restart = False
+            for idx in reversed(path):
+                blk = self.get_block(idx.hash)
+                if blk is None:
+                    break  # data not here yet (headers-first): stop at the last complete block
+                st = self._connect_one(blk, idx)
+                if not st.ok:
+                    failed[idx.hash] = st
+                    self.chain.invalidate(idx.hash)
+                    restart = True
+                    break
+                connected.append((blk, idx))
+            if not restart:
+                break
+        if disconnected or connected:
+            self._update_mempool(disconnected, [b for b, _ in connected])
+            for blk, idx in connected:
+                self._emit("block_connected", blk, idx)
+            new_tip = self.coins_tip()
             if new_tip.hash != old_tip.hash:
-                self._emit("block_connected", block, r.index)
                 self._emit("updated_block_tip", new_tip, old_tip, False)
                 self.cv_tip.notify_all()
                 log.log_print("validation", f"new tip {_core.u256_hex(new_tip.hash)} height {new_tip.height}")
-            return st
+        return failed
+
+    def _use_gpu_for(self, block) -> bool:
+        if self.gpu_signatures == "off":
+            return False
+        n_inputs = sum(len(tx.vin) for tx in block.vtx[1:])
+        if n_inputs < (1 if self.gpu_signatures == "on" else GPU_SIG_BATCH_MIN):
+            return False
+        try:
+            import torch
+
+            return torch.cuda.is_available()
+        except ImportError:  # pragma: no cover
+            return False
+
+    def _connect_one(self, block, idx) -> ValidationState:
+        """ConnectTip: connect `block` at `idx`, then the coinbase / community-fund rules on the
+        block's real fees; on any failure the UTXO set is left as it was."""
+        height = idx.height
+        prev = self.chain.find(idx.prev_hash)
+        mtp_prev = prev.median_time_past()
+
+        def mtp_at(h: int) -> int:
+            return self.chain.at_height(h).median_time_past()
+
+        flags = _core.BLOCK_SCRIPT_VERIFY_FLAGS
+        gpu = self._use_gpu_for(block)
+        res, undo = _core.connect_block(block, height, self.coins, True, gpu, mtp_at, mtp_prev, flags)
+        if gpu and not res.ok and "script-verify" in res.reject:
+            # a deferred (assume-valid) signature can flip a script that depends on a signature
+            # failing: the host run decides
+            res, undo = _core.connect_block(block, height, self.coins, True, False, mtp_at, mtp_prev, flags)
+        if not res.ok:
+            return ValidationState.invalid(res.reject, res.dos)
+        if gpu and res.num_sigs:
+            from ..ops import secp
+
+            verdicts = secp.verify_batch(res.sig_items())
+            self.sig_stats["gpu_batches"] += 1
+            self.sig_stats["gpu_sigs"] += len(verdicts)
+            for t, i in sorted({res.sig_at[k] for k, v in enumerate(verdicts) if not v}):
+                value, spk, _, _ = _core.block_undo_coin(undo, t, i)
+                self.sig_stats["host_rechecks"] += 1
+                ok, err = _core.verify_input_host(block, t, i, value, spk, flags)
+                if not ok:
+                    _core.disconnect_block(block, undo, self.coins)
+                    return ValidationState.invalid(f"mandatory-script-verify-flag-failed ({err})", 100)
+        ok, reason, dos = _core.check_coinbase_rewards(block, self.params, height, res.fees, True)
+        if not ok:
+            _core.disconnect_block(block, undo, self.coins)
+            return ValidationState.invalid(reason, dos)
+        self.undo.write(idx.hash, idx.prev_hash, undo)
+        self.coins.best_block = idx.hash
+        self.record_confirmations(block, height)
+        self._since_flush += 1
+        if self._since_flush >= self.flush_interval:
+            self.flush()
+        return ValidationState()
+
+    def flush(self) -> None:
+        """FlushStateToDisk: write the UTXO snapshot (atomically) if anything changed."""
+        if self.coins_path is None or self._since_flush == 0:
+            return
+        os.makedirs(os.path.dirname(self.coins_path), exist_ok=True)
+        self.coins.save(self.coins_path)
+        self._since_flush = 0
+
+    def _update_mempool(self, disconnected, connected) -> None:
+        """UpdateMempoolForReorg + removeForBlock: drop what the new blocks confirmed or
+        conflict with, return the disconnected blocks' transactions to the pool where they are
+        still valid, and evict anything whose inputs are gone."""
+        confirmed = {tx.txid() for blk in connected for tx in blk.vtx[1:]}
+        spent = {(i.prevout.hash, i.prevout.n) for blk in connected for tx in blk.vtx[1:] for i in tx.vin}
+        for txid in list(self.mempool):
+            e = self.mempool[txid]
+            if txid in confirmed or any((i.prevout.hash, i.prevout.n) in spent for i in e.tx.vin):
+                del self.mempool[txid]
+        for blk in reversed(disconnected):
+            for tx in blk.vtx[1:]:
+                self.accept_to_mempool(tx)
+        # evict transactions whose inputs are neither unspent outputs nor pool outputs
+        changed = True
+        while changed:
+            changed = False
+            for txid in list(self.mempool):
+                e = self.mempool[txid]
+                for i in e.tx.vin:
+                    if self.coins.get(i.prevout.hash, i.prevout.n) is None and i.prevout.hash not in self.mempool:
+                        del self.mempool[txid]
+                        changed = True
+                        break
+        self.transactions_updated += 1
+
+    # ------------------------------------------------------------------ AcceptToMemoryPool
+    def _spent_coin(self, prevout):
+        """(value, scriptPubKey, height, coinbase) of an unspent output, from the UTXO set or a
+        pool transaction (height = next block)."""
+        c = self.coins.get(prevout.hash, prevout.n)
+        if c is not None:
+            return c
+        e = self.mempool.get(prevout.hash)
+        if e is not None and prevout.n < len(e.tx.vout):
+            o = e.tx.vout[prevout.n]
+            return (o.value, o.script_pubkey, self.coins_tip().height + 1, False)
+        return None
+
+    def accept_to_mempool(self, tx, test_only: bool = False, max_fee: int | None = None) -> tuple[bool, str, int]:
+        """AcceptToMemoryPoolWorker (src/validation.cpp): context-free checks, standardness,
+        inputs present (UTXO set or pool), no pool conflict, coinbase maturity, fees and the
+        min relay fee, then every input script under the standard flags. Returns (accepted,
+        reject reason, fee)."""
+        with self.lock:
+            txid = tx.txid()
+            if txid in self.mempool:
+                return False, "txn-already-in-mempool", 0
+            raw = tx.serialize(True)
+            why = _core.check_transaction(raw)
+            if why:
+                return False, why, 0
+            if tx.is_coinbase():
+                return False, "coinbase", 0
+            if tx.version < 1 or tx.version > 2:
+                return False, "version", 0
+            weight = len(tx.serialize(False)) * 3 + len(raw)
+            if weight > MAX_STANDARD_TX_WEIGHT:
+                return False, "tx-size", 0
+            for i in tx.vin:
+                if len(i.script_sig) > MAX_STANDARD_SCRIPTSIG_SIZE:
+                    return False, "scriptsig-size", 0
+                if not _core.script_is_push_only(i.script_sig):
+                    return False, "scriptsig-not-pushonly", 0
+            pool_spent = {(i.prevout.hash, i.prevout.n) for e in self.mempool.values() for i in e.tx.vin}
+            tip = self.coins_tip()
+            next_height = tip.height + 1
+            # CheckFinalTx for the next block (IsFinalTx with the tip's median time past)
+            if tx.lock_time != 0 and any(i.sequence != 0xffffffff for i in tx.vin):
+                limit = next_height if tx.lock_time < 500_000_000 else tip.median_time_past()
+                if tx.lock_time >= limit:
+                    return False, "non-final", 0
+            in_sum, coins = 0, []
+            for i in tx.vin:
+                if (i.prevout.hash, i.prevout.n) in pool_spent:
+                    return False, "txn-mempool-conflict", 0
+                c = self._spent_coin(i.prevout)
+                if c is None:
+                    return False, "missing-inputs", 0
+                value, spk, h, coinbase = c
+                if coinbase and next_height - h < _core.COINBASE_MATURITY:
+                    return False, "bad-txns-premature-spend-of-coinbase", 0
+                in_sum += value
+                coins.append((value, spk))
+            fee = in_sum - tx.value_out()
+            if fee < 0:
+                return False, "bad-txns-in-belowout", 0
+            vsize = (weight + 3) // 4
+            if fee < self.min_relay_fee * vsize // 1000:
+                return False, "min relay fee not met", fee
+            if max_fee is not None and fee > max_fee:
+                return False, "absurdly-high-fee", fee
+            for k, (value, spk) in enumerate(coins):
+                vin = tx.vin[k]
+                ok, err = _core.verify_script(vin.script_sig, spk, list(vin.witness), _core.STANDARD_SCRIPT_VERIFY_FLAGS,
+                                              raw, k, value)
+                if not ok:
+                    ok2, _ = _core.verify_script(vin.script_sig, spk, list(vin.witness),
+                                                 _core.BLOCK_SCRIPT_VERIFY_FLAGS, raw, k, value)
+                    kind = "non-mandatory-script-verify-flag" if ok2 else "mandatory-script-verify-flag-failed"
+                    return False, f"{kind} ({err})", fee
+            if not test_only:
+                self.add_to_mempool(tx, fee)
+            return True, "", fee
 
     def wait_for_tip_change(self, old_hash: bytes, timeout: float) -> bool:
         with self.cv_tip:

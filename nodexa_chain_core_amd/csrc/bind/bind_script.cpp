@@ -2,12 +2,17 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <set>
+
+#include "../chain/coins.hpp"
 #include "../chain/interpreter.hpp"
 #include "../crypto/secp256k1.hpp"
 #include "../crypto/secp256k1_model32.hpp"
 
 namespace py = pybind11;
 using namespace nodexa;
+
+PYBIND11_MAKE_OPAQUE(std::vector<PendingSig>)
 
 namespace {
 
@@ -214,6 +219,128 @@ void bind_script(py::module_& m) {
     m.def("script_sigop_count", [](const py::bytes& s, bool accurate) {
         return script_sigop_count(bytes_of(s), accurate);
     }, py::arg("script"), py::arg("accurate") = false);
+    // ---------------------------------------------------------------- UTXO set / ConnectBlock
+    m.attr("COINBASE_MATURITY") = kCoinbaseMaturity;
+    m.attr("BLOCK_SCRIPT_VERIFY_FLAGS") = kBlockScriptFlags;
+    py::class_<CoinsView, std::shared_ptr<CoinsView>>(m, "CoinsView")
+        .def(py::init<>())
+        .def("__len__", &CoinsView::size)
+        .def("get", [](const CoinsView& v, const py::bytes& txid, u32 n) -> py::object {
+            OutPoint o;
+            const std::string h = txid;
+            need32(h, "txid");
+            o.hash = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
+            o.n = n;
+            const Coin* c = v.find(o);
+            if (!c) return py::none();
+            return py::make_tuple(c->out.value, pyb(c->out.script_pubkey), c->height, c->coinbase);
+        }, "(value, scriptPubKey, height, coinbase) of an unspent output, or None")
+        .def("height_of_txid", [](const CoinsView& v, const py::bytes& txid) -> py::object {
+            // AccessByTxid (src/coins.cpp): probe output indexes up to MAX_OUTPUTS_PER_BLOCK
+            // (MAX_BLOCK_WEIGHT / (WITNESS_SCALE_FACTOR * size of an empty CTxOut))
+            OutPoint o;
+            const std::string h = txid;
+            need32(h, "txid");
+            o.hash = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
+            for (o.n = 0; o.n < 8000000u / (4u * 9u); ++o.n)
+                if (const Coin* c = v.find(o)) return py::int_(c->height);
+            return py::none();
+        }, "height of the block holding a transaction with an unspent output, or None")
+        .def("add", [](CoinsView& v, const py::bytes& txid, u32 n, int64_t value, const py::bytes& spk, u32 height,
+                       bool coinbase) {
+            OutPoint o;
+            const std::string h = txid;
+            need32(h, "txid");
+            o.hash = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
+            o.n = n;
+            Coin c;
+            c.out.value = value;
+            c.out.script_pubkey = bytes_of(spk);
+            c.height = height;
+            c.coinbase = coinbase;
+            v.add(o, std::move(c));
+        })
+        .def_property("best_block", [](const CoinsView& v) { return pyb(v.best_block.data, 32); },
+                      [](CoinsView& v, const py::bytes& b) {
+                          const std::string h = b;
+                          need32(h, "best_block");
+                          v.best_block = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
+                      })
+        .def("save", &CoinsView::save, py::call_guard<py::gil_scoped_release>())
+        .def("load", &CoinsView::load, py::call_guard<py::gil_scoped_release>())
+        .def("stats", [](const CoinsView& v) {
+            const auto s = v.stats();
+            return py::make_tuple(s.txouts, s.transactions, s.total, pyb(s.hash.data, 32));
+        }, "(txouts, transactions, total amount, sha256d of the coins in outpoint order)")
+        .def("outputs_for_scripts", [](const CoinsView& v, const std::vector<py::bytes>& spks) {
+            std::set<Bytes> want;
+            for (auto& s : spks) want.insert(bytes_of(s));
+            py::list out;
+            v.for_each([&](const OutPoint& o, const Coin& c) {
+                if (want.count(c.out.script_pubkey))
+                    out.append(py::make_tuple(pyb(o.hash.data, 32), o.n, c.out.value, pyb(c.out.script_pubkey),
+                                              c.height, c.coinbase));
+            });
+            return out;
+        }, "unspent outputs paying any of these scriptPubKeys: (txid, n, value, spk, height, coinbase)");
+    py::class_<ConnectResult>(m, "ConnectResult")
+        .def_readonly("ok", &ConnectResult::ok)
+        .def_readonly("reject", &ConnectResult::reject)
+        .def_readonly("dos", &ConnectResult::dos)
+        .def_readonly("fees", &ConnectResult::fees)
+        .def_readonly("sigop_cost", &ConnectResult::sigop_cost)
+        .def_readonly("sig_at", &ConnectResult::sig_at)
+        .def_property_readonly("num_sigs", [](const ConnectResult& r) { return r.sigs.size(); })
+        .def("sig_items", [](const ConnectResult& r) {
+            py::list out;
+            for (auto& p : r.sigs) out.append(py::make_tuple(pyb(p.pubkey), pyb(p.sig), pyb(p.msg.data, 32)));
+            return out;
+        }, "deferred signatures as (pubkey, DER signature, message) for ops/secp.verify_batch");
+    m.def("connect_block", [](const Block& block, int height, CoinsView& view, bool check_scripts, bool defer_sigs,
+                              py::object mtp_at, int64_t block_mtp, u32 flags) {
+        ConnectOptions opt;
+        opt.script_flags = flags;
+        opt.check_scripts = check_scripts;
+        opt.defer_sigs = defer_sigs;
+        opt.block_mtp = block_mtp;
+        if (!mtp_at.is_none()) opt.mtp_at = [mtp_at](int h) { return mtp_at(h).cast<int64_t>(); };
+        BlockUndo undo;
+        ConnectResult r = connect_block(block, height, view, opt, undo);
+        py::bytes undo_bytes = r.ok ? pyb(serialize_block_undo(undo)) : py::bytes();
+        return py::make_tuple(std::move(r), undo_bytes);
+    }, py::arg("block"), py::arg("height"), py::arg("view"), py::arg("check_scripts") = true,
+       py::arg("defer_sigs") = false, py::arg("mtp_at") = py::none(), py::arg("block_mtp") = 0,
+       py::arg("flags") = kBlockScriptFlags,
+       "ConnectBlock against the view -> (ConnectResult, serialized CBlockUndo); the view is unchanged on failure");
+    m.def("disconnect_block", [](const Block& block, const py::bytes& undo, CoinsView& view) {
+        return disconnect_block(block, deserialize_block_undo(bytes_of(undo)), view);
+    }, "DisconnectBlock with its undo data: False if they did not match the view (it is still reverted)");
+    m.def("verify_input_host", [](const Block& block, u32 tx_index, u32 n_in, int64_t value, const py::bytes& spk,
+                                  u32 flags) {
+        if (tx_index >= block.vtx.size() || n_in >= block.vtx[tx_index].vin.size())
+            throw std::invalid_argument("no such input");
+        Coin c;
+        c.out.value = value;
+        c.out.script_pubkey = bytes_of(spk);
+        ScriptError err = ScriptError::UNKNOWN_ERROR;
+        const bool ok = verify_input_host(block.vtx[tx_index], n_in, c, flags, &err);
+        return py::make_tuple(ok, script_error_name(err));
+    });
+    m.def("block_undo_coin", [](const py::bytes& undo, u32 tx_index, u32 n_in) {
+        const BlockUndo u = deserialize_block_undo(bytes_of(undo));
+        if (tx_index == 0 || tx_index > u.vtxundo.size() || n_in >= u.vtxundo[tx_index - 1].prev.size())
+            throw std::invalid_argument("no such spent coin in the undo data");
+        const Coin& c = u.vtxundo[tx_index - 1].prev[n_in];
+        return py::make_tuple(c.out.value, pyb(c.out.script_pubkey), c.height, c.coinbase);
+    }, "the coin input n_in of transaction tx_index spent, from a block's undo data");
+    m.def("block_undo_roundtrip", [](const py::bytes& b) {
+        return pyb(serialize_block_undo(deserialize_block_undo(bytes_of(b))));
+    });
+    m.def("compress_amount", &compress_amount);
+    m.def("decompress_amount", &decompress_amount);
+    m.def("tx_legacy_sigops", [](const py::bytes& tx_raw) { return tx_legacy_sigops(tx_of(tx_raw)); },
+          "GetLegacySigOpCount of a transaction (no spent outputs needed)");
+
     m.def("script_is_push_only", [](const py::bytes& s) { return script_is_push_only(bytes_of(s)); });
     m.def("is_valid_signature_encoding", [](const py::bytes& s) { return is_valid_signature_encoding(bytes_of(s)); });
 }

@@ -1,0 +1,510 @@
+// UTXO set, undo data and block connection: see coins.hpp.
+#include "coins.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <fstream>
+#include <map>
+#include <set>
+
+#include "../crypto/secp256k1.hpp"
+#include "../crypto/sha256.hpp"
+
+namespace nodexa {
+
+// ------------------------------------------------------------------ CoinsView
+const Coin* CoinsView::find(const OutPoint& o) const {
+    auto it = map_.find(o);
+    return it == map_.end() ? nullptr : &it->second;
+}
+
+void CoinsView::add(const OutPoint& o, Coin c) { map_[o] = std::move(c); }
+
+bool CoinsView::spend(const OutPoint& o, Coin* moved) {
+    auto it = map_.find(o);
+    if (it == map_.end()) return false;
+    if (moved) *moved = std::move(it->second);
+    map_.erase(it);
+    return true;
+}
+
+namespace {
+
+constexpr char kCoinsMagic[8] = {'N', 'X', 'C', 'O', 'I', 'N', 'S', '1'};
+
+void write_coin_entry(Writer& w, const OutPoint& o, const Coin& c) {
+    w.u256(o.hash);
+    w.u32_(o.n);
+    w.u32_((c.height << 1) | (c.coinbase ? 1u : 0u));
+    w.i64_(c.out.value);
+    w.var_bytes(c.out.script_pubkey);
+}
+
+std::vector<std::pair<OutPoint, const Coin*>> sorted_coins(
+    const std::unordered_map<OutPoint, Coin, OutPointHasher, OutPointEq>& m) {
+    std::vector<std::pair<OutPoint, const Coin*>> v;
+    v.reserve(m.size());
+    for (auto& kv : m) v.emplace_back(kv.first, &kv.second);
+    std::sort(v.begin(), v.end(), [](auto& a, auto& b) {
+        const int c = std::memcmp(a.first.hash.data, b.first.hash.data, 32);
+        return c != 0 ? c < 0 : a.first.n < b.first.n;
+    });
+    return v;
+}
+
+}  // namespace
+
+void CoinsView::save(const std::string& path) const {
+    Writer w;
+    w.raw(reinterpret_cast<const u8*>(kCoinsMagic), 8);
+    w.u256(best_block);
+    w.u64_(map_.size());
+    for (auto& kv : map_) write_coin_entry(w, kv.first, kv.second);
+    u8 sum[32];
+    sha256d(w.buf.data(), w.buf.size(), sum);
+    w.raw(sum, 32);
+    const std::string tmp = path + ".new";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + tmp);
+    const bool ok = std::fwrite(w.buf.data(), 1, w.buf.size(), f) == w.buf.size() && std::fflush(f) == 0;
+    std::fclose(f);
+    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot replace " + path);
+}
+
+bool CoinsView::load(const std::string& path) {
+    map_.clear();
+    best_block = Uint256();
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    Bytes b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (b.size() < 8 + 32 + 8 + 32 || std::memcmp(b.data(), kCoinsMagic, 8) != 0) return false;
+    u8 sum[32];
+    sha256d(b.data(), b.size() - 32, sum);
+    if (std::memcmp(sum, b.data() + b.size() - 32, 32) != 0) return false;
+    try {
+        Reader r(b.data() + 8, b.size() - 8 - 32);
+        best_block = r.u256();
+        const u64 n = r.u64_();
+        map_.reserve(n);
+        for (u64 i = 0; i < n; ++i) {
+            OutPoint o;
+            o.hash = r.u256();
+            o.n = r.u32_();
+            Coin c;
+            const u32 code = r.u32_();
+            c.height = code >> 1;
+            c.coinbase = code & 1;
+            c.out.value = r.i64_();
+            c.out.script_pubkey = r.var_bytes();
+            map_.emplace(o, std::move(c));
+        }
+    } catch (const std::exception&) {
+        map_.clear();
+        best_block = Uint256();
+        return false;
+    }
+    return true;
+}
+
+CoinsView::Stats CoinsView::stats() const {
+    Stats s;
+    Writer w;
+    const Uint256* last = nullptr;
+    for (auto& [o, c] : sorted_coins(map_)) {
+        ++s.txouts;
+        if (!last || std::memcmp(last->data, o.hash.data, 32) != 0) ++s.transactions;
+        last = &o.hash;
+        s.total += c->out.value;
+        write_coin_entry(w, o, *c);
+    }
+    sha256d(w.buf.data(), w.buf.size(), s.hash.data);
+    return s;
+}
+
+// ------------------------------------------------------------------ undo encoding
+namespace {
+
+void write_varint(Writer& w, u64 n) {
+    u8 tmp[10];
+    int len = 0;
+    while (true) {
+        tmp[len] = u8((n & 0x7F) | (len ? 0x80 : 0x00));
+        if (n <= 0x7F) break;
+        n = (n >> 7) - 1;
+        ++len;
+    }
+    do {
+        w.u8_(tmp[len]);
+    } while (len--);
+}
+
+u64 read_varint(Reader& r) {
+    u64 n = 0;
+    while (true) {
+        const u8 ch = r.u8_();
+        if (n > (~u64(0) >> 7)) throw std::runtime_error("ReadVarInt(): size too large");
+        n = (n << 7) | (ch & 0x7F);
+        if (ch & 0x80) {
+            if (n == ~u64(0)) throw std::runtime_error("ReadVarInt(): size too large");
+            ++n;
+        } else {
+            return n;
+        }
+    }
+}
+
+constexpr u64 kSpecialScripts = 6;
+
+// CScriptCompressor::Compress: the 21/33-byte special forms, or false
+bool compress_script(const Bytes& s, Bytes& out) {
+    if (s.size() == 25 && s[0] == 0x76 && s[1] == 0xa9 && s[2] == 20 && s[23] == 0x88 && s[24] == 0xac) {
+        out.assign(1, 0x00);
+        out.insert(out.end(), s.begin() + 3, s.begin() + 23);
+        return true;
+    }
+    if (s.size() == 23 && s[0] == 0xa9 && s[1] == 20 && s[22] == 0x87) {
+        out.assign(1, 0x01);
+        out.insert(out.end(), s.begin() + 2, s.begin() + 22);
+        return true;
+    }
+    if (s.size() == 35 && s[0] == 33 && s[34] == 0xac && (s[1] == 0x02 || s[1] == 0x03)) {
+        out.assign(s.begin() + 1, s.begin() + 34);
+        return true;
+    }
+    if (s.size() == 67 && s[0] == 65 && s[66] == 0xac && s[1] == 0x04) {
+        secp::Ge p;
+        if (!secp::pubkey_parse(s.data() + 1, 65, p)) return false;  // IsFullyValid
+        out.assign(1, u8(0x04 | (s[65] & 0x01)));
+        out.insert(out.end(), s.begin() + 2, s.begin() + 34);
+        return true;
+    }
+    return false;
+}
+
+Bytes decompress_script(u64 kind, const Bytes& in) {
+    Bytes s;
+    switch (kind) {
+        case 0:
+            s = {0x76, 0xa9, 20};
+            s.insert(s.end(), in.begin(), in.end());
+            s.push_back(0x88);
+            s.push_back(0xac);
+            return s;
+        case 1:
+            s = {0xa9, 20};
+            s.insert(s.end(), in.begin(), in.end());
+            s.push_back(0x87);
+            return s;
+        case 2:
+        case 3:
+            s = {33, u8(kind)};
+            s.insert(s.end(), in.begin(), in.end());
+            s.push_back(0xac);
+            return s;
+        default: {  // 4, 5: uncompressed key stored as its x and the parity of y
+            u8 c[33];
+            c[0] = u8(kind - 2);
+            std::memcpy(c + 1, in.data(), 32);
+            secp::Ge p;
+            if (!secp::pubkey_parse(c, 33, p)) return s;
+            u8 full[65];
+            secp::pubkey_serialize(p, false, full);
+            s.push_back(65);
+            s.insert(s.end(), full, full + 65);
+            s.push_back(0xac);
+            return s;
+        }
+    }
+}
+
+void write_coin_undo(Writer& w, const Coin& c) {
+    write_varint(w, u64(c.height) * 2 + (c.coinbase ? 1 : 0));
+    if (c.height > 0) w.u8_(0);  // the old undo format's nVersion placeholder
+    write_varint(w, compress_amount(u64(c.out.value)));
+    Bytes comp;
+    if (compress_script(c.out.script_pubkey, comp)) {
+        w.raw(comp);
+    } else {
+        write_varint(w, c.out.script_pubkey.size() + kSpecialScripts);
+        w.raw(c.out.script_pubkey);
+    }
+}
+
+Coin read_coin_undo(Reader& r) {
+    Coin c;
+    const u64 code = read_varint(r);
+    c.height = u32(code >> 1);
+    c.coinbase = code & 1;
+    if (c.height > 0) (void)read_varint(r);
+    c.out.value = Amount(decompress_amount(read_varint(r)));
+    const u64 n = read_varint(r);
+    if (n < kSpecialScripts) {
+        const size_t len = n < 2 ? 20 : 32;
+        const u8* p = r.take(len);
+        c.out.script_pubkey = decompress_script(n, Bytes(p, p + len));
+    } else {
+        const u64 len = n - kSpecialScripts;
+        if (len > kMaxScriptSize) {  // unspendable: OP_RETURN, data skipped
+            r.take(size_t(len));
+            c.out.script_pubkey = {0x6a};
+        } else {
+            const u8* p = r.take(size_t(len));
+            c.out.script_pubkey.assign(p, p + len);
+        }
+    }
+    return c;
+}
+
+}  // namespace
+
+u64 compress_amount(u64 n) {
+    if (n == 0) return 0;
+    int e = 0;
+    while ((n % 10) == 0 && e < 9) {
+        n /= 10;
+        ++e;
+    }
+    if (e < 9) {
+        const int d = int(n % 10);
+        n /= 10;
+        return 1 + (n * 9 + u64(d) - 1) * 10 + u64(e);
+    }
+    return 1 + (n - 1) * 10 + 9;
+}
+
+u64 decompress_amount(u64 x) {
+    if (x == 0) return 0;
+    --x;
+    int e = int(x % 10);
+    x /= 10;
+    u64 n;
+    if (e < 9) {
+        const int d = int(x % 9) + 1;
+        x /= 9;
+        n = x * 10 + u64(d);
+    } else {
+        n = x + 1;
+    }
+    while (e--) n *= 10;
+    return n;
+}
+
+Bytes serialize_block_undo(const BlockUndo& u) {
+    Writer w;
+    w.compact_size(u.vtxundo.size());
+    for (auto& t : u.vtxundo) {
+        w.compact_size(t.prev.size());
+        for (auto& c : t.prev) write_coin_undo(w, c);
+    }
+    return w.buf;
+}
+
+BlockUndo deserialize_block_undo(const Bytes& b) {
+    Reader r(b);
+    BlockUndo u;
+    u.vtxundo.resize(size_t(r.compact_size()));
+    for (auto& t : u.vtxundo) {
+        t.prev.resize(size_t(r.compact_size()));
+        for (auto& c : t.prev) c = read_coin_undo(r);
+    }
+    if (!r.empty()) throw std::runtime_error("trailing data after block undo");
+    return u;
+}
+
+// ------------------------------------------------------------------ sigops
+namespace {
+
+// the last data push of a push-only scriptSig (the P2SH redeem script), or false
+bool last_push(const Bytes& script_sig, Bytes& data) {
+    size_t pc = 0;
+    u8 op;
+    Bytes d;
+    data.clear();
+    while (pc < script_sig.size()) {
+        if (!script_get_op(script_sig, pc, op, &d)) return false;
+        if (op > 0x60) return false;  // OP_16
+        data = d;
+    }
+    return true;
+}
+
+int64_t witness_sigops(int version, const Bytes& program, const std::vector<Bytes>& witness) {
+    if (version != 0) return 0;
+    if (program.size() == 20) return 1;
+    if (program.size() == 32 && !witness.empty()) return script_sigop_count(witness.back(), true);
+    return 0;
+}
+
+}  // namespace
+
+int64_t tx_legacy_sigops(const Transaction& tx) {
+    int64_t legacy = 0;
+    for (auto& in : tx.vin) legacy += script_sigop_count(in.script_sig, false);
+    for (auto& o : tx.vout) legacy += script_sigop_count(o.script_pubkey, false);
+    return legacy;
+}
+
+int64_t tx_sigop_cost(const Transaction& tx, const std::vector<const Coin*>& spent, u32 flags) {
+    int64_t cost = tx_legacy_sigops(tx) * 4;
+    if (tx.is_coinbase()) return cost;
+    if (spent.size() != tx.vin.size()) throw std::invalid_argument("tx_sigop_cost: one spent coin per input");
+    for (size_t i = 0; i < tx.vin.size(); ++i) {
+        const Bytes& spk = spent[i]->out.script_pubkey;
+        const TxIn& in = tx.vin[i];
+        Bytes redeem;
+        const bool p2sh = script_is_p2sh(spk) && last_push(in.script_sig, redeem);
+        if ((flags & SCRIPT_VERIFY_P2SH) && p2sh) cost += int64_t(script_sigop_count(redeem, true)) * 4;
+        if (flags & SCRIPT_VERIFY_WITNESS) {
+            int v;
+            Bytes prog;
+            if (script_is_witness_program(spk, v, prog)) cost += witness_sigops(v, prog, in.witness);
+            else if (p2sh && script_is_witness_program(redeem, v, prog)) cost += witness_sigops(v, prog, in.witness);
+        }
+    }
+    return cost;
+}
+
+// ------------------------------------------------------------------ connect / disconnect
+bool verify_input_host(const Transaction& tx, unsigned n_in, const Coin& coin, u32 flags, ScriptError* err) {
+    const PrecomputedTx cache(tx);
+    const TxSigChecker checker(&tx, n_in, coin.out.value, &cache);
+    return verify_script(tx.vin[n_in].script_sig, coin.out.script_pubkey, &tx.vin[n_in].witness, flags, checker, err);
+}
+
+namespace {
+
+bool is_unspendable(const Bytes& spk) { return (!spk.empty() && spk[0] == 0x6a) || spk.size() > kMaxScriptSize; }
+
+}  // namespace
+
+ConnectResult connect_block(const Block& block, int height, CoinsView& view, const ConnectOptions& opt,
+                            BlockUndo& undo) {
+    ConnectResult res;
+    undo.vtxundo.clear();
+    std::vector<OutPoint> added;
+    auto fail = [&](const std::string& reason, int dos) {
+        // roll back: restore what the block spent (later transactions first), then drop every
+        // output it added (that also removes in-block outputs the restore just put back)
+        for (size_t t = undo.vtxundo.size(); t-- > 0;) {
+            const Transaction& tx = block.vtx[t + 1];
+            for (size_t i = 0; i < undo.vtxundo[t].prev.size(); ++i)
+                view.add(tx.vin[i].prevout, undo.vtxundo[t].prev[i]);
+        }
+        for (auto it = added.rbegin(); it != added.rend(); ++it) view.spend(*it);
+        undo.vtxundo.clear();
+        res.ok = false;
+        res.reject = reason;
+        res.dos = dos;
+        res.sigs.clear();
+        res.sig_at.clear();
+        return res;
+    };
+    for (size_t t = 0; t < block.vtx.size(); ++t) {
+        const Transaction& tx = block.vtx[t];
+        const Uint256 txid = tx.txid();
+        std::vector<const Coin*> spent;
+        if (!tx.is_coinbase()) {
+            Amount in_sum = 0;
+            std::vector<int> prev_heights;
+            for (auto& in : tx.vin) {
+                const Coin* c = view.find(in.prevout);
+                if (!c) return fail("bad-txns-inputs-missingorspent", 100);
+                if (c->coinbase && height - int(c->height) < kCoinbaseMaturity)
+                    return fail("bad-txns-premature-spend-of-coinbase", 0);
+                if (c->out.value < 0 || c->out.value > kMaxMoney) return fail("bad-txns-inputvalues-outofrange", 100);
+                in_sum += c->out.value;
+                if (in_sum < 0 || in_sum > kMaxMoney) return fail("bad-txns-inputvalues-outofrange", 100);
+                spent.push_back(c);
+                prev_heights.push_back(int(c->height));
+            }
+            const Amount out_sum = tx.value_out();
+            if (in_sum < out_sum) return fail("bad-txns-in-belowout", 100);
+            const Amount fee = in_sum - out_sum;
+            res.fees += fee;
+            if (res.fees < 0 || res.fees > kMaxMoney) return fail("bad-txns-accumulated-fee-outofrange", 100);
+            // BIP68 relative lock-times (CalculateSequenceLocks / EvaluateSequenceLocks)
+            if (opt.sequence_locks && (opt.script_flags & SCRIPT_VERIFY_CHECKSEQUENCEVERIFY) && u32(tx.version) >= 2) {
+                int min_height = -1;
+                int64_t min_time = -1;
+                for (size_t i = 0; i < tx.vin.size(); ++i) {
+                    const u32 seq = tx.vin[i].sequence;
+                    if (seq & (1u << 31)) continue;
+                    if (seq & (1u << 22)) {
+                        const int64_t coin_time = opt.mtp_at ? opt.mtp_at(std::max(prev_heights[i] - 1, 0)) : 0;
+                        min_time = std::max(min_time, coin_time + (int64_t(seq & 0xffff) << 9) - 1);
+                    } else {
+                        min_height = std::max(min_height, prev_heights[i] + int(seq & 0xffff) - 1);
+                    }
+                }
+                if (min_height >= height || min_time >= opt.block_mtp) return fail("bad-txns-nonfinal", 100);
+            }
+        }
+        res.sigop_cost += tx_sigop_cost(tx, spent, opt.script_flags);
+        if (res.sigop_cost > kMaxBlockSigopsCost) return fail("bad-blk-sigops", 100);
+        if (!tx.is_coinbase() && opt.check_scripts) {
+            const PrecomputedTx cache(tx);
+            for (size_t i = 0; i < tx.vin.size(); ++i) {
+                TxSigChecker checker(&tx, unsigned(i), spent[i]->out.value, &cache);
+                const size_t before = res.sigs.size();
+                if (opt.defer_sigs) checker.pending = &res.sigs;
+                ScriptError err;
+                if (!verify_script(tx.vin[i].script_sig, spent[i]->out.script_pubkey, &tx.vin[i].witness,
+                                   opt.script_flags, checker, &err))
+                    return fail(std::string("mandatory-script-verify-flag-failed (") + script_error_name(err) + ")",
+                                100);
+                for (size_t k = before; k < res.sigs.size(); ++k) res.sig_at.emplace_back(u32(t), u32(i));
+            }
+        }
+        // spend the inputs, recording them for undo
+        if (!tx.is_coinbase()) {
+            TxUndo tu;
+            tu.prev.reserve(tx.vin.size());
+            for (auto& in : tx.vin) {
+                Coin c;
+                view.spend(in.prevout, &c);
+                tu.prev.push_back(std::move(c));
+            }
+            undo.vtxundo.push_back(std::move(tu));
+        }
+        for (u32 n = 0; n < tx.vout.size(); ++n) {
+            if (is_unspendable(tx.vout[n].script_pubkey)) continue;
+            OutPoint o;
+            o.hash = txid;
+            o.n = n;
+            if (view.find(o)) return fail("bad-txns-BIP30", 100);  // would overwrite an unspent output
+            Coin c;
+            c.out = tx.vout[n];
+            c.height = u32(height);
+            c.coinbase = tx.is_coinbase();
+            view.add(o, std::move(c));
+            added.push_back(o);
+        }
+    }
+    return res;
+}
+
+bool disconnect_block(const Block& block, const BlockUndo& undo, CoinsView& view) {
+    if (undo.vtxundo.size() + 1 != block.vtx.size()) return false;
+    bool clean = true;
+    for (size_t t = block.vtx.size(); t-- > 0;) {
+        const Transaction& tx = block.vtx[t];
+        const Uint256 txid = tx.txid();
+        for (u32 n = 0; n < tx.vout.size(); ++n) {
+            if (is_unspendable(tx.vout[n].script_pubkey)) continue;
+            OutPoint o;
+            o.hash = txid;
+            o.n = n;
+            if (!view.spend(o)) clean = false;
+        }
+        if (t == 0) break;
+        const TxUndo& tu = undo.vtxundo[t - 1];
+        if (tu.prev.size() != tx.vin.size()) return false;
+        for (size_t i = tx.vin.size(); i-- > 0;) {
+            if (view.find(tx.vin[i].prevout)) clean = false;
+            view.add(tx.vin[i].prevout, tu.prev[i]);
+        }
+    }
+    return clean;
+}
+
+}  // namespace nodexa

@@ -394,7 +394,17 @@ void HeaderChain::reconsider(const Uint256& hash) {
     std::lock_guard<std::recursive_mutex> g(mu_);
     auto it = index_.find(hash);
     if (it == index_.end()) return;
-    failed_.erase(it->second);
+    // ResetBlockFailureFlags: the block, its descendants and its ancestors become valid again
+    const HeaderIndex* node = it->second;
+    auto walk = [](const HeaderIndex* x, int height) {
+        while (x && x->height > height) x = x->prev;
+        return x;
+    };
+    for (auto f = failed_.begin(); f != failed_.end();) {
+        const HeaderIndex* x = f->first;
+        const bool related = x->height >= node->height ? walk(x, node->height) == node : walk(node, x->height) == x;
+        f = related ? failed_.erase(f) : std::next(f);
+    }
     update_active_chain();
 }
 

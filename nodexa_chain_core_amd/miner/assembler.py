@@ -10,8 +10,10 @@ with the 32-byte witness nonce; header: version = ComputeBlockVersion
 nNonce64 = 0, nHeight = tip+1. IncrementExtraNonce (src/miner.cpp:508-525):
 scriptSig = <height> <extranonce>, merkle root recomputed.
 
-Mempool selection (addPackageTxs) is out of scope: templates carry the
-transactions of the engine's mempool-lite in arrival order, capped by weight.
+Mempool selection: the pool's transactions in arrival order, reordered so that every in-pool
+parent precedes its children (after a reorg, re-accepted parents arrive after their children),
+capped by weight; a transaction whose parent did not fit is left out too. Fee-rate package
+selection (addPackageTxs) is not done.
 """
 from __future__ import annotations
 
@@ -60,11 +62,16 @@ class BlockAssembler:
             prev = st.tip()
             height = prev.height + 1
             txs, fees, weight = [], 0, 4000
-            for e in list(st.mempool.values()):
+            included: set[bytes] = set()
+            for txid in self._parents_first(st.mempool):
+                e = st.mempool[txid]
+                if any(i.prevout.hash in st.mempool and i.prevout.hash not in included for i in e.tx.vin):
+                    continue
                 w = len(e.tx.serialize(False)) * 3 + len(e.tx.serialize(True))
                 if weight + w > self.max_weight:
-                    break
+                    continue
                 txs.append(e.tx)
+                included.add(txid)
                 fees += e.fee
                 weight += w
             subsidy = _core.block_subsidy(height)
@@ -96,6 +103,28 @@ class BlockAssembler:
             blk.header = hdr
             target, _, _ = _core.set_compact(hdr.bits)
             return BlockTemplate(blk, height, fees, miner.value, community.value, commitment, target, time.time())
+
+    @staticmethod
+    def _parents_first(pool) -> list[bytes]:
+        """Pool txids in arrival order, each after its in-pool parents (iterative DFS)."""
+        order, seen = [], set()
+        for root in list(pool):
+            if root in seen:
+                continue
+            stack = [(root, False)]
+            while stack:
+                txid, expanded = stack.pop()
+                if expanded:
+                    order.append(txid)
+                    continue
+                if txid in seen:
+                    continue
+                seen.add(txid)
+                stack.append((txid, True))
+                for i in reversed(list(pool[txid].tx.vin)):
+                    if i.prevout.hash in pool and i.prevout.hash not in seen:
+                        stack.append((i.prevout.hash, False))
+        return order
 
     def _add_witness_commitment(self, blk) -> bytes:
         # segwit is enabled on every network (nSegwitEnabled = true in all three params)

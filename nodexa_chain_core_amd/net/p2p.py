@@ -363,14 +363,18 @@ class ConnectionManager:
             peer.send("getdata", P.inv_payload(want))
 
     def on_tx(self, peer: Peer, p: bytes) -> None:
-        """AcceptToMemoryPool for a relayed tx (context-free checks; no UTXO set), then relay."""
+        """AcceptToMemoryPool for a relayed tx (UTXO set, scripts, fees); accepted transactions
+        are relayed to the other peers by the mempool signal."""
         tx = _core.Transaction.deserialize(p)
         txid = tx.txid()
         peer.known_txs.add(txid)
         REGISTRY.inc("p2p_tx_received_total", 1)
-        if txid in self.state.mempool or tx.is_coinbase() or not tx.vin or not tx.vout:
+        if txid in self.state.mempool:
             return
-        self.state.add_to_mempool(tx, 0)  # the mempool signal relays it to the other peers
+        ok, reason, _ = self.state.accept_to_mempool(tx)
+        if not ok:
+            REGISTRY.inc("p2p_tx_rejected_total", 1)
+            log.log_print("mempool", f"tx {_core.u256_hex(txid)} from peer {peer.id} rejected: {reason}")
 
     def on_mempool(self, peer: Peer, p: bytes) -> None:
         """BIP35: inv of every pool txid (in MAX_INV_SZ chunks)."""

@@ -27,7 +27,7 @@ from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
 from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, GpuKawpowBackend, MinerController
-from .rpc import methods, methods_ext
+from .rpc import methods, methods_ext, methods_wallet
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
 from .utils import log, metrics
 from .utils.config import ArgsManager, gpu_list
@@ -103,6 +103,16 @@ class Node:
                 setattr(self.params, attr, a.get_int(flag, getattr(self.params, attr)))
         if self.network == "regtest" and a.is_set("blockversion"):  # -blockversion (src/miner.cpp:146-149)
             self.state.block_version_override = a.get_int("blockversion", 0)
+        self.wallet = None
+        if not a.get_bool("disablewallet", False):  # -disablewallet (src/wallet/init.cpp)
+            from .wallet import Wallet
+
+            self.wallet = Wallet(self.state, self.params,
+                                 os.path.join(self.datadir, "wallet.json") if self.datadir else None)
+            methods_wallet.register(self.table, self)
+        if a.get("minrelaytxfee") is not None:  # -minrelaytxfee=<CLORE per kvB>
+            self.state.min_relay_fee = round(float(a.get("minrelaytxfee")) * 100_000_000)
+        self.state.gpu_signatures = a.get("gpusigs", "auto")  # -gpusigs=auto|on|off: GPU batch ECDSA in blocks
         if self.datadir is not None and a.get_bool("persistmempool", True):  # -persistmempool (LoadMempool)
             n = self.state.load_mempool(os.path.join(self.datadir, "mempool.dat"))
             if n:

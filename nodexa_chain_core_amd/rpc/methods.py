@@ -17,7 +17,8 @@ from .. import core
 from ..chain.header import from_progpow, to_progpow
 from ..utils import log
 from .protocol import (RPC_DESERIALIZATION_ERROR, RPC_INVALID_ADDRESS_OR_KEY, RPC_INVALID_PARAMETER,
-                       RPC_INVALID_PARAMS, RPC_MISC_ERROR, RPC_TYPE_ERROR, RPC_VERIFY_ERROR, RPCError)
+                       RPC_INVALID_PARAMS, RPC_MISC_ERROR, RPC_TRANSACTION_ERROR, RPC_TYPE_ERROR,
+                       RPC_VERIFY_ALREADY_IN_CHAIN, RPC_VERIFY_ERROR, RPC_VERIFY_REJECTED, RPCError)
 
 _core = core()
 
@@ -231,14 +232,14 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         """invalidateblock "blockhash" """
         _need(p, 1, 'invalidateblock "blockhash"')
         idx = lookup(p[0])
-        st.chain.invalidate(idx.hash)
+        st.invalidate_block(idx.hash)
         return None
 
     def rpc_reconsiderblock(p):
         """reconsiderblock "blockhash" """
         _need(p, 1, 'reconsiderblock "blockhash"')
         idx = lookup(p[0])
-        st.chain.reconsider(idx.hash)
+        st.reconsider_block(idx.hash)
         return None
 
     def rpc_waitfornewblock(p):
@@ -476,15 +477,52 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             raise RPCError(RPC_DESERIALIZATION_ERROR, "TX decode failed")
 
     def rpc_sendrawtransaction(p):
-        """sendrawtransaction "hexstring" ( fee ) — add to the template mempool (no UTXO checks)."""
-        _need(p, 1, 'sendrawtransaction "hexstring"')
+        """sendrawtransaction "hexstring" ( allowhighfees ) — AcceptToMemoryPool, then relay
+        (src/rpc/rawtransaction.cpp sendrawtransaction)."""
+        _need(p, 1, 'sendrawtransaction "hexstring" ( allowhighfees )')
         try:
             tx = _core.Transaction.deserialize(bytes.fromhex(p[0]))
         except Exception:
             raise RPCError(RPC_DESERIALIZATION_ERROR, "TX decode failed")
-        if tx.is_coinbase():
-            raise RPCError(RPC_VERIFY_ERROR, "coinbase")
-        return _hex(st.add_to_mempool(tx, int(_arg(p, 1, 0))))
+        txid = tx.txid()
+        if txid in st.mempool:
+            return _hex(txid)
+        if st.coins.get(txid, 0) is not None:
+            raise RPCError(RPC_VERIFY_ALREADY_IN_CHAIN, "transaction already in block chain")
+        max_fee = None if _arg(p, 1, False) else 1_000_000 * max(1, len(tx.serialize(True)))  # absurd-fee guard
+        ok, reason, _ = st.accept_to_mempool(tx, max_fee=max_fee)
+        if not ok:
+            code = RPC_TRANSACTION_ERROR if reason == "missing-inputs" else RPC_VERIFY_REJECTED
+            raise RPCError(code, "Missing inputs" if reason == "missing-inputs" else f"16: {reason}")
+        return _hex(txid)
+
+    def rpc_gettxout(p):
+        """gettxout "txid" n ( include_mempool ) — an unspent output (src/rpc/blockchain.cpp gettxout)."""
+        _need(p, 2, 'gettxout "txid" n ( include_mempool )')
+        txid, n = _parse_hash(p[0]), int(p[1])
+        include_mempool = bool(_arg(p, 2, True))
+        if include_mempool and any(i.prevout.hash == txid and i.prevout.n == n
+                                   for e in st.mempool.values() for i in e.tx.vin):
+            return None
+        c = st.coins.get(txid, n)
+        confirmations_tip = st.coins_tip()
+        if c is None:
+            if not include_mempool or txid not in st.mempool or n >= len(st.mempool[txid].tx.vout):
+                return None
+            o = st.mempool[txid].tx.vout[n]
+            value, spk, height, coinbase, conf = o.value, o.script_pubkey, None, False, 0
+        else:
+            value, spk, height, coinbase = c
+            conf = confirmations_tip.height - height + 1
+        return {"bestblock": _hex(confirmations_tip.hash), "confirmations": conf, "value": value / 1e8,
+                "scriptPubKey": _spk_json(spk), "coinbase": coinbase}
+
+    def rpc_gettxoutsetinfo(p):
+        """gettxoutsetinfo — statistics about the UTXO set."""
+        tip = st.coins_tip()
+        txouts, ntx, total, h = st.coins.stats()
+        return {"height": tip.height, "bestblock": _hex(tip.hash), "transactions": ntx, "txouts": txouts,
+                "bogosize": txouts * 50, "hash_serialized_2": _hex(h), "disk_size": 0, "total_amount": total / 1e8}
 
     def rpc_getrawmempool(p):
         """getrawmempool ( verbose )"""
@@ -515,13 +553,35 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
                 if t.txid() == txid:
                     tx, in_block = t, bh
                     break
+        else:  # GetTransaction's fAllowSlow path: a transaction with an unspent output
+            h = st.coins.height_of_txid(txid)
+            idx = st.chain.at_height(h) if h is not None else None
+            blk = st.get_block(idx.hash) if idx is not None else None
+            for t in (blk.vtx if blk is not None else []):
+                if t.txid() == txid:
+                    tx, in_block = t, idx.hash
+                    break
         if tx is None:
             raise RPCError(RPC_INVALID_ADDRESS_OR_KEY, "No such mempool transaction. Use -txindex or provide a block hash")
         if not _arg(p, 1, False):
             return tx.serialize(True).hex()
         out = tx_json(tx)
-        if in_block is not None:
+        if in_block is not None:  # TxToJSON: confirmations / time of an active-chain block
             out["blockhash"] = _hex(in_block)
+            idx = st.chain.find(in_block)
+            if idx is not None and st.chain.in_active_chain(idx):
+                out["confirmations"] = 1 + st.height() - idx.height
+                out["time"] = out["blocktime"] = idx.time
+            else:
+                out["confirmations"] = 0
+        return out
+
+    def _spk_json(spk: bytes) -> dict:
+        out = {"hex": spk.hex()}
+        addr = _core.script_to_address(spk, params.pubkey_prefix, params.script_prefix)
+        if addr:
+            out["addresses"] = [addr]
+            out["type"] = "scripthash" if spk[0] == 0xa9 else "pubkeyhash"
         return out
 
     def rpc_validateaddress(p):
@@ -530,11 +590,15 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         spk = _core.address_to_script(p[0], params.pubkey_prefix, params.script_prefix)
         if spk is None:
             return {"isvalid": False}
-        return {"isvalid": True, "address": p[0], "scriptPubKey": spk.hex(), "isscript": spk[0] == 0xa9}
+        w = getattr(node, "wallet", None)
+        return {"isvalid": True, "address": p[0], "scriptPubKey": spk.hex(), "isscript": spk[0] == 0xa9,
+                "ismine": bool(w is not None and w.is_mine(spk))}
 
     for cat, name, fn, args in [
         ("rawtransactions", "decoderawtransaction", rpc_decoderawtransaction, ("hexstring",)),
-        ("rawtransactions", "sendrawtransaction", rpc_sendrawtransaction, ("hexstring", "fee")),
+        ("rawtransactions", "sendrawtransaction", rpc_sendrawtransaction, ("hexstring", "allowhighfees")),
+        ("blockchain", "gettxout", rpc_gettxout, ("txid", "n", "include_mempool")),
+        ("blockchain", "gettxoutsetinfo", rpc_gettxoutsetinfo, ()),
         ("blockchain", "getrawmempool", rpc_getrawmempool, ("verbose",)),
         ("blockchain", "getmempoolinfo", rpc_getmempoolinfo, ()),
         ("rawtransactions", "getrawtransaction", rpc_getrawtransaction, ("txid", "verbose", "blockhash")),

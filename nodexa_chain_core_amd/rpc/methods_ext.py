@@ -33,7 +33,7 @@ RPC_CLIENT_NODE_NOT_ADDED = -24
 RPC_CLIENT_NODE_NOT_CONNECTED = -29
 RPC_CLIENT_INVALID_IP_OR_SUBNET = -30
 RPC_CLIENT_P2P_DISABLED = -31
-MAX_MONEY = 5_000_000_000 * 100_000_000  # MAX_MONEY (src/amount.h), 5B CLORE
+MAX_MONEY = 1_300_000_000 * 100_000_000  # MAX_MONEY (src/amount.h:29), 1.3B CLORE
 
 # Opcode names for ScriptToAsmStr (src/script/script.cpp GetOpName).
 _OPS = {0x00: "0", 0x4f: "-1", 0x50: "OP_RESERVED", 0x61: "OP_NOP", 0x62: "OP_VER", 0x63: "OP_IF",
@@ -562,33 +562,9 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             out["p2sh"] = _core.script_to_address(p2sh, params.pubkey_prefix, params.script_prefix)
         return out
 
-    def _check_transaction(tx) -> str | None:
-        """CheckTransaction (src/consensus/tx_verify.cpp) context-free rules."""
-        if not tx.vin:
-            return "bad-txns-vin-empty"
-        if not tx.vout:
-            return "bad-txns-vout-empty"
-        total = 0
-        for o in tx.vout:
-            if o.value < 0:
-                return "bad-txns-vout-negative"
-            if o.value > MAX_MONEY:
-                return "bad-txns-vout-toolarge"
-            total += o.value
-            if total > MAX_MONEY:
-                return "bad-txns-txouttotal-toolarge"
-        outs = [(i.prevout.hash, i.prevout.n) for i in tx.vin]
-        if len(set(outs)) != len(outs):
-            return "bad-txns-inputs-duplicate"
-        if tx.is_coinbase():
-            return "coinbase"
-        if any(i.prevout.is_null() for i in tx.vin):
-            return "bad-txns-prevout-null"
-        return None
-
     def rpc_testmempoolaccept(p):
-        """testmempoolaccept ["rawtx"] ( allowhighfees ) — would the tx be accepted (context-free
-        checks + pool conflicts; no UTXO lookup in this engine)."""
+        """testmempoolaccept ["rawtx"] ( allowhighfees ) — AcceptToMemoryPool without adding
+        (src/rpc/rawtransaction.cpp testmempoolaccept)."""
         _need(p, 1, 'testmempoolaccept ["rawtx"] ( allowhighfees )')
         raws = p[0]
         if not isinstance(raws, list) or len(raws) != 1:
@@ -597,15 +573,10 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             tx = _core.Transaction.deserialize(bytes.fromhex(raws[0]))
         except Exception:
             raise RPCError(RPC_DESERIALIZATION_ERROR, "TX decode failed")
-        txid = tx.txid()
-        res = {"txid": _hex(txid)}
-        why = "txn-already-in-mempool" if txid in st.mempool else _check_transaction(tx)
-        if why is None:
-            spent = {(i.prevout.hash, i.prevout.n) for e in st.mempool.values() for i in e.tx.vin}
-            if any((i.prevout.hash, i.prevout.n) in spent for i in tx.vin):
-                why = "txn-mempool-conflict"
-        res["allowed"] = why is None
-        if why is not None:
+        max_fee = None if _arg(p, 1, False) else 1_000_000 * max(1, len(tx.serialize(True)))
+        ok, why, _ = st.accept_to_mempool(tx, test_only=True, max_fee=max_fee)
+        res = {"txid": _hex(tx.txid()), "allowed": ok}
+        if not ok:
             res["reject-reason"] = ("18: " if why == "txn-already-in-mempool" else "16: ") + why
         return [res]
 

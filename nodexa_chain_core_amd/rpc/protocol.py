@@ -8,6 +8,8 @@ RPC_INVALID_PARAMS = -32602
 RPC_INTERNAL_ERROR = -32603
 RPC_PARSE_ERROR = -32700
 RPC_MISC_ERROR = -1
+RPC_WALLET_ERROR = -4
+RPC_WALLET_INSUFFICIENT_FUNDS = -6
 RPC_TYPE_ERROR = -3
 RPC_INVALID_ADDRESS_OR_KEY = -5
 RPC_OUT_OF_MEMORY = -7
@@ -17,6 +19,7 @@ RPC_DESERIALIZATION_ERROR = -22
 RPC_VERIFY_ERROR = -25
 RPC_VERIFY_REJECTED = -26
 RPC_VERIFY_ALREADY_IN_CHAIN = -27
+RPC_TRANSACTION_ERROR = -25  # RPC_VERIFY_ERROR's alias for missing inputs (src/rpc/protocol.h)
 RPC_IN_WARMUP = -28
 RPC_METHOD_DEPRECATED = -32
 RPC_CLIENT_NOT_CONNECTED = -9

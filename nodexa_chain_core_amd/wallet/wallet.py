@@ -1,0 +1,305 @@
+"""Key wallet (the subset a mining / validating node uses).
+
+Parity (behaviour, not the BerkeleyDB format): CWallet key store and its RPCs in
+src/wallet/rpcwallet.cpp (getnewaddress, getbalance, listunspent, sendtoaddress, sendmany,
+dumpprivkey / importprivkey, signrawtransaction, getwalletinfo), CKey::Sign + the standard
+signature producers of src/script/sign.cpp for P2PKH, P2PK, P2WPKH and P2SH-P2WPKH outputs, WIF
+secrets (base58check: SECRET_KEY prefix, key, 0x01 for compressed keys; src/base58.cpp).
+
+Keys are secp256k1 secrets from os.urandom (csrc/crypto/secp256k1.cpp signs them with RFC 6979)
+kept in <datadir>/wallet.json, written atomically (no encryption: `walletpassphrase` is not
+offered). Balances come from the node's UTXO set (CoinsView.outputs_for_scripts) plus the
+mempool's unconfirmed outputs to the wallet's scripts.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+
+from .. import core
+
+_core = core()
+
+# base58Prefixes[SECRET_KEY] (src/chainparams.cpp:191, 350, 517)
+SECRET_PREFIX = {"main": 112, "test": 114, "regtest": 114}
+SIGHASH_ALL = 1
+COIN = 100_000_000
+DEFAULT_FEE_RATE = 2_000_000  # sat per kvB: above the 0.01 CLORE/kvB min relay fee
+
+
+def _push(d: bytes) -> bytes:
+    return _core.script_push_data(d)
+
+
+def p2pkh(h160: bytes) -> bytes:
+    return b"\x76\xa9\x14" + h160 + b"\x88\xac"
+
+
+class WalletError(Exception):
+    pass
+
+
+class Wallet:
+    def __init__(self, state, params, path: str | None):
+        self.state = state
+        self.params = params
+        self.path = path
+        self.lock = threading.RLock()
+        self.keys: dict[bytes, tuple[bytes, bytes]] = {}  # hash160(pubkey) -> (secret, compressed pubkey)
+        self.labels: dict[bytes, str] = {}
+        self.created: dict[bytes, int] = {}
+        self._p2sh_wpkh: dict[bytes, bytes] = {}  # hash160(0x0014 || h) -> h
+        if path and os.path.exists(path):
+            self._load()
+
+    # ------------------------------------------------------------------ persistence
+    def _load(self) -> None:
+        with open(self.path) as f:
+            data = json.load(f)
+        for k in data.get("keys", []):
+            self._add_secret(self.decode_wif(k["wif"]), k.get("label", ""), k.get("created", 0), save=False)
+
+    def _save(self) -> None:
+        if not self.path:
+            return
+        data = {"version": 1, "network": self.params.network_id,
+                "keys": [{"wif": self.encode_wif(sec), "label": self.labels.get(h, ""),
+                          "created": self.created.get(h, 0)} for h, (sec, _) in self.keys.items()]}
+        tmp = self.path + ".new"
+        with open(tmp, "w") as f:
+            json.dump(data, f, indent=1)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self.path)
+
+    # ------------------------------------------------------------------ keys
+    def encode_wif(self, secret: bytes) -> str:
+        return _core.base58check_encode(bytes([SECRET_PREFIX[self.params.network_id]]) + secret + b"\x01")
+
+    def decode_wif(self, wif: str) -> bytes:
+        raw = _core.base58check_decode(wif)
+        if raw is None or raw[0] != SECRET_PREFIX[self.params.network_id] or len(raw) not in (33, 34):
+            raise WalletError("Invalid private key encoding")
+        secret = raw[1:33]
+        if not _core.secp_seckey_valid(secret):
+            raise WalletError("Private key outside allowed range")
+        return secret
+
+    def _add_secret(self, secret: bytes, label: str = "", created: int | None = None, save: bool = True) -> bytes:
+        pub = _core.secp_pubkey_create(secret, True)
+        h = _core.hash160(pub)
+        with self.lock:
+            self.keys[h] = (secret, pub)
+            self._p2sh_wpkh[_core.hash160(b"\x00\x14" + h)] = h
+            self.labels[h] = label
+            self.created[h] = int(time.time()) if created is None else created
+            if save:
+                self._save()
+        return h
+
+    def address_of(self, h160: bytes) -> str:
+        return _core.base58check_encode(bytes([self.params.pubkey_prefix]) + h160)
+
+    def new_address(self, label: str = "") -> str:
+        while True:
+            secret = os.urandom(32)
+            if _core.secp_seckey_valid(secret):
+                return self.address_of(self._add_secret(secret, label))
+
+    def import_privkey(self, wif: str, label: str = "") -> str:
+        return self.address_of(self._add_secret(self.decode_wif(wif), label))
+
+    def dump_privkey(self, address: str) -> str:
+        h = self._h160_of(address)
+        if h not in self.keys:
+            raise WalletError("Private key for address is not known")
+        return self.encode_wif(self.keys[h][0])
+
+    def _h160_of(self, address: str) -> bytes:
+        raw = _core.base58check_decode(address)
+        if raw is None or len(raw) != 21 or raw[0] != self.params.pubkey_prefix:
+            raise WalletError("Invalid address")
+        return raw[1:]
+
+    def scripts(self) -> list[bytes]:
+        """Every scriptPubKey the wallet can spend: P2PKH, P2PK, P2WPKH and P2SH-P2WPKH of each key."""
+        with self.lock:
+            out = []
+            for h, (_, pub) in self.keys.items():
+                out.append(p2pkh(h))
+                out.append(_push(pub) + b"\xac")
+                out.append(b"\x00\x14" + h)
+            for sh in self._p2sh_wpkh:
+                out.append(b"\xa9\x14" + sh + b"\x87")
+            return out
+
+    def is_mine(self, spk: bytes) -> bool:
+        return self._key_for(spk) is not None
+
+    def _key_for(self, spk: bytes):
+        """(secret, pubkey, kind) for a scriptPubKey the wallet can sign, else None."""
+        if len(spk) == 25 and spk[:3] == b"\x76\xa9\x14" and spk[23:] == b"\x88\xac":
+            k = self.keys.get(spk[3:23])
+            return None if k is None else (k[0], k[1], "p2pkh")
+        if len(spk) == 35 and spk[0] == 33 and spk[34] == 0xac:
+            h = _core.hash160(spk[1:34])
+            k = self.keys.get(h)
+            return None if k is None else (k[0], k[1], "p2pk")
+        if len(spk) == 22 and spk[:2] == b"\x00\x14":
+            k = self.keys.get(spk[2:])
+            return None if k is None else (k[0], k[1], "p2wpkh")
+        if len(spk) == 23 and spk[:2] == b"\xa9\x14" and spk[22] == 0x87:  # P2SH-P2WPKH of one of our keys
+            h = self._p2sh_wpkh.get(spk[2:22])
+            k = None if h is None else self.keys.get(h)
+            return None if k is None else (k[0], k[1], "p2sh-p2wpkh")
+        return None
+
+    # ------------------------------------------------------------------ coins
+    def unspent(self, minconf: int = 1, maxconf: int = 9_999_999) -> list[dict]:
+        st = self.state
+        with st.lock:
+            tip = st.coins_tip().height
+            scripts = self.scripts()
+            pool_spent = {(i.prevout.hash, i.prevout.n) for e in st.mempool.values() for i in e.tx.vin}
+            out = []
+            for txid, n, value, spk, height, coinbase in st.coins.outputs_for_scripts(scripts):
+                conf = tip - height + 1
+                if (txid, n) in pool_spent or not (minconf <= conf <= maxconf):
+                    continue
+                # CWalletTx::GetBlocksToMaturity: a coinbase needs COINBASE_MATURITY + 1 confirmations
+                mature = not coinbase or conf > _core.COINBASE_MATURITY
+                out.append({"txid": txid, "vout": n, "amount": value, "scriptPubKey": spk,
+                            "confirmations": conf, "spendable": mature, "coinbase": coinbase})
+            if minconf <= 0:
+                mine = set(scripts)
+                for txid, e in st.mempool.items():
+                    for n, o in enumerate(e.tx.vout):
+                        if o.script_pubkey in mine and (txid, n) not in pool_spent:
+                            out.append({"txid": txid, "vout": n, "amount": o.value, "scriptPubKey": o.script_pubkey,
+                                        "confirmations": 0, "spendable": True, "coinbase": False})
+            return out
+
+    def balance(self, minconf: int = 1) -> int:
+        return sum(u["amount"] for u in self.unspent(minconf) if u["spendable"])
+
+    def immature_balance(self) -> int:
+        return sum(u["amount"] for u in self.unspent(1) if not u["spendable"])
+
+    # ------------------------------------------------------------------ signing
+    def sign(self, tx, prevouts: dict[tuple[bytes, int], tuple[bytes, int]], extra_keys: list[bytes] = (),
+             hash_type: int = SIGHASH_ALL) -> tuple[object, bool, list[dict]]:
+        """SignTransaction: every input whose spent output is known and spendable by a wallet
+        key (or one of `extra_keys`). Returns (tx, complete, errors)."""
+        with self.lock:
+            return self._sign(tx, prevouts, extra_keys, hash_type)
+
+    def _sign(self, tx, prevouts, extra_keys, hash_type):
+        extra = {}
+        for sec in extra_keys:
+            pub = _core.secp_pubkey_create(sec, True)
+            extra[_core.hash160(pub)] = (sec, pub)
+        keys = dict(self.keys)
+        keys.update(extra)
+        sh = dict(self._p2sh_wpkh)
+        sh.update({_core.hash160(b"\x00\x14" + h): h for h in extra})
+        saved, saved_sh = self.keys, self._p2sh_wpkh
+        self.keys, self._p2sh_wpkh = keys, sh
+        try:
+            vins = list(tx.vin)
+            errors = []
+            for i, vin in enumerate(vins):
+                prev = prevouts.get((vin.prevout.hash, vin.prevout.n))
+                if prev is None:
+                    errors.append({"txid": vin.prevout.hash[::-1].hex(), "vout": vin.prevout.n,
+                                   "error": "Input not found or already spent"})
+                    continue
+                spk, amount = prev
+                k = self._key_for(spk)
+                if k is None:
+                    errors.append({"txid": vin.prevout.hash[::-1].hex(), "vout": vin.prevout.n,
+                                   "error": "Unable to sign input, missing key"})
+                    continue
+                sec, pub, kind = k
+                tx.vin = vins
+                raw = tx.serialize(True)
+                if kind in ("p2pkh", "p2pk"):
+                    msg = _core.signature_hash(spk, raw, i, hash_type, amount, 0)
+                    sig = _core.secp_sign(msg, sec) + bytes([hash_type])
+                    vin.script_sig = _push(sig) + (_push(pub) if kind == "p2pkh" else b"")
+                    vin.witness = []
+                else:
+                    code = p2pkh(_core.hash160(pub))
+                    msg = _core.signature_hash(code, raw, i, hash_type, amount, 1)
+                    sig = _core.secp_sign(msg, sec) + bytes([hash_type])
+                    vin.witness = [sig, pub]
+                    vin.script_sig = _push(b"\x00\x14" + _core.hash160(pub)) if kind == "p2sh-p2wpkh" else b""
+                vins[i] = vin
+            tx.vin = vins
+            return tx, not errors, errors
+        finally:
+            self.keys, self._p2sh_wpkh = saved, saved_sh
+
+    def create_transaction(self, outputs: list[tuple[bytes, int]], fee_rate: int = DEFAULT_FEE_RATE,
+                           subtract_fee: bool = False, minconf: int = 1):
+        """CreateTransaction: largest-first coin selection over spendable wallet outputs, a change
+        output to a fresh key, fee = fee_rate per kvB of the signed size. Returns (tx, fee)."""
+        if not outputs or any(v <= 0 for _, v in outputs):
+            raise WalletError("Invalid amount")
+        target = sum(v for _, v in outputs)
+        coins = sorted((u for u in self.unspent(minconf) if u["spendable"]), key=lambda u: -u["amount"])
+        change_spk = None
+        fee = 0
+        for _ in range(20):  # fee depends on the size, size on the inputs chosen
+            need = target + (0 if subtract_fee else fee)
+            chosen, total = [], 0
+            for u in coins:
+                if total >= need:
+                    break
+                chosen.append(u)
+                total += u["amount"]
+            if total < need:
+                raise WalletError("Insufficient funds")
+            tx = _core.Transaction()
+            tx.version = 2
+            vins = []
+            for u in chosen:
+                vin = _core.TxIn()
+                op = _core.OutPoint()
+                op.hash, op.n = u["txid"], u["vout"]
+                vin.prevout = op
+                vin.sequence = 0xfffffffe
+                vins.append(vin)
+            tx.vin = vins
+            outs = [_core.TxOut(v, s) for s, v in outputs]
+            if subtract_fee:
+                first = outs[0]
+                outs[0] = _core.TxOut(first.value - fee, first.script_pubkey)
+                if outs[0].value <= 0:
+                    raise WalletError("The transaction amount is too small to pay the fee")
+            change = total - target - (0 if subtract_fee else fee)
+            if change > 0:
+                if change_spk is None:
+                    change_spk = _core.address_to_script(self.new_address("change"), self.params.pubkey_prefix,
+                                                         self.params.script_prefix)
+                outs.append(_core.TxOut(change, change_spk))
+            tx.vout = outs
+            tx.lock_time = max(0, self.state.coins_tip().height)  # anti fee-sniping (src/wallet/wallet.cpp)
+            prevs = {(u["txid"], u["vout"]): (u["scriptPubKey"], u["amount"]) for u in chosen}
+            tx, complete, errors = self.sign(tx, prevs)
+            if not complete:
+                raise WalletError(f"Signing transaction failed: {errors}")
+            size = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4
+            want_fee = max(1, fee_rate * size // 1000)
+            if fee >= want_fee:
+                return tx, fee
+            fee = want_fee + 68  # headroom for a changed signature size
+        raise WalletError("Transaction fee did not converge")
+
+    def send(self, outputs: list[tuple[bytes, int]], subtract_fee: bool = False) -> bytes:
+        tx, _ = self.create_transaction(outputs, subtract_fee=subtract_fee)
+        ok, reason, _ = self.state.accept_to_mempool(tx)
+        if not ok:
+            raise WalletError(f"Transaction rejected: {reason}")
+        return tx.txid()

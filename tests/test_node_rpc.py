@@ -105,6 +105,12 @@ def test_submitblock_rejects(core, node_factory):
     bad.vtx = [cb]
     h = bad.header
     h.merkle_root = bad.merkle_root()[0]
+    ctx = core.get_epoch_context(0)
+    for n in range(64):  # solve it (regtest target 2^255): the reward rule is checked at connection
+        fin, mix = core.kawpow_hash(ctx, h.height, h.kawpow_header_hash()[::-1], n)
+        if fin[0] < 0x80:
+            h.nonce64, h.mix_hash = n, mix[::-1]
+            break
     bad.header = h
     assert c.submitblock(bad.serialize(act).hex()) == "bad-cb-community-autonomous-amount"
     # merkle mismatch

@@ -176,24 +176,24 @@ def test_tx_relay_and_mempool_message(core, tmp_path):
     try:
         b = _node(core, tmp_path, "b", ["-listen", "-port=0", f"-connect=127.0.0.1:{a.connman.port}"])
         assert _wait(lambda: a.peer_count() == 1 and b.peer_count() == 1)
-        tx = core.Transaction()
-        i, o, op = core.TxIn(), core.TxOut(), core.OutPoint()
-        op.hash, op.n = bytes([7]) * 32, 0
-        i.prevout = op
-        o.value, o.script_pubkey = 5000, b"\x51"
-        tx.vin, tx.vout = [i], [o]
+        w = a.wallet.new_address()
+        wspk = core.address_to_script(w, a.params.pubkey_prefix, a.params.script_prefix)
+        a.miner.generate(wspk, 101)  # the first coinbase matures
+        assert _wait(lambda: b.state.height() == 101)
+        tx, fee = a.wallet.create_transaction([(b"\x51", 5000)])
+        assert fee > 0
         txid = a.table.execute("sendrawtransaction", [tx.serialize(True).hex()])
         h = core.u256_from_hex(txid)
         assert _wait(lambda: h in b.state.mempool)
-        # a third node joining b asks for its mempool and gets the tx too
+        # a third node joining b syncs the chain, asks for b's mempool and gets the tx too
         c = _node(core, tmp_path, "c", [f"-connect=127.0.0.1:{b.connman.port}"])
-        assert _wait(lambda: c.peer_count() == 1)
+        assert _wait(lambda: c.peer_count() == 1 and c.state.height() == 101)
         c.connman.peers[0].send("mempool")
         assert _wait(lambda: h in c.state.mempool)
         # mined on a: removed from a's pool; b learns the block and drops it too
         a.miner.generate(a.mining_script, 1)
         assert h not in a.state.mempool
-        assert _wait(lambda: b.state.height() == 1 and h not in b.state.mempool)
+        assert _wait(lambda: b.state.height() == 102 and h not in b.state.mempool)
     finally:
         for n in (c, b, a):
             if n is not None:

@@ -11,6 +11,7 @@ import os
 import pytest
 
 from test_node_rpc import client, node_factory  # noqa: F401 — shared fixtures
+from wallet_util import fund, mature_coin, spend
 
 
 def _rpc_error(fn, *a):
@@ -45,8 +46,9 @@ def test_control_and_hidden(core, node_factory):  # noqa: F811
 def test_mempool_packages_persist_and_proofs(core, node_factory):  # noqa: F811
     node, addr = node_factory()
     c = client(node)
-    c.generatetoaddress(2, addr)
-    parent = _tx(c, addr, "11" * 32)
+    fund(c)
+    u = mature_coin(c)
+    parent = spend(c, u["txid"], u["vout"], u["amount"], addr, 1.0)
     dec = c.decoderawtransaction(parent)
     assert dec["vout"][0]["valueSat"] == 100_000_000
     assert c.testmempoolaccept([parent]) == [{"txid": dec["txid"], "allowed": True}]
@@ -55,14 +57,18 @@ def test_mempool_packages_persist_and_proofs(core, node_factory):  # noqa: F811
     assert not res["allowed"] and "txn-already-in-mempool" in res["reject-reason"]
     bad = c.createrawtransaction([{"txid": "22" * 32, "vout": 0}, {"txid": "22" * 32, "vout": 0}], {addr: 1})
     assert "bad-txns-inputs-duplicate" in c.testmempoolaccept([bad])[0]["reject-reason"]
-    child = _tx(c, addr, ptxid, 0, 0.5)
+    assert "missing-inputs" in c.testmempoolaccept([_tx(c, addr, "33" * 32)])[0]["reject-reason"]
+    change = dec["vout"][1]["value"]
+    child = spend(c, ptxid, 1, change, addr, 0.5)
     ctxid = c.sendrawtransaction(child)
     assert c.getmempoolancestors(ctxid) == [ptxid]
     assert c.getmempooldescendants(ptxid) == [ctxid]
     e = c.getmempoolentry(ctxid)
     assert e["ancestorcount"] == 2 and e["depends"] == [ptxid] and e["descendantcount"] == 1
     assert list(c.getmempooldescendants(ptxid, True)) == [ctxid]
-    # savemempool + restart (-persistmempool default on)
+    # a second spend of the parent's change conflicts with the child
+    assert "txn-mempool-conflict" in c.testmempoolaccept([spend(c, ptxid, 1, change, addr, 0.25)])[0]["reject-reason"]
+    # savemempool + restart (-persistmempool default on): both re-enter through AcceptToMemoryPool
     c.savemempool()
     assert os.path.exists(os.path.join(node.datadir, "mempool.dat"))
     node.stop()
@@ -81,17 +87,19 @@ def test_mempool_packages_persist_and_proofs(core, node_factory):  # noqa: F811
     tampered = proof[:-2] + ("00" if proof[-2:] != "00" else "01")
     with pytest.raises(RuntimeError):
         assert c.verifytxoutproof(tampered) == [ctxid]
-    # chain tx stats: genesis + 3 coinbases + 2 txs
+    # chain tx stats: genesis + one coinbase per block + the 2 spends
+    height = c.getblockcount()
     stats = c.getchaintxstats()
-    assert stats["txcount"] == 1 + 3 + 2 and stats["window_block_count"] == 2
+    assert stats["txcount"] == 1 + height + 2
     assert c.decodeblock(c.getblock(h, 0))["hash"] == h
     # clearmempool
-    c.sendrawtransaction(_tx(c, addr, "33" * 32))
+    u = mature_coin(c)
+    c.sendrawtransaction(spend(c, u["txid"], u["vout"], u["amount"], addr, 1.0))
     c.clearmempool()
     assert c.getmempoolinfo()["size"] == 0
     # getblockhashes over the whole time range returns the active chain (minus genesis time filter)
     hs = c.getblockhashes(2**31 - 1, 0)
-    assert h in hs and len(hs) == 4
+    assert h in hs and len(hs) == height + 1
 
 
 def test_decodescript(core, node_factory):  # noqa: F811
@@ -147,7 +155,9 @@ def test_rest_block_tx_headers(core, node_factory):  # noqa: F811
     code, _, body = node.rest(f"/rest/headers/2/{hashes[0]}.json")
     assert [h["hash"] for h in json.loads(body)] == hashes[:2]
     assert node.rest(f"/rest/headers/0/{hashes[0]}.json")[0] == 400
-    txid = c.sendrawtransaction(_tx(c, addr, "44" * 32))
+    fund(c)
+    u = mature_coin(c)
+    txid = c.sendrawtransaction(spend(c, u["txid"], u["vout"], u["amount"], addr, 1.0))
     code, _, body = node.rest(f"/rest/tx/{txid}.json")
     assert code == 200 and json.loads(body)["txid"] == txid
     assert node.rest(f"/rest/tx/{txid}.hex")[2].decode() == c.getrawtransaction(txid)

@@ -1,0 +1,204 @@
+"""Wallet, UTXO set, block connection / undo and AcceptToMemoryPool through a regtest node's
+RPCs (the reference's functional wallet_basic / mempool_* / feature_reindex / rpc_blockchain
+gettxoutsetinfo tests, for the subset this engine offers)."""
+import os
+
+import pytest
+
+from test_node_rpc import client, node_factory  # noqa: F401 — shared fixtures
+from wallet_util import fund, mature_coin, spend
+
+
+
+def _external(core):
+    return core.base58check_encode(bytes([42]) + bytes(range(1, 21)))  # regtest PUBKEY_ADDRESS prefix
+
+
+def test_balance_send_confirm_gettxout(core, node_factory):  # noqa: F811
+    node, _ = node_factory()
+    c = client(node)
+    ext = _external(core)
+    fund(c)
+    info = c.getwalletinfo()
+    assert info["balance"] > 0 and info["immature_balance"] > 0
+    bal = c.getbalance()
+    assert bal == pytest.approx(mature_coin(c)["amount"])
+    txid = c.sendtoaddress(ext, 10)
+    assert txid in c.getrawmempool()
+    entry = c.getmempoolentry(txid)
+    fee = entry["fee"] if "fee" in entry else None
+    # the change is unconfirmed, the spent coinbase is gone from the confirmed balance
+    assert c.getbalance() == pytest.approx(0.0)
+    assert c.getunconfirmedbalance() == pytest.approx(bal - 10 - (fee or 0), abs=0.01)
+    before = c.gettxoutsetinfo()
+    c.generatetoaddress(1, c.getnewaddress())
+    assert c.getrawmempool() == []
+    out = c.gettxout(txid, 0)
+    assert out["value"] == 10 and out["confirmations"] == 1 and not out["coinbase"]
+    assert out["scriptPubKey"]["addresses"] == [ext]
+    after = c.gettxoutsetinfo()
+    # +2 outputs of the spend, +coinbase outputs, -1 spent coinbase output
+    assert after["height"] == before["height"] + 1
+    assert after["bestblock"] != before["bestblock"] and after["hash_serialized_2"] != before["hash_serialized_2"]
+    # spent outputs are gone; mempool-spent outputs are hidden unless include_mempool=false
+    u = mature_coin(c)
+    t2 = c.sendrawtransaction(spend(c, u["txid"], u["vout"], u["amount"], ext, 1.0))
+    assert c.gettxout(u["txid"], u["vout"]) is None
+    assert c.gettxout(u["txid"], u["vout"], False) is not None
+    assert c.gettxout(t2, 0)["confirmations"] == 0
+
+
+def test_consensus_rejections(core, node_factory):  # noqa: F811
+    node, _ = node_factory()
+    c = client(node)
+    ext = _external(core)
+    w = c.getnewaddress()
+    c.generatetoaddress(99, w)
+    cb = [u for u in c.listunspent(1, 9999999, [w])]
+    assert cb and not any(u["spendable"] for u in cb)
+    first = min(cb, key=lambda u: -u["confirmations"])
+    with pytest.raises(RuntimeError, match="premature-spend-of-coinbase"):
+        c.sendrawtransaction(spend(c, first["txid"], first["vout"], first["amount"], ext, 1.0))
+    c.generatetoaddress(1, w)
+    good = spend(c, first["txid"], first["vout"], first["amount"], ext, 1.0)
+    # a bad signature: flip a byte inside the DER signature of input 0
+    tx = core.Transaction.deserialize(bytes.fromhex(good))
+    vin = list(tx.vin)
+    sig = bytearray(vin[0].script_sig)
+    sig[10] ^= 1
+    vin[0].script_sig = bytes(sig)
+    tx.vin = vin
+    with pytest.raises(RuntimeError, match="script-verify|SCRIPT_ERR|mandatory"):
+        c.sendrawtransaction(tx.serialize(True).hex())
+    # no fee at all: below the min relay fee
+    nofee = spend(c, first["txid"], first["vout"], first["amount"], ext, first["amount"], fee=0)
+    with pytest.raises(RuntimeError, match="min relay fee"):
+        c.sendrawtransaction(nofee)
+    # a fee far above the absurd-fee cap is refused unless allowhighfees
+    high = spend(c, first["txid"], first["vout"], first["amount"], ext, 1.0, fee=first["amount"] - 1.0)
+    with pytest.raises(RuntimeError, match="absurdly-high-fee"):
+        c.sendrawtransaction(high)
+    txid = c.sendrawtransaction(good)
+    # double spend of the same coin
+    with pytest.raises(RuntimeError, match="txn-mempool-conflict"):
+        c.sendrawtransaction(spend(c, first["txid"], first["vout"], first["amount"], ext, 2.0))
+    c.generatetoaddress(1, w)
+    raw = c.createrawtransaction([{"txid": first["txid"], "vout": first["vout"]}], {ext: 2.0})
+    res = c.signrawtransaction(raw)
+    assert not res["complete"] and "already spent" in res["errors"][0]["error"]
+    with pytest.raises(RuntimeError, match="already in block chain"):
+        c.sendrawtransaction(good)  # RPC_VERIFY_ALREADY_IN_CHAIN
+    assert c.getrawtransaction(txid, True)["confirmations"] == 1
+
+
+def test_block_with_invalid_spend_is_rejected(core, node_factory):  # noqa: F811
+    """A block carrying a transaction with a bad signature fails ConnectBlock; the chain and the
+    UTXO set stay where they were."""
+    node, _ = node_factory()
+    c = client(node)
+    ext = _external(core)
+    fund(c)
+    u = mature_coin(c)
+    tx = core.Transaction.deserialize(bytes.fromhex(spend(c, u["txid"], u["vout"], u["amount"], ext, 1.0)))
+    vin = list(tx.vin)
+    sig = bytearray(vin[0].script_sig)
+    sig[10] ^= 1
+    vin[0].script_sig = bytes(sig)
+    tx.vin = vin
+    node.state.add_to_mempool(tx, 1_000_000)  # bypass ATMP to get it into a template
+    stats = c.gettxoutsetinfo()
+    with pytest.raises(RuntimeError, match="mandatory-script-verify-flag-failed"):
+        node.miner.generate(node.mining_script, 1)
+    assert c.getblockcount() == 101
+    assert c.gettxoutsetinfo()["hash_serialized_2"] == stats["hash_serialized_2"]
+
+
+def test_reorg_restores_utxo_and_mempool(core, node_factory):  # noqa: F811
+    node, _ = node_factory()
+    c = client(node)
+    ext = _external(core)
+    fund(c)
+    txid = c.sendtoaddress(ext, 3)
+    stats0 = c.gettxoutsetinfo()
+    h = c.generatetoaddress(1, c.getnewaddress())[0]
+    stats1 = c.gettxoutsetinfo()
+    assert c.getrawmempool() == []
+    c.invalidateblock(h)
+    assert c.getblockcount() == 101
+    assert c.gettxoutsetinfo()["hash_serialized_2"] == stats0["hash_serialized_2"]
+    assert c.getrawmempool() == [txid]  # back in the pool (UpdateMempoolForReorg)
+    c.reconsiderblock(h)
+    assert c.getbestblockhash() == h
+    assert c.gettxoutsetinfo()["hash_serialized_2"] == stats1["hash_serialized_2"]
+    assert c.getrawmempool() == []
+    # disconnect everything down to genesis: the UTXO set is empty again
+    c.invalidateblock(c.getblockhash(1))
+    s = c.gettxoutsetinfo()
+    assert s["height"] == 0 and s["txouts"] == 0 and s["total_amount"] == 0
+    c.reconsiderblock(c.getblockhash(1) if c.getblockcount() else h)
+    assert c.gettxoutsetinfo()["hash_serialized_2"] == stats1["hash_serialized_2"]
+
+
+def test_restart_reloads_and_rebuilds_utxo(core, node_factory, tmp_path):  # noqa: F811
+    node, _ = node_factory()
+    c = client(node)
+    ext = _external(core)
+    fund(c)
+    c.sendtoaddress(ext, 2)
+    c.generatetoaddress(1, c.getnewaddress())
+    stats = c.gettxoutsetinfo()
+    bal = c.getbalance()
+    node.stop()
+    chainstate = os.path.join(str(tmp_path), "regtest", "chainstate", "coins.dat")
+    assert os.path.exists(chainstate)
+    rev = os.path.join(str(tmp_path), "regtest", "blocks", "rev00000.dat")
+    assert open(rev, "rb").read(4) == b"DROW"
+    node, _ = node_factory()
+    c = client(node)
+    assert c.gettxoutsetinfo()["hash_serialized_2"] == stats["hash_serialized_2"]
+    assert c.getbalance() == pytest.approx(bal)  # the wallet's keys were persisted
+    node.stop()
+    os.remove(chainstate)  # lost snapshot: rebuilt by reconnecting the stored blocks
+    node, _ = node_factory()
+    c = client(node)
+    assert c.gettxoutsetinfo()["hash_serialized_2"] == stats["hash_serialized_2"]
+
+
+def test_segwit_outputs_sign_and_spend(core, node_factory):  # noqa: F811
+    """P2WPKH and P2SH-P2WPKH outputs of wallet keys: found, signed (BIP143) and spent."""
+    node, _ = node_factory()
+    c = client(node)
+    fund(c)
+    addr = c.getnewaddress()
+    h = core.base58check_decode(addr)[1:]
+    p2wpkh = b"\x00\x14" + h
+    p2sh = b"\xa9\x14" + core.hash160(p2wpkh) + b"\x87"
+    wtx = node.wallet.send([(p2wpkh, 4 * 10**8), (p2sh, 3 * 10**8)])
+    c.generatetoaddress(1, c.getnewaddress())
+    mine = {(u["txid"], u["vout"]): u for u in c.listunspent()}
+    wid = wtx[::-1].hex()
+    assert (wid, 0) in mine and (wid, 1) in mine
+    for n, amount in ((0, 4.0), (1, 3.0)):
+        signed = spend(c, wid, n, amount, _external(core), 1.0)
+        dec = c.decoderawtransaction(signed)
+        assert dec["vin"][0].get("txinwitness"), dec  # witness carries sig + pubkey
+        c.sendrawtransaction(signed)
+    c.generatetoaddress(1, c.getnewaddress())
+    assert c.getrawmempool() == []
+
+
+def test_privkey_import_export(core, node_factory):  # noqa: F811
+    node, _ = node_factory()
+    c = client(node)
+    addr = c.getnewaddress()
+    wif = c.dumpprivkey(addr)
+    assert core.base58check_decode(wif)[0] == 114 and len(core.base58check_decode(wif)) == 34
+    c.importprivkey(wif)
+    assert c.dumpprivkey(addr) == wif
+    with pytest.raises(RuntimeError, match="Invalid private key"):
+        c.importprivkey("notakey")
+    with pytest.raises(RuntimeError):
+        c.dumpprivkey(_external(core))
+    # sendtoaddress with no funds
+    with pytest.raises(RuntimeError, match="Insufficient funds"):
+        c.sendtoaddress(addr, 1)
