@@ -143,6 +143,7 @@ class ChainState:
         self.index_log: BlockIndexLog | None = None
         self._mem_blocks: dict[bytes, object] = {}  # block data when there is no datadir
         self.min_relay_fee = DEFAULT_MIN_RELAY_TX_FEE
+        self.script_threads = min(16, os.cpu_count() or 1)  # -par: script-check threads (CCheckQueue)
         self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
         self.flush_interval = 1000
         self._since_flush = 0
@@ -580,11 +581,12 @@ class ChainState:
 
         flags = _core.BLOCK_SCRIPT_VERIFY_FLAGS
         gpu = self._use_gpu_for(block)
-        res, undo = _core.connect_block(block, height, self.coins, True, gpu, mtp_at, mtp_prev, flags)
+        par = self.script_threads
+        res, undo = _core.connect_block(block, height, self.coins, True, gpu, mtp_at, mtp_prev, flags, par)
         if gpu and not res.ok and "script-verify" in res.reject:
             # a deferred (assume-valid) signature can flip a script that depends on a signature
             # failing: the host run decides
-            res, undo = _core.connect_block(block, height, self.coins, True, False, mtp_at, mtp_prev, flags)
+            res, undo = _core.connect_block(block, height, self.coins, True, False, mtp_at, mtp_prev, flags, par)
         if not res.ok:
             return ValidationState.invalid(res.reject, res.dos)
         if gpu and res.num_sigs:

@@ -297,20 +297,30 @@ void bind_script(py::module_& m) {
             return out;
         }, "deferred signatures as (pubkey, DER signature, message) for ops/secp.verify_batch");
     m.def("connect_block", [](const Block& block, int height, CoinsView& view, bool check_scripts, bool defer_sigs,
-                              py::object mtp_at, int64_t block_mtp, u32 flags) {
+                              py::object mtp_at, int64_t block_mtp, u32 flags, int threads) {
         ConnectOptions opt;
         opt.script_flags = flags;
         opt.check_scripts = check_scripts;
         opt.defer_sigs = defer_sigs;
         opt.block_mtp = block_mtp;
-        if (!mtp_at.is_none()) opt.mtp_at = [mtp_at](int h) { return mtp_at(h).cast<int64_t>(); };
+        opt.threads = threads;
+        if (!mtp_at.is_none())
+            opt.mtp_at = [mtp_at](int h) {
+                py::gil_scoped_acquire gil;
+                return mtp_at(h).cast<int64_t>();
+            };
         BlockUndo undo;
-        ConnectResult r = connect_block(block, height, view, opt, undo);
-        py::bytes undo_bytes = r.ok ? pyb(serialize_block_undo(undo)) : py::bytes();
-        return py::make_tuple(std::move(r), undo_bytes);
+        ConnectResult r;
+        Bytes ub;
+        {
+            py::gil_scoped_release rel;  // the UTXO pass and the script-check threads run without the GIL
+            r = connect_block(block, height, view, opt, undo);
+            if (r.ok) ub = serialize_block_undo(undo);
+        }
+        return py::make_tuple(std::move(r), pyb(ub));
     }, py::arg("block"), py::arg("height"), py::arg("view"), py::arg("check_scripts") = true,
        py::arg("defer_sigs") = false, py::arg("mtp_at") = py::none(), py::arg("block_mtp") = 0,
-       py::arg("flags") = kBlockScriptFlags,
+       py::arg("flags") = kBlockScriptFlags, py::arg("threads") = 1,
        "ConnectBlock against the view -> (ConnectResult, serialized CBlockUndo); the view is unchanged on failure");
     m.def("disconnect_block", [](const Block& block, const py::bytes& undo, CoinsView& view) {
         return disconnect_block(block, deserialize_block_undo(bytes_of(undo)), view);

@@ -2,7 +2,10 @@
 #include "coins.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <memory>
+#include <thread>
 #include <fstream>
 #include <map>
 #include <set>
@@ -399,6 +402,16 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
         res.sig_at.clear();
         return res;
     };
+    struct Check {
+        u32 t, i;
+        Amount value;
+        Bytes spk;
+        bool ok = true;
+        ScriptError err = ScriptError::OK;
+        std::vector<PendingSig> sigs;
+    };
+    std::vector<Check> checks;
+    std::vector<std::unique_ptr<PrecomputedTx>> caches(block.vtx.size());
     for (size_t t = 0; t < block.vtx.size(); ++t) {
         const Transaction& tx = block.vtx[t];
         const Uint256 txid = tx.txid();
@@ -442,18 +455,9 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
         res.sigop_cost += tx_sigop_cost(tx, spent, opt.script_flags);
         if (res.sigop_cost > kMaxBlockSigopsCost) return fail("bad-blk-sigops", 100);
         if (!tx.is_coinbase() && opt.check_scripts) {
-            const PrecomputedTx cache(tx);
-            for (size_t i = 0; i < tx.vin.size(); ++i) {
-                TxSigChecker checker(&tx, unsigned(i), spent[i]->out.value, &cache);
-                const size_t before = res.sigs.size();
-                if (opt.defer_sigs) checker.pending = &res.sigs;
-                ScriptError err;
-                if (!verify_script(tx.vin[i].script_sig, spent[i]->out.script_pubkey, &tx.vin[i].witness,
-                                   opt.script_flags, checker, &err))
-                    return fail(std::string("mandatory-script-verify-flag-failed (") + script_error_name(err) + ")",
-                                100);
-                for (size_t k = before; k < res.sigs.size(); ++k) res.sig_at.emplace_back(u32(t), u32(i));
-            }
+            caches[t] = std::make_unique<PrecomputedTx>(tx);
+            for (size_t i = 0; i < tx.vin.size(); ++i)
+                checks.push_back({u32(t), u32(i), spent[i]->out.value, spent[i]->out.script_pubkey});
         }
         // spend the inputs, recording them for undo
         if (!tx.is_coinbase()) {
@@ -478,6 +482,45 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
             c.coinbase = tx.is_coinbase();
             view.add(o, std::move(c));
             added.push_back(o);
+        }
+    }
+    // the script checks (CCheckQueue): inline, or spread over worker threads
+    auto run = [&](Check& c) {
+        const Transaction& tx = block.vtx[c.t];
+        TxSigChecker checker(&tx, c.i, c.value, caches[c.t].get());
+        if (opt.defer_sigs) checker.pending = &c.sigs;
+        c.ok = verify_script(tx.vin[c.i].script_sig, c.spk, &tx.vin[c.i].witness, opt.script_flags, checker, &c.err);
+    };
+    const int nthreads = std::max(1, std::min<int>(opt.threads, int(checks.size() / 16)));
+    if (nthreads <= 1) {
+        for (auto& c : checks) {
+            run(c);
+            if (!c.ok) break;
+        }
+    } else {
+        std::atomic<size_t> next{0};
+        std::atomic<size_t> first_bad{checks.size()};
+        auto worker = [&] {
+            for (size_t k; (k = next.fetch_add(1, std::memory_order_relaxed)) < checks.size();) {
+                if (k > first_bad.load(std::memory_order_relaxed)) break;  // a prior input already failed
+                run(checks[k]);
+                if (!checks[k].ok) {
+                    size_t cur = first_bad.load();
+                    while (k < cur && !first_bad.compare_exchange_weak(cur, k)) {}
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int w = 1; w < nthreads; ++w) pool.emplace_back(worker);
+        worker();
+        for (auto& th : pool) th.join();
+    }
+    for (auto& c : checks) {
+        if (!c.ok)
+            return fail(std::string("mandatory-script-verify-flag-failed (") + script_error_name(c.err) + ")", 100);
+        for (auto& p : c.sigs) {
+            res.sigs.push_back(std::move(p));
+            res.sig_at.emplace_back(c.t, c.i);
         }
     }
     return res;

@@ -100,6 +100,10 @@ struct ConnectOptions {
     // median time past of the block at `height` of this block's chain (BIP68 time locks)
     std::function<int64_t(int)> mtp_at;
     int64_t block_mtp = 0;     // MTP of the previous block (the block's lock-time reference)
+    // Script-check threads (CCheckQueue / -par): the UTXO pass stays serial, the collected
+    // input checks then run on this many threads (1 = inline). The first failing input in
+    // block order decides the reject reason, as with a serial run.
+    int threads = 1;
 };
 
 struct ConnectResult {

@@ -4,7 +4,6 @@
 #include "secp256k1.hpp"
 
 #include <cstring>
-#include <mutex>
 #include <vector>
 
 #include "hashes.hpp"
@@ -100,40 +99,67 @@ Fe fe_reduce512(const u64 t[8]) {
     return out;
 }
 
-// value (nl limbs) mod n
+// value (nl <= 8 limbs) mod n: fold hi * (2^256 - n) into lo until 4 limbs remain (fixed-size,
+// no allocation: 512 -> 386 -> 259 -> 256 bits)
 Scalar sc_reduce(const u64* t, int nl) {
-    std::vector<u64> v(t, t + nl);
-    while (v.size() > 4) {
-        bool hi_zero = true;
-        for (size_t i = 4; i < v.size(); ++i) hi_zero &= v[i] == 0;
-        if (hi_zero) {
-            v.resize(4);
-            break;
-        }
-        // v = lo + hi * NC
-        const size_t nh = v.size() - 4;
-        std::vector<u64> r(std::max<size_t>(4, nh + 3) + 1, 0);
-        for (int i = 0; i < 4; ++i) r[i] = v[i];
-        for (size_t i = 0; i < nh; ++i) {
+    u64 v[9] = {0};
+    for (int i = 0; i < nl; ++i) v[i] = t[i];
+    int n = nl;
+    while (n > 4 && v[n - 1] == 0) --n;
+    while (n > 4) {
+        const int nh = n - 4;
+        const int rn = (nh + 3 > 4 ? nh + 3 : 4) + 1;
+        u64 r[9] = {v[0], v[1], v[2], v[3], 0, 0, 0, 0, 0};
+        for (int i = 0; i < nh; ++i) {
             u64 carry = 0;
-            for (size_t j = 0; j < 3; ++j) {
+            for (int j = 0; j < 3; ++j) {
                 const u128 m = (u128)v[4 + i] * kNC[j] + r[i + j] + carry;
                 r[i + j] = (u64)m;
                 carry = (u64)(m >> 64);
             }
-            for (size_t k = i + 3; carry && k < r.size(); ++k) {
-                const u128 s = (u128)r[k] + carry;
-                r[k] = (u64)s;
-                carry = (u64)(s >> 64);
+            for (int k = i + 3; carry && k < rn; ++k) {
+                const u128 s2 = (u128)r[k] + carry;
+                r[k] = (u64)s2;
+                carry = (u64)(s2 >> 64);
             }
         }
-        while (r.size() > 4 && r.back() == 0) r.pop_back();
-        v.swap(r);
+        for (int i = 0; i < 9; ++i) v[i] = r[i];
+        n = rn;
+        while (n > 4 && v[n - 1] == 0) --n;
     }
     Scalar s;
-    for (size_t i = 0; i < 4 && i < v.size(); ++i) s.v[i] = v[i];
+    for (int i = 0; i < 4; ++i) s.v[i] = v[i];
     while (geq(s.v, kN)) sub4(s.v, s.v, kN);
     return s;
+}
+
+// 512-bit square: the six cross products once, doubled, plus the four squares
+void sqr4(const u64 a[4], u64 t[8]) {
+    u64 c[8] = {0};
+    for (int i = 0; i < 4; ++i) {
+        u64 carry = 0;
+        for (int j = i + 1; j < 4; ++j) {
+            const u128 m = (u128)a[i] * a[j] + c[i + j] + carry;
+            c[i + j] = (u64)m;
+            carry = (u64)(m >> 64);
+        }
+        c[i + 4] = carry;
+    }
+    u64 top = 0;
+    for (int i = 0; i < 8; ++i) {  // c *= 2
+        const u64 nt = c[i] >> 63;
+        c[i] = (c[i] << 1) | top;
+        top = nt;
+    }
+    u64 carry = 0;
+    for (int i = 0; i < 4; ++i) {
+        const u128 sq = (u128)a[i] * a[i];
+        u128 lo = (u128)c[2 * i] + (u64)sq + carry;
+        t[2 * i] = (u64)lo;
+        u128 hi = (u128)c[2 * i + 1] + (u64)(sq >> 64) + (u64)(lo >> 64);
+        t[2 * i + 1] = (u64)hi;
+        carry = (u64)(hi >> 64);
+    }
 }
 
 void be_to_limbs(const u8 b[32], u64 v[4]) {
@@ -155,7 +181,6 @@ Fe fe_small(u64 x) {
     return r;
 }
 
-Fe fe_mul_small(const Fe& a, u64 k) { return fe_mul(a, fe_small(k)); }
 
 }  // namespace
 
@@ -192,7 +217,11 @@ Fe fe_mul(const Fe& a, const Fe& b) {
     return fe_reduce512(t);
 }
 
-Fe fe_sqr(const Fe& a) { return fe_mul(a, a); }
+Fe fe_sqr(const Fe& a) {
+    u64 t[8];
+    sqr4(a.v, t);
+    return fe_reduce512(t);
+}
 
 bool fe_eq(const Fe& a, const Fe& b) { return std::memcmp(a.v, b.v, 32) == 0; }
 bool fe_is_zero(const Fe& a) { return (a.v[0] | a.v[1] | a.v[2] | a.v[3]) == 0; }
@@ -318,7 +347,7 @@ Gej gej_double(const Gej& a) {
     const Fe E = fe_add(fe_add(A, A), A), F = fe_sqr(E);
     Gej r;
     r.x = fe_sub(F, fe_add(D, D));
-    const Fe C8 = fe_mul_small(C, 8);
+    const Fe C2 = fe_add(C, C), C4 = fe_add(C2, C2), C8 = fe_add(C4, C4);
     r.y = fe_sub(fe_mul(E, fe_sub(D, r.x)), C8);
     const Fe yz = fe_mul(a.y, a.z);
     r.z = fe_add(yz, yz);
@@ -403,16 +432,61 @@ Gej mul_gen(const Scalar& k) {
     return r;
 }
 
+namespace {
+
+// width-5 NAF of k: digits in {0, +-1, +-3, ..., +-15}, least significant first
+int wnaf5(const Scalar& k, int8_t out[258]) {
+    u64 v[5] = {k.v[0], k.v[1], k.v[2], k.v[3], 0};
+    int len = 0;
+    while (v[0] | v[1] | v[2] | v[3] | v[4]) {
+        int d = 0;
+        if (v[0] & 1) {
+            d = int(v[0] & 31);
+            if (d >= 16) d -= 32;
+            if (d > 0) {  // v -= d
+                u64 b = u64(d);
+                for (int i = 0; i < 5 && b; ++i) {
+                    const u64 o = v[i];
+                    v[i] -= b;
+                    b = v[i] > o;
+                }
+            } else {  // v += -d
+                u64 c = u64(-d);
+                for (int i = 0; i < 5 && c; ++i) {
+                    v[i] += c;
+                    c = v[i] < c;
+                }
+            }
+        }
+        out[len++] = int8_t(d);
+        for (int i = 0; i < 4; ++i) v[i] = (v[i] >> 1) | (v[i + 1] << 63);
+        v[4] >>= 1;
+    }
+    return len;
+}
+
+Gej gej_neg(const Gej& a) {
+    Gej r = a;
+    if (!a.inf) r.y = fe_neg(a.y);
+    return r;
+}
+
+}  // namespace
+
 Gej mul(const Ge& p, const Scalar& k) {
     if (p.inf || k.is_zero()) return Gej{};
-    Gej tab[16];
-    tab[1] = gej_from_ge(p);
-    for (int j = 2; j < 16; ++j) tab[j] = gej_add_ge(tab[j - 1], p);
+    Gej tab[8];  // P, 3P, ..., 15P
+    tab[0] = gej_from_ge(p);
+    const Gej p2 = gej_double(tab[0]);
+    for (int j = 1; j < 8; ++j) tab[j] = gej_add(tab[j - 1], p2);
+    int8_t naf[258];
+    const int len = wnaf5(k, naf);
     Gej r;
-    for (int i = 63; i >= 0; --i) {
-        for (int d = 0; d < 4; ++d) r = gej_double(r);
-        const int nb = nibble(k, i);
-        if (nb) r = gej_add(r, tab[nb]);
+    for (int i = len - 1; i >= 0; --i) {
+        r = gej_double(r);
+        const int d = naf[i];
+        if (d > 0) r = gej_add(r, tab[d >> 1]);
+        else if (d < 0) r = gej_add(r, gej_neg(tab[(-d) >> 1]));
     }
     return r;
 }

@@ -112,6 +112,9 @@ class Node:
             methods_wallet.register(self.table, self)
         if a.get("minrelaytxfee") is not None:  # -minrelaytxfee=<CLORE per kvB>
             self.state.min_relay_fee = round(float(a.get("minrelaytxfee")) * 100_000_000)
+        par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free
+        cores = os.cpu_count() or 1
+        self.state.script_threads = max(1, min(16, cores + par if par <= 0 else par))
         self.state.gpu_signatures = a.get("gpusigs", "auto")  # -gpusigs=auto|on|off: GPU batch ECDSA in blocks
         if self.datadir is not None and a.get_bool("persistmempool", True):  # -persistmempool (LoadMempool)
             n = self.state.load_mempool(os.path.join(self.datadir, "mempool.dat"))

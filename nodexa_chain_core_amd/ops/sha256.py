@@ -18,7 +18,7 @@ def sha256d_batch(msgs, device: int = 0) -> np.ndarray:
         lens = {len(m) for m in msgs}
         if len(lens) > 1:
             raise ValueError("sha256d_batch needs equal-length messages")
-        msgs = np.frombuffer(b"".join(msgs), dtype=np.uint8).reshape(len(msgs), -1) if msgs else \
+        msgs = np.frombuffer(bytearray(b"".join(msgs)), dtype=np.uint8).reshape(len(msgs), -1) if msgs else \
             np.zeros((0, 0), np.uint8)
     n, length = msgs.shape
     if n == 0:
