@@ -162,9 +162,13 @@ class ChainState:
             self.block_pos[gh] = self.store.write(params.genesis)
             self.index_log.append(params.genesis.header.serialize(params.kawpow_activation_time),
                                   self.block_pos[gh], len(params.genesis.vtx))
-        self.undo = UndoStore(os.path.join(datadir, "blocks") if datadir else None, bytes(params.message_start))
+        bdir = os.path.join(datadir, "blocks") if datadir else None
+        self.undo = UndoStore(bdir, bytes(params.message_start))
+        self.asset_undo = UndoStore(bdir, bytes(params.message_start), prefix="aun")
         self.coins_path = os.path.join(datadir, "chainstate", "coins.dat") if datadir else None
+        self.assets_path = os.path.join(datadir, "chainstate", "assets.dat") if datadir else None
         self.coins = _core.CoinsView()
+        self.assets = _core.AssetsState()
         self._init_coins()
 
     # ------------------------------------------------------------------ load / reindex
@@ -236,6 +240,7 @@ class ChainState:
         if self.index_log is not None:
             self.index_log.close()
         self.undo.close()
+        self.asset_undo.close()
 
     # ------------------------------------------------------------------ signals
     def register(self, l: ValidationInterface) -> None:
@@ -430,12 +435,12 @@ class ChainState:
                 st = ValidationState.invalid("duplicate")
                 self._emit("block_checked", block, st)
                 return st
-            ok, reason, dos = _core.check_block(block, self.params, True)
+            prev = self.chain.find(block.header.prev)
+            ok, reason, dos = _core.check_block(block, self.params, True, self.asset_flags(prev))
             if not ok:
                 st = ValidationState.invalid(reason, dos)
                 self._emit("block_checked", block, st)
                 return st
-            prev = self.chain.find(block.header.prev)
             if prev is None:
                 st = ValidationState.invalid("prev-blk-not-found", 10)
                 self._emit("block_checked", block, st)
@@ -469,16 +474,35 @@ class ChainState:
         """Load the UTXO snapshot and bring it to the best stored chain (ReplayBlocks-lite)."""
         gh = self.chain.genesis().hash
         loaded = self.coins_path is not None and self.coins.load(self.coins_path)
+        if loaded:  # the asset state must describe the same block as the UTXO snapshot
+            raw = None
+            if os.path.exists(self.assets_path):
+                with open(self.assets_path, "rb") as f:
+                    raw = f.read()
+            if raw is None or not self.assets.deserialize(raw) or self.assets.best_block != self.coins.best_block:
+                log.log_printf("asset state missing or out of step with the UTXO snapshot; replaying from genesis")
+                loaded = False
         if not loaded or self.chain.find(self.coins.best_block) is None:
             if loaded:
                 log.log_printf("UTXO snapshot's best block is unknown; rebuilding the UTXO set from genesis")
             self.coins = _core.CoinsView()
             self.coins.best_block = gh  # the genesis coinbase is unspendable: never added
+            self.assets = _core.AssetsState()
         with self.lock:
             self._activate()
 
     def coins_tip(self):
         return self.chain.find(self.coins.best_block)
+
+    def asset_flags(self, prev):
+        """Asset deployments in force for the block after `prev` (AreAssetsDeployed,
+        AreMessagesDeployed / AreRestrictedAssetsDeployed, AreEnforcedValuesDeployed,
+        AreCoinbaseCheckAssetsDeployed: src/validation.cpp:13441-13510)."""
+        if prev is None:
+            return _core.AssetFlags()
+        states = {d.name: self.versionbits.state_for(prev, d) for d in self.versionbits.deployments}
+        return _core.AssetFlags(states.get("assets") == "active", states.get("messaging_restricted") == "active",
+                                states.get("enforce_value") in ("active", "locked_in"), states.get("coinbase") == "active")
 
     def invalidate_block(self, h: bytes) -> None:
         """InvalidateBlock: mark the block (and its descendants) invalid and move the UTXO set to
@@ -522,7 +546,8 @@ class ChainState:
                 undo = self.undo.read(cur.hash, cur.prev_hash)
                 if blk is None or undo is None:
                     raise RuntimeError(f"cannot disconnect {_core.u256_hex(cur.hash)}: block or undo data missing")
-                if not _core.disconnect_block(blk, undo, self.coins):
+                aundo = self.asset_undo.read(cur.hash, cur.prev_hash) or b""
+                if not _core.disconnect_block(blk, undo, self.coins, self.assets, aundo):
                     log.log_printf(f"disconnect of {_core.u256_hex(cur.hash)} found an inconsistent UTXO set")
                 self.coins.best_block = cur.prev_hash
                 disconnected.append(blk)
@@ -582,13 +607,20 @@ class ChainState:
         flags = _core.BLOCK_SCRIPT_VERIFY_FLAGS
         gpu = self._use_gpu_for(block)
         par = self.script_threads
-        res, undo = _core.connect_block(block, height, self.coins, True, gpu, mtp_at, mtp_prev, flags, par)
+        aflags = self.asset_flags(prev)
+
+        def connect(defer: bool):
+            return _core.connect_block(block, height, self.coins, True, defer, mtp_at, mtp_prev, flags, par,
+                                       self.assets, aflags, idx.hash)
+
+        res, undo = connect(gpu)
         if gpu and not res.ok and "script-verify" in res.reject:
             # a deferred (assume-valid) signature can flip a script that depends on a signature
             # failing: the host run decides
-            res, undo = _core.connect_block(block, height, self.coins, True, False, mtp_at, mtp_prev, flags, par)
+            res, undo = connect(False)
         if not res.ok:
             return ValidationState.invalid(res.reject, res.dos)
+        aundo = res.asset_undo
         if gpu and res.num_sigs:
             from ..ops import secp
 
@@ -600,13 +632,15 @@ class ChainState:
                 self.sig_stats["host_rechecks"] += 1
                 ok, err = _core.verify_input_host(block, t, i, value, spk, flags)
                 if not ok:
-                    _core.disconnect_block(block, undo, self.coins)
+                    _core.disconnect_block(block, undo, self.coins, self.assets, aundo)
                     return ValidationState.invalid(f"mandatory-script-verify-flag-failed ({err})", 100)
         ok, reason, dos = _core.check_coinbase_rewards(block, self.params, height, res.fees, True)
         if not ok:
-            _core.disconnect_block(block, undo, self.coins)
+            _core.disconnect_block(block, undo, self.coins, self.assets, aundo)
             return ValidationState.invalid(reason, dos)
         self.undo.write(idx.hash, idx.prev_hash, undo)
+        if aundo:
+            self.asset_undo.write(idx.hash, idx.prev_hash, aundo)
         self.coins.best_block = idx.hash
         self.record_confirmations(block, height)
         self._since_flush += 1
@@ -619,6 +653,15 @@ class ChainState:
         if self.coins_path is None or self._since_flush == 0:
             return
         os.makedirs(os.path.dirname(self.coins_path), exist_ok=True)
+        # assets.dat first: a crash between the two leaves an asset state that does not match the
+        # UTXO snapshot, which start-up detects (and replays) instead of mixing two states
+        self.assets.best_block = self.coins.best_block
+        tmp = self.assets_path + ".new"
+        with open(tmp, "wb") as f:
+            f.write(self.assets.serialize())
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self.assets_path)
         self.coins.save(self.coins_path)
         self._since_flush = 0
 
@@ -671,7 +714,8 @@ class ChainState:
             if txid in self.mempool:
                 return False, "txn-already-in-mempool", 0
             raw = tx.serialize(True)
-            why = _core.check_transaction(raw)
+            aflags = self.asset_flags(self.coins_tip())
+            why = _core.check_transaction(raw, self.params, aflags, False, True)
             if why:
                 return False, why, 0
             if tx.is_coinbase():
@@ -709,6 +753,9 @@ class ChainState:
             fee = in_sum - tx.value_out()
             if fee < 0:
                 return False, "bad-txns-in-belowout", 0
+            why = self._check_tx_assets(tx, raw, coins, aflags)
+            if why:
+                return False, why, 0
             vsize = (weight + 3) // 4
             if fee < self.min_relay_fee * vsize // 1000:
                 return False, "min relay fee not met", fee
@@ -726,6 +773,31 @@ class ChainState:
             if not test_only:
                 self.add_to_mempool(tx, fee)
             return True, "", fee
+
+    def _check_tx_assets(self, tx, raw: bytes, coins, aflags) -> str:
+        """The asset part of ATMP: no asset outputs before the deployment, CheckTxAssets against the
+        current asset state, names already being created in the pool (mapAssetToHash) and one
+        reissue per asset in the pool (mapReissuedAssets)."""
+        kinds = [_core.parse_asset_script(o.script_pubkey) for o in tx.vout]
+        nulls = [_core.parse_null_asset_script(o.script_pubkey) for o in tx.vout]
+        if not aflags.assets:
+            if any(kinds):
+                return "bad-txns-is-asset-and-asset-not-active"
+            if any(nulls):
+                return "bad-tx-null-asset-data-before-restricted-assets-activated"
+            return ""
+        pending, reissued = set(), set()
+        for e in self.mempool.values():
+            for o in e.tx.vout:
+                a = _core.parse_asset_script(o.script_pubkey)
+                if a is not None and a["type"] == "new_asset":
+                    pending.add(a["name"])
+                elif a is not None and a["type"] == "reissue_asset":
+                    reissued.add(a["name"])
+        for a in kinds:
+            if a is not None and a["type"] == "reissue_asset" and a["name"] in reissued:
+                return "bad-tx-reissue-chaining-not-allowed"
+        return _core.check_tx_assets(raw, coins, self.assets, aflags, pending)
 
     def wait_for_tip_change(self, old_hash: bytes, timeout: float) -> bool:
         with self.cv_tip:

@@ -6,6 +6,9 @@ CBlockUndo bytes come from the native core (`_core.connect_block`, the reference
 encoding). Files roll over at 128 MiB like blk files (MAX_BLOCKFILE_SIZE). Where each block's
 record lives is kept in an append-only `blocks/undo.idx` (block hash, file, offset, size), the
 counterpart of the undo position in CDiskBlockIndex; a torn last entry is ignored on load.
+
+A second store with prefix "aun" holds the asset undo records (the asset journal of each block,
+csrc/chain/assets.hpp), the role of CBlockAssetUndo in the reference's assets database.
 """
 from __future__ import annotations
 
@@ -22,8 +25,9 @@ def _sha256d(b: bytes) -> bytes:
 
 
 class UndoStore:
-    def __init__(self, bdir: str, magic: bytes):
+    def __init__(self, bdir: str, magic: bytes, prefix: str = "rev"):
         self.bdir = bdir
+        self.prefix = prefix
         self.magic = bytes(magic)
         self.pos: dict[bytes, tuple[int, int, int]] = {}
         self._mem: dict[bytes, bytes] = {}  # memory-only store (no datadir)
@@ -32,7 +36,7 @@ class UndoStore:
         if bdir is None:
             return
         os.makedirs(bdir, exist_ok=True)
-        idx = os.path.join(bdir, "undo.idx")
+        idx = os.path.join(bdir, "undo.idx" if prefix == "rev" else f"{prefix}.idx")
         if os.path.exists(idx):
             with open(idx, "rb") as f:
                 data = f.read()
@@ -46,7 +50,7 @@ class UndoStore:
         self._idx = open(idx, "ab")
 
     def _path(self, fi: int) -> str:
-        return os.path.join(self.bdir, f"rev{fi:05d}.dat")
+        return os.path.join(self.bdir, f"{self.prefix}{fi:05d}.dat")
 
     def write(self, block_hash: bytes, prev_hash: bytes, undo: bytes) -> None:
         if self.bdir is None:

@@ -445,8 +445,9 @@ void bind_extra(py::module_& m) {
 
     // ------------------------------------------------ block validation
     auto bc = [](const BlockCheck& c) { return py::make_tuple(c.ok, c.reject, c.dos); };
-    m.def("check_block", [bc](const Block& b, const ChainParams& p, bool merkle) { return bc(check_block(b, p, merkle)); },
-          py::arg("block"), py::arg("params"), py::arg("check_merkle") = true);
+    m.def("check_block", [bc](const Block& b, const ChainParams& p, bool merkle, const assets::Flags& f) {
+        return bc(check_block(b, p, merkle, f));
+    }, py::arg("block"), py::arg("params"), py::arg("check_merkle") = true, py::arg("asset_flags") = assets::Flags{});
     m.def("contextual_check_block", [bc](const Block& b, const ChainParams& p, int h) { return bc(contextual_check_block(b, p, h)); });
     m.def("check_coinbase_rewards", [bc](const Block& b, const ChainParams& p, int h, Amount fees, bool known) {
         return bc(check_coinbase_rewards(b, p, h, fees, known));

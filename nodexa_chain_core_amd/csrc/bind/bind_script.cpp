@@ -6,6 +6,7 @@
 
 #include "../chain/coins.hpp"
 #include "../chain/interpreter.hpp"
+#include "../chain/params.hpp"
 #include "../crypto/secp256k1.hpp"
 #include "../crypto/secp256k1_model32.hpp"
 
@@ -214,8 +215,12 @@ void bind_script(py::module_& m) {
         return pyb(h.data, 32);
     }, py::arg("script_code"), py::arg("tx"), py::arg("n_in"), py::arg("hash_type"), py::arg("amount") = 0,
        py::arg("sigversion") = 0, "SignatureHash (uint256 storage order)");
-    m.def("check_transaction", [](const py::bytes& tx_raw) { return check_transaction(tx_of(tx_raw)); },
-          "CheckTransaction reject reason, '' when valid");
+    m.def("check_transaction", [](const py::bytes& tx_raw, const ChainParams* params, const assets::Flags* flags,
+                                  bool block_check, bool mempool_check) {
+        return check_transaction(tx_of(tx_raw), true, params ? &params->assets : nullptr, flags, block_check,
+                                 mempool_check);
+    }, py::arg("tx"), py::arg("params") = nullptr, py::arg("asset_flags") = nullptr, py::arg("block_check") = false,
+       py::arg("mempool_check") = false, "CheckTransaction reject reason, '' when valid (asset rules with params)");
     m.def("script_sigop_count", [](const py::bytes& s, bool accurate) {
         return script_sigop_count(bytes_of(s), accurate);
     }, py::arg("script"), py::arg("accurate") = false);
@@ -290,6 +295,7 @@ void bind_script(py::module_& m) {
         .def_readonly("fees", &ConnectResult::fees)
         .def_readonly("sigop_cost", &ConnectResult::sigop_cost)
         .def_readonly("sig_at", &ConnectResult::sig_at)
+        .def_property_readonly("asset_undo", [](const ConnectResult& r) { return pyb(r.asset_undo); })
         .def_property_readonly("num_sigs", [](const ConnectResult& r) { return r.sigs.size(); })
         .def("sig_items", [](const ConnectResult& r) {
             py::list out;
@@ -297,8 +303,13 @@ void bind_script(py::module_& m) {
             return out;
         }, "deferred signatures as (pubkey, DER signature, message) for ops/secp.verify_batch");
     m.def("connect_block", [](const Block& block, int height, CoinsView& view, bool check_scripts, bool defer_sigs,
-                              py::object mtp_at, int64_t block_mtp, u32 flags, int threads) {
+                              py::object mtp_at, int64_t block_mtp, u32 flags, int threads, assets::State* asset_state,
+                              const assets::Flags& asset_flags, const py::bytes& block_hash) {
         ConnectOptions opt;
+        opt.assets = asset_state;
+        opt.asset_flags = asset_flags;
+        const std::string bh = block_hash;
+        if (bh.size() == 32) opt.block_hash = Uint256::from_bytes(reinterpret_cast<const u8*>(bh.data()));
         opt.script_flags = flags;
         opt.check_scripts = check_scripts;
         opt.defer_sigs = defer_sigs;
@@ -320,11 +331,15 @@ void bind_script(py::module_& m) {
         return py::make_tuple(std::move(r), pyb(ub));
     }, py::arg("block"), py::arg("height"), py::arg("view"), py::arg("check_scripts") = true,
        py::arg("defer_sigs") = false, py::arg("mtp_at") = py::none(), py::arg("block_mtp") = 0,
-       py::arg("flags") = kBlockScriptFlags, py::arg("threads") = 1,
+       py::arg("flags") = kBlockScriptFlags, py::arg("threads") = 1, py::arg("assets") = nullptr,
+       py::arg("asset_flags") = assets::Flags{}, py::arg("block_hash") = py::bytes(),
        "ConnectBlock against the view -> (ConnectResult, serialized CBlockUndo); the view is unchanged on failure");
-    m.def("disconnect_block", [](const Block& block, const py::bytes& undo, CoinsView& view) {
-        return disconnect_block(block, deserialize_block_undo(bytes_of(undo)), view);
-    }, "DisconnectBlock with its undo data: False if they did not match the view (it is still reverted)");
+    m.def("disconnect_block", [](const Block& block, const py::bytes& undo, CoinsView& view, assets::State* st,
+                                 const py::bytes& asset_undo) {
+        const Bytes au = bytes_of(asset_undo);
+        return disconnect_block(block, deserialize_block_undo(bytes_of(undo)), view, st, &au);
+    }, py::arg("block"), py::arg("undo"), py::arg("view"), py::arg("assets") = nullptr, py::arg("asset_undo") = py::bytes(),
+       "DisconnectBlock with its undo data: False if they did not match the view (it is still reverted)");
     m.def("verify_input_host", [](const Block& block, u32 tx_index, u32 n_in, int64_t value, const py::bytes& spk,
                                   u32 flags) {
         if (tx_index >= block.vtx.size() || n_in >= block.vtx[tx_index].vin.size())

@@ -376,7 +376,7 @@ bool verify_input_host(const Transaction& tx, unsigned n_in, const Coin& coin, u
 
 namespace {
 
-bool is_unspendable(const Bytes& spk) { return (!spk.empty() && spk[0] == 0x6a) || spk.size() > kMaxScriptSize; }
+bool is_unspendable(const Bytes& spk) { return assets::script_unspendable(spk); }
 
 }  // namespace
 
@@ -385,7 +385,9 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
     ConnectResult res;
     undo.vtxundo.clear();
     std::vector<OutPoint> added;
+    const size_t asset_mark = opt.assets ? opt.assets->mark() : 0;
     auto fail = [&](const std::string& reason, int dos) {
+        if (opt.assets) opt.assets->rollback_to(asset_mark);
         // roll back: restore what the block spent (later transactions first), then drop every
         // output it added (that also removes in-block outputs the restore just put back)
         for (size_t t = undo.vtxundo.size(); t-- > 0;) {
@@ -435,6 +437,19 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
             const Amount fee = in_sum - out_sum;
             res.fees += fee;
             if (res.fees < 0 || res.fees > kMaxMoney) return fail("bad-txns-accumulated-fee-outofrange", 100);
+            if (opt.assets) {
+                if (!opt.asset_flags.assets) {
+                    for (auto& o : tx.vout) {
+                        if (assets::asset_script_kind(o.script_pubkey) != assets::OutKind::NONE)
+                            return fail("bad-txns-assets-not-active", 100);
+                        if (assets::null_kind(o.script_pubkey) != assets::NullKind::NONE)
+                            return fail("bad-txns-null-data-assets-not-active", 100);
+                    }
+                } else {
+                    const std::string why = assets::check_tx_contextual(tx, spent, *opt.assets, opt.asset_flags);
+                    if (!why.empty()) return fail(why, 100);
+                }
+            }
             // BIP68 relative lock-times (CalculateSequenceLocks / EvaluateSequenceLocks)
             if (opt.sequence_locks && (opt.script_flags & SCRIPT_VERIFY_CHECKSEQUENCEVERIFY) && u32(tx.version) >= 2) {
                 int min_height = -1;
@@ -483,6 +498,11 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
             view.add(o, std::move(c));
             added.push_back(o);
         }
+        if (opt.assets && opt.asset_flags.assets) {
+            static const std::vector<Coin> kNoCoins;
+            assets::apply_tx(tx, tx.is_coinbase() ? kNoCoins : undo.vtxundo.back().prev, height, opt.block_hash,
+                             *opt.assets);
+        }
     }
     // the script checks (CCheckQueue): inline, or spread over worker threads
     auto run = [&](Check& c) {
@@ -523,12 +543,18 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
             res.sig_at.emplace_back(c.t, c.i);
         }
     }
+    if (opt.assets) {
+        res.asset_undo = opt.assets->journal_since(asset_mark);
+        opt.assets->clear_journal();  // the record now lives with the caller (asset undo store)
+    }
     return res;
 }
 
-bool disconnect_block(const Block& block, const BlockUndo& undo, CoinsView& view) {
+bool disconnect_block(const Block& block, const BlockUndo& undo, CoinsView& view, assets::State* assets,
+                      const Bytes* asset_undo) {
     if (undo.vtxundo.size() + 1 != block.vtx.size()) return false;
     bool clean = true;
+    if (assets && asset_undo && !asset_undo->empty() && !assets->undo(*asset_undo)) clean = false;
     for (size_t t = block.vtx.size(); t-- > 0;) {
         const Transaction& tx = block.vtx[t];
         const Uint256 txid = tx.txid();

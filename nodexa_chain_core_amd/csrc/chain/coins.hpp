@@ -10,8 +10,9 @@
 // coin as VARINT(height*2+coinbase) [VARINT(0)] + CTxOutCompressor, src/undo.h, compressor.h),
 // written with the blk-file framing plus the sha256d(block hash || undo) checksum.
 //
-// The asset layer's extra consensus rules (src/assets/) are not applied here: asset
-// outputs are carried and spent as plain outputs.
+// Assets: with `ConnectOptions::assets` set, every transaction also passes
+// Consensus::CheckTxAssets against the asset state and its asset effects are applied (assets.hpp);
+// the state changes are journalled and returned as the block's asset undo record.
 //
 // Signatures: with `defer_sigs` set, connect_block runs every script with a deferring checker and
 // returns the signatures for the GPU batch verifier (ops/secp.py); the caller then re-runs only
@@ -23,6 +24,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "assets.hpp"
 #include "interpreter.hpp"
 #include "primitives.hpp"
 
@@ -104,6 +106,10 @@ struct ConnectOptions {
     // input checks then run on this many threads (1 = inline). The first failing input in
     // block order decides the reject reason, as with a serial run.
     int threads = 1;
+    // Asset layer (null: asset outputs are plain outputs and no asset rule is applied)
+    assets::State* assets = nullptr;
+    assets::Flags asset_flags;
+    Uint256 block_hash;
 };
 
 struct ConnectResult {
@@ -114,6 +120,7 @@ struct ConnectResult {
     int64_t sigop_cost = 0;
     std::vector<PendingSig> sigs;            // with defer_sigs: every signature to verify
     std::vector<std::pair<u32, u32>> sig_at;  // (tx index, input index) of each entry of sigs
+    Bytes asset_undo;                          // the asset journal of the block (with opt.assets)
 };
 
 // Applies `block` (at `height`) to `view`; on failure the view is left unchanged.
@@ -121,8 +128,10 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
                             BlockUndo& undo);
 // Re-runs one input's scripts with host signature checks (the fallback for a rejected batch).
 bool verify_input_host(const Transaction& tx, unsigned n_in, const Coin& coin, u32 flags, ScriptError* err);
-// Reverts `block` with its undo data; false if the data do not match the view.
-bool disconnect_block(const Block& block, const BlockUndo& undo, CoinsView& view);
+// Reverts `block` with its undo data; false if the data do not match the view. With `assets`, the
+// block's asset undo record is reverted too.
+bool disconnect_block(const Block& block, const BlockUndo& undo, CoinsView& view, assets::State* assets = nullptr,
+                      const Bytes* asset_undo = nullptr);
 
 // GetLegacySigOpCount: inaccurate sigops of every scriptSig and scriptPubKey.
 int64_t tx_legacy_sigops(const Transaction& tx);

@@ -1,6 +1,8 @@
 // Script interpreter: see interpreter.hpp.
 #include "interpreter.hpp"
 
+#include "assets.hpp"
+
 #include <algorithm>
 #include <climits>
 #include <set>
@@ -902,7 +904,8 @@ bool verify_script(const Bytes& script_sig, const Bytes& script_pubkey, const st
     return set_err(err, ScriptError::OK);
 }
 
-std::string check_transaction(const Transaction& tx, bool check_duplicate_inputs) {
+std::string check_transaction(const Transaction& tx, bool check_duplicate_inputs, const assets::Params* asset_params,
+                              const assets::Flags* flags, bool block_check, bool mempool_check) {
     if (tx.vin.empty()) return "bad-txns-vin-empty";
     if (tx.vout.empty()) return "bad-txns-vout-empty";
     if (tx.bytes(false).size() * 4 > 8000000) return "bad-txns-oversize";  // GetMaxBlockWeight() after HIP2
@@ -923,6 +926,10 @@ std::string check_transaction(const Transaction& tx, bool check_duplicate_inputs
     } else {
         for (auto& in : tx.vin)
             if (in.prevout.is_null()) return "bad-txns-prevout-null";
+    }
+    if (asset_params) {
+        const assets::Flags none;
+        return assets::check_tx_structure(tx, *asset_params, flags ? *flags : none, block_check, mempool_check);
     }
     return "";
 }

@@ -141,7 +141,15 @@ bool verify_script(const Bytes& script_sig, const Bytes& script_pubkey, const st
 
 // Context-free transaction checks (CheckTransaction, src/consensus/tx_verify.cpp:169; the asset
 // null-data rules are not included). Returns "" or the reference's reject reason.
-std::string check_transaction(const Transaction& tx, bool check_duplicate_inputs = true);
+// CheckTransaction. With `asset_params`, also the asset rules of CheckTransaction (assets.hpp),
+// under the given deployment flags (block_check: called from CheckBlock; mempool_check: from ATMP).
+namespace assets {
+struct Params;
+struct Flags;
+}  // namespace assets
+std::string check_transaction(const Transaction& tx, bool check_duplicate_inputs = true,
+                              const assets::Params* asset_params = nullptr, const assets::Flags* flags = nullptr,
+                              bool block_check = false, bool mempool_check = false);
 constexpr Amount kMaxMoney = Amount(1300000000) * COIN;  // src/amount.h:29
 
 // DER / pubkey encoding rules exposed for tests and policy.

@@ -1,5 +1,8 @@
 #include "params.hpp"
 
+#include <stdexcept>
+#include <vector>
+
 #include "script.hpp"
 
 namespace nodexa {
@@ -38,6 +41,28 @@ Block clore_genesis(u32 time, u32 nonce, u32 bits, int32_t version, Amount rewar
 
 }  // namespace
 
+namespace {
+
+// test and regtest share one set of burn addresses (src/chainparams.cpp:393-403, 538-548)
+const std::vector<std::string> kTestBurnAddresses = {
+    "J1VQJKLSLVZ4syiCAx5hEPq8BrkFaxAXAi", "J2yh4DiLETuVVDvpvBNSq3QCmHcdMmNEdp", "J3PE3FsHqfszvz7nhwK2Gc32wykrc7pNMA",
+    "J4yKRTYF2nRryYEnupsNnQQmRKsQhdspYB", "J58ndjHjLYKHMszr4ehUg9YMWPAiXNEepa", "J68wpmVvdE6bMSkiCEDQWCHCKZs4VVdE2G",
+    "J7MSidYgNJrPE15ouEsXPYXFYH2AAPXmhr", "J8uX8jfZn14P1VNzh6YjSzLaRTQAdoFSHn", "J9CrKy8m548AvSbcv1mcn7tyJQkgcwVfj6",
+    "JGYQBki6wWWnJLp2dcgdtNZWs9a2e1nXM3"};
+
+void set_burn_addresses(ChainParams& p, const std::vector<std::string>& a) {
+    Bytes* spk[10] = {&p.assets.spk_root, &p.assets.spk_reissue, &p.assets.spk_sub, &p.assets.spk_unique,
+                      &p.assets.spk_msgchannel, &p.assets.spk_qualifier, &p.assets.spk_subqualifier,
+                      &p.assets.spk_restricted, &p.assets.spk_tag, &p.assets.spk_global};
+    for (int i = 0; i < 10; ++i) {
+        p.asset_burn_addresses[i] = a[size_t(i)];
+        if (!address_to_script(a[size_t(i)], p.pubkey_prefix, p.script_prefix, *spk[i]))
+            throw std::logic_error("bad burn address " + a[size_t(i)]);
+    }
+}
+
+}  // namespace
+
 ChainParams make_chain_params(const std::string& network) {
     ChainParams p;
     if (network == "main") {
@@ -59,6 +84,11 @@ ChainParams make_chain_params(const std::string& network) {
         p.dgw_activation_block = 1;
         p.kawpow_activation_time = 1651444217;
         p.x16rv2_activation_time = 1569945600;
+        set_burn_addresses(p, {"AP6RNAdjGgkX2QERU3Gr5VV5hvidu6xgau", "AKsyQ9K9Kxftcb77Veiv91kA2VugPY45PL",
+                               "AbXjGsYEt89DUARDsQoXLAB3t4EpKUd1D8", "APZ5XSUwfKXDtscpoPbWfNkeiNu3FFu6ee",
+                               "AVPHkMz1GCxqE85ZuoxsBWY62Fi1ygyBnG", "AXEv5tmqu6cnaskJbmrEEPKQGTnCkWBBTk",
+                               "AM2okBkzJb21QyMGepGqmintGNnCJuVoQs", "AMR2ckKABVwQnhdFaQiQaqfoqAQLSZdV2T",
+                               "AcjqNXmzBpoBCGgfzSMJqwZLnYiF4zoqtL", "AZuJi37imwSjTFBwExtJ12tG1BvSnUctZg"});
     } else if (network == "test") {
         p.network_id = "test";
         p.consensus.pow_limit = Uint256::from_hex("00ffffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff");
@@ -74,6 +104,8 @@ ChainParams make_chain_params(const std::string& network) {
         p.dgw_activation_block = 1;
         p.kawpow_activation_time = 1653247613;
         p.x16rv2_activation_time = 1567533600;
+        p.assets.testnet = true;
+        set_burn_addresses(p, kTestBurnAddresses);
     } else if (network == "regtest") {
         p.network_id = "regtest";
         p.consensus.subsidy_halving_interval = 150;
@@ -99,6 +131,7 @@ ChainParams make_chain_params(const std::string& network) {
         p.x16rv2_activation_time = 1569931200;
         p.mine_blocks_on_demand = true;
         p.mining_requires_peers = false;
+        set_burn_addresses(p, kTestBurnAddresses);
     } else {
         throw std::invalid_argument("unknown chain " + network);
     }

@@ -13,6 +13,7 @@
 
 #include <map>
 
+#include "assets.hpp"
 #include "primitives.hpp"
 
 namespace nodexa {
@@ -57,6 +58,10 @@ struct ChainParams {
     u32 equihash_activation_time = 0xffffffffu;
     int equihash_n = 200;
     int equihash_k = 9;
+    // Asset layer: burn amounts and burn scripts (src/chainparams.cpp burn addresses).
+    assets::Params assets;
+    std::string asset_burn_addresses[10];  // root, reissue, sub, unique, msgchannel, qualifier, subqualifier,
+                                           // restricted, tag, global
 
     PowAlgo algo_for(u32 time) const {
         if (time >= kawpow_activation_time) return PowAlgo::KAWPOW;

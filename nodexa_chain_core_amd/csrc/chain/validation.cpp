@@ -4,6 +4,7 @@
 #include <set>
 
 #include "../crypto/sha256.hpp"
+#include "interpreter.hpp"
 #include "script.hpp"
 
 namespace nodexa {
@@ -24,7 +25,7 @@ BlockCheck pass() {
 
 Bytes coinbase_height_prefix(int height) { return ScriptBuilder().push_int(height).s; }
 
-BlockCheck check_block(const Block& b, const ChainParams& p, bool check_merkle) {
+BlockCheck check_block(const Block& b, const ChainParams& p, bool check_merkle, const assets::Flags& asset_flags) {
     if (check_merkle) {
         bool mutated = false;
         const Uint256 root = block_merkle_root(b, &mutated);
@@ -39,16 +40,17 @@ BlockCheck check_block(const Block& b, const ChainParams& p, bool check_merkle) 
         if (b.vtx[i].is_coinbase()) return fail("bad-cb-multiple");
     const size_t sig = b.vtx[0].vin[0].script_sig.size();
     if (sig < 2 || sig > 100) return fail("bad-cb-length");
-    for (size_t i = 1; i < b.vtx.size(); ++i) {
-        const Transaction& tx = b.vtx[i];
-        if (tx.vin.empty()) return fail("bad-txns-vin-empty");
-        if (tx.vout.empty()) return fail("bad-txns-vout-empty");
-        for (auto& in : tx.vin)
-            if (in.prevout.is_null()) return fail("bad-txns-prevout-null");
+    // CheckTransaction on every transaction, with the asset rules (src/validation.cpp CheckBlock)
+    for (auto& tx : b.vtx) {
+        const std::string why = check_transaction(tx, true, &p.assets, &asset_flags, true, false);
+        if (!why.empty()) {
+            BlockCheck c;
+            c.reject = why;
+            c.dos = (why == "bad-txns-vin-empty" || why == "bad-txns-vout-empty" || why == "bad-txns-prevout-null") ? 10 : 100;
+            if (why == "bad-txns-coinbase-contains-asset-txes" || why == "bad-txns-asset-reissued-amount-isn't-zero") c.dos = 0;
+            return c;
+        }
     }
-    for (auto& tx : b.vtx)
-        for (auto& out : tx.vout)
-            if (out.value < 0) return fail("bad-txns-vout-negative");
     return pass();
 }
 

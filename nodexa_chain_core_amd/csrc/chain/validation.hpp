@@ -23,7 +23,8 @@ struct BlockCheck {
     int dos = 0;
 };
 
-BlockCheck check_block(const Block& b, const ChainParams& p, bool check_merkle = true);
+BlockCheck check_block(const Block& b, const ChainParams& p, bool check_merkle = true,
+                       const assets::Flags& asset_flags = assets::Flags{});
 BlockCheck contextual_check_block(const Block& b, const ChainParams& p, int height);
 BlockCheck check_coinbase_rewards(const Block& b, const ChainParams& p, int height, Amount fees,
                                   bool fees_known);
