@@ -287,7 +287,23 @@ void bind_script(py::module_& m) {
                                               c.height, c.coinbase));
             });
             return out;
-        }, "unspent outputs paying any of these scriptPubKeys: (txid, n, value, spk, height, coinbase)");
+        }, "unspent outputs paying any of these scriptPubKeys: (txid, n, value, spk, height, coinbase)")
+        .def("asset_outputs", [](const CoinsView& v, py::object hashes) {
+            // asset scripts (P2PKH prefix + OP_CLORE_ASSET payload) of these hash160s, or of all when None
+            std::set<std::string> want;
+            const bool all = hashes.is_none();
+            if (!all)
+                for (auto& h : hashes.cast<std::vector<py::bytes>>()) want.insert(std::string(h));
+            py::list out;
+            v.for_each([&](const OutPoint& o, const Coin& c) {
+                const Bytes& s = c.out.script_pubkey;
+                if (assets::asset_script_kind(s) == assets::OutKind::NONE) return;
+                if (!all && !want.count(std::string(reinterpret_cast<const char*>(s.data() + 3), 20))) return;
+                out.append(py::make_tuple(pyb(o.hash.data, 32), o.n, c.out.value, pyb(s), c.height, c.coinbase));
+            });
+            return out;
+        }, py::arg("hashes") = py::none(),
+           "unspent asset outputs to these hash160s (all when None): (txid, n, value, spk, height, coinbase)");
     py::class_<ConnectResult>(m, "ConnectResult")
         .def_readonly("ok", &ConnectResult::ok)
         .def_readonly("reject", &ConnectResult::reject)

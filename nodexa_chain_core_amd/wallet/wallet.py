@@ -140,6 +140,9 @@ class Wallet:
 
     def _key_for(self, spk: bytes):
         """(secret, pubkey, kind) for a scriptPubKey the wallet can sign, else None."""
+        if len(spk) > 31 and spk[25] == 0xC0 and _core.parse_asset_script(spk) is not None:
+            k = self._key_for(spk[:25])  # an asset output is spent like its P2PKH prefix
+            return None if k is None or k[2] != "p2pkh" else k
         if len(spk) == 25 and spk[:3] == b"\x76\xa9\x14" and spk[23:] == b"\x88\xac":
             k = self.keys.get(spk[3:23])
             return None if k is None else (k[0], k[1], "p2pkh")
@@ -240,6 +243,56 @@ class Wallet:
             return tx, not errors, errors
         finally:
             self.keys, self._p2sh_wpkh = saved, saved_sh
+
+    def fund_and_sign(self, pre_outputs: list, post_outputs: list, extra_inputs: list[dict] = (),
+                      fee_rate: int = DEFAULT_FEE_RATE, change_spk: bytes | None = None):
+        """A transaction whose outputs are `pre_outputs`, a CLORE change output, then `post_outputs`
+        (asset transactions need their issue / reissue data last), spending `extra_inputs`
+        (e.g. asset outputs: dicts with txid, vout, amount, scriptPubKey) plus CLORE coins for the
+        outputs' value and the fee. Returns (tx, fee)."""
+        target = sum(o.value for o in list(pre_outputs) + list(post_outputs))
+        coins = sorted((u for u in self.unspent(1) if u["spendable"]), key=lambda u: -u["amount"])
+        fee = 0
+        for _ in range(20):
+            need = target + fee
+            chosen, total = [], 0
+            for u in coins:
+                if total >= need:
+                    break
+                chosen.append(u)
+                total += u["amount"]
+            if total < need:
+                raise WalletError("Insufficient funds")
+            tx = _core.Transaction()
+            tx.version = 2
+            vins = []
+            for u in list(extra_inputs) + chosen:
+                vin = _core.TxIn()
+                op = _core.OutPoint()
+                op.hash, op.n = u["txid"], u["vout"]
+                vin.prevout = op
+                vin.sequence = 0xfffffffe
+                vins.append(vin)
+            tx.vin = vins
+            outs = list(pre_outputs)
+            change = total - need
+            if change > 0:
+                if change_spk is None:
+                    change_spk = _core.address_to_script(self.new_address("change"), self.params.pubkey_prefix,
+                                                         self.params.script_prefix)
+                outs.append(_core.TxOut(change, change_spk))
+            tx.vout = outs + list(post_outputs)
+            tx.lock_time = max(0, self.state.coins_tip().height)
+            prevs = {(u["txid"], u["vout"]): (u["scriptPubKey"], u["amount"]) for u in list(extra_inputs) + chosen}
+            tx, complete, errors = self.sign(tx, prevs)
+            if not complete:
+                raise WalletError(f"Signing transaction failed: {errors}")
+            size = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4
+            want = max(1, fee_rate * size // 1000)
+            if fee >= want:
+                return tx, fee
+            fee = want + 68
+        raise WalletError("Transaction fee did not converge")
 
     def create_transaction(self, outputs: list[tuple[bytes, int]], fee_rate: int = DEFAULT_FEE_RATE,
                            subtract_fee: bool = False, minconf: int = 1):
