@@ -121,7 +121,8 @@ def _read_compact_size(b: bytes, off: int) -> tuple[int, int]:
 
 
 class ChainState:
-    def __init__(self, params, datadir: str | None = None, strict_height: bool = False, reindex: bool = False):
+    def __init__(self, params, datadir: str | None = None, strict_height: bool = False, reindex: bool = False,
+                 indexes: dict | None = None):
         self.params = params
         self.chain = _core.HeaderChain(params)
         self.chain.strict_kawpow_height = strict_height
@@ -167,8 +168,11 @@ class ChainState:
         self.asset_undo = UndoStore(bdir, bytes(params.message_start), prefix="aun")
         self.coins_path = os.path.join(datadir, "chainstate", "coins.dat") if datadir else None
         self.assets_path = os.path.join(datadir, "chainstate", "assets.dat") if datadir else None
+        self.indexes_path = os.path.join(datadir, "chainstate", "indexes.dat") if datadir else None
+        self.index_flags = dict(indexes or {})  # txindex / addressindex / spentindex / timestampindex
         self.coins = _core.CoinsView()
         self.assets = _core.AssetsState()
+        self.indexes = _core.ChainIndexes(**self.index_flags)
         self._init_coins()
 
     # ------------------------------------------------------------------ load / reindex
@@ -482,12 +486,27 @@ class ChainState:
             if raw is None or not self.assets.deserialize(raw) or self.assets.best_block != self.coins.best_block:
                 log.log_printf("asset state missing or out of step with the UTXO snapshot; replaying from genesis")
                 loaded = False
+        if loaded and any(self.index_flags.values()):  # the indexes too (a changed -*index flag replays)
+            raw = None
+            if os.path.exists(self.indexes_path):
+                with open(self.indexes_path, "rb") as f:
+                    raw = f.read()
+            want = _core.ChainIndexes(**self.index_flags)
+            ok = raw is not None and want.deserialize(raw) and want.best_block == self.coins.best_block and \
+                all(getattr(want, k) == bool(v) for k, v in self.index_flags.items())
+            if ok:
+                self.indexes = want
+            else:
+                log.log_printf("chain indexes missing or built with other flags; replaying from genesis")
+                loaded = False
         if not loaded or self.chain.find(self.coins.best_block) is None:
             if loaded:
                 log.log_printf("UTXO snapshot's best block is unknown; rebuilding the UTXO set from genesis")
             self.coins = _core.CoinsView()
             self.coins.best_block = gh  # the genesis coinbase is unspendable: never added
             self.assets = _core.AssetsState()
+            self.indexes = _core.ChainIndexes(**self.index_flags)
+            self.indexes.best_block = gh
         with self.lock:
             self._activate()
 
@@ -549,6 +568,7 @@ class ChainState:
                 aundo = self.asset_undo.read(cur.hash, cur.prev_hash) or b""
                 if not _core.disconnect_block(blk, undo, self.coins, self.assets, aundo):
                     log.log_printf(f"disconnect of {_core.u256_hex(cur.hash)} found an inconsistent UTXO set")
+                self.indexes.disconnect(blk, cur.height, cur.hash, undo)
                 self.coins.best_block = cur.prev_hash
                 disconnected.append(blk)
                 cur = self.chain.find(cur.prev_hash)
@@ -639,6 +659,7 @@ class ChainState:
             _core.disconnect_block(block, undo, self.coins, self.assets, aundo)
             return ValidationState.invalid(reason, dos)
         self.undo.write(idx.hash, idx.prev_hash, undo)
+        self.indexes.connect(block, height, idx.hash, undo)
         if aundo:
             self.asset_undo.write(idx.hash, idx.prev_hash, aundo)
         self.coins.best_block = idx.hash
@@ -662,6 +683,13 @@ class ChainState:
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, self.assets_path)
+        if any(self.index_flags.values()):
+            tmp = self.indexes_path + ".new"
+            with open(tmp, "wb") as f:
+                f.write(self.indexes.serialize())
+                f.flush()
+                os.fsync(f.fileno())
+            os.replace(tmp, self.indexes_path)
         self.coins.save(self.coins_path)
         self._since_flush = 0
 

@@ -5,6 +5,7 @@
 #include <set>
 
 #include "../chain/coins.hpp"
+#include "../chain/indexes.hpp"
 #include "../chain/interpreter.hpp"
 #include "../chain/params.hpp"
 #include "../crypto/secp256k1.hpp"
@@ -356,6 +357,79 @@ void bind_script(py::module_& m) {
         return disconnect_block(block, deserialize_block_undo(bytes_of(undo)), view, st, &au);
     }, py::arg("block"), py::arg("undo"), py::arg("view"), py::arg("assets") = nullptr, py::arg("asset_undo") = py::bytes(),
        "DisconnectBlock with its undo data: False if they did not match the view (it is still reverted)");
+    py::class_<ChainIndexes, std::shared_ptr<ChainIndexes>>(m, "ChainIndexes")
+        .def(py::init([](bool tx, bool addr, bool spent, bool ts) {
+                 auto x = std::make_shared<ChainIndexes>();
+                 x->txindex = tx;
+                 x->addressindex = addr;
+                 x->spentindex = spent;
+                 x->timestampindex = ts;
+                 return x;
+             }),
+             py::arg("txindex") = false, py::arg("addressindex") = false, py::arg("spentindex") = false,
+             py::arg("timestampindex") = false)
+        .def_readonly("txindex", &ChainIndexes::txindex)
+        .def_readonly("addressindex", &ChainIndexes::addressindex)
+        .def_readonly("spentindex", &ChainIndexes::spentindex)
+        .def_readonly("timestampindex", &ChainIndexes::timestampindex)
+        .def_property("best_block", [](const ChainIndexes& x) { return pyb(x.best_block.data, 32); },
+                      [](ChainIndexes& x, const py::bytes& b) {
+                          const std::string h = b;
+                          need32(h, "best_block");
+                          x.best_block = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
+                      })
+        .def("connect", [](ChainIndexes& x, const Block& b, int height, const py::bytes& hash, const py::bytes& undo) {
+            const std::string h = hash;
+            need32(h, "hash");
+            x.connect(b, height, Uint256::from_bytes(reinterpret_cast<const u8*>(h.data())),
+                      deserialize_block_undo(bytes_of(undo)));
+        })
+        .def("disconnect", [](ChainIndexes& x, const Block& b, int height, const py::bytes& hash, const py::bytes& undo) {
+            const std::string h = hash;
+            need32(h, "hash");
+            x.disconnect(b, height, Uint256::from_bytes(reinterpret_cast<const u8*>(h.data())),
+                         deserialize_block_undo(bytes_of(undo)));
+        })
+        .def("tx_block", [](const ChainIndexes& x, const py::bytes& txid) -> py::object {
+            const std::string t = txid;
+            need32(t, "txid");
+            const Uint256* b = x.tx_block(Uint256::from_bytes(reinterpret_cast<const u8*>(t.data())));
+            if (!b) return py::none();
+            return pyb(b->data, 32);
+        })
+        .def("deltas", [](const ChainIndexes& x, int type, const py::bytes& h160, const std::string& asset, int start,
+                          int end) {
+            const std::string h = h160;
+            if (h.size() != 20) throw std::invalid_argument("hash160 must be 20 bytes");
+            py::list out;
+            for (auto& [name, d] : x.deltas(type, reinterpret_cast<const u8*>(h.data()), asset, start, end))
+                out.append(py::make_tuple(name, d.height, d.tx_index, pyb(d.txid.data, 32), d.index, d.spending, d.amount));
+            return out;
+        }, py::arg("type"), py::arg("hash160"), py::arg("asset") = "CLORE", py::arg("start") = 0, py::arg("end") = 0,
+           "[(asset, height, tx index, txid, index, spending, amount)] in chain order")
+        .def("unspent", [](const ChainIndexes& x, int type, const py::bytes& h160, const std::string& asset) {
+            const std::string h = h160;
+            if (h.size() != 20) throw std::invalid_argument("hash160 must be 20 bytes");
+            py::list out;
+            for (auto& [name, u] : x.unspent(type, reinterpret_cast<const u8*>(h.data()), asset))
+                out.append(py::make_tuple(name, pyb(u.txid.data, 32), u.index, u.amount, pyb(u.script), u.height));
+            return out;
+        }, py::arg("type"), py::arg("hash160"), py::arg("asset") = "CLORE",
+           "[(asset, txid, index, amount, script, height)] by height")
+        .def("spent", [](const ChainIndexes& x, const py::bytes& txid, u32 n) -> py::object {
+            const std::string t = txid;
+            need32(t, "txid");
+            const SpentInfo* s = x.spent(Uint256::from_bytes(reinterpret_cast<const u8*>(t.data())), n);
+            if (!s) return py::none();
+            return py::make_tuple(pyb(s->txid.data, 32), s->input, s->height, s->amount, s->addr_type, pyb(s->h160, 20));
+        })
+        .def("timestamps", [](const ChainIndexes& x, u32 low, u32 high) {
+            py::list out;
+            for (auto& h : x.timestamps(low, high)) out.append(pyb(h.data, 32));
+            return out;
+        })
+        .def("serialize", [](const ChainIndexes& x) { return pyb(x.serialize()); })
+        .def("deserialize", [](ChainIndexes& x, const py::bytes& b) { return x.deserialize(bytes_of(b)); });
     m.def("verify_input_host", [](const Block& block, u32 tx_index, u32 n_in, int64_t value, const py::bytes& spk,
                                   u32 flags) {
         if (tx_index >= block.vtx.size() || n_in >= block.vtx[tx_index].vin.size())

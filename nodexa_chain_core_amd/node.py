@@ -27,7 +27,7 @@ from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
 from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, GpuKawpowBackend, MinerController
-from .rpc import methods, methods_assets, methods_ext, methods_wallet
+from .rpc import methods, methods_assets, methods_ext, methods_index, methods_wallet
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
 from .utils import log, metrics
 from .utils.config import ArgsManager, gpu_list
@@ -95,8 +95,9 @@ class Node:
             from .utils import sync
 
             sync.enable(True)
+        indexes = {k: a.get_bool(k, False) for k in ("txindex", "addressindex", "spentindex", "timestampindex")}
         self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False),
-                                reindex=a.get_bool("reindex", False))
+                                reindex=a.get_bool("reindex", False), indexes=indexes)
         for flag, attr in (("maxreorg", "max_reorg_depth"), ("minreorgpeers", "min_reorg_peers"),
                            ("minreorgage", "min_reorg_age")):  # reorg guard knobs (src/init.cpp)
             if a.is_set(flag):
@@ -112,6 +113,7 @@ class Node:
             methods_wallet.register(self.table, self)
         self.asset_wallet = None
         methods_assets.register(self.table, self)  # chain-state asset methods work without a wallet
+        methods_index.register(self.table, self)
         if a.get("minrelaytxfee") is not None:  # -minrelaytxfee=<CLORE per kvB>
             self.state.min_relay_fee = round(float(a.get("minrelaytxfee")) * 100_000_000)
         par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free
@@ -330,12 +332,71 @@ class Node:
 
         return solve_cpu(inp)
 
+    def _rest_getutxos(self, parts: list[str], json):
+        """rest_getutxos (src/rest.cpp): which of up to 15 outpoints are unspent, optionally in the
+        mempool view. bin = int32 height, tip hash, bitmap, [u32 0, u32 height, CTxOut] per coin."""
+        import struct
+
+        def _cs(n: int) -> bytes:  # CompactSize
+            if n < 253:
+                return bytes([n])
+            return b"\xfd" + struct.pack("<H", n) if n <= 0xFFFF else b"\xfe" + struct.pack("<I", n)
+
+        if not parts:
+            return 400, "text/plain", b"Error: empty request"
+        last, _, fmt = parts[-1].partition(".")
+        parts = parts[:-1] + [last]
+        check_mempool = parts[0] == "checkmempool"
+        if check_mempool:
+            parts = parts[1:]
+        if fmt not in ("bin", "hex", "json"):
+            return 404, "text/plain", b"output format not found (available: .bin, .hex, .json)"
+        if not parts or len(parts) > 15:
+            return 400, "text/plain", b"Error: max outpoints exceeded (max: 15, tried: %d)" % len(parts)
+        st = self.state
+        outs = []
+        try:
+            for q in parts:
+                txid, _, n = q.partition("-")
+                outs.append((_core.u256_from_hex(txid), int(n)))
+        except ValueError:
+            return 400, "text/plain", b"Parse error"
+        with st.lock:
+            tip = st.coins_tip()
+            pool_spent = {(i.prevout.hash, i.prevout.n) for e in st.mempool.values() for i in e.tx.vin} \
+                if check_mempool else set()
+            found = []
+            for h, n in outs:
+                c = st.coins.get(h, n)
+                if c is None and check_mempool and h in st.mempool and n < len(st.mempool[h].tx.vout):
+                    o = st.mempool[h].tx.vout[n]
+                    c = (o.value, o.script_pubkey, 0x7FFFFFFF, False)  # MEMPOOL_HEIGHT
+                if c is not None and (h, n) in pool_spent:
+                    c = None
+                found.append(c)
+        bits = "".join("1" if c is not None else "0" for c in found)
+        coins = [c for c in found if c is not None]
+        if fmt == "json":
+            body = {"chainHeight": tip.height, "chaintipHash": _core.u256_hex(tip.hash), "bitmap": bits,
+                    "utxos": [{"height": c[2], "value": c[0] / 1e8,
+                               "scriptPubKey": {"hex": c[1].hex()}} for c in coins]}
+            return 200, "application/json", json.dumps(body).encode()
+        bitmap = bytearray((len(found) + 7) // 8)
+        for i, c in enumerate(found):
+            if c is not None:
+                bitmap[i // 8] |= 1 << (i % 8)
+        raw = struct.pack("<i", tip.height) + bytes(tip.hash) + _cs(len(bitmap)) + bytes(bitmap)
+        raw += _cs(len(coins))
+        for value, spk, height, _ in coins:
+            raw += struct.pack("<IIq", 0, height, value) + _cs(len(spk)) + spk
+        return (200, "application/octet-stream", raw) if fmt == "bin" else (200, "text/plain", raw.hex().encode())
+
     def rest(self, path: str):
         """REST (src/rest.cpp:569-580): /rest/chaininfo.json, /rest/block/<hash>.{bin,hex,json},
         /rest/block/notxdetails/<hash>.{bin,hex,json}, /rest/headers/<n>/<hash>.{bin,hex,json},
-        /rest/tx/<txid>.{bin,hex,json} (mempool), /rest/mempool/{info,contents}.json,
-        /rest/blockhashbyheight/<h>.{json,hex,bin}, /rest/metrics (Prometheus). /rest/getutxos
-        needs the UTXO set (DEFER)."""
+        /rest/tx/<txid>.{bin,hex,json} (mempool, -txindex or an unspent output), /rest/mempool/{info,contents}.json,
+        /rest/blockhashbyheight/<h>.{json,hex,bin}, /rest/getutxos[/checkmempool]/<txid>-<n>/....{bin,hex,json}
+        (rest_getutxos: at most 15 outpoints), /rest/metrics (Prometheus)."""
         import json
 
         parts = path.split("?")[0].split("/")[2:]
@@ -385,12 +446,14 @@ class Node:
             if fmt == "json":
                 return 200, "application/json", json.dumps([rpc("getblockheader", _core.u256_hex(i.hash)) for i in found]).encode()
             return (200, "application/octet-stream", out) if fmt == "bin" else (200, "text/plain", out.hex().encode())
-        if len(parts) == 2 and parts[0] == "tx":  # rest_tx: mempool (no -txindex in this engine)
+        if parts and parts[0] == "getutxos":
+            return self._rest_getutxos(parts[1:], json)
+        if len(parts) == 2 and parts[0] == "tx":  # rest_tx: GetTransaction (pool, -txindex, unspent output)
             h, _, fmt = parts[1].partition(".")
-            e = self.state.mempool.get(_core.u256_from_hex(h))
-            if e is None:
+            try:
+                raw = bytes.fromhex(rpc("getrawtransaction", h))
+            except Exception:  # noqa: BLE001 — not found in any of the places GetTransaction looks
                 return 404, "text/plain", f"{h} not found".encode()
-            raw = e.tx.serialize(True)
             if fmt == "json":
                 return 200, "application/json", json.dumps(rpc("getrawtransaction", h, True)).encode()
             return (200, "application/octet-stream", raw) if fmt == "bin" else (200, "text/plain", raw.hex().encode())

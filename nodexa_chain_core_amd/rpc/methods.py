@@ -537,7 +537,8 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
                 "mempoolminfee": 0.00001, "minrelaytxfee": 0.00001}
 
     def rpc_getrawtransaction(p):
-        """getrawtransaction "txid" ( verbose "blockhash" ) — mempool, or the given block (no -txindex)."""
+        """getrawtransaction "txid" ( verbose "blockhash" ) — mempool, the given block, -txindex, or a
+        transaction with an unspent output (GetTransaction)."""
         _need(p, 1, 'getrawtransaction "txid" ( verbose "blockhash" )')
         txid = _parse_hash(p[0])
         tx, in_block = None, None
@@ -550,6 +551,13 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             if blk is None:
                 raise RPCError(RPC_INVALID_ADDRESS_OR_KEY, "Block hash not found")
             for t in blk.vtx:
+                if t.txid() == txid:
+                    tx, in_block = t, bh
+                    break
+        elif st.indexes.txindex and st.indexes.tx_block(txid) is not None:  # -txindex
+            bh = st.indexes.tx_block(txid)
+            blk = st.get_block(bh)
+            for t in (blk.vtx if blk is not None else []):
                 if t.txid() == txid:
                     tx, in_block = t, bh
                     break

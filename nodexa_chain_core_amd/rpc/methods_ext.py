@@ -392,6 +392,13 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         high, low = int(p[0]), int(p[1])
         opts = _arg(p, 2, {}) or {}
         out = []
+        if st.indexes.timestampindex:  # GetTimestampIndex: the index, active-chain blocks only with noOrphans
+            for h in st.indexes.timestamps(low, high):
+                idx = st.chain.find(h)
+                if idx is None or (opts.get("noOrphans") and not st.chain.in_active_chain(idx)):
+                    continue
+                out.append({"blockhash": _hex(h), "logicalts": idx.time} if opts.get("logicalTimes") else _hex(h))
+            return out
         for height in range(st.height() + 1):
             idx = st.chain.at_height(height)
             if low <= idx.time < high:
@@ -591,6 +598,11 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             blk = st.get_block(_parse_hash(p[1]))
             if blk is None:
                 raise RPCError(RPC_INVALID_ADDRESS_OR_KEY, "Block not found")
+        elif st.indexes.txindex:
+            bh = st.indexes.tx_block(want[0])
+            blk = st.get_block(bh) if bh is not None else None
+            if blk is None:
+                raise RPCError(RPC_INVALID_ADDRESS_OR_KEY, "Transaction not yet in block")
         else:  # no -txindex: scan the active chain from the tip
             for height in range(st.height(), -1, -1):
                 b = st.get_block(st.chain.at_height(height).hash)
