@@ -27,7 +27,7 @@ from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
 from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, GpuKawpowBackend, MinerController
-from .rpc import methods, methods_assets, methods_ext, methods_index, methods_wallet
+from .rpc import methods, methods_assets, methods_ext, methods_index, methods_util, methods_wallet
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
 from .utils import log, metrics
 from .utils.config import ArgsManager, gpu_list
@@ -114,6 +114,7 @@ class Node:
         self.asset_wallet = None
         methods_assets.register(self.table, self)  # chain-state asset methods work without a wallet
         methods_index.register(self.table, self)
+        methods_util.register(self.table, self)
         if a.get("minrelaytxfee") is not None:  # -minrelaytxfee=<CLORE per kvB>
             self.state.min_relay_fee = round(float(a.get("minrelaytxfee")) * 100_000_000)
         par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free

@@ -136,16 +136,20 @@ def register(table, node) -> None:
             c = st._spent_coin(i.prevout)
             if c is not None:
                 prevouts[(i.prevout.hash, i.prevout.n)] = (c[1], c[0])
+        redeem = {}
         for d in _arg(p, 1, []) or []:
             try:
                 h = bytes.fromhex(d["txid"])[::-1]
                 prevouts[(h, int(d["vout"]))] = (bytes.fromhex(d["scriptPubKey"]),
                                                 round(float(d.get("amount", 0)) * COIN))
+                if d.get("redeemScript"):
+                    rs = bytes.fromhex(d["redeemScript"])
+                    redeem[_core.hash160(rs)] = rs
             except (KeyError, ValueError, TypeError):
                 raise RPCError(RPC_DESERIALIZATION_ERROR, "expected object with {\"txid\",\"vout\",\"scriptPubKey\"}")
         w = wallet()
         keys = [_wallet_call(w.decode_wif, k) for k in (_arg(p, 2, []) or [])]
-        tx, complete, errors = _wallet_call(w.sign, tx, prevouts, keys, ht)
+        tx, complete, errors = _wallet_call(w.sign, tx, prevouts, keys, ht, redeem)
         out = {"hex": tx.serialize(True).hex(), "complete": complete}
         if errors:
             out["errors"] = errors

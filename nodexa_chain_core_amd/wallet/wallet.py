@@ -41,6 +41,45 @@ class WalletError(Exception):
     pass
 
 
+def _pushes(script: bytes) -> list[bytes]:
+    """Data of each push of a push-only script (OP_0 as b"")."""
+    out, i = [], 0
+    while i < len(script):
+        op = script[i]
+        i += 1
+        if op == 0:
+            out.append(b"")
+            continue
+        if op < 0x4C:
+            n = op
+        elif op == 0x4C:
+            n = script[i]
+            i += 1
+        elif op == 0x4D:
+            n = int.from_bytes(script[i:i + 2], "little")
+            i += 2
+        else:
+            break
+        out.append(script[i:i + n])
+        i += n
+    return out
+
+
+def parse_multisig(script: bytes):
+    """OP_m <pubkey>... OP_n OP_CHECKMULTISIG -> (m, [pubkeys]) or None."""
+    if len(script) < 3 or script[-1] != 0xAE or not (0x51 <= script[0] <= 0x60) or not (0x51 <= script[-2] <= 0x60):
+        return None
+    m, n = script[0] - 0x50, script[-2] - 0x50
+    pubs = _pushes(script[1:-2])
+    if len(pubs) != n or m > n or any(len(p) not in (33, 65) for p in pubs):
+        return None
+    return m, pubs
+
+
+def multisig_script(m: int, pubkeys: list[bytes]) -> bytes:
+    return bytes([0x50 + m]) + b"".join(_push(p) for p in pubkeys) + bytes([0x50 + len(pubkeys), 0xAE])
+
+
 class Wallet:
     def __init__(self, state, params, path: str | None):
         self.state = state
@@ -51,6 +90,7 @@ class Wallet:
         self.labels: dict[bytes, str] = {}
         self.created: dict[bytes, int] = {}
         self._p2sh_wpkh: dict[bytes, bytes] = {}  # hash160(0x0014 || h) -> h
+        self.redeem_scripts: dict[bytes, bytes] = {}  # hash160(script) -> script (addmultisigaddress)
         if path and os.path.exists(path):
             self._load()
 
@@ -60,13 +100,17 @@ class Wallet:
             data = json.load(f)
         for k in data.get("keys", []):
             self._add_secret(self.decode_wif(k["wif"]), k.get("label", ""), k.get("created", 0), save=False)
+        for rs in data.get("redeem_scripts", []):
+            script = bytes.fromhex(rs)
+            self.redeem_scripts[_core.hash160(script)] = script
 
     def _save(self) -> None:
         if not self.path:
             return
         data = {"version": 1, "network": self.params.network_id,
                 "keys": [{"wif": self.encode_wif(sec), "label": self.labels.get(h, ""),
-                          "created": self.created.get(h, 0)} for h, (sec, _) in self.keys.items()]}
+                          "created": self.created.get(h, 0)} for h, (sec, _) in self.keys.items()],
+                "redeem_scripts": [rs.hex() for rs in self.redeem_scripts.values()]}
         tmp = self.path + ".new"
         with open(tmp, "w") as f:
             json.dump(data, f, indent=1)
@@ -122,6 +166,14 @@ class Wallet:
         if raw is None or len(raw) != 21 or raw[0] != self.params.pubkey_prefix:
             raise WalletError("Invalid address")
         return raw[1:]
+
+    def add_redeem_script(self, script: bytes) -> str:
+        """Remember a P2SH redeem script (addmultisigaddress); returns its P2SH address."""
+        h = _core.hash160(script)
+        with self.lock:
+            self.redeem_scripts[h] = script
+            self._save()
+        return _core.base58check_encode(bytes([self.params.script_prefix]) + h)
 
     def scripts(self) -> list[bytes]:
         """Every scriptPubKey the wallet can spend: P2PKH, P2PK, P2WPKH and P2SH-P2WPKH of each key."""
@@ -192,13 +244,39 @@ class Wallet:
 
     # ------------------------------------------------------------------ signing
     def sign(self, tx, prevouts: dict[tuple[bytes, int], tuple[bytes, int]], extra_keys: list[bytes] = (),
-             hash_type: int = SIGHASH_ALL) -> tuple[object, bool, list[dict]]:
+             hash_type: int = SIGHASH_ALL, redeem_scripts: dict | None = None) -> tuple[object, bool, list[dict]]:
         """SignTransaction: every input whose spent output is known and spendable by a wallet
         key (or one of `extra_keys`). Returns (tx, complete, errors)."""
         with self.lock:
-            return self._sign(tx, prevouts, extra_keys, hash_type)
+            return self._sign(tx, prevouts, extra_keys, hash_type, redeem_scripts)
 
-    def _sign(self, tx, prevouts, extra_keys, hash_type):
+    def _sign_multisig(self, tx, i: int, redeem: bytes, ms: tuple, amount: int, hash_type: int) -> bool:
+        """P2SH multisig input: keep the signatures already in its scriptSig, add the wallet's, in
+        key order (CombineMultisig / SignStep). True once m signatures are present."""
+        m, pubs = ms
+        vin = tx.vin[i]
+        msg = _core.signature_hash(redeem, tx.serialize(True), i, hash_type, amount, 0)
+        have = {}
+        for push in _pushes(vin.script_sig)[1:-1]:
+            for pub in pubs:
+                if pub not in have and push and _core.secp_verify(pub, push[:-1], msg):
+                    have[pub] = push
+                    break
+        for pub in pubs:
+            if pub in have or len(have) >= m:
+                continue
+            k = self.keys.get(_core.hash160(pub))
+            if k is not None and k[1] == pub:
+                have[pub] = _core.secp_sign(msg, k[0]) + bytes([hash_type])
+        sigs = [have[pub] for pub in pubs if pub in have][:m]
+        vin.script_sig = b"\x00" + b"".join(_push(x) for x in sigs) + _push(redeem)
+        vins = list(tx.vin)
+        vins[i] = vin
+        tx.vin = vins
+        return len(sigs) >= m
+
+    def _sign(self, tx, prevouts, extra_keys, hash_type, redeem_scripts=None):
+        redeem_scripts = redeem_scripts or {}
         extra = {}
         for sec in extra_keys:
             pub = _core.secp_pubkey_create(sec, True)
@@ -219,6 +297,17 @@ class Wallet:
                                    "error": "Input not found or already spent"})
                     continue
                 spk, amount = prev
+                if len(spk) == 23 and spk[:2] == b"\xa9\x14" and spk[22] == 0x87:
+                    redeem = self.redeem_scripts.get(spk[2:22]) or redeem_scripts.get(spk[2:22])
+                    ms = parse_multisig(redeem) if redeem else None
+                    if ms is not None:
+                        tx.vin = vins
+                        ok = self._sign_multisig(tx, i, redeem, ms, amount, hash_type)
+                        vins = list(tx.vin)
+                        if not ok:
+                            errors.append({"txid": vin.prevout.hash[::-1].hex(), "vout": vin.prevout.n,
+                                           "error": "Not enough signatures for the multisig input"})
+                        continue
                 k = self._key_for(spk)
                 if k is None:
                     errors.append({"txid": vin.prevout.hash[::-1].hex(), "vout": vin.prevout.n,
