@@ -276,6 +276,13 @@ void bind_extra(py::module_& m) {
         .def("kawpow_input", [](const BlockHeader& h) { Bytes b = h.kawpow_input(); return py::bytes(reinterpret_cast<const char*>(b.data()), b.size()); })
         .def("serialize", [](const BlockHeader& h, u32 act) { return pyb(h.bytes(act)); })
         .def_static("deserialize", [](const py::bytes& b, u32 act) { Bytes d = bytes_of(b); Reader r(d); return BlockHeader::deserialize(r, act); })
+        .def_static("deserialize_prefix", [](const py::bytes& b, u32 act, size_t off) {
+            Bytes d = bytes_of(b);
+            if (off > d.size()) throw std::out_of_range("offset past the end");
+            Reader r(d.data() + off, d.size() - off);
+            BlockHeader h = BlockHeader::deserialize(r, act);
+            return py::make_tuple(h, r.pos());
+        }, py::arg("data"), py::arg("act"), py::arg("offset") = 0, "(header, bytes used) from a prefix")
         .def("kawpow_header_hash", [](const BlockHeader& h) { return pyb(h.kawpow_header_hash()); })
         .def("legacy80", [](const BlockHeader& h) { return pyb(h.legacy80()); });
     m.def("deserialize_headers", [](const py::bytes& b, u32 act) {

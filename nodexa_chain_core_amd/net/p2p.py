@@ -17,6 +17,9 @@ the contextual rules run header by header on the C++ header chain.
 """
 from __future__ import annotations
 
+import ipaddress
+import os
+import random
 import socket
 import struct
 import threading
@@ -26,9 +29,39 @@ from .. import core
 from ..utils import log, sync
 from ..utils.metrics import REGISTRY
 from . import protocol as P
+from .addrman import AddrMan, load_banlist, save_banlist
+from .bloom import MAX_SCRIPT_ELEMENT_SIZE, BloomFilter, merkle_block
+from .compact import (CompactBlock, blocktxn_payload, getblocktxn_payload, parse_blocktxn, parse_getblocktxn)
 
 _core = core()
 DEFAULT_MISBEHAVING_BANTIME = 60 * 60 * 24  # -bantime (src/net.h)
+MSG_FILTERED_BLOCK, MSG_CMPCT_BLOCK = 3, 4
+MAX_ADDR_TO_SEND = 1000
+DEFAULT_MAX_OUTBOUND = 8  # MAX_OUTBOUND_CONNECTIONS
+
+
+def _ser_addr(entries) -> bytes:
+    """addr payload: (time u32, services u64, IPv6-mapped address, big-endian port) per entry."""
+    out = P.ser_compact(len(entries))
+    for ip, port, services, t in entries:
+        a = ipaddress.ip_address(ip)
+        raw = (b"\0" * 10 + b"\xff\xff" + a.packed) if a.version == 4 else a.packed
+        out += struct.pack("<IQ", int(t) & 0xFFFFFFFF, services) + raw + struct.pack(">H", port)
+    return out
+
+
+def _parse_addr(p: bytes) -> list[tuple[str, int, int, int]]:
+    n, off = P.de_compact(p, 0)
+    out = []
+    for _ in range(n):
+        t, services = struct.unpack_from("<IQ", p, off)
+        raw = p[off + 12:off + 28]
+        (port,) = struct.unpack_from(">H", p, off + 28)
+        off += 30
+        a = ipaddress.ip_address(raw)
+        ip = str(a.ipv4_mapped) if a.ipv4_mapped else str(a)
+        out.append((ip, port, services, t))
+    return out
 
 
 class Peer:
@@ -43,6 +76,11 @@ class Peer:
         self.bytes_sent = self.bytes_recv = 0
         self.known_txs: set[bytes] = set()  # filterInventoryKnown
         self.fee_filter = 0
+        self.bloom: BloomFilter | None = None   # BIP37 filterload
+        self.cmpct_version = 0                   # BIP152 sendcmpct version (0 = none)
+        self.cmpct_hb = False                    # high-bandwidth mode: push cmpctblock unasked
+        self.partial: dict[bytes, tuple] = {}    # block hash -> (CompactBlock, slots) awaiting blocktxn
+        self.getaddr_answered = False
         self.connected_at = time.time()
         self.last_recv = self.last_send = 0.0
         self._send_lock = threading.Lock()
@@ -114,7 +152,8 @@ class ConnectionManager:
     """Listener + outbound connections + message handling for one node."""
 
     def __init__(self, state, params, gpus: list[int] | None = None, listen: tuple[str, int] | None = None,
-                 verify_mode: str = "auto"):
+                 verify_mode: str = "auto", datadir: str | None = None, connect_only: bool = False,
+                 max_outbound: int = DEFAULT_MAX_OUTBOUND):
         self.state, self.params = state, params
         self.magic = bytes(params.message_start)
         self.gpus = gpus or None
@@ -133,6 +172,14 @@ class ConnectionManager:
         self.network_active = True
         self.banned: dict[str, dict] = {}   # address -> {"banned_until", "ban_created", "ban_reason"}
         self.added_nodes: list[str] = []    # addnode "add" list (getaddednodeinfo)
+        # peer addresses (peers.dat) and bans (banlist.dat), CConnman's addrman / CBanDB
+        self.datadir = datadir
+        self.addrman = AddrMan(os.path.join(datadir, "peers.dat") if datadir else None)
+        self.banlist_path = os.path.join(datadir, "banlist.dat") if datadir else None
+        if self.banlist_path:
+            self.banned.update(load_banlist(self.banlist_path))
+        self.connect_only = connect_only
+        self.max_outbound = max_outbound
 
     # ---------------------------------------------------------------- lifecycle
     def next_id(self) -> int:
@@ -150,6 +197,27 @@ class ConnectionManager:
             self.port = srv.getsockname()[1]
             threading.Thread(target=self._accept_loop, name="p2p-listen", daemon=True).start()
             log.log_printf(f"P2P listening on {self.listen_addr[0]}:{self.port}")
+        if not self.connect_only and self.max_outbound > 0:
+            threading.Thread(target=self._open_connections, name="p2p-opencon", daemon=True).start()
+
+    def _open_connections(self) -> None:
+        """ThreadOpenConnections: keep up to max_outbound outbound peers, picked from addrman."""
+        while not self._stop.wait(0.5):
+            if not self.network_active:
+                continue
+            with self._lock:
+                outbound = sum(1 for p in self.peers if not p.inbound)
+                connected = {f"{p.addr[0]}:{p.addr[1]}" for p in self.peers}
+            if outbound >= self.max_outbound or self.addrman.size() == 0:
+                continue
+            pick = self.addrman.select(exclude=connected)
+            if pick is None or self.is_banned(pick[0]) or (self.port and pick == ("127.0.0.1", self.port)):
+                continue
+            self.addrman.attempt(*pick)
+            try:
+                self.connect(pick[0], pick[1], timeout=3.0)
+            except OSError:
+                continue
 
     def _accept_loop(self) -> None:
         while not self._stop.is_set():
@@ -184,6 +252,12 @@ class ConnectionManager:
 
     def stop(self) -> None:
         self._stop.set()
+        try:
+            self.addrman.save()
+            if self.banlist_path:
+                save_banlist(self.banlist_path, self.banned)
+        except OSError as e:
+            log.log_printf(f"could not write peers.dat / banlist.dat: {e}")
         if self._server is not None:
             self._server.close()
         for p in list(self.peers):
@@ -198,12 +272,17 @@ class ConnectionManager:
         now = int(time.time())
         until = int(seconds) if absolute else now + int(seconds or DEFAULT_MISBEHAVING_BANTIME)
         self.banned[address] = {"address": address, "banned_until": until, "ban_created": now, "ban_reason": reason}
+        if self.banlist_path:
+            save_banlist(self.banlist_path, self.banned)
         for p in list(self.peers):
             if p.addr[0] == address:
                 p.close()
 
     def unban(self, address: str) -> bool:
-        return self.banned.pop(address, None) is not None
+        gone = self.banned.pop(address, None) is not None
+        if gone and self.banlist_path:
+            save_banlist(self.banlist_path, self.banned)
+        return gone
 
     def is_banned(self, address: str) -> bool:
         e = self.banned.get(address)
@@ -232,15 +311,21 @@ class ConnectionManager:
                 p.close()
 
     # ---------------------------------------------------------------- relay
-    def announce_block(self, header) -> None:
-        """New tip: `headers` to peers that asked for sendheaders, `inv` to the rest."""
+    def announce_block(self, header, block=None) -> None:
+        """New tip: `cmpctblock` to high-bandwidth BIP152 peers, `headers` to peers that asked for
+        sendheaders, `inv` to the rest."""
         act = self.params.kawpow_activation_time
         h = self.state.block_hash(header)
+        cmpct = None
         for p in list(self.peers):
             if not p.verack:
                 continue
             try:
-                if p.send_headers:
+                if p.cmpct_hb and block is not None:
+                    if cmpct is None:
+                        cmpct = CompactBlock.from_block(block, act).payload()
+                    p.send("cmpctblock", cmpct)
+                elif p.send_headers:
                     p.send("headers", _core.headers_msg_encode([header], act))
                 else:
                     p.send("inv", P.inv_payload([(P.MSG_BLOCK, h)]))
@@ -249,9 +334,16 @@ class ConnectionManager:
 
     def announce_tx(self, txid: bytes, skip: "Peer | None" = None) -> None:
         """RelayTransaction: `inv` MSG_TX to every peer that has not sent us this tx."""
+        tx = None
         for p in list(self.peers):
             if p is skip or not p.verack or not p.relay_txs or txid in p.known_txs:
                 continue
+            if p.bloom is not None:  # BIP37: relay only what the peer's filter matches
+                if tx is None:
+                    e = self.state.mempool.get(txid)
+                    tx = e.tx if e is not None else None
+                if tx is None or not p.bloom.is_relevant_and_update(tx):
+                    continue
             p.known_txs.add(txid)
             try:
                 p.send("inv", P.inv_payload([(P.MSG_TX, txid)]))
@@ -282,11 +374,129 @@ class ConnectionManager:
         if peer.inbound and not peer.sent_version:
             peer.send_version()
         peer.send("verack")
+        if not peer.inbound:  # an outbound peer that answered is a good address (MarkAddressGood)
+            self.addrman.good(peer.addr[0], peer.addr[1])
 
     def on_verack(self, peer: Peer, p: bytes) -> None:
         peer.verack = True
         peer.send("sendheaders")
+        peer.send("sendcmpct", struct.pack("<?Q", False, 2))  # BIP152 v2, low-bandwidth
+        if not peer.inbound:
+            peer.send("getaddr")
         self.request_headers(peer)
+
+    # ---------------------------------------------------------------- addresses (N4)
+    def on_addr(self, peer: Peer, p: bytes) -> None:
+        entries = _parse_addr(p)
+        if len(entries) > MAX_ADDR_TO_SEND:
+            peer.misbehaving(20, "oversized addr")
+            return
+        now = int(time.time())
+        fresh = [(ip, port, s, t if 100000000 < t <= now + 600 else now - 5 * 86400) for ip, port, s, t in entries]
+        self.addrman.add(fresh, peer.addr[0], penalty=2 * 3600)
+        if len(entries) <= 10:  # RelayAddress: small, fresh announcements go on to two peers
+            relay = [e for e in fresh if e[3] > now - 600]
+            others = [q for q in self.peers if q is not peer and q.verack]
+            for q in random.sample(others, min(2, len(others))) if relay else []:
+                try:
+                    q.send("addr", _ser_addr(relay))
+                except OSError:
+                    q.close()
+
+    def on_getaddr(self, peer: Peer, p: bytes) -> None:
+        """Answered once, for inbound peers only (fingerprinting protection, net_processing.cpp)."""
+        if not peer.inbound or peer.getaddr_answered:
+            return
+        peer.getaddr_answered = True
+        items = [(a.ip, a.port, a.services, a.time) for a in self.addrman.get_addr()]
+        for k in range(0, len(items), MAX_ADDR_TO_SEND):
+            peer.send("addr", _ser_addr(items[k:k + MAX_ADDR_TO_SEND]))
+
+    # ---------------------------------------------------------------- BIP37 (N5)
+    def on_filterload(self, peer: Peer, p: bytes) -> None:
+        f = BloomFilter.from_payload(p)
+        if not f.within_size_constraints():
+            peer.misbehaving(100, "oversized bloom filter")
+            return
+        peer.bloom = f
+        peer.info["relay"] = True
+
+    def on_filteradd(self, peer: Peer, p: bytes) -> None:
+        n, off = P.de_compact(p, 0)
+        data = p[off:off + n]
+        if len(data) > MAX_SCRIPT_ELEMENT_SIZE or peer.bloom is None:
+            peer.misbehaving(100, "bad filteradd")
+            return
+        peer.bloom.insert(data)
+
+    def on_filterclear(self, peer: Peer, p: bytes) -> None:
+        peer.bloom = None
+        peer.info["relay"] = True
+
+    # ---------------------------------------------------------------- BIP152 (N5)
+    def on_sendcmpct(self, peer: Peer, p: bytes) -> None:
+        announce, version = struct.unpack_from("<?Q", p, 0)
+        if version in (1, 2) and version >= peer.cmpct_version:
+            peer.cmpct_version = version
+            peer.cmpct_hb = bool(announce)
+
+    def on_cmpctblock(self, peer: Peer, p: bytes) -> None:
+        act = self.params.kawpow_activation_time
+        cb = CompactBlock.from_payload(p, act)
+        h = self.state.block_hash(cb.header)
+        if h in self.state.block_pos:
+            return
+        if self.state.chain.find(cb.header.prev) is None:
+            self.request_headers(peer)
+            return
+        with self.state.lock:
+            pool = [e.tx for e in self.state.mempool.values()]
+        slots, missing = cb.reconstruct(pool, peer.cmpct_version or 2)
+        if missing:
+            peer.partial[h] = (cb, slots)
+            peer.send("getblocktxn", getblocktxn_payload(h, missing))
+            REGISTRY.inc("p2p_cmpct_getblocktxn_total", 1)
+            return
+        self._finish_compact(peer, cb, slots)
+
+    def _finish_compact(self, peer: Peer, cb, slots) -> None:
+        blk = _core.Block()
+        blk.header = cb.header
+        blk.vtx = slots
+        root, _ = blk.merkle_root()
+        if root != cb.header.merkle_root:  # a short-id collision built the wrong block: fetch it whole
+            peer.send("getdata", P.inv_payload([(P.MSG_BLOCK | P.MSG_WITNESS_FLAG, self.state.block_hash(cb.header))]))
+            return
+        REGISTRY.inc("p2p_cmpct_reconstructed_total", 1)
+        self.state.arm_reorg_guard(self.peer_count())
+        st = self.state.process_new_block(blk)
+        if not st.ok and st.reject != "duplicate":
+            peer.misbehaving(st.dos or 0, f"invalid compact block: {st.reject}")
+
+    def on_getblocktxn(self, peer: Peer, p: bytes) -> None:
+        h, idx = parse_getblocktxn(p)
+        blk = self.state.get_block(h)
+        if blk is None:
+            return
+        vtx = list(blk.vtx)
+        if any(i >= len(vtx) for i in idx):
+            peer.misbehaving(100, "getblocktxn with out-of-bounds tx indices")
+            return
+        peer.send("blocktxn", blocktxn_payload(h, [vtx[i] for i in idx]))
+
+    def on_blocktxn(self, peer: Peer, p: bytes) -> None:
+        h, txs = parse_blocktxn(p)
+        pending = peer.partial.pop(h, None)
+        if pending is None:
+            return
+        cb, slots = pending
+        missing = [i for i, t in enumerate(slots) if t is None]
+        if len(txs) != len(missing):
+            peer.misbehaving(100, "blocktxn does not fill the block")
+            return
+        for i, t in zip(missing, txs):
+            slots[i] = t
+        self._finish_compact(peer, cb, slots)
 
     def on_sendheaders(self, peer: Peer, p: bytes) -> None:
         peer.send_headers = True
@@ -377,8 +587,9 @@ class ConnectionManager:
             log.log_print("mempool", f"tx {_core.u256_hex(txid)} from peer {peer.id} rejected: {reason}")
 
     def on_mempool(self, peer: Peer, p: bytes) -> None:
-        """BIP35: inv of every pool txid (in MAX_INV_SZ chunks)."""
-        ids = list(self.state.mempool)
+        """BIP35: inv of every pool txid (in MAX_INV_SZ chunks), through the peer's bloom filter."""
+        ids = [h for h, e in list(self.state.mempool.items())
+               if peer.bloom is None or peer.bloom.is_relevant_and_update(e.tx)]
         peer.known_txs.update(ids)
         for k in range(0, len(ids), P.MAX_INV_SZ):
             peer.send("inv", P.inv_payload([(P.MSG_TX, h) for h in ids[k:k + P.MAX_INV_SZ]]))
@@ -388,8 +599,23 @@ class ConnectionManager:
 
     def on_getdata(self, peer: Peer, p: bytes) -> None:
         missing = []
+        act = self.params.kawpow_activation_time
         for t, h in P.parse_inv(p):
-            if t & ~P.MSG_WITNESS_FLAG == P.MSG_BLOCK:
+            kind = t & ~P.MSG_WITNESS_FLAG
+            if kind == MSG_FILTERED_BLOCK or kind == MSG_CMPCT_BLOCK:
+                blk = self.state.get_block(h)
+                if blk is None:
+                    missing.append((t, h))
+                elif kind == MSG_CMPCT_BLOCK:
+                    peer.send("cmpctblock", CompactBlock.from_block(blk, act, peer.cmpct_version or 2).payload())
+                elif peer.bloom is not None:  # merkleblock, then the matched transactions
+                    payload, matched = merkle_block(blk, blk.header.serialize(act), peer.bloom)
+                    peer.send("merkleblock", payload)
+                    for tx in matched:
+                        if tx.txid() not in peer.known_txs:
+                            peer.send("tx", tx.serialize(False))
+                continue
+            if kind == P.MSG_BLOCK:
                 raw = self.state.get_block_raw(h)
                 if raw is None:
                     missing.append((t, h))

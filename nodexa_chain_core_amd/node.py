@@ -182,21 +182,31 @@ class Node:
         if a.get_bool("listen", False) or a.is_set("port"):
             listen = (a.get("bind", "127.0.0.1"), a.get_int("port", self.params.default_port))
         connect = a.get_list("connect")
-        if listen is None and not connect:
+        seeds, adds = a.get_list("seednode"), a.get_list("addnode")
+        if listen is None and not connect and not seeds and not adds:
             return
         self.connman = ConnectionManager(self.state, self.params, gpus=self.gpus, listen=listen,
-                                         verify_mode=a.get("p2pverifymode", "auto"))
+                                         verify_mode=a.get("p2pverifymode", "auto"), datadir=self.datadir,
+                                         connect_only=bool(connect),
+                                         max_outbound=a.get_int("maxconnections", 8) if not connect else 0)
         self.connman.start()
         cm = self.connman
+        st = self.state
 
         class _Relay(ValidationInterface):
             def transaction_added_to_mempool(self, tx) -> None:
                 cm.announce_tx(tx.txid())
 
             def updated_block_tip(self, tip, fork, initial_download: bool) -> None:
-                cm.announce_block(tip.header)
+                cm.announce_block(tip.header, st.get_block(tip.hash))
 
         self.state.register(_Relay())
+        # -seednode / -addnode: known to the address manager (ThreadOpenConnections dials them)
+        for c in seeds + adds:
+            host, _, port = c.rpartition(":")
+            cm.addrman.add([(host or "127.0.0.1", int(port), 1, int(time.time()))], "127.0.0.1")
+            if c in adds:
+                cm.added_nodes.append(c)
         for c in connect:
             host, _, port = c.rpartition(":")
             try:
