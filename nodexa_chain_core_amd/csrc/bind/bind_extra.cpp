@@ -237,13 +237,13 @@ void bind_extra(py::module_& m) {
         .def_readwrite("vout", &Transaction::vout)
         .def_readwrite("lock_time", &Transaction::lock_time)
         .def("serialize", [](const Transaction& t, bool w) { return pyb(t.bytes(w)); }, py::arg("with_witness") = true)
-        .def_static("deserialize", [](const py::bytes& b) {
+        .def_static("deserialize", [](const py::bytes& b, bool allow_witness) {
             Bytes d = bytes_of(b);
             Reader r(d);
-            Transaction t = Transaction::deserialize(r);
+            Transaction t = Transaction::deserialize(r, allow_witness);
             if (!r.empty()) throw std::runtime_error("trailing bytes after transaction");
             return t;
-        })
+        }, py::arg("data"), py::arg("allow_witness") = true)
         .def_static("deserialize_prefix", [](const py::bytes& b, size_t offset) {
             Bytes d = bytes_of(b);
             if (offset > d.size()) throw std::out_of_range("offset past the end");
