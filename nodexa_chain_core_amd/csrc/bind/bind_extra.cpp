@@ -1,5 +1,7 @@
 // Bindings for the consensus layer (chain/*), X16R and Equihash.
 #include <pybind11/pybind11.h>
+
+#include "../crypto/aes.hpp"
 #include <pybind11/stl.h>
 
 #include <thread>
@@ -144,6 +146,33 @@ void bind_extra(py::module_& m) {
     m.def("murmur3_32", [](u32 seed, const py::bytes& d) {
         std::string s = d;
         return murmur3_32(seed, reinterpret_cast<const u8*>(s.data()), s.size());
+    });
+    m.def("aes256_cbc_encrypt", [](const py::bytes& key, const py::bytes& iv, const py::bytes& plain) {
+        const std::string k = key, v = iv;
+        if (k.size() != 32 || v.size() != 16) throw std::invalid_argument("key must be 32 bytes, iv 16");
+        return pyb(aes256_cbc_encrypt(reinterpret_cast<const u8*>(k.data()), reinterpret_cast<const u8*>(v.data()),
+                                      bytes_of(plain)));
+    });
+    m.def("aes256_cbc_decrypt", [](const py::bytes& key, const py::bytes& iv, const py::bytes& cipher) -> py::object {
+        const std::string k = key, v = iv;
+        if (k.size() != 32 || v.size() != 16) throw std::invalid_argument("key must be 32 bytes, iv 16");
+        Bytes out;
+        if (!aes256_cbc_decrypt(reinterpret_cast<const u8*>(k.data()), reinterpret_cast<const u8*>(v.data()),
+                                bytes_of(cipher), out))
+            return py::none();
+        return pyb(out);
+    });
+    m.def("aes256_encrypt_block", [](const py::bytes& key, const py::bytes& block) {
+        const std::string k = key, b = block;
+        if (k.size() != 32 || b.size() != 16) throw std::invalid_argument("key 32 bytes, block 16");
+        u8 out[16];
+        Aes256(reinterpret_cast<const u8*>(k.data())).encrypt_block(reinterpret_cast<const u8*>(b.data()), out);
+        return py::bytes(reinterpret_cast<const char*>(out), 16);
+    });
+    m.def("bytes_to_key_sha512", [](const std::string& pass, const py::bytes& salt, int rounds) {
+        u8 k[32], v[16];
+        bytes_to_key_sha512(pass, bytes_of(salt), rounds, k, v);
+        return py::make_tuple(py::bytes(reinterpret_cast<const char*>(k), 32), py::bytes(reinterpret_cast<const char*>(v), 16));
     });
     m.def("sha512", [](const py::bytes& d) {
         std::string s = d;

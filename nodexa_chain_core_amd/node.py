@@ -108,8 +108,16 @@ class Node:
         if not a.get_bool("disablewallet", False):  # -disablewallet (src/wallet/init.cpp)
             from .wallet import Wallet
 
+            from .wallet.history import WalletHistory
+
             self.wallet = Wallet(self.state, self.params,
                                  os.path.join(self.datadir, "wallet.json") if self.datadir else None)
+            hist_path = os.path.join(self.datadir, "wallet_txs.json") if self.datadir else None
+            rescan = hist_path is not None and not os.path.exists(hist_path) and bool(self.wallet.keys)
+            self.wallet.history = WalletHistory(self.wallet, hist_path)
+            if rescan:
+                methods_wallet.rescan(self)
+            self.state.register(self.wallet.history)
             methods_wallet.register(self.table, self)
         self.asset_wallet = None
         methods_assets.register(self.table, self)  # chain-state asset methods work without a wallet

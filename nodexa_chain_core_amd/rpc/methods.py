@@ -599,8 +599,17 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         if spk is None:
             return {"isvalid": False}
         w = getattr(node, "wallet", None)
-        return {"isvalid": True, "address": p[0], "scriptPubKey": spk.hex(), "isscript": spk[0] == 0xa9,
-                "ismine": bool(w is not None and w.is_mine(spk))}
+        out = {"isvalid": True, "address": p[0], "scriptPubKey": spk.hex(), "isscript": spk[0] == 0xa9,
+               "ismine": bool(w is not None and w.is_mine(spk))}
+        if out["ismine"] and len(spk) == 25:
+            h = spk[3:23]
+            out["pubkey"] = w.keys[h][1].hex()
+            out["iscompressed"] = True
+            out["account"] = w.labels.get(h, "")
+            if h in w.hdpath:
+                out["hdkeypath"] = w.hdpath[h]
+                out["hdmasterkeyid"] = w.hd["master_id"][::-1].hex()
+        return out
 
     for cat, name, fn, args in [
         ("rawtransactions", "decoderawtransaction", rpc_decoderawtransaction, ("hexstring",)),

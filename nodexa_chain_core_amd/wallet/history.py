@@ -1,0 +1,204 @@
+"""Wallet transaction history (CWalletTx bookkeeping).
+
+Parity (behaviour): CWallet::AddToWalletIfInvolvingMe / SyncTransaction (src/wallet/wallet.cpp) —
+every transaction that pays a wallet script or spends a wallet output is recorded with the block
+that confirmed it (or none while in the pool); ListTransactions / GetAmounts (credit, debit, fee,
+categories send / receive / generate / immature / orphan) drive listtransactions, gettransaction,
+listsinceblock, getreceivedbyaddress and listreceivedbyaddress (src/wallet/rpcwallet.cpp).
+Records live in <datadir>/wallet_txs.json (the role of the wallet database's "tx" records),
+rewritten atomically once per connected block / wallet send.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+
+from .. import core
+from ..chain.state import ValidationInterface
+
+_core = core()
+COIN = 100_000_000
+
+
+class WalletTx:
+    __slots__ = ("tx", "time", "block", "abandoned", "comment", "order")
+
+    def __init__(self, tx, t: int, block: bytes | None = None, order: int = 0):
+        self.tx, self.time, self.block = tx, t, block
+        self.abandoned = False
+        self.comment = ""
+        self.order = order  # nOrderPos: insertion order
+
+
+class WalletHistory(ValidationInterface):
+    def __init__(self, wallet, path: str | None):
+        self.w = wallet
+        self.state = wallet.state
+        self.path = path
+        self.lock = threading.RLock()
+        self.txs: dict[bytes, WalletTx] = {}
+        self.locked: set[tuple[bytes, int]] = set()  # lockunspent
+        if path and os.path.exists(path):
+            self._load()
+
+    # ------------------------------------------------------------------ persistence
+    def _load(self) -> None:
+        with open(self.path) as f:
+            d = json.load(f)
+        for h, e in d.get("txs", {}).items():
+            wtx = WalletTx(_core.Transaction.deserialize(bytes.fromhex(e["hex"])), e["time"],
+                           bytes.fromhex(e["block"]) if e.get("block") else None)
+            wtx.abandoned = e.get("abandoned", False)
+            wtx.comment = e.get("comment", "")
+            wtx.order = e.get("order", len(self.txs))
+            self.txs[bytes.fromhex(h)] = wtx
+
+    def save(self) -> None:
+        if not self.path:
+            return
+        with self.lock:
+            d = {"txs": {h.hex(): {"hex": w.tx.serialize(True).hex(), "time": w.time,
+                                   "block": w.block.hex() if w.block else None, "abandoned": w.abandoned,
+                                   "comment": w.comment, "order": w.order} for h, w in self.txs.items()}}
+        tmp = self.path + ".new"
+        with open(tmp, "w") as f:
+            json.dump(d, f)
+        os.replace(tmp, self.path)
+
+    # ------------------------------------------------------------------ involvement
+    def _output_mine(self, prevout) -> tuple[int, bytes] | None:
+        w = self.txs.get(prevout.hash)
+        if w is None or prevout.n >= len(w.tx.vout):
+            return None
+        o = w.tx.vout[prevout.n]
+        return (o.value, o.script_pubkey) if self.w.is_mine(o.script_pubkey) else None
+
+    def involves_me(self, tx) -> bool:
+        if any(self.w.is_mine(o.script_pubkey) for o in tx.vout):
+            return True
+        return not tx.is_coinbase() and any(self._output_mine(i.prevout) for i in tx.vin)
+
+    def add(self, tx, block: bytes | None = None, save: bool = True) -> bool:
+        txid = tx.txid()
+        with self.lock:
+            w = self.txs.get(txid)
+            if w is None:
+                if not self.involves_me(tx):
+                    return False
+                w = self.txs[txid] = WalletTx(tx, int(time.time()), order=len(self.txs))
+            if block is not None:
+                w.block = block
+                w.abandoned = False
+        if save:
+            self.save()
+        return True
+
+    # ValidationInterface
+    def transaction_added_to_mempool(self, tx) -> None:
+        self.add(tx)
+
+    def block_connected(self, block, index) -> None:
+        changed = False
+        for tx in block.vtx:
+            changed |= self.add(tx, index.hash, save=False)
+        if changed:
+            self.save()
+
+    # ------------------------------------------------------------------ amounts
+    def confirmations(self, w: WalletTx) -> int:
+        st = self.state
+        if w.block is None:
+            return 0 if w.tx.txid() in st.mempool or not w.abandoned else -1
+        idx = st.chain.find(w.block)
+        if idx is None or not st.chain.in_active_chain(idx):
+            return 0
+        return st.height() - idx.height + 1
+
+    def debit(self, w: WalletTx) -> int:
+        if w.tx.is_coinbase():
+            return 0
+        return sum(m[0] for i in w.tx.vin if (m := self._output_mine(i.prevout)) is not None)
+
+    def credit(self, w: WalletTx) -> int:
+        return sum(o.value for o in w.tx.vout if self.w.is_mine(o.script_pubkey))
+
+    def fee(self, w: WalletTx) -> int | None:
+        """Only known when every input is ours (the reference reports fee for fully-from-me txs)."""
+        if w.tx.is_coinbase():
+            return None
+        ins = [self._output_mine(i.prevout) for i in w.tx.vin]
+        if any(m is None for m in ins):
+            return None
+        return sum(m[0] for m in ins) - w.tx.value_out()
+
+    def _address(self, spk: bytes) -> str | None:
+        p = self.w.params
+        return _core.script_to_address(spk, p.pubkey_prefix, p.script_prefix) or None
+
+    def entries(self, w: WalletTx) -> list[dict]:
+        """ListTransactions entries of one wallet transaction (sends, then receives)."""
+        conf = self.confirmations(w)
+        base = {"confirmations": conf, "txid": w.tx.txid()[::-1].hex(), "time": w.time, "timereceived": w.time,
+                "bip125-replaceable": "no", "walletconflicts": []}
+        if w.block is not None:
+            idx = self.state.chain.find(w.block)
+            if idx is not None:
+                base["blockhash"] = w.block[::-1].hex()
+                base["blocktime"] = idx.time
+                blk = self.state.get_block(w.block)
+                if blk is not None:
+                    base["blockindex"] = [t.txid() for t in blk.vtx].index(w.tx.txid()) if blk else 0
+        if w.comment:
+            base["comment"] = w.comment
+        out = []
+        debit = self.debit(w)
+        fee = self.fee(w)
+        sends, receives = [], []
+        for n, o in enumerate(w.tx.vout):  # GetAmounts: change (mine, no address-book label) is skipped
+            mine = self.w.is_mine(o.script_pubkey)
+            if debit > 0:
+                if mine and self._is_change(o.script_pubkey):
+                    continue
+                e = {"account": "", "address": self._address(o.script_pubkey), "category": "send",
+                     "amount": -o.value / COIN, "vout": n, "fee": -(fee or 0) / COIN, "abandoned": w.abandoned}
+                e.update(base)
+                sends.append(e)
+            if mine:
+                cat = "receive"
+                if w.tx.is_coinbase():
+                    cat = "orphan" if conf <= 0 else ("immature" if conf <= _core.COINBASE_MATURITY else "generate")
+                e = {"account": self._label(o.script_pubkey), "address": self._address(o.script_pubkey),
+                     "category": cat, "amount": o.value / COIN, "vout": n}
+                e.update(base)
+                receives.append(e)
+        out = sends + receives
+        return out
+
+    def _is_change(self, spk: bytes) -> bool:
+        return len(spk) == 25 and self.w.labels.get(spk[3:23]) == "change"
+
+    def _label(self, spk: bytes) -> str:
+        return self.w.labels.get(spk[3:23], "") if len(spk) == 25 else ""
+
+    def ordered(self) -> list[WalletTx]:
+        with self.lock:
+            return sorted(self.txs.values(), key=lambda w: w.order)
+
+    def received_by(self, minconf: int = 1) -> dict[bytes, tuple[int, int, list[str]]]:
+        """scriptPubKey -> (amount, min confirmations, txids) over non-coinbase wallet txs."""
+        out: dict[bytes, list] = {}
+        for w in self.ordered():
+            if w.tx.is_coinbase():
+                continue
+            conf = self.confirmations(w)
+            if conf < minconf:
+                continue
+            for o in w.tx.vout:
+                if self.w.is_mine(o.script_pubkey):
+                    e = out.setdefault(o.script_pubkey, [0, 1 << 30, []])
+                    e[0] += o.value
+                    e[1] = min(e[1], conf)
+                    e[2].append(w.tx.txid()[::-1].hex())
+        return {k: (v[0], v[1], v[2]) for k, v in out.items()}

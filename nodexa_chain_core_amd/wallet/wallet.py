@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import json
 import os
+import struct
 import threading
 import time
 
@@ -27,6 +28,27 @@ SECRET_PREFIX = {"main": 112, "test": 114, "regtest": 114}
 SIGHASH_ALL = 1
 COIN = 100_000_000
 DEFAULT_FEE_RATE = 2_000_000  # sat per kvB: above the 0.01 CLORE/kvB min relay fee
+DEFAULT_KEYPOOL_SIZE = 100
+DEFAULT_DERIVE_ROUNDS = 25000  # CMasterKey nDeriveIterations default
+UNLOCK_NEEDED = "Error: Please enter the wallet passphrase with walletpassphrase first."
+HARDENED = 0x80000000
+
+
+def _iv(pub: bytes) -> bytes:
+    """CCrypter IV for a key: the first 16 bytes of sha256d(pubkey) (EncryptSecret)."""
+    return _core.sha256d(pub)[:16]
+
+
+def _bip32_master(seed: bytes) -> tuple[bytes, bytes]:
+    i = _core.hmac_sha512(b"Bitcoin seed", seed)
+    return i[:32], i[32:]
+
+
+def _ckd_priv(k: bytes, c: bytes, index: int):
+    """BIP32 hardened private child: HMAC-SHA512(c, 0x00 || k || ser32(i | 2^31)); None if invalid."""
+    i = _core.hmac_sha512(c, b"\x00" + k + struct.pack(">I", index | HARDENED))
+    child = _core.secp_seckey_tweak_add(k, i[:32])
+    return None if child is None else (child, i[32:])
 
 
 def _push(d: bytes) -> bytes:
@@ -91,15 +113,49 @@ class Wallet:
         self.created: dict[bytes, int] = {}
         self._p2sh_wpkh: dict[bytes, bytes] = {}  # hash160(0x0014 || h) -> h
         self.redeem_scripts: dict[bytes, bytes] = {}  # hash160(script) -> script (addmultisigaddress)
+        self.history = None    # wallet/history.WalletHistory, attached by the node
+        self.fee_rate = DEFAULT_FEE_RATE  # settxfee
+        self.hdpath: dict[bytes, str] = {}      # hdkeypath of derived keys
+        self.pool: list[bytes] = []             # keypool: reserved keys not yet handed out
+        self.hd: dict | None = None             # {"master_id", "next", "seed", "seed_crypted"}
+        self.crypted: dict[bytes, bytes] = {}   # encrypted secrets (encryptwallet)
+        self.mkey: dict | None = None           # {"salt", "rounds", "crypted"} master key record
+        self._master: bytes | None = None       # the master key while unlocked
+        self._relock = None
+        self.unlocked_until = 0
         if path and os.path.exists(path):
             self._load()
+        if self.hd is None and not self.keys:  # a new wallet is HD (CWallet::GenerateNewHDMasterKey)
+            self._init_hd()
 
     # ------------------------------------------------------------------ persistence
     def _load(self) -> None:
         with open(self.path) as f:
             data = json.load(f)
+        mk = data.get("mkey")
+        if mk:
+            self.mkey = {"salt": bytes.fromhex(mk["salt"]), "rounds": int(mk["rounds"]),
+                         "crypted": bytes.fromhex(mk["crypted"])}
         for k in data.get("keys", []):
-            self._add_secret(self.decode_wif(k["wif"]), k.get("label", ""), k.get("created", 0), save=False)
+            if "wif" in k:
+                h = self._add_secret(self.decode_wif(k["wif"]), k.get("label", ""), k.get("created", 0), save=False)
+            else:
+                pub = bytes.fromhex(k["pub"])
+                h = _core.hash160(pub)
+                self.keys[h] = (None, pub)
+                self.crypted[h] = bytes.fromhex(k["crypted"])
+                self._p2sh_wpkh[_core.hash160(b"\x00\x14" + h)] = h
+                self.labels[h] = k.get("label", "")
+                self.created[h] = k.get("created", 0)
+            if k.get("hdkeypath"):
+                self.hdpath[h] = k["hdkeypath"]
+            if k.get("pool"):
+                self.pool.append(h)
+        hd = data.get("hd")
+        if hd:
+            self.hd = {"master_id": bytes.fromhex(hd["master_id"]), "next": dict(hd["next"]),
+                       "seed": bytes.fromhex(hd["seed"]) if hd.get("seed") else None,
+                       "seed_crypted": bytes.fromhex(hd["seed_crypted"]) if hd.get("seed_crypted") else None}
         for rs in data.get("redeem_scripts", []):
             script = bytes.fromhex(rs)
             self.redeem_scripts[_core.hash160(script)] = script
@@ -107,10 +163,27 @@ class Wallet:
     def _save(self) -> None:
         if not self.path:
             return
-        data = {"version": 1, "network": self.params.network_id,
-                "keys": [{"wif": self.encode_wif(sec), "label": self.labels.get(h, ""),
-                          "created": self.created.get(h, 0)} for h, (sec, _) in self.keys.items()],
+        keys = []
+        for h, (sec, pub) in self.keys.items():
+            e = {"label": self.labels.get(h, ""), "created": self.created.get(h, 0)}
+            if self.mkey is not None:
+                e.update({"pub": pub.hex(), "crypted": self.crypted[h].hex()})
+            else:
+                e["wif"] = self.encode_wif(sec)
+            if h in self.hdpath:
+                e["hdkeypath"] = self.hdpath[h]
+            if h in self.pool:
+                e["pool"] = True
+            keys.append(e)
+        data = {"version": 2, "network": self.params.network_id, "keys": keys,
                 "redeem_scripts": [rs.hex() for rs in self.redeem_scripts.values()]}
+        if self.hd is not None:
+            data["hd"] = {"master_id": self.hd["master_id"].hex(), "next": self.hd["next"],
+                          "seed": self.hd["seed"].hex() if self.hd["seed"] is not None and self.mkey is None else None,
+                          "seed_crypted": self.hd["seed_crypted"].hex() if self.hd.get("seed_crypted") else None}
+        if self.mkey is not None:
+            data["mkey"] = {"salt": self.mkey["salt"].hex(), "rounds": self.mkey["rounds"],
+                            "crypted": self.mkey["crypted"].hex()}
         tmp = self.path + ".new"
         with open(tmp, "w") as f:
             json.dump(data, f, indent=1)
@@ -131,14 +204,21 @@ class Wallet:
             raise WalletError("Private key outside allowed range")
         return secret
 
-    def _add_secret(self, secret: bytes, label: str = "", created: int | None = None, save: bool = True) -> bytes:
+    def _add_secret(self, secret: bytes, label: str = "", created: int | None = None, save: bool = True,
+                    hdkeypath: str | None = None) -> bytes:
         pub = _core.secp_pubkey_create(secret, True)
         h = _core.hash160(pub)
         with self.lock:
             self.keys[h] = (secret, pub)
+            if self.mkey is not None:
+                if self._master is None:
+                    raise WalletError(UNLOCK_NEEDED)
+                self.crypted[h] = _core.aes256_cbc_encrypt(self._master, _iv(pub), secret)
             self._p2sh_wpkh[_core.hash160(b"\x00\x14" + h)] = h
             self.labels[h] = label
             self.created[h] = int(time.time()) if created is None else created
+            if hdkeypath:
+                self.hdpath[h] = hdkeypath
             if save:
                 self._save()
         return h
@@ -146,11 +226,61 @@ class Wallet:
     def address_of(self, h160: bytes) -> str:
         return _core.base58check_encode(bytes([self.params.pubkey_prefix]) + h160)
 
-    def new_address(self, label: str = "") -> str:
+    # ------------------------------------------------------------------ HD chain (BIP32, hardened)
+    def _init_hd(self) -> None:
+        """SetHDMasterKey: a random seed; keys derive as m/0'/0'/i' (receive) and m/0'/1'/i' (change),
+        the 0.15 wallet layout (CWallet::DeriveNewChildKey)."""
+        seed = os.urandom(32)
+        mk, _ = _bip32_master(seed)
+        self.hd = {"master_id": _core.hash160(_core.secp_pubkey_create(mk, True)), "next": {"0": 0, "1": 0},
+                   "seed": seed, "seed_crypted": None}
+
+    def _hd_seed(self) -> bytes:
+        if self.hd["seed"] is None:
+            raise WalletError(UNLOCK_NEEDED)
+        return self.hd["seed"]
+
+    def _derive(self, change: bool) -> tuple[bytes, str]:
+        chain = "1" if change else "0"
+        k, c = _bip32_master(self._hd_seed())
+        for i in (0, int(chain)):
+            k, c = _ckd_priv(k, c, i)
         while True:
-            secret = os.urandom(32)
-            if _core.secp_seckey_valid(secret):
-                return self.address_of(self._add_secret(secret, label))
+            idx = self.hd["next"][chain]
+            self.hd["next"][chain] = idx + 1
+            child = _ckd_priv(k, c, idx)
+            if child is not None:
+                return child[0], f"m/0'/{chain}'/{idx}'"
+
+    def _fresh_key(self, label: str) -> bytes:
+        if self.hd is None:
+            while True:
+                secret = os.urandom(32)
+                if _core.secp_seckey_valid(secret):
+                    return self._add_secret(secret, label)
+        secret, path = self._derive(label == "change")
+        return self._add_secret(secret, label, hdkeypath=path)
+
+    def new_address(self, label: str = "") -> str:
+        """GetKeyFromPool: a reserved pool key when there is one (works while the wallet is locked),
+        else a freshly derived key."""
+        with self.lock:
+            if self.pool:
+                h = self.pool.pop(0)
+                self.labels[h] = label
+                self._save()
+                return self.address_of(h)
+            if self.mkey is not None and self._master is None:
+                raise WalletError("Error: Keypool ran out, please call keypoolrefill first")
+            return self.address_of(self._fresh_key(label))
+
+    def keypool_refill(self, size: int = DEFAULT_KEYPOOL_SIZE) -> None:
+        with self.lock:
+            if self.mkey is not None and self._master is None:
+                raise WalletError(UNLOCK_NEEDED)
+            while len(self.pool) < size:
+                self.pool.append(self._fresh_key(""))
+            self._save()
 
     def import_privkey(self, wif: str, label: str = "") -> str:
         return self.address_of(self._add_secret(self.decode_wif(wif), label))
@@ -159,7 +289,94 @@ class Wallet:
         h = self._h160_of(address)
         if h not in self.keys:
             raise WalletError("Private key for address is not known")
-        return self.encode_wif(self.keys[h][0])
+        sec = self.keys[h][0]
+        if sec is None:
+            raise WalletError(UNLOCK_NEEDED)
+        return self.encode_wif(sec)
+
+    # ------------------------------------------------------------------ encryption (CCryptoKeyStore)
+    @property
+    def encrypted(self) -> bool:
+        return self.mkey is not None
+
+    @property
+    def locked(self) -> bool:
+        return self.mkey is not None and self._master is None
+
+    def encrypt(self, passphrase: str, rounds: int = DEFAULT_DERIVE_ROUNDS) -> None:
+        """EncryptWallet: a random master key encrypted under the passphrase (BytesToKeySHA512AES),
+        every secret and the HD seed encrypted under the master key; the wallet ends up locked."""
+        with self.lock:
+            if self.mkey is not None:
+                raise WalletError("Error: running with an encrypted wallet, but encryptwallet was called.")
+            if not passphrase:
+                raise WalletError("passphrase can not be empty")
+            master = os.urandom(32)
+            salt = os.urandom(8)
+            key, iv = _core.bytes_to_key_sha512(passphrase, salt, rounds)
+            self.mkey = {"salt": salt, "rounds": rounds, "crypted": _core.aes256_cbc_encrypt(key, iv, master)}
+            for h, (sec, pub) in self.keys.items():
+                self.crypted[h] = _core.aes256_cbc_encrypt(master, _iv(pub), sec)
+            if self.hd is not None:
+                self.hd["seed_crypted"] = _core.aes256_cbc_encrypt(master, _iv(b"hdseed"), self.hd["seed"])
+            self._master = master
+            self.keypool_refill()
+            self._save()
+            self.lock_wallet()
+
+    def _master_from(self, passphrase: str) -> bytes | None:
+        key, iv = _core.bytes_to_key_sha512(passphrase, self.mkey["salt"], self.mkey["rounds"])
+        master = _core.aes256_cbc_decrypt(key, iv, self.mkey["crypted"])
+        if master is None or len(master) != 32:
+            return None
+        for h, (_, pub) in list(self.keys.items())[:1]:  # the check CCryptoKeyStore::Unlock does
+            sec = _core.aes256_cbc_decrypt(master, _iv(pub), self.crypted[h])
+            if sec is None or _core.secp_pubkey_create(sec, True) != pub:
+                return None
+        return master
+
+    def unlock(self, passphrase: str, timeout: int = 0) -> None:
+        with self.lock:
+            if self.mkey is None:
+                raise WalletError("Error: running with an unencrypted wallet, but walletpassphrase was called.")
+            master = self._master_from(passphrase)
+            if master is None:
+                raise WalletError("Error: The wallet passphrase entered was incorrect.")
+            self._master = master
+            for h, (_, pub) in list(self.keys.items()):
+                self.keys[h] = (_core.aes256_cbc_decrypt(master, _iv(pub), self.crypted[h]), pub)
+            if self.hd is not None and self.hd.get("seed_crypted"):
+                self.hd["seed"] = _core.aes256_cbc_decrypt(master, _iv(b"hdseed"), self.hd["seed_crypted"])
+            if self._relock is not None:
+                self._relock.cancel()
+            self.unlocked_until = int(time.time()) + int(timeout) if timeout else 0
+            if timeout:
+                self._relock = threading.Timer(float(timeout), self.lock_wallet)
+                self._relock.daemon = True
+                self._relock.start()
+
+    def lock_wallet(self) -> None:
+        with self.lock:
+            if self.mkey is None:
+                return
+            self._master = None
+            for h, (_, pub) in list(self.keys.items()):
+                self.keys[h] = (None, pub)
+            if self.hd is not None:
+                self.hd["seed"] = None
+            self.unlocked_until = 0
+
+    def change_passphrase(self, old: str, new: str) -> None:
+        with self.lock:
+            if self.mkey is None:
+                raise WalletError("Error: running with an unencrypted wallet, but walletpassphrasechange was called.")
+            master = self._master_from(old)
+            if master is None:
+                raise WalletError("Error: The wallet passphrase entered was incorrect.")
+            salt = os.urandom(8)
+            key, iv = _core.bytes_to_key_sha512(new, salt, self.mkey["rounds"])
+            self.mkey = {"salt": salt, "rounds": self.mkey["rounds"], "crypted": _core.aes256_cbc_encrypt(key, iv, master)}
+            self._save()
 
     def _h160_of(self, address: str) -> bytes:
         raw = _core.base58check_decode(address)
@@ -218,10 +435,11 @@ class Wallet:
             tip = st.coins_tip().height
             scripts = self.scripts()
             pool_spent = {(i.prevout.hash, i.prevout.n) for e in st.mempool.values() for i in e.tx.vin}
+            locked = self.history.locked if self.history is not None else set()
             out = []
             for txid, n, value, spk, height, coinbase in st.coins.outputs_for_scripts(scripts):
                 conf = tip - height + 1
-                if (txid, n) in pool_spent or not (minconf <= conf <= maxconf):
+                if (txid, n) in pool_spent or (txid, n) in locked or not (minconf <= conf <= maxconf):
                     continue
                 # CWalletTx::GetBlocksToMaturity: a coinbase needs COINBASE_MATURITY + 1 confirmations
                 mature = not coinbase or conf > _core.COINBASE_MATURITY
@@ -314,6 +532,8 @@ class Wallet:
                                    "error": "Unable to sign input, missing key"})
                     continue
                 sec, pub, kind = k
+                if sec is None:
+                    raise WalletError(UNLOCK_NEEDED)
                 tx.vin = vins
                 raw = tx.serialize(True)
                 if kind in ("p2pkh", "p2pk"):
@@ -334,17 +554,21 @@ class Wallet:
             self.keys, self._p2sh_wpkh = saved, saved_sh
 
     def fund_and_sign(self, pre_outputs: list, post_outputs: list, extra_inputs: list[dict] = (),
-                      fee_rate: int = DEFAULT_FEE_RATE, change_spk: bytes | None = None):
+                      fee_rate: int = DEFAULT_FEE_RATE, change_spk: bytes | None = None,
+                      require_complete: bool = True):
         """A transaction whose outputs are `pre_outputs`, a CLORE change output, then `post_outputs`
         (asset transactions need their issue / reissue data last), spending `extra_inputs`
         (e.g. asset outputs: dicts with txid, vout, amount, scriptPubKey) plus CLORE coins for the
         outputs' value and the fee. Returns (tx, fee)."""
         target = sum(o.value for o in list(pre_outputs) + list(post_outputs))
-        coins = sorted((u for u in self.unspent(1) if u["spendable"]), key=lambda u: -u["amount"])
+        given = {(u["txid"], u["vout"]) for u in extra_inputs}
+        base = sum(u["amount"] for u in extra_inputs)  # value the caller's inputs already bring
+        coins = sorted((u for u in self.unspent(1) if u["spendable"] and (u["txid"], u["vout"]) not in given),
+                       key=lambda u: -u["amount"])
         fee = 0
         for _ in range(20):
             need = target + fee
-            chosen, total = [], 0
+            chosen, total = [], base
             for u in coins:
                 if total >= need:
                     break
@@ -374,9 +598,10 @@ class Wallet:
             tx.lock_time = max(0, self.state.coins_tip().height)
             prevs = {(u["txid"], u["vout"]): (u["scriptPubKey"], u["amount"]) for u in list(extra_inputs) + chosen}
             tx, complete, errors = self.sign(tx, prevs)
-            if not complete:
+            if not complete and require_complete:
                 raise WalletError(f"Signing transaction failed: {errors}")
             size = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4
+            size += 110 * len(errors)  # inputs left for another signer: a P2PKH-sized scriptSig each
             want = max(1, fee_rate * size // 1000)
             if fee >= want:
                 return tx, fee
@@ -439,9 +664,15 @@ class Wallet:
             fee = want_fee + 68  # headroom for a changed signature size
         raise WalletError("Transaction fee did not converge")
 
-    def send(self, outputs: list[tuple[bytes, int]], subtract_fee: bool = False) -> bytes:
-        tx, _ = self.create_transaction(outputs, subtract_fee=subtract_fee)
+    def send(self, outputs: list[tuple[bytes, int]], subtract_fee: bool = False, comment: str = "") -> bytes:
+        tx, _ = self.create_transaction(outputs, fee_rate=self.fee_rate, subtract_fee=subtract_fee)
         ok, reason, _ = self.state.accept_to_mempool(tx)
         if not ok:
             raise WalletError(f"Transaction rejected: {reason}")
+        if self.history is not None:
+            self.history.add(tx)
+            w = self.history.txs.get(tx.txid())
+            if w is not None and comment:
+                w.comment = comment
+                self.history.save()
         return tx.txid()

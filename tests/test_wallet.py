@@ -202,3 +202,101 @@ def test_privkey_import_export(core, node_factory):  # noqa: F811
     # sendtoaddress with no funds
     with pytest.raises(RuntimeError, match="Insufficient funds"):
         c.sendtoaddress(addr, 1)
+
+
+def test_history_rpcs_and_coin_control(core, node_factory, tmp_path):  # noqa: F811
+    node, _ = node_factory()
+    c = client(node)
+    ext = _external(core)
+    w = fund(c)
+    txs = c.listtransactions("*", 1000)
+    assert len(txs) == 101 and all(t["category"] in ("generate", "immature") for t in txs)
+    assert sum(t["category"] == "generate" for t in txs) == 1
+    txid = c.sendtoaddress(ext, 7, "rent")
+    last = c.listtransactions("*", 1)[0]
+    assert (last["txid"], last["category"], last["amount"], last["confirmations"]) == (txid, "send", -7, 0)
+    assert last["fee"] < 0 and last["comment"] == "rent"
+    c.generatetoaddress(1, w)
+    t = c.gettransaction(txid)
+    assert t["confirmations"] == 1 and t["amount"] == -7 and t["fee"] < 0 and t["details"][0]["address"] == ext
+    # receive into a labelled address, then the received-by views
+    mine = c.getnewaddress("savings")
+    u = mature_coin(c)
+    c.sendrawtransaction(spend(c, u["txid"], u["vout"], u["amount"], mine, 3))
+    h = c.generatetoaddress(1, w)[0]
+    assert c.getreceivedbyaddress(mine) == 3
+    assert any(r["address"] == mine and r["amount"] == 3 and r["account"] == "savings"
+               for r in c.listreceivedbyaddress())
+    assert mine in c.getaddressesbyaccount("savings") and c.getaccount(mine) == "savings"
+    since = c.listsinceblock(c.getblockhash(c.getblockcount() - 1))
+    assert any(e["address"] == mine for e in since["transactions"]) and since["lastblock"] == h
+    # lockunspent keeps a coin out of coin selection
+    coin = mature_coin(c)
+    assert c.lockunspent(False, [{"txid": coin["txid"], "vout": coin["vout"]}])
+    assert c.listlockunspent() == [{"txid": coin["txid"], "vout": coin["vout"]}]
+    assert all((x["txid"], x["vout"]) != (coin["txid"], coin["vout"]) for x in c.listunspent())
+    c.lockunspent(True)
+    assert c.listlockunspent() == []
+    # fundrawtransaction: wallet inputs + change for a bare output list, then sign and send
+    raw = c.createrawtransaction([], {ext: 2.5})
+    funded = c.fundrawtransaction(raw)
+    assert funded["fee"] > 0 and funded["changepos"] >= 0
+    sent = c.sendrawtransaction(c.signrawtransaction(funded["hex"])["hex"])
+    assert sent in c.getrawmempool()
+    # dumpwallet / importwallet round trip into a second wallet
+    dump = str(tmp_path / "dump.txt")
+    c.dumpwallet(dump)
+    assert open(dump).read().count("# addr=") == len(node.wallet.keys)
+    c.backupwallet(str(tmp_path / "backup.json"))
+    assert (tmp_path / "backup.json").exists()
+    c.settxfee(0.05)
+    assert node.wallet.fee_rate == 5_000_000
+
+
+def test_hd_keys_and_encryption(core, node_factory):  # noqa: F811
+    from nodexa_chain_core_amd.wallet.wallet import _bip32_master, _ckd_priv
+
+    # BIP32 test vector 1 (seed 000102...0f): master chain code and m/0' key
+    k, c = _bip32_master(bytes(range(16)))
+    assert c.hex() == "873dff81c02f525623fd1fe5167eac3a55a049de3d314bb42ee227ffed37d508"
+    assert _ckd_priv(k, c, 0)[0].hex() == "edb2e14f9ee77d26dd93b4ecede8d16ed408ce149b6cd80b0715a2d911a0afea"
+    node, _ = node_factory()
+    c = client(node)
+    info = c.getwalletinfo()
+    assert "hdmasterkeyid" in info and "unlocked_until" not in info
+    a1, a2 = c.getnewaddress(), c.getnewaddress()
+    assert c.validateaddress(a1)["hdkeypath"] == "m/0'/0'/0'" and c.validateaddress(a2)["hdkeypath"] == "m/0'/0'/1'"
+    fund(c)
+    wif = c.dumpprivkey(a1)
+    # encrypt: locked afterwards; signing, dumping and fresh derivation need the passphrase
+    c.encryptwallet("correct horse")
+    info = c.getwalletinfo()
+    assert info["unlocked_until"] == 0 and info["keypoolsize"] >= 100
+    with pytest.raises(RuntimeError, match="-13"):
+        c.dumpprivkey(a1)
+    with pytest.raises(RuntimeError, match="-13"):
+        c.sendtoaddress(_external(core), 1)
+    assert c.getnewaddress().startswith("J")  # from the keypool while locked
+    with pytest.raises(RuntimeError, match="-14"):
+        c.walletpassphrase("wrong", 60)
+    c.walletpassphrase("correct horse", 60)
+    assert c.getwalletinfo()["unlocked_until"] > 0
+    assert c.dumpprivkey(a1) == wif
+    txid = c.sendtoaddress(_external(core), 1)
+    assert txid in c.getrawmempool()
+    c.generatetoaddress(1, a2)  # confirms the send (its change is ours)
+    c.walletlock()
+    with pytest.raises(RuntimeError, match="-13"):
+        c.dumpprivkey(a1)
+    c.walletpassphrasechange("correct horse", "battery staple")
+    with pytest.raises(RuntimeError, match="-14"):
+        c.walletpassphrase("correct horse", 10)
+    # the encrypted wallet survives a restart
+    node.stop()
+    node, _ = node_factory()
+    c = client(node)
+    with pytest.raises(RuntimeError, match="-13"):
+        c.dumpprivkey(a1)
+    c.walletpassphrase("battery staple", 30)
+    assert c.dumpprivkey(a1) == wif
+    assert c.getwalletinfo()["balance"] > 0
