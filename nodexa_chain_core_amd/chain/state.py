@@ -265,10 +265,12 @@ class ChainState:
 
     # ------------------------------------------------------------------ queries
     def tip(self):
-        return self.chain.tip()
+        """chainActive.Tip(): the last block connected to the UTXO set (the header chain may run
+        ahead of it while block data is still being fetched)."""
+        return self.coins_tip() if hasattr(self, "coins") else self.chain.tip()
 
     def height(self) -> int:
-        return self.chain.height()
+        return self.tip().height
 
     def block_hash(self, header) -> bytes:
         return self.chain.block_hash(header)

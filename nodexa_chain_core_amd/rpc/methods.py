@@ -214,7 +214,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
     def rpc_getblockchaininfo(p):
         """getblockchaininfo — state of the chain."""
         tip = st.tip()
-        return {"chain": params.network_id, "blocks": tip.height, "headers": tip.height,
+        return {"chain": params.network_id, "blocks": tip.height, "headers": st.chain.height(),
                 "bestblockhash": _hex(tip.hash), "difficulty": _core.difficulty_from_bits(tip.bits),
                 "mediantime": tip.median_time_past(), "verificationprogress": 1.0,
                 "chainwork": "%064x" % tip.chain_work, "size_on_disk": node.blocks_size_on_disk(),
