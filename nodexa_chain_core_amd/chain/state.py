@@ -65,6 +65,15 @@ class ValidationInterface:
 
     def transaction_added_to_mempool(self, tx) -> None: ...
 
+    # ConnectTip / DisconnectTip post-processing, called synchronously (under the chain lock) for
+    # each block as it joins or leaves the UTXO set, with that block's undo data (the coins it
+    # spent): the asset-messaging and reward-snapshot hooks of src/validation.cpp:10517, 11058
+    def connect_tip(self, block, index, undo: bytes) -> None: ...
+
+    def disconnect_tip(self, block, index, undo: bytes) -> None: ...
+
+    def new_asset_message(self, message) -> None: ...
+
 
 def make_params(network: str, kawpow_activation_time: int | None = None,
                 equihash_activation_time: int | None = None):
@@ -258,8 +267,11 @@ class ChainState:
 
     def _emit(self, name: str, *a) -> None:
         for l in list(self.listeners):
+            fn = getattr(l, name, None)
+            if fn is None:  # listeners need not implement every hook
+                continue
             try:
-                getattr(l, name)(*a)
+                fn(*a)
             except Exception as e:  # a subscriber must never break validation
                 log.log_printf(f"validation listener {type(l).__name__}.{name} failed: {e}")
 
@@ -572,6 +584,7 @@ class ChainState:
                     log.log_printf(f"disconnect of {_core.u256_hex(cur.hash)} found an inconsistent UTXO set")
                 self.indexes.disconnect(blk, cur.height, cur.hash, undo)
                 self.coins.best_block = cur.prev_hash
+                self._emit("disconnect_tip", blk, cur, undo)
                 disconnected.append(blk)
                 cur = self.chain.find(cur.prev_hash)
             path, x = [], target
@@ -666,6 +679,7 @@ class ChainState:
             self.asset_undo.write(idx.hash, idx.prev_hash, aundo)
         self.coins.best_block = idx.hash
         self.record_confirmations(block, height)
+        self._emit("connect_tip", block, idx, undo)
         self._since_flush += 1
         if self._since_flush >= self.flush_interval:
             self.flush()

@@ -3,7 +3,8 @@
 Parity: CZMQNotificationInterface + CZMQPublish*Notifier (src/zmq/
 zmqnotificationinterface.cpp:41-45, src/zmq/zmqpublishnotifier.cpp:25,136-143):
 `-zmqpubhashblock=tcp://host:port`, `-zmqpubrawblock=...`, `-zmqpubhashtx=...`,
-`-zmqpubrawtx=...`; every notification is a 3-frame multipart message
+`-zmqpubrawtx=...`, `-zmqpubrawmessage=...` (asset messages as the reference's JSON string);
+every notification is a 3-frame multipart message
 [topic][payload][little-endian u32 sequence number], one sequence counter per
 topic; block/tx hashes are sent in display (reversed) byte order as the
 reference does. libzmq is not available in this environment, so the endpoint
@@ -20,7 +21,7 @@ import threading
 
 from ..utils import log
 
-TOPICS = ("hashblock", "hashtx", "rawblock", "rawtx")
+TOPICS = ("hashblock", "hashtx", "rawblock", "rawtx", "rawmessage")
 
 
 def greeting(as_server: bool = True) -> bytes:
@@ -183,6 +184,10 @@ class ZmqNotifier:
             self.pubs["hashtx"].publish("hashtx", bytes(tx.txid())[::-1])
         if "rawtx" in self.pubs:
             self.pubs["rawtx"].publish("rawtx", tx.serialize(True))
+
+    def new_asset_message(self, message) -> None:  # CZMQPublishNewAssetMessageNotifier ("rawmessage")
+        if "rawmessage" in self.pubs:
+            self.pubs["rawmessage"].publish("rawmessage", message.zmq_json().encode())
 
     def updated_block_tip(self, *a) -> None: ...
 

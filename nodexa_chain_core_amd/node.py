@@ -27,7 +27,7 @@ from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
 from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, GpuKawpowBackend, MinerController
-from .rpc import methods, methods_assets, methods_ext, methods_index, methods_util, methods_wallet
+from .rpc import methods, methods_assets, methods_ext, methods_index, methods_messages, methods_util, methods_wallet
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
 from .utils import log, metrics
 from .utils.config import ArgsManager, gpu_list
@@ -120,7 +120,20 @@ class Node:
             self.state.register(self.wallet.history)
             methods_wallet.register(self.table, self)
         self.asset_wallet = None
+        from .wallet.messages import MessageStore
+        from .wallet.rewards import MINIMUM_REWARDS_PAYOUT_HEIGHT, Rewards
+
+        # asset messaging (-disablemessaging) and reward snapshots (-minrewardheight)
+        self.messages = MessageStore(self.state, self.wallet,
+                                     os.path.join(self.datadir, "messages.json") if self.datadir else None,
+                                     enabled=not a.get_bool("disablemessaging", False))
+        self.state.register(self.messages)
+        self.rewards = Rewards(self.state, self.wallet, self.asset_wallet_instance,
+                               os.path.join(self.datadir, "rewards.json") if self.datadir else None,
+                               a.get_int("minrewardheight", MINIMUM_REWARDS_PAYOUT_HEIGHT))
+        self.state.register(self.rewards)
         methods_assets.register(self.table, self)  # chain-state asset methods work without a wallet
+        methods_messages.register(self.table, self)
         methods_index.register(self.table, self)
         methods_util.register(self.table, self)
         if a.get("minrelaytxfee") is not None:  # -minrelaytxfee=<CLORE per kvB>
@@ -154,7 +167,8 @@ class Node:
         self.connman = None
         self._start_p2p()
         self.zmq = None
-        zmq_eps = {t: a.get("zmqpub" + t) for t in ("hashblock", "hashtx", "rawblock", "rawtx") if a.get("zmqpub" + t)}
+        zmq_eps = {t: a.get("zmqpub" + t) for t in ("hashblock", "hashtx", "rawblock", "rawtx", "rawmessage")
+                   if a.get("zmqpub" + t)}
         if zmq_eps:
             from .net.zmq_pub import ZmqNotifier
 
@@ -178,6 +192,18 @@ class Node:
                        f"kawpow_activation={self.params.kawpow_activation_time} gpus={self.gpus or 'none'}")
         if a.get_bool("gen", False) and self.network != "regtest":
             self.miner.set_generate(True, self.mining_script)
+
+    def asset_wallet_instance(self):
+        """The node's AssetWallet, built on first use (shared by the asset, message and reward RPCs)."""
+        if self.wallet is None:
+            from .rpc.protocol import RPC_METHOD_NOT_FOUND, RPCError
+
+            raise RPCError(RPC_METHOD_NOT_FOUND, "Method not found (wallet disabled)")
+        if self.asset_wallet is None:
+            from .wallet.assets import AssetWallet
+
+            self.asset_wallet = AssetWallet(self.wallet)
+        return self.asset_wallet
 
     def _start_p2p(self) -> None:
         """-listen / -port / -bind / -connect (CConnman subset, net/p2p.py). Listening is opt-in

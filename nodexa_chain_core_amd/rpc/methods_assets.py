@@ -13,7 +13,7 @@ import fnmatch
 from .. import core
 from ..wallet import WalletError
 from ..wallet.assets import AssetWallet
-from .protocol import (RPC_INVALID_ADDRESS_OR_KEY, RPC_INVALID_PARAMETER, RPC_METHOD_NOT_FOUND, RPC_WALLET_ERROR,
+from .protocol import (RPC_INVALID_ADDRESS_OR_KEY, RPC_INVALID_PARAMETER, RPC_INVALID_REQUEST, RPC_WALLET_ERROR,
                        RPC_WALLET_INSUFFICIENT_FUNDS, RPCError)
 
 _core = core()
@@ -38,11 +38,7 @@ def register(table, node) -> None:
         return p[i] if len(p) > i and p[i] is not None else default
 
     def aw() -> AssetWallet:
-        if getattr(node, "wallet", None) is None:
-            raise RPCError(RPC_METHOD_NOT_FOUND, "Method not found (wallet disabled)")
-        if getattr(node, "asset_wallet", None) is None:
-            node.asset_wallet = AssetWallet(node.wallet)
-        return node.asset_wallet
+        return node.asset_wallet_instance()
 
     def call(fn, *a, **k):
         try:
@@ -51,6 +47,8 @@ def register(table, node) -> None:
             msg = str(e)
             if "Insufficient" in msg:
                 raise RPCError(RPC_WALLET_INSUFFICIENT_FUNDS, msg)
+            if "doesn't have asset" in msg:
+                raise RPCError(RPC_INVALID_REQUEST, msg)
             if "Invalid" in msg or "aren't active" in msg:
                 raise RPCError(RPC_INVALID_PARAMETER, msg)
             raise RPCError(RPC_WALLET_ERROR, msg)

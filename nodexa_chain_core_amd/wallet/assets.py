@@ -100,6 +100,8 @@ class AssetWallet:
 
     def _owner_inputs(self, token: str) -> tuple[list[dict], list]:
         """Spend the wallet's `token` (owner token or qualifier) and send it back to the wallet."""
+        if not self.unspent(token):
+            raise WalletError(f"Wallet doesn't have asset: {token}")
         ins, _ = self._take(token, 1)
         qty = sum(u["qty"] for u in ins)
         back = _core.TxOut(0, _core.asset_script_transfer(ins[0]["hash160"], token, qty))
@@ -188,6 +190,28 @@ class AssetWallet:
         if change:
             outs.append(_core.TxOut(0, _core.asset_script_transfer(self._dest(change_to), name, change)))
         return self._send(outs, [], ins)
+
+    def build_transfer_many(self, name: str, dests: list[tuple[bytes, int]]):
+        """CreateTransferAssetTransaction with one transfer output per (hash160, qty): the signed
+        transaction, not yet submitted (reward distribution batches)."""
+        self._require_active()
+        ins, change = self._take(name, sum(q for _, q in dests))
+        outs = [_core.TxOut(0, _core.asset_script_transfer(h, name, q)) for h, q in dests]
+        if change:
+            outs.append(_core.TxOut(0, _core.asset_script_transfer(self._dest(None), name, change)))
+        tx, _ = self.w.fund_and_sign(outs, [], list(ins))
+        return tx
+
+    def send_message(self, channel: str, payload: bytes, expire: int = 0) -> bytes:
+        """sendmessage (src/rpc/messages.cpp:310): the channel token goes back to the address it is
+        held at, carrying the message (a message only counts when sent to the spending address)."""
+        self._require_active(True)
+        coins = self.unspent(channel)
+        if not coins:
+            raise WalletError(f"Wallet doesn't own the asset_name: {channel}")
+        coin = coins[0]
+        out = _core.TxOut(0, _core.asset_script_transfer(coin["hash160"], channel, coin["qty"], payload, expire))
+        return self._send([out], [], [coin])
 
     # ------------------------------------------------------------------ tags and restrictions
     def tag_address(self, qualifier: str, address: str, add: bool) -> bytes:
