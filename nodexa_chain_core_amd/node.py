@@ -110,8 +110,11 @@ class Node:
 
             from .wallet.history import WalletHistory
 
+            # -bip44 (default on): a new wallet derives from BIP39 words (-mnemonic / -mnemonicpassphrase)
             self.wallet = Wallet(self.state, self.params,
-                                 os.path.join(self.datadir, "wallet.json") if self.datadir else None)
+                                 os.path.join(self.datadir, "wallet.json") if self.datadir else None,
+                                 bip44=a.get_bool("bip44", True), mnemonic=a.get("mnemonic", "") or "",
+                                 mnemonic_passphrase=a.get("mnemonicpassphrase", "") or "")
             hist_path = os.path.join(self.datadir, "wallet_txs.json") if self.datadir else None
             rescan = hist_path is not None and not os.path.exists(hist_path) and bool(self.wallet.keys)
             self.wallet.history = WalletHistory(self.wallet, hist_path)

@@ -423,9 +423,14 @@ def register(table, node) -> None:
         if not p:
             raise RPCError(RPC_INVALID_PARAMETER, 'dumpwallet "filename"')
         w = wallet()
+        if w.locked:
+            raise RPCError(-13, "Error: Please enter the wallet passphrase with walletpassphrase first.")
         tip = st.tip()
         lines = ["# Wallet dump created by nodexa", f"# * Best block at time of backup was {tip.height} "
                  f"({tip.hash[::-1].hex()}),", ""]
+        if w.hd is not None and w.hd.get("bip44"):  # the BIP39 words (src/wallet/rpcdump.cpp:710)
+            words, pp = w.mnemonic()
+            lines[2:2] = [f"# mnemonic: {words}", f"# mnemonic passphrase: {pp}"]
         for h, (sec, _) in w.keys.items():
             t = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(w.created.get(h, 0)))
             lbl = w.labels.get(h, "")
@@ -438,6 +443,20 @@ def register(table, node) -> None:
         except OSError as e:
             raise RPCError(RPC_WALLET_ERROR, f"Cannot open wallet dump file: {e}")
         return {"filename": os.path.abspath(p[0])}
+
+    def rpc_getmywords(p):
+        """getmywords — the BIP39 words (and passphrase, if one was used) this wallet derives from."""
+        w = wallet()
+        if w.locked:
+            raise RPCError(-13, "Error: Please enter the wallet passphrase with walletpassphrase first.")
+        try:
+            words, pp = w.mnemonic()
+        except WalletError as e:
+            raise RPCError(RPC_WALLET_ERROR, str(e))
+        out = {"word_list": words}
+        if pp:
+            out["passphrase"] = pp
+        return out
 
     def rpc_importwallet(p):
         """importwallet "filename" — import the keys of a dumpwallet file, then rescan."""
@@ -551,6 +570,7 @@ def register(table, node) -> None:
         ("wallet", "abandontransaction", rpc_abandontransaction, ("txid",)),
         ("wallet", "backupwallet", rpc_backupwallet, ("destination",)),
         ("wallet", "dumpwallet", rpc_dumpwallet, ("filename",)),
+        ("wallet", "getmywords", rpc_getmywords, ()),
         ("wallet", "importwallet", rpc_importwallet, ("filename",)),
         ("wallet", "keypoolrefill", rpc_keypoolrefill, ("newsize",)),
         ("wallet", "listaddressgroupings", rpc_listaddressgroupings, ()),

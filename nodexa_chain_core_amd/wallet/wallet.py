@@ -6,9 +6,9 @@ dumpprivkey / importprivkey, signrawtransaction, getwalletinfo), CKey::Sign + th
 signature producers of src/script/sign.cpp for P2PKH, P2PK, P2WPKH and P2SH-P2WPKH outputs, WIF
 secrets (base58check: SECRET_KEY prefix, key, 0x01 for compressed keys; src/base58.cpp).
 
-Keys are secp256k1 secrets from os.urandom (csrc/crypto/secp256k1.cpp signs them with RFC 6979)
-kept in <datadir>/wallet.json, written atomically (no encryption: `walletpassphrase` is not
-offered). Balances come from the node's UTXO set (CoinsView.outputs_for_scripts) plus the
+Keys derive from a BIP39 mnemonic along BIP44 paths (or the 0.15 hardened BIP32 layout with
+-bip44=0; csrc/crypto/secp256k1.cpp signs with RFC 6979) and live in <datadir>/wallet.json,
+written atomically, optionally AES-256-CBC encrypted (encryptwallet). Balances come from the node's UTXO set (CoinsView.outputs_for_scripts) plus the
 mempool's unconfirmed outputs to the wallet's scripts.
 """
 from __future__ import annotations
@@ -32,6 +32,11 @@ DEFAULT_KEYPOOL_SIZE = 100
 DEFAULT_DERIVE_ROUNDS = 25000  # CMasterKey nDeriveIterations default
 UNLOCK_NEEDED = "Error: Please enter the wallet passphrase with walletpassphrase first."
 HARDENED = 0x80000000
+# nExtCoinType (src/chainparams.cpp:196, 355, 522): the BIP44 coin_type level
+EXT_COIN_TYPE = {"main": 1313, "test": 1, "regtest": 1}
+# base58Prefixes[EXT_SECRET_KEY] (src/chainparams.cpp:193, 352, 519)
+EXT_SECRET_PREFIX = {"main": bytes.fromhex("0488ADE4"), "test": bytes.fromhex("04358394"),
+                     "regtest": bytes.fromhex("04358394")}
 
 
 def _iv(pub: bytes) -> bytes:
@@ -44,11 +49,24 @@ def _bip32_master(seed: bytes) -> tuple[bytes, bytes]:
     return i[:32], i[32:]
 
 
-def _ckd_priv(k: bytes, c: bytes, index: int):
-    """BIP32 hardened private child: HMAC-SHA512(c, 0x00 || k || ser32(i | 2^31)); None if invalid."""
-    i = _core.hmac_sha512(c, b"\x00" + k + struct.pack(">I", index | HARDENED))
+def _ckd_priv(k: bytes, c: bytes, index: int, hardened: bool = True):
+    """BIP32 private child: HMAC-SHA512(c, 0x00 || k || ser32(i | 2^31)) when hardened, else
+    HMAC-SHA512(c, serP(k*G) || ser32(i)); child = k + IL. None if the child is invalid."""
+    if hardened:
+        data = b"\x00" + k + struct.pack(">I", index | HARDENED)
+    else:
+        data = _core.secp_pubkey_create(k, True) + struct.pack(">I", index)
+    i = _core.hmac_sha512(c, data)
     child = _core.secp_seckey_tweak_add(k, i[:32])
     return None if child is None else (child, i[32:])
+
+
+def ext_key_b58(k: bytes, c: bytes, network: str, depth: int = 0, fingerprint: bytes = b"\0" * 4,
+                child: int = 0) -> str:
+    """CExtKey::Encode under base58Prefixes[EXT_SECRET_KEY] (xprv / tprv)."""
+    version = EXT_SECRET_PREFIX[network]
+    return _core.base58check_encode(version + bytes([depth]) + fingerprint + struct.pack(">I", child) + c
+                                    + b"\x00" + k)
 
 
 def _push(d: bytes) -> bytes:
@@ -103,7 +121,8 @@ def multisig_script(m: int, pubkeys: list[bytes]) -> bytes:
 
 
 class Wallet:
-    def __init__(self, state, params, path: str | None):
+    def __init__(self, state, params, path: str | None, bip44: bool = True, mnemonic: str = "",
+                 mnemonic_passphrase: str = ""):
         self.state = state
         self.params = params
         self.path = path
@@ -125,8 +144,8 @@ class Wallet:
         self.unlocked_until = 0
         if path and os.path.exists(path):
             self._load()
-        if self.hd is None and not self.keys:  # a new wallet is HD (CWallet::GenerateNewHDMasterKey)
-            self._init_hd()
+        if self.hd is None and not self.keys:  # a new wallet is HD (CWallet::GenerateNewSeed)
+            self._init_hd(bip44, mnemonic, mnemonic_passphrase)
 
     # ------------------------------------------------------------------ persistence
     def _load(self) -> None:
@@ -155,7 +174,11 @@ class Wallet:
         if hd:
             self.hd = {"master_id": bytes.fromhex(hd["master_id"]), "next": dict(hd["next"]),
                        "seed": bytes.fromhex(hd["seed"]) if hd.get("seed") else None,
-                       "seed_crypted": bytes.fromhex(hd["seed_crypted"]) if hd.get("seed_crypted") else None}
+                       "seed_crypted": bytes.fromhex(hd["seed_crypted"]) if hd.get("seed_crypted") else None,
+                       "bip44": bool(hd.get("bip44", False)), "mnemonic": hd.get("mnemonic"),
+                       "mnemonic_passphrase": hd.get("mnemonic_passphrase"),
+                       "mnemonic_crypted": bytes.fromhex(hd["mnemonic_crypted"]) if hd.get("mnemonic_crypted")
+                       else None}
         for rs in data.get("redeem_scripts", []):
             script = bytes.fromhex(rs)
             self.redeem_scripts[_core.hash160(script)] = script
@@ -178,9 +201,15 @@ class Wallet:
         data = {"version": 2, "network": self.params.network_id, "keys": keys,
                 "redeem_scripts": [rs.hex() for rs in self.redeem_scripts.values()]}
         if self.hd is not None:
+            plain = self.mkey is None
             data["hd"] = {"master_id": self.hd["master_id"].hex(), "next": self.hd["next"],
-                          "seed": self.hd["seed"].hex() if self.hd["seed"] is not None and self.mkey is None else None,
-                          "seed_crypted": self.hd["seed_crypted"].hex() if self.hd.get("seed_crypted") else None}
+                          "seed": self.hd["seed"].hex() if self.hd["seed"] is not None and plain else None,
+                          "seed_crypted": self.hd["seed_crypted"].hex() if self.hd.get("seed_crypted") else None,
+                          "bip44": self.hd.get("bip44", False),
+                          "mnemonic": self.hd.get("mnemonic") if plain else None,
+                          "mnemonic_passphrase": self.hd.get("mnemonic_passphrase") if plain else None,
+                          "mnemonic_crypted": self.hd["mnemonic_crypted"].hex() if self.hd.get("mnemonic_crypted")
+                          else None}
         if self.mkey is not None:
             data["mkey"] = {"salt": self.mkey["salt"].hex(), "rounds": self.mkey["rounds"],
                             "crypted": self.mkey["crypted"].hex()}
@@ -226,14 +255,35 @@ class Wallet:
     def address_of(self, h160: bytes) -> str:
         return _core.base58check_encode(bytes([self.params.pubkey_prefix]) + h160)
 
-    # ------------------------------------------------------------------ HD chain (BIP32, hardened)
-    def _init_hd(self) -> None:
-        """SetHDMasterKey: a random seed; keys derive as m/0'/0'/i' (receive) and m/0'/1'/i' (change),
-        the 0.15 wallet layout (CWallet::DeriveNewChildKey)."""
-        seed = os.urandom(32)
+    # ------------------------------------------------------------------ HD chain (BIP32 / BIP39 / BIP44)
+    def _init_hd(self, bip44: bool = True, mnemonic: str = "", passphrase: str = "") -> None:
+        """GenerateNewSeed. With -bip44 (the default) the seed is the BIP39 seed of a 12-word mnemonic
+        (-mnemonic / -mnemonicpassphrase, or freshly generated) and keys derive as
+        m/44'/coin'/0'/change/i (CHDChain::SetMnemonic, CWallet::DeriveNewChildKey); with -bip44=0 a
+        random 32-byte seed and the 0.15 layout m/0'/0'/i' (receive), m/0'/1'/i' (change)."""
+        from . import bip39
+
+        if bip44:
+            mnemonic = " ".join(mnemonic.split()) or bip39.generate(128)
+            if not bip39.check(mnemonic):
+                raise WalletError(f"invalid mnemonic: `{mnemonic}`")
+            seed = bip39.to_seed(mnemonic, passphrase)
+        else:
+            seed = os.urandom(32)
         mk, _ = _bip32_master(seed)
         self.hd = {"master_id": _core.hash160(_core.secp_pubkey_create(mk, True)), "next": {"0": 0, "1": 0},
-                   "seed": seed, "seed_crypted": None}
+                   "seed": seed, "seed_crypted": None, "bip44": bip44,
+                   "mnemonic": mnemonic if bip44 else None, "mnemonic_passphrase": passphrase if bip44 else None,
+                   "mnemonic_crypted": None}
+
+    def mnemonic(self) -> tuple[str, str]:
+        """getmywords: (word list, passphrase) of a BIP39 wallet."""
+        if self.hd is None or not self.hd.get("bip44"):
+            raise WalletError("Error: Wallet doesn't have 12 words. Only new wallets generated by the mnemonic "
+                              "phrase will have 12 words")
+        if self.hd.get("mnemonic") is None:
+            raise WalletError(UNLOCK_NEEDED)
+        return self.hd["mnemonic"], self.hd.get("mnemonic_passphrase") or ""
 
     def _hd_seed(self) -> bytes:
         if self.hd["seed"] is None:
@@ -243,14 +293,21 @@ class Wallet:
     def _derive(self, change: bool) -> tuple[bytes, str]:
         chain = "1" if change else "0"
         k, c = _bip32_master(self._hd_seed())
-        for i in (0, int(chain)):
-            k, c = _ckd_priv(k, c, i)
+        bip44 = self.hd.get("bip44", False)
+        if bip44:
+            coin = EXT_COIN_TYPE[self.params.network_id]
+            for i, hard in ((44, True), (coin, True), (0, True), (int(chain), False)):
+                k, c = _ckd_priv(k, c, i, hard)
+        else:
+            for i in (0, int(chain)):
+                k, c = _ckd_priv(k, c, i)
         while True:
             idx = self.hd["next"][chain]
             self.hd["next"][chain] = idx + 1
-            child = _ckd_priv(k, c, idx)
+            child = _ckd_priv(k, c, idx, not bip44)
             if child is not None:
-                return child[0], f"m/0'/{chain}'/{idx}'"
+                path = f"m/44'/{coin}'/0'/{chain}/{idx}" if bip44 else f"m/0'/{chain}'/{idx}'"
+                return child[0], path
 
     def _fresh_key(self, label: str) -> bytes:
         if self.hd is None:
@@ -319,6 +376,9 @@ class Wallet:
                 self.crypted[h] = _core.aes256_cbc_encrypt(master, _iv(pub), sec)
             if self.hd is not None:
                 self.hd["seed_crypted"] = _core.aes256_cbc_encrypt(master, _iv(b"hdseed"), self.hd["seed"])
+                if self.hd.get("mnemonic") is not None:
+                    words = json.dumps([self.hd["mnemonic"], self.hd.get("mnemonic_passphrase") or ""]).encode()
+                    self.hd["mnemonic_crypted"] = _core.aes256_cbc_encrypt(master, _iv(b"bip39words"), words)
             self._master = master
             self.keypool_refill()
             self._save()
@@ -347,6 +407,9 @@ class Wallet:
                 self.keys[h] = (_core.aes256_cbc_decrypt(master, _iv(pub), self.crypted[h]), pub)
             if self.hd is not None and self.hd.get("seed_crypted"):
                 self.hd["seed"] = _core.aes256_cbc_decrypt(master, _iv(b"hdseed"), self.hd["seed_crypted"])
+            if self.hd is not None and self.hd.get("mnemonic_crypted"):
+                m, pp = json.loads(_core.aes256_cbc_decrypt(master, _iv(b"bip39words"), self.hd["mnemonic_crypted"]))
+                self.hd["mnemonic"], self.hd["mnemonic_passphrase"] = m, pp
             if self._relock is not None:
                 self._relock.cancel()
             self.unlocked_until = int(time.time()) + int(timeout) if timeout else 0
@@ -364,6 +427,8 @@ class Wallet:
                 self.keys[h] = (None, pub)
             if self.hd is not None:
                 self.hd["seed"] = None
+                if self.hd.get("mnemonic_crypted"):
+                    self.hd["mnemonic"] = self.hd["mnemonic_passphrase"] = None
             self.unlocked_until = 0
 
     def change_passphrase(self, old: str, new: str) -> None:

@@ -265,7 +265,11 @@ def test_hd_keys_and_encryption(core, node_factory):  # noqa: F811
     info = c.getwalletinfo()
     assert "hdmasterkeyid" in info and "unlocked_until" not in info
     a1, a2 = c.getnewaddress(), c.getnewaddress()
-    assert c.validateaddress(a1)["hdkeypath"] == "m/0'/0'/0'" and c.validateaddress(a2)["hdkeypath"] == "m/0'/0'/1'"
+    # -bip44 is the default: m/44'/coin_type'/account'/change/index, coin_type 1 off mainnet
+    assert c.validateaddress(a1)["hdkeypath"] == "m/44'/1'/0'/0/0"
+    assert c.validateaddress(a2)["hdkeypath"] == "m/44'/1'/0'/0/1"
+    words = c.getmywords()["word_list"].split()
+    assert len(words) == 12
     fund(c)
     wif = c.dumpprivkey(a1)
     # encrypt: locked afterwards; signing, dumping and fresh derivation need the passphrase
@@ -297,6 +301,84 @@ def test_hd_keys_and_encryption(core, node_factory):  # noqa: F811
     c = client(node)
     with pytest.raises(RuntimeError, match="-13"):
         c.dumpprivkey(a1)
+    with pytest.raises(RuntimeError, match="-13"):
+        c.getmywords()
     c.walletpassphrase("battery staple", 30)
     assert c.dumpprivkey(a1) == wif
     assert c.getwalletinfo()["balance"] > 0
+    assert c.getmywords()["word_list"].split() == words  # the words were kept encrypted
+
+
+# trezor/python-mnemonic vectors (passphrase "TREZOR"), as carried by the reference's
+# src/test/data/bip39_vectors.json: entropy, mnemonic, seed, master xprv (used as data)
+BIP39_VECTORS = [
+    ["00000000000000000000000000000000",
+     "abandon abandon abandon abandon abandon abandon abandon abandon abandon abandon abandon about",
+     "c55257c360c07c72029aebc1b53c05ed0362ada38ead3e3e9efa3708e53495531f09a6987599d18264c1e1c92f2cf141630c7a3c4ab7c81b2f"
+     "001698e7463b04",
+     "xprv9s21ZrQH143K3h3fDYiay8mocZ3afhfULfb5GX8kCBdno77K4HiA15Tg23wpbeF1pLfs1c5SPmYHrEpTuuRhxMwvKDwqdKiGJS9XFKzUsAF"],
+    ["ffffffffffffffffffffffffffffffff", "zoo zoo zoo zoo zoo zoo zoo zoo zoo zoo zoo wrong",
+     "ac27495480225222079d7be181583751e86f571027b0497b5b5d11218e0a8a13332572917f0f8e5a589620c6f15b11c61dee327651a14c34"
+     "e18231052e48c069",
+     "xprv9s21ZrQH143K2V4oox4M8Zmhi2Fjx5XK4Lf7GKRvPSgydU3mjZuKGCTg7UPiBUD7ydVPvSLtg9hjp7MQTYsW67rZHAXeccqYqrsx8LcXnyd"],
+    ["0000000000000000000000000000000000000000000000000000000000000000",
+     "abandon abandon abandon abandon abandon abandon abandon abandon abandon abandon abandon abandon abandon abandon "
+     "abandon abandon abandon abandon abandon abandon abandon abandon abandon art",
+     "bda85446c68413707090a52022edd26a1c9462295029f2e60cd7c4f2bbd3097170af7a4d73245cafa9c3cca8d561a7c3de6f5d4a10be8ed2"
+     "a5e608d68f92fcc8",
+     "xprv9s21ZrQH143K32qBagUJAMU2LsHg3ka7jqMcV98Y7gVeVyNStwYS3U7yVVoDZ4btbRNf4h6ibWpY22iRmXq35qgLs79f312g2kj5539ebPM"],
+    ["9f6a2878b2520799a44ef18bc7df394e7061a224d2c33cd015b157d746869863",
+     "panda eyebrow bullet gorilla call smoke muffin taste mesh discover soft ostrich alcohol speed nation flash devote "
+     "level hobby quick inner drive ghost inside",
+     "72be8e052fc4919d2adf28d5306b5474b0069df35b02303de8c1729c9538dbb6fc2d731d5f832193cd9fb6aeecbc469594a70e3dd50811b5"
+     "067f3b88b28c3e8d",
+     "xprv9s21ZrQH143K2WNnKmssvZYM96VAr47iHUQUTUyUXH3sAGNjhJANddnhw3i3y3pBbRAVk5M5qUGFr4rHbEWwXgX4qrvrceifCYQJbbFDems"],
+    ["f585c11aec520db57dd353c69554b21a89b20fb0650966fa0a9d6f74fd989d8f",
+     "void come effort suffer camp survey warrior heavy shoot primary clutch crush open amazing screen patrol group "
+     "space point ten exist slush involve unfold",
+     "01f5bced59dec48e362f2c45b5de68b9fd6c92c6634f44d6d40aab69056506f0e35524a518034ddc1192e1dacd32c1ed3eaa3c3b131c88ed"
+     "8e7e54c49a5d0998",
+     "xprv9s21ZrQH143K39rnQJknpH1WEPFJrzmAqqasiDcVrNuk926oizzJDDQkdiTvNPr2FYDYzWgiMiC63YmfPAa2oPyNB23r2g7d1yiK6WpqaQS"],
+]
+
+
+def test_bip39_reference_vectors():
+    from nodexa_chain_core_amd.wallet import bip39
+    from nodexa_chain_core_amd.wallet.wallet import _bip32_master, ext_key_b58
+
+    for entropy, words, seed, xprv in BIP39_VECTORS:
+        assert bip39.from_entropy(bytes.fromhex(entropy)) == words
+        assert bip39.check(words) and bip39.to_entropy(words).hex() == entropy
+        s = bip39.to_seed(words, "TREZOR")
+        assert s.hex() == seed
+        k, c = _bip32_master(s)
+        assert ext_key_b58(k, c, "main") == xprv
+    assert not bip39.check("abandon " * 11 + "abandon")  # checksum
+    assert not bip39.check("abandon " * 11 + "notaword")
+    assert len(bip39.generate().split()) == 12
+
+
+def test_wallet_from_mnemonic_is_deterministic(core, tmp_path):
+    from test_p2p import _node
+
+    words = BIP39_VECTORS[0][1]
+    nodes = [_node(core, tmp_path, n, [f"-mnemonic={words}", "-mnemonicpassphrase=TREZOR"]) for n in ("m1", "m2")]
+    try:
+        c1, c2 = client(nodes[0]), client(nodes[1])
+        assert [c1.getnewaddress() for _ in range(3)] == [c2.getnewaddress() for _ in range(3)]
+        assert c1.getmywords() == {"word_list": words, "passphrase": "TREZOR"}
+        assert c1.validateaddress(c1.getrawchangeaddress())["hdkeypath"] == "m/44'/1'/0'/1/0"
+        dump = tmp_path / "dump.txt"
+        c1.dumpwallet(str(dump))
+        assert f"# mnemonic: {words}" in dump.read_text()
+    finally:
+        for n in nodes:
+            n.stop()
+    legacy = _node(core, tmp_path, "legacy", ["-bip44=0"])
+    try:
+        c = client(legacy)
+        assert c.validateaddress(c.getnewaddress())["hdkeypath"] == "m/0'/0'/0'"
+        with pytest.raises(RuntimeError, match="doesn't have 12 words"):
+            c.getmywords()
+    finally:
+        legacy.stop()
