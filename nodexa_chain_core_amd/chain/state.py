@@ -32,6 +32,7 @@ from dataclasses import dataclass, field
 
 from .. import core
 from ..utils import log, sync
+from . import policy
 from .blockindex import BlockIndexLog, scan_blk_tail
 from .undo import UndoStore
 from .versionbits import VersionBits
@@ -103,6 +104,8 @@ class MempoolEntry:
 
 MEMPOOL_DUMP_VERSION = 1
 DEFAULT_MIN_RELAY_TX_FEE = 1_000_000   # sat per kvB (src/validation.h:69)
+DEFAULT_INCREMENTAL_RELAY_FEE = 1000   # sat per kvB (src/policy/policy.h:36)
+DEFAULT_ENABLE_REPLACEMENT = False     # -mempoolreplacement (src/validation.h:163)
 MAX_STANDARD_TX_WEIGHT = 400_000       # src/policy/policy.h:28
 MAX_STANDARD_SCRIPTSIG_SIZE = 1650
 GPU_SIG_BATCH_MIN = 16                 # below this many signatures a block is checked on the host
@@ -153,6 +156,9 @@ class ChainState:
         self.index_log: BlockIndexLog | None = None
         self._mem_blocks: dict[bytes, object] = {}  # block data when there is no datadir
         self.min_relay_fee = DEFAULT_MIN_RELAY_TX_FEE
+        self.incremental_relay_fee = DEFAULT_INCREMENTAL_RELAY_FEE  # -incrementalrelayfee
+        self.enable_replacement = DEFAULT_ENABLE_REPLACEMENT       # -mempoolreplacement
+        self.require_standard = params.network_id == "main"        # fRequireStandard / -acceptnonstdtxn
         self.script_threads = min(16, os.cpu_count() or 1)  # -par: script-check threads (CCheckQueue)
         self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
         self.flush_interval = 1000
@@ -764,17 +770,21 @@ class ChainState:
                 return False, why, 0
             if tx.is_coinbase():
                 return False, "coinbase", 0
-            if tx.version < 1 or tx.version > 2:
-                return False, "version", 0
             weight = len(tx.serialize(False)) * 3 + len(raw)
-            if weight > MAX_STANDARD_TX_WEIGHT:
-                return False, "tx-size", 0
-            for i in tx.vin:
-                if len(i.script_sig) > MAX_STANDARD_SCRIPTSIG_SIZE:
-                    return False, "scriptsig-size", 0
-                if not _core.script_is_push_only(i.script_sig):
-                    return False, "scriptsig-not-pushonly", 0
-            pool_spent = {(i.prevout.hash, i.prevout.n) for e in self.mempool.values() for i in e.tx.vin}
+            if self.require_standard:  # IsStandardTx (fRequireStandard: mainnet, or !-acceptnonstdtxn)
+                if tx.version < 1 or tx.version > 2:
+                    return False, "version", 0
+                if weight >= MAX_STANDARD_TX_WEIGHT:
+                    return False, "tx-size", 0
+                for i in tx.vin:
+                    if len(i.script_sig) > MAX_STANDARD_SCRIPTSIG_SIZE:
+                        return False, "scriptsig-size", 0
+                    if not _core.script_is_push_only(i.script_sig):
+                        return False, "scriptsig-not-pushonly", 0
+                why = policy.standard_outputs_reason(tx)
+                if why:
+                    return False, why, 0
+            pool_spent = {(i.prevout.hash, i.prevout.n): t for t, e in self.mempool.items() for i in e.tx.vin}
             tip = self.coins_tip()
             next_height = tip.height + 1
             # CheckFinalTx for the next block (IsFinalTx with the tip's median time past)
@@ -783,9 +793,12 @@ class ChainState:
                 if tx.lock_time >= limit:
                     return False, "non-final", 0
             in_sum, coins = 0, []
+            conflicts = {pool_spent[(i.prevout.hash, i.prevout.n)] for i in tx.vin
+                         if (i.prevout.hash, i.prevout.n) in pool_spent}
+            if conflicts and (not self.enable_replacement
+                              or not all(policy.signals_rbf(self.mempool[t].tx) for t in conflicts)):
+                return False, "txn-mempool-conflict", 0
             for i in tx.vin:
-                if (i.prevout.hash, i.prevout.n) in pool_spent:
-                    return False, "txn-mempool-conflict", 0
                 c = self._spent_coin(i.prevout)
                 if c is None:
                     return False, "missing-inputs", 0
@@ -803,6 +816,11 @@ class ChainState:
             vsize = (weight + 3) // 4
             if fee < self.min_relay_fee * vsize // 1000:
                 return False, "min relay fee not met", fee
+            replaced = set()
+            if conflicts:
+                why, replaced = self._check_replacement(tx, fee, vsize, conflicts)
+                if why:
+                    return False, why, fee
             if max_fee is not None and fee > max_fee:
                 return False, "absurdly-high-fee", fee
             for k, (value, spk) in enumerate(coins):
@@ -815,8 +833,42 @@ class ChainState:
                     kind = "non-mandatory-script-verify-flag" if ok2 else "mandatory-script-verify-flag-failed"
                     return False, f"{kind} ({err})", fee
             if not test_only:
+                for t in replaced:  # BIP125: the replaced transactions and their descendants leave
+                    self.mempool.pop(t, None)
                 self.add_to_mempool(tx, fee)
             return True, "", fee
+
+    def _check_replacement(self, tx, fee: int, vsize: int, conflicts: set) -> tuple[str, set]:
+        """The BIP125 rules of AcceptToMemoryPoolWorker (src/validation.cpp, -mempoolreplacement):
+        a higher feerate than every direct conflict, at most 100 evicted transactions (conflicts
+        and their descendants), no spend of an evicted transaction, no new unconfirmed inputs, a
+        fee covering the evicted fees plus the incremental relay fee for this transaction."""
+        evict = set(conflicts)
+        frontier = list(conflicts)
+        while frontier:
+            t = frontier.pop()
+            for c, e in self.mempool.items():
+                if c not in evict and any(i.prevout.hash == t for i in e.tx.vin):
+                    evict.add(c)
+                    frontier.append(c)
+            if len(evict) > policy.MAX_BIP125_REPLACEMENTS:
+                return "too many potential replacements", set()
+        for t in conflicts:
+            e = self.mempool[t]
+            if fee * max(1, e.size) <= e.fee * vsize:  # new feerate must beat each direct conflict's
+                return "insufficient fee", set()
+        if any(i.prevout.hash in evict for i in tx.vin):
+            return "bad-txns-spends-conflicting-tx", set()
+        old_parents = {i.prevout.hash for t in conflicts for i in self.mempool[t].tx.vin}
+        for i in tx.vin:
+            if i.prevout.hash in self.mempool and i.prevout.hash not in old_parents:
+                return "replacement-adds-unconfirmed", set()
+        evicted_fees = sum(self.mempool[t].fee for t in evict)
+        if fee < evicted_fees:
+            return "insufficient fee", set()
+        if fee - evicted_fees < self.incremental_relay_fee * vsize // 1000:
+            return "insufficient fee", set()
+        return "", evict
 
     def _check_tx_assets(self, tx, raw: bytes, coins, aflags) -> str:
         """The asset part of ATMP: no asset outputs before the deployment, CheckTxAssets against the

@@ -27,7 +27,8 @@ from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
 from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, GpuKawpowBackend, MinerController
-from .rpc import methods, methods_assets, methods_ext, methods_index, methods_messages, methods_util, methods_wallet
+from .rpc import (methods, methods_assets, methods_ext, methods_index, methods_messages, methods_util, methods_wallet,
+                  methods_wallet_ext)
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
 from .utils import log, metrics
 from .utils.config import ArgsManager, gpu_list
@@ -122,6 +123,7 @@ class Node:
                 methods_wallet.rescan(self)
             self.state.register(self.wallet.history)
             methods_wallet.register(self.table, self)
+            methods_wallet_ext.register(self.table, self)
         self.asset_wallet = None
         from .wallet.messages import MessageStore
         from .wallet.rewards import MINIMUM_REWARDS_PAYOUT_HEIGHT, Rewards
@@ -141,6 +143,12 @@ class Node:
         methods_util.register(self.table, self)
         if a.get("minrelaytxfee") is not None:  # -minrelaytxfee=<CLORE per kvB>
             self.state.min_relay_fee = round(float(a.get("minrelaytxfee")) * 100_000_000)
+        if a.get("incrementalrelayfee") is not None:
+            self.state.incremental_relay_fee = round(float(a.get("incrementalrelayfee")) * 100_000_000)
+        self.state.enable_replacement = a.get_bool("mempoolreplacement", self.state.enable_replacement)
+        self.state.require_standard = not a.get_bool("acceptnonstdtxn", not self.state.require_standard)
+        if self.wallet is not None:
+            self.wallet.walletrbf = a.get_bool("walletrbf", False)
         par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free
         cores = os.cpu_count() or 1
         self.state.script_threads = max(1, min(16, cores + par if par <= 0 else par))

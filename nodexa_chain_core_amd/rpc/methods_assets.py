@@ -117,15 +117,31 @@ def register(table, node) -> None:
         return _txids(call(aw().transfer, p[0], _qty(p[1]), p[2], _ipfs(_arg(p, 3)), int(_arg(p, 4, 0)),
                            _arg(p, 6) or None))
 
+    def _from_transfer(name, froms, qty, to, message, expire, clore_change, asset_change):
+        for a in froms:
+            _h160(a)
+        if not aw().unspent(name):
+            raise RPCError(RPC_INVALID_PARAMETER, "Wallet doesn't own the asset_name: " + name)
+        _h160(to)
+        return _txids(call(aw().transfer, name, _qty(qty), to, _ipfs(message), int(expire or 0),
+                           asset_change or None, list(froms), clore_change or None))
+
     def rpc_transferfromaddress(p):
-        """transferfromaddress "asset_name" "from_address" qty "to_address" ... — the wallet's coins of that
-        address (this wallet selects from all of its keys; the from address must be one of them)."""
+        """transferfromaddress "asset_name" "from_address" qty "to_address" "message" expire_time
+        "clore_change_address" "asset_change_address" — only the asset coins held at from_address."""
         if len(p) < 4:
             raise RPCError(RPC_INVALID_PARAMETER, 'transferfromaddress "asset_name" "from_address" qty "to_address"')
-        if _h160(p[1]) not in aw().w.keys:
-            raise RPCError(RPC_INVALID_ADDRESS_OR_KEY, "from_address is not in this wallet")
-        return _txids(call(aw().transfer, p[0], _qty(p[2]), p[3], _ipfs(_arg(p, 4)), int(_arg(p, 5, 0)),
-                           _arg(p, 7) or None))
+        return _from_transfer(p[0], [p[1]], p[2], p[3], _arg(p, 4), _arg(p, 5, 0), _arg(p, 6), _arg(p, 7))
+
+    def rpc_transferfromaddresses(p):
+        """transferfromaddresses "asset_name" ["from_addresses"] qty "to_address" "message" expire_time
+        "clore_change_address" "asset_change_address" (src/rpc/assets.cpp:1271)"""
+        if len(p) < 4:
+            raise RPCError(RPC_INVALID_PARAMETER, 'transferfromaddresses "asset_name" ["from_addresses"] qty '
+                                                  '"to_address"')
+        if not isinstance(p[1], list) or not p[1]:
+            raise RPCError(RPC_INVALID_PARAMETER, "From addresses must be a non-empty array.")
+        return _from_transfer(p[0], p[1], p[2], p[3], _arg(p, 4), _arg(p, 5, 0), _arg(p, 6), _arg(p, 7))
 
     def rpc_listmyassets(p):
         """listmyassets "( asset )" ( verbose ) ( count ) ( start ) ( confs )"""
@@ -316,6 +332,10 @@ def register(table, node) -> None:
         ("assets", "transferfromaddress", rpc_transferfromaddress, ("asset_name", "from_address", "qty", "to_address",
                                                                      "message", "expire_time", "clore_change_address",
                                                                      "asset_change_address")),
+        ("assets", "transferfromaddresses", rpc_transferfromaddresses, ("asset_name", "from_addresses", "qty",
+                                                                         "to_address", "message", "expire_time",
+                                                                         "clore_change_address",
+                                                                         "asset_change_address")),
         ("assets", "transfer", rpc_transfer, ("asset_name", "qty", "to_address", "message", "expire_time",
                                                "change_address", "asset_change_address")),
         ("assets", "reissue", rpc_reissue, ("asset_name", "qty", "to_address", "change_address", "reissuable",

@@ -32,7 +32,22 @@ def rescan(node, start_height: int = 0) -> int:
     history; returns the number of wallet transactions found."""
     st, hist = node.state, node.wallet.history
     n = 0
+    abort = getattr(node, "rescan_abort", None)
+    if abort is not None:
+        abort.clear()
+    node.rescan_running = True
+    try:
+        n = _scan(node, st, hist, start_height, abort)
+    finally:
+        node.rescan_running = False
+    return n
+
+
+def _scan(node, st, hist, start_height: int, abort) -> int:
+    n = 0
     for h in range(max(0, start_height), st.height() + 1):
+        if abort is not None and abort.is_set():  # abortrescan
+            break
         idx = st.chain.at_height(h)
         blk = st.get_block(idx.hash)
         if blk is None:
@@ -87,8 +102,17 @@ def register(table, node) -> None:
         return _wallet_call(wallet().new_address, str(_arg(p, 0, "")))
 
     def rpc_getbalance(p):
-        """getbalance ( "account" minconf ) — spendable (mature) wallet balance."""
-        return wallet().balance(int(_arg(p, 1, 1))) / COIN
+        """getbalance ( "account" minconf include_watchonly ) — spendable (mature) wallet balance; a
+        named account gives that account's balance (accounts = labels)."""
+        w = wallet()
+        minconf = int(_arg(p, 1, 1))
+        acct = _arg(p, 0)
+        if acct is not None and acct != "*":
+            return node.account_balance(str(acct), minconf) / COIN
+        total = w.balance(minconf)
+        if bool(_arg(p, 2, False)):
+            total += w.watch_balance(minconf)
+        return total / COIN
 
     def rpc_getunconfirmedbalance(p):
         """getunconfirmedbalance — wallet outputs in the mempool."""
@@ -100,14 +124,21 @@ def register(table, node) -> None:
         w = wallet()
         want = set(_arg(p, 2, []) or [])
         out = []
-        for u in w.unspent(int(_arg(p, 0, 1)), int(_arg(p, 1, 9_999_999))):
+        for u in w.unspent(int(_arg(p, 0, 1)), int(_arg(p, 1, 9_999_999)), include_watch=True):
             addr = _core.script_to_address(u["scriptPubKey"], params.pubkey_prefix, params.script_prefix)
             if want and addr not in want:
                 continue
-            out.append({"txid": u["txid"][::-1].hex(), "vout": u["vout"], "address": addr,
-                        "scriptPubKey": u["scriptPubKey"].hex(), "amount": u["amount"] / COIN,
-                        "confirmations": u["confirmations"], "spendable": u["spendable"], "solvable": True,
-                        "safe": u["confirmations"] > 0})
+            wo = u["watchonly"]
+            solvable = w.watch[u["scriptPubKey"]]["solvable"] if wo else True
+            e = {"txid": u["txid"][::-1].hex(), "vout": u["vout"], "address": addr,
+                 "scriptPubKey": u["scriptPubKey"].hex(), "amount": u["amount"] / COIN,
+                 "confirmations": u["confirmations"], "spendable": u["spendable"], "solvable": solvable,
+                 "safe": u["confirmations"] > 0}
+            lbl = w.watch[u["scriptPubKey"]]["label"] if wo else (w.labels.get(u["scriptPubKey"][3:23])
+                                                                  if len(u["scriptPubKey"]) == 25 else None)
+            if lbl is not None:
+                e["account"] = lbl
+            out.append(e)
         return out
 
     def rpc_sendtoaddress(p):
@@ -124,7 +155,14 @@ def register(table, node) -> None:
         if len(p) < 2 or not isinstance(p[1], dict) or not p[1]:
             raise RPCError(RPC_INVALID_PARAMETER, 'sendmany "" {"address":amount,...}')
         outs = [(_spk(a), _amount(v)) for a, v in p[1].items()]
-        txid = _wallet_call(wallet().send, outs)
+        subtract = set(_arg(p, 4, []) or [])
+        if subtract and list(p[1])[0] not in subtract:
+            # the wallet subtracts the fee from the first output; move a subtract-from output first
+            first = next(k for k, a in enumerate(p[1]) if a in subtract)
+            outs.insert(0, outs.pop(first))
+        acct = str(p[0]) if p[0] not in (None, "") else None
+        txid = _wallet_call(wallet().send, outs, subtract_fee=bool(subtract), comment=str(_arg(p, 3, "")),
+                            from_account=acct, minconf=int(_arg(p, 2, 1)))
         return txid[::-1].hex()
 
     def rpc_dumpprivkey(p):
@@ -138,6 +176,8 @@ def register(table, node) -> None:
         if not p:
             raise RPCError(RPC_INVALID_PARAMETER, 'importprivkey "privkey" ( "label" rescan )')
         _wallet_call(wallet().import_privkey, p[0], str(_arg(p, 1, "")))
+        if bool(_arg(p, 2, True)):  # the balance is always current; the history needs the rescan
+            rescan(node)
         return None
 
     def rpc_getwalletinfo(p):
@@ -233,7 +273,15 @@ def register(table, node) -> None:
         count, skip = int(_arg(p, 1, 10)), int(_arg(p, 2, 0))
         if count < 0 or skip < 0:
             raise RPCError(RPC_INVALID_PARAMETER, "Negative count" if count < 0 else "Negative from")
-        entries = [e for w in hist().ordered() for e in hist().entries(w)]
+        watch = bool(_arg(p, 3, False))
+        acct = str(_arg(p, 0, "*"))
+        entries = [e for w in hist().ordered() for e in hist().entries(w, watch)]
+        if acct != "*":
+            entries = [e for e in entries if e.get("account", "") == acct]
+        for a, amount, t, other, comment in hist().moves:  # accounting entries ("move")
+            if acct in ("*", a):
+                entries.append({"account": a, "category": "move", "time": t, "amount": amount / COIN,
+                                "otheraccount": other, "comment": comment})
         entries = entries[::-1][skip:skip + count][::-1]
         return entries
 
@@ -256,7 +304,8 @@ def register(table, node) -> None:
         ents = hist().entries(w)
         base = {k: v for k, v in (ents[0] if ents else {}).items()
                 if k in ("confirmations", "blockhash", "blockindex", "blocktime", "txid", "time", "timereceived",
-                         "bip125-replaceable", "walletconflicts", "comment")}
+                         "bip125-replaceable", "walletconflicts", "comment", "to", "replaced_by_txid",
+                         "replaces_txid")}
         if not ents:
             base = {"confirmations": hist().confirmations(w), "txid": p[0], "time": w.time, "timereceived": w.time}
         out.update(base)

@@ -15,6 +15,10 @@ from .wallet import WalletError
 
 _core = core()
 COIN = 100_000_000
+
+
+def p2pkh_of(h160: bytes) -> bytes:
+    return b"\x76\xa9\x14" + h160 + b"\x88\xac"
 OWNER_AMOUNT = COIN
 
 
@@ -85,9 +89,11 @@ class AssetWallet:
             out[u["name"]] = out.get(u["name"], 0) + u["qty"]
         return out
 
-    def _take(self, name: str, qty: int) -> tuple[list[dict], int]:
-        """Asset coins of `name` covering `qty` (largest first) and the change."""
-        coins = sorted(self.unspent(name), key=lambda u: -u["qty"])
+    def _take(self, name: str, qty: int, from_h160s: set | None = None) -> tuple[list[dict], int]:
+        """Asset coins of `name` (held at `from_h160s` when given) covering `qty`, largest first, and
+        the change."""
+        coins = sorted((u for u in self.unspent(name) if from_h160s is None or u["hash160"] in from_h160s),
+                       key=lambda u: -u["qty"])
         chosen, total = [], 0
         for u in coins:
             if total >= qty:
@@ -183,13 +189,24 @@ class AssetWallet:
         return self._send(pre, post, ins)
 
     def transfer(self, name: str, qty: int, to: str, message: bytes = b"", expire: int = 0,
-                 change_to: str | None = None) -> bytes:
+                 change_to: str | None = None, from_addresses: list[str] | None = None,
+                 clore_change_to: str | None = None) -> bytes:
+        """CreateTransferAssetTransaction; `from_addresses` restricts the asset coins
+        (transferfromaddress / transferfromaddresses), the change addresses are optional."""
         self._require_active()
-        ins, change = self._take(name, qty)
+        srcs = None if from_addresses is None else {self._h160(a) for a in from_addresses}
+        ins, change = self._take(name, qty, srcs)
         outs = [_core.TxOut(0, _core.asset_script_transfer(self._h160(to), name, qty, message, expire))]
         if change:
             outs.append(_core.TxOut(0, _core.asset_script_transfer(self._dest(change_to), name, change)))
-        return self._send(outs, [], ins)
+        change_spk = p2pkh_of(self._h160(clore_change_to)) if clore_change_to else None
+        tx, _ = self.w.fund_and_sign(outs, [], list(ins), change_spk=change_spk)
+        ok, reason, _ = self.state.accept_to_mempool(tx)
+        if not ok:
+            raise WalletError(f"Transaction rejected: {reason}")
+        if self.w.history is not None:
+            self.w.history.add(tx)
+        return tx.txid()
 
     def build_transfer_many(self, name: str, dests: list[tuple[bytes, int]]):
         """CreateTransferAssetTransaction with one transfer output per (hash160, qty): the signed

@@ -23,13 +23,18 @@ COIN = 100_000_000
 
 
 class WalletTx:
-    __slots__ = ("tx", "time", "block", "abandoned", "comment", "order")
+    __slots__ = ("tx", "time", "block", "abandoned", "comment", "order", "comment_to", "from_account",
+                 "replaced_by", "replaces")
 
     def __init__(self, tx, t: int, block: bytes | None = None, order: int = 0):
         self.tx, self.time, self.block = tx, t, block
         self.abandoned = False
         self.comment = ""
         self.order = order  # nOrderPos: insertion order
+        self.comment_to = ""
+        self.from_account = None  # strFromAccount (sendfrom)
+        self.replaced_by = None   # bumpfee bookkeeping (mapValue "replaced_by_txid" / "replaces_txid")
+        self.replaces = None
 
 
 class WalletHistory(ValidationInterface):
@@ -40,6 +45,7 @@ class WalletHistory(ValidationInterface):
         self.lock = threading.RLock()
         self.txs: dict[bytes, WalletTx] = {}
         self.locked: set[tuple[bytes, int]] = set()  # lockunspent
+        self.moves: list[tuple] = []  # CAccountingEntry: (account, amount, time, other_account, comment)
         if path and os.path.exists(path):
             self._load()
 
@@ -53,7 +59,12 @@ class WalletHistory(ValidationInterface):
             wtx.abandoned = e.get("abandoned", False)
             wtx.comment = e.get("comment", "")
             wtx.order = e.get("order", len(self.txs))
+            wtx.comment_to = e.get("comment_to", "")
+            wtx.from_account = e.get("from_account")
+            wtx.replaced_by = bytes.fromhex(e["replaced_by"]) if e.get("replaced_by") else None
+            wtx.replaces = bytes.fromhex(e["replaces"]) if e.get("replaces") else None
             self.txs[bytes.fromhex(h)] = wtx
+        self.moves = [tuple(m) for m in d.get("moves", [])]
 
     def save(self) -> None:
         if not self.path:
@@ -61,24 +72,48 @@ class WalletHistory(ValidationInterface):
         with self.lock:
             d = {"txs": {h.hex(): {"hex": w.tx.serialize(True).hex(), "time": w.time,
                                    "block": w.block.hex() if w.block else None, "abandoned": w.abandoned,
-                                   "comment": w.comment, "order": w.order} for h, w in self.txs.items()}}
+                                   "comment": w.comment, "order": w.order, "comment_to": w.comment_to,
+                                   "from_account": w.from_account,
+                                   "replaced_by": w.replaced_by.hex() if w.replaced_by else None,
+                                   "replaces": w.replaces.hex() if w.replaces else None}
+                         for h, w in self.txs.items()},
+                 "moves": self.moves}
         tmp = self.path + ".new"
         with open(tmp, "w") as f:
             json.dump(d, f)
         os.replace(tmp, self.path)
 
     # ------------------------------------------------------------------ involvement
-    def _output_mine(self, prevout) -> tuple[int, bytes] | None:
+    def _ours(self, spk: bytes, watch: bool) -> bool:
+        return self.w.is_mine(spk) or (watch and self.w.is_watch(spk))
+
+    def _output_mine(self, prevout, watch: bool = False) -> tuple[int, bytes] | None:
         w = self.txs.get(prevout.hash)
         if w is None or prevout.n >= len(w.tx.vout):
             return None
         o = w.tx.vout[prevout.n]
-        return (o.value, o.script_pubkey) if self.w.is_mine(o.script_pubkey) else None
+        return (o.value, o.script_pubkey) if self._ours(o.script_pubkey, watch) else None
 
     def involves_me(self, tx) -> bool:
-        if any(self.w.is_mine(o.script_pubkey) for o in tx.vout):
+        """IsMine(ISMINE_ALL) of an output or of a spent wallet output (watch-only included)."""
+        if any(self._ours(o.script_pubkey, True) for o in tx.vout):
             return True
-        return not tx.is_coinbase() and any(self._output_mine(i.prevout) for i in tx.vin)
+        return not tx.is_coinbase() and any(self._output_mine(i.prevout, True) for i in tx.vin)
+
+    def involves_watch(self, w: "WalletTx") -> bool:
+        tx = w.tx
+        if any(self.w.is_watch(o.script_pubkey) for o in tx.vout):
+            return True
+        return not tx.is_coinbase() and any(
+            (m := self._output_mine(i.prevout, True)) is not None and self.w.is_watch(m[1]) for i in tx.vin)
+
+    def remove(self, txid: bytes) -> bool:
+        """removeprunedfunds: forget a wallet transaction."""
+        with self.lock:
+            found = self.txs.pop(txid, None) is not None
+        if found:
+            self.save()
+        return found
 
     def add(self, tx, block: bytes | None = None, save: bool = True) -> bool:
         txid = tx.txid()
@@ -116,13 +151,13 @@ class WalletHistory(ValidationInterface):
             return 0
         return st.height() - idx.height + 1
 
-    def debit(self, w: WalletTx) -> int:
+    def debit(self, w: WalletTx, watch: bool = False) -> int:
         if w.tx.is_coinbase():
             return 0
-        return sum(m[0] for i in w.tx.vin if (m := self._output_mine(i.prevout)) is not None)
+        return sum(m[0] for i in w.tx.vin if (m := self._output_mine(i.prevout, watch)) is not None)
 
-    def credit(self, w: WalletTx) -> int:
-        return sum(o.value for o in w.tx.vout if self.w.is_mine(o.script_pubkey))
+    def credit(self, w: WalletTx, watch: bool = False) -> int:
+        return sum(o.value for o in w.tx.vout if self._ours(o.script_pubkey, watch))
 
     def fee(self, w: WalletTx) -> int | None:
         """Only known when every input is ours (the reference reports fee for fully-from-me txs)."""
@@ -137,11 +172,21 @@ class WalletHistory(ValidationInterface):
         p = self.w.params
         return _core.script_to_address(spk, p.pubkey_prefix, p.script_prefix) or None
 
-    def entries(self, w: WalletTx) -> list[dict]:
-        """ListTransactions entries of one wallet transaction (sends, then receives)."""
+    def entries(self, w: WalletTx, watch: bool = False) -> list[dict]:
+        """ListTransactions entries of one wallet transaction (sends, then receives); watch-only
+        outputs count when `watch` (include_watchonly) and are flagged involvesWatchonly."""
         conf = self.confirmations(w)
+        rbf = "no"
+        if conf <= 0:
+            rbf = "yes" if any(i.sequence <= 0xfffffffd for i in w.tx.vin) else "unknown" if conf < 0 else "no"
         base = {"confirmations": conf, "txid": w.tx.txid()[::-1].hex(), "time": w.time, "timereceived": w.time,
-                "bip125-replaceable": "no", "walletconflicts": []}
+                "bip125-replaceable": rbf, "walletconflicts": []}
+        if w.replaced_by:
+            base["replaced_by_txid"] = w.replaced_by[::-1].hex()
+        if w.replaces:
+            base["replaces_txid"] = w.replaces[::-1].hex()
+        if w.comment_to:
+            base["to"] = w.comment_to
         if w.block is not None:
             idx = self.state.chain.find(w.block)
             if idx is not None:
@@ -153,16 +198,19 @@ class WalletHistory(ValidationInterface):
         if w.comment:
             base["comment"] = w.comment
         out = []
-        debit = self.debit(w)
+        debit = self.debit(w, watch)
         fee = self.fee(w)
         sends, receives = [], []
         for n, o in enumerate(w.tx.vout):  # GetAmounts: change (mine, no address-book label) is skipped
-            mine = self.w.is_mine(o.script_pubkey)
+            mine = self._ours(o.script_pubkey, watch)
+            wo = mine and self.w.is_watch(o.script_pubkey)
             if debit > 0:
                 if mine and self._is_change(o.script_pubkey):
                     continue
-                e = {"account": "", "address": self._address(o.script_pubkey), "category": "send",
+                e = {"account": w.from_account or "", "address": self._address(o.script_pubkey), "category": "send",
                      "amount": -o.value / COIN, "vout": n, "fee": -(fee or 0) / COIN, "abandoned": w.abandoned}
+                if wo:
+                    e["involvesWatchonly"] = True
                 e.update(base)
                 sends.append(e)
             if mine:
@@ -171,6 +219,8 @@ class WalletHistory(ValidationInterface):
                     cat = "orphan" if conf <= 0 else ("immature" if conf <= _core.COINBASE_MATURITY else "generate")
                 e = {"account": self._label(o.script_pubkey), "address": self._address(o.script_pubkey),
                      "category": cat, "amount": o.value / COIN, "vout": n}
+                if wo:
+                    e["involvesWatchonly"] = True
                 e.update(base)
                 receives.append(e)
         out = sends + receives
@@ -180,13 +230,15 @@ class WalletHistory(ValidationInterface):
         return len(spk) == 25 and self.w.labels.get(spk[3:23]) == "change"
 
     def _label(self, spk: bytes) -> str:
+        if spk in self.w.watch:
+            return self.w.watch[spk].get("label", "")
         return self.w.labels.get(spk[3:23], "") if len(spk) == 25 else ""
 
     def ordered(self) -> list[WalletTx]:
         with self.lock:
             return sorted(self.txs.values(), key=lambda w: w.order)
 
-    def received_by(self, minconf: int = 1) -> dict[bytes, tuple[int, int, list[str]]]:
+    def received_by(self, minconf: int = 1, watch: bool = False) -> dict[bytes, tuple[int, int, list[str]]]:
         """scriptPubKey -> (amount, min confirmations, txids) over non-coinbase wallet txs."""
         out: dict[bytes, list] = {}
         for w in self.ordered():
@@ -196,7 +248,7 @@ class WalletHistory(ValidationInterface):
             if conf < minconf:
                 continue
             for o in w.tx.vout:
-                if self.w.is_mine(o.script_pubkey):
+                if self._ours(o.script_pubkey, watch):
                     e = out.setdefault(o.script_pubkey, [0, 1 << 30, []])
                     e[0] += o.value
                     e[1] = min(e[1], conf)

@@ -32,6 +32,8 @@ DEFAULT_KEYPOOL_SIZE = 100
 DEFAULT_DERIVE_ROUNDS = 25000  # CMasterKey nDeriveIterations default
 UNLOCK_NEEDED = "Error: Please enter the wallet passphrase with walletpassphrase first."
 HARDENED = 0x80000000
+WALLET_INCREMENTAL_RELAY_FEE = 5000  # sat per kB (src/wallet/wallet.h:59)
+DUST_THRESHOLD = 546  # GetDustThreshold of a P2PKH output at DUST_RELAY_TX_FEE (chain/policy.py)
 # nExtCoinType (src/chainparams.cpp:196, 355, 522): the BIP44 coin_type level
 EXT_COIN_TYPE = {"main": 1313, "test": 1, "regtest": 1}
 # base58Prefixes[EXT_SECRET_KEY] (src/chainparams.cpp:193, 352, 519)
@@ -132,6 +134,8 @@ class Wallet:
         self.created: dict[bytes, int] = {}
         self._p2sh_wpkh: dict[bytes, bytes] = {}  # hash160(0x0014 || h) -> h
         self.redeem_scripts: dict[bytes, bytes] = {}  # hash160(script) -> script (addmultisigaddress)
+        self.watch: dict[bytes, dict] = {}  # watch-only scriptPubKey -> {"label", "solvable"} (importaddress)
+        self.walletrbf = False  # -walletrbf: sends signal BIP125 replaceability (DEFAULT_WALLET_RBF)
         self.history = None    # wallet/history.WalletHistory, attached by the node
         self.fee_rate = DEFAULT_FEE_RATE  # settxfee
         self.hdpath: dict[bytes, str] = {}      # hdkeypath of derived keys
@@ -182,6 +186,8 @@ class Wallet:
         for rs in data.get("redeem_scripts", []):
             script = bytes.fromhex(rs)
             self.redeem_scripts[_core.hash160(script)] = script
+        for wo in data.get("watch", []):
+            self.watch[bytes.fromhex(wo["spk"])] = {"label": wo.get("label", ""), "solvable": wo.get("solvable", False)}
 
     def _save(self) -> None:
         if not self.path:
@@ -199,7 +205,8 @@ class Wallet:
                 e["pool"] = True
             keys.append(e)
         data = {"version": 2, "network": self.params.network_id, "keys": keys,
-                "redeem_scripts": [rs.hex() for rs in self.redeem_scripts.values()]}
+                "redeem_scripts": [rs.hex() for rs in self.redeem_scripts.values()],
+                "watch": [{"spk": k.hex(), **v} for k, v in self.watch.items()]}
         if self.hd is not None:
             plain = self.mkey is None
             data["hd"] = {"master_id": self.hd["master_id"].hex(), "next": self.hd["next"],
@@ -472,6 +479,20 @@ class Wallet:
     def is_mine(self, spk: bytes) -> bool:
         return self._key_for(spk) is not None
 
+    def is_watch(self, spk: bytes) -> bool:
+        """ISMINE_WATCH_ONLY: an imported script (or an asset output paying one) without a key."""
+        if spk in self.watch:
+            return not self.is_mine(spk)
+        return len(spk) > 31 and spk[25] == 0xC0 and spk[:25] in self.watch and not self.is_mine(spk)
+
+    def add_watch(self, spk: bytes, label: str = "", solvable: bool = False) -> None:
+        """AddWatchOnly (importaddress / importpubkey / importmulti)."""
+        with self.lock:
+            if self.is_mine(spk):
+                raise WalletError("The wallet already contains the private key for this address or script")
+            self.watch[spk] = {"label": label, "solvable": solvable or self.watch.get(spk, {}).get("solvable", False)}
+            self._save()
+
     def _key_for(self, spk: bytes):
         """(secret, pubkey, kind) for a scriptPubKey the wallet can sign, else None."""
         if len(spk) > 31 and spk[25] == 0xC0 and _core.parse_asset_script(spk) is not None:
@@ -494,11 +515,18 @@ class Wallet:
         return None
 
     # ------------------------------------------------------------------ coins
-    def unspent(self, minconf: int = 1, maxconf: int = 9_999_999) -> list[dict]:
+    def unspent(self, minconf: int = 1, maxconf: int = 9_999_999, include_watch: bool = False) -> list[dict]:
+        """AvailableCoins: wallet outputs in the UTXO set (and, for minconf 0, the pool) that the
+        pool does not spend and lockunspent has not locked. Watch-only outputs (include_watch) come
+        back with spendable False and watchonly True."""
         st = self.state
         with st.lock:
             tip = st.coins_tip().height
             scripts = self.scripts()
+            watch = set()
+            if include_watch:
+                watch = {spk for spk in self.watch if spk not in set(scripts)}
+                scripts = scripts + sorted(watch)
             pool_spent = {(i.prevout.hash, i.prevout.n) for e in st.mempool.values() for i in e.tx.vin}
             locked = self.history.locked if self.history is not None else set()
             out = []
@@ -508,22 +536,29 @@ class Wallet:
                     continue
                 # CWalletTx::GetBlocksToMaturity: a coinbase needs COINBASE_MATURITY + 1 confirmations
                 mature = not coinbase or conf > _core.COINBASE_MATURITY
+                wo = spk in watch
                 out.append({"txid": txid, "vout": n, "amount": value, "scriptPubKey": spk,
-                            "confirmations": conf, "spendable": mature, "coinbase": coinbase})
+                            "confirmations": conf, "spendable": mature and not wo, "coinbase": coinbase,
+                            "watchonly": wo, "mature": mature})
             if minconf <= 0:
                 mine = set(scripts)
                 for txid, e in st.mempool.items():
                     for n, o in enumerate(e.tx.vout):
                         if o.script_pubkey in mine and (txid, n) not in pool_spent:
+                            wo = o.script_pubkey in watch
                             out.append({"txid": txid, "vout": n, "amount": o.value, "scriptPubKey": o.script_pubkey,
-                                        "confirmations": 0, "spendable": True, "coinbase": False})
+                                        "confirmations": 0, "spendable": not wo, "coinbase": False,
+                                        "watchonly": wo, "mature": True})
             return out
+
+    def watch_balance(self, minconf: int = 1) -> int:
+        return sum(u["amount"] for u in self.unspent(minconf, include_watch=True) if u["watchonly"] and u["mature"])
 
     def balance(self, minconf: int = 1) -> int:
         return sum(u["amount"] for u in self.unspent(minconf) if u["spendable"])
 
     def immature_balance(self) -> int:
-        return sum(u["amount"] for u in self.unspent(1) if not u["spendable"])
+        return sum(u["amount"] for u in self.unspent(1) if not u["mature"])
 
     # ------------------------------------------------------------------ signing
     def sign(self, tx, prevouts: dict[tuple[bytes, int], tuple[bytes, int]], extra_keys: list[bytes] = (),
@@ -674,14 +709,18 @@ class Wallet:
         raise WalletError("Transaction fee did not converge")
 
     def create_transaction(self, outputs: list[tuple[bytes, int]], fee_rate: int = DEFAULT_FEE_RATE,
-                           subtract_fee: bool = False, minconf: int = 1):
-        """CreateTransaction: largest-first coin selection over spendable wallet outputs, a change
-        output to a fresh key, fee = fee_rate per kvB of the signed size. Returns (tx, fee)."""
+                           subtract_fee: bool = False, minconf: int = 1, replaceable: bool | None = None,
+                           from_scripts: set | None = None, change_spk: bytes | None = None):
+        """CreateTransaction: largest-first coin selection over spendable wallet outputs (only those
+        paying `from_scripts` when given: sendfromaddress), a change output to a fresh key (or
+        `change_spk`), fee = fee_rate per kvB of the signed size; inputs signal BIP125 when
+        `replaceable` (default -walletrbf). Returns (tx, fee)."""
         if not outputs or any(v <= 0 for _, v in outputs):
             raise WalletError("Invalid amount")
         target = sum(v for _, v in outputs)
-        coins = sorted((u for u in self.unspent(minconf) if u["spendable"]), key=lambda u: -u["amount"])
-        change_spk = None
+        coins = sorted((u for u in self.unspent(minconf) if u["spendable"]
+                        and (from_scripts is None or u["scriptPubKey"] in from_scripts)), key=lambda u: -u["amount"])
+        seq = 0xfffffffd if (self.walletrbf if replaceable is None else replaceable) else 0xfffffffe
         fee = 0
         for _ in range(20):  # fee depends on the size, size on the inputs chosen
             need = target + (0 if subtract_fee else fee)
@@ -701,7 +740,7 @@ class Wallet:
                 op = _core.OutPoint()
                 op.hash, op.n = u["txid"], u["vout"]
                 vin.prevout = op
-                vin.sequence = 0xfffffffe
+                vin.sequence = seq
                 vins.append(vin)
             tx.vin = vins
             outs = [_core.TxOut(v, s) for s, v in outputs]
@@ -729,15 +768,92 @@ class Wallet:
             fee = want_fee + 68  # headroom for a changed signature size
         raise WalletError("Transaction fee did not converge")
 
-    def send(self, outputs: list[tuple[bytes, int]], subtract_fee: bool = False, comment: str = "") -> bytes:
-        tx, _ = self.create_transaction(outputs, fee_rate=self.fee_rate, subtract_fee=subtract_fee)
+    def send(self, outputs: list[tuple[bytes, int]], subtract_fee: bool = False, comment: str = "",
+             replaceable: bool | None = None, from_scripts: set | None = None, change_spk: bytes | None = None,
+             comment_to: str = "", from_account: str | None = None, minconf: int = 1) -> bytes:
+        """SendMoney / CommitTransaction: build, submit to the pool, record in the history."""
+        tx, _ = self.create_transaction(outputs, fee_rate=self.fee_rate, subtract_fee=subtract_fee, minconf=minconf,
+                                        replaceable=replaceable, from_scripts=from_scripts, change_spk=change_spk)
+        return self.commit(tx, comment, comment_to, from_account)
+
+    def commit(self, tx, comment: str = "", comment_to: str = "", from_account: str | None = None) -> bytes:
         ok, reason, _ = self.state.accept_to_mempool(tx)
         if not ok:
             raise WalletError(f"Transaction rejected: {reason}")
         if self.history is not None:
             self.history.add(tx)
             w = self.history.txs.get(tx.txid())
-            if w is not None and comment:
+            if w is not None and (comment or comment_to or from_account is not None):
                 w.comment = comment
+                w.comment_to = comment_to
+                w.from_account = from_account
                 self.history.save()
         return tx.txid()
+
+    # ------------------------------------------------------------------ fee bumping (src/wallet/feebumper.cpp)
+    def bump_fee(self, txid: bytes, total_fee: int | None = None, replaceable: bool = True) -> tuple[bytes, int, int]:
+        """CFeeBumper: a replacement of an opted-in wallet transaction in the pool, paying the extra
+        fee out of its change output. Returns (new txid, old fee, new fee)."""
+        st = self.state
+        with st.lock, self.lock:
+            e = st.mempool.get(txid)
+            if e is None:
+                raise WalletError("Transaction is not in the mempool" if self.history is None or
+                                  txid not in self.history.txs else "Transaction has been mined, or is conflicted "
+                                  "with a mined transaction")
+            tx = e.tx
+            if any(i.prevout.hash == txid for x in st.mempool.values() for i in x.tx.vin):
+                raise WalletError("Transaction has descendants in the wallet")
+            if not any(i.sequence < 0xfffffffe for i in tx.vin):
+                raise WalletError("Transaction is not BIP 125 replaceable")
+            coins = []
+            for i in tx.vin:
+                c = st._spent_coin(i.prevout)
+                if c is None or not self.is_mine(c[1]):
+                    raise WalletError("Transaction contains inputs that don't belong to this wallet")
+                coins.append(c)
+            change = [k for k, o in enumerate(tx.vout) if self.is_mine(o.script_pubkey)
+                      and self.labels.get(o.script_pubkey[3:23] if len(o.script_pubkey) == 25 else b"") == "change"]
+            if len(change) != 1:
+                raise WalletError("Transaction does not have a change output")
+            old_fee = sum(c[0] for c in coins) - tx.value_out()
+            size = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4 + 2  # room for a longer sig
+            old_rate = old_fee * 1000 // size
+            if total_fee is not None:
+                min_total = old_rate * size // 1000 + st.incremental_relay_fee * size // 1000
+                if total_fee < min_total:
+                    raise WalletError(f"Insufficient totalFee, must be at least {min_total / COIN:.8f}")
+                new_fee = total_fee
+            else:
+                rate = max(self.fee_rate, old_rate + 1 + max(WALLET_INCREMENTAL_RELAY_FEE, st.incremental_relay_fee))
+                new_fee = rate * size // 1000
+            k = change[0]
+            ch = tx.vout[k]
+            left = ch.value - (new_fee - old_fee)
+            outs = list(tx.vout)
+            if left < 0:
+                raise WalletError("Change output is too small to bump the fee")
+            if left < DUST_THRESHOLD:  # the whole change goes to the fee
+                new_fee += left
+                del outs[k]
+            else:
+                outs[k] = _core.TxOut(left, ch.script_pubkey)
+            new = _core.Transaction()
+            new.version, new.lock_time = tx.version, tx.lock_time
+            vins = []
+            for i in tx.vin:
+                v = _core.TxIn()
+                v.prevout = i.prevout
+                v.sequence = 0xfffffffd if replaceable else 0xfffffffe
+                vins.append(v)
+            new.vin, new.vout = vins, outs
+            prevs = {(i.prevout.hash, i.prevout.n): (c[1], c[0]) for i, c in zip(tx.vin, coins)}
+            new, complete, errors = self._sign(new, prevs, (), SIGHASH_ALL)
+            if not complete:
+                raise WalletError(f"Can't sign transaction: {errors}")
+            new_id = self.commit(new)
+            if self.history is not None and txid in self.history.txs:
+                self.history.txs[txid].replaced_by = new_id
+                self.history.txs[new_id].replaces = txid
+                self.history.save()
+            return new_id, old_fee, new_fee

@@ -233,6 +233,19 @@ def test_rewards_snapshot_and_distribution(core, tmp_path):
         assert c.getdistributestatus("STOCK1", h, "PAYOUT", 20000, owner)["Status"] == 5
         with pytest.raises(RuntimeError, match="ownership token"):
             c.distributereward("STOCK1", h, "STOCK1/NOPE", 1, owner)
+        # transferfromaddresses: only the listed addresses' coins are spent
+        before = c.listaddressesbyasset("PAYOUT")
+        c.transferfromaddresses("PAYOUT", [sh0], 2, sh2, "", 0, "", sh0)
+        c.generatetoaddress(1, w)
+        after = c.listaddressesbyasset("PAYOUT")
+        assert after.get(sh0, 0) == before[sh0] - 2 and after[sh2] == before[sh2] + 2
+        assert sum(after.values()) == sum(before.values())
+        assert {a: v for a, v in after.items() if a not in (sh0, sh2)} == \
+            {a: v for a, v in before.items() if a not in (sh0, sh2)}
+        with pytest.raises(RuntimeError, match="Insufficient asset funds"):
+            c.transferfromaddress("PAYOUT", sh1, 100, sh2)
+        with pytest.raises(RuntimeError, match="non-empty array"):
+            c.transferfromaddresses("PAYOUT", [], 1, sh2)
         assert c.purgesnapshot("STOCK1", h) == {"name": "STOCK1", "height": h}
         assert c.getsnapshot("STOCK1", h) is None
     finally:
