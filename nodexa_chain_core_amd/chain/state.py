@@ -107,6 +107,7 @@ DEFAULT_MIN_RELAY_TX_FEE = 1_000_000   # sat per kvB (src/validation.h:69)
 DEFAULT_INCREMENTAL_RELAY_FEE = 1000   # sat per kvB (src/policy/policy.h:36)
 DEFAULT_ENABLE_REPLACEMENT = False     # -mempoolreplacement (src/validation.h:163)
 MAX_STANDARD_TX_WEIGHT = 400_000       # src/policy/policy.h:28
+MAX_FEE_ESTIMATION_TIP_AGE = 3 * 60 * 60  # src/validation.h (IsCurrentForFeeEstimation)
 MAX_STANDARD_SCRIPTSIG_SIZE = 1650
 GPU_SIG_BATCH_MIN = 16                 # below this many signatures a block is checked on the host
 
@@ -146,7 +147,7 @@ class ChainState:
         self.mempool: dict[bytes, MempoolEntry] = {}
         self.ntx: dict[bytes, int] = {}      # transactions per stored block (CBlockIndex::nTx)
         self._chain_tx: dict[bytes, int] = {}  # memo of chain_tx_count
-        self.fee_stats: list[tuple[float, int]] = []  # (sat/vB, blocks to confirm) of mined pool txs
+        self.fee_estimator = _core.FeeEstimator()  # CBlockPolicyEstimator (csrc/chain/fees.cpp)
         self.mocktime = 0                     # setmocktime (0 = wall clock)
         self.block_version_override: int | None = None  # -blockversion (regtest only)
         self.transactions_updated = 0
@@ -340,21 +341,65 @@ class ChainState:
         return n
 
     # ------------------------------------------------------------------ mempool-lite
-    def add_to_mempool(self, tx, fee: int, entry_time: float | None = None, fee_delta: int = 0) -> bytes:
+    def add_to_mempool(self, tx, fee: int, entry_time: float | None = None, fee_delta: int = 0,
+                       replacement: bool = False) -> bytes:
         txid = tx.txid()
         with self.lock:
             new = txid not in self.mempool
-            self.mempool[txid] = MempoolEntry(tx, int(fee) + int(fee_delta), entry_time or time.time(),
-                                              self.chain.height(), int(fee_delta), len(tx.serialize(True)))
+            e = MempoolEntry(tx, int(fee) + int(fee_delta), entry_time or time.time(),
+                             self.chain.height(), int(fee_delta), len(tx.serialize(True)))
+            if new:
+                # processTransaction: fee estimates only learn from a node that is current, and not
+                # from replacements or children of pool transactions (validFeeEstimate)
+                valid = (not replacement and self.is_current_for_fee_estimation()
+                         and not any(i.prevout.hash in self.mempool for i in tx.vin))
+                tip = self.coins_tip()
+                self.fee_estimator.process_tx(txid, tip.height, int(fee), e.vsize(), valid)
+            self.mempool[txid] = e
             self.transactions_updated += 1
         if new:
             self._emit("transaction_added_to_mempool", tx)  # TransactionAddedToMempool: P2P relay, ZMQ
         return txid
 
+    def pool_remove(self, txid: bytes, in_block: bool = False) -> None:
+        """removeUnchecked: drop a pool entry and stop tracking it for fee estimation (an entry
+        that leaves unconfirmed counts as a failure at its feerate)."""
+        if self.mempool.pop(txid, None) is not None:
+            self.fee_estimator.remove_tx(txid, in_block)
+
+    def is_current_for_fee_estimation(self) -> bool:
+        """IsCurrentForFeeEstimation (src/validation.cpp): the tip is under 3 hours old and
+        within one block of the best header."""
+        tip = self.coins_tip()
+        if tip is None or tip.time < self.adjusted_time() - MAX_FEE_ESTIMATION_TIP_AGE:
+            return False
+        return tip.height >= self.chain.height() - 1
+
+    def save_fee_estimates(self, path: str) -> None:
+        """Shutdown: FlushUnconfirmed (every tracked pool entry counts as unconfirmed), then
+        fee_estimates.dat in the reference's format, written to path.new and renamed."""
+        self.fee_estimator.flush_unconfirmed()
+        tmp = path + ".new"
+        with open(tmp, "wb") as f:
+            f.write(self.fee_estimator.serialize())
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+
+    def load_fee_estimates(self, path: str) -> bool:
+        if not os.path.exists(path):
+            return False
+        with open(path, "rb") as f:
+            ok, err = self.fee_estimator.deserialize(f.read())
+        if not ok:
+            log.log_printf(f"CBlockPolicyEstimator::Read(): unable to read policy estimator data (non-fatal): {err}")
+        return ok
+
     def clear_mempool(self) -> int:
         with self.lock:
             n = len(self.mempool)
-            self.mempool.clear()
+            for t in list(self.mempool):
+                self.pool_remove(t)
             self.transactions_updated += 1
         return n
 
@@ -427,21 +472,10 @@ class ChainState:
         return n
 
     def record_confirmations(self, block, height: int) -> None:
-        """Fee-estimator input (CBlockPolicyEstimator::processBlock, simplified): the feerate of
-        every pool tx the block confirms and how many blocks it waited."""
-        for tx in block.vtx[1:]:
-            e = self.mempool.get(tx.txid())
-            if e is not None:
-                self.fee_stats.append((e.fee / max(1, e.vsize()), max(1, height - e.height)))
-        del self.fee_stats[:-10000]
-
-    def estimate_fee(self, target: int) -> float | None:
-        """Median feerate (sat/vB) of recently mined pool txs confirmed within `target`
-        blocks, or None with fewer than 10 samples (the reference's 'insufficient data')."""
-        xs = sorted(f for f, waited in self.fee_stats if waited <= target)
-        if len(xs) < 10:
-            return None
-        return xs[len(xs) // 2]
+        """removeForBlock -> CBlockPolicyEstimator::processBlock: the block's pool transactions
+        are recorded at the number of blocks they waited; blocks at or below the best height the
+        estimator has seen (reorgs, side chains) are ignored."""
+        self.fee_estimator.process_block(height, [tx.txid() for tx in block.vtx[1:]])
 
     # ------------------------------------------------------------------ ProcessNewBlock
     def check_block_header(self, header) -> ValidationState:
@@ -724,7 +758,7 @@ class ChainState:
         for txid in list(self.mempool):
             e = self.mempool[txid]
             if txid in confirmed or any((i.prevout.hash, i.prevout.n) in spent for i in e.tx.vin):
-                del self.mempool[txid]
+                self.pool_remove(txid, txid in confirmed)
         for blk in reversed(disconnected):
             for tx in blk.vtx[1:]:
                 self.accept_to_mempool(tx)
@@ -736,7 +770,7 @@ class ChainState:
                 e = self.mempool[txid]
                 for i in e.tx.vin:
                     if self.coins.get(i.prevout.hash, i.prevout.n) is None and i.prevout.hash not in self.mempool:
-                        del self.mempool[txid]
+                        self.pool_remove(txid)
                         changed = True
                         break
         self.transactions_updated += 1
@@ -834,8 +868,8 @@ class ChainState:
                     return False, f"{kind} ({err})", fee
             if not test_only:
                 for t in replaced:  # BIP125: the replaced transactions and their descendants leave
-                    self.mempool.pop(t, None)
-                self.add_to_mempool(tx, fee)
+                    self.pool_remove(t)
+                self.add_to_mempool(tx, fee, replacement=bool(replaced))
             return True, "", fee
 
     def _check_replacement(self, tx, fee: int, vsize: int, conflicts: set) -> tuple[str, set]:

@@ -29,6 +29,7 @@ std::string as_str(const py::bytes& b) { return std::string(b); }
 void bind_extra(py::module_& m);  // bind_extra.cpp: chain, X16R, Equihash
 void bind_script(py::module_& m);  // bind_script.cpp: secp256k1, script interpreter
 void bind_assets(py::module_& m);  // bind_assets.cpp: asset layer
+void bind_fees(py::module_& m);    // bind_fees.cpp: fee estimator
 
 PYBIND11_MODULE(_core, m) {
     m.doc() = "nodexa native CPU core: crypto, ethash/KawPow golden model, Equihash, consensus";
@@ -171,4 +172,5 @@ PYBIND11_MODULE(_core, m) {
     bind_assets(m);  // first: AssetFlags is a default argument of later bindings
     bind_extra(m);
     bind_script(m);
+    bind_fees(m);
 }

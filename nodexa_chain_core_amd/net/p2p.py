@@ -32,6 +32,7 @@ from . import protocol as P
 from .addrman import AddrMan, load_banlist, save_banlist
 from .bloom import MAX_SCRIPT_ELEMENT_SIZE, BloomFilter, merkle_block
 from .compact import (CompactBlock, blocktxn_payload, getblocktxn_payload, parse_blocktxn, parse_getblocktxn)
+from .netbase import ProxyTable
 
 _core = core()
 DEFAULT_MISBEHAVING_BANTIME = 60 * 60 * 24  # -bantime (src/net.h)
@@ -180,6 +181,8 @@ class ConnectionManager:
             self.banned.update(load_banlist(self.banlist_path))
         self.connect_only = connect_only
         self.max_outbound = max_outbound
+        self.proxies = ProxyTable()          # -proxy / -onion / -onlynet (netbase SetProxy / SetLimited)
+        self.local_addrs: dict[tuple[str, int], int] = {}  # AddLocal: (host, port) -> score
 
     # ---------------------------------------------------------------- lifecycle
     def next_id(self) -> int:
@@ -233,9 +236,18 @@ class ConnectionManager:
     def connect(self, host: str, port: int, timeout: float = 10.0) -> Peer:
         if not self.network_active:
             raise ConnectionError("network is disabled (setnetworkactive false)")
-        sock = socket.create_connection((host, port), timeout=timeout)
+        sock = self.proxies.connect(host, port, timeout=timeout)  # direct, or SOCKS5 through the net's proxy
         sock.settimeout(None)
         return self._add(sock, (host, port), inbound=False)
+
+    def add_local(self, host: str, port: int, score: int = 1) -> None:
+        """AddLocal (src/net.cpp): an address this node is reachable at, e.g. its onion service."""
+        with self._lock:
+            self.local_addrs[(host, port)] = max(score, self.local_addrs.get((host, port), 0))
+
+    def remove_local(self, host: str, port: int) -> None:
+        with self._lock:
+            self.local_addrs.pop((host, port), None)
 
     def _add(self, sock, addr, inbound: bool) -> Peer:
         sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)

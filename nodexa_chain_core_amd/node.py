@@ -149,10 +149,18 @@ class Node:
         self.state.require_standard = not a.get_bool("acceptnonstdtxn", not self.state.require_standard)
         if self.wallet is not None:
             self.wallet.walletrbf = a.get_bool("walletrbf", False)
+            w = self.wallet  # -paytxfee / -fallbackfee / -txconfirmtarget (amounts in CLORE per kB)
+            if a.get("paytxfee") is not None:
+                w.pay_tx_fee = round(float(a.get("paytxfee")) * 100_000_000)
+            if a.get("fallbackfee") is not None:
+                w.fallback_fee = round(float(a.get("fallbackfee")) * 100_000_000)
+            w.tx_confirm_target = a.get_int("txconfirmtarget", w.tx_confirm_target)
         par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free
         cores = os.cpu_count() or 1
         self.state.script_threads = max(1, min(16, cores + par if par <= 0 else par))
         self.state.gpu_signatures = a.get("gpusigs", "auto")  # -gpusigs=auto|on|off: GPU batch ECDSA in blocks
+        if self.datadir is not None:  # fee_estimates.dat (src/init.cpp: est_filein), before the mempool
+            self.state.load_fee_estimates(os.path.join(self.datadir, "fee_estimates.dat"))
         if self.datadir is not None and a.get_bool("persistmempool", True):  # -persistmempool (LoadMempool)
             n = self.state.load_mempool(os.path.join(self.datadir, "mempool.dat"))
             if n:
@@ -234,8 +242,17 @@ class Node:
                                          verify_mode=a.get("p2pverifymode", "auto"), datadir=self.datadir,
                                          connect_only=bool(connect),
                                          max_outbound=a.get_int("maxconnections", 8) if not connect else 0)
+        self.connman.proxies.configure(a)
         self.connman.start()
         cm = self.connman
+        if listen is not None and a.get_bool("listenonion", True):  # StartTorControl (src/init.cpp)
+            from .net.torcontrol import DEFAULT_TOR_CONTROL, TorController
+
+            self.torcontrol = TorController(a.get("torcontrol", DEFAULT_TOR_CONTROL), self.datadir, cm.port,
+                                            proxies=cm.proxies, add_local=lambda h, p: cm.add_local(h, p, 4),
+                                            remove_local=cm.remove_local, password=a.get("torpassword", ""),
+                                            onion_arg_set=a.get("onion") is not None)
+            self.torcontrol.start()
         st = self.state
 
         class _Relay(ValidationInterface):
@@ -294,6 +311,13 @@ class Node:
                 self.state.save_mempool(os.path.join(self.datadir, "mempool.dat"))  # DumpMempool on shutdown
             except OSError as e:
                 log.log_printf(f"Failed to dump mempool: {e}")
+        if self.state is not None and self.datadir is not None:
+            try:  # Shutdown: FlushUnconfirmed, then fee_estimates.dat
+                self.state.save_fee_estimates(os.path.join(self.datadir, "fee_estimates.dat"))
+            except OSError as e:
+                log.log_printf(f"Failed to write fee estimates: {e}")
+        if getattr(self, "torcontrol", None) is not None:
+            self.torcontrol.stop()  # InterruptTorControl / StopTorControl
         if getattr(self, "connman", None) is not None:
             self.connman.stop()
         if self.state is not None:

@@ -674,9 +674,12 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         return {"version": 40404, "subversion": P.USER_AGENT, "protocolversion": P.PROTOCOL_VERSION,
                 "localservices": "%016x" % (P.NODE_NETWORK | P.NODE_WITNESS), "localrelay": True,
                 "timeoffset": 0, "networkactive": cm is not None, "connections": node.peer_count(),
-                "networks": [], "relayfee": 0.00001, "incrementalfee": 0.00001,
+                "networks": cm.proxies.describe() if cm is not None else [],
+                "relayfee": 0.00001, "incrementalfee": 0.00001,
                 "localaddresses": ([{"address": cm.listen_addr[0], "port": cm.port, "score": 1}]
-                                   if cm is not None and cm.port else []), "warnings": ""}
+                                   if cm is not None and cm.port else [])
+                + ([{"address": h, "port": pt, "score": sc} for (h, pt), sc in sorted(cm.local_addrs.items())]
+                   if cm is not None else []), "warnings": ""}
 
     def rpc_addnode(p):
         """addnode "node" "add|remove|onetry" — only onetry/add connect immediately here."""

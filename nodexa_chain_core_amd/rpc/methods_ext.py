@@ -23,8 +23,8 @@ import time
 from .. import core
 from ..chain.state import _compact_size, _read_compact_size
 from .methods import _arg, _hex, _need, _parse_hash
-from .protocol import (RPC_DESERIALIZATION_ERROR, RPC_INVALID_ADDRESS_OR_KEY, RPC_INVALID_PARAMETER, RPC_MISC_ERROR,
-                       RPC_TYPE_ERROR, RPCError)
+from .protocol import (RPC_DESERIALIZATION_ERROR, RPC_INVALID_ADDRESS_OR_KEY, RPC_INVALID_PARAMETER,
+                       RPC_METHOD_DEPRECATED, RPC_MISC_ERROR, RPC_TYPE_ERROR, RPCError)
 
 _core = core()
 
@@ -659,38 +659,81 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
     table.append("blockchain", "verifytxoutproof", rpc_verifytxoutproof, ("proof",))
 
     # ------------------------------------------------------------------ fee estimation
+    # CBlockPolicyEstimator lives in csrc/chain/fees.cpp; these are src/rpc/mining.cpp:1009-1212.
+    def _conf_target(v) -> int:
+        """ParseConfirmTarget: 1 .. the long horizon's highest tracked target (1008)."""
+        if isinstance(v, bool) or not isinstance(v, (int, float)):
+            raise RPCError(RPC_TYPE_ERROR, "Expected type number")
+        hi = st.fee_estimator.highest_target_tracked("long")
+        t = int(v)
+        if t < 1 or t > hi:
+            raise RPCError(RPC_INVALID_PARAMETER, f"Invalid conf_target, must be between 1 - {hi}")
+        return t
+
+    def _amount(sat_per_kb: int) -> float:
+        return round(sat_per_kb / 1e8, 8)
+
     def rpc_estimatefee(p):
-        """estimatefee nblocks — DEPRECATED. Fee per kB for confirmation within nblocks, -1 without data."""
+        """estimatefee nblocks — DEPRECATED (needs -deprecatedrpc=estimatefee). Fee per kB for
+        confirmation within nblocks from the medium horizon at 95 %, -1 without an estimate."""
         _need(p, 1, "estimatefee nblocks")
-        n = max(1, int(p[0]))
-        if n == 1:
-            return -1.0
-        r = st.estimate_fee(n)
-        return -1.0 if r is None else round(r * 1000 / 1e8, 8)
+        if "estimatefee" not in node.args.get_list("deprecatedrpc"):
+            raise RPCError(RPC_METHOD_DEPRECATED,
+                           "estimatefee is deprecated and will be fully removed in v0.17. To use estimatefee in v0.16, "
+                           "restart clore_blockchaind with -deprecatedrpc=estimatefee.\nProjects should transition to "
+                           "using estimatesmartfee before upgrading to v0.17")
+        if isinstance(p[0], bool) or not isinstance(p[0], (int, float)):
+            raise RPCError(RPC_TYPE_ERROR, "Expected type number")
+        r = st.fee_estimator.estimate_fee(max(1, int(p[0])))
+        return -1.0 if r == 0 else _amount(r)
 
     def rpc_estimatesmartfee(p):
         """estimatesmartfee conf_target ( "estimate_mode" ) — {"feerate", "blocks"} or {"errors", "blocks"}."""
         _need(p, 1, 'estimatesmartfee conf_target ( "estimate_mode" )')
-        target = min(max(1, int(p[0])), 1008)
-        r = st.estimate_fee(target)
-        if r is None:
-            return {"errors": ["Insufficient data or no feerate found"], "blocks": target}
-        return {"feerate": round(r * 1000 / 1e8, 8), "blocks": target}
+        target = _conf_target(p[0])
+        conservative = True
+        mode = _arg(p, 1)
+        if mode is not None:
+            if mode not in ("UNSET", "ECONOMICAL", "CONSERVATIVE"):
+                raise RPCError(RPC_INVALID_PARAMETER, "Invalid estimate_mode parameter")
+            conservative = mode != "ECONOMICAL"
+        rate, returned, _reason, _est = st.fee_estimator.estimate_smart_fee(target, conservative)
+        out = {"feerate": _amount(rate)} if rate else {"errors": ["Insufficient data or no feerate found"]}
+        out["blocks"] = returned
+        return out
 
     def rpc_estimaterawfee(p):
-        """estimaterawfee conf_target ( threshold ) — raw estimate per horizon."""
+        """estimaterawfee conf_target ( threshold ) — per-horizon raw estimate with its pass / fail
+        bucket ranges, for every horizon that tracks the target."""
         _need(p, 1, "estimaterawfee conf_target ( threshold )")
-        target = min(max(1, int(p[0])), 1008)
-        r = st.estimate_fee(target)
+        target = _conf_target(p[0])
+        threshold = 0.95 if _arg(p, 1) is None else float(p[1])
+        if threshold < 0 or threshold > 1:
+            raise RPCError(RPC_INVALID_PARAMETER, "Invalid threshold")
+
+        def bucket(b):
+            return {"startrange": round(b["startrange"]), "endrange": round(b["endrange"]),
+                    **{k: round(b[k] * 100.0) / 100.0 for k in ("withintarget", "totalconfirmed", "inmempool",
+                                                                 "leftmempool")}}
         out = {}
         for horizon in ("short", "medium", "long"):
-            if r is None:
-                out[horizon] = {"fail": {"startrange": 0, "endrange": 0, "withintarget": 0, "totalconfirmed": 0,
-                                         "inmempool": len(st.mempool), "leftmempool": 0},
-                                "errors": ["Insufficient data or no feerate found which meets threshold"],
-                                "decay": 0.962, "scale": 1}
+            if target > st.fee_estimator.highest_target_tracked(horizon):
+                continue
+            rate, est = st.fee_estimator.estimate_raw_fee(target, threshold, horizon)
+            h = {}
+            if rate:
+                h["feerate"] = _amount(rate)
+                h["decay"] = est["decay"]
+                h["scale"] = est["scale"]
+                h["pass"] = bucket(est["pass"])
+                if est["fail"]["startrange"] != -1:  # -1: every bucket passed, no fail range
+                    h["fail"] = bucket(est["fail"])
             else:
-                out[horizon] = {"feerate": round(r * 1000 / 1e8, 8), "decay": 0.962, "scale": 1}
+                h["decay"] = est["decay"]
+                h["scale"] = est["scale"]
+                h["fail"] = bucket(est["fail"])
+                h["errors"] = ["Insufficient data or no feerate found which meets threshold"]
+            out[horizon] = h
         return out
 
     table.append("util", "estimatefee", rpc_estimatefee, ("nblocks",))

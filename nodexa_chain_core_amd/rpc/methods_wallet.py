@@ -188,7 +188,7 @@ def register(table, node) -> None:
                "immature_balance": w.immature_balance() / COIN,
                "txcount": len(w.history.txs) if w.history is not None else len(w.unspent(0)),
                "keypoololdest": min(w.created.values(), default=0), "keypoolsize": len(w.pool),
-               "paytxfee": w.fee_rate / COIN}
+               "paytxfee": w.pay_tx_fee / COIN}
         if w.encrypted:
             out["unlocked_until"] = w.unlocked_until
         if w.hd is not None:
@@ -390,7 +390,7 @@ def register(table, node) -> None:
         """settxfee amount — fee rate in CLORE per kB for wallet sends."""
         if not p:
             raise RPCError(RPC_INVALID_PARAMETER, "settxfee amount")
-        wallet().fee_rate = max(round(float(p[0]) * COIN), st.min_relay_fee)
+        wallet().pay_tx_fee = round(float(p[0]) * COIN)  # payTxFee = CFeeRate(nAmount, 1000); 0 = estimate
         return True
 
     def rpc_getrawchangeaddress(p):

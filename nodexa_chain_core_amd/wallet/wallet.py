@@ -29,6 +29,8 @@ SIGHASH_ALL = 1
 COIN = 100_000_000
 DEFAULT_FEE_RATE = 2_000_000  # sat per kvB: above the 0.01 CLORE/kvB min relay fee
 DEFAULT_KEYPOOL_SIZE = 100
+DEFAULT_TX_CONFIRM_TARGET = 6   # src/wallet/wallet.h:69
+DEFAULT_TRANSACTION_MINFEE = 1_000_000  # -mintxfee (src/wallet/wallet.h:57)
 DEFAULT_DERIVE_ROUNDS = 25000  # CMasterKey nDeriveIterations default
 UNLOCK_NEEDED = "Error: Please enter the wallet passphrase with walletpassphrase first."
 HARDENED = 0x80000000
@@ -137,7 +139,9 @@ class Wallet:
         self.watch: dict[bytes, dict] = {}  # watch-only scriptPubKey -> {"label", "solvable"} (importaddress)
         self.walletrbf = False  # -walletrbf: sends signal BIP125 replaceability (DEFAULT_WALLET_RBF)
         self.history = None    # wallet/history.WalletHistory, attached by the node
-        self.fee_rate = DEFAULT_FEE_RATE  # settxfee
+        self.pay_tx_fee = 0               # settxfee / -paytxfee (sat per kvB; 0 = use fee estimation)
+        self.fallback_fee = DEFAULT_FEE_RATE  # -fallbackfee: used while the estimator has no answer
+        self.tx_confirm_target = DEFAULT_TX_CONFIRM_TARGET  # -txconfirmtarget
         self.hdpath: dict[bytes, str] = {}      # hdkeypath of derived keys
         self.pool: list[bytes] = []             # keypool: reserved keys not yet handed out
         self.hd: dict | None = None             # {"master_id", "next", "seed", "seed_crypted"}
@@ -152,6 +156,24 @@ class Wallet:
             self._init_hd(bip44, mnemonic, mnemonic_passphrase)
 
     # ------------------------------------------------------------------ persistence
+
+    @property
+    def fee_rate(self) -> int:
+        """GetMinimumFee's feerate (src/wallet/fees.cpp): -paytxfee / settxfee when set, else the
+        node's estimatesmartfee at -txconfirmtarget (economical when the wallet signals BIP125),
+        else -fallbackfee; never below -mintxfee or the min relay fee."""
+        rate = self.pay_tx_fee
+        if not rate:
+            est = getattr(self.state, "fee_estimator", None) if self.state is not None else None
+            if est is not None:
+                rate, _, _, _ = est.estimate_smart_fee(self.tx_confirm_target, not self.walletrbf)
+            rate = rate or self.fallback_fee
+        floor = max(DEFAULT_TRANSACTION_MINFEE, getattr(self.state, "min_relay_fee", 0) if self.state else 0)
+        return max(rate, floor)
+
+    @fee_rate.setter
+    def fee_rate(self, v: int) -> None:
+        self.pay_tx_fee = int(v)
     def _load(self) -> None:
         with open(self.path) as f:
             data = json.load(f)

@@ -38,8 +38,8 @@ def test_control_and_hidden(core, node_factory):  # noqa: F811
     assert c.waitforblockheight(2, 10)["height"] == 3
     assert c.waitforblock(c.getbestblockhash(), 10)["height"] == 3
     est = c.estimatesmartfee(6)
-    assert est["errors"] and est["blocks"] == 6
-    assert c.estimatefee(6) == -1
+    assert est["errors"] and est["blocks"] == 0  # clamped to the (empty) usable history
+    assert "deprecated" in _rpc_error(c.estimatefee, 6)
     assert "fail" in c.estimaterawfee(6)["short"]
 
 
