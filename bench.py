@@ -108,7 +108,7 @@ def main() -> int:
     searcher = KawpowSearcher(ep, height)
     gather = ShareGather(searcher)
     nonce_base = 0x5EED_0000_0000_0000
-    batch = args.batch
+    batch = args.batch // searcher.block * searcher.block  # whole workgroups of the tuned kernel
 
     def step(i: int) -> None:
         start = nonce_base + (i * ws + rank) * batch

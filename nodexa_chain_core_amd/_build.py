@@ -15,7 +15,7 @@ valid in our kernels. Device code is never linked into the host .so; every
 kernel is a code object loaded with hipModuleLoadData, which also serves the
 per-period KawPow kernels that are generated at run time (see ops/jit.py).
 
-Usage: python -m nodexa_chain_core_amd._build [--force] [--jobs N] [core|bench|hip|kernels|tsan|asan]
+Usage: python -m nodexa_chain_core_amd._build [--force] [--jobs N] [core|bench|hip|kernels|tsan|asan|fuzz]
 """
 from __future__ import annotations
 
@@ -92,7 +92,7 @@ def _compile_all(srcs: list[str], flags: list[str], objdir: str, jobs: int, forc
 
 def core_sources() -> list[str]:
     srcs = glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)
-    skip = (os.sep + "daemon" + os.sep, os.sep + "bench" + os.sep, os.sep + "stress" + os.sep)
+    skip = (os.sep + "daemon" + os.sep, os.sep + "bench" + os.sep, os.sep + "stress" + os.sep, os.sep + "fuzz" + os.sep)
     return sorted(s for s in srcs if not any(k in s for k in skip))
 
 
@@ -136,6 +136,29 @@ def build_sanitized(kind: str, force: bool = False, jobs: int = 8) -> str:
     out = os.path.join(out_dir, "stress_" + kind)
     if force or _newer(out, objs):
         _run(["g++", *san, "-o", out, *objs, "-pthread"])
+    return out
+
+
+def build_fuzz(force: bool = False, jobs: int = 8) -> str:
+    """bin/fuzz_nodexa: csrc/fuzz (a libFuzzer entry point) + every core source (no bindings),
+    compiled by ROCm's clang with coverage instrumentation and ASan + UBSan, host code only
+    (the reference's test_clore_fuzzy tier)."""
+    clang = os.path.join(ROCM, "lib", "llvm", "bin", "clang++")
+    # nonnull-attribute off: memcpy(dst, nullptr, 0) from empty inputs is defined behaviour from
+    # C2y (N3322) and harmless in glibc; every other UB check aborts the run
+    san = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-sanitize=nonnull-attribute"]
+    # -asan-globals=0: this clang registers some merged string literals twice and aborts with a
+    # spurious odr-violation; heap, stack and UB checks are unaffected
+    flags = ["-O1", "-g", "-std=c++17", "-fno-omit-frame-pointer", "-march=x86-64-v3", "-w",
+             "-fsanitize=fuzzer-no-link", "-mllvm", "-asan-globals=0", *san]
+    srcs = [s for s in core_sources() if os.sep + "bind" + os.sep not in s]
+    srcs += sorted(glob.glob(os.path.join(CSRC, "fuzz", "*.cpp")))
+    objs = _compile_all(srcs, flags, os.path.join(BUILD, "fuzz"), jobs, force, compiler=clang)
+    out_dir = os.path.join(PKG, "bin")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "fuzz_nodexa")
+    if force or _newer(out, objs):
+        _run([clang, "-fsanitize=fuzzer", *san, "-o", out, *objs, "-pthread"])
     return out
 
 
@@ -205,6 +228,8 @@ def main() -> None:
             print(build_bench(a.force, a.jobs))
         if w in ("tsan", "asan"):
             print(build_sanitized(w, a.force, a.jobs))
+        if w == "fuzz":
+            print(build_fuzz(a.force, a.jobs))
         if w in ("all", "hip"):
             print(build_hip_runtime(a.force, a.jobs))
         if w in ("all", "kernels"):

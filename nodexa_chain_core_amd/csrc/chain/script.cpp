@@ -213,7 +213,7 @@ void ripemd160(const u8* data, size_t n, u8 out[20]) {
     for (; i + 64 <= n; i += 64) rmd_compress(h, data + i);
     u8 tail[128] = {0};
     const size_t rem = n - i;
-    std::memcpy(tail, data + i, rem);
+    if (rem) std::memcpy(tail, data + i, rem);
     tail[rem] = 0x80;
     const size_t tl = (rem < 56) ? 64 : 128;
     store_le64(tail + tl - 8, u64(n) * 8);

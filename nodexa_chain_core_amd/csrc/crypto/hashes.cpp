@@ -71,7 +71,7 @@ void sha1(const u8* data, size_t n, u8 out[20]) {
     data += n / 64 * 64;
     n %= 64;
     u8 buf[128] = {0};
-    std::memcpy(buf, data, n);
+    if (n) std::memcpy(buf, data, n);  // data may be null when n == 0
     buf[n] = 0x80;
     const size_t len = n < 56 ? 64 : 128;
     store_be64(buf + len - 8, bits);

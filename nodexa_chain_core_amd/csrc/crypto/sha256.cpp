@@ -108,7 +108,7 @@ Sha256& Sha256::write(const u8* data, size_t n) {
         data += n / 64 * 64;
         n %= 64;
     }
-    std::memcpy(buf_, data, n);
+    if (n) std::memcpy(buf_, data, n);
     return *this;
 }
 

@@ -187,7 +187,8 @@ Hash512 x16r_single(int algo, const u8* data, size_t n) {
 
 void x16r_hash(const u8* data, size_t n, const u8 prev_le[32], bool v2, u8 out[32]) {
     Hash512 h;
-    const u8* in = data;
+    static const u8 kEmpty[1] = {0};
+    const u8* in = n ? data : kEmpty;  // an empty message may come with a null pointer
     size_t len = n;
     for (int i = 0; i < 16; ++i) {
         const int sel = x16r_selection(prev_le, i);

@@ -58,6 +58,10 @@
 //   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride), DAG < 4 GiB only
 //   KP_L1X4       L1 replicated 4x in LDS (64 KiB) so an L1 address is one
 //                 16-bit shift: ((x << 2) & 0xffff) reads l1[x % 4096]
+//   KP_DIGEST_REG each finished hash's 8 digest words go straight to the lane that
+//                 owns the hash's nonce (8 DPP broadcasts + 8 selects per hash, 8 VGPRs)
+//                 instead of a 32 B/nonce LDS buffer: the workgroup's LDS is then only
+//                 the L1 table, so 1024-thread groups fit twice per CU (8 waves/SIMD)
 #ifndef KP_BLOCK
 #define KP_BLOCK NODEXA_KAWPOW_BLOCK
 #endif
@@ -282,7 +286,8 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMo
 }
 
 NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
-                            uint32_t st0, uint32_t st1, uint32_t lane, uint32_t* dig) {
+                            uint32_t st0, uint32_t st1, uint32_t lane, uint32_t* dig,
+                            uint32_t (&own)[8]) {
 #pragma unroll 1
     for (uint32_t h0 = 0; h0 < 16; h0 += KP_HASHES) {
         uint32_t mx[KP_HASHES][32];
@@ -331,14 +336,36 @@ NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t
             for (int i = 0; i < 32; ++i) lh = kp_fnv1a(lh, mx[k][i]);
             // digest[j] = fnv1a(fnv1a(basis, lane_hash[j]), lane_hash[j + 8]); lanes 0..7 own j
             const uint32_t hi = __shfl(lh, (int)(lane + 8), 16);
+#ifdef KP_DIGEST_REG
+            // lanes 0..7 hold the digest words; lane h0+k keeps all 8 of them
+            const uint32_t word = kp_fnv1a(kp_fnv1a(0x811c9dc5u, lh), hi);
+            const bool mine = lane == h0 + (uint32_t)k;
+            // every lane runs the (convergent) broadcasts; only the owner keeps them
+            const uint32_t b0 = kp_bcast<0>(word), b1 = kp_bcast<1>(word), b2 = kp_bcast<2>(word),
+                           b3 = kp_bcast<3>(word), b4 = kp_bcast<4>(word), b5 = kp_bcast<5>(word),
+                           b6 = kp_bcast<6>(word), b7 = kp_bcast<7>(word);
+            own[0] = mine ? b0 : own[0];
+            own[1] = mine ? b1 : own[1];
+            own[2] = mine ? b2 : own[2];
+            own[3] = mine ? b3 : own[3];
+            own[4] = mine ? b4 : own[4];
+            own[5] = mine ? b5 : own[5];
+            own[6] = mine ? b6 : own[6];
+            own[7] = mine ? b7 : own[7];
+            (void)dig;
+#else
             if (lane < 8) dig[(h0 + k) * 8 + lane] = kp_fnv1a(kp_fnv1a(0x811c9dc5u, lh), hi);
+            (void)own;
+#endif
         }
     }
 }
 
 extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     __shared__ uint32_t l1[KP_L1_WORDS];
-#ifdef KP_DIGEST_GLOBAL
+#if defined(KP_DIGEST_REG)
+    uint32_t* digs = nullptr;
+#elif defined(KP_DIGEST_GLOBAL)
     // digests parked in HBM (32 B per nonce, <0.2% of the DAG traffic) so the
     // 64 KiB L1X4 table leaves LDS room for 2 workgroups of KP_BLOCK per CU
     uint32_t* digs = p.scratch + (size_t)blockIdx.x * KP_BLOCK * 8;
@@ -351,18 +378,21 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
 
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t nonce = p.start_nonce + (uint64_t)blockIdx.x * KP_BLOCK + threadIdx.x;
-    uint32_t* dig = digs + (threadIdx.x & ~15u) * 8;
+    uint32_t* dig = digs ? digs + (threadIdx.x & ~15u) * 8 : nullptr;
+    uint32_t digest[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     {
         uint32_t st2[8];
         kp_seed(p.header, nonce, st2);
-        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig);
+        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig, digest);
     }
+#ifndef KP_DIGEST_REG
     __threadfence_block();  // digest words written by lanes 0..7 are read by lane h below
     __syncthreads();
-    uint32_t st2[8], digest[8], fin[8];
-    kp_seed(p.header, nonce, st2);  // recomputed: cheaper than 6 VGPRs held across the mix loop
 #pragma unroll
     for (int k = 0; k < 8; ++k) digest[k] = dig[lane * 8 + k];
+#endif
+    uint32_t st2[8], fin[8];
+    kp_seed(p.header, nonce, st2);  // recomputed: cheaper than 6 VGPRs held across the mix loop
     kp_final(st2, digest, fin);
     const uint64_t head = ((uint64_t)__builtin_bswap32(fin[0]) << 32) | __builtin_bswap32(fin[1]);
     if (head <= p.target) {
@@ -383,7 +413,11 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
 // all share this period and epoch. One job per thread, grouped as in search.
 extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     __shared__ uint32_t l1[KP_L1_WORDS];
+#ifdef KP_DIGEST_REG
+    uint32_t* digs = nullptr;
+#else
     __shared__ uint32_t digs[KP_BLOCK * 8];
+#endif
     if (blockDim.x != KP_BLOCK) return;
     kp_fill_l1(l1, p.dag);
     __syncthreads();
@@ -391,14 +425,15 @@ extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     const uint32_t job = blockIdx.x * KP_BLOCK + threadIdx.x;
     const bool valid = job < p.num_jobs;
     const KawpowVerifyJob j = p.jobs[valid ? job : 0];
-    uint32_t* dig = digs + (threadIdx.x & ~15u) * 8;
-    uint32_t st2[8];
+    uint32_t* dig = digs ? digs + (threadIdx.x & ~15u) * 8 : nullptr;
+    uint32_t st2[8], digest[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fin[8];
     kp_seed(j.header, j.nonce, st2);
-    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig);
+    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig, digest);
+#ifndef KP_DIGEST_REG
     __syncthreads();
-    uint32_t digest[8], fin[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) digest[k] = dig[lane * 8 + k];
+#endif
     kp_final(st2, digest, fin);
     if (valid) {
         uint32_t* o = p.out + (size_t)job * 16;

@@ -82,7 +82,12 @@ def _atomic_copy(src: str, dst: str) -> None:
 
 # Tuned variant of the search template (profiles/README.md has the sweep that
 # picked it); NODEXA_KAWPOW_DEFINES="A,B=1" overrides it ("none" = plain template).
-TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_SBUFFER", "KP_L1X4", "KP_BLOCK=512", "KP_NT_DAG")
+# r2l / r2m: digests held in registers (KP_DIGEST_REG) leave only the 64 KiB L1 table in LDS, so
+# two 768-thread workgroups share a CU (6 waves/SIMD instead of 4): +0.7 / +0.8 % in two
+# interleaved sweeps; 640 / 896 threads (waves uneven across the 4 SIMDs) and 1024 (64 VGPRs,
+# heavy spills) lose.
+TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_SBUFFER", "KP_L1X4", "KP_BLOCK=768",
+                                  "KP_DIGEST_REG", "KP_MIN_WAVES=6", "KP_NT_DAG")
 _env = os.environ.get("NODEXA_KAWPOW_DEFINES")
 DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
     d for d in _env.split(",") if d and d != "none")

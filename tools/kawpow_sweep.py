@@ -86,7 +86,8 @@ def main() -> int:
         for w in range(a.check_windows):
             res.zero_()
             h.launch_kawpow_search(kern[v], ep.dag.data_ptr(), ep.items2048, res.data_ptr(), header,
-                                   1000 + w * 7919 * 5120, (1 << 64) - 1, 5120, stream, *sargs)
+                                   1000 + w * 7919 * 5120, (1 << 64) - 1, -(-5120 // kern[v].max_threads) * kern[v].max_threads,
+                                   stream, *sargs)
             raw = res.cpu().numpy().tobytes()
             n = min(struct.unpack_from("<I", raw, 0)[0], 64)
             for i in range(n):
