@@ -64,8 +64,12 @@ def is_dust(value: int, spk: bytes, dust_fee: int = DUST_RELAY_TX_FEE) -> bool:
     return value < dust_threshold(spk, dust_fee)
 
 
-def standard_outputs_reason(tx, witness_enabled: bool = True, permit_bare_multisig: bool = True) -> str:
-    """The output half of IsStandardTx: '' when standard, else the reject reason."""
+def standard_outputs_reason(tx, witness_enabled: bool = True, permit_bare_multisig: bool = True,
+                            datacarrier: bool = True, datacarrier_size: int = MAX_OP_RETURN_RELAY,
+                            dust_fee: int = DUST_RELAY_TX_FEE) -> str:
+    """The output half of IsStandardTx: '' when standard, else the reject reason. -datacarrier /
+    -datacarriersize (fAcceptDatacarrier, nMaxDatacarrierBytes), -permitbaremultisig and
+    -dustrelayfee select the policy knobs."""
     data_out = asset_data_out = 0
     for o in tx.vout:
         t = output_type(o.script_pubkey)
@@ -75,7 +79,7 @@ def standard_outputs_reason(tx, witness_enabled: bool = True, permit_bare_multis
             m, n = o.script_pubkey[0] - 0x50, o.script_pubkey[-2] - 0x50
             if not (1 <= n <= 3 and 1 <= m <= n):
                 return "scriptpubkey"
-        if t == "nulldata" and len(o.script_pubkey) > MAX_OP_RETURN_RELAY:
+        if t == "nulldata" and (not datacarrier or len(o.script_pubkey) > datacarrier_size):
             return "scriptpubkey"
         if t == "null_asset" and len(o.script_pubkey) > MAX_OP_RETURN_RELAY:
             return "scriptpubkey"
@@ -87,7 +91,7 @@ def standard_outputs_reason(tx, witness_enabled: bool = True, permit_bare_multis
             asset_data_out += 1
         elif t == "multisig" and not permit_bare_multisig:
             return "bare-multisig"
-        elif is_dust(o.value, o.script_pubkey):
+        elif is_dust(o.value, o.script_pubkey, dust_fee):
             return "dust"
     if data_out > 1:
         return "multi-op-return"

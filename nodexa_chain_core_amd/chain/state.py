@@ -108,6 +108,12 @@ DEFAULT_INCREMENTAL_RELAY_FEE = 1000   # sat per kvB (src/policy/policy.h:36)
 DEFAULT_ENABLE_REPLACEMENT = False     # -mempoolreplacement (src/validation.h:163)
 MAX_STANDARD_TX_WEIGHT = 400_000       # src/policy/policy.h:28
 MAX_FEE_ESTIMATION_TIP_AGE = 3 * 60 * 60  # src/validation.h (IsCurrentForFeeEstimation)
+# package and expiry limits (src/validation.h:77-85) and the raw-tx fee cap (DEFAULT_TRANSACTION_MAXFEE)
+DEFAULT_ANCESTOR_LIMIT, DEFAULT_ANCESTOR_SIZE_LIMIT = 200, 250        # count, kvB
+DEFAULT_DESCENDANT_LIMIT, DEFAULT_DESCENDANT_SIZE_LIMIT = 200, 250
+DEFAULT_MEMPOOL_EXPIRY = 336                                          # hours
+DEFAULT_TRANSACTION_MAXFEE = 1000 * 100_000_000
+DEFAULT_BLOCK_MIN_TX_FEE = 1000                                       # sat per kvB (src/policy/policy.h:26)
 MAX_STANDARD_SCRIPTSIG_SIZE = 1650
 GPU_SIG_BATCH_MIN = 16                 # below this many signatures a block is checked on the host
 
@@ -160,6 +166,16 @@ class ChainState:
         self.incremental_relay_fee = DEFAULT_INCREMENTAL_RELAY_FEE  # -incrementalrelayfee
         self.enable_replacement = DEFAULT_ENABLE_REPLACEMENT       # -mempoolreplacement
         self.require_standard = params.network_id == "main"        # fRequireStandard / -acceptnonstdtxn
+        self.datacarrier, self.datacarrier_size = True, policy.MAX_OP_RETURN_RELAY  # -datacarrier[size]
+        self.permit_bare_multisig = True                            # -permitbaremultisig
+        self.dust_relay_fee = policy.DUST_RELAY_TX_FEE              # -dustrelayfee
+        self.ancestor_limits = (DEFAULT_ANCESTOR_LIMIT, DEFAULT_ANCESTOR_SIZE_LIMIT * 1000)        # -limitancestor*
+        self.descendant_limits = (DEFAULT_DESCENDANT_LIMIT, DEFAULT_DESCENDANT_SIZE_LIMIT * 1000)  # -limitdescendant*
+        self.mempool_expiry = DEFAULT_MEMPOOL_EXPIRY * 3600         # -mempoolexpiry (seconds)
+        self.max_tx_fee = DEFAULT_TRANSACTION_MAXFEE                # -maxtxfee (absurd-fee cap)
+        self.block_max_weight = 7_999_000                           # -blockmaxweight
+        self.block_max_size: int | None = None                      # -blockmaxsize
+        self.block_min_fee_rate = DEFAULT_BLOCK_MIN_TX_FEE          # -blockmintxfee
         self.script_threads = min(16, os.cpu_count() or 1)  # -par: script-check threads (CCheckQueue)
         self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
         self.flush_interval = 1000
@@ -346,7 +362,7 @@ class ChainState:
         txid = tx.txid()
         with self.lock:
             new = txid not in self.mempool
-            e = MempoolEntry(tx, int(fee) + int(fee_delta), entry_time or time.time(),
+            e = MempoolEntry(tx, int(fee) + int(fee_delta), entry_time or self.adjusted_time(),  # GetTime(): mocktime aware
                              self.chain.height(), int(fee_delta), len(tx.serialize(True)))
             if new:
                 # processTransaction: fee estimates only learn from a node that is current, and not
@@ -815,7 +831,10 @@ class ChainState:
                         return False, "scriptsig-size", 0
                     if not _core.script_is_push_only(i.script_sig):
                         return False, "scriptsig-not-pushonly", 0
-                why = policy.standard_outputs_reason(tx)
+                why = policy.standard_outputs_reason(tx, permit_bare_multisig=self.permit_bare_multisig,
+                                                     datacarrier=self.datacarrier,
+                                                     datacarrier_size=self.datacarrier_size,
+                                                     dust_fee=self.dust_relay_fee)
                 if why:
                     return False, why, 0
             pool_spent = {(i.prevout.hash, i.prevout.n): t for t, e in self.mempool.items() for i in e.tx.vin}
@@ -857,6 +876,9 @@ class ChainState:
                     return False, why, fee
             if max_fee is not None and fee > max_fee:
                 return False, "absurdly-high-fee", fee
+            why = self._check_package_limits(tx, vsize, conflicts | replaced)
+            if why:
+                return False, why, fee
             for k, (value, spk) in enumerate(coins):
                 vin = tx.vin[k]
                 ok, err = _core.verify_script(vin.script_sig, spk, list(vin.witness), _core.STANDARD_SCRIPT_VERIFY_FLAGS,
@@ -870,7 +892,44 @@ class ChainState:
                 for t in replaced:  # BIP125: the replaced transactions and their descendants leave
                     self.pool_remove(t)
                 self.add_to_mempool(tx, fee, replacement=bool(replaced))
+                self.expire_mempool()  # LimitMempoolSize -> Expire
             return True, "", fee
+
+    def _check_package_limits(self, tx, vsize: int, leaving: set) -> str:
+        """CalculateMemPoolAncestors with -limitancestorcount / -limitancestorsize and, for each
+        ancestor, -limitdescendantcount / -limitdescendantsize (transactions being replaced do not
+        count). Returns "" or "too-long-mempool-chain"."""
+        parents = {i.prevout.hash for i in tx.vin if i.prevout.hash in self.mempool and i.prevout.hash not in leaving}
+        if not parents:
+            return ""
+        anc = set(parents)
+        for p in parents:
+            anc |= self.mempool_ancestors(p)
+        anc -= leaving
+        n_max, size_max = self.ancestor_limits
+        if len(anc) + 1 > n_max or sum(self.mempool[a].vsize() for a in anc) + vsize > size_max:
+            return "too-long-mempool-chain"
+        d_max, dsize_max = self.descendant_limits
+        for a in anc:
+            desc = self.mempool_descendants(a) - leaving
+            if len(desc) + 2 > d_max or (self.mempool[a].vsize() + sum(self.mempool[d].vsize() for d in desc)
+                                         + vsize) > dsize_max:
+                return "too-long-mempool-chain"
+        return ""
+
+    def expire_mempool(self, now: float | None = None) -> int:
+        """CTxMemPool::Expire: entries older than -mempoolexpiry leave with their descendants."""
+        cutoff = (self.adjusted_time() if now is None else now) - self.mempool_expiry
+        with self.lock:
+            old = [t for t, e in self.mempool.items() if e.time < cutoff]
+            gone = set(old)
+            for t in old:
+                gone |= self.mempool_descendants(t)
+            for t in gone:
+                self.pool_remove(t)
+            if gone:
+                self.transactions_updated += 1
+        return len(gone)
 
     def _check_replacement(self, tx, fee: int, vsize: int, conflicts: set) -> tuple[str, set]:
         """The BIP125 rules of AcceptToMemoryPoolWorker (src/validation.cpp, -mempoolreplacement):

@@ -50,10 +50,13 @@ def script_for_address(params, address: str) -> bytes:
 
 
 class BlockAssembler:
-    def __init__(self, state: ChainState, max_weight: int = 7_999_000):
+    def __init__(self, state: ChainState, max_weight: int | None = None):
         self.state = state
         self.params = state.params
-        self.max_weight = max_weight
+        # -blockmaxweight / -blockmaxsize / -blockmintxfee (BlockAssembler::Options, src/miner.cpp)
+        self.max_weight = max_weight if max_weight is not None else getattr(state, "block_max_weight", 7_999_000)
+        self.max_size = getattr(state, "block_max_size", None)
+        self.min_fee_rate = getattr(state, "block_min_fee_rate", 0)
 
     @traced("miner.create_new_block")
     def create_new_block(self, script_pubkey: bytes, now: int | None = None) -> BlockTemplate:
@@ -61,19 +64,25 @@ class BlockAssembler:
         with st.lock:
             prev = st.tip()
             height = prev.height + 1
-            txs, fees, weight = [], 0, 4000
+            txs, fees, weight, size = [], 0, 4000, 1000
             included: set[bytes] = set()
             for txid in self._parents_first(st.mempool):
                 e = st.mempool[txid]
                 if any(i.prevout.hash in st.mempool and i.prevout.hash not in included for i in e.tx.vin):
                     continue
-                w = len(e.tx.serialize(False)) * 3 + len(e.tx.serialize(True))
+                stripped = len(e.tx.serialize(False))
+                w = stripped * 3 + len(e.tx.serialize(True))
                 if weight + w > self.max_weight:
+                    continue
+                if self.max_size is not None and size + stripped > self.max_size:
+                    continue
+                if e.fee * 1000 < self.min_fee_rate * e.vsize():  # below -blockmintxfee: left out
                     continue
                 txs.append(e.tx)
                 included.add(txid)
                 fees += e.fee
                 weight += w
+                size += stripped
             subsidy = _core.block_subsidy(height)
             pct = self.params.community_autonomous_pct
             cb = _core.Transaction()

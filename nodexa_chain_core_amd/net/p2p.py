@@ -99,13 +99,22 @@ class Peer:
 
     def send_version(self) -> None:
         self.sent_version = True
-        self.send("version", P.version_payload(self.mgr.state.height(), nonce=self.mgr.local_nonce))
+        m = self.mgr
+        self.send("version", P.version_payload(m.state.height(), nonce=m.local_nonce, services=m.local_services,
+                                               relay=not m.blocks_only, agent=m.user_agent))
+
+    @property
+    def whitelisted(self) -> bool:
+        """-whitelist: peers from these subnets are never banned and keep tx relay (-whitelistrelay)."""
+        return self.mgr.is_whitelisted(self.addr[0])
 
     def misbehaving(self, score: int, why: str) -> None:
         """Misbehaving() / DoS ban score (src/net_processing.cpp): disconnect at 100."""
         self.misbehavior += score
         log.log_print("net", f"peer {self.id} misbehaving +{score} ({why}), total {self.misbehavior}")
-        if self.misbehavior >= 100:
+        if self.misbehavior >= 100 and self.whitelisted:
+            log.log_printf(f"Warning: not punishing whitelisted peer {self.addr[0]}!")
+        elif self.misbehavior >= 100:
             self.mgr.ban(self.addr[0], DEFAULT_MISBEHAVING_BANTIME)
             self.close()
 
@@ -146,7 +155,8 @@ class Peer:
                 "subver": self.info.get("user_agent", ""), "startingheight": self.info.get("start_height", -1),
                 "bytessent": self.bytes_sent, "bytesrecv": self.bytes_recv, "conntime": int(self.connected_at),
                 "lastsend": int(self.last_send), "lastrecv": int(self.last_recv), "banscore": self.misbehavior,
-                "synced_headers": self.mgr.state.height(), "relaytxes": self.info.get("relay", True)}
+                "synced_headers": self.mgr.state.height(), "relaytxes": self.info.get("relay", True),
+                "services": "%016x" % self.info.get("services", 0), "whitelisted": self.whitelisted}
 
 
 class ConnectionManager:
@@ -182,6 +192,10 @@ class ConnectionManager:
         self.connect_only = connect_only
         self.max_outbound = max_outbound
         self.proxies = ProxyTable()          # -proxy / -onion / -onlynet (netbase SetProxy / SetLimited)
+        self.whitelist: list = []            # -whitelist subnets (ipaddress networks)
+        self.blocks_only = False             # -blocksonly: no transaction relay in either direction
+        self.peer_bloom_filters = True       # -peerbloomfilters: NODE_BLOOM and the BIP37 messages
+        self.user_agent = P.USER_AGENT       # with -uacomment
         self.local_addrs: dict[tuple[str, int], int] = {}  # AddLocal: (host, port) -> score
 
     # ---------------------------------------------------------------- lifecycle
@@ -239,6 +253,17 @@ class ConnectionManager:
         sock = self.proxies.connect(host, port, timeout=timeout)  # direct, or SOCKS5 through the net's proxy
         sock.settimeout(None)
         return self._add(sock, (host, port), inbound=False)
+
+    @property
+    def local_services(self) -> int:
+        return P.NODE_NETWORK | P.NODE_WITNESS | (P.NODE_BLOOM if self.peer_bloom_filters else 0)
+
+    def is_whitelisted(self, ip: str) -> bool:
+        try:
+            a = ipaddress.ip_address(ip)
+        except ValueError:
+            return False
+        return any(a.version == n.version and a in n for n in self.whitelist)
 
     def add_local(self, host: str, port: int, score: int = 1) -> None:
         """AddLocal (src/net.cpp): an address this node is reachable at, e.g. its onion service."""
@@ -425,7 +450,16 @@ class ConnectionManager:
             peer.send("addr", _ser_addr(items[k:k + MAX_ADDR_TO_SEND]))
 
     # ---------------------------------------------------------------- BIP37 (N5)
+    def _bloom_allowed(self, peer: Peer) -> bool:
+        """-peerbloomfilters=0: BIP111 says a peer asking for a filter we do not serve goes."""
+        if self.peer_bloom_filters:
+            return True
+        peer.misbehaving(100, "bloom filter message while NODE_BLOOM is off")
+        return False
+
     def on_filterload(self, peer: Peer, p: bytes) -> None:
+        if not self._bloom_allowed(peer):
+            return
         f = BloomFilter.from_payload(p)
         if not f.within_size_constraints():
             peer.misbehaving(100, "oversized bloom filter")
@@ -587,6 +621,9 @@ class ConnectionManager:
     def on_tx(self, peer: Peer, p: bytes) -> None:
         """AcceptToMemoryPool for a relayed tx (UTXO set, scripts, fees); accepted transactions
         are relayed to the other peers by the mempool signal."""
+        if self.blocks_only and not peer.whitelisted:  # fBlocksOnly: tx sent in violation of protocol
+            log.log_print("net", f"transaction sent in violation of protocol peer={peer.id}")
+            return
         tx = _core.Transaction.deserialize(p)
         txid = tx.txid()
         peer.known_txs.add(txid)

@@ -27,6 +27,7 @@ KAWPOW_VERSION = 70027
 MIN_PEER_PROTO_VERSION = 70025  # X16RV2_VERSION
 NODE_NETWORK = 1
 NODE_WITNESS = 1 << 3
+NODE_BLOOM = 1 << 2    # BIP111: bloom filters served (-peerbloomfilters)
 MAX_HEADERS_RESULTS = 2000
 MAX_MESSAGE_SIZE = 32 * 1024 * 1024  # MAX_PROTOCOL_MESSAGE_LENGTH after the HIP2 block-size change
 MSG_TX, MSG_BLOCK = 1, 2
@@ -125,11 +126,18 @@ def ser_netaddr(services: int, ip: str = "127.0.0.1", port: int = 0) -> bytes:
     return struct.pack("<Q", services) + ipv6 + struct.pack(">H", port)
 
 
+def user_agent(comments: list[str] | None = None) -> str:
+    """FormatSubVersion: /name:version(comment; comment)/ with -uacomment entries."""
+    if not comments:
+        return USER_AGENT
+    return USER_AGENT[:-1] + "(" + "; ".join(comments) + ")/"
+
+
 def version_payload(start_height: int, nonce: int | None = None, services: int = NODE_NETWORK | NODE_WITNESS,
-                    relay: bool = True, their: tuple[str, int] = ("127.0.0.1", 0)) -> bytes:
+                    relay: bool = True, their: tuple[str, int] = ("127.0.0.1", 0), agent: str = USER_AGENT) -> bytes:
     nonce = int.from_bytes(os.urandom(8), "little") if nonce is None else nonce
     return (struct.pack("<iQq", PROTOCOL_VERSION, services, int(time.time())) + ser_netaddr(services, *their) +
-            ser_netaddr(services) + struct.pack("<Q", nonce) + ser_str(USER_AGENT.encode()) +
+            ser_netaddr(services) + struct.pack("<Q", nonce) + ser_str(agent.encode()) +
             struct.pack("<i?", start_height, relay))
 
 

@@ -78,8 +78,15 @@ class Node:
         a = self.args
         log.configure(a.get_list("debug"), a.get_list("debugexclude"),
                       os.path.join(self.datadir, "debug.log") if self.datadir else None,
-                      console=a.get_bool("printtoconsole", True))
+                      console=a.get_bool("printtoconsole", True), timestamps=a.get_bool("logtimestamps", True),
+                      micros=a.get_bool("logtimemicros", False), ips=a.get_bool("logips", False),
+                      shrink=a.get_bool("shrinkdebugfile") if a.is_set("shrinkdebugfile") else None)
         self.lock_datadir()
+        self._pidfile = None
+        if self.datadir is not None:  # CreatePidFile: -pid=<file> (relative to the data directory)
+            self._pidfile = os.path.join(self.datadir, a.get("pid", "nodexad.pid"))
+            with open(self._pidfile, "w") as f:
+                f.write(f"{os.getpid()}\n")
         # RPC comes up first in warm-up mode (AppInitServers)
         self.table.warmup = "Loading block index..."
         methods.register(self.table, self)
@@ -146,6 +153,24 @@ class Node:
         if a.get("incrementalrelayfee") is not None:
             self.state.incremental_relay_fee = round(float(a.get("incrementalrelayfee")) * 100_000_000)
         self.state.enable_replacement = a.get_bool("mempoolreplacement", self.state.enable_replacement)
+        st, coin = self.state, 100_000_000  # relay / package / block policy knobs (src/init.cpp)
+        st.datacarrier = a.get_bool("datacarrier", True)
+        st.datacarrier_size = a.get_int("datacarriersize", st.datacarrier_size)
+        st.permit_bare_multisig = a.get_bool("permitbaremultisig", True)
+        if a.get("dustrelayfee") is not None:
+            st.dust_relay_fee = round(float(a.get("dustrelayfee")) * coin)
+        st.ancestor_limits = (a.get_int("limitancestorcount", st.ancestor_limits[0]),
+                              a.get_int("limitancestorsize", st.ancestor_limits[1] // 1000) * 1000)
+        st.descendant_limits = (a.get_int("limitdescendantcount", st.descendant_limits[0]),
+                                a.get_int("limitdescendantsize", st.descendant_limits[1] // 1000) * 1000)
+        st.mempool_expiry = a.get_int("mempoolexpiry", st.mempool_expiry // 3600) * 3600
+        if a.get("maxtxfee") is not None:
+            st.max_tx_fee = round(float(a.get("maxtxfee")) * coin)
+        st.block_max_weight = a.get_int("blockmaxweight", st.block_max_weight)
+        if a.is_set("blockmaxsize"):
+            st.block_max_size = a.get_int("blockmaxsize", 0)
+        if a.get("blockmintxfee") is not None:
+            st.block_min_fee_rate = round(float(a.get("blockmintxfee")) * coin)
         self.state.require_standard = not a.get_bool("acceptnonstdtxn", not self.state.require_standard)
         if self.wallet is not None:
             self.wallet.walletrbf = a.get_bool("walletrbf", False)
@@ -155,6 +180,10 @@ class Node:
             if a.get("fallbackfee") is not None:
                 w.fallback_fee = round(float(a.get("fallbackfee")) * 100_000_000)
             w.tx_confirm_target = a.get_int("txconfirmtarget", w.tx_confirm_target)
+            if a.get("mintxfee") is not None:
+                w.min_tx_fee = round(float(a.get("mintxfee")) * 100_000_000)
+            w.keypool_size = max(1, a.get_int("keypool", w.keypool_size))
+            w.broadcast = a.get_bool("walletbroadcast", True)
         par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free
         cores = os.cpu_count() or 1
         self.state.script_threads = max(1, min(16, cores + par if par <= 0 else par))
@@ -193,6 +222,21 @@ class Node:
 
             self.zmq = ZmqNotifier(self.state, zmq_eps)
             self.state.register(self.zmq)
+        from .utils.notify import Notifier
+
+        self.notifier = Notifier(a.get("blocknotify"), a.get("walletnotify"), a.get("alertnotify"))
+        if self.notifier.block:  # -blocknotify: BlockNotifyCallback on every tip change
+            from .chain.state import ValidationInterface
+
+            notifier = self.notifier
+
+            class _BlockNotify(ValidationInterface):
+                def updated_block_tip(self, tip, fork, initial_download: bool) -> None:
+                    notifier.block_tip(tip.hash[::-1].hex(), initial_download)
+
+            self.state.register(_BlockNotify())
+        if self.notifier.wallet and getattr(self, "wallet", None) is not None and self.wallet.history is not None:
+            self.wallet.history.on_change = lambda txid: self.notifier.wallet_tx(txid[::-1].hex())
         stop_at = a.get_int("stopatheight", 0)
         if stop_at > 0:  # -stopatheight (src/validation.cpp:11280): shut down once the tip reaches it
             from .chain.state import ValidationInterface
@@ -243,8 +287,20 @@ class Node:
                                          connect_only=bool(connect),
                                          max_outbound=a.get_int("maxconnections", 8) if not connect else 0)
         self.connman.proxies.configure(a)
+        from .net import protocol as P
+        from .rpc.server import parse_allow_subnets
+
+        self.connman.whitelist = parse_allow_subnets(a.get_list("whitelist"))
+        self.connman.blocks_only = a.get_bool("blocksonly", False)
+        self.connman.peer_bloom_filters = a.get_bool("peerbloomfilters", True)
+        self.connman.user_agent = P.user_agent(a.get_list("uacomment"))
         self.connman.start()
         cm = self.connman
+        for ext in a.get_list("externalip"):  # -externalip: AddLocal(LOCAL_MANUAL)
+            from .net.netbase import parse_host_port
+
+            h, pt = parse_host_port(ext, cm.port or self.params.default_port)
+            cm.add_local(h, pt, 4)
         if listen is not None and a.get_bool("listenonion", True):  # StartTorControl (src/init.cpp)
             from .net.torcontrol import DEFAULT_TOR_CONTROL, TorController
 
@@ -282,11 +338,16 @@ class Node:
         user, pw = a.get("rpcuser"), a.get("rpcpassword")
         if user and pw:
             creds.append(f"{user}:{pw}")
-        elif self.datadir is not None:
-            creds.append(make_cookie(self.datadir))
+        elif self.datadir is not None and not a.get_list("rpcauth"):
+            creds.append(make_cookie(self.datadir, a.get("rpccookiefile")))
         port = a.get_int("rpcport", self.params.default_rpc_port)
         host = a.get("rpcbind", "127.0.0.1")
-        self.rpc = RPCServer(self.table, host, port, creds, a.get_int("rpcworkqueue", 16), rest=self.rest)
+        from .rpc.server import parse_allow_subnets
+
+        self.rpc = RPCServer(self.table, host, port, creds, a.get_int("rpcworkqueue", 16),
+                             rest=self.rest if a.get_bool("rest", False) else None,  # -rest (DEFAULT_REST_ENABLE=false)
+                             rpcauth=a.get_list("rpcauth"), allow=parse_allow_subnets(a.get_list("rpcallowip")),
+                             threads=a.get_int("rpcthreads", 4), idle_timeout=float(a.get("rpcservertimeout", "30")))
         self.rpc.start()
         log.log_printf(f"RPC listening on {host}:{self.rpc.port}")
 
@@ -329,7 +390,13 @@ class Node:
         if self.rpc is not None:
             self.rpc.stop()
         if self.datadir is not None:
-            delete_cookie(self.datadir)
+            delete_cookie(self.datadir, self.args.get("rpccookiefile"))
+        if getattr(self, "_pidfile", None):
+            try:
+                os.unlink(self._pidfile)  # RemovePidFile
+            except OSError:
+                pass
+            self._pidfile = None
         if self._lock_file is not None:
             fcntl.flock(self._lock_file, fcntl.LOCK_UN)
             self._lock_file.close()

@@ -13,6 +13,7 @@ import http.client
 import json
 import os
 import sys
+import time
 
 from ..utils.config import ArgsManager
 
@@ -97,8 +98,11 @@ def main(argv: list[str] | None = None) -> int:
     if args.network != "main":
         datadir = os.path.join(datadir, "testnet7" if args.network == "test" else "regtest")
     cli = RPCClient(args.get("rpcconnect", "127.0.0.1"), args.get_int("rpcport", params.default_rpc_port),
-                    args.get("rpcuser"), args.get("rpcpassword"), os.path.join(datadir, ".cookie"),
+                    args.get("rpcuser"), args.get("rpcpassword"),
+                    os.path.join(datadir, os.path.expanduser(args.get("rpccookiefile", ".cookie"))),
                     timeout=float(args.get_int("rpcclienttimeout", 900)))
+    if args.get_bool("stdin", False):  # -stdin: one extra argument per input line
+        rest = rest + [line.rstrip("\n") for line in sys.stdin]
     method, p = rest[0], rest[1:]
     if args.get_bool("named", False):
         named = {}
@@ -108,9 +112,26 @@ def main(argv: list[str] | None = None) -> int:
                 named[k] = json.loads(v)
             except ValueError:
                 named[k] = v
-        status, rep = cli.call_raw({"method": method, "params": named, "id": 1})
+        req = {"method": method, "params": named, "id": 1}
     else:
-        status, rep = cli.call_raw({"method": method, "params": convert_params(method, p), "id": 1})
+        req = {"method": method, "params": convert_params(method, p), "id": 1}
+    wait = args.get_bool("rpcwait", False)
+    while True:  # -rpcwait: retry while the server is down or still warming up (CommandLineRPC)
+        try:
+            status, rep = cli.call_raw(req)
+        except PermissionError as e:
+            print(f"error: {e}", file=sys.stderr)
+            return 1
+        except (ConnectionError, OSError) as e:
+            if not wait:
+                print(f"error: couldn't connect to server: {e}", file=sys.stderr)
+                return 87  # EXIT_FAILURE path of CConnectionFailed in the reference CLI
+            time.sleep(1.0)
+            continue
+        if wait and (rep.get("error") or {}).get("code") == -28:  # RPC_IN_WARMUP
+            time.sleep(1.0)
+            continue
+        break
     if rep.get("error"):
         e = rep["error"]
         print(f"error code: {e.get('code')}\nerror message:\n{e.get('message')}", file=sys.stderr)

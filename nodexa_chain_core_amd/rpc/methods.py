@@ -489,7 +489,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             return _hex(txid)
         if st.coins.get(txid, 0) is not None:
             raise RPCError(RPC_VERIFY_ALREADY_IN_CHAIN, "transaction already in block chain")
-        max_fee = None if _arg(p, 1, False) else 1_000_000 * max(1, len(tx.serialize(True)))  # absurd-fee guard
+        max_fee = None if _arg(p, 1, False) else st.max_tx_fee  # nAbsurdFee = -maxtxfee unless allowhighfees
         ok, reason, _ = st.accept_to_mempool(tx, max_fee=max_fee)
         if not ok:
             code = RPC_TRANSACTION_ERROR if reason == "missing-inputs" else RPC_VERIFY_REJECTED

@@ -580,7 +580,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             tx = _core.Transaction.deserialize(bytes.fromhex(raws[0]))
         except Exception:
             raise RPCError(RPC_DESERIALIZATION_ERROR, "TX decode failed")
-        max_fee = None if _arg(p, 1, False) else 1_000_000 * max(1, len(tx.serialize(True)))
+        max_fee = None if _arg(p, 1, False) else st.max_tx_fee
         ok, why, _ = st.accept_to_mempool(tx, test_only=True, max_fee=max_fee)
         res = {"txid": _hex(tx.txid()), "allowed": ok}
         if not ok:

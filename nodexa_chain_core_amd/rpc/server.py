@@ -4,8 +4,12 @@ Parity:
   * HTTP front-end with a bounded work queue and N worker threads
     (src/httpserver.cpp:68-460, -rpcworkqueue / -rpcthreads, 503 "Work queue
     depth exceeded" when full), persistent connections.
-  * Basic auth against -rpcuser/-rpcpassword or the `.cookie` file
-    (src/httprpc.cpp:128, RPCAuthorized; GenerateAuthCookie).
+  * Basic auth against -rpcuser/-rpcpassword, the `.cookie` file (src/httprpc.cpp:128,
+    RPCAuthorized; GenerateAuthCookie, -rpccookiefile) or -rpcauth user:salt$hmac entries
+    (multiUserAuthorized: HMAC-SHA256 keyed by the salt over the password).
+  * -rpcallowip (ClientAllowed / InitHTTPAllowList: loopback always, then addresses and
+    subnets as CIDR or netmask; 403 for the rest), -rpcthreads workers executing requests,
+    -rpcservertimeout for idle keep-alive connections.
   * Single and batch requests (JSONRPCExecBatch, src/rpc/server.cpp:501),
     error -> HTTP status mapping (JSONErrorReply), warm-up gate (RPC_IN_WARMUP).
   * CRPCTable: category/name/handler/arg names, `help`, positional and named
@@ -15,7 +19,9 @@ The daemon runs this in-process next to the chain state and the GPU miner.
 from __future__ import annotations
 
 import base64
+import hashlib
 import hmac
+import ipaddress
 import http.server
 import json
 import os
@@ -110,9 +116,66 @@ class RPCTable:
             return reply(None, {"code": -1, "message": str(e)}, id_)
 
 
+def parse_allow_subnets(specs: list[str]) -> list:
+    """-rpcallowip values: an address, addr/prefix or addr/netmask (LookupSubNet)."""
+    out = []
+    for s in specs:
+        try:
+            out.append(ipaddress.ip_network(s.strip(), strict=False))
+        except ValueError:
+            raise ValueError(f"Invalid -rpcallowip subnet specification: {s}") from None
+    return out
+
+
+def ip_allowed(ip: str, nets: list) -> bool:
+    try:
+        a = ipaddress.ip_address(ip.split("%")[0])
+    except ValueError:
+        return False
+    if a.is_loopback or (a.version == 6 and a.ipv4_mapped is not None and a.ipv4_mapped.is_loopback):
+        return True
+    if a.version == 6 and a.ipv4_mapped is not None:
+        a = a.ipv4_mapped
+    return any(a.version == n.version and a in n for n in nets)
+
+
+def rpcauth_matches(entries: list[str], user: str, password: str) -> bool:
+    """-rpcauth=<user>:<salt>$<hex hmac_sha256(key=salt, msg=password)>."""
+    for e in entries:
+        name, sep, rest = e.partition(":")
+        salt, sep2, digest = rest.partition("$")
+        if not sep or not sep2 or not hmac.compare_digest(name, user):
+            continue
+        want = hmac.new(salt.encode(), password.encode(), hashlib.sha256).hexdigest()
+        if hmac.compare_digest(want, digest.lower()):
+            return True
+    return False
+
+
 class _Handler(http.server.BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
     server_version = "nodexa-json-rpc/0.1"
+
+    def setup(self):
+        self.timeout = self.server.idle_timeout  # -rpcservertimeout
+        super().setup()
+
+    def handle_one_request(self):
+        if not self.server.client_allowed(self.client_address[0]):  # http_request_cb: ClientAllowed
+            log.log_print("http", f"HTTP request from {self.client_address[0]} rejected: not in -rpcallowip")
+            self.close_connection = True
+            try:
+                self.raw_requestline = self.rfile.readline(65537)
+                self.send_response(403)
+                self.send_header("Content-Length", "0")
+                self.end_headers()
+            except OSError:
+                pass
+            return
+        try:
+            super().handle_one_request()
+        except TimeoutError:
+            self.close_connection = True
 
     def log_message(self, fmt, *args):  # route to category logging
         log.log_print("http", fmt % args)
@@ -132,11 +195,14 @@ class _Handler(http.server.BaseHTTPRequestHandler):
             userpass = base64.b64decode(auth[6:].strip()).decode()
         except Exception:
             return False
-        return any(hmac.compare_digest(userpass, c) for c in self.server.credentials)
+        if any(hmac.compare_digest(userpass, c) for c in self.server.credentials):
+            return True
+        user, _, pw = userpass.partition(":")
+        return rpcauth_matches(self.server.rpcauth, user, pw)
 
     def do_POST(self):  # noqa: N802
         srv: RPCHTTPServer = self.server
-        if srv.credentials and not self._authorized():
+        if (srv.credentials or srv.rpcauth) and not self._authorized():
             log.log_printf(f"ThreadRPCServer incorrect password attempt from {self.client_address[0]}")
             time.sleep(0.25)
             self.send_response(401)
@@ -147,6 +213,7 @@ class _Handler(http.server.BaseHTTPRequestHandler):
         if not srv.slots.acquire(blocking=False):
             self._send(503, b"Work queue depth exceeded", "text/plain")
             return
+        srv.workers.acquire()  # -rpcthreads: requests past the work queue wait for a worker
         try:
             length = int(self.headers.get("Content-Length", "0"))
             raw = self.rfile.read(length)
@@ -164,6 +231,7 @@ class _Handler(http.server.BaseHTTPRequestHandler):
             status = 200 if rep["error"] is None else http_status_for(rep["error"]["code"])
             self._send(status, json.dumps(rep).encode())
         finally:
+            srv.workers.release()
             srv.slots.release()
 
     def do_GET(self):  # noqa: N802
@@ -175,6 +243,9 @@ class _Handler(http.server.BaseHTTPRequestHandler):
                 status, ctype, body = 400, "text/plain", str(e).encode()
             self._send(status, body, ctype)
             return
+        if self.path.startswith("/rest/"):  # -rest off: no handler registered for the prefix
+            self._send(404, b"", "text/plain")
+            return
         self._send(405, b"JSONRPC server handles only POST requests", "text/plain")
 
 
@@ -182,35 +253,50 @@ class RPCHTTPServer(socketserver.ThreadingMixIn, http.server.HTTPServer):
     daemon_threads = True
     allow_reuse_address = True
 
-    def __init__(self, addr, table: RPCTable, credentials: list[str], work_queue: int, rest=None):
+    def __init__(self, addr, table: RPCTable, credentials: list[str], work_queue: int, rest=None,
+                 rpcauth: list[str] | None = None, allow: list | None = None, threads: int = 4,
+                 idle_timeout: float = 30.0):
         super().__init__(addr, _Handler)
         self.table = table
         self.credentials = credentials
-        self.slots = threading.BoundedSemaphore(max(1, work_queue))
+        self.rpcauth = list(rpcauth or [])
+        self.allow = list(allow or [])
+        # -rpcworkqueue bounds the requests admitted (queued + running); -rpcthreads the running
+        self.slots = threading.BoundedSemaphore(max(1, work_queue) + max(1, threads))
+        self.workers = threading.BoundedSemaphore(max(1, threads))
+        self.idle_timeout = idle_timeout
         self.rest = rest
 
+    def client_allowed(self, ip: str) -> bool:
+        return ip_allowed(ip, self.allow)
 
-def make_cookie(datadir: str) -> str:
-    """GenerateAuthCookie: `__cookie__:<64 hex>` in <datadir>/.cookie (0600)."""
+
+def cookie_path(datadir: str, cookiefile: str | None = None) -> str:
+    """GetAuthCookieFile: -rpccookiefile (relative to the data directory) or <datadir>/.cookie."""
+    return os.path.join(datadir, os.path.expanduser(cookiefile or ".cookie"))
+
+
+def make_cookie(datadir: str, cookiefile: str | None = None) -> str:
+    """GenerateAuthCookie: `__cookie__:<64 hex>` in the cookie file (0600)."""
     token = "__cookie__:" + secrets.token_hex(32)
-    path = os.path.join(datadir, ".cookie")
+    path = cookie_path(datadir, cookiefile)
     fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
     with os.fdopen(fd, "w") as f:
         f.write(token)
     return token
 
 
-def delete_cookie(datadir: str) -> None:
+def delete_cookie(datadir: str, cookiefile: str | None = None) -> None:
     try:
-        os.unlink(os.path.join(datadir, ".cookie"))
+        os.unlink(cookie_path(datadir, cookiefile))
     except OSError:
         pass
 
 
 class RPCServer:
     def __init__(self, table: RPCTable, host: str, port: int, credentials: list[str], work_queue: int = 16,
-                 rest=None):
-        self.httpd = RPCHTTPServer((host, port), table, credentials, work_queue, rest)
+                 rest=None, **kw):
+        self.httpd = RPCHTTPServer((host, port), table, credentials, work_queue, rest, **kw)
         self.port = self.httpd.server_address[1]
         self.thread = threading.Thread(target=self.httpd.serve_forever, name="http", daemon=True)
 

@@ -7,6 +7,7 @@ LogAcceptCategory (src/util.h:116), `-debug=<cat>` / `-debugexclude`,
 """
 from __future__ import annotations
 
+import os
 import sys
 import threading
 import time
@@ -23,12 +24,44 @@ _lock = threading.Lock()
 _enabled: set[str] = set()
 _file = None
 _print_to_console = True
+_timestamps = True   # -logtimestamps
+_micros = False      # -logtimemicros
+log_ips = False      # -logips: peer addresses in net log lines
+RECENT_DEBUG_HISTORY_SIZE = 10 * 1_000_000
+
+
+def timestamp_format(t: float) -> str:
+    s = time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(t))
+    return s + (".%06dZ" % int(round((t % 1) * 1e6)) if _micros else "Z")
+
+
+def shrink_debug_file(path: str) -> None:
+    """ShrinkDebugFile (src/util.cpp): past 11 MB keep the last 10 MB, cut at a line start."""
+    try:
+        size = os.path.getsize(path)
+    except OSError:
+        return
+    if size <= RECENT_DEBUG_HISTORY_SIZE * 11 // 10:
+        return
+    with open(path, "rb") as f:
+        f.seek(size - RECENT_DEBUG_HISTORY_SIZE)
+        tail = f.read()
+    nl = tail.find(b"\n")
+    tail = tail[nl + 1:] if 0 <= nl < len(tail) - 1 else tail
+    tmp = path + ".shrink"
+    with open(tmp, "wb") as f:
+        f.write(tail)
+    os.replace(tmp, path)
 
 
 def configure(debug: list[str], exclude: list[str] | None = None, logfile: str | None = None,
-              console: bool = True) -> None:
-    global _file, _print_to_console
+              console: bool = True, timestamps: bool = True, micros: bool = False, ips: bool = False,
+              shrink: bool | None = None) -> None:
+    global _file, _print_to_console, _timestamps, _micros, log_ips
+    if logfile and (shrink if shrink is not None else not debug):  # -shrinkdebugfile (default !fDebug)
+        shrink_debug_file(logfile)
     with _lock:
+        _timestamps, _micros, log_ips = timestamps, micros, ips
         _enabled.clear()
         if any(d in ("1", "all") for d in debug):
             _enabled.update(CATEGORIES)
@@ -66,7 +99,7 @@ def active() -> dict[str, bool]:
 
 
 def log_printf(msg: str) -> None:
-    line = time.strftime("%Y-%m-%dT%H:%M:%SZ ", time.gmtime()) + msg.rstrip("\n")
+    line = (timestamp_format(time.time()) + " " if _timestamps else "") + msg.rstrip("\n")
     with _lock:
         if _file is not None:
             _file.write(line + "\n")

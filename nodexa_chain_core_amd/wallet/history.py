@@ -40,6 +40,7 @@ class WalletTx:
 class WalletHistory(ValidationInterface):
     def __init__(self, wallet, path: str | None):
         self.w = wallet
+        self.on_change = None  # callable(txid) for -walletnotify
         self.state = wallet.state
         self.path = path
         self.lock = threading.RLock()
@@ -119,15 +120,19 @@ class WalletHistory(ValidationInterface):
         txid = tx.txid()
         with self.lock:
             w = self.txs.get(txid)
+            new = w is None
             if w is None:
                 if not self.involves_me(tx):
                     return False
                 w = self.txs[txid] = WalletTx(tx, int(time.time()), order=len(self.txs))
+            updated = block is not None and w.block != block
             if block is not None:
                 w.block = block
                 w.abandoned = False
         if save:
             self.save()
+        if (new or updated) and self.on_change is not None:  # AddToWallet -> -walletnotify
+            self.on_change(txid)
         return True
 
     # ValidationInterface

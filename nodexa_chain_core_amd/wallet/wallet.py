@@ -142,6 +142,10 @@ class Wallet:
         self.pay_tx_fee = 0               # settxfee / -paytxfee (sat per kvB; 0 = use fee estimation)
         self.fallback_fee = DEFAULT_FEE_RATE  # -fallbackfee: used while the estimator has no answer
         self.tx_confirm_target = DEFAULT_TX_CONFIRM_TARGET  # -txconfirmtarget
+        self.min_tx_fee = DEFAULT_TRANSACTION_MINFEE  # -mintxfee (sat per kvB)
+        self.max_tx_fee: int | None = None            # -maxtxfee cap on one transaction's fee (None: node's)
+        self.keypool_size = DEFAULT_KEYPOOL_SIZE      # -keypool
+        self.broadcast = True                         # -walletbroadcast
         self.hdpath: dict[bytes, str] = {}      # hdkeypath of derived keys
         self.pool: list[bytes] = []             # keypool: reserved keys not yet handed out
         self.hd: dict | None = None             # {"master_id", "next", "seed", "seed_crypted"}
@@ -168,7 +172,7 @@ class Wallet:
             if est is not None:
                 rate, _, _, _ = est.estimate_smart_fee(self.tx_confirm_target, not self.walletrbf)
             rate = rate or self.fallback_fee
-        floor = max(DEFAULT_TRANSACTION_MINFEE, getattr(self.state, "min_relay_fee", 0) if self.state else 0)
+        floor = max(self.min_tx_fee, getattr(self.state, "min_relay_fee", 0) if self.state else 0)
         return max(rate, floor)
 
     @fee_rate.setter
@@ -360,7 +364,8 @@ class Wallet:
                 raise WalletError("Error: Keypool ran out, please call keypoolrefill first")
             return self.address_of(self._fresh_key(label))
 
-    def keypool_refill(self, size: int = DEFAULT_KEYPOOL_SIZE) -> None:
+    def keypool_refill(self, size: int | None = None) -> None:
+        size = self.keypool_size if size is None else size
         with self.lock:
             if self.mkey is not None and self._master is None:
                 raise WalletError(UNLOCK_NEEDED)
@@ -724,7 +729,7 @@ class Wallet:
                 raise WalletError(f"Signing transaction failed: {errors}")
             size = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4
             size += 110 * len(errors)  # inputs left for another signer: a P2PKH-sized scriptSig each
-            want = max(1, fee_rate * size // 1000)
+            want = self._capped_fee(max(1, fee_rate * size // 1000))
             if fee >= want:
                 return tx, fee
             fee = want + 68
@@ -784,7 +789,7 @@ class Wallet:
             if not complete:
                 raise WalletError(f"Signing transaction failed: {errors}")
             size = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4
-            want_fee = max(1, fee_rate * size // 1000)
+            want_fee = self._capped_fee(max(1, fee_rate * size // 1000))
             if fee >= want_fee:
                 return tx, fee
             fee = want_fee + 68  # headroom for a changed signature size
@@ -798,10 +803,19 @@ class Wallet:
                                         replaceable=replaceable, from_scripts=from_scripts, change_spk=change_spk)
         return self.commit(tx, comment, comment_to, from_account)
 
+    def _capped_fee(self, fee: int) -> int:
+        """GetMinimumFee's last step: never above -maxtxfee (CreateTransaction then reports
+        "Fee exceeds maximum configured by -maxtxfee" if the cap cannot pay the relay fee)."""
+        cap = self.max_tx_fee if self.max_tx_fee is not None else getattr(self.state, "max_tx_fee", None)
+        if cap is not None and fee > cap:
+            raise WalletError("Fee exceeds maximum configured by -maxtxfee")
+        return fee
+
     def commit(self, tx, comment: str = "", comment_to: str = "", from_account: str | None = None) -> bytes:
-        ok, reason, _ = self.state.accept_to_mempool(tx)
-        if not ok:
-            raise WalletError(f"Transaction rejected: {reason}")
+        if self.broadcast:  # -walletbroadcast=0: recorded in the wallet, never submitted or relayed
+            ok, reason, _ = self.state.accept_to_mempool(tx)
+            if not ok:
+                raise WalletError(f"Transaction rejected: {reason}")
         if self.history is not None:
             self.history.add(tx)
             w = self.history.txs.get(tx.txid())

@@ -1,0 +1,221 @@
+"""Operator flags of the reference daemon that shape the RPC server, notifications, logging and
+the process (src/init.cpp, src/httpserver.cpp, src/httprpc.cpp):
+
+* -rpcauth=<user>:<salt>$<hmac-sha256(salt, password)> (share/rpcauth; multiUserAuthorized),
+  -rpcallowip (ClientAllowed: loopback always, others by address or subnet, 403 otherwise),
+  -rpcthreads (workers executing requests), -rpcservertimeout, -rpccookiefile, -rest (off by
+  default, as DEFAULT_REST_ENABLE);
+* -blocknotify / -walletnotify with "%s" substitution;
+* -logtimestamps / -logtimemicros, -shrinkdebugfile, -pid.
+"""
+import base64
+import hashlib
+import hmac
+import http.client
+import json
+import os
+import time
+
+import pytest
+
+from test_node_rpc import client, node_factory  # noqa: F401 — shared fixtures
+from wallet_util import fund
+
+
+def _post(port, user, pw, method="getblockcount"):
+    conn = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+    tok = base64.b64encode(f"{user}:{pw}".encode()).decode()
+    conn.request("POST", "/", json.dumps({"id": 1, "method": method, "params": []}),
+                 {"Authorization": "Basic " + tok, "Content-Type": "application/json"})
+    r = conn.getresponse()
+    body = r.read()
+    conn.close()
+    return r.status, body
+
+
+def _wait_for(pred, timeout=10.0):
+    end = time.time() + timeout
+    while time.time() < end:
+        if pred():
+            return True
+        time.sleep(0.05)
+    return False
+
+
+def test_rpcauth_allowip_and_rest_default(core, node_factory):  # noqa: F811
+    salt = "cb77f0957de88ff388cf817ddbc7273"
+    digest = hmac.new(salt.encode(), b"hunter2", hashlib.sha256).hexdigest()
+    node, _ = node_factory((f"-rpcauth=alice:{salt}${digest}", "-rpcallowip=10.0.0.0/8", "-rpcthreads=2",
+                            "-norest"))
+    port = node.rpc.port
+    assert _post(port, "alice", "hunter2")[0] == 200
+    assert _post(port, "alice", "wrong")[0] == 401
+    assert _post(port, "u", "p")[0] == 200  # -rpcuser / -rpcpassword still work next to -rpcauth
+    srv = node.rpc.httpd
+    assert srv.client_allowed("127.0.0.1") and srv.client_allowed("::1")
+    assert srv.client_allowed("10.1.2.3") and not srv.client_allowed("192.168.1.1")
+    conn = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+    conn.request("GET", "/rest/chaininfo.json")
+    assert conn.getresponse().status == 404  # REST is opt-in (-rest)
+    conn.close()
+
+
+def test_rpc_allowip_subnet_forms():
+    from nodexa_chain_core_amd.rpc.server import parse_allow_subnets
+
+    nets = parse_allow_subnets(["192.168.0.0/255.255.0.0", "172.16.5.4", "fd00::/8"])
+    from nodexa_chain_core_amd.rpc.server import ip_allowed
+
+    assert ip_allowed("192.168.7.9", nets) and ip_allowed("172.16.5.4", nets) and ip_allowed("fd00::1", nets)
+    assert not ip_allowed("172.16.5.5", nets) and not ip_allowed("8.8.8.8", nets)
+    with pytest.raises(ValueError):
+        parse_allow_subnets(["not-an-ip"])
+
+
+def test_notifications_and_logging(core, node_factory, tmp_path):  # noqa: F811
+    blk = tmp_path / "blocks.txt"
+    wtx = tmp_path / "wallet.txt"
+    node, addr = node_factory((f"-blocknotify=echo %s >> {blk}", f"-walletnotify=echo %s >> {wtx}",
+                               "-logtimemicros", "-pid=nodexa_test.pid", "-rest"))
+    c = client(node)
+    h = c.generatetoaddress(2, addr)
+    assert _wait_for(lambda: blk.exists() and len(blk.read_text().split()) >= 2)
+    assert set(blk.read_text().split()) >= set(h)
+    w = fund(c, 101)
+    txid = c.sendtoaddress(w, 1.0)
+    assert _wait_for(lambda: wtx.exists() and txid in wtx.read_text().split())
+    pidfile = os.path.join(node.datadir, "nodexa_test.pid")
+    assert open(pidfile).read().strip() == str(os.getpid())
+    from nodexa_chain_core_amd.utils import log
+
+    assert log.timestamp_format(1_700_000_000.123456).endswith(".123456Z")
+    conn = http.client.HTTPConnection("127.0.0.1", node.rpc.port, timeout=5)
+    conn.request("GET", "/rest/chaininfo.json")
+    assert conn.getresponse().status == 200
+    conn.close()
+    node.stop()
+    assert not os.path.exists(pidfile)
+
+
+def test_shrink_debug_file(tmp_path):
+    from nodexa_chain_core_amd.utils import log
+
+    p = tmp_path / "debug.log"
+    p.write_bytes(b"x" * (12 * 1_000_000) + b"\nlast line\n")
+    log.shrink_debug_file(str(p))
+    data = p.read_bytes()
+    assert len(data) <= 10 * 1_000_000 + 16 and data.endswith(b"last line\n")
+    small = tmp_path / "small.log"
+    small.write_bytes(b"keep\n")
+    log.shrink_debug_file(str(small))
+    assert small.read_bytes() == b"keep\n"
+
+
+def test_relay_package_and_block_policy_flags(core, node_factory):  # noqa: F811
+    """-datacarrier, -limitancestorcount, -maxtxfee, -blockmintxfee and -mempoolexpiry."""
+    from wallet_util import spend
+
+    node, addr = node_factory(("-acceptnonstdtxn=0", "-datacarrier=0", "-limitancestorcount=2", "-maxtxfee=0.5",
+                               "-blockmintxfee=0.05", "-mempoolexpiry=1"))
+    c = client(node)
+    w = fund(c, 110)
+    coins = sorted((u for u in c.listunspent() if u["spendable"]), key=lambda u: u["txid"])
+    # -datacarrier=0: an OP_RETURN output is non-standard
+    u = coins.pop()
+    raw = c.createrawtransaction([{"txid": u["txid"], "vout": u["vout"]}], {"data": "00" * 8, w: 1.0})
+    signed = c.signrawtransaction(raw)["hex"]
+    assert c.testmempoolaccept([signed])[0]["reject-reason"].endswith("scriptpubkey")
+    # -maxtxfee=0.5: a 1 CLORE fee is absurd unless allowhighfees
+    u = coins.pop()
+    hi = spend(c, u["txid"], u["vout"], u["amount"], w, 1.0, fee=1.0)
+    with pytest.raises(RuntimeError, match="absurdly-high-fee"):
+        c.sendrawtransaction(hi)
+    assert c.sendrawtransaction(hi, True)
+    # -limitancestorcount=2: a third unconfirmed generation is refused
+    u = coins.pop()
+    t1 = c.sendrawtransaction(spend(c, u["txid"], u["vout"], u["amount"], w, 5.0))
+    t2 = c.sendrawtransaction(spend(c, t1, 0, 5.0, w, 4.0))
+    t3 = spend(c, t2, 0, 4.0, w, 3.0)
+    with pytest.raises(RuntimeError, match="too-long-mempool-chain"):
+        c.sendrawtransaction(t3)
+    # -blockmintxfee=0.05 CLORE/kB: the 0.01-fee transactions (~4.4M sat/kB) stay out of templates
+    # while the 1 CLORE one (above the floor) goes in
+    tpl = {t["txid"] for t in c.getblocktemplate({"rules": ["segwit"]})["transactions"]}
+    assert t1 not in tpl and t2 not in tpl and c.decoderawtransaction(hi)["txid"] in tpl
+    # -mempoolexpiry=1 (hour): two hours later the next admission expires the old entries
+    pool_before = set(c.getrawmempool())
+    assert {t1, t2} <= pool_before
+    c.setmocktime(int(time.time()) + 2 * 3600)
+    u = coins.pop()
+    fresh = c.sendrawtransaction(spend(c, u["txid"], u["vout"], u["amount"], w, 1.0))
+    assert set(c.getrawmempool()) == {fresh}
+    c.setmocktime(0)
+
+
+def test_wallet_flags(core, node_factory, tmp_path):  # noqa: F811
+    """-keypool, -mintxfee, -maxtxfee (wallet cap) and -walletbroadcast=0."""
+    node, addr = node_factory(("-keypool=5", "-mintxfee=0.05", "-walletbroadcast=0"))
+    c = client(node)
+    assert len(node.wallet.pool) >= 5 or node.wallet.keypool_size == 5
+    w = fund(c, 101)
+    txid = c.sendtoaddress(w, 1.0)
+    assert txid not in c.getrawmempool()  # recorded in the wallet, not broadcast
+    t = c.gettransaction(txid)
+    size = len(bytes.fromhex(t["hex"]))
+    assert -t["fee"] * 1e8 * 1000 / size >= 5_000_000 * 0.99  # -mintxfee floor (sat per kB)
+    node.stop()
+    os.makedirs(tmp_path / "n2", exist_ok=True)
+    node2, _ = node_factory((f"-datadir={tmp_path / 'n2'}", "-maxtxfee=0.0001"))
+    c2 = client(node2)
+    w2 = fund(c2, 101)
+    with pytest.raises(RuntimeError, match="maxtxfee"):
+        c2.sendtoaddress(w2, 1.0)
+
+
+def test_p2p_flags(core, node_factory, tmp_path):  # noqa: F811
+    """-uacomment, -whitelist, -blocksonly, -peerbloomfilters=0 and -externalip."""
+    a, addr = node_factory(("-listen=1", "-port=0", "-listenonion=0", "-uacomment=gpu-node", "-whitelist=127.0.0.1",
+                            "-blocksonly", "-peerbloomfilters=0", "-externalip=203.0.113.7"))
+    client(a).generatetoaddress(2, addr)
+    os.makedirs(tmp_path / "b", exist_ok=True)
+    b, _ = node_factory((f"-datadir={tmp_path / 'b'}", f"-connect=127.0.0.1:{a.connman.port}"))
+    cb = client(b)
+    assert _wait_for(lambda: cb.getblockcount() == 2, 20)
+    peer_a = cb.getpeerinfo()[0]
+    assert peer_a["subver"].endswith("(gpu-node)/")
+    assert int(peer_a["services"], 16) & (1 << 2) == 0  # NODE_BLOOM off
+    assert peer_a["relaytxes"] is False                  # -blocksonly announces relay=false
+    ca = client(a)
+    assert _wait_for(lambda: ca.getpeerinfo() and ca.getpeerinfo()[0]["whitelisted"] is True)
+    local = {(x["address"], x["port"]) for x in ca.getnetworkinfo()["localaddresses"]}
+    assert ("203.0.113.7", a.connman.port) in local
+    # a bloom filter message to a node without NODE_BLOOM costs the peer 100 points, but a
+    # whitelisted peer is never banned
+    peer_b = a.connman.peers[0]
+    a.connman.on_filterload(peer_b, b"\x01\x00" + bytes(9))
+    assert peer_b.misbehavior >= 100 and not a.connman.is_banned("127.0.0.1")
+
+
+def test_cli_stdin_and_rpcwait(core, node_factory, tmp_path, capsys, monkeypatch):  # noqa: F811
+    import io
+
+    from nodexa_chain_core_amd.rpc import client as cli
+
+    node, addr = node_factory()
+    port = node.rpc.port
+    base = ["-regtest", "-rpcuser=u", "-rpcpassword=p", f"-rpcport={port}"]
+    monkeypatch.setattr("sys.stdin", io.StringIO("1\n"))
+    assert cli.main(base + ["-stdin", "getblockhash"]) == 8  # abs(RPC_INVALID_PARAMETER): no height 1 yet
+    client(node).generatetoaddress(1, addr)
+    monkeypatch.setattr("sys.stdin", io.StringIO("1\n"))
+    capsys.readouterr()
+    assert cli.main(base + ["-stdin", "getblockhash"]) == 0
+    assert len(capsys.readouterr().out.strip()) == 64
+    # nothing listens on this port: without -rpcwait the CLI fails at once
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    dead = s.getsockname()[1]
+    s.close()
+    assert cli.main(["-regtest", "-rpcuser=u", "-rpcpassword=p", f"-rpcport={dead}", "getblockcount"]) != 0

@@ -74,7 +74,9 @@ def test_consensus_rejections(core, node_factory):  # noqa: F811
     nofee = spend(c, first["txid"], first["vout"], first["amount"], ext, first["amount"], fee=0)
     with pytest.raises(RuntimeError, match="min relay fee"):
         c.sendrawtransaction(nofee)
-    # a fee far above the absurd-fee cap is refused unless allowhighfees
+    # a fee above -maxtxfee (nAbsurdFee; the reference default is 1000 CLORE, lowered here to
+    # 100 so a regtest coinbase can exceed it) is refused unless allowhighfees
+    node.state.max_tx_fee = 100 * 100_000_000
     high = spend(c, first["txid"], first["vout"], first["amount"], ext, 1.0, fee=first["amount"] - 1.0)
     with pytest.raises(RuntimeError, match="absurdly-high-fee"):
         c.sendrawtransaction(high)
