@@ -25,6 +25,7 @@ rebuilt from genesis.
 from __future__ import annotations
 
 import os
+import random
 import struct
 import threading
 import time
@@ -114,6 +115,7 @@ DEFAULT_DESCENDANT_LIMIT, DEFAULT_DESCENDANT_SIZE_LIMIT = 200, 250
 DEFAULT_MEMPOOL_EXPIRY = 336                                          # hours
 DEFAULT_TRANSACTION_MAXFEE = 1000 * 100_000_000
 DEFAULT_BLOCK_MIN_TX_FEE = 1000                                       # sat per kvB (src/policy/policy.h:26)
+DEFAULT_MAX_TIP_AGE = 24 * 60 * 60                                    # -maxtipage (src/validation.h)
 MAX_STANDARD_SCRIPTSIG_SIZE = 1650
 GPU_SIG_BATCH_MIN = 16                 # below this many signatures a block is checked on the host
 
@@ -176,6 +178,13 @@ class ChainState:
         self.block_max_weight = 7_999_000                           # -blockmaxweight
         self.block_max_size: int | None = None                      # -blockmaxsize
         self.block_min_fee_rate = DEFAULT_BLOCK_MIN_TX_FEE          # -blockmintxfee
+        self.assume_valid: bytes | None = None                      # -assumevalid (block hash, storage order)
+        self.minimum_chain_work = 0                                 # -minimumchainwork
+        self.max_tip_age = DEFAULT_MAX_TIP_AGE                      # -maxtipage
+        self.importing = False                                      # -loadblock / -reindex in progress
+        self._ibd_latched = False
+        self.scripts_skipped = 0                                    # blocks connected under -assumevalid
+        self.db_crash_ratio = 0                                     # -dbcrashratio fault injection
         self.script_threads = min(16, os.cpu_count() or 1)  # -par: script-check threads (CCheckQueue)
         self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
         self.flush_interval = 1000
@@ -383,6 +392,39 @@ class ChainState:
         if self.mempool.pop(txid, None) is not None:
             self.fee_estimator.remove_tx(txid, in_block)
 
+    def is_initial_block_download(self) -> bool:
+        """IsInitialBlockDownload (src/validation.cpp): importing, a tip with less work than
+        -minimumchainwork, or a tip older than -maxtipage; once false it stays false (latched)."""
+        if self._ibd_latched:
+            return False
+        tip = self.coins_tip()
+        if self.importing or tip is None or tip.chain_work < self.minimum_chain_work:
+            return True
+        if tip.time < self.adjusted_time() - self.max_tip_age:
+            return True
+        self._ibd_latched = True
+        return False
+
+    def _assumed_valid(self, idx) -> bool:
+        """ConnectBlock's fScriptChecks = false: `idx` is an ancestor of the -assumevalid block and
+        of the best header, and the best header has at least -minimumchainwork."""
+        if self.assume_valid is None:
+            return False
+        av = self.chain.find(self.assume_valid)
+        if av is None or av.height < idx.height:
+            return False
+        best = self.chain.tip()
+        if best.chain_work < self.minimum_chain_work:
+            return False
+
+        def ancestor(i, h):
+            while i is not None and i.height > h:
+                i = self.chain.find(i.prev_hash)
+            return i
+
+        a1, a2 = ancestor(av, idx.height), ancestor(best, idx.height)
+        return a1 is not None and a2 is not None and a1.hash == idx.hash and a2.hash == idx.hash
+
     def is_current_for_fee_estimation(self) -> bool:
         """IsCurrentForFeeEstimation (src/validation.cpp): the tip is under 3 hours old and
         within one block of the best header."""
@@ -445,6 +487,52 @@ class ChainState:
                 out.add(t)
                 todo.extend(children.get(t, ()))
         return out
+
+    def load_external_block_file(self, path: str) -> int:
+        """LoadExternalBlockFile (-loadblock, bootstrap.dat): scan for the network magic, read
+        each `magic | u32 size | block` record, and process blocks whose parent is known; blocks
+        that arrive before their parent wait until it is connected. Returns blocks accepted."""
+        magic = bytes(self.params.message_start)
+        act = self.params.kawpow_activation_time
+        with open(path, "rb") as f:
+            data = f.read()
+        waiting: dict[bytes, list] = {}
+        n, off = 0, 0
+
+        def process(blk) -> int:
+            if not self.process_new_block(blk, check_pow=True).ok:
+                return 0
+            done, todo = 1, [self.block_hash(blk.header)]
+            while todo:
+                for child in waiting.pop(todo.pop(), []):
+                    if self.process_new_block(child, check_pow=True).ok:
+                        done += 1
+                        todo.append(self.block_hash(child.header))
+            return done
+
+        while True:
+            off = data.find(magic, off)
+            if off < 0 or off + 8 > len(data):
+                break
+            size = struct.unpack_from("<I", data, off + 4)[0]
+            start = off + 8
+            if size < 80 or start + size > len(data):
+                off += 1
+                continue
+            try:
+                blk = _core.Block.deserialize(data[start:start + size], act)
+            except Exception:
+                off += 1
+                continue
+            off = start + size
+            h = self.block_hash(blk.header)
+            if self.chain.find(h) is not None and h in self.block_pos:
+                continue
+            if self.chain.find(blk.header.prev) is None:
+                waiting.setdefault(blk.header.prev, []).append(blk)
+                continue
+            n += process(blk)
+        return n
 
     def save_mempool(self, path: str) -> int:
         """DumpMempool (src/validation.cpp): version, count, then per tx the witness
@@ -696,12 +784,15 @@ class ChainState:
             return self.chain.at_height(h).median_time_past()
 
         flags = _core.BLOCK_SCRIPT_VERIFY_FLAGS
-        gpu = self._use_gpu_for(block)
+        check_scripts = not self._assumed_valid(idx)
+        if not check_scripts:
+            self.scripts_skipped += 1
+        gpu = check_scripts and self._use_gpu_for(block)
         par = self.script_threads
         aflags = self.asset_flags(prev)
 
         def connect(defer: bool):
-            return _core.connect_block(block, height, self.coins, True, defer, mtp_at, mtp_prev, flags, par,
+            return _core.connect_block(block, height, self.coins, check_scripts, defer, mtp_at, mtp_prev, flags, par,
                                        self.assets, aflags, idx.hash)
 
         res, undo = connect(gpu)
@@ -755,6 +846,11 @@ class ChainState:
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, self.assets_path)
+        if self.db_crash_ratio and random.randrange(self.db_crash_ratio) == 0:
+            # -dbcrashratio (CCoinsViewDB::BatchWrite, src/txdb.cpp:96): die between the two halves
+            # of the flush; start-up must notice the mismatch and replay (feature_dbcrash.py)
+            log.log_printf("Simulating a crash. Goodbye.")
+            os._exit(0)
         if any(self.index_flags.values()):
             tmp = self.indexes_path + ".new"
             with open(tmp, "wb") as f:

@@ -154,6 +154,15 @@ class Node:
             self.state.incremental_relay_fee = round(float(a.get("incrementalrelayfee")) * 100_000_000)
         self.state.enable_replacement = a.get_bool("mempoolreplacement", self.state.enable_replacement)
         st, coin = self.state, 100_000_000  # relay / package / block policy knobs (src/init.cpp)
+        av = a.get("assumevalid", self.params_assume_valid())  # -assumevalid=<hex>; 0 = check every script
+        st.assume_valid = None if av in (None, "", "0") else bytes.fromhex(av.rjust(64, "0"))[::-1]
+        if a.get("minimumchainwork"):
+            st.minimum_chain_work = int(a.get("minimumchainwork"), 16)
+        st.max_tip_age = a.get_int("maxtipage", st.max_tip_age)
+        st.db_crash_ratio = a.get_int("dbcrashratio", 0)
+        for spec in a.get_list("vbparams"):  # -vbparams=deployment:start:end (regtest only)
+            self._apply_vbparams(spec)
+        self._verify_db(a.get_int("checkblocks", 6), a.get_int("checklevel", 3))
         st.datacarrier = a.get_bool("datacarrier", True)
         st.datacarrier_size = a.get_int("datacarriersize", st.datacarrier_size)
         st.permit_bare_multisig = a.get_bool("permitbaremultisig", True)
@@ -250,11 +259,78 @@ class Node:
                         node.request_shutdown()
 
             self.state.register(_StopAt())
+        if a.get_list("loadblock"):
+            self._import_blocks(a.get_list("loadblock"))
         self.table.warmup = None
         log.log_printf(f"nodexad started: network={self.network} height={self.state.height()} "
                        f"kawpow_activation={self.params.kawpow_activation_time} gpus={self.gpus or 'none'}")
         if a.get_bool("gen", False) and self.network != "regtest":
             self.miner.set_generate(True, self.mining_script)
+
+    def params_assume_valid(self) -> str | None:
+        """consensus.defaultAssumeValid: none is set for these networks here (the reference's main
+        value names a block of its own chain, which a fresh datadir would not have)."""
+        return None
+
+    def _apply_vbparams(self, spec: str) -> None:
+        if self.network != "regtest":
+            raise SystemExit("Version bits parameters may only be overridden on regtest.")
+        import dataclasses
+
+        parts = spec.split(":")
+        if len(parts) != 3:
+            raise SystemExit("Version bits parameters malformed, expecting deployment:start:end")
+        name, start, end = parts[0], int(parts[1]), int(parts[2])
+        vb = self.state.versionbits
+        for i, d in enumerate(vb.deployments):
+            if d.name == name:
+                vb.deployments = list(vb.deployments)
+                vb.deployments[i] = dataclasses.replace(d, start=start, timeout=end)
+                vb._cache.clear()
+                log.log_printf(f"Setting version bits activation parameters for {name} to start={start}, timeout={end}")
+                return
+        raise SystemExit(f"Invalid deployment ({name})")
+
+    def _verify_db(self, nblocks: int, level: int) -> None:
+        """CVerifyDB at start-up (-checkblocks / -checklevel): the last blocks must read back,
+        pass CheckBlock and their proof of work (level >= 1), and have undo data (level >= 2)."""
+        st = self.state
+        tip = st.tip()
+        if nblocks <= 0 or tip is None or tip.height == 0 or st.store is None:
+            return
+        for h in range(max(1, tip.height - nblocks + 1), tip.height + 1):
+            idx = st.chain.at_height(h)
+            blk = st.get_block(idx.hash)
+            if blk is None:
+                raise SystemExit(f"Corrupted block database detected: block {h} unreadable (use -reindex)")
+            if level >= 1 and not (_core.check_block(blk, self.params, True)[0]
+                                   and _core.check_proof_of_work(st.block_hash(blk.header), blk.header.bits, self.params)):
+                raise SystemExit(f"Corrupted block database detected: block {h} invalid (use -reindex)")
+            if level >= 2:
+                try:
+                    ok = st.undo.read(idx.hash, idx.prev_hash) is not None
+                except IOError:
+                    ok = False
+                if not ok:
+                    raise SystemExit(f"Corrupted block database detected: bad undo data for block {h} (use -reindex)")
+        log.log_printf(f"Verified the last {min(nblocks, tip.height)} blocks at level {level}")
+
+    def _import_blocks(self, files: list[str]) -> None:
+        """ThreadImport: -loadblock files, then -stopafterblockimport."""
+        st = self.state
+        st.importing = True
+        try:
+            for path in files:
+                try:
+                    n = st.load_external_block_file(os.path.expanduser(path))
+                    log.log_printf(f"Imported {n} blocks from {path}")
+                except OSError as e:
+                    log.log_printf(f"Warning: Could not open blocks file {path}: {e}")
+        finally:
+            st.importing = False
+        if self.args.get_bool("stopafterblockimport", False):
+            log.log_printf("Stopping after block import")
+            self.request_shutdown()
 
     def asset_wallet_instance(self):
         """The node's AssetWallet, built on first use (shared by the asset, message and reward RPCs)."""

@@ -217,6 +217,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         return {"chain": params.network_id, "blocks": tip.height, "headers": st.chain.height(),
                 "bestblockhash": _hex(tip.hash), "difficulty": _core.difficulty_from_bits(tip.bits),
                 "mediantime": tip.median_time_past(), "verificationprogress": 1.0,
+                "initialblockdownload": st.is_initial_block_download(),
                 "chainwork": "%064x" % tip.chain_work, "size_on_disk": node.blocks_size_on_disk(),
                 "pruned": False, "warnings": "",
                 "bip9_softforks": st.versionbits.bip9_softforks(tip),

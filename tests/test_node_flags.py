@@ -219,3 +219,75 @@ def test_cli_stdin_and_rpcwait(core, node_factory, tmp_path, capsys, monkeypatch
     dead = s.getsockname()[1]
     s.close()
     assert cli.main(["-regtest", "-rpcuser=u", "-rpcpassword=p", f"-rpcport={dead}", "getblockcount"]) != 0
+
+
+def test_chain_flags_loadblock_assumevalid_vbparams_checkblocks(core, node_factory, tmp_path):  # noqa: F811
+    """-loadblock (+ -stopafterblockimport), -assumevalid, -vbparams, -checkblocks/-checklevel and
+    getblockchaininfo.initialblockdownload."""
+    src, addr = node_factory((f"-datadir={tmp_path / 'src'}",) if os.makedirs(tmp_path / "src") is None else ())
+    c = client(src)
+    hashes = c.generatetoaddress(12, addr)
+    assert c.getblockchaininfo()["initialblockdownload"] is False
+    headers = [src.state.get_block(bytes.fromhex(h)[::-1]).header for h in hashes]
+    src.stop()
+    blk0 = os.path.join(src.datadir, "blocks", "blk00000.dat")
+    # import the first node's block file into a fresh node, with every script check skipped up to
+    # the assumed-valid tip
+    os.makedirs(tmp_path / "dst")
+    dst, _ = node_factory((f"-datadir={tmp_path / 'dst'}", f"-loadblock={blk0}", f"-assumevalid={hashes[-1]}",
+                           "-vbparams=testdummy:0:1", "-checkblocks=12", "-checklevel=3"))
+    cd = client(dst)
+    assert cd.getblockcount() == 12 and cd.getbestblockhash() == hashes[-1]
+    # blocks read one by one: the assumed-valid header is known only when its own block arrives,
+    # so only that block skips its scripts (as LoadExternalBlockFile in the reference)
+    assert dst.state.scripts_skipped == 1
+    td = {d.name: d for d in dst.state.versionbits.deployments}["testdummy"]
+    assert (td.start, td.timeout) == (0, 1)
+    dst.stop()
+    # restart with start-up block verification over the imported chain
+    dst2, _ = node_factory((f"-datadir={tmp_path / 'dst'}", "-checkblocks=12", "-checklevel=2"))
+    assert client(dst2).getblockcount() == 12
+    dst2.stop()
+    # headers first (as P2P sync delivers them): every ancestor of the assumed-valid block skips
+    os.makedirs(tmp_path / "hf")
+    hf, _ = node_factory((f"-datadir={tmp_path / 'hf'}", f"-assumevalid={hashes[-1]}"))
+    res = hf.state.chain.accept_headers(headers, int(time.time()) + 7200, True)
+    assert all(r.ok for r in res)
+    assert hf.state.load_external_block_file(blk0) == 12 and hf.state.scripts_skipped == 12
+    hf.stop()
+    with pytest.raises(SystemExit, match="regtest|malformed|Invalid deployment"):
+        node_factory((f"-datadir={tmp_path / 'dst'}", "-vbparams=nosuch:0:1"))
+
+
+def test_dbcrashratio_crash_and_recovery(core, node_factory, tmp_path):  # noqa: F811
+    """-dbcrashratio=1 kills the daemon between the asset and UTXO snapshot writes of its flush
+    (feature_dbcrash.py); the next start notices the mismatch and replays the blocks."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = tmp_path / "crash"
+    os.makedirs(d)
+    code = f"""
+import sys
+sys.path.insert(0, {root!r})
+from nodexa_chain_core_amd.node import Node
+from nodexa_chain_core_amd.utils.config import ArgsManager
+from nodexa_chain_core_amd import _core
+a = ArgsManager()
+a.parse_parameters(["-regtest", "-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p", "-printtoconsole=0",
+                    "-dbcrashratio=1"])
+n = Node(a)
+n.start()
+addr = _core.base58check_encode(bytes([42]) + bytes(range(20)))
+from nodexa_chain_core_amd.rpc.client import RPCClient
+RPCClient("127.0.0.1", n.rpc.port, "u", "p").generatetoaddress(5, addr)
+n.stop()
+print("not reached")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "not reached" not in r.stdout, r.stderr[-2000:]
+    assert os.path.exists(d / "regtest" / "chainstate" / "assets.dat") or os.path.exists(d / "chainstate" / "assets.dat")
+    node, _ = node_factory((f"-datadir={d}",))
+    assert client(node).getblockcount() == 5
+    assert client(node).gettxoutsetinfo()["height"] == 5
