@@ -65,6 +65,11 @@ def _parse_addr(p: bytes) -> list[tuple[str, int, int, int]]:
     return out
 
 
+DEFAULT_MAX_ORPHAN_TRANSACTIONS = 100   # -maxorphantx (src/net_processing.h)
+ORPHAN_TX_EXPIRE_TIME = 20 * 60           # seconds (src/net_processing.cpp)
+MAX_ORPHAN_TX_WEIGHT = 400_000            # MAX_STANDARD_TX_WEIGHT
+
+
 class Peer:
     def __init__(self, mgr: "ConnectionManager", sock: socket.socket, addr, inbound: bool):
         self.mgr, self.sock, self.addr, self.inbound = mgr, sock, addr, inbound
@@ -196,6 +201,11 @@ class ConnectionManager:
         self.blocks_only = False             # -blocksonly: no transaction relay in either direction
         self.peer_bloom_filters = True       # -peerbloomfilters: NODE_BLOOM and the BIP37 messages
         self.user_agent = P.USER_AGENT       # with -uacomment
+        # orphan transactions (mapOrphanTransactions): txid -> (tx, peer id, expiry), -maxorphantx
+        self.orphans: dict[bytes, tuple] = {}
+        self.orphans_by_prev: dict[tuple[bytes, int], set[bytes]] = {}
+        self.max_orphans = DEFAULT_MAX_ORPHAN_TRANSACTIONS
+        self._orphan_lock = threading.RLock()
         self.local_addrs: dict[tuple[str, int], int] = {}  # AddLocal: (host, port) -> score
 
     # ---------------------------------------------------------------- lifecycle
@@ -286,6 +296,76 @@ class ConnectionManager:
         with self._lock:
             if p in self.peers:
                 self.peers.remove(p)
+        self.erase_orphans_for(p.id)  # FinalizeNode -> EraseOrphansFor
+
+    # ---------------------------------------------------------------- orphan transactions
+    def add_orphan(self, tx, peer_id: int) -> bool:
+        """AddOrphanTx: keep a transaction whose inputs are unknown (at most MAX_STANDARD_TX_WEIGHT,
+        expiring after ORPHAN_TX_EXPIRE_TIME), then LimitOrphanTxSize to -maxorphantx."""
+        txid = tx.txid()
+        with self._orphan_lock:
+            if txid in self.orphans:
+                return False
+            if len(tx.serialize(False)) * 3 + len(tx.serialize(True)) > MAX_ORPHAN_TX_WEIGHT:
+                log.log_print("mempool", f"ignoring large orphan tx {_core.u256_hex(txid)}")
+                return False
+            self.orphans[txid] = (tx, peer_id, time.time() + ORPHAN_TX_EXPIRE_TIME)
+            for i in tx.vin:
+                self.orphans_by_prev.setdefault((i.prevout.hash, i.prevout.n), set()).add(txid)
+            self.limit_orphans()
+        return True
+
+    def erase_orphan(self, txid: bytes) -> None:
+        with self._orphan_lock:
+            ent = self.orphans.pop(txid, None)
+            if ent is None:
+                return
+            for i in ent[0].vin:
+                s = self.orphans_by_prev.get((i.prevout.hash, i.prevout.n))
+                if s is not None:
+                    s.discard(txid)
+                    if not s:
+                        del self.orphans_by_prev[(i.prevout.hash, i.prevout.n)]
+
+    def erase_orphans_for(self, peer_id: int) -> None:
+        with self._orphan_lock:
+            for t in [t for t, e in self.orphans.items() if e[1] == peer_id]:
+                self.erase_orphan(t)
+
+    def limit_orphans(self) -> int:
+        """LimitOrphanTxSize: drop expired orphans, then random ones above the limit."""
+        now, gone = time.time(), 0
+        with self._orphan_lock:
+            for t in [t for t, e in self.orphans.items() if e[2] <= now]:
+                self.erase_orphan(t)
+                gone += 1
+            while len(self.orphans) > self.max_orphans:
+                self.erase_orphan(random.choice(list(self.orphans)))
+                gone += 1
+        return gone
+
+    def process_orphans(self, parent_txid: bytes, n_out: int) -> list[bytes]:
+        """The ProcessMessage("tx") work queue: orphans spending a newly accepted transaction are
+        retried; accepted ones queue their own children, invalid ones are dropped."""
+        accepted, work = [], [(parent_txid, n_out)]
+        while work:
+            txid, n = work.pop()
+            for k in range(n):
+                with self._orphan_lock:
+                    kids = list(self.orphans_by_prev.get((txid, k), ()))
+                for o in kids:
+                    with self._orphan_lock:
+                        ent = self.orphans.get(o)
+                    if ent is None:
+                        continue
+                    ok, reason, _ = self.state.accept_to_mempool(ent[0])
+                    if ok:
+                        accepted.append(o)
+                        self.erase_orphan(o)
+                        work.append((o, len(ent[0].vout)))
+                    elif reason != "missing-inputs":
+                        self.erase_orphan(o)
+        return accepted
 
     def stop(self) -> None:
         self._stop.set()
@@ -631,9 +711,18 @@ class ConnectionManager:
         if txid in self.state.mempool:
             return
         ok, reason, _ = self.state.accept_to_mempool(tx)
-        if not ok:
-            REGISTRY.inc("p2p_tx_rejected_total", 1)
-            log.log_print("mempool", f"tx {_core.u256_hex(txid)} from peer {peer.id} rejected: {reason}")
+        if ok:
+            self.process_orphans(txid, len(tx.vout))
+            return
+        if reason == "missing-inputs":
+            # keep it as an orphan and ask the sender for the parents we do not have
+            missing = [i.prevout.hash for i in tx.vin
+                       if i.prevout.hash not in self.state.mempool and i.prevout.hash not in self.orphans]
+            if self.add_orphan(tx, peer.id) and missing:
+                peer.send("getdata", P.inv_payload([(P.MSG_TX, h) for h in dict.fromkeys(missing)]))
+            return
+        REGISTRY.inc("p2p_tx_rejected_total", 1)
+        log.log_print("mempool", f"tx {_core.u256_hex(txid)} from peer {peer.id} rejected: {reason}")
 
     def on_mempool(self, peer: Peer, p: bytes) -> None:
         """BIP35: inv of every pool txid (in MAX_INV_SZ chunks), through the peer's bloom filter."""

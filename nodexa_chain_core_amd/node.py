@@ -368,6 +368,7 @@ class Node:
 
         self.connman.whitelist = parse_allow_subnets(a.get_list("whitelist"))
         self.connman.blocks_only = a.get_bool("blocksonly", False)
+        self.connman.max_orphans = a.get_int("maxorphantx", self.connman.max_orphans)
         self.connman.peer_bloom_filters = a.get_bool("peerbloomfilters", True)
         self.connman.user_agent = P.user_agent(a.get_list("uacomment"))
         self.connman.start()

@@ -291,3 +291,53 @@ print("not reached")
     node, _ = node_factory((f"-datadir={d}",))
     assert client(node).getblockcount() == 5
     assert client(node).gettxoutsetinfo()["height"] == 5
+
+
+class _FakePeer:
+    def __init__(self, pid=99):
+        self.id, self.addr, self.sent = pid, ("127.0.0.1", 1), []
+        self.known_txs, self.whitelisted, self.misbehavior = set(), False, 0
+
+    def send(self, cmd, payload=b""):
+        self.sent.append((cmd, payload))
+
+    def misbehaving(self, score, why):
+        self.misbehavior += score
+
+
+def test_orphan_transactions_and_maxorphantx(core, node_factory):  # noqa: F811
+    """A child that arrives before its parent waits in the orphan pool, the parent is requested
+    with getdata, and both enter the mempool once the parent arrives (net_processing's orphan
+    handling); -maxorphantx bounds the pool and a disconnect erases the peer's orphans."""
+    from wallet_util import spend
+
+    node, addr = node_factory(("-listen=1", "-port=0", "-listenonion=0", "-maxorphantx=3"))
+    c = client(node)
+    w = fund(c, 105)
+    coins = sorted((u for u in c.listunspent() if u["spendable"]), key=lambda u: u["txid"])
+    cm = node.connman
+    assert cm.max_orphans == 3
+    u = coins.pop()
+    parent_hex = spend(c, u["txid"], u["vout"], u["amount"], w, 5.0)
+    parent = core.Transaction.deserialize(bytes.fromhex(parent_hex))
+    ptxid = parent.txid()[::-1].hex()
+    raw = c.createrawtransaction([{"txid": ptxid, "vout": 0}], {w: 4.99})
+    prev = [{"txid": ptxid, "vout": 0, "scriptPubKey": parent.vout[0].script_pubkey.hex(), "amount": 5.0}]
+    signed = c.signrawtransaction(raw, prev)
+    assert signed["complete"], signed
+    child = core.Transaction.deserialize(bytes.fromhex(signed["hex"]))
+    peer = _FakePeer()
+    cm.on_tx(peer, child.serialize(True))
+    assert child.txid() in cm.orphans and child.txid() not in node.state.mempool
+    assert peer.sent and peer.sent[-1][0] == "getdata" and parent.txid() in peer.sent[-1][1]
+    cm.on_tx(peer, parent.serialize(True))
+    assert parent.txid() in node.state.mempool and child.txid() in node.state.mempool
+    assert not cm.orphans
+    # the pool is capped at -maxorphantx; a disconnect removes what that peer sent
+    for k in range(5):
+        fake = core.Transaction.deserialize(bytes.fromhex(
+            c.createrawtransaction([{"txid": "%064x" % (k + 1), "vout": 0}], {w: 0.5})))
+        cm.on_tx(peer, fake.serialize(True))
+    assert len(cm.orphans) == 3
+    cm.erase_orphans_for(peer.id)
+    assert not cm.orphans and not cm.orphans_by_prev
