@@ -116,6 +116,9 @@ DEFAULT_MEMPOOL_EXPIRY = 336                                          # hours
 DEFAULT_TRANSACTION_MAXFEE = 1000 * 100_000_000
 DEFAULT_BLOCK_MIN_TX_FEE = 1000                                       # sat per kvB (src/policy/policy.h:26)
 DEFAULT_MAX_TIP_AGE = 24 * 60 * 60                                    # -maxtipage (src/validation.h)
+DEFAULT_MAX_MEMPOOL_SIZE = 300                                        # -maxmempool, MB (src/policy/policy.h:34)
+ROLLING_FEE_HALFLIFE = 60 * 60 * 12                                   # src/txmempool.h
+MEMPOOL_ENTRY_OVERHEAD = 320  # bytes of bookkeeping per entry counted by mempool_usage (DynamicMemoryUsage analogue)
 MAX_STANDARD_SCRIPTSIG_SIZE = 1650
 GPU_SIG_BATCH_MIN = 16                 # below this many signatures a block is checked on the host
 
@@ -185,6 +188,10 @@ class ChainState:
         self._ibd_latched = False
         self.scripts_skipped = 0                                    # blocks connected under -assumevalid
         self.db_crash_ratio = 0                                     # -dbcrashratio fault injection
+        self.max_mempool_bytes = DEFAULT_MAX_MEMPOOL_SIZE * 1_000_000  # -maxmempool
+        self.rolling_min_fee = 0.0       # rollingMinimumFeeRate (sat per kvB)
+        self._last_rolling_update = 0.0
+        self._block_since_bump = False
         self.script_threads = min(16, os.cpu_count() or 1)  # -par: script-check threads (CCheckQueue)
         self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
         self.flush_interval = 1000
@@ -386,6 +393,57 @@ class ChainState:
             self._emit("transaction_added_to_mempool", tx)  # TransactionAddedToMempool: P2P relay, ZMQ
         return txid
 
+    def mempool_usage(self) -> int:
+        """DynamicMemoryUsage analogue: serialized sizes plus a fixed per-entry overhead."""
+        return sum(e.size + MEMPOOL_ENTRY_OVERHEAD for e in self.mempool.values())
+
+    def mempool_min_fee(self) -> int:
+        """CTxMemPool::GetMinFee (sat per kvB): the rolling floor left by TrimToSize, decaying
+        with a 12 h half-life (3 h / 6 h while the pool is under a quarter / half full) once a
+        block has arrived since the last bump; 0 below half the incremental relay fee."""
+        if not self._block_since_bump or self.rolling_min_fee == 0:
+            return int(round(self.rolling_min_fee))
+        now = self.adjusted_time()
+        if now > self._last_rolling_update + 10:
+            half, usage = ROLLING_FEE_HALFLIFE, self.mempool_usage()
+            if usage < self.max_mempool_bytes / 4:
+                half /= 4
+            elif usage < self.max_mempool_bytes / 2:
+                half /= 2
+            self.rolling_min_fee /= 2.0 ** ((now - self._last_rolling_update) / half)
+            self._last_rolling_update = now
+            if self.rolling_min_fee < self.incremental_relay_fee / 2:
+                self.rolling_min_fee = 0.0
+                return 0
+        return max(int(round(self.rolling_min_fee)), self.incremental_relay_fee)
+
+    def trim_mempool(self) -> int:
+        """TrimToSize: while over -maxmempool, evict the package (an entry and its descendants)
+        with the lowest descendant feerate and raise the rolling floor to that feerate plus the
+        incremental relay fee."""
+        gone = 0
+        with self.lock:
+            while self.mempool and self.mempool_usage() > self.max_mempool_bytes:
+                best = None
+                for t, e in self.mempool.items():
+                    desc = self.mempool_descendants(t)
+                    fee = e.fee + sum(self.mempool[d].fee for d in desc)
+                    size = e.vsize() + sum(self.mempool[d].vsize() for d in desc)
+                    score = fee * 1000 / max(1, size)
+                    if best is None or score < best[0]:
+                        best = (score, t, desc)
+                score, t, desc = best
+                rate = score + self.incremental_relay_fee
+                if rate > self.rolling_min_fee:  # trackPackageRemoved
+                    self.rolling_min_fee = rate
+                    self._block_since_bump = False
+                for x in {t} | desc:
+                    self.pool_remove(x)
+                    gone += 1
+            if gone:
+                self.transactions_updated += 1
+        return gone
+
     def pool_remove(self, txid: bytes, in_block: bool = False) -> None:
         """removeUnchecked: drop a pool entry and stop tracking it for fee estimation (an entry
         that leaves unconfirmed counts as a failure at its feerate)."""
@@ -580,6 +638,8 @@ class ChainState:
         are recorded at the number of blocks they waited; blocks at or below the best height the
         estimator has seen (reorgs, side chains) are ignored."""
         self.fee_estimator.process_block(height, [tx.txid() for tx in block.vtx[1:]])
+        self._last_rolling_update = self.adjusted_time()  # removeForBlock: the floor starts decaying
+        self._block_since_bump = True
 
     # ------------------------------------------------------------------ ProcessNewBlock
     def check_block_header(self, header) -> ValidationState:
@@ -963,6 +1023,9 @@ class ChainState:
             if why:
                 return False, why, 0
             vsize = (weight + 3) // 4
+            pool_floor = self.mempool_min_fee() * vsize // 1000
+            if pool_floor > 0 and fee < pool_floor:
+                return False, f"mempool min fee not met, {fee} < {pool_floor}", fee
             if fee < self.min_relay_fee * vsize // 1000:
                 return False, "min relay fee not met", fee
             replaced = set()
@@ -988,7 +1051,10 @@ class ChainState:
                 for t in replaced:  # BIP125: the replaced transactions and their descendants leave
                     self.pool_remove(t)
                 self.add_to_mempool(tx, fee, replacement=bool(replaced))
-                self.expire_mempool()  # LimitMempoolSize -> Expire
+                self.expire_mempool()  # LimitMempoolSize -> Expire, TrimToSize
+                self.trim_mempool()
+                if txid not in self.mempool:
+                    return False, "mempool full", fee
             return True, "", fee
 
     def _check_package_limits(self, tx, vsize: int, leaving: set) -> str:

@@ -172,6 +172,11 @@ class Node:
                               a.get_int("limitancestorsize", st.ancestor_limits[1] // 1000) * 1000)
         st.descendant_limits = (a.get_int("limitdescendantcount", st.descendant_limits[0]),
                                 a.get_int("limitdescendantsize", st.descendant_limits[1] // 1000) * 1000)
+        max_pool = a.get_int("maxmempool", st.max_mempool_bytes // 1_000_000)
+        min_pool = st.descendant_limits[1] * 40 // 1_000_000  # nMempoolSizeMin = limitdescendantsize * 40
+        if max_pool < min_pool:
+            raise SystemExit(f"-maxmempool must be at least {min_pool} MB")
+        st.max_mempool_bytes = max_pool * 1_000_000
         st.mempool_expiry = a.get_int("mempoolexpiry", st.mempool_expiry // 3600) * 3600
         if a.get("maxtxfee") is not None:
             st.max_tx_fee = round(float(a.get("maxtxfee")) * coin)

@@ -533,9 +533,10 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
 
     def rpc_getmempoolinfo(p):
         """getmempoolinfo — size / bytes of the template mempool."""
-        sizes = [len(e.tx.serialize(True)) for e in st.mempool.values()]
-        return {"size": len(sizes), "bytes": sum(sizes), "usage": sum(sizes), "maxmempool": 300_000_000,
-                "mempoolminfee": 0.00001, "minrelaytxfee": 0.00001}
+        sizes = [e.vsize() for e in st.mempool.values()]
+        return {"size": len(sizes), "bytes": sum(sizes), "usage": st.mempool_usage(), "maxmempool": st.max_mempool_bytes,
+                "mempoolminfee": max(st.mempool_min_fee(), st.min_relay_fee) / 1e8,
+                "minrelaytxfee": st.min_relay_fee / 1e8}
 
     def rpc_getrawtransaction(p):
         """getrawtransaction "txid" ( verbose "blockhash" ) — mempool, the given block, -txindex, or a

@@ -341,3 +341,43 @@ def test_orphan_transactions_and_maxorphantx(core, node_factory):  # noqa: F811
     assert len(cm.orphans) == 3
     cm.erase_orphans_for(peer.id)
     assert not cm.orphans and not cm.orphans_by_prev
+
+
+def test_maxmempool_trim_and_rolling_min_fee(core, node_factory):  # noqa: F811
+    """TrimToSize: over the limit the lowest-feerate package leaves and the pool's minimum fee
+    rises to its feerate plus the incremental relay fee; getmempoolinfo reports both; the floor
+    decays once a block arrives. (-maxmempool below 10 MB is refused as in the reference, so the
+    limit is lowered on the state object to keep the test small.)"""
+    from wallet_util import spend
+
+    node, addr = node_factory()
+    c = client(node)
+    w = fund(c, 110)
+    st = node.state
+    coins = sorted((u for u in c.listunspent() if u["spendable"]), key=lambda u: u["txid"])
+    fees = [0.02, 0.03, 0.05, 0.01]
+    ids = []
+    for f in fees[:3]:
+        u = coins.pop()
+        ids.append(c.sendrawtransaction(spend(c, u["txid"], u["vout"], u["amount"], w, 1.0, fee=f)))
+    st.max_mempool_bytes = st.mempool_usage() - 1  # one entry too many
+    assert st.trim_mempool() == 1
+    pool = set(c.getrawmempool())
+    assert ids[0] not in pool and ids[1] in pool and ids[2] in pool  # the 0.02-fee tx went
+    info = c.getmempoolinfo()
+    assert info["maxmempool"] == st.max_mempool_bytes and info["mempoolminfee"] > info["minrelaytxfee"]
+    floor = st.mempool_min_fee()
+    assert floor > st.incremental_relay_fee
+    u = coins.pop()  # below the new floor: refused
+    cheap = spend(c, u["txid"], u["vout"], u["amount"], w, 1.0, fee=fees[3])
+    with pytest.raises(RuntimeError, match="mempool min fee not met"):
+        c.sendrawtransaction(cheap)
+    # a block resets the decay clock; a week later (3 h half-life while nearly empty) it is gone
+    st.max_mempool_bytes = 300_000_000
+    c.generatetoaddress(1, addr)
+    c.setmocktime(int(time.time()) + 7 * 24 * 3600)
+    assert st.mempool_min_fee() == 0
+    c.setmocktime(0)
+    node.stop()
+    with pytest.raises(SystemExit, match="maxmempool must be at least"):
+        node_factory(("-maxmempool=5",))
