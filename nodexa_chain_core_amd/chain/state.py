@@ -344,7 +344,8 @@ class ChainState:
         return self.store.read_raw(pos)
 
     def adjusted_time(self) -> int:
-        return int(self.mocktime or time.time())
+        """GetAdjustedTime: the clock (or setmocktime) plus the peers' median offset (timedata)."""
+        return int(self.mocktime or time.time()) + getattr(self, "time_offset", 0)
 
     def arm_reorg_guard(self, peer_count: int) -> bool:
         """-maxreorg / -minreorgpeers / -minreorgage (ContextualCheckBlockHeader,

@@ -33,6 +33,7 @@ from .addrman import AddrMan, load_banlist, save_banlist
 from .bloom import MAX_SCRIPT_ELEMENT_SIZE, BloomFilter, merkle_block
 from .compact import (CompactBlock, blocktxn_payload, getblocktxn_payload, parse_blocktxn, parse_getblocktxn)
 from .netbase import ProxyTable
+from .timedata import TimeData
 
 _core = core()
 DEFAULT_MISBEHAVING_BANTIME = 60 * 60 * 24  # -bantime (src/net.h)
@@ -161,7 +162,8 @@ class Peer:
                 "bytessent": self.bytes_sent, "bytesrecv": self.bytes_recv, "conntime": int(self.connected_at),
                 "lastsend": int(self.last_send), "lastrecv": int(self.last_recv), "banscore": self.misbehavior,
                 "synced_headers": self.mgr.state.height(), "relaytxes": self.info.get("relay", True),
-                "services": "%016x" % self.info.get("services", 0), "whitelisted": self.whitelisted}
+                "services": "%016x" % self.info.get("services", 0), "whitelisted": self.whitelisted,
+                "timeoffset": self.info.get("timeoffset", 0)}
 
 
 class ConnectionManager:
@@ -205,6 +207,9 @@ class ConnectionManager:
         self.orphans: dict[bytes, tuple] = {}
         self.orphans_by_prev: dict[tuple[bytes, int], set[bytes]] = {}
         self.max_orphans = DEFAULT_MAX_ORPHAN_TRANSACTIONS
+        self.timedata = TimeData()           # -maxtimeadjustment
+        self.dns_seeds: list[str] = []       # chainparams vSeeds (-dnsseed / -forcednsseed)
+        self.force_dns_seed = False
         self._orphan_lock = threading.RLock()
         self.local_addrs: dict[tuple[str, int], int] = {}  # AddLocal: (host, port) -> score
 
@@ -226,6 +231,31 @@ class ConnectionManager:
             log.log_printf(f"P2P listening on {self.listen_addr[0]}:{self.port}")
         if not self.connect_only and self.max_outbound > 0:
             threading.Thread(target=self._open_connections, name="p2p-opencon", daemon=True).start()
+        if self.dns_seeds and not self.connect_only:
+            threading.Thread(target=self.dns_address_seed, name="p2p-dnsseed", daemon=True).start()
+
+    def dns_address_seed(self, resolve=None) -> int:
+        """ThreadDNSAddressSeed: unless the address manager already knows peers (and -forcednsseed
+        is off), resolve every DNS seed to addresses on the default port and add them to addrman
+        with the seed as their source. Returns the number of addresses added."""
+        if self.addrman.size() > 0 and not self.force_dns_seed:
+            log.log_print("net", "P2P peers available. Skipped DNS seeding.")
+            return 0
+        resolve = resolve or socket.getaddrinfo
+        found = 0
+        for seed in self.dns_seeds:
+            try:
+                infos = resolve(seed, self.params.default_port, socket.AF_INET, socket.SOCK_STREAM)
+            except OSError as e:
+                log.log_print("net", f"DNS seed {seed} unavailable: {e}")
+                continue
+            now = int(time.time())
+            # seed addresses are stamped 3-7 days old, as the reference does, so they rank low
+            entries = [(info[4][0], self.params.default_port, P.NODE_NETWORK, now - 3 * 86400 - random.randrange(4 * 86400))
+                       for info in infos]
+            found += self.addrman.add(entries, seed) or 0
+        log.log_printf(f"{found} addresses found from DNS seeds")
+        return found
 
     def _open_connections(self) -> None:
         """ThreadOpenConnections: keep up to max_outbound outbound peers, picked from addrman."""
@@ -488,6 +518,11 @@ class ConnectionManager:
             peer.close()
             return
         peer.info = info
+        # AddTimeData: outbound peers' clocks feed the network-adjusted time
+        offset = int(info.get("time", 0)) - int(time.time())
+        peer.info["timeoffset"] = offset
+        if not peer.inbound:
+            self.state.time_offset = self.timedata.add(peer.addr[0], offset)
         if peer.inbound and not peer.sent_version:
             peer.send_version()
         peer.send("verack")

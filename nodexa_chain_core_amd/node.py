@@ -36,6 +36,10 @@ from .utils.config import ArgsManager, gpu_list
 _core = core()
 
 
+# chainparams vSeeds (src/chainparams.cpp:184-186, 346): DNS names resolved by ThreadDNSAddressSeed
+DNS_SEEDS = {"main": ["seed.clore.ai", "seed1.clore.ai", "seed2.clore.ai"], "test": ["testnet.clore.ai"], "regtest": []}
+
+
 class Node:
     def __init__(self, args: ArgsManager):
         self.args = args
@@ -125,8 +129,21 @@ class Node:
                                  mnemonic_passphrase=a.get("mnemonicpassphrase", "") or "")
             hist_path = os.path.join(self.datadir, "wallet_txs.json") if self.datadir else None
             rescan = hist_path is not None and not os.path.exists(hist_path) and bool(self.wallet.keys)
+            rescan = rescan or a.get_bool("rescan", False)  # -rescan: rebuild the history at start-up
             self.wallet.history = WalletHistory(self.wallet, hist_path)
-            if rescan:
+            zap = a.get_int("zapwallettxes", 0)
+            if zap:  # -zapwallettxes=1|2: drop every wallet transaction, rescan (1 keeps their metadata)
+                hist = self.wallet.history
+                keep = {t: (w.comment, w.comment_to, w.from_account) for t, w in hist.txs.items()} if zap == 1 else {}
+                hist.txs.clear()
+                methods_wallet.rescan(self)
+                for t, (cm, ct, acct) in keep.items():
+                    w = hist.txs.get(t)
+                    if w is not None:
+                        w.comment, w.comment_to, w.from_account = cm, ct, acct
+                hist.save()
+                log.log_printf(f"Zapped wallet transactions (mode {zap}); {len(hist.txs)} found again by the rescan")
+            elif rescan:
                 methods_wallet.rescan(self)
             self.state.register(self.wallet.history)
             methods_wallet.register(self.table, self)
@@ -374,6 +391,12 @@ class Node:
         self.connman.whitelist = parse_allow_subnets(a.get_list("whitelist"))
         self.connman.blocks_only = a.get_bool("blocksonly", False)
         self.connman.max_orphans = a.get_int("maxorphantx", self.connman.max_orphans)
+        from .net.timedata import DEFAULT_MAX_TIME_ADJUSTMENT, TimeData
+
+        self.connman.timedata = TimeData(max(0, a.get_int("maxtimeadjustment", DEFAULT_MAX_TIME_ADJUSTMENT)))
+        if a.get_bool("dnsseed", not connect) and not a.get_list("connect"):  # -dnsseed (off with -connect)
+            self.connman.dns_seeds = list(DNS_SEEDS.get(self.network, []))
+        self.connman.force_dns_seed = a.get_bool("forcednsseed", False)
         self.connman.peer_bloom_filters = a.get_bool("peerbloomfilters", True)
         self.connman.user_agent = P.user_agent(a.get_list("uacomment"))
         self.connman.start()

@@ -675,7 +675,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         cm = _cm()
         return {"version": 40404, "subversion": P.USER_AGENT, "protocolversion": P.PROTOCOL_VERSION,
                 "localservices": "%016x" % (P.NODE_NETWORK | P.NODE_WITNESS), "localrelay": True,
-                "timeoffset": 0, "networkactive": cm is not None, "connections": node.peer_count(),
+                "timeoffset": getattr(st, "time_offset", 0), "networkactive": cm is not None, "connections": node.peer_count(),
                 "networks": cm.proxies.describe() if cm is not None else [],
                 "relayfee": 0.00001, "incrementalfee": 0.00001,
                 "localaddresses": ([{"address": cm.listen_addr[0], "port": cm.port, "score": 1}]

@@ -381,3 +381,58 @@ def test_maxmempool_trim_and_rolling_min_fee(core, node_factory):  # noqa: F811
     node.stop()
     with pytest.raises(SystemExit, match="maxmempool must be at least"):
         node_factory(("-maxmempool=5",))
+
+
+def test_timedata_median_and_limit():
+    from nodexa_chain_core_amd.net.timedata import TimeData
+
+    td = TimeData(max_adjustment=600)
+    offsets = [30, 40, 50, 60]
+    for i, o in enumerate(offsets):
+        td.add(f"10.0.0.{i}", o)
+    assert td.offset == 40  # 5 samples with our own 0: median of [0, 30, 40, 50, 60]
+    td.add("10.0.0.1", 9999)  # one sample per address
+    assert td.offset == 40
+    far = TimeData(max_adjustment=600)
+    for i in range(6):
+        far.add(f"10.1.0.{i}", 3600)
+    assert far.offset == 0  # median beyond -maxtimeadjustment: no adjustment
+
+
+def test_dns_seeding(core, node_factory):  # noqa: F811
+    node, _ = node_factory(("-listen=1", "-port=0", "-listenonion=0", "-maxconnections=0"))
+    cm = node.connman
+    cm.dns_seeds = ["seed.example"]
+    calls = []
+
+    def fake_resolve(host, port, *a):
+        calls.append((host, port))
+        return [(2, 1, 6, "", ("198.51.100.7", port)), (2, 1, 6, "", ("198.51.100.8", port))]
+    assert cm.dns_address_seed(fake_resolve) == 2
+    assert calls == [("seed.example", node.params.default_port)] and cm.addrman.size() == 2
+    assert cm.dns_address_seed(fake_resolve) == 0  # addrman has peers now: skipped
+    cm.force_dns_seed = True
+    assert cm.dns_address_seed(lambda *a: (_ for _ in ()).throw(OSError("offline"))) == 0
+
+
+def test_zapwallettxes_and_rescan(core, node_factory, tmp_path):  # noqa: F811
+    d = tmp_path / "zap"
+    os.makedirs(d)
+    node, _ = node_factory((f"-datadir={d}",))
+    c = client(node)
+    w = fund(c, 101)
+    txid = c.sendtoaddress(w, 1.0, "rent", "bob")
+    c.generatetoaddress(1, w)
+    before = {t["txid"] for t in c.listtransactions("*", 1000)}
+    node.stop()
+    node2, _ = node_factory((f"-datadir={d}", "-zapwallettxes=1"))
+    c2 = client(node2)
+    after = {t["txid"] for t in c2.listtransactions("*", 1000)}
+    assert after == before  # everything confirmed comes back from the rescan
+    assert c2.gettransaction(txid).get("comment") == "rent"  # mode 1 keeps the metadata
+    node2.stop()
+    node3, _ = node_factory((f"-datadir={d}", "-zapwallettxes=2"))
+    assert "comment" not in client(node3).gettransaction(txid) or not client(node3).gettransaction(txid)["comment"]
+    node3.stop()
+    node4, _ = node_factory((f"-datadir={d}", "-rescan"))
+    assert {t["txid"] for t in client(node4).listtransactions("*", 1000)} == before
