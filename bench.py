@@ -52,7 +52,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epoch", type=int, default=384, help="384 -> 4 GiB DAG (BASELINE config)")
-    ap.add_argument("--batch", type=int, default=1 << 23, help="nonces per GPU per step")
+    ap.add_argument("--batch", type=int, default=1 << 25,
+                    help="nonces per GPU per step (profiles/r2q: 2^25 amortises the kernel tail, +0.9 %% vs 2^23)")
     ap.add_argument("--equihash", type=int, default=12,
                     help="Equihash(200,9): batches of 8 solves per GPU to time (0 = skip)")
     ap.add_argument("--quiet", action="store_true")
