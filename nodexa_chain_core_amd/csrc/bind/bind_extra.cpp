@@ -391,6 +391,7 @@ void bind_extra(py::module_& m) {
         .def_property_readonly("pow_target_spacing", [](const ChainParams& p) { return p.consensus.pow_target_spacing; })
         .def_property_readonly("pow_allow_min_difficulty_blocks", [](const ChainParams& p) { return p.consensus.pow_allow_min_difficulty_blocks; })
         .def_property_readonly("checkpoints", [](const ChainParams& p) { py::dict d; for (auto& kv : p.checkpoints) d[py::int_(kv.first)] = pyb(kv.second); return d; })
+        .def("clear_checkpoints", [](ChainParams& p) { p.checkpoints.clear(); })  // -checkpoints=0
         .def_readwrite("community_autonomous_pct", &ChainParams::community_autonomous_pct)
         .def_readwrite("community_autonomous_address", &ChainParams::community_autonomous_address)
         .def_readwrite("dgw_activation_block", &ChainParams::dgw_activation_block)

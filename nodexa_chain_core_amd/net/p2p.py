@@ -305,6 +305,26 @@ class ConnectionManager:
             return False
         return any(a.version == n.version and a in n for n in self.whitelist)
 
+    def discover_local_addresses(self, resolve=None) -> int:
+        """Discover(): the host's own addresses (by hostname lookup) that are routable, added with
+        LOCAL_IF score; loopback, private and link-local addresses are skipped (IsRoutable)."""
+        resolve = resolve or (lambda: socket.getaddrinfo(socket.gethostname(), None))
+        try:
+            infos = resolve()
+        except OSError:
+            return 0
+        n = 0
+        for info in infos:
+            ip = info[4][0]
+            try:
+                a = ipaddress.ip_address(ip.split("%")[0])
+            except ValueError:
+                continue
+            if a.is_global:
+                self.add_local(str(a), self.port or self.params.default_port, 1)
+                n += 1
+        return n
+
     def add_local(self, host: str, port: int, score: int = 1) -> None:
         """AddLocal (src/net.cpp): an address this node is reachable at, e.g. its onion service."""
         with self._lock:

@@ -48,6 +48,8 @@ class Node:
         eq = args.get("equihash")
         self.params = make_params(self.network, int(act) if act is not None else None,
                                   int(eq) if eq not in (None, "", "1") else None)
+        if not args.get_bool("checkpoints", True):  # -checkpoints=0: fCheckpointsEnabled = false
+            self.params.clear_checkpoints()
         self.datadir = args.data_dir() if args.get("datadir") is not None or not args.get_bool("nodatadir") else None
         self._lock_file = None
         self._shutdown = threading.Event()
@@ -177,6 +179,10 @@ class Node:
             st.minimum_chain_work = int(a.get("minimumchainwork"), 16)
         st.max_tip_age = a.get_int("maxtipage", st.max_tip_age)
         st.db_crash_ratio = a.get_int("dbcrashratio", 0)
+        if a.is_set("mocktime"):  # -mocktime=<n> (regtest tooling): SetMockTime at start-up
+            if self.network != "regtest":
+                raise SystemExit("-mocktime is for regression testing (-regtest mode) only")
+            st.mocktime = a.get_int("mocktime", 0)
         for spec in a.get_list("vbparams"):  # -vbparams=deployment:start:end (regtest only)
             self._apply_vbparams(spec)
         self._verify_db(a.get_int("checkblocks", 6), a.get_int("checklevel", 3))
@@ -401,6 +407,8 @@ class Node:
         self.connman.user_agent = P.user_agent(a.get_list("uacomment"))
         self.connman.start()
         cm = self.connman
+        if listen is not None and a.get_bool("discover", not a.get_list("externalip") and not a.is_set("bind")):
+            cm.discover_local_addresses()  # -discover: Discover() adds this host's routable addresses
         for ext in a.get_list("externalip"):  # -externalip: AddLocal(LOCAL_MANUAL)
             from .net.netbase import parse_host_port
 

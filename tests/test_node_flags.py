@@ -436,3 +436,16 @@ def test_zapwallettxes_and_rescan(core, node_factory, tmp_path):  # noqa: F811
     node3.stop()
     node4, _ = node_factory((f"-datadir={d}", "-rescan"))
     assert {t["txid"] for t in client(node4).listtransactions("*", 1000)} == before
+
+
+def test_checkpoints_mocktime_discover(core, node_factory, tmp_path):  # noqa: F811
+    main = core.make_chain_params("main")
+    assert main.checkpoints
+    main.clear_checkpoints()
+    assert not main.checkpoints
+    node, _ = node_factory(("-mocktime=1700000000", "-listen=1", "-port=0", "-listenonion=0"))
+    assert node.state.adjusted_time() == 1700000000
+    cm = node.connman
+    n = cm.discover_local_addresses(lambda: [(2, 1, 6, "", ("10.0.0.5", 0)), (2, 1, 6, "", ("8.8.4.4", 0)),
+                                             (2, 1, 6, "", ("127.0.0.1", 0))])
+    assert n == 1 and ("8.8.4.4", cm.port) in cm.local_addrs
