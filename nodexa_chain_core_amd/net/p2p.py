@@ -100,6 +100,7 @@ class Peer:
             self.sock.sendall(msg)
         self.bytes_sent += len(msg)
         self.mgr.total_sent += len(msg)
+        self.mgr.record_sent(len(msg))
         self.last_send = time.time()
         REGISTRY.inc("p2p_bytes_sent_total", len(msg), command=cmd)
 
@@ -208,6 +209,10 @@ class ConnectionManager:
         self.orphans_by_prev: dict[tuple[bytes, int], set[bytes]] = {}
         self.max_orphans = DEFAULT_MAX_ORPHAN_TRANSACTIONS
         self.timedata = TimeData()           # -maxtimeadjustment
+        self.max_outbound_limit = 0          # -maxuploadtarget (bytes per 24 h cycle; 0 = none)
+        self.max_outbound_timeframe = 24 * 60 * 60
+        self.outbound_cycle_start = 0.0
+        self.outbound_cycle_bytes = 0
         self.dns_seeds: list[str] = []       # chainparams vSeeds (-dnsseed / -forcednsseed)
         self.force_dns_seed = False
         self._orphan_lock = threading.RLock()
@@ -324,6 +329,34 @@ class ConnectionManager:
                 self.add_local(str(a), self.port or self.params.default_port, 1)
                 n += 1
         return n
+
+    # ---------------------------------------------------------------- -maxuploadtarget
+    def record_sent(self, n: int) -> None:
+        """RecordBytesSent: bytes in the current upload cycle (a new cycle every timeframe)."""
+        now = time.time()
+        if now > self.outbound_cycle_start + self.max_outbound_timeframe:
+            self.outbound_cycle_start, self.outbound_cycle_bytes = now, 0
+        self.outbound_cycle_bytes += n
+
+    def outbound_target_reached(self, historical_only: bool) -> bool:
+        """OutboundTargetReached: with `historical_only`, true once less than one MAX_BLOCK_SERIALIZED
+        buffer of the target is left (recent blocks are still served until the target itself)."""
+        if not self.max_outbound_limit:
+            return False
+        if historical_only:
+            buffer = self.max_outbound_timeframe // 600 * 8_000_000  # MAX_BLOCK_SERIALIZED_SIZE per expected block
+            return buffer >= self.max_outbound_limit or self.outbound_cycle_bytes >= self.max_outbound_limit - buffer
+        return self.outbound_cycle_bytes >= self.max_outbound_limit
+
+    def upload_target_info(self) -> dict:
+        now = time.time()
+        left_t = max(0, int(self.outbound_cycle_start + self.max_outbound_timeframe - now)) if self.max_outbound_limit else 0
+        return {"timeframe": self.max_outbound_timeframe, "target": self.max_outbound_limit,
+                "target_reached": self.outbound_target_reached(False),
+                "serve_historical_blocks": not self.outbound_target_reached(True),
+                "bytes_left_in_cycle": max(0, self.max_outbound_limit - self.outbound_cycle_bytes)
+                if self.max_outbound_limit else 0,
+                "time_left_in_cycle": left_t}
 
     def add_local(self, host: str, port: int, score: int = 1) -> None:
         """AddLocal (src/net.cpp): an address this node is reachable at, e.g. its onion service."""
@@ -809,6 +842,13 @@ class ConnectionManager:
                             peer.send("tx", tx.serialize(False))
                 continue
             if kind == P.MSG_BLOCK:
+                idx = self.state.chain.find(h)
+                historical = idx is not None and idx.time < time.time() - 7 * 24 * 3600
+                if historical and not peer.whitelisted and self.outbound_target_reached(True):
+                    # historical block serving limit reached: disconnect (ProcessGetData)
+                    log.log_print("net", f"historical block serving limit reached, disconnect peer={peer.id}")
+                    peer.close()
+                    return
                 raw = self.state.get_block_raw(h)
                 if raw is None:
                     missing.append((t, h))

@@ -397,6 +397,7 @@ class Node:
         self.connman.whitelist = parse_allow_subnets(a.get_list("whitelist"))
         self.connman.blocks_only = a.get_bool("blocksonly", False)
         self.connman.max_orphans = a.get_int("maxorphantx", self.connman.max_orphans)
+        self.connman.max_outbound_limit = a.get_int("maxuploadtarget", 0) * 1024 * 1024  # MiB per 24 h
         from .net.timedata import DEFAULT_MAX_TIME_ADJUSTMENT, TimeData
 
         self.connman.timedata = TimeData(max(0, a.get_int("maxtimeadjustment", DEFAULT_MAX_TIME_ADJUSTMENT)))

@@ -451,8 +451,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         """getnettotals — network traffic totals."""
         cm = _cm()
         return {"totalbytesrecv": cm.total_recv, "totalbytessent": cm.total_sent, "timemillis": int(time.time() * 1000),
-                "uploadtarget": {"timeframe": 86400, "target": 0, "target_reached": False,
-                                 "serve_historical_blocks": True, "bytes_left_in_cycle": 0, "time_left_in_cycle": 0}}
+                "uploadtarget": cm.upload_target_info()}
 
     def rpc_setban(p):
         """setban "subnet" "add|remove" ( bantime absolute ) — manage the ban list."""

@@ -449,3 +449,17 @@ def test_checkpoints_mocktime_discover(core, node_factory, tmp_path):  # noqa: F
     n = cm.discover_local_addresses(lambda: [(2, 1, 6, "", ("10.0.0.5", 0)), (2, 1, 6, "", ("8.8.4.4", 0)),
                                              (2, 1, 6, "", ("127.0.0.1", 0))])
     assert n == 1 and ("8.8.4.4", cm.port) in cm.local_addrs
+
+
+def test_maxuploadtarget(core, node_factory):  # noqa: F811
+    node, _ = node_factory(("-listen=1", "-port=0", "-listenonion=0", "-maxuploadtarget=200"))
+    cm = node.connman
+    info = client(node).getnettotals()["uploadtarget"]
+    assert info["target"] == 200 * 1024 * 1024 and info["serve_historical_blocks"] is False  # < one day of blocks
+    assert info["target_reached"] is False
+    cm.max_outbound_limit = 2_000_000_000
+    cm.record_sent(10)
+    assert cm.upload_target_info()["serve_historical_blocks"] is True
+    cm.record_sent(2_000_000_000)
+    t = cm.upload_target_info()
+    assert t["target_reached"] and not t["serve_historical_blocks"] and t["bytes_left_in_cycle"] == 0
