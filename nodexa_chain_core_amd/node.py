@@ -58,6 +58,7 @@ class Node:
         self.pprpc_templates: dict[str, object] = {}
         self._last_pprpc: tuple[str, float] | None = None
         self.gpus = gpu_list(args)
+        self.rpc_witness = True  # -rpcserialversion=1
         self.state: ChainState | None = None
         self.miner: MinerController | None = None
         self.rpc: RPCServer | None = None
@@ -179,6 +180,10 @@ class Node:
             st.minimum_chain_work = int(a.get("minimumchainwork"), 16)
         st.max_tip_age = a.get_int("maxtipage", st.max_tip_age)
         st.db_crash_ratio = a.get_int("dbcrashratio", 0)
+        ser = a.get_int("rpcserialversion", 1)  # -rpcserialversion: 0 = non-segwit, 1 = segwit serialization
+        if ser not in (0, 1):
+            raise SystemExit("unknown rpcserialversion requested." if ser > 1 else "rpcserialversion must be non-negative.")
+        self.rpc_witness = ser == 1
         if a.is_set("mocktime"):  # -mocktime=<n> (regtest tooling): SetMockTime at start-up
             if self.network != "regtest":
                 raise SystemExit("-mocktime is for regression testing (-regtest mode) only")
@@ -221,6 +226,7 @@ class Node:
                 w.min_tx_fee = round(float(a.get("mintxfee")) * 100_000_000)
             w.keypool_size = max(1, a.get_int("keypool", w.keypool_size))
             w.broadcast = a.get_bool("walletbroadcast", True)
+            w.spend_zeroconf_change = a.get_bool("spendzeroconfchange", True)
         par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free
         cores = os.cpu_count() or 1
         self.state.script_threads = max(1, min(16, cores + par if par <= 0 else par))

@@ -173,6 +173,9 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         if raw is None:
             raise RPCError(RPC_MISC_ERROR, "Block not available (pruned data)")
         if verbosity == 0:
+            if not node.rpc_witness:  # -rpcserialversion=0: the block without witness data
+                blk = _core.Block.deserialize(raw, params.kawpow_activation_time)
+                return blk.serialize(params.kawpow_activation_time, False).hex()
             return raw.hex()
         blk = _core.Block.deserialize(raw, params.kawpow_activation_time)
         out = header_json(idx, blk.header)
@@ -205,7 +208,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             vout.append(e)
         return {"txid": _hex(tx.txid()), "hash": _hex(tx.wtxid()), "version": tx.version,
                 "size": len(tx.serialize(True)), "vsize": (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4,
-                "locktime": tx.lock_time, "vin": vin, "vout": vout, "hex": tx.serialize(True).hex()}
+                "locktime": tx.lock_time, "vin": vin, "vout": vout, "hex": tx.serialize(node.rpc_witness).hex()}
 
     def rpc_getdifficulty(p):
         """getdifficulty — proof-of-work difficulty as a multiple of the minimum difficulty."""
@@ -574,7 +577,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         if tx is None:
             raise RPCError(RPC_INVALID_ADDRESS_OR_KEY, "No such mempool transaction. Use -txindex or provide a block hash")
         if not _arg(p, 1, False):
-            return tx.serialize(True).hex()
+            return tx.serialize(node.rpc_witness).hex()  # RPCSerializationFlags (-rpcserialversion)
         out = tx_json(tx)
         if in_block is not None:  # TxToJSON: confirmations / time of an active-chain block
             out["blockhash"] = _hex(in_block)

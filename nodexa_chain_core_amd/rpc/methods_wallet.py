@@ -311,7 +311,7 @@ def register(table, node) -> None:
         out.update(base)
         out["details"] = [{k: v for k, v in e.items() if k in ("account", "address", "category", "amount", "vout",
                                                                  "fee", "abandoned")} for e in ents]
-        out["hex"] = w.tx.serialize(True).hex()
+        out["hex"] = w.tx.serialize(getattr(node, "rpc_witness", True)).hex()
         return out
 
     def rpc_listsinceblock(p):

@@ -146,6 +146,7 @@ class Wallet:
         self.max_tx_fee: int | None = None            # -maxtxfee cap on one transaction's fee (None: node's)
         self.keypool_size = DEFAULT_KEYPOOL_SIZE      # -keypool
         self.broadcast = True                         # -walletbroadcast
+        self.spend_zeroconf_change = True             # -spendzeroconfchange (DEFAULT_SPEND_ZEROCONF_CHANGE)
         self.hdpath: dict[bytes, str] = {}      # hdkeypath of derived keys
         self.pool: list[bytes] = []             # keypool: reserved keys not yet handed out
         self.hd: dict | None = None             # {"master_id", "next", "seed", "seed_crypted"}
@@ -747,6 +748,12 @@ class Wallet:
         target = sum(v for _, v in outputs)
         coins = sorted((u for u in self.unspent(minconf) if u["spendable"]
                         and (from_scripts is None or u["scriptPubKey"] in from_scripts)), key=lambda u: -u["amount"])
+        if minconf >= 1 and self.spend_zeroconf_change and sum(u["amount"] for u in coins) < target:
+            # SelectCoins' last pass (nConfMine 0): our own unconfirmed change from trusted wallet
+            # transactions, after every confirmed coin
+            extra = [u for u in self.unspent(0) if u["confirmations"] == 0 and u["spendable"]
+                     and (from_scripts is None or u["scriptPubKey"] in from_scripts) and self._trusted(u["txid"])]
+            coins += sorted(extra, key=lambda u: -u["amount"])
         seq = 0xfffffffd if (self.walletrbf if replaceable is None else replaceable) else 0xfffffffe
         fee = 0
         for _ in range(20):  # fee depends on the size, size on the inputs chosen
@@ -802,6 +809,18 @@ class Wallet:
         tx, _ = self.create_transaction(outputs, fee_rate=self.fee_rate, subtract_fee=subtract_fee, minconf=minconf,
                                         replaceable=replaceable, from_scripts=from_scripts, change_spk=change_spk)
         return self.commit(tx, comment, comment_to, from_account)
+
+    def _trusted(self, txid: bytes) -> bool:
+        """CWalletTx::IsTrusted for a pool transaction: every input spends one of our outputs."""
+        e = self.state.mempool.get(txid)
+        if e is None or self.history is None:
+            return False
+        mine = set(self.scripts())
+        for i in e.tx.vin:
+            prev = self.history.txs.get(i.prevout.hash)
+            if prev is None or i.prevout.n >= len(prev.tx.vout) or prev.tx.vout[i.prevout.n].script_pubkey not in mine:
+                return False
+        return True
 
     def _capped_fee(self, fee: int) -> int:
         """GetMinimumFee's last step: never above -maxtxfee (CreateTransaction then reports

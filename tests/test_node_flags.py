@@ -463,3 +463,25 @@ def test_maxuploadtarget(core, node_factory):  # noqa: F811
     cm.record_sent(2_000_000_000)
     t = cm.upload_target_info()
     assert t["target_reached"] and not t["serve_historical_blocks"] and t["bytes_left_in_cycle"] == 0
+
+
+def test_spend_zeroconf_change_and_rpcserialversion(core, node_factory, tmp_path):  # noqa: F811
+    node, addr = node_factory(("-rpcserialversion=0",))
+    c = client(node)
+    w = fund(c, 101)  # exactly one mature coinbase
+    coin = [u for u in c.listunspent() if u["spendable"]][0]["amount"]
+    t1 = c.sendtoaddress(addr, round(coin / 2, 8))  # the change stays unconfirmed
+    t2 = c.sendtoaddress(addr, round(coin / 4, 8))  # only possible by spending that change
+    pool = c.getrawmempool()
+    assert t1 in pool and t2 in pool
+    raw = c.getrawtransaction(t2)
+    assert core.Transaction.deserialize(bytes.fromhex(raw)).serialize(False).hex() == raw  # no witness form
+    node.stop()
+    os.makedirs(tmp_path / "nz")
+    node2, addr2 = node_factory((f"-datadir={tmp_path / 'nz'}", "-spendzeroconfchange=0"))
+    c2 = client(node2)
+    fund(c2, 101)
+    coin2 = [u for u in c2.listunspent() if u["spendable"]][0]["amount"]
+    c2.sendtoaddress(addr2, round(coin2 / 2, 8))
+    with pytest.raises(RuntimeError, match="Insufficient funds"):
+        c2.sendtoaddress(addr2, round(coin2 / 4, 8))
