@@ -81,8 +81,28 @@ class Node:
         except OSError:
             raise SystemExit(f"Cannot obtain a lock on data directory {self.datadir}. Nodexa is probably already running.")
 
+    def _check_legacy_flags(self) -> None:
+        """AppInitParameterInteraction's removed / renamed options: hard errors for -socks,
+        -rpcssl and -tor, warnings for options that are ignored now."""
+        a = self.args
+        if a.is_set("socks"):
+            raise SystemExit("Unsupported argument -socks found. Setting SOCKS version isn't possible anymore, "
+                             "only SOCKS5 proxies are supported.")
+        if a.get_bool("rpcssl", False):
+            raise SystemExit("SSL mode for RPC (-rpcssl) is no longer supported.")
+        if a.is_set("tor"):
+            raise SystemExit("Unsupported argument -tor found, use -onion.")
+        for old, hint in (("benchmark", "-benchmark is ignored, use -debug=bench."),
+                          ("debugnet", "Unsupported argument -debugnet ignored, use -debug=net."),
+                          ("whitelistalwaysrelay", "Unsupported argument -whitelistalwaysrelay ignored, use "
+                                                   "-whitelistrelay and/or -whitelistforcerelay."),
+                          ("blockminsize", "Unsupported argument -blockminsize ignored.")):
+            if a.is_set(old):
+                log.log_printf("Warning: " + hint)
+
     def start(self) -> None:
         a = self.args
+        self._check_legacy_flags()
         log.configure(a.get_list("debug"), a.get_list("debugexclude"),
                       os.path.join(self.datadir, "debug.log") if self.datadir else None,
                       console=a.get_bool("printtoconsole", True), timestamps=a.get_bool("logtimestamps", True),

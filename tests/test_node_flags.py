@@ -485,3 +485,13 @@ def test_spend_zeroconf_change_and_rpcserialversion(core, node_factory, tmp_path
     c2.sendtoaddress(addr2, round(coin2 / 2, 8))
     with pytest.raises(RuntimeError, match="Insufficient funds"):
         c2.sendtoaddress(addr2, round(coin2 / 4, 8))
+
+
+def test_removed_flags(core, node_factory, tmp_path):  # noqa: F811
+    for i, bad in enumerate(("-socks=4", "-rpcssl=1", "-tor=127.0.0.1:9050")):
+        d = tmp_path / f"old{i}"
+        os.makedirs(d)
+        with pytest.raises(SystemExit, match="socks|SSL|onion"):
+            node_factory((f"-datadir={d}", bad))
+    node, _ = node_factory(("-benchmark", "-debugnet"))  # accepted with a warning
+    assert client(node).getblockcount() == 0
