@@ -203,6 +203,8 @@ class ConnectionManager:
         self.whitelist: list = []            # -whitelist subnets (ipaddress networks)
         self.blocks_only = False             # -blocksonly: no transaction relay in either direction
         self.peer_bloom_filters = True       # -peerbloomfilters: NODE_BLOOM and the BIP37 messages
+        self.whitelist_relay = True          # -whitelistrelay: whitelisted peers' txs even with -blocksonly
+        self.whitelist_force_relay = True    # -whitelistforcerelay: re-announce their txs we already have
         self.user_agent = P.USER_AGENT       # with -uacomment
         # orphan transactions (mapOrphanTransactions): txid -> (tx, peer id, expiry), -maxorphantx
         self.orphans: dict[bytes, tuple] = {}
@@ -789,7 +791,7 @@ class ConnectionManager:
     def on_tx(self, peer: Peer, p: bytes) -> None:
         """AcceptToMemoryPool for a relayed tx (UTXO set, scripts, fees); accepted transactions
         are relayed to the other peers by the mempool signal."""
-        if self.blocks_only and not peer.whitelisted:  # fBlocksOnly: tx sent in violation of protocol
+        if self.blocks_only and not (peer.whitelisted and self.whitelist_relay):  # fBlocksOnly
             log.log_print("net", f"transaction sent in violation of protocol peer={peer.id}")
             return
         tx = _core.Transaction.deserialize(p)
@@ -797,6 +799,8 @@ class ConnectionManager:
         peer.known_txs.add(txid)
         REGISTRY.inc("p2p_tx_received_total", 1)
         if txid in self.state.mempool:
+            if peer.whitelisted and self.whitelist_force_relay:  # -whitelistforcerelay
+                self.announce_tx(txid)
             return
         ok, reason, _ = self.state.accept_to_mempool(tx)
         if ok:

@@ -431,6 +431,8 @@ class Node:
             self.connman.dns_seeds = list(DNS_SEEDS.get(self.network, []))
         self.connman.force_dns_seed = a.get_bool("forcednsseed", False)
         self.connman.peer_bloom_filters = a.get_bool("peerbloomfilters", True)
+        self.connman.whitelist_relay = a.get_bool("whitelistrelay", True)
+        self.connman.whitelist_force_relay = a.get_bool("whitelistforcerelay", True)
         self.connman.user_agent = P.user_agent(a.get_list("uacomment"))
         self.connman.start()
         cm = self.connman
