@@ -59,6 +59,7 @@ class Node:
         self._last_pprpc: tuple[str, float] | None = None
         self.gpus = gpu_list(args)
         self.rpc_witness = True  # -rpcserialversion=1
+        self.asset_index = args.get_bool("assetindex", False)  # -assetindex: per-address asset balance RPCs
         self.state: ChainState | None = None
         self.miner: MinerController | None = None
         self.rpc: RPCServer | None = None

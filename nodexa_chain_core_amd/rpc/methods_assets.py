@@ -242,7 +242,9 @@ def register(table, node) -> None:
         return out
 
     def rpc_listaddressesbyasset(p):
-        """listaddressesbyasset "asset_name" ( onlytotal ) ( count ) ( start )"""
+        """listaddressesbyasset "asset_name" ( onlytotal ) ( count ) ( start ) — needs -assetindex."""
+        if not getattr(node, "asset_index", False):  # fAssetIndex (src/rpc/assets.cpp:1074)
+            return "_This rpc call is not functional unless -assetindex is enabled. To enable, please run the wallet with -assetindex, this will require a reindex to occur"
         if not p:
             raise RPCError(RPC_INVALID_PARAMETER, 'listaddressesbyasset "asset_name"')
         rows = {_addr_of(h): amt / COIN for name, h, amt in st.assets.balances() if name == p[0]}
@@ -251,7 +253,9 @@ def register(table, node) -> None:
         return rows
 
     def rpc_listassetbalancesbyaddress(p):
-        """listassetbalancesbyaddress "address" ( onlytotal ) ( count ) ( start )"""
+        """listassetbalancesbyaddress "address" ( onlytotal ) ( count ) ( start ) — needs -assetindex."""
+        if not getattr(node, "asset_index", False):  # fAssetIndex (src/rpc/assets.cpp:742)
+            return "_This rpc call is not functional unless -assetindex is enabled. To enable, please run the wallet with -assetindex, this will require a reindex to occur"
         if not p:
             raise RPCError(RPC_INVALID_PARAMETER, 'listassetbalancesbyaddress "address"')
         h = _h160(p[0])

@@ -91,8 +91,11 @@ def _ext(core):
 
 
 def test_asset_lifecycle_regtest(core, node_factory):  # noqa: F811
-    node, _ = node_factory()
+    node, _ = node_factory(("-assetindex",))
     c = client(node)
+    node.asset_index = False  # without -assetindex the per-address views answer with the reference's notice
+    assert c.listaddressesbyasset("ROSE").startswith("_This rpc call is not functional unless -assetindex")
+    node.asset_index = True
     w = c.getnewaddress()
     c.generatetoaddress(120, w)
     with pytest.raises(RuntimeError, match="Assets aren't active"):

@@ -152,7 +152,7 @@ def test_reward_snapshot_hash_layout():
 
 
 def test_rewards_snapshot_and_distribution(core, tmp_path):
-    node = _node(core, tmp_path, "r", ["-minrewardheight=3"])
+    node = _node(core, tmp_path, "r", ["-minrewardheight=3", "-assetindex"])
     try:
         c = client(node)
         w = c.getnewaddress()
