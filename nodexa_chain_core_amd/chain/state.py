@@ -188,6 +188,7 @@ class ChainState:
         self._ibd_latched = False
         self.scripts_skipped = 0                                    # blocks connected under -assumevalid
         self.db_crash_ratio = 0                                     # -dbcrashratio fault injection
+        self.check_block_index_enabled = False                      # -checkblockindex
         self.max_mempool_bytes = DEFAULT_MAX_MEMPOOL_SIZE * 1_000_000  # -maxmempool
         self.rolling_min_fee = 0.0       # rollingMinimumFeeRate (sat per kvB)
         self._last_rolling_update = 0.0
@@ -689,8 +690,32 @@ class ChainState:
             self.ntx[h] = len(block.vtx)
             failed = self._activate()
             st = failed.get(h, ValidationState())
+            if self.check_block_index_enabled:
+                self.check_block_index()
             self._emit("block_checked", block, st)
             return st
+
+    def check_block_index(self) -> None:
+        """CheckBlockIndex (-checkblockindex): the active chain links back to genesis one height at
+        a time with strictly growing work, its tip is the UTXO set's block, every connected block
+        has its data stored, and the best header carries at least the tip's work. Raises
+        AssertionError on the first inconsistency."""
+        gen = self.chain.genesis()
+        tip = self.coins_tip()
+        assert tip is not None and self.chain.in_active_chain(tip), "UTXO tip not on the active chain"
+        prev = None
+        for height in range(0, tip.height + 1):
+            idx = self.chain.at_height(height)
+            assert idx is not None and idx.height == height, f"active chain hole at {height}"
+            if height == 0:
+                assert idx.hash == gen.hash, "active chain does not start at genesis"
+            else:
+                assert idx.prev_hash == prev.hash, f"active chain broken at {height}"
+                assert idx.chain_work > prev.chain_work, f"chain work not increasing at {height}"
+            assert idx.hash in self.block_pos or idx.hash in self._mem_blocks or height == 0, \
+                f"connected block {height} has no data"
+            prev = idx
+        assert self.chain.tip().chain_work >= tip.chain_work, "best header has less work than the tip"
 
     # ------------------------------------------------------------------ UTXO set / ActivateBestChain
     def _init_coins(self) -> None:

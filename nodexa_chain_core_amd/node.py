@@ -201,6 +201,9 @@ class Node:
             st.minimum_chain_work = int(a.get("minimumchainwork"), 16)
         st.max_tip_age = a.get_int("maxtipage", st.max_tip_age)
         st.db_crash_ratio = a.get_int("dbcrashratio", 0)
+        # -checkblockindex: off by default here (the reference turns it on for regtest; it is an
+        # O(chain) walk per block, so the suites enable it where they test it)
+        st.check_block_index_enabled = a.get_bool("checkblockindex", False)
         ser = a.get_int("rpcserialversion", 1)  # -rpcserialversion: 0 = non-segwit, 1 = segwit serialization
         if ser not in (0, 1):
             raise SystemExit("unknown rpcserialversion requested." if ser > 1 else "rpcserialversion must be non-negative.")

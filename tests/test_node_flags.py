@@ -495,3 +495,18 @@ def test_removed_flags(core, node_factory, tmp_path):  # noqa: F811
             node_factory((f"-datadir={d}", bad))
     node, _ = node_factory(("-benchmark", "-debugnet"))  # accepted with a warning
     assert client(node).getblockcount() == 0
+
+
+def test_checkblockindex(core, node_factory):  # noqa: F811
+    node, addr = node_factory(("-checkblockindex",))
+    c = client(node)
+    c.generatetoaddress(15, addr)
+    tip = c.getbestblockhash()
+    c.invalidateblock(c.getblockhash(10))  # disconnect back to height 9
+    node.state.check_block_index()
+    assert c.getblockcount() == 9
+    c.reconsiderblock(tip)
+    node.state.check_block_index()
+    assert c.getbestblockhash() == tip
+    c.generatetoaddress(3, addr)  # the checker runs inside every ProcessNewBlock
+    assert c.getblockcount() == 18
