@@ -309,6 +309,11 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
             from .protocol import RPC_CLIENT_NOT_CONNECTED
 
             raise RPCError(RPC_CLIENT_NOT_CONNECTED, "Clore is not connected!")
+        if params.mining_requires_peers and not node.args.get_bool("bypassdownload", False) \
+                and st.is_initial_block_download():
+            from .protocol import RPC_CLIENT_IN_INITIAL_DOWNLOAD
+
+            raise RPCError(RPC_CLIENT_IN_INITIAL_DOWNLOAD, "Clore is downloading blocks...")
         lp = req.get("longpollid")
         if isinstance(lp, str) and len(lp) >= 64:
             want = _core.u256_from_hex(lp[:64])
