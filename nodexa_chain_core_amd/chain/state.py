@@ -97,6 +97,7 @@ class MempoolEntry:
     height: int = 0          # tip height when the tx entered the pool
     fee_delta: int = 0       # prioritisetransaction adjustment (included in `fee`)
     size: int = 0            # serialized size with witness
+    sigop_cost: int = -1     # GetTransactionSigOpCost (-1: not computed, e.g. loaded from mempool.dat)
 
     def vsize(self) -> int:
         base = len(self.tx.serialize(False))
@@ -108,6 +109,7 @@ DEFAULT_MIN_RELAY_TX_FEE = 1_000_000   # sat per kvB (src/validation.h:69)
 DEFAULT_INCREMENTAL_RELAY_FEE = 1000   # sat per kvB (src/policy/policy.h:36)
 DEFAULT_ENABLE_REPLACEMENT = False     # -mempoolreplacement (src/validation.h:163)
 MAX_STANDARD_TX_WEIGHT = 400_000       # src/policy/policy.h:28
+MAX_STANDARD_TX_SIGOPS_COST = 80_000 // 5  # MAX_BLOCK_SIGOPS_COST / 5 (src/policy/policy.h)
 MAX_FEE_ESTIMATION_TIP_AGE = 3 * 60 * 60  # src/validation.h (IsCurrentForFeeEstimation)
 # package and expiry limits (src/validation.h:77-85) and the raw-tx fee cap (DEFAULT_TRANSACTION_MAXFEE)
 DEFAULT_ANCESTOR_LIMIT, DEFAULT_ANCESTOR_SIZE_LIMIT = 200, 250        # count, kvB
@@ -376,12 +378,12 @@ class ChainState:
 
     # ------------------------------------------------------------------ mempool-lite
     def add_to_mempool(self, tx, fee: int, entry_time: float | None = None, fee_delta: int = 0,
-                       replacement: bool = False) -> bytes:
+                       replacement: bool = False, sigop_cost: int = -1) -> bytes:
         txid = tx.txid()
         with self.lock:
             new = txid not in self.mempool
             e = MempoolEntry(tx, int(fee) + int(fee_delta), entry_time or self.adjusted_time(),  # GetTime(): mocktime aware
-                             self.chain.height(), int(fee_delta), len(tx.serialize(True)))
+                             self.chain.height(), int(fee_delta), len(tx.serialize(True)), int(sigop_cost))
             if new:
                 # processTransaction: fee estimates only learn from a node that is current, and not
                 # from replacements or children of pool transactions (validFeeEstimate)
@@ -986,6 +988,19 @@ class ChainState:
             return (o.value, o.script_pubkey, self.coins_tip().height + 1, False)
         return None
 
+    def mempool_sigop_cost(self, txid: bytes) -> int:
+        """GetTransactionSigOpCost of a pool transaction (cached on its entry; computed from the
+        spent outputs when the entry predates it, e.g. one loaded from mempool.dat)."""
+        with self.lock:
+            e = self.mempool[txid]
+            if e.sigop_cost < 0:
+                spent = [self._spent_coin(i.prevout) for i in e.tx.vin]
+                if any(c is None for c in spent):  # inputs gone: count what needs no spent outputs
+                    return _core.tx_legacy_sigops(e.tx.serialize(True)) * 4
+                e.sigop_cost = _core.tx_sigop_cost(e.tx.serialize(True), [c[1] for c in spent],
+                                                   _core.STANDARD_SCRIPT_VERIFY_FLAGS)
+            return e.sigop_cost
+
     def accept_to_mempool(self, tx, test_only: bool = False, max_fee: int | None = None) -> tuple[bool, str, int]:
         """AcceptToMemoryPoolWorker (src/validation.cpp): context-free checks, standardness,
         inputs present (UTXO set or pool), no pool conflict, coinbase maturity, fees and the
@@ -1045,6 +1060,10 @@ class ChainState:
             fee = in_sum - tx.value_out()
             if fee < 0:
                 return False, "bad-txns-in-belowout", 0
+            # GetTransactionSigOpCost with the spent outputs (P2SH redeem scripts, witness programs)
+            sigop_cost = _core.tx_sigop_cost(raw, [spk for _, spk in coins], _core.STANDARD_SCRIPT_VERIFY_FLAGS)
+            if sigop_cost > MAX_STANDARD_TX_SIGOPS_COST:
+                return False, "bad-txns-too-many-sigops", fee
             why = self._check_tx_assets(tx, raw, coins, aflags)
             if why:
                 return False, why, 0
@@ -1076,7 +1095,7 @@ class ChainState:
             if not test_only:
                 for t in replaced:  # BIP125: the replaced transactions and their descendants leave
                     self.pool_remove(t)
-                self.add_to_mempool(tx, fee, replacement=bool(replaced))
+                self.add_to_mempool(tx, fee, replacement=bool(replaced), sigop_cost=sigop_cost)
                 self.expire_mempool()  # LimitMempoolSize -> Expire, TrimToSize
                 self.trim_mempool()
                 if txid not in self.mempool:

@@ -455,6 +455,16 @@ void bind_script(py::module_& m) {
     m.def("decompress_amount", &decompress_amount);
     m.def("tx_legacy_sigops", [](const py::bytes& tx_raw) { return tx_legacy_sigops(tx_of(tx_raw)); },
           "GetLegacySigOpCount of a transaction (no spent outputs needed)");
+    m.def("tx_sigop_cost", [](const py::bytes& tx_raw, const std::vector<py::bytes>& spent_spks, u32 flags) {
+        const Transaction tx = tx_of(tx_raw);
+        std::vector<Coin> coins(spent_spks.size());
+        std::vector<const Coin*> ptrs;
+        for (size_t i = 0; i < spent_spks.size(); ++i) {
+            coins[i].out.script_pubkey = bytes_of(spent_spks[i]);
+            ptrs.push_back(&coins[i]);
+        }
+        return tx_sigop_cost(tx, ptrs, flags);
+    }, "GetTransactionSigOpCost: legacy x4 + P2SH redeem x4 + witness, given the spent scriptPubKeys");
 
     m.def("script_is_push_only", [](const py::bytes& s) { return script_is_push_only(bytes_of(s)); });
     m.def("is_valid_signature_encoding", [](const py::bytes& s) { return is_valid_signature_encoding(bytes_of(s)); });

@@ -152,7 +152,9 @@ def _ser_compact(n: int) -> bytes:
         return bytes([n])
     if n <= 0xFFFF:
         return b"\xfd" + struct.pack("<H", n)
-    return b"\xfe" + struct.pack("<I", n)
+    if n <= 0xFFFFFFFF:
+        return b"\xfe" + struct.pack("<I", n)
+    return b"\xff" + struct.pack("<Q", n)
 
 
 def _de_compact(b: bytes, off: int) -> tuple[int, int]:

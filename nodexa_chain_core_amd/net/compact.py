@@ -17,6 +17,8 @@ from .bloom import _de_compact, _ser_compact
 
 _core = core()
 SHORTID_MASK = (1 << 48) - 1
+# More transactions than fit a maximum-size block (8 MB / 60-byte minimum tx) is malformed.
+MAX_COMPACT_TXS = 1_000_000
 
 
 def _keys(header_bytes: bytes, nonce: int) -> tuple[int, int]:
@@ -58,9 +60,15 @@ class CompactBlock:
         (nonce,) = struct.unpack_from("<Q", p, off)
         off += 8
         n, off = _de_compact(p, off)
+        # the declared count is peer-controlled (CompactSize up to 2^64): bound it by the bytes
+        # actually present and by the block-size cap before building anything
+        if n > MAX_COMPACT_TXS or n > (len(p) - off) // 6:
+            raise ValueError("cmpctblock short-id count exceeds the payload")
         ids = [int.from_bytes(p[off + 6 * i:off + 6 * i + 6], "little") for i in range(n)]
         off += 6 * n
         m, off = _de_compact(p, off)
+        if n + m > MAX_COMPACT_TXS or m > len(p) - off:
+            raise ValueError("cmpctblock prefilled count exceeds the payload")
         prefilled, last = [], -1
         for _ in range(m):
             d, off = _de_compact(p, off)
@@ -68,8 +76,6 @@ class CompactBlock:
             off += used
             last += d + 1
             prefilled.append((last, tx))
-        if len(ids) + len(prefilled) > 1_000_000:
-            raise ValueError("compact block too large")
         return cls(header, hb, nonce, ids, prefilled)
 
     def reconstruct(self, pool_txs, version: int = 2):
@@ -112,10 +118,14 @@ def getblocktxn_payload(block_hash: bytes, indexes: list[int]) -> bytes:
 def parse_getblocktxn(p: bytes) -> tuple[bytes, list[int]]:
     h = p[:32]
     n, off = _de_compact(p, 32)
+    if n > len(p) - off:  # every index takes at least one byte
+        raise ValueError("getblocktxn index count exceeds the payload")
     out, last = [], -1
     for _ in range(n):
         d, off = _de_compact(p, off)
         last += d + 1
+        if last > 0xFFFF:  # BlockTransactionsRequest: differential index overflowed 16 bits
+            raise ValueError("getblocktxn index out of range")
         out.append(last)
     return h, out
 
@@ -127,6 +137,8 @@ def blocktxn_payload(block_hash: bytes, txs: list, witness: bool = True) -> byte
 def parse_blocktxn(p: bytes) -> tuple[bytes, list]:
     h = p[:32]
     n, off = _de_compact(p, 32)
+    if n > len(p) - off:
+        raise ValueError("blocktxn count exceeds the payload")
     txs = []
     for _ in range(n):
         tx, used = _core.Transaction.deserialize_prefix(p, off)

@@ -323,11 +323,17 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         tpl = node.template_for_gbt()
         blk = tpl.block
         hdr = blk.header
-        txs = []
+        # depends = 1-based template positions of in-template parents; sigops = GetTransactionSigOpCost
+        # (segwit is active on every network, so never divided by 4): src/rpc/mining.cpp:585-617
+        txs, pos = [], {blk.vtx[0].txid(): 0}
         for i, tx in enumerate(blk.vtx[1:], start=1):
-            e = st.mempool.get(tx.txid())
-            txs.append({"data": tx.serialize(True).hex(), "txid": _hex(tx.txid()), "hash": _hex(tx.wtxid()),
-                        "depends": [], "fee": e.fee if e else 0, "sigops": 0,
+            txid = tx.txid()
+            pos[txid] = i
+            e = st.mempool.get(txid)
+            deps = sorted({pos[x.prevout.hash] for x in tx.vin if x.prevout.hash in pos})
+            sigops = st.mempool_sigop_cost(txid) if e else _core.tx_legacy_sigops(tx.serialize(True)) * 4
+            txs.append({"data": tx.serialize(True).hex(), "txid": _hex(txid), "hash": _hex(tx.wtxid()),
+                        "depends": deps, "fee": e.fee if e else 0, "sigops": sigops,
                         "weight": len(tx.serialize(False)) * 3 + len(tx.serialize(True))})
         res = {
             "capabilities": ["proposal"],

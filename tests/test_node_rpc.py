@@ -88,6 +88,30 @@ def test_gbt_pprpcsb_roundtrip(core, node_factory):
         c.pprpcsb("00" * 32, mix.hex(), "%016x" % nonce)
 
 
+def test_gbt_depends_and_sigops(core, node_factory):
+    """getblocktemplate `depends` lists in-template parents by 1-based position and `sigops` is the
+    transaction's sigop cost (src/rpc/mining.cpp:585-617); pool software must not assume []/0."""
+    from wallet_util import fund, mature_coin, spend
+
+    node, addr = node_factory()
+    c = client(node)
+    w = fund(c, 101)
+    u = mature_coin(c)
+    parent = c.sendrawtransaction(spend(c, u["txid"], u["vout"], u["amount"], w, 5.0))
+    child = c.sendrawtransaction(spend(c, parent, 0, 5.0, w, 4.0))
+    tpl = c.getblocktemplate({"rules": ["segwit"]})
+    txs = {t["txid"]: (i + 1, t) for i, t in enumerate(tpl["transactions"])}
+    assert set(txs) == {parent, child}
+    ppos, pent = txs[parent]
+    cpos, cent = txs[child]
+    assert ppos == 1 and cpos == 2
+    assert pent["depends"] == [] and cent["depends"] == [1]
+    # two P2PKH outputs (OP_CHECKSIG each) x WITNESS_SCALE_FACTOR; P2PKH inputs add nothing
+    assert pent["sigops"] == cent["sigops"] == 8
+    raw = bytes.fromhex(cent["data"])
+    assert cent["sigops"] == core.tx_legacy_sigops(raw) * 4
+
+
 def test_submitblock_rejects(core, node_factory):
     node, addr = node_factory()
     c = client(node)

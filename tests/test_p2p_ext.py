@@ -5,6 +5,8 @@ import socket
 import struct
 import time
 
+import pytest
+
 from nodexa_chain_core_amd.net import protocol as P
 from nodexa_chain_core_amd.net.addrman import AddrMan
 from nodexa_chain_core_amd.net.bloom import BLOOM_UPDATE_ALL, BloomFilter
@@ -67,6 +69,30 @@ def test_compact_block_encoding_and_reconstruction(core):
     assert missing == [4, 5]
     h, idx = parse_getblocktxn(getblocktxn_payload(b"\x01" * 32, [4, 5, 9]))
     assert h == b"\x01" * 32 and idx == [4, 5, 9]
+
+
+def test_compact_block_rejects_oversized_counts(core):
+    """A ~90-byte cmpctblock declaring 2^64-1 short ids must be refused before any allocation
+    (the reference's deserialiser fails at end of stream); same for getblocktxn / blocktxn."""
+
+    from nodexa_chain_core_amd.net.bloom import _ser_compact
+    from nodexa_chain_core_amd.net.compact import parse_blocktxn
+
+    hdr = core.BlockHeader()
+    hdr.version, hdr.time, hdr.bits = 0x30000000, 1600000000, 0x207FFFFF
+    act = 2**31
+    head = hdr.serialize(act) + struct.pack("<Q", 7)
+    for n in (2**64 - 1, 2**32, 1_000_001, 3):
+        t0 = time.time()
+        with pytest.raises(ValueError):
+            CompactBlock.from_payload(head + _ser_compact(n) + b"\x00" * 12, act)
+        assert time.time() - t0 < 1.0
+    with pytest.raises(ValueError):
+        parse_getblocktxn(b"\x01" * 32 + _ser_compact(2**40) + b"\x00")
+    with pytest.raises(ValueError):
+        parse_getblocktxn(getblocktxn_payload(b"\x01" * 32, [0, 70000]))
+    with pytest.raises(ValueError):
+        parse_blocktxn(b"\x01" * 32 + _ser_compact(2**63))
 
 
 def _handshake(port, magic):
