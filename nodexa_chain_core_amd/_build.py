@@ -180,7 +180,10 @@ def hipcc_genco(src: str, out: str, defines: list[str] | None = None, includes: 
     cmd = [os.path.join(ROCM, "bin", "hipcc"), "--genco", "--offload-arch=" + ARCH, "-O3", "-std=c++17",
            "-mcode-object-version=5", "-ffp-contract=fast", "-I" + os.path.join(HIPDIR, "kernels")]
     for d in defines or []:
-        cmd.append("-D" + d)
+        if d.startswith("-mllvm:"):  # backend option of a tuning variant, e.g. "-mllvm:-amdgpu-sched-strategy=max-ilp"
+            cmd += ["-mllvm", d[len("-mllvm:"):]]
+        else:
+            cmd.append("-D" + d)
     for i in includes or []:
         cmd.append("-I" + i)
     _run(cmd + [src, "-o", out])

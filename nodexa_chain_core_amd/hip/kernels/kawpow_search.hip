@@ -43,6 +43,8 @@
 //   KP_HASHES     hashes interleaved per 16-lane group (1, 2, 4 or 8)
 //   KP_MIN_WAVES  minimum waves per SIMD for __launch_bounds__ (caps VGPRs)
 //   KP_NT_DAG     non-temporal DAG loads (the 4 GiB DAG has no L2 reuse)
+//   KP_SCHED_FENCE scheduling barriers around each round's cache/math program, so the DAG
+//                 gather issued at the top of the round is consumed only at its end
 #ifndef KP_HASHES
 #define KP_HASHES 2
 #endif
@@ -279,8 +281,17 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMo
     const uint32_t part = lane ^ (uint32_t)J;
 #pragma unroll
     for (int k = 0; k < KP_HASHES; ++k) d[k] = kp_dag_item(dag, kp_fastmod(kp_bcast<J>(mx[k][0]), items), part);
+#ifdef KP_SCHED_FENCE
+    // Keep the round's DAG merge after the whole cache/math program: left alone, the register-
+    // pressure scheduler pulls the merge (and its vmcnt wait) into the middle of the program, so
+    // a third of the round's work waits behind a ~1 us HBM gather instead of hiding it.
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM(l1, mx[k]);
+#ifdef KP_SCHED_FENCE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
 }
@@ -372,9 +383,19 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
 #else
     __shared__ uint32_t digs[KP_BLOCK * 8];
 #endif
+    __shared__ uint32_t stale;
     if (blockDim.x != KP_BLOCK) return;  // launched with the wrong block: no shares rather than bad ones
+    if (threadIdx.x == 0) {
+        // one uncached read of the host-mapped generation word per workgroup, overlapped with the
+        // L1 fill below: a template change stops queued work within one workgroup's lifetime
+        uint32_t s = 0;
+        if (p.gen_word) s = __hip_atomic_load(p.gen_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != p.generation;
+        stale = s;
+        if (s) atomicAdd(&p.results->skipped, 1u);
+    }
     kp_fill_l1(l1, p.dag);
     __syncthreads();
+    if (stale) return;  // uniform over the workgroup, after its only barrier
 
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t nonce = p.start_nonce + (uint64_t)blockIdx.x * KP_BLOCK + threadIdx.x;
@@ -392,7 +413,12 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     for (int k = 0; k < 8; ++k) digest[k] = dig[lane * 8 + k];
 #endif
     uint32_t st2[8], fin[8];
-    kp_seed(p.header, nonce, st2);  // recomputed: cheaper than 6 VGPRs held across the mix loop
+    // recomputed: cheaper than 6 VGPRs held across the mix loop. The nonce goes through an empty
+    // asm so the compiler cannot CSE this keccak with the first one (it would keep those results
+    // live across the whole hash loop and spill them).
+    uint32_t nlo = (uint32_t)nonce, nhi = (uint32_t)(nonce >> 32);
+    asm volatile("" : "+v"(nlo), "+v"(nhi));
+    kp_seed(p.header, ((uint64_t)nhi << 32) | nlo, st2);
     kp_final(st2, digest, fin);
     const uint64_t head = ((uint64_t)__builtin_bswap32(fin[0]) << 32) | __builtin_bswap32(fin[1]);
     if (head <= p.target) {

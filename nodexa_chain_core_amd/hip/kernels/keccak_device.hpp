@@ -76,8 +76,15 @@ __constant__ static const uint64_t nx_keccak_rc[24] = {
 #define NX_R32(x, n) nx_rotl32((x), (n) & 31)
 #define NX_R64(x, n) nx_rotl64((x), (n))
 
+// NX_KECCAK800_ROLLED keeps the 22 rounds as a loop: ~55 live VGPRs at most, where the unrolled
+// form lets the scheduler overlap rounds and, under a tight register budget (the 6-wave KawPow
+// search kernel has 80), spill.
 NX_DEV void keccak_f800(uint32_t a[25]) {
+#ifdef NX_KECCAK800_ROLLED
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
     for (int r = 0; r < 22; ++r) NX_KECCAK_ROUND(uint32_t, a, NX_R32, (uint32_t)nx_keccak_rc[r]);
 }
 

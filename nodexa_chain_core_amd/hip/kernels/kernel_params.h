@@ -36,7 +36,8 @@ struct KawpowShare {
 
 struct KawpowResults {
     uint32_t count;     // number of shares appended (may exceed MAX; extra dropped)
-    uint32_t pad[3];
+    uint32_t skipped;   // workgroups that found their launch stale (generation moved on) and searched nothing
+    uint32_t pad[2];
     struct KawpowShare shares[NODEXA_KAWPOW_MAX_SHARES];
 };
 
@@ -48,6 +49,11 @@ struct KawpowSearchParams {
     uint32_t header[8];        // header hash words (storage order)
     struct FastMod32 items;    // modulo by number of 2048-bit items (full_items / 2)
     uint32_t* scratch;         // >= 8 words per nonce of the launch (variants that park digests in HBM)
+    // Stale-work abort: each workgroup reads *gen_word (host-mapped, written by the miner when the
+    // template changes) once at its start and searches nothing if it differs from `generation`.
+    const uint32_t* gen_word;  // nullptr: never abort
+    uint32_t generation;
+    uint32_t pad;
 };
 
 // Light-mode / full-DAG batch verification of (header, nonce) pairs.

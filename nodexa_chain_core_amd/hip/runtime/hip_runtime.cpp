@@ -282,7 +282,7 @@ PYBIND11_MODULE(_hip, m) {
     m.def("launch_kawpow_search", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t results,
                                      const py::bytes& header, uint64_t start_nonce, uint64_t target,
                                      uint64_t num_nonces, uintptr_t stream, uintptr_t scratch,
-                                     uint64_t scratch_bytes) {
+                                     uint64_t scratch_bytes, uintptr_t gen_word, uint32_t generation) {
         // search variants are compiled for different block sizes (KP_BLOCK); their
         // __launch_bounds__ is the block, one nonce per thread
         const unsigned block = unsigned(k.max_threads);
@@ -299,9 +299,37 @@ PYBIND11_MODULE(_hip, m) {
         p.target = target;
         load_words(header, p.header);
         p.items = make_fastmod(dag_items2048);
+        p.gen_word = reinterpret_cast<const uint32_t*>(gen_word);
+        p.generation = generation;
         const uint64_t grid = num_nonces / block;
         if (grid == 0 || grid > 0x7fffffffULL) throw std::invalid_argument("bad search grid");
         k.launch_bytes(dim3(unsigned(grid)), dim3(block), 0, as_stream(stream), &p, sizeof(p));
+    }, py::arg("kernel"), py::arg("dag"), py::arg("dag_items2048"), py::arg("results"), py::arg("header"),
+       py::arg("start_nonce"), py::arg("target"), py::arg("num_nonces"), py::arg("stream"), py::arg("scratch"),
+       py::arg("scratch_bytes"), py::arg("gen_word") = 0, py::arg("generation") = 0);
+
+    // Host-mapped words (fine-grained, coherent pinned memory): the miner's stale-work generation
+    // word that running search kernels poll once per workgroup. The pointer is valid on the host
+    // and, under HIP's unified addressing, in device code of every GPU of the process.
+    m.def("host_words_alloc", [](size_t n) {
+        void* p = nullptr;
+        check(hipHostMalloc(&p, n * 4, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable),
+              "hipHostMalloc(words)");
+        std::memset(p, 0, n * 4);
+        void* d = nullptr;
+        check(hipHostGetDevicePointer(&d, p, 0), "hipHostGetDevicePointer");
+        if (d != p) {
+            (void)hipHostFree(p);
+            throw std::runtime_error("host-mapped word has a different device address (no unified addressing)");
+        }
+        return reinterpret_cast<uintptr_t>(p);
+    });
+    m.def("host_words_free", [](uintptr_t p) { check(hipHostFree(reinterpret_cast<void*>(p)), "hipHostFree"); });
+    m.def("host_word_store", [](uintptr_t p, size_t i, uint32_t v) {
+        __atomic_store_n(reinterpret_cast<uint32_t*>(p) + i, v, __ATOMIC_SEQ_CST);
+    });
+    m.def("host_word_load", [](uintptr_t p, size_t i) {
+        return __atomic_load_n(reinterpret_cast<const uint32_t*>(p) + i, __ATOMIC_SEQ_CST);
     });
 
     m.def("launch_kawpow_hash_batch", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t jobs,

@@ -33,11 +33,33 @@ class Share:
     final_hash: bytes  # 32 bytes, storage order
 
     def verify_host(self, block_number: int, header_hash: bytes, boundary: bytes | None = None) -> bool:
-        """Mix-only recomputation (cheap) + optional full 256-bit boundary check."""
+        """Mix-only recomputation (cheap: the final keccak from the GPU's own mix) + optional full
+        256-bit boundary check. A wrong DAG gather or program would pass this; `verify_full` not."""
         fin = _core.kawpow_hash_no_verify(block_number, header_hash, self.mix_hash, self.nonce)
         if fin != self.final_hash:
             return False
         return boundary is None or _core.hash_le(fin, boundary)
+
+    def verify_full(self, block_number: int, header_hash: bytes, boundary: bytes | None = None, ctx=None) -> bool:
+        """Full light-mode KawPow on the host (progpow::verify, src/crypto/ethash/lib/ethash/
+        progpow.cpp:431-495): recompute mix and final from the epoch's light cache and require both
+        to equal what the GPU reported (+ optional 256-bit boundary check)."""
+        ctx = ctx if ctx is not None else _core.get_epoch_context(block_number // _core.EPOCH_LENGTH)
+        fin, mix = _core.kawpow_hash(ctx, block_number, header_hash, self.nonce)
+        if fin != self.final_hash or mix != self.mix_hash:
+            return False
+        return boundary is None or _core.hash_le(fin, boundary)
+
+
+def parse_results(raw: bytes, max_shares: int) -> tuple[list[Share], int, int]:
+    """(shares sorted by nonce, appended count, skipped workgroups) of one KawpowResults ring."""
+    count, skipped = struct.unpack_from("<II", raw, 0)
+    shares = []
+    for i in range(min(count, max_shares)):
+        vals = struct.unpack_from(SHARE_FMT, raw, 16 + i * SHARE_SIZE)
+        shares.append(Share(vals[0], struct.pack("<8I", *vals[1:9]), struct.pack("<8I", *vals[9:17])))
+    shares.sort(key=lambda s: s.nonce)
+    return shares, count, skipped
 
 
 def target_prefix(boundary: bytes) -> int:
@@ -88,17 +110,22 @@ class KawpowSearcher:
 
     # ------------------------------------------------------------------
     def launch(self, header_hash: bytes, start_nonce: int, num_nonces: int, target64: int,
-               stream: int | None = None) -> None:
-        """Queue one search window on `stream` (no host sync)."""
+               stream: int | None = None, results: torch.Tensor | None = None, gen_word: int = 0,
+               generation: int = 0) -> None:
+        """Queue one search window on `stream` (no host sync). `results`: the share ring to append
+        to (default: this searcher's own; the caller clears a ring it passes). `gen_word`: host-mapped
+        generation word; workgroups that start after it moved past `generation` search nothing."""
         if num_nonces % self.block:
             raise ValueError(f"num_nonces must be a multiple of {self.block}")
         with torch.cuda.device(self.device):
             s = runtime.current_stream_handle() if stream is None else stream
             scratch = self.scratch(num_nonces)
-            self.results[:4].zero_()
+            if results is None:
+                results = self.results
+                results[:4].zero_()
             self.h.launch_kawpow_search(self.kernel, self.epoch_dev.dag.data_ptr(), self.epoch_dev.items2048,
-                                        self.results.data_ptr(), header_hash, start_nonce, target64, num_nonces, s,
-                                        scratch.data_ptr(), scratch.numel() * 4)
+                                        results.data_ptr(), header_hash, start_nonce, target64, num_nonces, s,
+                                        scratch.data_ptr(), scratch.numel() * 4, gen_word, generation)
 
     def scratch(self, num_nonces: int) -> torch.Tensor:
         """Per-nonce digest parking space (8 words/nonce) for the launch; grown on demand.
@@ -112,16 +139,7 @@ class KawpowSearcher:
         """Copy the share ring back (synchronises the current stream)."""
         with torch.cuda.device(self.device):
             self.results_host.copy_(self.results, non_blocking=False)
-        raw = self.results_host.numpy().tobytes()
-        count = struct.unpack_from("<I", raw, 0)[0]
-        shares = []
-        for i in range(min(count, self.h.KAWPOW_MAX_SHARES)):
-            vals = struct.unpack_from(SHARE_FMT, raw, 16 + i * SHARE_SIZE)
-            mix = struct.pack("<8I", *vals[1:9])
-            fin = struct.pack("<8I", *vals[9:17])
-            shares.append(Share(vals[0], mix, fin))
-        shares.sort(key=lambda s: s.nonce)
-        return shares
+        return parse_results(self.results_host.numpy().tobytes(), self.h.KAWPOW_MAX_SHARES)[0]
 
     @traced("kawpow.search")
     def search(self, header_hash: bytes, start_nonce: int, num_nonces: int, boundary: bytes) -> list[Share]:

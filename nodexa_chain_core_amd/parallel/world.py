@@ -41,8 +41,9 @@ class World:
 _WORLD: World | None = None
 
 
-def init(use_gpu: bool | None = None, timeout_s: int = 600) -> World:
-    """Initialise from RANK/WORLD_SIZE/LOCAL_RANK (torchrun) or single-process."""
+def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | None = None) -> World:
+    """Initialise from RANK/WORLD_SIZE/LOCAL_RANK (torchrun, or the node's spawned miner ranks)
+    or single-process. `device_index`: the GPU of this rank (default: LOCAL_RANK)."""
     global _WORLD
     if _WORLD is not None:
         return _WORLD
@@ -52,7 +53,8 @@ def init(use_gpu: bool | None = None, timeout_s: int = 600) -> World:
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
     if use_gpu:
-        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(device_index if device_index is not None
+                              else local_rank % max(1, torch.cuda.device_count()))
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")

@@ -1,0 +1,63 @@
+"""Rank 0 of a multi-process mining world for tests/test_miner_service.py (gloo, CPU devices).
+
+Runs a regtest ChainState with the ChainLeader and mines `NODEXA_TEST_BLOCKS` blocks to one
+script, then switches the request to a second script (a template change that is not a tip
+change) for as many more, then sends the stop packet. Writes a JSON report to argv[1]."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main(out_path: str) -> int:
+    from nodexa_chain_core_amd import core
+    from nodexa_chain_core_amd.chain.state import ChainState, make_params
+    from nodexa_chain_core_amd.miner.search import CpuSearchDevice
+    from nodexa_chain_core_amd.miner.service import ChainLeader, MiningService
+    from nodexa_chain_core_amd.parallel import world as W
+
+    _core = core()
+    timeout = float(os.environ.get("NODEXA_MINER_COLLECTIVE_TIMEOUT", "30"))
+    W.init(use_gpu=False, timeout_s=int(max(timeout, 10)))
+    blocks = int(os.environ.get("NODEXA_TEST_BLOCKS", "2"))
+    window = int(os.environ.get("NODEXA_MINER_WINDOW", "8"))
+    state = ChainState(make_params("regtest"), None)
+    leader = ChainLeader(state, target_bits=int(os.environ.get("NODEXA_TEST_TARGET_BITS", "7")))
+    svc = MiningService(CpuSearchDevice(max_window=window), leader, window=window, collective_timeout_s=timeout,
+                        record_windows=True)
+    scripts = [bytes([0x51]), bytes([0x52])]
+    found, t0 = [], time.time()
+    for spk in scripts:
+        req = leader.mine(spk, blocks=blocks)
+        while not req.done.is_set():
+            if time.time() - t0 > 240:
+                raise SystemExit("rank 0: mining took too long")
+            try:
+                svc.step()
+            except Exception as e:  # noqa: BLE001 — a lost rank: rebuild the world and go on
+                from nodexa_chain_core_amd.miner.service import CollectiveError
+
+                if not isinstance(e, CollectiveError):
+                    raise
+                svc.recover(e)
+        found.append(list(req.found))
+    leader.shutdown()
+    while svc.step():
+        pass
+    act = state.params.kawpow_activation_time
+    coinbase = [[_core.Block.deserialize(state.get_block_raw(_core.u256_from_hex(h)), act).vtx[0].vout[0]
+                 .script_pubkey.hex() for h in hs] for hs in found]
+    report = {"coinbase": coinbase, "height": state.height(), "found": found, "windows": svc.windows, "world_size": svc.world_size,
+              "hashes_total": svc.hashes_total, "stats": leader.stats, "steps": svc.steps,
+              "tip": _core.u256_hex(state.tip().hash), "rank_hashes": svc.rank_hashes}
+    with open(out_path, "w") as f:
+        json.dump(report, f)
+    W.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1]))
