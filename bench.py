@@ -1,20 +1,29 @@
 #!/usr/bin/env python3
-"""Headline benchmark: KawPow MH/s (+ Equihash(200,9) Sol/s), whole node, N MI355X.
+"""Headline benchmark: KawPow MH/s (+ Equihash(200,9) Sol/s, + batch header verify), whole node, N MI355X.
 
-BASELINE.json config 2/4: KawPow miner on a synthetic regtest header with a
-4 GiB DAG (epoch 384), nonce-range data parallelism over N GPUs (one process
-per GPU, RCCL over xGMI): the work packet (header hash, target, height) is
-broadcast from rank 0, every rank searches its own disjoint nonce window per
-step, and the per-rank share rings are all-gathered on the GPU stream after
-every search kernel — the full mining step, nothing skipped.
+BASELINE.json config 2/4: KawPow mining on a synthetic regtest header with a 4 GiB DAG (epoch
+384), nonce-range data parallelism over N GPUs, one process per GPU, RCCL over xGMI. The timed
+step is the node's own mining loop — `miner/service.MiningService.step`, the code `nodexad
+-gpus=...` mines with — driven by a fixed synthetic job (BenchLeader) instead of a chain:
+
+  queue the next 2^25-nonce window on this GPU / take the previous window's shares
+  -> all-gather the share records -> all-reduce the hash counters -> rank 0 consumes the shares
+  -> broadcast the 96-byte work packet from rank 0.
+
+The DAG is built sharded over the ranks and all-gathered before timing (reported as
+dag_build_s). After timing, rank 0 re-hashes up to 8 of the gathered shares with the host
+golden model (light mode, `_core.kawpow_hash`) and exits non-zero on any mismatch.
+
+Extras on the same line: Equihash(200,9) Sol/s (config 3) and batch header verification of
+the committed 10k-header fixture through models/verify.process_headers, PoW + DGW/contextual,
+every header required to be accepted (config 5; per-epoch setup excluded, reported).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
           --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
 
-One step = one search window of --batch nonces per GPU (weak scaling).
-Timing: W untimed steps, barrier + synchronize, K timed steps, synchronize +
-barrier, max elapsed over ranks. Rank 0 prints ONE JSON line.
+Timing: W untimed steps, barrier + synchronize, K timed steps, synchronize + barrier, max
+elapsed over ranks. Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -27,6 +36,8 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+VERIFY_FIXTURE = os.path.join(ROOT, "tests", "data", "testnet_mixed_10k.hdr")
+
 
 def _baseline() -> tuple[float | None, str | None]:
     """The reference publishes no KawPow number. Use a published one if
@@ -46,6 +57,44 @@ def _baseline() -> tuple[float | None, str | None]:
         return None, None
 
 
+def _verify_headers_bench(log) -> dict | None:
+    """BASELINE config 5 over the ranks (parallel/verify.py: full-hash slices + RCCL all-gather)."""
+    import functools
+
+    import torch
+
+    from nodexa_chain_core_amd import _core
+    from nodexa_chain_core_amd.models import synthetic
+    from nodexa_chain_core_amd.models.verify import process_headers
+    from nodexa_chain_core_amd.parallel import world as W
+    from nodexa_chain_core_amd.parallel.verify import verify_headers_distributed
+
+    if not os.path.exists(VERIFY_FIXTURE):
+        return None
+    params, headers = synthetic.load(VERIFY_FIXTURE)
+    adjusted = headers[-1].time + 3600
+    n = len(headers)
+    out = {"headers": n, "fixture": os.path.relpath(VERIFY_FIXTURE, ROOT)}
+    for mode in ("dag", "light"):
+        fn = functools.partial(verify_headers_distributed, mode=mode)
+        t0 = time.perf_counter()
+        warm = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn)  # every epoch's state
+        torch.cuda.synchronize()
+        setup = W.all_reduce_max(time.perf_counter() - t0)
+        W.barrier()
+        t0 = time.perf_counter()
+        r = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn)
+        torch.cuda.synchronize()
+        W.barrier()
+        dt = W.all_reduce_max(time.perf_counter() - t0)
+        if r["accepted"] != n or warm["accepted"] != n:
+            raise SystemExit(f"header verify ({mode}): accepted {r['accepted']}/{n}, first reject {r['reject']}")
+        out[mode] = {"headers_per_s": round(n / dt, 1), "ms": round(dt * 1e3, 2), "pow_ms": round(r["pow_s"] * 1e3, 2),
+                     "context_ms": round(r["context_s"] * 1e3, 2), "first_run_incl_epoch_setup_s": round(setup, 3)}
+        log(f"[bench] verify {n} headers ({mode}): {n / dt:.0f} headers/s")
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -53,9 +102,15 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--epoch", type=int, default=384, help="384 -> 4 GiB DAG (BASELINE config)")
     ap.add_argument("--batch", type=int, default=1 << 25,
-                    help="nonces per GPU per step (profiles/r2q: 2^25 amortises the kernel tail, +0.9 %% vs 2^23)")
+                    help="nonces per GPU per step (profiles/r2q: 2^25 amortises the kernel tail)")
     ap.add_argument("--equihash", type=int, default=12,
                     help="Equihash(200,9): batches of 8 solves per GPU to time (0 = skip)")
+    ap.add_argument("--verify", type=int, default=1, help="1: time BASELINE config 5 (batch header verify)")
+    ap.add_argument("--check-shares", type=int, default=8, help="shares re-hashed on the host after timing")
+    ap.add_argument("--corrupt-dag", action="store_true",
+                    help="test hook: damage every 64th DAG item after the build; the share check must fail")
+    ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
+                    help="cpu: rehearse the same loop and collectives on host devices over gloo (tests)")
     ap.add_argument("--quiet", action="store_true")
     args = ap.parse_args()
 
@@ -63,82 +118,108 @@ def main() -> int:
 
     from nodexa_chain_core_amd import _build
 
-    _build.build_all()
+    cpu = args.device == "cpu"
+    if cpu:
+        _build.build_core()
+    else:
+        _build.build_all()
     from nodexa_chain_core_amd import _core
     from nodexa_chain_core_amd.chain.header import BlockHeader
-    from nodexa_chain_core_amd.ops import jit
-    from nodexa_chain_core_amd.ops.ethash import DeviceEpoch
-    from nodexa_chain_core_amd.ops.kawpow import KawpowSearcher
-    from nodexa_chain_core_amd.parallel import dag as pdag
+    from nodexa_chain_core_amd.miner.search import CpuSearchDevice, Work
+    from nodexa_chain_core_amd.miner.service import BenchLeader, MiningService
     from nodexa_chain_core_amd.parallel import world as W
-    from nodexa_chain_core_amd.parallel.shares import ShareGather
 
-    world = W.init(use_gpu=True)
+    world = W.init(use_gpu=not cpu)
     rank, ws = world.rank, world.world_size
     log = (lambda *a: print(*a, file=sys.stderr, flush=True)) if (rank == 0 and not args.quiet) else (lambda *a: None)
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
 
     height = args.epoch * _core.EPOCH_LENGTH + 123
-    period = height // 3
-    # Compile the period kernel before touching the DAG (child-process compile).
-    jit.get(period) if rank == 0 else None
+    if not cpu:
+        from nodexa_chain_core_amd.ops import jit
+
+        # compile this period's kernel (child-process hipcc, cached on disk) before the DAG exists
+        jit.get(height // 3) if rank == 0 else None
     W.barrier()
 
-    # Synthetic regtest header (KawPow layout; time after activation).
+    # synthetic regtest header (KawPow layout); ~1 share per 2^22 nonces so shares flow every step
     hdr = BlockHeader(version=0x20000000, prev=_core.sha256d(b"nodexa-bench-prev"),
                       merkle_root=_core.sha256d(b"nodexa-bench-merkle"), time=1_700_000_000,
                       bits=0x1b00ffff, height=height)
-    work = struct.pack("<32sQII", hdr.progpow_header_hash(), 0, height, 0)
-    work = W.broadcast_bytes(work if rank == 0 else None, len(work))
-    header_hash, _, height, _ = struct.unpack("<32sQII", work)
-    # Target: ~1 share per 2^22 nonces, so the share path is exercised every step.
-    target64 = (1 << 64) // (1 << 22)
+    share_bits = 1 if cpu else 22
+    boundary = ((1 << 256) // (1 << share_bits) - 1).to_bytes(32, "big")
+    work = Work(hdr.progpow_header_hash(), boundary, height, 1, 0x5EED_0000_0000_0000, 0)
 
     t0 = time.time()
     ctx = _core.get_epoch_context(args.epoch)
-    log(f"[bench] light cache epoch {args.epoch}: {ctx.light_bytes/2**20:.0f} MiB in {time.time()-t0:.1f}s")
-    ep = DeviceEpoch(args.epoch, ctx=ctx, world_size=ws)
-    torch.cuda.synchronize()
-    t0 = time.time()
-    pdag.build_dag(ep)
-    torch.cuda.synchronize()
-    dag_s = time.time() - t0
-    log(f"[bench] DAG {ep.dag_bytes/2**30:.2f} GiB built in {dag_s:.2f}s over {ws} GPU(s)")
-    if not ep.l1_matches():
-        raise SystemExit("DAG L1 mismatch vs host golden model")
+    log(f"[bench] light cache epoch {args.epoch}: {ctx.light_bytes / 2**20:.0f} MiB in {time.time() - t0:.1f}s")
+    if cpu:
+        dev, block, dag_s = CpuSearchDevice(max_window=args.batch), 1, 0.0
+    else:
+        from nodexa_chain_core_amd.miner.search import GpuSearchDevice
 
-    searcher = KawpowSearcher(ep, height)
-    gather = ShareGather(searcher)
-    nonce_base = 0x5EED_0000_0000_0000
-    batch = args.batch // searcher.block * searcher.block  # whole workgroups of the tuned kernel
+        dev = GpuSearchDevice(world.device.index, collective_dag=world.distributed)
+        sync()
+        W.barrier()
+        t0 = time.time()
+        block = dev.searcher(height).block  # sharded DAG build + all-gather, L1 self-check, period kernel
+        sync()
+        dag_s = W.all_reduce_max(time.time() - t0)
+        ep = dev.epochs[args.epoch]
+        log(f"[bench] DAG {ep.dag_bytes / 2**30:.2f} GiB built in {dag_s:.2f}s over {ws} GPU(s)")
+        if args.corrupt_dag:
+            v = ep.dag.view(torch.int32)
+            rows = v[:v.numel() // 64 * 64].view(-1, 64)  # one row per 256-byte 2048-bit item
+            rows[64::64, :] ^= 0x5A5A5A5A  # the first 64 items are the L1 (checked above); spare them
+            sync()
+        del ep
 
-    def step(i: int) -> None:
-        start = nonce_base + (i * ws + rank) * batch
-        searcher.launch(header_hash, start, batch, target64)
-        gather.enqueue()
+    leader = BenchLeader(work) if rank == 0 else None
+    svc = MiningService(dev, leader, window=max(block, args.batch // block * block))
+    batch = svc.window
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
+    svc.step()  # the work packet goes out (the loop starts idle)
+    for _ in range(args.warmup):
+        svc.step()
+    sync()
     W.barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
-        step(i)
-    torch.cuda.synchronize()
+    for _ in range(args.steps):
+        svc.step()
+    sync()
     W.barrier()
-    elapsed = time.perf_counter() - t_start
-    elapsed = W.all_reduce_max(elapsed)
-
-    # Validate the last step's gathered shares bit-exactly on the host.
-    shares = gather.collect()
-    bad = [s for s in shares if not s.verify_host(height, header_hash)]
-    if bad:
-        raise SystemExit(f"{len(bad)} invalid shares from the GPU")
+    elapsed = W.all_reduce_max(time.perf_counter() - t_start)
     total = batch * ws * args.steps
     mhs = total / elapsed / 1e6
+    # stop every rank's loop (stop packet; the queued window is aborted), then drain
+    if leader is not None:
+        leader.shutdown()
+    while svc.step():
+        pass
+    svc.pipe.drain()
+
+    checked = bad = 0
+    if rank == 0:
+        # full host re-hash (light mode) of the gathered shares: mix and final must both match
+        t0 = time.time()
+        for s in leader.shares[:args.check_shares]:
+            checked += 1
+            bad += not s.verify_full(height, work.header_hash, work.boundary, ctx=ctx)
+        log(f"[bench] {checked} shares re-hashed on the host in {time.time() - t0:.1f}s: {bad} mismatches")
+    bad = W.all_reduce_sum_int(bad)
+    if args.check_shares and W.all_reduce_sum_int(checked) == 0:
+        raise SystemExit("no shares to re-hash: the search produced none")
+    if bad:
+        raise SystemExit(f"{bad} GPU shares failed the full host re-hash")
+    del svc
+    dev.close()
+    del dev
+    if not cpu:
+        torch.cuda.empty_cache()
 
     eq_sols = None
-    if args.equihash:
+    if args.equihash and not cpu:
         # Equihash(200,9): every rank solves its own nonces (weak scaling);
         # node Sol/s = all solutions / slowest rank's time.
         from nodexa_chain_core_amd.ops.equihash import EquihashSolver
@@ -162,6 +243,8 @@ def main() -> int:
         del solver
         log(f"[bench] Equihash(200,9): {eq_sols} Sol/s ({args.equihash} x 8 solves per rank)")
 
+    verify = _verify_headers_bench(log) if args.verify and not cpu else None
+
     if rank == 0:
         base, base_src = _baseline()
         out = {
@@ -176,27 +259,34 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(mhs / base, 3) if base else None,
             "dtype": "u32",
+            "device": args.device,
             "data": "synthetic regtest header + sequential nonces; the real epoch DAG generated on the GPU "
                     "(no chain data)",
             "config": {
                 "model": f"KawPow (ProgPoW 0.9.4, RAVENCOINKAWPOW) epoch {args.epoch}, "
-                         f"{ep.dag_bytes/2**30:.2f} GiB DAG, height {height}",
+                         f"{ep_bytes_gib(args.epoch):.2f} GiB DAG, height {height}",
                 "global_batch": batch * ws,
                 "seq_len": None,
                 "parallelism": f"dp{ws}",
             },
-            "shares_last_step": len(shares),
+            "loop": "miner/service.MiningService.step (the node's mining loop)",
+            "shares_rehashed": checked,
             "dag_build_s": round(dag_s, 3),
             "equihash_sol_per_s": eq_sols,
+            "verify_headers": verify,
+            "verify_headers_per_s": verify["dag"]["headers_per_s"] if verify else None,
             "baseline_mhs": base,
             "baseline_source": base_src,
         }
-        for k, v in list(out.items()) + [("config." + a, b) for a, b in out["config"].items()]:
-            if isinstance(v, (bytes, bytearray)):
-                print(f"[bench] warning: field {k} is bytes", file=sys.stderr)
-        print(json.dumps(out, default=lambda o: o.hex() if isinstance(o, (bytes, bytearray)) else str(o)), flush=True)
+        print(json.dumps(out), flush=True)
     W.shutdown()
     return 0
+
+
+def ep_bytes_gib(epoch: int) -> float:
+    from nodexa_chain_core_amd import _core
+
+    return _core.full_dataset_num_items(epoch) * 128 / 2**30
 
 
 if __name__ == "__main__":

@@ -182,8 +182,10 @@ def hipcc_genco(src: str, out: str, defines: list[str] | None = None, includes: 
     for d in defines or []:
         if d.startswith("-mllvm:"):  # backend option of a tuning variant, e.g. "-mllvm:-amdgpu-sched-strategy=max-ilp"
             cmd += ["-mllvm", d[len("-mllvm:"):]]
-        else:
-            cmd.append("-D" + d)
+            continue
+        if d == "KP_SCHED_ILP":  # tuning variant: the AMDGPU max-ILP machine scheduler
+            cmd += ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+        cmd.append("-D" + d)
     for i in includes or []:
         cmd.append("-I" + i)
     _run(cmd + [src, "-o", out])

@@ -7,13 +7,15 @@ nHashesPerSec for getmininginfo). Fixed here: the reference's internal miner
 bumps the 32-bit nNonce, which KawPow headers do not serialize or hash
 (SURVEY §3.6); this controller always searches nNonce64.
 
-Backends
-  * GpuKawpowBackend — the MI355X path: epoch DAG resident in HBM (next
-    epoch prebuilt on demand), per-period JIT kernel, nonce windows of
-    `intensity` nonces per launch, every share re-checked on the host.
-  * CpuKawpowBackend — the reference-equivalent light-mode CPU search
-    (progpow::search_light), used when no GPU is configured (e.g. regtest
-    plumbing tests on CPU-only hosts).
+Two ways to mine:
+  * the mining service (miner/service.py) — the MI355X path and the only KawPow path of a GPU
+    node: one process per GPU in one torch.distributed world (RCCL), a pipelined 2^25-nonce
+    search loop per GPU, rank 0 (this node) turning shares into blocks. `MinerController` then
+    only forwards generate / setgenerate / getmininginfo to the service's leader.
+  * host backends in threads — CpuKawpowBackend (the reference-equivalent light-mode search,
+    progpow::search_light) for CPU-only nodes, and the host X16R / X16RV2 search for templates
+    before the KawPow activation. GpuKawpowBackend remains as a synchronous single-window search
+    object (remote miner, tests), not as a mining thread.
 """
 from __future__ import annotations
 
@@ -145,8 +147,8 @@ class GpuKawpowBackend:
             shares = [x for x in shares if x.nonce < end]
             if shares:
                 sh = shares[0]
-                if not sh.verify_host(block_number, header_hash, boundary):
-                    raise RuntimeError("GPU share failed host re-verification")
+                if not sh.verify_full(block_number, header_hash, boundary):
+                    raise RuntimeError("GPU share failed the full host re-hash")
                 return sh.nonce, sh.mix_hash, sh.final_hash
             pos += n
         return None
@@ -221,17 +223,19 @@ class MinerController:
     template (and no nonce range under it) searched before the restart is searched again."""
 
     def __init__(self, state: ChainState, backends: list, *, max_failures: int = 3, watchdog_s: float = 120.0,
-                 state_path: str | None = None):
+                 state_path: str | None = None, service=None):
         from ..utils.metrics import REGISTRY
 
         self.state = state
         self.backends = backends
+        self.service = service  # miner/service.MiningService with a ChainLeader (GPU nodes)
+        self._service_req = None
         self.metrics = REGISTRY
         self.health = [WorkerHealth(i, b) for i, b in enumerate(backends)]
         self.max_failures, self.watchdog_s = int(max_failures), float(watchdog_s)
         self.state_path = state_path
         self.hashes_done = 0
-        self.hashrate = 0.0
+        self._hashrate = 0.0
         self._rate_t0 = time.time()
         self._threads: list[threading.Thread] = []
         self._stop = threading.Event()
@@ -240,12 +244,50 @@ class MinerController:
         self.generating = False
 
     # --------------------------------------------------------------- helpers
+    @property
+    def hashrate(self) -> float:
+        """getmininginfo.hashespersec: the service's all-reduced rate over every rank, else the
+        host threads' rate (src/miner.cpp:685-687)."""
+        if self.service is not None and (self._service_req is not None or self._hashrate == 0.0):
+            return self.service.hashrate()
+        return self._hashrate
+
+    def workers(self) -> list[dict]:
+        if self.service is None:
+            return [h.as_dict() for h in self.health]
+        svc = self.service
+        return [{"worker": r, "backend": f"{getattr(svc.dev, 'name', 'dev')}-rank{r}", "alive": True,
+                 "hashes": int(svc.rank_hashes.get(r, 0)),
+                 "blocks": svc.leader.stats["blocks"] if r == 0 and svc.leader is not None else 0}
+                for r in range(svc.world_size)]
+
+    def _kawpow_template_time(self) -> bool:
+        tip = self.state.tip()
+        return max(tip.median_time_past() + 1, int(time.time())) >= self.state.params.kawpow_activation_time
+
+    def _service_generate(self, script_pubkey: bytes, nblocks: int, max_tries: int) -> list[str] | None:
+        """generate through the mining service; None if the template is pre-KawPow (host search)."""
+        svc = self.service
+        if svc.error is not None:
+            raise RuntimeError(f"miner service stopped: {svc.error}")
+        req = svc.leader.mine(script_pubkey, blocks=nblocks, max_tries=max_tries)
+        while not req.done.wait(0.5):
+            if svc.error is not None:
+                raise RuntimeError(f"miner service stopped: {svc.error}")
+        if req.error is not None and "KawPow activation" in req.error:
+            return None
+        if req.error is not None and not req.found:
+            raise RuntimeError(req.error)
+        for h in req.found:
+            self.metrics.inc("miner_blocks_total", 1, worker="service")
+        return list(req.found)
+
     def _account(self, n: int, worker: int | None = None) -> None:
         with self._lock:
             self.hashes_done += n
             dt = time.time() - self._rate_t0
             if dt > 4.0:
-                self.hashrate = self.hashes_done / dt
+                self._hashrate = self.hashes_done / dt
                 self.hashes_done = 0
                 self._rate_t0 = time.time()
         label = self.health[worker].label if worker is not None else "generate"
@@ -371,6 +413,10 @@ class MinerController:
     def generate(self, script_pubkey: bytes, nblocks: int, max_tries: int = 1_000_000) -> list[str]:
         """generateBlocks: returns the new block hashes (display hex). Uses the first alive
         backend; a backend that raises is evicted and the next one takes over."""
+        if self.service is not None and self._kawpow_template_time():
+            found = self._service_generate(script_pubkey, nblocks, max_tries)
+            if found is not None:
+                return found
         out: list[str] = []
         extranonce = ExtraNonce()
         while len(out) < nblocks and max_tries > 0:
@@ -414,6 +460,10 @@ class MinerController:
             return
         if script_pubkey is None:
             raise ValueError("setgenerate true needs -miningaddress")
+        if self.service is not None and self._kawpow_template_time():
+            self._service_req = self.service.leader.mine(script_pubkey)  # until setgenerate false
+            self.generating = True
+            return
         self._stop.clear()
         self.generating = True
         for h in self.alive_workers():
@@ -463,7 +513,16 @@ class MinerController:
                 self._failure(worker, e)
                 time.sleep(0.05)
 
+    def close(self) -> None:
+        """Node shutdown: stop mining and end the service loop (its stop packet ends every rank)."""
+        self.stop()
+        if self.service is not None:
+            self.service.stop()
+
     def stop(self) -> None:
+        if self._service_req is not None:
+            self.service.leader.stop_mining()
+            self._service_req = None
         self._stop.set()
         for t in self._threads:
             t.join(timeout=30)

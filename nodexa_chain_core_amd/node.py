@@ -26,7 +26,7 @@ import time
 from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
-from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, GpuKawpowBackend, MinerController
+from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, MinerController
 from .rpc import (methods, methods_assets, methods_ext, methods_index, methods_messages, methods_util, methods_wallet,
                   methods_wallet_ext)
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
@@ -261,18 +261,16 @@ class Node:
             n = self.state.load_mempool(os.path.join(self.datadir, "mempool.dat"))
             if n:
                 log.log_printf(f"Imported mempool transactions from disk: {n} succeeded")
-        backends = []
-        for d in self.gpus:
-            backends.append(GpuKawpowBackend(d, a.get_int("gpuintensity", 1 << 22)))
-        if not backends:
-            backends.append(CpuKawpowBackend(a.get_int("genproclimit", 1)))
+        # host threads: the CPU KawPow search (CPU-only nodes) and X16R/X16RV2 before the activation
+        backends = [CpuKawpowBackend(a.get_int("genproclimit", 1))]
         fail, drop = float(a.get("gpufailrate", "0") or 0), float(a.get("dropshare", "0") or 0)
         if fail or drop:  # fault injection for failure-handling tests (never on by default)
             backends = [FaultInjector(b, fail, drop, seed=i) for i, b in enumerate(backends)]
         self.miner = MinerController(
             self.state, backends, max_failures=a.get_int("minermaxfailures", 3),
             watchdog_s=float(a.get("minerwatchdog", "120")),
-            state_path=os.path.join(self.datadir, "miner_state.json") if self.datadir else None)
+            state_path=os.path.join(self.datadir, "miner_state.json") if self.datadir else None,
+            service=self._start_miner_service(a))
         self.metrics_writer = None
         if a.get("metricslog"):
             path = a.get("metricslog")
@@ -324,6 +322,49 @@ class Node:
                        f"kawpow_activation={self.params.kawpow_activation_time} gpus={self.gpus or 'none'}")
         if a.get_bool("gen", False) and self.network != "regtest":
             self.miner.set_generate(True, self.mining_script)
+
+    def _start_miner_service(self, a: ArgsManager):
+        """The KawPow mining service (miner/service.py): one rank per GPU of `-gpus`, this node being
+        rank 0. Ranks 1..n-1 are spawned as child processes here, before this process touches a
+        GPU; under torchrun (WORLD_SIZE > 1 in the environment) the launcher made them and this is
+        its rank 0. `-minerservice` runs the same loop on CPU devices (`-minerranks=N` processes),
+        for nodes and tests without a GPU."""
+        if not self.gpus and not a.get_bool("minerservice", False):
+            return None
+        from .miner import service as MS
+        from .miner.search import CpuSearchDevice, GpuSearchDevice
+        from .parallel import world as W
+
+        cpu = not self.gpus
+        timeout = float(a.get("minercollectivetimeout", "60"))
+        self.miner_procs = []
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)))
+        else:
+            gpus = self.gpus or [0] * max(1, a.get_int("minerranks", 1))
+            if len(gpus) > 1:
+                import socket
+
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    port = sk.getsockname()[1]
+                os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+                env = {"NODEXA_MINER_COLLECTIVE_TIMEOUT": str(timeout),
+                       "NODEXA_MINER_WATCHDOG": a.get("minerwatchdog", "120")}
+                if a.get("gpuintensity"):
+                    env["NODEXA_MINER_WINDOW"] = a.get("gpuintensity")
+                self.miner_procs = MS.spawn_followers(gpus, port, cpu=cpu, extra_env=env)
+            W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)), device_index=None if cpu else gpus[0],
+                   rank=0, world_size=len(gpus))
+        w = W.get()
+        window = a.get_int("gpuintensity", 4096 if cpu else 1 << 25)
+        dev = CpuSearchDevice(max_window=window) if cpu else GpuSearchDevice(w.device.index,
+                                                                            collective_dag=w.distributed)
+        leader = MS.ChainLeader(self.state, target_bits=a.get_int("minertargetbits", 0))
+        log.log_printf(f"miner service: {w.world_size} rank(s), backend {w.backend}, "
+                       f"{'cpu' if cpu else 'gpu'} devices, {window} nonces per window")
+        return MS.MiningService(dev, leader, window=window, watchdog_s=float(a.get("minerwatchdog", "120")),
+                                collective_timeout_s=timeout).start()
 
     def params_assume_valid(self) -> str | None:
         """consensus.defaultAssumeValid: none is set for these networks here (the reference's main
@@ -512,7 +553,16 @@ class Node:
             return
         self._stopped = True
         if self.miner is not None:
-            self.miner.stop()
+            self.miner.close()
+            if self.miner.service is not None:
+                for p in getattr(self, "miner_procs", []):
+                    try:
+                        p.wait(timeout=30)
+                    except Exception:  # noqa: BLE001 — a follower that does not stop is killed
+                        p.kill()
+                from .parallel import world as W
+
+                W.shutdown()
         if self.state is not None and self.datadir is not None and self.args.get_bool("persistmempool", True):
             try:
                 self.state.save_mempool(os.path.join(self.datadir, "mempool.dat"))  # DumpMempool on shutdown
@@ -582,10 +632,12 @@ class Node:
 
     def gpu_info(self) -> list[dict]:
         out = []
-        for be in (self.miner.backends if self.miner else []):
+        svc = self.miner.service if self.miner else None
+        for be in ([svc.dev] if svc is not None else []):
             if getattr(be, "name", "") != "gpu":
                 continue
-            info = {"device": be.device, "epochs_resident": sorted(be.epochs.keys()), "intensity": be.intensity}
+            info = {"device": be.device, "epochs_resident": sorted(be.epochs.keys()), "intensity": svc.window,
+                    "ranks": svc.world_size, "last_step_ms": round(svc.last_step_ms, 3)}
             try:
                 from .ops import runtime
 
@@ -754,6 +806,11 @@ class Node:
 
 
 def main(argv: list[str] | None = None) -> int:
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and int(os.environ.get("RANK", "0")) != 0:
+        # torchrun launched the node on every GPU: ranks >= 1 are mining followers of rank 0
+        from .miner.service import follower_main
+
+        return follower_main()
     args = ArgsManager()
     rest = args.parse_parameters(sys.argv[1:] if argv is None else argv)
     if rest:

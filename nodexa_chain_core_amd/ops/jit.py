@@ -86,8 +86,11 @@ def _atomic_copy(src: str, dst: str) -> None:
 # two 768-thread workgroups share a CU (6 waves/SIMD instead of 4): +0.7 / +0.8 % in two
 # interleaved sweeps; 640 / 896 threads (waves uneven across the 4 SIMDs) and 1024 (64 VGPRs,
 # heavy spills) lose.
+# r3b / r3c: scheduling fences around each round's cache/math program (KP_SCHED_FENCE) keep the
+# DAG merge, and with it the wait for the round's HBM gather, at the end of the round: +3.2 / +3.6 %
+# in two interleaved 7-round sweeps (profiles/r3b_r3c_sched_fence).
 TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_SBUFFER", "KP_L1X4", "KP_BLOCK=768",
-                                  "KP_DIGEST_REG", "KP_MIN_WAVES=6", "KP_NT_DAG")
+                                  "KP_DIGEST_REG", "KP_MIN_WAVES=6", "KP_NT_DAG", "KP_SCHED_FENCE")
 _env = os.environ.get("NODEXA_KAWPOW_DEFINES")
 DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
     d for d in _env.split(",") if d and d != "none")

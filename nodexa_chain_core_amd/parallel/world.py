@@ -41,14 +41,16 @@ class World:
 _WORLD: World | None = None
 
 
-def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | None = None) -> World:
+def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | None = None,
+         rank: int | None = None, world_size: int | None = None) -> World:
     """Initialise from RANK/WORLD_SIZE/LOCAL_RANK (torchrun, or the node's spawned miner ranks)
-    or single-process. `device_index`: the GPU of this rank (default: LOCAL_RANK)."""
+    or single-process; `rank` / `world_size` override the environment. `device_index`: the GPU
+    of this rank (default: LOCAL_RANK)."""
     global _WORLD
     if _WORLD is not None:
         return _WORLD
-    rank = int(os.environ.get("RANK", "0"))
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
+    world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else int(world_size)
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()

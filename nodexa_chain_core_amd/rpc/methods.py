@@ -286,7 +286,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
                 "difficulty": _core.difficulty_from_bits(tip.bits), "networkhashps": st.network_hashps(120, -1),
                 "hashespersec": int(node.miner.hashrate), "pooledtx": len(st.mempool), "chain": params.network_id,
                 "warnings": "", "gpus": node.gpu_info(),
-                "workers": [h.as_dict() for h in node.miner.health]}
+                "workers": node.miner.workers()}
 
     def rpc_getnetworkhashps(p):
         """getnetworkhashps ( nblocks height )"""

@@ -112,3 +112,102 @@ def test_next_epoch_dag_prebuild(core, gpu):
     nonce, mix, fin = res
     ctx = core.get_epoch_context(1)
     assert core.kawpow_hash(ctx, core.EPOCH_LENGTH, hh, nonce) == (fin, mix)
+
+
+def _headline_epoch(core, epoch):
+    import torch
+
+    from nodexa_chain_core_amd.ops.ethash import DeviceEpoch
+
+    e = DeviceEpoch(epoch, device=0, ctx=core.get_epoch_context(epoch))
+    e.build()
+    torch.cuda.synchronize()
+    assert e.l1_matches()
+    return e
+
+
+@pytest.mark.parametrize("epoch", [384, 390])
+def test_shipped_variant_full_hash_at_headline_epochs(core, gpu, epoch):
+    """The kernel variant that ships at each DAG size — epoch 384 (4.00 GiB: structured-buffer
+    loads, 768 threads, register digests, scheduling fences) and epoch 390 (4.05 GiB: 64-bit
+    pointer path) — hashes bit-exactly like the host golden model (_core.kawpow_hash, light mode),
+    both through hash_batch and through search (every share of a window re-hashed in full)."""
+    import torch
+
+    from nodexa_chain_core_amd.ops import jit
+    from nodexa_chain_core_amd.ops.kawpow import KawpowSearcher
+
+    e = _headline_epoch(core, epoch)
+    height = epoch * core.EPOCH_LENGTH + 123
+    s = KawpowSearcher(e, height)
+    variant = jit.defines_for(e.dag_bytes)
+    assert ("KP_SBUFFER" in variant) == (epoch == 384)
+    rng = random.Random(epoch)
+    headers = [rng.randbytes(32) for _ in range(64)]
+    nonces = [rng.getrandbits(64) for _ in range(64)]
+    out = s.hash_batch(headers, nonces)
+    for i in range(0, 64, 9):
+        assert out[i] == core.kawpow_hash(e.ctx, height, headers[i], nonces[i]), (epoch, i)
+    hh = core.sha256d(b"headline-%d" % epoch)
+    shares = s.search(hh, 1 << 40, s.block * 64, bytes.fromhex("07" + "ff" * 31))  # ~1/32 pass
+    assert len(shares) >= 8
+    for sh in shares[:12]:
+        assert sh.verify_full(height, hh, ctx=e.ctx), (epoch, sh.nonce)
+    del s, e
+    torch.cuda.empty_cache()
+
+
+def test_corrupted_dag_item_is_caught(core, gpu):
+    """A damaged DAG row makes the full host re-hash reject the GPU's result (the mix-only check
+    would accept it: the final hash is consistent with the GPU's own wrong mix)."""
+    import torch
+
+    from nodexa_chain_core_amd.ops.ethash import DeviceEpoch
+    from nodexa_chain_core_amd.ops.kawpow import KawpowSearcher, Share
+
+    e = DeviceEpoch(0, device=0, ctx=core.get_epoch_context(0))
+    e.build()
+    torch.cuda.synchronize()
+    height, hh, nonce = 5, core.sha256d(b"corrupt"), 77
+    s = KawpowSearcher(e, height)
+    (f, m), = s.hash_batch([hh], [nonce])
+    assert Share(nonce, m, f).verify_full(height, hh, ctx=e.ctx)
+    rows = e.dag.view(torch.int32)
+    rows = rows[:rows.numel() // 64 * 64].view(-1, 64)
+    rows[64:, :] ^= 0x01000000  # every item this nonce can gather outside the L1
+    torch.cuda.synchronize()
+    (f2, m2), = s.hash_batch([hh], [nonce])
+    bad = Share(nonce, m2, f2)
+    assert (f2, m2) != (f, m)
+    assert bad.verify_host(height, hh)          # mix-only: consistent with its own mix
+    assert not bad.verify_full(height, hh, ctx=e.ctx)  # full re-hash: caught
+
+
+def test_pipelined_search_loop_on_gpu(core, gpu):
+    """miner/search: two windows in flight, ring copies behind each kernel, the generation word
+    aborting a queued window, exact hash accounting, shares re-hashed in full."""
+    import time
+
+    from nodexa_chain_core_amd.miner.search import GpuSearchDevice, SearchPipeline, Work
+
+    dev = GpuSearchDevice(0)
+    height = 4242
+    hh = core.sha256d(b"pipeline")
+    w = Work(hh, bytes.fromhex("003f" + "ff" * 30), height, 1, 0, 0)  # ~1 in 1024 passes
+    pipe = SearchPipeline(dev, watchdog_s=60)
+    block = dev.block_for(height)
+    n = block * 512
+    assert pipe.step(w, 0, n) is None
+    r0 = pipe.step(w, n, n)
+    assert r0.hashes == n and r0.start == 0 and len(r0.shares) > 100
+    ctx = core.get_epoch_context(0)
+    for sh in r0.shares[:6]:
+        assert sh.verify_full(height, hh, w.boundary, ctx=ctx)
+    # a big window queued behind the running one, then the template changes: it stops early
+    big = block * 40000
+    pipe.step(w, 2 * n, big)
+    dev.abort()
+    t0 = time.time()
+    r_big = pipe.drain()
+    assert r_big.hashes < big // 4 and time.time() - t0 < 5
+    dev.close()

@@ -214,3 +214,37 @@ def test_gloo_world_survives_hung_rank(tmp_path, core):
     r1 = json.load(open(tmp_path / "rank1.json"))
     assert r1["world_size"] == 2 and r1["rank"] == 1
     _check_disjoint(tmp_path, n, rep)
+
+
+def test_node_mines_through_service_with_follower_rank(core, tmp_path):
+    """nodexad -minerservice -minerranks=2: the node is rank 0 of a gloo world and spawns rank 1
+    itself; generate / setgenerate / getmininginfo go through the service."""
+    from nodexa_chain_core_amd.node import Node
+    from nodexa_chain_core_amd.rpc.client import RPCClient
+    from nodexa_chain_core_amd.utils.config import ArgsManager
+
+    addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
+    args = ArgsManager()
+    args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+                           f"-miningaddress={addr}", "-printtoconsole=0", "-minerservice", "-minerranks=2",
+                           "-gpuintensity=8", "-minertargetbits=5", "-minercollectivetimeout=20"])
+    n = Node(args)
+    n.start()
+    try:
+        c = RPCClient("127.0.0.1", n.rpc.port, "u", "p")
+        hashes = c.generatetoaddress(3, addr)
+        assert len(hashes) == 3 and c.getblockcount() == 3
+        assert n.miner.service.world_size == 2 and len(n.miner_procs) == 1
+        c.setgenerate(True)
+        assert c.getgenerate() is True
+        deadline = time.time() + 120
+        while c.getblockcount() < 5 and time.time() < deadline:
+            time.sleep(0.2)
+        info = c.getmininginfo()
+        assert c.getblockcount() >= 5 and info["hashespersec"] > 0
+        assert [w["worker"] for w in info["workers"]] == [0, 1] and all(w["hashes"] > 0 for w in info["workers"])
+        c.setgenerate(False)
+        assert c.getgenerate() is False
+    finally:
+        n.stop()
+    assert [p.returncode for p in n.miner_procs] == [0]
