@@ -28,8 +28,11 @@
 //   hashes [2][ni][BUCKETS][EQP_SLOTS][8] u32  (levels alternate between the two buffers)
 //   counts [ni][LEVELS][P][BUCKETS] u8
 //   refs   [ni][LEVELS][BUCKETS][EQP_REF_STRIDE] u32
-// Overflowing segments or staging areas drop rows (counted in p.stats per level); with
-// C = 16 at a mean of 4 rows per segment that is a few rows per 2M.
+// Overflowing segments or staging areas drop rows (counted in p.stats per level), and a chain of
+// equal sub-digits longer than EQ_MAX_CHAIN is cut (counted in p.stats[EQP_STAT_CHAIN]); at
+// C = 32 for a mean of 8 rows per segment, 768 staged for a mean of 512 per bucket and 24 for a
+// mean chain of 2, none of them has been seen in any run. The host (ops/equihash.py) re-solves an
+// instance with any such count on the golden solver, so the solution set is exact either way.
 #include "equihash_device.hpp"
 
 #define EQP_BLOCK 512
@@ -209,7 +212,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     eqp_clear_counts(cnt2);
     for (uint32_t i = threadIdx.x; i < 256; i += EQP_BLOCK) head[i] = -1;
     uint32_t cv[4] = {0, 0, 0, 0};
-    uint32_t dropped = 0;
+    uint32_t dropped = 0, truncated = 0;
     // every producer wave scans the counts itself and gathers rows pos = thread, thread + NP, ...
     auto stage = [&](uint32_t bk, uint32_t buf) {
         const uint32_t total = eqp_wave_scan(P, cv, my_segc);
@@ -245,7 +248,8 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
                 const uint32_t* a = rc + i * ST - K0;
                 if constexpr (R == 9) {  // final round: equal d_8 (chain) and d_9 make a candidate
                     const uint32_t di = eq_digit<9>(a);
-                    for (int j = nxt[i], steps = 0; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
+                    int j = nxt[i], steps = 0;
+                    for (; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
                         if (di != eq_digit<9>(rc + (uint32_t)j * ST - K0)) continue;
                         uint32_t* c = p.cands + (size_t)inst * (1 + 2 * EQ_MAX_CAND);
                         const uint32_t k = atomicAdd(&c[0], 1u);
@@ -254,9 +258,11 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
                             c[2 + 2 * k] = b * EQP_REF_STRIDE + (uint32_t)j;
                         }
                     }
+                    truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
                     continue;
                 }
-                for (int j = nxt[i], steps = 0; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
+                int j = nxt[i], steps = 0;
+                for (; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
                     uint32_t x[8];
                     eq_xor_rows<R>(a, rc + (uint32_t)j * ST - K0, x);
                     if (eq_zero_from<R>(x)) continue;  // identical remainder: only duplicate indices
@@ -273,12 +279,14 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
                         }
                     }
                 }
+                truncated += j >= 0;
             }
         }
     }
     __syncthreads();
     if constexpr (R < 9) eqp_flush_counts(p, inst, R, cnt2, dropped);
     else if (dropped) atomicAdd(&p.stats[inst * EQP_STATS + 8], dropped);
+    if (truncated) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_CHAIN], truncated);
 }
 
 // 2 workgroups of 512 per CU (4 waves per SIMD): at most 128 VGPRs.

@@ -98,6 +98,7 @@ struct EquihashDev {
 #define EQP_STAGE 768      // rows of one bucket staged in LDS (mean 512, sd ~23)
 #define EQP_REF_STRIDE 1024  // refs per bucket: a 10-bit staged index
 #define EQP_STATS 16
+#define EQP_STAT_CHAIN 9   // stats slot: chains cut at EQ_MAX_CHAIN (slots 0-8: rows dropped per level)
 #define EQP_FINAL_GROUPS 1024  // final-round workgroups per instance (it writes no level)
 struct EquihashPsDev {
     const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashDev)

@@ -124,6 +124,10 @@ class EquihashSolver:
             # back on the stream right after its kernels, so launch i+1 can be
             # queued before the host verifies launch i (GPU and CPU overlap)
             self._landing = [torch.empty(self.sols.numel(), dtype=torch.int32).pin_memory() for _ in range(2)]
+            # per launch: [inst][EQP_STATS] truncation counters (ps) + [inst] candidate counts
+            nstat = ni * self.h.EQP_STATS if ps else 0
+            self._land_stats = [torch.zeros(nstat + ni, dtype=torch.int32).pin_memory() for _ in range(2)]
+            self.fallbacks = 0  # instances re-solved on the host because the device truncated something
             self._stage = [torch.empty(ni * 16, dtype=torch.int64).pin_memory() for _ in range(2)]
         self._pending: list[tuple[list[bytes], torch.Tensor, torch.cuda.Event]] = []
         self._next = 0
@@ -163,11 +167,16 @@ class EquihashSolver:
             else:
                 self._issue_global(s)
             land = self._landing[self._next]
+            lstat = self._land_stats[self._next]
             self._next = (self._next + 1) % len(self._landing)
             land.copy_(self.sols, non_blocking=True)
+            nstat = lstat.numel() - self.num_inst
+            if nstat:
+                lstat[:nstat].copy_(self.stats_buf, non_blocking=True)
+            lstat[nstat:].copy_(self.cands.view(self.num_inst, -1)[:, 0], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
-        self._pending.append((list(inputs), land, ev))
+        self._pending.append((list(inputs), (land, lstat), ev))
 
     def _issue_global(self, s: int) -> None:
         args = (self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst, self.hashes.data_ptr(),
@@ -186,15 +195,28 @@ class EquihashSolver:
         """Solutions of the oldest queued launch (waits only for that launch)."""
         if not self._pending:
             raise RuntimeError("nothing launched")
-        launched, land, ev = self._pending.pop(0)
+        launched, (land, lstat), ev = self._pending.pop(0)
         if inputs is not None and list(inputs) != launched:
             raise ValueError("collect() inputs differ from the oldest launch")
         inputs = launched
         ev.synchronize()
         raw = land.numpy()
         per = 1 + self.h.EQ_MAX_SOL * 512
+        st = lstat.numpy()
+        nstat = st.size - self.num_inst
         out = []
         for i in range(self.num_inst):
+            truncated = int(st[nstat + i]) > self.h.EQ_MAX_CAND
+            if nstat:
+                truncated |= bool(st[i * self.h.EQP_STATS:i * self.h.EQP_STATS + self.h.EQP_STAT_CHAIN + 1].any())
+            if truncated:
+                # a bucket, chain or candidate cap cut something: the device result may miss a
+                # solution, so this instance is solved again on the golden solver (never seen in
+                # practice; it keeps the solution set exact by construction)
+                self.fallbacks += 1
+                sols, _ = _core.equihash_solve_cpu(self.params, inputs[i], self.h.EQ_MAX_SOL, 0)
+                out.append([list(x) for x in sols])
+                continue
             base = i * per
             n = min(int(raw[base]), self.h.EQ_MAX_SOL)
             sols = []

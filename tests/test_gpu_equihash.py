@@ -45,6 +45,28 @@ def test_gpu_solutions_valid_and_match_cpu(core, solver):
     assert total_gpu >= total_cpu - 1  # bucket-capacity drops may lose at most a rare solution
 
 
+def test_ps_solver_exactly_matches_cpu_on_16_inputs(core, gpu):
+    """The default engine is lossless: every device-side cap (segment, staging, chain, candidate)
+    is counted per instance and a counted instance is re-solved on the golden solver, so the
+    solution sets equal the CPU solver's on every input."""
+    import torch
+
+    from nodexa_chain_core_amd.ops.equihash import EquihashSolver
+
+    s = EquihashSolver(num_inst=8, device=0, engine="ps")
+    p = core.EquihashParams(200, 9)
+    inputs = [bytes([0x5A]) * 80 + i.to_bytes(32, "little") for i in range(16)]
+    gpu = s.solve(inputs[:8]) + s.solve(inputs[8:])
+    total = 0
+    for inp, g in zip(inputs, gpu):
+        cpu, _ = core.equihash_solve_cpu(p, inp, 16, 0)
+        assert sorted(map(tuple, g)) == sorted(map(tuple, cpu)), inp[-32:].hex()
+        total += len(g)
+    assert total > 8
+    del s
+    torch.cuda.empty_cache()
+
+
 def test_gpu_batch_verify_matches_cpu(core, solver):
     from nodexa_chain_core_amd.ops.equihash import verify_solutions
 

@@ -193,13 +193,13 @@ def test_pipelined_search_loop_on_gpu(core, gpu):
     dev = GpuSearchDevice(0)
     height = 4242
     hh = core.sha256d(b"pipeline")
-    w = Work(hh, bytes.fromhex("003f" + "ff" * 30), height, 1, 0, 0)  # ~1 in 1024 passes
+    w = Work(hh, bytes.fromhex("0001" + "ff" * 30), height, 1, 0, 0)  # ~1 in 32768 passes
     pipe = SearchPipeline(dev, watchdog_s=60)
     block = dev.block_for(height)
     n = block * 512
     assert pipe.step(w, 0, n) is None
     r0 = pipe.step(w, n, n)
-    assert r0.hashes == n and r0.start == 0 and len(r0.shares) > 100
+    assert r0.hashes == n and r0.start == 0 and 2 <= len(r0.shares) < 64  # ~12 expected, ring not full
     ctx = core.get_epoch_context(0)
     for sh in r0.shares[:6]:
         assert sh.verify_full(height, hh, w.boundary, ctx=ctx)
