@@ -10,7 +10,8 @@ template when the tip or the mempool changes, so the miner re-reads the template
 previous block hash changes or `refresh` seconds have passed.
 
 Nonce partition: worker `rank` of `world` searches nonce_base + rank * 2^56 + k, so several
-processes (one per GPU) never overlap, mirroring the in-process controller's partition.
+processes (one per GPU) never overlap, mirroring the in-process controller's partition. The
+search itself is the node's pipelined mining loop (miner/service.py) with a RemoteLeader.
 """
 from __future__ import annotations
 
@@ -20,67 +21,128 @@ import time
 from ..utils import log
 
 
+class RemoteLeader:
+    """Rank 0 of a remote miner's mining loop (miner/service.MiningService): the work packet comes
+    from the node's getblocktemplate and shares go back through pprpcsb, after a full host
+    re-hash. Several processes (torchrun, one per GPU) share one node connection this way: rank 0
+    talks to the node, every rank searches its own nonce range."""
+
+    def __init__(self, rpc, refresh: float = 15.0, nonce_base: int = 0, rules=("segwit",)):
+        self.rpc = rpc
+        self.refresh = float(refresh)
+        self.nonce_base = int(nonce_base)
+        self.rules = list(rules)
+        self.stats = {"templates": 0, "windows": 0, "hashes": 0, "submitted": 0, "accepted": 0, "rejected": 0,
+                      "bad_shares": 0}
+        self.tpl = None
+        self.tpl_time = 0.0
+        self.job_id = 0
+        self.force = False
+        self.stopping = False
+        self.last_result = None
+
+    def template(self) -> dict:
+        """The current work, re-read after `refresh` seconds or when the tip moved."""
+        now = time.time()
+        if self.tpl is not None and not self.force and now - self.tpl_time < self.refresh:
+            if self.rpc.getbestblockhash() == self.tpl["previousblockhash"]:
+                return self.tpl
+        tpl = self.rpc.getblocktemplate({"rules": self.rules})
+        if "pprpcheader" not in tpl:
+            raise RuntimeError("the node's template has no pprpcheader (KawPow not active, or no -miningaddress)")
+        if self.tpl is None or tpl["pprpcheader"] != self.tpl["pprpcheader"]:
+            self.job_id += 1
+        self.tpl, self.tpl_time, self.force = tpl, now, False
+        self.stats["templates"] += 1
+        return tpl
+
+    def next_work(self, repartitioned: bool = False):
+        from .search import FLAG_CLEAN, FLAG_STOP, Work
+
+        if self.stopping:
+            return Work(flags=FLAG_STOP)
+        before = self.job_id
+        if repartitioned:
+            self.force = True
+        tpl = self.template()
+        flags = FLAG_CLEAN if self.job_id != before or repartitioned else 0
+        return Work(bytes.fromhex(tpl["pprpcheader"]), bytes.fromhex(tpl["target"]), int(tpl["height"]),
+                    self.job_id, self.nonce_base, flags)
+
+    def on_results(self, records) -> None:
+        tpl = self.tpl
+        for job_id, hashes, shares in records:
+            self.stats["hashes"] += hashes
+            self.stats["windows"] += hashes > 0
+            if tpl is None or job_id != self.job_id or not shares:
+                continue
+            sh = shares[0]  # one block per template: the tip moves after it
+            height, hh = int(tpl["height"]), bytes.fromhex(tpl["pprpcheader"])
+            if not sh.verify_full(height, hh, bytes.fromhex(tpl["target"])):
+                self.stats["bad_shares"] += 1
+                log.log_printf(f"remote miner: share nonce {sh.nonce:016x} failed the full re-hash; dropped")
+                continue
+            self.stats["submitted"] += 1
+            try:
+                out = self.rpc.pprpcsb(tpl["pprpcheader"], bytes(sh.mix_hash).hex(), "%016x" % sh.nonce)
+            except RuntimeError as e:  # stale header, or a node that rejected the block
+                out = str(e)
+            ok = out is True or out is None or out == "duplicate"
+            self.stats["accepted" if ok else "rejected"] += 1
+            self.last_result = out
+            log.log_printf(f"remote miner: height {height} nonce {sh.nonce:016x} -> {out}")
+            self.force = True  # the tip moves on an accepted block: fetch new work
+            tpl = None
+
+    def shutdown(self) -> None:
+        self.stopping = True
+
+
+def _device_for(backend):
+    """A miner/search device for `backend`: a search device as is, or the device that replaces a
+    synchronous backend object (CpuKawpowBackend -> CpuSearchDevice, GpuKawpowBackend ->
+    GpuSearchDevice on its GPU)."""
+    from .search import CpuSearchDevice, GpuSearchDevice
+
+    if hasattr(backend, "submit") and hasattr(backend, "wait"):
+        return backend
+    if getattr(backend, "name", "") == "gpu":
+        return GpuSearchDevice(backend.device)
+    return CpuSearchDevice()
+
+
 class RemoteMiner:
+    """The remote-mode miner: the node's own mining loop (pipelined windows, device-side stale-work
+    abort, full share re-hash) with a RemoteLeader in place of the chain.
+
+    Nonce partition: worker `rank` of an external set of miners searches nonce_base + rank * 2^56
+    + k (inside one torchrun world the service adds its own rank the same way)."""
+
     def __init__(self, rpc, backend, window: int = 1 << 22, refresh: float = 15.0, rank: int = 0,
                  nonce_base: int = 0, rules=("segwit",)):
+        from .service import MiningService
+
         self.rpc = rpc
-        self.backend = backend
-        self.window = int(window)
-        self.refresh = float(refresh)
         self.rank = int(rank)
-        self.nonce_base = int(nonce_base) + (self.rank << 56)
-        self.rules = list(rules)
-        self.stats = {"templates": 0, "windows": 0, "hashes": 0, "submitted": 0, "accepted": 0, "rejected": 0}
+        self.leader = RemoteLeader(rpc, refresh, int(nonce_base) + (self.rank << 56), rules)
+        self.dev = _device_for(backend)
+        if getattr(self.dev, "name", "") == "cpu":
+            self.dev.max_window = min(self.dev.max_window, int(window))
+        self.service = MiningService(self.dev, self.leader, window=int(window))
+        self.stats = self.leader.stats
         self._stop = threading.Event()
-        self._tpl = None
-        self._tpl_time = 0.0
-        self._cursor = 0
 
     def stop(self) -> None:
         self._stop.set()
 
     def template(self) -> dict:
-        """The current work, re-read after `refresh` seconds or when the tip moved."""
-        now = time.time()
-        if self._tpl is not None and now - self._tpl_time < self.refresh:
-            best = self.rpc.getbestblockhash()
-            if best == self._tpl["previousblockhash"]:
-                return self._tpl
-        tpl = self.rpc.getblocktemplate({"rules": self.rules})
-        if "pprpcheader" not in tpl:
-            raise RuntimeError("the node's template has no pprpcheader (KawPow not active, or no -miningaddress)")
-        if self._tpl is None or tpl["pprpcheader"] != self._tpl["pprpcheader"]:
-            self._cursor = 0
-        self._tpl, self._tpl_time = tpl, now
-        self.stats["templates"] += 1
-        return tpl
+        return self.leader.template()
 
     def step(self) -> str | None:
-        """One search window on the current template; submits a solution if one is found.
-        Returns the pprpcsb result (None when the window had no solution)."""
-        tpl = self.template()
-        header_hash = bytes.fromhex(tpl["pprpcheader"])
-        boundary = bytes.fromhex(tpl["target"])
-        start = self.nonce_base + self._cursor
-        res = self.backend.search(int(tpl["height"]), header_hash, boundary, start, self.window)
-        self.stats["windows"] += 1
-        if res is None:
-            self._cursor += self.window
-            self.stats["hashes"] += self.window
-            return None
-        nonce, mix, _final = res
-        self.stats["hashes"] += nonce - start + 1
-        self._cursor = nonce - self.nonce_base + 1
-        self.stats["submitted"] += 1
-        try:
-            out = self.rpc.pprpcsb(tpl["pprpcheader"], bytes(mix).hex(), "%016x" % nonce)
-        except RuntimeError as e:  # stale header, or a node that rejected the block
-            out = str(e)
-        ok = out is True or out is None or out == "duplicate"
-        self.stats["accepted" if ok else "rejected"] += 1
-        log.log_printf(f"remote miner: height {tpl['height']} nonce {nonce:016x} -> {out}")
-        self._tpl = None  # the tip moves on an accepted block: fetch new work
-        return out
+        """One iteration of the loop; returns the pprpcsb result of a share submitted in it."""
+        self.leader.last_result = None
+        self.service.step()
+        return self.leader.last_result
 
     def run(self, max_blocks: int | None = None, max_seconds: float | None = None) -> dict:
         t0 = time.time()
@@ -94,6 +156,10 @@ class RemoteMiner:
             except (OSError, ConnectionError) as e:
                 log.log_printf(f"remote miner: node unreachable ({e}); retrying")
                 self._stop.wait(1.0)
+        try:
+            self.service.pipe.drain()
+        except Exception:  # noqa: BLE001
+            pass
         self.stats["seconds"] = round(time.time() - t0, 3)
         return dict(self.stats)
 
@@ -112,15 +178,10 @@ def main(argv: list[str] | None = None) -> int:
     params = make_params(a.network)
     rpc = RPCClient(a.get("rpcconnect", "127.0.0.1"), a.get_int("rpcport", params.default_rpc_port),
                     a.get("rpcuser"), a.get("rpcpassword"), None, timeout=60.0)
-    if a.get_bool("cpu", False):
-        from .kawpow_miner import CpuKawpowBackend
+    from .search import CpuSearchDevice, GpuSearchDevice
 
-        backend = CpuKawpowBackend(a.get_int("genproclimit", 1))
-    else:
-        from .kawpow_miner import GpuKawpowBackend
-
-        backend = GpuKawpowBackend(a.get_int("gpu", 0), a.get_int("gpuintensity", 1 << 24))
-    m = RemoteMiner(rpc, backend, window=a.get_int("minerwindow", 1 << 24), rank=a.get_int("minerrank", 0))
+    backend = CpuSearchDevice() if a.get_bool("cpu", False) else GpuSearchDevice(a.get_int("gpu", 0))
+    m = RemoteMiner(rpc, backend, window=a.get_int("minerwindow", 1 << 25), rank=a.get_int("minerrank", 0))
     blocks = a.get_int("blocks", 0)
     stats = m.run(max_blocks=blocks or None)
     print(stats)
