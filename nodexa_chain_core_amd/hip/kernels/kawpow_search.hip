@@ -45,6 +45,7 @@
 //   KP_NT_DAG     non-temporal DAG loads (the 4 GiB DAG has no L2 reuse)
 //   KP_SCHED_FENCE scheduling barriers around each round's cache/math program, so the DAG
 //                 gather issued at the top of the round is consumed only at its end
+//   KP_PRIO       raised wave priority from the DAG merge to the next gather's issue
 #ifndef KP_HASHES
 #define KP_HASHES 2
 #endif
@@ -281,6 +282,10 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMo
     const uint32_t part = lane ^ (uint32_t)J;
 #pragma unroll
     for (int k = 0; k < KP_HASHES; ++k) d[k] = kp_dag_item(dag, kp_fastmod(kp_bcast<J>(mx[k][0]), items), part);
+#ifdef KP_PRIO
+    // the gather is out: back to normal priority for the round's program (see below)
+    __builtin_amdgcn_s_setprio(0);
+#endif
 #ifdef KP_SCHED_FENCE
     // Keep the round's DAG merge after the whole cache/math program: left alone, the register-
     // pressure scheduler pulls the merge (and its vmcnt wait) into the middle of the program, so
@@ -291,6 +296,11 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMo
     for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM(l1, mx[k]);
 #ifdef KP_SCHED_FENCE
     __builtin_amdgcn_sched_barrier(0);
+#endif
+#ifdef KP_PRIO
+    // DAG merge -> next item index -> next gather is each hash's critical path: raise this wave's
+    // issue priority over the co-resident waves' programs until the next gather has been issued
+    __builtin_amdgcn_s_setprio(2);
 #endif
 #pragma unroll
     for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);

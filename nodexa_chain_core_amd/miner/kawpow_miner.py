@@ -14,8 +14,7 @@ Two ways to mine:
     only forwards generate / setgenerate / getmininginfo to the service's leader.
   * host backends in threads — CpuKawpowBackend (the reference-equivalent light-mode search,
     progpow::search_light) for CPU-only nodes, and the host X16R / X16RV2 search for templates
-    before the KawPow activation. GpuKawpowBackend remains as a synchronous single-window search
-    object (remote miner, tests), not as a mining thread.
+    before the KawPow activation.
 """
 from __future__ import annotations
 
@@ -41,117 +40,6 @@ class CpuKawpowBackend:
         ctx = _core.get_epoch_context(block_number // _core.EPOCH_LENGTH)
         ok, nonce, fin, mix = _core.kawpow_search_light(ctx, block_number, header_hash, boundary, start, count)
         return (nonce, mix, fin) if ok else None
-
-
-class GpuKawpowBackend:
-    name = "gpu"
-
-    # Start building epoch e+1's DAG this many blocks before the boundary (SURVEY P9:
-    # double-buffered next-epoch prebuild). Two 4 GiB DAGs are ~3 % of 288 GB HBM3E.
-    PREBUILD_WINDOW = 120
-
-    def __init__(self, device: int = 0, intensity: int = 1 << 22):
-        from ..ops.ethash import DeviceEpoch  # noqa: F401  (imports torch + _hip)
-
-        self.device = int(device)
-        self.intensity = int(intensity) // 256 * 256
-        self.epochs: dict[int, object] = {}
-        self.searchers: dict[int, object] = {}
-        self.lock = threading.Lock()
-        self._prebuild: threading.Thread | None = None
-        self.prebuilt_epochs: list[int] = []
-
-    def maybe_prebuild(self, block_number: int) -> threading.Thread | None:
-        """Near an epoch boundary, build the next epoch's DAG on a side HIP stream in a
-        background thread, so the switch costs no search time."""
-        nxt = block_number // _core.EPOCH_LENGTH + 1
-        if block_number % _core.EPOCH_LENGTH < _core.EPOCH_LENGTH - self.PREBUILD_WINDOW:
-            return None
-        with self.lock:
-            if nxt in self.epochs or (self._prebuild is not None and self._prebuild.is_alive()):
-                return None
-            t = threading.Thread(target=self._build_side, args=(nxt,), name=f"dag-prebuild-{nxt}", daemon=True)
-            self._prebuild = t
-        t.start()
-        return t
-
-    def _build_side(self, epoch: int) -> None:
-        import torch
-
-        from ..ops.ethash import DeviceEpoch
-        from ..utils.metrics import REGISTRY
-
-        t0 = time.time()
-        with torch.cuda.device(self.device):
-            side = torch.cuda.Stream(device=self.device)
-            with torch.cuda.stream(side):  # current stream is per thread: the DAG kernels go to `side`
-                e = DeviceEpoch(epoch, device=self.device)
-                e.build()
-            side.synchronize()
-            if not e.l1_matches():
-                log.log_printf(f"gpu{self.device}: prebuilt epoch {epoch} DAG failed its L1 self-check")
-                return
-        REGISTRY.set("dag_build_seconds", time.time() - t0, device=f"gpu{self.device}", epoch=epoch)
-        with self.lock:
-            self.epochs.setdefault(epoch, e)
-            self.prebuilt_epochs.append(epoch)
-        log.log_print("gpu", f"device {self.device}: epoch {epoch} DAG prebuilt in {time.time() - t0:.2f}s")
-
-    def _epoch(self, epoch: int):
-        import torch
-
-        from ..ops.ethash import DeviceEpoch
-
-        if epoch not in self.epochs:
-            from ..utils.metrics import REGISTRY
-
-            t0 = time.time()
-            with torch.cuda.device(self.device):
-                e = DeviceEpoch(epoch, device=self.device)
-                e.build()
-                torch.cuda.synchronize()
-                if not e.l1_matches():
-                    raise RuntimeError("GPU DAG failed its L1 self-check")
-            REGISTRY.set("dag_build_seconds", time.time() - t0, device=f"gpu{self.device}", epoch=epoch)
-            REGISTRY.set("dag_bytes", e.dag_bytes, device=f"gpu{self.device}", epoch=epoch)
-            # keep at most the current and the next epoch resident
-            for old in [k for k in self.epochs if k < epoch - 1]:
-                self.epochs.pop(old)
-                self.searchers.pop(old, None)
-            self.epochs[epoch] = e
-            log.log_print("gpu", f"device {self.device}: epoch {epoch} DAG {e.dag_bytes / 2**30:.2f} GiB ready")
-        return self.epochs[epoch]
-
-    def searcher(self, block_number: int):
-        from ..ops.kawpow import KawpowSearcher
-
-        epoch = block_number // _core.EPOCH_LENGTH
-        self.maybe_prebuild(block_number)
-        with self.lock:
-            ep = self._epoch(epoch)
-            s = self.searchers.get(epoch)
-            if s is None:
-                s = KawpowSearcher(ep, block_number, prefetch_next=True)
-                self.searchers[epoch] = s
-            else:
-                s.set_block(block_number)
-            return s
-
-    def search(self, block_number: int, header_hash: bytes, boundary: bytes, start: int, count: int):
-        s = self.searcher(block_number)
-        pos, end = start, start + count
-        while pos < end:
-            b = s.block
-            n = max(b, min(self.intensity, end - pos + b - 1) // b * b)
-            shares = s.search(header_hash, pos, n, boundary)
-            shares = [x for x in shares if x.nonce < end]
-            if shares:
-                sh = shares[0]
-                if not sh.verify_full(block_number, header_hash, boundary):
-                    raise RuntimeError("GPU share failed the full host re-hash")
-                return sh.nonce, sh.mix_hash, sh.final_hash
-            pos += n
-        return None
 
 
 class InjectedFault(RuntimeError):

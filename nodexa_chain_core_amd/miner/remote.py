@@ -99,15 +99,12 @@ class RemoteLeader:
 
 
 def _device_for(backend):
-    """A miner/search device for `backend`: a search device as is, or the device that replaces a
-    synchronous backend object (CpuKawpowBackend -> CpuSearchDevice, GpuKawpowBackend ->
-    GpuSearchDevice on its GPU)."""
-    from .search import CpuSearchDevice, GpuSearchDevice
+    """A miner/search device for `backend`: a search device as is; a host backend object
+    (CpuKawpowBackend) becomes a CpuSearchDevice."""
+    from .search import CpuSearchDevice
 
     if hasattr(backend, "submit") and hasattr(backend, "wait"):
         return backend
-    if getattr(backend, "name", "") == "gpu":
-        return GpuSearchDevice(backend.device)
     return CpuSearchDevice()
 
 

@@ -94,24 +94,29 @@ def test_vectors_other_epochs(core, gpu):
 
 
 def test_next_epoch_dag_prebuild(core, gpu):
-    """Within PREBUILD_WINDOW blocks of an epoch boundary the backend builds the next
-    epoch's DAG on a side stream; the first block of the new epoch then finds it resident
-    and a search there is bit-exact against the golden model."""
-    from nodexa_chain_core_amd.miner.kawpow_miner import GpuKawpowBackend
+    """The mining service prebuilds the next epoch's DAG on a side stream (GpuSearchDevice.prebuild,
+    voted in by every rank near the boundary); the first block of the new epoch then finds it
+    resident, and a search there is bit-exact against the golden model."""
+    import torch
 
-    be = GpuKawpowBackend(0, intensity=1 << 16)
-    last = core.EPOCH_LENGTH - 5  # block 7495, epoch 0
-    t = be.maybe_prebuild(last)
-    assert t is not None
-    t.join(120)
-    assert 1 in be.epochs and be.prebuilt_epochs == [1]
-    assert be.maybe_prebuild(last) is None  # already resident
+    from nodexa_chain_core_amd.miner.search import GpuSearchDevice, SearchPipeline, Work
+
+    dev = GpuSearchDevice(0)
+    dev.searcher(core.EPOCH_LENGTH - 5)  # epoch 0 resident (block 7495)
+    dev.prebuild(1)
+    assert 1 in dev.pending_build and not dev.epoch_ready(1)
+    dev.prebuild(1)  # idempotent
     hh = core.sha256d(b"prebuild")
-    res = be.search(core.EPOCH_LENGTH, hh, bytes.fromhex("0f" + "ff" * 31), 0, 1 << 12)
-    assert res is not None
-    nonce, mix, fin = res
+    w = Work(hh, bytes.fromhex("0f" + "ff" * 31), core.EPOCH_LENGTH, 1, 0, 0)
+    pipe = SearchPipeline(dev, watchdog_s=120)
+    pipe.step(w, 0, 1 << 12)
+    res = pipe.drain()
+    assert dev.epoch_ready(1) and not dev.pending_build and res.shares
     ctx = core.get_epoch_context(1)
-    assert core.kawpow_hash(ctx, core.EPOCH_LENGTH, hh, nonce) == (fin, mix)
+    for sh in res.shares[:4]:
+        assert core.kawpow_hash(ctx, core.EPOCH_LENGTH, hh, sh.nonce) == (sh.final_hash, sh.mix_hash)
+    dev.close()
+    torch.cuda.empty_cache()
 
 
 def _headline_epoch(core, epoch):

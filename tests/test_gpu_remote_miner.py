@@ -8,12 +8,12 @@ pytestmark = pytest.mark.gpu
 
 
 def test_gpu_remote_miner(gpu, core, node_factory):  # noqa: F811
-    from nodexa_chain_core_amd.miner.kawpow_miner import GpuKawpowBackend
     from nodexa_chain_core_amd.miner.remote import RemoteMiner
+    from nodexa_chain_core_amd.miner.search import GpuSearchDevice
 
     node, _ = node_factory()
     c = client(node)
-    m = RemoteMiner(c, GpuKawpowBackend(0, 1 << 16), window=1 << 16, rank=2)
+    m = RemoteMiner(c, GpuSearchDevice(0), window=1 << 16, rank=2)
     stats = m.run(max_blocks=3, max_seconds=180)
     assert stats["accepted"] == 3 and stats["rejected"] == 0, stats
     assert c.getblockcount() == 3
