@@ -17,10 +17,14 @@ result is only trusted where it cannot differ from the reference: any input whos
 batch rejects is re-run on the host, and a block whose deferred run fails is re-connected with
 host checks (`_connect_one`).
 
-The UTXO snapshot is chainstate/coins.dat (no LevelDB in this environment: SURVEY S6), flushed
-every `flush_interval` connected blocks and at shutdown; on start-up blocks stored past the
-snapshot are reconnected (ReplayBlocks-lite), and a snapshot whose best block is unknown is
-rebuilt from genesis.
+The UTXO set persists as chainstate/coins.dat (a checksummed snapshot) plus chainstate/coins.log
+(no LevelDB in this environment: SURVEY S6). A flush — every `flush_interval` connected blocks and
+at shutdown — appends one fsynced journal record with only the outputs added or spent since the
+previous flush (CCoinsViewDB::BatchWrite's change set, src/txdb.cpp:91-), so its cost follows the
+blocks connected, not the size of the UTXO set; the journal is folded into a new snapshot once it
+outgrows it. On start-up the snapshot is loaded, newer complete journal records are replayed (a
+torn tail is cut), blocks stored past that point are reconnected (ReplayBlocks-lite), and a state
+whose best block is unknown is rebuilt from genesis.
 """
 from __future__ import annotations
 
@@ -198,6 +202,7 @@ class ChainState:
         self.script_threads = min(16, os.cpu_count() or 1)  # -par: script-check threads (CCheckQueue)
         self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
         self.flush_interval = 1000
+        self.journal_compact_bytes = 64 << 20  # fold coins.log into coins.dat past this size (or the snapshot's)
         self._since_flush = 0
         self.sig_stats = {"gpu_batches": 0, "gpu_sigs": 0, "host_rechecks": 0}
         if datadir is not None:
@@ -218,6 +223,7 @@ class ChainState:
         self.undo = UndoStore(bdir, bytes(params.message_start))
         self.asset_undo = UndoStore(bdir, bytes(params.message_start), prefix="aun")
         self.coins_path = os.path.join(datadir, "chainstate", "coins.dat") if datadir else None
+        self.coins_log = os.path.join(datadir, "chainstate", "coins.log") if datadir else None
         self.assets_path = os.path.join(datadir, "chainstate", "assets.dat") if datadir else None
         self.indexes_path = os.path.join(datadir, "chainstate", "indexes.dat") if datadir else None
         self.index_flags = dict(indexes or {})  # txindex / addressindex / spentindex / timestampindex
@@ -723,7 +729,9 @@ class ChainState:
     def _init_coins(self) -> None:
         """Load the UTXO snapshot and bring it to the best stored chain (ReplayBlocks-lite)."""
         gh = self.chain.genesis().hash
-        loaded = self.coins_path is not None and self.coins.load(self.coins_path)
+        loaded = self.coins_path is not None and self.coins.load_with_journal(self.coins_path, self.coins_log)
+        if loaded and self.coins.replayed:
+            log.log_printf(f"UTXO journal: {self.coins.replayed} flush record(s) replayed onto the snapshot")
         if loaded:  # the asset state must describe the same block as the UTXO snapshot
             raw = None
             if os.path.exists(self.assets_path):
@@ -753,6 +761,8 @@ class ChainState:
             self.assets = _core.AssetsState()
             self.indexes = _core.ChainIndexes(**self.index_flags)
             self.indexes.best_block = gh
+            if self.coins_path is not None and (os.path.exists(self.coins_path) or os.path.exists(self.coins_log)):
+                self.coins.compact(self.coins_path, self.coins_log)  # a fresh snapshot restarts the journal
         with self.lock:
             self._activate()
 
@@ -946,7 +956,12 @@ class ChainState:
                 f.flush()
                 os.fsync(f.fileno())
             os.replace(tmp, self.indexes_path)
-        self.coins.save(self.coins_path)
+        if not os.path.exists(self.coins_path):  # first flush of this datadir: start from a snapshot
+            self.coins.compact(self.coins_path, self.coins_log)
+        else:
+            self.coins.append_journal(self.coins_log)  # O(outputs changed since the last flush)
+            if os.path.getsize(self.coins_log) > max(self.journal_compact_bytes, os.path.getsize(self.coins_path)):
+                self.coins.compact(self.coins_path, self.coins_log)
         self._since_flush = 0
 
     def _update_mempool(self, disconnected, connected) -> None:

@@ -231,6 +231,14 @@ void bind_script(py::module_& m) {
     py::class_<CoinsView, std::shared_ptr<CoinsView>>(m, "CoinsView")
         .def(py::init<>())
         .def("__len__", &CoinsView::size)
+        .def("append_journal", &CoinsView::append_journal, py::call_guard<py::gil_scoped_release>(),
+             "append the outputs added / spent since the last flush as one fsynced journal record")
+        .def("load_with_journal", &CoinsView::load_with_journal, py::call_guard<py::gil_scoped_release>())
+        .def("compact", &CoinsView::compact, py::call_guard<py::gil_scoped_release>(),
+             "fold the journal into a fresh snapshot and truncate it")
+        .def_property_readonly("dirty", &CoinsView::dirty)
+        .def_readonly("journal_seq", &CoinsView::journal_seq)
+        .def_readonly("replayed", &CoinsView::replayed)
         .def("get", [](const CoinsView& v, const py::bytes& txid, u32 n) -> py::object {
             OutPoint o;
             const std::string h = txid;
@@ -272,6 +280,14 @@ void bind_script(py::module_& m) {
                           need32(h, "best_block");
                           v.best_block = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
                       })
+        .def("spend", [](CoinsView& v, const py::bytes& txid, u32 n) {
+            OutPoint o;
+            const std::string h = txid;
+            need32(h, "txid");
+            o.hash = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
+            o.n = n;
+            return v.spend(o);
+        }, "remove an unspent output (True if it existed)")
         .def("save", &CoinsView::save, py::call_guard<py::gil_scoped_release>())
         .def("load", &CoinsView::load, py::call_guard<py::gil_scoped_release>())
         .def("stats", [](const CoinsView& v) {

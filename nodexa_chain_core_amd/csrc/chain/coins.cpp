@@ -1,8 +1,13 @@
 // UTXO set, undo data and block connection: see coins.hpp.
 #include "coins.hpp"
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <cstdio>
 #include <memory>
 #include <thread>
@@ -21,19 +26,39 @@ const Coin* CoinsView::find(const OutPoint& o) const {
     return it == map_.end() ? nullptr : &it->second;
 }
 
-void CoinsView::add(const OutPoint& o, Coin c) { map_[o] = std::move(c); }
+void CoinsView::add(const OutPoint& o, Coin c) {
+    map_[o] = std::move(c);
+    dirty_[o] = true;
+}
 
 bool CoinsView::spend(const OutPoint& o, Coin* moved) {
     auto it = map_.find(o);
     if (it == map_.end()) return false;
     if (moved) *moved = std::move(it->second);
     map_.erase(it);
+    dirty_[o] = false;
     return true;
 }
 
 namespace {
 
-constexpr char kCoinsMagic[8] = {'N', 'X', 'C', 'O', 'I', 'N', 'S', '1'};
+constexpr char kCoinsMagic[8] = {'N', 'X', 'C', 'O', 'I', 'N', 'S', '1'};   // snapshot, no journal seq
+constexpr char kCoinsMagic2[8] = {'N', 'X', 'C', 'O', 'I', 'N', 'S', '2'};  // snapshot + journal seq
+constexpr char kJournalMagic[4] = {'N', 'X', 'C', 'J'};
+
+// write(2) the whole buffer and fsync: a journal record is durable before flush returns
+void write_all_fsync(int fd, const u8* p, size_t n, const std::string& what) {
+    while (n) {
+        const ssize_t k = ::write(fd, p, n);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            throw std::runtime_error("cannot write " + what);
+        }
+        p += k;
+        n -= size_t(k);
+    }
+    if (::fsync(fd) != 0) throw std::runtime_error("cannot fsync " + what);
+}
 
 void write_coin_entry(Writer& w, const OutPoint& o, const Coin& c) {
     w.u256(o.hash);
@@ -59,19 +84,25 @@ std::vector<std::pair<OutPoint, const Coin*>> sorted_coins(
 
 void CoinsView::save(const std::string& path) const {
     Writer w;
-    w.raw(reinterpret_cast<const u8*>(kCoinsMagic), 8);
+    w.raw(reinterpret_cast<const u8*>(kCoinsMagic2), 8);
     w.u256(best_block);
+    w.u64_(journal_seq);
     w.u64_(map_.size());
     for (auto& kv : map_) write_coin_entry(w, kv.first, kv.second);
     u8 sum[32];
     sha256d(w.buf.data(), w.buf.size(), sum);
     w.raw(sum, 32);
     const std::string tmp = path + ".new";
-    FILE* f = std::fopen(tmp.c_str(), "wb");
-    if (!f) throw std::runtime_error("cannot write " + tmp);
-    const bool ok = std::fwrite(w.buf.data(), 1, w.buf.size(), f) == w.buf.size() && std::fflush(f) == 0;
-    std::fclose(f);
-    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot replace " + path);
+    const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) throw std::runtime_error("cannot write " + tmp);
+    try {
+        write_all_fsync(fd, w.buf.data(), w.buf.size(), tmp);
+    } catch (...) {
+        ::close(fd);
+        throw;
+    }
+    ::close(fd);
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot replace " + path);
 }
 
 bool CoinsView::load(const std::string& path) {
@@ -80,13 +111,17 @@ bool CoinsView::load(const std::string& path) {
     std::ifstream f(path, std::ios::binary);
     if (!f) return false;
     Bytes b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-    if (b.size() < 8 + 32 + 8 + 32 || std::memcmp(b.data(), kCoinsMagic, 8) != 0) return false;
+    if (b.size() < 8 + 32 + 8 + 32) return false;
+    const bool v2 = std::memcmp(b.data(), kCoinsMagic2, 8) == 0;
+    if (!v2 && std::memcmp(b.data(), kCoinsMagic, 8) != 0) return false;
     u8 sum[32];
     sha256d(b.data(), b.size() - 32, sum);
     if (std::memcmp(sum, b.data() + b.size() - 32, 32) != 0) return false;
+    dirty_.clear();
     try {
         Reader r(b.data() + 8, b.size() - 8 - 32);
         best_block = r.u256();
+        journal_seq = v2 ? r.u64_() : 0;
         const u64 n = r.u64_();
         map_.reserve(n);
         for (u64 i = 0; i < n; ++i) {
@@ -104,9 +139,116 @@ bool CoinsView::load(const std::string& path) {
     } catch (const std::exception&) {
         map_.clear();
         best_block = Uint256();
+        journal_seq = 0;
         return false;
     }
     return true;
+}
+
+void CoinsView::append_journal(const std::string& journal) {
+    Writer pay;
+    pay.u64_(journal_seq + 1);
+    pay.u256(best_block);
+    pay.u64_(dirty_.size());
+    for (auto& [o, present] : dirty_) {
+        pay.u256(o.hash);
+        pay.u32_(o.n);
+        const Coin* c = present ? find(o) : nullptr;
+        pay.u8_(c ? 1 : 0);
+        if (c) {
+            pay.u32_((c->height << 1) | (c->coinbase ? 1u : 0u));
+            pay.i64_(c->out.value);
+            pay.var_bytes(c->out.script_pubkey);
+        }
+    }
+    Writer rec;
+    rec.raw(reinterpret_cast<const u8*>(kJournalMagic), 4);
+    rec.u32_(u32(pay.buf.size()));
+    rec.raw(pay.buf);
+    u8 sum[32];
+    sha256d(pay.buf.data(), pay.buf.size(), sum);
+    rec.raw(sum, 32);
+    const int fd = ::open(journal.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+    if (fd < 0) throw std::runtime_error("cannot open " + journal);
+    try {
+        write_all_fsync(fd, rec.buf.data(), rec.buf.size(), journal);
+    } catch (...) {
+        ::close(fd);
+        throw;
+    }
+    ::close(fd);
+    ++journal_seq;
+    dirty_.clear();
+}
+
+bool CoinsView::load_with_journal(const std::string& snapshot, const std::string& journal) {
+    const bool have_snapshot = load(snapshot);
+    if (!have_snapshot) {  // no (valid) snapshot: the journal alone is replayed from sequence 1
+        map_.clear();
+        best_block = Uint256();
+        journal_seq = 0;
+    }
+    replayed = 0;
+    std::ifstream f(journal, std::ios::binary);
+    if (!f) return have_snapshot;
+    Bytes b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    f.close();
+    size_t pos = 0, good = 0;
+    while (b.size() - pos >= 8 + 32) {
+        if (std::memcmp(b.data() + pos, kJournalMagic, 4) != 0) break;
+        const u32 len = load_le32(b.data() + pos + 4);
+        if (b.size() - pos - 8 < size_t(len) + 32) break;  // torn tail record
+        const u8* payload = b.data() + pos + 8;
+        u8 sum[32];
+        sha256d(payload, len, sum);
+        if (std::memcmp(sum, payload + len, 32) != 0) break;
+        try {
+            Reader r(payload, len);
+            const u64 seq = r.u64_();
+            const Uint256 best = r.u256();
+            const u64 n = r.u64_();
+            if (seq > journal_seq + 1) break;  // a gap: records after it cannot apply
+            if (seq == journal_seq + 1) {
+                for (u64 i = 0; i < n; ++i) {
+                    OutPoint o;
+                    o.hash = r.u256();
+                    o.n = r.u32_();
+                    if (r.u8_()) {
+                        Coin c;
+                        const u32 code = r.u32_();
+                        c.height = code >> 1;
+                        c.coinbase = code & 1;
+                        c.out.value = r.i64_();
+                        c.out.script_pubkey = r.var_bytes();
+                        map_[o] = std::move(c);
+                    } else {
+                        map_.erase(o);
+                    }
+                }
+                best_block = best;
+                journal_seq = seq;
+                ++replayed;
+            }
+        } catch (const std::exception&) {
+            break;
+        }
+        pos += 8 + size_t(len) + 32;
+        good = pos;
+    }
+    if (good < b.size()) {  // cut a torn or corrupt tail so later appends follow a complete record
+        if (::truncate(journal.c_str(), off_t(good)) != 0) throw std::runtime_error("cannot truncate " + journal);
+    }
+    dirty_.clear();
+    return have_snapshot || replayed > 0;
+}
+
+void CoinsView::compact(const std::string& snapshot, const std::string& journal) {
+    if (!dirty_.empty()) append_journal(journal);
+    save(snapshot);  // carries journal_seq: every record up to it is now folded in
+    const int fd = ::open(journal.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) throw std::runtime_error("cannot truncate " + journal);
+    ::fsync(fd);
+    ::close(fd);
 }
 
 CoinsView::Stats CoinsView::stats() const {

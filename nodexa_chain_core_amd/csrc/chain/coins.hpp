@@ -64,6 +64,19 @@ public:
     // Snapshot persistence (chainstate/coins.dat): written to path.new, fsynced and renamed.
     void save(const std::string& path) const;
     bool load(const std::string& path);  // false if absent or corrupt (the view is then empty)
+    // Incremental persistence, the analogue of CCoinsViewDB::BatchWrite (src/txdb.cpp:91-): a
+    // flush appends one checksummed record holding only the outputs added or spent since the
+    // previous flush (plus the new best block) to a journal (chainstate/coins.log) and fsyncs it,
+    // so flush cost follows the change set, not the UTXO set. Records carry a sequence number and
+    // the snapshot the one of the last record folded into it; start-up loads the snapshot and
+    // replays the newer complete records (a torn tail record from a crash is cut off). compact()
+    // folds the journal into a fresh snapshot.
+    void append_journal(const std::string& journal);
+    bool load_with_journal(const std::string& snapshot, const std::string& journal);
+    void compact(const std::string& snapshot, const std::string& journal);
+    size_t dirty() const { return dirty_.size(); }
+    u64 journal_seq = 0;      // records written (or replayed) so far
+    size_t replayed = 0;      // records applied by the last load_with_journal
     // gettxoutsetinfo: (number of unspent outputs, transactions with unspent outputs, total value,
     // sha256d over the coins in (txid, n) order).
     struct Stats {
@@ -79,6 +92,7 @@ public:
 
 private:
     std::unordered_map<OutPoint, Coin, OutPointHasher, OutPointEq> map_;
+    std::unordered_map<OutPoint, bool, OutPointHasher, OutPointEq> dirty_;  // since the last flush
 };
 
 struct TxUndo {
