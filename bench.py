@@ -240,8 +240,9 @@ def main() -> int:
         torch.cuda.synchronize()
         eq_dt = W.all_reduce_max(time.perf_counter() - t0)
         eq_sols = round(W.all_reduce_sum_int(found) / eq_dt, 2)
+        log(f"[bench] Equihash(200,9): {eq_sols} Sol/s ({args.equihash} x 8 solves per rank, {found} solutions "
+            f"in {eq_dt:.3f}s, {solver.fallbacks} host re-solves)")
         del solver
-        log(f"[bench] Equihash(200,9): {eq_sols} Sol/s ({args.equihash} x 8 solves per rank)")
 
     verify = _verify_headers_bench(log) if args.verify and not cpu else None
 

@@ -393,19 +393,31 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
 #else
     __shared__ uint32_t digs[KP_BLOCK * 8];
 #endif
-    __shared__ uint32_t stale;
+#if defined(KP_DIGEST_REG) || defined(KP_DIGEST_GLOBAL)
+    __shared__ uint32_t stale_word;
+    uint32_t* stale = &stale_word;
+#else
+    // the LDS-digest form is at 80 KiB per workgroup, two per CU: a separate flag word would push
+    // it past the 160 KiB and halve the occupancy, so the flag borrows the digest buffer's first
+    // word (digests land there only after the second barrier below)
+    uint32_t* stale = digs;
+#endif
     if (blockDim.x != KP_BLOCK) return;  // launched with the wrong block: no shares rather than bad ones
     if (threadIdx.x == 0) {
         // one uncached read of the host-mapped generation word per workgroup, overlapped with the
         // L1 fill below: a template change stops queued work within one workgroup's lifetime
         uint32_t s = 0;
         if (p.gen_word) s = __hip_atomic_load(p.gen_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != p.generation;
-        stale = s;
+        *stale = s;
         if (s) atomicAdd(&p.results->skipped, 1u);
     }
     kp_fill_l1(l1, p.dag);
     __syncthreads();
-    if (stale) return;  // uniform over the workgroup, after its only barrier
+    const uint32_t is_stale = *stale;
+#if !(defined(KP_DIGEST_REG) || defined(KP_DIGEST_GLOBAL))
+    __syncthreads();  // every wave has read the flag before a digest can overwrite it
+#endif
+    if (is_stale) return;  // uniform over the workgroup
 
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t nonce = p.start_nonce + (uint64_t)blockIdx.x * KP_BLOCK + threadIdx.x;

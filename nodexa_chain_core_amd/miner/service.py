@@ -94,10 +94,25 @@ class Comm:
         self.rebind()
 
     def rebind(self) -> None:
-        torch = self.torch
+        """Bind to the current world. The loop gets a communicator of its own (not the default
+        group), so a failed one can be aborted (RCCL) and replaced without touching the default
+        group or its rendezvous store."""
+        torch, dist = self.torch, self.W.dist
         self.w = self.W.get()
         self.gpu = self.w.backend == "nccl"
         self.stream = torch.cuda.Stream(device=self.w.device) if self.gpu else None
+        self.group = self.w.group
+        if self.w.distributed and self.group is None:
+            self.group = dist.new_group(ranks=list(range(self.w.world_size)), timeout=self.timeout)
+
+    def abort(self) -> None:
+        """Tear down the loop's communicator after a failure: RCCL kernels still waiting for a dead
+        peer are cancelled (ncclCommAbort); gloo needs nothing (its ops already raised)."""
+        if self.gpu and self.group is not None:
+            try:
+                self.W.dist.distributed_c10d._abort_process_group(self.group)
+            except Exception as e:  # noqa: BLE001 — best effort; the survivors re-form regardless
+                log.log_printf(f"miner: aborting the failed communicator: {e}")
 
     def _wait(self, work, what: str) -> None:
         try:
@@ -127,7 +142,7 @@ class Comm:
                 t.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
             if self.gpu:
                 t = t.to(self.w.device, non_blocking=True)
-            self._wait(dist.broadcast(t, src=self.w.global_rank(0), group=self.w.group, async_op=True), "broadcast")
+            self._wait(dist.broadcast(t, src=self.w.global_rank(0), group=self.group, async_op=True), "broadcast")
             return bytes(t.cpu().numpy().tobytes())
 
         return self._run(go, "broadcast")
@@ -143,11 +158,11 @@ class Comm:
             if self.gpu:
                 mine = mine.to(self.w.device, non_blocking=True)
                 out = torch.empty(ws * n, dtype=torch.uint8, device=self.w.device)
-                self._wait(dist.all_gather_into_tensor(out, mine, group=self.w.group, async_op=True), "all_gather")
+                self._wait(dist.all_gather_into_tensor(out, mine, group=self.group, async_op=True), "all_gather")
             else:
                 out = torch.empty(ws * n, dtype=torch.uint8)
                 parts = list(out.view(ws, n).unbind(0))
-                self._wait(dist.all_gather(parts, mine, group=self.w.group, async_op=True), "all_gather")
+                self._wait(dist.all_gather(parts, mine, group=self.group, async_op=True), "all_gather")
             raw = bytes(out.cpu().numpy().tobytes())
             return [raw[i * n:(i + 1) * n] for i in range(ws)]
 
@@ -162,7 +177,7 @@ class Comm:
             t = torch.tensor(vals, dtype=torch.int64)
             if self.gpu:
                 t = t.to(self.w.device, non_blocking=True)
-            self._wait(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.w.group, async_op=True), "all_reduce")
+            self._wait(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True), "all_reduce")
             return [int(x) for x in t.cpu().tolist()]
 
         return self._run(go, "all_reduce")
@@ -510,6 +525,7 @@ class MiningService:
             raise
         except Exception:  # noqa: BLE001 — the window of the broken step is discarded
             pass
+        self.comm.abort()
         W.shrink(alive, timeout_s=int(max(1, self.collective_timeout_s)))
         self.comm.rebind()
         self.work = Work()
@@ -586,7 +602,7 @@ def follower_main() -> int:
     watchdog = float(os.environ.get("NODEXA_MINER_WATCHDOG", "120"))
     window = int(os.environ.get("NODEXA_MINER_WINDOW", str(1 << 25)))
     W.init(use_gpu=not cpu, device_index=None if dev_index is None else int(dev_index),
-           timeout_s=int(max(timeout, 10)))
+           timeout_s=int(max(timeout, 10)), elastic=True)
     if cpu:
         from .search import CpuSearchDevice
 

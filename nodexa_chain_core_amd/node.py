@@ -339,7 +339,7 @@ class Node:
         timeout = float(a.get("minercollectivetimeout", "60"))
         self.miner_procs = []
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)))
+            W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)), elastic=True)
         else:
             gpus = self.gpus or [0] * max(1, a.get_int("minerranks", 1))
             if len(gpus) > 1:
@@ -355,7 +355,7 @@ class Node:
                     env["NODEXA_MINER_WINDOW"] = a.get("gpuintensity")
                 self.miner_procs = MS.spawn_followers(gpus, port, cpu=cpu, extra_env=env)
             W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)), device_index=None if cpu else gpus[0],
-                   rank=0, world_size=len(gpus))
+                   rank=0, world_size=len(gpus), elastic=True)
         w = W.get()
         window = a.get_int("gpuintensity", 4096 if cpu else 1 << 25)
         dev = CpuSearchDevice(max_window=window) if cpu else GpuSearchDevice(w.device.index,

@@ -42,7 +42,7 @@ _WORLD: World | None = None
 
 
 def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | None = None,
-         rank: int | None = None, world_size: int | None = None) -> World:
+         rank: int | None = None, world_size: int | None = None, elastic: bool = False) -> World:
     """Initialise from RANK/WORLD_SIZE/LOCAL_RANK (torchrun, or the node's spawned miner ranks)
     or single-process; `rank` / `world_size` override the environment. `device_index`: the GPU
     of this rank (default: LOCAL_RANK)."""
@@ -65,6 +65,10 @@ def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         backend = "nccl" if use_gpu else "gloo"
+        if elastic and use_gpu:
+            # a collective that times out must raise to the caller (which aborts the communicator
+            # and re-forms the group over the survivors), not make RCCL's watchdog end the process
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
         kw = {}
         if use_gpu:
             kw["device_id"] = device
