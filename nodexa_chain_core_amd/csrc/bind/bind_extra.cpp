@@ -90,6 +90,22 @@ void bind_extra(py::module_& m) {
         }
         return py::make_tuple(py::bytes(kinds), py::bytes(jobs), py::bytes(mix), py::bytes(bound), py::bytes(pre));
     }, py::arg("headers"), py::arg("kawpow_activation_time"));
+    // The GPU form of the pass above (hip sha256d.hip: kawpow_mixonly_batch): only the header
+    // kinds and the raw 120-byte KawPow headers are made on the host; SHA256d, both keccak-f800
+    // absorbs and the nBits boundary run on the device. kind: 0 = KawPow, 2 = Equihash, 3 = X16R.
+    m.def("kawpow_batch_headers", [](const py::list& headers, u32 kawpow_activation_time) {
+        const size_t n = headers.size();
+        std::string kinds(n, '\0'), raw(n * 120, '\0');
+        for (size_t i = 0; i < n; ++i) {
+            const BlockHeader& h = headers[i].cast<const BlockHeader&>();
+            if (h.is_equihash()) { kinds[i] = 2; continue; }
+            if (!h.is_kawpow(kawpow_activation_time)) { kinds[i] = 3; continue; }
+            const Bytes b = h.bytes(kawpow_activation_time);
+            if (b.size() != 120) throw std::runtime_error("KawPow header does not serialize to 120 bytes");
+            std::memcpy(raw.data() + 120 * i, b.data(), 120);
+        }
+        return py::make_tuple(py::bytes(kinds), py::bytes(raw));
+    }, py::arg("headers"), py::arg("kawpow_activation_time"));
     m.def("kawpow_programs_bytes", [](const std::vector<u64>& periods) {
         std::string out(periods.size() * 256, '\0');
         {

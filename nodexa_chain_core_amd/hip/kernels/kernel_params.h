@@ -192,6 +192,16 @@ struct KawpowHashParams {
 
 // Batch SHA-256d (sha256d.hip). sha256d_batch: n messages of len bytes, stride bytes apart.
 // sha256d_merkle_level: n output nodes from len 32-byte input nodes (stride unused).
+// Mix-only batch header check (K4 + K6, sha256d.hip: kawpow_mixonly_batch), one lane per header:
+// 120-byte KawPow headers in, 128-byte rows out = header hash | mix-only final | nBits boundary |
+// claimed mix, all four in ProgPoW byte order (the boundary big-endian).
+struct MixOnlyParams {
+    const uint8_t* headers;
+    uint8_t* out;      // n x 128 bytes
+    uint32_t n;
+    uint32_t stride;   // bytes between headers (>= 120)
+};
+
 struct Sha256dParams {
     const uint8_t* in;
     uint8_t* out;      // n x 32 bytes

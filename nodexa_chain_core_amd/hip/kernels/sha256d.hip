@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include "kernel_params.h"
+#include "keccak_device.hpp"
 
 __constant__ uint32_t SHA256_K[64] = {
     0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
@@ -131,4 +132,80 @@ extern "C" __global__ __launch_bounds__(256) void sha256d_merkle_level(Sha256dPa
     sha256_compress(s1, pad);
     sha256_of_digest(s1, s2);
     store_digest(p.out + size_t(i) * 32, s2);
+}
+
+// ---------------------------------------------------------------- K4: mix-only header check
+// progpow::hash_no_verify (src/crypto/ethash/lib/ethash/progpow.cpp:498-550) for a batch of KawPow
+// headers, fused with the SHA256d header hash it needs (K6): header hash = SHA256d of the 80-byte
+// CKAWPOWInput (src/primitives/block.h:213-233), byte-reversed into ProgPoW order (GetHex ->
+// to_hash256, src/hash.cpp:269-270); seed = keccak-f800(header hash, nonce64, "rAVENCOINKAWPOW");
+// final = keccak-f800(seed[0..7], claimed mix, "RAVENCOIN"). The host then sends only the headers
+// whose final meets their nBits boundary to the full (DAG) check — the reference's CheckBlockHeader
+// does that cheap check first for the same reason (src/validation.cpp:11638-11665).
+__device__ __forceinline__ uint32_t mo_le32(const uint8_t* p) {
+    return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+}
+
+__device__ __forceinline__ void mo_store_le(uint8_t* o, uint32_t w) {
+    o[0] = uint8_t(w); o[1] = uint8_t(w >> 8); o[2] = uint8_t(w >> 16); o[3] = uint8_t(w >> 24);
+}
+
+extern "C" __global__ __launch_bounds__(256) void kawpow_mixonly_batch(MixOnlyParams p) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    const uint8_t* h = p.headers + size_t(i) * p.stride;
+    uint8_t* o = p.out + size_t(i) * 128;
+    uint32_t s1[8], s2[8];
+    sha256_bytes(h, 80, s1);
+    sha256_of_digest(s1, s2);
+    // ProgPoW word k of the byte-reversed digest is SHA state word 7-k (its big-endian bytes reversed)
+    uint32_t st[25];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st[k] = s2[7 - k];
+    st[8] = mo_le32(h + 80);   // nonce64 low
+    st[9] = mo_le32(h + 84);   // nonce64 high
+    const uint32_t pad1[15] = {0x72, 0x41, 0x56, 0x45, 0x4E, 0x43, 0x4F, 0x49, 0x4E, 0x4B, 0x41, 0x57, 0x50, 0x4F, 0x57};
+#pragma unroll
+    for (int k = 0; k < 15; ++k) st[10 + k] = pad1[k];
+    uint32_t hh[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hh[k] = st[k];
+    keccak_f800(st);
+    uint32_t mix[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mix[k] = __builtin_bswap32(mo_le32(h + 88 + 28 - 4 * k));  // reversed mix_hash
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st[8 + k] = mix[k];  // st[0..7] = seed state words
+    const uint32_t pad2[9] = {0x72, 0x41, 0x56, 0x45, 0x4E, 0x43, 0x4F, 0x49, 0x4E};
+#pragma unroll
+    for (int k = 0; k < 9; ++k) st[16 + k] = pad2[k];
+    keccak_f800(st);
+    // nBits -> 256-bit target, big-endian bytes (arith_uint256::SetCompact; zero when negative or
+    // overflowing, so nothing meets it)
+    const uint32_t bits = mo_le32(h + 72);
+    const uint32_t ex = bits >> 24;
+    uint32_t mant = bits & 0x007fffffu;
+    const bool neg = mant != 0 && (bits & 0x00800000u) != 0;
+    const bool ovf = mant != 0 && (ex > 34 || (mant > 0xff && ex > 33) || (mant > 0xffff && ex > 32));
+    uint8_t b[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) b[k] = 0;
+    if (!neg && !ovf) {
+        if (ex <= 3) {
+            mant >>= 8 * (3 - ex);
+            b[31] = uint8_t(mant); b[30] = uint8_t(mant >> 8); b[29] = uint8_t(mant >> 16);
+        } else {
+            const uint32_t s = ex - 3;  // little-endian byte position of the mantissa's low byte
+            for (uint32_t q = 0; q < 3; ++q)
+                if (s + q < 32) b[31 - (s + q)] = uint8_t(mant >> (8 * q));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        mo_store_le(o + 4 * k, hh[k]);
+        mo_store_le(o + 32 + 4 * k, st[k]);
+        mo_store_le(o + 96 + 4 * k, mix[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) o[64 + k] = b[k];
 }

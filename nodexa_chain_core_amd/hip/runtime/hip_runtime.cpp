@@ -429,6 +429,17 @@ PYBIND11_MODULE(_hip, m) {
     m.attr("EQ_SOL_WORDS") = EQ_SOL_WORDS;
     // Batch SHA-256d (sha256d.hip): messages of `len` bytes at `stride`, or (merkle=true) one
     // ComputeMerkleRoot level of `len` 32-byte nodes into (len + 1) / 2 nodes.
+    m.def("launch_kawpow_mixonly", [](const Kernel& k, uintptr_t headers, uint32_t n, uint32_t stride, uintptr_t out,
+                                      uintptr_t stream) {
+        if (stride < 120) throw std::invalid_argument("KawPow headers are 120 bytes");
+        if (n == 0) return;
+        MixOnlyParams p{};
+        p.headers = reinterpret_cast<const uint8_t*>(headers);
+        p.out = reinterpret_cast<uint8_t*>(out);
+        p.n = n;
+        p.stride = stride;
+        k.launch_bytes(dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("launch_sha256d", [](const Kernel& k, uintptr_t in, uint32_t len, uint32_t stride, uint32_t n, uintptr_t out,
                                bool merkle, uintptr_t stream) {
         if (n == 0) return;

@@ -56,7 +56,11 @@ def _verify_native(params, headers, gpus, threads: int, mode: str, rows_fn=None)
     rows are checked with numpy, so host time per header stays ~1-2 us."""
     t0 = time.perf_counter()
     n = len(headers)
-    kinds_b, jobs_b, mix_b, bound_b, pre_b = _core.kawpow_batch_prepare(list(headers), params.kawpow_activation_time)
+    if gpus and n >= MIXONLY_GPU_MIN and os.environ.get("NODEXA_MIXONLY", "gpu") == "gpu":
+        kinds_b, jobs_b, mix_b, bound_b, pre_b = _prepare_gpu(params, headers, gpus[0])
+    else:
+        kinds_b, jobs_b, mix_b, bound_b, pre_b = _core.kawpow_batch_prepare(list(headers),
+                                                                            params.kawpow_activation_time)
     kinds = np.frombuffer(kinds_b, dtype=np.uint8)
     out: list[dict] = [{} for _ in range(n)]
     pre = np.frombuffer(pre_b, dtype=np.uint8).reshape(n, 32)
@@ -94,6 +98,33 @@ def _verify_native(params, headers, gpus, threads: int, mode: str, rows_fn=None)
     LAST_TIMING.update(prepare_s=t1 - t0, kawpow_s=t2 - t1, check_s=t3 - t2, equihash_s=t4 - t3,
                        x16r_s=time.perf_counter() - t4)
     return out
+
+
+# Batches at least this large take the device prefilter; smaller ones (a block, a few
+# headers) stay on the native host pass, whose cost is below a launch's.
+MIXONLY_GPU_MIN = 256
+
+
+def _prepare_gpu(params, headers, device: int):
+    """kawpow_batch_prepare's outputs with the mix-only stage on the GPU: the host only sorts the
+    header kinds and lays out the 120-byte KawPow headers (_core.kawpow_batch_headers)."""
+    from ..ops.sha256 import kawpow_mixonly_batch
+
+    n = len(headers)
+    kinds_b, raw_b = _core.kawpow_batch_headers(list(headers), params.kawpow_activation_time)
+    kinds = np.frombuffer(kinds_b, dtype=np.uint8).copy()
+    raw = np.frombuffer(raw_b, dtype=np.uint8).reshape(n, 120)
+    kp = np.flatnonzero(kinds == 0)
+    rows = np.zeros((n, 128), np.uint8)
+    rows[kp] = kawpow_mixonly_batch(raw[kp], device)
+    pre, bound = rows[:, 32:64], rows[:, 64:96]
+    kinds[kp[~_rows_le(np.ascontiguousarray(pre[kp]), np.ascontiguousarray(bound[kp]))]] = 1
+    jobs = np.zeros((n, 48), np.uint8)
+    jobs[:, :32] = rows[:, :32]
+    jobs[:, 32:40] = raw[:, 80:88]   # nNonce64 (LE)
+    jobs[:, 40:44] = raw[:, 76:80]   # nHeight (LE)
+    return (kinds.tobytes(), jobs.tobytes(), np.ascontiguousarray(rows[:, 96:128]).tobytes(),
+            np.ascontiguousarray(bound).tobytes(), np.ascontiguousarray(pre).tobytes())
 
 
 def _gpu_rows(jobs: np.ndarray, gpus: list[int], mode: str) -> np.ndarray:

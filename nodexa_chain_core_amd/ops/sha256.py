@@ -48,3 +48,21 @@ def merkle_root(txids: list[bytes], device: int = 0) -> bytes:
                                          runtime.current_stream_handle())
             cur, n = nxt, m
         return cur.cpu().numpy().tobytes()
+
+
+def kawpow_mixonly_batch(raw: np.ndarray, device: int = 0) -> np.ndarray:
+    """(n, 128) rows for an (n, 120) uint8 array of KawPow headers: header hash | mix-only final |
+    nBits boundary | claimed mix, ProgPoW byte order (hash_no_verify fused with the SHA256d header
+    hash, hip/kernels/sha256d.hip: kawpow_mixonly_batch)."""
+    n = len(raw)
+    if n == 0:
+        return np.zeros((0, 128), np.uint8)
+    if raw.shape[1] != 120:
+        raise ValueError("KawPow headers are 120 bytes")
+    dev = torch.device("cuda", device)
+    with torch.cuda.device(device):
+        d_in = torch.from_numpy(np.ascontiguousarray(raw)).to(dev)
+        d_out = torch.empty((n, 128), dtype=torch.uint8, device=dev)
+        runtime.hip().launch_kawpow_mixonly(runtime.static_kernel("sha256d", "kawpow_mixonly_batch"), d_in.data_ptr(),
+                                            n, 120, d_out.data_ptr(), runtime.current_stream_handle())
+        return d_out.cpu().numpy()
