@@ -1100,8 +1100,10 @@ class ChainState:
                 return False, why, fee
             for k, (value, spk) in enumerate(coins):
                 vin = tx.vin[k]
+                # sigcache=1: signatures that verify are remembered, so the block that confirms this
+                # transaction skips them (CSignatureCache, src/script/sigcache.cpp:76-86)
                 ok, err = _core.verify_script(vin.script_sig, spk, list(vin.witness), _core.STANDARD_SCRIPT_VERIFY_FLAGS,
-                                              raw, k, value)
+                                              raw, k, value, 1)
                 if not ok:
                     ok2, _ = _core.verify_script(vin.script_sig, spk, list(vin.witness),
                                                  _core.BLOCK_SCRIPT_VERIFY_FLAGS, raw, k, value)

@@ -7,6 +7,7 @@
 #include "../chain/coins.hpp"
 #include "../chain/indexes.hpp"
 #include "../chain/interpreter.hpp"
+#include "../chain/sigcache.hpp"
 #include "../chain/params.hpp"
 #include "../crypto/secp256k1.hpp"
 #include "../crypto/secp256k1_model32.hpp"
@@ -186,11 +187,13 @@ void bind_script(py::module_& m) {
     }, "the reference's flag names (src/test/transaction_tests.cpp mapFlagNames)");
     m.def("verify_script", [](const py::bytes& script_sig, const py::bytes& script_pubkey,
                               const std::vector<py::bytes>& witness, u32 flags, const py::bytes& tx_raw, unsigned n_in,
-                              int64_t amount) {
+                              int64_t amount, int sigcache) {
         const Transaction tx = tx_of(tx_raw);
         if (n_in >= tx.vin.size()) throw std::invalid_argument("input index out of range");
         const PrecomputedTx cache(tx);
-        const TxSigChecker checker(&tx, n_in, amount, &cache);
+        TxSigChecker checker(&tx, n_in, amount, &cache);
+        if (sigcache < 0 || sigcache > 2) throw std::invalid_argument("sigcache: 0 none, 1 store, 2 use");
+        checker.sigcache = TxSigChecker::CacheMode(sigcache);
         const std::vector<Bytes> wit = stack_of(witness);
         ScriptError err = ScriptError::UNKNOWN_ERROR;
         py::gil_scoped_release rel;
@@ -198,8 +201,23 @@ void bind_script(py::module_& m) {
         py::gil_scoped_acquire acq;
         return py::make_tuple(ok, script_error_name(err));
     }, py::arg("script_sig"), py::arg("script_pubkey"), py::arg("witness"), py::arg("flags"), py::arg("tx"),
-       py::arg("n_in"), py::arg("amount"),
-       "VerifyScript of input n_in of the serialized tx -> (ok, error name)");
+       py::arg("n_in"), py::arg("amount"), py::arg("sigcache") = 0,
+       "VerifyScript of input n_in of the serialized tx -> (ok, error name); sigcache 1 = store verified "
+       "signatures (mempool acceptance), 2 = answer from the cache (block validation)");
+    m.def("sigcache_set_max_bytes", [](size_t b) { SigCache::instance().set_max_bytes(b); },
+          "-maxsigcachesize (bytes of 32-byte entries)");
+    m.def("sigcache_clear", [] { SigCache::instance().clear(); });
+    m.def("sigcache_stats", [] {
+        const SigCache::Stats s = SigCache::instance().stats();
+        py::dict d;
+        d["entries"] = s.entries;
+        d["max_entries"] = s.max_entries;
+        d["hits"] = s.hits;
+        d["misses"] = s.misses;
+        d["inserts"] = s.inserts;
+        d["evictions"] = s.evictions;
+        return d;
+    });
     m.def("eval_script", [](const std::vector<py::bytes>& stack, const py::bytes& script, u32 flags) {
         std::vector<Bytes> st = stack_of(stack);
         ScriptError err = ScriptError::UNKNOWN_ERROR;
@@ -337,7 +355,7 @@ void bind_script(py::module_& m) {
         }, "deferred signatures as (pubkey, DER signature, message) for ops/secp.verify_batch");
     m.def("connect_block", [](const Block& block, int height, CoinsView& view, bool check_scripts, bool defer_sigs,
                               py::object mtp_at, int64_t block_mtp, u32 flags, int threads, assets::State* asset_state,
-                              const assets::Flags& asset_flags, const py::bytes& block_hash) {
+                              const assets::Flags& asset_flags, const py::bytes& block_hash, bool sigcache) {
         ConnectOptions opt;
         opt.assets = asset_state;
         opt.asset_flags = asset_flags;
@@ -346,6 +364,7 @@ void bind_script(py::module_& m) {
         opt.script_flags = flags;
         opt.check_scripts = check_scripts;
         opt.defer_sigs = defer_sigs;
+        opt.sigcache = sigcache;
         opt.block_mtp = block_mtp;
         opt.threads = threads;
         if (!mtp_at.is_none())
@@ -365,7 +384,7 @@ void bind_script(py::module_& m) {
     }, py::arg("block"), py::arg("height"), py::arg("view"), py::arg("check_scripts") = true,
        py::arg("defer_sigs") = false, py::arg("mtp_at") = py::none(), py::arg("block_mtp") = 0,
        py::arg("flags") = kBlockScriptFlags, py::arg("threads") = 1, py::arg("assets") = nullptr,
-       py::arg("asset_flags") = assets::Flags{}, py::arg("block_hash") = py::bytes(),
+       py::arg("asset_flags") = assets::Flags{}, py::arg("block_hash") = py::bytes(), py::arg("sigcache") = true,
        "ConnectBlock against the view -> (ConnectResult, serialized CBlockUndo); the view is unchanged on failure");
     m.def("disconnect_block", [](const Block& block, const py::bytes& undo, CoinsView& view, assets::State* st,
                                  const py::bytes& asset_undo) {

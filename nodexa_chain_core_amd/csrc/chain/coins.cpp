@@ -651,6 +651,7 @@ ConnectResult connect_block(const Block& block, int height, CoinsView& view, con
         const Transaction& tx = block.vtx[c.t];
         TxSigChecker checker(&tx, c.i, c.value, caches[c.t].get());
         if (opt.defer_sigs) checker.pending = &c.sigs;
+        if (opt.sigcache) checker.sigcache = TxSigChecker::CacheMode::USE;
         c.ok = verify_script(tx.vin[c.i].script_sig, c.spk, &tx.vin[c.i].witness, opt.script_flags, checker, &c.err);
     };
     const int nthreads = std::max(1, std::min<int>(opt.threads, int(checks.size() / 16)));

@@ -112,6 +112,7 @@ struct ConnectOptions {
     u32 script_flags = kBlockScriptFlags;
     bool check_scripts = true;
     bool defer_sigs = false;   // collect signatures for a batch verifier instead of checking them
+    bool sigcache = true;      // skip (and drop) signatures the mempool already verified (sigcache.hpp)
     bool sequence_locks = true;
     // median time past of the block at `height` of this block's chain (BIP68 time locks)
     std::function<int64_t(int)> mtp_at;

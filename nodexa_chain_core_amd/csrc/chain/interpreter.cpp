@@ -1,5 +1,6 @@
 // Script interpreter: see interpreter.hpp.
 #include "interpreter.hpp"
+#include "sigcache.hpp"
 
 #include "assets.hpp"
 
@@ -421,11 +422,15 @@ bool TxSigChecker::check_sig(const Bytes& sig_in, const Bytes& pubkey, const Byt
     const int hash_type = sig_in.back();
     const Bytes sig(sig_in.begin(), sig_in.end() - 1);
     const Uint256 msg = signature_hash(script_code, *tx_, n_in_, hash_type, amount_, sv, cache_);
+    if (sigcache != CacheMode::NONE && SigCache::instance().get(msg.data, pubkey, sig, sigcache == CacheMode::USE))
+        return true;  // verified when the transaction entered the mempool
     if (pending) {
         pending->push_back(PendingSig{msg, sig, pubkey});
         return true;
     }
-    return secp::verify_der(pubkey.data(), pubkey.size(), sig.data(), sig.size(), msg.data);
+    const bool ok = secp::verify_der(pubkey.data(), pubkey.size(), sig.data(), sig.size(), msg.data);
+    if (ok && sigcache == CacheMode::STORE) SigCache::instance().put(msg.data, pubkey, sig);
+    return ok;
 }
 
 bool TxSigChecker::check_lock_time(int64_t n) const {

@@ -126,6 +126,11 @@ public:
     // valid for scripts whose outcome cannot depend on a signature failing, i.e. for blocks,
     // where any failing signature invalidates the block anyway.
     std::vector<PendingSig>* pending = nullptr;
+    // Signature cache (sigcache.hpp): STORE remembers every signature that verifies (mempool
+    // acceptance); USE answers from the cache first and erases what it hits (block validation,
+    // CachingTransactionSignatureChecker with store = false).
+    enum class CacheMode : u8 { NONE, STORE, USE };
+    CacheMode sigcache = CacheMode::NONE;
 
 protected:
     const Transaction* tx_;

@@ -251,6 +251,8 @@ class Node:
             w.keypool_size = max(1, a.get_int("keypool", w.keypool_size))
             w.broadcast = a.get_bool("walletbroadcast", True)
             w.spend_zeroconf_change = a.get_bool("spendzeroconfchange", True)
+        # -maxsigcachesize (MiB, src/script/sigcache.cpp InitSignatureCache): bounded by its 32-byte entries
+        _core.sigcache_set_max_bytes(max(0, a.get_int("maxsigcachesize", 32)) << 20)
         par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free
         cores = os.cpu_count() or 1
         self.state.script_threads = max(1, min(16, cores + par if par <= 0 else par))
