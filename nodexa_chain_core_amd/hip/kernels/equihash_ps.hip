@@ -212,7 +212,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     eqp_clear_counts(cnt2);
     for (uint32_t i = threadIdx.x; i < 256; i += EQP_BLOCK) head[i] = -1;
     uint32_t cv[4] = {0, 0, 0, 0};
-    uint32_t dropped = 0, truncated = 0;
+    uint32_t dropped = 0, truncated = 0, staged_max = 0;
     // every producer wave scans the counts itself and gathers rows pos = thread, thread + NP, ...
     auto stage = [&](uint32_t bk, uint32_t buf) {
         const uint32_t total = eqp_wave_scan(P, cv, my_segc);
@@ -221,6 +221,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
         if (threadIdx.x == 0) {
             nstaged[buf] = n;
             dropped += total - n;
+            staged_max = max(staged_max, total);
         }
         if (bk + G < EQ_BUCKETS) eqp_load_counts(p, inst, R - 1, bk + G, cv);
     };
@@ -284,8 +285,11 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
         }
     }
     __syncthreads();
-    if constexpr (R < 9) eqp_flush_counts(p, inst, R, cnt2, dropped);
-    else if (dropped) atomicAdd(&p.stats[inst * EQP_STATS + 8], dropped);
+    // staging overflow (rows of a level-(R-1) bucket beyond EQP_STAGE) and segment overflow (level R
+    // rows beyond a segment) are counted apart
+    if (dropped) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_STAGE], dropped);
+    if (threadIdx.x == 0) atomicMax(&p.stats[inst * EQP_STATS + EQP_STAT_STAGE_MAX], staged_max);
+    if constexpr (R < 9) eqp_flush_counts(p, inst, R, cnt2, 0);
     if (truncated) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_CHAIN], truncated);
 }
 

@@ -95,10 +95,12 @@ struct EquihashDev {
 // row (the global-slot solver's per-row atomics execute at the memory side and bound its
 // rounds: profiles/README r2c). P * C = EQP_SLOTS rows of address space per bucket.
 #define EQP_SLOTS 2048
-#define EQP_STAGE 768      // rows of one bucket staged in LDS (mean 512, sd ~23)
+#define EQP_STAGE 1024     // rows of one bucket staged in LDS (mean 512-560; the 10-bit staged index caps it)
 #define EQP_REF_STRIDE 1024  // refs per bucket: a 10-bit staged index
 #define EQP_STATS 16
-#define EQP_STAT_CHAIN 9   // stats slot: chains cut at EQ_MAX_CHAIN (slots 0-8: rows dropped per level)
+#define EQP_STAT_CHAIN 9   // stats slot: chains cut at EQ_MAX_CHAIN (slots 0-8: segment overflow per level)
+#define EQP_STAT_STAGE 10  // rows beyond EQP_STAGE in a staged bucket (any round)
+#define EQP_STAT_STAGE_MAX 11  // largest bucket seen by a round (diagnostic, not a loss)
 #define EQP_FINAL_GROUPS 1024  // final-round workgroups per instance (it writes no level)
 struct EquihashPsDev {
     const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashDev)

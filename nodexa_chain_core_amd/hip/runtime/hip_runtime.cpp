@@ -483,6 +483,8 @@ PYBIND11_MODULE(_hip, m) {
     m.attr("EQP_REF_STRIDE") = EQP_REF_STRIDE;
     m.attr("EQP_STATS") = EQP_STATS;
     m.attr("EQP_STAT_CHAIN") = EQP_STAT_CHAIN;
+    m.attr("EQP_STAT_STAGE") = EQP_STAT_STAGE;
+    m.attr("EQP_STAT_STAGE_MAX") = EQP_STAT_STAGE_MAX;
     m.def("launch_equihash_ps_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
                                          uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uint32_t groups,
                                          uintptr_t hashes, uintptr_t refs, uintptr_t counts, uintptr_t cands,

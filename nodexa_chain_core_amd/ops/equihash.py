@@ -128,6 +128,7 @@ class EquihashSolver:
             nstat = ni * self.h.EQP_STATS if ps else 0
             self._land_stats = [torch.zeros(nstat + ni, dtype=torch.int32).pin_memory() for _ in range(2)]
             self.fallbacks = 0  # instances re-solved on the host because the device truncated something
+            self.fallback_log: list[dict] = []
             self._stage = [torch.empty(ni * 16, dtype=torch.int64).pin_memory() for _ in range(2)]
         self._pending: list[tuple[list[bytes], torch.Tensor, torch.cuda.Event]] = []
         self._next = 0
@@ -208,12 +209,14 @@ class EquihashSolver:
         for i in range(self.num_inst):
             truncated = int(st[nstat + i]) > self.h.EQ_MAX_CAND
             if nstat:
-                truncated |= bool(st[i * self.h.EQP_STATS:i * self.h.EQP_STATS + self.h.EQP_STAT_CHAIN + 1].any())
+                truncated |= bool(st[i * self.h.EQP_STATS:i * self.h.EQP_STATS + self.h.EQP_STAT_STAGE + 1].any())
             if truncated:
                 # a bucket, chain or candidate cap cut something: the device result may miss a
-                # solution, so this instance is solved again on the golden solver (never seen in
-                # practice; it keeps the solution set exact by construction)
+                # solution, so this instance is solved again on the golden solver (it keeps the
+                # solution set exact by construction)
                 self.fallbacks += 1
+                self.fallback_log.append({"stats": st[i * self.h.EQP_STATS:(i + 1) * self.h.EQP_STATS].tolist()
+                                          if nstat else [], "candidates": int(st[nstat + i])})
                 sols, _ = _core.equihash_solve_cpu(self.params, inputs[i], self.h.EQ_MAX_SOL, 0)
                 out.append([list(x) for x in sols])
                 continue
@@ -241,7 +244,9 @@ class EquihashSolver:
             c = self.counts[: L * self.groups * B].view(L, self.groups, B).to(torch.int32).sum(1).cpu()
             dropped = self.stats_buf[: self.h.EQP_STATS].cpu().tolist()
             return {"rows_per_level": [int(x) for x in c.sum(1)], "max_fill": [int(x) for x in c.max(1).values],
-                    "cap": self.h.EQP_STAGE, "dropped_per_level": dropped[:L], "candidates": int(self.cands[0].item())}
+                    "cap": self.h.EQP_STAGE, "dropped_per_level": dropped[:L],
+                    "stage_dropped": dropped[self.h.EQP_STAT_STAGE], "largest_bucket": dropped[self.h.EQP_STAT_STAGE_MAX],
+                    "candidates": int(self.cands[0].item())}
         nb = self.h.EQ_MAX_BANKS
         per = self.h.EQ_CAP // self.banks
         c = self.counts[: (L + 1) * B * nb].view(L + 1, B, nb)[:, :, :self.banks].cpu()
