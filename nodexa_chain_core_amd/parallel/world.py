@@ -47,10 +47,14 @@ def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | 
     or single-process; `rank` / `world_size` override the environment. `device_index`: the GPU
     of this rank (default: LOCAL_RANK)."""
     global _WORLD
-    if _WORLD is not None:
-        return _WORLD
     rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
     world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else int(world_size)
+    if _WORLD is not None:
+        # a single-process world left by an earlier user of this process (no communicator to
+        # tear down) gives way to a request for a real one; anything else is reused as it is
+        if not (_WORLD.world_size == 1 and world_size > 1 and not dist.is_initialized()):
+            return _WORLD
+        _WORLD = None
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
