@@ -24,8 +24,16 @@
 // refs[level][b][index], so a back-pointer (bucket << 20 | index a << 10 | index b) fits in 32
 // bits and reconstruction (equihash_device.hpp) is the same as for the global-slot solver.
 //
+// Row format (every level L): word 0 = back-pointer (level 0: the leaf index), then the row's
+// bits [20L + 12, 200) big-endian and contiguous — the "payload". Bits [20L, 20L + 12) are the
+// bucket and live in the row's address. So payload bits [0, 8) are the sub-digit a round chains
+// on, bits [8, 28) the next digit, and a row takes 1 + ceil((188 - 20L) / 32)
+// words, padded to 8, 8, 6, 5, 5, 4, 4, 4, 2 for levels 0..8 (eqp_words; 180 bytes per row over
+// the nine levels against 224 for 32 / 16-byte slots). Two same-bucket rows collide into
+// XOR(payload) << 20.
+//
 // Layouts (num_inst = ni):
-//   hashes [2][ni][BUCKETS][EQP_SLOTS][8] u32  (levels alternate between the two buffers)
+//   hashes [2][ni][BUCKETS][EQP_SLOTS][eqp_words(level)] u32  (levels alternate between two buffers)
 //   counts [ni][LEVELS][P][BUCKETS] u8
 //   refs   [ni][LEVELS][BUCKETS][EQP_REF_STRIDE] u32
 // Overflowing segments or staging areas drop rows (counted in p.stats per level), and a chain of
@@ -35,14 +43,39 @@
 // instance with any such count on the golden solver, so the solution set is exact either way.
 #include "equihash_device.hpp"
 
-#define EQP_BLOCK 512
+#ifndef EQP_BLOCK
+#define EQP_BLOCK 512  // threads per workgroup (the launcher's `block`)
+#endif
+#ifndef EQP_MIN_WAVES
+#define EQP_MIN_WAVES 4  // waves per SIMD the round kernels are register-limited for (4: 128 VGPRs)
+#endif
+#ifndef EQP_NP
+#define EQP_NP (EQP_BLOCK / 4)  // producer threads of a round workgroup
+#endif
+#define EQP_PAIR_CAP 256  // pair-list entries per consumer wave (emitted whenever 64 more might not fit)
 
-// Word offset of a row slot of `level` (buffer level & 1): 32-byte slots, 16-byte slots for the
-// packed levels (so a segment's rows stay contiguous).
-NX_DEV size_t eqp_hidx(const EquihashPsDev& p, int level, uint32_t inst, uint32_t bucket, uint32_t grp, uint32_t slot) {
+// Payload words of a level-`level` row: 6, 6, 5, 4, 4, 3, 3, 2, 1.
+constexpr int eqp_payload(int level) { return (188 - 20 * level + 31) / 32; }
+// Words per row slot in global memory: the payload plus the back-pointer, except that a 28-byte
+// row is padded to 32 and a 12-byte one to 16 (measured r3j: 28-byte rows made round 1 slower
+// and 12-byte rows rounds 7-8, while 24- and 20-byte rows made rounds 3-5 faster).
+constexpr int eqp_words(int level) {
+    return eqp_payload(level) == 6 ? 8 : eqp_payload(level) == 2 ? 4 : 1 + eqp_payload(level);
+}
+// LDS words per staged row: a 3-word payload is padded to 4 (one ds_read_b128 per row).
+constexpr int eqp_lds_stride(int level) { return eqp_payload(level) == 3 ? 4 : eqp_payload(level); }
+
+template <int N>
+struct __attribute__((aligned(4))) EqpRow {
+    uint32_t w[N];
+};
+
+// Word offset of a row slot of `level` (buffer level & 1); a segment's rows are contiguous.
+template <int L>
+NX_DEV size_t eqp_hidx(const EquihashPsDev& p, uint32_t inst, uint32_t bucket, uint32_t grp, uint32_t slot) {
     const size_t buf_words = (size_t)p.num_inst * EQ_BUCKETS * EQP_SLOTS * EQ_WORDS;  // one level buffer
     const size_t row = ((size_t)inst * EQ_BUCKETS + bucket) * EQP_SLOTS + grp * p.seg + slot;
-    return (size_t)(level & 1) * buf_words + row * (eq_half_row(level) ? 4 : EQ_WORDS);
+    return (size_t)(L & 1) * buf_words + row * eqp_words(L);
 }
 
 // LDS slot counters, two u16 per word (the counts of one workgroup never reach 2^16).
@@ -92,12 +125,15 @@ extern "C" __global__ __launch_bounds__(EQP_BLOCK) void eqp_gen(EquihashPsDev p)
         for (int half = 0; half < 2; ++half) {
             uint32_t w[8];
             eq_leaf_words(out, half, w);
-            const uint32_t nb = eq_digit<0>(w) >> 8;
+            const uint32_t nb = w[1] >> 20;  // bits [0, 12)
             const uint32_t slot = eqp_take_slot(cnt2, nb);
             if (slot < p.seg) {
-                uint4* dst = (uint4*)(p.hashes + eqp_hidx(p, 0, inst, nb, grp, slot));
-                dst[0] = make_uint4(2 * g + half, w[1], w[2], w[3]);
-                dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+                EqpRow<eqp_words(0)> r;
+                r.w[0] = 2 * g + half;
+#pragma unroll
+                for (int k = 0; k < eqp_words(0) - 1; ++k)
+                    r.w[1 + k] = k < eqp_payload(0) ? (w[k + 1] << 12) | (w[k + 2] >> 20) : 0u;
+                *(EqpRow<eqp_words(0)>*)(p.hashes + eqp_hidx<0>(p, inst, nb, grp, slot)) = r;
             }
         }
     }
@@ -139,19 +175,18 @@ NX_DEV uint32_t eqp_wave_scan(uint32_t P, const uint32_t v[4], uint32_t* segc) {
 }
 
 // Producer threads pt = 0..NP-1 gather the staged rows pos = pt, pt + NP, ... of bucket b of
-// `level` into LDS rows (words K0..7 at stride ST) and copy their back-pointers to
-// refs[level][b][pos]. A row's segment is found by binary search over the prefix segc, so every
-// load is a real row (about 4 per producer lane per bucket, all in flight together).
-template <int K0, int ST, uint32_t NP>
-NX_DEV void eqp_gather_rows(const EquihashPsDev& p, uint32_t inst, int level, uint32_t b, const uint32_t* segc,
+// level L into LDS rows (payload words at stride ST = eqp_lds_stride(L), zero padded) and copy their
+// back-pointers to refs[L][b][pos]. A row's segment is found by binary search over the prefix
+// segc, so every load is a real row (about 4 per producer lane per bucket, all in flight together).
+template <int L, uint32_t NP>
+NX_DEV void eqp_gather_rows(const EquihashPsDev& p, uint32_t inst, uint32_t b, const uint32_t* segc,
                             uint32_t n, uint32_t* rows, uint32_t pt) {
-    constexpr int BATCH = 4;
-    const bool packed = eq_half_row(level);
+    constexpr int BATCH = 4, W = eqp_words(L), PL = eqp_payload(L), ST = eqp_lds_stride(L);
     const uint32_t P = p.groups;
-    uint32_t* refs = p.refs + (((size_t)inst * EQ_LEVELS + level) * EQ_BUCKETS + b) * EQP_REF_STRIDE;
+    uint32_t* refs = p.refs + (((size_t)inst * EQ_LEVELS + L) * EQ_BUCKETS + b) * EQP_REF_STRIDE;
 #pragma unroll 1
     for (uint32_t p0 = pt; p0 < n; p0 += NP * BATCH) {
-        uint4 lo[BATCH], hi[BATCH];
+        EqpRow<W> r[BATCH];
 #pragma unroll
         for (int k = 0; k < BATCH; ++k) {
             const uint32_t pos = p0 + k * NP;
@@ -161,24 +196,17 @@ NX_DEV void eqp_gather_rows(const EquihashPsDev& p, uint32_t inst, int level, ui
                 const uint32_t mid = (a + z) >> 1;
                 if (segc[mid] <= pos) a = mid; else z = mid;
             }
-            const uint4* src = (const uint4*)(p.hashes + eqp_hidx(p, level, inst, b, a, pos - segc[a]));
-            lo[k] = src[0];
-            if (!packed) hi[k] = src[1];
+            r[k] = *(const EqpRow<W>*)(p.hashes + eqp_hidx<L>(p, inst, b, a, pos - segc[a]));
         }
 #pragma unroll
         for (int k = 0; k < BATCH; ++k) {
             const uint32_t pos = p0 + k * NP;
             if (pos >= n) continue;
-            uint32_t w[8];
-            if (packed) {
-                eq_unpack16(lo[k], level == 5 ? b << 16 : 0u, w);
-            } else {
-                w[1] = lo[k].y; w[2] = lo[k].z; w[3] = lo[k].w;
-                w[4] = hi[k].x; w[5] = hi[k].y; w[6] = hi[k].z; w[7] = hi[k].w;
-            }
-            refs[pos] = lo[k].x;
+#ifndef EQP_NO_REFS
+            refs[pos] = r[k].w[0];
+#endif
 #pragma unroll
-            for (int q = K0; q < 8; ++q) rows[pos * ST + (q - K0)] = w[q];
+            for (int q = 0; q < ST; ++q) rows[pos * ST + q] = q < PL ? r[k].w[1 + q] : 0u;
         }
     }
 }
@@ -194,15 +222,15 @@ NX_DEV void eqp_gather_rows(const EquihashPsDev& p, uint32_t inst, int level, ui
 // Two barriers per bucket: after staging (A: rows ready) and after chaining (B: links ready).
 template <int R>
 NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
-    constexpr int K0 = eq_half_row(R - 1) ? 4 : 1;  // first word a level-(R-1) row still needs
-    constexpr int ST = 8 - K0;
-    constexpr uint32_t NP = 128, NC = EQP_BLOCK - NP;  // producer / consumer threads
+    constexpr int ST = eqp_lds_stride(R - 1);  // LDS words per staged level-(R-1) row
+    constexpr uint32_t NP = EQP_NP, NC = EQP_BLOCK - NP;  // producer / consumer threads
     __shared__ uint32_t cnt2[EQ_BUCKETS / 2];
     __shared__ __attribute__((aligned(16))) uint32_t rows[2][EQP_STAGE * ST];
     __shared__ int head[256];
     __shared__ short nxt[EQP_STAGE];
     __shared__ uint32_t segc[NP / 64][256];  // one prefix copy per producer wave (no cross-wave sync)
     __shared__ uint32_t nstaged[2];
+    __shared__ uint32_t pairs[NC / 64][EQP_PAIR_CAP];  // per consumer wave: colliding pairs (i << 10 | j)
     // P = writers per level (the counts layout); the workgroups stride over the buckets by the
     // grid width, which is P for rounds 1..8 (workgroup = writer) and wider for the final round
     const uint32_t inst = blockIdx.y, grp = blockIdx.x, P = p.groups, G = gridDim.x;
@@ -217,7 +245,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     auto stage = [&](uint32_t bk, uint32_t buf) {
         const uint32_t total = eqp_wave_scan(P, cv, my_segc);
         const uint32_t n = min(total, (uint32_t)EQP_STAGE);
-        eqp_gather_rows<K0, ST, NP>(p, inst, R - 1, bk, my_segc, n, rows[buf], threadIdx.x);
+        eqp_gather_rows<R - 1, NP>(p, inst, bk, my_segc, n, rows[buf], threadIdx.x);
         if (threadIdx.x == 0) {
             nstaged[buf] = n;
             dropped += total - n;
@@ -236,7 +264,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
         const uint32_t* rc = rows[cur];
         if (!producer) {
             for (uint32_t i = ct; i < n; i += NC) {
-                const uint32_t sub = eq_digit<R - 1>(rc + i * ST - K0) & 0xFFu;
+                const uint32_t sub = rc[i * ST] >> 24;
                 nxt[i] = (short)atomicExch(&head[sub], (int)i);
             }
         }
@@ -244,44 +272,116 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
         if (producer) {
             for (uint32_t i = threadIdx.x; i < 256; i += NP) head[i] = -1;  // chain building is over
             if (b + G < EQ_BUCKETS) stage(b + G, cur ^ 1);
-        } else {
+        } else if constexpr (R == 9) {  // final round: equal d_8 (chain) and d_9 make a candidate
             for (uint32_t i = ct; i < n; i += NC) {
-                const uint32_t* a = rc + i * ST - K0;
-                if constexpr (R == 9) {  // final round: equal d_8 (chain) and d_9 make a candidate
-                    const uint32_t di = eq_digit<9>(a);
-                    int j = nxt[i], steps = 0;
-                    for (; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
-                        if (di != eq_digit<9>(rc + (uint32_t)j * ST - K0)) continue;
-                        uint32_t* c = p.cands + (size_t)inst * (1 + 2 * EQ_MAX_CAND);
-                        const uint32_t k = atomicAdd(&c[0], 1u);
-                        if (k < EQ_MAX_CAND) {
-                            c[1 + 2 * k] = b * EQP_REF_STRIDE + i;
-                            c[2 + 2 * k] = b * EQP_REF_STRIDE + (uint32_t)j;
-                        }
-                    }
-                    truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
-                    continue;
-                }
+                // a level-8 payload is one word: the low bits of d_8, d_9, zero padding
+                const uint32_t di = rc[i * ST];
                 int j = nxt[i], steps = 0;
                 for (; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
-                    uint32_t x[8];
-                    eq_xor_rows<R>(a, rc + (uint32_t)j * ST - K0, x);
-                    if (eq_zero_from<R>(x)) continue;  // identical remainder: only duplicate indices
-                    const uint32_t nb = eq_digit<R>(x) >> 8;
-                    const uint32_t slot = eqp_take_slot(cnt2, nb);
-                    if (slot < p.seg) {
-                        uint4* dst = (uint4*)(p.hashes + eqp_hidx(p, R, inst, nb, grp, slot));
-                        const uint32_t ref = (b << 20) | (i << 10) | (uint32_t)j;
-                        if constexpr (eq_half_row(R)) {
-                            dst[0] = eq_pack16(ref, x);
-                        } else {
-                            dst[0] = make_uint4(ref, x[1], x[2], x[3]);
-                            dst[1] = make_uint4(x[4], x[5], x[6], x[7]);
-                        }
+                    if (di != rc[(uint32_t)j * ST]) continue;
+                    uint32_t* c = p.cands + (size_t)inst * (1 + 2 * EQ_MAX_CAND);
+                    const uint32_t k = atomicAdd(&c[0], 1u);
+                    if (k < EQ_MAX_CAND) {
+                        c[1 + 2 * k] = b * EQP_REF_STRIDE + i;
+                        c[2 + 2 * k] = b * EQP_REF_STRIDE + (uint32_t)j;
                     }
                 }
-                truncated += j >= 0;
+                truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
             }
+        } else {
+#ifdef EQP_DENSE
+            // Dense emission. Walking a chain per lane leaves most lanes idle after the first link
+            // (chains are short and of uneven length), and every row store then issues from a
+            // nearly empty wave (r3l: 13 store instructions per 64 rows). So each consumer wave
+            // first lists its rows' pairs in LDS (ballot + mbcnt, no atomics), then collides and
+            // stores them with every lane busy, 64 pairs per instruction.
+            constexpr int WO = eqp_words(R), MO = eqp_payload(R);
+            const uint32_t lane = threadIdx.x & 63;
+            uint32_t* plist = pairs[ct >> 6];
+            uint32_t fill = 0;  // wave-uniform
+            auto emit = [&](uint32_t cnt) {
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                for (uint32_t k = lane; k < cnt; k += 64) {
+                    const uint32_t pr = plist[k], i = pr >> 10, j = pr & 1023u;
+                    const uint32_t* ra = rc + i * ST;
+                    const uint32_t* rb = rc + j * ST;
+                    uint32_t x[ST];
+                    uint32_t rest = 0;
+#pragma unroll
+                    for (int q = 0; q < ST; ++q) {
+                        x[q] = ra[q] ^ rb[q];
+                        rest |= q ? x[q] : (x[q] & 0x00FFFFFFu);
+                    }
+                    if (rest == 0) continue;  // identical remainder: only duplicate indices
+                    const uint32_t nb = (x[0] >> 12) & 0xFFFu;
+                    const uint32_t slot = eqp_take_slot(cnt2, nb);
+                    if (slot < p.seg) {
+                        EqpRow<WO> r;
+                        r.w[0] = (b << 20) | pr;
+#pragma unroll
+                        for (int q = 0; q < WO - 1; ++q)
+                            r.w[1 + q] = q < MO ? (x[q] << 20) | (q + 1 < ST ? x[q + 1] >> 12 : 0u) : 0u;
+                        *(EqpRow<WO>*)(p.hashes + eqp_hidx<R>(p, inst, nb, grp, slot)) = r;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            };
+            for (uint32_t i0 = ct - lane; i0 < n; i0 += NC) {  // wave-uniform trip count
+                const uint32_t i = i0 + lane;
+                int j = i < n ? nxt[i] : -1, steps = 0;
+                for (;;) {
+                    const bool act = j >= 0 && steps < EQ_MAX_CHAIN;
+                    const uint64_t m = __ballot(act);
+                    if (m == 0) break;
+                    if (fill + 64 > EQP_PAIR_CAP) {
+                        emit(fill);
+                        fill = 0;
+                    }
+                    if (act) {
+                        const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        plist[fill + at] = (i << 10) | (uint32_t)j;
+                        j = nxt[j];
+                        ++steps;
+                    }
+                    fill += __popcll(m);
+                }
+                truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
+            }
+            emit(fill);
+#else
+            constexpr int WO = eqp_words(R), MO = eqp_payload(R);
+            for (uint32_t i = ct; i < n; i += NC) {
+                const uint32_t* ra = rc + i * ST;
+                int j = nxt[i], steps = 0;
+                for (; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
+                    const uint32_t* rb = rc + (uint32_t)j * ST;
+                    uint32_t x[ST];
+                    uint32_t rest = 0;
+#pragma unroll
+                    for (int q = 0; q < ST; ++q) {
+                        x[q] = ra[q] ^ rb[q];
+                        rest |= q ? x[q] : (x[q] & 0x00FFFFFFu);
+                    }
+                    if (rest == 0) continue;  // identical remainder: only duplicate indices
+                    const uint32_t nb = (x[0] >> 12) & 0xFFFu;
+                    const uint32_t slot = eqp_take_slot(cnt2, nb);
+                    if (slot < p.seg) {
+                        EqpRow<WO> r;
+                        r.w[0] = (b << 20) | (i << 10) | (uint32_t)j;
+#pragma unroll
+                        for (int q = 0; q < WO - 1; ++q)
+                            r.w[1 + q] = q < MO ? (x[q] << 20) | (q + 1 < ST ? x[q + 1] >> 12 : 0u) : 0u;
+#ifndef EQP_NO_STORE
+                        *(EqpRow<WO>*)(p.hashes + eqp_hidx<R>(p, inst, nb, grp, slot)) = r;
+#else
+                        if (r.w[1] == 0x12345678u && r.w[0] == 0x9u) p.stats[15] = r.w[WO - 1];
+#endif
+                    }
+                }
+                truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
+            }
+#endif
         }
     }
     __syncthreads();
@@ -295,7 +395,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
 
 // 2 workgroups of 512 per CU (4 waves per SIMD): at most 128 VGPRs.
 #define EQP_ROUND_KERNEL(R) \
-    extern "C" __global__ __launch_bounds__(EQP_BLOCK, 4) void eqp_round##R(EquihashPsDev p) { eqp_round_impl<R>(p); }
+    extern "C" __global__ __launch_bounds__(EQP_BLOCK, EQP_MIN_WAVES) void eqp_round##R(EquihashPsDev p) { eqp_round_impl<R>(p); }
 EQP_ROUND_KERNEL(1)
 EQP_ROUND_KERNEL(2)
 EQP_ROUND_KERNEL(3)
@@ -305,7 +405,7 @@ EQP_ROUND_KERNEL(6)
 EQP_ROUND_KERNEL(7)
 EQP_ROUND_KERNEL(8)
 
-extern "C" __global__ __launch_bounds__(EQP_BLOCK, 4) void eqp_final(EquihashPsDev p) { eqp_round_impl<9>(p); }
+extern "C" __global__ __launch_bounds__(EQP_BLOCK, EQP_MIN_WAVES) void eqp_final(EquihashPsDev p) { eqp_round_impl<9>(p); }
 
 // Leaf indices of every candidate (shared body: equihash_device.hpp).
 extern "C" __global__ __launch_bounds__(256) void eqp_reconstruct(EquihashPsDev p) {

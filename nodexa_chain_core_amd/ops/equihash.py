@@ -82,7 +82,8 @@ def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | 
 
 class EquihashSolver:
     def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 8,
-                 code_object: str | None = None, engine: str | None = None, groups: int = 64):
+                 code_object: str | None = None, engine: str | None = None, groups: int = 64,
+                 block: int = 512):
         """`code_object`: path of an alternative build of the engine's .hip (tuning sweeps).
         `engine`: "ps" (private slot segments, `groups` workgroups per instance per round) or
         "global" (global slot atomics, `banks` counters per bucket)."""
@@ -91,6 +92,7 @@ class EquihashSolver:
             raise ValueError(f"unknown Equihash engine {self.engine!r}")
         self.banks = int(banks)
         self.groups = int(groups)
+        self.block = int(block)  # ps: threads per workgroup, must match the code object's EQP_BLOCK
         runtime.require_gpu()
         self.h = runtime.hip()
         self.num_inst = int(num_inst)
@@ -164,7 +166,7 @@ class EquihashSolver:
                 self.h.launch_equihash_ps_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
                                                 self.num_inst, self.groups, self.hashes.data_ptr(),
                                                 self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
-                                                self.sols.data_ptr(), self.stats_buf.data_ptr(), s)
+                                                self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block)
             else:
                 self._issue_global(s)
             land = self._landing[self._next]

@@ -21,17 +21,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def variant_object(defines: tuple[str, ...]) -> str | None:
+def variant_object(defines: tuple[str, ...], source: str = "equihash.hip") -> str | None:
     if not defines:
         return None
     from nodexa_chain_core_amd import _build
 
-    src = os.path.join(_build.HIPDIR, "kernels", "equihash.hip")
-    h = hashlib.sha256("|".join(defines).encode())
-    for name in ("equihash.hip", "kernel_params.h"):
+    src = os.path.join(_build.HIPDIR, "kernels", source)
+    h = hashlib.sha256(("|".join(defines) + source).encode())
+    for name in (source, "equihash_device.hpp", "kernel_params.h"):
         with open(os.path.join(_build.HIPDIR, "kernels", name), "rb") as f:
             h.update(f.read())
-    out = os.path.join(ROOT, ".kernel_cache", f"equihash_{h.hexdigest()[:12]}.hsaco")
+    out = os.path.join(ROOT, ".kernel_cache", f"{source.split('.')[0]}_{h.hexdigest()[:12]}.hsaco")
     if not os.path.exists(out):
         os.makedirs(os.path.dirname(out), exist_ok=True)
         _build.hipcc_genco(src, out, defines=list(defines))
@@ -48,9 +48,11 @@ def main() -> int:
     ap.add_argument("--engines", nargs="*", default=["global"], help="global and/or ps[:groups]")
     a = ap.parse_args()
     variants = [tuple(x for x in v.split(",") if x) for v in a.variants]
-    objs = {v: variant_object(v) for v in variants}
+    objs = {v: variant_object(v) for v in variants} if "global" in a.engines else {}
+    ps_objs = {v: variant_object(v, "equihash_ps.hip") for v in variants} if any(
+        e.startswith("ps") for e in a.engines) else {}
     if a.compile_only:
-        print(json.dumps({",".join(v) or "base": o for v, o in objs.items()}))
+        print(json.dumps({",".join(v) or "base": o for v, o in list(objs.items()) + list(ps_objs.items())}))
         return 0
     import torch
 
@@ -60,13 +62,16 @@ def main() -> int:
     for e in a.engines:
         if e == "global":
             cfgs += [(b, v) for v in variants for b in a.banks]
-        else:  # "ps" or "ps:<groups>": the private-slot engine (its own .hip, no variants)
-            cfgs.append((e, ()))
+        else:  # "ps" or "ps:<groups>": the private-slot engine (variants of equihash_ps.hip)
+            cfgs += [(e, v) for v in variants]
 
     def make(c):
         if isinstance(c[0], str):
-            g = int(c[0].split(":")[1]) if ":" in c[0] else 64
-            return EquihashSolver(num_inst=a.inst, device=0, engine="ps", groups=g)
+            f = c[0].split(":")  # ps[:groups[:block]]
+            g = int(f[1]) if len(f) > 1 else 64
+            blk = int(f[2]) if len(f) > 2 else 512
+            return EquihashSolver(num_inst=a.inst, device=0, engine="ps", groups=g, block=blk,
+                                  code_object=ps_objs[c[1]])
         return EquihashSolver(num_inst=a.inst, device=0, engine="global", banks=c[0], code_object=objs[c[1]])
 
     solvers = {c: make(c) for c in cfgs}

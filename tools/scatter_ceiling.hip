@@ -1,0 +1,105 @@
+// Random row scatter ceiling on one MI355X (the Equihash row-emission pattern).
+//
+// Every Wagner round appends ~2M rows per instance to random buckets (equihash_ps.hip). This
+// program prices that store pattern with nothing around it: each group of G lanes writes one
+// run of G * S contiguous bytes (S per lane) at a random run-aligned offset of a 4 GiB buffer.
+// G = 1 is Equihash's one row per lane; G > 1 shows what a write-combined (bucket-major) layout
+// would get for the same bytes. NT = nontemporal stores.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o scatter_ceiling tools/scatter_ceiling.hip && ./scatter_ceiling
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                                           \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int PER = 16;  // rows per lane per launch
+
+template <int S, int G, bool NT>
+__global__ __launch_bounds__(256) void scatter(uint32_t* __restrict__ buf, uint32_t nruns, uint32_t seed) {
+    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t grp = gid / G, lane = gid % G;
+#pragma unroll 1
+    for (int k = 0; k < PER; ++k) {
+        const uint32_t run = mix32(seed ^ (grp * PER + k)) % nruns;
+        uint32_t* dst = buf + ((size_t)run * G * S + (size_t)lane * S) / 4;
+        const uint32_t v = gid ^ k;
+#pragma unroll
+        for (int q = 0; q < S / 16; ++q) {
+            const u32x4 w = {v, v + 1, v + 2, (uint32_t)q};
+            if (NT)
+                __builtin_nontemporal_store(w, (u32x4*)dst + q);
+            else
+                ((u32x4*)dst)[q] = w;
+        }
+        if constexpr (S % 16 == 8) {
+            uint2* d2 = (uint2*)(dst + (S / 16) * 4);
+            *d2 = make_uint2(v, k);
+        }
+        if constexpr (S % 16 == 4) dst[(S / 16) * 4] = v;
+    }
+}
+
+template <int S, int G, bool NT>
+static void run(const char* name, uint32_t* buf, size_t bytes, uint64_t lanes) {
+    const uint32_t nruns = uint32_t(bytes / (size_t(G) * S));
+    const unsigned grid = unsigned(lanes / 256);
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    scatter<S, G, NT><<<grid, 256>>>(buf, nruns, 1);
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+        CHECK(hipEventRecord(a));
+        scatter<S, G, NT><<<grid, 256>>>(buf, nruns, 2 + rep);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        best = ms < best ? ms : best;
+    }
+    const double rows = double(grid) * 256 * PER;
+    std::printf("{\"variant\":\"%s\",\"row_bytes\":%d,\"run_lanes\":%d,\"nt\":%d,\"ms\":%.3f,\"tb_s\":%.3f,"
+                "\"grows_s\":%.2f}\n",
+                name, S, G, int(NT), best, rows * S / best / 1e9, rows / best / 1e6);
+    std::fflush(stdout);
+}
+
+int main() {
+    const size_t bytes = size_t(4) << 30;
+    uint32_t* buf = nullptr;
+    CHECK(hipMalloc(&buf, bytes));
+    CHECK(hipMemset(buf, 0, bytes));
+    const uint64_t lanes = 1ull << 22;  // x PER rows = 64M rows per launch
+    run<16, 1, false>("row16", buf, bytes, lanes);
+    run<20, 1, false>("row20", buf, bytes, lanes);
+    run<24, 1, false>("row24", buf, bytes, lanes);
+    run<32, 1, false>("row32", buf, bytes, lanes);
+    run<64, 1, false>("row64", buf, bytes, lanes);
+    run<16, 1, true>("row16-nt", buf, bytes, lanes);
+    run<32, 1, true>("row32-nt", buf, bytes, lanes);
+    run<32, 2, false>("row32-run64", buf, bytes, lanes);
+    run<32, 4, false>("row32-run128", buf, bytes, lanes);
+    run<16, 8, false>("row16-run128", buf, bytes, lanes);
+    run<32, 8, false>("row32-run256", buf, bytes, lanes);
+    run<16, 4, false>("row16-run64", buf, bytes, lanes);
+    CHECK(hipFree(buf));
+    return 0;
+}
