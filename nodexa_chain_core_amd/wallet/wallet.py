@@ -872,8 +872,12 @@ class Wallet:
             if len(change) != 1:
                 raise WalletError("Transaction does not have a change output")
             old_fee = sum(c[0] for c in coins) - tx.value_out()
-            size = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4 + 2  # room for a longer sig
-            old_rate = old_fee * 1000 // size
+            vsize = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4
+            # the new signatures may come out longer (DER r and s each 32 or 33 bytes): price the
+            # replacement for up to 2 more bytes per input, at a rate above the old one's actual rate,
+            # so its feerate beats the original whatever lengths the new signatures get
+            size = vsize + 2 * len(tx.vin)
+            old_rate = -(-old_fee * 1000 // vsize)
             if total_fee is not None:
                 min_total = old_rate * size // 1000 + st.incremental_relay_fee * size // 1000
                 if total_fee < min_total:
