@@ -5,10 +5,17 @@
 // returning global atomicAdd on its bucket's counter, and its 4096 one-bucket workgroups per
 // round each pay that round trip before their stores. Measured on MI355X (profiles/README r2d):
 // removing the atomics alone changed nothing (the rounds are bound by the scattered row stores,
-// two 16-byte requests per row), so this engine also (1) packs rows into ONE 16-byte store from
-// level 5 on (eq_pack16) and (2) pipelines each workgroup's bucket sequence so that the gathers
-// of the next bucket run beside the collisions of the current one. Device time per 8-solve
-// batch: 5.64 ms against 6.54 ms for the global-slot engine.
+// two 16-byte requests per row), so this engine (1) stores each level's rows at their payload
+// size (below) and (2) pipelines each workgroup's bucket sequence so that the gathers of the next
+// bucket run beside the collisions of the current one.
+//
+// What bounds it (profiles/README r3_equihash): a random row store costs one memory transaction
+// whatever its size (tools/scatter_ceiling.hip: 22-24 G rows/s for 16-64 byte rows, against
+// 145 G/s when 4 lanes write one 128-byte run), and a level's rows go to 4096 buckets from every
+// workgroup, so no store instruction can cover two rows of one line. With stores left out a round
+// takes half its time; the other half is the producers' staging latency, which the workgroup
+// shape sets: 1024 threads with 7 producer waves per workgroup and 32 writers per level cut the
+// 8-solve batch from 5.52 ms (512 threads, 2 producer waves, 64 writers) to 4.37 ms.
 //
 // Here nothing per row is global. A round runs P = p.groups workgroups per instance; workgroup
 // w processes the source buckets b ≡ w (mod P) one after another, and owns, in EVERY bucket of
@@ -44,15 +51,14 @@
 #include "equihash_device.hpp"
 
 #ifndef EQP_BLOCK
-#define EQP_BLOCK 512  // threads per workgroup (the launcher's `block`)
+#define EQP_BLOCK 1024  // threads per workgroup (the launcher's `block`)
 #endif
 #ifndef EQP_MIN_WAVES
 #define EQP_MIN_WAVES 4  // waves per SIMD the round kernels are register-limited for (4: 128 VGPRs)
 #endif
 #ifndef EQP_NP
-#define EQP_NP (EQP_BLOCK / 4)  // producer threads of a round workgroup
+#define EQP_NP 448  // producer threads of a round workgroup (7 of its 16 waves)
 #endif
-#define EQP_PAIR_CAP 256  // pair-list entries per consumer wave (emitted whenever 64 more might not fit)
 
 // Payload words of a level-`level` row: 6, 6, 5, 4, 4, 3, 3, 2, 1.
 constexpr int eqp_payload(int level) { return (188 - 20 * level + 31) / 32; }
@@ -202,9 +208,7 @@ NX_DEV void eqp_gather_rows(const EquihashPsDev& p, uint32_t inst, uint32_t b, c
         for (int k = 0; k < BATCH; ++k) {
             const uint32_t pos = p0 + k * NP;
             if (pos >= n) continue;
-#ifndef EQP_NO_REFS
             refs[pos] = r[k].w[0];
-#endif
 #pragma unroll
             for (int q = 0; q < ST; ++q) rows[pos * ST + q] = q < PL ? r[k].w[1 + q] : 0u;
         }
@@ -214,11 +218,12 @@ NX_DEV void eqp_gather_rows(const EquihashPsDev& p, uint32_t inst, uint32_t b, c
 // Round R (1..8): collide level R-1 on digit R-1 bucket by bucket, write level R. R = 9 is the
 // final round: level-8 rows colliding on d_8 and d_9 (40 bits) become candidates.
 //
-// Producer / consumer split: waves 0-1 stage the NEXT bucket (count scan, row gathers into the
-// other LDS row buffer, back-pointer copies, the counts of the bucket after that) while waves
-// 2..7 chain and collide the current bucket and emit rows. A wave's vmcnt counts its loads and
-// stores together in issue order, so keeping the gathers out of the emitting waves means no load
-// ever waits behind a scattered row store; the gathers' latency hides behind the collisions.
+// Producer / consumer split: the first EQP_NP threads (7 waves) stage the NEXT bucket (count
+// scan, row gathers into the other LDS row buffer, back-pointer copies, the counts of the bucket
+// after that) while the other 9 waves chain and collide the current bucket and emit rows. A wave's
+// vmcnt counts its loads and stores together in issue order, so keeping the gathers out of the
+// emitting waves means no load ever waits behind a scattered row store; the gathers' latency
+// hides behind the collisions.
 // Two barriers per bucket: after staging (A: rows ready) and after chaining (B: links ready).
 template <int R>
 NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
@@ -230,7 +235,6 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     __shared__ short nxt[EQP_STAGE];
     __shared__ uint32_t segc[NP / 64][256];  // one prefix copy per producer wave (no cross-wave sync)
     __shared__ uint32_t nstaged[2];
-    __shared__ uint32_t pairs[NC / 64][EQP_PAIR_CAP];  // per consumer wave: colliding pairs (i << 10 | j)
     // P = writers per level (the counts layout); the workgroups stride over the buckets by the
     // grid width, which is P for rounds 1..8 (workgroup = writer) and wider for the final round
     const uint32_t inst = blockIdx.y, grp = blockIdx.x, P = p.groups, G = gridDim.x;
@@ -289,67 +293,6 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
                 truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
             }
         } else {
-#ifdef EQP_DENSE
-            // Dense emission. Walking a chain per lane leaves most lanes idle after the first link
-            // (chains are short and of uneven length), and every row store then issues from a
-            // nearly empty wave (r3l: 13 store instructions per 64 rows). So each consumer wave
-            // first lists its rows' pairs in LDS (ballot + mbcnt, no atomics), then collides and
-            // stores them with every lane busy, 64 pairs per instruction.
-            constexpr int WO = eqp_words(R), MO = eqp_payload(R);
-            const uint32_t lane = threadIdx.x & 63;
-            uint32_t* plist = pairs[ct >> 6];
-            uint32_t fill = 0;  // wave-uniform
-            auto emit = [&](uint32_t cnt) {
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                for (uint32_t k = lane; k < cnt; k += 64) {
-                    const uint32_t pr = plist[k], i = pr >> 10, j = pr & 1023u;
-                    const uint32_t* ra = rc + i * ST;
-                    const uint32_t* rb = rc + j * ST;
-                    uint32_t x[ST];
-                    uint32_t rest = 0;
-#pragma unroll
-                    for (int q = 0; q < ST; ++q) {
-                        x[q] = ra[q] ^ rb[q];
-                        rest |= q ? x[q] : (x[q] & 0x00FFFFFFu);
-                    }
-                    if (rest == 0) continue;  // identical remainder: only duplicate indices
-                    const uint32_t nb = (x[0] >> 12) & 0xFFFu;
-                    const uint32_t slot = eqp_take_slot(cnt2, nb);
-                    if (slot < p.seg) {
-                        EqpRow<WO> r;
-                        r.w[0] = (b << 20) | pr;
-#pragma unroll
-                        for (int q = 0; q < WO - 1; ++q)
-                            r.w[1 + q] = q < MO ? (x[q] << 20) | (q + 1 < ST ? x[q + 1] >> 12 : 0u) : 0u;
-                        *(EqpRow<WO>*)(p.hashes + eqp_hidx<R>(p, inst, nb, grp, slot)) = r;
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            };
-            for (uint32_t i0 = ct - lane; i0 < n; i0 += NC) {  // wave-uniform trip count
-                const uint32_t i = i0 + lane;
-                int j = i < n ? nxt[i] : -1, steps = 0;
-                for (;;) {
-                    const bool act = j >= 0 && steps < EQ_MAX_CHAIN;
-                    const uint64_t m = __ballot(act);
-                    if (m == 0) break;
-                    if (fill + 64 > EQP_PAIR_CAP) {
-                        emit(fill);
-                        fill = 0;
-                    }
-                    if (act) {
-                        const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        plist[fill + at] = (i << 10) | (uint32_t)j;
-                        j = nxt[j];
-                        ++steps;
-                    }
-                    fill += __popcll(m);
-                }
-                truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
-            }
-            emit(fill);
-#else
             constexpr int WO = eqp_words(R), MO = eqp_payload(R);
             for (uint32_t i = ct; i < n; i += NC) {
                 const uint32_t* ra = rc + i * ST;
@@ -372,16 +315,11 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
 #pragma unroll
                         for (int q = 0; q < WO - 1; ++q)
                             r.w[1 + q] = q < MO ? (x[q] << 20) | (q + 1 < ST ? x[q + 1] >> 12 : 0u) : 0u;
-#ifndef EQP_NO_STORE
                         *(EqpRow<WO>*)(p.hashes + eqp_hidx<R>(p, inst, nb, grp, slot)) = r;
-#else
-                        if (r.w[1] == 0x12345678u && r.w[0] == 0x9u) p.stats[15] = r.w[WO - 1];
-#endif
                     }
                 }
                 truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
             }
-#endif
         }
     }
     __syncthreads();
@@ -393,7 +331,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     if (truncated) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_CHAIN], truncated);
 }
 
-// 2 workgroups of 512 per CU (4 waves per SIMD): at most 128 VGPRs.
+// One 1024-thread workgroup per CU (4 waves per SIMD): at most 128 VGPRs.
 #define EQP_ROUND_KERNEL(R) \
     extern "C" __global__ __launch_bounds__(EQP_BLOCK, EQP_MIN_WAVES) void eqp_round##R(EquihashPsDev p) { eqp_round_impl<R>(p); }
 EQP_ROUND_KERNEL(1)

@@ -520,7 +520,7 @@ PYBIND11_MODULE(_hip, m) {
         ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
     }, py::arg("ks"), py::arg("h0"), py::arg("msgs"), py::arg("input_len"), py::arg("num_inst"), py::arg("groups"),
        py::arg("hashes"), py::arg("refs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
-       py::arg("stream"), py::arg("block") = 512);
+       py::arg("stream"), py::arg("block") = 1024);
     // The 11 kernel launches captured once into a hipGraph (fixed device buffers, so the graph
     // stays valid across batches; only the message words change, in place). Per batch: 3
     // memsets + one hipGraphLaunch instead of 14 stream operations.

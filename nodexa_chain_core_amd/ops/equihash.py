@@ -82,8 +82,8 @@ def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | 
 
 class EquihashSolver:
     def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 8,
-                 code_object: str | None = None, engine: str | None = None, groups: int = 64,
-                 block: int = 512):
+                 code_object: str | None = None, engine: str | None = None, groups: int = 32,
+                 block: int = 1024):
         """`code_object`: path of an alternative build of the engine's .hip (tuning sweeps).
         `engine`: "ps" (private slot segments, `groups` workgroups per instance per round) or
         "global" (global slot atomics, `banks` counters per bucket)."""

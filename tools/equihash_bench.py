@@ -68,8 +68,8 @@ def main() -> int:
     def make(c):
         if isinstance(c[0], str):
             f = c[0].split(":")  # ps[:groups[:block]]
-            g = int(f[1]) if len(f) > 1 else 64
-            blk = int(f[2]) if len(f) > 2 else 512
+            g = int(f[1]) if len(f) > 1 else 32
+            blk = int(f[2]) if len(f) > 2 else 1024
             return EquihashSolver(num_inst=a.inst, device=0, engine="ps", groups=g, block=blk,
                                   code_object=ps_objs[c[1]])
         return EquihashSolver(num_inst=a.inst, device=0, engine="global", banks=c[0], code_object=objs[c[1]])
