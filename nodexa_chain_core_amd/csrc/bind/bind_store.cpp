@@ -1,0 +1,93 @@
+// Bindings for the LevelDB-format store (store/ldb.hpp).
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../store/ldb.hpp"
+
+namespace py = pybind11;
+using namespace nodexa;
+
+void bind_store(py::module_& m) {
+    py::class_<ldb::DB>(m, "LevelDB", "A LevelDB-format store directory (blocks/index, chainstate, ...)")
+        .def(py::init([](const std::string& path, bool create_if_missing, size_t write_buffer_size, int bloom_bits,
+                         size_t max_file_size, size_t block_size, int l0_trigger, uint64_t level1_bytes) {
+                 ldb::Options o;
+                 o.create_if_missing = create_if_missing;
+                 o.write_buffer_size = write_buffer_size;
+                 o.bloom_bits_per_key = bloom_bits;
+                 o.max_file_size = max_file_size;
+                 o.block_size = block_size;
+                 o.l0_compaction_trigger = l0_trigger;
+                 o.level1_bytes = level1_bytes;
+                 return ldb::DB::open(path, o);
+             }),
+             py::arg("path"), py::arg("create_if_missing") = true, py::arg("write_buffer_size") = size_t(4) << 20,
+             py::arg("bloom_bits") = 10, py::arg("max_file_size") = size_t(2) << 20, py::arg("block_size") = 4096,
+             py::arg("l0_trigger") = 4, py::arg("level1_bytes") = uint64_t(10) << 20)
+        .def("get",
+             [](ldb::DB& db, const py::bytes& k) -> py::object {
+                 std::string v;
+                 bool found;
+                 {
+                     const std::string key = k;
+                     py::gil_scoped_release rel;
+                     found = db.get(key, &v);
+                 }
+                 if (!found) return py::none();
+                 return py::bytes(v);
+             })
+        .def("put", [](ldb::DB& db, const py::bytes& k, const py::bytes& v,
+                       bool sync) { db.put(std::string(k), std::string(v), sync); },
+             py::arg("key"), py::arg("value"), py::arg("sync") = false)
+        .def("delete", [](ldb::DB& db, const py::bytes& k, bool sync) { db.del(std::string(k), sync); },
+             py::arg("key"), py::arg("sync") = false)
+        .def("write",
+             [](ldb::DB& db, const py::list& ops, bool sync) {
+                 // ops: [(key, value)] puts and [(key, None)] deletes, applied in order as one batch
+                 ldb::WriteBatch b;
+                 for (const py::handle& h : ops) {
+                     py::tuple t = py::reinterpret_borrow<py::tuple>(h);
+                     if (t[1].is_none()) b.del(std::string(py::bytes(t[0])));
+                     else b.put(std::string(py::bytes(t[0])), std::string(py::bytes(t[1])));
+                 }
+                 py::gil_scoped_release rel;
+                 db.write(b, sync);
+             },
+             py::arg("ops"), py::arg("sync") = false)
+        .def("items",
+             [](ldb::DB& db, const py::bytes& start, const py::bytes& end) {
+                 std::vector<std::pair<std::string, std::string>> out;
+                 {
+                     const std::string s = start, e = end;
+                     py::gil_scoped_release rel;
+                     db.scan(s, e, [&](const std::string& k, const std::string& v) {
+                         out.emplace_back(k, v);
+                         return true;
+                     });
+                 }
+                 py::list l;
+                 for (auto& kv : out) l.append(py::make_tuple(py::bytes(kv.first), py::bytes(kv.second)));
+                 return l;
+             },
+             py::arg("start") = py::bytes(""), py::arg("end") = py::bytes(""),
+             "live (key, value) pairs with start <= key < end (empty end: unbounded), in key order")
+        .def("compact", &ldb::DB::compact_all, py::call_guard<py::gil_scoped_release>())
+        .def("flush", &ldb::DB::flush_memtable, py::call_guard<py::gil_scoped_release>())
+        .def("files_per_level", &ldb::DB::files_per_level)
+        .def_property_readonly("last_sequence", &ldb::DB::last_sequence)
+        .def_property_readonly("disk_bytes", &ldb::DB::disk_bytes)
+        .def("close", &ldb::DB::close);
+    m.def("ldb_destroy", &ldb::destroy);
+    m.def("ldb_crc32c", [](const py::bytes& b) {
+        const std::string s = b;
+        return ldb::crc32c(s.data(), s.size());
+    });
+    m.def("ldb_bloom_hash", [](const py::bytes& b) { return ldb::bloom_hash(std::string(b)); });
+    m.def("snappy_uncompress", [](const py::bytes& b) -> py::object {
+        const std::string s = b;
+        std::string out;
+        if (!ldb::snappy_uncompress(s.data(), s.size(), &out)) return py::none();
+        return py::bytes(out);
+    });
+}

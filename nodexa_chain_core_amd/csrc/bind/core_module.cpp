@@ -30,6 +30,7 @@ void bind_extra(py::module_& m);  // bind_extra.cpp: chain, X16R, Equihash
 void bind_script(py::module_& m);  // bind_script.cpp: secp256k1, script interpreter
 void bind_assets(py::module_& m);  // bind_assets.cpp: asset layer
 void bind_fees(py::module_& m);    // bind_fees.cpp: fee estimator
+void bind_store(py::module_& m);   // bind_store.cpp: LevelDB-format store
 
 PYBIND11_MODULE(_core, m) {
     m.doc() = "nodexa native CPU core: crypto, ethash/KawPow golden model, Equihash, consensus";
@@ -173,4 +174,5 @@ PYBIND11_MODULE(_core, m) {
     bind_extra(m);
     bind_script(m);
     bind_fees(m);
+    bind_store(m);
 }
