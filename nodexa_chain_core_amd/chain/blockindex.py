@@ -1,11 +1,12 @@
-"""Persistent block index: blocks/index.log.
+"""Persistent block index: blocks/index/ (BlockTreeDB, the default) or blocks/index.log.
 
 Role of the reference's CBlockTreeDB (src/txdb.h:115, LevelDB `blocks/index/`): on
 start-up the node rebuilds its block index from compact per-block records instead of
-re-reading every block in the blk files (what `-reindex` does). LevelDB is not part
-of this engine, so the store is an append-only log (one record per stored block), which
-is also how the index is written: blocks are only ever added; invalidation state is
-recomputed by the header chain.
+re-reading every block in the blk files (what `-reindex` does). `BlockTreeDB` keeps those
+records in the reference's own LevelDB layout (csrc/store/ldb.cpp + chaindb.cpp), so the
+two implementations can open each other's datadirs. `BlockIndexLog` is the earlier
+append-only log of this engine (one record per stored block), kept for datadirs that use
+it (-dbformat=journal).
 
 Record: u32 payload length | payload | first 4 bytes of SHA256d(payload), where payload =
 i32 file, u32 data offset, u32 size, u32 nTx, then the serialized block header. A torn
@@ -53,7 +54,7 @@ class BlockIndexLog:
                 f.truncate(off)
         return out
 
-    def append(self, header_bytes: bytes, pos, n_tx: int) -> None:
+    def append(self, header_bytes: bytes, pos, n_tx: int, **_) -> None:
         payload = _POS.pack(pos.file, pos.offset, pos.size, n_tx) + header_bytes
         if self._f is None:
             self._f = open(self.path, "ab")
@@ -61,11 +62,11 @@ class BlockIndexLog:
         self._f.flush()
 
     def rewrite(self, records) -> None:
-        """Replace the log (after a full -reindex scan): records of (header bytes, pos, n_tx)."""
+        """Replace the log (after a full -reindex scan): records of (header bytes, pos, n_tx, ...)."""
         self.close()
         tmp = self.path + ".new"
         with open(tmp, "wb") as f:
-            for hb, pos, ntx in records:
+            for hb, pos, ntx, *_ in records:
                 payload = _POS.pack(pos.file, pos.offset, pos.size, ntx) + hb
                 f.write(_LEN.pack(len(payload)) + payload + _core.sha256d(payload)[:4])
             f.flush()
@@ -82,6 +83,132 @@ class BlockIndexLog:
             self.sync()
             self._f.close()
             self._f = None
+
+
+BLOCK_VALID_TRANSACTIONS, BLOCK_VALID_SCRIPTS, BLOCK_VALID_MASK = 3, 5, 7
+BLOCK_HAVE_DATA, BLOCK_HAVE_UNDO = 8, 16
+BLOCK_FAILED_VALID, BLOCK_FAILED_CHILD = 32, 64
+_I32 = struct.Struct("<i")
+
+
+class BlockTreeDB:
+    """blocks/index/ in the reference's LevelDB layout (CBlockTreeDB, src/txdb.cpp:23-38, 180-260).
+
+    One 'b' record (CDiskBlockIndex: height, status, nTx, file / data / undo positions, header)
+    per stored block, 'f' + i32 CBlockFileInfo per blk file, 'l' the last blk file, 'R' while a
+    reindex runs, 'F' + name for flags; values XOR-ed with the store's obfuscation key. A datadir
+    written by the reference loads from these records without -reindex, and one written here
+    opens in the reference. Records are written unsynced as blocks arrive (they sit in the store's
+    write-ahead log) and made durable by `sync()` at each chain-state flush, as the reference's
+    FlushStateToDisk does with WriteBatchSync.
+    """
+
+    def __init__(self, path: str, kawpow_activation_time: int):
+        self.path = path
+        self.act = kawpow_activation_time
+        self.db = _core.LevelDB(path, write_buffer_size=8 << 20)
+        self.obf = _core.chaindb_obfuscation_key(self.db, True)
+        self.files: dict[int, list[int]] = {}  # blocks, size, undo size, height first/last, time first/last
+        self.entries: dict[bytes, list] = {}    # hash -> [height, status, ntx, file, data_pos, undo_pos, header]
+        for k, v in self.db.items(b"f", b"g"):
+            if len(k) == 5:
+                fi = _core.decode_file_info(self._x(v))
+                if fi is not None:
+                    self.files[_I32.unpack(k[1:])[0]] = list(fi)
+        v = self.db.get(b"l")
+        self.last_file = _I32.unpack(self._x(v))[0] if v is not None and len(v) == 4 else 0
+
+    def _x(self, v: bytes) -> bytes:
+        return _core.chaindb_xor(v, self.obf)
+
+    def load(self) -> list[tuple]:
+        """Every 'b' record as (hash, height, status, ntx, file, data_pos, undo_pos, header bytes),
+        in height order (parents first)."""
+        recs, bad = _core.load_block_index_ldb(self.db, self.obf, self.act)
+        if bad:
+            raise IOError(f"{bad} unreadable block index record(s) in {self.path}")
+        recs.sort(key=lambda r: r[1])
+        for h, height, status, ntx, fi, dpos, upos, hb in recs:
+            self.entries[h] = [height, status, ntx, fi, dpos, upos, hb]
+        return recs
+
+    def _index_op(self, h: bytes) -> tuple[bytes, bytes]:
+        height, status, ntx, fi, dpos, upos, hb = self.entries[h]
+        return b"b" + h, self._x(_core.encode_disk_index(height, status, ntx, fi, dpos, upos, hb, self.act))
+
+    def _file_op(self, fi: int) -> tuple[bytes, bytes]:
+        return b"f" + _I32.pack(fi), self._x(_core.encode_file_info(*self.files[fi]))
+
+    def append(self, header_bytes: bytes, pos, n_tx: int, height: int = 0, block_hash: bytes = b"",
+               time: int = 0) -> None:
+        """A block's data was stored at `pos` (BLOCK_HAVE_DATA, transactions valid)."""
+        old = self.entries.get(block_hash)
+        status = BLOCK_HAVE_DATA | max(BLOCK_VALID_TRANSACTIONS, old[1] & BLOCK_VALID_MASK if old else 0)
+        upos = 0
+        if old is not None and old[1] & BLOCK_HAVE_UNDO:
+            status |= BLOCK_HAVE_UNDO
+            upos = old[5]
+        self.entries[block_hash] = [height, status, n_tx, pos.file, pos.offset, upos, header_bytes]
+        f = self.files.get(pos.file)
+        if f is None or f[0] == 0:
+            f = self.files[pos.file] = [0, 0, f[2] if f else 0, height, height, time, time]
+        f[0] += 1
+        f[1] = max(f[1], pos.offset + pos.size)
+        f[3], f[4] = min(f[3], height), max(f[4], height)
+        f[5], f[6] = min(f[5], time), max(f[6], time)
+        self.last_file = max(self.last_file, pos.file)
+        self.db.write([self._index_op(block_hash), self._file_op(pos.file), (b"l", self._x(_I32.pack(self.last_file)))])
+
+    def set_undo(self, block_hash: bytes, file: int, undo_pos: int, undo_size: int) -> None:
+        """The block was connected and its undo record written at rev`file`:`undo_pos`."""
+        e = self.entries.get(block_hash)
+        if e is None:
+            return
+        e[1] = (e[1] & ~BLOCK_VALID_MASK) | BLOCK_VALID_SCRIPTS | BLOCK_HAVE_UNDO
+        e[3], e[5] = file, undo_pos
+        f = self.files.setdefault(file, [0, 0, 0, 0, 0, 0, 0])
+        f[2] = max(f[2], undo_pos + undo_size + 32)
+        self.db.write([self._index_op(block_hash), self._file_op(file)])
+
+    def set_failed(self, block_hash: bytes, failed: bool) -> None:
+        e = self.entries.get(block_hash)
+        if e is None:
+            return
+        e[1] = (e[1] | BLOCK_FAILED_VALID) if failed else (e[1] & ~(BLOCK_FAILED_VALID | BLOCK_FAILED_CHILD))
+        self.db.write([self._index_op(block_hash)])
+
+    def rewrite(self, records) -> None:
+        """After a full -reindex scan: records of (header bytes, pos, n_tx, height, hash, time)."""
+        ops = [(k, None) for k, _ in self.db.items(b"b", b"c")] + [(k, None) for k, _ in self.db.items(b"f", b"g")]
+        self.db.write(ops)
+        self.entries.clear()
+        self.files.clear()
+        self.last_file = 0
+        for hb, pos, ntx, height, h, t in records:
+            self.append(hb, pos, ntx, height=height, block_hash=h, time=t)
+        self.sync()
+
+    def reindexing(self) -> bool:
+        return self.db.get(b"R") is not None
+
+    def set_reindexing(self, on: bool) -> None:
+        self.db.write([(b"R", self._x(b"1") if on else None)], sync=True)
+
+    def flag(self, name: str) -> bool | None:
+        v = self.db.get(b"F" + bytes([len(name)]) + name.encode())
+        return None if v is None else self._x(v) == b"1"
+
+    def set_flag(self, name: str, value: bool) -> None:
+        self.db.write([(b"F" + bytes([len(name)]) + name.encode(), self._x(b"1" if value else b"0"))], sync=True)
+
+    def sync(self) -> None:
+        self.db.write([(b"l", self._x(_I32.pack(self.last_file)))], sync=True)
+
+    def close(self) -> None:
+        if self.db is not None:
+            self.sync()
+            self.db.close()
+            self.db = None
 
 
 def scan_blk_tail(blocks_dir: str, magic: bytes, file: int, offset: int):

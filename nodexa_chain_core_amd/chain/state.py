@@ -17,14 +17,17 @@ result is only trusted where it cannot differ from the reference: any input whos
 batch rejects is re-run on the host, and a block whose deferred run fails is re-connected with
 host checks (`_connect_one`).
 
-The UTXO set persists as chainstate/coins.dat (a checksummed snapshot) plus chainstate/coins.log
-(no LevelDB in this environment: SURVEY S6). A flush — every `flush_interval` connected blocks and
-at shutdown — appends one fsynced journal record with only the outputs added or spent since the
-previous flush (CCoinsViewDB::BatchWrite's change set, src/txdb.cpp:91-), so its cost follows the
-blocks connected, not the size of the UTXO set; the journal is folded into a new snapshot once it
-outgrows it. On start-up the snapshot is loaded, newer complete journal records are replayed (a
-torn tail is cut), blocks stored past that point are reconnected (ReplayBlocks-lite), and a state
-whose best block is unknown is rebuilt from genesis.
+Storage (-dbformat, `detect_db_format`): by default the block index and the UTXO set live in
+LevelDB-format stores with the reference's keys — blocks/index/ (BlockTreeDB: 'b' CDiskBlockIndex
+records, 'f' file infos, 'l', 'R') and chainstate/ (CCoinsViewDB: 'C' coins, 'B' best block),
+values obfuscated as CDBWrapper does (csrc/store/) — so a reference datadir opens here without
+-reindex and ours opens in the reference. A flush — every `flush_interval` connected blocks and at
+shutdown — writes only the outputs added or spent since the previous flush plus 'B' as one synced
+batch (CCoinsViewDB::BatchWrite, src/txdb.cpp:91-), so its cost follows the blocks connected, not
+the size of the UTXO set. The older "journal" layout (chainstate/coins.dat snapshot + coins.log
+journal, blocks/index.log) is still read and written for datadirs that hold it. On start-up
+blocks stored past the UTXO set's best block are reconnected (ReplayBlocks-lite), and a state
+whose best block is unknown, or whose last flush did not complete, is rebuilt from genesis.
 """
 from __future__ import annotations
 
@@ -38,7 +41,7 @@ from dataclasses import dataclass, field
 from .. import core
 from ..utils import log, sync
 from . import policy
-from .blockindex import BlockIndexLog, scan_blk_tail
+from .blockindex import BLOCK_FAILED_VALID, BLOCK_HAVE_DATA, BLOCK_HAVE_UNDO, BlockIndexLog, BlockTreeDB, scan_blk_tail
 from .undo import UndoStore
 from .versionbits import VersionBits
 
@@ -79,6 +82,34 @@ class ValidationInterface:
     def disconnect_tip(self, block, index, undo: bytes) -> None: ...
 
     def new_asset_message(self, message) -> None: ...
+
+
+DB_FORMATS = ("leveldb", "journal")
+
+
+def detect_db_format(datadir: str | None, requested: str | None = None) -> str:
+    """Storage layout of a datadir (-dbformat):
+
+    "leveldb"  blocks/index/ and chainstate/ as LevelDB-format stores in the reference's key
+               layout (BlockTreeDB, CCoinsViewDB): reference datadirs open without -reindex and
+               ours open in the reference. The default for new datadirs.
+    "journal"  blocks/index.log plus chainstate/coins.dat + coins.log (this engine's earlier
+               layout); existing datadirs of that layout keep it unless another is requested.
+    Requesting a format a datadir does not hold migrates it: the block index is rebuilt from the
+    blk files (-reindex) and the UTXO set replayed from the stored blocks.
+    """
+    if requested:
+        if requested not in DB_FORMATS:
+            raise ValueError(f"-dbformat must be one of {', '.join(DB_FORMATS)}")
+        return requested
+    if datadir is None:
+        return "memory"
+    if os.path.exists(os.path.join(datadir, "blocks", "index", "CURRENT")):
+        return "leveldb"
+    if any(os.path.exists(os.path.join(datadir, *p)) for p in (("blocks", "index.log"), ("chainstate", "coins.dat"),
+                                                               ("chainstate", "coins.log"))):
+        return "journal"
+    return "leveldb"
 
 
 def make_params(network: str, kawpow_activation_time: int | None = None,
@@ -152,7 +183,7 @@ def _read_compact_size(b: bytes, off: int) -> tuple[int, int]:
 
 class ChainState:
     def __init__(self, params, datadir: str | None = None, strict_height: bool = False, reindex: bool = False,
-                 indexes: dict | None = None):
+                 indexes: dict | None = None, db_format: str | None = None):
         self.params = params
         self.chain = _core.HeaderChain(params)
         self.chain.strict_kawpow_height = strict_height
@@ -205,11 +236,18 @@ class ChainState:
         self.journal_compact_bytes = 64 << 20  # fold coins.log into coins.dat past this size (or the snapshot's)
         self._since_flush = 0
         self.sig_stats = {"gpu_batches": 0, "gpu_sigs": 0, "host_rechecks": 0}
+        self.db_format = detect_db_format(datadir, db_format)
+        self.coins_db = None
+        self._coins_obf = b""
         if datadir is not None:
             bdir = os.path.join(datadir, "blocks")
             os.makedirs(bdir, exist_ok=True)
             self.store = _core.BlockStore(bdir, params.message_start, params.kawpow_activation_time)
-            self.index_log = BlockIndexLog(os.path.join(bdir, "index.log"))
+            if self.db_format == "leveldb":
+                self.index_log = BlockTreeDB(os.path.join(bdir, "index"), params.kawpow_activation_time)
+                reindex = reindex or self.index_log.reindexing()  # an interrupted -reindex resumes
+            else:
+                self.index_log = BlockIndexLog(os.path.join(bdir, "index.log"))
             if reindex or not self._load_index(bdir):
                 self._load_block_files()
         self.versionbits = VersionBits(self.chain, params.network_id)
@@ -218,15 +256,30 @@ class ChainState:
         if self.store is not None and gh not in self.block_pos:
             self.block_pos[gh] = self.store.write(params.genesis)
             self.index_log.append(params.genesis.header.serialize(params.kawpow_activation_time),
-                                  self.block_pos[gh], len(params.genesis.vtx))
+                                  self.block_pos[gh], len(params.genesis.vtx), height=0, block_hash=gh,
+                                  time=params.genesis.header.time)
         bdir = os.path.join(datadir, "blocks") if datadir else None
         self.undo = UndoStore(bdir, bytes(params.message_start))
+        for h, fi, upos in getattr(self, "_undo_adopt", ()):  # undo records a reference index located
+            if h not in self.undo.pos and not self.undo.adopt(h, fi, upos):
+                log.log_printf(f"undo record of {_core.u256_hex(h)} not found at rev{fi:05d}:{upos}")
+        self._undo_adopt = []
+        if self.db_format == "leveldb" and self.index_log is not None:
+            # records rebuilt by a reindex carry no undo position yet: take them from the undo store
+            for h, e in list(self.index_log.entries.items()):
+                u = self.undo.pos.get(h)
+                if u is not None and not e[1] & BLOCK_HAVE_UNDO and u[0] == e[3]:
+                    self.index_log.set_undo(h, u[0], u[1], u[2])
         self.asset_undo = UndoStore(bdir, bytes(params.message_start), prefix="aun")
         self.coins_path = os.path.join(datadir, "chainstate", "coins.dat") if datadir else None
         self.coins_log = os.path.join(datadir, "chainstate", "coins.log") if datadir else None
         self.assets_path = os.path.join(datadir, "chainstate", "assets.dat") if datadir else None
         self.indexes_path = os.path.join(datadir, "chainstate", "indexes.dat") if datadir else None
         self.index_flags = dict(indexes or {})  # txindex / addressindex / spentindex / timestampindex
+        if self.db_format == "leveldb" and self.index_log is not None:
+            for k, v in self.index_flags.items():  # WriteFlag (src/init.cpp), read back by the reference
+                if self.index_log.flag(k) != bool(v):
+                    self.index_log.set_flag(k, bool(v))
         self.coins = _core.CoinsView()
         self.assets = _core.AssetsState()
         self.indexes = _core.ChainIndexes(**self.index_flags)
@@ -237,22 +290,26 @@ class ChainState:
         """-reindex: rebuild the index from every record of the blk files, then rewrite
         blocks/index.log from the result."""
         act = self.params.kawpow_activation_time
+        if self.db_format == "leveldb":
+            self.index_log.set_reindexing(True)  # DB_REINDEX_FLAG: an interrupted reindex restarts
         n, records = 0, []
         for pos, raw in self.store.scan():
             blk = _core.Block.deserialize(raw, act)
             h = self.chain.block_hash(blk.header)
             if h == self.chain.genesis().hash:
                 self.block_pos[h] = pos
-                records.append((blk.header.serialize(act), pos, len(blk.vtx)))
+                records.append((blk.header.serialize(act), pos, len(blk.vtx), 0, h, blk.header.time))
                 continue
             # blocks in our files were fully validated before they were written
             r = self.chain.accept_header(blk.header, 2**62, False)
             if r.ok:
                 self.block_pos[h] = pos
                 self.ntx[h] = len(blk.vtx)
-                records.append((blk.header.serialize(act), pos, len(blk.vtx)))
+                records.append((blk.header.serialize(act), pos, len(blk.vtx), r.index.height, h, blk.header.time))
                 n += 1
         self.index_log.rewrite(records)
+        if self.db_format == "leveldb":
+            self.index_log.set_reindexing(False)
         if n:
             log.log_printf(f"reindexed {n} blocks from block files, tip height {self.chain.height()}")
 
@@ -261,6 +318,8 @@ class ChainState:
         then any blocks written after the last good record are recovered from the blk-file
         tail. False = no usable index (caller reindexes)."""
         act = self.params.kawpow_activation_time
+        if self.db_format == "leveldb":
+            return self._load_block_tree(bdir)
         recs = self.index_log.load()
         if not recs:
             return not os.path.exists(os.path.join(bdir, "blk00000.dat"))
@@ -296,12 +355,87 @@ class ChainState:
                        f"tip height {self.chain.height()}")
         return True
 
+    def _load_block_tree(self, bdir: str) -> bool:
+        """LoadBlockIndexGuts from blocks/index/ in the reference's LevelDB layout
+        (src/txdb.cpp:230-260, validation.cpp LoadBlockIndexDB): every 'b' record's header is
+        accepted in height order in one batch (header-only entries included), stored blocks and
+        their undo records are located from the records, failed blocks are marked again, and
+        blocks written to the blk files after the last record are recovered from the file tail.
+        False = no usable index (the caller reindexes)."""
+        act = self.params.kawpow_activation_time
+        try:
+            recs = self.index_log.load()
+        except IOError as e:
+            log.log_printf(f"{e}; reindexing")
+            return False
+        if not recs:
+            return not os.path.exists(os.path.join(bdir, "blk00000.dat"))
+        hdrs = [_core.BlockHeader.deserialize(r[7], act) for r in recs]
+        res = self.chain.accept_headers(hdrs, 2**62, False)
+        if len(res) != len(recs) or not all(r.ok for r in res):
+            log.log_printf("block index records inconsistent with the header rules; reindexing")
+            self.chain = _core.HeaderChain(self.params)
+            self.chain.strict_kawpow_height = self.strict_height
+            self.block_pos.clear()
+            self.ntx.clear()
+            return False
+        fds: dict[int, int] = {}
+        last, failed, n_data = (0, 0, 0), [], 0
+        self._undo_adopt = []
+        try:
+            for (h, height, status, ntx, fi, dpos, upos, hb), r in zip(recs, res):
+                if status & BLOCK_HAVE_DATA:
+                    fd = fds.get(fi)
+                    if fd is None:
+                        fd = fds[fi] = os.open(self.store.path(fi), os.O_RDONLY)
+                    frame = os.pread(fd, 8, dpos - 8)
+                    if len(frame) != 8 or frame[:4] != bytes(self.params.message_start):
+                        log.log_printf(f"block {_core.u256_hex(h)} missing at blk{fi:05d}:{dpos}; reindexing")
+                        return False
+                    pos = _core.BlockPos()
+                    pos.file, pos.offset, pos.size = fi, dpos, struct.unpack("<I", frame[4:])[0]
+                    self.block_pos[r.index.hash] = pos
+                    self.ntx[r.index.hash] = ntx
+                    last = max(last, (fi, dpos, pos.size))
+                    n_data += 1
+                if status & BLOCK_HAVE_UNDO:
+                    self._undo_adopt.append((h, fi, upos))
+                if status & BLOCK_FAILED_VALID:
+                    failed.append(h)
+        except OSError as e:
+            log.log_printf(f"cannot read the blk files the block index names ({e}); reindexing")
+            return False
+        finally:
+            for fd in fds.values():
+                os.close(fd)
+        for h in failed:
+            self.chain.invalidate(h)
+        n = 0
+        for fi, fo, raw in scan_blk_tail(bdir, bytes(self.params.message_start), last[0], last[1] + last[2]):
+            blk = _core.Block.deserialize(raw, act)
+            r = self.chain.accept_header(blk.header, 2**62, False)
+            if not r.ok:
+                break
+            pos = _core.BlockPos()
+            pos.file, pos.offset, pos.size = fi, fo, len(raw)
+            self.block_pos[r.index.hash] = pos
+            self.ntx[r.index.hash] = len(blk.vtx)
+            self.index_log.append(blk.header.serialize(act), pos, len(blk.vtx), height=r.index.height,
+                                  block_hash=r.index.hash, time=blk.header.time)
+            n += 1
+        log.log_printf(f"loaded block index (LevelDB): {len(recs)} records, {n_data} with data "
+                       f"(+{n} recovered from blk files), tip height {self.chain.height()}")
+        return True
+
     def close(self) -> None:
         self.flush()
         if self.index_log is not None:
             self.index_log.close()
         self.undo.close()
         self.asset_undo.close()
+        if self.coins_db is not None:
+            self.coins_db.close()
+            self.coins_db = None
 
     # ------------------------------------------------------------------ signals
     def register(self, l: ValidationInterface) -> None:
@@ -691,7 +825,7 @@ class ChainState:
             if self.store is not None:
                 self.block_pos[h] = self.store.write(block)
                 self.index_log.append(block.header.serialize(self.params.kawpow_activation_time), self.block_pos[h],
-                                      len(block.vtx))
+                                      len(block.vtx), height=height, block_hash=h, time=block.header.time)
             else:
                 self.block_pos[h] = None
                 self._mem_blocks[h] = block
@@ -729,7 +863,19 @@ class ChainState:
     def _init_coins(self) -> None:
         """Load the UTXO snapshot and bring it to the best stored chain (ReplayBlocks-lite)."""
         gh = self.chain.genesis().hash
-        loaded = self.coins_path is not None and self.coins.load_with_journal(self.coins_path, self.coins_log)
+        if self.db_format == "leveldb" and self.coins_path is not None:
+            # chainstate/ in the reference's layout (CCoinsViewDB): 'C' coins, 'B' best block
+            self.coins_db = _core.LevelDB(os.path.dirname(self.coins_path), write_buffer_size=32 << 20)
+            self._coins_obf = _core.chaindb_obfuscation_key(self.coins_db, True)
+            r = _core.coins_load_ldb(self.coins, self.coins_db, self._coins_obf)
+            loaded = r["have_best"] and not r["head_blocks"] and not r["bad"]
+            if r["head_blocks"] or r["bad"]:
+                log.log_printf(f"chainstate: {'interrupted flush (head blocks)' if r['head_blocks'] else ''}"
+                               f"{r['bad']} unreadable coin record(s); rebuilding the UTXO set")
+            elif loaded:
+                log.log_printf(f"chainstate: {r['coins']} coins loaded")
+        else:
+            loaded = self.coins_path is not None and self.coins.load_with_journal(self.coins_path, self.coins_log)
         if loaded and self.coins.replayed:
             log.log_printf(f"UTXO journal: {self.coins.replayed} flush record(s) replayed onto the snapshot")
         if loaded:  # the asset state must describe the same block as the UTXO snapshot
@@ -761,7 +907,12 @@ class ChainState:
             self.assets = _core.AssetsState()
             self.indexes = _core.ChainIndexes(**self.index_flags)
             self.indexes.best_block = gh
-            if self.coins_path is not None and (os.path.exists(self.coins_path) or os.path.exists(self.coins_log)):
+            if self.coins_db is not None:
+                # drop the stale set: every coin record, then the fresh (empty) state's 'B'
+                stale = [(k, None) for k, _ in self.coins_db.items(b"C", b"D")]
+                self.coins_db.write(stale + [(b"H", None)])
+                _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True)
+            elif self.coins_path is not None and (os.path.exists(self.coins_path) or os.path.exists(self.coins_log)):
                 self.coins.compact(self.coins_path, self.coins_log)  # a fresh snapshot restarts the journal
         with self.lock:
             self._activate()
@@ -918,7 +1069,14 @@ class ChainState:
         if not ok:
             _core.disconnect_block(block, undo, self.coins, self.assets, aundo)
             return ValidationState.invalid(reason, dos)
-        self.undo.write(idx.hash, idx.prev_hash, undo)
+        bpos = self.block_pos.get(idx.hash)
+        if self.db_format == "leveldb" and bpos is not None:
+            u = self.undo.pos.get(idx.hash)
+            if u is None or u[0] != bpos.file:  # written once, beside the block (WriteUndoDataForBlock)
+                u = self.undo.write(idx.hash, idx.prev_hash, undo, file=bpos.file)
+            self.index_log.set_undo(idx.hash, u[0], u[1], u[2])
+        else:
+            self.undo.write(idx.hash, idx.prev_hash, undo)
         self.indexes.connect(block, height, idx.hash, undo)
         if aundo:
             self.asset_undo.write(idx.hash, idx.prev_hash, aundo)
@@ -956,7 +1114,12 @@ class ChainState:
                 f.flush()
                 os.fsync(f.fileno())
             os.replace(tmp, self.indexes_path)
-        if not os.path.exists(self.coins_path):  # first flush of this datadir: start from a snapshot
+        if self.coins_db is not None:
+            # block index records first (their undo positions must be durable before the coins
+            # that depend on them), then the UTXO change set and 'B' in one synced batch
+            self.index_log.sync()
+            _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True)
+        elif not os.path.exists(self.coins_path):  # first flush of this datadir: start from a snapshot
             self.coins.compact(self.coins_path, self.coins_log)
         else:
             self.coins.append_journal(self.coins_log)  # O(outputs changed since the last flush)

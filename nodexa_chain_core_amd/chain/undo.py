@@ -52,21 +52,47 @@ class UndoStore:
     def _path(self, fi: int) -> str:
         return os.path.join(self.bdir, f"{self.prefix}{fi:05d}.dat")
 
-    def write(self, block_hash: bytes, prev_hash: bytes, undo: bytes) -> None:
+    def write(self, block_hash: bytes, prev_hash: bytes, undo: bytes, file: int | None = None):
+        """Append the record; returns its (file, data offset, size). With `file` (the block's blk
+        file number) it goes to rev`file`, as the reference keeps a block's undo data beside it
+        (CBlockIndex::nFile serves both); otherwise files roll over at MAX_FILE."""
         if self.bdir is None:
             self._mem[block_hash] = undo
-            return
-        path = self._path(self.file)
-        size = os.path.getsize(path) if os.path.exists(path) else 0
-        if size + len(undo) + 40 > MAX_FILE and size > 0:
-            self.file += 1
-            path, size = self._path(self.file), 0
+            return None
+        if file is not None:
+            self.file = max(self.file, file)
+            path = self._path(file)
+            size = os.path.getsize(path) if os.path.exists(path) else 0
+        else:
+            file = self.file
+            path = self._path(file)
+            size = os.path.getsize(path) if os.path.exists(path) else 0
+            if size + len(undo) + 40 > MAX_FILE and size > 0:
+                self.file = file = file + 1
+                path, size = self._path(file), 0
         rec = self.magic + struct.pack("<I", len(undo)) + undo + _sha256d(prev_hash + undo)
         with open(path, "ab") as f:
             f.write(rec)
-        self.pos[block_hash] = (self.file, size + 8, len(undo))
-        self._idx.write(_IDX.pack(block_hash, self.file, size + 8, len(undo)))
+        self.pos[block_hash] = (file, size + 8, len(undo))
+        self._idx.write(_IDX.pack(block_hash, file, size + 8, len(undo)))
         self._idx.flush()
+        return self.pos[block_hash]
+
+    def adopt(self, block_hash: bytes, file: int, offset: int) -> bool:
+        """Register a record another index located (a reference blocks/index 'b' record's
+        nUndoPos); the size comes from the record's framing. False if the framing is wrong."""
+        path = self._path(file)
+        try:
+            with open(path, "rb") as f:
+                f.seek(offset - 8)
+                head = f.read(8)
+        except OSError:
+            return False
+        if len(head) != 8 or head[:4] != self.magic:
+            return False
+        self.pos[block_hash] = (file, offset, struct.unpack("<I", head[4:])[0])
+        self.file = max(self.file, file)
+        return True
 
     def read(self, block_hash: bytes, prev_hash: bytes) -> bytes | None:
         if self.bdir is None:

@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "../store/chaindb.hpp"
 #include "../store/ldb.hpp"
 
 namespace py = pybind11;
@@ -89,5 +90,102 @@ void bind_store(py::module_& m) {
         std::string out;
         if (!ldb::snappy_uncompress(s.data(), s.size(), &out)) return py::none();
         return py::bytes(out);
+    });
+
+    // ---------------- chain databases (store/chaindb.hpp)
+    m.def("chaindb_obfuscation_key",
+          [](ldb::DB& db, bool create) { return py::bytes(chaindb::obfuscation_key(db, create)); });
+    m.def("chaindb_xor", [](const py::bytes& v, const py::bytes& key) {
+        std::string s = v;
+        chaindb::xor_obf(s, std::string(key));
+        return py::bytes(s);
+    });
+    m.def("coins_load_ldb", [](CoinsView& view, ldb::DB& db, const py::bytes& obf) {
+        chaindb::CoinsLoad r;
+        {
+            const std::string k = obf;
+            py::gil_scoped_release rel;
+            r = chaindb::coins_load(view, db, k);
+        }
+        py::dict d;
+        d["have_best"] = r.have_best;
+        d["head_blocks"] = r.head_blocks;
+        d["coins"] = r.coins;
+        d["bad"] = r.bad;
+        return d;
+    });
+    m.def("coins_flush_ldb", [](CoinsView& view, ldb::DB& db, const py::bytes& obf, bool sync) {
+        const std::string k = obf;
+        py::gil_scoped_release rel;
+        return chaindb::coins_flush(view, db, k, sync);
+    });
+    m.def("coin_db_key", [](const py::bytes& txid, u32 n) {
+        const std::string s = txid;
+        if (s.size() != 32) throw std::invalid_argument("expected a 32-byte txid");
+        OutPoint o;
+        o.hash = Uint256::from_bytes(reinterpret_cast<const u8*>(s.data()));
+        o.n = n;
+        return py::bytes(chaindb::coin_key(o));
+    });
+    m.def("coin_db_serialize", [](int64_t value, const py::bytes& spk, u32 height, bool coinbase) {
+        Coin c;
+        c.out.value = value;
+        const std::string s = spk;
+        c.out.script_pubkey.assign(s.begin(), s.end());
+        c.height = height;
+        c.coinbase = coinbase;
+        const Bytes b = serialize_coin_db(c);
+        return py::bytes(reinterpret_cast<const char*>(b.data()), b.size());
+    });
+    m.def("coin_db_deserialize", [](const py::bytes& v) -> py::object {
+        const std::string s = v;
+        Coin c;
+        if (!deserialize_coin_db(reinterpret_cast<const u8*>(s.data()), s.size(), c)) return py::none();
+        return py::make_tuple(c.out.value,
+                              py::bytes(reinterpret_cast<const char*>(c.out.script_pubkey.data()), c.out.script_pubkey.size()),
+                              c.height, c.coinbase);
+    });
+    m.def("encode_disk_index",
+          [](int height, u32 status, u32 ntx, int file, u32 data_pos, u32 undo_pos, const py::bytes& header, u32 act) {
+              chaindb::DiskIndex d;
+              d.height = height;
+              d.status = status;
+              d.ntx = ntx;
+              d.file = file;
+              d.data_pos = data_pos;
+              d.undo_pos = undo_pos;
+              const std::string h = header;
+              d.header.assign(h.begin(), h.end());
+              return py::bytes(chaindb::encode_disk_index(d, act));
+          });
+    m.def("decode_disk_index", [](const py::bytes& v, u32 act) -> py::object {
+        chaindb::DiskIndex d;
+        if (!chaindb::decode_disk_index(std::string(v), act, &d)) return py::none();
+        return py::make_tuple(d.height, d.status, d.ntx, d.file, d.data_pos, d.undo_pos,
+                              py::bytes(reinterpret_cast<const char*>(d.header.data()), d.header.size()));
+    });
+    m.def("load_block_index_ldb", [](ldb::DB& db, const py::bytes& obf, u32 act) {
+        std::vector<chaindb::DiskIndex> v;
+        size_t bad = 0;
+        {
+            const std::string k = obf;
+            py::gil_scoped_release rel;
+            v = chaindb::load_block_index(db, k, act, &bad);
+        }
+        py::list out;
+        for (const auto& d : v)
+            out.append(py::make_tuple(py::bytes(reinterpret_cast<const char*>(d.hash.data), 32), d.height, d.status,
+                                      d.ntx, d.file, d.data_pos, d.undo_pos,
+                                      py::bytes(reinterpret_cast<const char*>(d.header.data()), d.header.size())));
+        return py::make_tuple(out, bad);
+    });
+    m.def("encode_file_info", [](u32 blocks, u32 size, u32 undo_size, u32 hfirst, u32 hlast, u64 tfirst, u64 tlast) {
+        chaindb::FileInfo f{blocks, size, undo_size, hfirst, hlast, tfirst, tlast};
+        return py::bytes(chaindb::encode_file_info(f));
+    });
+    m.def("decode_file_info", [](const py::bytes& v) -> py::object {
+        chaindb::FileInfo f;
+        if (!chaindb::decode_file_info(std::string(v), &f)) return py::none();
+        return py::make_tuple(f.blocks, f.size, f.undo_size, f.height_first, f.height_last, f.time_first, f.time_last);
     });
 }

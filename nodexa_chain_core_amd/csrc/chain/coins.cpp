@@ -402,6 +402,66 @@ Coin read_coin_undo(Reader& r) {
 
 }  // namespace
 
+Bytes serialize_coin_db(const Coin& c) {
+    Writer w;
+    write_varint(w, u64(c.height) * 2 + (c.coinbase ? 1 : 0));
+    write_varint(w, compress_amount(u64(c.out.value)));
+    Bytes comp;
+    if (compress_script(c.out.script_pubkey, comp)) {
+        w.raw(comp);
+    } else {
+        write_varint(w, c.out.script_pubkey.size() + kSpecialScripts);
+        w.raw(c.out.script_pubkey);
+    }
+    return std::move(w.buf);
+}
+
+bool deserialize_coin_db(const u8* p, size_t n, Coin& c) {
+    try {
+        Reader r(p, n);
+        const u64 code = read_varint(r);
+        c.height = u32(code >> 1);
+        c.coinbase = code & 1;
+        c.out.value = Amount(decompress_amount(read_varint(r)));
+        const u64 k = read_varint(r);
+        if (k < kSpecialScripts) {
+            const size_t len = k < 2 ? 20 : 32;
+            const u8* q = r.take(len);
+            c.out.script_pubkey = decompress_script(k, Bytes(q, q + len));
+            if (c.out.script_pubkey.empty()) return false;  // an invalid compressed key
+        } else {
+            const u64 len = k - kSpecialScripts;
+            if (len > kMaxScriptSize) {  // stored unspendable: OP_RETURN, data skipped
+                r.take(size_t(len));
+                c.out.script_pubkey = {0x6a};
+            } else {
+                const u8* q = r.take(size_t(len));
+                c.out.script_pubkey.assign(q, q + len);
+            }
+        }
+        return true;
+    } catch (const std::exception&) {
+        return false;
+    }
+}
+
+void append_varint(Bytes& out, u64 n) {
+    Writer w;
+    write_varint(w, n);
+    out.insert(out.end(), w.buf.begin(), w.buf.end());
+}
+
+bool parse_varint(const u8*& p, const u8* end, u64& n) {
+    try {
+        Reader r(p, size_t(end - p));
+        n = read_varint(r);
+        p = end - r.remaining();
+        return true;
+    } catch (const std::exception&) {
+        return false;
+    }
+}
+
 u64 compress_amount(u64 n) {
     if (n == 0) return 0;
     int e = 0;

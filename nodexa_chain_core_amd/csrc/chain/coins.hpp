@@ -89,6 +89,19 @@ public:
     void for_each(F&& f) const {
         for (auto& kv : map_) f(kv.first, kv.second);
     }
+    // The change set since the last flush: f(outpoint, coin or nullptr when spent).
+    template <class F>
+    void for_each_dirty(F&& f) const {
+        for (auto& kv : dirty_) f(kv.first, kv.second ? find(kv.first) : nullptr);
+    }
+    void clear_dirty() { dirty_.clear(); }
+    void reset() {
+        map_.clear();
+        dirty_.clear();
+        best_block = Uint256();
+    }
+    void insert_clean(const OutPoint& o, Coin c) { map_[o] = std::move(c); }  // loaded state, not a change
+    void reserve(size_t n) { map_.reserve(n); }
 
 private:
     std::unordered_map<OutPoint, Coin, OutPointHasher, OutPointEq> map_;
@@ -107,6 +120,12 @@ BlockUndo deserialize_block_undo(const Bytes& b);
 // CompressAmount / DecompressAmount and the script compressor (src/compressor.cpp)
 u64 compress_amount(u64 n);
 u64 decompress_amount(u64 x);
+// The chainstate database's coin record (Coin::Serialize, src/coins.h:58-72: VARINT(height*2 +
+// coinbase) then CTxOutCompressor) and the serialize.h VARINT (MSB base-128, +1 per continuation).
+Bytes serialize_coin_db(const Coin& c);
+bool deserialize_coin_db(const u8* p, size_t n, Coin& c);
+void append_varint(Bytes& out, u64 n);
+bool parse_varint(const u8*& p, const u8* end, u64& n);
 
 struct ConnectOptions {
     u32 script_flags = kBlockScriptFlags;

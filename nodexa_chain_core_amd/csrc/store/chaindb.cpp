@@ -1,0 +1,248 @@
+// Chain databases in the reference's key layout: see chaindb.hpp.
+#include "chaindb.hpp"
+
+#include <random>
+#include <stdexcept>
+
+#include "../chain/primitives.hpp"
+
+namespace nodexa {
+namespace chaindb {
+
+namespace {
+
+const std::string kObfKey = std::string("\x0e\x00obfuscate_key", 15);  // CompactSize(14) + "\0obfuscate_key"
+
+std::string bytes_str(const Bytes& b) { return std::string(reinterpret_cast<const char*>(b.data()), b.size()); }
+
+}  // namespace
+
+std::string obfuscation_key(ldb::DB& db, bool create) {
+    std::string v;
+    if (db.get(kObfKey, &v)) {
+        // a serialized vector<unsigned char>: CompactSize(8) + 8 bytes (written before any key
+        // was in force, so not itself obfuscated)
+        if (v.size() == 9 && uint8_t(v[0]) == 8) return v.substr(1);
+        throw std::runtime_error("chaindb: malformed obfuscation key record");
+    }
+    bool empty = true;
+    db.scan(std::string(), std::string(), [&](const std::string&, const std::string&) {
+        empty = false;
+        return false;
+    });
+    if (!create || !empty) return std::string(8, '\0');
+    std::random_device rd;
+    std::string key(8, '\0');
+    for (char& c : key) c = char(rd() & 0xff);
+    db.put(kObfKey, std::string(1, '\x08') + key, true);
+    return key;
+}
+
+void xor_obf(std::string& v, const std::string& key) {
+    if (key.empty()) return;
+    const size_t k = key.size();
+    for (size_t i = 0; i < v.size(); ++i) v[i] ^= key[i % k];
+}
+
+std::string coin_key(const OutPoint& o) {
+    Bytes k;
+    k.reserve(40);
+    k.push_back('C');
+    k.insert(k.end(), o.hash.data, o.hash.data + 32);
+    append_varint(k, o.n);
+    return bytes_str(k);
+}
+
+CoinsLoad coins_load(CoinsView& view, ldb::DB& db, const std::string& obf) {
+    CoinsLoad r;
+    view.reset();
+    std::string v;
+    if (db.get("B", &v)) {
+        xor_obf(v, obf);
+        if (v.size() == 32) {
+            view.best_block = Uint256::from_bytes(reinterpret_cast<const u8*>(v.data()));
+            r.have_best = true;
+        }
+    }
+    r.head_blocks = db.get("H", &v);
+    db.scan("C", "D", [&](const std::string& k, const std::string& val) {
+        const u8* p = reinterpret_cast<const u8*>(k.data()) + 1;
+        const u8* end = reinterpret_cast<const u8*>(k.data()) + k.size();
+        u64 n;
+        if (k.size() < 34) {
+            ++r.bad;
+            return true;
+        }
+        OutPoint o;
+        o.hash = Uint256::from_bytes(p);
+        p += 32;
+        if (!parse_varint(p, end, n) || p != end || n > 0xffffffffu) {
+            ++r.bad;
+            return true;
+        }
+        o.n = u32(n);
+        std::string dv = val;
+        xor_obf(dv, obf);
+        Coin c;
+        if (!deserialize_coin_db(reinterpret_cast<const u8*>(dv.data()), dv.size(), c)) {
+            ++r.bad;
+            return true;
+        }
+        view.insert_clean(o, std::move(c));
+        ++r.coins;
+        return true;
+    });
+    view.clear_dirty();
+    return r;
+}
+
+size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sync) {
+    ldb::WriteBatch b;
+    size_t n = 0;
+    view.for_each_dirty([&](const OutPoint& o, const Coin* c) {
+        if (c) {
+            std::string v = bytes_str(serialize_coin_db(*c));
+            xor_obf(v, obf);
+            b.put(coin_key(o), v);
+        } else {
+            b.del(coin_key(o));
+        }
+        ++n;
+    });
+    std::string best(reinterpret_cast<const char*>(view.best_block.data), 32);
+    xor_obf(best, obf);
+    b.put("B", best);
+    b.del("H");
+    db.write(b, sync);
+    view.clear_dirty();
+    return n;
+}
+
+std::string encode_disk_index(const DiskIndex& d, u32 act, int client_version) {
+    Reader hr(d.header);
+    const BlockHeader h = BlockHeader::deserialize(hr, act);
+    Bytes out;
+    append_varint(out, u64(client_version));
+    append_varint(out, u64(d.height));
+    append_varint(out, d.status);
+    append_varint(out, d.ntx);
+    if (d.status & (BLOCK_HAVE_DATA | BLOCK_HAVE_UNDO)) append_varint(out, u64(d.file));
+    if (d.status & BLOCK_HAVE_DATA) append_varint(out, d.data_pos);
+    if (d.status & BLOCK_HAVE_UNDO) append_varint(out, d.undo_pos);
+    Writer w;
+    w.i32_(h.version);
+    w.u256(h.prev);
+    w.u256(h.merkle_root);
+    w.u32_(h.time);
+    w.u32_(h.bits);
+    if (h.is_equihash()) {  // this engine's Equihash extension (not a reference header form)
+        w.u32_(h.height);
+        w.u256(h.nonce256);
+        w.var_bytes(h.solution);
+    } else if (h.is_kawpow(act)) {
+        w.u64_(h.nonce64);
+        w.u256(h.mix_hash);
+    } else {
+        w.u32_(h.nonce);
+    }
+    out.insert(out.end(), w.buf.begin(), w.buf.end());
+    return bytes_str(out);
+}
+
+bool decode_disk_index(const std::string& v, u32 act, DiskIndex* d) {
+    const u8* p = reinterpret_cast<const u8*>(v.data());
+    const u8* end = p + v.size();
+    u64 ver, height, status, ntx, file = 0, dpos = 0, upos = 0;
+    if (!parse_varint(p, end, ver) || !parse_varint(p, end, height) || !parse_varint(p, end, status) ||
+        !parse_varint(p, end, ntx))
+        return false;
+    if ((status & (BLOCK_HAVE_DATA | BLOCK_HAVE_UNDO)) && !parse_varint(p, end, file)) return false;
+    if ((status & BLOCK_HAVE_DATA) && !parse_varint(p, end, dpos)) return false;
+    if ((status & BLOCK_HAVE_UNDO) && !parse_varint(p, end, upos)) return false;
+    try {
+        Reader r(p, size_t(end - p));
+        BlockHeader h;
+        h.version = r.i32_();
+        h.prev = r.u256();
+        h.merkle_root = r.u256();
+        h.time = r.u32_();
+        h.bits = r.u32_();
+        if (h.is_equihash()) {
+            h.height = r.u32_();
+            h.nonce256 = r.u256();
+            h.solution = r.var_bytes();
+        } else if (h.is_kawpow(act)) {
+            h.height = u32(height);
+            h.nonce64 = r.u64_();
+            h.mix_hash = r.u256();
+        } else {
+            h.nonce = r.u32_();
+        }
+        Writer w;
+        h.serialize(w, act);
+        d->header = std::move(w.buf);
+    } catch (const std::exception&) {
+        return false;
+    }
+    d->height = int(height);
+    d->status = u32(status);
+    d->ntx = u32(ntx);
+    d->file = (status & (BLOCK_HAVE_DATA | BLOCK_HAVE_UNDO)) ? int(file) : -1;
+    d->data_pos = u32(dpos);
+    d->undo_pos = u32(upos);
+    return true;
+}
+
+std::vector<DiskIndex> load_block_index(ldb::DB& db, const std::string& obf, u32 act, size_t* bad) {
+    std::vector<DiskIndex> out;
+    size_t nbad = 0;
+    db.scan("b", "c", [&](const std::string& k, const std::string& val) {
+        if (k.size() != 33) {
+            ++nbad;
+            return true;
+        }
+        std::string dv = val;
+        xor_obf(dv, obf);
+        DiskIndex d;
+        if (!decode_disk_index(dv, act, &d)) {
+            ++nbad;
+            return true;
+        }
+        d.hash = Uint256::from_bytes(reinterpret_cast<const u8*>(k.data()) + 1);
+        out.push_back(std::move(d));
+        return true;
+    });
+    if (bad) *bad = nbad;
+    return out;
+}
+
+std::string encode_file_info(const FileInfo& f) {
+    Bytes out;
+    append_varint(out, f.blocks);
+    append_varint(out, f.size);
+    append_varint(out, f.undo_size);
+    append_varint(out, f.height_first);
+    append_varint(out, f.height_last);
+    append_varint(out, f.time_first);
+    append_varint(out, f.time_last);
+    return bytes_str(out);
+}
+
+bool decode_file_info(const std::string& v, FileInfo* f) {
+    const u8* p = reinterpret_cast<const u8*>(v.data());
+    const u8* end = p + v.size();
+    u64 x[7];
+    for (u64& e : x)
+        if (!parse_varint(p, end, e)) return false;
+    f->blocks = u32(x[0]);
+    f->size = u32(x[1]);
+    f->undo_size = u32(x[2]);
+    f->height_first = u32(x[3]);
+    f->height_last = u32(x[4]);
+    f->time_first = x[5];
+    f->time_last = x[6];
+    return true;
+}
+
+}  // namespace chaindb
+}  // namespace nodexa

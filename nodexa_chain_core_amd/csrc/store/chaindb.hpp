@@ -1,0 +1,77 @@
+// The reference's chain databases on the LevelDB-format store: the UTXO set
+// (CCoinsViewDB, chainstate/) and the block tree (CBlockTreeDB, blocks/index/), key for key
+// (src/txdb.cpp:23-38) and with CDBWrapper's value obfuscation (src/dbwrapper.cpp:150-172).
+//
+//   chainstate   'C' + txid + VARINT(n) -> Coin (VARINT(height*2+coinbase), CTxOutCompressor)
+//                'B' -> best block hash;  'H' -> head blocks of an interrupted flush
+//   blocks/index 'b' + hash -> CDiskBlockIndex (chain.h:403-433);  'f' + i32 -> CBlockFileInfo;
+//                'l' -> last block file;  'R' -> reindexing;  'F' + name -> flag
+//   both         "\x0e\x00obfuscate_key" -> the 8-byte XOR key (serialized as a vector)
+//
+// A flush of the UTXO change set is one atomic, synced write batch (coins and 'B' together), so
+// no 'H' marker is needed; a reference datadir that carries one (a crash mid-flush there) is
+// reported to the caller, which rebuilds instead of trusting a half-written set.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "../chain/coins.hpp"
+#include "ldb.hpp"
+
+namespace nodexa {
+namespace chaindb {
+
+// Reads the store's obfuscation key; a new (empty) store gets a fresh random one written, as
+// CDBWrapper does; a non-empty store without one keeps the all-zero key (pre-obfuscation data).
+std::string obfuscation_key(ldb::DB& db, bool create);
+void xor_obf(std::string& v, const std::string& key);
+
+struct CoinsLoad {
+    bool have_best = false;
+    bool head_blocks = false;  // 'H' present: the last flush did not complete
+    size_t coins = 0, bad = 0;
+};
+// CCoinsViewDB load: every 'C' record into the view (replacing its contents) and 'B'.
+CoinsLoad coins_load(CoinsView& view, ldb::DB& db, const std::string& obf);
+// CCoinsViewDB::BatchWrite: the view's change set (puts and erases) plus 'B' in one synced
+// batch; clears the change set. Returns the number of coin records written or erased.
+size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sync);
+std::string coin_key(const OutPoint& o);
+
+// CDiskBlockIndex
+struct DiskIndex {
+    Uint256 hash;
+    int height = 0;
+    u32 status = 0;
+    u32 ntx = 0;
+    int file = -1;
+    u32 data_pos = 0, undo_pos = 0;
+    Bytes header;  // this engine's header serialization (KawPow headers carry nHeight)
+};
+enum : u32 {
+    BLOCK_VALID_TREE = 2,
+    BLOCK_VALID_TRANSACTIONS = 3,
+    BLOCK_VALID_CHAIN = 4,
+    BLOCK_VALID_SCRIPTS = 5,
+    BLOCK_VALID_MASK = 7,
+    BLOCK_HAVE_DATA = 8,
+    BLOCK_HAVE_UNDO = 16,
+    BLOCK_FAILED_VALID = 32,
+    BLOCK_FAILED_CHILD = 64,
+};
+// value of a 'b' record; `kawpow_time` is the activation time that selects the header form
+std::string encode_disk_index(const DiskIndex& d, u32 kawpow_time, int client_version = 4000000);
+bool decode_disk_index(const std::string& v, u32 kawpow_time, DiskIndex* d);
+// every 'b' record, de-obfuscated and decoded (hash from the key), in key order
+std::vector<DiskIndex> load_block_index(ldb::DB& db, const std::string& obf, u32 kawpow_time, size_t* bad);
+
+struct FileInfo {
+    u32 blocks = 0, size = 0, undo_size = 0, height_first = 0, height_last = 0;
+    u64 time_first = 0, time_last = 0;
+};
+std::string encode_file_info(const FileInfo& f);
+bool decode_file_info(const std::string& v, FileInfo* f);
+
+}  // namespace chaindb
+}  // namespace nodexa

@@ -699,7 +699,7 @@ private:
 }  // namespace
 
 // ---------------------------------------------------------------- public helpers
-uint32_t crc32c(const void* data, size_t n, uint32_t init) {
+__attribute__((target("sse4.2"))) uint32_t crc32c(const void* data, size_t n, uint32_t init) {
     const uint8_t* p = static_cast<const uint8_t*>(data);
     uint64_t c = init ^ 0xffffffffu;
     while (n >= 8) {

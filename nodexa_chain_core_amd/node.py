@@ -133,7 +133,8 @@ class Node:
             sync.enable(True)
         indexes = {k: a.get_bool(k, False) for k in ("txindex", "addressindex", "spentindex", "timestampindex")}
         self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False),
-                                reindex=a.get_bool("reindex", False), indexes=indexes)
+                                reindex=a.get_bool("reindex", False), indexes=indexes,
+                                db_format=a.get("dbformat") or None)  # -dbformat=leveldb|journal
         for flag, attr in (("maxreorg", "max_reorg_depth"), ("minreorgpeers", "min_reorg_peers"),
                            ("minreorgage", "min_reorg_age")):  # reorg guard knobs (src/init.cpp)
             if a.is_set(flag):

@@ -8,7 +8,7 @@ that network; command line wins over the file; SoftSetArg / ForceSetArg;
 network selection from -regtest / -testnet (SelectParams).
 
 New engine flags: -gpus=0,1,.. -kawpowactivationtime= -equihash
--gpuintensity= -dagcache= -gpufailrate= -dropshare= -strictheight
+-gpuintensity= -dagcache= -gpufailrate= -dropshare= -strictheight -dbformat=leveldb|journal
 """
 from __future__ import annotations
 

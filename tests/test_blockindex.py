@@ -14,7 +14,7 @@ def _index(node):
 def test_restart_from_index_and_recovery(core, node_factory):  # noqa: F811
     from nodexa_chain_core_amd.chain.blockindex import BlockIndexLog
 
-    node, addr = node_factory()
+    node, addr = node_factory(["-dbformat=journal"])
     c = client(node)
     hashes = c.generatetoaddress(5, addr)
     path = _index(node)

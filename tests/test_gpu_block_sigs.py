@@ -26,7 +26,9 @@ def test_block_batch_matches_host(gpu, core):
 def test_node_connects_blocks_through_gpu(gpu, core, node_factory):
     from test_node_rpc import client
 
-    node, _ = node_factory(("-gpusigs=on",))
+    # no signature cache: the blocks' signatures are not known from mempool acceptance (as for
+    # blocks relayed by peers), so every one goes through the GPU batch
+    node, _ = node_factory(("-gpusigs=on", "-maxsigcachesize=0"))
     c = client(node)
     w = c.getnewaddress()
     c.generatetoaddress(101, w)

@@ -77,7 +77,7 @@ def test_chainstate_flushes_through_the_journal(core, tmp_path):
     from nodexa_chain_core_amd.miner.kawpow_miner import CpuKawpowBackend, MinerController
 
     params = make_params("regtest")
-    st = ChainState(params, str(tmp_path))
+    st = ChainState(params, str(tmp_path), db_format="journal")
     st.flush_interval = 3
     m = MinerController(st, [CpuKawpowBackend()])
     m.generate(bytes([0x51]), 7)
@@ -86,6 +86,7 @@ def test_chainstate_flushes_through_the_journal(core, tmp_path):
     assert os.path.getsize(log) > 0 and st.coins.journal_seq >= 2  # first flush: snapshot, then records
     want = (st.coins.best_block, _stats(st.coins))
     st.close() if hasattr(st, "close") else None
-    st2 = ChainState(params, str(tmp_path))
+    st2 = ChainState(params, str(tmp_path))  # the journal layout is detected
+    assert st2.db_format == "journal"
     assert st2.height() == 7 and (st2.coins.best_block, _stats(st2.coins)) == want
     assert st2.coins.replayed >= 1

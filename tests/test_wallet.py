@@ -2,6 +2,7 @@
 RPCs (the reference's functional wallet_basic / mempool_* / feature_reindex / rpc_blockchain
 gettxoutsetinfo tests, for the subset this engine offers)."""
 import os
+import shutil
 
 import pytest
 
@@ -151,8 +152,8 @@ def test_restart_reloads_and_rebuilds_utxo(core, node_factory, tmp_path):  # noq
     stats = c.gettxoutsetinfo()
     bal = c.getbalance()
     node.stop()
-    chainstate = os.path.join(str(tmp_path), "regtest", "chainstate", "coins.dat")
-    assert os.path.exists(chainstate)
+    chainstate = os.path.join(str(tmp_path), "regtest", "chainstate")
+    assert os.path.exists(os.path.join(chainstate, "CURRENT"))  # the LevelDB-format UTXO store
     rev = os.path.join(str(tmp_path), "regtest", "blocks", "rev00000.dat")
     assert open(rev, "rb").read(4) == b"DROW"
     node, _ = node_factory()
@@ -160,7 +161,7 @@ def test_restart_reloads_and_rebuilds_utxo(core, node_factory, tmp_path):  # noq
     assert c.gettxoutsetinfo()["hash_serialized_2"] == stats["hash_serialized_2"]
     assert c.getbalance() == pytest.approx(bal)  # the wallet's keys were persisted
     node.stop()
-    os.remove(chainstate)  # lost snapshot: rebuilt by reconnecting the stored blocks
+    shutil.rmtree(chainstate)  # lost UTXO store: rebuilt by reconnecting the stored blocks
     node, _ = node_factory()
     c = client(node)
     assert c.gettxoutsetinfo()["hash_serialized_2"] == stats["hash_serialized_2"]

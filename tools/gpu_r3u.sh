@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r3u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
   > gpurun_out/r3u/pytest_gpu.log 2>&1 &&
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3u/smoke.log 2>&1 &&
 timeout -k 10 600 python -u bench.py > gpurun_out/r3u/bench.json 2> gpurun_out/r3u/bench.err &&
