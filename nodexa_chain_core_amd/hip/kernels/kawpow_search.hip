@@ -131,12 +131,10 @@ __device__ uint32_t kp_mul_u24(uint32_t a, uint32_t b) __asm("llvm.amdgcn.mul.u2
 #endif
 NX_DEV uint32_t kp_fastmod(uint32_t x, const FastMod32& f) {
 #if defined(KP_FASTMOD24)
-    if (f.m24 != 0u) {  // uniform: m24 is 0 outside 2^16 < d < 2^24 (ops/jit.defines_for avoids that)
-        const uint32_t q = kp_mulhi_u24(x >> 8, f.m24);
-        const uint32_t r = x - kp_mul_u24(q, f.d);
-        return min(r, r - f.d);
-    }
-    const uint32_t r = x - __umulhi(x, f.mb) * f.d;
+    // no fallback path: ops/jit.defines_for selects this variant only for 2^16 < d < 2^24 (a
+    // uniform runtime branch to the 32-bit form doubled the round code and spilled 198 VGPRs)
+    const uint32_t q = kp_mulhi_u24(x >> 8, f.m24);
+    const uint32_t r = x - kp_mul_u24(q, f.d);
     return min(r, r - f.d);
 #elif defined(KP_BARRETT)
     // q' = floor(x * floor(2^32/d) / 2^32) is q or q-1, so r' < 2d and one
