@@ -276,14 +276,23 @@ class ChainState:
         self.assets_path = os.path.join(datadir, "chainstate", "assets.dat") if datadir else None
         self.indexes_path = os.path.join(datadir, "chainstate", "indexes.dat") if datadir else None
         self.index_flags = dict(indexes or {})  # txindex / addressindex / spentindex / timestampindex
+        self._stored_index_flags = {}
         if self.db_format == "leveldb" and self.index_log is not None:
             for k, v in self.index_flags.items():  # WriteFlag (src/init.cpp), read back by the reference
-                if self.index_log.flag(k) != bool(v):
+                self._stored_index_flags[k] = self.index_log.flag(k)
+                if self._stored_index_flags[k] != bool(v):
                     self.index_log.set_flag(k, bool(v))
         self.coins = _core.CoinsView()
         self.assets = _core.AssetsState()
-        self.indexes = _core.ChainIndexes(**self.index_flags)
+        self.indexes = self._new_indexes()
         self._init_coins()
+
+    def _new_indexes(self):
+        ix = _core.ChainIndexes(**self.index_flags)
+        # blocks/index keeps the indexes as records (CBlockTreeDB layout): connect / disconnect
+        # journal their changes for the next flush
+        ix.journal = self.db_format == "leveldb" and self.index_log is not None and any(self.index_flags.values())
+        return ix
 
     # ------------------------------------------------------------------ load / reindex
     def _load_block_files(self) -> None:
@@ -878,7 +887,13 @@ class ChainState:
             loaded = self.coins_path is not None and self.coins.load_with_journal(self.coins_path, self.coins_log)
         if loaded and self.coins.replayed:
             log.log_printf(f"UTXO journal: {self.coins.replayed} flush record(s) replayed onto the snapshot")
-        if loaded:  # the asset state must describe the same block as the UTXO snapshot
+        if loaded and self.coins_db is not None:
+            # asset records live in the same store and are flushed in the same batch as the coins
+            if not _core.assets_load_ldb(self.assets, self.coins_db, self._coins_obf) or \
+                    self.assets.best_block != self.coins.best_block:
+                log.log_printf("asset records missing or out of step with the UTXO set; replaying from genesis")
+                loaded = False
+        elif loaded:  # the asset state must describe the same block as the UTXO snapshot
             raw = None
             if os.path.exists(self.assets_path):
                 with open(self.assets_path, "rb") as f:
@@ -887,13 +902,24 @@ class ChainState:
                 log.log_printf("asset state missing or out of step with the UTXO snapshot; replaying from genesis")
                 loaded = False
         if loaded and any(self.index_flags.values()):  # the indexes too (a changed -*index flag replays)
-            raw = None
-            if os.path.exists(self.indexes_path):
-                with open(self.indexes_path, "rb") as f:
-                    raw = f.read()
-            want = _core.ChainIndexes(**self.index_flags)
-            ok = raw is not None and want.deserialize(raw) and want.best_block == self.coins.best_block and \
-                all(getattr(want, k) == bool(v) for k, v in self.index_flags.items())
+            want = self._new_indexes()
+            if self.coins_db is not None:
+                # blocks/index records, built with the flags the store recorded ('F')
+                at = {(p.file, p.offset): h for h, p in self.block_pos.items() if p is not None}
+                ok_load, have_best = _core.indexes_load_ldb(want, self.index_log.db, self.index_log.obf, at)
+                if not have_best:
+                    # a reference datadir: its ConnectBlock writes the index records with the block,
+                    # so they describe at least the chainstate's block
+                    want.best_block = self.coins.best_block
+                ok = ok_load and want.best_block == self.coins.best_block and \
+                    all(self._stored_index_flags.get(k) == bool(v) for k, v in self.index_flags.items())
+            else:
+                raw = None
+                if os.path.exists(self.indexes_path):
+                    with open(self.indexes_path, "rb") as f:
+                        raw = f.read()
+                ok = raw is not None and want.deserialize(raw) and want.best_block == self.coins.best_block and \
+                    all(getattr(want, k) == bool(v) for k, v in self.index_flags.items())
             if ok:
                 self.indexes = want
             else:
@@ -905,13 +931,16 @@ class ChainState:
             self.coins = _core.CoinsView()
             self.coins.best_block = gh  # the genesis coinbase is unspendable: never added
             self.assets = _core.AssetsState()
-            self.indexes = _core.ChainIndexes(**self.index_flags)
+            self.indexes = self._new_indexes()
             self.indexes.best_block = gh
             if self.coins_db is not None:
                 # drop the stale set: every coin record, then the fresh (empty) state's 'B'
                 stale = [(k, None) for k, _ in self.coins_db.items(b"C", b"D")]
+                stale += [(k, None) for k, _ in self.coins_db.items(b"\x01", b"\x02")]  # asset records
                 self.coins_db.write(stale + [(b"H", None)])
-                _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True)
+                self.assets.best_block = gh
+                _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True, self.assets)
+                _core.indexes_purge_ldb(self.index_log.db)  # the indexes are rebuilt by the replay
             elif self.coins_path is not None and (os.path.exists(self.coins_path) or os.path.exists(self.coins_log)):
                 self.coins.compact(self.coins_path, self.coins_log)  # a fresh snapshot restarts the journal
         with self.lock:
@@ -1077,7 +1106,10 @@ class ChainState:
             self.index_log.set_undo(idx.hash, u[0], u[1], u[2])
         else:
             self.undo.write(idx.hash, idx.prev_hash, undo)
-        self.indexes.connect(block, height, idx.hash, undo)
+        if bpos is not None:
+            self.indexes.connect(block, height, idx.hash, undo, bpos.file, bpos.offset)
+        else:
+            self.indexes.connect(block, height, idx.hash, undo)
         if aundo:
             self.asset_undo.write(idx.hash, idx.prev_hash, aundo)
         self.coins.best_block = idx.hash
@@ -1093,21 +1125,26 @@ class ChainState:
         if self.coins_path is None or self._since_flush == 0:
             return
         os.makedirs(os.path.dirname(self.coins_path), exist_ok=True)
-        # assets.dat first: a crash between the two leaves an asset state that does not match the
-        # UTXO snapshot, which start-up detects (and replays) instead of mixing two states
         self.assets.best_block = self.coins.best_block
-        tmp = self.assets_path + ".new"
-        with open(tmp, "wb") as f:
-            f.write(self.assets.serialize())
-            f.flush()
-            os.fsync(f.fileno())
-        os.replace(tmp, self.assets_path)
+        if self.coins_db is None:
+            # assets.dat first: a crash between the two leaves an asset state that does not match
+            # the UTXO snapshot, which start-up detects (and replays) instead of mixing two states
+            tmp = self.assets_path + ".new"
+            with open(tmp, "wb") as f:
+                f.write(self.assets.serialize())
+                f.flush()
+                os.fsync(f.fileno())
+            os.replace(tmp, self.assets_path)
         if self.db_crash_ratio and random.randrange(self.db_crash_ratio) == 0:
             # -dbcrashratio (CCoinsViewDB::BatchWrite, src/txdb.cpp:96): die between the two halves
             # of the flush; start-up must notice the mismatch and replay (feature_dbcrash.py)
             log.log_printf("Simulating a crash. Goodbye.")
             os._exit(0)
-        if any(self.index_flags.values()):
+        if any(self.index_flags.values()) and self.coins_db is not None:
+            # the index changes since the last flush, as blocks/index records (made durable by the
+            # synced block-tree write below)
+            _core.indexes_flush_ldb(self.indexes, self.index_log.db, self.index_log.obf, False)
+        elif any(self.index_flags.values()):
             tmp = self.indexes_path + ".new"
             with open(tmp, "wb") as f:
                 f.write(self.indexes.serialize())
@@ -1116,9 +1153,9 @@ class ChainState:
             os.replace(tmp, self.indexes_path)
         if self.coins_db is not None:
             # block index records first (their undo positions must be durable before the coins
-            # that depend on them), then the UTXO change set and 'B' in one synced batch
+            # that depend on them), then the UTXO and asset change sets with 'B' in one synced batch
             self.index_log.sync()
-            _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True)
+            _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True, self.assets)
         elif not os.path.exists(self.coins_path):  # first flush of this datadir: start from a snapshot
             self.coins.compact(self.coins_path, self.coins_log)
         else:

@@ -413,12 +413,16 @@ void bind_script(py::module_& m) {
                           need32(h, "best_block");
                           x.best_block = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
                       })
-        .def("connect", [](ChainIndexes& x, const Block& b, int height, const py::bytes& hash, const py::bytes& undo) {
+        .def("connect", [](ChainIndexes& x, const Block& b, int height, const py::bytes& hash, const py::bytes& undo,
+                           int file, u32 data_pos) {
             const std::string h = hash;
             need32(h, "hash");
             x.connect(b, height, Uint256::from_bytes(reinterpret_cast<const u8*>(h.data())),
-                      deserialize_block_undo(bytes_of(undo)));
-        })
+                      deserialize_block_undo(bytes_of(undo)), file, data_pos);
+        }, py::arg("block"), py::arg("height"), py::arg("hash"), py::arg("undo"), py::arg("file") = -1,
+           py::arg("data_pos") = 0)
+        .def_readwrite("journal", &ChainIndexes::journal)
+        .def_property_readonly("pending_changes", &ChainIndexes::pending_changes)
         .def("disconnect", [](ChainIndexes& x, const Block& b, int height, const py::bytes& hash, const py::bytes& undo) {
             const std::string h = hash;
             need32(h, "hash");

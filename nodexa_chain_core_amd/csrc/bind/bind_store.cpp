@@ -114,10 +114,15 @@ void bind_store(py::module_& m) {
         d["bad"] = r.bad;
         return d;
     });
-    m.def("coins_flush_ldb", [](CoinsView& view, ldb::DB& db, const py::bytes& obf, bool sync) {
+    m.def("coins_flush_ldb", [](CoinsView& view, ldb::DB& db, const py::bytes& obf, bool sync, assets::State* st) {
         const std::string k = obf;
         py::gil_scoped_release rel;
-        return chaindb::coins_flush(view, db, k, sync);
+        return chaindb::coins_flush(view, db, k, sync, st);
+    }, py::arg("view"), py::arg("db"), py::arg("obf"), py::arg("sync"), py::arg("assets") = nullptr);
+    m.def("assets_load_ldb", [](assets::State& st, ldb::DB& db, const py::bytes& obf) {
+        const std::string k = obf;
+        py::gil_scoped_release rel;
+        return chaindb::assets_load(st, db, k);
     });
     m.def("coin_db_key", [](const py::bytes& txid, u32 n) {
         const std::string s = txid;
@@ -179,7 +184,34 @@ void bind_store(py::module_& m) {
                                       py::bytes(reinterpret_cast<const char*>(d.header.data()), d.header.size())));
         return py::make_tuple(out, bad);
     });
-    m.def("encode_file_info", [](u32 blocks, u32 size, u32 undo_size, u32 hfirst, u32 hlast, u64 tfirst, u64 tlast) {
+    m.def("indexes_flush_ldb", [](ChainIndexes& ix, ldb::DB& db, const py::bytes& obf, bool sync) {
+        const std::string k = obf;
+        py::gil_scoped_release rel;
+        return chaindb::indexes_flush(ix, db, k, sync);
+    });
+    m.def("indexes_load_ldb", [](ChainIndexes& ix, ldb::DB& db, const py::bytes& obf, const py::dict& block_at) {
+        // block_at: {(file, data_pos): block hash}
+        std::map<std::pair<int, u32>, Uint256> at;
+        for (auto kv : block_at) {
+            auto key = kv.first.cast<std::pair<int, u32>>();
+            const std::string h = kv.second.cast<py::bytes>();
+            if (h.size() == 32) at[key] = Uint256::from_bytes(reinterpret_cast<const u8*>(h.data()));
+        }
+        bool have_best = false, ok;
+        {
+            const std::string k = obf;
+            py::gil_scoped_release rel;
+            ok = chaindb::indexes_load(ix, db, k, [&](int f, u32 p, Uint256* out) {
+                auto it = at.find({f, p});
+                if (it == at.end()) return false;
+                *out = it->second;
+                return true;
+            }, &have_best);
+        }
+        return py::make_tuple(ok, have_best);
+    });
+    m.def("indexes_purge_ldb", [](ldb::DB& db) { chaindb::indexes_purge(db); });
+    m.def("encode_file_info",[](u32 blocks, u32 size, u32 undo_size, u32 hfirst, u32 hlast, u64 tfirst, u64 tlast) {
         chaindb::FileInfo f{blocks, size, undo_size, hfirst, hlast, tfirst, tlast};
         return py::bytes(chaindb::encode_file_info(f));
     });

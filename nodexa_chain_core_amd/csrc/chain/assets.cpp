@@ -1048,7 +1048,55 @@ void State::log(u8 kind, const std::string& a, const std::string& b) {
         }
     }
     op.old = std::move(w.buf);
+    dirty_.insert({kind, {a, b}});
     journal_.push_back(std::move(op));
+}
+
+void State::for_each_dirty(
+    const std::function<void(u8, const std::string&, const std::string&, const Bytes*)>& f) const {
+    for (auto& [kind, k] : dirty_) {
+        Writer w;
+        bool has = false;
+        switch (kind) {
+            case 0: {
+                auto it = meta_.find(k.first);
+                if ((has = it != meta_.end())) write_meta(w, it->second);
+                break;
+            }
+            case 1: {
+                auto it = bal_.find(k);
+                if ((has = it != bal_.end())) w.i64_(it->second);
+                break;
+            }
+            case 2: has = tags_.count(k) != 0; break;
+            case 3: has = frozen_.count(k) != 0; break;
+            case 4: has = global_.count(k.first) != 0; break;
+            case 5: {
+                auto it = verifier_.find(k.first);
+                if ((has = it != verifier_.end())) write_str(w, it->second);
+                break;
+            }
+        }
+        f(kind, k.first, k.second, has ? &w.buf : nullptr);
+    }
+}
+
+bool State::load_entry(u8 kind, const std::string& a, const std::string& b, const Bytes& value) {
+    try {
+        Reader r(value);
+        switch (kind) {
+            case 0: meta_[a] = read_meta(r); break;
+            case 1: bal_[{a, b}] = r.i64_(); break;
+            case 2: tags_.insert({a, b}); break;
+            case 3: frozen_.insert({a, b}); break;
+            case 4: global_.insert(a); break;
+            case 5: verifier_[a] = read_str(r); break;
+            default: return false;
+        }
+    } catch (const std::exception&) {
+        return false;
+    }
+    return true;
 }
 
 void State::set_meta(const Meta& m) {
@@ -1087,6 +1135,7 @@ void State::set_verifier(const std::string& r, const std::string& v) {
 }
 
 void State::restore(const Op& op) {
+    dirty_.insert({op.kind, {op.a, op.b}});
     Reader r(op.old);
     switch (op.kind) {
         case 0:

@@ -18,6 +18,7 @@
 //    same operators (| & ! parentheses, 1/0 constants) and the same error cases.
 #pragma once
 
+#include <functional>
 #include <map>
 #include <optional>
 #include <set>
@@ -178,6 +179,15 @@ public:
     bool deserialize(const Bytes& b);
     Uint256 best_block;
 
+    // Incremental persistence (store/chaindb.hpp assets records): every entry changed since
+    // clear_dirty() as (kind, a, b, current value or nullptr when absent); load_entry() inserts a
+    // stored value without marking it changed.
+    void for_each_dirty(const std::function<void(u8, const std::string&, const std::string&, const Bytes*)>& f) const;
+    void clear_dirty() { dirty_.clear(); }
+    size_t dirty_count() const { return dirty_.size(); }
+    bool load_entry(u8 kind, const std::string& a, const std::string& b, const Bytes& value);
+    void reset() { *this = State(); }
+
 private:
     struct Op {
         u8 kind;  // 0 meta, 1 balance, 2 tag, 3 frozen, 4 global, 5 verifier
@@ -194,6 +204,7 @@ private:
     std::set<std::string> global_;
     std::map<std::string, std::string> verifier_;
     std::vector<Op> journal_;
+    std::set<std::pair<u8, AddrKey>> dirty_;
 };
 
 // Consensus::CheckTxAssets against `st` (spent: the coin of every input). "" or reject reason.

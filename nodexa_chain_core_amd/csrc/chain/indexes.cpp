@@ -39,6 +39,91 @@ bool index_address(const Bytes& s, int& type, u8 h160[20], std::string& asset, i
     return false;
 }
 
+namespace {
+
+// record encodings of the reference's index keys/values (addressindex.h, spentindex.h,
+// timestampindex.h, txdb.h CDiskTxPos): big-endian heights / positions in keys so that they sort
+void put_be32(std::string& s, u32 v) {
+    for (int i = 3; i >= 0; --i) s.push_back(char(v >> (8 * i)));
+}
+void put_le32(std::string& s, u32 v) {
+    for (int i = 0; i < 4; ++i) s.push_back(char(v >> (8 * i)));
+}
+void put_le64(std::string& s, u64 v) {
+    for (int i = 0; i < 8; ++i) s.push_back(char(v >> (8 * i)));
+}
+void put_u256(std::string& s, const Uint256& u) { s.append(reinterpret_cast<const char*>(u.data), 32); }
+void put_compact(std::string& s, u64 n) {
+    Writer w;
+    w.compact_size(n);
+    s.append(reinterpret_cast<const char*>(w.buf.data()), w.buf.size());
+}
+// 'a' / 'u' key prefix: type, hash160, asset name (serialized std::string)
+std::string addr_prefix(char p, const std::string& k) {
+    std::string s(1, p);
+    s.append(k, 0, 21);
+    put_compact(s, k.size() - 21);
+    s.append(k, 21, std::string::npos);
+    return s;
+}
+std::string delta_key(const std::string& k, const AddrDelta& d) {
+    std::string s = addr_prefix('a', k);
+    put_be32(s, u32(d.height));
+    put_be32(s, d.tx_index);
+    put_u256(s, d.txid);
+    put_le32(s, d.index);
+    s.push_back(d.spending ? 1 : 0);
+    return s;
+}
+std::string le64_str(int64_t v) {
+    std::string s;
+    put_le64(s, u64(v));
+    return s;
+}
+std::string unspent_key(const std::string& k, const Uint256& txid, u32 n) {
+    std::string s = addr_prefix('u', k);
+    put_u256(s, txid);
+    put_le32(s, n);
+    return s;
+}
+std::string unspent_value(const AddrUnspent& u) {
+    std::string s;
+    put_le64(s, u64(u.amount));
+    put_compact(s, u.script.size());
+    s.append(reinterpret_cast<const char*>(u.script.data()), u.script.size());
+    put_le32(s, u32(u.height));
+    return s;
+}
+std::string spent_key(const Uint256& txid, u32 n) {
+    std::string s(1, 'p');
+    put_u256(s, txid);
+    put_le32(s, n);
+    return s;
+}
+std::string spent_value(const SpentInfo& si) {
+    std::string s;
+    put_u256(s, si.txid);
+    put_le32(s, si.input);
+    put_le32(s, u32(si.height));
+    put_le64(s, u64(si.amount));
+    put_le32(s, u32(si.addr_type));
+    s.append(reinterpret_cast<const char*>(si.h160), 20);
+    return s;
+}
+std::string time_key(u32 t, const Uint256& h) {
+    std::string s(1, 's');
+    put_be32(s, t);
+    put_u256(s, h);
+    return s;
+}
+std::string tx_key(const Uint256& txid) {
+    std::string s(1, 't');
+    put_u256(s, txid);
+    return s;
+}
+
+}  // namespace
+
 ChainIndexes::Key ChainIndexes::key(int type, const u8 h160[20], const std::string& asset) {
     Key k(1, char(type));
     k.append(reinterpret_cast<const char*>(h160), 20);
@@ -46,12 +131,37 @@ ChainIndexes::Key ChainIndexes::key(int type, const u8 h160[20], const std::stri
     return k;
 }
 
-void ChainIndexes::connect(const Block& block, int height, const Uint256& hash, const BlockUndo& undo) {
-    if (timestampindex) time_.emplace(block.header.time, hash);
+void ChainIndexes::connect(const Block& block, int height, const Uint256& hash, const BlockUndo& undo, int file,
+                           u32 data_pos) {
+    if (timestampindex) {
+        time_.emplace(block.header.time, hash);
+        rec_put(time_key(block.header.time, hash), std::string(4, '\0'));
+        std::string z(1, 'z'), ts;
+        put_u256(z, hash);
+        put_be32(ts, block.header.time);
+        rec_put(z, ts);
+    }
+    // CDiskTxPos offsets count from the end of the header: CompactSize(#tx), then each tx in turn
+    u64 tx_off = 0;
+    if (txindex && journal && file >= 0) {
+        Writer w;
+        w.compact_size(block.vtx.size());
+        tx_off = w.buf.size();
+    }
     for (size_t t = 0; t < block.vtx.size(); ++t) {
         const Transaction& tx = block.vtx[t];
         const Uint256 txid = tx.txid();
-        if (txindex) tx_[txid] = hash;
+        if (txindex) {
+            tx_[txid] = hash;
+            if (journal && file >= 0) {
+                Bytes pos;
+                append_varint(pos, u64(file));
+                append_varint(pos, data_pos);
+                append_varint(pos, tx_off);
+                rec_put(tx_key(txid), std::string(pos.begin(), pos.end()));
+                tx_off += tx.bytes(true).size();
+            }
+        }
         if ((addressindex || spentindex) && !tx.is_coinbase() && t - 1 < undo.vtxundo.size()) {
             const TxUndo& tu = undo.vtxundo[t - 1];
             for (size_t i = 0; i < tx.vin.size() && i < tu.prev.size(); ++i) {
@@ -64,11 +174,13 @@ void ChainIndexes::connect(const Block& block, int height, const Uint256& hash, 
                 if (addressindex && has) {
                     const Key k = key(type, h, asset);
                     deltas_[k].push_back({height, u32(t), txid, u32(i), true, -amount});
+                    rec_put(delta_key(k, deltas_[k].back()), le64_str(-amount));
                     auto it = unspent_.find(k);
                     if (it != unspent_.end()) {
                         it->second.erase({tx.vin[i].prevout.hash, tx.vin[i].prevout.n});
                         if (it->second.empty()) unspent_.erase(it);
                     }
+                    rec_erase(unspent_key(k, tx.vin[i].prevout.hash, tx.vin[i].prevout.n));
                 }
                 if (spentindex) {
                     SpentInfo si;
@@ -79,6 +191,7 @@ void ChainIndexes::connect(const Block& block, int height, const Uint256& hash, 
                     si.addr_type = has ? type : 0;
                     std::memcpy(si.h160, h, 20);
                     spent_[{tx.vin[i].prevout.hash, tx.vin[i].prevout.n}] = si;
+                    rec_put(spent_key(tx.vin[i].prevout.hash, tx.vin[i].prevout.n), spent_value(si));
                 }
             }
         }
@@ -91,8 +204,12 @@ void ChainIndexes::connect(const Block& block, int height, const Uint256& hash, 
                 if (!index_address(tx.vout[n].script_pubkey, type, h, asset, amount, tx.vout[n].value)) continue;
                 const Key k = key(type, h, asset);
                 deltas_[k].push_back({height, u32(t), txid, n, false, amount});
-                if (!assets::script_unspendable(tx.vout[n].script_pubkey))
-                    unspent_[k][{txid, n}] = {txid, n, amount, tx.vout[n].script_pubkey, height};
+                rec_put(delta_key(k, deltas_[k].back()), le64_str(amount));
+                if (!assets::script_unspendable(tx.vout[n].script_pubkey)) {
+                    const AddrUnspent u{txid, n, amount, tx.vout[n].script_pubkey, height};
+                    unspent_[k][{txid, n}] = u;
+                    rec_put(unspent_key(k, txid, n), unspent_value(u));
+                }
             }
         }
     }
@@ -108,13 +225,20 @@ void ChainIndexes::disconnect(const Block& block, int height, const Uint256& has
                 time_.erase(it);
                 break;
             }
+        rec_erase(time_key(block.header.time, hash));
+        std::string z(1, 'z');
+        put_u256(z, hash);
+        rec_erase(z);
     }
     for (size_t t = block.vtx.size(); t-- > 0;) {
         const Transaction& tx = block.vtx[t];
         const Uint256 txid = tx.txid();
         if (txindex) {
             auto it = tx_.find(txid);
-            if (it != tx_.end() && it->second == hash) tx_.erase(it);
+            if (it != tx_.end() && it->second == hash) {
+                tx_.erase(it);
+                rec_erase(tx_key(txid));
+            }
         }
         if (addressindex) {
             for (u32 n = 0; n < tx.vout.size(); ++n) {
@@ -130,6 +254,7 @@ void ChainIndexes::disconnect(const Block& block, int height, const Uint256& has
                     it->second.erase({txid, n});
                     if (it->second.empty()) unspent_.erase(it);
                 }
+                rec_erase(unspent_key(k, txid, n));
             }
         }
         if ((addressindex || spentindex) && !tx.is_coinbase() && t - 1 < undo.vtxundo.size()) {
@@ -143,10 +268,15 @@ void ChainIndexes::disconnect(const Block& block, int height, const Uint256& has
                 if (addressindex && index_address(c.out.script_pubkey, type, h, asset, amount, c.out.value)) {
                     const Key k = key(type, h, asset);
                     touched.insert(k);
-                    unspent_[k][{tx.vin[i].prevout.hash, tx.vin[i].prevout.n}] = {
-                        tx.vin[i].prevout.hash, tx.vin[i].prevout.n, amount, c.out.script_pubkey, int(c.height)};
+                    const AddrUnspent u{tx.vin[i].prevout.hash, tx.vin[i].prevout.n, amount, c.out.script_pubkey,
+                                        int(c.height)};
+                    unspent_[k][{u.txid, u.index}] = u;
+                    rec_put(unspent_key(k, u.txid, u.index), unspent_value(u));
                 }
-                if (spentindex) spent_.erase({tx.vin[i].prevout.hash, tx.vin[i].prevout.n});
+                if (spentindex) {
+                    spent_.erase({tx.vin[i].prevout.hash, tx.vin[i].prevout.n});
+                    rec_erase(spent_key(tx.vin[i].prevout.hash, tx.vin[i].prevout.n));
+                }
             }
         }
     }
@@ -154,7 +284,10 @@ void ChainIndexes::disconnect(const Block& block, int height, const Uint256& has
         auto it = deltas_.find(k);
         if (it == deltas_.end()) continue;
         auto& v = it->second;
-        while (!v.empty() && v.back().height >= height) v.pop_back();
+        while (!v.empty() && v.back().height >= height) {
+            rec_erase(delta_key(k, v.back()));
+            v.pop_back();
+        }
         if (v.empty()) deltas_.erase(it);
     }
     best_block = block.header.prev;
@@ -331,6 +464,125 @@ bool ChainIndexes::deserialize(const Bytes& b) {
     }
     *this = std::move(x);
     return true;
+}
+
+bool ChainIndexes::load_records(
+    const std::function<void(const std::function<void(const std::string&, const std::string&)>&)>& scan,
+    const std::function<bool(int, u32, Uint256*)>& tx_block_at) {
+    bool ok = true;
+    auto be32 = [](const u8* p) { return (u32(p[0]) << 24) | (u32(p[1]) << 16) | (u32(p[2]) << 8) | u32(p[3]); };
+    // key after the prefix byte: type, hash160, CompactSize asset length, asset -> (Key, rest offset)
+    auto addr = [&](const std::string& k, Key* out, size_t* rest) {
+        if (k.size() < 23) return false;
+        try {
+            Reader r(reinterpret_cast<const u8*>(k.data()) + 22, k.size() - 22);
+            const u64 n = r.compact_size();
+            const size_t off = 22 + r.pos();
+            if (k.size() < off + n) return false;
+            *out = k.substr(1, 21) + k.substr(off, size_t(n));
+            *rest = off + size_t(n);
+            return true;
+        } catch (const std::exception&) {
+            return false;
+        }
+    };
+    tx_.clear();
+    deltas_.clear();
+    unspent_.clear();
+    spent_.clear();
+    time_.clear();
+    scan([&](const std::string& k, const std::string& v) {
+        const u8* kp = reinterpret_cast<const u8*>(k.data());
+        const u8* vp = reinterpret_cast<const u8*>(v.data());
+        try {
+            switch (k[0]) {
+                case 't': {
+                    if (!txindex || k.size() != 33) return;
+                    const u8* p = vp;
+                    u64 file, pos, off;
+                    if (!parse_varint(p, vp + v.size(), file) || !parse_varint(p, vp + v.size(), pos) ||
+                        !parse_varint(p, vp + v.size(), off)) {
+                        ok = false;
+                        return;
+                    }
+                    Uint256 h;
+                    if (tx_block_at(int(file), u32(pos), &h)) tx_[Uint256::from_bytes(kp + 1)] = h;
+                    return;
+                }
+                case 'a': {
+                    Key key;
+                    size_t o;
+                    if (!addressindex) return;
+                    if (!addr(k, &key, &o) || k.size() != o + 4 + 4 + 32 + 4 + 1 || v.size() != 8) {
+                        ok = false;
+                        return;
+                    }
+                    AddrDelta d;
+                    d.height = int(be32(kp + o));
+                    d.tx_index = be32(kp + o + 4);
+                    d.txid = Uint256::from_bytes(kp + o + 8);
+                    d.index = load_le32(kp + o + 40);
+                    d.spending = kp[o + 44] != 0;
+                    d.amount = int64_t(load_le64(vp));
+                    deltas_[key].push_back(d);
+                    return;
+                }
+                case 'u': {
+                    Key key;
+                    size_t o;
+                    if (!addressindex) return;
+                    if (!addr(k, &key, &o) || k.size() != o + 36) {
+                        ok = false;
+                        return;
+                    }
+                    Reader r(vp, v.size());
+                    AddrUnspent u;
+                    u.txid = Uint256::from_bytes(kp + o);
+                    u.index = load_le32(kp + o + 32);
+                    u.amount = r.i64_();
+                    u.script = r.var_bytes();
+                    u.height = r.i32_();
+                    unspent_[key][{u.txid, u.index}] = std::move(u);
+                    return;
+                }
+                case 'p': {
+                    if (!spentindex) return;
+                    if (k.size() != 37 || v.size() != 32 + 4 + 4 + 8 + 4 + 20) {
+                        ok = false;
+                        return;
+                    }
+                    Reader r(vp, v.size());
+                    SpentInfo si;
+                    si.txid = r.u256();
+                    si.input = r.u32_();
+                    si.height = r.i32_();
+                    si.amount = r.i64_();
+                    si.addr_type = r.i32_();
+                    std::memcpy(si.h160, r.take(20), 20);
+                    spent_[{Uint256::from_bytes(kp + 1), load_le32(kp + 33)}] = si;
+                    return;
+                }
+                case 's':
+                    if (!timestampindex) return;
+                    if (k.size() != 37) {
+                        ok = false;
+                        return;
+                    }
+                    time_.emplace(be32(kp + 1), Uint256::from_bytes(kp + 5));
+                    return;
+                default: return;
+            }
+        } catch (const std::exception&) {
+            ok = false;
+        }
+    });
+    // deltas in (height, position) order, as connect appends them
+    for (auto& kv : deltas_)
+        std::stable_sort(kv.second.begin(), kv.second.end(), [](const AddrDelta& a, const AddrDelta& b) {
+            return a.height != b.height ? a.height < b.height : a.tx_index < b.tx_index;
+        });
+    changes_.clear();
+    return ok;
 }
 
 }  // namespace nodexa

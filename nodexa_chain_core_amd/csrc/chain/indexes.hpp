@@ -13,6 +13,7 @@
 // asset amount, CLORE outputs under "CLORE" (the reference's default asset name).
 #pragma once
 
+#include <functional>
 #include <map>
 #include <optional>
 #include <set>
@@ -59,8 +60,25 @@ public:
     bool txindex = false, addressindex = false, spentindex = false, timestampindex = false;
     Uint256 best_block;
 
-    void connect(const Block& block, int height, const Uint256& hash, const BlockUndo& undo);
+    // `file` / `data_pos`: where the block's data lives (blk file, offset after the framing); the
+    // txindex records of the change journal address transactions by them (CDiskTxPos), -1 = none.
+    void connect(const Block& block, int height, const Uint256& hash, const BlockUndo& undo, int file = -1,
+                 u32 data_pos = 0);
     void disconnect(const Block& block, int height, const Uint256& hash, const BlockUndo& undo);
+
+    // Change journal in the reference's blocks/index record layout (CBlockTreeDB, txdb.cpp:250-440):
+    // 't' txid -> CDiskTxPos, 'a' CAddressIndexKey -> amount, 'u' CAddressUnspentKey ->
+    // CAddressUnspentValue, 'p' CSpentIndexKey -> CSpentIndexValue, 's' CTimestampIndexKey -> 0,
+    // 'z' block hash -> timestamp. With `journal` on, connect / disconnect append every record they
+    // add (value) or remove (nullopt); take_changes() hands them over for one write batch.
+    bool journal = false;
+    using Change = std::pair<std::string, std::optional<std::string>>;
+    std::vector<Change> take_changes() { return std::move(changes_); }
+    size_t pending_changes() const { return changes_.size(); }
+    // Rebuilds the resident maps from such records (`tx_block_at` maps a (file, data_pos) to the
+    // block hash stored there). False on a malformed record.
+    bool load_records(const std::function<void(const std::function<void(const std::string&, const std::string&)>&)>& scan,
+                      const std::function<bool(int, u32, Uint256*)>& tx_block_at);
 
     const Uint256* tx_block(const Uint256& txid) const;
     // asset "*" = every asset; start/end = inclusive height range (0, 0 = all)
@@ -100,6 +118,13 @@ private:
             return a.second == b.second && std::memcmp(a.first.data, b.first.data, 32) == 0;
         }
     };
+    void rec_put(std::string k, std::string v) {
+        if (journal) changes_.emplace_back(std::move(k), std::move(v));
+    }
+    void rec_erase(std::string k) {
+        if (journal) changes_.emplace_back(std::move(k), std::nullopt);
+    }
+    std::vector<Change> changes_;
     std::unordered_map<Uint256, Uint256, U256Hash, U256Eq> tx_;
     std::map<Key, std::vector<AddrDelta>> deltas_;
     std::map<Key, std::map<std::pair<Uint256, u32>, AddrUnspent>> unspent_;

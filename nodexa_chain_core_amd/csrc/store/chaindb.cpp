@@ -96,9 +96,66 @@ CoinsLoad coins_load(CoinsView& view, ldb::DB& db, const std::string& obf) {
     return r;
 }
 
-size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sync) {
+namespace {
+const std::string kAssetsBest = "\x02" "assets.best";
+
+void put_str(std::string& s, const std::string& v) {
+    Writer w;
+    w.compact_size(v.size());
+    s.append(reinterpret_cast<const char*>(w.buf.data()), w.buf.size());
+    s += v;
+}
+}  // namespace
+
+bool assets_load(assets::State& st, ldb::DB& db, const std::string& obf) {
+    st.reset();
+    std::string v;
+    if (!db.get(kAssetsBest, &v)) return false;
+    xor_obf(v, obf);
+    if (v.size() != 32) return false;
+    bool ok = true;
+    db.scan("\x01", "\x02", [&](const std::string& k, const std::string& val) {
+        try {
+            if (k.size() < 2) throw std::runtime_error("short key");
+            Reader r(reinterpret_cast<const u8*>(k.data()) + 2, k.size() - 2);
+            const Bytes a = r.var_bytes(), bb = r.var_bytes();
+            std::string dv = val;
+            xor_obf(dv, obf);
+            if (!r.empty() || !st.load_entry(u8(k[1]), std::string(a.begin(), a.end()), std::string(bb.begin(), bb.end()),
+                                             Bytes(dv.begin(), dv.end())))
+                ok = false;
+        } catch (const std::exception&) {
+            ok = false;
+        }
+        return ok;
+    });
+    st.best_block = Uint256::from_bytes(reinterpret_cast<const u8*>(v.data()));
+    st.clear_dirty();
+    return ok;
+}
+
+size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sync, assets::State* assets) {
     ldb::WriteBatch b;
     size_t n = 0;
+    if (assets) {
+        assets->for_each_dirty([&](u8 kind, const std::string& a, const std::string& k, const Bytes* val) {
+            std::string key(1, '\x01');
+            key.push_back(char(kind));
+            put_str(key, a);
+            put_str(key, k);
+            if (val) {
+                std::string v(val->begin(), val->end());
+                if (v.empty()) v = "\x01";  // set members: a present marker
+                xor_obf(v, obf);
+                b.put(key, v);
+            } else {
+                b.del(key);
+            }
+        });
+        std::string best(reinterpret_cast<const char*>(assets->best_block.data), 32);
+        xor_obf(best, obf);
+        b.put(kAssetsBest, best);
+    }
     view.for_each_dirty([&](const OutPoint& o, const Coin* c) {
         if (c) {
             std::string v = bytes_str(serialize_coin_db(*c));
@@ -115,6 +172,7 @@ size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sy
     b.del("H");
     db.write(b, sync);
     view.clear_dirty();
+    if (assets) assets->clear_dirty();
     return n;
 }
 
@@ -214,6 +272,65 @@ std::vector<DiskIndex> load_block_index(ldb::DB& db, const std::string& obf, u32
     });
     if (bad) *bad = nbad;
     return out;
+}
+
+namespace {
+const std::string kIndexBest = std::string("\x00nodexa.indexes.best", 20);
+const char kIndexPrefixes[] = {'t', 'a', 'u', 'p', 's', 'z'};
+}  // namespace
+
+size_t indexes_flush(ChainIndexes& ix, ldb::DB& db, const std::string& obf, bool sync) {
+    ldb::WriteBatch b;
+    auto ch = ix.take_changes();
+    for (auto& c : ch) {
+        if (c.second) {
+            std::string v = std::move(*c.second);
+            xor_obf(v, obf);
+            b.put(c.first, v);
+        } else {
+            b.del(c.first);
+        }
+    }
+    std::string best(reinterpret_cast<const char*>(ix.best_block.data), 32);
+    xor_obf(best, obf);
+    b.put(kIndexBest, best);
+    db.write(b, sync);
+    return ch.size();
+}
+
+bool indexes_load(ChainIndexes& ix, ldb::DB& db, const std::string& obf,
+                  const std::function<bool(int, u32, Uint256*)>& block_at, bool* have_best) {
+    std::string v;
+    *have_best = false;
+    if (db.get(kIndexBest, &v)) {
+        xor_obf(v, obf);
+        if (v.size() == 32) {
+            ix.best_block = Uint256::from_bytes(reinterpret_cast<const u8*>(v.data()));
+            *have_best = true;
+        }
+    }
+    return ix.load_records(
+        [&](const std::function<void(const std::string&, const std::string&)>& f) {
+            for (char p : kIndexPrefixes)
+                db.scan(std::string(1, p), std::string(1, char(p + 1)), [&](const std::string& k, const std::string& val) {
+                    std::string dv = val;
+                    xor_obf(dv, obf);
+                    f(k, dv);
+                    return true;
+                });
+        },
+        block_at);
+}
+
+void indexes_purge(ldb::DB& db) {
+    ldb::WriteBatch b;
+    for (char p : kIndexPrefixes)
+        db.scan(std::string(1, p), std::string(1, char(p + 1)), [&](const std::string& k, const std::string&) {
+            b.del(k);
+            return true;
+        });
+    b.del(kIndexBest);
+    db.write(b, true);
 }
 
 std::string encode_file_info(const FileInfo& f) {

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../chain/coins.hpp"
+#include "../chain/indexes.hpp"
 #include "ldb.hpp"
 
 namespace nodexa {
@@ -35,8 +36,14 @@ struct CoinsLoad {
 // CCoinsViewDB load: every 'C' record into the view (replacing its contents) and 'B'.
 CoinsLoad coins_load(CoinsView& view, ldb::DB& db, const std::string& obf);
 // CCoinsViewDB::BatchWrite: the view's change set (puts and erases) plus 'B' in one synced
-// batch; clears the change set. Returns the number of coin records written or erased.
-size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sync);
+// batch; clears the change set. Returns the number of coin records written or erased. With
+// `assets`, the asset state's changed entries and its best block go into the same batch
+// (this engine's keys: 0x01 kind name key -> value, "\x02assets.best"), so the UTXO set and the
+// asset state on disk always describe the same block.
+size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sync,
+                   assets::State* assets = nullptr);
+// the asset state from those records; false if they are malformed or absent
+bool assets_load(assets::State& st, ldb::DB& db, const std::string& obf);
 std::string coin_key(const OutPoint& o);
 
 // CDiskBlockIndex
@@ -65,6 +72,15 @@ std::string encode_disk_index(const DiskIndex& d, u32 kawpow_time, int client_ve
 bool decode_disk_index(const std::string& v, u32 kawpow_time, DiskIndex* d);
 // every 'b' record, de-obfuscated and decoded (hash from the key), in key order
 std::vector<DiskIndex> load_block_index(ldb::DB& db, const std::string& obf, u32 kawpow_time, size_t* bad);
+
+// Optional indexes (-txindex/-addressindex/-spentindex/-timestampindex) in blocks/index: the
+// journal of `ix` plus the block it describes ("\x00nodexa.indexes.best", this engine's key) in
+// one batch; the load rebuilds the resident maps ('t' positions resolved through `block_at`).
+size_t indexes_flush(ChainIndexes& ix, ldb::DB& db, const std::string& obf, bool sync);
+bool indexes_load(ChainIndexes& ix, ldb::DB& db, const std::string& obf,
+                  const std::function<bool(int, u32, Uint256*)>& block_at, bool* have_best);
+// drops every index record (a rebuild with other flags)
+void indexes_purge(ldb::DB& db);
 
 struct FileInfo {
     u32 blocks = 0, size = 0, undo_size = 0, height_first = 0, height_last = 0;

@@ -164,3 +164,48 @@ def test_reference_library_reads_chain_stores(tmp_path, ref_tool):
         keys = [line.split(" ")[0] for line in r.stdout.splitlines()]
         assert sum(1 for k in keys if k.startswith(prefix)) == (n if n is not None else coins)
         assert "0e006f62667573636174655f6b6579" in keys  # "\x0e\x00obfuscate_key"
+
+
+def test_indexes_persist_as_block_tree_records(tmp_path):
+    from nodexa_chain_core_amd.miner.kawpow_miner import CpuKawpowBackend, MinerController
+
+    flags = dict(txindex=True, addressindex=True, spentindex=True, timestampindex=True)
+    h160 = bytes(range(20))
+    spk = bytes.fromhex("76a914") + h160 + bytes.fromhex("88ac")
+    st = _state(tmp_path, indexes=flags)
+    MinerController(st, [CpuKawpowBackend()]).generate(spk, 4)
+    tip = st.chain.tip()
+    blk = st.get_block(tip.hash)
+    cb = blk.vtx[0].txid()
+    deltas = st.indexes.deltas(1, h160, "*")
+    assert st.indexes.tx_block(cb) == tip.hash and len(deltas) >= 4
+    st.close()
+
+    # reference record layout: 't' txid -> VARINT(file) VARINT(pos) VARINT(offset after the header)
+    db = _core.LevelDB(str(tmp_path / "blocks" / "index"))
+    obf = _core.chaindb_obfuscation_key(db, False)
+    v = _core.chaindb_xor(db.get(b"t" + cb), obf)
+    assert v[0] == 0  # blk00000
+    pos = st.block_pos[tip.hash]
+    raw = open(tmp_path / "blocks" / "blk00000.dat", "rb").read()
+    hdr_len = len(blk.header.serialize(st.params.kawpow_activation_time))
+    off = v[-1]  # one-byte VARINTs here: file, pos (< 128 only for the first blocks) or more bytes
+    assert raw[pos.offset + hdr_len + off: pos.offset + hdr_len + off + 4] == blk.vtx[0].serialize()[:4]
+    # 'a' keys: type, hash160, asset name (CompactSize + "CLORE"), BE height, ...
+    akeys = [k for k, _ in db.items(b"a", b"b")]
+    mine = [k for k in akeys if k[2:22] == h160]  # (the community-fund outputs have their own address)
+    assert len(mine) == len(deltas) and all(k[1] == 1 and k[22:28] == b"\x05CLORE" for k in mine)
+    assert [k for k, _ in db.items(b"s", b"t")] and [k for k, _ in db.items(b"z", b"{")]
+    db.close()
+
+    st2 = _state(tmp_path, indexes=flags)
+    assert st2.indexes.pending_changes == 0  # loaded from the records, not replayed
+    assert st2.indexes.tx_block(cb) == tip.hash
+    assert st2.indexes.deltas(1, h160, "*") == deltas
+    st2.close()
+    # turning an index off and on again rebuilds it (the stored 'F' flags differ)
+    st3 = _state(tmp_path, indexes=dict(flags, txindex=False))
+    st3.close()
+    st4 = _state(tmp_path, indexes=flags)
+    assert st4.indexes.tx_block(cb) == tip.hash and st4.indexes.deltas(1, h160, "*") == deltas
+    st4.close()
