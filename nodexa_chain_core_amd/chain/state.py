@@ -872,6 +872,7 @@ class ChainState:
     def _init_coins(self) -> None:
         """Load the UTXO snapshot and bring it to the best stored chain (ReplayBlocks-lite)."""
         gh = self.chain.genesis().hash
+        self.rebuilt = False
         if self.db_format == "leveldb" and self.coins_path is not None:
             # chainstate/ in the reference's layout (CCoinsViewDB): 'C' coins, 'B' best block
             self.coins_db = _core.LevelDB(os.path.dirname(self.coins_path), write_buffer_size=32 << 20)
@@ -933,6 +934,7 @@ class ChainState:
             self.assets = _core.AssetsState()
             self.indexes = self._new_indexes()
             self.indexes.best_block = gh
+            self.rebuilt = self.coins_path is not None  # start-up replayed the chain from genesis
             if self.coins_db is not None:
                 # drop the stale set: every coin record, then the fresh (empty) state's 'B'
                 stale = [(k, None) for k, _ in self.coins_db.items(b"C", b"D")]

@@ -171,6 +171,7 @@ def test_asset_lifecycle_regtest(core, node_factory):  # noqa: F811
     # restart: the asset state is reloaded with the UTXO snapshot
     node.stop()
     node, _ = node_factory()
+    assert not node.state.rebuilt  # loaded from the stored asset records, not replayed
     c = client(node)
     assert {n: c.getassetdata(n) for n in c.listassets()} == snapshot
     assert c.checkglobalrestriction("$ROSE")

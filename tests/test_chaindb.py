@@ -85,6 +85,7 @@ def test_store_restart_and_records(tmp_path):
     db.close()
 
     st2 = _state(tmp_path)
+    assert not st2.rebuilt  # coins and asset records loaded, nothing replayed
     assert st2.chain.tip().hash == tip and st2.height() == 6
     assert _utxo(st2)[0] == want[0] and _utxo(st2)[1] == want[1]
     _mine(st2, 1)
