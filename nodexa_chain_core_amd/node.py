@@ -537,7 +537,10 @@ class Node:
         self.rpc = RPCServer(self.table, host, port, creds, a.get_int("rpcworkqueue", 16),
                              rest=self.rest if a.get_bool("rest", False) else None,  # -rest (DEFAULT_REST_ENABLE=false)
                              rpcauth=a.get_list("rpcauth"), allow=parse_allow_subnets(a.get_list("rpcallowip")),
-                             threads=a.get_int("rpcthreads", 4), idle_timeout=float(a.get("rpcservertimeout", "30")))
+                             threads=a.get_int("rpcthreads", 4), idle_timeout=float(a.get("rpcservertimeout", "30")),
+                             # -webgui: the wallet page at http://<rpcbind>:<rpcport>/gui (on by default)
+                             gui=os.path.join(os.path.dirname(os.path.abspath(__file__)), "gui", "index.html")
+                             if a.get_bool("webgui", True) else None)
         self.rpc.start()
         log.log_printf(f"RPC listening on {host}:{self.rpc.port}")
 

@@ -235,6 +235,19 @@ class _Handler(http.server.BaseHTTPRequestHandler):
             srv.slots.release()
 
     def do_GET(self):  # noqa: N802
+        # the web wallet (gui/index.html, the Qt GUI's role): behind the RPC credentials like the
+        # JSON-RPC endpoint it talks to
+        if self.path.split("?")[0] in ("/gui", "/gui/", "/gui/index.html") and self.server.gui is not None:
+            srv = self.server
+            if (srv.credentials or srv.rpcauth) and not self._authorized():
+                self.send_response(401)
+                self.send_header("WWW-Authenticate", 'Basic realm="jsonrpc"')
+                self.send_header("Content-Length", "0")
+                self.end_headers()
+                return
+            with open(srv.gui, "rb") as f:
+                self._send(200, f.read(), "text/html; charset=utf-8")
+            return
         # REST subset (src/rest.cpp:569-580): /rest/chaininfo.json
         if self.path.startswith("/rest/") and self.server.rest is not None:
             try:
@@ -255,8 +268,9 @@ class RPCHTTPServer(socketserver.ThreadingMixIn, http.server.HTTPServer):
 
     def __init__(self, addr, table: RPCTable, credentials: list[str], work_queue: int, rest=None,
                  rpcauth: list[str] | None = None, allow: list | None = None, threads: int = 4,
-                 idle_timeout: float = 30.0):
+                 idle_timeout: float = 30.0, gui: str | None = None):
         super().__init__(addr, _Handler)
+        self.gui = gui  # path of the web wallet page, or None (-webgui=0)
         self.table = table
         self.credentials = credentials
         self.rpcauth = list(rpcauth or [])
