@@ -451,8 +451,21 @@ void bind_extra(py::module_& m) {
         .def("check_header", &HeaderChain::check_header, py::call_guard<py::gil_scoped_release>())
         .def("accept_header", &HeaderChain::accept_header, py::arg("header"), py::arg("adjusted_time"), py::arg("check_pow") = true,
              py::call_guard<py::gil_scoped_release>())
-        .def("accept_headers", &HeaderChain::accept_headers, py::arg("headers"), py::arg("adjusted_time"), py::arg("check_pow") = true,
-             py::call_guard<py::gil_scoped_release>())
+        .def("accept_headers",
+             [](HeaderChain& c, const std::vector<BlockHeader>& hs, int64_t adjusted_time, bool check_pow,
+                const py::object& hashes) {
+                 std::vector<Uint256> known;
+                 if (!hashes.is_none()) {  // n x 32 bytes, storage order
+                     const std::string b = hashes.cast<py::bytes>();
+                     if (b.size() != hs.size() * 32) throw std::invalid_argument("hashes: expected 32 bytes per header");
+                     known.resize(hs.size());
+                     for (size_t i = 0; i < hs.size(); ++i)
+                         known[i] = Uint256::from_bytes(reinterpret_cast<const u8*>(b.data()) + 32 * i);
+                 }
+                 py::gil_scoped_release rel;
+                 return c.accept_headers(hs, adjusted_time, check_pow, known.empty() ? nullptr : &known);
+             },
+             py::arg("headers"), py::arg("adjusted_time"), py::arg("check_pow") = true, py::arg("hashes") = py::none())
         .def("tip", &HeaderChain::tip, py::return_value_policy::reference_internal)
         .def("genesis", &HeaderChain::genesis, py::return_value_policy::reference_internal)
         .def("at_height", &HeaderChain::at_height, py::return_value_policy::reference_internal)

@@ -271,7 +271,7 @@ void parallel_for(size_t n, F&& fn) {
 // wait for header i-1 to be indexed. The serial pass then does the index updates and
 // the remaining contextual checks. Results are identical to accepting one by one.
 std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHeader>& hs, int64_t adjusted_time,
-                                                      bool check_pow) {
+                                                      bool check_pow, const std::vector<Uint256>* known_hashes) {
     std::lock_guard<std::recursive_mutex> g(mu_);
     const size_t n = hs.size();
     std::vector<AcceptResult> out;
@@ -285,8 +285,12 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
         parallel_for(n, [&](size_t i) { pre[i] = check_header(hs[i], true); });
     }
     if (n >= kParallelAcceptMin) {
-        hashes.resize(n);
-        parallel_for(n, [&](size_t i) { hashes[i] = verifier_->block_hash(hs[i], params_); });
+        if (known_hashes && known_hashes->size() == n) {
+            hashes = *known_hashes;
+        } else {
+            hashes.resize(n);
+            parallel_for(n, [&](size_t i) { hashes[i] = verifier_->block_hash(hs[i], params_); });
+        }
         auto pit = index_.find(hs[0].prev);
         bool linear = pit != index_.end();
         for (size_t i = 1; linear && i < n; ++i) linear = hs[i].prev == hashes[i - 1];

@@ -61,8 +61,10 @@ public:
     AcceptResult check_header(const BlockHeader& h, bool check_pow) const;
     AcceptResult accept_header(const BlockHeader& h, int64_t adjusted_time, bool check_pow = true);
     // Accepts headers in order; stops at the first failure (ProcessNewBlockHeaders).
+    // `known_hashes` (one per header, storage order): block hashes the caller already has (the
+    // batch PoW stage computes them), so the host does not hash the batch again.
     std::vector<AcceptResult> accept_headers(const std::vector<BlockHeader>& hs, int64_t adjusted_time,
-                                             bool check_pow = true);
+                                             bool check_pow = true, const std::vector<Uint256>* known_hashes = nullptr);
 
     const HeaderIndex* tip() const;
     const HeaderIndex* genesis() const { return genesis_; }

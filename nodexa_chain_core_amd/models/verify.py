@@ -20,6 +20,7 @@ import os
 import time
 
 import numpy as np
+from collections.abc import Sequence
 
 from .. import core
 from ..utils.trace import traced
@@ -42,6 +43,73 @@ def verify_headers(params, headers, gpus: list[int] | None = None, threads: int 
     return _verify_native(params, hs, gpus, threads, mode)
 
 
+class VerifyResults(Sequence):
+    """verify_headers' per-header {"valid", "hash", "reason"?} dicts, built on access: the KawPow
+    rows stay as arrays (validity, reason code, 32-byte final hash) so a 10k-header batch costs
+    no per-header Python work unless a caller looks at the entries; `first_invalid()` is one
+    array scan. Entries of other header kinds (high-hash prefilter, Equihash, X16R) are stored
+    as dicts in `extra`."""
+
+    REASONS = ("", "invalid-mix-hash", "high-hash")
+
+    def __init__(self, n: int):
+        self.n = n
+        self.valid = np.zeros(n, dtype=bool)
+        self.code = np.zeros(n, dtype=np.uint8)   # index into REASONS for array-held rows
+        self.held = np.zeros(n, dtype=bool)       # row i lives in the arrays
+        self.final = np.zeros((n, 32), dtype=np.uint8)
+        self.extra: dict[int, dict] = {}
+        # block hashes (storage order) the PoW stage produced, for the contextual stage
+        self.block_hash = np.zeros((n, 32), dtype=np.uint8)
+        self.has_hash = np.zeros(n, dtype=bool)
+
+    def set(self, i: int, d: dict, block_hash: bytes | None = None) -> None:
+        self.extra[i] = d
+        self.held[i] = False
+        self.valid[i] = bool(d.get("valid"))
+        if block_hash is not None:
+            self.block_hash[i] = np.frombuffer(block_hash, dtype=np.uint8)
+            self.has_hash[i] = True
+
+    def hashes_blob(self, upto: int) -> bytes | None:
+        """The first `upto` block hashes as one n x 32 blob, or None if any is missing."""
+        if upto and self.has_hash[:upto].all():
+            return np.ascontiguousarray(self.block_hash[:upto]).tobytes()
+        return None
+
+    def __len__(self) -> int:
+        return self.n
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(self.n))]
+        if i < 0:
+            i += self.n
+        if not 0 <= i < self.n:
+            raise IndexError(i)
+        if not self.held[i]:
+            return self.extra.get(i, {})
+        d = {"valid": bool(self.valid[i]), "hash": self.final[i].tobytes().hex()}
+        if self.code[i]:
+            d["reason"] = self.REASONS[self.code[i]]
+        return d
+
+    def first_invalid(self) -> int:
+        bad = np.flatnonzero(~self.valid)
+        return int(bad[0]) if len(bad) else self.n
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, (list, tuple, VerifyResults)) and list(self) == list(other)
+
+    __hash__ = None
+
+
+def first_invalid(res) -> int:
+    if isinstance(res, VerifyResults):
+        return res.first_invalid()
+    return next((i for i, r in enumerate(res) if not r["valid"]), len(res))
+
+
 def _rows_le(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Row-wise big-endian a <= b over (m, 32) uint8 arrays (ethash is_less_or_equal)."""
     diff = a != b
@@ -62,11 +130,14 @@ def _verify_native(params, headers, gpus, threads: int, mode: str, rows_fn=None)
         kinds_b, jobs_b, mix_b, bound_b, pre_b = _core.kawpow_batch_prepare(list(headers),
                                                                             params.kawpow_activation_time)
     kinds = np.frombuffer(kinds_b, dtype=np.uint8)
-    out: list[dict] = [{} for _ in range(n)]
+    out = VerifyResults(n)
     pre = np.frombuffer(pre_b, dtype=np.uint8).reshape(n, 32)
-    for i in np.flatnonzero(kinds == 1).tolist():
-        out[i] = {"valid": False, "reason": "high-hash", "hash": pre[i].tobytes().hex()}
+    hp = np.flatnonzero(kinds == 1)  # failed the mix-only prefilter: high hash, already final
+    out.held[hp], out.code[hp], out.final[hp] = True, 2, pre[hp]
     cand = np.flatnonzero(kinds == 0)
+    kp = np.flatnonzero(kinds <= 1)  # KawPow: the mix-only final hash is the block hash (byte-reversed)
+    out.block_hash[kp] = pre[kp, ::-1]
+    out.has_hash[kp] = True
     t1 = t2 = time.perf_counter()
     if len(cand):
         jobs = np.frombuffer(jobs_b, dtype=np.uint8).reshape(n, 48)[cand]
@@ -78,15 +149,10 @@ def _verify_native(params, headers, gpus, threads: int, mode: str, rows_fn=None)
         mix_ok = (res[:, :32] == np.frombuffer(mix_b, dtype=np.uint8).reshape(n, 32)[cand]).all(axis=1)
         fin = np.ascontiguousarray(res[:, 32:])
         le = _rows_le(fin, np.frombuffer(bound_b, dtype=np.uint8).reshape(n, 32)[cand])
-        hexes = fin.tobytes().hex()
-        for k, i in enumerate(cand.tolist()):
-            hx = hexes[64 * k: 64 * k + 64]
-            if not mix_ok[k]:
-                out[i] = {"valid": False, "reason": "invalid-mix-hash", "hash": hx}
-            elif not le[k]:
-                out[i] = {"valid": False, "reason": "high-hash", "hash": hx}
-            else:
-                out[i] = {"valid": True, "hash": hx}
+        out.held[cand] = True
+        out.final[cand] = fin
+        out.valid[cand] = mix_ok & le
+        out.code[cand] = np.where(mix_ok, np.where(le, 0, 2), 1)
     t3 = time.perf_counter()
     eq = np.flatnonzero(kinds == 2).tolist()
     if eq:
@@ -164,8 +230,8 @@ def _verify_x16r(params, headers, idxs: list[int], out: list[dict], threads: int
     with cf.ThreadPoolExecutor(max_workers=threads or (os.cpu_count() or 4)) as ex:
         for i, hsh in zip(idxs, ex.map(one, idxs)):
             ok = _core.check_proof_of_work(hsh, headers[i].bits, params)
-            out[i] = {"valid": bool(ok), "hash": _core.u256_hex(hsh)} if ok else \
-                {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(hsh)}
+            out.set(i, {"valid": bool(ok), "hash": _core.u256_hex(hsh)} if ok else
+                    {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(hsh)}, hsh)
 
 
 def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, threads: int) -> None:
@@ -201,11 +267,11 @@ def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, th
         h = headers[i]
         hsh = hashes.get(i) or h.equihash_hash(act)
         if not ok[i]:
-            out[i] = {"valid": False, "reason": "invalid-solution", "hash": _core.u256_hex(hsh)}
+            out.set(i, {"valid": False, "reason": "invalid-solution", "hash": _core.u256_hex(hsh)}, hsh)
         elif not _core.check_proof_of_work(hsh, h.bits, params):
-            out[i] = {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(hsh)}
+            out.set(i, {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(hsh)}, hsh)
         else:
-            out[i] = {"valid": True, "hash": _core.u256_hex(hsh)}
+            out.set(i, {"valid": True, "hash": _core.u256_hex(hsh)}, hsh)
 
 
 @traced("verify.process_headers")
@@ -221,10 +287,12 @@ def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None =
     pow_res = verify_fn(chain.params, headers) if verify_fn is not None else \
         verify_headers(chain.params, headers, gpus=gpus, mode=mode)
     t1 = time.perf_counter()
-    first_bad = next((i for i, r in enumerate(pow_res) if not r["valid"]), len(headers))
+    first_bad = first_invalid(pow_res)
     accepted, reject = 0, None
-    # contextual checks of the PoW-valid prefix in one native call (GIL released)
-    for ar in chain.accept_headers(list(headers[:first_bad]), adjusted_time, False):
+    # contextual checks of the PoW-valid prefix in one native call (GIL released), with the block
+    # hashes the PoW stage already computed
+    known = pow_res.hashes_blob(first_bad) if isinstance(pow_res, VerifyResults) else None
+    for ar in chain.accept_headers(list(headers[:first_bad]), adjusted_time, False, known):
         if not ar.ok:
             reject = {"index": accepted, "reason": ar.reject}
             break

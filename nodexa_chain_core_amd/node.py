@@ -668,7 +668,7 @@ class Node:
         """Full PoW verification of a header batch (models/verify.py picks GPU or CPU)."""
         from .models import verify
 
-        return verify.verify_headers(self.params, headers, gpus=self.gpus)
+        return list(verify.verify_headers(self.params, headers, gpus=self.gpus))
 
     def equihash_solve(self, inp: bytes) -> list[list[int]]:
         if self.gpus:
