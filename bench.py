@@ -78,19 +78,23 @@ def _verify_headers_bench(log) -> dict | None:
     for mode in ("dag", "light"):
         fn = functools.partial(verify_headers_distributed, mode=mode)
         t0 = time.perf_counter()
-        warm = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn)  # every epoch's state
+        dev = W.get().device
+        dgw_dev = dev.index if dev.type == "cuda" else None  # DGW nBits of the batch from the GPU kernel
+        warm = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn,
+                               dgw_device=dgw_dev)  # every epoch's state
         torch.cuda.synchronize()
         setup = W.all_reduce_max(time.perf_counter() - t0)
         W.barrier()
         t0 = time.perf_counter()
-        r = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn)
+        r = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn, dgw_device=dgw_dev)
         torch.cuda.synchronize()
         W.barrier()
         dt = W.all_reduce_max(time.perf_counter() - t0)
         if r["accepted"] != n or warm["accepted"] != n:
             raise SystemExit(f"header verify ({mode}): accepted {r['accepted']}/{n}, first reject {r['reject']}")
         out[mode] = {"headers_per_s": round(n / dt, 1), "ms": round(dt * 1e3, 2), "pow_ms": round(r["pow_s"] * 1e3, 2),
-                     "context_ms": round(r["context_s"] * 1e3, 2), "first_run_incl_epoch_setup_s": round(setup, 3)}
+                     "context_ms": round(r["context_s"] * 1e3, 2), "dgw_on_gpu": r["dgw_gpu"],
+                     "first_run_incl_epoch_setup_s": round(setup, 3)}
         log(f"[bench] verify {n} headers ({mode}): {n / dt:.0f} headers/s")
     return out
 

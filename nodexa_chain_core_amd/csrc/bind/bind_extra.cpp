@@ -45,6 +45,26 @@ ArithU256 int_to_arith(const py::int_& v) {
 void bind_extra(py::module_& m) {
     m.attr("EQUIHASH_VERSION_BIT") = kEquihashVersionBit;
 
+    // The constants the GPU DarkGravityWave kernel (hip/kernels/dgw.hip) needs, from the params.
+    m.def("dgw_constants", [](const ChainParams& p) {
+        const ConsensusParams& c = p.consensus;
+        const Uint256 eq = c.equihash_limit.is_null() ? c.pow_limit : c.equihash_limit;
+        std::vector<u32> limits;
+        for (const Uint256* u : {&c.pow_limit, &c.kawpow_limit, &eq})
+            for (int i = 0; i < 8; ++i) limits.push_back(load_le32(u->data + 4 * i));
+        std::vector<u32> compacts = {ArithU256::from_uint256(c.pow_limit).get_compact(),
+                                     ArithU256::from_uint256(c.kawpow_limit).get_compact(),
+                                     ArithU256::from_uint256(eq).get_compact()};
+        py::dict d;
+        d["dgw_activation_block"] = p.dgw_activation_block;
+        d["kawpow_time"] = p.kawpow_activation_time;
+        d["equihash_time"] = p.equihash_activation_time;
+        d["limits"] = limits;
+        d["compacts"] = compacts;
+        d["target_timespan"] = u32(kDgwPastBlocks * c.pow_target_spacing);
+        return d;
+    });
+
     // ------------------------------------------------ batch header verification (models/verify.py)
     // One pass over a header batch: for every KawPow header the 48-byte job record the GPU
     // verify kernels read (header hash progpow order, nonce64, height), its claimed mix and
@@ -453,8 +473,9 @@ void bind_extra(py::module_& m) {
              py::call_guard<py::gil_scoped_release>())
         .def("accept_headers",
              [](HeaderChain& c, const std::vector<BlockHeader>& hs, int64_t adjusted_time, bool check_pow,
-                const py::object& hashes) {
+                const py::object& hashes, const py::object& bits) {
                  std::vector<Uint256> known;
+                 std::vector<u32> kbits;
                  if (!hashes.is_none()) {  // n x 32 bytes, storage order
                      const std::string b = hashes.cast<py::bytes>();
                      if (b.size() != hs.size() * 32) throw std::invalid_argument("hashes: expected 32 bytes per header");
@@ -462,10 +483,32 @@ void bind_extra(py::module_& m) {
                      for (size_t i = 0; i < hs.size(); ++i)
                          known[i] = Uint256::from_bytes(reinterpret_cast<const u8*>(b.data()) + 32 * i);
                  }
+                 if (!bits.is_none()) {  // n little-endian u32
+                     const std::string b = bits.cast<py::bytes>();
+                     if (b.size() != hs.size() * 4) throw std::invalid_argument("bits: expected 4 bytes per header");
+                     kbits.resize(hs.size());
+                     std::memcpy(kbits.data(), b.data(), b.size());
+                 }
                  py::gil_scoped_release rel;
-                 return c.accept_headers(hs, adjusted_time, check_pow, known.empty() ? nullptr : &known);
+                 return c.accept_headers(hs, adjusted_time, check_pow, known.empty() ? nullptr : &known,
+                                         kbits.empty() ? nullptr : &kbits);
              },
-             py::arg("headers"), py::arg("adjusted_time"), py::arg("check_pow") = true, py::arg("hashes") = py::none())
+             py::arg("headers"), py::arg("adjusted_time"), py::arg("check_pow") = true, py::arg("hashes") = py::none(),
+             py::arg("bits") = py::none())
+        .def("dgw_series",
+             [](const HeaderChain& c, const std::vector<BlockHeader>& hs, const py::bytes& hashes) -> py::object {
+                 const std::string b = hashes;
+                 if (b.size() != hs.size() * 32) throw std::invalid_argument("hashes: expected 32 bytes per header");
+                 std::vector<Uint256> hv(hs.size());
+                 for (size_t i = 0; i < hs.size(); ++i) hv[i] = Uint256::from_bytes(reinterpret_cast<const u8*>(b.data()) + 32 * i);
+                 std::vector<u32> times, bits;
+                 size_t a = 0;
+                 int base = 0;
+                 if (!c.dgw_series(hs, hv, times, bits, a, base)) return py::none();
+                 return py::make_tuple(py::bytes(reinterpret_cast<const char*>(times.data()), times.size() * 4),
+                                       py::bytes(reinterpret_cast<const char*>(bits.data()), bits.size() * 4), a, base);
+             },
+             "(times, bits, a, base_height) of a linear batch (u32 little-endian series), or None")
         .def("tip", &HeaderChain::tip, py::return_value_policy::reference_internal)
         .def("genesis", &HeaderChain::genesis, py::return_value_policy::reference_internal)
         .def("at_height", &HeaderChain::at_height, py::return_value_policy::reference_internal)

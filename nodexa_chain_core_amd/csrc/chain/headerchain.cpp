@@ -270,8 +270,37 @@ void parallel_for(size_t n, F&& fn) {
 // (nTime, nBits) pairs, which the batch itself supplies, so header i's retarget does not
 // wait for header i-1 to be indexed. The serial pass then does the index updates and
 // the remaining contextual checks. Results are identical to accepting one by one.
+bool HeaderChain::dgw_series(const std::vector<BlockHeader>& hs, const std::vector<Uint256>& hashes,
+                             std::vector<u32>& times, std::vector<u32>& bits, size_t& a, int& base_height) const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    const size_t n = hs.size();
+    if (n == 0 || hashes.size() != n) return false;
+    auto pit = index_.find(hs[0].prev);
+    bool linear = pit != index_.end();
+    for (size_t i = 1; linear && i < n; ++i) linear = hs[i].prev == hashes[i - 1];
+    const ConsensusParams& c = params_.consensus;
+    if (!linear || (c.pow_allow_min_difficulty_blocks && c.pow_no_retargeting)) return false;
+    const HeaderIndex* base = pit->second;
+    std::vector<const HeaderIndex*> anc;  // base and up to 179 ancestors, newest first
+    for (const HeaderIndex* p = base; p && anc.size() < size_t(kDgwPastBlocks); p = p->prev) anc.push_back(p);
+    a = anc.size();
+    base_height = base->height;
+    times.assign(a + n, 0);
+    bits.assign(a + n, 0);
+    for (size_t k = 0; k < a; ++k) {
+        times[k] = anc[a - 1 - k]->time;
+        bits[k] = anc[a - 1 - k]->bits;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        times[a + i] = hs[i].time;
+        bits[a + i] = hs[i].bits;
+    }
+    return true;
+}
+
 std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHeader>& hs, int64_t adjusted_time,
-                                                      bool check_pow, const std::vector<Uint256>* known_hashes) {
+                                                      bool check_pow, const std::vector<Uint256>* known_hashes,
+                                                      const std::vector<u32>* known_bits) {
     std::lock_guard<std::recursive_mutex> g(mu_);
     const size_t n = hs.size();
     std::vector<AcceptResult> out;
@@ -291,34 +320,28 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
             hashes.resize(n);
             parallel_for(n, [&](size_t i) { hashes[i] = verifier_->block_hash(hs[i], params_); });
         }
-        auto pit = index_.find(hs[0].prev);
-        bool linear = pit != index_.end();
-        for (size_t i = 1; linear && i < n; ++i) linear = hs[i].prev == hashes[i - 1];
-        const ConsensusParams& c = params_.consensus;
-        if (linear && !(c.pow_allow_min_difficulty_blocks && c.pow_no_retargeting)) {
-            const HeaderIndex* base = pit->second;
-            std::vector<const HeaderIndex*> anc;  // base and up to 179 ancestors, newest first
-            for (const HeaderIndex* p = base; p && anc.size() < size_t(kDgwPastBlocks); p = p->prev) anc.push_back(p);
-            const size_t a = anc.size();
-            std::vector<u32> times(a + n), bits(a + n);
-            for (size_t k = 0; k < a; ++k) {
-                times[k] = anc[a - 1 - k]->time;
-                bits[k] = anc[a - 1 - k]->bits;
+        std::vector<u32> times, bits;
+        size_t a = 0;
+        int base_height = 0;
+        if (dgw_series(hs, hashes, times, bits, a, base_height)) {
+            if (known_bits && known_bits->size() == n) {
+                // computed by the caller from the same series (the GPU batch kernel, dgw.hip);
+                // 0 = not a DGW header, left to the serial path
+                expected = *known_bits;
+                for (size_t i = 0; i < n; ++i) have[i] = expected[i] != 0;
+            } else {
+                const u32 limit_compact = ArithU256::from_uint256(params_.consensus.pow_limit).get_compact();
+                expected.resize(n);
+                parallel_for(n, [&](size_t i) {
+                    const int last_height = base_height + int(i);  // height of header i's parent
+                    if (last_height + 1 < params_.dgw_activation_block) return;  // BTC retarget: serial path
+                    expected[i] = last_height < kDgwPastBlocks
+                                      ? limit_compact
+                                      : dgw_average(times.data(), bits.data(), int64_t(a) - 1 + int64_t(i), hs[i].time,
+                                                    params_);
+                    have[i] = 1;
+                });
             }
-            for (size_t i = 0; i < n; ++i) {
-                times[a + i] = hs[i].time;
-                bits[a + i] = hs[i].bits;
-            }
-            const u32 limit_compact = ArithU256::from_uint256(c.pow_limit).get_compact();
-            expected.resize(n);
-            parallel_for(n, [&](size_t i) {
-                const int last_height = base->height + int(i);  // height of header i's parent
-                if (last_height + 1 < params_.dgw_activation_block) return;  // BTC retarget: serial path
-                expected[i] = last_height < kDgwPastBlocks
-                                  ? limit_compact
-                                  : dgw_average(times.data(), bits.data(), int64_t(a) - 1 + int64_t(i), hs[i].time, params_);
-                have[i] = 1;
-            });
         }
     }
     for (size_t i = 0; i < n; ++i) {

@@ -63,8 +63,16 @@ public:
     // Accepts headers in order; stops at the first failure (ProcessNewBlockHeaders).
     // `known_hashes` (one per header, storage order): block hashes the caller already has (the
     // batch PoW stage computes them), so the host does not hash the batch again.
+    // `known_bits` (one per header, 0 = unknown): the DGW nBits of each header, computed by the
+    // caller from dgw_series (the GPU batch kernel hip/kernels/dgw.hip).
     std::vector<AcceptResult> accept_headers(const std::vector<BlockHeader>& hs, int64_t adjusted_time,
-                                             bool check_pow = true, const std::vector<Uint256>* known_hashes = nullptr);
+                                             bool check_pow = true, const std::vector<Uint256>* known_hashes = nullptr,
+                                             const std::vector<u32>* known_bits = nullptr);
+    // The (nTime, nBits) series DarkGravityWave reads for a batch that extends a known header
+    // linearly: up to 180 ancestors of the batch's parent (oldest first, `a` of them) then the
+    // batch. False if the batch is not linear or the network does not retarget with DGW.
+    bool dgw_series(const std::vector<BlockHeader>& hs, const std::vector<Uint256>& hashes, std::vector<u32>& times,
+                    std::vector<u32>& bits, size_t& a, int& base_height) const;
 
     const HeaderIndex* tip() const;
     const HeaderIndex* genesis() const { return genesis_; }

@@ -204,6 +204,22 @@ struct MixOnlyParams {
     uint32_t stride;   // bytes between headers (>= 120)
 };
 
+// Batch DarkGravityWave v3 (dgw.hip): the expected nBits of every header of a linear batch from
+// one (nTime, nBits) series = `a` ancestors of the batch (oldest first) then the n batch headers.
+// out[i] = 0: header i is not a DGW header (BTC-retarget era): the host computes it.
+struct DgwParams {
+    const uint32_t* times;
+    const uint32_t* bits;
+    uint32_t* out;
+    uint32_t a, n;
+    int32_t base_height;           // height of the batch's parent
+    int32_t dgw_activation_block;
+    uint32_t kawpow_time, equihash_time;
+    uint32_t pow_limit[8], kawpow_limit[8], equihash_limit[8];  // little-endian 32-bit limbs
+    uint32_t pow_limit_compact, kawpow_limit_compact, equihash_limit_compact;
+    uint32_t target_timespan;      // 180 x target spacing
+};
+
 struct Sha256dParams {
     const uint8_t* in;
     uint8_t* out;      // n x 32 bytes

@@ -453,6 +453,35 @@ PYBIND11_MODULE(_hip, m) {
         p.n = n;
         k.launch_bytes(dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), &p, sizeof(p));
     });
+    // Batch DarkGravityWave (dgw.hip): limits as 8 little-endian u32 limbs, compacts precomputed.
+    m.def("launch_dgw", [](const Kernel& k, uintptr_t times, uintptr_t bits, uintptr_t out, uint32_t a, uint32_t n,
+                           int32_t base_height, int32_t dgw_activation_block, uint32_t kawpow_time, uint32_t equihash_time,
+                           std::vector<uint32_t> limits, std::vector<uint32_t> compacts, uint32_t target_timespan,
+                           uintptr_t stream) {
+        if (limits.size() != 24 || compacts.size() != 3) throw std::invalid_argument("3 limits of 8 limbs, 3 compacts");
+        if (target_timespan == 0) throw std::invalid_argument("target_timespan must be positive");
+        if (n == 0) return;
+        DgwParams p{};
+        p.times = reinterpret_cast<const uint32_t*>(times);
+        p.bits = reinterpret_cast<const uint32_t*>(bits);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        p.a = a;
+        p.n = n;
+        p.base_height = base_height;
+        p.dgw_activation_block = dgw_activation_block;
+        p.kawpow_time = kawpow_time;
+        p.equihash_time = equihash_time;
+        for (int i = 0; i < 8; ++i) {
+            p.pow_limit[i] = limits[i];
+            p.kawpow_limit[i] = limits[8 + i];
+            p.equihash_limit[i] = limits[16 + i];
+        }
+        p.pow_limit_compact = compacts[0];
+        p.kawpow_limit_compact = compacts[1];
+        p.equihash_limit_compact = compacts[2];
+        p.target_timespan = target_timespan;
+        k.launch_bytes(dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("launch_equihash_verify", [](const Kernel& k, std::vector<uint64_t> h0, uintptr_t msgs, uint32_t input_len,
                                        uint32_t num, uintptr_t sols, uintptr_t out, uintptr_t stream) {
         if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");

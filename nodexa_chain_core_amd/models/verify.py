@@ -274,14 +274,20 @@ def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, th
             out.set(i, {"valid": True, "hash": _core.u256_hex(hsh)}, hsh)
 
 
+DGW_GPU_MIN = 256  # batches from this size get their DGW nBits from the GPU kernel
+
+
 @traced("verify.process_headers")
 def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None = None, mode: str = "auto",
-                    verify_fn=None) -> dict:
+                    verify_fn=None, dgw_device: int | None = None) -> dict:
     """ProcessNewBlockHeaders for a batch (src/validation.cpp:12017-12035): PoW of the whole
     batch in bulk (GPU or all cores), then the contextual rules — nBits == DarkGravityWave,
     MTP, future time, version — header by header on the host chain. Like the reference it
     stops at the first invalid header. Returns counts, the first rejection and stage times.
-    verify_fn(params, headers) replaces the PoW stage (parallel/verify.py: across ranks)."""
+    verify_fn(params, headers) replaces the PoW stage (parallel/verify.py: across ranks).
+    dgw_device (default: the first of `gpus`): the GPU that computes every header's
+    DarkGravityWave nBits in one launch for batches of DGW_GPU_MIN or more (ops/dgw.py); the
+    host stage then only checks them and updates the index."""
 
     t0 = time.perf_counter()
     pow_res = verify_fn(chain.params, headers) if verify_fn is not None else \
@@ -292,7 +298,16 @@ def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None =
     # contextual checks of the PoW-valid prefix in one native call (GIL released), with the block
     # hashes the PoW stage already computed
     known = pow_res.hashes_blob(first_bad) if isinstance(pow_res, VerifyResults) else None
-    for ar in chain.accept_headers(list(headers[:first_bad]), adjusted_time, False, known):
+    prefix = list(headers[:first_bad])
+    if dgw_device is None and gpus:
+        dgw_device = gpus[0]
+    bits = None
+    if dgw_device is not None and known is not None and first_bad >= DGW_GPU_MIN:
+        from ..ops import dgw  # every header's DarkGravityWave nBits in one launch (hip/kernels/dgw.hip)
+
+        bits = dgw.batch_bits(chain, prefix, known, dgw_device)
+    t_dgw = time.perf_counter()
+    for ar in chain.accept_headers(prefix, adjusted_time, False, known, bits):
         if not ar.ok:
             reject = {"index": accepted, "reason": ar.reject}
             break
@@ -300,4 +315,5 @@ def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None =
     if reject is None and first_bad < len(headers):
         reject = {"index": first_bad, "reason": pow_res[first_bad].get("reason", "high-hash")}
     t2 = time.perf_counter()
-    return {"accepted": accepted, "reject": reject, "pow_s": t1 - t0, "context_s": t2 - t1}
+    return {"accepted": accepted, "reject": reject, "pow_s": t1 - t0, "context_s": t2 - t1,
+            "dgw_gpu": bits is not None, "dgw_s": t_dgw - t1}

@@ -115,3 +115,41 @@ def test_distributed_verify_single_rank_gpu():
         W.shutdown()
     assert got == verify_headers(params, batch, gpus=[0], mode="light")
     assert all(r["valid"] for r in got)
+
+
+@pytest.mark.parametrize("fixture", ["testnet_kawpow_10k.hdr", "testnet_mixed_10k.hdr"])
+def test_gpu_dgw_matches_host(core, gpu, fixture):
+    """hip/kernels/dgw.hip against the host's DarkGravityWave: every DGW header of the 10k
+    fixtures (bootstrap, KawPow switch, Equihash switch and overflow eras) gets exactly the nBits
+    the host rules gave it; a tampered nBits is caught as bad-diffbits; process_headers takes
+    the GPU path for the batch."""
+    import os
+    import struct
+
+    import numpy as np
+
+    from nodexa_chain_core_amd.models import synthetic
+    from nodexa_chain_core_amd.models.verify import process_headers
+    from nodexa_chain_core_amd.ops import dgw
+
+    params, headers = synthetic.load(os.path.join(os.path.dirname(__file__), "data", fixture))
+    hs = list(headers)
+    adj = headers[-1].time + 3600
+    ref = core.HeaderChain(params)
+    assert all(r.ok for r in ref.accept_headers(hs, adj, False))
+    hashes = b"".join(ref.block_hash(h) for h in hs)
+    times, bits, a, base = core.HeaderChain(params).dgw_series(hs, hashes)
+    got = dgw.expected_bits(params, times, bits, a, len(hs), base, device=0)
+    have = got != 0
+    assert have.sum() >= len(hs) - 1  # every header with a parent in the DGW era
+    want = np.array([h.bits for h in hs], dtype=np.uint32)
+    assert np.array_equal(got[have], want[have])
+    # accept with the GPU's nBits: same chain; a tampered header is refused at its index
+    c = core.HeaderChain(params)
+    assert all(r.ok for r in c.accept_headers(hs, adj, False, hashes, got.tobytes())) and c.tip().hash == ref.tip().hash
+    bad = bytearray(got.tobytes())
+    struct.pack_into("<I", bad, 4 * 5000, int(got[5000]) ^ 1)
+    rc = core.HeaderChain(params).accept_headers(hs, adj, False, hashes, bytes(bad))
+    assert len(rc) == 5001 and rc[-1].reject == "bad-diffbits"
+    r = process_headers(core.HeaderChain(params), headers, adj, gpus=[0])
+    assert r["accepted"] == len(hs) and r["dgw_gpu"]

@@ -126,6 +126,36 @@ def test_accept_headers_batch_equals_serial(fixture):
     assert all(r.ok for r in d.accept_headers(list(headers[:96]), adj, True))
 
 
+def test_accept_headers_with_precomputed_hashes_and_bits():
+    """The batch path's inputs from the PoW stage / GPU: block hashes and the DGW nBits of each
+    header (`dgw_series` is the series the GPU kernel reads). Correct values give the same chain;
+    a wrong expected nBits is a bad-diffbits reject at that header; 0 leaves it to the host."""
+    import struct
+
+    params, headers = synthetic.load(os.path.join(os.path.dirname(__file__), "data", "testnet_mixed_10k.hdr"))
+    hs = list(headers[:3000])
+    adj = headers[-1].time + 3600
+    ref = _core.HeaderChain(params)
+    assert all(r.ok for r in ref.accept_headers(hs, adj, False))
+    hashes = b"".join(ref.block_hash(h) for h in hs)
+    fresh = _core.HeaderChain(params)
+    times, bits, a, base = fresh.dgw_series(hs, hashes)
+    assert a == 1 and base == 0 and len(times) == len(bits) == 4 * (a + len(hs))
+    assert struct.unpack_from("<I", bits, 4 * (a + 7))[0] == hs[7].bits
+    want = b"".join(struct.pack("<I", h.bits) for h in hs)  # a valid chain carries its expected nBits
+    r = fresh.accept_headers(hs, adj, False, hashes, want)
+    assert all(x.ok for x in r) and fresh.tip().hash == ref.tip().hash
+    wrong = bytearray(want)
+    struct.pack_into("<I", wrong, 4 * 1500, hs[1500].bits ^ 1)
+    c = _core.HeaderChain(params)
+    rc = c.accept_headers(hs, adj, False, hashes, bytes(wrong))
+    assert len(rc) == 1501 and rc[-1].reject == "bad-diffbits"
+    zeros = _core.HeaderChain(params)
+    assert all(x.ok for x in zeros.accept_headers(hs, adj, False, hashes, bytes(4 * len(hs))))
+    with pytest.raises(ValueError):
+        _core.HeaderChain(params).accept_headers(hs, adj, False, hashes[:-1])
+
+
 def test_max_reorg_depth_guard(chain_fixture):
     """-maxreorg (ContextualCheckBlockHeader): with the guard armed a fork from >= 60 blocks
     below the tip is rejected with DoS 10; disarmed it is stored as a side branch."""
