@@ -495,6 +495,44 @@ void bind_extra(py::module_& m) {
              },
              py::arg("headers"), py::arg("adjusted_time"), py::arg("check_pow") = true, py::arg("hashes") = py::none(),
              py::arg("bits") = py::none())
+        .def("accept_headers_summary",
+             [](HeaderChain& c, const std::vector<BlockHeader>& hs, int64_t adjusted_time, bool check_pow,
+                const py::object& hashes, const py::object& bits) {
+                 // accept_headers for large batches without one Python object per header:
+                 // (accepted, reject reason or None, dos)
+                 std::vector<Uint256> known;
+                 std::vector<u32> kbits;
+                 if (!hashes.is_none()) {
+                     const std::string b = hashes.cast<py::bytes>();
+                     if (b.size() != hs.size() * 32) throw std::invalid_argument("hashes: expected 32 bytes per header");
+                     known.resize(hs.size());
+                     for (size_t i = 0; i < hs.size(); ++i)
+                         known[i] = Uint256::from_bytes(reinterpret_cast<const u8*>(b.data()) + 32 * i);
+                 }
+                 if (!bits.is_none()) {
+                     const std::string b = bits.cast<py::bytes>();
+                     if (b.size() != hs.size() * 4) throw std::invalid_argument("bits: expected 4 bytes per header");
+                     kbits.resize(hs.size());
+                     std::memcpy(kbits.data(), b.data(), b.size());
+                 }
+                 std::vector<AcceptResult> r;
+                 {
+                     py::gil_scoped_release rel;
+                     r = c.accept_headers(hs, adjusted_time, check_pow, known.empty() ? nullptr : &known,
+                                          kbits.empty() ? nullptr : &kbits);
+                 }
+                 size_t ok = 0;
+                 while (ok < r.size() && r[ok].ok) ++ok;
+                 py::object why = py::none();
+                 int dos = 0;
+                 if (ok < r.size()) {
+                     why = py::str(r[ok].reject);
+                     dos = r[ok].dos;
+                 }
+                 return py::make_tuple(ok, why, dos);
+             },
+             py::arg("headers"), py::arg("adjusted_time"), py::arg("check_pow") = true, py::arg("hashes") = py::none(),
+             py::arg("bits") = py::none())
         .def("dgw_series",
              [](const HeaderChain& c, const std::vector<BlockHeader>& hs, const py::bytes& hashes) -> py::object {
                  const std::string b = hashes;

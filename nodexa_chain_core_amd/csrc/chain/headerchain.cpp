@@ -55,7 +55,8 @@ HeaderChain::HeaderChain(ChainParams params, std::shared_ptr<const PowVerifier> 
     update_active_chain();
 }
 
-const HeaderIndex* HeaderChain::add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev) {
+const HeaderIndex* HeaderChain::add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev,
+                                              const ArithU256* proof) {
     storage_.emplace_back();
     HeaderIndex& idx = storage_.back();
     idx.hash = hash;
@@ -64,7 +65,7 @@ const HeaderIndex* HeaderChain::add_to_index(const BlockHeader& h, const Uint256
     idx.time = h.time;
     idx.bits = h.bits;
     idx.header = h;
-    idx.chain_work = (prev ? prev->chain_work : ArithU256()) + block_proof(h.bits);
+    idx.chain_work = (prev ? prev->chain_work : ArithU256()) + (proof ? *proof : block_proof(h.bits));
     if (prev) {
         // skip pointer: GetSkipHeight (src/chain.cpp)
         auto invert_low = [](int n) { return n & (n - 1); };
@@ -140,7 +141,8 @@ AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_t
 }
 
 AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256* known_hash, int64_t adjusted_time,
-                                             bool check_pow, const u32* expected_bits, const AcceptResult* precheck) {
+                                             bool check_pow, const u32* expected_bits, const AcceptResult* precheck,
+                                             const ArithU256* proof, const int64_t* prev_mtp) {
     std::lock_guard<std::recursive_mutex> g(mu_);
     AcceptResult r;
     const Uint256 hash = known_hash ? *known_hash : verifier_->block_hash(h, params_);
@@ -200,7 +202,7 @@ AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256
         r.dos = 100;
         return r;
     }
-    if (int64_t(h.time) <= prev->median_time_past()) {
+    if (int64_t(h.time) <= (prev_mtp ? *prev_mtp : prev->median_time_past())) {
         r.reject = "time-too-old";
         return r;
     }
@@ -237,7 +239,7 @@ AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256
         r.dos = 100;
         return r;
     }
-    r.index = add_to_index(h, hash, prev);
+    r.index = add_to_index(h, hash, prev, proof);
     r.ok = true;
     consider_new_header(r.index);
     return r;
@@ -307,7 +309,9 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
     out.reserve(n);
     std::vector<Uint256> hashes;
     std::vector<u32> expected;
-    std::vector<u8> have(n, 0);
+    std::vector<u8> have(n, 0), have_mtp(n, 0);
+    std::vector<ArithU256> proofs;
+    std::vector<int64_t> mtp;
     std::vector<AcceptResult> pre;
     if (n >= kParallelAcceptMin && check_pow) {  // CheckBlockHeader (full PoW) is context-free
         pre.resize(n);
@@ -320,10 +324,27 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
             hashes.resize(n);
             parallel_for(n, [&](size_t i) { hashes[i] = verifier_->block_hash(hs[i], params_); });
         }
+        // context-free per-header work of the serial pass, done up front on all cores: the block
+        // proof (2^256 / (target + 1), a 256-bit division) and, for a linear batch, the median
+        // time past of each header's parent from the batch's own time series
+        proofs.resize(n);
+        parallel_for(n, [&](size_t i) { proofs[i] = block_proof(hs[i].bits); });
         std::vector<u32> times, bits;
         size_t a = 0;
         int base_height = 0;
         if (dgw_series(hs, hashes, times, bits, a, base_height)) {
+            const bool from_genesis = a == size_t(base_height) + 1;  // the series reaches genesis
+            mtp.resize(n);
+            parallel_for(n, [&](size_t i) {
+                const int64_t j = int64_t(a) - 1 + int64_t(i);  // series index of header i's parent
+                if (j < 10 && !from_genesis) return;
+                int64_t w[11];
+                int m = 0;
+                for (int64_t k = j; k >= 0 && m < 11; --k) w[m++] = times[size_t(k)];
+                std::sort(w, w + m);
+                mtp[i] = w[m / 2];
+                have_mtp[i] = 1;
+            });
             if (known_bits && known_bits->size() == n) {
                 // computed by the caller from the same series (the GPU batch kernel, dgw.hip);
                 // 0 = not a DGW header, left to the serial path
@@ -346,7 +367,8 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
     }
     for (size_t i = 0; i < n; ++i) {
         out.push_back(accept_header_impl(hs[i], hashes.empty() ? nullptr : &hashes[i], adjusted_time, check_pow,
-                                         have[i] ? &expected[i] : nullptr, pre.empty() ? nullptr : &pre[i]));
+                                         have[i] ? &expected[i] : nullptr, pre.empty() ? nullptr : &pre[i],
+                                         proofs.empty() ? nullptr : &proofs[i], have_mtp[i] ? &mtp[i] : nullptr));
         if (!out.back().ok) break;
     }
     return out;

@@ -95,8 +95,10 @@ public:
 
 private:
     AcceptResult accept_header_impl(const BlockHeader& h, const Uint256* known_hash, int64_t adjusted_time,
-                                    bool check_pow, const u32* expected_bits, const AcceptResult* precheck);
-    const HeaderIndex* add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev);
+                                    bool check_pow, const u32* expected_bits, const AcceptResult* precheck, const ArithU256* proof = nullptr,
+                                    const int64_t* prev_mtp = nullptr);
+    const HeaderIndex* add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev,
+                                    const ArithU256* proof = nullptr);
     void update_active_chain();
     void set_active_tip(const HeaderIndex* best);
     void consider_new_header(const HeaderIndex* idx);

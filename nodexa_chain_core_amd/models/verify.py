@@ -307,11 +307,9 @@ def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None =
 
         bits = dgw.batch_bits(chain, prefix, known, dgw_device)
     t_dgw = time.perf_counter()
-    for ar in chain.accept_headers(prefix, adjusted_time, False, known, bits):
-        if not ar.ok:
-            reject = {"index": accepted, "reason": ar.reject}
-            break
-        accepted += 1
+    accepted, why, _ = chain.accept_headers_summary(prefix, adjusted_time, False, known, bits)
+    if why is not None:
+        reject = {"index": accepted, "reason": why}
     if reject is None and first_bad < len(headers):
         reject = {"index": first_bad, "reason": pow_res[first_bad].get("reason", "high-hash")}
     t2 = time.perf_counter()

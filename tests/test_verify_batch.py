@@ -124,6 +124,18 @@ def test_accept_headers_batch_equals_serial(fixture):
     # full PoW checked in parallel (check_pow=True) accepts the valid prefix
     d = _core.HeaderChain(params)
     assert all(r.ok for r in d.accept_headers(list(headers[:96]), adj, True))
+    # the batch's median-time-past comes from its own time series: a last header at (or below)
+    # its parent's MTP is refused as one by one (the batch stays linear: nothing follows it)
+    for cut in (12, 3000):
+        hs = list(headers[:cut])
+        e = _core.HeaderChain(params)
+        assert all(r.ok for r in e.accept_headers(hs[:-1], adj, False))
+        mtp = e.tip().median_time_past()
+        late = _copy(hs[-1], act)
+        late.time = mtp
+        f = _core.HeaderChain(params)
+        rf = f.accept_headers(hs[:-1] + [late], adj, False)
+        assert len(rf) == cut and rf[-1].reject == "time-too-old", (cut, rf[-1].reject)
 
 
 def test_accept_headers_with_precomputed_hashes_and_bits():
