@@ -12,7 +12,8 @@ using namespace nodexa;
 void bind_store(py::module_& m) {
     py::class_<ldb::DB>(m, "LevelDB", "A LevelDB-format store directory (blocks/index, chainstate, ...)")
         .def(py::init([](const std::string& path, bool create_if_missing, size_t write_buffer_size, int bloom_bits,
-                         size_t max_file_size, size_t block_size, int l0_trigger, uint64_t level1_bytes) {
+                         size_t max_file_size, size_t block_size, int l0_trigger, uint64_t level1_bytes,
+                         size_t max_open_files) {
                  ldb::Options o;
                  o.create_if_missing = create_if_missing;
                  o.write_buffer_size = write_buffer_size;
@@ -21,11 +22,13 @@ void bind_store(py::module_& m) {
                  o.block_size = block_size;
                  o.l0_compaction_trigger = l0_trigger;
                  o.level1_bytes = level1_bytes;
+                 o.max_open_files = max_open_files;
                  return ldb::DB::open(path, o);
              }),
              py::arg("path"), py::arg("create_if_missing") = true, py::arg("write_buffer_size") = size_t(4) << 20,
              py::arg("bloom_bits") = 10, py::arg("max_file_size") = size_t(2) << 20, py::arg("block_size") = 4096,
-             py::arg("l0_trigger") = 4, py::arg("level1_bytes") = uint64_t(10) << 20)
+             py::arg("l0_trigger") = 4, py::arg("level1_bytes") = uint64_t(10) << 20,
+             py::arg("max_open_files") = size_t(512))
         .def("get",
              [](ldb::DB& db, const py::bytes& k) -> py::object {
                  std::string v;

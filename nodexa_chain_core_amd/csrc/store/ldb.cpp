@@ -844,6 +844,7 @@ void DB::close() {
     }
     if (manifest_fd_ >= 0) ::close(manifest_fd_);
     tables_.clear();
+    table_used_.clear();
     if (lock_fd_ >= 0) ::close(lock_fd_);  // releases the fcntl lock
     log_fd_ = manifest_fd_ = lock_fd_ = -1;
 }
@@ -1016,20 +1017,37 @@ void DB::delete_obsolete() {
         else if (kind == 't') keep = std::find(live.begin(), live.end(), num) != live.end();
         else if (kind == 'x') keep = false;
         if (!keep) {
-            if (kind == 't') tables_.erase(num);
+            if (kind == 't') {
+                tables_.erase(num);
+                table_used_.erase(num);
+            }
             ::unlink((dir_ + "/" + n).c_str());
         }
     }
 }
 
 std::shared_ptr<Table> DB::table(uint64_t number, uint64_t size) {
+    const uint64_t stamp = ++table_clock_;
     auto it = tables_.find(number);
-    if (it != tables_.end()) return it->second;
+    if (it != tables_.end()) {
+        table_used_[number] = stamp;
+        return it->second;
+    }
+    // bounded like the reference's max_open_files: a full chainstate has thousands of tables, each
+    // an open descriptor plus its index and filter blocks; the least recently used one is closed
+    // (a scan that only runs when a table is opened past the bound)
+    if (tables_.size() >= std::max<size_t>(1, opt_.max_open_files)) {
+        auto victim = std::min_element(table_used_.begin(), table_used_.end(),
+                                       [](const auto& a, const auto& b) { return a.second < b.second; });
+        tables_.erase(victim->first);
+        table_used_.erase(victim);
+    }
     std::string path = fname(dir_, number, "ldb");
     struct stat st;
     if (::stat(path.c_str(), &st) != 0) path = fname(dir_, number, "sst");
     auto t = std::make_shared<Table>(path, size);
     tables_[number] = t;
+    table_used_[number] = stamp;
     return t;
 }
 
@@ -1189,6 +1207,7 @@ void DB::compact_level(int level, bool whole) {
     for (const auto* fs : {&in0, &in1})
         for (const FileMeta& m : *fs) {
             tables_.erase(m.number);
+            table_used_.erase(m.number);
             ::unlink(fname(dir_, m.number, "ldb").c_str());
             ::unlink(fname(dir_, m.number, "sst").c_str());
         }

@@ -42,6 +42,7 @@ struct Options {
     int bloom_bits_per_key = 10;          // 0: tables carry no filter block
     int l0_compaction_trigger = 4;
     uint64_t level1_bytes = 10ull << 20;  // level L holds up to level1_bytes x 10^(L-1)
+    size_t max_open_files = 512;          // open table files kept (least recently used closed first)
 };
 
 class WriteBatch {
@@ -126,7 +127,9 @@ private:
     std::map<std::string, MemEntry> mem_;
     size_t mem_bytes_ = 0;
     std::vector<FileMeta> levels_[7];
-    std::map<uint64_t, std::shared_ptr<Table>> tables_;
+    std::map<uint64_t, std::shared_ptr<Table>> tables_;  // open tables (cursors may hold others alive)
+    std::map<uint64_t, uint64_t> table_used_;             // last use stamp of each open table
+    uint64_t table_clock_ = 0;
     size_t compact_cursor_[7] = {0, 0, 0, 0, 0, 0, 0};
     bool closed_ = false;
 };

@@ -176,3 +176,22 @@ def test_we_read_reference_written_store(tmp_path, ref_tool):
     db.close()
     assert bytes.fromhex(_ref(ref_tool, "get", path, stdin=b"mine".hex() + "\n").strip()) == b"1"
     shutil.rmtree(path)
+
+
+def test_bounded_open_tables(tmp_path):
+    """max_open_files: with far more table files than the bound, point reads and scans still see
+    every key (least recently used tables are closed and reopened on demand)."""
+    rng = random.Random(9)
+    path = str(tmp_path / "db")
+    kw = dict(write_buffer_size=8 << 10, max_file_size=4 << 10, level1_bytes=1 << 30, max_open_files=3)
+    db = _core.LevelDB(path, **kw)
+    ref = {}
+    _random_ops(rng, 6000, ref, db)
+    assert sum(db.files_per_level()) > 20
+    for k in sorted(ref)[::5]:
+        assert db.get(k) == ref[k]
+    assert dict(db.items()) == ref
+    db.close()
+    db = _core.LevelDB(path, **kw)
+    assert dict(db.items()) == ref
+    db.close()
