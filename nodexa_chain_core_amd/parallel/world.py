@@ -69,6 +69,9 @@ def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         backend = "nccl" if use_gpu else "gloo"
+        # NODEXA_DIST_BACKEND=gloo: ranks that share one GPU (a multi-rank rehearsal on a 1-GPU box:
+        # RCCL refuses two ranks on one device) exchange through gloo instead
+        backend = os.environ.get("NODEXA_DIST_BACKEND", backend)
         if elastic and use_gpu:
             # a collective that times out must raise to the caller (which aborts the communicator
             # and re-forms the group over the survivors), not make RCCL's watchdog end the process
