@@ -45,9 +45,10 @@
 //   refs   [ni][LEVELS][BUCKETS][EQP_REF_STRIDE] u32
 // Overflowing segments or staging areas drop rows (counted in p.stats per level), and a chain of
 // equal sub-digits longer than EQ_MAX_CHAIN is cut (counted in p.stats[EQP_STAT_CHAIN]); at
-// C = 32 for a mean of 8 rows per segment, 768 staged for a mean of 512 per bucket and 24 for a
-// mean chain of 2, none of them has been seen in any run. The host (ops/equihash.py) re-solves an
-// instance with any such count on the golden solver, so the solution set is exact either way.
+// C = 32 for a mean of 8 rows per segment, 1024 staged for a mean of 512 per bucket and 64 for a
+// mean chain of 2 they are rare (a chain cap of 24 and a candidate cap of 4096 were not: 0.03 % and
+// 0.2 % of nonces, profiles r3zb). The host (ops/equihash.py) re-solves an instance with any such
+// count on the golden solver, so the solution set is exact either way.
 #include "equihash_device.hpp"
 
 #ifndef EQP_BLOCK

@@ -70,7 +70,8 @@ struct KawpowVerifyJob {
 #define EQ_CAP 768  // mean fill 512..537 rows/bucket, max observed 647 over 4096 buckets
 #define EQ_WORDS 8
 #define EQ_LEVELS 9
-#define EQ_MAX_CAND 4096  // ~500-1100 final-round collisions per nonce, almost all duplicate trees
+#define EQ_MAX_CAND 16384  // ~500-1100 final-round collisions per nonce (almost all duplicate trees), 4300-4900
+                          // in ~0.2 % of nonces: a 4096 cap sent those to the host re-solve (profiles r3zb)
 #define EQ_RECON_GROUPS 128  // reconstruct workgroups per instance (grid-stride over candidates)
 #define EQ_MAX_BANKS 8
 #define EQ_MAX_SOL 16

@@ -56,11 +56,12 @@ def main() -> int:
         dt = time.perf_counter() - t0
         solves = batches * inst * nsolv
         fb = sum(sv.fallbacks for sv in solvers)
+        fb_log = [x for sv in solvers for x in sv.fallback_log]
         del solvers
         torch.cuda.empty_cache()
         return {"inst": inst, "groups": groups, "solvers": nsolv, "solves": solves, "solutions": found,
                 "s": round(dt, 4), "ms_per_solve": round(dt / solves * 1e3, 4), "sol_per_s": round(found / dt, 1),
-                "solves_per_s": round(solves / dt, 1), "fallbacks": fb}
+                "solves_per_s": round(solves / dt, 1), "fallbacks": fb, "fallback_log": fb_log}
 
     for rep in range(a.reps):
         for k, c in enumerate(a.configs):
