@@ -183,8 +183,12 @@ def _read_compact_size(b: bytes, off: int) -> tuple[int, int]:
 
 class ChainState:
     def __init__(self, params, datadir: str | None = None, strict_height: bool = False, reindex: bool = False,
-                 indexes: dict | None = None, db_format: str | None = None):
+                 indexes: dict | None = None, db_format: str | None = None, reindex_chainstate: bool = False):
+        """`reindex`: rebuild the block index from the blk files (and the chain state with it);
+        `reindex_chainstate`: keep the block index, rebuild the UTXO set, asset state and indexes by
+        connecting the stored blocks again from genesis (-reindex-chainstate, src/init.cpp:1500)."""
         self.params = params
+        self.reindex_chainstate = reindex_chainstate
         self.chain = _core.HeaderChain(params)
         self.chain.strict_kawpow_height = strict_height
         self.strict_height = strict_height
@@ -873,19 +877,22 @@ class ChainState:
         """Load the UTXO snapshot and bring it to the best stored chain (ReplayBlocks-lite)."""
         gh = self.chain.genesis().hash
         self.rebuilt = False
+        if self.reindex_chainstate and self.coins_path is not None:
+            log.log_printf("-reindex-chainstate: rebuilding the chain state from the stored blocks")
         if self.db_format == "leveldb" and self.coins_path is not None:
             # chainstate/ in the reference's layout (CCoinsViewDB): 'C' coins, 'B' best block
             self.coins_db = _core.LevelDB(os.path.dirname(self.coins_path), write_buffer_size=32 << 20)
             self._coins_obf = _core.chaindb_obfuscation_key(self.coins_db, True)
             r = _core.coins_load_ldb(self.coins, self.coins_db, self._coins_obf)
-            loaded = r["have_best"] and not r["head_blocks"] and not r["bad"]
+            loaded = r["have_best"] and not r["head_blocks"] and not r["bad"] and not self.reindex_chainstate
             if r["head_blocks"] or r["bad"]:
                 log.log_printf(f"chainstate: {'interrupted flush (head blocks)' if r['head_blocks'] else ''}"
                                f"{r['bad']} unreadable coin record(s); rebuilding the UTXO set")
             elif loaded:
                 log.log_printf(f"chainstate: {r['coins']} coins loaded")
         else:
-            loaded = self.coins_path is not None and self.coins.load_with_journal(self.coins_path, self.coins_log)
+            loaded = self.coins_path is not None and not self.reindex_chainstate and \
+                self.coins.load_with_journal(self.coins_path, self.coins_log)
         if loaded and self.coins.replayed:
             log.log_printf(f"UTXO journal: {self.coins.replayed} flush record(s) replayed onto the snapshot")
         if loaded and self.coins_db is not None:
@@ -1137,11 +1144,8 @@ class ChainState:
                 f.flush()
                 os.fsync(f.fileno())
             os.replace(tmp, self.assets_path)
-        if self.db_crash_ratio and random.randrange(self.db_crash_ratio) == 0:
-            # -dbcrashratio (CCoinsViewDB::BatchWrite, src/txdb.cpp:96): die between the two halves
-            # of the flush; start-up must notice the mismatch and replay (feature_dbcrash.py)
-            log.log_printf("Simulating a crash. Goodbye.")
-            os._exit(0)
+        if self.coins_db is None:
+            self._maybe_crash()
         if any(self.index_flags.values()) and self.coins_db is not None:
             # the index changes since the last flush, as blocks/index records (made durable by the
             # synced block-tree write below)
@@ -1157,6 +1161,7 @@ class ChainState:
             # block index records first (their undo positions must be durable before the coins
             # that depend on them), then the UTXO and asset change sets with 'B' in one synced batch
             self.index_log.sync()
+            self._maybe_crash()  # blocks and their index durable, the UTXO set still at the last flush
             _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True, self.assets)
         elif not os.path.exists(self.coins_path):  # first flush of this datadir: start from a snapshot
             self.coins.compact(self.coins_path, self.coins_log)
@@ -1165,6 +1170,23 @@ class ChainState:
             if os.path.getsize(self.coins_log) > max(self.journal_compact_bytes, os.path.getsize(self.coins_path)):
                 self.coins.compact(self.coins_path, self.coins_log)
         self._since_flush = 0
+
+    def _maybe_crash(self) -> None:
+        if self.db_crash_ratio and random.randrange(self.db_crash_ratio) == 0:
+            # -dbcrashratio (CCoinsViewDB::BatchWrite, src/txdb.cpp:96): die between the two halves
+            # of the flush; start-up must notice the mismatch and replay (feature_dbcrash.py)
+            log.log_printf("Simulating a crash. Goodbye.")
+            os._exit(0)
+
+    def chainstate_disk_size(self) -> int:
+        """gettxoutsetinfo.disk_size (CCoinsViewDB::EstimateSize): bytes of the chainstate store."""
+        if self.coins_db is not None:
+            # the tables, plus the write-ahead log that holds what has not reached a table yet
+            d = os.path.dirname(self.coins_path)
+            return int(self.coins_db.disk_bytes) + sum(os.path.getsize(os.path.join(d, f)) for f in os.listdir(d)
+                                                        if f.endswith(".log") and f != "LOG")
+        return sum(os.path.getsize(p) for p in (self.coins_path, self.coins_log, self.assets_path)
+                   if p is not None and os.path.exists(p))
 
     def _update_mempool(self, disconnected, connected) -> None:
         """UpdateMempoolForReorg + removeForBlock: drop what the new blocks confirmed or

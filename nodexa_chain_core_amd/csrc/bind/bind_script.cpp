@@ -310,8 +310,8 @@ void bind_script(py::module_& m) {
         .def("load", &CoinsView::load, py::call_guard<py::gil_scoped_release>())
         .def("stats", [](const CoinsView& v) {
             const auto s = v.stats();
-            return py::make_tuple(s.txouts, s.transactions, s.total, pyb(s.hash.data, 32));
-        }, "(txouts, transactions, total amount, sha256d of the coins in outpoint order)")
+            return py::make_tuple(s.txouts, s.transactions, s.total, pyb(s.hash.data, 32), s.bogosize);
+        }, "(txouts, transactions, total amount, hash_serialized_2, bogosize)")
         .def("outputs_for_scripts", [](const CoinsView& v, const std::vector<py::bytes>& spks) {
             std::set<Bytes> want;
             for (auto& s : spks) want.insert(bytes_of(s));

@@ -252,16 +252,32 @@ void CoinsView::compact(const std::string& snapshot, const std::string& journal)
 }
 
 CoinsView::Stats CoinsView::stats() const {
+    // hash_serialized_2 as GetUTXOStats / ApplyStats define it (src/rpc/blockchain.cpp:1076-1130):
+    // the best block, then per transaction (coins in 'C' key order) its txid, VARINT(height * 2 +
+    // coinbase), per output VARINT(n + 1), the script and VARINT(value), closed by VARINT(0)
     Stats s;
     Writer w;
+    w.u256(best_block);
     const Uint256* last = nullptr;
+    auto close_tx = [&] {
+        if (last) append_varint(w.buf, 0);
+    };
     for (auto& [o, c] : sorted_coins(map_)) {
-        ++s.txouts;
-        if (!last || std::memcmp(last->data, o.hash.data, 32) != 0) ++s.transactions;
+        if (!last || std::memcmp(last->data, o.hash.data, 32) != 0) {
+            close_tx();
+            ++s.transactions;
+            w.u256(o.hash);
+            append_varint(w.buf, u64(c->height) * 2 + (c->coinbase ? 1 : 0));
+        }
         last = &o.hash;
+        ++s.txouts;
         s.total += c->out.value;
-        write_coin_entry(w, o, *c);
+        append_varint(w.buf, u64(o.n) + 1);
+        w.var_bytes(c->out.script_pubkey);
+        append_varint(w.buf, u64(c->out.value));
+        s.bogosize += 32 + 4 + 4 + 8 + 2 + c->out.script_pubkey.size();
     }
+    close_tx();
     sha256d(w.buf.data(), w.buf.size(), s.hash.data);
     return s;
 }

@@ -78,9 +78,9 @@ public:
     u64 journal_seq = 0;      // records written (or replayed) so far
     size_t replayed = 0;      // records applied by the last load_with_journal
     // gettxoutsetinfo: (number of unspent outputs, transactions with unspent outputs, total value,
-    // sha256d over the coins in (txid, n) order).
+    // hash_serialized_2 over the best block and the coins in (txid, n) order, bogosize).
     struct Stats {
-        u64 txouts = 0, transactions = 0;
+        u64 txouts = 0, transactions = 0, bogosize = 0;
         Amount total = 0;
         Uint256 hash;
     };

@@ -134,7 +134,8 @@ class Node:
         indexes = {k: a.get_bool(k, False) for k in ("txindex", "addressindex", "spentindex", "timestampindex")}
         self.state = ChainState(self.params, self.datadir, strict_height=a.get_bool("strictheight", False),
                                 reindex=a.get_bool("reindex", False), indexes=indexes,
-                                db_format=a.get("dbformat") or None)  # -dbformat=leveldb|journal
+                                db_format=a.get("dbformat") or None,  # -dbformat=leveldb|journal
+                                reindex_chainstate=a.get_bool("reindex-chainstate", False))
         for flag, attr in (("maxreorg", "max_reorg_depth"), ("minreorgpeers", "min_reorg_peers"),
                            ("minreorgage", "min_reorg_age")):  # reorg guard knobs (src/init.cpp)
             if a.is_set(flag):

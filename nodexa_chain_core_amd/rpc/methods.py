@@ -534,10 +534,13 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
 
     def rpc_gettxoutsetinfo(p):
         """gettxoutsetinfo — statistics about the UTXO set."""
-        tip = st.coins_tip()
-        txouts, ntx, total, h = st.coins.stats()
+        with st.lock:
+            st.flush()  # FlushStateToDisk first, as the reference does: the stats describe the stored set
+            tip = st.coins_tip()
+            txouts, ntx, total, h, bogo = st.coins.stats()
         return {"height": tip.height, "bestblock": _hex(tip.hash), "transactions": ntx, "txouts": txouts,
-                "bogosize": txouts * 50, "hash_serialized_2": _hex(h), "disk_size": 0, "total_amount": total / 1e8}
+                "bogosize": bogo, "hash_serialized_2": _hex(h), "disk_size": st.chainstate_disk_size(),
+                "total_amount": total / 1e8}
 
     def rpc_getrawmempool(p):
         """getrawmempool ( verbose )"""
