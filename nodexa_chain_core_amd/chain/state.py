@@ -133,10 +133,15 @@ class MempoolEntry:
     fee_delta: int = 0       # prioritisetransaction adjustment (included in `fee`)
     size: int = 0            # serialized size with witness
     sigop_cost: int = -1     # GetTransactionSigOpCost (-1: not computed, e.g. loaded from mempool.dat)
+    bytes_per_sigop: int = 20  # -bytespersigop in force when the entry was made
+    _weight: int = field(default=-1, repr=False, compare=False)
 
     def vsize(self) -> int:
-        base = len(self.tx.serialize(False))
-        return (base * 3 + self.size + 3) // 4
+        """GetTxSize = GetVirtualTransactionSize(weight, sigop cost) (src/policy/policy.cpp): a
+        transaction heavy in signature operations counts as bytes_per_sigop bytes per sigop."""
+        if self._weight < 0:
+            self._weight = len(self.tx.serialize(False)) * 3 + self.size
+        return (max(self._weight, max(0, self.sigop_cost) * self.bytes_per_sigop) + 3) // 4
 
 
 MEMPOOL_DUMP_VERSION = 1
@@ -144,6 +149,8 @@ DEFAULT_MIN_RELAY_TX_FEE = 1_000_000   # sat per kvB (src/validation.h:69)
 DEFAULT_INCREMENTAL_RELAY_FEE = 1000   # sat per kvB (src/policy/policy.h:36)
 DEFAULT_ENABLE_REPLACEMENT = False     # -mempoolreplacement (src/validation.h:163)
 MAX_STANDARD_TX_WEIGHT = 400_000       # src/policy/policy.h:28
+DEFAULT_BYTES_PER_SIGOP = 20           # -bytespersigop (src/policy/policy.h)
+COIN_CACHE_ENTRY_BYTES = 128           # memory of one pending UTXO change (entry + map node), for -dbcache
 MAX_STANDARD_TX_SIGOPS_COST = 80_000 // 5  # MAX_BLOCK_SIGOPS_COST / 5 (src/policy/policy.h)
 MAX_FEE_ESTIMATION_TIP_AGE = 3 * 60 * 60  # src/validation.h (IsCurrentForFeeEstimation)
 # package and expiry limits (src/validation.h:77-85) and the raw-tx fee cap (DEFAULT_TRANSACTION_MAXFEE)
@@ -219,6 +226,7 @@ class ChainState:
         self.descendant_limits = (DEFAULT_DESCENDANT_LIMIT, DEFAULT_DESCENDANT_SIZE_LIMIT * 1000)  # -limitdescendant*
         self.mempool_expiry = DEFAULT_MEMPOOL_EXPIRY * 3600         # -mempoolexpiry (seconds)
         self.max_tx_fee = DEFAULT_TRANSACTION_MAXFEE                # -maxtxfee (absurd-fee cap)
+        self.bytes_per_sigop = DEFAULT_BYTES_PER_SIGOP              # -bytespersigop
         self.block_max_weight = 7_999_000                           # -blockmaxweight
         self.block_max_size: int | None = None                      # -blockmaxsize
         self.block_min_fee_rate = DEFAULT_BLOCK_MIN_TX_FEE          # -blockmintxfee
@@ -237,6 +245,7 @@ class ChainState:
         self.script_threads = min(16, os.cpu_count() or 1)  # -par: script-check threads (CCheckQueue)
         self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
         self.flush_interval = 1000
+        self.coins_cache_bytes = 450 << 20     # -dbcache: flush once the pending UTXO changes pass it
         self.journal_compact_bytes = 64 << 20  # fold coins.log into coins.dat past this size (or the snapshot's)
         self._since_flush = 0
         self.sig_stats = {"gpu_batches": 0, "gpu_sigs": 0, "host_rechecks": 0}
@@ -536,7 +545,8 @@ class ChainState:
         with self.lock:
             new = txid not in self.mempool
             e = MempoolEntry(tx, int(fee) + int(fee_delta), entry_time or self.adjusted_time(),  # GetTime(): mocktime aware
-                             self.chain.height(), int(fee_delta), len(tx.serialize(True)), int(sigop_cost))
+                             self.chain.height(), int(fee_delta), len(tx.serialize(True)), int(sigop_cost),
+                             self.bytes_per_sigop)
             if new:
                 # processTransaction: fee estimates only learn from a node that is current, and not
                 # from replacements or children of pool transactions (validFeeEstimate)
@@ -1125,7 +1135,8 @@ class ChainState:
         self.record_confirmations(block, height)
         self._emit("connect_tip", block, idx, undo)
         self._since_flush += 1
-        if self._since_flush >= self.flush_interval:
+        if self._since_flush >= self.flush_interval or \
+                self.coins.dirty * COIN_CACHE_ENTRY_BYTES > self.coins_cache_bytes:
             self.flush()
         return ValidationState()
 
@@ -1306,7 +1317,7 @@ class ChainState:
             why = self._check_tx_assets(tx, raw, coins, aflags)
             if why:
                 return False, why, 0
-            vsize = (weight + 3) // 4
+            vsize = (max(weight, sigop_cost * self.bytes_per_sigop) + 3) // 4  # GetVirtualTransactionSize
             pool_floor = self.mempool_min_fee() * vsize // 1000
             if pool_floor > 0 and fee < pool_floor:
                 return False, f"mempool min fee not met, {fee} < {pool_floor}", fee

@@ -74,6 +74,7 @@ MAX_ORPHAN_TX_WEIGHT = 400_000            # MAX_STANDARD_TX_WEIGHT
 class Peer:
     def __init__(self, mgr: "ConnectionManager", sock: socket.socket, addr, inbound: bool):
         self.mgr, self.sock, self.addr, self.inbound = mgr, sock, addr, inbound
+        self.whitebind = False  # accepted on a -whitebind socket
         self.id = mgr.next_id()
         self.info: dict = {}
         self.sent_version = False
@@ -113,7 +114,7 @@ class Peer:
     @property
     def whitelisted(self) -> bool:
         """-whitelist: peers from these subnets are never banned and keep tx relay (-whitelistrelay)."""
-        return self.mgr.is_whitelisted(self.addr[0])
+        return self.whitebind or self.mgr.is_whitelisted(self.addr[0])
 
     def misbehaving(self, score: int, why: str) -> None:
         """Misbehaving() / DoS ban score (src/net_processing.cpp): disconnect at 100."""
@@ -183,6 +184,15 @@ class ConnectionManager:
         self._lock = sync.make_lock("cs_vNodes")
         self._id = 0
         self._server: socket.socket | None = None
+        # further listening sockets: (host, port, whitelisted) for extra -bind / -whitebind
+        # addresses; peers accepted on a -whitebind socket are whitelisted whatever their address
+        self.extra_binds: list[tuple[str, int, bool]] = []
+        self._extra_servers: list[socket.socket] = []
+        # -maxreceivebuffer / -maxsendbuffer (x1000 bytes per connection, src/net.h): each peer is
+        # read and answered by its own thread, so a peer's only queues are its socket buffers;
+        # they are sized to these bounds
+        self.max_receive_buffer = 5000 * 1000
+        self.max_send_buffer = 1000 * 1000
         self._stop = threading.Event()
         self.port: int | None = None
         self.sync_lock = sync.make_lock("cs_headers")  # one headers batch is processed at a time
@@ -236,6 +246,14 @@ class ConnectionManager:
             self.port = srv.getsockname()[1]
             threading.Thread(target=self._accept_loop, name="p2p-listen", daemon=True).start()
             log.log_printf(f"P2P listening on {self.listen_addr[0]}:{self.port}")
+        for host, port, white in self.extra_binds:
+            srv = socket.socket(socket.AF_INET6 if ":" in host else socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((host, port))
+            srv.listen(16)
+            self._extra_servers.append(srv)
+            threading.Thread(target=self._accept_loop, args=(srv, white), name="p2p-listen", daemon=True).start()
+            log.log_printf(f"P2P listening on {host}:{srv.getsockname()[1]}{' (whitelisted)' if white else ''}")
         if not self.connect_only and self.max_outbound > 0:
             threading.Thread(target=self._open_connections, name="p2p-opencon", daemon=True).start()
         if self.dns_seeds and not self.connect_only:
@@ -283,16 +301,17 @@ class ConnectionManager:
             except OSError:
                 continue
 
-    def _accept_loop(self) -> None:
+    def _accept_loop(self, srv: socket.socket | None = None, white: bool = False) -> None:
+        srv = srv or self._server
         while not self._stop.is_set():
             try:
-                sock, addr = self._server.accept()
+                sock, addr = srv.accept()
             except OSError:
                 break
-            if not self.network_active or self.is_banned(addr[0]):
+            if not self.network_active or (self.is_banned(addr[0]) and not white):
                 sock.close()  # CConnman::AcceptConnection drops banned / inactive-network peers
                 continue
-            self._add(sock, addr, inbound=True)
+            self._add(sock, addr, inbound=True, whitebind=white)
 
     def connect(self, host: str, port: int, timeout: float = 10.0) -> Peer:
         if not self.network_active:
@@ -369,9 +388,12 @@ class ConnectionManager:
         with self._lock:
             self.local_addrs.pop((host, port), None)
 
-    def _add(self, sock, addr, inbound: bool) -> Peer:
+    def _add(self, sock, addr, inbound: bool, whitebind: bool = False) -> Peer:
         sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, max(4096, self.max_receive_buffer))
+        sock.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, max(4096, self.max_send_buffer))
         p = Peer(self, sock, addr, inbound)
+        p.whitebind = whitebind
         with self._lock:
             self.peers.append(p)
         p.thread.start()
@@ -462,6 +484,8 @@ class ConnectionManager:
             log.log_printf(f"could not write peers.dat / banlist.dat: {e}")
         if self._server is not None:
             self._server.close()
+        for srv in self._extra_servers:
+            srv.close()
         for p in list(self.peers):
             p.close()
 

@@ -40,6 +40,8 @@ _core = core()
 DNS_SEEDS = {"main": ["seed.clore.ai", "seed1.clore.ai", "seed2.clore.ai"], "test": ["testnet.clore.ai"], "regtest": []}
 
 
+DEFAULT_WALLET = "wallet.json"  # -wallet default (the reference: wallet.dat)
+
 class Node:
     def __init__(self, args: ArgsManager):
         self.args = args
@@ -102,6 +104,19 @@ class Node:
                 log.log_printf("Warning: " + hint)
 
     def start(self) -> None:
+        """AppInit: on a start-up error the node shuts down what it had brought up (RPC server,
+        chain state, data-directory lock) before the error propagates, as the reference's
+        Shutdown() after a failed AppInitMain."""
+        try:
+            self._start()
+        except BaseException:
+            try:
+                self.stop()
+            except Exception as e:  # noqa: BLE001 — the start-up error is the one to report
+                log.log_printf(f"shutdown after a failed start: {e}")
+            raise
+
+    def _start(self) -> None:
         a = self.args
         self._check_legacy_flags()
         log.configure(a.get_list("debug"), a.get_list("debugexclude"),
@@ -142,39 +157,55 @@ class Node:
                 setattr(self.params, attr, a.get_int(flag, getattr(self.params, attr)))
         if self.network == "regtest" and a.is_set("blockversion"):  # -blockversion (src/miner.cpp:146-149)
             self.state.block_version_override = a.get_int("blockversion", 0)
-        self.wallet = None
+        self.wallets: dict = {}  # name -> Wallet, in -wallet order (the first is the default)
         if not a.get_bool("disablewallet", False):  # -disablewallet (src/wallet/init.cpp)
             from .wallet import Wallet
 
             from .wallet.history import WalletHistory
 
-            # -bip44 (default on): a new wallet derives from BIP39 words (-mnemonic / -mnemonicpassphrase)
-            self.wallet = Wallet(self.state, self.params,
-                                 os.path.join(self.datadir, "wallet.json") if self.datadir else None,
-                                 bip44=a.get_bool("bip44", True), mnemonic=a.get("mnemonic", "") or "",
-                                 mnemonic_passphrase=a.get("mnemonicpassphrase", "") or "")
-            hist_path = os.path.join(self.datadir, "wallet_txs.json") if self.datadir else None
-            rescan = hist_path is not None and not os.path.exists(hist_path) and bool(self.wallet.keys)
-            rescan = rescan or a.get_bool("rescan", False)  # -rescan: rebuild the history at start-up
-            self.wallet.history = WalletHistory(self.wallet, hist_path)
-            zap = a.get_int("zapwallettxes", 0)
-            if zap:  # -zapwallettxes=1|2: drop every wallet transaction, rescan (1 keeps their metadata)
-                hist = self.wallet.history
-                keep = {t: (w.comment, w.comment_to, w.from_account) for t, w in hist.txs.items()} if zap == 1 else {}
-                hist.txs.clear()
-                methods_wallet.rescan(self)
-                for t, (cm, ct, acct) in keep.items():
-                    w = hist.txs.get(t)
-                    if w is not None:
-                        w.comment, w.comment_to, w.from_account = cm, ct, acct
-                hist.save()
-                log.log_printf(f"Zapped wallet transactions (mode {zap}); {len(hist.txs)} found again by the rescan")
-            elif rescan:
-                methods_wallet.rescan(self)
-            self.state.register(self.wallet.history)
+            from .rpc.protocol import REQUEST_WALLET
+
+            names = a.get_list("wallet") or [DEFAULT_WALLET]
+            for k, name in enumerate(names):  # WalletVerify (src/wallet/init.cpp): plain, distinct file names
+                if os.path.basename(name) != name or name in (".", ".."):
+                    raise SystemExit(f"Error loading wallet {name}. -wallet parameter must only specify a filename (not a path).")
+                if name in names[:k]:
+                    raise SystemExit(f"Error loading wallet {name}. Duplicate -wallet filename specified.")
+            for name in names:
+                wpath, hist_path = self._wallet_paths(name)
+                # -bip44 (default on): a new wallet derives from BIP39 words (-mnemonic /
+                # -mnemonicpassphrase; the default wallet only)
+                first = not self.wallets
+                w = Wallet(self.state, self.params, wpath, bip44=a.get_bool("bip44", True),
+                           mnemonic=(a.get("mnemonic", "") or "") if first else "",
+                           mnemonic_passphrase=(a.get("mnemonicpassphrase", "") or "") if first else "")
+                w.name = name
+                self.wallets[name] = w
+                rescan = hist_path is not None and not os.path.exists(hist_path) and bool(w.keys)
+                rescan = rescan or a.get_bool("rescan", False)  # -rescan: rebuild the history at start-up
+                w.history = WalletHistory(w, hist_path)
+                token = REQUEST_WALLET.set(name)  # rescans below address this wallet
+                try:
+                    zap = a.get_int("zapwallettxes", 0)
+                    if zap:  # -zapwallettxes=1|2: drop every wallet transaction, rescan (1 keeps their metadata)
+                        hist = w.history
+                        keep = {t: (x.comment, x.comment_to, x.from_account) for t, x in hist.txs.items()} if zap == 1 else {}
+                        hist.txs.clear()
+                        methods_wallet.rescan(self)
+                        for t, (cm, ct, acct) in keep.items():
+                            x = hist.txs.get(t)
+                            if x is not None:
+                                x.comment, x.comment_to, x.from_account = cm, ct, acct
+                        hist.save()
+                        log.log_printf(f"Zapped wallet transactions (mode {zap}); {len(hist.txs)} found again by the rescan")
+                    elif rescan:
+                        methods_wallet.rescan(self)
+                finally:
+                    REQUEST_WALLET.reset(token)
+                self.state.register(w.history)
             methods_wallet.register(self.table, self)
             methods_wallet_ext.register(self.table, self)
-        self.asset_wallet = None
+        self._asset_wallets: dict = {}  # wallet name -> AssetWallet, built on first use
         from .wallet.messages import MessageStore
         from .wallet.rewards import MINIMUM_REWARDS_PAYOUT_HEIGHT, Rewards
 
@@ -203,6 +234,10 @@ class Node:
             st.minimum_chain_work = int(a.get("minimumchainwork"), 16)
         st.max_tip_age = a.get_int("maxtipage", st.max_tip_age)
         st.db_crash_ratio = a.get_int("dbcrashratio", 0)
+        st.bytes_per_sigop = a.get_int("bytespersigop", st.bytes_per_sigop)
+        # -dbcache (MiB, src/txdb.h nDefaultDbCache / nMinDbCache / nMaxDbCache): bounds the UTXO
+        # changes held between flushes; a flush also runs every flush_interval blocks
+        st.coins_cache_bytes = min(max(a.get_int("dbcache", 450), 4), 16384) << 20
         # -checkblockindex: off by default here (the reference turns it on for regtest; it is an
         # O(chain) walk per block, so the suites enable it where they test it)
         st.check_block_index_enabled = a.get_bool("checkblockindex", False)
@@ -240,9 +275,8 @@ class Node:
         if a.get("blockmintxfee") is not None:
             st.block_min_fee_rate = round(float(a.get("blockmintxfee")) * coin)
         self.state.require_standard = not a.get_bool("acceptnonstdtxn", not self.state.require_standard)
-        if self.wallet is not None:
-            self.wallet.walletrbf = a.get_bool("walletrbf", False)
-            w = self.wallet  # -paytxfee / -fallbackfee / -txconfirmtarget (amounts in CLORE per kB)
+        for w in self.wallets.values():  # -paytxfee / -fallbackfee / -txconfirmtarget (amounts in CLORE per kB)
+            w.walletrbf = a.get_bool("walletrbf", False)
             if a.get("paytxfee") is not None:
                 w.pay_tx_fee = round(float(a.get("paytxfee")) * 100_000_000)
             if a.get("fallbackfee") is not None:
@@ -304,8 +338,9 @@ class Node:
                     notifier.block_tip(tip.hash[::-1].hex(), initial_download)
 
             self.state.register(_BlockNotify())
-        if self.notifier.wallet and getattr(self, "wallet", None) is not None and self.wallet.history is not None:
-            self.wallet.history.on_change = lambda txid: self.notifier.wallet_tx(txid[::-1].hex())
+        for w in self.wallets.values() if self.notifier.wallet else ():
+            if w.history is not None:
+                w.history.on_change = lambda txid: self.notifier.wallet_tx(txid[::-1].hex())
         stop_at = a.get_int("stopatheight", 0)
         if stop_at > 0:  # -stopatheight (src/validation.cpp:11280): shut down once the tip reaches it
             from .chain.state import ValidationInterface
@@ -435,17 +470,60 @@ class Node:
             log.log_printf("Stopping after block import")
             self.request_shutdown()
 
-    def asset_wallet_instance(self):
-        """The node's AssetWallet, built on first use (shared by the asset, message and reward RPCs)."""
-        if self.wallet is None:
-            from .rpc.protocol import RPC_METHOD_NOT_FOUND, RPCError
+    def _wallet_paths(self, name: str) -> tuple[str | None, str | None]:
+        """Files of wallet `name`: the wallet itself (keys, accounts, labels) and its transaction
+        history, `<name without .json>_txs.json` (wallet.json -> wallet_txs.json)."""
+        if not self.datadir:
+            return None, None
+        stem = name[:-5] if name.endswith(".json") else name
+        return os.path.join(self.datadir, name), os.path.join(self.datadir, stem + "_txs.json")
 
+    def resolve_wallet(self):
+        """GetWalletForJSONRPCRequest + EnsureWalletIsAvailable (src/wallet/rpcwallet.cpp:40-78): the
+        wallet a request's /wallet/<name> endpoint names, the only wallet, or an error."""
+        from .rpc.protocol import (REQUEST_WALLET, RPC_METHOD_NOT_FOUND, RPC_WALLET_NOT_FOUND,
+                                   RPC_WALLET_NOT_SPECIFIED, RPCError)
+
+        if not self.wallets:
             raise RPCError(RPC_METHOD_NOT_FOUND, "Method not found (wallet disabled)")
-        if self.asset_wallet is None:
+        name = REQUEST_WALLET.get()
+        if name:
+            w = self.wallets.get(name)
+            if w is None:
+                raise RPCError(RPC_WALLET_NOT_FOUND, "Requested wallet does not exist or is not loaded")
+            return w
+        if name == "" and len(self.wallets) > 1:
+            raise RPCError(RPC_WALLET_NOT_SPECIFIED,
+                           "Wallet file not specified (must request wallet RPC through /wallet/<filename> uri-path).")
+        return next(iter(self.wallets.values()))  # the only wallet, or the default outside a request
+
+    @property
+    def wallet(self):
+        """The wallet of the current request (see resolve_wallet), None where there is none to
+        name: no wallet loaded, or several and the request did not pick one."""
+        from .rpc.protocol import RPCError
+
+        try:
+            return self.resolve_wallet()
+        except RPCError as e:
+            if e.code == -18:
+                raise
+            return None
+
+    @property
+    def asset_wallet(self):
+        return self._asset_wallets.get(getattr(self.wallet, "name", None))
+
+    def asset_wallet_instance(self):
+        """The request wallet's AssetWallet, built on first use (shared by the asset, message and
+        reward RPCs)."""
+        w = self.resolve_wallet()
+        aw = self._asset_wallets.get(w.name)
+        if aw is None:
             from .wallet.assets import AssetWallet
 
-            self.asset_wallet = AssetWallet(self.wallet)
-        return self.asset_wallet
+            aw = self._asset_wallets[w.name] = AssetWallet(w)
+        return aw
 
     def _start_p2p(self) -> None:
         """-listen / -port / -bind / -connect (CConnman subset, net/p2p.py). Listening is opt-in
@@ -454,18 +532,27 @@ class Node:
         from .net.p2p import ConnectionManager
 
         a = self.args
+        from .net.netbase import parse_host_port
+
         listen = None
-        if a.get_bool("listen", False) or a.is_set("port"):
-            listen = (a.get("bind", "127.0.0.1"), a.get_int("port", self.params.default_port))
+        port = a.get_int("port", self.params.default_port)
+        binds = [parse_host_port(b, port) + (False,) for b in a.get_list("bind")]
+        binds += [parse_host_port(b, port) + (True,) for b in a.get_list("whitebind")]  # -whitebind=addr:port
+        if a.get_bool("listen", False) or a.is_set("port") or binds:
+            first = binds.pop(0) if binds and not binds[0][2] else None
+            listen = (first[0], first[1]) if first else (("127.0.0.1", port) if not binds else None)
         connect = a.get_list("connect")
         seeds, adds = a.get_list("seednode"), a.get_list("addnode")
-        if listen is None and not connect and not seeds and not adds:
+        if listen is None and not binds and not connect and not seeds and not adds:
             return
         self.connman = ConnectionManager(self.state, self.params, gpus=self.gpus, listen=listen,
                                          verify_mode=a.get("p2pverifymode", "auto"), datadir=self.datadir,
                                          connect_only=bool(connect),
                                          max_outbound=a.get_int("maxconnections", 8) if not connect else 0)
         self.connman.proxies.configure(a)
+        self.connman.extra_binds = binds
+        self.connman.max_receive_buffer = a.get_int("maxreceivebuffer", 5000) * 1000
+        self.connman.max_send_buffer = a.get_int("maxsendbuffer", 1000) * 1000
         from .net import protocol as P
         from .rpc.server import parse_allow_subnets
 

@@ -14,24 +14,49 @@ import json
 import os
 import sys
 import time
+import urllib.parse
 
 from ..utils.config import ArgsManager
 
-# (method, param index) pairs whose CLI strings are parsed as JSON
-CONVERT = {
-    ("generate", 0), ("generate", 1), ("generatetoaddress", 0), ("generatetoaddress", 2),
-    ("getblockhash", 0), ("getblock", 1), ("getblockheader", 1), ("getnetworkhashps", 0), ("getnetworkhashps", 1),
-    ("getblocktemplate", 0), ("setgenerate", 0), ("setgenerate", 1), ("getkawpowhash", 3),
-    ("prioritisetransaction", 1), ("prioritisetransaction", 2), ("waitfornewblock", 0), ("verifychain", 0),
-    ("verifychain", 1), ("logging", 0), ("logging", 1), ("getrawmempool", 0), ("verifyheaders", 0),
-    ("sendrawtransaction", 1),
+# params parsed as JSON when given as CLI strings, by method and position: the reference's
+# vRPCConvertParams (src/rpc/client.cpp), plus this engine's verifyheaders
+_CONVERT_POSITIONS = {
+    "issue": (1, 4, 5, 6), "issuerestrictedasset": (1, 5, 6, 7), "issuequalifierasset": (1, 4),
+    "reissuerestrictedasset": (1, 3, 6, 7), "issueunique": (1, 2), "transfer": (1, 4), "transferfromaddress":
+    (2, 5), "transferfromaddresses": (1, 2, 5), "transferqualifier": (2, 5), "reissue": (1, 4, 5),
+    "listmyassets": (1, 2, 3, 4), "listassets": (1, 2, 3), "setmocktime": (0,), "generate": (0, 1),
+    "setgenerate": (0, 1), "generatetoaddress": (0, 2), "getnetworkhashps": (0, 1), "sendtoaddress": (1, 4),
+    "sendfromaddress": (2, 5), "settxfee": (0,), "getreceivedbyaddress": (1,), "getreceivedbyaccount": (1,),
+    "listreceivedbyaddress": (0, 1, 2), "listreceivedbyaccount": (0, 1, 2), "getbalance": (1, 2),
+    "getblockhash": (0,), "waitforblockheight": (0, 1), "waitforblock": (1,), "waitfornewblock": (0,), "move":
+    (2, 3), "sendfrom": (2, 3), "listtransactions": (1, 2, 3), "listaccounts": (0, 1), "walletpassphrase": (1,),
+    "getblocktemplate": (0,), "listsinceblock": (1, 2, 3), "sendmany": (1, 2, 4), "addmultisigaddress": (0, 1),
+    "createmultisig": (0, 1), "listunspent": (0, 1, 2, 3, 4), "getblock": (1,), "getblockheader": (1,),
+    "getchaintxstats": (0,), "gettransaction": (1,), "getrawtransaction": (1,), "createrawtransaction": (0, 1,
+    2, 3), "signrawtransaction": (1, 2), "sendrawtransaction": (1,), "testmempoolaccept": (0, 1),
+    "combinerawtransaction": (0,), "fundrawtransaction": (1,), "gettxout": (1, 2), "gettxoutproof": (0,),
+    "lockunspent": (0, 1), "importprivkey": (2,), "importaddress": (2, 3), "importpubkey": (2,), "importmulti":
+    (0, 1), "verifychain": (0, 1), "pruneblockchain": (0,), "keypoolrefill": (0,), "getrawmempool": (0,),
+    "estimatefee": (0,), "estimatesmartfee": (0,), "estimaterawfee": (0, 1), "prioritisetransaction": (1, 2),
+    "setban": (2, 3), "setnetworkactive": (0,), "getmempoolancestors": (1,), "getmempooldescendants": (1,),
+    "getblockhashes": (1, 2), "getspentinfo": (0,), "getaddresstxids": (0, 1), "getaddressbalance": (0, 1),
+    "getaddressdeltas": (0,), "getaddressutxos": (0,), "getaddressmempool": (0, 1), "bumpfee": (1,), "logging":
+    (0, 1), "disconnectnode": (1,), "echojson": (0, 1, 2, 3, 4, 5, 6, 7, 8, 9), "rescanblockchain": (0, 1),
+    "listaddressesbyasset": (1, 2, 3), "listassetbalancesbyaddress": (1, 2, 3), "sendmessage": (2,),
+    "requestsnapshot": (1,), "getsnapshotrequest": (1,), "listsnapshotrequests": (1,), "cancelsnapshotrequest":
+    (1,), "distributereward": (1, 3), "getdistributestatus": (1, 3), "getsnapshot": (1,), "purgesnapshot": (1,),
+    "stop": (0,), "getkawpowhash": (3,), "verifyheaders": (0,),
 }
+CONVERT = {(m, i) for m, ix in _CONVERT_POSITIONS.items() for i in ix}
 
 
 class RPCClient:
     def __init__(self, host: str = "127.0.0.1", port: int = 19443, user: str | None = None,
-                 password: str | None = None, cookie: str | None = None, timeout: float = 900):
+                 password: str | None = None, cookie: str | None = None, timeout: float = 900,
+                 wallet: str | None = None):
         self.host, self.port, self.timeout = host, port, timeout
+        # -rpcwallet: wallet calls go to /wallet/<name> (multiwallet endpoint, src/wallet/rpcwallet.cpp)
+        self.path = "/" if wallet is None else "/wallet/" + urllib.parse.quote(wallet)
         if cookie and os.path.exists(cookie) and not user:
             with open(cookie) as f:
                 user, _, password = f.read().strip().partition(":")
@@ -45,7 +70,7 @@ class RPCClient:
         headers = {"Content-Type": "application/json"}
         if self.auth:
             headers["Authorization"] = self.auth
-        conn.request("POST", "/", json.dumps(payload), headers)
+        conn.request("POST", self.path, json.dumps(payload), headers)
         r = conn.getresponse()
         body = r.read()
         conn.close()
@@ -97,12 +122,18 @@ def main(argv: list[str] | None = None) -> int:
     datadir = os.path.expanduser(args.get("datadir", "~/.nodexa"))
     if args.network != "main":
         datadir = os.path.join(datadir, "testnet7" if args.network == "test" else "regtest")
+    password = args.get("rpcpassword")
+    stdin_lines = None
+    if args.get_bool("stdinrpcpass", False):  # -stdinrpcpass: the password is the first stdin line
+        stdin_lines = sys.stdin.read().split("\n")
+        password = stdin_lines.pop(0)
     cli = RPCClient(args.get("rpcconnect", "127.0.0.1"), args.get_int("rpcport", params.default_rpc_port),
-                    args.get("rpcuser"), args.get("rpcpassword"),
+                    args.get("rpcuser"), password,
                     os.path.join(datadir, os.path.expanduser(args.get("rpccookiefile", ".cookie"))),
-                    timeout=float(args.get_int("rpcclienttimeout", 900)))
+                    timeout=float(args.get_int("rpcclienttimeout", 900)), wallet=args.get("rpcwallet"))
     if args.get_bool("stdin", False):  # -stdin: one extra argument per input line
-        rest = rest + [line.rstrip("\n") for line in sys.stdin]
+        lines = stdin_lines if stdin_lines is not None else sys.stdin.read().split("\n")
+        rest = rest + (lines[:-1] if lines and lines[-1] == "" else lines)
     method, p = rest[0], rest[1:]
     if args.get_bool("named", False):
         named = {}

@@ -66,9 +66,7 @@ def register(table, node) -> None:
     params = node.params
 
     def wallet():
-        if getattr(node, "wallet", None) is None:
-            raise RPCError(RPC_METHOD_NOT_FOUND, "Method not found (wallet disabled)")
-        return node.wallet
+        return node.resolve_wallet()  # the request's /wallet/<name>, the only wallet, or an RPC error
 
     def _arg(p, i, default=None):
         return p[i] if len(p) > i and p[i] is not None else default

@@ -42,12 +42,7 @@ def register(table, node) -> None:
     node.rescan_abort = rescan_abort
 
     def wallet():
-        w = getattr(node, "wallet", None)
-        if w is None:
-            from .protocol import RPC_METHOD_NOT_FOUND
-
-            raise RPCError(RPC_METHOD_NOT_FOUND, "Method not found (wallet disabled)")
-        return w
+        return node.resolve_wallet()  # the request's /wallet/<name>, the only wallet, or an RPC error
 
     def _arg(p, i, default=None):
         return p[i] if len(p) > i and p[i] is not None else default
@@ -389,7 +384,7 @@ def register(table, node) -> None:
     # ------------------------------------------------------------------ misc
     def rpc_listwallets(p):
         """listwallets"""
-        return ["wallet.json"] if getattr(node, "wallet", None) is not None else []
+        return list(getattr(node, "wallets", {}))
 
     def rpc_resendwallettransactions(p):
         """resendwallettransactions — re-announce the wallet's unconfirmed pool transactions."""

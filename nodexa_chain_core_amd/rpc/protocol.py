@@ -1,9 +1,17 @@
 """JSON-RPC protocol constants and helpers (src/rpc/protocol.h parity)."""
 from __future__ import annotations
 
+import contextvars
+
+# the wallet a JSON-RPC request addresses: None outside a request, "" for the "/" endpoint, the
+# name for "/wallet/<name>" (multiwallet endpoints, src/wallet/rpcwallet.cpp:40-53)
+REQUEST_WALLET: contextvars.ContextVar = contextvars.ContextVar("request_wallet", default=None)
+
 # RPCErrorCode values used by the reference (src/rpc/protocol.h)
 RPC_INVALID_REQUEST = -32600
 RPC_METHOD_NOT_FOUND = -32601
+RPC_WALLET_NOT_FOUND = -18      # the /wallet/<name> endpoint names no loaded wallet
+RPC_WALLET_NOT_SPECIFIED = -19  # several wallets loaded and the request named none
 RPC_INVALID_PARAMS = -32602
 RPC_INTERNAL_ERROR = -32603
 RPC_PARSE_ERROR = -32700

@@ -30,11 +30,12 @@ import secrets
 import socketserver
 import threading
 import time
+import urllib.parse
 from dataclasses import dataclass
 from typing import Callable
 
 from ..utils import log
-from .protocol import (RPC_IN_WARMUP, RPC_INTERNAL_ERROR, RPC_INVALID_PARAMETER, RPC_INVALID_REQUEST,
+from .protocol import (REQUEST_WALLET, RPC_IN_WARMUP, RPC_INTERNAL_ERROR, RPC_INVALID_PARAMETER, RPC_INVALID_REQUEST,
                        RPC_METHOD_NOT_FOUND, RPC_PARSE_ERROR, RPCError, http_status_for, reply)
 
 
@@ -213,7 +214,13 @@ class _Handler(http.server.BaseHTTPRequestHandler):
         if not srv.slots.acquire(blocking=False):
             self._send(503, b"Work queue depth exceeded", "text/plain")
             return
+        path = self.path.split("?")[0]
+        if path != "/" and not path.startswith("/wallet/"):  # the two JSON-RPC handlers the reference registers
+            srv.slots.release()
+            self._send(404, b"", "text/plain")
+            return
         srv.workers.acquire()  # -rpcthreads: requests past the work queue wait for a worker
+        token = REQUEST_WALLET.set(urllib.parse.unquote(path[len("/wallet/"):]) if path != "/" else "")
         try:
             length = int(self.headers.get("Content-Length", "0"))
             raw = self.rfile.read(length)
@@ -231,6 +238,7 @@ class _Handler(http.server.BaseHTTPRequestHandler):
             status = 200 if rep["error"] is None else http_status_for(rep["error"]["code"])
             self._send(status, json.dumps(rep).encode())
         finally:
+            REQUEST_WALLET.reset(token)
             srv.workers.release()
             srv.slots.release()
 

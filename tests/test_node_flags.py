@@ -196,6 +196,30 @@ def test_p2p_flags(core, node_factory, tmp_path):  # noqa: F811
     assert peer_b.misbehavior >= 100 and not a.connman.is_banned("127.0.0.1")
 
 
+def test_whitebind_and_socket_buffers(core, node_factory, tmp_path):  # noqa: F811
+    """-whitebind: peers accepted on that socket are whitelisted whatever their address (and a
+    banned address still gets in there); -bind / -listen keep the ordinary socket; -maxsendbuffer /
+    -maxreceivebuffer size each peer's socket buffers."""
+    import socket
+
+    a, addr = node_factory(("-listen=1", "-bind=127.0.0.1:0", "-whitebind=127.0.0.1:0", "-listenonion=0",
+                            "-maxsendbuffer=200", "-maxreceivebuffer=300"))
+    cm = a.connman
+    white_port = cm._extra_servers[0].getsockname()[1]
+    assert cm.port and white_port != cm.port
+    client(a).generatetoaddress(2, addr)
+    cm.ban("127.0.0.1", 3600)
+    os.makedirs(tmp_path / "b", exist_ok=True)
+    b, _ = node_factory((f"-datadir={tmp_path / 'b'}", f"-connect=127.0.0.1:{white_port}"))
+    assert _wait_for(lambda: client(b).getblockcount() == 2, 20)
+    ca = client(a)
+    assert _wait_for(lambda: ca.getpeerinfo() and ca.getpeerinfo()[0]["whitelisted"] is True)
+    sock = cm.peers[0].sock
+    # Linux doubles the requested size for its bookkeeping (and caps it at wmem_max / rmem_max)
+    assert 2 * 4096 <= sock.getsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF) <= 2 * 200_000
+    assert 2 * 4096 <= sock.getsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF) <= 2 * 300_000
+
+
 def test_cli_stdin_and_rpcwait(core, node_factory, tmp_path, capsys, monkeypatch):  # noqa: F811
     import io
 
