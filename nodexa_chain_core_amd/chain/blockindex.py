@@ -61,6 +61,19 @@ class BlockIndexLog:
         self._f.write(_LEN.pack(len(payload)) + payload + _core.sha256d(payload)[:4])
         self._f.flush()
 
+    def prune_file(self, fi: int) -> list[bytes]:
+        """PruneOneBlockFile (src/validation.cpp:12208-12240): every block stored in blk`fi` loses
+        its data and undo (status bits and positions cleared, the header stays), and the file's
+        CBlockFileInfo is reset. Returns the blocks' hashes."""
+        hit = [h for h, e in self.entries.items() if e[3] == fi and e[1] & (BLOCK_HAVE_DATA | BLOCK_HAVE_UNDO)]
+        for h in hit:
+            e = self.entries[h]
+            e[1] &= ~(BLOCK_HAVE_DATA | BLOCK_HAVE_UNDO)
+            e[3] = e[4] = e[5] = 0
+        self.files[fi] = [0, 0, 0, 0, 0, 0, 0]
+        self.db.write([self._index_op(h) for h in hit] + [self._file_op(fi)])
+        return hit
+
     def rewrite(self, records) -> None:
         """Replace the log (after a full -reindex scan): records of (header bytes, pos, n_tx, ...)."""
         self.close()
@@ -176,6 +189,19 @@ class BlockTreeDB:
             return
         e[1] = (e[1] | BLOCK_FAILED_VALID) if failed else (e[1] & ~(BLOCK_FAILED_VALID | BLOCK_FAILED_CHILD))
         self.db.write([self._index_op(block_hash)])
+
+    def prune_file(self, fi: int) -> list[bytes]:
+        """PruneOneBlockFile (src/validation.cpp:12208-12240): every block stored in blk`fi` loses
+        its data and undo (status bits and positions cleared, the header stays), and the file's
+        CBlockFileInfo is reset. Returns the blocks' hashes."""
+        hit = [h for h, e in self.entries.items() if e[3] == fi and e[1] & (BLOCK_HAVE_DATA | BLOCK_HAVE_UNDO)]
+        for h in hit:
+            e = self.entries[h]
+            e[1] &= ~(BLOCK_HAVE_DATA | BLOCK_HAVE_UNDO)
+            e[3] = e[4] = e[5] = 0
+        self.files[fi] = [0, 0, 0, 0, 0, 0, 0]
+        self.db.write([self._index_op(h) for h in hit] + [self._file_op(fi)])
+        return hit
 
     def rewrite(self, records) -> None:
         """After a full -reindex scan: records of (header bytes, pos, n_tx, height, hash, time)."""

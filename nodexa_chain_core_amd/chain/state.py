@@ -150,6 +150,10 @@ DEFAULT_INCREMENTAL_RELAY_FEE = 1000   # sat per kvB (src/policy/policy.h:36)
 DEFAULT_ENABLE_REPLACEMENT = False     # -mempoolreplacement (src/validation.h:163)
 MAX_STANDARD_TX_WEIGHT = 400_000       # src/policy/policy.h:28
 DEFAULT_BYTES_PER_SIGOP = 20           # -bytespersigop (src/policy/policy.h)
+MIN_BLOCKS_TO_KEEP = 288              # blocks below the tip never pruned (src/validation.h:240)
+MIN_DISK_SPACE_FOR_BLOCK_FILES = 550 << 20  # smallest -prune target (src/validation.h:253)
+PRUNE_AFTER_HEIGHT = {"main": 100_000, "test": 1000, "regtest": 1000}  # nPruneAfterHeight
+BLOCKFILE_CHUNK_SIZE, UNDOFILE_CHUNK_SIZE = 16 << 20, 1 << 20  # headroom FindFilesToPrune keeps
 COIN_CACHE_ENTRY_BYTES = 128           # memory of one pending UTXO change (entry + map node), for -dbcache
 MAX_STANDARD_TX_SIGOPS_COST = 80_000 // 5  # MAX_BLOCK_SIGOPS_COST / 5 (src/policy/policy.h)
 MAX_FEE_ESTIMATION_TIP_AGE = 3 * 60 * 60  # src/validation.h (IsCurrentForFeeEstimation)
@@ -246,6 +250,9 @@ class ChainState:
         self.gpu_signatures = "auto"          # "auto" (GPU when present), "on" or "off" (-gpusigs)
         self.flush_interval = 1000
         self.coins_cache_bytes = 450 << 20     # -dbcache: flush once the pending UTXO changes pass it
+        self.prune_target = 0                  # -prune: 0 off, 1 manual (pruneblockchain), else bytes
+        self.prune_after_height = PRUNE_AFTER_HEIGHT.get(params.network_id, 1000)
+        self._check_for_pruning = False
         self.journal_compact_bytes = 64 << 20  # fold coins.log into coins.dat past this size (or the snapshot's)
         self._since_flush = 0
         self.sig_stats = {"gpu_batches": 0, "gpu_sigs": 0, "host_rechecks": 0}
@@ -417,9 +424,10 @@ class ChainState:
                     pos = _core.BlockPos()
                     pos.file, pos.offset, pos.size = fi, dpos, struct.unpack("<I", frame[4:])[0]
                     self.block_pos[r.index.hash] = pos
-                    self.ntx[r.index.hash] = ntx
                     last = max(last, (fi, dpos, pos.size))
                     n_data += 1
+                if ntx:  # nTx stays with a pruned block's header
+                    self.ntx[r.index.hash] = ntx
                 if status & BLOCK_HAVE_UNDO:
                     self._undo_adopt.append((h, fi, upos))
                 if status & BLOCK_FAILED_VALID:
@@ -847,6 +855,9 @@ class ChainState:
                 return st
             if self.store is not None:
                 self.block_pos[h] = self.store.write(block)
+                if self.prune_target > 1 and self.block_pos[h].file != getattr(self, "_last_blk_file", -1):
+                    self._last_blk_file = self.block_pos[h].file  # a new blk file: look for files to prune
+                    self._check_for_pruning = True
                 self.index_log.append(block.header.serialize(self.params.kawpow_activation_time), self.block_pos[h],
                                       len(block.vtx), height=height, block_hash=h, time=block.header.time)
             else:
@@ -943,6 +954,10 @@ class ChainState:
             else:
                 log.log_printf("chain indexes missing or built with other flags; replaying from genesis")
                 loaded = False
+        if (not loaded or self.chain.find(self.coins.best_block) is None) and self.have_pruned:
+            # replaying from genesis needs every block, and the pruned ones are gone
+            raise SystemExit("Unable to rebuild the chain state: block files were pruned. "
+                             "You will need to rebuild the database using -reindex.")
         if not loaded or self.chain.find(self.coins.best_block) is None:
             if loaded:
                 log.log_printf("UTXO snapshot's best block is unknown; rebuilding the UTXO set from genesis")
@@ -1129,13 +1144,13 @@ class ChainState:
             self.indexes.connect(block, height, idx.hash, undo, bpos.file, bpos.offset)
         else:
             self.indexes.connect(block, height, idx.hash, undo)
-        if aundo:
-            self.asset_undo.write(idx.hash, idx.prev_hash, aundo)
+        if aundo:  # beside the block's file too, so pruning a blk file drops its asset undo with it
+            self.asset_undo.write(idx.hash, idx.prev_hash, aundo, file=bpos.file if bpos is not None else None)
         self.coins.best_block = idx.hash
         self.record_confirmations(block, height)
         self._emit("connect_tip", block, idx, undo)
         self._since_flush += 1
-        if self._since_flush >= self.flush_interval or \
+        if self._since_flush >= self.flush_interval or self._check_for_pruning or \
                 self.coins.dirty * COIN_CACHE_ENTRY_BYTES > self.coins_cache_bytes:
             self.flush()
         return ValidationState()
@@ -1181,6 +1196,94 @@ class ChainState:
             if os.path.getsize(self.coins_log) > max(self.journal_compact_bytes, os.path.getsize(self.coins_path)):
                 self.coins.compact(self.coins_path, self.coins_log)
         self._since_flush = 0
+        if self._check_for_pruning:
+            # FlushStateToDisk -> FindFilesToPrune: only after the UTXO set and the block index
+            # are durable, so no state still needs what the deleted files held
+            self._check_for_pruning = False
+            self.prune_block_files(self.files_to_prune())
+
+    # ------------------------------------------------------------------ pruning
+    @property
+    def prune_mode(self) -> bool:
+        return self.prune_target > 0
+
+    @property
+    def have_pruned(self) -> bool:
+        return bool(self.index_log is not None and hasattr(self.index_log, "flag")
+                    and self.index_log.flag("prunedblockfiles"))
+
+    def _blk_file_bytes(self, fi: int) -> int:
+        n = 0
+        for path in (self.store.path(fi), self.undo._path(fi), self.asset_undo._path(fi)):
+            try:
+                n += os.path.getsize(path)
+            except OSError:
+                pass
+        return n
+
+    def files_to_prune(self, manual_height: int | None = None) -> list[int]:
+        """FindFilesToPrune / FindFilesToPruneManual (src/validation.cpp:12255-12343): blk files
+        (never the one being written) whose highest block is at least MIN_BLOCKS_TO_KEEP below the
+        tip; automatic pruning takes them oldest first until the files, plus a chunk of headroom,
+        fit under the -prune target, manual pruning takes every one at or below `manual_height`."""
+        if not self.prune_mode or self.store is None or not hasattr(self.index_log, "files"):
+            return []
+        tip = self.chain.height()
+        if tip <= self.prune_after_height:
+            return []
+        last_ok = tip - MIN_BLOCKS_TO_KEEP
+        if manual_height is not None:
+            last_ok = min(last_ok, manual_height)
+        current = self.store.current_file()
+        files = sorted(f for f, info in self.index_log.files.items() if f < current and info[0] > 0)
+        if manual_height is not None:
+            return [f for f in files if self.index_log.files[f][4] <= last_ok]
+        if self.prune_target <= 1:
+            return []
+        usage = sum(self._blk_file_bytes(f) for f in range(current + 1))
+        buffer = BLOCKFILE_CHUNK_SIZE + UNDOFILE_CHUNK_SIZE
+        out = []
+        for f in files:
+            if usage + buffer < self.prune_target:
+                break
+            if self.index_log.files[f][4] > last_ok:
+                continue
+            out.append(f)
+            usage -= self._blk_file_bytes(f)
+        return out
+
+    def prune_block_files(self, files: list[int]) -> int:
+        """PruneOneBlockFile + UnlinkPrunedFiles: forget the files' blocks and undo data, mark
+        the store as pruned ('F' prunedblockfiles) and delete blk/rev files. Returns the count."""
+        if not files:
+            return 0
+        with self.lock:
+            self.flush()
+            if not self.have_pruned:
+                self.index_log.set_flag("prunedblockfiles", True)
+            for f in files:
+                for h in self.index_log.prune_file(f):
+                    self.block_pos.pop(h, None)
+                self.index_log.sync()
+                self.undo.drop_file(f)
+                self.asset_undo.drop_file(f)
+                try:
+                    os.remove(self.store.path(f))
+                except OSError:
+                    pass
+                log.log_print("prune", f"Prune: deleted blk/rev ({f:05d})")
+        return len(files)
+
+    def prune_height(self) -> int:
+        """getblockchaininfo.pruneheight: the lowest height from which every active-chain block
+        down from the tip still has its data."""
+        idx = self.chain.tip()
+        while idx.height > 0:
+            prev = self.chain.find(idx.prev_hash)
+            if prev is None or prev.hash not in self.block_pos:
+                break
+            idx = prev
+        return idx.height
 
     def _maybe_crash(self) -> None:
         if self.db_crash_ratio and random.randrange(self.db_crash_ratio) == 0:

@@ -40,8 +40,13 @@ class UndoStore:
         if os.path.exists(idx):
             with open(idx, "rb") as f:
                 data = f.read()
+            present: dict[int, bool] = {}
             for off in range(0, len(data) - len(data) % _IDX.size, _IDX.size):
                 h, fi, fo, size = _IDX.unpack_from(data, off)
+                if fi not in present:
+                    present[fi] = os.path.exists(self._path(fi))
+                if not present[fi]:  # a pruned file: its records are gone
+                    continue
                 self.pos[h] = (fi, fo, size)
                 self.file = max(self.file, fi)
             if len(data) % _IDX.size:  # torn tail from a crash: cut it
@@ -77,6 +82,20 @@ class UndoStore:
         self._idx.write(_IDX.pack(block_hash, file, size + 8, len(undo)))
         self._idx.flush()
         return self.pos[block_hash]
+
+    def drop_file(self, fi: int) -> int:
+        """Pruning: forget every record of file `fi` and delete it; returns the bytes freed."""
+        for h in [h for h, p in self.pos.items() if p[0] == fi]:
+            del self.pos[h]
+        if self.bdir is None:
+            return 0
+        path = self._path(fi)
+        try:
+            n = os.path.getsize(path)
+            os.remove(path)
+            return n
+        except OSError:
+            return 0
 
     def adopt(self, block_hash: bytes, file: int, offset: int) -> bool:
         """Register a record another index located (a reference blocks/index 'b' record's

@@ -588,7 +588,8 @@ void bind_extra(py::module_& m) {
         .def("read", &BlockStore::read)
         .def("scan", [](const BlockStore& s) { py::list l; for (auto& kv : s.scan()) l.append(py::make_tuple(kv.first, pyb(kv.second))); return l; })
         .def("path", &BlockStore::path)
-        .def("current_file", &BlockStore::current_file);
+        .def("current_file", &BlockStore::current_file)
+        .def("set_max_file_size", &BlockStore::set_max_file_size);
 
     // ------------------------------------------------ block validation
     auto bc = [](const BlockCheck& c) { return py::make_tuple(c.ok, c.reject, c.dos); };

@@ -1,9 +1,11 @@
 #include "headerchain.hpp"
 
+#include <dirent.h>
 #include <sys/stat.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <thread>
 #include <unordered_set>
 
@@ -461,20 +463,23 @@ void HeaderChain::reconsider(const Uint256& hash) {
 BlockStore::BlockStore(std::string dir, const u8 magic[4], u32 act) : dir_(std::move(dir)), act_(act) {
     std::memcpy(magic_, magic, 4);
     ::mkdir(dir_.c_str(), 0755);
-    // continue after the last existing file
-    for (;;) {
-        struct stat st;
-        if (::stat(path(file_).c_str(), &st) != 0) break;
-        if (::stat(path(file_ + 1).c_str(), &st) != 0) {
-            file_size_ = u32(st.st_size);
-            break;
+    // continue after the highest-numbered blk file (pruning leaves gaps below it)
+    file_ = -1;
+    if (DIR* d = ::opendir(dir_.c_str())) {
+        while (dirent* e = ::readdir(d)) {
+            int n = -1;
+            char tail = 0;
+            if (std::sscanf(e->d_name, "blk%5d.dat%c", &n, &tail) == 1 && n >= 0 && std::strlen(e->d_name) == 12)
+                file_ = std::max(file_, n);
         }
-        ++file_;
+        ::closedir(d);
     }
-    if (file_ > 0 || file_size_ > 0) {
-        struct stat st;
-        if (::stat(path(file_).c_str(), &st) == 0) file_size_ = u32(st.st_size);
+    if (file_ < 0) {
+        file_ = 0;
+        return;
     }
+    struct stat st;
+    if (::stat(path(file_).c_str(), &st) == 0) file_size_ = u32(st.st_size);
 }
 
 std::string BlockStore::path(int file) const {
@@ -488,7 +493,7 @@ BlockStore::Pos BlockStore::write(const Block& b) { return write_raw(b.bytes(act
 BlockStore::Pos BlockStore::write_raw(const Bytes& data) {
     std::lock_guard<std::mutex> g(mu_);
     const u32 rec = u32(data.size()) + 8;
-    if (file_size_ > 0 && file_size_ + rec > kMaxBlockfileSize) {
+    if (file_size_ > 0 && file_size_ + rec > max_file_) {
         ++file_;
         file_size_ = 0;
     }
@@ -529,9 +534,9 @@ Block BlockStore::read(const Pos& pos) const {
 
 std::vector<std::pair<BlockStore::Pos, Bytes>> BlockStore::scan() const {
     std::vector<std::pair<Pos, Bytes>> out;
-    for (int file = 0;; ++file) {
+    for (int file = 0; file <= file_; ++file) {
         FILE* f = std::fopen(path(file).c_str(), "rb");
-        if (!f) break;
+        if (!f) continue;  // a pruned file
         u32 off = 0;
         for (;;) {
             u8 hdr[8];

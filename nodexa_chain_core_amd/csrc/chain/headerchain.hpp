@@ -126,6 +126,8 @@ public:
     std::vector<std::pair<Pos, Bytes>> scan() const;
     std::string path(int file) const;
     int current_file() const { return file_; }
+    // files roll over past this size (MAX_BLOCKFILE_SIZE; smaller only to exercise pruning)
+    void set_max_file_size(u32 n) { max_file_ = n; }
 
 private:
     std::string dir_;
@@ -133,6 +135,7 @@ private:
     u32 act_;
     int file_ = 0;
     u32 file_size_ = 0;
+    u32 max_file_ = kMaxBlockfileSize;
     mutable std::mutex mu_;
 };
 

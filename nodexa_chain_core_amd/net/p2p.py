@@ -322,7 +322,9 @@ class ConnectionManager:
 
     @property
     def local_services(self) -> int:
-        return P.NODE_NETWORK | P.NODE_WITNESS | (P.NODE_BLOOM if self.peer_bloom_filters else 0)
+        # a pruning node cannot serve the whole chain: no NODE_NETWORK (src/init.cpp, fPruneMode)
+        network = 0 if getattr(self.state, "prune_mode", False) else P.NODE_NETWORK
+        return network | P.NODE_WITNESS | (P.NODE_BLOOM if self.peer_bloom_filters else 0)
 
     def is_whitelisted(self, ip: str) -> bool:
         try:

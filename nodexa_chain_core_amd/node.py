@@ -235,6 +235,7 @@ class Node:
         st.max_tip_age = a.get_int("maxtipage", st.max_tip_age)
         st.db_crash_ratio = a.get_int("dbcrashratio", 0)
         st.bytes_per_sigop = a.get_int("bytespersigop", st.bytes_per_sigop)
+        self._configure_pruning(a)
         # -dbcache (MiB, src/txdb.h nDefaultDbCache / nMinDbCache / nMaxDbCache): bounds the UTXO
         # changes held between flushes; a flush also runs every flush_interval blocks
         st.coins_cache_bytes = min(max(a.get_int("dbcache", 450), 4), 16384) << 20
@@ -469,6 +470,34 @@ class Node:
         if self.args.get_bool("stopafterblockimport", False):
             log.log_printf("Stopping after block import")
             self.request_shutdown()
+
+    def _configure_pruning(self, a) -> None:
+        """-prune=<n> (src/init.cpp AppInitParameterInteraction / AppInitMain): 0 keeps every
+        block, 1 allows pruneblockchain, a larger n is a target in MiB for automatic pruning."""
+        from .chain.state import MIN_DISK_SPACE_FOR_BLOCK_FILES
+
+        st, prune = self.state, a.get_int("prune", 0)
+        if prune < 0:
+            raise SystemExit("Prune cannot be configured with a negative value.")
+        if not prune:
+            if st.have_pruned:
+                raise SystemExit("You need to rebuild the database using -reindex to go back to unpruned mode.  "
+                                 "This will redownload the entire blockchain")
+            return
+        if a.get_bool("txindex", False):
+            raise SystemExit("Prune mode is incompatible with -txindex.")
+        if a.get_bool("rescan", False):
+            raise SystemExit("Rescans are not possible in pruned mode. You will need to use -reindex which will "
+                             "download the whole blockchain again.")
+        if st.store is not None and st.db_format != "leveldb":
+            raise SystemExit("Prune mode needs the LevelDB block index (-dbformat=leveldb).")
+        target = 1 if prune == 1 else prune << 20
+        if prune != 1 and target < MIN_DISK_SPACE_FOR_BLOCK_FILES:
+            raise SystemExit(f"Prune configured below the minimum of {MIN_DISK_SPACE_FOR_BLOCK_FILES >> 20} MiB.  "
+                             "Please use a higher number.")
+        st.prune_target = target
+        st._check_for_pruning = target > 1  # AppInitMain: look once at start-up
+        log.log_printf(f"Prune mode: {'manual (pruneblockchain)' if target == 1 else f'target {prune} MiB'}")
 
     def _wallet_paths(self, name: str) -> tuple[str | None, str | None]:
         """Files of wallet `name`: the wallet itself (keys, accounts, labels) and its transaction

@@ -217,15 +217,21 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
     def rpc_getblockchaininfo(p):
         """getblockchaininfo — state of the chain."""
         tip = st.tip()
-        return {"chain": params.network_id, "blocks": tip.height, "headers": st.chain.height(),
-                "bestblockhash": _hex(tip.hash), "difficulty": _core.difficulty_from_bits(tip.bits),
-                "mediantime": tip.median_time_past(), "verificationprogress": 1.0,
-                "initialblockdownload": st.is_initial_block_download(),
-                "chainwork": "%064x" % tip.chain_work, "size_on_disk": node.blocks_size_on_disk(),
-                "pruned": False, "warnings": "",
-                "bip9_softforks": st.versionbits.bip9_softforks(tip),
-                "kawpow_activation_time": params.kawpow_activation_time,
-                "equihash_activation_time": params.equihash_activation_time}
+        out = {"chain": params.network_id, "blocks": tip.height, "headers": st.chain.height(),
+               "bestblockhash": _hex(tip.hash), "difficulty": _core.difficulty_from_bits(tip.bits),
+               "mediantime": tip.median_time_past(), "verificationprogress": 1.0,
+               "initialblockdownload": st.is_initial_block_download(),
+               "chainwork": "%064x" % tip.chain_work, "size_on_disk": node.blocks_size_on_disk(),
+               "pruned": st.prune_mode, "warnings": "",
+               "bip9_softforks": st.versionbits.bip9_softforks(tip),
+               "kawpow_activation_time": params.kawpow_activation_time,
+               "equihash_activation_time": params.equihash_activation_time}
+        if st.prune_mode:  # src/rpc/blockchain.cpp:1474-1490
+            out["pruneheight"] = st.prune_height()
+            out["automatic_pruning"] = st.prune_target != 1
+            if st.prune_target != 1:
+                out["prune_target_size"] = st.prune_target
+        return out
 
     def rpc_getchaintips(p):
         """getchaintips — the active tip (side branches are tracked by the header chain)."""
@@ -691,7 +697,9 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
 
         cm = _cm()
         return {"version": 40404, "subversion": P.USER_AGENT, "protocolversion": P.PROTOCOL_VERSION,
-                "localservices": "%016x" % (P.NODE_NETWORK | P.NODE_WITNESS), "localrelay": True,
+                "localservices": "%016x" % (cm.local_services if cm is not None else
+                                            (0 if st.prune_mode else P.NODE_NETWORK) | P.NODE_WITNESS),
+                "localrelay": True,
                 "timeoffset": getattr(st, "time_offset", 0), "networkactive": cm is not None, "connections": node.peer_count(),
                 "networks": cm.proxies.describe() if cm is not None else [],
                 "relayfee": 0.00001, "incrementalfee": 0.00001,

@@ -21,6 +21,7 @@ import struct
 import time
 
 from .. import core
+from ..utils import log
 from ..chain.state import _compact_size, _read_compact_size
 from .methods import _arg, _hex, _need, _parse_hash
 from .protocol import (RPC_DESERIALIZATION_ERROR, RPC_INVALID_ADDRESS_OR_KEY, RPC_INVALID_PARAMETER,
@@ -382,8 +383,33 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         return _wait(lambda: st.height() >= h, int(_arg(p, 1, 0)))
 
     def rpc_pruneblockchain(p):
-        """pruneblockchain height — not in prune mode (blk files are kept)."""
-        raise RPCError(RPC_MISC_ERROR, "Cannot prune blocks because node is not in prune mode.")
+        """pruneblockchain height — delete the blk / rev files whose blocks are all at or below
+        `height` (or a unix time: blocks at least 2 hours older), keeping MIN_BLOCKS_TO_KEEP below
+        the tip; returns the height pruned up to (src/rpc/blockchain.cpp:1133-1180)."""
+        from ..chain.state import MIN_BLOCKS_TO_KEEP
+
+        _need(p, 1, "pruneblockchain height")
+        if not st.prune_mode:
+            raise RPCError(RPC_MISC_ERROR, "Cannot prune blocks because node is not in prune mode.")
+        height = int(p[0])
+        if height < 0:
+            raise RPCError(RPC_INVALID_PARAMETER, "Negative block height.")
+        with st.lock:
+            if height > 1_000_000_000:  # a block time, with TIMESTAMP_WINDOW of slack
+                found = next((h for h in range(st.height() + 1) if st.chain.at_height(h).time >= height - 7200), None)
+                if found is None:
+                    raise RPCError(RPC_INVALID_PARAMETER, "Could not find block with at least the specified timestamp.")
+                height = found
+            tip = st.height()
+            if tip < st.prune_after_height:
+                raise RPCError(RPC_MISC_ERROR, "Blockchain is too short for pruning.")
+            if height > tip:
+                raise RPCError(RPC_INVALID_PARAMETER, "Blockchain is shorter than the attempted prune height.")
+            if height > tip - MIN_BLOCKS_TO_KEEP:
+                log.log_print("rpc", "Attempt to prune blocks close to the tip.  Retaining the minimum number of blocks.")
+                height = tip - MIN_BLOCKS_TO_KEEP
+            st.prune_block_files(st.files_to_prune(manual_height=height))
+        return height
 
     def rpc_getblockhashes(p):
         """getblockhashes high low ( {"noOrphans", "logicalTimes"} ) — active-chain blocks with

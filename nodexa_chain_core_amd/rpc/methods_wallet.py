@@ -31,6 +31,9 @@ def rescan(node, start_height: int = 0) -> int:
     """ScanForWalletTransactions: feed every active-chain block from start_height to the wallet
     history; returns the number of wallet transactions found."""
     st, hist = node.state, node.wallet.history
+    if st.prune_mode and st.have_pruned and start_height < st.prune_height():
+        raise RPCError(RPC_MISC_ERROR, "Can't rescan beyond pruned data. Use RPC call getblockchaininfo to "
+                                       "determine your pruned height.")
     n = 0
     abort = getattr(node, "rescan_abort", None)
     if abort is not None:
