@@ -10,24 +10,48 @@ with the 32-byte witness nonce; header: version = ComputeBlockVersion
 nNonce64 = 0, nHeight = tip+1. IncrementExtraNonce (src/miner.cpp:508-525):
 scriptSig = <height> <extranonce>, merkle root recomputed.
 
-Mempool selection: the pool's transactions in arrival order, reordered so that every in-pool
-parent precedes its children (after a reorg, re-accepted parents arrive after their children),
-capped by weight; a transaction whose parent did not fit is left out too. Fee-rate package
-selection (addPackageTxs) is not done.
+Mempool selection: addPackageTxs (src/miner.cpp:380-500) — the transaction whose package (itself
+plus its not-yet-included in-pool ancestors) has the highest fee rate, with prioritisetransaction
+deltas and sigop-adjusted virtual sizes, goes next, its package in parent-first order; including
+a package re-scores every in-pool descendant of it (mapModifiedTx); a package that would break the
+weight, -blockmaxsize or the 80000 sigop-cost limit is skipped (and selection ends after 1000
+consecutive misses with the block nearly full); selection stops at the first package below
+-blockmintxfee.
 """
 from __future__ import annotations
+
+import heapq
 
 import time
 from dataclasses import dataclass
 
 from .. import core
 from ..chain.state import ChainState
+from ..utils import log
 from ..utils.trace import traced
 
 _core = core()
 
 BLOCK_VERSION_ASSETS = 0x30000000
 WITNESS_COMMITMENT_HEADER = bytes([0x6a, 0x24, 0xaa, 0x21, 0xa9, 0xed])
+
+
+MAX_BLOCK_SIGOPS_COST = 80_000   # src/consensus/consensus.h
+MAX_CONSECUTIVE_FAILURES = 1000  # addPackageTxs
+
+
+class _Rate:
+    """Heap key ordering packages by descending fee rate (fee / vsize, compared exactly)."""
+    __slots__ = ("fee", "size")
+
+    def __init__(self, fee: int, size: int):
+        self.fee, self.size = fee, max(1, size)
+
+    def __lt__(self, other: "_Rate") -> bool:
+        return self.fee * other.size > other.fee * self.size
+
+    def __eq__(self, other) -> bool:
+        return self.fee * other.size == other.fee * self.size
 
 
 @dataclass
@@ -64,25 +88,7 @@ class BlockAssembler:
         with st.lock:
             prev = st.tip()
             height = prev.height + 1
-            txs, fees, weight, size = [], 0, 4000, 1000
-            included: set[bytes] = set()
-            for txid in self._parents_first(st.mempool):
-                e = st.mempool[txid]
-                if any(i.prevout.hash in st.mempool and i.prevout.hash not in included for i in e.tx.vin):
-                    continue
-                stripped = len(e.tx.serialize(False))
-                w = stripped * 3 + len(e.tx.serialize(True))
-                if weight + w > self.max_weight:
-                    continue
-                if self.max_size is not None and size + stripped > self.max_size:
-                    continue
-                if e.fee * 1000 < self.min_fee_rate * e.vsize():  # below -blockmintxfee: left out
-                    continue
-                txs.append(e.tx)
-                included.add(txid)
-                fees += e.fee
-                weight += w
-                size += stripped
+            txs, fees = self._select_packages(st)
             subsidy = _core.block_subsidy(height)
             pct = self.params.community_autonomous_pct
             cb = _core.Transaction()
@@ -112,6 +118,85 @@ class BlockAssembler:
             blk.header = hdr
             target, _, _ = _core.set_compact(hdr.bits)
             return BlockTemplate(blk, height, fees, miner.value, community.value, commitment, target, time.time())
+
+    def _select_packages(self, st) -> tuple[list, int]:
+        pool = st.mempool
+        parents = {t: {i.prevout.hash for i in e.tx.vin if i.prevout.hash in pool} for t, e in pool.items()}
+        children: dict[bytes, set] = {t: set() for t in pool}
+        for t, ps in parents.items():
+            for q in ps:
+                children[q].add(t)
+        anc: dict[bytes, frozenset] = {}
+        for t in self._parents_first(pool):  # parents first: their ancestor sets are ready
+            a = set(parents[t])
+            for q in parents[t]:
+                a |= anc[q]
+            anc[t] = frozenset(a)
+        stat = {}
+        for t, e in pool.items():
+            stripped = len(e.tx.serialize(False))
+            stat[t] = (e.fee, e.vsize(), stripped * 3 + len(e.tx.serialize(True)), stripped,
+                       max(0, st.mempool_sigop_cost(t)))
+
+        in_block: set[bytes] = set()
+        failed: set[bytes] = set()
+
+        def score(t):
+            pkg = [q for q in anc[t] if q not in in_block] + [t]
+            return sum(stat[q][0] for q in pkg), sum(stat[q][1] for q in pkg), pkg
+
+        heap = []
+
+        def push(t):
+            fee, vsz, _ = score(t)
+            # CompareTxMemPoolEntryByAncestorFee: higher fee / size first, then the lower txid
+            heapq.heappush(heap, (_Rate(fee, vsz), t, fee, vsz))
+
+        for t in pool:
+            push(t)
+        txs, fees = [], 0
+        weight, size, sigops = 4000, 1000, 400  # coinbase reservation (BlockAssembler::resetBlock)
+        misses = 0
+        while heap:
+            _, t, fee, vsz = heapq.heappop(heap)
+            if t in in_block or t in failed:
+                continue
+            cur_fee, cur_vsz, pkg = score(t)
+            if (cur_fee, cur_vsz) != (fee, vsz):  # stale: an ancestor went into the block since
+                push(t)
+                continue
+            if fee * 1000 < self.min_fee_rate * vsz:  # below -blockmintxfee: nothing better remains
+                break
+            pw = sum(stat[q][2] for q in pkg)
+            ps = sum(stat[q][3] for q in pkg)
+            pso = sum(stat[q][4] for q in pkg)
+            if (weight + pw >= self.max_weight or sigops + pso >= MAX_BLOCK_SIGOPS_COST
+                    or (self.max_size is not None and size + ps >= self.max_size)
+                    or any(q in failed for q in pkg)):
+                failed.add(t)
+                misses += 1
+                if misses > MAX_CONSECUTIVE_FAILURES and weight > self.max_weight - 4000:
+                    break
+                continue
+            misses = 0
+            for q in sorted(pkg, key=lambda q: (len(anc[q]), q)):  # parents before children
+                if getattr(st, "print_priority", False):  # -printpriority
+                    log.log_printf(f"fee {stat[q][0] * 1000 // max(1, stat[q][1])} sat/kvB txid {q[::-1].hex()}")
+                txs.append(pool[q].tx)
+                in_block.add(q)
+                fees += stat[q][0]
+            weight, size, sigops = weight + pw, size + ps, sigops + pso
+            touched: set[bytes] = set()
+            stack = list(pkg)
+            while stack:  # UpdatePackagesForAdded: every in-pool descendant is re-scored
+                for c in children[stack.pop()]:
+                    if c not in touched and c not in in_block:
+                        touched.add(c)
+                        stack.append(c)
+            for c in touched:
+                if c not in failed:
+                    push(c)
+        return txs, fees
 
     @staticmethod
     def _parents_first(pool) -> list[bytes]:

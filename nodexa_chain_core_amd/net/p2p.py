@@ -145,6 +145,10 @@ class Peer:
                 self.mgr.total_recv += P.HEADER_SIZE + len(payload)
                 self.last_recv = time.time()
                 REGISTRY.inc("p2p_bytes_recv_total", P.HEADER_SIZE + len(payload), command=cmd)
+                if self.mgr.drop_messages_test and random.randrange(self.mgr.drop_messages_test) == 0:
+                    # -dropmessagestest=<n> (src/net_processing.cpp:1530)
+                    log.log_printf("dropmessagestest DROPPING RECV MESSAGE")
+                    continue
                 self.mgr.handle(self, cmd, payload)
         except (ConnectionError, OSError, P.ProtocolError, struct.error, ValueError) as e:
             if not self.closed.is_set():
@@ -193,6 +197,8 @@ class ConnectionManager:
         # they are sized to these bounds
         self.max_receive_buffer = 5000 * 1000
         self.max_send_buffer = 1000 * 1000
+        self.drop_messages_test = 0  # -dropmessagestest=<n>: drop 1 in n received messages
+        self.allow_dns = True        # -dns: resolve names given to -addnode / -seednode / -connect
         self._stop = threading.Event()
         self.port: int | None = None
         self.sync_lock = sync.make_lock("cs_headers")  # one headers batch is processed at a time
@@ -316,6 +322,11 @@ class ConnectionManager:
     def connect(self, host: str, port: int, timeout: float = 10.0) -> Peer:
         if not self.network_active:
             raise ConnectionError("network is disabled (setnetworkactive false)")
+        if not self.allow_dns and not host.endswith(".onion"):
+            try:
+                ipaddress.ip_address(host)
+            except ValueError:  # -dns=0: names are not looked up (Lookup's fAllowLookup)
+                raise ConnectionError(f"cannot connect to {host}: DNS lookups are disabled (-dns=0)") from None
         sock = self.proxies.connect(host, port, timeout=timeout)  # direct, or SOCKS5 through the net's proxy
         sock.settimeout(None)
         return self._add(sock, (host, port), inbound=False)

@@ -118,6 +118,8 @@ class Node:
 
     def _start(self) -> None:
         a = self.args
+        if not a.get_bool("sysperms", False):
+            os.umask(0o077)  # files this node creates are private unless -sysperms (src/init.cpp)
         self._check_legacy_flags()
         log.configure(a.get_list("debug"), a.get_list("debugexclude"),
                       os.path.join(self.datadir, "debug.log") if self.datadir else None,
@@ -132,6 +134,7 @@ class Node:
                 f.write(f"{os.getpid()}\n")
         # RPC comes up first in warm-up mode (AppInitServers)
         self.table.warmup = "Loading block index..."
+        self.table.safe_mode = self.observe_safe_mode
         methods.register(self.table, self)
         methods_ext.register(self.table, self)
         if a.get_bool("server", True):
@@ -235,6 +238,7 @@ class Node:
         st.max_tip_age = a.get_int("maxtipage", st.max_tip_age)
         st.db_crash_ratio = a.get_int("dbcrashratio", 0)
         st.bytes_per_sigop = a.get_int("bytespersigop", st.bytes_per_sigop)
+        st.print_priority = a.get_bool("printpriority", False)
         self._configure_pruning(a)
         # -dbcache (MiB, src/txdb.h nDefaultDbCache / nMinDbCache / nMaxDbCache): bounds the UTXO
         # changes held between flushes; a flush also runs every flush_interval blocks
@@ -471,6 +475,40 @@ class Node:
             log.log_printf("Stopping after block import")
             self.request_shutdown()
 
+    def get_warnings(self) -> str:
+        """GetWarnings("rpc") (src/warnings.cpp): -testsafemode, else the unknown-version warning
+        the tip update raises when more than half of the last 100 blocks carry version bits no
+        known deployment sets (src/validation.cpp UpdateTip)."""
+        if self.args.get_bool("testsafemode", False):
+            return "testsafemode enabled"
+        st = self.state
+        if st is None:
+            return ""
+        tip = st.tip()
+        if getattr(self, "_warn_tip", None) != tip.hash:
+            self._warn_tip, self._warn = tip.hash, ""
+            upgraded, idx = 0, tip
+            for _ in range(100):
+                if idx is None or idx.height == 0:
+                    break
+                prev = st.chain.find(idx.prev_hash)
+                v = idx.header.version
+                if (v & 0xE0000000) == 0x20000000 and (v & ~st.versionbits.block_version(prev)) & 0x1FFFFFFF:
+                    upgraded += 1
+                idx = prev
+            if upgraded > 50:
+                self._warn = "Warning: Unknown block versions being mined! It's possible unknown rules are in effect"
+        return self._warn
+
+    def observe_safe_mode(self) -> None:
+        """ObserveSafeMode (src/rpc/safemode.cpp): a standing warning refuses the RPC, unless
+        -disablesafemode."""
+        from .rpc.protocol import RPC_FORBIDDEN_BY_SAFE_MODE, RPCError
+
+        w = self.get_warnings()
+        if w and not self.args.get_bool("disablesafemode", False):
+            raise RPCError(RPC_FORBIDDEN_BY_SAFE_MODE, "Safe mode: " + w)
+
     def _configure_pruning(self, a) -> None:
         """-prune=<n> (src/init.cpp AppInitParameterInteraction / AppInitMain): 0 keeps every
         block, 1 allows pruneblockchain, a larger n is a target in MiB for automatic pruning."""
@@ -582,6 +620,8 @@ class Node:
         self.connman.extra_binds = binds
         self.connman.max_receive_buffer = a.get_int("maxreceivebuffer", 5000) * 1000
         self.connman.max_send_buffer = a.get_int("maxsendbuffer", 1000) * 1000
+        self.connman.drop_messages_test = max(0, a.get_int("dropmessagestest", 0))
+        self.connman.allow_dns = a.get_bool("dns", True)
         from .net import protocol as P
         from .rpc.server import parse_allow_subnets
 

@@ -222,7 +222,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
                "mediantime": tip.median_time_past(), "verificationprogress": 1.0,
                "initialblockdownload": st.is_initial_block_download(),
                "chainwork": "%064x" % tip.chain_work, "size_on_disk": node.blocks_size_on_disk(),
-               "pruned": st.prune_mode, "warnings": "",
+               "pruned": st.prune_mode, "warnings": node.get_warnings(),
                "bip9_softforks": st.versionbits.bip9_softforks(tip),
                "kawpow_activation_time": params.kawpow_activation_time,
                "equihash_activation_time": params.equihash_activation_time}
@@ -291,7 +291,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         return {"blocks": tip.height, "currentblockweight": node.last_block_weight, "currentblocktx": node.last_block_tx,
                 "difficulty": _core.difficulty_from_bits(tip.bits), "networkhashps": st.network_hashps(120, -1),
                 "hashespersec": int(node.miner.hashrate), "pooledtx": len(st.mempool), "chain": params.network_id,
-                "warnings": "", "gpus": node.gpu_info(),
+                "warnings": node.get_warnings(), "gpus": node.gpu_info(),
                 "workers": node.miner.workers()}
 
     def rpc_getnetworkhashps(p):
@@ -706,7 +706,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
                 "localaddresses": ([{"address": cm.listen_addr[0], "port": cm.port, "score": 1}]
                                    if cm is not None and cm.port else [])
                 + ([{"address": h, "port": pt, "score": sc} for (h, pt), sc in sorted(cm.local_addrs.items())]
-                   if cm is not None else []), "warnings": ""}
+                   if cm is not None else []), "warnings": node.get_warnings()}
 
     def rpc_addnode(p):
         """addnode "node" "add|remove|onetry" — only onetry/add connect immediately here."""

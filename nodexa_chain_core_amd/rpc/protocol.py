@@ -16,6 +16,7 @@ RPC_INVALID_PARAMS = -32602
 RPC_INTERNAL_ERROR = -32603
 RPC_PARSE_ERROR = -32700
 RPC_MISC_ERROR = -1
+RPC_FORBIDDEN_BY_SAFE_MODE = -2
 RPC_WALLET_ERROR = -4
 RPC_WALLET_INSUFFICIENT_FUNDS = -6
 RPC_TYPE_ERROR = -3

@@ -48,9 +48,23 @@ class RPCCommand:
     help: str = ""
 
 
+# RPCs that call ObserveSafeMode() in the reference (src/wallet/rpcwallet.cpp, rpcdump.cpp,
+# src/rpc/assets.cpp, messages.cpp, rawtransaction.cpp, rewards.cpp): refused while a safe-mode
+# warning stands, unless -disablesafemode
+SAFE_MODE_METHODS = frozenset((
+    "sendtoaddress sendfromaddress listaddressgroupings getreceivedbyaddress getreceivedbyaccount getbalance "
+    "getunconfirmedbalance move sendfrom sendmany listreceivedbyaddress listreceivedbyaccount listtransactions "
+    "listaccounts listsinceblock gettransaction abandontransaction listlockunspent getwalletinfo listunspent "
+    "fundrawtransaction abortrescan issue issueunique listassetbalancesbyaddress listmyassets transfer "
+    "transferfromaddresses transferfromaddress reissue listassets issuequalifierasset issuerestrictedasset "
+    "reissuerestrictedasset transferqualifier isvalidverifierstring sendmessage signrawtransaction "
+    "sendrawtransaction testmempoolaccept distributereward getdistributestatus").split())
+
+
 class RPCTable:
     def __init__(self) -> None:
         self.commands: dict[str, RPCCommand] = {}
+        self.safe_mode: Callable[[], None] | None = None  # ObserveSafeMode (raises while in safe mode)
         self.warmup: str | None = None
         self.started = time.time()
         self.active: dict[int, tuple[str, float]] = {}
@@ -82,6 +96,8 @@ class RPCTable:
         cmd = self.commands.get(method)
         if cmd is None:
             raise RPCError(RPC_METHOD_NOT_FOUND, "Method not found")
+        if self.safe_mode is not None and method in SAFE_MODE_METHODS:
+            self.safe_mode()
         if isinstance(params, dict):  # named arguments
             unknown = set(params) - set(cmd.arg_names)
             if unknown:

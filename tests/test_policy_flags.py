@@ -50,3 +50,31 @@ def test_dbcache_bounds_pending_utxo_changes(core, node_factory):  # noqa: F811
     c.generatetoaddress(6, addr)
     assert st._since_flush < 6
     assert c.gettxoutsetinfo()["height"] == 9
+
+
+def test_safe_mode(core, node_factory, tmp_path):  # noqa: F811
+    """-testsafemode: the reference's ObserveSafeMode RPCs refuse with RPC_FORBIDDEN_BY_SAFE_MODE,
+    the warning shows in getblockchaininfo / getnetworkinfo / getmininginfo; -disablesafemode
+    overrides it; other RPCs are unaffected."""
+    node, _ = node_factory(("-testsafemode",))
+    c = client(node)
+    with pytest.raises(RuntimeError, match=r"RPC error -2: Safe mode: testsafemode enabled"):
+        c.getbalance()
+    assert c.getblockchaininfo()["warnings"] == "testsafemode enabled"
+    assert c.getmininginfo()["warnings"] == "testsafemode enabled"
+    assert c.getblockcount() == 0
+    node.stop()
+    node, _ = node_factory(("-testsafemode", "-disablesafemode"))
+    assert client(node).getbalance() == 0
+
+
+def test_dns_off_and_sysperms(core, node_factory, tmp_path):  # noqa: F811
+    import os
+    import stat
+
+    node, _ = node_factory(("-listen=1", "-port=0", "-listenonion=0", "-dns=0"))
+    with pytest.raises(ConnectionError, match="DNS lookups are disabled"):
+        node.connman.connect("localhost", 1)
+    # without -sysperms the node's files are private to its user (umask 077)
+    mode = os.stat(os.path.join(node.datadir, "debug.log")).st_mode
+    assert stat.S_IMODE(mode) & 0o077 == 0
