@@ -231,6 +231,7 @@ class ChainState:
         self.mempool_expiry = DEFAULT_MEMPOOL_EXPIRY * 3600         # -mempoolexpiry (seconds)
         self.max_tx_fee = DEFAULT_TRANSACTION_MAXFEE                # -maxtxfee (absurd-fee cap)
         self.bytes_per_sigop = DEFAULT_BYTES_PER_SIGOP              # -bytespersigop
+        self.last_replaced: list = []  # transactions the last accepted replacement pushed out
         self.block_max_weight = 7_999_000                           # -blockmaxweight
         self.block_max_size: int | None = None                      # -blockmaxsize
         self.block_min_fee_rate = DEFAULT_BLOCK_MIN_TX_FEE          # -blockmintxfee
@@ -1448,7 +1449,10 @@ class ChainState:
                     kind = "non-mandatory-script-verify-flag" if ok2 else "mandatory-script-verify-flag-failed"
                     return False, f"{kind} ({err})", fee
             if not test_only:
-                for t in replaced:  # BIP125: the replaced transactions and their descendants leave
+                # BIP125: the replaced transactions and their descendants leave (kept aside for
+                # compact-block reconstruction: vExtraTxnForCompact)
+                self.last_replaced = [self.mempool[t].tx for t in replaced if t in self.mempool]
+                for t in replaced:
                     self.pool_remove(t)
                 self.add_to_mempool(tx, fee, replacement=bool(replaced), sigop_cost=sigop_cost)
                 self.expire_mempool()  # LimitMempoolSize -> Expire, TrimToSize

@@ -17,6 +17,7 @@ the contextual rules run header by header on the C++ header chain.
 """
 from __future__ import annotations
 
+import collections
 import ipaddress
 import os
 import random
@@ -198,6 +199,9 @@ class ConnectionManager:
         self.max_receive_buffer = 5000 * 1000
         self.max_send_buffer = 1000 * 1000
         self.drop_messages_test = 0  # -dropmessagestest=<n>: drop 1 in n received messages
+        # vExtraTxnForCompact: orphans, rejected and replaced transactions kept for compact-block
+        # reconstruction (-blockreconstructionextratxn, DEFAULT_BLOCK_RECONSTRUCTION_EXTRA_TXN)
+        self.extra_txn: collections.deque = collections.deque(maxlen=100)
         self.allow_dns = True        # -dns: resolve names given to -addnode / -seednode / -connect
         self._stop = threading.Event()
         self.port: int | None = None
@@ -704,6 +708,7 @@ class ConnectionManager:
             return
         with self.state.lock:
             pool = [e.tx for e in self.state.mempool.values()]
+        pool += list(self.extra_txn)  # PartiallyDownloadedBlock::InitData's extra_txn
         slots, missing = cb.reconstruct(pool, peer.cmpct_version or 2)
         if missing:
             peer.partial[h] = (cb, slots)
@@ -839,11 +844,16 @@ class ConnectionManager:
             if peer.whitelisted and self.whitelist_force_relay:  # -whitelistforcerelay
                 self.announce_tx(txid)
             return
+        self.state.last_replaced = []
         ok, reason, _ = self.state.accept_to_mempool(tx)
         if ok:
+            if self.extra_txn.maxlen:  # transactions a replacement pushed out stay usable for compact blocks
+                self.extra_txn.extend(self.state.last_replaced)
             self.process_orphans(txid, len(tx.vout))
             return
         if reason == "missing-inputs":
+            if self.extra_txn.maxlen:
+                self.extra_txn.append(tx)
             # keep it as an orphan and ask the sender for the parents we do not have
             missing = [i.prevout.hash for i in tx.vin
                        if i.prevout.hash not in self.state.mempool and i.prevout.hash not in self.orphans]
@@ -852,6 +862,8 @@ class ConnectionManager:
             return
         REGISTRY.inc("p2p_tx_rejected_total", 1)
         log.log_print("mempool", f"tx {_core.u256_hex(txid)} from peer {peer.id} rejected: {reason}")
+        if self.extra_txn.maxlen:  # a policy reject may still be in a block
+            self.extra_txn.append(tx)
 
     def on_mempool(self, peer: Peer, p: bytes) -> None:
         """BIP35: inv of every pool txid (in MAX_INV_SZ chunks), through the peer's bloom filter."""

@@ -292,6 +292,16 @@ class Node:
             w.keypool_size = max(1, a.get_int("keypool", w.keypool_size))
             w.broadcast = a.get_bool("walletbroadcast", True)
             w.spend_zeroconf_change = a.get_bool("spendzeroconfchange", True)
+            if a.get("discardfee") is not None:
+                w.discard_fee = round(float(a.get("discardfee")) * 100_000_000)
+            w.reject_long_chains = a.get_bool("walletrejectlongchains", False)
+        # Berkeley DB tuning / recovery options of the reference wallet (src/wallet/init.cpp): the
+        # wallet here is a JSON file rewritten atomically on every change (older layouts upgraded
+        # on load), so these have nothing to act on; -upnp needs miniupnpc, not built here either
+        for flag in ("dblogsize", "flushwallet", "privdb", "salvagewallet", "upgradewallet", "upnp",
+                     "fuzzmessagestest"):
+            if a.is_set(flag):
+                log.log_printf(f"-{flag} has no effect in this build")
         # -maxsigcachesize (MiB, src/script/sigcache.cpp InitSignatureCache): bounded by its 32-byte entries
         _core.sigcache_set_max_bytes(max(0, a.get_int("maxsigcachesize", 32)) << 20)
         par = int(a.get("par", "0"))  # -par: 0 = one per core (as the reference), <0 leaves that many cores free
@@ -622,6 +632,9 @@ class Node:
         self.connman.max_send_buffer = a.get_int("maxsendbuffer", 1000) * 1000
         self.connman.drop_messages_test = max(0, a.get_int("dropmessagestest", 0))
         self.connman.allow_dns = a.get_bool("dns", True)
+        import collections
+
+        self.connman.extra_txn = collections.deque(maxlen=max(0, a.get_int("blockreconstructionextratxn", 100)))
         from .net import protocol as P
         from .rpc.server import parse_allow_subnets
 

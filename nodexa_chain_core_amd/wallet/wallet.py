@@ -35,6 +35,7 @@ DEFAULT_DERIVE_ROUNDS = 25000  # CMasterKey nDeriveIterations default
 UNLOCK_NEEDED = "Error: Please enter the wallet passphrase with walletpassphrase first."
 HARDENED = 0x80000000
 WALLET_INCREMENTAL_RELAY_FEE = 5000  # sat per kB (src/wallet/wallet.h:59)
+DEFAULT_DISCARD_FEE = 10_000  # sat per kvB (src/wallet/wallet.h): change worth less than spending it is dropped
 DUST_THRESHOLD = 546  # GetDustThreshold of a P2PKH output at DUST_RELAY_TX_FEE (chain/policy.py)
 # nExtCoinType (src/chainparams.cpp:196, 355, 522): the BIP44 coin_type level
 EXT_COIN_TYPE = {"main": 1313, "test": 1, "regtest": 1}
@@ -147,6 +148,8 @@ class Wallet:
         self.keypool_size = DEFAULT_KEYPOOL_SIZE      # -keypool
         self.broadcast = True                         # -walletbroadcast
         self.spend_zeroconf_change = True             # -spendzeroconfchange (DEFAULT_SPEND_ZEROCONF_CHANGE)
+        self.discard_fee = DEFAULT_DISCARD_FEE        # -discardfee (sat per kvB)
+        self.reject_long_chains = False               # -walletrejectlongchains
         self.hdpath: dict[bytes, str] = {}      # hdkeypath of derived keys
         self.pool: list[bytes] = []             # keypool: reserved keys not yet handed out
         self.hd: dict | None = None             # {"master_id", "next", "seed", "seed_crypted"}
@@ -784,6 +787,10 @@ class Wallet:
                 if outs[0].value <= 0:
                     raise WalletError("The transaction amount is too small to pay the fee")
             change = total - target - (0 if subtract_fee else fee)
+            if 0 < change < self._change_discard_threshold():
+                # dust at the discard rate (GetDiscardRate: -discardfee, at least the dust relay fee):
+                # the change goes to the fee instead of an output not worth spending
+                change = 0
             if change > 0:
                 if change_spk is None:
                     change_spk = _core.address_to_script(self.new_address("change"), self.params.pubkey_prefix,
@@ -798,7 +805,7 @@ class Wallet:
             size = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4
             want_fee = self._capped_fee(max(1, fee_rate * size // 1000))
             if fee >= want_fee:
-                return tx, fee
+                return tx, total - sum(o.value for o in outs)  # a discarded change is part of the fee
             fee = want_fee + 68  # headroom for a changed signature size
         raise WalletError("Transaction fee did not converge")
 
@@ -808,7 +815,19 @@ class Wallet:
         """SendMoney / CommitTransaction: build, submit to the pool, record in the history."""
         tx, _ = self.create_transaction(outputs, fee_rate=self.fee_rate, subtract_fee=subtract_fee, minconf=minconf,
                                         replaceable=replaceable, from_scripts=from_scripts, change_spk=change_spk)
+        if self.reject_long_chains:
+            # -walletrejectlongchains: refuse what the pool's ancestor / descendant limits would refuse
+            vsize = (len(tx.serialize(False)) * 3 + len(tx.serialize(True)) + 3) // 4
+            with self.state.lock:
+                if self.state._check_package_limits(tx, vsize, set()):
+                    raise WalletError("Transaction has too long of a mempool chain")
         return self.commit(tx, comment, comment_to, from_account)
+
+    def _change_discard_threshold(self) -> int:
+        """GetDustThreshold of a P2PKH change output (34 bytes, spent by a 148-byte input) at the
+        discard rate."""
+        rate = max(self.discard_fee, getattr(self.state, "dust_relay_fee", 0))
+        return (34 + 148) * rate // 1000
 
     def _trusted(self, txid: bytes) -> bool:
         """CWalletTx::IsTrusted for a pool transaction: every input spends one of our outputs."""

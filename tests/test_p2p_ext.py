@@ -171,3 +171,33 @@ def test_bloom_merkleblock_and_getaddr(core, tmp_path):
         sock.close()
     finally:
         a.stop()
+
+
+def test_compact_block_uses_extra_txn(core, tmp_path):
+    """-blockreconstructionextratxn (vExtraTxnForCompact): a transaction b saw but no longer holds
+    in its mempool (rejected, orphaned or replaced) still fills its slot of a compact block."""
+    a = _node(core, tmp_path, "a", ["-listen", "-port=0"])
+    b = None
+    try:
+        w = a.wallet.new_address()
+        wspk = core.address_to_script(w, a.params.pubkey_prefix, a.params.script_prefix)
+        a.miner.generate(wspk, 101)
+        b = _node(core, tmp_path, "b", [f"-connect=127.0.0.1:{a.connman.port}", "-blockreconstructionextratxn=10"])
+        assert b.connman.extra_txn.maxlen == 10
+        assert _wait(lambda: b.state.height() == 101 and b.peer_count() == 1)
+        b.connman.peers[0].send("sendcmpct", struct.pack("<?Q", True, 2))
+        assert _wait(lambda: a.connman.peers and a.connman.peers[0].cmpct_hb)
+        txid = a.wallet.send([(b"\x51", 10**8)])
+        assert _wait(lambda: txid in b.state.mempool)
+        with b.state.lock:
+            tx = b.state.mempool[txid].tx
+            b.state.pool_remove(txid)
+        b.connman.extra_txn.append(tx)
+        asked = REGISTRY.total("p2p_cmpct_getblocktxn_total")
+        a.miner.generate(a.mining_script, 1)
+        assert _wait(lambda: b.state.coins_tip().hash == a.state.tip().hash)
+        assert REGISTRY.total("p2p_cmpct_getblocktxn_total") == asked  # no round trip for it
+    finally:
+        if b is not None:
+            b.stop()
+        a.stop()

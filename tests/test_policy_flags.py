@@ -78,3 +78,30 @@ def test_dns_off_and_sysperms(core, node_factory, tmp_path):  # noqa: F811
     # without -sysperms the node's files are private to its user (umask 077)
     mode = os.stat(os.path.join(node.datadir, "debug.log")).st_mode
     assert stat.S_IMODE(mode) & 0o077 == 0
+
+
+def test_discardfee_drops_dust_change(core, node_factory):  # noqa: F811
+    node, _ = node_factory(("-discardfee=0.0001",))
+    c = client(node)
+    fund(c)
+    w = node.wallet
+    assert w._change_discard_threshold() == (34 + 148) * 10_000 // 1000
+    u = mature_coin(c)
+    coin = round(u["amount"] * 1e8)
+    dest = core.address_to_script(c.getnewaddress(), node.params.pubkey_prefix, node.params.script_prefix)
+    tx, fee = w.create_transaction([(dest, coin // 2)])
+    assert len(tx.vout) == 2  # ordinary change
+    amount = coin - fee - 1000  # would leave 1000 sat of change: dust at the discard rate
+    tx2, fee2 = w.create_transaction([(dest, amount)])
+    assert len(tx2.vout) == 1 and fee2 == coin - amount
+
+
+def test_walletrejectlongchains(core, node_factory):  # noqa: F811
+    node, _ = node_factory(("-walletrejectlongchains", "-limitancestorcount=2"))
+    c = client(node)
+    fund(c)
+    to = c.getnewaddress()
+    c.sendtoaddress(to, 1.0)  # spends the one mature coin; its change is unconfirmed
+    c.sendtoaddress(to, 1.0)  # spends that change (ancestors: 1)
+    with pytest.raises(RuntimeError, match="too long of a mempool chain"):
+        c.sendtoaddress(to, 1.0)
