@@ -65,6 +65,10 @@
 //                 owns the hash's nonce (8 DPP broadcasts + 8 selects per hash, 8 VGPRs)
 //                 instead of a 32 B/nonce LDS buffer: the workgroup's LDS is then only
 //                 the L1 table, so 1024-thread groups fit twice per CU (8 waves/SIMD)
+//   KP_L1G=<mask> cache accesses i with bit i set in <mask> read the L1 word from the DAG's first
+//                 16 KiB in HBM (a buffer_load that hits the CU's vector L1) instead of the LDS copy:
+//                 the LDS array, not the TA/TCP path, is the busy unit of the round (profiles/r3z),
+//                 so a few of the 11 lookups per round move to the idle one
 #ifndef KP_BLOCK
 #define KP_BLOCK NODEXA_KAWPOW_BLOCK
 #endif
@@ -87,6 +91,20 @@ NX_DEV uint32_t kp_l1_read(const uint32_t* l1, uint32_t x) {
 #else
 #define KP_L1_WORDS 4096
 #define KP_L1(l1, x) (l1)[(x) & 4095u]
+#endif
+#ifdef KP_L1G
+NX_DEV uint32_t kp_l1g_read(__amdgpu_buffer_rsrc_t g, uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(g, (x << 2) & 0x3ffcu, 0, 0);
+}
+#undef KP_L1S
+#define KP_L1S(i, l1, x) (((KP_L1G) >> (i)) & 1 ? kp_l1g_read(l1g, (x)) : KP_L1(l1, x))
+typedef __amdgpu_buffer_rsrc_t kp_l1g_t;
+NX_DEV kp_l1g_t kp_l1g_handle(const void* dag) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(dag), (short)0, 16384, 0x00020000);
+}
+#else
+typedef const void* kp_l1g_t;
+NX_DEV kp_l1g_t kp_l1g_handle(const void* dag) { return dag; }
 #endif
 
 // LDS copy of the L1 (first 16 KiB of the DAG), KP_L1_WORDS / 4096 times.
@@ -275,7 +293,8 @@ NX_DEV void kp_final(const uint32_t st2[8], const uint32_t digest[8], uint32_t o
 // from lane J of the row via DPP and the lane's 16-byte slice is lane ^ J.
 template <int J>
 NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
-                       uint32_t lane) {
+                       kp_l1g_t l1g, uint32_t lane) {
+    (void)l1g;
     uint4 d[KP_HASHES];
     const uint32_t part = lane ^ (uint32_t)J;
 #pragma unroll
@@ -304,7 +323,7 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMo
     for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
 }
 
-NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
+NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t* l1, kp_l1g_t l1g,
                             uint32_t st0, uint32_t st1, uint32_t lane, uint32_t* dig,
                             uint32_t (&own)[8]) {
 #pragma unroll 1
@@ -325,14 +344,14 @@ NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t
         // 64 rounds = 4 x 16 with the round index mod 16 baked into each copy
 #pragma unroll 1
         for (uint32_t rr = 0; rr < 64; rr += 16) {
-            kp_round_c<0>(mx, dag, items, l1, lane);   kp_round_c<1>(mx, dag, items, l1, lane);
-            kp_round_c<2>(mx, dag, items, l1, lane);   kp_round_c<3>(mx, dag, items, l1, lane);
-            kp_round_c<4>(mx, dag, items, l1, lane);   kp_round_c<5>(mx, dag, items, l1, lane);
-            kp_round_c<6>(mx, dag, items, l1, lane);   kp_round_c<7>(mx, dag, items, l1, lane);
-            kp_round_c<8>(mx, dag, items, l1, lane);   kp_round_c<9>(mx, dag, items, l1, lane);
-            kp_round_c<10>(mx, dag, items, l1, lane);  kp_round_c<11>(mx, dag, items, l1, lane);
-            kp_round_c<12>(mx, dag, items, l1, lane);  kp_round_c<13>(mx, dag, items, l1, lane);
-            kp_round_c<14>(mx, dag, items, l1, lane);  kp_round_c<15>(mx, dag, items, l1, lane);
+            kp_round_c<0>(mx, dag, items, l1, l1g, lane);   kp_round_c<1>(mx, dag, items, l1, l1g, lane);
+            kp_round_c<2>(mx, dag, items, l1, l1g, lane);   kp_round_c<3>(mx, dag, items, l1, l1g, lane);
+            kp_round_c<4>(mx, dag, items, l1, l1g, lane);   kp_round_c<5>(mx, dag, items, l1, l1g, lane);
+            kp_round_c<6>(mx, dag, items, l1, l1g, lane);   kp_round_c<7>(mx, dag, items, l1, l1g, lane);
+            kp_round_c<8>(mx, dag, items, l1, l1g, lane);   kp_round_c<9>(mx, dag, items, l1, l1g, lane);
+            kp_round_c<10>(mx, dag, items, l1, l1g, lane);  kp_round_c<11>(mx, dag, items, l1, l1g, lane);
+            kp_round_c<12>(mx, dag, items, l1, l1g, lane);  kp_round_c<13>(mx, dag, items, l1, l1g, lane);
+            kp_round_c<14>(mx, dag, items, l1, l1g, lane);  kp_round_c<15>(mx, dag, items, l1, l1g, lane);
         }
 #else
 #pragma unroll 1
@@ -424,7 +443,7 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     {
         uint32_t st2[8];
         kp_seed(p.header, nonce, st2);
-        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig, digest);
+        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, kp_l1g_handle(p.dag), st2[0], st2[1], lane, dig, digest);
     }
 #ifndef KP_DIGEST_REG
     __threadfence_block();  // digest words written by lanes 0..7 are read by lane h below
@@ -474,7 +493,7 @@ extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     uint32_t* dig = digs ? digs + (threadIdx.x & ~15u) * 8 : nullptr;
     uint32_t st2[8], digest[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fin[8];
     kp_seed(j.header, j.nonce, st2);
-    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig, digest);
+    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, kp_l1g_handle(p.dag), st2[0], st2[1], lane, dig, digest);
 #ifndef KP_DIGEST_REG
     __syncthreads();
 #pragma unroll
