@@ -11,6 +11,7 @@
 #include "../chain/validation.hpp"
 #include "../pow/equihash.hpp"
 #include "../crypto/hashes.hpp"
+#include "../pow/legacy_algos.hpp"
 #include "../pow/x16r.hpp"
 #include "../pow/x16r_prims.hpp"
 #include "../pow/kawpow.hpp"
@@ -241,6 +242,26 @@ void bind_extra(py::module_& m) {
         return py::bytes(reinterpret_cast<const char*>(h.bytes), 64);
     });
     m.def("x16r_slot_available", &x16r_slot_available);
+
+    // ------------------------------------------------ HAVAL / Lyra2 (linked by the reference, unused by consensus)
+    m.def("haval", [](const py::bytes& data, int passes, int out_bits) {
+        std::string s = data;
+        std::vector<u8> h = haval_hash(reinterpret_cast<const u8*>(s.data()), s.size(), passes, out_bits);
+        return py::bytes(reinterpret_cast<const char*>(h.data()), h.size());
+    }, py::arg("data"), py::arg("passes") = 3, py::arg("out_bits") = 256);
+    m.def("lyra2", [](const py::bytes& pwd, const py::bytes& salt, u64 klen, u64 time_cost, u64 n_rows, u64 n_cols,
+                      bool old_absorb) {
+        std::string p = pwd, s = salt;
+        std::vector<u8> k;
+        {
+            py::gil_scoped_release nogil;
+            k = lyra2_hash(reinterpret_cast<const u8*>(p.data()), p.size(), reinterpret_cast<const u8*>(s.data()),
+                           s.size(), klen, time_cost, n_rows, n_cols, old_absorb);
+        }
+        if (k.empty() && klen) throw std::invalid_argument("lyra2: nRows must be a power of two >= 4, input must fit the matrix");
+        return py::bytes(reinterpret_cast<const char*>(k.data()), k.size());
+    }, py::arg("pwd"), py::arg("salt"), py::arg("klen") = 32, py::arg("time_cost") = 1, py::arg("n_rows") = 4,
+       py::arg("n_cols") = 4, py::arg("old_absorb") = false);
     m.def("x16r_search", [](const py::bytes& header80, bool v2, const py::bytes& target, u32 start, u64 count,
                             int threads) -> py::object {
         std::string h = header80;
