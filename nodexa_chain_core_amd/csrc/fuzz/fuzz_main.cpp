@@ -21,6 +21,7 @@
 #include "../chain/interpreter.hpp"
 #include "../chain/primitives.hpp"
 #include "../crypto/secp256k1.hpp"
+#include "../pow/legacy_algos.hpp"
 #include "../pow/x16r.hpp"
 
 using namespace nodexa;
@@ -148,7 +149,7 @@ void fuzz_der(const Bytes& in) {
 extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     if (size == 0) return 0;
     const Bytes in(data + 1, data + size);
-    switch (data[0] % 12) {
+    switch (data[0] % 13) {
     case 0: fuzz_block(in, kKawpowAlways); break;
     case 1: fuzz_block(in, kKawpowNever); break;
     case 2: fuzz_header(in, kKawpowAlways); break;
@@ -164,6 +165,16 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         u8 prev[32] = {0}, out[32];
         if (in.size() >= 32) std::memcpy(prev, in.data(), 32);
         x16r_hash(in.data(), in.size(), prev, in.size() & 1, out);
+        break;
+    }
+    case 12: {
+        // HAVAL over the whole input; Lyra2 with small parameters taken from its first bytes and
+        // the rest split into password and salt (inputs larger than the matrix must be refused)
+        if (in.size() < 8) break;
+        (void)haval_hash(in.data() + 7, in.size() - 7, 3 + in[0] % 3, 128 + 32 * (in[1] % 5));
+        const size_t body = in.size() - 7, split = body ? in[6] % (body + 1) : 0;
+        (void)lyra2_hash(in.data() + 7, split, in.data() + 7 + split, body - split, in[5], 1 + in[4] % 3,
+                         u64(4) << (in[2] % 3), 1 + in[3] % 4, in[6] & 1);
         break;
     }
     }

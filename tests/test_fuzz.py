@@ -40,6 +40,7 @@ def _seeds(core):
     out.append(b"\x0a" + bytes.fromhex("3044022057e8f2a6e4b4d3e8b8a7a9a9c1f2e1d0b0a090807060504030201000fedcba98"
                                        "022046e1f2a3b4c5d6e7f8091a2b3c4d5e6f708192a3b4c5d6e7f8091a2b3c4d5e6f"))
     out.append(b"\x0b" + bytes(80))
+    out.append(b"\x0c" + bytes([2, 4, 1, 3, 1, 32, 17]) + bytes(range(40)))
     return out
 
 

@@ -86,8 +86,8 @@ def test_discardfee_drops_dust_change(core, node_factory):  # noqa: F811
     fund(c)
     w = node.wallet
     assert w._change_discard_threshold() == (34 + 148) * 10_000 // 1000
-    u = mature_coin(c)
-    coin = round(u["amount"] * 1e8)
+    # selection is largest-first, so size the payments against the largest spendable coin
+    coin = max(round(u["amount"] * 1e8) for u in c.listunspent())
     dest = core.address_to_script(c.getnewaddress(), node.params.pubkey_prefix, node.params.script_prefix)
     tx, fee = w.create_transaction([(dest, coin // 2)])
     assert len(tx.vout) == 2  # ordinary change
