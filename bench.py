@@ -99,6 +99,85 @@ def _verify_headers_bench(log) -> dict | None:
     return out
 
 
+def _equihash_bench(args, hdr, height: int, rank: int, log) -> dict:
+    """BASELINE config 3 through the node's mining loop: MiningService.step with an Equihash work
+    packet (miner/equihash_search.EquihashGpuDevice: 16 solver instances per window, two windows in
+    flight, every solution verified on the device, SHA256d of the candidate headers on the host),
+    the same collectives as the KawPow loop. Sol/s = all ranks' distinct valid solutions over the
+    slowest rank's time. The standalone solver (two 8-instance launches in flight, host-verified)
+    is timed after it for comparison."""
+    import torch
+
+    from nodexa_chain_core_amd import _core
+    from nodexa_chain_core_amd.miner.equihash_search import EquihashGpuDevice
+    from nodexa_chain_core_amd.miner.search import ALGO_EQUIHASH, Work, equihash_block_hash
+    from nodexa_chain_core_amd.miner.service import BenchLeader, MiningService
+    from nodexa_chain_core_amd.ops.equihash import EquihashSolver
+    from nodexa_chain_core_amd.parallel import world as W
+
+    dev_index = W.get().device.index
+    prefix = struct.pack("<i32s32sIII", hdr.version | _core.EQUIHASH_VERSION_BIT, hdr.prev, hdr.merkle_root,
+                         hdr.time, hdr.bits, height)
+    boundary = ((1 << 252) - 1).to_bytes(32, "big")  # ~1 in 16 solutions is a share
+    work = Work(prefix, boundary, height, 1, 0xE9_0000_0000_0000, 0, ALGO_EQUIHASH)
+    edev = EquihashGpuDevice(dev_index, num_inst=16)
+    leader = BenchLeader(work) if rank == 0 else None
+    svc = MiningService(edev, leader, window=16)
+    svc.step()
+    for _ in range(3):
+        svc.step()
+    torch.cuda.synchronize()
+    W.barrier()
+    before = svc.hashes_total
+    t0 = time.perf_counter()
+    for _ in range(args.equihash):
+        svc.step()
+    edev.synchronize()
+    W.barrier()
+    dt = W.all_reduce_max(time.perf_counter() - t0)
+    sols = svc.hashes_total - before  # all-reduced over the ranks every step
+    node_rate = sols / dt
+    if leader is not None:
+        leader.shutdown()
+    while svc.step():
+        pass
+    svc.pipe.drain()
+    bad = checked = 0
+    if rank == 0:  # golden verifier + block hash of the shares the loop shipped
+        p = _core.EquihashParams(200, 9)
+        for s in leader.shares[:4]:
+            checked += 1
+            ok = _core.equihash_verify(p, prefix + s.nonce256(), _core.equihash_unpack(p, s.solution))[0]
+            bad += not (ok and equihash_block_hash(prefix, s.nonce, s.solution) == s.block_hash)
+    if W.all_reduce_sum_int(bad):
+        raise SystemExit("Equihash shares of the mining loop failed the host check")
+    del svc, edev
+    # the standalone solver: two launches in flight, host-verified solutions
+    solver = EquihashSolver(num_inst=8)
+    mk = lambda i, j: prefix + struct.pack("<QQQQ", rank, i, j, 0xE9)  # noqa: E731
+    solver.solve([mk(-1 & 0xFFFF, j) for j in range(8)])
+    torch.cuda.synchronize()
+    W.barrier()
+    t0 = time.perf_counter()
+    found = 0
+    nb = max(1, args.equihash * 2)
+    for i in range(nb):
+        solver.launch([mk(i, j) for j in range(8)])
+        if i >= 1:
+            found += sum(len(s) for s in solver.collect())
+    found += sum(len(s) for s in solver.collect())
+    torch.cuda.synchronize()
+    sdt = W.all_reduce_max(time.perf_counter() - t0)
+    solo = W.all_reduce_sum_int(found) / sdt
+    log(f"[bench] Equihash(200,9) node loop: {node_rate:.1f} Sol/s ({args.equihash} steps x 16 solves per rank, "
+        f"{sols} solutions in {dt:.3f}s, {checked} shares host-checked); standalone solver {solo:.1f} Sol/s "
+        f"({solver.fallbacks} host re-solves)")
+    return {"node_sol_per_s": round(node_rate, 2), "standalone_sol_per_s": round(solo, 2),
+            "node_vs_standalone": round(node_rate / solo, 4) if solo else None, "steps": args.equihash,
+            "solves_per_step": 16, "loop": "miner/service.MiningService.step (Equihash work packet)",
+            "shares_checked": checked}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,8 +186,11 @@ def main() -> int:
     ap.add_argument("--epoch", type=int, default=384, help="384 -> 4 GiB DAG (BASELINE config)")
     ap.add_argument("--batch", type=int, default=1 << 25,
                     help="nonces per GPU per step (profiles/r2q: 2^25 amortises the kernel tail)")
-    ap.add_argument("--equihash", type=int, default=12,
-                    help="Equihash(200,9): batches of 8 solves per GPU to time (0 = skip)")
+    ap.add_argument("--equihash", type=int, default=32,
+                    help="Equihash(200,9): mining-loop steps (16 solves each) per GPU to time (0 = skip)")
+    ap.add_argument("--collectives", action="store_true",
+                    help="force the process group even at one rank (one-rank RCCL: every collective of the "
+                         "loop, the DAG build and batch verify runs, as on a multi-GPU node)")
     ap.add_argument("--verify", type=int, default=1, help="1: time BASELINE config 5 (batch header verify)")
     ap.add_argument("--check-shares", type=int, default=8, help="shares re-hashed on the host after timing")
     ap.add_argument("--corrupt-dag", action="store_true",
@@ -133,7 +215,7 @@ def main() -> int:
     from nodexa_chain_core_amd.miner.service import BenchLeader, MiningService
     from nodexa_chain_core_amd.parallel import world as W
 
-    world = W.init(use_gpu=not cpu)
+    world = W.init(use_gpu=not cpu, force_collectives=args.collectives or None)
     rank, ws = world.rank, world.world_size
     log = (lambda *a: print(*a, file=sys.stderr, flush=True)) if (rank == 0 and not args.quiet) else (lambda *a: None)
     sync = (lambda: None) if cpu else torch.cuda.synchronize
@@ -162,7 +244,7 @@ def main() -> int:
     else:
         from nodexa_chain_core_amd.miner.search import GpuSearchDevice
 
-        dev = GpuSearchDevice(world.device.index, collective_dag=world.distributed)
+        dev = GpuSearchDevice(world.device.index, collective_dag=world.collective)
         sync()
         W.barrier()
         t0 = time.time()
@@ -222,31 +304,9 @@ def main() -> int:
     if not cpu:
         torch.cuda.empty_cache()
 
-    eq_sols = None
+    eq = None
     if args.equihash and not cpu:
-        # Equihash(200,9): every rank solves its own nonces (weak scaling);
-        # node Sol/s = all solutions / slowest rank's time.
-        from nodexa_chain_core_amd.ops.equihash import EquihashSolver
-
-        solver = EquihashSolver(num_inst=8)
-        mk = lambda i, j: hdr.kawpow_input() + struct.pack("<QQQQ", rank, i, j, 0xE9)  # noqa: E731
-        solver.solve([mk(-1 & 0xFFFF, j) for j in range(8)])  # warm-up
-        torch.cuda.synchronize()
-        W.barrier()
-        t0 = time.perf_counter()
-        found = 0
-        # two batches in flight: the GPU solves batch i+1 while the host verifies batch i
-        for i in range(args.equihash):
-            solver.launch([mk(i, j) for j in range(8)])
-            if i >= 1:
-                found += sum(len(s) for s in solver.collect())
-        found += sum(len(s) for s in solver.collect())
-        torch.cuda.synchronize()
-        eq_dt = W.all_reduce_max(time.perf_counter() - t0)
-        eq_sols = round(W.all_reduce_sum_int(found) / eq_dt, 2)
-        log(f"[bench] Equihash(200,9): {eq_sols} Sol/s ({args.equihash} x 8 solves per rank, {found} solutions "
-            f"in {eq_dt:.3f}s, {solver.fallbacks} host re-solves)")
-        del solver
+        eq = _equihash_bench(args, hdr, height, rank, log)
 
     verify = _verify_headers_bench(log) if args.verify and not cpu else None
 
@@ -277,7 +337,8 @@ def main() -> int:
             "loop": "miner/service.MiningService.step (the node's mining loop)",
             "shares_rehashed": checked,
             "dag_build_s": round(dag_s, 3),
-            "equihash_sol_per_s": eq_sols,
+            "equihash_sol_per_s": eq["node_sol_per_s"] if eq else None,
+            "equihash": eq,
             "verify_headers": verify,
             "verify_headers_per_s": verify["dag"]["headers_per_s"] if verify else None,
             "baseline_mhs": base,

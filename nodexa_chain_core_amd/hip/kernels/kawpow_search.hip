@@ -34,6 +34,16 @@
 #include "kernel_params.h"
 #include "keccak_device.hpp"
 
+// Ceiling microbenchmark (tools/kawpow_sweep.py, profiles/r4a): compile one class of the period's
+// ops out of the real kernel at the shipping occupancy. KP_SKEL_NOMATH keeps the DAG gather chain
+// and the 11 L1 lookups (+ their merges) per round, KP_SKEL_NOCACHE the gathers and the 18 math
+// ops, KP_SKEL_GATHER only the gather chain and its merge. Never bit-exact; never shipped.
+#if defined(KP_SKEL_NOMATH) || defined(KP_SKEL_GATHER)
+#define KP_MATH_OP(...)
+#endif
+#if defined(KP_SKEL_NOCACHE) || defined(KP_SKEL_GATHER)
+#define KP_CACHE_OP(...)
+#endif
 #ifndef KAWPOW_PROGRAM_HEADER
 #define KAWPOW_PROGRAM_HEADER "kawpow_program_default.inc"
 #endif

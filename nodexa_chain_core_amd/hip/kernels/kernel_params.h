@@ -148,6 +148,16 @@ struct EquihashVerifyParams {
     const uint32_t* sols;   // [num][EQ_SOL_WORDS] packed solutions
     uint32_t* out;          // [num] 0 = valid, else the failing rule (EQ_V_*)
 };
+// The solver's own solution slots, verified on the device (equihash.hip eq_verify_slots).
+struct EquihashSlotVerifyParams {
+    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashDev)
+    uint64_t h0[8];
+    uint32_t input_len;
+    uint32_t num_inst;
+    const uint32_t* sols;   // [inst][1 + EQ_MAX_SOL*512]: count, then unpacked indices
+    uint32_t* out;          // [inst][EQ_MAX_SOL]: EQ_V_* per slot, EQ_V_EMPTY past the count
+};
+#define EQ_V_EMPTY 255
 #define EQ_V_OK 0
 #define EQ_V_COLLISION 1
 #define EQ_V_ORDER 2

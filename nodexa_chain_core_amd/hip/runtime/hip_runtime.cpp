@@ -496,6 +496,21 @@ PYBIND11_MODULE(_hip, m) {
         p.out = reinterpret_cast<uint32_t*>(out);
         k.launch_bytes(dim3(num), dim3(256), 0, as_stream(stream), &p, sizeof(p));
     });
+    m.attr("EQ_V_EMPTY") = EQ_V_EMPTY;
+    m.def("launch_equihash_verify_slots", [](const Kernel& k, std::vector<uint64_t> h0, uintptr_t msgs,
+                                             uint32_t input_len, uint32_t num_inst, uintptr_t sols, uintptr_t out,
+                                             uintptr_t stream) {
+        if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
+        if (input_len > 124 || num_inst == 0 || num_inst > 65535) throw std::invalid_argument("bad equihash geometry");
+        EquihashSlotVerifyParams p{};
+        p.msgs = reinterpret_cast<const uint64_t*>(msgs);
+        for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
+        p.input_len = input_len;
+        p.num_inst = num_inst;
+        p.sols = reinterpret_cast<const uint32_t*>(sols);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        k.launch_bytes(dim3(EQ_MAX_SOL, num_inst), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("launch_equihash_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
                                       uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
                                       uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols,

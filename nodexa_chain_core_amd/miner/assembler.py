@@ -108,6 +108,10 @@ class BlockAssembler:
             hdr.prev = prev.hash
             t = int(time.time()) if now is None else int(now)
             hdr.time = max(prev.median_time_past() + 1, t)
+            if hdr.time >= self.params.equihash_activation_time:
+                # Equihash(200,9) extension era: the version bit selects the
+                # extended header (nonce256 + solution) that consensus requires from the activation
+                hdr.version = hdr.version | _core.EQUIHASH_VERSION_BIT
             hdr.height = height
             hdr.nonce = 0
             hdr.nonce64 = 0

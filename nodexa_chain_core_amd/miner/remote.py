@@ -1,4 +1,4 @@
-"""Remote-mode KawPow miner: this engine as the external GPU miner of a node.
+"""Remote-mode miner: this engine as the external GPU miner of a node.
 
 The node side of the protocol is src/rpc/mining.cpp:722-739 and :841-932 (served here by
 rpc/methods.py, and by any reference clore_blockchaind started with -miningaddress):
@@ -7,7 +7,9 @@ rpc/methods.py, and by any reference clore_blockchaind started with -miningaddre
 answers `pprpcsb(header_hash, mix_hash, nonce)` with the mix in ProgPoW byte order and the
 nonce as 16 hex digits. The reference keeps each header's block for 30 s and rebuilds the
 template when the tip or the mempool changes, so the miner re-reads the template whenever the
-previous block hash changes or `refresh` seconds have passed.
+previous block hash changes or `refresh` seconds have passed. In the Equihash extension's era the
+template carries `equihash.input` (the 80-byte prefix) instead, and solutions go back through
+`equihashsubmit(input, nonce256, solution)`.
 
 Nonce partition: worker `rank` of `world` searches nonce_base + rank * 2^56 + k, so several
 processes (one per GPU) never overlap, mirroring the in-process controller's partition. The
@@ -48,16 +50,21 @@ class RemoteLeader:
             if self.rpc.getbestblockhash() == self.tpl["previousblockhash"]:
                 return self.tpl
         tpl = self.rpc.getblocktemplate({"rules": self.rules})
-        if "pprpcheader" not in tpl:
-            raise RuntimeError("the node's template has no pprpcheader (KawPow not active, or no -miningaddress)")
-        if self.tpl is None or tpl["pprpcheader"] != self.tpl["pprpcheader"]:
+        if "pprpcheader" not in tpl and "equihash" not in tpl:
+            raise RuntimeError("the node's template has no pprpcheader / equihash input (no -miningaddress, "
+                               "or a pre-KawPow template)")
+        if self.tpl is None or self._key(tpl) != self._key(self.tpl):
             self.job_id += 1
         self.tpl, self.tpl_time, self.force = tpl, now, False
         self.stats["templates"] += 1
         return tpl
 
+    @staticmethod
+    def _key(tpl: dict) -> str:
+        return tpl["equihash"]["input"] if "equihash" in tpl else tpl["pprpcheader"]
+
     def next_work(self, repartitioned: bool = False):
-        from .search import FLAG_CLEAN, FLAG_STOP, Work
+        from .search import ALGO_EQUIHASH, FLAG_CLEAN, FLAG_STOP, Work
 
         if self.stopping:
             return Work(flags=FLAG_STOP)
@@ -66,27 +73,43 @@ class RemoteLeader:
             self.force = True
         tpl = self.template()
         flags = FLAG_CLEAN if self.job_id != before or repartitioned else 0
+        if "equihash" in tpl:
+            return Work(bytes.fromhex(tpl["equihash"]["input"]), bytes.fromhex(tpl["target"]), int(tpl["height"]),
+                        self.job_id, self.nonce_base, flags, ALGO_EQUIHASH)
         return Work(bytes.fromhex(tpl["pprpcheader"]), bytes.fromhex(tpl["target"]), int(tpl["height"]),
                     self.job_id, self.nonce_base, flags)
 
     def on_results(self, records) -> None:
+        from .service import _as_record
+
         tpl = self.tpl
-        for job_id, hashes, shares in records:
+        for rec in records:
+            rec = _as_record(rec)
+            job_id, hashes, shares = rec.job_id, rec.hashes, rec.shares
             self.stats["hashes"] += hashes
             self.stats["windows"] += hashes > 0
             if tpl is None or job_id != self.job_id or not shares:
                 continue
             sh = shares[0]  # one block per template: the tip moves after it
-            height, hh = int(tpl["height"]), bytes.fromhex(tpl["pprpcheader"])
-            if not sh.verify_full(height, hh, bytes.fromhex(tpl["target"])):
-                self.stats["bad_shares"] += 1
-                log.log_printf(f"remote miner: share nonce {sh.nonce:016x} failed the full re-hash; dropped")
-                continue
-            self.stats["submitted"] += 1
-            try:
-                out = self.rpc.pprpcsb(tpl["pprpcheader"], bytes(sh.mix_hash).hex(), "%016x" % sh.nonce)
-            except RuntimeError as e:  # stale header, or a node that rejected the block
-                out = str(e)
+            height = int(tpl["height"])
+            if "equihash" in tpl:
+                inp = tpl["equihash"]["input"]
+                self.stats["submitted"] += 1
+                try:
+                    out = self.rpc.equihashsubmit(inp, sh.nonce256().hex(), sh.solution.hex())
+                except RuntimeError as e:
+                    out = str(e)
+            else:
+                hh = bytes.fromhex(tpl["pprpcheader"])
+                if not sh.verify_full(height, hh, bytes.fromhex(tpl["target"])):
+                    self.stats["bad_shares"] += 1
+                    log.log_printf(f"remote miner: share nonce {sh.nonce:016x} failed the full re-hash; dropped")
+                    continue
+                self.stats["submitted"] += 1
+                try:
+                    out = self.rpc.pprpcsb(tpl["pprpcheader"], bytes(sh.mix_hash).hex(), "%016x" % sh.nonce)
+                except RuntimeError as e:  # stale header, or a node that rejected the block
+                    out = str(e)
             ok = out is True or out is None or out == "duplicate"
             self.stats["accepted" if ok else "rejected"] += 1
             self.last_result = out
@@ -99,11 +122,10 @@ class RemoteLeader:
 
 
 def _device_for(backend):
-    """A miner/search device for `backend`: a search device as is; a host backend object
-    (CpuKawpowBackend) becomes a CpuSearchDevice."""
+    """A miner/search device for `backend`: a search device as is; None means this host's CPU."""
     from .search import CpuSearchDevice
 
-    if hasattr(backend, "submit") and hasattr(backend, "wait"):
+    if backend is not None and hasattr(backend, "submit") and hasattr(backend, "wait"):
         return backend
     return CpuSearchDevice()
 
@@ -123,7 +145,7 @@ class RemoteMiner:
         self.rank = int(rank)
         self.leader = RemoteLeader(rpc, refresh, int(nonce_base) + (self.rank << 56), rules)
         self.dev = _device_for(backend)
-        if getattr(self.dev, "name", "") == "cpu":
+        if getattr(self.dev, "name", "") == "cpu" and hasattr(self.dev, "max_window"):
             self.dev.max_window = min(self.dev.max_window, int(window))
         self.service = MiningService(self.dev, self.leader, window=int(window))
         self.stats = self.leader.stats
@@ -175,9 +197,10 @@ def main(argv: list[str] | None = None) -> int:
     params = make_params(a.network)
     rpc = RPCClient(a.get("rpcconnect", "127.0.0.1"), a.get_int("rpcport", params.default_rpc_port),
                     a.get("rpcuser"), a.get("rpcpassword"), None, timeout=60.0)
-    from .search import CpuSearchDevice, GpuSearchDevice
+    from .service import make_rank_device
 
-    backend = CpuSearchDevice() if a.get_bool("cpu", False) else GpuSearchDevice(a.get_int("gpu", 0))
+    cpu = a.get_bool("cpu", False)
+    backend = make_rank_device(cpu, None if cpu else a.get_int("gpu", 0), window=a.get_int("minerwindow", 4096))
     m = RemoteMiner(rpc, backend, window=a.get_int("minerwindow", 1 << 25), rank=a.get_int("minerrank", 0))
     blocks = a.get_int("blocks", 0)
     stats = m.run(max_blocks=blocks or None)

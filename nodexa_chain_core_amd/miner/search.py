@@ -1,28 +1,33 @@
-"""Pipelined KawPow nonce search on one device — the loop the node mines with and bench.py times.
+"""Pipelined nonce search on one device — the loop the node mines with and bench.py times.
 
 Reference behaviour: the miner's inner loop (CloreMiner, src/miner.cpp:566-726: search, check
-for a stale tip, count hashes) and progpow::search (src/crypto/ethash/lib/ethash/progpow.cpp:
-553-579). The MI355X form differs in three ways that matter for throughput:
+for a stale tip, count hashes), progpow::search (src/crypto/ethash/lib/ethash/progpow.cpp:
+553-579) and generateBlocks' legacy nNonce scan (src/rpc/mining.cpp:141-149). One work packet
+format and one two-slot device protocol carry every proof of work the chain knows:
 
-* **Big windows, two result slots.** Each launch searches 2^25 nonces (about 120 ms at epoch
-  384: ~43k workgroups, far past the 512 that fill the chip). The device owns two share rings;
-  the host queues window k+1 before it reads window k, and each ring is copied to pinned host
-  memory on the search stream right behind its kernel, so the GPU is never idle waiting for the
-  host and the host never blocks on the kernel it just queued.
-* **Stale-work abort on the device.** Every launch carries a generation number; the device
-  reads a host-mapped generation word once per workgroup (kawpow_search.hip). `abort()` bumps
-  the word when the template changes, so queued work of the old template stops within one
-  workgroup's lifetime (~1.4 ms) instead of finishing a 120 ms window. Workgroups that exit this
-  way are counted in the ring (`skipped`), so the hash counter stays exact.
-* **Shares are only candidates.** The kernel tests the top 64 bits of the final hash; the
-  host applies the full 256-bit boundary and the miner fully re-hashes a share (light mode)
-  before it builds a block from it (service.ChainLeader).
+* **KawPow** (GpuSearchDevice / CpuSearchDevice). Each GPU launch searches 2^25 nonces (~120 ms at
+  epoch 384: ~43k workgroups, far past the 512 that fill the chip). The device owns two share
+  rings; the host queues window k+1 before it reads window k, and each ring is copied to pinned
+  host memory on the search stream right behind its kernel, so the GPU is never idle waiting for
+  the host. Every launch carries a generation number that the kernel reads once per workgroup from
+  a host-mapped word: `abort()` bumps it when the template changes, so queued work of the old
+  template stops within one workgroup's lifetime (~1.4 ms). The kernel tests the top 64 bits of the
+  final hash; the host applies the full 256-bit boundary and the leader fully re-hashes a share
+  (light mode) before it builds a block from it (service.ChainLeader).
+* **Equihash(200,9)** (miner/equihash_search.py). A window is `count` nonce256 values
+  (le64(nonce) || 24 zero bytes) appended to the 80-byte header prefix; the GPU solves them in one
+  launch sequence, verifies every solution on the device and the host keeps the solutions whose
+  SHA256d(header) meets the boundary.
+* **X16R / X16RV2** (LegacyHostDevice): templates before the KawPow activation (the default on
+  regtest) scan the 32-bit nNonce on the host cores (csrc/pow/x16r.cpp).
 
-`CpuSearchDevice` runs the same protocol on the host (light-mode search, the reference's
-search_light) so the multi-rank loop can be tested with the gloo backend on CPU-only machines.
+`RankDevice` routes each slot to the device of its work packet's algorithm, so one loop, one set
+of collectives and one failure path serve every era of the chain; `FaultInjectingDevice`
+(-gpufailrate / -dropshare) and `HangingDevice` wrap any of them for the failure tests.
 """
 from __future__ import annotations
 
+import hashlib
 import struct
 import threading
 import time
@@ -33,27 +38,44 @@ from .. import core
 _core = core()
 
 # Work packet (collective #1): broadcast from rank 0 on every step of the mining loop.
-#   header_hash 32 | boundary 32 (big-endian 256-bit target) | height u32 | epoch u32 |
-#   job_id u64 | nonce_base u64 | flags u64  = 96 bytes
-WORK_FMT = "<32s32sIIQQQ"
+#   header 80 (KawPow: the header hash in bytes 0..31; Equihash: the 80-byte CKAWPOWInput-layout
+#   prefix the nonce256 is appended to; X16R: the 80-byte legacy header with nNonce 0) |
+#   boundary 32 (big-endian 256-bit target) | height u32 | algo u32 | job_id u64 |
+#   nonce_base u64 | flags u64  = 144 bytes
+WORK_FMT = "<80s32sIIQQQ"
 WORK_SIZE = struct.calcsize(WORK_FMT)
-assert WORK_SIZE == 96
+assert WORK_SIZE == 144
 
 FLAG_IDLE = 1    # nothing to mine: drain and wait for the next packet
 FLAG_STOP = 2    # leave the mining loop
 FLAG_CLEAN = 4   # the previous job is stale: abort its queued work
 
+ALGO_KAWPOW, ALGO_EQUIHASH, ALGO_X16R, ALGO_X16RV2 = 0, 1, 2, 3
+ALGO_NAMES = ("kawpow", "equihash", "x16r", "x16rv2")
+
 EPOCH_PREBUILD_WINDOW = 120  # blocks before an epoch boundary at which the next DAG is prebuilt
+LEGACY_WINDOW = 1 << 16      # nNonce values per host X16R window
+EQ_SOLUTION_PREFIX = b"\xfd\x40\x05"  # CompactSize(1344) in front of the packed solution
 
 
 @dataclass(frozen=True)
 class Work:
-    header_hash: bytes = bytes(32)   # KawPow header hash, progpow storage order
+    header: bytes = bytes(80)
     boundary: bytes = bytes(32)      # share/block target, big-endian
     height: int = 0
     job_id: int = 0
     nonce_base: int = 0
     flags: int = FLAG_IDLE
+    algo: int = ALGO_KAWPOW
+
+    def __post_init__(self):
+        if len(self.header) != 80:
+            object.__setattr__(self, "header", bytes(self.header)[:80].ljust(80, b"\0"))
+
+    @property
+    def header_hash(self) -> bytes:
+        """KawPow header hash (progpow storage order)."""
+        return self.header[:32]
 
     @property
     def epoch(self) -> int:
@@ -68,34 +90,72 @@ class Work:
         return bool(self.flags & FLAG_STOP)
 
     def pack(self) -> bytes:
-        return struct.pack(WORK_FMT, self.header_hash, self.boundary, self.height, self.epoch, self.job_id,
+        return struct.pack(WORK_FMT, self.header, self.boundary, self.height, self.algo, self.job_id,
                            self.nonce_base, self.flags)
 
     @classmethod
     def unpack(cls, raw: bytes) -> "Work":
-        hh, b, height, _epoch, job, base, flags = struct.unpack(WORK_FMT, raw)
-        return cls(hh, b, height, job, base, flags)
+        hdr, b, height, algo, job, base, flags = struct.unpack(WORK_FMT, raw)
+        return cls(hdr, b, height, job, base, flags, algo)
 
     def target64(self) -> int:
         """Upper 64 bits of the boundary: the kernel's prefix test never rejects a hash the full
         256-bit compare would accept."""
         return int.from_bytes(self.boundary[:8], "big")
 
+    def target(self) -> int:
+        return int.from_bytes(self.boundary, "big")
+
+
+def equihash_nonce256(nonce: int) -> bytes:
+    """The nonce256 a window's 64-bit nonce stands for (the rest of the space is left unused)."""
+    return struct.pack("<Q", nonce & 0xFFFFFFFFFFFFFFFF) + bytes(24)
+
+
+def equihash_block_hash(prefix80: bytes, nonce: int, solution: bytes) -> bytes:
+    """SHA256d of the serialized extended header (storage order, as uint256): the Equihash
+    extension's block hash (csrc/chain/primitives.cpp BlockHeader::equihash_hash)."""
+    ser = prefix80 + equihash_nonce256(nonce) + EQ_SOLUTION_PREFIX + solution
+    return hashlib.sha256(hashlib.sha256(ser).digest()).digest()
+
+
+@dataclass
+class EquihashShare:
+    nonce: int           # the 64-bit nonce of equihash_nonce256
+    solution: bytes      # 1344-byte packed solution
+    block_hash: bytes    # SHA256d(header), storage order
+
+    def nonce256(self) -> bytes:
+        return equihash_nonce256(self.nonce)
+
+
+@dataclass
+class LegacyShare:
+    nonce: int           # 32-bit nNonce
+    block_hash: bytes    # X16R / X16RV2 hash, storage order
+
 
 @dataclass
 class SlotResult:
-    """One finished window: the shares that pass the full 256-bit boundary and the nonces that
-    were actually evaluated (an aborted window counts only the workgroups that ran)."""
+    """One finished window: the shares that pass the full 256-bit boundary and the work that was
+    actually done (nonces hashed; Equihash: solutions found). An aborted window counts only the
+    workgroups that ran; `aborted` is the number that did not."""
     job_id: int
     start: int
     count: int
     hashes: int
     shares: list = field(default_factory=list)
     device_ms: float = 0.0
+    aborted: int = 0
+    algo: int = ALGO_KAWPOW
 
 
 class DeviceHung(RuntimeError):
     """A window did not finish within the watchdog limit."""
+
+
+class DeviceFault(RuntimeError):
+    """A window failed on the device (a kernel error, a lost device, an injected fault)."""
 
 
 class GpuSearchDevice:
@@ -121,6 +181,7 @@ class GpuSearchDevice:
         self.epochs: dict[int, object] = {}
         self.searchers: dict[int, object] = {}
         self.lock = threading.Lock()
+        self.dag_build_s: dict[int, float] = {}
         nbytes = self.h.sizeof_results()
         with torch.cuda.device(self.device):
             self.stream = torch.cuda.Stream(device=self.device)
@@ -154,6 +215,7 @@ class GpuSearchDevice:
 
         torch = self.torch
         ws = W.get().world_size if self.collective_dag else 1
+        t0 = time.perf_counter()
         with torch.cuda.device(self.device):
             e = DeviceEpoch(epoch, device=self.device, world_size=ws)
             with torch.cuda.stream(stream or self.stream):
@@ -161,10 +223,14 @@ class GpuSearchDevice:
                     pdag.build_dag(e)
                 else:
                     e.build()
+        self.dag_build_s[epoch] = time.perf_counter() - t0  # host-side issue time; completion below
         return e
 
     def epoch_ready(self, epoch: int) -> bool:
         return epoch in self.epochs
+
+    def resident_epochs(self) -> list[int]:
+        return sorted(self.epochs)
 
     def prebuild(self, epoch: int) -> None:
         """Queue epoch's DAG build on the side stream (collective when sharded; every rank calls this
@@ -183,6 +249,7 @@ class GpuSearchDevice:
         if epoch in self.epochs:
             return self.epochs[epoch]
         torch = self.torch
+        t0 = time.perf_counter()
         if epoch in self.pending_build:
             e, ev = self.pending_build.pop(epoch)
             self.stream.wait_event(ev)  # search kernels after the build, without a host sync
@@ -192,6 +259,7 @@ class GpuSearchDevice:
             self.stream.synchronize()
             if not e.l1_matches():
                 raise RuntimeError(f"gpu{self.device}: epoch {epoch} DAG failed its L1 self-check")
+        self.dag_build_s[epoch] = self.dag_build_s.get(epoch, 0.0) + time.perf_counter() - t0
         for old in [k for k in self.epochs if k < epoch - 1]:
             self.epochs.pop(old)
             self.searchers.pop(old, None)
@@ -215,6 +283,10 @@ class GpuSearchDevice:
 
     def block_for(self, height: int) -> int:
         return self.searcher(height).block
+
+    def window_for(self, work: Work, window: int) -> int:
+        b = self.block_for(work.height)
+        return max(b, window // b * b)
 
     # ------------------------------------------------------------------ the two slots
     def submit(self, slot: int, work: Work, start: int, count: int) -> None:
@@ -248,7 +320,8 @@ class GpuSearchDevice:
         shares, _n, skipped = parse_results(self.host[slot].numpy().tobytes(), self.h.KAWPOW_MAX_SHARES)
         shares = [x for x in shares if _core.hash_le(x.final_hash, work.boundary)]
         hashes = max(0, count - skipped * block)
-        return SlotResult(work.job_id, start, count, hashes, shares, self.starts[slot].elapsed_time(ev))
+        return SlotResult(work.job_id, start, count, hashes, shares, self.starts[slot].elapsed_time(ev), skipped,
+                          ALGO_KAWPOW)
 
     def abort(self) -> None:
         """Make every queued or running window stale (its remaining workgroups exit at start)."""
@@ -276,8 +349,14 @@ class CpuSearchDevice:
     def block_for(self, height: int) -> int:
         return 1
 
+    def window_for(self, work: Work, window: int) -> int:
+        return max(1, min(int(window), self.max_window))
+
     def epoch_ready(self, epoch: int) -> bool:
         return True
+
+    def resident_epochs(self) -> list[int]:
+        return []
 
     def prebuild(self, epoch: int) -> None:
         _core.get_epoch_context(epoch)
@@ -291,7 +370,7 @@ class CpuSearchDevice:
         work, start, count, gen = self.meta[slot]
         self.meta[slot] = None
         if gen != self.generation:  # aborted before it ran
-            return SlotResult(work.job_id, start, count, 0, [])
+            return SlotResult(work.job_id, start, count, 0, [], 0.0, 1, ALGO_KAWPOW)
         t0 = time.perf_counter()
         ctx = _core.get_epoch_context(work.epoch)
         ok, nonce, fin, mix = _core.kawpow_search_light(ctx, work.height, work.header_hash, work.boundary,
@@ -309,6 +388,129 @@ class CpuSearchDevice:
 
     def close(self) -> None:
         pass
+
+
+class LegacyHostDevice:
+    """X16R / X16RV2 templates (before the KawPow activation; the regtest default): the 32-bit
+    nNonce scanned on the host cores by the native multi-threaded search (csrc/pow/x16r.cpp,
+    `_core.x16r_search`), first hit of each window — generateBlocks' loop (src/rpc/mining.cpp:
+    141-149) in windows. The 32-bit space is split 2^28 per rank (`start` wraps inside it)."""
+
+    name = "host-x16r"
+    device = -1
+
+    def __init__(self):
+        self.meta: list[tuple | None] = [None, None]
+        self.generation = 0
+
+    def window_for(self, work: Work, window: int) -> int:
+        return LEGACY_WINDOW
+
+    def submit(self, slot: int, work: Work, start: int, count: int) -> None:
+        self.meta[slot] = (work, start & 0xFFFFFFFF, count, self.generation)
+
+    def wait(self, slot: int, timeout_s: float | None = None) -> SlotResult:
+        work, start, count, gen = self.meta[slot]
+        self.meta[slot] = None
+        if gen != self.generation:
+            return SlotResult(work.job_id, start, count, 0, [], 0.0, 1, work.algo)
+        count = min(count, (1 << 32) - start)
+        t0 = time.perf_counter()
+        target_le = work.boundary[::-1]
+        res, hashes = _core.x16r_search(work.header, work.algo == ALGO_X16RV2, target_le, start, count)
+        dt = (time.perf_counter() - t0) * 1e3
+        shares = [LegacyShare(int(res[0]), bytes(res[1]))] if res is not None else []
+        return SlotResult(work.job_id, start, count, int(hashes), shares, dt, 0, work.algo)
+
+    def abort(self) -> None:
+        self.generation += 1
+
+    def synchronize(self) -> None:
+        pass
+
+    def close(self) -> None:
+        pass
+
+
+class RankDevice:
+    """Everything one rank mines with, behind the two-slot protocol: the KawPow device (GPU or host),
+    the Equihash device (made on first use: GPU solver or host golden solver) and the host X16R
+    search. Each slot goes to the device of its work's algorithm, so a chain crossing an activation
+    time switches algorithms between two windows with no change to the loop."""
+
+    def __init__(self, kawpow, equihash=None, legacy=None, equihash_factory=None):
+        self.kawpow = kawpow
+        self._equihash = equihash
+        self._eq_factory = equihash_factory
+        self.legacy = legacy if legacy is not None else LegacyHostDevice()
+        self.slot_dev: list[object | None] = [None, None]
+        self.name = getattr(kawpow, "name", "dev")
+        self.device = getattr(kawpow, "device", -1)
+
+    @property
+    def collective_dag(self) -> bool:
+        return getattr(self.kawpow, "collective_dag", False)
+
+    @property
+    def equihash(self):
+        if self._equihash is None:
+            if self._eq_factory is None:
+                from .equihash_search import EquihashCpuDevice
+
+                self._equihash = EquihashCpuDevice()
+            else:
+                self._equihash = self._eq_factory()
+        return self._equihash
+
+    def dev_for(self, work: Work):
+        if work.algo == ALGO_KAWPOW:
+            return self.kawpow
+        if work.algo == ALGO_EQUIHASH:
+            return self.equihash
+        return self.legacy
+
+    def window_for(self, work: Work, window: int) -> int:
+        return self.dev_for(work).window_for(work, window)
+
+    def block_for(self, height: int) -> int:
+        return self.kawpow.block_for(height)
+
+    def epoch_ready(self, epoch: int) -> bool:
+        return self.kawpow.epoch_ready(epoch)
+
+    def resident_epochs(self) -> list[int]:
+        return self.kawpow.resident_epochs() if hasattr(self.kawpow, "resident_epochs") else []
+
+    def prebuild(self, epoch: int) -> None:
+        self.kawpow.prebuild(epoch)
+
+    def submit(self, slot: int, work: Work, start: int, count: int) -> None:
+        d = self.dev_for(work)
+        self.slot_dev[slot] = d
+        d.submit(slot, work, start, count)
+
+    def wait(self, slot: int, timeout_s: float | None = None) -> SlotResult:
+        d, self.slot_dev[slot] = self.slot_dev[slot], None
+        return d.wait(slot, timeout_s)
+
+    def abort(self) -> None:
+        for d in (self.kawpow, self._equihash, self.legacy):
+            if d is not None:
+                d.abort()
+
+    def synchronize(self) -> None:
+        for d in (self.kawpow, self._equihash):
+            if d is not None:
+                d.synchronize()
+
+    def close(self) -> None:
+        for d in (self.kawpow, self._equihash, self.legacy):
+            if d is not None and hasattr(d, "close"):
+                d.close()
+
+
+def as_rank_device(dev) -> RankDevice:
+    return dev if isinstance(dev, (RankDevice, FaultInjectingDevice, HangingDevice)) else RankDevice(dev)
 
 
 class SearchPipeline:
@@ -336,18 +538,50 @@ class SearchPipeline:
         return self.dev.wait(prev, self.watchdog_s)
 
 
-class HangingDevice:
+class _Wrapper:
+    def __init__(self, inner):
+        self.inner = inner
+
+    def __getattr__(self, name):
+        return getattr(self.inner, name)
+
+
+class FaultInjectingDevice(_Wrapper):
+    """-gpufailrate / -dropshare (SURVEY §5 fault injection; never on by default): each window fails
+    with probability `fail_rate` (wait() raises DeviceFault after the window ran, as a device error
+    surfaces), and each share is silently lost with probability `drop_rate` (a share lost between
+    device and host). Wraps any device of the two-slot protocol."""
+
+    def __init__(self, inner, fail_rate: float = 0.0, drop_rate: float = 0.0, seed: int | None = None):
+        import random
+
+        super().__init__(inner)
+        self.fail_rate, self.drop_rate = float(fail_rate), float(drop_rate)
+        self.rng = random.Random(seed)
+        self.dropped = 0
+        self.faults = 0
+
+    def wait(self, slot: int, timeout_s: float | None = None) -> SlotResult:
+        res = self.inner.wait(slot, timeout_s)
+        if self.fail_rate and self.rng.random() < self.fail_rate:
+            self.faults += 1
+            raise DeviceFault(f"injected device fault on {getattr(self.inner, 'name', 'dev')}")
+        if self.drop_rate and res.shares:
+            kept = [s for s in res.shares if self.rng.random() >= self.drop_rate]
+            self.dropped += len(res.shares) - len(kept)
+            res.shares = kept
+        return res
+
+
+class HangingDevice(_Wrapper):
     """Fault injection (tests, `NODEXA_MINER_HANG_AFTER`): behaves like `inner` for `after` windows,
     then every window hangs — wait() blocks until the watchdog limit and raises DeviceHung, which is
     what a GPU whose kernel never returns looks like to the mining loop."""
 
     def __init__(self, inner, after: int):
-        self.inner = inner
+        super().__init__(inner)
         self.after = int(after)
         self.waits = 0
-
-    def __getattr__(self, name):
-        return getattr(self.inner, name)
 
     def wait(self, slot: int, timeout_s: float | None = None) -> SlotResult:
         self.waits += 1

@@ -1,35 +1,47 @@
-"""The node's KawPow miner: one process per GPU, nonce-space data parallelism over RCCL.
+"""The node's miner: one process per GPU, nonce-space data parallelism over RCCL.
 
 Reference: GenerateClores / CloreMiner (src/miner.cpp:566-759) run N host threads, each with its
-own template and a 32-bit nonce scan, and getmininginfo reports their nHashesPerSec
-(src/rpc/mining.cpp:209-250). Here every GPU is a rank of one torch.distributed world (backend
-"nccl" = RCCL over xGMI on the MI355X node; "gloo" for CPU rehearsals) and all ranks run the
-same loop, `MiningService.step`:
+own template and a 32-bit nonce scan; generateBlocks (src/rpc/mining.cpp:117-173) is a second,
+separate loop; getmininginfo reports nHashesPerSec (src/rpc/mining.cpp:209-250). Here there is
+one loop for everything. Every GPU is a rank of one torch.distributed world (backend "nccl" =
+RCCL over xGMI on the MI355X node; "gloo" for CPU rehearsals; a single CPU-only rank needs no
+process group at all) and all ranks run the same step, `MiningService.step`:
 
-  1. queue the next 2^25-nonce window on this rank's device and take the previous window's
-     result (miner/search.SearchPipeline: the GPU never waits for the host);
-  2. all-gather every rank's share record (fixed 1176-byte slot: job, hashes, up to 16 shares);
-  3. all-reduce the step's hash counters (and the next-epoch readiness votes);
-  4. rank 0 (the node: chain state, RPC) fully re-hashes shares in light mode, builds the block
-     of the share's job and runs ProcessNewBlock; then it decides the next work packet;
-  5. broadcast the 96-byte work packet from rank 0; a new job with FLAG_CLEAN makes every rank
+  1. queue the next window on this rank's device and take the previous window's result
+     (miner/search.SearchPipeline: the GPU never waits for the host). The work packet says which
+     proof of work: KawPow (2^25-nonce GPU windows), Equihash(200,9) (16 solver instances per
+     window) or X16R/X16RV2 (host windows of 2^16 nNonce values, before the KawPow activation);
+  2. all-gather every rank's record (fixed 5592-byte slot: job, work done, shares, and the rank's
+     own telemetry: device time, aborted workgroups, collective wait, failures, resident epochs);
+  3. all-reduce the step's work counters (and the next-epoch readiness votes);
+  4. rank 0 (the node: chain state, RPC) checks shares again (KawPow: full light-mode re-hash;
+     Equihash: the golden verifier; X16R: the block check), builds the block of the share's job
+     and runs ProcessNewBlock; then it decides the next work packet;
+  5. broadcast the 144-byte work packet from rank 0; a new job with FLAG_CLEAN makes every rank
      abort its queued window of the stale job on the device.
 
-Nonce partition: rank r of n searches job-local windows from nonce_base + (r << 56), so ranks
-never overlap and a job change (new extranonce -> new header hash) restarts every cursor.
-DAGs are built sharded over the ranks and all-gathered (parallel/dag.py); the next epoch's DAG is
-prebuilt on a side stream once every rank reports its light cache ready (an all-reduced vote, so
-the collective build starts on the same step everywhere).
+Nonce partition: rank r of n searches job-local windows from nonce_base + (r << 56) (X16R's 32-bit
+nNonce: r << 28), so ranks never overlap and a job change (new extranonce -> new header) restarts
+every cursor. DAGs are built sharded over the ranks and all-gathered (parallel/dag.py); the next
+epoch's DAG is prebuilt on a side stream once every rank reports its light cache ready (an
+all-reduced vote, so the collective build starts on the same step everywhere).
 
-Failure handling: a rank whose window outlives the watchdog exits with
-EXIT_DEVICE_HUNG (a fresh process on restart, never a re-exec). Survivors see their next
-collective fail or time out, register in the rendezvous store under a new membership epoch, wait
-out a grace period, rebuild the group over the ranks that registered (parallel/world.shrink) and
-carry on; rank 0 then issues a clean job so the nonce space is re-partitioned over the new ranks.
+Failure handling (the reference's miner just exits on errors, src/miner.cpp:716-725):
+* a window that raises (a device fault; -gpufailrate injects them) counts a failure; after
+  `max_failures` in a row the rank's device is evicted: a follower rank exits with
+  EXIT_DEVICE_FAILED and the survivors re-form without it, rank 0 keeps leading without searching;
+* a rank whose window outlives the watchdog exits with EXIT_DEVICE_HUNG (a fresh process on
+  restart, never a re-exec). Survivors see their next collective fail or time out, register in the
+  rendezvous store under a new membership epoch, wait out a grace period, rebuild the group over
+  the ranks that registered (parallel/world.shrink) and carry on; rank 0 then issues a clean job
+  so the nonce space is re-partitioned over the new ranks.
+Resume: the leader persists {tip, extranonce} (miner_state.json); a restart on the same tip
+continues the extranonce sequence, so no template searched before the restart is searched again.
 """
 from __future__ import annotations
 
 import datetime
+import json
 import os
 import struct
 import sys
@@ -40,40 +52,100 @@ from dataclasses import dataclass, field
 
 from .. import core
 from ..utils import log
-from .search import (EPOCH_PREBUILD_WINDOW, FLAG_CLEAN, FLAG_IDLE, FLAG_STOP, WORK_SIZE, DeviceHung,
-                     SearchPipeline, SlotResult, Work)
+from .search import (ALGO_EQUIHASH, ALGO_KAWPOW, ALGO_NAMES, ALGO_X16R, ALGO_X16RV2, EPOCH_PREBUILD_WINDOW,
+                     FLAG_CLEAN, FLAG_IDLE, FLAG_STOP, WORK_SIZE, DeviceFault, DeviceHung, EquihashShare,
+                     LegacyShare, SearchPipeline, SlotResult, Work, as_rank_device)
 
 _core = core()
 
 EXIT_DEVICE_HUNG = 75
-MAX_SHARES_PER_STEP = 16
-_REC_HEAD = struct.Struct("<QQII")           # job_id, hashes, nshares, flags
-_REC_SHARE = struct.Struct("<Q32s32s")        # nonce, mix, final
-RECORD_SIZE = _REC_HEAD.size + MAX_SHARES_PER_STEP * _REC_SHARE.size  # 1176
+EXIT_DEVICE_FAILED = 76
+MAX_SHARES = {ALGO_KAWPOW: 16, ALGO_EQUIHASH: 4, ALGO_X16R: 16, ALGO_X16RV2: 16}
+MAX_SHARES_PER_STEP = MAX_SHARES[ALGO_KAWPOW]
+# job, work done, nshares, algo, device_us, aborted workgroups, collective wait us (previous step),
+# consecutive failures, first resident epoch, resident epochs, status bits, device index
+_REC_HEAD = struct.Struct("<QQIIIIIIIIIi")
+_SHARE = {ALGO_KAWPOW: struct.Struct("<Q32s32s"),        # nonce, mix, final
+          ALGO_EQUIHASH: struct.Struct("<Q1344s32s"),    # nonce, packed solution, block hash
+          ALGO_X16R: struct.Struct("<Q32s"),             # nNonce, block hash
+          ALGO_X16RV2: struct.Struct("<Q32s")}
+RECORD_PAYLOAD = max(MAX_SHARES[a] * s.size for a, s in _SHARE.items())  # 5536
+RECORD_SIZE = _REC_HEAD.size + RECORD_PAYLOAD                           # 5592
+STATUS_RESULT, STATUS_ALIVE = 1, 2
 
 
 class CollectiveError(RuntimeError):
     """A collective of the mining loop failed or timed out (a peer rank is gone or hung)."""
 
 
-def pack_record(res: SlotResult | None) -> bytes:
-    if res is None:
-        return bytes(RECORD_SIZE)
-    shares = res.shares[:MAX_SHARES_PER_STEP]
+class DeviceEvicted(RuntimeError):
+    """This rank's device failed `max_failures` windows in a row."""
+
+
+@dataclass
+class RankRecord:
+    """One rank's gathered step record."""
+    job_id: int = 0
+    hashes: int = 0
+    shares: list = field(default_factory=list)
+    algo: int = ALGO_KAWPOW
+    device_ms: float = 0.0
+    aborted: int = 0
+    coll_ms: float = 0.0
+    failures: int = 0
+    epochs: list = field(default_factory=list)
+    has_result: bool = False
+    alive: bool = True
+    device: int = -1
+
+
+def _as_record(r) -> RankRecord:
+    if isinstance(r, RankRecord):
+        return r
+    job, hashes, shares = r  # (job_id, hashes, shares) tuples: tests, remote leader
+    return RankRecord(job, hashes, list(shares), has_result=True)
+
+
+def pack_record(res: SlotResult | None, *, coll_ms: float = 0.0, failures: int = 0, epochs=(),
+                alive: bool = True, device: int = -1) -> bytes:
     out = bytearray(RECORD_SIZE)
-    _REC_HEAD.pack_into(out, 0, res.job_id, res.hashes, len(shares), 1)
+    ep = sorted(epochs)
+    lo, n = (ep[0], ep[-1] - ep[0] + 1) if ep else (0, 0)
+    status = (STATUS_RESULT if res is not None else 0) | (STATUS_ALIVE if alive else 0)
+    if res is None:
+        _REC_HEAD.pack_into(out, 0, 0, 0, 0, 0, 0, 0, int(coll_ms * 1e3), failures, lo, n, status, device)
+        return bytes(out)
+    fmt = _SHARE[res.algo]
+    shares = res.shares[:MAX_SHARES[res.algo]]
+    _REC_HEAD.pack_into(out, 0, res.job_id, res.hashes, len(shares), res.algo, min(int(res.device_ms * 1e3), 2**32 - 1),
+                        res.aborted, min(int(coll_ms * 1e3), 2**32 - 1), failures, lo, n, status, device)
     for i, s in enumerate(shares):
-        _REC_SHARE.pack_into(out, _REC_HEAD.size + i * _REC_SHARE.size, s.nonce, s.mix_hash, s.final_hash)
+        off = _REC_HEAD.size + i * fmt.size
+        if res.algo == ALGO_KAWPOW:
+            fmt.pack_into(out, off, s.nonce, s.mix_hash, s.final_hash)
+        elif res.algo == ALGO_EQUIHASH:
+            fmt.pack_into(out, off, s.nonce, s.solution, s.block_hash)
+        else:
+            fmt.pack_into(out, off, s.nonce, s.block_hash)
     return bytes(out)
 
 
-def unpack_record(raw: bytes) -> tuple[int, int, list]:
+def unpack_record(raw: bytes) -> RankRecord:
     from ..ops.kawpow import Share
 
-    job, hashes, n, _flags = _REC_HEAD.unpack_from(raw, 0)
-    shares = [Share(*_REC_SHARE.unpack_from(raw, _REC_HEAD.size + i * _REC_SHARE.size))
-              for i in range(min(n, MAX_SHARES_PER_STEP))]
-    return job, hashes, shares
+    job, hashes, n, algo, dev_us, aborted, coll_us, failures, lo, nep, status, device = _REC_HEAD.unpack_from(raw, 0)
+    fmt = _SHARE.get(algo, _SHARE[ALGO_KAWPOW])
+    shares = []
+    for i in range(min(n, MAX_SHARES.get(algo, 0))):
+        vals = fmt.unpack_from(raw, _REC_HEAD.size + i * fmt.size)
+        if algo == ALGO_KAWPOW:
+            shares.append(Share(*vals))
+        elif algo == ALGO_EQUIHASH:
+            shares.append(EquihashShare(*vals))
+        else:
+            shares.append(LegacyShare(*vals))
+    return RankRecord(job, hashes, shares, algo, dev_us / 1e3, aborted, coll_us / 1e3, failures,
+                      list(range(lo, lo + nep)), bool(status & STATUS_RESULT), bool(status & STATUS_ALIVE), device)
 
 
 class Comm:
@@ -81,29 +153,37 @@ class Comm:
 
     RCCL: tensors live on the GPU and the collectives are issued from a stream of their own, so
     they never queue behind the search kernel that is running on the search stream. gloo: host
-    tensors. A single rank needs no collective at all."""
+    tensors. Without a process group (a single CPU rank) there is nothing to exchange. A world
+    initialised with forced collectives (parallel/world.init(force_collectives=True)) runs them
+    even at world size 1, so a one-GPU box executes the same RCCL path as an 8-GPU node."""
 
     def __init__(self, timeout_s: float):
-        import torch
-
         from ..parallel import world as W
 
-        self.torch = torch
         self.W = W
         self.timeout = datetime.timedelta(seconds=timeout_s)
+        self.fail_at_step = int(os.environ.get("NODEXA_MINER_FAIL_COLLECTIVE_AT", "0"))  # test hook
+        self.calls = 0
         self.rebind()
 
     def rebind(self) -> None:
         """Bind to the current world. The loop gets a communicator of its own (not the default
         group), so a failed one can be aborted (RCCL) and replaced without touching the default
         group or its rendezvous store."""
-        torch, dist = self.torch, self.W.dist
         self.w = self.W.get()
+        self.active = self.w.collective
         self.gpu = self.w.backend == "nccl"
-        self.stream = torch.cuda.Stream(device=self.w.device) if self.gpu else None
+        self.stream = None
         self.group = self.w.group
-        if self.w.distributed and self.group is None:
-            self.group = dist.new_group(ranks=list(range(self.w.world_size)), timeout=self.timeout)
+        if self.active:
+            import torch
+
+            self.torch = torch
+            dist = self.W.dist
+            if self.gpu:
+                self.stream = torch.cuda.Stream(device=self.w.device)
+            if self.group is None:
+                self.group = dist.new_group(ranks=list(range(self.w.world_size)), timeout=self.timeout)
 
     def abort(self) -> None:
         """Tear down the loop's communicator after a failure: RCCL kernels still waiting for a dead
@@ -113,6 +193,8 @@ class Comm:
                 self.W.dist.distributed_c10d._abort_process_group(self.group)
             except Exception as e:  # noqa: BLE001 — best effort; the survivors re-form regardless
                 log.log_printf(f"miner: aborting the failed communicator: {e}")
+        if self.w.group is None:
+            self.group = None  # rebind() makes a fresh loop communicator
 
     def _wait(self, work, what: str) -> None:
         try:
@@ -123,6 +205,9 @@ class Comm:
             raise CollectiveError(f"{what}: timed out")
 
     def _run(self, fn, what: str):
+        self.calls += 1
+        if self.fail_at_step and self.calls == self.fail_at_step:
+            raise CollectiveError(f"{what}: timed out (injected, NODEXA_MINER_FAIL_COLLECTIVE_AT)")
         torch = self.torch
         if self.gpu:
             with torch.cuda.device(self.w.device), torch.cuda.stream(self.stream):
@@ -132,7 +217,7 @@ class Comm:
         return fn()
 
     def broadcast(self, payload: bytes | None, size: int) -> bytes:
-        if not self.w.distributed:
+        if not self.active:
             return payload
         torch, dist = self.torch, self.W.dist
 
@@ -148,7 +233,7 @@ class Comm:
         return self._run(go, "broadcast")
 
     def all_gather(self, record: bytes) -> list[bytes]:
-        if not self.w.distributed:
+        if not self.active:
             return [record]
         torch, dist = self.torch, self.W.dist
         n, ws = len(record), self.w.world_size
@@ -169,7 +254,7 @@ class Comm:
         return self._run(go, "all_gather")
 
     def all_reduce_sum(self, vals: list[int]) -> list[int]:
-        if not self.w.distributed:
+        if not self.active:
             return list(vals)
         torch, dist = self.torch, self.W.dist
 
@@ -184,7 +269,7 @@ class Comm:
 
 
 class RateMeter:
-    """Hashes per second over a sliding window (getmininginfo.hashespersec)."""
+    """Work per second over a sliding window (getmininginfo.hashespersec)."""
 
     def __init__(self, window_s: float = 8.0):
         self.window_s = window_s
@@ -209,7 +294,7 @@ class RateMeter:
 @dataclass
 class MiningRequest:
     """generate / setgenerate on rank 0: mine with `script` until `blocks` are found (None =
-    until stopped) or `max_tries` hashes are spent."""
+    until stopped) or `max_tries` units of work (hashes; Equihash: solutions) are spent."""
     script: bytes
     blocks: int | None = None
     max_tries: int | None = None
@@ -224,12 +309,24 @@ class Job:
     job_id: int
     block: object
     height: int
-    header_hash: bytes
+    header: bytes         # the work packet's header field
     boundary: bytes
     prev: bytes
     tx_updated: int
     created: float
     script: bytes
+    algo: int = ALGO_KAWPOW
+    tries: int = 0
+
+
+def algo_for_time(params, t: int) -> int:
+    """Which proof of work a header with nTime `t` carries (src/primitives/block.cpp:38-74 +
+    the Equihash extension's activation)."""
+    if t >= params.equihash_activation_time:
+        return ALGO_EQUIHASH
+    if t >= params.kawpow_activation_time:
+        return ALGO_KAWPOW
+    return ALGO_X16RV2 if t >= params.x16rv2_activation_time else ALGO_X16R
 
 
 class ChainLeader:
@@ -237,12 +334,14 @@ class ChainLeader:
 
     Templates come from BlockAssembler (src/miner.cpp:123-256) with IncrementExtraNonce
     (:508-525) per job; a job is replaced when the tip moves, when the pool changed and the job is
-    older than `refresh_s` (the reference's 60 s mempool check, src/miner.cpp:700-705), or when
-    the world was re-partitioned. Every share is re-hashed in full (light mode) before its block is
-    built; only shares of a job whose parent is still the tip are submitted (the reference's
-    "generated block is stale" check, ProcessBlockFound)."""
+    older than `refresh_s` (the reference's 60 s mempool check, src/miner.cpp:700-705), when a
+    legacy job has spent its 2^28 nNonce values per rank, or when the world was re-partitioned.
+    Every share is checked again before its block is built; only shares of a job whose parent is
+    still the tip are submitted (the reference's "generated block is stale" check,
+    ProcessBlockFound)."""
 
-    def __init__(self, state, *, refresh_s: float = 10.0, target_bits: int = 0, on_block=None):
+    def __init__(self, state, *, refresh_s: float = 10.0, target_bits: int = 0, on_block=None,
+                 state_path: str | None = None):
         from .assembler import ExtraNonce
 
         self.state = state
@@ -257,6 +356,29 @@ class ChainLeader:
         self.force_new = False
         self.stopping = False
         self.stats = {"shares": 0, "stale_shares": 0, "bad_shares": 0, "blocks": 0, "rejected": 0}
+        self.per_rank: dict[int, dict] = {}
+        self.state_path = state_path
+        self._resume = self._load_state()
+
+    # ---------------------------------------------------------------- resume state
+    def _load_state(self) -> dict:
+        if not self.state_path or not os.path.exists(self.state_path):
+            return {}
+        try:
+            with open(self.state_path) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return {}
+
+    def save_state(self) -> None:
+        if not self.state_path:
+            return
+        data = {"tip": _core.u256_hex(self.extranonce.prev) if self.extranonce.prev else None,
+                "extranonce": self.extranonce.n, "job": self.job_seq, "time": int(time.time())}
+        tmp = self.state_path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(data, f)
+        os.replace(tmp, self.state_path)
 
     # ---------------------------------------------------------------- called from RPC threads
     def mine(self, script: bytes, blocks: int | None = None, max_tries: int | None = None) -> MiningRequest:
@@ -275,15 +397,53 @@ class ChainLeader:
         if req is not None:
             req.done.set()
 
+    def fail(self, why: str) -> None:
+        """The loop cannot mine any more (every device evicted): end the request with an error."""
+        with self.lock:
+            req = self.request
+        if req is not None and not req.done.is_set():
+            req.error = why
+            req.done.set()
+
     def shutdown(self) -> None:
         self.stop_mining()
         self.stopping = True
 
     # ---------------------------------------------------------------- called from the loop thread
-    def next_work(self, repartitioned: bool = False) -> Work:
+    def _new_job(self, req: MiningRequest) -> Job:
         from ..chain.header import to_progpow
         from .assembler import BlockAssembler
 
+        st = self.state
+        tpl = BlockAssembler(st).create_new_block(req.script)
+        blk = tpl.block
+        hdr = blk.header
+        if self.extranonce.prev != hdr.prev and self._resume.get("tip") == _core.u256_hex(hdr.prev):
+            # a restart on the tip of a saved run: continue its extranonce sequence
+            self.extranonce.prev, self.extranonce.n = hdr.prev, int(self._resume.get("extranonce", 0))
+        self.extranonce.increment(blk, tpl.height)
+        hdr = blk.header
+        algo = algo_for_time(st.params, hdr.time)
+        target = tpl.target if self.miner_target is None else min(tpl.target, self.miner_target)
+        if algo == ALGO_KAWPOW:
+            header = to_progpow(hdr.kawpow_header_hash())
+        elif algo == ALGO_EQUIHASH:
+            header = hdr.kawpow_input()  # version (with the extension bit), prev, merkle, time, bits, height
+        else:
+            header = hdr.legacy80()
+        self.job_seq += 1
+        job = Job(self.job_seq, blk, tpl.height, header, target.to_bytes(32, "big"), hdr.prev,
+                  st.transactions_updated, time.time(), req.script, algo)
+        self.jobs[job.job_id] = job
+        while len(self.jobs) > 8:
+            self.jobs.popitem(last=False)
+        try:
+            self.save_state()
+        except OSError:
+            pass
+        return job
+
+    def next_work(self, repartitioned: bool = False) -> Work:
         if self.stopping:
             return Work(flags=FLAG_STOP)
         with self.lock:
@@ -296,61 +456,84 @@ class ChainLeader:
         tip = st.tip()
         cur = next(reversed(self.jobs.values())) if self.jobs else None
         stale = (cur is None or force or cur.prev != tip.hash or cur.script != req.script
-                 or (st.transactions_updated != cur.tx_updated and time.time() - cur.created > self.refresh_s))
+                 or (st.transactions_updated != cur.tx_updated and time.time() - cur.created > self.refresh_s)
+                 or (cur.algo in (ALGO_X16R, ALGO_X16RV2) and cur.tries >= 1 << 28))
         if not stale:
-            return Work(cur.header_hash, cur.boundary, cur.height, cur.job_id, 0, 0)
-        tpl = BlockAssembler(st).create_new_block(req.script)
-        blk = tpl.block
-        if blk.header.time < st.params.kawpow_activation_time:
-            req.error = "template is before the KawPow activation time (X16R/X16RV2 is mined on the host)"
-            req.done.set()
-            return Work(flags=FLAG_IDLE)
-        self.extranonce.increment(blk, tpl.height)
-        hdr = blk.header
-        target = tpl.target if self.miner_target is None else min(tpl.target, self.miner_target)
-        self.job_seq += 1
-        job = Job(self.job_seq, blk, tpl.height, to_progpow(hdr.kawpow_header_hash()), target.to_bytes(32, "big"),
-                  hdr.prev, st.transactions_updated, time.time(), req.script)
-        self.jobs[job.job_id] = job
-        while len(self.jobs) > 8:
-            self.jobs.popitem(last=False)
-        return Work(job.header_hash, job.boundary, job.height, job.job_id, 0, FLAG_CLEAN)
+            return Work(cur.header, cur.boundary, cur.height, cur.job_id, 0, 0, cur.algo)
+        job = self._new_job(req)
+        return Work(job.header, job.boundary, job.height, job.job_id, 0, FLAG_CLEAN, job.algo)
 
-    def on_results(self, records: list[tuple[int, int, list]]) -> None:
+    def _rank_stats(self, r: int) -> dict:
+        return self.per_rank.setdefault(r, {"shares": 0, "stale_shares": 0, "bad_shares": 0, "blocks": 0})
+
+    def _check_share(self, job: Job, sh) -> bool:
+        if job.algo == ALGO_KAWPOW:
+            return sh.verify_full(job.height, job.header[:32], job.boundary)
+        if job.algo == ALGO_EQUIHASH:
+            from .search import equihash_block_hash
+
+            p = _core.EquihashParams(200, 9)
+            inp = job.header + sh.nonce256()
+            ok = bool(_core.equihash_verify(p, inp, _core.equihash_unpack(p, sh.solution))[0])
+            bh = equihash_block_hash(job.header, sh.nonce, sh.solution)
+            return ok and bh == sh.block_hash and int.from_bytes(bh, "little") <= int.from_bytes(job.boundary, "big")
+        return int.from_bytes(sh.block_hash, "little") <= int.from_bytes(job.boundary, "big")
+
+    def _block_for(self, job: Job, sh):
         from ..chain.header import from_progpow
 
+        act = self.state.params.kawpow_activation_time
+        blk = _core.Block.deserialize(job.block.serialize(act), act)
+        hdr = blk.header
+        if job.algo == ALGO_KAWPOW:
+            hdr.nonce64 = sh.nonce
+            hdr.mix_hash = from_progpow(sh.mix_hash)
+        elif job.algo == ALGO_EQUIHASH:
+            hdr.nonce256 = sh.nonce256()
+            hdr.solution = sh.solution
+        else:
+            hdr.nonce = sh.nonce
+        blk.header = hdr
+        return blk
+
+    def on_results(self, records) -> None:
+        records = [_as_record(r) for r in records]
         req = self.request
-        hashes = sum(h for _, h, _ in records)
+        for r, rec in enumerate(records):
+            job = self.jobs.get(rec.job_id)
+            if job is not None:
+                job.tries += rec.hashes
         if req is None:
             return
-        req.tries += hashes
+        req.tries += sum(rec.hashes for rec in records)
         st = self.state
-        act = st.params.kawpow_activation_time
-        for job_id, _h, shares in records:
-            for sh in shares:
+        for r, rec in enumerate(records):
+            rs = self._rank_stats(r)
+            for sh in rec.shares:
                 if req.done.is_set():
                     break
                 self.stats["shares"] += 1
-                job = self.jobs.get(job_id)
+                rs["shares"] += 1
+                job = self.jobs.get(rec.job_id)
                 if job is None or job.prev != st.tip().hash:
                     self.stats["stale_shares"] += 1
+                    rs["stale_shares"] += 1
                     continue
-                if not sh.verify_full(job.height, job.header_hash, job.boundary):
+                if not self._check_share(job, sh):
                     self.stats["bad_shares"] += 1
-                    log.log_printf(f"miner: share nonce {sh.nonce:#x} of job {job_id} failed full re-hash; dropped")
+                    rs["bad_shares"] += 1
+                    log.log_printf(f"miner: {ALGO_NAMES[job.algo]} share nonce {sh.nonce:#x} of job {rec.job_id} "
+                                   f"(rank {r}) failed the host check; dropped")
                     continue
-                blk = _core.Block.deserialize(job.block.serialize(act), act)
-                hdr = blk.header
-                hdr.nonce64 = sh.nonce
-                hdr.mix_hash = from_progpow(sh.mix_hash)
-                blk.header = hdr
+                blk = self._block_for(job, sh)
                 res = st.process_new_block(blk)
                 if not res.ok:
                     self.stats["rejected"] += 1
-                    log.log_printf(f"miner: block of job {job_id} rejected: {res.reject}")
+                    log.log_printf(f"miner: block of job {rec.job_id} rejected: {res.reject}")
                     continue
-                bh = st.block_hash(hdr)
+                bh = st.block_hash(blk.header)
                 self.stats["blocks"] += 1
+                rs["blocks"] += 1
                 req.found.append(_core.u256_hex(bh))
                 st._emit("block_found", bh)
                 if self.on_block is not None:
@@ -364,14 +547,15 @@ class ChainLeader:
 
 
 class BenchLeader:
-    """A fixed synthetic job (bench.py): the same loop, no chain. Shares are kept for the full
-    re-hash check after the timed region."""
+    """A fixed synthetic job (bench.py): the same loop, no chain. Shares are kept for the host
+    re-check after the timed region."""
 
     def __init__(self, work: Work, keep: int = 64):
-        self.work = Work(work.header_hash, work.boundary, work.height, work.job_id or 1, work.nonce_base, 0)
+        self.work = Work(work.header, work.boundary, work.height, work.job_id or 1, work.nonce_base, 0, work.algo)
         self.first = True
         self.keep = keep
         self.shares: list = []
+        self.records = 0
         self.stopping = False
 
     def next_work(self, repartitioned: bool = False) -> Work:
@@ -380,13 +564,14 @@ class BenchLeader:
         if self.first or repartitioned:
             self.first = False
             w = self.work
-            return Work(w.header_hash, w.boundary, w.height, w.job_id, w.nonce_base, FLAG_CLEAN)
+            return Work(w.header, w.boundary, w.height, w.job_id, w.nonce_base, FLAG_CLEAN, w.algo)
         return self.work
 
     def on_results(self, records) -> None:
-        for _job, _h, shares in records:
+        for rec in (_as_record(r) for r in records):
+            self.records += rec.has_result
             if len(self.shares) < self.keep:
-                self.shares.extend(shares[:self.keep - len(self.shares)])
+                self.shares.extend(rec.shares[:self.keep - len(self.shares)])
 
     def shutdown(self) -> None:
         self.stopping = True
@@ -397,23 +582,26 @@ class MiningService:
 
     def __init__(self, device, leader=None, *, window: int = 1 << 25, watchdog_s: float = 120.0,
                  collective_timeout_s: float = 60.0, grace_s: float | None = None, idle_sleep_s: float = 0.02,
-                 record_windows: bool = False):
+                 record_windows: bool = False, max_failures: int = 3):
         from ..parallel import world as W
 
         self.W = W
-        self.dev = device
+        self.dev = as_rank_device(device)
         self.leader = leader
         self.window = int(window)
-        self.pipe = SearchPipeline(device, watchdog_s)
+        self.pipe = SearchPipeline(self.dev, watchdog_s)
         self.comm = Comm(collective_timeout_s)
         self.collective_timeout_s = float(collective_timeout_s)
         self.grace_s = float(grace_s) if grace_s is not None else 2 * self.collective_timeout_s + 1
         self.idle_sleep_s = float(idle_sleep_s)
+        self.max_failures = int(max_failures)
         self.work = Work()
         self.cursor = 0
         self.rate = RateMeter()
         self.hashes_total = 0
         self.rank_hashes: dict[int, int] = {}
+        self.rank_info_raw: dict[int, dict] = {}
+        self.rank_rates: dict[int, RateMeter] = {}
         self.steps = 0
         self.membership = 0
         self.repartitioned = False
@@ -422,6 +610,11 @@ class MiningService:
         self._thread: threading.Thread | None = None
         self.error: BaseException | None = None
         self.last_step_ms = 0.0
+        self.coll_ms = 0.0
+        self.failures = 0          # consecutive failed windows on this rank
+        self.total_failures = 0
+        self.dev_alive = True
+        self.last_error = ""
 
     @property
     def rank(self) -> int:
@@ -438,7 +631,7 @@ class MiningService:
     def _next_epoch_vote(self) -> int:
         """1 when this rank has the next epoch's light cache (prebuild window only)."""
         w = self.work
-        if w.idle or w.height % _core.EPOCH_LENGTH < _core.EPOCH_LENGTH - EPOCH_PREBUILD_WINDOW:
+        if w.idle or w.algo != ALGO_KAWPOW or w.height % _core.EPOCH_LENGTH < _core.EPOCH_LENGTH - EPOCH_PREBUILD_WINDOW:
             return 0
         nxt = w.epoch + 1
         if self.dev.epoch_ready(nxt):
@@ -452,25 +645,55 @@ class MiningService:
             return 0
         return 1
 
+    def _window_start(self, w: Work) -> int:
+        if w.algo in (ALGO_X16R, ALGO_X16RV2):
+            return ((self.rank & 0xF) << 28) | (self.cursor & 0x0FFFFFFF)
+        return (w.nonce_base + (self.rank << 56) + self.cursor) & 0xFFFFFFFFFFFFFFFF
+
+    def _device_failure(self, err: Exception) -> None:
+        self.failures += 1
+        self.total_failures += 1
+        self.last_error = f"{type(err).__name__}: {err}"
+        log.log_printf(f"miner rank {self.rank}: window failed ({self.last_error}), {self.failures} in a row")
+        if self.failures >= self.max_failures and self.dev_alive:
+            self.dev_alive = False
+            log.log_printf(f"miner rank {self.rank}: device evicted after {self.failures} failed windows")
+            try:
+                self.pipe.drain()
+            except Exception:  # noqa: BLE001 — the device is being given up
+                self.pipe.inflight = None
+            if self.leader is None:
+                raise DeviceEvicted(self.last_error)
+
     def step(self) -> bool:
         """One iteration of the loop on this rank; False once a stop packet has been processed."""
         t0 = time.perf_counter()
         w = self.work
-        if w.idle:
-            res = self.pipe.drain()
-            if res is None:
-                time.sleep(self.idle_sleep_s)
-        else:
-            start = w.nonce_base + (self.rank << 56) + self.cursor
-            block = self.dev.block_for(w.height)
-            count = max(block, self.window // block * block)
-            if self.windows is not None:
-                self.windows.append((w.job_id, start, count))
-            res = self.pipe.step(w, start, count)
-            self.cursor += count
+        res = None
+        try:
+            if w.idle or not self.dev_alive:
+                res = self.pipe.drain() if self.pipe.inflight is not None else None
+                if res is None:
+                    time.sleep(self.idle_sleep_s)
+            else:
+                count = self.dev.window_for(w, self.window)
+                start = self._window_start(w)
+                if self.windows is not None:
+                    self.windows.append((w.job_id, start, count))
+                self.cursor += count  # before the step: a window that fails was still searched once
+                res = self.pipe.step(w, start, count)
+            if res is not None:
+                self.failures = 0
+        except DeviceFault as e:
+            self._device_failure(e)
+            res = None
         vote = self._next_epoch_vote()
-        gathered = self.comm.all_gather(pack_record(res))
+        rec = pack_record(res, coll_ms=self.coll_ms, failures=self.failures, epochs=self.dev.resident_epochs(),
+                          alive=self.dev_alive, device=int(getattr(self.dev, "device", -1)))
+        tc = time.perf_counter()
+        gathered = self.comm.all_gather(rec)
         sums = self.comm.all_reduce_sum([res.hashes if res is not None else 0, vote])
+        coll = time.perf_counter() - tc
         self.hashes_total += sums[0]
         self.rate.add(sums[0])
         if vote and sums[1] == self.world_size:
@@ -480,12 +703,25 @@ class MiningService:
         payload = None
         if self.leader is not None:
             records = [unpack_record(r) for r in gathered]
-            for i, (_j, h, _s) in enumerate(records):
-                self.rank_hashes[i] = self.rank_hashes.get(i, 0) + h
+            now = time.monotonic()
+            for i, rec_i in enumerate(records):
+                self.rank_hashes[i] = self.rank_hashes.get(i, 0) + rec_i.hashes
+                self.rank_rates.setdefault(i, RateMeter()).add(rec_i.hashes, now)
+                info = self.rank_info_raw.setdefault(i, {"aborted": 0, "windows": 0})
+                info.update(alive=rec_i.alive, failures=rec_i.failures, epochs=rec_i.epochs, device=rec_i.device,
+                            coll_ms=rec_i.coll_ms)
+                if rec_i.has_result:
+                    info["windows"] += 1
+                    info["aborted"] += rec_i.aborted
+                    info.update(algo=rec_i.algo, device_ms=rec_i.device_ms)
             self.leader.on_results(records)
+            if self.world_size == 1 and not self.dev_alive and hasattr(self.leader, "fail"):
+                self.leader.fail("no mining device left (all evicted): " + self.last_error)
             payload = self.leader.next_work(self.repartitioned).pack()
             self.repartitioned = False
+        tc = time.perf_counter()
         new = Work.unpack(self.comm.broadcast(payload, WORK_SIZE))
+        self.coll_ms = (coll + time.perf_counter() - tc) * 1e3
         if new.job_id != w.job_id:
             self.cursor = 0
         if new.flags & FLAG_CLEAN or new.idle:
@@ -494,6 +730,40 @@ class MiningService:
         self.steps += 1
         self.last_step_ms = (time.perf_counter() - t0) * 1e3
         return not new.stop
+
+    # ---------------------------------------------------------------- observability
+    def rank_info(self) -> list[dict]:
+        """getmininginfo.gpus[]: one entry per rank of the world (rank 0 only)."""
+        out = []
+        stats = getattr(self.leader, "per_rank", {}) if self.leader is not None else {}
+        for r in range(self.world_size):
+            info = self.rank_info_raw.get(r, {})
+            rs = stats.get(r, {})
+            algo = info.get("algo", self.work.algo)
+            shares, stale = rs.get("shares", 0), rs.get("stale_shares", 0)
+            rate = self.rank_rates[r].rate() if r in self.rank_rates else 0.0
+            out.append({
+                "rank": r,
+                "device": info.get("device", -1),
+                "alive": info.get("alive", True) if r else self.dev_alive,
+                "algo": ALGO_NAMES[algo] if algo < len(ALGO_NAMES) else str(algo),
+                ("solutionspersec" if algo == ALGO_EQUIHASH else "hashespersec"): round(rate, 1),
+                "mhs": round(rate / 1e6, 3) if algo != ALGO_EQUIHASH else None,
+                "hashes": int(self.rank_hashes.get(r, 0)),
+                "shares": shares,
+                "stale_shares": stale,
+                "stale_rate": round(stale / shares, 4) if shares else 0.0,
+                "bad_shares": rs.get("bad_shares", 0),
+                "blocks": rs.get("blocks", 0),
+                "epochs_resident": info.get("epochs", []),
+                "last_device_ms": round(info.get("device_ms", 0.0), 3),
+                "last_step_ms": round(self.last_step_ms, 3),
+                "collective_ms": round(info.get("coll_ms", 0.0), 3),
+                "aborted_workgroups": info.get("aborted", 0),
+                "windows": info.get("windows", 0),
+                "failures": info.get("failures", 0),
+            })
+        return out
 
     # ---------------------------------------------------------------- failures
     def recover(self, err: Exception) -> None:
@@ -574,6 +844,97 @@ class MiningService:
         self._thread = None
 
 
+class Miner:
+    """The node's miner front-end (node.miner): generate / generatetoaddress / setgenerate /
+    getmininginfo on top of the mining service's leader. Every proof of work and every device
+    goes through the one loop; there is no second, thread-per-backend miner."""
+
+    def __init__(self, state, service: MiningService):
+        from ..utils.metrics import REGISTRY
+
+        self.state = state
+        self.service = service
+        self.leader: ChainLeader = service.leader
+        self.metrics = REGISTRY
+        self._req: MiningRequest | None = None
+        self.generating = False
+        self._last_hashes = 0
+        self._last_shares = 0
+
+    @classmethod
+    def local(cls, state, *, window: int = 4096, fail_rate: float = 0.0, drop_rate: float = 0.0,
+              max_failures: int = 3, watchdog_s: float = 120.0, state_path: str | None = None,
+              target_bits: int = 0, start: bool = True) -> "Miner":
+        """A single-rank miner on this host's CPU devices (CPU-only nodes, tests)."""
+        from .search import CpuSearchDevice, FaultInjectingDevice, RankDevice
+
+        dev = RankDevice(CpuSearchDevice(max_window=window))
+        if fail_rate or drop_rate:
+            dev = FaultInjectingDevice(dev, fail_rate, drop_rate, seed=0)
+        leader = ChainLeader(state, state_path=state_path, target_bits=target_bits)
+        svc = MiningService(dev, leader, window=window, watchdog_s=watchdog_s, max_failures=max_failures)
+        return cls(state, svc.start() if start else svc)
+
+    @property
+    def hashrate(self) -> float:
+        """getmininginfo.hashespersec: the all-reduced rate over every rank (src/miner.cpp:685-687)."""
+        return self.service.hashrate()
+
+    def workers(self) -> list[dict]:
+        return [{"worker": g["rank"], "backend": f"{getattr(self.service.dev, 'name', 'dev')}-rank{g['rank']}",
+                 "alive": g["alive"], "hashes": g["hashes"], "blocks": g["blocks"], "failures": g["failures"]}
+                for g in self.service.rank_info()]
+
+    def _export_metrics(self) -> None:
+        h, s = self.service.hashes_total, self.leader.stats["shares"]
+        if h > self._last_hashes:
+            self.metrics.inc("miner_hashes_total", h - self._last_hashes, worker="service")
+        if s > self._last_shares:
+            self.metrics.inc("miner_shares_total", s - self._last_shares, worker="service")
+        self._last_hashes, self._last_shares = h, s
+
+    def generate(self, script_pubkey: bytes, nblocks: int, max_tries: int = 1_000_000) -> list[str]:
+        """generateBlocks: the new block hashes (display hex), mined by the service."""
+        svc = self.service
+        if svc.error is not None:
+            raise RuntimeError(f"miner service stopped: {svc.error}")
+        req = self.leader.mine(script_pubkey, blocks=nblocks, max_tries=max_tries)
+        while not req.done.wait(0.2):
+            if svc.error is not None:
+                raise RuntimeError(f"miner service stopped: {svc.error}")
+        self._export_metrics()
+        for _ in req.found:
+            self.metrics.inc("miner_blocks_total", 1, worker="service")
+        if req.error is not None and not req.found:
+            if req.error == "superseded":
+                return []
+            raise RuntimeError(req.error)
+        return list(req.found)
+
+    def set_generate(self, on: bool, script_pubkey: bytes | None = None) -> None:
+        self.stop()
+        if not on:
+            return
+        if script_pubkey is None:
+            raise ValueError("setgenerate true needs -miningaddress")
+        self._req = self.leader.mine(script_pubkey)  # until setgenerate false
+        self.generating = True
+
+    def stop(self) -> None:
+        if self._req is not None:
+            self.leader.stop_mining()
+            for _ in self._req.found:
+                self.metrics.inc("miner_blocks_total", 1, worker="service")
+            self._req = None
+        self._export_metrics()
+        self.generating = False
+
+    def close(self) -> None:
+        """Node shutdown: stop mining and end the service loop (its stop packet ends every rank)."""
+        self.stop()
+        self.service.stop()
+
+
 # -------------------------------------------------------------------- follower processes
 def spawn_followers(gpus: list[int], port: int, cpu: bool = False, extra_env: dict | None = None) -> list:
     """Start ranks 1..n-1 of the miner world as child processes (before this process touches a GPU;
@@ -592,6 +953,27 @@ def spawn_followers(gpus: list[int], port: int, cpu: bool = False, extra_env: di
     return procs
 
 
+def make_rank_device(cpu: bool, device_index: int | None = None, collective_dag: bool = False, window: int = 4096,
+                     fail_rate: float = 0.0, drop_rate: float = 0.0, seed: int = 0, eq_window: int = 1):
+    """This rank's RankDevice: GPU KawPow + GPU Equihash (built on first use), or the host
+    equivalents; -gpufailrate / -dropshare wrap it."""
+    from .equihash_search import EquihashCpuDevice
+    from .search import CpuSearchDevice, FaultInjectingDevice, RankDevice
+
+    if cpu:
+        dev = RankDevice(CpuSearchDevice(max_window=window), EquihashCpuDevice(eq_window))
+    else:
+        from .equihash_search import EquihashGpuDevice
+        from .search import GpuSearchDevice
+
+        idx = int(device_index or 0)
+        dev = RankDevice(GpuSearchDevice(idx, collective_dag=collective_dag),
+                         equihash_factory=lambda: EquihashGpuDevice(idx))
+    if fail_rate or drop_rate:
+        dev = FaultInjectingDevice(dev, fail_rate, drop_rate, seed=seed)
+    return dev
+
+
 def follower_main() -> int:
     """Entry point of ranks >= 1 (spawned by the node or launched by torchrun)."""
     from ..parallel import world as W
@@ -603,14 +985,10 @@ def follower_main() -> int:
     window = int(os.environ.get("NODEXA_MINER_WINDOW", str(1 << 25)))
     W.init(use_gpu=not cpu, device_index=None if dev_index is None else int(dev_index),
            timeout_s=int(max(timeout, 10)), elastic=True)
-    if cpu:
-        from .search import CpuSearchDevice
-
-        dev = CpuSearchDevice(max_window=window)
-    else:
-        from .search import GpuSearchDevice
-
-        dev = GpuSearchDevice(W.get().device.index, collective_dag=W.get().distributed)
+    w = W.get()
+    dev = make_rank_device(cpu, w.device.index if not cpu else None, collective_dag=w.collective, window=window,
+                           fail_rate=float(os.environ.get("NODEXA_MINER_FAILRATE", "0") or 0),
+                           drop_rate=float(os.environ.get("NODEXA_MINER_DROPSHARE", "0") or 0), seed=w.rank)
     hang = int(os.environ.get("NODEXA_MINER_HANG_AFTER", "0"))
     if hang > 0:  # fault injection for the failure-handling tests
         from .search import HangingDevice
@@ -618,15 +996,14 @@ def follower_main() -> int:
         dev = HangingDevice(dev, hang)
     wlog = os.environ.get("NODEXA_MINER_WINDOWS_LOG")
     svc = MiningService(dev, None, window=window, watchdog_s=watchdog, collective_timeout_s=timeout,
-                        record_windows=bool(wlog))
+                        record_windows=bool(wlog), max_failures=int(os.environ.get("NODEXA_MINER_MAXFAILURES", "3")))
 
     def dump():
         if wlog:
-            import json
-
             with open(wlog, "w") as f:
                 json.dump({"rank": svc.rank, "world_size": svc.world_size, "windows": svc.windows,
-                           "steps": svc.steps, "hashes_total": svc.hashes_total}, f)
+                           "steps": svc.steps, "hashes_total": svc.hashes_total,
+                           "failures": svc.total_failures}, f)
 
     try:
         svc.run()
@@ -634,6 +1011,10 @@ def follower_main() -> int:
         log.log_printf(f"miner rank {W.get().rank}: {e}; exiting so the survivors re-partition")
         dump()
         os._exit(EXIT_DEVICE_HUNG)
+    except DeviceEvicted as e:
+        log.log_printf(f"miner rank {W.get().rank}: device evicted ({e}); exiting so the survivors re-partition")
+        dump()
+        os._exit(EXIT_DEVICE_FAILED)
     except RuntimeError as e:
         log.log_printf(f"miner rank {W.get().rank}: {e}")
         dump()

@@ -26,7 +26,7 @@ import time
 from . import core
 from .chain.state import ChainState, make_params
 from .miner.assembler import BlockAssembler, ExtraNonce
-from .miner.kawpow_miner import CpuKawpowBackend, FaultInjector, MinerController
+from .miner.service import Miner
 from .rpc import (methods, methods_assets, methods_ext, methods_index, methods_messages, methods_util, methods_wallet,
                   methods_wallet_ext)
 from .rpc.server import RPCServer, RPCTable, delete_cookie, make_cookie
@@ -58,12 +58,13 @@ class Node:
         self.last_block_tx = 0
         self.last_block_weight = 0
         self.pprpc_templates: dict[str, object] = {}
+        self.equihash_templates: dict[str, object] = {}
         self._last_pprpc: tuple[str, float] | None = None
         self.gpus = gpu_list(args)
         self.rpc_witness = True  # -rpcserialversion=1
         self.asset_index = args.get_bool("assetindex", False)  # -assetindex: per-address asset balance RPCs
         self.state: ChainState | None = None
-        self.miner: MinerController | None = None
+        self.miner: Miner | None = None
         self.rpc: RPCServer | None = None
         self.table = RPCTable()
         addr = args.get("miningaddress")
@@ -314,16 +315,9 @@ class Node:
             n = self.state.load_mempool(os.path.join(self.datadir, "mempool.dat"))
             if n:
                 log.log_printf(f"Imported mempool transactions from disk: {n} succeeded")
-        # host threads: the CPU KawPow search (CPU-only nodes) and X16R/X16RV2 before the activation
-        backends = [CpuKawpowBackend(a.get_int("genproclimit", 1))]
-        fail, drop = float(a.get("gpufailrate", "0") or 0), float(a.get("dropshare", "0") or 0)
-        if fail or drop:  # fault injection for failure-handling tests (never on by default)
-            backends = [FaultInjector(b, fail, drop, seed=i) for i, b in enumerate(backends)]
-        self.miner = MinerController(
-            self.state, backends, max_failures=a.get_int("minermaxfailures", 3),
-            watchdog_s=float(a.get("minerwatchdog", "120")),
-            state_path=os.path.join(self.datadir, "miner_state.json") if self.datadir else None,
-            service=self._start_miner_service(a))
+        # the one miner: the mining service (miner/service.py) on every node — GPU ranks, or this
+        # host's CPU devices — with -gpufailrate / -dropshare fault injection around its devices
+        self.miner = Miner(self.state, self._start_miner_service(a))
         self.metrics_writer = None
         if a.get("metricslog"):
             path = a.get("metricslog")
@@ -378,24 +372,25 @@ class Node:
             self.miner.set_generate(True, self.mining_script)
 
     def _start_miner_service(self, a: ArgsManager):
-        """The KawPow mining service (miner/service.py): one rank per GPU of `-gpus`, this node being
-        rank 0. Ranks 1..n-1 are spawned as child processes here, before this process touches a
-        GPU; under torchrun (WORLD_SIZE > 1 in the environment) the launcher made them and this is
-        its rank 0. `-minerservice` runs the same loop on CPU devices (`-minerranks=N` processes),
-        for nodes and tests without a GPU."""
-        if not self.gpus and not a.get_bool("minerservice", False):
-            return None
+        """The mining service (miner/service.py): one rank per GPU of `-gpus`, this node being rank 0.
+        Ranks 1..n-1 are spawned as child processes here, before this process touches a GPU; under
+        torchrun (WORLD_SIZE > 1 in the environment) the launcher made them and this is its rank 0.
+        Without GPUs the same loop runs on this host's CPU devices: one rank and no process group,
+        or `-minerservice -minerranks=N` processes over gloo (rehearsals of the multi-GPU path)."""
         from .miner import service as MS
-        from .miner.search import CpuSearchDevice, GpuSearchDevice
         from .parallel import world as W
 
         cpu = not self.gpus
         timeout = float(a.get("minercollectivetimeout", "60"))
+        fail, drop = float(a.get("gpufailrate", "0") or 0), float(a.get("dropshare", "0") or 0)
         self.miner_procs = []
+        ranks = max(1, a.get_int("minerranks", 1)) if a.get_bool("minerservice", False) else 1
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)), elastic=True)
+        elif cpu and ranks == 1 and not a.get_bool("minerforcecollectives", False):
+            pass  # a single host rank: nothing to exchange, no process group
         else:
-            gpus = self.gpus or [0] * max(1, a.get_int("minerranks", 1))
+            gpus = self.gpus or [0] * ranks
             if len(gpus) > 1:
                 import socket
 
@@ -404,21 +399,25 @@ class Node:
                     port = sk.getsockname()[1]
                 os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
                 env = {"NODEXA_MINER_COLLECTIVE_TIMEOUT": str(timeout),
-                       "NODEXA_MINER_WATCHDOG": a.get("minerwatchdog", "120")}
+                       "NODEXA_MINER_WATCHDOG": a.get("minerwatchdog", "120"),
+                       "NODEXA_MINER_MAXFAILURES": str(a.get_int("minermaxfailures", 3)),
+                       "NODEXA_MINER_FAILRATE": str(fail), "NODEXA_MINER_DROPSHARE": str(drop)}
                 if a.get("gpuintensity"):
                     env["NODEXA_MINER_WINDOW"] = a.get("gpuintensity")
                 self.miner_procs = MS.spawn_followers(gpus, port, cpu=cpu, extra_env=env)
             W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)), device_index=None if cpu else gpus[0],
-                   rank=0, world_size=len(gpus), elastic=True)
+                   rank=0, world_size=len(gpus), elastic=True,
+                   force_collectives=a.get_bool("minerforcecollectives", False) or None)
         w = W.get()
         window = a.get_int("gpuintensity", 4096 if cpu else 1 << 25)
-        dev = CpuSearchDevice(max_window=window) if cpu else GpuSearchDevice(w.device.index,
-                                                                            collective_dag=w.distributed)
-        leader = MS.ChainLeader(self.state, target_bits=a.get_int("minertargetbits", 0))
+        dev = MS.make_rank_device(cpu, None if cpu else w.device.index, collective_dag=w.collective, window=window,
+                                  fail_rate=fail, drop_rate=drop, seed=0)
+        leader = MS.ChainLeader(self.state, target_bits=a.get_int("minertargetbits", 0),
+                                state_path=os.path.join(self.datadir, "miner_state.json") if self.datadir else None)
         log.log_printf(f"miner service: {w.world_size} rank(s), backend {w.backend}, "
                        f"{'cpu' if cpu else 'gpu'} devices, {window} nonces per window")
         return MS.MiningService(dev, leader, window=window, watchdog_s=float(a.get("minerwatchdog", "120")),
-                                collective_timeout_s=timeout).start()
+                                collective_timeout_s=timeout, max_failures=a.get_int("minermaxfailures", 3)).start()
 
     def params_assume_valid(self) -> str | None:
         """consensus.defaultAssumeValid: none is set for these networks here (the reference's main
@@ -791,6 +790,20 @@ class Node:
         ExtraNonce().increment(tpl.block, tpl.height)
         return tpl
 
+    def register_equihash_template(self, tpl) -> dict:
+        """The Equihash extension's template cache (the analogue of mapHVNKAWBlockTemplates): keyed by
+        the 80-byte input prefix, which an external solver extends with its nonce256."""
+        hdr = tpl.block.header
+        prefix = hdr.kawpow_input()
+        key = prefix.hex()
+        self.equihash_templates[key] = tpl
+        while len(self.equihash_templates) > 64:
+            self.equihash_templates.pop(next(iter(self.equihash_templates)))
+        return {"n": self.params.equihash_n, "k": self.params.equihash_k, "personalization": "ZcashPoW",
+                "input": key, "nonce_bytes": 32, "solution_bytes": _core.EquihashParams(
+                    self.params.equihash_n, self.params.equihash_k).solution_bytes,
+                "header_version": hdr.version}
+
     def register_pprpc_template(self, tpl) -> str:
         """mapHVNKAWBlockTemplates: reuse the last header for 30 s (src/rpc/mining.cpp:722-739)."""
         if self._last_pprpc is not None:
@@ -807,20 +820,22 @@ class Node:
         return hh
 
     def gpu_info(self) -> list[dict]:
-        out = []
+        """getmininginfo.gpus[]: every rank of the miner world (rate, shares, stale rate, resident
+        epochs, device / step / collective times, failures), plus this GPU's properties."""
         svc = self.miner.service if self.miner else None
-        for be in ([svc.dev] if svc is not None else []):
-            if getattr(be, "name", "") != "gpu":
-                continue
-            info = {"device": be.device, "epochs_resident": sorted(be.epochs.keys()), "intensity": svc.window,
-                    "ranks": svc.world_size, "last_step_ms": round(svc.last_step_ms, 3)}
+        if svc is None:
+            return []
+        out = svc.rank_info()
+        for g in out:
+            g["intensity"] = svc.window
+            g["ranks"] = svc.world_size
+        if out and self.gpus:
             try:
                 from .ops import runtime
 
-                info.update(runtime.hip().device_props(be.device))
+                out[0].update(runtime.hip().device_props(self.gpus[0]))
             except Exception as e:  # pragma: no cover
-                info["error"] = str(e)
-            out.append(info)
+                out[0]["error"] = str(e)
         return out
 
     def gpu_memory_info(self) -> list[dict]:

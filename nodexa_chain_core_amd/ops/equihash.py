@@ -16,6 +16,7 @@ from __future__ import annotations
 import os
 import struct
 
+import numpy as np
 import torch
 
 from .. import _core
@@ -43,6 +44,16 @@ def blake2b_h0(n: int = 200, k: int = 9) -> list[int]:
     param[60:64] = struct.pack("<I", k)
     words = struct.unpack("<8Q", bytes(param))
     return [a ^ b for a, b in zip(iv, words)]
+
+
+def pack_solutions(sols: np.ndarray) -> list[bytes]:
+    """(m, 512) leaf indices -> m packed 1344-byte solutions (512 x 21-bit big-endian), vectorised
+    (the same bytes as _core.equihash_pack)."""
+    sols = np.ascontiguousarray(np.asarray(sols, dtype=np.uint32).reshape(-1, 512))
+    be = (sols << np.uint32(11)).astype(">u4").view(np.uint8).reshape(-1, 512, 4)
+    bits = np.unpackbits(be, axis=2)[:, :, :21].reshape(len(sols), 512 * 21)
+    packed = np.packbits(bits, axis=1)
+    return [r.tobytes() for r in packed]
 
 
 @traced("equihash.verify")
@@ -129,6 +140,13 @@ class EquihashSolver:
             # per launch: [inst][EQP_STATS] truncation counters (ps) + [inst] candidate counts
             nstat = ni * self.h.EQP_STATS if ps else 0
             self._land_stats = [torch.zeros(nstat + ni, dtype=torch.int32).pin_memory() for _ in range(2)]
+            # device-side check of every solution slot (equihash.hip eq_verify_slots) right after the
+            # solve: the verdicts ride back with the solutions, so collect() needs no host pass over
+            # the 512 leaves of each solution (~225 us per solution on one core)
+            self.verify_kernel = runtime.static_kernel("equihash", "eq_verify_slots")
+            self.verdicts = torch.empty(ni * self.h.EQ_MAX_SOL, dtype=torch.int32, device=self.device)
+            self._land_verdicts = [torch.empty(ni * self.h.EQ_MAX_SOL, dtype=torch.int32).pin_memory()
+                                   for _ in range(2)]
             self.fallbacks = 0  # instances re-solved on the host because the device truncated something
             self.fallback_log: list[dict] = []
             self._stage = [torch.empty(ni * 16, dtype=torch.int64).pin_memory() for _ in range(2)]
@@ -169,17 +187,21 @@ class EquihashSolver:
                                                 self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block)
             else:
                 self._issue_global(s)
+            self.h.launch_equihash_verify_slots(self.verify_kernel, self.h0, self.msgs.data_ptr(), self.input_len,
+                                                self.num_inst, self.sols.data_ptr(), self.verdicts.data_ptr(), s)
             land = self._landing[self._next]
             lstat = self._land_stats[self._next]
+            lver = self._land_verdicts[self._next]
             self._next = (self._next + 1) % len(self._landing)
             land.copy_(self.sols, non_blocking=True)
+            lver.copy_(self.verdicts, non_blocking=True)
             nstat = lstat.numel() - self.num_inst
             if nstat:
                 lstat[:nstat].copy_(self.stats_buf, non_blocking=True)
             lstat[nstat:].copy_(self.cands.view(self.num_inst, -1)[:, 0], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
-        self._pending.append((list(inputs), (land, lstat), ev))
+        self._pending.append((list(inputs), (land, lstat, lver), ev))
 
     def _issue_global(self, s: int) -> None:
         args = (self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst, self.hashes.data_ptr(),
@@ -194,18 +216,23 @@ class EquihashSolver:
         else:
             self.h.launch_equihash_solve(*args, s, self.banks)
 
-    def collect(self, inputs: list[bytes] | None = None, verify: bool = True) -> list[list[list[int]]]:
-        """Solutions of the oldest queued launch (waits only for that launch)."""
+    def collect_arrays(self, inputs: list[bytes] | None = None, verify: str = "device") -> list[np.ndarray]:
+        """Solutions of the oldest queued launch (waits only for that launch), one (m, 512) uint32
+        array of leaf indices per instance. verify: "device" (the eq_verify_slots verdicts that came
+        back with the launch), "host" (the C++ golden verifier as well) or "none". A solution that
+        fails is a solver bug and raises."""
         if not self._pending:
             raise RuntimeError("nothing launched")
-        launched, (land, lstat), ev = self._pending.pop(0)
+        launched, (land, lstat, lver), ev = self._pending.pop(0)
         if inputs is not None and list(inputs) != launched:
             raise ValueError("collect() inputs differ from the oldest launch")
         inputs = launched
         ev.synchronize()
+        ms = self.h.EQ_MAX_SOL
         raw = land.numpy()
-        per = 1 + self.h.EQ_MAX_SOL * 512
+        per = 1 + ms * 512
         st = lstat.numpy()
+        verdicts = lver.numpy().reshape(self.num_inst, ms)
         nstat = st.size - self.num_inst
         out = []
         for i in range(self.num_inst):
@@ -219,20 +246,30 @@ class EquihashSolver:
                 self.fallbacks += 1
                 self.fallback_log.append({"stats": st[i * self.h.EQP_STATS:(i + 1) * self.h.EQP_STATS].tolist()
                                           if nstat else [], "candidates": int(st[nstat + i])})
-                sols, _ = _core.equihash_solve_cpu(self.params, inputs[i], self.h.EQ_MAX_SOL, 0)
-                out.append([list(x) for x in sols])
+                sols, _ = _core.equihash_solve_cpu(self.params, inputs[i], ms, 0)
+                out.append(np.asarray(sols, dtype=np.uint32).reshape(-1, 512))
                 continue
             base = i * per
-            n = min(int(raw[base]), self.h.EQ_MAX_SOL)
-            sols = []
-            for s in range(n):
-                idx = [int(v) for v in raw[base + 1 + s * 512: base + 1 + (s + 1) * 512]]
-                if verify and not _core.equihash_verify(self.params, inputs[i], idx)[0]:
-                    raise RuntimeError(f"GPU produced an invalid Equihash solution for instance {i}")
-                if idx not in sols:
-                    sols.append(idx)
-            out.append(sols)
+            n = min(int(raw[base]), ms)
+            sols = raw[base + 1: base + 1 + n * 512].view(np.uint32).reshape(n, 512)
+            if verify != "none" and n:
+                bad = np.flatnonzero(verdicts[i, :n] != 0)
+                if len(bad):
+                    raise RuntimeError(f"GPU produced an invalid Equihash solution for instance {i} "
+                                       f"(device verdict {int(verdicts[i, bad[0]])})")
+            if verify == "host":
+                for s in range(n):
+                    if not _core.equihash_verify(self.params, inputs[i], sols[s].tolist())[0]:
+                        raise RuntimeError(f"GPU produced an invalid Equihash solution for instance {i}")
+            if n > 1:  # distinct solutions only (the reconstruct stage may emit one tree twice)
+                _, first = np.unique(sols, axis=0, return_index=True)
+                sols = sols[np.sort(first)]
+            out.append(np.array(sols))
         return out
+
+    def collect(self, inputs: list[bytes] | None = None, verify: bool = True) -> list[list[list[int]]]:
+        """collect_arrays() as lists of index lists; verify=True also runs the host verifier."""
+        return [a.tolist() for a in self.collect_arrays(inputs, "host" if verify else "device")]
 
     @traced("equihash.solve")
     def solve(self, inputs: list[bytes]) -> list[list[list[int]]]:

@@ -18,7 +18,7 @@ from . import world as W
 def allgather_shards(full: torch.Tensor, per: int) -> None:
     """In place: rank r's bytes [r*per, (r+1)*per) of `full` are replicated to every rank."""
     w = W.get()
-    if not w.distributed:
+    if not w.collective:
         return
     if full.numel() != per * w.world_size:
         raise ValueError("buffer must hold exactly world_size shards")
@@ -33,7 +33,7 @@ def allgather_shards(full: torch.Tensor, per: int) -> None:
 def build_dag(epoch_dev) -> None:
     """Build `epoch_dev` (ops.ethash.DeviceEpoch): 1/world per rank, then all-gather."""
     w = W.get()
-    if not w.distributed:
+    if not w.collective:
         epoch_dev.build()
         return
     epoch_dev.build(shard=(w.rank, w.world_size))

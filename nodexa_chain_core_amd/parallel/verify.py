@@ -35,7 +35,7 @@ def _sharded_rows(jobs: np.ndarray, mode: str) -> np.ndarray:
     buf = torch.zeros((per, 64), dtype=torch.uint8, device=w.device)
     if len(local):
         buf[:len(local)] = torch.from_numpy(np.ascontiguousarray(local)).to(w.device)
-    if not w.distributed:
+    if not w.collective:
         return buf.cpu().numpy()[:m]
     out = torch.empty((per * w.world_size, 64), dtype=torch.uint8, device=w.device)
     dist.all_gather_into_tensor(out, buf, group=w.group)

@@ -34,6 +34,11 @@ class World:
         return self.world_size > 1
 
     @property
+    def collective(self) -> bool:
+        """There is a process group: collectives run (also at world size 1 when forced)."""
+        return self.backend != "none"
+
+    @property
     def is_main(self) -> bool:
         return self.rank == 0
 
@@ -42,17 +47,22 @@ _WORLD: World | None = None
 
 
 def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | None = None,
-         rank: int | None = None, world_size: int | None = None, elastic: bool = False) -> World:
+         rank: int | None = None, world_size: int | None = None, elastic: bool = False,
+         force_collectives: bool | None = None) -> World:
     """Initialise from RANK/WORLD_SIZE/LOCAL_RANK (torchrun, or the node's spawned miner ranks)
     or single-process; `rank` / `world_size` override the environment. `device_index`: the GPU
-    of this rank (default: LOCAL_RANK)."""
+    of this rank (default: LOCAL_RANK). `force_collectives` (env NODEXA_FORCE_COLLECTIVES=1):
+    make a process group even for one rank, so every collective of the miner, the DAG build and
+    batch verify really runs (one-rank RCCL on a 1-GPU box exercises the 8-GPU code path)."""
     global _WORLD
     rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
     world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else int(world_size)
+    if force_collectives is None:
+        force_collectives = os.environ.get("NODEXA_FORCE_COLLECTIVES", "0") == "1"
     if _WORLD is not None:
         # a single-process world left by an earlier user of this process (no communicator to
         # tear down) gives way to a request for a real one; anything else is reused as it is
-        if not (_WORLD.world_size == 1 and world_size > 1 and not dist.is_initialized()):
+        if not ((world_size > 1 or force_collectives) and not _WORLD.collective and not dist.is_initialized()):
             return _WORLD
         _WORLD = None
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -65,7 +75,7 @@ def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | 
     else:
         device = torch.device("cpu")
     backend = "none"
-    if world_size > 1:
+    if world_size > 1 or force_collectives:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         backend = "nccl" if use_gpu else "gloo"
@@ -111,14 +121,14 @@ def get() -> World:
 
 def shutdown() -> None:
     global _WORLD
-    if _WORLD is not None and _WORLD.distributed and dist.is_initialized():
+    if _WORLD is not None and _WORLD.collective and dist.is_initialized():
         dist.destroy_process_group()
     _WORLD = None
 
 
 def barrier() -> None:
     w = get()
-    if w.distributed:
+    if w.collective:
         if w.backend == "nccl":
             dist.barrier(group=w.group, device_ids=[w.device.index])
         else:
@@ -133,14 +143,14 @@ def broadcast_bytes(payload: bytes | None, size: int, src: int = 0) -> bytes:
         if len(payload) != size:
             raise ValueError("payload size mismatch")
         t.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
-    if w.distributed:
+    if w.collective:
         dist.broadcast(t, src=w.global_rank(src), group=w.group)
     return bytes(t.cpu().numpy().tobytes())
 
 
 def all_reduce_max(x: float) -> float:
     w = get()
-    if not w.distributed:
+    if not w.collective:
         return x
     t = torch.tensor([x], dtype=torch.float64, device=w.device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=w.group)
@@ -149,7 +159,7 @@ def all_reduce_max(x: float) -> float:
 
 def all_reduce_sum_int(x: int) -> int:
     w = get()
-    if not w.distributed:
+    if not w.collective:
         return x
     t = torch.tensor([x], dtype=torch.int64, device=w.device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=w.group)

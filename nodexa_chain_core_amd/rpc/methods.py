@@ -365,7 +365,13 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         }
         if tpl.witness_commitment:
             res["default_witness_commitment"] = tpl.witness_commitment.hex()
-        if hdr.time >= params.kawpow_activation_time and node.mining_script is not None:
+        if hdr.time >= params.equihash_activation_time:
+            # Equihash(200,9) extension era (new; the reference has no Equihash): the 80-byte input
+            # prefix of the cached template, for external solvers answering with equihashsubmit
+            # (the analogue of pprpcheader / pprpcsb); a full block goes through submitblock as usual
+            if node.mining_script is not None:
+                res["equihash"] = node.register_equihash_template(tpl)
+        elif hdr.time >= params.kawpow_activation_time and node.mining_script is not None:
             hh = node.register_pprpc_template(tpl)
             res["pprpcheader"] = hh
             res["pprpcepoch"] = tpl.height // _core.EPOCH_LENGTH
@@ -412,6 +418,36 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         blk.header = hdr
         pow_hash, _mix = st.chain.block_hash_full(hdr)
         if not _core.check_proof_of_work(pow_hash, hdr.bits, params):
+            raise RPCError(RPC_DESERIALIZATION_ERROR, "Block does not solve the boundary")
+        r = _submit(blk)
+        return True if r is None else r
+
+    def rpc_equihashsubmit(p):
+        """equihashsubmit "input_hex" "nonce256_hex" "solution_hex" — submit an Equihash(200,9)
+        solution for a template whose 80-byte input prefix getblocktemplate returned (the
+        extension's pprpcsb). Returns true, or the BIP22 rejection reason."""
+        if len(p) != 3:
+            raise RPCError(RPC_MISC_ERROR, 'equihashsubmit "input_hex" "nonce256_hex" "solution_hex"')
+        tpl = node.equihash_templates.get(str(p[0]).lower())
+        if tpl is None:
+            raise RPCError(RPC_INVALID_PARAMS, "Equihash input not found in block data")
+        try:
+            nonce256, solution = bytes.fromhex(p[1]), bytes.fromhex(p[2])
+        except (TypeError, ValueError):
+            raise RPCError(RPC_INVALID_PARAMS, "Invalid hex nonce or solution")
+        if len(nonce256) != 32:
+            raise RPCError(RPC_INVALID_PARAMS, "nonce256 must be 32 bytes")
+        act = params.kawpow_activation_time
+        blk = _core.Block.deserialize(tpl.block.serialize(act), act)
+        hdr = blk.header
+        hdr.nonce256 = nonce256
+        hdr.solution = solution
+        blk.header = hdr
+        ep = _core.EquihashParams(params.equihash_n, params.equihash_k)
+        if len(solution) != ep.solution_bytes or not _core.equihash_verify(ep, hdr.equihash_input(),
+                                                                           _core.equihash_unpack(ep, solution))[0]:
+            raise RPCError(RPC_DESERIALIZATION_ERROR, "Invalid Equihash solution")
+        if not _core.check_proof_of_work(hdr.equihash_hash(act), hdr.bits, params):
             raise RPCError(RPC_DESERIALIZATION_ERROR, "Block does not solve the boundary")
         r = _submit(blk)
         return True if r is None else r
@@ -480,6 +516,7 @@ def register(table, node) -> None:  # noqa: C901 — one table, like the referen
         ("getblocktemplate", rpc_getblocktemplate, ("template_request",)),
         ("submitblock", rpc_submitblock, ("hexdata", "dummy")),
         ("pprpcsb", rpc_pprpcsb, ("header_hash", "mix_hash", "nonce")),
+        ("equihashsubmit", rpc_equihashsubmit, ("input", "nonce256", "solution")),
         ("getkawpowhash", rpc_getkawpowhash, ("header_hash", "mix_hash", "nonce", "height", "target")),
         ("prioritisetransaction", rpc_prioritisetransaction, ("txid", "dummy", "fee_delta")),
         ("getgenerate", rpc_getgenerate, ()), ("setgenerate", rpc_setgenerate, ("generate", "genproclimit")),

@@ -16,10 +16,14 @@ _core = core()
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _mine(st, n):
-    from nodexa_chain_core_amd.miner.kawpow_miner import CpuKawpowBackend, MinerController
+def _mine(st, n, spk=bytes([0x51])):
+    from nodexa_chain_core_amd.miner.service import Miner
 
-    MinerController(st, [CpuKawpowBackend()]).generate(bytes([0x51]), n)
+    m = Miner.local(st)
+    try:
+        m.generate(spk, n)
+    finally:
+        m.close()
 
 
 def _utxo(st):
@@ -168,13 +172,11 @@ def test_reference_library_reads_chain_stores(tmp_path, ref_tool):
 
 
 def test_indexes_persist_as_block_tree_records(tmp_path):
-    from nodexa_chain_core_amd.miner.kawpow_miner import CpuKawpowBackend, MinerController
-
     flags = dict(txindex=True, addressindex=True, spentindex=True, timestampindex=True)
     h160 = bytes(range(20))
     spk = bytes.fromhex("76a914") + h160 + bytes.fromhex("88ac")
     st = _state(tmp_path, indexes=flags)
-    MinerController(st, [CpuKawpowBackend()]).generate(spk, 4)
+    _mine(st, 4, spk)
     tip = st.chain.tip()
     blk = st.get_block(tip.hash)
     cb = blk.vtx[0].txid()

@@ -1,7 +1,8 @@
-"""Multi-process (gloo, world_size 2 and 4, CPU) rehearsal of the RCCL paths in parallel/:
-work-packet broadcast, max/sum reductions, in-place DAG shard all-gather (slices
-filled with golden ethash items), share-ring all-gather, and the disjoint nonce
-partition bench.py and the miner use. Same code as the GPU path, gloo backend."""
+"""Multi-process (gloo, world_size 2 and 4, CPU) rehearsal of the RCCL paths in parallel/ and the
+miner: work-packet broadcast, max/sum reductions, in-place DAG shard all-gather (slices filled
+with golden ethash items), the mining loop's record all-gather (miner/service.Comm), and the
+disjoint nonce partition bench.py and the miner use. Same code as the GPU path, gloo backend.
+World size 1 with forced collectives is the one-rank process group a 1-GPU box runs over RCCL."""
 import os
 import socket
 import struct
@@ -29,10 +30,12 @@ def _worker(rank, world, port, q):
         from nodexa_chain_core_amd import _core
         from nodexa_chain_core_amd.parallel import dag as pdag
         from nodexa_chain_core_amd.parallel import world as W
-        from nodexa_chain_core_amd.parallel.shares import RING_HEADER, SHARE_SIZE, ShareGather
+        from nodexa_chain_core_amd.miner.search import SlotResult
+        from nodexa_chain_core_amd.miner.service import Comm, pack_record, unpack_record
+        from nodexa_chain_core_amd.ops.kawpow import Share
 
-        w = W.init(use_gpu=False)
-        assert w.backend == "gloo" and w.world_size == world
+        w = W.init(use_gpu=False, force_collectives=world == 1)
+        assert w.backend == "gloo" and w.world_size == world and w.collective
         # 1. work packet broadcast from rank 0
         pkt = struct.pack("<32sQII", bytes(range(32)), 7, 1234, 0)
         got = W.broadcast_bytes(pkt if rank == 0 else None, len(pkt))
@@ -52,16 +55,13 @@ def _worker(rank, world, port, q):
         raw = full.numpy().tobytes()
         for item in range(world * per_items):
             assert raw[item * 256:(item + 1) * 256] == _core.dataset_item_2048(ctx, item), item
-        # 4. share-ring all-gather: rank r reports r+1 shares with nonces r*1000+i
-        max_shares = 4
-        ring = bytearray(RING_HEADER + max_shares * SHARE_SIZE)
-        struct.pack_into("<I", ring, 0, rank + 1)
-        for i in range(rank + 1):
-            struct.pack_into("<Q8I8I", ring, RING_HEADER + i * SHARE_SIZE, rank * 1000 + i, *([rank] * 8), *([i] * 8))
-        g = ShareGather(results=torch.frombuffer(ring, dtype=torch.int32).clone(), max_shares=max_shares)
-        g.enqueue()
-        shares = g.collect()
-        assert [s.nonce for s in shares] == sorted(r * 1000 + i for r in range(world) for i in range(r + 1))
+        # 4. the mining loop's record all-gather: rank r reports r+1 shares with nonces r*1000+i
+        comm = Comm(60.0)
+        shares = [Share(rank * 1000 + i, bytes([rank]) * 32, bytes([i]) * 32) for i in range(rank + 1)]
+        recs = [unpack_record(x) for x in comm.all_gather(pack_record(SlotResult(7, 0, 64, 64 + rank, shares)))]
+        assert [s.nonce for r in recs for s in r.shares] == [r * 1000 + i for r in range(world) for i in range(r + 1)]
+        assert comm.all_reduce_sum([rank + 1, 1]) == [world * (world + 1) // 2, world]
+        assert comm.broadcast(b"w" * 144 if rank == 0 else None, 144) == b"w" * 144
         # 5. nonce partition of bench.py: disjoint windows across ranks and steps
         batch, base = 1 << 20, 0x5EED_0000_0000_0000
         windows = [(base + (i * world + r) * batch, batch) for i in range(3) for r in range(world)]
@@ -77,7 +77,7 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4])
 def test_gloo_collectives(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -28,27 +28,40 @@ def state(core):
 
 
 def test_work_packet_roundtrip():
-    from nodexa_chain_core_amd.miner.search import FLAG_CLEAN, WORK_SIZE, Work
+    from nodexa_chain_core_amd.miner.search import ALGO_EQUIHASH, FLAG_CLEAN, WORK_SIZE, Work
 
     w = Work(bytes(range(32)), bytes([0x7F] + [0xFF] * 31), 7500 * 3 + 5, 42, 1 << 56, FLAG_CLEAN)
     raw = w.pack()
-    assert len(raw) == WORK_SIZE == 96
+    assert len(raw) == WORK_SIZE == 144
     back = Work.unpack(raw)
     assert back == w and back.epoch == 3 and not back.idle and back.target64() == 0x7FFFFFFFFFFFFFFF
+    assert back.header_hash == bytes(range(32)) and back.algo == 0
     assert Work().idle and Work.unpack(Work().pack()).idle
+    e = Work(bytes(range(80)), bytes(32), 9, 3, 0, 0, ALGO_EQUIHASH)  # the 80-byte Equihash prefix
+    assert Work.unpack(e.pack()) == e and Work.unpack(e.pack()).header == bytes(range(80))
 
 
 def test_record_roundtrip():
-    from nodexa_chain_core_amd.miner.search import SlotResult
-    from nodexa_chain_core_amd.miner.service import MAX_SHARES_PER_STEP, RECORD_SIZE, pack_record, unpack_record
+    from nodexa_chain_core_amd.miner.search import ALGO_EQUIHASH, ALGO_X16RV2, EquihashShare, LegacyShare, SlotResult
+    from nodexa_chain_core_amd.miner.service import (MAX_SHARES, MAX_SHARES_PER_STEP, RECORD_SIZE, pack_record,
+                                                     unpack_record)
     from nodexa_chain_core_amd.ops.kawpow import Share
 
     shares = [Share(i, bytes([i]) * 32, bytes([255 - i]) * 32) for i in range(MAX_SHARES_PER_STEP + 3)]
-    raw = pack_record(SlotResult(9, 100, 4096, 4000, shares))
+    raw = pack_record(SlotResult(9, 100, 4096, 4000, shares, 12.5, 7), coll_ms=0.25, failures=1, epochs=[3, 4],
+                      device=5)
     assert len(raw) == RECORD_SIZE
-    job, hashes, back = unpack_record(raw)
-    assert (job, hashes) == (9, 4000) and back == shares[:MAX_SHARES_PER_STEP]
-    assert unpack_record(pack_record(None)) == (0, 0, [])
+    rec = unpack_record(raw)
+    assert (rec.job_id, rec.hashes) == (9, 4000) and rec.shares == shares[:MAX_SHARES_PER_STEP]
+    assert (rec.device_ms, rec.aborted, rec.coll_ms, rec.failures, rec.epochs, rec.device) == (12.5, 7, 0.25, 1, [3, 4], 5)
+    assert rec.has_result and rec.alive
+    empty = unpack_record(pack_record(None, alive=False))
+    assert (empty.job_id, empty.hashes, empty.shares, empty.has_result, empty.alive) == (0, 0, [], False, False)
+    eq = [EquihashShare(i, bytes([i]) * 1344, bytes([i + 1]) * 32) for i in range(6)]
+    back = unpack_record(pack_record(SlotResult(2, 0, 16, 31, eq, 8.0, 0, ALGO_EQUIHASH)))
+    assert back.algo == ALGO_EQUIHASH and back.hashes == 31 and back.shares == eq[:MAX_SHARES[ALGO_EQUIHASH]]
+    lg = [LegacyShare(7, bytes(32))]
+    assert unpack_record(pack_record(SlotResult(4, 0, 65536, 8, lg, 1.0, 0, ALGO_X16RV2))).shares == lg
 
 
 def test_single_rank_loop_mines_blocks(state):
@@ -122,7 +135,7 @@ def test_leader_rejects_share_failing_full_rehash(state):
     bad_mix = bytes([mix[0] ^ 1]) + mix[1:]
     # a share whose final hash is right but whose mix is not (a wrong DAG gather would look like
     # this after the mix-only check) is dropped by the full re-hash
-    leader.on_results([(w.job_id, 10, [Share(nonce, bad_mix, fin)])])
+    leader.on_results([(w.job_id, 10, [Share(nonce, bad_mix, fin)])])  # (job, hashes, shares) tuples work too
     assert leader.stats["bad_shares"] == 1 and state.height() == 0 and not req.done.is_set()
     leader.on_results([(w.job_id, 10, [Share(nonce, mix, fin)])])
     assert state.height() == 1 and req.done.is_set() and len(req.found) == 1
@@ -134,7 +147,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run_world(tmp_path, n, blocks=2, hang_rank=None, timeout_s=8.0, extra_env=None):
+def _run_world(tmp_path, n, blocks=2, hang_rank=None, timeout_s=8.0, extra_env=None, rank_env=None):
     port = _free_port()
     procs = []
     base = dict(os.environ)
@@ -149,6 +162,7 @@ def _run_world(tmp_path, n, blocks=2, hang_rank=None, timeout_s=8.0, extra_env=N
         env["NODEXA_MINER_WINDOWS_LOG"] = str(tmp_path / f"rank{r}.json")
         if r == hang_rank:
             env["NODEXA_MINER_HANG_AFTER"] = "3"
+        env.update((rank_env or {}).get(r, {}))
         if r == 0:
             cmd = [sys.executable, os.path.join(ROOT, "tests", "miner_world_rank0.py"), str(report)]
         else:

@@ -74,13 +74,14 @@ def test_journal_roundtrip_torn_tail_and_compaction(core, tmp_path):
 
 def test_chainstate_flushes_through_the_journal(core, tmp_path):
     from nodexa_chain_core_amd.chain.state import ChainState, make_params
-    from nodexa_chain_core_amd.miner.kawpow_miner import CpuKawpowBackend, MinerController
+    from nodexa_chain_core_amd.miner.service import Miner
 
     params = make_params("regtest")
     st = ChainState(params, str(tmp_path), db_format="journal")
     st.flush_interval = 3
-    m = MinerController(st, [CpuKawpowBackend()])
+    m = Miner.local(st)
     m.generate(bytes([0x51]), 7)
+    m.close()
     st.flush()
     log = os.path.join(str(tmp_path), "chainstate", "coins.log")
     assert os.path.getsize(log) > 0 and st.coins.journal_seq >= 2  # first flush: snapshot, then records
