@@ -941,15 +941,15 @@ class ChainState:
                     # a reference datadir: its ConnectBlock writes the index records with the block,
                     # so they describe at least the chainstate's block
                     want.best_block = self.coins.best_block
-                ok = ok_load and want.best_block == self.coins.best_block and \
-                    all(self._stored_index_flags.get(k) == bool(v) for k, v in self.index_flags.items())
+                ok = ok_load and all(self._stored_index_flags.get(k) == bool(v) for k, v in self.index_flags.items()) \
+                    and self._rewind_indexes(want)
             else:
                 raw = None
                 if os.path.exists(self.indexes_path):
                     with open(self.indexes_path, "rb") as f:
                         raw = f.read()
-                ok = raw is not None and want.deserialize(raw) and want.best_block == self.coins.best_block and \
-                    all(getattr(want, k) == bool(v) for k, v in self.index_flags.items())
+                ok = raw is not None and want.deserialize(raw) and \
+                    all(getattr(want, k) == bool(v) for k, v in self.index_flags.items()) and self._rewind_indexes(want)
             if ok:
                 self.indexes = want
             else:
@@ -980,6 +980,36 @@ class ChainState:
                 self.coins.compact(self.coins_path, self.coins_log)  # a fresh snapshot restarts the journal
         with self.lock:
             self._activate()
+
+    def _rewind_indexes(self, ix) -> bool:
+        """Bring loaded indexes to the UTXO set's block. A flush writes the index records before the
+        coins, so a crash between the two leaves the indexes ahead of the chainstate by the blocks of
+        one flush interval; their index changes are undone here from the stored blocks and undo data
+        (ChainIndexes.disconnect), and the start-up replay then connects those blocks — coins and
+        index together — exactly once. (The reference writes index records with each block and
+        reconnects idempotently; rewinding keeps the in-memory delta lists free of duplicates.)
+        False when the index is not on the chainstate's chain or a block needed is missing."""
+        have, want = self.coins.best_block, ix.best_block
+        if want == have:
+            return True
+        a, b = self.chain.find(want), self.chain.find(have)
+        if a is None or b is None or a.height <= b.height:
+            return False
+        path, cur = [], a
+        while cur is not None and cur.height > b.height:
+            path.append(cur)
+            cur = self.chain.find(cur.prev_hash)
+        if cur is None or cur.hash != have:
+            return False
+        for x in path:  # newest first
+            blk = self.get_block(x.hash)
+            undo = self.undo.read(x.hash, x.prev_hash)
+            if blk is None or undo is None:
+                return False
+            ix.disconnect(blk, x.height, x.hash, undo)
+        log.log_printf(f"chain indexes were {len(path)} block(s) ahead of the UTXO set (interrupted flush); "
+                       f"rewound to {_core.u256_hex(have)}")
+        return ix.best_block == have
 
     def coins_tip(self):
         return self.chain.find(self.coins.best_block)

@@ -7,7 +7,8 @@
 #include <random>
 #include <shared_mutex>
 #include <string>
-#include <unordered_set>
+#include <unordered_map>
+#include <utility>
 
 #include "../crypto/sha256.hpp"
 
@@ -29,11 +30,26 @@ struct KeyHash {
 
 struct SigCache::Impl {
     mutable std::shared_mutex mu;
-    std::unordered_set<std::string, KeyHash> set;
-    std::deque<std::string> order;  // insertion order, for eviction of the oldest entries
+    // live entries with the insertion generation of their slot in `order`: an entry erased by
+    // get(erase) and stored again later owns only its newest slot, so eviction of the stale slot
+    // (a generation that no longer matches) leaves the re-inserted entry alone
+    std::unordered_map<std::string, uint64_t, KeyHash> set;
+    std::deque<std::pair<std::string, uint64_t>> order;  // insertion order, for eviction of the oldest
+    uint64_t gen = 0;
     size_t max_entries = kDefaultMaxBytes / 32;
     u8 salt[32];
     uint64_t hits = 0, misses = 0, inserts = 0, evictions = 0;
+
+    // drop the oldest slot; evicts its entry only if the slot is the entry's current one
+    void pop_oldest() {
+        auto& f = order.front();
+        auto it = set.find(f.first);
+        if (it != set.end() && it->second == f.second) {
+            set.erase(it);
+            ++evictions;
+        }
+        order.pop_front();
+    }
 
     Impl() {
         std::random_device rd;
@@ -62,11 +78,7 @@ SigCache& SigCache::instance() {
 void SigCache::set_max_bytes(size_t bytes) {
     std::unique_lock<std::shared_mutex> g(impl_->mu);
     impl_->max_entries = bytes / 32;
-    while (impl_->set.size() > impl_->max_entries && !impl_->order.empty()) {
-        impl_->set.erase(impl_->order.front());
-        impl_->order.pop_front();
-        ++impl_->evictions;
-    }
+    while (impl_->set.size() > impl_->max_entries && !impl_->order.empty()) impl_->pop_oldest();
 }
 
 bool SigCache::get(const u8 msg[32], const Bytes& pubkey, const Bytes& sig, bool erase) {
@@ -87,17 +99,18 @@ bool SigCache::get(const u8 msg[32], const Bytes& pubkey, const Bytes& sig, bool
 void SigCache::put(const u8 msg[32], const Bytes& pubkey, const Bytes& sig) {
     std::string k = impl_->key(msg, pubkey, sig);
     std::unique_lock<std::shared_mutex> g(impl_->mu);
-    if (impl_->max_entries == 0 || !impl_->set.insert(k).second) return;
-    impl_->order.push_back(std::move(k));
+    if (impl_->max_entries == 0) return;
+    const uint64_t g_new = ++impl_->gen;
+    if (!impl_->set.emplace(k, g_new).second) return;
+    impl_->order.emplace_back(std::move(k), g_new);
     ++impl_->inserts;
-    while (impl_->set.size() > impl_->max_entries && !impl_->order.empty()) {
-        if (impl_->set.erase(impl_->order.front())) ++impl_->evictions;
-        impl_->order.pop_front();
-    }
+    while (impl_->set.size() > impl_->max_entries && !impl_->order.empty()) impl_->pop_oldest();
     if (impl_->order.size() > 2 * impl_->max_entries + 1024) {  // drop the slots of erased entries
-        std::deque<std::string> live;
-        for (auto& x : impl_->order)
-            if (impl_->set.count(x)) live.push_back(x);
+        std::deque<std::pair<std::string, uint64_t>> live;
+        for (auto& x : impl_->order) {
+            auto it = impl_->set.find(x.first);
+            if (it != impl_->set.end() && it->second == x.second) live.push_back(x);
+        }
         impl_->order.swap(live);
     }
 }

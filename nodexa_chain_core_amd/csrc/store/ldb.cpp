@@ -17,8 +17,12 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <climits>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <queue>
+#include <set>
 #include <stdexcept>
 
 namespace nodexa {
@@ -806,9 +810,28 @@ void destroy(const std::string& dir) {
 // ---------------------------------------------------------------- DB
 DB::DB(const std::string& dir, const Options& opt) : dir_(dir), opt_(opt) {}
 
+namespace {
+// Stores this process has open. fcntl locks belong to the process (a second open of the same
+// store in this process would succeed, and closing either descriptor would drop the lock for
+// both), so like LevelDB's PosixLockTable the process keeps its own set as well.
+std::mutex g_open_mu;
+std::set<std::string> g_open_dirs;
+
+std::string canonical_dir(const std::string& dir) {
+    char buf[PATH_MAX];
+    return ::realpath(dir.c_str(), buf) ? std::string(buf) : dir;
+}
+}  // namespace
+
 std::unique_ptr<DB> DB::open(const std::string& dir, const Options& opt) {
     std::unique_ptr<DB> db(new DB(dir, opt));
     if (opt.create_if_missing) ::mkdir(dir.c_str(), 0755);
+    {
+        std::lock_guard<std::mutex> g(g_open_mu);
+        const std::string key = canonical_dir(dir);
+        if (!g_open_dirs.insert(key).second) fail("store " + dir + " is already open in this process");
+        db->open_key_ = key;
+    }
     db->lock_fd_ = ::open((dir + "/LOCK").c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
     if (db->lock_fd_ < 0) fail("cannot open " + dir + "/LOCK: " + std::strerror(errno));
     struct flock fl;
@@ -847,6 +870,11 @@ void DB::close() {
     table_used_.clear();
     if (lock_fd_ >= 0) ::close(lock_fd_);  // releases the fcntl lock
     log_fd_ = manifest_fd_ = lock_fd_ = -1;
+    if (!open_key_.empty()) {
+        std::lock_guard<std::mutex> og(g_open_mu);
+        g_open_dirs.erase(open_key_);
+        open_key_.clear();
+    }
 }
 
 void DB::recover() {

@@ -120,6 +120,7 @@ private:
     Options opt_;
     std::mutex mu_;
     int lock_fd_ = -1;
+    std::string open_key_;  // canonical path in the process's set of open stores
     int log_fd_ = -1;
     int manifest_fd_ = -1;
     uint64_t log_number_ = 0, manifest_number_ = 0, next_file_ = 2, last_seq_ = 0;

@@ -707,9 +707,10 @@ class Node:
                              rest=self.rest if a.get_bool("rest", False) else None,  # -rest (DEFAULT_REST_ENABLE=false)
                              rpcauth=a.get_list("rpcauth"), allow=parse_allow_subnets(a.get_list("rpcallowip")),
                              threads=a.get_int("rpcthreads", 4), idle_timeout=float(a.get("rpcservertimeout", "30")),
-                             # -webgui: the wallet page at http://<rpcbind>:<rpcport>/gui (on by default)
+                             # -webgui: the wallet page at http://<rpcbind>:<rpcport>/gui (off by default:
+                             # a browser that saved the RPC credentials is a CSRF target, rpc/server.py)
                              gui=os.path.join(os.path.dirname(os.path.abspath(__file__)), "gui", "index.html")
-                             if a.get_bool("webgui", True) else None)
+                             if a.get_bool("webgui", False) else None)
         self.rpc.start()
         log.log_printf(f"RPC listening on {host}:{self.rpc.port}")
 

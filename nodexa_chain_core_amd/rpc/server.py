@@ -217,6 +217,25 @@ class _Handler(http.server.BaseHTTPRequestHandler):
         user, _, pw = userpass.partition(":")
         return rpcauth_matches(self.server.rpcauth, user, pw)
 
+    def _same_origin_or_cli(self) -> bool:
+        """CSRF guard. A browser that holds the RPC credentials (Basic auth remembered
+        after opening /gui) would attach them to a cross-site form POST (enctype=text/plain) or to a
+        page's fetch(). Browsers mark such requests with Origin / Referer / Sec-Fetch-* headers;
+        command-line clients (nodexa-cli, curl, the reference's clore-cli) send none of them and
+        pass as before. A browser request must come from this server's own origin AND carry the
+        per-process token that only the served /gui page holds (a custom header: a cross-site form
+        cannot set one, and a cross-site fetch() with one needs a CORS preflight this server never
+        grants)."""
+        h = self.headers
+        if not any(h.get(k) for k in ("Origin", "Referer", "Sec-Fetch-Site", "Sec-Fetch-Mode")):
+            return True
+        src = h.get("Origin") or h.get("Referer") or ""
+        if src and src != "null":
+            same = urllib.parse.urlsplit(src).netloc == h.get("Host", "")
+        else:
+            same = h.get("Sec-Fetch-Site") in ("same-origin", "none")
+        return same and hmac.compare_digest(h.get("X-Nodexa-CSRF", ""), self.server.csrf_token)
+
     def do_POST(self):  # noqa: N802
         srv: RPCHTTPServer = self.server
         if (srv.credentials or srv.rpcauth) and not self._authorized():
@@ -226,6 +245,11 @@ class _Handler(http.server.BaseHTTPRequestHandler):
             self.send_header("WWW-Authenticate", 'Basic realm="jsonrpc"')
             self.send_header("Content-Length", "0")
             self.end_headers()
+            return
+        if not self._same_origin_or_cli():
+            log.log_printf(f"JSON-RPC POST from {self.client_address[0]} rejected: browser request without the "
+                           f"web wallet's token (Origin {self.headers.get('Origin')!r})")
+            self._send(403, b"Forbidden: cross-site request", "text/plain")
             return
         if not srv.slots.acquire(blocking=False):
             self._send(503, b"Work queue depth exceeded", "text/plain")
@@ -270,7 +294,14 @@ class _Handler(http.server.BaseHTTPRequestHandler):
                 self.end_headers()
                 return
             with open(srv.gui, "rb") as f:
-                self._send(200, f.read(), "text/html; charset=utf-8")
+                page = f.read().replace(b"__NODEXA_CSRF__", srv.csrf_token.encode())
+            self.send_response(200)
+            self.send_header("Content-Type", "text/html; charset=utf-8")
+            self.send_header("Content-Length", str(len(page)))
+            self.send_header("Cache-Control", "no-store")  # the token is per process
+            self.send_header("X-Frame-Options", "DENY")
+            self.end_headers()
+            self.wfile.write(page)
             return
         # REST subset (src/rest.cpp:569-580): /rest/chaininfo.json
         if self.path.startswith("/rest/") and self.server.rest is not None:
@@ -294,7 +325,8 @@ class RPCHTTPServer(socketserver.ThreadingMixIn, http.server.HTTPServer):
                  rpcauth: list[str] | None = None, allow: list | None = None, threads: int = 4,
                  idle_timeout: float = 30.0, gui: str | None = None):
         super().__init__(addr, _Handler)
-        self.gui = gui  # path of the web wallet page, or None (-webgui=0)
+        self.gui = gui  # path of the web wallet page, or None (-webgui=0, the default)
+        self.csrf_token = secrets.token_hex(16)  # handed to the /gui page; required on browser POSTs
         self.table = table
         self.credentials = credentials
         self.rpcauth = list(rpcauth or [])

@@ -93,7 +93,15 @@ def test_lock_excludes_second_open(tmp_path):
     r = subprocess.run(["python3", "-c", f"from nodexa_chain_core_amd import core; core().LevelDB({path!r})"],
                        cwd=ROOT, capture_output=True, text=True)
     assert r.returncode != 0 and "in use" in r.stderr
+    # fcntl locks are per process, so this process keeps its own set of open stores
+    with pytest.raises(Exception, match="already open in this process"):
+        _core.LevelDB(path)
+    (tmp_path / "x").mkdir()
+    with pytest.raises(Exception, match="already open in this process"):
+        _core.LevelDB(str(tmp_path / "x" / ".." / "db"))  # the same store under another spelling
     db.close()
+    db2 = _core.LevelDB(path)  # closing released it
+    db2.close()
 
 
 def test_crc32c_bloom_hash_and_snappy():

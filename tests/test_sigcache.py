@@ -43,3 +43,35 @@ def test_cache_modes_and_eviction(core, node_factory):  # noqa: F811
     core.sigcache_set_max_bytes(0)
     assert core.verify_script(*args, 1)[0] and st()["entries"] == 0      # -maxsigcachesize=0: nothing kept
     core.sigcache_set_max_bytes(32 << 20)
+
+
+def test_reinserted_entry_keeps_its_age(core, node_factory):  # noqa: F811
+    """an entry erased by a block connect (use mode) and stored again later (mempool
+    after a reorg) owns only its newest slot; eviction of its stale older slot must not drop it."""
+    node, addr = node_factory()
+    c = client(node)
+    w = fund(c, 101)
+    u = mature_coin(c)
+    value, spk, _, _ = None, None, None, None
+    checks = []
+    for dest in (c.getnewaddress(), c.getnewaddress(), c.getnewaddress()):
+        raw = bytes.fromhex(spend(c, u["txid"], u["vout"], u["amount"], dest, 5.0))
+        tx = core.Transaction.deserialize(raw)
+        vin = tx.vin[0]
+        value, spk, _, _ = node.state._spent_coin(vin.prevout)
+        checks.append(lambda mode, raw=raw, vin=vin, spk=spk, value=value: core.verify_script(
+            vin.script_sig, spk, list(vin.witness), core.STANDARD_SCRIPT_VERIFY_FLAGS, raw, 0, value, mode)[0])
+    a, b, cc = checks
+    core.sigcache_clear()
+    core.sigcache_set_max_bytes(2 * 32)  # two entries
+    try:
+        st = core.sigcache_stats
+        assert a(1) and a(2) and st()["entries"] == 0  # A stored, then used (erased)
+        assert b(1) and a(1) and st()["entries"] == 2   # B, then A again: slots [A(stale), B, A]
+        assert cc(1) and st()["entries"] == 2           # C evicts the oldest live entry: B, not A
+        h, m = st()["hits"], st()["misses"]
+        assert a(2) and st()["hits"] == h + 1           # A survived
+        assert b(2) and st()["misses"] == m + 1         # B was the one evicted
+    finally:
+        core.sigcache_set_max_bytes(32 << 20)
+        core.sigcache_clear()

@@ -25,7 +25,7 @@ def _get(port, path, auth=None):
 
 
 def test_gui_served_behind_auth_and_its_rpc_contract(core, node_factory):  # noqa: F811
-    node, addr = node_factory()
+    node, addr = node_factory(("-webgui",))
     port = node.rpc.port
     assert _get(port, "/gui")[0] == 401
     assert _get(port, "/gui", "u:wrong")[0] == 401
@@ -69,7 +69,7 @@ def test_gui_script_drives_the_node(core, node_factory):  # noqa: F811
     """The page's own JavaScript, run under Node.js with a DOM stub against the live node: the
     overview shows the balance, a new receiving address, a payment sent from the send page, the
     transactions / mining / peers pages and the RPC console."""
-    node, _ = node_factory()
+    node, _ = node_factory(("-webgui",))
     c = client(node)
     c.generatetoaddress(101, c.getnewaddress())
     dest = c.getnewaddress("dest")
@@ -93,3 +93,38 @@ def test_gui_script_drives_the_node(core, node_factory):  # noqa: F811
 def test_gui_can_be_disabled(core, node_factory):  # noqa: F811
     node, _ = node_factory(("-webgui=0",))
     assert _get(node.rpc.port, "/gui", "u:p")[0] == 405
+    node.stop()
+    node2, _ = node_factory()  # off by default
+    assert _get(node2.rpc.port, "/gui", "u:p")[0] == 405
+
+
+def _post(port, body: bytes, headers: dict):
+    conn = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+    h = {"Authorization": "Basic " + base64.b64encode(b"u:p").decode()}
+    h.update(headers)
+    conn.request("POST", "/", body=body, headers=h)
+    r = conn.getresponse()
+    out = r.read()
+    conn.close()
+    return r.status, out
+
+
+def test_cross_site_posts_are_refused(core, node_factory):  # noqa: F811
+    """with the browser holding the RPC credentials, a cross-site form POST
+    (text/plain body that parses as JSON-RPC) must not run; the served page's own requests must."""
+    node, _ = node_factory(("-webgui",))
+    port = node.rpc.port
+    body = b'{"method": "getblockcount", "params": [], "id": 1}'
+    evil = {"Content-Type": "text/plain", "Origin": "http://evil.example", "Sec-Fetch-Site": "cross-site"}
+    assert _post(port, body, evil)[0] == 403
+    same_origin_no_token = {"Origin": f"http://127.0.0.1:{port}", "Content-Type": "application/json"}
+    assert _post(port, body, same_origin_no_token)[0] == 403
+    assert _post(port, body, {"Referer": "http://evil.example/x", "X-Nodexa-CSRF": "guess"})[0] == 403
+    page = _get(port, "/gui", "u:p")[2].decode()
+    token = re.search(r'const CSRF = "([0-9a-f]{32})"', page).group(1)
+    ok = {"Origin": f"http://127.0.0.1:{port}", "X-Nodexa-CSRF": token, "Content-Type": "application/json"}
+    status, out = _post(port, body, ok)
+    assert status == 200 and json.loads(out)["result"] == 0
+    assert _post(port, body, dict(ok, Origin="http://evil.example"))[0] == 403  # the token alone is not enough
+    status, out = _post(port, body, {"Content-Type": "text/plain"})  # curl / nodexa-cli: no browser headers
+    assert status == 200 and json.loads(out)["result"] == 0
