@@ -58,44 +58,78 @@ def _baseline() -> tuple[float | None, str | None]:
 
 
 def _verify_headers_bench(log) -> dict | None:
-    """BASELINE config 5 over the ranks (parallel/verify.py: full-hash slices + RCCL all-gather)."""
+    """BASELINE config 5: the 10k-header fixture through ProcessNewBlockHeaders' work — parse the
+    wire bytes, PoW of every header, DarkGravityWave + contextual rules, index insert — timed end to
+    end (parse included). "resident" is the device-resident pipeline (models/verify.
+    process_batch_resident: one upload, PoW + block hashes + DGW nBits on the GPU, one download, the
+    serial insert on the host; over N ranks every GPU takes a slice and the results are
+    all-gathered over RCCL); "light" is the no-DAG kernel path. Per-epoch setup (DAG, program
+    tables) is excluded and reported; the median of 5 timed runs is the number."""
     import functools
+    import statistics
 
     import torch
 
     from nodexa_chain_core_amd import _core
     from nodexa_chain_core_amd.models import synthetic
-    from nodexa_chain_core_amd.models.verify import process_headers
+    from nodexa_chain_core_amd.models.verify import process_batch_resident, process_headers
     from nodexa_chain_core_amd.parallel import world as W
     from nodexa_chain_core_amd.parallel.verify import verify_headers_distributed
 
     if not os.path.exists(VERIFY_FIXTURE):
         return None
     params, headers = synthetic.load(VERIFY_FIXTURE)
+    with open(VERIFY_FIXTURE, "rb") as f:
+        raw = f.read()
+    act = params.kawpow_activation_time
     adjusted = headers[-1].time + 3600
     n = len(headers)
+    w = W.get()
+    dev = w.device.index
     out = {"headers": n, "fixture": os.path.relpath(VERIFY_FIXTURE, ROOT)}
-    for mode in ("dag", "light"):
-        fn = functools.partial(verify_headers_distributed, mode=mode)
-        t0 = time.perf_counter()
-        dev = W.get().device
-        dgw_dev = dev.index if dev.type == "cuda" else None  # DGW nBits of the batch from the GPU kernel
-        warm = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn,
-                               dgw_device=dgw_dev)  # every epoch's state
-        torch.cuda.synchronize()
-        setup = W.all_reduce_max(time.perf_counter() - t0)
+
+    def resident():
+        b = _core.HeaderBatch.from_bytes(raw, act)
+        return process_batch_resident(_core.HeaderChain(params), b, adjusted, device=dev, world=w)
+
+    t0 = time.perf_counter()
+    warm = resident()  # every epoch's DAG and program table
+    torch.cuda.synchronize()
+    setup = W.all_reduce_max(time.perf_counter() - t0)
+    runs = []
+    for _ in range(5):
         W.barrier()
         t0 = time.perf_counter()
-        r = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn, dgw_device=dgw_dev)
-        torch.cuda.synchronize()
+        r = resident()
         W.barrier()
-        dt = W.all_reduce_max(time.perf_counter() - t0)
+        runs.append((W.all_reduce_max(time.perf_counter() - t0), r))
         if r["accepted"] != n or warm["accepted"] != n:
-            raise SystemExit(f"header verify ({mode}): accepted {r['accepted']}/{n}, first reject {r['reject']}")
-        out[mode] = {"headers_per_s": round(n / dt, 1), "ms": round(dt * 1e3, 2), "pow_ms": round(r["pow_s"] * 1e3, 2),
-                     "context_ms": round(r["context_s"] * 1e3, 2), "dgw_on_gpu": r["dgw_gpu"],
-                     "first_run_incl_epoch_setup_s": round(setup, 3)}
-        log(f"[bench] verify {n} headers ({mode}): {n / dt:.0f} headers/s")
+            raise SystemExit(f"header verify (resident): accepted {r['accepted']}/{n}, first reject {r['reject']}")
+    dt = statistics.median(x for x, _ in runs)
+    r = min(runs, key=lambda x: abs(x[0] - dt))[1]
+    out["resident"] = {"headers_per_s": round(n / dt, 1), "ms": round(dt * 1e3, 3),
+                       "ms_min_max": [round(min(x for x, _ in runs) * 1e3, 3), round(max(x for x, _ in runs) * 1e3, 3)],
+                       "host_ms": r["host_ms"], "device_ms": r["device_ms"], "pack_ms": r["pack_ms"],
+                       "issue_ms": r["issue_ms"], "wait_ms": r["wait_ms"], "accept_ms": r["accept_ms"],
+                       "dgw_on_gpu": r["dgw_gpu"], "parse_included": True,
+                       "first_run_incl_epoch_setup_s": round(setup, 3)}
+    log(f"[bench] verify {n} headers (resident): {n / dt:.0f} headers/s (host {r['host_ms']:.2f} ms, device "
+        f"{r['device_ms']:.2f} ms, accept {r['accept_ms']:.2f} ms)")
+    fn = functools.partial(verify_headers_distributed, mode="light")
+    dgw_dev = dev if w.device.type == "cuda" else None
+    process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn, dgw_device=dgw_dev)  # light epochs
+    torch.cuda.synchronize()
+    W.barrier()
+    t0 = time.perf_counter()
+    r = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn, dgw_device=dgw_dev)
+    torch.cuda.synchronize()
+    W.barrier()
+    dt = W.all_reduce_max(time.perf_counter() - t0)
+    if r["accepted"] != n:
+        raise SystemExit(f"header verify (light): accepted {r['accepted']}/{n}, first reject {r['reject']}")
+    out["light"] = {"headers_per_s": round(n / dt, 1), "ms": round(dt * 1e3, 2), "pow_ms": round(r["pow_s"] * 1e3, 2),
+                    "context_ms": round(r["context_s"] * 1e3, 2), "dgw_on_gpu": r["dgw_gpu"]}
+    log(f"[bench] verify {n} headers (light, no DAG): {n / dt:.0f} headers/s")
     return out
 
 
@@ -340,7 +374,7 @@ def main() -> int:
             "equihash_sol_per_s": eq["node_sol_per_s"] if eq else None,
             "equihash": eq,
             "verify_headers": verify,
-            "verify_headers_per_s": verify["dag"]["headers_per_s"] if verify else None,
+            "verify_headers_per_s": verify["resident"]["headers_per_s"] if verify else None,
             "baseline_mhs": base,
             "baseline_source": base_src,
         }

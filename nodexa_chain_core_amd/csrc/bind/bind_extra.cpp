@@ -6,6 +6,7 @@
 
 #include <thread>
 
+#include "../chain/headerbatch.hpp"
 #include "../chain/headerchain.hpp"
 #include "../chain/script.hpp"
 #include "../chain/validation.hpp"
@@ -442,6 +443,7 @@ void bind_extra(py::module_& m) {
         .def_readwrite("genesis", &ChainParams::genesis)
         .def_property_readonly("genesis_hash", [](const ChainParams& p) { return pyb(p.consensus.genesis_hash); })
         .def_property_readonly("pow_limit", [](const ChainParams& p) { return pyb(p.consensus.pow_limit); })
+        .def_property_readonly("last_checkpoint_height", &ChainParams::last_checkpoint_height)
         .def_property_readonly("kawpow_limit", [](const ChainParams& p) { return pyb(p.consensus.kawpow_limit); })
         .def_property("equihash_limit", [](const ChainParams& p) { return pyb(p.consensus.equihash_limit); },
                       [](ChainParams& p, const py::bytes& b) { p.consensus.equihash_limit = u256(b); })
@@ -483,7 +485,119 @@ void bind_extra(py::module_& m) {
         .def_readonly("dos", &AcceptResult::dos)
         .def_property_readonly("index", [](const AcceptResult& r) { return r.index; }, py::return_value_policy::reference);
 
+    // ------------------------------------------------ HeaderBatch (models/verify.py resident pipeline)
+    static_assert(sizeof(Uint256) == 32, "hash blobs are read as Uint256 arrays");
+    auto view = [](const std::string& s) {  // zero-copy, read-only: the batch must outlive it
+        return py::memoryview::from_memory(const_cast<char*>(s.data()), py::ssize_t(s.size()), true);
+    };
+    py::class_<HeaderBatch, std::shared_ptr<HeaderBatch>>(m, "HeaderBatch")
+        .def_static("from_bytes", [](const py::buffer& buf, u32 act) {
+            const py::buffer_info bi = buf.request();
+            const u8* p = static_cast<const u8*>(bi.ptr);
+            const size_t len = size_t(bi.size) * size_t(bi.itemsize);
+            py::gil_scoped_release rel;
+            return std::make_shared<HeaderBatch>(HeaderBatch::from_bytes(p, len, act));
+        }, py::arg("data"), py::arg("kawpow_activation_time"),
+           "parse concatenated serialized headers (80 / 120 / Equihash-extended) and pack them")
+        .def_static("from_headers", [](std::vector<BlockHeader> hs, u32 act) {
+            py::gil_scoped_release rel;
+            return std::make_shared<HeaderBatch>(HeaderBatch::from_headers(std::move(hs), act));
+        }, py::arg("headers"), py::arg("kawpow_activation_time"))
+        .def("__len__", &HeaderBatch::size)
+        .def_readonly("kawpow_activation_time", &HeaderBatch::act)
+        .def_property_readonly("kinds", [view](const HeaderBatch& b) { return view(b.kinds); })
+        .def_property_readonly("rows", [view](const HeaderBatch& b) { return view(b.rows); })
+        .def_property_readonly("eq_index", [](const HeaderBatch& b) {
+            return py::memoryview::from_memory(const_cast<u32*>(b.eq_index.data()), py::ssize_t(b.eq_index.size() * 4),
+                                               true);
+        })
+        .def_property_readonly("eq_msgs", [view](const HeaderBatch& b) { return view(b.eq_msgs); })
+        .def_property_readonly("eq_sols", [view](const HeaderBatch& b) { return view(b.eq_sols); })
+        .def_property_readonly("eq_ser", [view](const HeaderBatch& b) { return view(b.eq_ser); })
+        .def_readonly("eq_ser_len", &HeaderBatch::eq_ser_len)
+        .def_readonly("eq_uniform", &HeaderBatch::eq_uniform)
+        .def("header", [](const HeaderBatch& b, size_t i) {
+            if (i >= b.hs.size()) throw py::index_error();
+            return b.hs[i];
+        })
+        .def("headers", [](const HeaderBatch& b, size_t lo, size_t hi) {
+            hi = std::min(hi, b.hs.size());
+            return std::vector<BlockHeader>(b.hs.begin() + std::min(lo, hi), b.hs.begin() + hi);
+        }, py::arg("lo") = 0, py::arg("hi") = size_t(-1));
+
     py::class_<HeaderChain, std::shared_ptr<HeaderChain>>(m, "HeaderChain")
+        .def("accept_batch",
+             [](HeaderChain& c, const HeaderBatch& b, int64_t adjusted_time, const py::object& hashes,
+                const py::object& bits, size_t lo, size_t hi) {
+                 // accept_headers over batch headers [lo, hi) with the device pipeline's block hashes
+                 // (n x 32, storage order) and DGW nBits (n x u32, 0 = host decides), both indexed
+                 // by batch position: (accepted, reject reason or None, dos)
+                 hi = std::min(hi, b.hs.size());
+                 lo = std::min(lo, hi);
+                 const Uint256* kh = nullptr;
+                 const u32* kb = nullptr;
+                 py::buffer_info hb, bb;
+                 if (!hashes.is_none()) {
+                     hb = hashes.cast<py::buffer>().request();
+                     if (size_t(hb.size * hb.itemsize) != b.hs.size() * 32) throw std::invalid_argument("hashes: n x 32 bytes");
+                     kh = reinterpret_cast<const Uint256*>(hb.ptr) + lo;
+                 }
+                 if (!bits.is_none()) {
+                     bb = bits.cast<py::buffer>().request();
+                     if (size_t(bb.size * bb.itemsize) != b.hs.size() * 4) throw std::invalid_argument("bits: n x 4 bytes");
+                     kb = static_cast<const u32*>(bb.ptr) + lo;
+                 }
+                 std::vector<AcceptResult> r;
+                 {
+                     py::gil_scoped_release rel;
+                     r = c.accept_headers(b.hs.data() + lo, hi - lo, adjusted_time, false, kh, kb);
+                 }
+                 size_t ok = 0;
+                 while (ok < r.size() && r[ok].ok) ++ok;
+                 py::object why = py::none();
+                 int dos = 0;
+                 if (ok < r.size()) {
+                     why = py::str(r[ok].reject);
+                     dos = r[ok].dos;
+                 }
+                 return py::make_tuple(ok, why, dos);
+             },
+             py::arg("batch"), py::arg("adjusted_time"), py::arg("hashes") = py::none(), py::arg("bits") = py::none(),
+             py::arg("lo") = 0, py::arg("hi") = size_t(-1))
+        .def("dgw_ancestors",
+             [](const HeaderChain& c, const py::bytes& prev) -> py::object {
+                 // the DGW series prefix of a batch whose first header builds on `prev`: prev and up
+                 // to 179 of its ancestors, oldest first -> (times, bits, a, base_height) or None
+                 const HeaderIndex* base = c.find(u256(prev));
+                 const ConsensusParams& cp = c.params().consensus;
+                 if (base == nullptr || (cp.pow_allow_min_difficulty_blocks && cp.pow_no_retargeting)) return py::none();
+                 std::vector<const HeaderIndex*> anc;
+                 for (const HeaderIndex* q = base; q && anc.size() < size_t(kDgwPastBlocks); q = q->prev) anc.push_back(q);
+                 const size_t a = anc.size();
+                 std::vector<u32> times(a), bits(a);
+                 for (size_t k = 0; k < a; ++k) {
+                     times[k] = anc[a - 1 - k]->time;
+                     bits[k] = anc[a - 1 - k]->bits;
+                 }
+                 return py::make_tuple(py::bytes(reinterpret_cast<const char*>(times.data()), a * 4),
+                                       py::bytes(reinterpret_cast<const char*>(bits.data()), a * 4), a, base->height);
+             }, py::arg("prev"))
+        .def("dgw_series_batch",
+             [](const HeaderChain& c, const HeaderBatch& b, const py::buffer& hashes, size_t lo, size_t hi) -> py::object {
+                 hi = std::min(hi, b.hs.size());
+                 lo = std::min(lo, hi);
+                 const py::buffer_info hb = hashes.request();
+                 if (size_t(hb.size * hb.itemsize) != b.hs.size() * 32) throw std::invalid_argument("hashes: n x 32 bytes");
+                 std::vector<u32> times, bits;
+                 size_t a = 0;
+                 int base = 0;
+                 if (!c.dgw_series(b.hs.data() + lo, hi - lo, reinterpret_cast<const Uint256*>(hb.ptr) + lo, times, bits,
+                                   a, base))
+                     return py::none();
+                 return py::make_tuple(py::bytes(reinterpret_cast<const char*>(times.data()), times.size() * 4),
+                                       py::bytes(reinterpret_cast<const char*>(bits.data()), bits.size() * 4), a, base);
+             },
+             py::arg("batch"), py::arg("hashes"), py::arg("lo") = 0, py::arg("hi") = size_t(-1))
         .def(py::init([](const ChainParams& p) { return std::make_shared<HeaderChain>(p, std::make_shared<CpuPowVerifier>()); }))
         .def_property_readonly("params", &HeaderChain::params, py::return_value_policy::reference_internal)
         .def("set_kawpow_activation_time", [](HeaderChain& c, u32 t) { c.mutable_params().kawpow_activation_time = t; })

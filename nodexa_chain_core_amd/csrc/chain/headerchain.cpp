@@ -12,6 +12,7 @@
 #include "../pow/equihash.hpp"
 #include "../pow/kawpow.hpp"
 #include "../pow/x16r.hpp"
+#include "../util/workpool.hpp"
 
 namespace nodexa {
 
@@ -251,19 +252,7 @@ namespace {
 
 template <class F>
 void parallel_for(size_t n, F&& fn) {
-    const size_t threads = std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
-    if (threads <= 1 || n < 2 * threads) {
-        for (size_t i = 0; i < n; ++i) fn(i);
-        return;
-    }
-    std::vector<std::thread> pool;
-    const size_t step = (n + threads - 1) / threads;
-    for (size_t t = 0; t < threads; ++t) {
-        const size_t lo = t * step, hi = std::min(n, lo + step);
-        if (lo >= hi) break;
-        pool.emplace_back([&fn, lo, hi] { for (size_t i = lo; i < hi; ++i) fn(i); });
-    }
-    for (auto& th : pool) th.join();
+    parallel_for_each(n, fn, 128);  // the persistent pool (util/workpool.hpp): no thread spawn per call
 }
 
 }  // namespace
@@ -274,11 +263,10 @@ void parallel_for(size_t n, F&& fn) {
 // (nTime, nBits) pairs, which the batch itself supplies, so header i's retarget does not
 // wait for header i-1 to be indexed. The serial pass then does the index updates and
 // the remaining contextual checks. Results are identical to accepting one by one.
-bool HeaderChain::dgw_series(const std::vector<BlockHeader>& hs, const std::vector<Uint256>& hashes,
-                             std::vector<u32>& times, std::vector<u32>& bits, size_t& a, int& base_height) const {
+bool HeaderChain::dgw_series(const BlockHeader* hs, size_t n, const Uint256* hashes, std::vector<u32>& times,
+                             std::vector<u32>& bits, size_t& a, int& base_height) const {
     std::lock_guard<std::recursive_mutex> g(mu_);
-    const size_t n = hs.size();
-    if (n == 0 || hashes.size() != n) return false;
+    if (n == 0 || hashes == nullptr) return false;
     auto pit = index_.find(hs[0].prev);
     bool linear = pit != index_.end();
     for (size_t i = 1; linear && i < n; ++i) linear = hs[i].prev == hashes[i - 1];
@@ -305,8 +293,15 @@ bool HeaderChain::dgw_series(const std::vector<BlockHeader>& hs, const std::vect
 std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHeader>& hs, int64_t adjusted_time,
                                                       bool check_pow, const std::vector<Uint256>* known_hashes,
                                                       const std::vector<u32>* known_bits) {
+    return accept_headers(hs.data(), hs.size(), adjusted_time, check_pow,
+                          known_hashes && known_hashes->size() == hs.size() ? known_hashes->data() : nullptr,
+                          known_bits && known_bits->size() == hs.size() ? known_bits->data() : nullptr);
+}
+
+std::vector<AcceptResult> HeaderChain::accept_headers(const BlockHeader* hs, size_t n, int64_t adjusted_time,
+                                                      bool check_pow, const Uint256* known_hashes,
+                                                      const u32* known_bits) {
     std::lock_guard<std::recursive_mutex> g(mu_);
-    const size_t n = hs.size();
     std::vector<AcceptResult> out;
     out.reserve(n);
     std::vector<Uint256> hashes;
@@ -320,8 +315,8 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
         parallel_for(n, [&](size_t i) { pre[i] = check_header(hs[i], true); });
     }
     if (n >= kParallelAcceptMin) {
-        if (known_hashes && known_hashes->size() == n) {
-            hashes = *known_hashes;
+        if (known_hashes) {
+            hashes.assign(known_hashes, known_hashes + n);
         } else {
             hashes.resize(n);
             parallel_for(n, [&](size_t i) { hashes[i] = verifier_->block_hash(hs[i], params_); });
@@ -334,7 +329,7 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
         std::vector<u32> times, bits;
         size_t a = 0;
         int base_height = 0;
-        if (dgw_series(hs, hashes, times, bits, a, base_height)) {
+        if (dgw_series(hs, n, hashes.data(), times, bits, a, base_height)) {
             const bool from_genesis = a == size_t(base_height) + 1;  // the series reaches genesis
             mtp.resize(n);
             parallel_for(n, [&](size_t i) {
@@ -347,10 +342,10 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
                 mtp[i] = w[m / 2];
                 have_mtp[i] = 1;
             });
-            if (known_bits && known_bits->size() == n) {
+            if (known_bits) {
                 // computed by the caller from the same series (the GPU batch kernel, dgw.hip);
                 // 0 = not a DGW header, left to the serial path
-                expected = *known_bits;
+                expected.assign(known_bits, known_bits + n);
                 for (size_t i = 0; i < n; ++i) have[i] = expected[i] != 0;
             } else {
                 const u32 limit_compact = ArithU256::from_uint256(params_.consensus.pow_limit).get_compact();

@@ -72,7 +72,14 @@ public:
     // linearly: up to 180 ancestors of the batch's parent (oldest first, `a` of them) then the
     // batch. False if the batch is not linear or the network does not retarget with DGW.
     bool dgw_series(const std::vector<BlockHeader>& hs, const std::vector<Uint256>& hashes, std::vector<u32>& times,
+                    std::vector<u32>& bits, size_t& a, int& base_height) const {
+        return dgw_series(hs.data(), hs.size(), hashes.data(), times, bits, a, base_height);
+    }
+    // The same over a contiguous range of headers (a HeaderBatch's own storage: no copies).
+    bool dgw_series(const BlockHeader* hs, size_t n, const Uint256* hashes, std::vector<u32>& times,
                     std::vector<u32>& bits, size_t& a, int& base_height) const;
+    std::vector<AcceptResult> accept_headers(const BlockHeader* hs, size_t n, int64_t adjusted_time, bool check_pow,
+                                             const Uint256* known_hashes, const u32* known_bits);
 
     const HeaderIndex* tip() const;
     const HeaderIndex* genesis() const { return genesis_; }

@@ -239,3 +239,23 @@ struct Sha256dParams {
     uint32_t n;
     uint32_t pad;
 };
+
+// Device-resident batch header verification (header_batch.hip; models/verify.py).
+struct HeaderBatchParams {
+    const uint8_t* rows;       // n x 128: the packed batch (csrc/chain/headerbatch.hpp)
+    const uint8_t* kinds;      // n: 0 KawPow, 2 Equihash, 3 pre-KawPow
+    const uint8_t* mixonly;    // n x 128: kawpow_mixonly_batch rows
+    struct KawpowVerifyJob* jobs;  // n
+    uint32_t* job_program;     // n
+    const uint32_t* full;      // n x 16: kawpow_verify_dag output (mix, final)
+    uint8_t* out;              // n codes, then n x 32 block hashes (storage order)
+    const uint32_t* eq_index;  // eq_n batch positions of the Equihash headers
+    const uint32_t* eq_verdict;  // eq_n eq_verify verdicts
+    const uint8_t* eq_hash;    // eq_n x 32 SHA256d of the serialized headers
+    uint32_t n, eq_n;          // rows in the batch (the layout of `out`), Equihash headers given
+    uint32_t first, count;     // the rows this launch covers: [first, first + count)
+    uint32_t epoch_length;     // ethash epoch (7500 blocks; 2500 ProgPoW periods)
+    int32_t last_checkpoint;   // KawPow headers at or below it get the mix-only check only (-1: none)
+    uint8_t pow_limit[32];     // consensus powLimit, little-endian (CheckProofOfWork's target cap)
+};
+

@@ -429,6 +429,39 @@ PYBIND11_MODULE(_hip, m) {
     m.attr("EQ_SOL_WORDS") = EQ_SOL_WORDS;
     // Batch SHA-256d (sha256d.hip): messages of `len` bytes at `stride`, or (merkle=true) one
     // ComputeMerkleRoot level of `len` 32-byte nodes into (len + 1) / 2 nodes.
+    // header_batch.hip: hb_jobs / hb_verdict over rows [first, first + count) (`which` 0 / 1), or
+    // hb_eq_scatter over the eq_n Equihash headers given (`which` 2)
+    m.def("launch_header_batch", [](const Kernel& k, int which, uintptr_t rows, uintptr_t kinds, uintptr_t mixonly,
+                                    uintptr_t jobs, uintptr_t job_program, uintptr_t full, uintptr_t out,
+                                    uintptr_t eq_index, uintptr_t eq_verdict, uintptr_t eq_hash, uint32_t n,
+                                    uint32_t eq_n, uint32_t first, uint32_t count, uint32_t epoch_length,
+                                    int32_t last_checkpoint, const py::bytes& pow_limit_le, uintptr_t stream) {
+        if (which < 2 && (first > n || count > n - first)) throw std::invalid_argument("row range outside the batch");
+        if (epoch_length == 0 || epoch_length % 3) throw std::invalid_argument("epoch length must be a multiple of 3");
+        const std::string lim = pow_limit_le;
+        if (lim.size() != 32) throw std::invalid_argument("pow_limit must be 32 bytes");
+        HeaderBatchParams p{};
+        p.rows = reinterpret_cast<const uint8_t*>(rows);
+        p.kinds = reinterpret_cast<const uint8_t*>(kinds);
+        p.mixonly = reinterpret_cast<const uint8_t*>(mixonly);
+        p.jobs = reinterpret_cast<KawpowVerifyJob*>(jobs);
+        p.job_program = reinterpret_cast<uint32_t*>(job_program);
+        p.full = reinterpret_cast<const uint32_t*>(full);
+        p.out = reinterpret_cast<uint8_t*>(out);
+        p.eq_index = reinterpret_cast<const uint32_t*>(eq_index);
+        p.eq_verdict = reinterpret_cast<const uint32_t*>(eq_verdict);
+        p.eq_hash = reinterpret_cast<const uint8_t*>(eq_hash);
+        p.n = n;
+        p.eq_n = eq_n;
+        p.first = first;
+        p.count = count;
+        p.epoch_length = epoch_length;
+        p.last_checkpoint = last_checkpoint;
+        std::memcpy(p.pow_limit, lim.data(), 32);
+        const uint32_t threads = which == 2 ? eq_n : count;
+        if (threads == 0) return;
+        k.launch_bytes(dim3((threads + 255) / 256), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("launch_kawpow_mixonly", [](const Kernel& k, uintptr_t headers, uint32_t n, uint32_t stride, uintptr_t out,
                                       uintptr_t stream) {
         if (stride < 120) throw std::invalid_argument("KawPow headers are 120 bytes");

@@ -315,3 +315,63 @@ def process_headers(chain, headers, adjusted_time: int, gpus: list[int] | None =
     t2 = time.perf_counter()
     return {"accepted": accepted, "reject": reject, "pow_s": t1 - t0, "context_s": t2 - t1,
             "dgw_gpu": bits is not None, "dgw_s": t_dgw - t1}
+
+
+_RESIDENT: dict[int, object] = {}
+
+
+def resident_verifier(device: int):
+    from ..ops.header_batch import ResidentHeaderVerifier
+
+    v = _RESIDENT.get(device)
+    if v is None:
+        v = _RESIDENT[device] = ResidentHeaderVerifier(device)
+    return v
+
+
+@traced("verify.process_batch_resident")
+def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, world=None) -> dict | None:
+    """ProcessNewBlockHeaders for a native HeaderBatch with the device-resident pipeline
+    (ops/header_batch.py): one upload, PoW + block hashes + DGW nBits of every header on the GPU,
+    one download, then the serial index insert on the host (HeaderChain.accept_batch). Pre-KawPow
+    (X16R) headers, if any, are hashed on the host cores. Same result as process_headers; None when
+    the batch does not suit the resident path (not in height order), so the caller falls back."""
+    from ..ops.header_batch import CODES
+
+    t0 = time.perf_counter()
+    v = resident_verifier(device)
+    plan = v.plan(batch)
+    if plan is None or len(batch) == 0:
+        return None
+    params = chain.params
+    series = chain.dgw_ancestors(batch.header(0).prev)
+    r = v.run(params, batch, series, plan, world)
+    t1 = time.perf_counter()
+    codes = r["codes"]
+    n = len(batch)
+    legacy = np.flatnonzero(codes == 255)
+    hashes = r["hashes"]
+    if len(legacy):  # X16R / X16RV2 headers: host cores, then their hashes join the device ones
+        hs = [batch.header(int(i)) for i in legacy]
+        hashes = np.array(hashes)
+        codes = np.array(codes)
+        for i, hdr in zip(legacy.tolist(), hs):
+            fn = _core.x16rv2 if hdr.time >= params.x16rv2_activation_time else _core.x16r
+            hsh = fn(hdr.legacy80(), hdr.prev)
+            hashes[i] = np.frombuffer(hsh, np.uint8)
+            ok = _core.check_proof_of_work(hsh, hdr.bits, params)
+            codes[i] = 0 if ok else 2
+    bad = np.flatnonzero(codes != 0)
+    first_bad = int(bad[0]) if len(bad) else n
+    t2 = time.perf_counter()
+    accepted, why, _dos = chain.accept_batch(batch, adjusted_time, hashes, r["bits"], 0, first_bad)
+    t3 = time.perf_counter()
+    reject = {"index": accepted, "reason": why} if why is not None else None
+    if reject is None and first_bad < n:
+        reject = {"index": first_bad, "reason": CODES.get(int(codes[first_bad]), "high-hash")}
+    return {"accepted": accepted, "reject": reject, "pow_s": t1 - t0 + (t2 - t1), "context_s": t3 - t2,
+            "dgw_gpu": series is not None, "resident": True,
+            "host_ms": round((t1 - t0) * 1e3 - r["wait_ms"] + (t3 - t1) * 1e3, 3),
+            "device_ms": round(r["device_ms"], 3), "pack_ms": round(r["pack_ms"], 3),
+            "issue_ms": round(r["issue_ms"], 3), "wait_ms": round(r["wait_ms"], 3),
+            "accept_ms": round((t3 - t2) * 1e3, 3)}

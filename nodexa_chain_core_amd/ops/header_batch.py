@@ -1,0 +1,249 @@
+"""Device-resident batch header verification (BASELINE config 5).
+
+Reference: ProcessNewBlockHeaders (src/validation.cpp:12017-12035) runs CheckBlockHeader
+(:11638-11665: full KawPow light-mode hash + mix_hash equality) and ContextualCheckBlockHeader
+(:11811-11875: DarkGravityWave nBits, MTP, future time, version) header by header under cs_main.
+
+Here the batch (csrc/chain/headerbatch.hpp: parsed once from its wire bytes, packed into 128-byte
+rows in one parallel pass) crosses the PCIe bus twice in total:
+
+  host  -> device  one copy: rows | kinds | DGW ancestor series | Equihash messages, solutions
+                   and serialized headers (one pinned staging buffer)
+  device           kawpow_mixonly_batch (SHA256d header hash + mix-only final + nBits boundary),
+                   hb_jobs, kawpow_verify_dag per epoch range (resident DAG, per-epoch program
+                   table resident too), hb_verdict, eq_verify + sha256d_batch + hb_eq_scatter,
+                   dgw_batch — all on one stream, no host synchronisation in between
+  device -> host   one copy: per-header code | block hash | expected nBits
+
+and the host keeps only the serial index insert (HeaderChain.accept_batch, native, GIL released,
+with the device's block hashes and nBits). Over N ranks each GPU runs the rows of its slice and the
+compact results are all-gathered device to device (RCCL) before the single copy back.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .. import core
+from . import runtime
+
+_core = core()
+ROW = 128
+CODES = {1: "invalid-mix-hash", 2: "high-hash", 3: "invalid-solution"}
+_ALIGN = 256
+
+
+def _al(x: int) -> int:
+    return (x + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class ResidentHeaderVerifier:
+    """One device's pipeline: persistent device / pinned buffers (grown on demand), a stream,
+    resident per-epoch ProgPoW program tables; DAGs come from ops/verify's resident-epoch LRU."""
+
+    def __init__(self, device: int = 0):
+        runtime.require_gpu()
+        self.device = int(device)
+        self.h = runtime.hip()
+        self.dev = torch.device("cuda", self.device)
+        with torch.cuda.device(self.dev):
+            self.stream = torch.cuda.Stream(device=self.dev)
+            self.ev_start = torch.cuda.Event(enable_timing=True)
+            self.ev_end = torch.cuda.Event(enable_timing=True)
+        self.cap = 0
+        self.in_cap = 0
+        self.programs: dict[int, torch.Tensor] = {}
+        self.k = {name: runtime.static_kernel("header_batch", name) for name in ("hb_jobs", "hb_verdict", "hb_eq_scatter")}
+        self.k_mo = runtime.static_kernel("sha256d", "kawpow_mixonly_batch")
+        self.k_sha = runtime.static_kernel("sha256d", "sha256d_batch")
+        self.k_dag = runtime.static_kernel("kawpow_verify_light", "kawpow_verify_dag")
+        self.k_eq = runtime.static_kernel("equihash", "eq_verify")
+        self.k_dgw = runtime.static_kernel("dgw", "dgw_batch")
+        from .equihash import blake2b_h0
+
+        self.h0 = blake2b_h0()
+
+    # ------------------------------------------------------------------ resident state
+    def program_table(self, epoch: int) -> torch.Tensor:
+        """The epoch's 2500 ProgPoW programs (64 words each), resident (per-epoch setup)."""
+        t = self.programs.get(epoch)
+        if t is None:
+            per = _core.EPOCH_LENGTH // 3
+            raw = _core.kawpow_programs_bytes(list(range(epoch * per, (epoch + 1) * per)))
+            with torch.cuda.device(self.dev):
+                t = torch.frombuffer(bytearray(raw), dtype=torch.int32).to(self.dev)
+            if len(self.programs) >= 8:
+                self.programs.pop(next(iter(self.programs)))
+            self.programs[epoch] = t
+        return t
+
+    def _ensure(self, n: int, in_bytes: int) -> None:
+        with torch.cuda.device(self.dev):
+            if n > self.cap:
+                cap = max(n, 2 * self.cap, 1024)
+                self.mo = torch.empty(cap * 128, dtype=torch.uint8, device=self.dev)
+                self.jobs = torch.empty(cap * 48, dtype=torch.uint8, device=self.dev)
+                self.jprog = torch.empty(cap, dtype=torch.int32, device=self.dev)
+                self.full = torch.empty(cap * 16, dtype=torch.int32, device=self.dev)
+                self.out = torch.empty(cap * 37, dtype=torch.uint8, device=self.dev)  # codes | hashes | bits
+                self.gath = torch.empty(cap * 33 * 2 + 64 * 33, dtype=torch.uint8, device=self.dev)
+                self.out_host = torch.empty(cap * 37, dtype=torch.uint8).pin_memory()
+                self.cap = cap
+            if in_bytes > self.in_cap:
+                cap = max(in_bytes, 2 * self.in_cap)
+                self.din = torch.empty(cap, dtype=torch.uint8, device=self.dev)
+                self.in_host = torch.empty(cap, dtype=torch.uint8).pin_memory()
+                self.in_cap = cap
+
+    # ------------------------------------------------------------------ one batch
+    def plan(self, batch) -> dict | None:
+        """Host-side numpy planning (no device work): epoch ranges of the KawPow rows. None when
+        the batch is not in height order (the resident path wants contiguous epoch ranges)."""
+        n = len(batch)
+        rows = np.frombuffer(batch.rows, dtype=np.uint8).reshape(n, ROW)
+        kinds = np.frombuffer(batch.kinds, dtype=np.uint8)
+        kp = np.flatnonzero(kinds == 0)
+        ranges = []
+        if len(kp):
+            heights = np.ascontiguousarray(rows[kp, 76:80]).view("<u4").ravel()
+            epochs = heights // _core.EPOCH_LENGTH
+            if np.any(np.diff(epochs.astype(np.int64)) < 0):
+                return None
+            for e in np.unique(epochs).tolist():
+                idx = kp[epochs == e]
+                ranges.append((int(e), int(idx[0]), int(idx[-1]) + 1))
+        return {"rows": rows, "kinds": kinds, "ranges": ranges}
+
+    def run(self, params, batch, series, plan: dict | None = None, world=None) -> dict:
+        """Verify the PoW of every header and compute every header's DGW nBits on the device.
+        `series`: (ancestor times bytes, ancestor bits bytes, a, base_height) of the batch's parent
+        (HeaderChain.dgw_ancestors) or None. Returns codes (n,) u8, hashes (n, 32) u8, bits (n,) u32
+        as numpy views of the pinned result buffer, plus timings."""
+        from . import verify as V
+
+        t0 = time.perf_counter()
+        n = len(batch)
+        plan = plan or self.plan(batch)
+        if plan is None:
+            raise ValueError("batch is not in height order")
+        rows, kinds = plan["rows"], plan["kinds"]
+        ws, rank = (world.world_size, world.rank) if world is not None and world.collective else (1, 0)
+        per = -(-n // ws)
+        lo_r, hi_r = min(n, rank * per), min(n, (rank + 1) * per)
+        eq_index = np.frombuffer(batch.eq_index, dtype=np.uint32)
+        mine_eq = np.flatnonzero((eq_index >= lo_r) & (eq_index < hi_r))
+        m = len(mine_eq)
+        eq_len = int(batch.eq_ser_len)
+        if m and not batch.eq_uniform:
+            raise ValueError("malformed Equihash header in the batch")
+        # staging layout (one pinned buffer, one H2D copy)
+        a = series[2] if series is not None else 0
+        off = {}
+        cur = 0
+        for name, size in (("rows", n * ROW), ("kinds", n), ("times", (a + n) * 4), ("bits", (a + n) * 4),
+                           ("eq_index", m * 4), ("eq_msgs", m * 128), ("eq_sols", m * 1344),
+                           ("eq_ser", m * eq_len), ("eq_verdict", m * 4), ("eq_hash", m * 32)):
+            off[name] = (cur, size)
+            cur = _al(cur + size)
+        self._ensure(n, cur)
+        stage = self.in_host.numpy()
+
+        def put(name, arr):
+            o, size = off[name]
+            if size:
+                stage[o:o + size] = np.frombuffer(arr, dtype=np.uint8) if not isinstance(arr, np.ndarray) else \
+                    arr.view(np.uint8).ravel()[:size]
+
+        put("rows", rows.ravel())
+        put("kinds", kinds)
+        if series is not None:
+            times = np.empty(a + n, dtype="<u4")
+            bits = np.empty(a + n, dtype="<u4")
+            times[:a] = np.frombuffer(series[0], dtype="<u4")
+            bits[:a] = np.frombuffer(series[1], dtype="<u4")
+            times[a:] = np.ascontiguousarray(rows[:, 68:72]).view("<u4").ravel()
+            bits[a:] = np.ascontiguousarray(rows[:, 72:76]).view("<u4").ravel()
+            put("times", times)
+            put("bits", bits)
+        if m:
+            put("eq_index", eq_index[mine_eq].astype(np.uint32))
+            put("eq_msgs", np.frombuffer(batch.eq_msgs, np.uint8).reshape(-1, 128)[mine_eq])
+            put("eq_sols", np.frombuffer(batch.eq_sols, np.uint8).reshape(-1, 1344)[mine_eq])
+            put("eq_ser", np.frombuffer(batch.eq_ser, np.uint8).reshape(-1, eq_len)[mine_eq])
+        t_pack = time.perf_counter()
+        h = self.h
+        base = self.din.data_ptr()
+        P = lambda name: base + off[name][0]  # noqa: E731
+        out = self.out.data_ptr()
+        lim = bytes(params.pow_limit)
+        cp = int(params.last_checkpoint_height)
+        nr = hi_r - lo_r
+
+        def glue(which: int, first: int, count: int) -> None:
+            kern = self.k[("hb_jobs", "hb_verdict", "hb_eq_scatter")[which]]
+            h.launch_header_batch(kern, which, P("rows"), P("kinds"), self.mo.data_ptr(), self.jobs.data_ptr(),
+                                  self.jprog.data_ptr(), self.full.data_ptr(), out, P("eq_index"), P("eq_verdict"),
+                                  P("eq_hash"), n, m, first, count, _core.EPOCH_LENGTH, cp, lim, s)
+
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
+            s = int(self.stream.cuda_stream)
+            self.ev_start.record(self.stream)
+            self.din[:cur].copy_(self.in_host[:cur], non_blocking=True)
+            if nr:
+                h.launch_kawpow_mixonly(self.k_mo, P("rows") + lo_r * ROW, nr, ROW, self.mo.data_ptr() + lo_r * 128, s)
+                glue(0, lo_r, nr)
+                for epoch, lo, hi in plan["ranges"]:
+                    lo, hi = max(lo, lo_r), min(hi, hi_r)
+                    if lo >= hi:
+                        continue
+                    ep = V._device_epoch(epoch, self.device)
+                    h.launch_kawpow_verify_dag(self.k_dag, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(),
+                                               self.jobs.data_ptr() + lo * 48, self.program_table(epoch).data_ptr(),
+                                               _core.EPOCH_LENGTH // 3, self.jprog.data_ptr() + lo * 4, hi - lo,
+                                               self.full.data_ptr() + lo * 64, s)
+                glue(1, lo_r, nr)
+            if m:
+                h.launch_equihash_verify(self.k_eq, self.h0, P("eq_msgs"), 112, m, P("eq_sols"), P("eq_verdict"), s)
+                h.launch_sha256d(self.k_sha, P("eq_ser"), eq_len, eq_len, m, P("eq_hash"), False, s)
+                glue(2, 0, 0)
+            bits_view = self.out[n * 33:n * 37]
+            if series is not None:
+                c = _core.dgw_constants(params)
+                h.launch_dgw(self.k_dgw, P("times"), P("bits"), out + n * 33, a, n, series[3], c["dgw_activation_block"],
+                             c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], s)
+            else:
+                bits_view.zero_()
+            if ws > 1:
+                self._gather(world, n, per, lo_r, hi_r)
+            self.out_host[:n * 37].copy_(self.out[:n * 37], non_blocking=True)
+            self.ev_end.record(self.stream)
+        t_issue = time.perf_counter()
+        self.ev_end.synchronize()
+        t_done = time.perf_counter()
+        res = self.out_host.numpy()
+        return {"codes": res[:n], "hashes": res[n:n * 33].reshape(n, 32), "bits": res[n * 33:n * 37].view("<u4"),
+                "pack_ms": (t_pack - t0) * 1e3, "issue_ms": (t_issue - t_pack) * 1e3,
+                "wait_ms": (t_done - t_issue) * 1e3, "device_ms": self.ev_start.elapsed_time(self.ev_end)}
+
+    def _gather(self, world, n: int, per: int, lo_r: int, hi_r: int) -> None:
+        """All ranks' codes and block hashes (33 bytes per row) into every rank's result buffer:
+        one all_gather_into_tensor of per x 33 bytes per rank, RCCL over xGMI device to device
+        (the DGW nBits are computed by every rank for the whole batch: nothing to exchange)."""
+        import torch.distributed as dist
+
+        ws = world.world_size
+        cnt = hi_r - lo_r
+        send = self.gath[ws * per * 33: ws * per * 33 + per * 33].view(per, 33)
+        if cnt:
+            send[:cnt, 0] = self.out[lo_r:hi_r]
+            send[:cnt, 1:] = self.out[n + lo_r * 32:n + hi_r * 32].view(cnt, 32)
+        recv = self.gath[:ws * per * 33]
+        dist.all_gather_into_tensor(recv, send.reshape(-1), group=world.group)
+        g = recv.view(ws, per, 33)
+        for r in range(ws):
+            lo, hi = min(n, r * per), min(n, (r + 1) * per)
+            if hi > lo:
+                self.out[lo:hi] = g[r, :hi - lo, 0]
+                self.out[n + lo * 32:n + hi * 32] = g[r, :hi - lo, 1:].reshape(-1)

@@ -1,0 +1,115 @@
+"""Device-resident batch header verify (ops/header_batch.py, models/verify.process_batch_resident;
+BASELINE config 5): one upload, PoW + block hashes + DGW nBits on the GPU, one download, the serial
+index insert on the host. Must give the same chain and the same first rejection (index and
+reason) as the host path (HeaderChain.accept_headers with the CPU golden PoW)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DATA = os.path.join(os.path.dirname(__file__), "data")
+
+
+def _load(core, fixture):
+    from nodexa_chain_core_amd.models import synthetic
+
+    params, headers = synthetic.load(os.path.join(DATA, fixture))
+    raw = open(os.path.join(DATA, fixture), "rb").read()
+    return params, list(headers), raw
+
+
+@pytest.mark.parametrize("fixture", ["testnet_kawpow_10k.hdr", "testnet_mixed_10k.hdr"])
+def test_resident_matches_host_chain(core, gpu, fixture):
+    from nodexa_chain_core_amd.models.verify import process_batch_resident
+
+    params, hs, raw = _load(core, fixture)
+    act = params.kawpow_activation_time
+    adj = hs[-1].time + 3600
+    ref = core.HeaderChain(params)
+    assert all(r.ok for r in ref.accept_headers(hs, adj, False))
+    batch = core.HeaderBatch.from_bytes(raw, act)
+    for _ in range(2):  # cold (epoch DAGs, program tables) and warm
+        c = core.HeaderChain(params)
+        r = process_batch_resident(c, batch, adj, device=0)
+        assert r["accepted"] == len(hs) and r["reject"] is None, r
+        assert c.tip().hash == ref.tip().hash and c.height() == ref.height()
+    assert r["device_ms"] > 0 and r["dgw_gpu"]
+
+
+def _tampered(core, params, hs, i, field):
+    act = params.kawpow_activation_time
+    bad = [core.BlockHeader.deserialize(h.serialize(act), act) for h in hs]
+    h = bad[i]
+    if field == "mix":
+        m = bytearray(h.mix_hash)
+        m[3] ^= 1
+        h.mix_hash = bytes(m)
+    elif field == "nonce":
+        h.nonce64 ^= 1 << 40
+    elif field == "bits":
+        h.bits ^= 1
+    elif field == "solution":
+        s = bytearray(h.solution)
+        s[100] ^= 0x10
+        h.solution = bytes(s)
+    bad[i] = h
+    return bad
+
+
+@pytest.mark.parametrize("field,fixture,index", [("mix", "testnet_kawpow_10k.hdr", 4321),
+                                                 ("nonce", "testnet_kawpow_10k.hdr", 9000),
+                                                 ("bits", "testnet_kawpow_10k.hdr", 7000),
+                                                 ("solution", "testnet_mixed_10k.hdr", None)])
+def test_resident_rejects_like_host(core, gpu, field, fixture, index):
+    from nodexa_chain_core_amd.models.verify import process_batch_resident
+
+    params, hs, _raw = _load(core, fixture)
+    act = params.kawpow_activation_time
+    if index is None:
+        index = next(i for i in range(len(hs) - 1, 0, -1) if hs[i].is_equihash())
+    bad = _tampered(core, params, hs, index, field)
+    adj = hs[-1].time + 3600
+    want = core.HeaderChain(params).accept_headers(bad, adj, True)  # host golden PoW
+    batch = core.HeaderBatch.from_headers(bad, act)
+    c = core.HeaderChain(params)
+    r = process_batch_resident(c, batch, adj, device=0)
+    assert r["accepted"] == len(want) - 1 == index, (r, want[-1].reject)
+    assert r["reject"]["index"] == index and r["reject"]["reason"] == want[-1].reject
+
+
+def test_resident_one_rank_rccl_gather(core, gpu, tmp_path):
+    """The multi-rank form (slices + the RCCL all-gather of codes and hashes) on a forced one-rank
+    process group: same result as the plain run."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = f"""
+import sys, json
+sys.path.insert(0, {root!r})
+from nodexa_chain_core_amd import _core as core
+from nodexa_chain_core_amd.models import synthetic
+from nodexa_chain_core_amd.models.verify import process_batch_resident
+from nodexa_chain_core_amd.parallel import world as W
+w = W.init(use_gpu=True, force_collectives=True)
+params, hs = synthetic.load({os.path.join(DATA, 'testnet_mixed_10k.hdr')!r})
+batch = core.HeaderBatch.from_headers(list(hs), params.kawpow_activation_time)
+c = core.HeaderChain(params)
+r = process_batch_resident(c, batch, hs[-1].time + 3600, device=0, world=w)
+print(json.dumps({{"accepted": r["accepted"], "backend": w.backend, "tip": core.u256_hex(c.tip().hash)}}))
+W.shutdown()
+"""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 500), RANK="0",
+               WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    import json
+
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    params, hs, _ = _load(core, "testnet_mixed_10k.hdr")
+    ref = core.HeaderChain(params)
+    ref.accept_headers(hs, hs[-1].time + 3600, False)
+    assert out["backend"] == "nccl" and out["accepted"] == len(hs) and out["tip"] == core.u256_hex(ref.tip().hash)
+    assert np.all(True)

@@ -189,3 +189,42 @@ def test_max_reorg_depth_guard(chain_fixture):
     assert chain.accept_header(shallow, adj, False).ok
     chain.max_reorg_depth = 0
     assert chain.accept_header(fork, adj, False).ok and chain.tip().hash == tip
+
+
+def test_header_batch_rows_and_accept_batch(core):
+    """csrc/chain/headerbatch.hpp: parsed from the wire bytes in parallel, packed rows equal the
+    serializations, and HeaderChain.accept_batch over [lo, hi) ranges builds the same chain as
+    accept_headers (hashes / nBits omitted: computed on the host)."""
+    import os
+
+    import numpy as np
+
+    from nodexa_chain_core_amd.models import synthetic
+
+    path = os.path.join(os.path.dirname(__file__), "data", "testnet_mixed_10k.hdr")
+    params, hs = synthetic.load(path)
+    act = params.kawpow_activation_time
+    raw = open(path, "rb").read()
+    b = core.HeaderBatch.from_bytes(raw, act)
+    assert len(b) == len(hs) and b.eq_uniform and b.eq_ser_len == len(hs[-1].serialize(act))
+    rows = np.frombuffer(b.rows, np.uint8).reshape(-1, 128)
+    kinds = np.frombuffer(b.kinds, np.uint8)
+    eq = np.frombuffer(b.eq_index, np.uint32)
+    for i in (0, 1, 4999, int(eq[0]), len(hs) - 1):
+        h = hs[i]
+        if h.is_equihash():
+            assert kinds[i] == 2 and rows[i, :80].tobytes() == h.kawpow_input()
+        else:
+            assert kinds[i] == 0 and rows[i, :120].tobytes() == h.serialize(act)
+    k = list(eq).index(int(eq[0]))
+    assert bytes(b.eq_sols)[k * 1344:(k + 1) * 1344] == hs[int(eq[0])].solution
+    assert bytes(b.eq_msgs)[k * 128:k * 128 + 112] == hs[int(eq[0])].equihash_input()
+    adj = hs[-1].time + 3600
+    ref = core.HeaderChain(params)
+    ref.accept_headers(list(hs[:3000]), adj, True)
+    c = core.HeaderChain(params)
+    assert c.accept_batch(b, adj, None, None, 0, 1500) == (1500, None, 0)
+    assert c.accept_batch(b, adj, None, None, 1500, 3000) == (1500, None, 0)
+    assert c.tip().hash == ref.tip().hash
+    with pytest.raises(Exception):
+        core.HeaderBatch.from_bytes(raw[:-7], act)  # truncated
