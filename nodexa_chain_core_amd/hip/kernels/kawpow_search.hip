@@ -49,13 +49,15 @@
 #endif
 #include KAWPOW_PROGRAM_HEADER
 
-// Tuning knobs (compile-time; ops/jit.py passes them as -D variants):
+// Tuning knobs (compile-time; ops/jit.py passes them as -D variants). The variants measured and
+// lost were removed after round 3 (profiles/README r4a: KP_L1G, KP_BUFFER, KP_MUL33_SHIFT,
+// KP_DIGEST_GLOBAL, KP_FASTMOD24, KP_PRIO and the loop without DPP broadcasts); the search is
+// bounded by its own gather + L1-lookup skeleton (the KP_SKEL_* ceiling above), not by a knob.
 //   KP_HASHES     hashes interleaved per 16-lane group (1, 2, 4 or 8)
 //   KP_MIN_WAVES  minimum waves per SIMD for __launch_bounds__ (caps VGPRs)
 //   KP_NT_DAG     non-temporal DAG loads (the 4 GiB DAG has no L2 reuse)
 //   KP_SCHED_FENCE scheduling barriers around each round's cache/math program, so the DAG
 //                 gather issued at the top of the round is consumed only at its end
-//   KP_PRIO       raised wave priority from the DAG merge to the next gather's issue
 #ifndef KP_HASHES
 #define KP_HASHES 2
 #endif
@@ -64,10 +66,9 @@
 #endif
 //   KP_BLOCK      threads per workgroup (the host launcher reads it back from
 //                 the kernel's max-threads attribute)
-//   KP_DPP        rounds unrolled by 16; item index broadcast by DPP row_newbcast
+//   KP_DPP        (always on; accepted for compatibility) rounds unrolled by 16, the item index
+//                 broadcast by DPP row_newbcast
 //   KP_BARRETT    5-op Barrett modulo for the item index
-//   KP_FASTMOD24  the same with 24-bit (full-rate) multiplies, items < 2^24 (DAG < 4 GiB)
-//   KP_BUFFER     raw-buffer DAG loads with a 32-bit offset (DAG < 4 GiB only)
 //   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride), DAG < 4 GiB only
 //   KP_L1X4       L1 replicated 4x in LDS (64 KiB) so an L1 address is one
 //                 16-bit shift: ((x << 2) & 0xffff) reads l1[x % 4096]
@@ -75,10 +76,6 @@
 //                 owns the hash's nonce (8 DPP broadcasts + 8 selects per hash, 8 VGPRs)
 //                 instead of a 32 B/nonce LDS buffer: the workgroup's LDS is then only
 //                 the L1 table, so 1024-thread groups fit twice per CU (8 waves/SIMD)
-//   KP_L1G=<mask> cache accesses i with bit i set in <mask> read the L1 word from the DAG's first
-//                 16 KiB in HBM (a buffer_load that hits the CU's vector L1) instead of the LDS copy:
-//                 the LDS array, not the TA/TCP path, is the busy unit of the round (profiles/r3z),
-//                 so a few of the 11 lookups per round move to the idle one
 #ifndef KP_BLOCK
 #define KP_BLOCK NODEXA_KAWPOW_BLOCK
 #endif
@@ -102,20 +99,6 @@ NX_DEV uint32_t kp_l1_read(const uint32_t* l1, uint32_t x) {
 #define KP_L1_WORDS 4096
 #define KP_L1(l1, x) (l1)[(x) & 4095u]
 #endif
-#ifdef KP_L1G
-NX_DEV uint32_t kp_l1g_read(__amdgpu_buffer_rsrc_t g, uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(g, (x << 2) & 0x3ffcu, 0, 0);
-}
-#undef KP_L1S
-#define KP_L1S(i, l1, x) (((KP_L1G) >> (i)) & 1 ? kp_l1g_read(l1g, (x)) : KP_L1(l1, x))
-typedef __amdgpu_buffer_rsrc_t kp_l1g_t;
-NX_DEV kp_l1g_t kp_l1g_handle(const void* dag) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(dag), (short)0, 16384, 0x00020000);
-}
-#else
-typedef const void* kp_l1g_t;
-NX_DEV kp_l1g_t kp_l1g_handle(const void* dag) { return dag; }
-#endif
 
 // LDS copy of the L1 (first 16 KiB of the DAG), KP_L1_WORDS / 4096 times.
 NX_DEV void kp_fill_l1(uint32_t* l1, const void* dag) {
@@ -134,37 +117,14 @@ NX_DEV uint4 kp_dag_load(const uint4* p) {
 #endif
 }
 
-// x*33 for the merge ops. Left to itself the compiler folds `a*33 + b` into
-// v_mad_u64_u32 (a multi-cycle integer MAD); KP_MUL33_SHIFT pins it to one
-// full-rate v_lshl_add_u32 (a<<5)+a, leaving the +b as a plain add.
-#ifdef KP_MUL33_SHIFT
-NX_DEV uint32_t kp_mul33(uint32_t a) {
-    uint32_t r;
-    asm("v_lshl_add_u32 %0, %1, 5, %1" : "=v"(r) : "v"(a));
-    return r;
-}
-#else
+// x*33 for the merge ops: the compiler's v_mad_u64_u32 for `a*33 + b` beats a shift-add
+// (profiles/README r2b).
 NX_DEV uint32_t kp_mul33(uint32_t a) { return a * 33u; }
-#endif
 
 NX_DEV uint32_t kp_clz(uint32_t x) { return x ? (uint32_t)__builtin_clz(x) : 32u; }
 NX_DEV uint32_t kp_fnv1a(uint32_t h, uint32_t d) { return (h ^ d) * 0x01000193u; }
-#ifdef KP_FASTMOD24
-// 24-bit Barrett for 2^16 < d < 2^24 (DAGs < 4 GiB, with KP_SBUFFER): q' = mulhi24(x >> 8,
-// floor(2^40/d)) is q or q-1 (the dropped low byte and the floor of m24 move the estimate by
-// < 2^-7), then r = x - mul24(q', d) and one min(). Every op is a full-rate VALU op, where the
-// 32-bit v_mul_hi_u32 / v_mul_lo_u32 of KP_BARRETT issue at a quarter of that rate.
-__device__ uint32_t kp_mulhi_u24(uint32_t a, uint32_t b) __asm("llvm.amdgcn.mulhi.u24");
-__device__ uint32_t kp_mul_u24(uint32_t a, uint32_t b) __asm("llvm.amdgcn.mul.u24");
-#endif
 NX_DEV uint32_t kp_fastmod(uint32_t x, const FastMod32& f) {
-#if defined(KP_FASTMOD24)
-    // no fallback path: ops/jit.defines_for selects this variant only for 2^16 < d < 2^24 (a
-    // uniform runtime branch to the 32-bit form doubled the round code and spilled 198 VGPRs)
-    const uint32_t q = kp_mulhi_u24(x >> 8, f.m24);
-    const uint32_t r = x - kp_mul_u24(q, f.d);
-    return min(r, r - f.d);
-#elif defined(KP_BARRETT)
+#if defined(KP_BARRETT)
     // q' = floor(x * floor(2^32/d) / 2^32) is q or q-1, so r' < 2d and one
     // unsigned min(r', r'-d) finishes it (r'-d wraps high when r' < d).
     const uint32_t r = x - __umulhi(x, f.mb) * f.d;
@@ -176,14 +136,12 @@ NX_DEV uint32_t kp_fastmod(uint32_t x, const FastMod32& f) {
 #endif
 }
 
-// DAG item access. KP_BUFFER addresses the (< 4 GiB) DAG through a raw buffer
-// resource with a 32-bit byte offset (one v_lshl_add) instead of 64-bit
-// pointer arithmetic.
+// DAG item access: structured-buffer loads below 4 GiB, 64-bit pointers above.
 #if defined(KP_SBUFFER)
 // Structured-buffer addressing: vindex = item, stride 256 B in the V#, voffset = the lane's
 // 16-byte slice: one buffer_load_dwordx4 idxen offen per round and no address VALU at all
-// (KP_BUFFER still needs one v_lshl_add): +1.1 % at epoch 384 (profiles/r1s_kawpow). The
-// hardware forms index*stride+offset in 32 bits, so like KP_BUFFER it is for DAGs < 4 GiB
+// (a raw-buffer form needed one v_lshl_add): +1.1 % at epoch 384 (profiles/r1s_kawpow). The
+// hardware forms index*stride+offset in 32 bits, so it is for DAGs < 4 GiB
 // (measured: not bit-exact at epoch 390). clang has no struct-buffer builtin, so the LLVM
 // intrinsic is bound by name (the compiler still tracks its vmcnt like any other load).
 typedef int32_t kp_i32x4 __attribute__((ext_vector_type(4)));
@@ -196,7 +154,7 @@ NX_DEV kp_dag_t kp_dag_handle(const void* dag) {
     r.x = (int32_t)(uint32_t)base;
     r.y = (int32_t)(((uint32_t)(base >> 32) & 0xffffu) | (256u << 16));  // stride 256 B
     r.z = -1;                                                             // num_records: no clamp
-    r.w = 0x00020000;                                                     // DATA_FORMAT 32 (as KP_BUFFER)
+    r.w = 0x00020000;                                                     // DATA_FORMAT 32
     return r;
 }
 NX_DEV uint4 kp_dag_item(kp_dag_t dag, uint32_t index, uint32_t part) {
@@ -207,22 +165,6 @@ NX_DEV uint4 kp_dag_item(kp_dag_t dag, uint32_t index, uint32_t part) {
 #endif
     const kp_i32x4 v = kp_struct_load(dag, (int)index, (int)(part << 4), 0, aux);
     return make_uint4((uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w);
-}
-#elif defined(KP_BUFFER)
-typedef __amdgpu_buffer_rsrc_t kp_dag_t;
-NX_DEV kp_dag_t kp_dag_handle(const void* dag) {
-    // num_records 0xffffffff: no range clamp; the host only selects KP_BUFFER for DAGs < 4 GiB
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(dag), (short)0, -1, 0x00020000);
-}
-NX_DEV uint4 kp_dag_item(kp_dag_t dag, uint32_t index, uint32_t part) {
-#ifdef KP_NT_DAG
-    const int aux = 2;
-#else
-    const int aux = 0;
-#endif
-    const kp_u32x4 v = __builtin_bit_cast(kp_u32x4,
-        __builtin_amdgcn_raw_buffer_load_b128(dag, (index << 8) + (part << 4), 0, aux));
-    return make_uint4(v.x, v.y, v.z, v.w);
 }
 #else
 typedef const uint4* kp_dag_t;
@@ -303,16 +245,11 @@ NX_DEV void kp_final(const uint32_t st2[8], const uint32_t digest[8], uint32_t o
 // from lane J of the row via DPP and the lane's 16-byte slice is lane ^ J.
 template <int J>
 NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
-                       kp_l1g_t l1g, uint32_t lane) {
-    (void)l1g;
+                       uint32_t lane) {
     uint4 d[KP_HASHES];
     const uint32_t part = lane ^ (uint32_t)J;
 #pragma unroll
     for (int k = 0; k < KP_HASHES; ++k) d[k] = kp_dag_item(dag, kp_fastmod(kp_bcast<J>(mx[k][0]), items), part);
-#ifdef KP_PRIO
-    // the gather is out: back to normal priority for the round's program (see below)
-    __builtin_amdgcn_s_setprio(0);
-#endif
 #ifdef KP_SCHED_FENCE
     // Keep the round's DAG merge after the whole cache/math program: left alone, the register-
     // pressure scheduler pulls the merge (and its vmcnt wait) into the middle of the program, so
@@ -324,16 +261,11 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMo
 #ifdef KP_SCHED_FENCE
     __builtin_amdgcn_sched_barrier(0);
 #endif
-#ifdef KP_PRIO
-    // DAG merge -> next item index -> next gather is each hash's critical path: raise this wave's
-    // issue priority over the co-resident waves' programs until the next gather has been issued
-    __builtin_amdgcn_s_setprio(2);
-#endif
 #pragma unroll
     for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
 }
 
-NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t* l1, kp_l1g_t l1g,
+NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
                             uint32_t st0, uint32_t st1, uint32_t lane, uint32_t* dig,
                             uint32_t (&own)[8]) {
 #pragma unroll 1
@@ -350,33 +282,18 @@ NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t
 #pragma unroll
             for (int i = 0; i < 32; ++i) mx[k][i] = rng.next();
         }
-#ifdef KP_DPP
         // 64 rounds = 4 x 16 with the round index mod 16 baked into each copy
 #pragma unroll 1
         for (uint32_t rr = 0; rr < 64; rr += 16) {
-            kp_round_c<0>(mx, dag, items, l1, l1g, lane);   kp_round_c<1>(mx, dag, items, l1, l1g, lane);
-            kp_round_c<2>(mx, dag, items, l1, l1g, lane);   kp_round_c<3>(mx, dag, items, l1, l1g, lane);
-            kp_round_c<4>(mx, dag, items, l1, l1g, lane);   kp_round_c<5>(mx, dag, items, l1, l1g, lane);
-            kp_round_c<6>(mx, dag, items, l1, l1g, lane);   kp_round_c<7>(mx, dag, items, l1, l1g, lane);
-            kp_round_c<8>(mx, dag, items, l1, l1g, lane);   kp_round_c<9>(mx, dag, items, l1, l1g, lane);
-            kp_round_c<10>(mx, dag, items, l1, l1g, lane);  kp_round_c<11>(mx, dag, items, l1, l1g, lane);
-            kp_round_c<12>(mx, dag, items, l1, l1g, lane);  kp_round_c<13>(mx, dag, items, l1, l1g, lane);
-            kp_round_c<14>(mx, dag, items, l1, l1g, lane);  kp_round_c<15>(mx, dag, items, l1, l1g, lane);
+            kp_round_c<0>(mx, dag, items, l1, lane);   kp_round_c<1>(mx, dag, items, l1, lane);
+            kp_round_c<2>(mx, dag, items, l1, lane);   kp_round_c<3>(mx, dag, items, l1, lane);
+            kp_round_c<4>(mx, dag, items, l1, lane);   kp_round_c<5>(mx, dag, items, l1, lane);
+            kp_round_c<6>(mx, dag, items, l1, lane);   kp_round_c<7>(mx, dag, items, l1, lane);
+            kp_round_c<8>(mx, dag, items, l1, lane);   kp_round_c<9>(mx, dag, items, l1, lane);
+            kp_round_c<10>(mx, dag, items, l1, lane);  kp_round_c<11>(mx, dag, items, l1, lane);
+            kp_round_c<12>(mx, dag, items, l1, lane);  kp_round_c<13>(mx, dag, items, l1, lane);
+            kp_round_c<14>(mx, dag, items, l1, lane);  kp_round_c<15>(mx, dag, items, l1, lane);
         }
-#else
-#pragma unroll 1
-        for (uint32_t r = 0; r < 64; ++r) {
-            uint4 d[KP_HASHES];
-            const uint32_t part = (lane ^ r) & 15;
-#pragma unroll
-            for (int k = 0; k < KP_HASHES; ++k)
-                d[k] = kp_dag_item(dag, kp_fastmod(__shfl(mx[k][0], (int)(r & 15), 16), items), part);
-#pragma unroll
-            for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM(l1, mx[k]);
-#pragma unroll
-            for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
-        }
-#endif
 #pragma unroll
         for (int k = 0; k < KP_HASHES; ++k) {
             uint32_t lh = 0x811c9dc5u;
@@ -413,14 +330,10 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     __shared__ uint32_t l1[KP_L1_WORDS];
 #if defined(KP_DIGEST_REG)
     uint32_t* digs = nullptr;
-#elif defined(KP_DIGEST_GLOBAL)
-    // digests parked in HBM (32 B per nonce, <0.2% of the DAG traffic) so the
-    // 64 KiB L1X4 table leaves LDS room for 2 workgroups of KP_BLOCK per CU
-    uint32_t* digs = p.scratch + (size_t)blockIdx.x * KP_BLOCK * 8;
 #else
     __shared__ uint32_t digs[KP_BLOCK * 8];
 #endif
-#if defined(KP_DIGEST_REG) || defined(KP_DIGEST_GLOBAL)
+#if defined(KP_DIGEST_REG)
     __shared__ uint32_t stale_word;
     uint32_t* stale = &stale_word;
 #else
@@ -441,7 +354,7 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     kp_fill_l1(l1, p.dag);
     __syncthreads();
     const uint32_t is_stale = *stale;
-#if !(defined(KP_DIGEST_REG) || defined(KP_DIGEST_GLOBAL))
+#if !defined(KP_DIGEST_REG)
     __syncthreads();  // every wave has read the flag before a digest can overwrite it
 #endif
     if (is_stale) return;  // uniform over the workgroup
@@ -453,7 +366,7 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     {
         uint32_t st2[8];
         kp_seed(p.header, nonce, st2);
-        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, kp_l1g_handle(p.dag), st2[0], st2[1], lane, dig, digest);
+        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig, digest);
     }
 #ifndef KP_DIGEST_REG
     __threadfence_block();  // digest words written by lanes 0..7 are read by lane h below
@@ -503,7 +416,7 @@ extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     uint32_t* dig = digs ? digs + (threadIdx.x & ~15u) * 8 : nullptr;
     uint32_t st2[8], digest[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fin[8];
     kp_seed(j.header, j.nonce, st2);
-    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, kp_l1g_handle(p.dag), st2[0], st2[1], lane, dig, digest);
+    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig, digest);
 #ifndef KP_DIGEST_REG
     __syncthreads();
 #pragma unroll

@@ -228,14 +228,6 @@ PYBIND11_MODULE(_hip, m) {
         const uint32_t q = (t + ((x - t) >> 1)) >> (f.s - 1);
         return x - q * f.d;
     }, "host model of the device FastMod32 (tests compare it with x % d)");
-    m.def("fastmod24_eval", [](uint32_t x, uint32_t d) {
-        FastMod32 f = make_fastmod(d);
-        if (!f.m24) throw std::invalid_argument("24-bit Barrett needs 2^16 < d < 2^24");
-        // v_mul_hi_u24 / v_mul_u24: 24x24 -> 48-bit product, high / low 32 bits
-        const uint32_t q = uint32_t((uint64_t(x >> 8) * (f.m24 & 0xffffffu)) >> 32);
-        const uint32_t r = x - uint32_t(uint64_t(q & 0xffffffu) * (f.d & 0xffffffu));
-        return std::min(r, r - f.d);
-    }, "host model of the device KP_FASTMOD24 modulo (tests compare it with x % d)");
     m.def("sizeof_results", [] { return sizeof(KawpowResults); });
     m.def("sizeof_share", [] { return sizeof(KawpowShare); });
     m.attr("KAWPOW_MAX_SHARES") = NODEXA_KAWPOW_MAX_SHARES;

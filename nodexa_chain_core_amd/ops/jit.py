@@ -97,23 +97,18 @@ DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
 
 
 def defines_for(dag_bytes: int, defines: tuple[str, ...] | None = None) -> tuple[str, ...]:
-    """The variant to compile for a DAG of `dag_bytes`: KP_SBUFFER / KP_BUFFER address the DAG
-    with 32-bit buffer offsets, so they are dropped for DAGs of 4 GiB or more (epochs >= 385;
-    measured there: the structured form is not bit-exact, the pointer form is), and there the
-    768-thread register-digest form falls back to 512 threads. KP_FASTMOD24 is dropped at 4 GiB
-    and above and for DAGs of 2^16 items or fewer (outside its exact range)."""
+    """The variant to compile for a DAG of `dag_bytes`: KP_SBUFFER addresses the DAG with 32-bit
+    buffer offsets, so it is dropped for DAGs of 4 GiB or more (epochs >= 385; measured there: the
+    structured form is not bit-exact, the pointer form is), and there the 768-thread
+    register-digest form falls back to 512 threads."""
     d = DEFAULT_DEFINES if defines is None else tuple(defines)
     if dag_bytes >= 1 << 32:  # 32-bit buffer offsets: 64-bit pointers for DAGs of 4 GiB or more
-        d = tuple(x for x in d if x not in ("KP_BUFFER", "KP_SBUFFER", "KP_FASTMOD24"))
+        d = tuple(x for x in d if x != "KP_SBUFFER")
         if "KP_BLOCK=768" in d:
             # the pointer path needs more VGPRs: at 6 waves/SIMD it spills and loses 3 % to the
             # 512-thread / 4-wave form (profiles/r2n_kawpow768, epoch 390)
             d = tuple("KP_BLOCK=512" if x == "KP_BLOCK=768" else x for x in d
                       if x not in ("KP_DIGEST_REG", "KP_MIN_WAVES=6"))
-    if dag_bytes // 256 <= 1 << 16:
-        # the 24-bit Barrett needs 2^16 < items (FastMod32.m24 is 0 below that); real epoch
-        # DAGs always have more items, small test DAGs do not
-        d = tuple(x for x in d if x != "KP_FASTMOD24")
     return d
 
 

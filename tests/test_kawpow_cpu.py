@@ -117,7 +117,7 @@ def test_light_cache_disk_cache(core, tmp_path):
 
 
 def test_search_variant_selection_by_dag_size(core):
-    """ops/jit.defines_for: the 32-bit buffer-offset DAG loads (KP_SBUFFER / KP_BUFFER) are used
+    """ops/jit.defines_for: the 32-bit buffer-offset DAG loads (KP_SBUFFER) are used
     below 4 GiB only (epoch 384 is 4294962304 bytes; epoch 385 is above 2^32)."""
     from nodexa_chain_core_amd.ops import jit
 
@@ -126,40 +126,11 @@ def test_search_variant_selection_by_dag_size(core):
     assert below < 1 << 32 <= above
     assert "KP_SBUFFER" in jit.defines_for(below, jit.TUNED_DEFINES)
     big = jit.defines_for(above, jit.TUNED_DEFINES)
-    assert "KP_SBUFFER" not in big and "KP_BUFFER" not in big and "KP_DPP" in big
+    assert "KP_SBUFFER" not in big and "KP_DPP" in big
     # 768-thread register-digest form below 4 GiB, the 512-thread form on the pointer path
     small = jit.defines_for(below, jit.TUNED_DEFINES)
     assert {"KP_BLOCK=768", "KP_DIGEST_REG", "KP_MIN_WAVES=6"} <= set(small)
     assert "KP_BLOCK=512" in big and "KP_BLOCK=768" not in big and "KP_DIGEST_REG" not in big
-    assert "KP_BUFFER" not in jit.defines_for(above, ("KP_BUFFER", "KP_DPP"))
-    assert "KP_FASTMOD24" not in jit.defines_for(above, ("KP_FASTMOD24", "KP_SBUFFER"))
-    # the 24-bit Barrett is exact only for 2^16 < items: small DAGs fall back to KP_BARRETT
-    assert "KP_FASTMOD24" in jit.defines_for(below, ("KP_FASTMOD24", "KP_BARRETT"))
-    tiny = (1 << 16) * 256
-    assert "KP_FASTMOD24" not in jit.defines_for(tiny, ("KP_FASTMOD24", "KP_BARRETT"))
-    assert "KP_FASTMOD24" in jit.defines_for(tiny + 256, ("KP_FASTMOD24", "KP_BARRETT"))
+    assert "KP_SBUFFER" not in jit.defines_for(above, ("KP_SBUFFER", "KP_DPP"))
 
 
-def test_fastmod24_model_matches_modulo():
-    """KP_FASTMOD24 (kawpow_search.hip kp_fastmod): the 24-bit Barrett is exact for every DAG
-    item count below 2^24 (DAGs < 4 GiB), checked on random and edge-case numerators."""
-    import random
-
-    from nodexa_chain_core_amd.ops import runtime
-
-    try:
-        h = runtime.hip()
-    except runtime.NativeUnavailable:
-        pytest.skip("_hip extension not built")
-    rng = random.Random(24)
-    divisors = [(1 << 16) + 1, (1 << 16) + 2, (1 << 24) - 1, 16777213, 4294962304 // 256, 8388593]
-    divisors += [rng.randrange(1 << 16, 1 << 24) for _ in range(40)]
-    for d in divisors:
-        xs = [0, 1, d - 1, d, d + 1, (1 << 32) - 1, (1 << 32) - d, ((1 << 32) // d) * d - 1]
-        xs += [rng.getrandbits(32) for _ in range(500)]
-        for x in xs:
-            assert h.fastmod24_eval(x, d) == x % d, (x, d)
-    with pytest.raises(ValueError):
-        h.fastmod24_eval(5, 1 << 24)
-    with pytest.raises(ValueError):
-        h.fastmod24_eval(5, 1 << 16)
