@@ -476,6 +476,8 @@ void bind_extra(py::module_& m) {
         .def_readonly("header", &HeaderIndex::header)
         .def_property_readonly("chain_work", [](const HeaderIndex& i) { return arith_to_int(i.chain_work); })
         .def_property_readonly("prev_hash", [](const HeaderIndex& i) { return i.prev ? pyb(i.prev->hash) : pyb(Uint256()); })
+        .def_property_readonly("skip_height", [](const HeaderIndex& i) { return i.skip ? i.skip->height : -1; })
+        .def("ancestor", &HeaderIndex::ancestor, py::return_value_policy::reference_internal)
         .def("median_time_past", &HeaderIndex::median_time_past);
 
     py::class_<AcceptResult>(m, "AcceptResult")

@@ -48,6 +48,16 @@ Uint256 CpuPowVerifier::block_hash_full(const BlockHeader& h, const ChainParams&
 }
 
 // ---------------------------------------------------------------- chain
+namespace {
+
+// GetSkipHeight (src/chain.cpp): the height an entry's skip pointer targets
+int skip_height(int h) {
+    auto invert_low = [](int n) { return n & (n - 1); };
+    return h < 2 ? 0 : ((h & 1) ? invert_low(invert_low(h - 1)) + 1 : invert_low(h));
+}
+
+}  // namespace
+
 HeaderChain::HeaderChain(ChainParams params, std::shared_ptr<const PowVerifier> verifier)
     : params_(std::move(params)), verifier_(std::move(verifier)) {
     const BlockHeader& g = params_.genesis.header;
@@ -59,9 +69,8 @@ HeaderChain::HeaderChain(ChainParams params, std::shared_ptr<const PowVerifier> 
 }
 
 const HeaderIndex* HeaderChain::add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev,
-                                              const ArithU256* proof) {
-    storage_.emplace_back();
-    HeaderIndex& idx = storage_.back();
+                                              const ArithU256* proof, const std::vector<const HeaderIndex*>* batch) {
+    HeaderIndex& idx = *storage_.alloc();
     idx.hash = hash;
     idx.prev = prev;
     idx.height = prev ? prev->height + 1 : 0;
@@ -70,13 +79,13 @@ const HeaderIndex* HeaderChain::add_to_index(const BlockHeader& h, const Uint256
     idx.header = h;
     idx.chain_work = (prev ? prev->chain_work : ArithU256()) + (proof ? *proof : block_proof(h.bits));
     if (prev) {
-        // skip pointer: GetSkipHeight (src/chain.cpp)
-        auto invert_low = [](int n) { return n & (n - 1); };
-        const int hgt = idx.height;
-        const int skip_h = hgt < 2 ? 0 : ((hgt & 1) ? invert_low(invert_low(hgt - 1)) + 1 : invert_low(hgt));
-        idx.skip = prev->ancestor(skip_h);
+        const int skip_h = skip_height(idx.height);
+        // inside a linear batch the skip target is often a node added moments ago: look it up
+        // directly instead of walking back from prev
+        const int b0 = batch && !batch->empty() ? (*batch)[0]->height : 0;
+        idx.skip = batch && !batch->empty() && skip_h >= b0 ? (*batch)[size_t(skip_h - b0)] : prev->ancestor(skip_h);
     }
-    index_[hash] = &idx;
+    index_.insert(&idx);
     return &idx;
 }
 
@@ -143,6 +152,68 @@ AcceptResult HeaderChain::accept_header(const BlockHeader& h, int64_t adjusted_t
     return accept_header_impl(h, nullptr, adjusted_time, check_pow, nullptr, nullptr);
 }
 
+// ContextualCheckBlockHeader after the -maxreorg guard, in the reference's order, on values the
+// caller supplies: the expected nBits, the parent's median time past and whether the header forks
+// below the last checkpoint (the only rule that reads the active chain). Context-free otherwise,
+// so a linear batch evaluates it for all headers at once.
+bool HeaderChain::contextual_rules(const BlockHeader& h, const Uint256& hash, int height, u32 expected_bits,
+                                   int64_t prev_mtp, int64_t adjusted_time, bool cp_fork, AcceptResult& r) const {
+    if (h.bits != expected_bits) {
+        r.reject = "bad-diffbits";
+        r.dos = 100;
+        return false;
+    }
+    if (cp_fork) {
+        r.reject = "bad-fork-prior-to-checkpoint";
+        r.dos = 100;
+        return false;
+    }
+    auto cpit = params_.checkpoints.find(height);
+    if (cpit != params_.checkpoints.end() && cpit->second != hash) {
+        r.reject = "checkpoint mismatch";
+        r.dos = 100;
+        return false;
+    }
+    if (int64_t(h.time) <= prev_mtp) {
+        r.reject = "time-too-old";
+        return false;
+    }
+    const int64_t max_future = (height >= params_.dgw_activation_block) ? kMaxFutureBlockTimeDgw : kMaxFutureBlockTime;
+    if (int64_t(h.time) > adjusted_time + max_future) {
+        r.reject = "time-too-new";
+        return false;
+    }
+    if (h.version < kVersionBitsTopBitsAssets) {
+        char buf[48];
+        std::snprintf(buf, sizeof(buf), "bad-version(0x%08x)", unsigned(h.version));
+        r.reject = buf;
+        return false;
+    }
+    // Equihash extension era (new): the flag bit is required from the activation
+    // time on and forbidden before it (so reference-network headers never parse
+    // as extended ones), and the extended header commits to its height.
+    const bool eq_era = h.time >= params_.equihash_activation_time;
+    if (eq_era != h.is_equihash()) {
+        r.reject = eq_era ? "bad-version(equihash-required)" : "bad-version(equihash-not-active)";
+        r.dos = 100;
+        return false;
+    }
+    if (h.is_equihash() && int(h.height) != height) {
+        r.reject = "bad-height";
+        r.dos = 100;
+        return false;
+    }
+    // The reference never checks that a KawPow header's nHeight equals its index
+    // height (the epoch/period therefore follow the claimed height). Off by
+    // default for consensus compatibility; -strictheight turns it on as policy.
+    if (strict_kawpow_height && params_.algo_for(h.time) == PowAlgo::KAWPOW && int(h.height) != height) {
+        r.reject = "bad-height";
+        r.dos = 100;
+        return false;
+    }
+    return true;
+}
+
 AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256* known_hash, int64_t adjusted_time,
                                              bool check_pow, const u32* expected_bits, const AcceptResult* precheck,
                                              const ArithU256* proof, const int64_t* prev_mtp) {
@@ -155,11 +226,10 @@ AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256
         r.index = genesis_;
         return r;
     }
-    auto self = index_.find(hash);
-    if (self != index_.end()) {
-        r.index = self->second;
+    if (const HeaderIndex* self = index_.find(hash)) {
+        r.index = self;
         r.duplicate = true;
-        if (failed_.count(self->second)) {
+        if (failed_.count(self)) {
             r.reject = "duplicate";
             return r;
         }
@@ -169,13 +239,12 @@ AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256
     r = precheck ? *precheck : check_header(h, check_pow);
     if (!r.ok) return r;
     r.ok = false;
-    auto pit = index_.find(h.prev);
-    if (pit == index_.end()) {
+    const HeaderIndex* prev = index_.find(h.prev);
+    if (prev == nullptr) {
         r.reject = "prev-blk-not-found";
         r.dos = 10;
         return r;
     }
-    const HeaderIndex* prev = pit->second;
     if (failed_.count(prev)) {
         r.reject = "bad-prevblk";
         r.dos = 100;
@@ -188,60 +257,11 @@ AcceptResult HeaderChain::accept_header_impl(const BlockHeader& h, const Uint256
         r.dos = 10;
         return r;
     }
-    if (h.bits != (expected_bits ? *expected_bits : next_work_required(prev, h, params_))) {
-        r.reject = "bad-diffbits";
-        r.dos = 100;
-        return r;
-    }
     const int cp = params_.last_checkpoint_height();
-    if (cp >= 0 && height < cp && at_height(cp) != nullptr) {
-        r.reject = "bad-fork-prior-to-checkpoint";
-        r.dos = 100;
+    const bool cp_fork = cp >= 0 && height < cp && at_height(cp) != nullptr;
+    if (!contextual_rules(h, hash, height, expected_bits ? *expected_bits : next_work_required(prev, h, params_),
+                          prev_mtp ? *prev_mtp : prev->median_time_past(), adjusted_time, cp_fork, r))
         return r;
-    }
-    auto cpit = params_.checkpoints.find(height);
-    if (cpit != params_.checkpoints.end() && cpit->second != hash) {
-        r.reject = "checkpoint mismatch";
-        r.dos = 100;
-        return r;
-    }
-    if (int64_t(h.time) <= (prev_mtp ? *prev_mtp : prev->median_time_past())) {
-        r.reject = "time-too-old";
-        return r;
-    }
-    const int64_t max_future = (height >= params_.dgw_activation_block) ? kMaxFutureBlockTimeDgw : kMaxFutureBlockTime;
-    if (int64_t(h.time) > adjusted_time + max_future) {
-        r.reject = "time-too-new";
-        return r;
-    }
-    if (h.version < kVersionBitsTopBitsAssets) {
-        char buf[48];
-        std::snprintf(buf, sizeof(buf), "bad-version(0x%08x)", unsigned(h.version));
-        r.reject = buf;
-        return r;
-    }
-    // Equihash extension era (new): the flag bit is required from the activation
-    // time on and forbidden before it (so reference-network headers never parse
-    // as extended ones), and the extended header commits to its height.
-    const bool eq_era = h.time >= params_.equihash_activation_time;
-    if (eq_era != h.is_equihash()) {
-        r.reject = eq_era ? "bad-version(equihash-required)" : "bad-version(equihash-not-active)";
-        r.dos = 100;
-        return r;
-    }
-    if (h.is_equihash() && int(h.height) != height) {
-        r.reject = "bad-height";
-        r.dos = 100;
-        return r;
-    }
-    // The reference never checks that a KawPow header's nHeight equals its index
-    // height (the epoch/period therefore follow the claimed height). Off by
-    // default for consensus compatibility; -strictheight turns it on as policy.
-    if (strict_kawpow_height && params_.algo_for(h.time) == PowAlgo::KAWPOW && int(h.height) != height) {
-        r.reject = "bad-height";
-        r.dos = 100;
-        return r;
-    }
     r.index = add_to_index(h, hash, prev, proof);
     r.ok = true;
     consider_new_header(r.index);
@@ -267,12 +287,11 @@ bool HeaderChain::dgw_series(const BlockHeader* hs, size_t n, const Uint256* has
                              std::vector<u32>& bits, size_t& a, int& base_height) const {
     std::lock_guard<std::recursive_mutex> g(mu_);
     if (n == 0 || hashes == nullptr) return false;
-    auto pit = index_.find(hs[0].prev);
-    bool linear = pit != index_.end();
+    const HeaderIndex* base = index_.find(hs[0].prev);
+    bool linear = base != nullptr;
     for (size_t i = 1; linear && i < n; ++i) linear = hs[i].prev == hashes[i - 1];
     const ConsensusParams& c = params_.consensus;
     if (!linear || (c.pow_allow_min_difficulty_blocks && c.pow_no_retargeting)) return false;
-    const HeaderIndex* base = pit->second;
     std::vector<const HeaderIndex*> anc;  // base and up to 179 ancestors, newest first
     for (const HeaderIndex* p = base; p && anc.size() < size_t(kDgwPastBlocks); p = p->prev) anc.push_back(p);
     a = anc.size();
@@ -314,6 +333,8 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const BlockHeader* hs, siz
         pre.resize(n);
         parallel_for(n, [&](size_t i) { pre[i] = check_header(hs[i], true); });
     }
+    std::vector<u8> ctx, fresh;
+    int base_height = 0;
     if (n >= kParallelAcceptMin) {
         if (known_hashes) {
             hashes.assign(known_hashes, known_hashes + n);
@@ -321,64 +342,177 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const BlockHeader* hs, siz
             hashes.resize(n);
             parallel_for(n, [&](size_t i) { hashes[i] = verifier_->block_hash(hs[i], params_); });
         }
-        // context-free per-header work of the serial pass, done up front on all cores: the block
-        // proof (2^256 / (target + 1), a 256-bit division) and, for a linear batch, the median
-        // time past of each header's parent from the batch's own time series
+        // The context-free per-header work of the serial pass, done up front in one pass on all
+        // cores: the block proof (2^256 / (target + 1)) and, for a linear batch, the parent's
+        // median time past and the expected nBits from the batch's own (nTime, nBits) series --
+        // and then, when nothing in the index has failed, the contextual rules themselves
+        // (ctx: 1 ok, 0 failed or not evaluated, 2 failed at bad-diffbits) and whether the header
+        // is new to the index (a linear batch cannot repeat a hash).
         proofs.resize(n);
-        parallel_for(n, [&](size_t i) { proofs[i] = block_proof(hs[i].bits); });
         std::vector<u32> times, bits;
         size_t a = 0;
-        int base_height = 0;
-        if (dgw_series(hs, n, hashes.data(), times, bits, a, base_height)) {
+        if (!dgw_series(hs, n, hashes.data(), times, bits, a, base_height)) {
+            parallel_for(n, [&](size_t i) { proofs[i] = block_proof(hs[i].bits); });
+        } else {
             const bool from_genesis = a == size_t(base_height) + 1;  // the series reaches genesis
-            mtp.resize(n);
+            const bool fast = failed_.empty() && !(check_pow && pre.empty());
+            const u32 limit_compact = ArithU256::from_uint256(params_.consensus.pow_limit).get_compact();
+            mtp.assign(n, 0);
+            expected.assign(n, 0);
+            if (fast) {
+                ctx.assign(n, 0);
+                fresh.assign(n, 0);
+            }
             parallel_for(n, [&](size_t i) {
+                proofs[i] = block_proof(hs[i].bits);
                 const int64_t j = int64_t(a) - 1 + int64_t(i);  // series index of header i's parent
-                if (j < 10 && !from_genesis) return;
-                int64_t w[11];
-                int m = 0;
-                for (int64_t k = j; k >= 0 && m < 11; --k) w[m++] = times[size_t(k)];
-                std::sort(w, w + m);
-                mtp[i] = w[m / 2];
-                have_mtp[i] = 1;
-            });
-            if (known_bits) {
-                // computed by the caller from the same series (the GPU batch kernel, dgw.hip);
-                // 0 = not a DGW header, left to the serial path
-                expected.assign(known_bits, known_bits + n);
-                for (size_t i = 0; i < n; ++i) have[i] = expected[i] != 0;
-            } else {
-                const u32 limit_compact = ArithU256::from_uint256(params_.consensus.pow_limit).get_compact();
-                expected.resize(n);
-                parallel_for(n, [&](size_t i) {
-                    const int last_height = base_height + int(i);  // height of header i's parent
-                    if (last_height + 1 < params_.dgw_activation_block) return;  // BTC retarget: serial path
+                if (j >= 10 || from_genesis) {
+                    int64_t w[11];
+                    int m = 0;
+                    for (int64_t k = j; k >= 0 && m < 11; --k) w[m++] = times[size_t(k)];
+                    std::sort(w, w + m);
+                    mtp[i] = w[m / 2];
+                    have_mtp[i] = 1;
+                }
+                // expected nBits: from the caller where it has them (the GPU batch kernel, dgw.hip,
+                // computes them from the same series; 0 = not computed there), else from the
+                // series here; BTC-retarget-era headers are left to the serial path
+                const int last_height = base_height + int(i);  // height of header i's parent
+                if (known_bits && known_bits[i] != 0) {
+                    expected[i] = known_bits[i];
+                    have[i] = 1;
+                } else if (last_height + 1 >= params_.dgw_activation_block) {
                     expected[i] = last_height < kDgwPastBlocks
                                       ? limit_compact
-                                      : dgw_average(times.data(), bits.data(), int64_t(a) - 1 + int64_t(i), hs[i].time,
-                                                    params_);
+                                      : dgw_average(times.data(), bits.data(), j, hs[i].time, params_);
                     have[i] = 1;
-                });
-            }
+                }
+                if (!fast) return;
+                fresh[i] = index_.find(hashes[i]) == nullptr;
+                if (!have[i] || !have_mtp[i]) return;
+                AcceptResult r;
+                ctx[i] = contextual_rules(hs[i], hashes[i], last_height + 1, expected[i], mtp[i], adjusted_time, false, r)
+                             ? 1
+                             : (r.reject == "bad-diffbits" ? 2 : 0);
+            });
         }
     }
-    for (size_t i = 0; i < n; ++i) {
-        out.push_back(accept_header_impl(hs[i], hashes.empty() ? nullptr : &hashes[i], adjusted_time, check_pow,
-                                         have[i] ? &expected[i] : nullptr, pre.empty() ? nullptr : &pre[i],
-                                         proofs.empty() ? nullptr : &proofs[i], have_mtp[i] ? &mtp[i] : nullptr));
-        if (!out.back().ok) break;
+    if (ctx.empty()) {
+        for (size_t i = 0; i < n; ++i) {
+            out.push_back(accept_header_impl(hs[i], hashes.empty() ? nullptr : &hashes[i], adjusted_time, check_pow,
+                                             have[i] ? &expected[i] : nullptr, pre.empty() ? nullptr : &pre[i],
+                                             proofs.empty() ? nullptr : &proofs[i], have_mtp[i] ? &mtp[i] : nullptr));
+            if (!out.back().ok) break;
+        }
+        return out;
     }
+    // A linear batch with nothing failed in the index (every P2P `headers` message of a syncing
+    // node): one serial pass does only what needs the index -- the duplicate and -maxreorg
+    // checks, the checkpoint-fork rule, the insert (parent = the header just added, skip pointers
+    // from the batch) and the tip extension. Same results and reject reasons as
+    // accept_header_impl per header.
+    index_.reserve(index_.size() + n);
+    const int cp = params_.last_checkpoint_height();
+    std::vector<const HeaderIndex*> batch;  // batch[k]: the index entry at height base_height + 1 + k
+    batch.reserve(n);
+    out.resize(n);
+    std::vector<HeaderIndex*> nodes;
+    std::vector<ArithU256> work;
+    const HeaderIndex* prev = index_.find(hs[0].prev);
+    size_t i = 0;
+    while (i < n) {
+        // A run of new headers that pass every rule on top of the active tip becomes the tip one
+        // header after another (the -maxreorg and checkpoint-fork rules cannot fire on a header
+        // whose parent is the tip): the entries are filled on all cores, only the chain-work
+        // prefix sum, the table inserts and the active-chain append stay serial.
+        size_t m = 0;
+        if (!active_.empty() && prev == active_.back())
+            while (i + m < n && fresh[i + m] && ctx[i + m] == 1 && (pre.empty() || pre[i + m].ok) &&
+                   !(hashes[i + m] == params_.consensus.genesis_hash))
+                ++m;
+        if (m > 0) {
+            const size_t s0 = batch.size();
+            nodes.resize(m);
+            storage_.reserve_raw(m, nodes.data());
+            batch.insert(batch.end(), nodes.begin(), nodes.end());
+            work.resize(m);
+            ArithU256 w = prev->chain_work;
+            for (size_t k = 0; k < m; ++k) work[k] = w += proofs[i + k];
+            parallel_for(m, [&](size_t k) {
+                HeaderIndex& e = *new (nodes[k]) HeaderIndex();
+                const size_t j = i + k;
+                e.hash = hashes[j];
+                e.prev = k ? nodes[k - 1] : prev;
+                e.height = base_height + 1 + int(j);
+                e.time = hs[j].time;
+                e.bits = hs[j].bits;
+                e.header = hs[j];
+                e.chain_work = work[k];
+                const int sh = skip_height(e.height);
+                e.skip = sh > base_height ? batch[size_t(sh - base_height - 1)] : prev->ancestor(sh);
+                index_.insert_concurrent(&e);
+                out[j].ok = true;
+                out[j].index = &e;
+            });
+            index_.add_count(m);
+            active_.insert(active_.end(), batch.begin() + std::ptrdiff_t(s0), batch.end());
+            prev = batch.back();
+            i += m;
+            continue;
+        }
+        AcceptResult& r = out[i];
+        if (!have[i] || !have_mtp[i] || hashes[i] == params_.consensus.genesis_hash) {
+            r = accept_header_impl(hs[i], &hashes[i], adjusted_time, check_pow, have[i] ? &expected[i] : nullptr,
+                                   pre.empty() ? nullptr : &pre[i], &proofs[i], have_mtp[i] ? &mtp[i] : nullptr);
+            if (!r.ok) break;
+            batch.push_back(prev = r.index);
+            ++i;
+            continue;
+        }
+        if (!fresh[i]) {  // already indexed (failed_ is empty: never "duplicate")
+            r.ok = r.duplicate = true;
+            r.index = prev = index_.find(hashes[i]);
+            batch.push_back(prev);
+            ++i;
+            continue;
+        }
+        const int height = base_height + 1 + int(i);
+        if (!pre.empty() && !pre[i].ok) {
+            r = pre[i];
+        } else if (max_reorg_depth > 0 && int(active_.size()) - 1 - (height - 1) >= max_reorg_depth) {
+            r.reject = "bad-fork-prior-to-maxreorgdepth";
+            r.dos = 10;
+        } else if (ctx[i] != 1) {
+            const bool cp_fork = ctx[i] == 0 && cp >= 0 && height < cp && size_t(cp) < active_.size();
+            contextual_rules(hs[i], hashes[i], height, expected[i], mtp[i], adjusted_time, cp_fork, r);
+        } else if (cp >= 0 && height < cp && size_t(cp) < active_.size()) {
+            r.reject = "bad-fork-prior-to-checkpoint";
+            r.dos = 100;
+        } else {  // passes, but off the active tip (a fork): the general insert
+            const HeaderIndex* idx = add_to_index(hs[i], hashes[i], prev, &proofs[i], &batch);
+            consider_new_header(idx);
+            r.ok = true;
+            r.index = prev = idx;
+            batch.push_back(idx);
+            ++i;
+            continue;
+        }
+        r.ok = false;
+        break;
+    }
+    out.resize(std::min(n, i + 1));  // up to and including the first failure
     return out;
 }
 
 // Full recompute (after invalidate / reconsider): one pass in height order marks every
 // descendant of a failed header bad, then the most-work good header becomes the tip. O(n).
 void HeaderChain::update_active_chain() {
+    // in arrival order, so among equal-work tips the first one received wins (nSequenceId)
     std::vector<const HeaderIndex*> nodes;
-    nodes.reserve(index_.size());
-    for (auto& kv : index_) nodes.push_back(kv.second);
-    std::sort(nodes.begin(), nodes.end(),
-              [](const HeaderIndex* a, const HeaderIndex* b) { return a->height < b->height; });
+    nodes.reserve(storage_.size());
+    storage_.for_each([&](const HeaderIndex* e) { nodes.push_back(e); });
+    std::stable_sort(nodes.begin(), nodes.end(),
+                     [](const HeaderIndex* a, const HeaderIndex* b) { return a->height < b->height; });
     std::unordered_set<const HeaderIndex*> bad;
     const HeaderIndex* best = genesis_;
     for (const HeaderIndex* c : nodes) {
@@ -424,24 +558,22 @@ const HeaderIndex* HeaderChain::at_height(int h) const {
 
 const HeaderIndex* HeaderChain::find(const Uint256& hash) const {
     std::lock_guard<std::recursive_mutex> g(mu_);
-    auto it = index_.find(hash);
-    return it == index_.end() ? nullptr : it->second;
+    return index_.find(hash);
 }
 
 void HeaderChain::invalidate(const Uint256& hash) {
     std::lock_guard<std::recursive_mutex> g(mu_);
-    auto it = index_.find(hash);
-    if (it == index_.end() || it->second == genesis_) return;
-    failed_[it->second] = true;
+    const HeaderIndex* e = index_.find(hash);
+    if (e == nullptr || e == genesis_) return;
+    failed_[e] = true;
     update_active_chain();
 }
 
 void HeaderChain::reconsider(const Uint256& hash) {
     std::lock_guard<std::recursive_mutex> g(mu_);
-    auto it = index_.find(hash);
-    if (it == index_.end()) return;
+    const HeaderIndex* node = index_.find(hash);
+    if (node == nullptr) return;
     // ResetBlockFailureFlags: the block, its descendants and its ancestors become valid again
-    const HeaderIndex* node = it->second;
     auto walk = [](const HeaderIndex* x, int height) {
         while (x && x->height > height) x = x->prev;
         return x;

@@ -15,6 +15,8 @@
 
 #include <deque>
 #include <functional>
+#include <memory>
+#include <new>
 #include <mutex>
 #include <unordered_map>
 
@@ -47,6 +49,107 @@ struct AcceptResult {
     std::string reject;  // reference reject reason ("high-hash", "bad-diffbits", ...)
     int dos = 0;
     const HeaderIndex* index = nullptr;
+};
+
+// Index entries live in fixed 1024-entry chunks: stable addresses, one allocation per chunk
+// instead of one per header. A batch takes its entries' storage in one call and constructs them
+// in parallel (the first touch of fresh pages is then spread over the cores too).
+class HeaderArena {
+public:
+    static constexpr size_t kChunk = 1024;
+    HeaderArena() = default;
+    HeaderArena(const HeaderArena&) = delete;
+    HeaderArena& operator=(const HeaderArena&) = delete;
+    ~HeaderArena() {
+        for (size_t i = 0; i < used_; ++i) at(i)->~HeaderIndex();
+        for (void* c : chunks_) ::operator delete(c);
+    }
+    HeaderIndex* alloc() {
+        HeaderIndex* e = nullptr;
+        reserve_raw(1, &e);
+        return new (e) HeaderIndex();
+    }
+    // storage for n entries (not constructed: the caller placement-news every one of them
+    // before anything else reads the arena)
+    void reserve_raw(size_t n, HeaderIndex** out) {
+        for (size_t k = 0; k < n; ++k, ++used_) {
+            if (used_ == chunks_.size() * kChunk) chunks_.push_back(::operator new(kChunk * sizeof(HeaderIndex)));
+            out[k] = at(used_);
+        }
+    }
+    size_t size() const { return used_; }
+    template <class F>
+    void for_each(F&& f) const {  // allocation order
+        for (size_t i = 0; i < used_; ++i) f(at(i));
+    }
+
+private:
+    HeaderIndex* at(size_t i) const { return static_cast<HeaderIndex*>(chunks_[i / kChunk]) + i % kChunk; }
+    std::vector<void*> chunks_;
+    size_t used_ = 0;
+};
+
+// The block index (mapBlockIndex): an open-addressing table of entries keyed by their own
+// block hash. No per-entry allocation and one probe sequence per lookup; entries are never
+// removed (an invalid header stays indexed and is marked failed). Lookups are safe from many
+// threads while nothing inserts.
+class HeaderHashTable {
+public:
+    HeaderIndex* find(const Uint256& h) const {
+        if (slots_.empty()) return nullptr;
+        for (size_t i = slot(h);; i = (i + 1) & mask_) {
+            HeaderIndex* e = slots_[i];
+            if (e == nullptr || e->hash == h) return e;
+        }
+    }
+    void insert(HeaderIndex* e) {  // e->hash must not be present
+        if ((n_ + 1) * 2 > slots_.size()) grow(std::max<size_t>(64, slots_.size() * 2));
+        size_t i = slot(e->hash);
+        while (slots_[i]) i = (i + 1) & mask_;
+        slots_[i] = e;
+        ++n_;
+    }
+    // Inserts from many threads at once into a table reserve()d for them (claims empty slots
+    // with a compare-and-swap; nothing reads the table meanwhile). The caller adds the count.
+    void insert_concurrent(HeaderIndex* e) {
+        size_t i = slot(e->hash);
+        for (;; i = (i + 1) & mask_) {
+            HeaderIndex* expect = nullptr;
+            if (__atomic_compare_exchange_n(&slots_[i], &expect, e, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return;
+        }
+    }
+    void add_count(size_t k) { n_ += k; }
+    void reserve(size_t n) {
+        size_t cap = 64;
+        while (cap < 2 * n) cap *= 2;
+        if (cap > slots_.size()) grow(cap);
+    }
+    size_t size() const { return n_; }
+    template <class F>
+    void for_each(F&& f) const {
+        for (HeaderIndex* e : slots_)
+            if (e) f(e);
+    }
+
+private:
+    size_t slot(const Uint256& h) const {
+        u64 x;
+        std::memcpy(&x, h.data, 8);
+        return size_t((x * 0x9E3779B97F4A7C15ull) >> shift_);
+    }
+    void grow(size_t cap) {
+        std::vector<HeaderIndex*> old;
+        old.swap(slots_);
+        slots_.assign(cap, nullptr);
+        mask_ = cap - 1;
+        shift_ = 64 - unsigned(__builtin_ctzll(cap));
+        n_ = 0;
+        for (HeaderIndex* e : old)
+            if (e) insert(e);
+    }
+    std::vector<HeaderIndex*> slots_;
+    size_t n_ = 0, mask_ = 0;
+    unsigned shift_ = 64;
 };
 
 class HeaderChain {
@@ -104,8 +207,12 @@ private:
     AcceptResult accept_header_impl(const BlockHeader& h, const Uint256* known_hash, int64_t adjusted_time,
                                     bool check_pow, const u32* expected_bits, const AcceptResult* precheck, const ArithU256* proof = nullptr,
                                     const int64_t* prev_mtp = nullptr);
+    // `batch`: the entries a linear batch added so far (batch[k] at height batch[0]->height + k)
     const HeaderIndex* add_to_index(const BlockHeader& h, const Uint256& hash, const HeaderIndex* prev,
-                                    const ArithU256* proof = nullptr);
+                                    const ArithU256* proof = nullptr,
+                                    const std::vector<const HeaderIndex*>* batch = nullptr);
+    bool contextual_rules(const BlockHeader& h, const Uint256& hash, int height, u32 expected_bits, int64_t prev_mtp,
+                          int64_t adjusted_time, bool cp_fork, AcceptResult& r) const;
     void update_active_chain();
     void set_active_tip(const HeaderIndex* best);
     void consider_new_header(const HeaderIndex* idx);
@@ -113,8 +220,8 @@ private:
     ChainParams params_;
     std::shared_ptr<const PowVerifier> verifier_;
     mutable std::recursive_mutex mu_;
-    std::deque<HeaderIndex> storage_;
-    std::unordered_map<Uint256, HeaderIndex*, Uint256Hasher> index_;
+    HeaderArena storage_;
+    HeaderHashTable index_;
     std::unordered_map<const HeaderIndex*, bool> failed_;
     std::vector<const HeaderIndex*> active_;
     const HeaderIndex* genesis_ = nullptr;

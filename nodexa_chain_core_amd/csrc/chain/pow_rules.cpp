@@ -175,7 +175,26 @@ ArithU256 block_proof(u32 bits) {
     target.set_compact(bits, &negative, &overflow);
     if (negative || overflow || target.is_zero()) return ArithU256();
     // 2**256 / (target+1) == ~target / (target+1) + 1
-    return (~target / (target + ArithU256(1))) + ArithU256(1);
+    const ArithU256 num = ~target, d = target + ArithU256(1);
+    const unsigned L = d.bits();
+    if (L < 193) return (num / d) + ArithU256(1);
+    // Every real target is >= 2^192, so the quotient fits in 64 bits: estimate it from the top
+    // 64 bits of d (rounded up, so the estimate never exceeds the quotient and d * q cannot
+    // wrap) and the matching top bits of the numerator (< 2^128), then correct upward by the
+    // remainder. The estimate is at most a few units low, so this is exact in a few steps --
+    // much cheaper than the bit-serial long division (block proofs are computed for every
+    // header of every batch).
+    const unsigned s = L - 64;
+    const ArithU256 nh = num >> s;
+    const unsigned __int128 top = (static_cast<unsigned __int128>((nh >> 64).low64()) << 64) | nh.low64();
+    const unsigned __int128 q128 = top / (static_cast<unsigned __int128>((d >> s).low64()) + 1);
+    u64 q = u64(q128);
+    ArithU256 rem = num - (d * u32(q) + ((d * u32(q >> 32)) << 32));
+    while (rem >= d) {
+        rem -= d;
+        ++q;
+    }
+    return ArithU256(q) + ArithU256(1);
 }
 
 Amount block_subsidy(int height) {

@@ -530,6 +530,10 @@ class ChainLeader:
                 if not res.ok:
                     self.stats["rejected"] += 1
                     log.log_printf(f"miner: block of job {rec.job_id} rejected: {res.reject}")
+                    if req.blocks is not None:  # generateBlocks: "ProcessNewBlock, block not accepted"
+                        req.error = f"ProcessNewBlock, block not accepted: {res.reject}"
+                        req.done.set()
+                        break
                     continue
                 bh = st.block_hash(blk.header)
                 self.stats["blocks"] += 1

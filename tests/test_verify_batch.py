@@ -228,3 +228,86 @@ def test_header_batch_rows_and_accept_batch(core):
     assert c.tip().hash == ref.tip().hash
     with pytest.raises(Exception):
         core.HeaderBatch.from_bytes(raw[:-7], act)  # truncated
+
+
+def _serial(params, headers, adj, check_pow=False, chain=None):
+    c = chain or _core.HeaderChain(params)
+    out = []
+    for h in headers:
+        r = c.accept_header(h, adj, check_pow)
+        out.append((r.ok, r.reject, r.dos, r.duplicate))
+        if not r.ok:
+            break
+    return c, out
+
+
+def _results(rs):
+    return [(r.ok, r.reject, r.dos, r.duplicate) for r in rs]
+
+
+def _same_chain(a, b):
+    assert a.height() == b.height() and a.size() == b.size()
+    assert a.tip().hash == b.tip().hash and a.tip().chain_work == b.tip().chain_work
+    for h in range(0, a.height() + 1, 97):  # skip pointers: ancestor walks agree everywhere
+        x, y = a.at_height(h), b.at_height(h)
+        assert x.hash == y.hash and x.skip_height == y.skip_height
+        assert a.tip().ancestor(h).hash == x.hash
+
+
+def test_accept_headers_fast_path_equals_serial(chain_fixture):
+    """The linear-batch path of accept_headers (contextual rules on all cores, runs of new headers
+    on top of the tip inserted in bulk) against header-by-header acceptance: the same results,
+    reject reasons, DoS scores, duplicate flags and chain -- for a batch that overlaps headers
+    already indexed, one that forks below the tip, and a corrupted header at random positions."""
+    import random
+
+    params, headers = chain_fixture
+    act = params.kawpow_activation_time
+    adj = headers[-1].time + 3600
+    hs = list(headers[:4000])
+    rng = random.Random(11)
+    cases = [("clean", hs, 0)]
+    for kind in ("bits", "time-old", "time-new", "version", "mix-pow"):
+        pos = rng.randrange(200, len(hs))
+        bad = list(hs)
+        h = _copy(hs[pos], act)
+        if kind == "bits":
+            h.bits ^= 1
+        elif kind == "time-old":
+            h.time = hs[pos - 6].time - 1
+        elif kind == "time-new":
+            h.time = adj + 3 * 3600
+        elif kind == "version":
+            h.version = 0x20000000
+        else:
+            h.mix_hash = bytes(32)
+        bad[pos] = h
+        cases.append((kind, bad[: pos + 1 + rng.randrange(0, 50)], 0))
+    cases.append(("overlap", hs, 1500))  # the first 1500 are indexed before the batch arrives
+    for name, batch, pre in cases:
+        for check_pow in (False, True) if name == "mix-pow" else (False,):
+            a, b = _core.HeaderChain(params), _core.HeaderChain(params)
+            if pre:
+                assert all(r.ok for r in a.accept_headers(batch[:pre], adj, False))
+                _serial(params, batch[:pre], adj, chain=b)
+            ra = _results(a.accept_headers(batch, adj, check_pow))
+            _, rb = _serial(params, batch, adj, check_pow, chain=b)
+            assert ra == rb, (name, check_pow, ra[-1], rb[-1], len(ra), len(rb))
+            _same_chain(a, b)
+    # a batch that forks below the active tip: a side branch with less work, then more work
+    a, b = _core.HeaderChain(params), _core.HeaderChain(params)
+    assert all(r.ok for r in a.accept_headers(hs[:3000], adj, False))
+    _serial(params, hs[:3000], adj, chain=b)
+    fork = []
+    for i in range(2500, 2500 + 700):
+        h = _copy(hs[i], act)
+        if i == 2500:
+            h.nonce64 ^= 1
+        else:
+            h.prev = a.block_hash(fork[-1]) if fork else h.prev
+        fork.append(h)
+    ra = _results(a.accept_headers(fork, adj, False))
+    _, rb = _serial(params, fork, adj, chain=b)
+    assert ra == rb and all(r[0] for r in ra) and a.tip().hash == b.tip().hash
+    assert a.tip().hash == a.block_hash(fork[-1]) and a.height() == hs[2500].height + 699
+    _same_chain(a, b)
