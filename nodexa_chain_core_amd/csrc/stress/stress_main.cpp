@@ -127,6 +127,43 @@ static void stress_headerchain() {
     CHECK(chain.height() == 400);
 }
 
+// accept_headers' linear-batch path on a DGW network: contextual rules on the pool, a run on top
+// of the tip built on the pool (entries constructed and inserted into the block-index table
+// concurrently), then header-by-header for the part that forks.
+static void stress_headerchain_batch() {
+    ChainParams p = make_chain_params("test");
+    p.kawpow_activation_time = p.genesis.header.time;
+    auto verifier = std::make_shared<CpuPowVerifier>();
+    HeaderChain scratch(p, verifier);
+    std::vector<BlockHeader> hs;
+    const HeaderIndex* prev = scratch.tip();
+    u32 t = p.genesis.header.time;
+    for (int h = 1; h <= 1500; ++h) {
+        BlockHeader b;
+        b.version = 0x30000000;
+        b.prev = prev->hash;
+        b.merkle_root.data[0] = u8(h);
+        b.merkle_root.data[1] = u8(h >> 8);
+        t += 50 + (h * 7) % 40;
+        b.time = t;
+        b.height = u32(h);
+        b.bits = scratch.next_bits(b);
+        AcceptResult r = scratch.accept_header(b, t + 10, false);
+        CHECK(r.ok);
+        if (!r.ok) return;
+        prev = r.index;
+        hs.push_back(b);
+    }
+    for (int round = 0; round < 3; ++round) {
+        HeaderChain chain(p, verifier);
+        const auto r = chain.accept_headers(hs.data(), hs.size(), int64_t(t) + 10, false, nullptr, nullptr);
+        CHECK(r.size() == hs.size() && r.back().ok);
+        CHECK(chain.height() == 1500 && chain.tip()->hash == scratch.tip()->hash);
+        CHECK(chain.tip()->chain_work == scratch.tip()->chain_work);
+        for (int h = 0; h <= 1500; h += 37) CHECK(chain.tip()->ancestor(h) == chain.at_height(h));
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string dir = argc > 1 ? argv[1] : "/tmp";
     const bool quick = argc > 2 && std::string(argv[2]) == "--quick";  // one epoch (CI)
@@ -135,6 +172,7 @@ int main(int argc, char** argv) {
     stress_hostdag();
     stress_x16r();
     stress_headerchain();
+    stress_headerchain_batch();
     std::printf("stress: %s (%d failed checks)\n", g_fail.load() ? "FAIL" : "ok", g_fail.load());
     return g_fail.load() ? 1 : 0;
 }

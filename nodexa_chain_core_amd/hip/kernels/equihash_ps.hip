@@ -61,6 +61,18 @@
 #define EQP_NP 448  // producer threads of a round workgroup (7 of its 16 waves)
 #endif
 
+// Instance and writer of this workgroup in a (writers x instances) grid. Workgroups are dispatched
+// to the 8 XCDs round-robin by linear id, so blockIdx.y = instance spreads every instance over all
+// XCDs; EQP_XCD_LOCAL (measured variant) takes instance = id mod instances instead, which keeps
+// an instance's writers -- and the rows of its buckets -- on one XCD's L2.
+#ifdef EQP_XCD_LOCAL
+#define EQP_INST_GRP(inst, grp)                                           \
+    const uint32_t eqp_lin_ = blockIdx.x + blockIdx.y * gridDim.x;        \
+    const uint32_t inst = eqp_lin_ % gridDim.y, grp = eqp_lin_ / gridDim.y
+#else
+#define EQP_INST_GRP(inst, grp) const uint32_t inst = blockIdx.y, grp = blockIdx.x
+#endif
+
 // Payload words of a level-`level` row: 6, 6, 5, 4, 4, 3, 3, 2, 1.
 constexpr int eqp_payload(int level) { return (188 - 20 * level + 31) / 32; }
 // Words per row slot in global memory: the payload plus the back-pointer, except that a 28-byte
@@ -97,9 +109,9 @@ NX_DEV void eqp_clear_counts(uint32_t* cnt2) {
 
 // This workgroup's 4096 segment fills of `level`, clamped to C, as one coalesced u8 row.
 // `dropped` (this thread's staging overflow) plus the segment overflow go to p.stats.
-NX_DEV void eqp_flush_counts(const EquihashPsDev& p, uint32_t inst, int level, const uint32_t* cnt2,
+NX_DEV void eqp_flush_counts(const EquihashPsDev& p, uint32_t inst, uint32_t grp, int level, const uint32_t* cnt2,
                              uint32_t dropped) {
-    uint32_t* out = (uint32_t*)(p.counts + (((size_t)inst * EQ_LEVELS + level) * p.groups + blockIdx.x) * EQ_BUCKETS);
+    uint32_t* out = (uint32_t*)(p.counts + (((size_t)inst * EQ_LEVELS + level) * p.groups + grp) * EQ_BUCKETS);
     for (uint32_t k = threadIdx.x; k < EQ_BUCKETS / 4; k += EQP_BLOCK) {
         const uint32_t a = cnt2[2 * k], b = cnt2[2 * k + 1];
         const uint32_t c[4] = {a & 0xFFFFu, a >> 16, b & 0xFFFFu, b >> 16};
@@ -119,7 +131,7 @@ NX_DEV void eqp_flush_counts(const EquihashPsDev& p, uint32_t inst, int level, c
 // this workgroup's segment of their level-0 bucket (word 0 = leaf index).
 extern "C" __global__ __launch_bounds__(EQP_BLOCK) void eqp_gen(EquihashPsDev p) {
     __shared__ uint32_t cnt2[EQ_BUCKETS / 2];
-    const uint32_t inst = blockIdx.y, grp = blockIdx.x;
+    EQP_INST_GRP(inst, grp);
     eqp_clear_counts(cnt2);
     __syncthreads();
     const uint32_t per = (1u << 20) / p.groups;
@@ -145,7 +157,7 @@ extern "C" __global__ __launch_bounds__(EQP_BLOCK) void eqp_gen(EquihashPsDev p)
         }
     }
     __syncthreads();
-    eqp_flush_counts(p, inst, 0, cnt2, 0);
+    eqp_flush_counts(p, inst, grp, 0, cnt2, 0);
 }
 
 // Counts of bucket b of `level` into lane registers of the calling wave (lane l holds the counts
@@ -238,7 +250,8 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     __shared__ uint32_t nstaged[2];
     // P = writers per level (the counts layout); the workgroups stride over the buckets by the
     // grid width, which is P for rounds 1..8 (workgroup = writer) and wider for the final round
-    const uint32_t inst = blockIdx.y, grp = blockIdx.x, P = p.groups, G = gridDim.x;
+    EQP_INST_GRP(inst, grp);
+    const uint32_t P = p.groups, G = gridDim.x;
     const bool producer = threadIdx.x < NP;
     const uint32_t ct = threadIdx.x - NP;
     uint32_t* my_segc = segc[threadIdx.x / 64 % (NP / 64)];
@@ -328,7 +341,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     // rows beyond a segment) are counted apart
     if (dropped) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_STAGE], dropped);
     if (threadIdx.x == 0) atomicMax(&p.stats[inst * EQP_STATS + EQP_STAT_STAGE_MAX], staged_max);
-    if constexpr (R < 9) eqp_flush_counts(p, inst, R, cnt2, 0);
+    if constexpr (R < 9) eqp_flush_counts(p, inst, grp, R, cnt2, 0);
     if (truncated) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_CHAIN], truncated);
 }
 
