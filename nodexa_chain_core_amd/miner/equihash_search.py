@@ -45,6 +45,7 @@ def _passing(work: Work, start: int, per_nonce: list[list[bytes]]) -> tuple[list
 
 class EquihashGpuDevice:
     name = "gpu-equihash"
+    algo = ALGO_EQUIHASH
 
     def __init__(self, device: int = 0, num_inst: int = 16):
         import torch
@@ -112,6 +113,7 @@ class EquihashCpuDevice:
     """The host golden solver, `count` nonces per window (1 by default)."""
 
     name = "cpu-equihash"
+    algo = ALGO_EQUIHASH
     device = -1
 
     def __init__(self, window: int = 1):

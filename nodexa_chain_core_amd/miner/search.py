@@ -510,7 +510,41 @@ class RankDevice:
 
 
 def as_rank_device(dev) -> RankDevice:
-    return dev if isinstance(dev, (RankDevice, FaultInjectingDevice, HangingDevice)) else RankDevice(dev)
+    """A bare device becomes a rank's device for its own algorithm: an Equihash device serves the
+    Equihash windows (a KawPow or X16R packet would find no device of its kind and fail), any
+    other device the KawPow ones."""
+    if isinstance(dev, (RankDevice, FaultInjectingDevice, HangingDevice)):
+        return dev
+    if getattr(dev, "algo", None) == ALGO_EQUIHASH:
+        return RankDevice(_NoKawpow(dev), equihash=dev)
+    return RankDevice(dev)
+
+
+class _NoKawpow:
+    """The KawPow slot of a rank that only has an Equihash device (bench.py's Equihash loop)."""
+
+    def __init__(self, eq):
+        self.name, self.device = eq.name, eq.device
+
+    def window_for(self, work, window):
+        raise DeviceFault("this rank has no KawPow device")
+
+    submit = block_for = window_for
+
+    def epoch_ready(self, epoch: int) -> bool:
+        return True
+
+    def resident_epochs(self) -> list[int]:
+        return []
+
+    def prebuild(self, epoch: int) -> None:
+        pass
+
+    def abort(self) -> None:
+        pass
+
+    def synchronize(self) -> None:
+        pass
 
 
 class SearchPipeline:

@@ -107,3 +107,19 @@ def test_remote_miner_mines_equihash(core, node_factory):  # noqa: F811
     hdr = core.Block.deserialize(bytes.fromhex(c.getblock(c.getbestblockhash(), 0)),
                                  node.params.kawpow_activation_time).header
     assert hdr.is_equihash() and int.from_bytes(hdr.nonce256[:8], "little") >> 56 == 1  # rank 1's nonce range
+
+
+def test_bare_equihash_device_serves_equihash_windows(core):
+    """A MiningService built on a bare Equihash device (bench.py's Equihash loop) sends the Equihash
+    windows to THAT device -- not to a host golden solver made on first use -- and a KawPow packet
+    on such a rank is a device fault, not a silent CPU search."""
+    from nodexa_chain_core_amd.miner.equihash_search import EquihashCpuDevice
+    from nodexa_chain_core_amd.miner.search import ALGO_EQUIHASH, ALGO_KAWPOW, DeviceFault, Work, as_rank_device
+
+    dev = EquihashCpuDevice(window=3)
+    rd = as_rank_device(dev)
+    eq = Work(bytes(80), b"\xff" * 32, 1, 1, 0, 0, ALGO_EQUIHASH)
+    assert rd.equihash is dev and rd.dev_for(eq) is dev and rd.window_for(eq, 16) == 3
+    assert rd.name == dev.name and rd.resident_epochs() == []
+    with pytest.raises(DeviceFault):
+        rd.window_for(Work(bytes(32), b"\xff" * 32, 1, 1, 0, 0, ALGO_KAWPOW), 16)
