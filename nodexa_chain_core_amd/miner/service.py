@@ -181,7 +181,10 @@ class Comm:
             self.torch = torch
             dist = self.W.dist
             if self.gpu:
-                self.stream = torch.cuda.Stream(device=self.w.device)
+                # the highest priority: its copies must not share a hardware queue with the search
+                # stream, where they would wait behind the window queued for the next step and
+                # drain the two-window pipeline every step (profiles/README r4b)
+                self.stream = torch.cuda.Stream(device=self.w.device, priority=-16)
             if self.group is None:
                 self.group = dist.new_group(ranks=list(range(self.w.world_size)), timeout=self.timeout)
 

@@ -86,6 +86,11 @@ def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | 
             # a collective that times out must raise to the caller (which aborts the communicator
             # and re-forms the group over the survivors), not make RCCL's watchdog end the process
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
+        if backend == "nccl":
+            # RCCL's internal streams at high priority: with 4 hardware queues per process, a
+            # normal-priority stream can share a queue with the search stream, and a collective
+            # queued there waits behind the ~117 ms search window already queued (profiles r4b)
+            os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
         kw = {}
         if use_gpu:
             kw["device_id"] = device
