@@ -22,13 +22,14 @@
 //       - a 5-op Barrett modulo for the item index,
 //       - raw-buffer DAG loads with a 32-bit byte offset,
 //       - the L1 replicated 4x in LDS so each of the 11 cache lookups needs a
-//         single v_lshlrev_b16 for its address (512-thread workgroups keep 4
-//         waves/SIMD within the 160 KiB LDS).
+//         single v_lshlrev_b16 for its address (two 768-thread workgroups, 6
+//         waves/SIMD, within the 160 KiB LDS).
 //   * the mix registers are arrays subscripted only by literals (the emitted
 //     program bakes every index in), so they are scalarised into VGPRs.
-//   * everything not needed inside the round loop leaves the VGPR file: the 8
-//     digest words go to LDS as each hash finishes, and the keccak state words
-//     2..7 are recomputed for the final absorb instead of being held live.
+//   * everything not needed inside the round loop leaves the VGPR file: each
+//     hash's 8 digest words are parked in the 8 VGPRs of the lane that owns it,
+//     and the keccak state words 2..7 are recomputed for the final absorb
+//     instead of being held live.
 //   * each round's 256-byte DAG item is one coalesced 16 B/lane load by the
 //     group (lane l takes words ((l^r)%16)*4..+3).
 #include "kernel_params.h"
@@ -72,10 +73,10 @@
 //   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride), DAG < 4 GiB only
 //   KP_L1X4       L1 replicated 4x in LDS (64 KiB) so an L1 address is one
 //                 16-bit shift: ((x << 2) & 0xffff) reads l1[x % 4096]
-//   KP_DIGEST_REG each finished hash's 8 digest words go straight to the lane that
-//                 owns the hash's nonce (8 DPP broadcasts + 8 selects per hash, 8 VGPRs)
-//                 instead of a 32 B/nonce LDS buffer: the workgroup's LDS is then only
-//                 the L1 table, so 1024-thread groups fit twice per CU (8 waves/SIMD)
+// Digests: each finished hash's 8 digest words go straight to the lane that owns the hash's
+// nonce (8 DPP broadcasts + 8 selects per hash, 8 VGPRs), so the workgroup's LDS is only the L1
+// table and two 768-thread groups share a CU. (The 32 B/nonce LDS-digest form measured equal on
+// the >4 GiB pointer path, 269.8 vs 269.3 MH/s at epoch 390, profiles r4b, and was removed.)
 #ifndef KP_BLOCK
 #define KP_BLOCK NODEXA_KAWPOW_BLOCK
 #endif
@@ -240,7 +241,7 @@ NX_DEV void kp_final(const uint32_t st2[8], const uint32_t digest[8], uint32_t o
 
 // The group's 16 hashes, KP_HASHES at a time. `st0/st1` are this thread's own
 // nonce seed words (hash h's seed lives in lane h). Each finished hash's 8
-// digest words are written to dig[h * 8 + k] (LDS, this group's 128 words).
+// digest words go to `own` of the lane that owns the hash (8 DPP broadcasts).
 // One ProgPoW round with the round index known mod 16 (J): the item index comes
 // from lane J of the row via DPP and the lane's 16-byte slice is lane ^ J.
 template <int J>
@@ -266,8 +267,7 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag, const FastMo
 }
 
 NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
-                            uint32_t st0, uint32_t st1, uint32_t lane, uint32_t* dig,
-                            uint32_t (&own)[8]) {
+                            uint32_t st0, uint32_t st1, uint32_t lane, uint32_t (&own)[8]) {
 #pragma unroll 1
     for (uint32_t h0 = 0; h0 < 16; h0 += KP_HASHES) {
         uint32_t mx[KP_HASHES][32];
@@ -301,7 +301,6 @@ NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t
             for (int i = 0; i < 32; ++i) lh = kp_fnv1a(lh, mx[k][i]);
             // digest[j] = fnv1a(fnv1a(basis, lane_hash[j]), lane_hash[j + 8]); lanes 0..7 own j
             const uint32_t hi = __shfl(lh, (int)(lane + 8), 16);
-#ifdef KP_DIGEST_REG
             // lanes 0..7 hold the digest words; lane h0+k keeps all 8 of them
             const uint32_t word = kp_fnv1a(kp_fnv1a(0x811c9dc5u, lh), hi);
             const bool mine = lane == h0 + (uint32_t)k;
@@ -317,31 +316,14 @@ NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t
             own[5] = mine ? b5 : own[5];
             own[6] = mine ? b6 : own[6];
             own[7] = mine ? b7 : own[7];
-            (void)dig;
-#else
-            if (lane < 8) dig[(h0 + k) * 8 + lane] = kp_fnv1a(kp_fnv1a(0x811c9dc5u, lh), hi);
-            (void)own;
-#endif
         }
     }
 }
 
 extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     __shared__ uint32_t l1[KP_L1_WORDS];
-#if defined(KP_DIGEST_REG)
-    uint32_t* digs = nullptr;
-#else
-    __shared__ uint32_t digs[KP_BLOCK * 8];
-#endif
-#if defined(KP_DIGEST_REG)
     __shared__ uint32_t stale_word;
     uint32_t* stale = &stale_word;
-#else
-    // the LDS-digest form is at 80 KiB per workgroup, two per CU: a separate flag word would push
-    // it past the 160 KiB and halve the occupancy, so the flag borrows the digest buffer's first
-    // word (digests land there only after the second barrier below)
-    uint32_t* stale = digs;
-#endif
     if (blockDim.x != KP_BLOCK) return;  // launched with the wrong block: no shares rather than bad ones
     if (threadIdx.x == 0) {
         // one uncached read of the host-mapped generation word per workgroup, overlapped with the
@@ -354,26 +336,16 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     kp_fill_l1(l1, p.dag);
     __syncthreads();
     const uint32_t is_stale = *stale;
-#if !defined(KP_DIGEST_REG)
-    __syncthreads();  // every wave has read the flag before a digest can overwrite it
-#endif
     if (is_stale) return;  // uniform over the workgroup
 
     const uint32_t lane = threadIdx.x & 15;
     const uint64_t nonce = p.start_nonce + (uint64_t)blockIdx.x * KP_BLOCK + threadIdx.x;
-    uint32_t* dig = digs ? digs + (threadIdx.x & ~15u) * 8 : nullptr;
     uint32_t digest[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     {
         uint32_t st2[8];
         kp_seed(p.header, nonce, st2);
-        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig, digest);
+        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, digest);
     }
-#ifndef KP_DIGEST_REG
-    __threadfence_block();  // digest words written by lanes 0..7 are read by lane h below
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) digest[k] = dig[lane * 8 + k];
-#endif
     uint32_t st2[8], fin[8];
     // recomputed: cheaper than 6 VGPRs held across the mix loop. The nonce goes through an empty
     // asm so the compiler cannot CSE this keccak with the first one (it would keep those results
@@ -401,11 +373,6 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
 // all share this period and epoch. One job per thread, grouped as in search.
 extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     __shared__ uint32_t l1[KP_L1_WORDS];
-#ifdef KP_DIGEST_REG
-    uint32_t* digs = nullptr;
-#else
-    __shared__ uint32_t digs[KP_BLOCK * 8];
-#endif
     if (blockDim.x != KP_BLOCK) return;
     kp_fill_l1(l1, p.dag);
     __syncthreads();
@@ -413,15 +380,9 @@ extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     const uint32_t job = blockIdx.x * KP_BLOCK + threadIdx.x;
     const bool valid = job < p.num_jobs;
     const KawpowVerifyJob j = p.jobs[valid ? job : 0];
-    uint32_t* dig = digs ? digs + (threadIdx.x & ~15u) * 8 : nullptr;
     uint32_t st2[8], digest[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fin[8];
     kp_seed(j.header, j.nonce, st2);
-    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, dig, digest);
-#ifndef KP_DIGEST_REG
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) digest[k] = dig[lane * 8 + k];
-#endif
+    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, digest);
     kp_final(st2, digest, fin);
     if (valid) {
         uint32_t* o = p.out + (size_t)job * 16;

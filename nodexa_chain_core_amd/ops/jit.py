@@ -82,7 +82,7 @@ def _atomic_copy(src: str, dst: str) -> None:
 
 # Tuned variant of the search template (profiles/README.md has the sweep that
 # picked it); NODEXA_KAWPOW_DEFINES="A,B=1" overrides it ("none" = plain template).
-# r2l / r2m: digests held in registers (KP_DIGEST_REG) leave only the 64 KiB L1 table in LDS, so
+# r2l / r2m: digests held in registers (the only digest form since r4b) leave only the 64 KiB L1 table in LDS, so
 # two 768-thread workgroups share a CU (6 waves/SIMD instead of 4): +0.7 / +0.8 % in two
 # interleaved sweeps; 640 / 896 threads (waves uneven across the 4 SIMDs) and 1024 (64 VGPRs,
 # heavy spills) lose.
@@ -90,7 +90,7 @@ def _atomic_copy(src: str, dst: str) -> None:
 # DAG merge, and with it the wait for the round's HBM gather, at the end of the round: +3.2 / +3.6 %
 # in two interleaved 7-round sweeps (profiles/r3b_r3c_sched_fence).
 TUNED_DEFINES: tuple[str, ...] = ("KP_HASHES=1", "KP_DPP", "KP_BARRETT", "KP_SBUFFER", "KP_L1X4", "KP_BLOCK=768",
-                                  "KP_DIGEST_REG", "KP_MIN_WAVES=6", "KP_NT_DAG", "KP_SCHED_FENCE")
+                                  "KP_MIN_WAVES=6", "KP_NT_DAG", "KP_SCHED_FENCE")
 _env = os.environ.get("NODEXA_KAWPOW_DEFINES")
 DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
     d for d in _env.split(",") if d and d != "none")
@@ -99,16 +99,15 @@ DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
 def defines_for(dag_bytes: int, defines: tuple[str, ...] | None = None) -> tuple[str, ...]:
     """The variant to compile for a DAG of `dag_bytes`: KP_SBUFFER addresses the DAG with 32-bit
     buffer offsets, so it is dropped for DAGs of 4 GiB or more (epochs >= 385; measured there: the
-    structured form is not bit-exact, the pointer form is), and there the 768-thread
-    register-digest form falls back to 512 threads."""
+    structured form is not bit-exact, the pointer form is), and there the 768-thread form falls
+    back to 512 threads."""
     d = DEFAULT_DEFINES if defines is None else tuple(defines)
     if dag_bytes >= 1 << 32:  # 32-bit buffer offsets: 64-bit pointers for DAGs of 4 GiB or more
         d = tuple(x for x in d if x != "KP_SBUFFER")
         if "KP_BLOCK=768" in d:
-            # the pointer path needs more VGPRs: at 6 waves/SIMD it spills and loses 3 % to the
-            # 512-thread / 4-wave form (profiles/r2n_kawpow768, epoch 390)
-            d = tuple("KP_BLOCK=512" if x == "KP_BLOCK=768" else x for x in d
-                      if x not in ("KP_DIGEST_REG", "KP_MIN_WAVES=6"))
+            # the pointer path needs more VGPRs: at 6 waves/SIMD it spills and loses 4.5 % to the
+            # 512-thread / 4-wave form (profiles/r2n_kawpow768; r4b: 257.7 vs 269.3 MH/s, epoch 390)
+            d = tuple("KP_BLOCK=512" if x == "KP_BLOCK=768" else x for x in d if x != "KP_MIN_WAVES=6")
     return d
 
 

@@ -129,8 +129,8 @@ def test_search_variant_selection_by_dag_size(core):
     assert "KP_SBUFFER" not in big and "KP_DPP" in big
     # 768-thread register-digest form below 4 GiB, the 512-thread form on the pointer path
     small = jit.defines_for(below, jit.TUNED_DEFINES)
-    assert {"KP_BLOCK=768", "KP_DIGEST_REG", "KP_MIN_WAVES=6"} <= set(small)
-    assert "KP_BLOCK=512" in big and "KP_BLOCK=768" not in big and "KP_DIGEST_REG" not in big
+    assert {"KP_BLOCK=768", "KP_MIN_WAVES=6"} <= set(small)
+    assert "KP_BLOCK=512" in big and "KP_BLOCK=768" not in big and "KP_MIN_WAVES=6" not in big
     assert "KP_SBUFFER" not in jit.defines_for(above, ("KP_SBUFFER", "KP_DPP"))
 
 
