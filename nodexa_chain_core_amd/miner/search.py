@@ -28,6 +28,7 @@ of collectives and one failure path serve every era of the chain; `FaultInjectin
 from __future__ import annotations
 
 import hashlib
+import os
 import struct
 import threading
 import time
@@ -184,7 +185,12 @@ class GpuSearchDevice:
         self.dag_build_s: dict[int, float] = {}
         nbytes = self.h.sizeof_results()
         with torch.cuda.device(self.device):
+            # one stream per slot (NODEXA_SEARCH_STREAMS=1: both slots on one): the queued window
+            # starts on the CUs the running one's last workgroups leave idle instead of waiting
+            # for its whole grid to drain (the tail of a 2^25-nonce window is ~0.8 % of it)
             self.stream = torch.cuda.Stream(device=self.device)
+            two = os.environ.get("NODEXA_SEARCH_STREAMS", "2") != "1"
+            self.slot_streams = [self.stream, torch.cuda.Stream(device=self.device) if two else self.stream]
             self.side = torch.cuda.Stream(device=self.device)  # next-epoch DAG builds
             self.rings = [torch.zeros(nbytes // 4, dtype=torch.int32, device=self.device) for _ in range(2)]
             self.host = [torch.zeros(nbytes // 4, dtype=torch.int32).pin_memory() for _ in range(2)]
@@ -252,11 +258,13 @@ class GpuSearchDevice:
         t0 = time.perf_counter()
         if epoch in self.pending_build:
             e, ev = self.pending_build.pop(epoch)
-            self.stream.wait_event(ev)  # search kernels after the build, without a host sync
+            for st in self.slot_streams:
+                st.wait_event(ev)  # search kernels after the build, without a host sync
         else:
             e = self._build_epoch(epoch)
         with torch.cuda.device(self.device):
-            self.stream.synchronize()
+            for st in self.slot_streams:
+                st.synchronize()
             if not e.l1_matches():
                 raise RuntimeError(f"gpu{self.device}: epoch {epoch} DAG failed its L1 self-check")
         self.dag_build_s[epoch] = self.dag_build_s.get(epoch, 0.0) + time.perf_counter() - t0
@@ -294,14 +302,15 @@ class GpuSearchDevice:
         s = self.searcher(work.height)
         b = s.block
         count = max(b, count // b * b)
-        with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
+        st = self.slot_streams[slot]
+        with torch.cuda.device(self.device), torch.cuda.stream(st):
             ring = self.rings[slot]
             ring[:4].zero_()
-            self.starts[slot].record(self.stream)
-            s.launch(work.header_hash, start, count, work.target64(), stream=int(self.stream.cuda_stream),
+            self.starts[slot].record(st)
+            s.launch(work.header_hash, start, count, work.target64(), stream=int(st.cuda_stream),
                      results=ring, gen_word=self.gen_ptr, generation=self.generation)
             self.host[slot].copy_(ring, non_blocking=True)
-            self.events[slot].record(self.stream)
+            self.events[slot].record(st)
         self.meta[slot] = (work, start, count, b)
 
     def wait(self, slot: int, timeout_s: float | None = None) -> SlotResult:
@@ -329,7 +338,8 @@ class GpuSearchDevice:
         self.h.host_word_store(self.gen_ptr, 0, self.generation)
 
     def synchronize(self) -> None:
-        self.stream.synchronize()
+        for st in self.slot_streams:
+            st.synchronize()
 
 
 class CpuSearchDevice:
