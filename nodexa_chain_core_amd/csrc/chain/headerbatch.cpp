@@ -80,21 +80,24 @@ void HeaderBatch::pack() {
             std::memcpy(row + 88, h.mix_hash.data, 32);
         }
     }, 512);
-    bool uniform = true;
-    for (size_t k = 0; k < m; ++k) {  // few (an activation-era batch); serial is fine
+    // the Equihash inputs, solutions and serializations (1.5 KB each) on all cores too
+    std::vector<u8> ok(m, 1);
+    parallel_for_each(m, [&](size_t k) {
         const BlockHeader& h = hs[eq_index[k]];
         const Bytes in = h.equihash_input();
         std::memcpy(&eq_msgs[k * 128], in.data(), std::min<size_t>(in.size(), 128));
         if (h.solution.size() == 1344)
             std::memcpy(&eq_sols[k * 1344], h.solution.data(), 1344);
         else
-            uniform = false;
+            ok[k] = 0;
         const Bytes s = h.bytes(act);
         if (s.size() == eq_ser_len)
             std::memcpy(&eq_ser[k * eq_ser_len], s.data(), s.size());
         else
-            uniform = false;
-    }
+            ok[k] = 0;
+    }, 16);
+    bool uniform = true;
+    for (u8 x : ok) uniform = uniform && x;
     eq_uniform = uniform;
 }
 
