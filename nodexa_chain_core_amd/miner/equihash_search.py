@@ -6,11 +6,11 @@ SHA256d(serialized header) <= nBits target. A window of `count` nonces is `count
 instances: nonce k of the window stands for nonce256 = le64(start + k) || 0^24, so the ranks'
 64-bit nonce partition (rank << 56) carries over unchanged.
 
-* `EquihashGpuDevice`: one `ops.equihash.EquihashSolver` with `num_inst` instances per launch
-  (16: ~8.6 ms of device work, so the loop's per-step host work and collectives hide behind the
-  window that is running). The solver already keeps two launches in flight on its stream with two
-  pinned landing buffers — exactly the two slots. Every solution is verified on the device
-  (eq_verify_slots) before it is counted; the host only SHA256d's the candidate headers.
+* `EquihashGpuDevice`: one `ops.equihash.EquihashSolver` per slot with `num_inst` instances per
+  launch (16: ~8.6 ms of device work, so the loop's per-step host work and collectives hide behind
+  the window that is running), each slot on its own stream so the two windows overlap at their
+  kernel tails. Every solution is verified on the device (eq_verify_slots) before it is counted;
+  the host only SHA256d's the candidate headers.
 * `EquihashCpuDevice`: the C++ golden solver (~2.3 s per nonce on one core) for CPU-only nodes and
   the gloo rehearsals of the loop.
 
@@ -48,6 +48,8 @@ class EquihashGpuDevice:
     algo = ALGO_EQUIHASH
 
     def __init__(self, device: int = 0, num_inst: int = 16):
+        import os
+
         import torch
 
         from ..ops.equihash import EquihashSolver
@@ -55,14 +57,26 @@ class EquihashGpuDevice:
         self.torch = torch
         self.device = int(device)
         self.num_inst = int(num_inst)
+        # one solver (its own ~8.6 GB of level buffers at 16 instances) and one stream per slot
+        # (NODEXA_EQ_STREAMS=1: one of each): the queued window's kernels fill the running one's
+        # tails -- every round kernel is two partial waves of 1024-thread workgroups, and the final
+        # round, reconstruction and verdicts use a fraction of the CUs
+        two = os.environ.get("NODEXA_EQ_STREAMS", "2") != "1"
         with torch.cuda.device(self.device):
-            self.stream = torch.cuda.Stream(device=self.device)
-            with torch.cuda.stream(self.stream):
-                self.solver = EquihashSolver(num_inst=self.num_inst, device=self.device)
+            self.streams = [torch.cuda.Stream(device=self.device)]
+            self.streams.append(torch.cuda.Stream(device=self.device) if two else self.streams[0])
+            self.solvers = []
+            for k in range(2 if two else 1):
+                with torch.cuda.stream(self.streams[k]):
+                    self.solvers.append(EquihashSolver(num_inst=self.num_inst, device=self.device))
+            if not two:
+                self.solvers.append(self.solvers[0])
             self.starts = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             self.ends = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        self.stream = self.streams[0]
+        self.solver = self.solvers[0]
         self.meta: list[tuple | None] = [None, None]
-        self.order: list[int] = []  # slots in launch order (the solver collects oldest first)
+        self.order: list[int] = []  # slots in launch order (collected oldest first)
 
     def window_for(self, work: Work, window: int) -> int:
         return self.num_inst
@@ -70,10 +84,11 @@ class EquihashGpuDevice:
     def submit(self, slot: int, work: Work, start: int, count: int) -> None:
         torch = self.torch
         inputs = [work.header + equihash_nonce256(start + k) for k in range(self.num_inst)]
-        with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
-            self.starts[slot].record(self.stream)
-            self.solver.launch(inputs)
-            self.ends[slot].record(self.stream)
+        st = self.streams[slot]
+        with torch.cuda.device(self.device), torch.cuda.stream(st):
+            self.starts[slot].record(st)
+            self.solvers[slot].launch(inputs)
+            self.ends[slot].record(st)
         self.meta[slot] = (work, start)
         self.order.append(slot)
 
@@ -91,7 +106,7 @@ class EquihashGpuDevice:
                     raise DeviceHung(f"gpu{self.device}: Equihash window did not finish in {timeout_s:.0f}s")
                 time.sleep(0.0002)
         self.order.pop(0)
-        arrays = self.solver.collect_arrays(verify="device")
+        arrays = self.solvers[slot].collect_arrays(verify="device")
         work, start = self.meta[slot]
         self.meta[slot] = None
         shares, sols = _passing(work, start, [pack_solutions(a) if len(a) else [] for a in arrays])
@@ -103,7 +118,8 @@ class EquihashGpuDevice:
         leader drops their shares as stale."""
 
     def synchronize(self) -> None:
-        self.stream.synchronize()
+        for st in self.streams:
+            st.synchronize()
 
     def close(self) -> None:
         pass
