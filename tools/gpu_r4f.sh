@@ -12,10 +12,6 @@ for v in 1 2 1 2 1 2; do
   NODEXA_SEARCH_STREAMS=$v timeout -k 10 200 python3 bench.py --steps 20 --warmup 4 --equihash 0 --verify 0 \
     > $O/bench_s$v.$(date +%s).json 2>> $O/bench_s$v.err || exit $?
 done
-# the Equihash loop's per-step host timings with and without the one-rank RCCL group
-for c in; do
-  timeout -k 10 200 python3 tools/eq_loop_probe.py $c >> $O/eq_loop.jsonl 2>> $O/eq_loop.err || exit $?
-done
 # kernel time of the resident verify pipeline (BASELINE config 5)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_verify -o v \
   -- python3 bench.py --steps 2 --warmup 1 --equihash 0 --verify 1 > $O/prof_verify.log 2>&1 || exit $?
