@@ -11,8 +11,9 @@ rows in one parallel pass) crosses the PCIe bus twice in total:
                    and serialized headers (one pinned staging buffer)
   device           kawpow_mixonly_batch (SHA256d header hash + mix-only final + nBits boundary),
                    hb_jobs, kawpow_verify_dag per epoch range (resident DAG, per-epoch program
-                   table resident too), hb_verdict, eq_verify + sha256d_batch + hb_eq_scatter,
-                   dgw_batch — all on one stream, no host synchronisation in between
+                   table resident too; the ranges side by side on their own streams), hb_verdict;
+                   beside that chain eq_verify + sha256d_batch and dgw_batch on a side stream;
+                   then hb_eq_scatter — ordered by events, no host synchronisation in between
   device -> host   one copy: per-header code | block hash | expected nBits
 
 and the host keeps only the serial index insert (HeaderChain.accept_batch, native, GIL released,
@@ -50,8 +51,11 @@ class ResidentHeaderVerifier:
         self.dev = torch.device("cuda", self.device)
         with torch.cuda.device(self.dev):
             self.stream = torch.cuda.Stream(device=self.dev)
+            self.side = [torch.cuda.Stream(device=self.dev) for _ in range(3)]  # Equihash + DGW, epoch ranges
             self.ev_start = torch.cuda.Event(enable_timing=True)
             self.ev_end = torch.cuda.Event(enable_timing=True)
+            self.ev_in, self.ev_jobs = torch.cuda.Event(), torch.cuda.Event()
+            self.ev_side = [torch.cuda.Event() for _ in self.side]
         self.cap = 0
         self.in_cap = 0
         self.programs: dict[int, torch.Tensor] = {}
@@ -181,44 +185,65 @@ class ResidentHeaderVerifier:
         cp = int(params.last_checkpoint_height)
         nr = hi_r - lo_r
 
-        def glue(which: int, first: int, count: int) -> None:
+        def glue(which: int, first: int, count: int, st: int) -> None:
             kern = self.k[("hb_jobs", "hb_verdict", "hb_eq_scatter")[which]]
             h.launch_header_batch(kern, which, P("rows"), P("kinds"), self.mo.data_ptr(), self.jobs.data_ptr(),
                                   self.jprog.data_ptr(), self.full.data_ptr(), out, P("eq_index"), P("eq_verdict"),
-                                  P("eq_hash"), n, m, first, count, _core.EPOCH_LENGTH, cp, lim, s)
+                                  P("eq_hash"), n, m, first, count, _core.EPOCH_LENGTH, cp, lim, st)
 
-        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
-            s = int(self.stream.cuda_stream)
-            self.ev_start.record(self.stream)
+        main = self.stream
+        with torch.cuda.device(self.dev), torch.cuda.stream(main):
+            s = int(main.cuda_stream)
+            self.ev_start.record(main)
             self.din[:cur].copy_(self.in_host[:cur], non_blocking=True)
+            self.ev_in.record(main)
+            # Equihash solutions + block hashes and the DGW nBits depend only on the upload: a side
+            # stream runs them beside the KawPow chain (mix-only -> jobs -> full hashes -> verdicts)
+            side = self.side[0]
+            side.wait_event(self.ev_in)
+            s0 = int(side.cuda_stream)
+            if m:
+                h.launch_equihash_verify(self.k_eq, self.h0, P("eq_msgs"), 112, m, P("eq_sols"), P("eq_verdict"), s0)
+                h.launch_sha256d(self.k_sha, P("eq_ser"), eq_len, eq_len, m, P("eq_hash"), False, s0)
+            if series is not None:
+                c = _core.dgw_constants(params)
+                h.launch_dgw(self.k_dgw, P("times"), P("bits"), out + n * 33, a, n, series[3], c["dgw_activation_block"],
+                             c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], s0)
+            self.ev_side[0].record(side)
             if nr:
                 h.launch_kawpow_mixonly(self.k_mo, P("rows") + lo_r * ROW, nr, ROW, self.mo.data_ptr() + lo_r * 128, s)
-                glue(0, lo_r, nr)
+                glue(0, lo_r, nr, s)
+                self.ev_jobs.record(main)
+                # one full-hash launch per epoch range, the ranges side by side: each is bound by
+                # its 64 dependent rounds per job (~0.65 ms whatever its job count), not by width
+                k = 0
                 for epoch, lo, hi in plan["ranges"]:
                     lo, hi = max(lo, lo_r), min(hi, hi_r)
                     if lo >= hi:
                         continue
+                    st = main if k == 0 else self.side[1 + (k - 1) % (len(self.side) - 1)]
+                    if st is not main:
+                        st.wait_event(self.ev_jobs)
                     ep = V._device_epoch(epoch, self.device)
                     h.launch_kawpow_verify_dag(self.k_dag, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(),
                                                self.jobs.data_ptr() + lo * 48, self.program_table(epoch).data_ptr(),
                                                _core.EPOCH_LENGTH // 3, self.jprog.data_ptr() + lo * 4, hi - lo,
-                                               self.full.data_ptr() + lo * 64, s)
-                glue(1, lo_r, nr)
+                                               self.full.data_ptr() + lo * 64, int(st.cuda_stream))
+                    if st is not main:
+                        ev = self.ev_side[1 + (k - 1) % (len(self.side) - 1)]
+                        ev.record(st)
+                        main.wait_event(ev)
+                    k += 1
+                glue(1, lo_r, nr, s)
+            main.wait_event(self.ev_side[0])
             if m:
-                h.launch_equihash_verify(self.k_eq, self.h0, P("eq_msgs"), 112, m, P("eq_sols"), P("eq_verdict"), s)
-                h.launch_sha256d(self.k_sha, P("eq_ser"), eq_len, eq_len, m, P("eq_hash"), False, s)
-                glue(2, 0, 0)
-            bits_view = self.out[n * 33:n * 37]
-            if series is not None:
-                c = _core.dgw_constants(params)
-                h.launch_dgw(self.k_dgw, P("times"), P("bits"), out + n * 33, a, n, series[3], c["dgw_activation_block"],
-                             c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], s)
-            else:
-                bits_view.zero_()
+                glue(2, 0, 0, s)  # after the verdicts: it overwrites the Equihash rows' codes
+            if series is None:
+                self.out[n * 33:n * 37].zero_()
             if ws > 1:
                 self._gather(world, n, per, lo_r, hi_r)
             self.out_host[:n * 37].copy_(self.out[:n * 37], non_blocking=True)
-            self.ev_end.record(self.stream)
+            self.ev_end.record(main)
         t_issue = time.perf_counter()
         self.ev_end.synchronize()
         t_done = time.perf_counter()
