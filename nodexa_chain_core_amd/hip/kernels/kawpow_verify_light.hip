@@ -253,3 +253,122 @@ NX_DEV void kl_verify(const KawpowLightParams& p) {
 
 extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_light(KawpowLightParams p) { kl_verify<false>(p); }
 extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_dag(KawpowLightParams p) { kl_verify<true>(p); }
+
+// ---------------------------------------------------------------- wave-uniform programs
+// kawpow_verify_waves: one job per 16-lane group against the resident DAG, like kawpow_verify_dag,
+// but the 4 groups of a wave64 hold jobs of ONE period (p.slots, built by the host: the batch's
+// KawPow rows grouped by period, 4 slots per wave, -1 = idle group). The program is then uniform
+// over the wave: its op words come through scalar loads, the op and merge kinds are scalar
+// branches, and the 32-word mix stays in VGPRs, addressed by uniform register moves -- where the
+// LDS-mix interpreter above pays two or three dependent LDS round trips per op. A batch of 3
+// headers per period idles a quarter of the groups; each job is ~64 dependent DAG rounds, so the
+// launch is latency-bound and the idle groups cost nothing measurable.
+typedef uint32_t kw_mix_t __attribute__((ext_vector_type(32)));
+
+NX_DEV uint32_t kw_get(const kw_mix_t& m, uint32_t i) { return m[i & 31]; }
+NX_DEV void kw_set(kw_mix_t& m, uint32_t i, uint32_t v) { m[i & 31] = v; }
+
+extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(KawpowLightParams p) {
+    __shared__ uint32_t l1[4096];
+    for (int i = threadIdx.x; i < 4096; i += KL_BLOCK) l1[i] = p.l1[i];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 15;
+    const uint32_t g = (threadIdx.x >> 4) & 3;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (KL_BLOCK / 64) + (threadIdx.x >> 6));
+    if (wave * 4 >= p.num_slots) return;  // wave-uniform: whole waves only
+    const int32_t first = __builtin_amdgcn_readfirstlane(p.slots[wave * 4]);  // slot 0 of a wave is never idle
+    const int32_t row = p.slots[wave * 4 + g];
+    const bool valid = row >= 0;
+    const uint32_t jj = (uint32_t)(valid ? row : first);
+    uint32_t pi = __builtin_amdgcn_readfirstlane(p.job_program[first]);
+    pi = pi < p.num_programs ? pi : 0;  // host validates; never index past the table
+    const uint32_t* prog = p.programs + (size_t)pi * KV_PROG_WORDS;
+    const KawpowVerifyJob j = p.jobs[jj];
+
+    uint32_t st2[8];
+    {
+        uint32_t s[25];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[i] = j.header[i];
+        s[8] = (uint32_t)j.nonce;
+        s[9] = (uint32_t)(j.nonce >> 32);
+        const uint32_t pad[15] = {0x72, 0x41, 0x56, 0x45, 0x4E, 0x43, 0x4F, 0x49, 0x4E, 0x4B, 0x41, 0x57, 0x50, 0x4F, 0x57};
+#pragma unroll
+        for (int i = 0; i < 15; ++i) s[10 + i] = pad[i];
+        keccak_f800(s);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st2[i] = s[i];
+    }
+    kw_mix_t mix;
+    {
+        const uint32_t z0 = kl_fnv1a(0x811c9dc5u, st2[0]);
+        const uint32_t w0 = kl_fnv1a(z0, st2[1]);
+        const uint32_t jsr0 = kl_fnv1a(w0, lane);
+        uint32_t kz = z0, kw = w0, kj = jsr0, kc = kl_fnv1a(jsr0, lane);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            kz = 36969u * (kz & 0xffffu) + (kz >> 16);
+            kw = 18000u * (kw & 0xffffu) + (kw >> 16);
+            kc = 69069u * kc + 1234567u;
+            kj ^= (kj << 17);
+            kj ^= (kj >> 13);
+            kj ^= (kj << 5);
+            mix[r] = (((kz << 16) + kw) ^ kc) + kj;
+        }
+    }
+    const uint4* dag = (const uint4*)p.dag;
+#pragma unroll 1
+    for (uint32_t r = 0; r < 64; ++r) {
+        const uint32_t index = kl_mod(__shfl(mix[0], (int)(r & 15), 16), p.items);
+        // lane l merges words ((l^r)%16)*4..+3 of the 2048-bit item: load exactly that slice
+        const uint4 d = dag[(size_t)index * 16 + ((lane ^ r) & 15)];
+#pragma unroll 1
+        for (int i = 0; i < 18; ++i) {
+            if (i < 11) {
+                const uint32_t op = __builtin_amdgcn_readfirstlane(prog[i]);
+                const uint32_t a = kw_get(mix, op);
+                const uint32_t dst = (op >> 8) & 31;
+                kw_set(mix, dst, kl_merge(kw_get(mix, dst), l1[a & 4095u], (op >> 16) & 3, op >> 24));
+            }
+            const uint32_t op = __builtin_amdgcn_readfirstlane(prog[11 + i]);
+            const uint32_t mg = __builtin_amdgcn_readfirstlane(prog[29 + i]);
+            const uint32_t v = kl_math(kw_get(mix, op), kw_get(mix, op >> 8), (op >> 16) & 15);
+            const uint32_t dst = op >> 24;
+            kw_set(mix, dst, kl_merge(kw_get(mix, dst), v, mg & 3, mg >> 8));
+        }
+        const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t op = __builtin_amdgcn_readfirstlane(prog[47 + i]);
+            kw_set(mix, op, kl_merge(kw_get(mix, op), dw[i], (op >> 8) & 3, op >> 16));
+        }
+    }
+    uint32_t lh = 0x811c9dc5u;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) lh = kl_fnv1a(lh, mix[r]);
+    uint32_t digest[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t a = __shfl(lh, k, 16);
+        const uint32_t b = __shfl(lh, k + 8, 16);
+        digest[k] = kl_fnv1a(kl_fnv1a(0x811c9dc5u, a), b);
+    }
+    uint32_t st[25];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = st2[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[8 + i] = digest[i];
+    const uint32_t pad[9] = {0x72, 0x41, 0x56, 0x45, 0x4E, 0x43, 0x4F, 0x49, 0x4E};
+#pragma unroll
+    for (int i = 0; i < 9; ++i) st[16 + i] = pad[i];
+    keccak_f800(st);
+    if (valid && lane == 0) {
+        uint32_t* o = p.out + (size_t)row * 16;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            o[k] = digest[k];
+            o[8 + k] = st[k];
+        }
+    }
+}
+

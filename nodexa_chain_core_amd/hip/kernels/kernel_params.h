@@ -192,6 +192,10 @@ struct KawpowLightParams {
     struct FastMod32 light_items;       // modulo by the number of 512-bit light items
     struct FastMod32 items;             // modulo by the number of 2048-bit DAG items
     const void* dag;                    // kawpow_verify_dag: resident DAG (2048-bit items); else null
+    const int32_t* slots;               // kawpow_verify_waves: job per 16-lane group slot, 4 slots per
+                                        // wave, all of one period; -1 = idle group
+    uint32_t num_slots;
+    uint32_t pad;
 };
 
 struct KawpowHashParams {

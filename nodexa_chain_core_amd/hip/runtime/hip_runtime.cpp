@@ -380,6 +380,31 @@ PYBIND11_MODULE(_hip, m) {
         if (grid == 0) return;
         k.launch_bytes(dim3(grid), dim3(256), 0, as_stream(stream), &p, sizeof(p));
     });
+    // kawpow_verify_waves: `slots` holds num_slots job indices (-1 = idle), 4 per wave, one period
+    // per wave (ops/header_batch.py builds them); 4 waves per 256-thread workgroup
+    m.def("launch_kawpow_verify_waves", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t l1,
+                                           uintptr_t jobs, uintptr_t programs, uint32_t num_programs,
+                                           uintptr_t job_program, uint32_t num_jobs, uintptr_t slots,
+                                           uint32_t num_slots, uintptr_t out, uintptr_t stream) {
+        if (num_programs == 0) throw std::invalid_argument("no programs");
+        if (dag == 0) throw std::invalid_argument("kawpow_verify_waves needs a resident DAG");
+        if (num_slots % 4) throw std::invalid_argument("slots: 4 per wave");
+        KawpowLightParams p{};
+        p.dag = reinterpret_cast<const void*>(dag);
+        p.l1 = reinterpret_cast<const uint32_t*>(l1);
+        p.jobs = reinterpret_cast<const KawpowVerifyJob*>(jobs);
+        p.programs = reinterpret_cast<const uint32_t*>(programs);
+        p.job_program = reinterpret_cast<const uint32_t*>(job_program);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        p.num_jobs = num_jobs;
+        p.num_programs = num_programs;
+        p.items = make_fastmod(dag_items2048);
+        p.slots = reinterpret_cast<const int32_t*>(slots);
+        p.num_slots = num_slots;
+        const unsigned grid = (num_slots + 15) / 16;  // 16 slots (4 waves) per workgroup
+        if (grid == 0) return;
+        k.launch_bytes(dim3(grid), dim3(256), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("launch_kawpow_verify_batch", [](const Kernel& k, uintptr_t dag, uint32_t dag_items2048, uintptr_t jobs,
                                            uintptr_t programs, uintptr_t job_program, uint32_t num_jobs, uintptr_t out,
                                            uintptr_t stream) {

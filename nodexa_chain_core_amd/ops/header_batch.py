@@ -22,6 +22,7 @@ compact results are all-gathered device to device (RCCL) before the single copy 
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -34,6 +35,9 @@ _core = core()
 ROW = 128
 CODES = {1: "invalid-mix-hash", 2: "high-hash", 3: "invalid-solution"}
 _ALIGN = 256
+# full hashes with wave-uniform programs (kawpow_verify_waves: mix in VGPRs) instead of the
+# LDS-mix interpreter (kawpow_verify_dag); NODEXA_VERIFY_WAVES=0 selects the latter
+WAVES = os.environ.get("NODEXA_VERIFY_WAVES", "1") != "0"
 
 
 def _al(x: int) -> int:
@@ -63,6 +67,7 @@ class ResidentHeaderVerifier:
         self.k_mo = runtime.static_kernel("sha256d", "kawpow_mixonly_batch")
         self.k_sha = runtime.static_kernel("sha256d", "sha256d_batch")
         self.k_dag = runtime.static_kernel("kawpow_verify_light", "kawpow_verify_dag")
+        self.k_waves = runtime.static_kernel("kawpow_verify_light", "kawpow_verify_waves")
         self.k_eq = runtime.static_kernel("equihash", "eq_verify")
         self.k_dgw = runtime.static_kernel("dgw", "dgw_batch")
         from .equihash import blake2b_h0
@@ -118,7 +123,27 @@ class ResidentHeaderVerifier:
             for e in np.unique(epochs).tolist():
                 idx = kp[epochs == e]
                 ranges.append((int(e), int(idx[0]), int(idx[-1]) + 1))
-        return {"rows": rows, "kinds": kinds, "ranges": ranges}
+        return {"rows": rows, "kinds": kinds, "ranges": ranges,
+                "heights": np.ascontiguousarray(rows[:, 76:80]).view("<u4").ravel()}
+
+    @staticmethod
+    def wave_slots(rows_idx: np.ndarray, heights: np.ndarray, lo: int) -> np.ndarray:
+        """kawpow_verify_waves' slot table for the KawPow rows `rows_idx` of one epoch range: the
+        rows grouped by ProgPoW period (height // 3), each period's rows in slots of 4 (one wave64
+        of four 16-lane groups per 4 rows, -1 for an idle group), values relative to `lo`."""
+        if len(rows_idx) == 0:
+            return np.zeros(0, dtype=np.int32)
+        per = heights[rows_idx] // 3
+        order = np.argsort(per, kind="stable")
+        r, per = rows_idx[order], per[order]
+        start = np.flatnonzero(np.r_[True, per[1:] != per[:-1]])  # first row of each period run
+        length = np.diff(np.r_[start, len(per)])
+        waves = (length + 3) // 4
+        base = np.r_[0, np.cumsum(waves)[:-1]] * 4  # first slot of each run
+        pos = np.arange(len(per)) - np.repeat(start, length)
+        slots = np.full(int(waves.sum()) * 4, -1, dtype=np.int32)
+        slots[np.repeat(base, length) + pos] = (r - lo).astype(np.int32)
+        return slots
 
     def run(self, params, batch, series, plan: dict | None = None, world=None) -> dict:
         """Verify the PoW of every header and compute every header's DGW nBits on the device.
@@ -146,9 +171,20 @@ class ResidentHeaderVerifier:
         a = series[2] if series is not None else 0
         off = {}
         cur = 0
+        # per epoch range of this rank: the wave-uniform slot table (kawpow_verify_waves)
+        slot_tabs = []
+        if WAVES:
+            kmask = kinds == 0
+            for epoch, lo, hi in plan["ranges"]:
+                lo, hi = max(lo, lo_r), min(hi, hi_r)
+                if lo < hi:
+                    idx = np.flatnonzero(kmask[lo:hi]) + lo
+                    slot_tabs.append(self.wave_slots(idx, plan["heights"], lo))
+        nslots = sum(len(t) for t in slot_tabs)
         for name, size in (("rows", n * ROW), ("kinds", n), ("times", (a + n) * 4), ("bits", (a + n) * 4),
                            ("eq_index", m * 4), ("eq_msgs", m * 128), ("eq_sols", m * 1344),
-                           ("eq_ser", m * eq_len), ("eq_verdict", m * 4), ("eq_hash", m * 32)):
+                           ("eq_ser", m * eq_len), ("eq_verdict", m * 4), ("eq_hash", m * 32),
+                           ("slots", nslots * 4)):
             off[name] = (cur, size)
             cur = _al(cur + size)
         self._ensure(n, cur)
@@ -171,6 +207,8 @@ class ResidentHeaderVerifier:
             bits[a:] = np.ascontiguousarray(rows[:, 72:76]).view("<u4").ravel()
             put("times", times)
             put("bits", bits)
+        if nslots:
+            put("slots", np.concatenate(slot_tabs))
         if m:
             put("eq_index", eq_index[mine_eq].astype(np.uint32))
             put("eq_msgs", np.frombuffer(batch.eq_msgs, np.uint8).reshape(-1, 128)[mine_eq])
@@ -215,7 +253,8 @@ class ResidentHeaderVerifier:
                 glue(0, lo_r, nr, s)
                 self.ev_jobs.record(main)
                 # one full-hash launch per epoch range, the ranges side by side: each is bound by
-                # its 64 dependent rounds per job (~0.65 ms whatever its job count), not by width
+                # its 64 dependent rounds per job, not by width
+                slot_off = np.r_[0, np.cumsum([len(t) for t in slot_tabs])].tolist()
                 k = 0
                 for epoch, lo, hi in plan["ranges"]:
                     lo, hi = max(lo, lo_r), min(hi, hi_r)
@@ -225,10 +264,19 @@ class ResidentHeaderVerifier:
                     if st is not main:
                         st.wait_event(self.ev_jobs)
                     ep = V._device_epoch(epoch, self.device)
-                    h.launch_kawpow_verify_dag(self.k_dag, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(),
-                                               self.jobs.data_ptr() + lo * 48, self.program_table(epoch).data_ptr(),
-                                               _core.EPOCH_LENGTH // 3, self.jprog.data_ptr() + lo * 4, hi - lo,
-                                               self.full.data_ptr() + lo * 64, int(st.cuda_stream))
+                    if WAVES:
+                        tab = slot_tabs[k]
+                        h.launch_kawpow_verify_waves(self.k_waves, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(),
+                                                     self.jobs.data_ptr() + lo * 48,
+                                                     self.program_table(epoch).data_ptr(), _core.EPOCH_LENGTH // 3,
+                                                     self.jprog.data_ptr() + lo * 4, hi - lo,
+                                                     P("slots") + slot_off[k] * 4, len(tab),
+                                                     self.full.data_ptr() + lo * 64, int(st.cuda_stream))
+                    else:
+                        h.launch_kawpow_verify_dag(self.k_dag, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(),
+                                                   self.jobs.data_ptr() + lo * 48, self.program_table(epoch).data_ptr(),
+                                                   _core.EPOCH_LENGTH // 3, self.jprog.data_ptr() + lo * 4, hi - lo,
+                                                   self.full.data_ptr() + lo * 64, int(st.cuda_stream))
                     if st is not main:
                         ev = self.ev_side[1 + (k - 1) % (len(self.side) - 1)]
                         ev.record(st)

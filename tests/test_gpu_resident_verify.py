@@ -113,3 +113,36 @@ W.shutdown()
     ref.accept_headers(hs, hs[-1].time + 3600, False)
     assert out["backend"] == "nccl" and out["accepted"] == len(hs) and out["tip"] == core.u256_hex(ref.tip().hash)
     assert np.all(True)
+
+
+def test_wave_uniform_full_hashes_equal_lds_interpreter(core, gpu):
+    """kawpow_verify_waves (wave-uniform programs, mix in VGPRs) against kawpow_verify_dag (the
+    LDS-mix interpreter): the same digest and final hash for every KawPow row of the batch."""
+    import torch
+
+    from nodexa_chain_core_amd.models.verify import resident_verifier
+    from nodexa_chain_core_amd.ops import header_batch as HB
+
+    params, hs, raw = _load(core, "testnet_kawpow_10k.hdr")
+    batch = core.HeaderBatch.from_bytes(raw, params.kawpow_activation_time)
+    v = resident_verifier(0)
+    plan = v.plan(batch)
+    series = core.HeaderChain(params).dgw_ancestors(batch.header(0).prev)
+    out = {}
+    saved = HB.WAVES
+    try:
+        for waves in (False, True):
+            HB.WAVES = waves
+            if hasattr(v, "full"):
+                v.full.zero_()
+                torch.cuda.synchronize()
+            r = v.run(params, batch, series, plan)
+            torch.cuda.synchronize()
+            out[waves] = (v.full[:len(hs) * 16].cpu().numpy().copy(), np.array(r["codes"]))
+    finally:
+        HB.WAVES = saved
+    kp = np.flatnonzero(np.frombuffer(batch.kinds, np.uint8) == 0)
+    a = out[False][0].reshape(-1, 16)[kp]
+    b = out[True][0].reshape(-1, 16)[kp]
+    assert (a == b).all(), int((a != b).any(1).sum())
+    assert (out[False][1] == out[True][1]).all()

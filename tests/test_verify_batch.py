@@ -311,3 +311,29 @@ def test_accept_headers_fast_path_equals_serial(chain_fixture):
     assert ra == rb and all(r[0] for r in ra) and a.tip().hash == b.tip().hash
     assert a.tip().hash == a.block_hash(fork[-1]) and a.height() == hs[2500].height + 699
     _same_chain(a, b)
+
+
+def test_wave_slots_group_rows_by_period():
+    """ops/header_batch.wave_slots (kawpow_verify_waves' table): every KawPow row exactly once, the
+    4 slots of a wave all of one ProgPoW period, slot 0 of a wave never idle, values relative to lo."""
+    import numpy as np
+
+    from nodexa_chain_core_amd.ops.header_batch import ResidentHeaderVerifier
+
+    rng = np.random.default_rng(5)
+    for _ in range(20):
+        n = int(rng.integers(1, 400))
+        heights = np.sort(rng.integers(7500, 7500 + 600, n)).astype(np.uint32)
+        if rng.random() < 0.3:
+            heights = rng.permutation(heights)  # arbitrary claimed heights: still grouped correctly
+        lo = int(rng.integers(0, 5))
+        idx = np.sort(rng.choice(np.arange(lo, n), size=int(rng.integers(1, max(2, n - lo))), replace=False)) \
+            if n > lo else np.arange(0)
+        slots = ResidentHeaderVerifier.wave_slots(idx, heights, lo)
+        assert len(slots) % 4 == 0
+        got = slots[slots >= 0] + lo
+        assert sorted(got.tolist()) == sorted(idx.tolist())
+        for w in slots.reshape(-1, 4):
+            assert w[0] >= 0
+            per = {int(heights[x + lo]) // 3 for x in w if x >= 0}
+            assert len(per) == 1
