@@ -433,26 +433,27 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const BlockHeader* hs, siz
         if (m > 0) {
             const size_t s0 = batch.size();
             nodes.resize(m);
-            storage_.reserve_raw(m, nodes.data());
-            batch.insert(batch.end(), nodes.begin(), nodes.end());
             work.resize(m);
             ArithU256 w = prev->chain_work;
             for (size_t k = 0; k < m; ++k) work[k] = w += proofs[i + k];
-            parallel_for(m, [&](size_t k) {
-                HeaderIndex& e = *new (nodes[k]) HeaderIndex();
-                const size_t j = i + k;
-                e.hash = hashes[j];
-                e.prev = k ? nodes[k - 1] : prev;
-                e.height = base_height + 1 + int(j);
-                e.time = hs[j].time;
-                e.bits = hs[j].bits;
-                e.header = hs[j];
-                e.chain_work = work[k];
-                const int sh = skip_height(e.height);
-                e.skip = sh > base_height ? batch[size_t(sh - base_height - 1)] : prev->ancestor(sh);
-                index_.insert_concurrent(&e);
-                out[j].ok = true;
-                out[j].index = &e;
+            storage_.emplace_n(m, nodes.data(), [&] {
+                batch.insert(batch.end(), nodes.begin(), nodes.end());  // reserved: no reallocation
+                parallel_for(m, [&](size_t k) {
+                    HeaderIndex& e = *new (nodes[k]) HeaderIndex();
+                    const size_t j = i + k;
+                    e.hash = hashes[j];
+                    e.prev = k ? nodes[k - 1] : prev;
+                    e.height = base_height + 1 + int(j);
+                    e.time = hs[j].time;
+                    e.bits = hs[j].bits;
+                    e.header = hs[j];
+                    e.chain_work = work[k];
+                    const int sh = skip_height(e.height);
+                    e.skip = sh > base_height ? batch[size_t(sh - base_height - 1)] : prev->ancestor(sh);
+                    index_.insert_concurrent(&e);
+                    out[j].ok = true;
+                    out[j].index = &e;
+                });
             });
             index_.add_count(m);
             active_.insert(active_.end(), batch.begin() + std::ptrdiff_t(s0), batch.end());

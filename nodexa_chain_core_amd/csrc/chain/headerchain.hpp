@@ -66,16 +66,18 @@ public:
     }
     HeaderIndex* alloc() {
         HeaderIndex* e = nullptr;
-        reserve_raw(1, &e);
-        return new (e) HeaderIndex();
+        emplace_n(1, &e, [&] { new (e) HeaderIndex(); });
+        return e;
     }
-    // storage for n entries (not constructed: the caller placement-news every one of them
-    // before anything else reads the arena)
-    void reserve_raw(size_t n, HeaderIndex** out) {
-        for (size_t k = 0; k < n; ++k, ++used_) {
-            if (used_ == chunks_.size() * kChunk) chunks_.push_back(::operator new(kChunk * sizeof(HeaderIndex)));
-            out[k] = at(used_);
-        }
+    // Storage for n entries (out[k]); `construct` placement-news every one of them (from any
+    // number of threads). The entries count as allocated -- and are destroyed with the arena --
+    // only once `construct` has returned, so a throw leaves nothing half-built behind.
+    template <class F>
+    void emplace_n(size_t n, HeaderIndex** out, F&& construct) {
+        while (used_ + n > chunks_.size() * kChunk) chunks_.push_back(::operator new(kChunk * sizeof(HeaderIndex)));
+        for (size_t k = 0; k < n; ++k) out[k] = at(used_ + k);
+        construct();
+        used_ += n;
     }
     size_t size() const { return used_; }
     template <class F>
