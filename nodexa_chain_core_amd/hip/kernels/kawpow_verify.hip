@@ -6,8 +6,11 @@
 // program is data: the host materialises each distinct period's op list
 // (csrc/pow/kawpow.cpp make_kawpow_program) and sorts jobs so that every
 // wave64 (4 hashes x 16 lanes, 64 jobs walked by the wave) shares one period.
-// The op fields are then wave-uniform (readfirstlane), so the 32-word mix is
-// indexed with uniform register moves instead of a divergent waterfall.
+// The op fields are then wave-uniform (readfirstlane), so the 32-word mix (in
+// LDS, [wave][group][reg][lane]) is addressed with uniform offsets instead of a
+// divergent waterfall. Each group walks 16 jobs of its slab, so this layout
+// suits periods with many jobs; a header batch (3 headers per period) uses
+// kawpow_verify_waves (kawpow_verify_light.hip) instead.
 #include "kernel_params.h"
 #include "keccak_device.hpp"
 
