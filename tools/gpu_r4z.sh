@@ -10,5 +10,7 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-m
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4z/smoke.log 2>&1 &&
 timeout -k 10 600 python3 -u bench.py > gpurun_out/r4z/bench.json 2> gpurun_out/r4z/bench.err &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r4z/prof -o bench --output-format csv \
-  -- python3 bench.py --steps 6 --warmup 2 > gpurun_out/r4z/prof.log 2>&1
+  -- python3 bench.py --steps 6 --warmup 2 > gpurun_out/r4z/prof.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4z/prof_verify -o v --output-format csv \
+  -- python3 bench.py --steps 2 --warmup 1 --equihash 0 --verify 1 > gpurun_out/r4z/prof_verify.log 2>&1
 echo "exit=$?"
