@@ -492,6 +492,34 @@ void bind_extra(py::module_& m) {
     auto view = [](const std::string& s) {  // zero-copy, read-only: the batch must outlive it
         return py::memoryview::from_memory(const_cast<char*>(s.data()), py::ssize_t(s.size()), true);
     };
+    m.def("wave_slots", [](const py::buffer& kinds_buf, const py::buffer& heights_buf, size_t lo, size_t hi) {
+        // kawpow_verify_waves' slot table for the KawPow rows (kind 0) of [lo, hi): the rows grouped
+        // by ProgPoW period (height / 3), 4 slots per wave64 (one 16-lane group each), -1 = idle
+        // group, values relative to lo; little-endian int32 bytes
+        const py::buffer_info kb = kinds_buf.request(), hb = heights_buf.request();
+        const u8* kinds = static_cast<const u8*>(kb.ptr);
+        const u32* heights = static_cast<const u32*>(hb.ptr);
+        const size_t n = std::min(size_t(kb.size * kb.itemsize), size_t(hb.size * hb.itemsize) / 4);
+        hi = std::min(hi, n);
+        std::vector<u32> rows;
+        rows.reserve(hi > lo ? hi - lo : 0);
+        bool sorted = true;
+        for (size_t r = lo; r < hi; ++r) {
+            if (kinds[r] != 0) continue;
+            if (!rows.empty() && heights[r] / 3 < heights[rows.back()] / 3) sorted = false;
+            rows.push_back(u32(r));
+        }
+        if (!sorted)
+            std::stable_sort(rows.begin(), rows.end(), [&](u32 a, u32 b) { return heights[a] / 3 < heights[b] / 3; });
+        std::vector<int32_t> out;
+        out.reserve(rows.size() * 2 + 4);
+        for (size_t i = 0; i < rows.size();) {
+            const u32 per = heights[rows[i]] / 3;
+            for (; i < rows.size() && heights[rows[i]] / 3 == per; ++i) out.push_back(int32_t(rows[i] - lo));
+            while (out.size() % 4) out.push_back(-1);
+        }
+        return py::bytes(reinterpret_cast<const char*>(out.data()), out.size() * 4);
+    }, py::arg("kinds"), py::arg("heights"), py::arg("lo"), py::arg("hi"));
     py::class_<HeaderBatch, std::shared_ptr<HeaderBatch>>(m, "HeaderBatch")
         .def_static("from_bytes", [](const py::buffer& buf, u32 act) {
             const py::buffer_info bi = buf.request();

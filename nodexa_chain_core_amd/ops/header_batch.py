@@ -174,12 +174,10 @@ class ResidentHeaderVerifier:
         # per epoch range of this rank: the wave-uniform slot table (kawpow_verify_waves)
         slot_tabs = []
         if WAVES:
-            kmask = kinds == 0
             for epoch, lo, hi in plan["ranges"]:
                 lo, hi = max(lo, lo_r), min(hi, hi_r)
                 if lo < hi:
-                    idx = np.flatnonzero(kmask[lo:hi]) + lo
-                    slot_tabs.append(self.wave_slots(idx, plan["heights"], lo))
+                    slot_tabs.append(np.frombuffer(_core.wave_slots(kinds, plan["heights"], lo, hi), dtype=np.int32))
         nslots = sum(len(t) for t in slot_tabs)
         for name, size in (("rows", n * ROW), ("kinds", n), ("times", (a + n) * 4), ("bits", (a + n) * 4),
                            ("eq_index", m * 4), ("eq_msgs", m * 128), ("eq_sols", m * 1344),

@@ -337,3 +337,8 @@ def test_wave_slots_group_rows_by_period():
             assert w[0] >= 0
             per = {int(heights[x + lo]) // 3 for x in w if x >= 0}
             assert len(per) == 1
+        # the native table the resident pipeline uses (_core.wave_slots) is the same table
+        kinds = np.full(n, 2, dtype=np.uint8)
+        kinds[idx] = 0
+        hi = int(idx[-1]) + 1 if len(idx) else lo
+        assert (np.frombuffer(_core.wave_slots(kinds, heights, lo, hi), dtype=np.int32) == slots).all()
