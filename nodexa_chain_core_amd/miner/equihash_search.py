@@ -6,11 +6,11 @@ SHA256d(serialized header) <= nBits target. A window of `count` nonces is `count
 instances: nonce k of the window stands for nonce256 = le64(start + k) || 0^24, so the ranks'
 64-bit nonce partition (rank << 56) carries over unchanged.
 
-* `EquihashGpuDevice`: one `ops.equihash.EquihashSolver` per slot with `num_inst` instances per
-  launch (16: ~8.6 ms of device work, so the loop's per-step host work and collectives hide behind
-  the window that is running), each slot on its own stream so the two windows overlap at their
-  kernel tails. Every solution is verified on the device (eq_verify_slots) before it is counted;
-  the host only SHA256d's the candidate headers.
+* `EquihashGpuDevice`: one `ops.equihash.EquihashSolver` with `num_inst` instances per launch
+  (16: ~8.4 ms of device work, so the loop's per-step host work and collectives hide behind the
+  window that is running); the solver keeps two launches in flight on its stream with two pinned
+  landing buffers, one per slot. Every solution is verified on the device (eq_verify_slots)
+  before it is counted; the host only SHA256d's the candidate headers.
 * `EquihashCpuDevice`: the C++ golden solver (~2.3 s per nonce on one core) for CPU-only nodes and
   the gloo rehearsals of the loop.
 
@@ -57,11 +57,12 @@ class EquihashGpuDevice:
         self.torch = torch
         self.device = int(device)
         self.num_inst = int(num_inst)
-        # one solver (its own ~8.6 GB of level buffers at 16 instances) and one stream per slot
-        # (NODEXA_EQ_STREAMS=1: one of each): the queued window's kernels fill the running one's
-        # tails -- every round kernel is two partial waves of 1024-thread workgroups, and the final
-        # round, reconstruction and verdicts use a fraction of the CUs
-        two = os.environ.get("NODEXA_EQ_STREAMS", "2") != "1"
+        # NODEXA_EQ_STREAMS=2: a solver (its own ~8.6 GB of level buffers at 16 instances) and a
+        # stream per slot, so the queued window's kernels could fill the running one's tails.
+        # Measured no gain (profiles/README r4g: 7.5-8.3 vs 8.0-8.1 ms per window; r4z: the two
+        # streams landed on one hardware queue and the loop ran 1 ms per step slower), so one
+        # solver on one stream is the default: the solver keeps both slots' launches in flight
+        two = os.environ.get("NODEXA_EQ_STREAMS", "1") == "2"
         with torch.cuda.device(self.device):
             self.streams = [torch.cuda.Stream(device=self.device)]
             self.streams.append(torch.cuda.Stream(device=self.device) if two else self.streams[0])

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r4g: the Equihash mining loop with one solver+stream per slot (NODEXA_EQ_STREAMS=2, default) vs
+# r4g: the Equihash mining loop with one solver+stream per slot (NODEXA_EQ_STREAMS=2) vs
 # one shared (=1), with and without the one-rank RCCL group: per-step host timings and Sol/s
 # (tools/eq_loop_probe.py); the Equihash GPU tests on the two-solver device.
 set -o pipefail
