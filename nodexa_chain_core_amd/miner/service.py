@@ -12,19 +12,21 @@ process group at all) and all ranks run the same step, `MiningService.step`:
      proof of work: KawPow (2^25-nonce GPU windows), Equihash(200,9) (16 solver instances per
      window) or X16R/X16RV2 (host windows of 2^16 nNonce values, before the KawPow activation);
   2. all-gather every rank's record (fixed 5592-byte slot: job, work done, shares, and the rank's
-     own telemetry: device time, aborted workgroups, collective wait, failures, resident epochs);
-  3. all-reduce the step's work counters (and the next-epoch readiness votes);
-  4. rank 0 (the node: chain state, RPC) checks shares again (KawPow: full light-mode re-hash;
+     own telemetry: device time, aborted workgroups, collective wait, failures, resident epochs,
+     next-epoch readiness vote); every rank sums the work counters and votes from it;
+  3. rank 0 (the node: chain state, RPC) checks shares again (KawPow: full light-mode re-hash;
      Equihash: the golden verifier; X16R: the block check), builds the block of the share's job
      and runs ProcessNewBlock; then it decides the next work packet;
-  5. broadcast the 144-byte work packet from rank 0; a new job with FLAG_CLEAN makes every rank
+  4. broadcast the 144-byte work packet from rank 0; a new job with FLAG_CLEAN makes every rank
      abort its queued window of the stale job on the device.
 
 Nonce partition: rank r of n searches job-local windows from nonce_base + (r << 56) (X16R's 32-bit
 nNonce: r << 28), so ranks never overlap and a job change (new extranonce -> new header) restarts
 every cursor. DAGs are built sharded over the ranks and all-gathered (parallel/dag.py); the next
-epoch's DAG is prebuilt on a side stream once every rank reports its light cache ready (an
-all-reduced vote, so the collective build starts on the same step everywhere).
+epoch's DAG is prebuilt on a side stream once every rank reports its light cache ready (a vote in
+the gathered records, so the collective build starts on the same step everywhere). On RCCL the two
+collectives run from a high-priority stream with persistent pinned/device buffers, so they never
+queue behind a search window on a shared hardware queue.
 
 Failure handling (the reference's miner just exits on errors, src/miner.cpp:716-725):
 * a window that raises (a device fault; -gpufailrate injects them) counts a failure; after
@@ -920,7 +922,8 @@ class Miner:
 
     @property
     def hashrate(self) -> float:
-        """getmininginfo.hashespersec: the all-reduced rate over every rank (src/miner.cpp:685-687)."""
+        """getmininginfo.hashespersec: the rate summed over every rank's gathered record
+        (src/miner.cpp:685-687)."""
         return self.service.hashrate()
 
     def workers(self) -> list[dict]:
