@@ -330,6 +330,25 @@ def resident_verifier(device: int):
 
 
 @traced("verify.process_batch_resident")
+def resident_ready(headers, act: int, device: int, mode: str = "auto") -> bool:
+    """Whether a header batch should take the device-resident path (process_batch_resident): always
+    for mode "dag"; for "auto" when every epoch of its KawPow headers already has a resident DAG on
+    `device` or has more headers than ops/verify.LIGHT_MAX_JOBS (the DAG build then pays for
+    itself); "light" never (no DAG is built for a P2P `headers` message of 2000 headers)."""
+    if mode == "dag":
+        return True
+    if mode != "auto":
+        return False
+    from ..ops import verify as V
+
+    epochs: dict[int, int] = {}
+    for h in headers:
+        if h.time >= act and not h.is_equihash():
+            e = int(h.height) // _core.EPOCH_LENGTH
+            epochs[e] = epochs.get(e, 0) + 1
+    return bool(epochs) and all((device, e) in V._epochs or n > V.LIGHT_MAX_JOBS for e, n in epochs.items())
+
+
 def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, world=None) -> dict | None:
     """ProcessNewBlockHeaders for a native HeaderBatch with the device-resident pipeline
     (ops/header_batch.py): one upload, PoW + block hashes + DGW nBits of every header on the GPU,

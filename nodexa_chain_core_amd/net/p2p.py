@@ -11,9 +11,11 @@ sendheaders. Headers-first sync follows src/net_processing.cpp:1369-1500:
 
 The MI355X difference is where a `headers` batch goes: instead of the reference's
 serial CheckBlockHeader per header under cs_main (src/validation.cpp:12017-12035),
-the whole batch is PoW-checked in bulk (models/verify.process_headers — GPU batch
-kernels when the node has GPUs, all host cores otherwise), then DarkGravityWave and
-the contextual rules run header by header on the C++ header chain.
+the whole batch is PoW-checked in bulk, then DarkGravityWave and the contextual rules run on
+the C++ header chain. With a GPU whose epoch DAGs are resident (a mining node), or with
+`-p2pverifymode=dag`, the batch takes the device-resident path (models/verify.
+process_batch_resident: one upload, PoW + block hashes + nBits on the GPU, one download, the bulk
+insert); otherwise models/verify.process_headers (GPU light-mode kernels, or all host cores).
 """
 from __future__ import annotations
 
@@ -786,7 +788,7 @@ class ConnectionManager:
         peer.send("headers", _core.headers_msg_encode(out, self.params.kawpow_activation_time))
 
     def on_headers(self, peer: Peer, p: bytes) -> None:
-        from ..models.verify import process_headers
+        from ..models.verify import process_batch_resident, process_headers, resident_ready
 
         headers = _core.headers_msg_decode(p, self.params.kawpow_activation_time)
         if not headers:
@@ -798,7 +800,18 @@ class ConnectionManager:
                 return
             self.state.arm_reorg_guard(self.peer_count())
             t0 = time.perf_counter()
-            res = process_headers(chain, headers, self.state.adjusted_time(), gpus=self.gpus, mode=self.verify_mode)
+            res = None
+            act = self.params.kawpow_activation_time
+            if self.gpus and resident_ready(headers, act, self.gpus[0], self.verify_mode):
+                # one upload, PoW + block hashes + DGW nBits on the GPU, one download, the bulk
+                # insert on the host (None: not height-ordered -> the staged path below)
+                res = process_batch_resident(chain, _core.HeaderBatch.from_headers(headers, act),
+                                             self.state.adjusted_time(), device=self.gpus[0])
+                if res is not None:
+                    REGISTRY.inc("p2p_headers_resident_total", len(headers))
+            if res is None:
+                res = process_headers(chain, headers, self.state.adjusted_time(), gpus=self.gpus,
+                                      mode=self.verify_mode)
             REGISTRY.inc("p2p_headers_accepted_total", res["accepted"])
             REGISTRY.set("p2p_headers_batch_seconds", time.perf_counter() - t0)
             log.log_print("net", f"peer {peer.id}: {res['accepted']}/{len(headers)} headers accepted "

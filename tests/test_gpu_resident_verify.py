@@ -146,3 +146,40 @@ def test_wave_uniform_full_hashes_equal_lds_interpreter(core, gpu):
     b = out[True][0].reshape(-1, 16)[kp]
     assert (a == b).all(), int((a != b).any(1).sum())
     assert (out[False][1] == out[True][1]).all()
+
+
+def test_p2p_header_sync_takes_the_resident_path(core, gpu, tmp_path):
+    """nodexad -gpus=0 -p2pverifymode=dag syncing headers from a peer: every `headers` message goes
+    through the device-resident pipeline (process_batch_resident) and the chain matches the peer's."""
+    import time
+
+    from nodexa_chain_core_amd.node import Node
+    from nodexa_chain_core_amd.utils.config import ArgsManager
+    from nodexa_chain_core_amd.utils.metrics import REGISTRY
+
+    def node(name, extra):
+        addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
+        d = tmp_path / name
+        d.mkdir()
+        args = ArgsManager()
+        args.parse_parameters(["-regtest", f"-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+                               f"-miningaddress={addr}", "-printtoconsole=0", *extra])
+        n = Node(args)
+        n.start()
+        return n
+
+    a = node("a", ["-listen", "-port=0"])
+    b = None
+    try:
+        a.miner.generate(a.mining_script, 40)
+        before = REGISTRY.counter("p2p_headers_resident_total")
+        b = node("b", [f"-connect=127.0.0.1:{a.connman.port}", "-gpus=0", "-p2pverifymode=dag"])
+        t = time.time() + 120
+        while time.time() < t and b.state.chain.height() < 40:
+            time.sleep(0.05)
+        assert b.state.chain.height() == 40 and b.state.chain.tip().hash == a.state.chain.tip().hash
+        assert REGISTRY.counter("p2p_headers_resident_total") - before >= 40
+    finally:
+        if b is not None:
+            b.stop()
+        a.stop()
