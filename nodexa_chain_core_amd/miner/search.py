@@ -268,6 +268,9 @@ class GpuSearchDevice:
             if not e.l1_matches():
                 raise RuntimeError(f"gpu{self.device}: epoch {epoch} DAG failed its L1 self-check")
         self.dag_build_s[epoch] = self.dag_build_s.get(epoch, 0.0) + time.perf_counter() - t0
+        from ..ops import verify as V
+
+        V.share_epoch(self.device, epoch, e)  # header batches of this epoch verify against it too
         for old in [k for k in self.epochs if k < epoch - 1]:
             self.epochs.pop(old)
             self.searchers.pop(old, None)

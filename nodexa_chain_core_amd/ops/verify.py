@@ -53,6 +53,13 @@ def _device_epoch(epoch: int, device: int) -> DeviceEpoch:
     return e
 
 
+def share_epoch(device: int, epoch: int, e: DeviceEpoch) -> None:
+    """Offer a DAG built elsewhere on `device` (the miner's, miner/search.GpuSearchDevice) to batch
+    verify: a mining node then verifies the current epoch's headers against the DAG it mines on
+    instead of building a second 4 GiB copy (read-only on both sides)."""
+    _epochs.setdefault((device, epoch), e)
+
+
 def _light_epoch(epoch: int, device: int) -> DeviceEpoch:
     key = (device, epoch)
     e = _light.get(key)
