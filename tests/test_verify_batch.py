@@ -342,3 +342,27 @@ def test_wave_slots_group_rows_by_period():
         kinds[idx] = 0
         hi = int(idx[-1]) + 1 if len(idx) else lo
         assert (np.frombuffer(_core.wave_slots(kinds, heights, lo, hi), dtype=np.int32) == slots).all()
+
+
+def test_resident_ready_policy(chain_fixture):
+    """models/verify.resident_ready: P2P header batches take the device-resident path with
+    -p2pverifymode=dag, or under "auto" once every epoch of the batch has a resident DAG on the
+    device (a mining node's, shared through ops/verify.share_epoch) -- never by building a DAG for
+    a 2000-header message."""
+    from nodexa_chain_core_amd.models.verify import resident_ready
+    from nodexa_chain_core_amd.ops import verify as V
+
+    params, headers = chain_fixture
+    act = params.kawpow_activation_time
+    hs = list(headers[:2000])  # epoch 0
+    assert resident_ready(hs, act, 0, "dag") and not resident_ready(hs, act, 0, "light")
+    saved = dict(V._epochs)
+    try:
+        V._epochs.clear()
+        assert not resident_ready(hs, act, 0, "auto")
+        V.share_epoch(0, 0, object())
+        assert resident_ready(hs, act, 0, "auto") and not resident_ready(hs, act, 1, "auto")
+        assert not resident_ready(list(headers[7400:7600]), act, 0, "auto")  # spans epochs 0 and 1
+    finally:
+        V._epochs.clear()
+        V._epochs.update(saved)
