@@ -578,12 +578,15 @@ PYBIND11_MODULE(_hip, m) {
     m.attr("EQP_STATS") = EQP_STATS;
     m.attr("EQP_STAT_CHAIN") = EQP_STAT_CHAIN;
     m.attr("EQP_STAT_STAGE") = EQP_STAT_STAGE;
+    m.attr("EQP_FINAL_GROUPS") = EQP_FINAL_GROUPS;
     m.attr("EQP_STAT_STAGE_MAX") = EQP_STAT_STAGE_MAX;
     m.def("launch_equihash_ps_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
                                          uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uint32_t groups,
                                          uintptr_t hashes, uintptr_t refs, uintptr_t counts, uintptr_t cands,
-                                         uintptr_t sols, uintptr_t stats, uintptr_t stream, uint32_t block) {
+                                         uintptr_t sols, uintptr_t stats, uintptr_t stream, uint32_t block,
+                                         uint32_t final_groups) {
         if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash_ps kernels");
+        if (final_groups == 0 || final_groups > EQ_BUCKETS) throw std::invalid_argument("final_groups: 1..4096");
         if (block < 256 || block > 1024 || block % 256) throw std::invalid_argument("block: 256..1024, a multiple of 256 (the build's EQP_BLOCK)");
         if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
         if (input_len > 124 || num_inst == 0 || num_inst > 65535) throw std::invalid_argument("bad equihash geometry");
@@ -610,11 +613,11 @@ PYBIND11_MODULE(_hip, m) {
         // counts need no clear: every workgroup writes its whole row of every level
         const dim3 grid(groups, num_inst);
         for (size_t k = 0; k < 9; ++k) ks[k]->launch_bytes(grid, dim3(block), 0, s, &p, sizeof(p));
-        ks[9]->launch_bytes(dim3(EQP_FINAL_GROUPS, num_inst), dim3(block), 0, s, &p, sizeof(p));
+        ks[9]->launch_bytes(dim3(final_groups, num_inst), dim3(block), 0, s, &p, sizeof(p));
         ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
     }, py::arg("ks"), py::arg("h0"), py::arg("msgs"), py::arg("input_len"), py::arg("num_inst"), py::arg("groups"),
        py::arg("hashes"), py::arg("refs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
-       py::arg("stream"), py::arg("block") = 1024);
+       py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQP_FINAL_GROUPS);
     // The 11 kernel launches captured once into a hipGraph (fixed device buffers, so the graph
     // stays valid across batches; only the message words change, in place). Per batch: 3
     // memsets + one hipGraphLaunch instead of 14 stream operations.

@@ -94,7 +94,7 @@ def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | 
 class EquihashSolver:
     def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 8,
                  code_object: str | None = None, engine: str | None = None, groups: int = 32,
-                 block: int = 1024):
+                 block: int = 1024, final_groups: int | None = None):
         """`code_object`: path of an alternative build of the engine's .hip (tuning sweeps).
         `engine`: "ps" (private slot segments, `groups` workgroups per instance per round) or
         "global" (global slot atomics, `banks` counters per bucket)."""
@@ -104,6 +104,8 @@ class EquihashSolver:
         self.banks = int(banks)
         self.groups = int(groups)
         self.block = int(block)  # ps: threads per workgroup, must match the code object's EQP_BLOCK
+        # ps: workgroups per instance of the final round (it writes no level, so any width works)
+        self.final_groups = int(final_groups or os.environ.get("NODEXA_EQP_FINAL_GROUPS", 0) or 0)
         runtime.require_gpu()
         self.h = runtime.hip()
         self.num_inst = int(num_inst)
@@ -184,7 +186,8 @@ class EquihashSolver:
                 self.h.launch_equihash_ps_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
                                                 self.num_inst, self.groups, self.hashes.data_ptr(),
                                                 self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
-                                                self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block)
+                                                self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block,
+                                                self.final_groups or self.h.EQP_FINAL_GROUPS)
             else:
                 self._issue_global(s)
             self.h.launch_equihash_verify_slots(self.verify_kernel, self.h0, self.msgs.data_ptr(), self.input_len,

@@ -67,11 +67,12 @@ def main() -> int:
 
     def make(c):
         if isinstance(c[0], str):
-            f = c[0].split(":")  # ps[:groups[:block]]
+            f = c[0].split(":")  # ps[:groups[:block[:final_groups]]]
             g = int(f[1]) if len(f) > 1 else 32
             blk = int(f[2]) if len(f) > 2 else 1024
+            fin = int(f[3]) if len(f) > 3 else None
             return EquihashSolver(num_inst=a.inst, device=0, engine="ps", groups=g, block=blk,
-                                  code_object=ps_objs[c[1]])
+                                  code_object=ps_objs[c[1]], final_groups=fin)
         return EquihashSolver(num_inst=a.inst, device=0, engine="global", banks=c[0], code_object=objs[c[1]])
 
     solvers = {c: make(c) for c in cfgs}
