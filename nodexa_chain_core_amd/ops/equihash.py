@@ -93,7 +93,7 @@ def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | 
 
 class EquihashSolver:
     def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 8,
-                 code_object: str | None = None, engine: str | None = None, groups: int = 32,
+                 code_object: str | None = None, engine: str | None = None, groups: int | None = None,
                  block: int = 1024, final_groups: int | None = None):
         """`code_object`: path of an alternative build of the engine's .hip (tuning sweeps).
         `engine`: "ps" (private slot segments, `groups` workgroups per instance per round) or
@@ -102,10 +102,15 @@ class EquihashSolver:
         if self.engine not in ("ps", "global"):
             raise ValueError(f"unknown Equihash engine {self.engine!r}")
         self.banks = int(banks)
-        self.groups = int(groups)
+        # ps writers per instance: one 1024-thread workgroup per CU over the whole launch (P x
+        # instances = 256: 32 at 8 instances, 16 at the mining window's 16; profiles/README r4k:
+        # 8.50 vs 8.65 ms at 16 instances, and 7.48 vs 4.38 ms when P=16 leaves half the CUs idle at 8)
+        self.groups = int(groups) if groups else min(256, max(16, 1 << max(0, (256 // max(1, int(num_inst))).bit_length() - 1)))
         self.block = int(block)  # ps: threads per workgroup, must match the code object's EQP_BLOCK
-        # ps: workgroups per instance of the final round (it writes no level, so any width works)
-        self.final_groups = int(final_groups or os.environ.get("NODEXA_EQP_FINAL_GROUPS", 0) or 0)
+        # ps: workgroups per instance of the final round (it writes no level, so any width works):
+        # ~4096 over the launch (256 at 16 instances: -1 % against 1024, r4k)
+        self.final_groups = int(final_groups or os.environ.get("NODEXA_EQP_FINAL_GROUPS", 0) or 0) or \
+            min(1024, max(64, 4096 // max(1, int(num_inst))))
         runtime.require_gpu()
         self.h = runtime.hip()
         self.num_inst = int(num_inst)
@@ -187,7 +192,7 @@ class EquihashSolver:
                                                 self.num_inst, self.groups, self.hashes.data_ptr(),
                                                 self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
                                                 self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block,
-                                                self.final_groups or self.h.EQP_FINAL_GROUPS)
+                                                self.final_groups)
             else:
                 self._issue_global(s)
             self.h.launch_equihash_verify_slots(self.verify_kernel, self.h0, self.msgs.data_ptr(), self.input_len,

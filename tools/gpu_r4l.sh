@@ -1,0 +1,11 @@
+#!/bin/bash
+# r4l: Equihash with writers per instance sized to fill the CUs (16 at the mining window's 16
+# instances) and a 256-wide final round: the exactness and mining GPU tests, then the bench line.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r4l
+mkdir -p $O
+timeout -k 10 500 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_equihash.py \
+  tests/test_gpu_equihash_mining.py tests/test_gpu_eq_graph.py > $O/pytest.log 2>&1 || exit $?
+timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit $?
+echo "exit=0"
