@@ -8,4 +8,7 @@ mkdir -p $O
 timeout -k 10 500 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_equihash.py \
   tests/test_gpu_equihash_mining.py tests/test_gpu_eq_graph.py > $O/pytest.log 2>&1 || exit $?
 timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit $?
+# producer threads per round workgroup (EQP_NP) re-swept in the new shape (r4m)
+timeout -k 10 500 python3 tools/equihash_bench.py --inst 16 --batches 10 --engines ps:16:1024:256 \
+  --variants "" EQP_NP=384 EQP_NP=512 EQP_NP=576 > $O/eq_np.jsonl 2> $O/eq_np.err || exit $?
 echo "exit=0"
