@@ -11,4 +11,7 @@ timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit $?
 # producer threads per round workgroup (EQP_NP) re-swept in the new shape (r4m)
 timeout -k 10 500 python3 tools/equihash_bench.py --inst 16 --batches 10 --engines ps:16:1024:256 \
   --variants "" EQP_NP=384 EQP_NP=512 EQP_NP=576 > $O/eq_np.jsonl 2> $O/eq_np.err || exit $?
+# EA write requests per kernel in the 16-writer shape (r4c: the 32-writer shape at 8 instances)
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum -d $O/pmc16 -o eq \
+  --output-format csv -- python3 tools/equihash_bench.py --engines ps --inst 16 --batches 1 > $O/pmc16.log 2>&1 || exit $?
 echo "exit=0"
