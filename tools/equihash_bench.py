@@ -68,7 +68,7 @@ def main() -> int:
     def make(c):
         if isinstance(c[0], str):
             f = c[0].split(":")  # ps[:groups[:block[:final_groups]]]
-            g = int(f[1]) if len(f) > 1 else 32
+            g = int(f[1]) if len(f) > 1 else None  # None: the solver's own choice (P x instances = 256)
             blk = int(f[2]) if len(f) > 2 else 1024
             fin = int(f[3]) if len(f) > 3 else None
             return EquihashSolver(num_inst=a.inst, device=0, engine="ps", groups=g, block=blk,
