@@ -143,7 +143,7 @@ def _equihash_bench(args, hdr, height: int, rank: int, log) -> dict:
     packet (miner/equihash_search.EquihashGpuDevice: 16 solver instances per window, two windows in
     flight, every solution verified on the device, SHA256d of the candidate headers on the host),
     the same collectives as the KawPow loop. Sol/s = all ranks' distinct valid solutions over the
-    slowest rank's time. The standalone solver (two 8-instance launches in flight, host-verified)
+    slowest rank's time. The standalone solver (two 16-instance launches in flight, device verdicts)
     is timed after it for comparison."""
     import torch
 
@@ -191,20 +191,21 @@ def _equihash_bench(args, hdr, height: int, rank: int, log) -> dict:
     if W.all_reduce_sum_int(bad):
         raise SystemExit("Equihash shares of the mining loop failed the host check")
     del svc, edev
-    # the standalone solver: two launches in flight, host-verified solutions
-    solver = EquihashSolver(num_inst=8)
+    # the standalone solver: two launches in flight, every solution checked on the device (as in
+    # the loop), at the loop's 16 instances per launch
+    solver = EquihashSolver(num_inst=16)
     mk = lambda i, j: prefix + struct.pack("<QQQQ", rank, i, j, 0xE9)  # noqa: E731
-    solver.solve([mk(-1 & 0xFFFF, j) for j in range(8)])
+    solver.solve([mk(-1 & 0xFFFF, j) for j in range(16)])
     torch.cuda.synchronize()
     W.barrier()
     t0 = time.perf_counter()
     found = 0
-    nb = max(1, args.equihash * 2)
+    nb = max(1, args.equihash)
     for i in range(nb):
-        solver.launch([mk(i, j) for j in range(8)])
+        solver.launch([mk(i, j) for j in range(16)])
         if i >= 1:
-            found += sum(len(s) for s in solver.collect())
-    found += sum(len(s) for s in solver.collect())
+            found += sum(len(s) for s in solver.collect_arrays(verify="device"))
+    found += sum(len(s) for s in solver.collect_arrays(verify="device"))
     torch.cuda.synchronize()
     sdt = W.all_reduce_max(time.perf_counter() - t0)
     solo = W.all_reduce_sum_int(found) / sdt
