@@ -108,15 +108,29 @@ def _grouped(jobs: np.ndarray, device):
 
 
 def _run_dag(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
-    """Resident-DAG batch: one job per 16-lane group with its period's program staged in LDS
-    (kawpow_verify_dag), so headers of thousands of different periods share one dense launch."""
+    """Resident-DAG batch: one job per 16-lane group, headers of thousands of different periods in
+    one dense launch. kawpow_verify_waves (jobs grouped by period four to a wave64, the program
+    wave-uniform, the mix in VGPRs) unless NODEXA_VERIFY_WAVES=0 selects kawpow_verify_dag (each
+    group's program and mix in LDS)."""
+    from . import header_batch as HB
+
     m = len(jobs)
     dj, progs, nprog, jp = _grouped(jobs, ep.device)
     res = torch.empty(m * 16, dtype=torch.int32, device=ep.device)
-    runtime.hip().launch_kawpow_verify_dag(
-        runtime.static_kernel("kawpow_verify_light", "kawpow_verify_dag"), ep.dag.data_ptr(), ep.items2048,
-        ep.l1.data_ptr(), dj.data_ptr(), progs.data_ptr(), nprog, jp.data_ptr(), m, res.data_ptr(),
-        runtime.current_stream_handle())
+    h = runtime.hip()
+    if HB.WAVES:
+        heights = np.ascontiguousarray(_block_numbers(jobs), dtype="<u4")
+        slots = np.frombuffer(_core.wave_slots(np.zeros(m, dtype=np.uint8), heights, 0, m), dtype=np.int32)
+        ds = torch.from_numpy(slots.copy()).to(ep.device)
+        h.launch_kawpow_verify_waves(runtime.static_kernel("kawpow_verify_light", "kawpow_verify_waves"),
+                                     ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(), dj.data_ptr(),
+                                     progs.data_ptr(), nprog, jp.data_ptr(), m, ds.data_ptr(), len(slots),
+                                     res.data_ptr(), runtime.current_stream_handle())
+    else:
+        h.launch_kawpow_verify_dag(
+            runtime.static_kernel("kawpow_verify_light", "kawpow_verify_dag"), ep.dag.data_ptr(), ep.items2048,
+            ep.l1.data_ptr(), dj.data_ptr(), progs.data_ptr(), nprog, jp.data_ptr(), m, res.data_ptr(),
+            runtime.current_stream_handle())
     return res.cpu().numpy().view(np.uint8).reshape(m, 64)
 
 
