@@ -73,6 +73,18 @@
 #define EQP_INST_GRP(inst, grp) const uint32_t inst = blockIdx.y, grp = blockIdx.x
 #endif
 
+// EQP_NO_ROW_STORE (measurement only, results invalid): the row stores compiled out, the rest of
+// each kernel (gathers, chains, slot counters, back-pointer copies) unchanged -- what the rows'
+// own stores cost in time and in EA write requests (profiles/README r4r).
+#ifdef EQP_NO_ROW_STORE
+#define EQP_ROW_STORE(...) \
+    do {                   \
+        (void)r;           \
+    } while (0)
+#else
+#define EQP_ROW_STORE(...) __VA_ARGS__
+#endif
+
 // Payload words of a level-`level` row: 6, 6, 5, 4, 4, 3, 3, 2, 1.
 constexpr int eqp_payload(int level) { return (188 - 20 * level + 31) / 32; }
 // Words per row slot in global memory: the payload plus the back-pointer, except that a 28-byte
@@ -152,7 +164,7 @@ extern "C" __global__ __launch_bounds__(EQP_BLOCK) void eqp_gen(EquihashPsDev p)
 #pragma unroll
                 for (int k = 0; k < eqp_words(0) - 1; ++k)
                     r.w[1 + k] = k < eqp_payload(0) ? (w[k + 1] << 12) | (w[k + 2] >> 20) : 0u;
-                *(EqpRow<eqp_words(0)>*)(p.hashes + eqp_hidx<0>(p, inst, nb, grp, slot)) = r;
+                EQP_ROW_STORE(*(EqpRow<eqp_words(0)>*)(p.hashes + eqp_hidx<0>(p, inst, nb, grp, slot)) = r);
             }
         }
     }
@@ -329,7 +341,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
 #pragma unroll
                         for (int q = 0; q < WO - 1; ++q)
                             r.w[1 + q] = q < MO ? (x[q] << 20) | (q + 1 < ST ? x[q + 1] >> 12 : 0u) : 0u;
-                        *(EqpRow<WO>*)(p.hashes + eqp_hidx<R>(p, inst, nb, grp, slot)) = r;
+                        EQP_ROW_STORE(*(EqpRow<WO>*)(p.hashes + eqp_hidx<R>(p, inst, nb, grp, slot)) = r);
                     }
                 }
                 truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
