@@ -64,6 +64,19 @@ def test_record_roundtrip():
     assert unpack_record(pack_record(SlotResult(4, 0, 65536, 8, lg, 1.0, 0, ALGO_X16RV2))).shares == lg
 
 
+def test_record_totals_replace_the_counter_all_reduce():
+    """The step's hash counter and next-epoch votes ride in the gathered records: every rank sums
+    them from the all-gather (one collective less per step than an all-reduce of their own)."""
+    from nodexa_chain_core_amd.miner.search import SlotResult
+    from nodexa_chain_core_amd.miner.service import pack_record, record_totals
+
+    recs = [pack_record(SlotResult(1, 0, 4096, 4096, [], 1.0), vote=True),
+            pack_record(None, vote=True),
+            pack_record(SlotResult(1, 4096, 4096, 4000, [], 1.0), vote=False)]
+    assert record_totals(recs) == (8096, 2)
+    assert record_totals([pack_record(None)]) == (0, 0)
+
+
 def test_single_rank_loop_mines_blocks(state):
     from nodexa_chain_core_amd.miner.search import CpuSearchDevice
     from nodexa_chain_core_amd.miner.service import ChainLeader, MiningService
