@@ -183,3 +183,29 @@ def test_p2p_header_sync_takes_the_resident_path(core, gpu, tmp_path):
         if b is not None:
             b.stop()
         a.stop()
+
+
+def test_miner_dag_doubles_as_verify_epoch(core, gpu):
+    """A mining node's DAG (miner/search.GpuSearchDevice) is offered to batch verify
+    (ops/verify.share_epoch): resident_ready() then sends epoch-0 header batches down the resident
+    path, and that path runs on the miner's own DAG tensor (no second build)."""
+    from nodexa_chain_core_amd.miner.search import GpuSearchDevice
+    from nodexa_chain_core_amd.models.verify import process_batch_resident, resident_ready
+    from nodexa_chain_core_amd.ops import verify as V
+
+    params, hs, raw = _load(core, "testnet_kawpow_10k.hdr")
+    act = params.kawpow_activation_time
+    V._epochs.pop((0, 0), None)
+    dev = GpuSearchDevice(0)
+    try:
+        dev.searcher(5)  # builds (or reuses) epoch 0 for mining
+        mined = dev.epochs[0]
+        assert V._epochs.get((0, 0)) is mined
+        batch_hs = hs[:2000]  # heights 1..2000: epoch 0 only
+        assert resident_ready(batch_hs, act, 0, "auto")
+        c = core.HeaderChain(params)
+        r = process_batch_resident(c, core.HeaderBatch.from_headers(batch_hs, act), hs[-1].time + 3600, device=0)
+        assert r["accepted"] == 2000 and r["reject"] is None
+        assert V._epochs.get((0, 0)) is mined  # verify used it, built nothing of its own
+    finally:
+        dev.close()
