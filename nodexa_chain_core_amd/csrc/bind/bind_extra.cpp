@@ -489,7 +489,7 @@ void bind_extra(py::module_& m) {
 
     // ------------------------------------------------ HeaderBatch (models/verify.py resident pipeline)
     static_assert(sizeof(Uint256) == 32, "hash blobs are read as Uint256 arrays");
-    auto view = [](const std::string& s) {  // zero-copy, read-only: the batch must outlive it
+    auto view = [](const auto& s) {  // zero-copy, read-only: the batch must outlive it
         return py::memoryview::from_memory(const_cast<char*>(s.data()), py::ssize_t(s.size()), true);
     };
     m.def("wave_slots", [](const py::buffer& kinds_buf, const py::buffer& heights_buf, size_t lo, size_t hi) {
@@ -525,8 +525,19 @@ void bind_extra(py::module_& m) {
             const py::buffer_info bi = buf.request();
             const u8* p = static_cast<const u8*>(bi.ptr);
             const size_t len = size_t(bi.size) * size_t(bi.itemsize);
+            // an immutable bytes object is read in place by the deferred decode (the batch holds a
+            // reference); any other buffer could change under it, so its records are copied
+            std::shared_ptr<const void> keep;
+            if (PyBytes_Check(buf.ptr())) {
+                PyObject* o = buf.ptr();
+                Py_INCREF(o);
+                keep = std::shared_ptr<const void>(o, [](const void* q) {
+                    py::gil_scoped_acquire g;
+                    Py_DECREF(reinterpret_cast<PyObject*>(const_cast<void*>(q)));
+                });
+            }
             py::gil_scoped_release rel;
-            return std::make_shared<HeaderBatch>(HeaderBatch::from_bytes(p, len, act));
+            return std::make_shared<HeaderBatch>(HeaderBatch::from_bytes(p, len, act, std::move(keep)));
         }, py::arg("data"), py::arg("kawpow_activation_time"),
            "parse concatenated serialized headers (80 / 120 / Equihash-extended) and pack them")
         .def_static("from_headers", [](std::vector<BlockHeader> hs, u32 act) {
@@ -546,19 +557,36 @@ void bind_extra(py::module_& m) {
         .def_property_readonly("eq_ser", [view](const HeaderBatch& b) { return view(b.eq_ser); })
         .def_readonly("eq_ser_len", &HeaderBatch::eq_ser_len)
         .def_readonly("eq_uniform", &HeaderBatch::eq_uniform)
-        .def("header", [](const HeaderBatch& b, size_t i) {
-            if (i >= b.hs.size()) throw py::index_error();
+        .def("materialize", [](HeaderBatch& b) {
+            py::gil_scoped_release rel;
+            b.materialize();
+        }, "decode the wire records into header objects now (from_bytes defers it; every accessor "
+           "below does it on first use)")
+        .def("header", [](HeaderBatch& b, size_t i) {
+            if (i >= b.size()) throw py::index_error();
+            {
+                py::gil_scoped_release rel;
+                b.materialize();
+            }
             return b.hs[i];
         })
-        .def("headers", [](const HeaderBatch& b, size_t lo, size_t hi) {
+        .def("headers", [](HeaderBatch& b, size_t lo, size_t hi) {
+            {
+                py::gil_scoped_release rel;
+                b.materialize();
+            }
             hi = std::min(hi, b.hs.size());
             return std::vector<BlockHeader>(b.hs.begin() + std::min(lo, hi), b.hs.begin() + hi);
         }, py::arg("lo") = 0, py::arg("hi") = size_t(-1));
 
     py::class_<HeaderChain, std::shared_ptr<HeaderChain>>(m, "HeaderChain")
         .def("accept_batch",
-             [](HeaderChain& c, const HeaderBatch& b, int64_t adjusted_time, const py::object& hashes,
+             [](HeaderChain& c, HeaderBatch& b, int64_t adjusted_time, const py::object& hashes,
                 const py::object& bits, size_t lo, size_t hi) {
+                 {
+                     py::gil_scoped_release rel;
+                     b.materialize();
+                 }
                  // accept_headers over batch headers [lo, hi) with the device pipeline's block hashes
                  // (n x 32, storage order) and DGW nBits (n x u32, 0 = host decides), both indexed
                  // by batch position: (accepted, reject reason or None, dos)

@@ -7,42 +7,93 @@
 
 namespace nodexa {
 
-HeaderBatch HeaderBatch::from_bytes(const u8* data, size_t len, u32 act) {
+HeaderBatch HeaderBatch::from_bytes(const u8* data, size_t len, u32 act, std::shared_ptr<const void> keep) {
     HeaderBatch b;
     b.act = act;
+    b.keep_ = std::move(keep);
+    b.src_ = b.keep_ ? data : nullptr;
     // one cheap serial scan for the record boundaries (80 / 120 / extended by version bit and
-    // nTime), then every header is decoded in parallel straight from the caller's buffer
-    std::vector<size_t> off;
-    off.reserve(len / 120 + 1);
+    // nTime) and the Equihash records; everything else is one parallel pass over the wire bytes
+    std::vector<size_t>& off = b.off_;
+    off.reserve(len / 120 + 2);
+    std::vector<u32> sol_at;  // offset of each Equihash solution within its record
     size_t o = 0;
     while (o < len) {
         if (len - o < 80) throw std::out_of_range("HeaderBatch: truncated header");
-        off.push_back(o);
         const u32 version = load_le32(data + o);
         const u32 time = load_le32(data + o + 68);
         if (version & u32(kEquihashVersionBit)) {
-            Reader r(data + o + 112, len - std::min(len, o + 112));
+            if (len - o < 112) throw std::out_of_range("HeaderBatch: truncated header");
+            Reader r(data + o + 112, len - o - 112);
             const u64 sol = r.compact_size();
+            if (sol > 4096) throw std::runtime_error("equihash solution too large");
+            b.eq_index.push_back(u32(off.size()));
+            sol_at.push_back(u32(sol == 1344 ? 112 + r.pos() : 0));
+            off.push_back(o);
             o += 112 + r.pos() + sol;
         } else {
+            off.push_back(o);
             o += time < act ? 80 : 120;
         }
     }
     if (o != len) throw std::out_of_range("HeaderBatch: truncated header");
-    b.hs.resize(off.size());
-    parallel_for_each(off.size(), [&](size_t i) {
-        const size_t end = i + 1 < off.size() ? off[i + 1] : len;
-        Reader r(data + off[i], end - off[i]);
-        b.hs[i] = BlockHeader::deserialize(r, act);
+    const size_t n = off.size();
+    off.push_back(len);
+    b.n_ = n;
+    b.materialized_ = false;
+    if (!b.keep_) b.raw_.resize(len);
+    b.kinds.resize(n);
+    b.rows.resize(n * kBatchRow);
+    const size_t m = b.eq_index.size();
+    b.eq_ser_len = m ? off[b.eq_index[0] + 1] - off[b.eq_index[0]] : 0;
+    b.eq_msgs.assign(m * 128, '\0');
+    b.eq_sols.assign(m * 1344, '\0');
+    b.eq_ser.resize(m * b.eq_ser_len);
+    bool uniform = true;
+    for (size_t k = 0; k < m; ++k) {
+        const size_t i = b.eq_index[k];
+        uniform = uniform && sol_at[k] != 0 && off[i + 1] - off[i] == b.eq_ser_len;
+    }
+    b.eq_uniform = uniform;
+    char* raw = b.keep_ ? nullptr : b.raw_.data();
+    parallel_for_each(n, [&](size_t i) {
+        const u8* src = data + off[i];
+        const size_t rl = off[i + 1] - off[i];
+        if (raw) std::memcpy(raw + off[i], src, rl);
+        u8* row = reinterpret_cast<u8*>(&b.rows[i * kBatchRow]);
+        const bool eq = load_le32(src) & u32(kEquihashVersionBit);
+        const size_t keep = eq ? 80 : rl;  // nHeight sits at bytes 76..79 of the Equihash prefix
+        std::memcpy(row, src, keep);
+        std::memset(row + keep, 0, kBatchRow - keep);
+        b.kinds[i] = eq ? 2 : rl == 80 ? 3 : 0;
     }, 512);
-    b.pack();
+    parallel_for_each(m, [&](size_t k) {
+        const size_t i = b.eq_index[k];
+        const u8* src = data + off[i];
+        std::memcpy(&b.eq_msgs[k * 128], src, 112);  // CKAWPOWInput (80 bytes) + nNonce256
+        if (sol_at[k]) std::memcpy(&b.eq_sols[k * 1344], src + sol_at[k], 1344);
+        if (off[i + 1] - off[i] == b.eq_ser_len) std::memcpy(&b.eq_ser[k * b.eq_ser_len], src, b.eq_ser_len);
+    }, 16);
     return b;
+}
+
+void HeaderBatch::materialize() {
+    std::lock_guard<std::mutex> lk(*mu_);
+    if (materialized_) return;
+    hs.resize(n_);
+    const u8* raw = keep_ ? src_ : reinterpret_cast<const u8*>(raw_.data());
+    parallel_for_each(n_, [&](size_t i) {
+        Reader r(raw + off_[i], off_[i + 1] - off_[i]);
+        hs[i] = BlockHeader::deserialize(r, act);
+    }, 512);
+    materialized_ = true;
 }
 
 HeaderBatch HeaderBatch::from_headers(std::vector<BlockHeader> headers, u32 act) {
     HeaderBatch b;
     b.act = act;
     b.hs = std::move(headers);
+    b.n_ = b.hs.size();
     b.pack();
     return b;
 }
@@ -50,7 +101,7 @@ HeaderBatch HeaderBatch::from_headers(std::vector<BlockHeader> headers, u32 act)
 void HeaderBatch::pack() {
     const size_t n = hs.size();
     kinds.assign(n, '\0');
-    rows.assign(n * kBatchRow, '\0');
+    rows.assign(n * kBatchRow, '\0');  // (the object path fills only the fields it writes)
     eq_index.clear();
     for (size_t i = 0; i < n; ++i)
         if (hs[i].is_equihash()) eq_index.push_back(u32(i));

@@ -13,9 +13,17 @@
 //   eq_*   the Equihash headers: their batch index, 128-byte BLAKE2b message blocks (the 112-byte
 //          input), packed 1344-byte solutions and the serialized headers (for SHA256d).
 // HeaderChain::accept_headers then reads the batch's own headers (a contiguous range of them).
+//
+// from_bytes packs all of that straight from the wire bytes (a KawPow row IS its 120-byte wire
+// form, a legacy or Equihash row the first 80 bytes of its, an Equihash input the first 112) and
+// defers the BlockHeader objects: materialize() decodes them later, so the resident pipeline
+// (ops/header_batch.py) decodes while the device verifies, and only the accept stays after it.
 #pragma once
 
+#include <memory>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "primitives.hpp"
@@ -24,19 +32,60 @@ namespace nodexa {
 
 constexpr size_t kBatchRow = 128;
 
+// Byte buffer whose resize leaves new bytes uninitialised: the batch's packing passes write every
+// byte of the 1.3 MB row array themselves, in parallel, so a serial zero fill would be pure cost.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <class U>
+    void construct(U* p) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+using RawBytes = std::vector<char, NoInitAlloc<char>>;
+
 struct HeaderBatch {
     u32 act = 0;
-    std::vector<BlockHeader> hs;
-    std::string kinds, rows;
+    std::vector<BlockHeader> hs;  // complete once materialize() has run (from_headers: always)
+    RawBytes kinds, rows;
     std::vector<u32> eq_index;
     std::string eq_msgs, eq_sols, eq_ser;
     size_t eq_ser_len = 0;   // bytes of one serialized Equihash header (all equal for (200, 9))
     bool eq_uniform = true;  // every Equihash header has a well-formed 1344-byte solution
 
-    static HeaderBatch from_bytes(const u8* data, size_t len, u32 kawpow_activation_time);
+    // `keep`: an owner of `data` that keeps it alive and unchanged for the batch's lifetime (an
+    // immutable Python bytes object): the deferred decode then reads it in place, else the wire
+    // records are copied
+    static HeaderBatch from_bytes(const u8* data, size_t len, u32 kawpow_activation_time,
+                                  std::shared_ptr<const void> keep = nullptr);
     static HeaderBatch from_headers(std::vector<BlockHeader> headers, u32 kawpow_activation_time);
     void pack();
-    size_t size() const { return hs.size(); }
+    // decode the wire records into hs (parallel; no-op when done; concurrent callers wait for one)
+    void materialize();
+    const std::vector<BlockHeader>& headers() {
+        materialize();
+        return hs;
+    }
+    size_t size() const { return n_; }
+
+private:
+    std::string raw_;          // the wire records, back to back (from_bytes without an owner)
+    std::shared_ptr<const void> keep_;
+    const u8* src_ = nullptr;  // the owner's bytes (keep_ set)
+    std::vector<size_t> off_;  // record offsets into raw_ (and raw_.size() at the end)
+    size_t n_ = 0;
+    bool materialized_ = true;
+    std::shared_ptr<std::mutex> mu_ = std::make_shared<std::mutex>();  // shared_ptr: the batch stays movable
 };
 
 }  // namespace nodexa

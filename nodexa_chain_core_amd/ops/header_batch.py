@@ -145,11 +145,12 @@ class ResidentHeaderVerifier:
         slots[np.repeat(base, length) + pos] = (r - lo).astype(np.int32)
         return slots
 
-    def run(self, params, batch, series, plan: dict | None = None, world=None) -> dict:
+    def run(self, params, batch, series, plan: dict | None = None, world=None, overlap=None) -> dict:
         """Verify the PoW of every header and compute every header's DGW nBits on the device.
         `series`: (ancestor times bytes, ancestor bits bytes, a, base_height) of the batch's parent
-        (HeaderChain.dgw_ancestors) or None. Returns codes (n,) u8, hashes (n, 32) u8, bits (n,) u32
-        as numpy views of the pinned result buffer, plus timings."""
+        (HeaderChain.dgw_ancestors) or None. `overlap`: host work to run while the device works
+        (models/verify.py passes the batch's deferred header decode). Returns codes (n,) u8, hashes
+        (n, 32) u8, bits (n,) u32 as numpy views of the pinned result buffer, plus timings."""
         from . import verify as V
 
         t0 = time.perf_counter()
@@ -291,12 +292,16 @@ class ResidentHeaderVerifier:
             self.out_host[:n * 37].copy_(self.out[:n * 37], non_blocking=True)
             self.ev_end.record(main)
         t_issue = time.perf_counter()
+        if overlap is not None:
+            overlap()
+        t_overlap = time.perf_counter()
         self.ev_end.synchronize()
         t_done = time.perf_counter()
         res = self.out_host.numpy()
         return {"codes": res[:n], "hashes": res[n:n * 33].reshape(n, 32), "bits": res[n * 33:n * 37].view("<u4"),
                 "pack_ms": (t_pack - t0) * 1e3, "issue_ms": (t_issue - t_pack) * 1e3,
-                "wait_ms": (t_done - t_issue) * 1e3, "device_ms": self.ev_start.elapsed_time(self.ev_end)}
+                "overlap_ms": (t_overlap - t_issue) * 1e3, "wait_ms": (t_done - t_overlap) * 1e3,
+                "device_ms": self.ev_start.elapsed_time(self.ev_end)}
 
     def _gather(self, world, n: int, per: int, lo_r: int, hi_r: int) -> None:
         """All ranks' codes and block hashes (33 bytes per row) into every rank's result buffer:

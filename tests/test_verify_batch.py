@@ -230,6 +230,44 @@ def test_header_batch_rows_and_accept_batch(core):
         core.HeaderBatch.from_bytes(raw[:-7], act)  # truncated
 
 
+def test_header_batch_wire_pack_equals_object_pack(core):
+    """from_bytes packs rows / kinds / Equihash inputs, solutions and serializations straight from
+    the wire records and decodes the header objects later (materialize): every packed byte equals
+    from_headers' packing of the decoded objects, legacy 80-byte records included."""
+    import os
+
+    import numpy as np
+
+    from nodexa_chain_core_amd.models import synthetic
+
+    path = os.path.join(os.path.dirname(__file__), "data", "testnet_mixed_10k.hdr")
+    params, hs = synthetic.load(path)
+    act = params.kawpow_activation_time
+    # a legacy (pre-KawPow) record in front: the same fields, 80-byte wire form
+    leg = core.BlockHeader()
+    leg.version, leg.prev, leg.merkle_root = 0x20000000, hs[0].prev, hs[0].merkle_root
+    leg.time, leg.bits, leg.nonce = act - 60, hs[0].bits, 12345
+    objs = [leg] + list(hs)
+    raw = b"".join(h.serialize(act) for h in objs)
+    a = core.HeaderBatch.from_bytes(raw, act)
+    b = core.HeaderBatch.from_headers(objs, act)
+    assert len(a) == len(b) == len(objs)
+    for name in ("rows", "kinds", "eq_index", "eq_msgs", "eq_sols", "eq_ser"):
+        assert bytes(getattr(a, name)) == bytes(getattr(b, name)), name
+    assert (a.eq_ser_len, a.eq_uniform) == (b.eq_ser_len, b.eq_uniform)
+    assert np.frombuffer(a.kinds, np.uint8)[0] == 3
+    a.materialize()
+    a.materialize()  # idempotent
+    for i in (0, 1, 2, 5000, len(objs) - 1):
+        assert a.header(i).serialize(act) == objs[i].serialize(act)
+    # an accessor decodes on first use without an explicit materialize
+    c = core.HeaderBatch.from_bytes(raw, act)
+    assert [h.serialize(act) for h in c.headers(0, 3)] == [h.serialize(act) for h in objs[:3]]
+    bad = bytearray(raw[80:80 + 120 * 3])
+    with pytest.raises(Exception):
+        core.HeaderBatch.from_bytes(bytes(bad[:-1]), act)
+
+
 def _serial(params, headers, adj, check_pow=False, chain=None):
     c = chain or _core.HeaderChain(params)
     out = []

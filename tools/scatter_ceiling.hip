@@ -56,6 +56,45 @@ __global__ __launch_bounds__(256) void scatter(uint32_t* __restrict__ buf, uint3
     }
 }
 
+// L2 write merging probe: rows written by DIFFERENT store instructions (other lanes, waves and
+// workgroups) into the same 128-byte lines. Workgroup b writes its 256 x PER rows of S bytes at
+// random row positions of region r(b); BPR workgroups share a region of BPR * 256 * PER rows, so
+// each line is filled by ~128/S stores from as many workgroups, close together in time. XCD = 1:
+// only workgroups of one XCD share a region (b and b + 8 share an XCD); XCD = 0: consecutive
+// workgroups (eight XCDs) share it. EA write requests per row ~1 mean no merging in L2.
+template <int S, bool XCD>
+__global__ __launch_bounds__(256) void l2merge(uint32_t* __restrict__ buf, uint32_t bpr, uint32_t nreg, uint32_t seed) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t reg = (XCD ? (b % 8) * (gridDim.x / 8 / bpr) + (b / 8) / bpr : b / bpr) % nreg;
+    const uint32_t rrows = bpr * 256 * PER;
+    const uint32_t gid = b * 256 + threadIdx.x;
+#pragma unroll 1
+    for (int k = 0; k < PER; ++k) {
+        const uint32_t row = mix32(seed ^ (gid * PER + k)) % rrows;
+        u32x4* dst = (u32x4*)(buf + ((size_t)reg * rrows + row) * (S / 4));
+#pragma unroll
+        for (int q = 0; q < S / 16; ++q) dst[q] = u32x4{gid, (uint32_t)k, seed, (uint32_t)q};
+    }
+}
+
+// Random row gathers: each lane reads PER rows of S bytes at random row positions of a `bytes`
+// working set (the price of a layout that moves the scatter to the next round's reads).
+template <int S>
+__global__ __launch_bounds__(256) void gather(const uint32_t* __restrict__ buf, uint32_t nrows, uint32_t seed,
+                                              uint32_t* __restrict__ sink) {
+    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+    uint32_t acc = 0;
+    u32x4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const uint32_t row = mix32(seed ^ (gid * PER + k)) % nrows;
+        v[k] = ((const u32x4*)(buf + (size_t)row * (S / 4)))[0];
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) acc ^= v[k].x + v[k].y + v[k].z + v[k].w;
+    if (acc == 0x12345678u) sink[0] = gid;
+}
+
 template <int S, int G, bool NT>
 static void run(const char* name, uint32_t* buf, size_t bytes, uint64_t lanes) {
     const uint32_t nruns = uint32_t(bytes / (size_t(G) * S));
@@ -82,7 +121,78 @@ static void run(const char* name, uint32_t* buf, size_t bytes, uint64_t lanes) {
     std::fflush(stdout);
 }
 
-int main() {
+template <int S, bool XCD>
+static void run_merge(const char* name, uint32_t* buf, size_t bytes, uint32_t bpr) {
+    const unsigned grid = 16384;  // 4M lanes x PER = 64M rows
+    const uint32_t rrows = bpr * 256 * PER;
+    const uint32_t nreg = uint32_t(bytes / (size_t(rrows) * S));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    l2merge<S, XCD><<<grid, 256>>>(buf, bpr, nreg, 1);
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+        CHECK(hipEventRecord(a));
+        l2merge<S, XCD><<<grid, 256>>>(buf, bpr, nreg, 2 + rep);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        best = ms < best ? ms : best;
+    }
+    const double rows = double(grid) * 256 * PER;
+    std::printf("{\"variant\":\"%s\",\"row_bytes\":%d,\"xcd_local\":%d,\"region_kib\":%u,\"ms\":%.3f,"
+                "\"grows_s\":%.2f}\n",
+                name, S, int(XCD), unsigned(size_t(rrows) * S / 1024), best, rows / best / 1e6);
+    std::fflush(stdout);
+}
+
+template <int S>
+static void run_gather(const char* name, uint32_t* buf, size_t ws, uint32_t* sink) {
+    const unsigned grid = 16384;
+    const uint32_t nrows = uint32_t(ws / S);
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    gather<S><<<grid, 256>>>(buf, nrows, 1, sink);
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+        CHECK(hipEventRecord(a));
+        gather<S><<<grid, 256>>>(buf, nrows, 2 + rep, sink);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        best = ms < best ? ms : best;
+    }
+    const double rows = double(grid) * 256 * PER;
+    std::printf("{\"variant\":\"%s\",\"row_bytes\":%d,\"ws_mib\":%u,\"ms\":%.3f,\"grows_s\":%.2f}\n", name, S,
+                unsigned(ws >> 20), best, rows / best / 1e6);
+    std::fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+    if (argc > 1 && argv[1][0] == 'm') {  // merge + gather probes only (tools/gpu_r4t.sh)
+        const size_t bytes = size_t(4) << 30;
+        uint32_t *buf = nullptr, *sink = nullptr;
+        CHECK(hipMalloc(&buf, bytes));
+        CHECK(hipMalloc(&sink, 64));
+        CHECK(hipMemset(buf, 0, bytes));
+        run_merge<16, true>("merge16-xcd-bpr1", buf, bytes, 1);    // 64 KiB regions, one workgroup each
+        run_merge<16, true>("merge16-xcd-bpr16", buf, bytes, 16);  // 1 MiB, 16 workgroups of one XCD
+        run_merge<16, true>("merge16-xcd-bpr64", buf, bytes, 64);  // 4 MiB
+        run_merge<16, false>("merge16-all-bpr16", buf, bytes, 16);  // 1 MiB shared by all XCDs
+        run_merge<16, false>("merge16-all-bpr64", buf, bytes, 64);
+        run_merge<32, true>("merge32-xcd-bpr16", buf, bytes, 16);
+        run_gather<16>("gather16-4g", buf, bytes, sink);
+        run_gather<16>("gather16-256m", buf, size_t(256) << 20, sink);
+        run_gather<16>("gather16-64m", buf, size_t(64) << 20, sink);
+        CHECK(hipFree(buf));
+        CHECK(hipFree(sink));
+        return 0;
+    }
     const size_t bytes = size_t(4) << 30;
     uint32_t* buf = nullptr;
     CHECK(hipMalloc(&buf, bytes));
