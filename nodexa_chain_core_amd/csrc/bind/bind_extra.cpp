@@ -7,6 +7,7 @@
 #include <thread>
 
 #include "../chain/headerbatch.hpp"
+#include "../util/workpool.hpp"
 #include "../chain/headerchain.hpp"
 #include "../chain/script.hpp"
 #include "../chain/validation.hpp"
@@ -492,6 +493,26 @@ void bind_extra(py::module_& m) {
     auto view = [](const auto& s) {  // zero-copy, read-only: the batch must outlive it
         return py::memoryview::from_memory(const_cast<char*>(s.data()), py::ssize_t(s.size()), true);
     };
+    m.def("copy_into", [](const py::buffer& dst, size_t offset, const py::buffer& src) {
+        // dst[offset : offset + len(src)] = src on all cores (dst: a writable buffer such as the
+        // numpy view of a pinned staging tensor; bounds checked): the resident verify stages its
+        // 1.3 MB of rows in a fraction of a single-threaded copy
+        const py::buffer_info db = dst.request(true), sb = src.request();
+        const size_t dlen = size_t(db.size) * size_t(db.itemsize), len = size_t(sb.size) * size_t(sb.itemsize);
+        if (offset > dlen || len > dlen - offset) throw std::out_of_range("copy_into: source does not fit");
+        const char* s = static_cast<const char*>(sb.ptr);
+        char* d = static_cast<char*>(db.ptr) + offset;
+        constexpr size_t kChunk = 64 << 10;
+        py::gil_scoped_release rel;
+        if (len < 4 * kChunk) {
+            std::memcpy(d, s, len);
+            return;
+        }
+        parallel_for_each((len + kChunk - 1) / kChunk, [&](size_t c) {
+            const size_t o = c * kChunk;
+            std::memcpy(d + o, s + o, std::min(kChunk, len - o));
+        }, 1);
+    }, py::arg("dst"), py::arg("offset"), py::arg("src"));
     m.def("wave_slots", [](const py::buffer& kinds_buf, const py::buffer& heights_buf, size_t lo, size_t hi) {
         // kawpow_verify_waves' slot table for the KawPow rows (kind 0) of [lo, hi): the rows grouped
         // by ProgPoW period (height / 3), 4 slots per wave64 (one 16-lane group each), -1 = idle

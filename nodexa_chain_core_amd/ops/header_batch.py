@@ -195,7 +195,7 @@ class ResidentHeaderVerifier:
                 stage[o:o + size] = np.frombuffer(arr, dtype=np.uint8) if not isinstance(arr, np.ndarray) else \
                     arr.view(np.uint8).ravel()[:size]
 
-        put("rows", rows.ravel())
+        _core.copy_into(stage, off["rows"][0], batch.rows)  # the 1.3 MB of rows on all cores
         put("kinds", kinds)
         if series is not None:
             times = np.empty(a + n, dtype="<u4")

@@ -268,6 +268,26 @@ def test_header_batch_wire_pack_equals_object_pack(core):
         core.HeaderBatch.from_bytes(bytes(bad[:-1]), act)
 
 
+def test_copy_into_is_bounded(core):
+    """_core.copy_into (the resident verify's row staging): a parallel copy into a writable buffer
+    at an offset, refusing anything that would not fit."""
+    import numpy as np
+
+    src = np.random.default_rng(1).integers(0, 256, 1 << 20, dtype=np.uint8)
+    dst = np.zeros((1 << 20) + 4096, dtype=np.uint8)
+    core.copy_into(dst, 4096, src)
+    assert bytes(dst[4096:]) == src.tobytes() and not dst[:4096].any()
+    small = np.zeros(16, dtype=np.uint8)
+    core.copy_into(small, 8, b"abcdefgh")
+    assert bytes(small[8:]) == b"abcdefgh"
+    with pytest.raises(Exception):
+        core.copy_into(small, 9, b"abcdefgh")
+    with pytest.raises(Exception):
+        core.copy_into(small, 17, b"")
+    with pytest.raises(Exception):
+        core.copy_into(b"read-only target", 0, b"x")
+
+
 def _serial(params, headers, adj, check_pow=False, chain=None):
     c = chain or _core.HeaderChain(params)
     out = []
