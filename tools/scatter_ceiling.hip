@@ -95,6 +95,76 @@ __global__ __launch_bounds__(256) void gather(const uint32_t* __restrict__ buf, 
     if (acc == 0x12345678u) sink[0] = gid;
 }
 
+// Equihash-shaped append probe: 256 workgroups of 1024 threads = 16 instances x 16 writers, each
+// thread appending ROWS_PER_THREAD rows of S bytes to random buckets of its instance (4096 buckets,
+// 2^21 rows per instance, 512 per bucket on average). GLOBAL = 0: the private-slot scheme of
+// equihash_ps.hip (LDS slot counters, writer-private segments of SEG slots in every bucket);
+// GLOBAL = 1: one returning global atomic per row on the instance's bucket counter, so the rows
+// of all writers of a bucket land next to each other. XCD = 1 puts all 16 writers of an instance
+// on one XCD (instance = workgroup id mod 16), so with GLOBAL = 1 a bucket's tail line is written
+// by one L2 only.
+constexpr uint32_t AP_BUCKETS = 4096, AP_INST = 16, AP_WRITERS = 16, AP_SEG = 48, AP_CAP = AP_WRITERS * AP_SEG;
+constexpr int ROWS_PER_THREAD = 128;
+
+template <int S, bool GLOBAL, bool XCD>
+__global__ __launch_bounds__(1024) void append_probe(uint32_t* __restrict__ buf, uint32_t* __restrict__ gcnt,
+                                                     uint32_t seed, uint32_t* __restrict__ dropped) {
+    __shared__ uint32_t cnt2[AP_BUCKETS / 2];
+    const uint32_t lin = blockIdx.x;
+    const uint32_t inst = XCD ? lin % AP_INST : lin / AP_WRITERS, grp = XCD ? lin / AP_INST : lin % AP_WRITERS;
+    if (!GLOBAL) {
+        for (uint32_t k = threadIdx.x; k < AP_BUCKETS / 2; k += 1024) cnt2[k] = 0;
+        __syncthreads();
+    }
+    const uint32_t gid = lin * 1024 + threadIdx.x;
+    uint32_t drop = 0;
+#pragma unroll 1
+    for (int k = 0; k < ROWS_PER_THREAD; ++k) {
+        const uint32_t b = mix32(seed ^ (gid * ROWS_PER_THREAD + k)) % AP_BUCKETS;
+        size_t row;
+        if (GLOBAL) {
+            const uint32_t slot = atomicAdd(&gcnt[inst * AP_BUCKETS + b], 1u);
+            if (slot >= AP_CAP) { ++drop; continue; }
+            row = ((size_t)inst * AP_BUCKETS + b) * AP_CAP + slot;
+        } else {
+            const uint32_t sh = (b & 1u) << 4;
+            const uint32_t slot = (atomicAdd(&cnt2[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
+            if (slot >= AP_SEG) { ++drop; continue; }
+            row = ((size_t)inst * AP_BUCKETS + b) * AP_CAP + grp * AP_SEG + slot;
+        }
+        uint32_t* dst = buf + row * (S / 4);
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q) dst[q] = gid ^ (uint32_t)(k + q);
+    }
+    if (drop) atomicAdd(dropped, drop);
+}
+
+template <int S, bool GLOBAL, bool XCD>
+static void run_append(const char* name, uint32_t* buf, uint32_t* gcnt, uint32_t* dropped) {
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    float best = 1e30f;
+    for (int rep = 0; rep < 4; ++rep) {
+        CHECK(hipMemset(gcnt, 0, AP_INST * AP_BUCKETS * 4));
+        CHECK(hipMemset(dropped, 0, 4));
+        CHECK(hipEventRecord(a));
+        append_probe<S, GLOBAL, XCD><<<AP_INST * AP_WRITERS, 1024>>>(buf, gcnt, 7 + rep, dropped);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        if (rep) best = ms < best ? ms : best;  // rep 0 warms
+    }
+    uint32_t d = 0;
+    CHECK(hipMemcpy(&d, dropped, 4, hipMemcpyDeviceToHost));
+    const double rows = double(AP_INST) * AP_WRITERS * 1024 * ROWS_PER_THREAD;
+    std::printf("{\"variant\":\"%s\",\"row_bytes\":%d,\"global_atomic\":%d,\"xcd_local\":%d,\"ms\":%.3f,"
+                "\"grows_s\":%.2f,\"dropped\":%u}\n",
+                name, S, int(GLOBAL), int(XCD), best, rows / best / 1e6, d);
+    std::fflush(stdout);
+}
+
 template <int S, int G, bool NT>
 static void run(const char* name, uint32_t* buf, size_t bytes, uint64_t lanes) {
     const uint32_t nruns = uint32_t(bytes / (size_t(G) * S));
@@ -174,6 +244,26 @@ static void run_gather(const char* name, uint32_t* buf, size_t ws, uint32_t* sin
 }
 
 int main(int argc, char** argv) {
+    if (argc > 1 && argv[1][0] == 'a') {  // Equihash-shaped append probes (tools/gpu_r4v.sh)
+        uint32_t *buf = nullptr, *gcnt = nullptr, *dropped = nullptr;
+        const size_t bytes = size_t(AP_INST) * AP_BUCKETS * AP_CAP * 32;
+        CHECK(hipMalloc(&buf, bytes));
+        CHECK(hipMalloc(&gcnt, AP_INST * AP_BUCKETS * 4));
+        CHECK(hipMalloc(&dropped, 4));
+        CHECK(hipMemset(buf, 0, bytes));
+        run_append<24, false, false>("private24", buf, gcnt, dropped);
+        run_append<24, false, true>("private24-xcd", buf, gcnt, dropped);
+        run_append<24, true, false>("global24", buf, gcnt, dropped);
+        run_append<24, true, true>("global24-xcd", buf, gcnt, dropped);
+        run_append<32, false, false>("private32", buf, gcnt, dropped);
+        run_append<32, true, true>("global32-xcd", buf, gcnt, dropped);
+        run_append<16, false, false>("private16", buf, gcnt, dropped);
+        run_append<16, true, true>("global16-xcd", buf, gcnt, dropped);
+        CHECK(hipFree(buf));
+        CHECK(hipFree(gcnt));
+        CHECK(hipFree(dropped));
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'm') {  // merge + gather probes only (tools/gpu_r4t.sh)
         const size_t bytes = size_t(4) << 30;
         uint32_t *buf = nullptr, *sink = nullptr;
