@@ -585,11 +585,7 @@ void bind_extra(py::module_& m) {
            "below does it on first use)")
         .def("header", [](HeaderBatch& b, size_t i) {
             if (i >= b.size()) throw py::index_error();
-            {
-                py::gil_scoped_release rel;
-                b.materialize();
-            }
-            return b.hs[i];
+            return b.header(i);  // one record decoded if the batch is not materialized yet
         })
         .def("headers", [](HeaderBatch& b, size_t lo, size_t hi) {
             {

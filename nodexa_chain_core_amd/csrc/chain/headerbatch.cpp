@@ -77,6 +77,15 @@ HeaderBatch HeaderBatch::from_bytes(const u8* data, size_t len, u32 act, std::sh
     return b;
 }
 
+BlockHeader HeaderBatch::header(size_t i) {
+    std::lock_guard<std::mutex> lk(*mu_);
+    if (i >= n_) throw std::out_of_range("HeaderBatch: index out of range");
+    if (materialized_) return hs[i];
+    const u8* raw = keep_ ? src_ : reinterpret_cast<const u8*>(raw_.data());
+    Reader r(raw + off_[i], off_[i + 1] - off_[i]);
+    return BlockHeader::deserialize(r, act);
+}
+
 void HeaderBatch::materialize() {
     std::lock_guard<std::mutex> lk(*mu_);
     if (materialized_) return;

@@ -76,6 +76,8 @@ struct HeaderBatch {
         materialize();
         return hs;
     }
+    // header i, decoded on its own while the batch is not materialized yet
+    BlockHeader header(size_t i);
     size_t size() const { return n_; }
 
 private:

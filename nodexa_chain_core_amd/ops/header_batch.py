@@ -208,7 +208,12 @@ class ResidentHeaderVerifier:
             put("bits", bits)
         if nslots:
             put("slots", np.concatenate(slot_tabs))
-        if m:
+        if m == len(eq_index):  # every Equihash header is this rank's: the packed arrays as they are
+            put("eq_index", eq_index)
+            put("eq_msgs", batch.eq_msgs)
+            put("eq_sols", batch.eq_sols)
+            put("eq_ser", batch.eq_ser)
+        elif m:
             put("eq_index", eq_index[mine_eq].astype(np.uint32))
             put("eq_msgs", np.frombuffer(batch.eq_msgs, np.uint8).reshape(-1, 128)[mine_eq])
             put("eq_sols", np.frombuffer(batch.eq_sols, np.uint8).reshape(-1, 1344)[mine_eq])
