@@ -9,6 +9,12 @@
 // size (below) and (2) pipelines each workgroup's bucket sequence so that the gathers of the next
 // bucket run beside the collisions of the current one.
 //
+// Why not global per-bucket slots with an instance's writers on one XCD, so that one L2 merges
+// all writers' rows of a bucket (the L2 does merge different workgroups' stores into a line:
+// profiles/README r4t)? Each row then needs a returning global atomic, atomics execute at the
+// memory side, and they top out near 29.5 G/s against 47.7 G/s for private appends of 24-byte
+// rows (r4v); built into this engine it took 13.6 ms per 16-solve window against 8.6 (r4w).
+//
 // What bounds it (profiles/README r3_equihash): a random row store costs one memory transaction
 // whatever its size (tools/scatter_ceiling.hip: 22-24 G rows/s for 16-64 byte rows, against
 // 145 G/s when 4 lanes write one 128-byte run), and a level's rows go to 4096 buckets from every
@@ -61,20 +67,6 @@
 #define EQP_NP 448  // producer threads of a round workgroup (7 of its 16 waves)
 #endif
 
-// EQP_GLOBAL_SLOTS (measured variant, profiles/README r4w): rows are appended with one returning
-// global atomic per row on the instance's bucket counter (u32 [inst][LEVELS][BUCKETS] in p.counts)
-// instead of writer-private segments, so all writers' rows of a bucket are contiguous; with every
-// writer of an instance on one XCD (implied EQP_XCD_LOCAL) a bucket's tail line is written through
-// ONE L2, which merges the rows of different workgroups into full-line writes (r4t: 0.3-0.5 EA
-// requests per 16-byte row at 64 KiB-1 MiB of open lines per XCD, against 1.0 cross-XCD). The
-// round that consumes a level's bucket clears its counter, so the counters start every launch at
-// zero (allocated zeroed).
-#ifdef EQP_GLOBAL_SLOTS
-#ifndef EQP_XCD_LOCAL
-#define EQP_XCD_LOCAL
-#endif
-#endif
-
 // Instance and writer of this workgroup in a (writers x instances) grid. Workgroups are dispatched
 // to the 8 XCDs round-robin by linear id, so blockIdx.y = instance spreads every instance over all
 // XCDs; EQP_XCD_LOCAL (measured variant) takes instance = id mod instances instead, which keeps
@@ -122,12 +114,6 @@ NX_DEV size_t eqp_hidx(const EquihashPsDev& p, uint32_t inst, uint32_t bucket, u
     const size_t row = ((size_t)inst * EQ_BUCKETS + bucket) * EQP_SLOTS + grp * p.seg + slot;
     return (size_t)(L & 1) * buf_words + row * eqp_words(L);
 }
-
-#ifdef EQP_GLOBAL_SLOTS
-NX_DEV uint32_t* eqp_gcnt(const EquihashPsDev& p, uint32_t inst, int level) {
-    return reinterpret_cast<uint32_t*>(p.counts) + ((size_t)inst * EQ_LEVELS + level) * EQ_BUCKETS;
-}
-#endif
 
 // LDS slot counters, two u16 per word (the counts of one workgroup never reach 2^16).
 NX_DEV uint32_t eqp_take_slot(uint32_t* cnt2, uint32_t nb) {
@@ -177,35 +163,24 @@ extern "C" __global__ __launch_bounds__(EQP_BLOCK) void eqp_gen(EquihashPsDev p)
             uint32_t w[8];
             eq_leaf_words(out, half, w);
             const uint32_t nb = w[1] >> 20;  // bits [0, 12)
-#ifdef EQP_GLOBAL_SLOTS
-            const uint32_t slot = atomicAdd(eqp_gcnt(p, inst, 0) + nb, 1u), cap = EQP_STAGE, sg = 0;
-#else
-            const uint32_t slot = eqp_take_slot(cnt2, nb), cap = p.seg, sg = grp;
-#endif
-            if (slot < cap) {
+            const uint32_t slot = eqp_take_slot(cnt2, nb);
+            if (slot < p.seg) {
                 EqpRow<eqp_words(0)> r;
                 r.w[0] = 2 * g + half;
 #pragma unroll
                 for (int k = 0; k < eqp_words(0) - 1; ++k)
                     r.w[1 + k] = k < eqp_payload(0) ? (w[k + 1] << 12) | (w[k + 2] >> 20) : 0u;
-                EQP_ROW_STORE(*(EqpRow<eqp_words(0)>*)(p.hashes + eqp_hidx<0>(p, inst, nb, sg, slot)) = r);
+                EQP_ROW_STORE(*(EqpRow<eqp_words(0)>*)(p.hashes + eqp_hidx<0>(p, inst, nb, grp, slot)) = r);
             }
         }
     }
-#ifndef EQP_GLOBAL_SLOTS
     __syncthreads();
     eqp_flush_counts(p, inst, grp, 0, cnt2, 0);
-#endif
 }
 
 // Counts of bucket b of `level` into lane registers of the calling wave (lane l holds the counts
 // of segments l*per .. l*per+per-1, per = P / 64 rounded up).
 NX_DEV void eqp_load_counts(const EquihashPsDev& p, uint32_t inst, int level, uint32_t b, uint32_t v[4]) {
-#ifdef EQP_GLOBAL_SLOTS
-    v[0] = eqp_gcnt(p, inst, level)[b];  // the bucket's one counter (every lane: a broadcast load)
-    v[1] = v[2] = v[3] = 0;
-    return;
-#endif
     const uint32_t P = p.groups, lane = threadIdx.x & 63, per = (P + 63) / 64;
     const uint8_t* cin = p.counts + ((size_t)inst * EQ_LEVELS + level) * P * EQ_BUCKETS + b;
 #pragma unroll
@@ -271,34 +246,6 @@ NX_DEV void eqp_gather_rows(const EquihashPsDev& p, uint32_t inst, uint32_t b, c
     }
 }
 
-#ifdef EQP_GLOBAL_SLOTS
-// EQP_GLOBAL_SLOTS staging: bucket b's n rows are slots 0..n-1 of one contiguous run.
-template <int L, uint32_t NP>
-NX_DEV void eqp_gather_run(const EquihashPsDev& p, uint32_t inst, uint32_t b, uint32_t n, uint32_t* rows,
-                           uint32_t pt) {
-    constexpr int BATCH = 4, W = eqp_words(L), PL = eqp_payload(L), ST = eqp_lds_stride(L);
-    uint32_t* refs = p.refs + (((size_t)inst * EQ_LEVELS + L) * EQ_BUCKETS + b) * EQP_REF_STRIDE;
-    const EqpRow<W>* src = (const EqpRow<W>*)(p.hashes + eqp_hidx<L>(p, inst, b, 0, 0));
-#pragma unroll 1
-    for (uint32_t p0 = pt; p0 < n; p0 += NP * BATCH) {
-        EqpRow<W> r[BATCH];
-#pragma unroll
-        for (int k = 0; k < BATCH; ++k) {
-            const uint32_t pos = p0 + k * NP;
-            if (pos < n) r[k] = src[pos];
-        }
-#pragma unroll
-        for (int k = 0; k < BATCH; ++k) {
-            const uint32_t pos = p0 + k * NP;
-            if (pos >= n) continue;
-            refs[pos] = r[k].w[0];
-#pragma unroll
-            for (int q = 0; q < ST; ++q) rows[pos * ST + q] = q < PL ? r[k].w[1 + q] : 0u;
-        }
-    }
-}
-#endif
-
 // Round R (1..8): collide level R-1 on digit R-1 bucket by bucket, write level R. R = 9 is the
 // final round: level-8 rows colliding on d_8 and d_9 (40 bits) become candidates.
 //
@@ -332,18 +279,9 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     uint32_t dropped = 0, truncated = 0, staged_max = 0;
     // every producer wave scans the counts itself and gathers rows pos = thread, thread + NP, ...
     auto stage = [&](uint32_t bk, uint32_t buf) {
-#ifdef EQP_GLOBAL_SLOTS
-        // every producer wave reads the bucket's counter; the last wave to need it clears it
-        // (a barrier of the producer waves separates the reads from the clear: below)
-        const uint32_t total = cv[0];
-        const uint32_t n = min(total, (uint32_t)EQP_STAGE);
-        eqp_gather_run<R - 1, NP>(p, inst, bk, n, rows[buf], threadIdx.x);
-        (void)my_segc;
-#else
         const uint32_t total = eqp_wave_scan(P, cv, my_segc);
         const uint32_t n = min(total, (uint32_t)EQP_STAGE);
         eqp_gather_rows<R - 1, NP>(p, inst, bk, my_segc, n, rows[buf], threadIdx.x);
-#endif
         if (threadIdx.x == 0) {
             nstaged[buf] = n;
             dropped += total - n;
@@ -360,11 +298,6 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
         __syncthreads();  // A: rows[cur] staged, head reset, previous bucket's emission done
         const uint32_t n = nstaged[cur];
         const uint32_t* rc = rows[cur];
-#ifdef EQP_GLOBAL_SLOTS
-        // every producer wave consumed bucket b's counter in stage(b), before barrier A: clear it
-        // for the next launch (a vector store by one lane)
-        if (threadIdx.x == NP) __hip_atomic_store(eqp_gcnt(p, inst, R - 1) + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
         if (!producer) {
             for (uint32_t i = ct; i < n; i += NC) {
                 const uint32_t sub = rc[i * ST] >> 24;
@@ -407,18 +340,14 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
                     }
                     if (rest == 0) continue;  // identical remainder: only duplicate indices
                     const uint32_t nb = (x[0] >> 12) & 0xFFFu;
-#ifdef EQP_GLOBAL_SLOTS
-                    const uint32_t slot = atomicAdd(eqp_gcnt(p, inst, R) + nb, 1u), cap = EQP_STAGE, sg = 0;
-#else
-                    const uint32_t slot = eqp_take_slot(cnt2, nb), cap = p.seg, sg = grp;
-#endif
-                    if (slot < cap) {
+                    const uint32_t slot = eqp_take_slot(cnt2, nb);
+                    if (slot < p.seg) {
                         EqpRow<WO> r;
                         r.w[0] = (b << 20) | (i << 10) | (uint32_t)j;
 #pragma unroll
                         for (int q = 0; q < WO - 1; ++q)
                             r.w[1 + q] = q < MO ? (x[q] << 20) | (q + 1 < ST ? x[q + 1] >> 12 : 0u) : 0u;
-                        EQP_ROW_STORE(*(EqpRow<WO>*)(p.hashes + eqp_hidx<R>(p, inst, nb, sg, slot)) = r);
+                        EQP_ROW_STORE(*(EqpRow<WO>*)(p.hashes + eqp_hidx<R>(p, inst, nb, grp, slot)) = r);
                     }
                 }
                 truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
@@ -430,12 +359,7 @@ NX_DEV void eqp_round_impl(const EquihashPsDev& p) {
     // rows beyond a segment) are counted apart
     if (dropped) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_STAGE], dropped);
     if (threadIdx.x == 0) atomicMax(&p.stats[inst * EQP_STATS + EQP_STAT_STAGE_MAX], staged_max);
-#ifdef EQP_GLOBAL_SLOTS
-    if constexpr (R < 9) {  // rows beyond a bucket's EQP_STAGE slots are counted by its consumer
-    }
-#else
     if constexpr (R < 9) eqp_flush_counts(p, inst, grp, R, cnt2, 0);
-#endif
     if (truncated) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_CHAIN], truncated);
 }
 

@@ -130,9 +130,7 @@ class EquihashSolver:
                 S, R = self.h.EQP_SLOTS, self.h.EQP_REF_STRIDE
                 self.hashes = torch.empty(2 * ni * B * S * W, dtype=torch.int32, device=self.device)
                 self.refs = torch.empty(ni * L * B * R, dtype=torch.int32, device=self.device)
-                # zeroed once: an EQP_GLOBAL_SLOTS build keeps its bucket counters here and clears them as
-                # it consumes them (the default build rewrites every byte each launch)
-                self.counts = torch.zeros(ni * L * self.groups * B, dtype=torch.uint8, device=self.device)
+                self.counts = torch.empty(ni * L * self.groups * B, dtype=torch.uint8, device=self.device)
                 self.stats_buf = torch.zeros(ni * self.h.EQP_STATS, dtype=torch.int32, device=self.device)
             else:
                 self.hashes = torch.empty(2 * ni * B * C * W, dtype=torch.int32, device=self.device)
