@@ -365,7 +365,9 @@ def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, wo
     params = chain.params
     series = chain.dgw_ancestors(batch.header(0).prev)
     # the header objects the index insert needs are decoded on the host cores while the device
-    # verifies (HeaderBatch.from_bytes defers them)
+    # verifies (HeaderBatch.from_bytes defers them); NODEXA_VERIFY_OVERLAP=0 decodes them first
+    if os.environ.get("NODEXA_VERIFY_OVERLAP", "1") == "0":
+        batch.materialize()
     r = v.run(params, batch, series, plan, world, overlap=batch.materialize)
     t1 = time.perf_counter()
     codes = r["codes"]
