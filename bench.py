@@ -90,7 +90,6 @@ def _verify_headers_bench(log) -> dict | None:
 
     # a node's header chain exists before a `headers` message arrives: each run gets a fresh
     # chain made (and, after the run, freed) outside the timed region
-    chains = [_core.HeaderChain(params) for _ in range(6)]
 
     def resident(chain):
         t = time.perf_counter()
@@ -103,12 +102,12 @@ def _verify_headers_bench(log) -> dict | None:
         return r
 
     t0 = time.perf_counter()
-    warm = resident(chains.pop())  # every epoch's DAG and program table
+    warm = resident(_core.HeaderChain(params))  # every epoch's DAG and program table
     torch.cuda.synchronize()
     setup = W.all_reduce_max(time.perf_counter() - t0)
     runs = []
-    for _ in range(5):
-        chain = chains.pop()
+    for _ in range(15):  # ~2 ms each: the median of 15 is steady box to box
+        chain = _core.HeaderChain(params)
         W.barrier()
         t0 = time.perf_counter()
         r = resident(chain)
