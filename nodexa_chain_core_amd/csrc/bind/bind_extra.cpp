@@ -251,6 +251,12 @@ void bind_extra(py::module_& m) {
         std::vector<u8> h = haval_hash(reinterpret_cast<const u8*>(s.data()), s.size(), passes, out_bits);
         return py::bytes(reinterpret_cast<const char*>(h.data()), h.size());
     }, py::arg("data"), py::arg("passes") = 3, py::arg("out_bits") = 256);
+    m.def("gost", [](const py::bytes& data, int out_bits) {
+        const std::string s = data;
+        std::vector<u8> h = gost_streebog(reinterpret_cast<const u8*>(s.data()), s.size(), out_bits);
+        return py::bytes(reinterpret_cast<const char*>(h.data()), h.size());
+    }, py::arg("data"), py::arg("out_bits") = 512,
+       "GOST R 34.11-2012 (Streebog), the reference's sph_gost256/512 byte conventions");
     m.def("lyra2", [](const py::bytes& pwd, const py::bytes& salt, u64 klen, u64 time_cost, u64 n_rows, u64 n_cols,
                       bool old_absorb) {
         std::string p = pwd, s = salt;

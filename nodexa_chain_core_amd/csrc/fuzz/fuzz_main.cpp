@@ -168,10 +168,12 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         break;
     }
     case 12: {
-        // HAVAL over the whole input; Lyra2 with small parameters taken from its first bytes and
-        // the rest split into password and salt (inputs larger than the matrix must be refused)
+        // HAVAL and GOST Streebog over the whole input; Lyra2 with small parameters taken from its
+        // first bytes and the rest split into password and salt (inputs larger than the matrix
+        // must be refused)
         if (in.size() < 8) break;
         (void)haval_hash(in.data() + 7, in.size() - 7, 3 + in[0] % 3, 128 + 32 * (in[1] % 5));
+        (void)gost_streebog(in.data() + 7, in.size() - 7, in[1] & 1 ? 256 : 512);
         const size_t body = in.size() - 7, split = body ? in[6] % (body + 1) : 0;
         (void)lyra2_hash(in.data() + 7, split, in.data() + 7 + split, body - split, in[5], 1 + in[4] % 3,
                          u64(4) << (in[2] % 3), 1 + in[3] % 4, in[6] & 1);

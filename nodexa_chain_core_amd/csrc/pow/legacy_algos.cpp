@@ -328,4 +328,172 @@ std::vector<u8> lyra2_hash(const u8* pwd, size_t pwdlen, const u8* salt, size_t 
     return out;
 }
 
+// ------------------------------------------------------------------ GOST R 34.11-2012 (Streebog)
+// The reference's sph_gost256 / sph_gost512 (src/algo/gost_streebog.c; linked, never called from
+// consensus). Its byte convention: the state, the message blocks and the digest are big-endian
+// byte strings (byte 0 most significant), i.e. the standard's test vectors byte-reversed
+// (tests/test_legacy_algos.py checks example M1 both ways). The LPS layer is one table lookup per
+// state byte; the 8 x 256 table is expanded at first use from its GF(2) structure: 8 bases of the
+// linear layer's images and one S-box code shared by all byte positions (tools/gost_compact_tables.py
+// derives them from the reference's table).
+namespace {
+
+// basis[i][b]: LPS image of basis byte b at input byte position i
+static const u64 kGostBasis[8][8] = {
+    {0xe6f87e5c5b711fd0ULL, 0x258377800924fa16ULL, 0xc849e07e852ea4a8ULL, 0x5b4686a18f06c16aULL, 0xabda37a467815c66ULL, 0xf61796a81a686676ULL, 0xf5dc0b706391954bULL, 0xff5c629a68bd85c5ULL},
+    {0xc811a8058c3f55deULL, 0x65f5b43196b50619ULL, 0xf74f96b1d6706e43ULL, 0x859d1e8bcb43d336ULL, 0xf9c7bf99c295fcfdULL, 0xa21fd5a1de4b630fULL, 0xcdb3ef763b8b456dULL, 0xb27c73be5f31913cULL},
+    {0x45b268a93acde4ccULL, 0xaf7f0be884549d08ULL, 0x048354b3c1468263ULL, 0x925435c2c80efed2ULL, 0x167a33920c60f14dULL, 0xfb123b52ea03e584ULL, 0x4a0cab53fdbb9007ULL, 0xcb48ec558f0cb32aULL},
+    {0x05ba7bc82c9b3220ULL, 0x31a54665f8b65e4fULL, 0xb1b651f77547f4d4ULL, 0x8bfa0d857ba46682ULL, 0x990faef908eb79c9ULL, 0xa15e37a247f4a62dULL, 0x76857dcd5d27741eULL, 0xbe65dcb201f7a2b4ULL},
+    {0x3ef29d249b2c0a19ULL, 0xe9e16322b6f8622fULL, 0x5536994047757f7aULL, 0x9f4d56d5a47b0b33ULL, 0xb8f5057deb082fb2ULL, 0xcc48c10bf4475f53ULL, 0x373088d4275dec3aULL, 0x173d232cf7016151ULL},
+    {0x8ab0a96846e06a6dULL, 0x43c7e80b4bf0b33aULL, 0x08c9b3546b161ee5ULL, 0x39f1c235eba990beULL, 0x2c209233614569aaULL, 0xeb01523b6fc3289aULL, 0x946953ab935aceddULL, 0x8b0455eca12ba052ULL},
+    {0x7e37e62dfc7d40c3ULL, 0x776f25a4ee939e5bULL, 0xe045c850dd8fb5adULL, 0x86ed5ba711ff1952ULL, 0x37e0ab256e408ffbULL, 0x9607f6c031025a7aULL, 0x0b02f5e116d23c9dULL, 0x621cff27c40875f5ULL},
+    {0xd031c397ce553fe6ULL, 0x16ba5b01b006b525ULL, 0xa89bade6296e70c8ULL, 0x6a1f525d77d3435bULL, 0x660efb2a17fc95abULL, 0x76327a9e97634bf6ULL, 0x4bad9d6462458bf5ULL, 0xc5c8f542669131ffULL},
+};
+// code[x]: the S-box output of x in that basis
+static const u8 kGostCode[256] = {
+      1,   2,   4,   8,   7,  16,  32,  64,  73, 128, 100,  76,  35, 173,  67,  51,
+     74, 148, 206,  97,  60, 193, 150, 181, 109, 104, 227, 152, 102,  33,  48, 238,
+    111, 169, 151,  94, 205,  59,  47,   5,  63, 234, 194, 247, 149,  45, 251,  21,
+    110,  81,  38, 211, 224,  83, 214,  58, 101, 135,   9, 187,  24, 165, 237, 225,
+    108,  78, 231, 217,  65,  79,  93, 189, 232, 130, 117,  28,  44, 167,  42,  12,
+    113, 220, 233, 145, 140, 207, 185,   3, 219, 250,  46, 153, 248,  87,  22,  90,
+     75,  23,  82, 137,  37,  91, 157, 139, 197,  26,  80,  61, 213, 222,  57,  50,
+     43, 178, 132, 239,  10,  99, 184,  53,  27, 183, 166,  18, 200, 253, 226, 188,
+     34, 160, 107, 155, 228, 182, 218,  98, 174, 125, 131, 171,  19,  14, 190,  11,
+    235, 196,  36,  15, 118, 116,  31, 208,  41, 103, 164, 244,  56,   6, 170, 123,
+    114, 127, 249, 215, 204,   0, 223, 146, 143, 147, 129,  52, 186, 243,  77, 252,
+    216, 191, 180,  17,  96,  29, 154, 236, 221,  49,  84,  62,  88, 136,  89, 138,
+     72, 120,  20, 209, 119, 245, 199, 134,  13,  69, 126, 168, 158,  71, 163, 179,
+    198, 162,  25, 112,  30, 201,  66,  39, 240, 255, 144,  55, 105, 106, 124, 212,
+     40, 241, 177, 121, 202, 175, 161, 115,  68, 176,  70, 230, 246, 133,  54, 210,
+     85,  95, 159, 192, 142, 141,  92, 195, 203, 156, 254, 229, 172,  86, 242, 122,
+};
+// iteration constants C_1..C_12 as little-endian words of the state layout
+static const u64 kGostC[12][8] = {
+    {0xe9daca1eda5b08b1ULL, 0x1f7c65c0812fcbebULL, 0x16d0452e43766a2fULL, 0xfcc485758db84e71ULL, 0x0169679291e07c4bULL, 0x15d360a4082a42a2ULL, 0x234d74cc36747605ULL, 0x0745a6f2596580ddULL},
+    {0x1a2f9da98ab5a36fULL, 0xd7b5700f469de34fULL, 0x982b230a72eafef3ULL, 0x3101b5160f5ed561ULL, 0x5899d6126b17b59aULL, 0xcaa70adbc261b55cULL, 0x56cdcbd71ba2dd55ULL, 0xb79bb121700479e6ULL},
+    {0xc72fce2bacdc74f5ULL, 0x35843d6a28fc390aULL, 0x8b1f9c525f5ef106ULL, 0x7b7b29b11475eaf2ULL, 0xb19e3590e40fe2d3ULL, 0x09db6260373ac9c1ULL, 0x31db7a8643f4b6c2ULL, 0xb20aba0af5961e99ULL},
+    {0xd26615e8b3df1fefULL, 0xdde4715da0e148f9ULL, 0x7d3c5c337e858e48ULL, 0x3f355e68ad1c729dULL, 0x75d603ed822cd7a9ULL, 0xbe0352933313b7d8ULL, 0xf137e893a1ea5334ULL, 0x2ed1e384bcbe0c22ULL},
+    {0x994747adac6bea4bULL, 0x6323a96c0c413f9aULL, 0x4a1086161f1c157fULL, 0xbdff0f80d7359e35ULL, 0xa3f53a254717cdbfULL, 0x161a2723b700ffdfULL, 0xf563eaa97ea2567aULL, 0x57fe6c7cfd581760ULL},
+    {0xd9d33a1daeae4faeULL, 0xc039307a3bc3a46fULL, 0x6ca44251f9c4662dULL, 0xc68ef09ab49a7f18ULL, 0xb4b79a1cb7a6facfULL, 0xb6c6bec2661ff20aULL, 0x354f903672c571bfULL, 0x6e7d64467a4068faULL},
+    {0xecc5aaee160ec7f4ULL, 0x540924bffe86ac51ULL, 0xc987bfe6c7c69e39ULL, 0xc9937a19333e47d3ULL, 0x372c822dc5ab9209ULL, 0x04054a2883694706ULL, 0xf34a3ca24c451735ULL, 0x93d4143a4d568688ULL},
+    {0xa7c9934d425b1f9bULL, 0x41416e0c02aae703ULL, 0x1ede369c71f8b74eULL, 0x9ac4db4d3b44b489ULL, 0x90069b92cb2b89f4ULL, 0x2fc4a5d12b8dd169ULL, 0xd9a8515935c2ac36ULL, 0x1ee702bfd40d7fa4ULL},
+    {0x9b223116545a8f37ULL, 0xde5f16ecd89a4c94ULL, 0x244289251b3a7d3aULL, 0x84090de0b755d93cULL, 0xb1ceb2db0b440a80ULL, 0x549c07a69a8a2b7bULL, 0x602a1fcb92dc380eULL, 0xdb5a238351446172ULL},
+    {0x526f0580a6debeabULL, 0xf3f3e4b248e52a38ULL, 0xdb788aff1ce74189ULL, 0x0361331b8ae1ff1fULL, 0x4b3369af0267e79fULL, 0xf452763b306c1e7aULL, 0xc3b63b15d1fa9836ULL, 0xed9c4598fbc7b474ULL},
+    {0xfb89c8efd09ecd7bULL, 0x94fe5a63cdc60230ULL, 0x6107abebbb6bfad8ULL, 0x7966841421800120ULL, 0xcab948eaef711d8aULL, 0x986e477d1dcdbaefULL, 0x5dd86fc04a59a2deULL, 0x1b2df381cda4ca6bULL},
+    {0xba3116f167e78e37ULL, 0x7ab14904b08013d2ULL, 0x771ddfbc323ca4cdULL, 0x9b9f2130d41220f8ULL, 0x86cc91189def805dULL, 0x5228e188aaa41de7ULL, 0x991bb2d9d517f4faULL, 0x20d71bf14a92bc48ULL},
+};
+
+struct GostLps {
+    u64 t[8][256];
+    GostLps() {
+        for (int i = 0; i < 8; ++i)
+            for (int x = 0; x < 256; ++x) {
+                u64 acc = 0;
+                for (int b = 0; b < 8; ++b)
+                    if (kGostCode[x] >> b & 1) acc ^= kGostBasis[i][b];
+                t[i][x] = acc;
+            }
+    }
+};
+
+const GostLps& gost_lps() {
+    static const GostLps tab;
+    return tab;
+}
+
+// The 512-bit state as 8 little-endian words: byte j of the byte string is byte j % 8 of w[j / 8].
+struct G512 {
+    u64 w[8];
+};
+
+inline G512 gost_xor(const G512& a, const G512& b) {
+    G512 r;
+    for (int k = 0; k < 8; ++k) r.w[k] = a.w[k] ^ b.w[k];
+    return r;
+}
+
+// S, P and L in one pass: output word k takes byte k of every input word, position 7 - word.
+inline G512 gost_lps_apply(const G512& s) {
+    const GostLps& T = gost_lps();
+    G512 r;
+    for (int k = 0; k < 8; ++k) {
+        u64 acc = 0;
+        for (int i = 0; i < 8; ++i) acc ^= T.t[i][(s.w[7 - i] >> (8 * k)) & 0xFF];
+        r.w[k] = acc;
+    }
+    return r;
+}
+
+inline G512 gost_from_bytes(const u8* b) {
+    G512 r;
+    std::memcpy(r.w, b, 64);  // little-endian host: byte j -> byte j % 8 of word j / 8
+    return r;
+}
+
+// a + b mod 2^512 on the big-endian byte strings
+inline G512 gost_add(const G512& a, const G512& b) {
+    u8 x[64], y[64], z[64];
+    std::memcpy(x, a.w, 64);
+    std::memcpy(y, b.w, 64);
+    unsigned carry = 0;
+    for (int j = 63; j >= 0; --j) {
+        const unsigned t = unsigned(x[j]) + y[j] + carry;
+        z[j] = u8(t);
+        carry = t >> 8;
+    }
+    return gost_from_bytes(z);
+}
+
+// g_N(h, m): E over the key N ^ h, then the Miyaguchi-Preneel feed-forward
+G512 gost_g(const G512& n, const G512& h, const G512& m) {
+    G512 k = gost_lps_apply(gost_xor(n, h));
+    G512 s = gost_xor(m, k);
+    for (int i = 0; i < 12; ++i) {
+        s = gost_lps_apply(s);
+        G512 c;
+        std::memcpy(c.w, kGostC[i], 64);
+        k = gost_lps_apply(gost_xor(k, c));
+        s = gost_xor(s, k);
+    }
+    return gost_xor(gost_xor(s, h), m);
+}
+
+}  // namespace
+
+std::vector<u8> gost_streebog(const u8* data, size_t n, int out_bits) {
+    if (out_bits != 256 && out_bits != 512) throw std::invalid_argument("gost: out_bits is 256 or 512");
+    G512 h;
+    for (u64& x : h.w) x = out_bits == 256 ? 0x0101010101010101ULL : 0;
+    G512 nsum{}, sigma{}, zero{};
+    G512 step{};  // 512 as a big-endian byte string: byte 62 = 0x02
+    reinterpret_cast<u8*>(step.w)[62] = 0x02;
+    // full 64-byte blocks from the END of the message (the big-endian number's low end)
+    size_t rem = n;
+    while (rem >= 64) {
+        const G512 m = gost_from_bytes(data + rem - 64);
+        h = gost_g(nsum, h, m);
+        nsum = gost_add(nsum, step);
+        sigma = gost_add(sigma, m);
+        rem -= 64;
+    }
+    // the remaining head, right-aligned, with a 1 bit just above it
+    u8 last[64] = {0};
+    std::memcpy(last + 64 - rem, data, rem);
+    last[63 - rem] |= 1;
+    const G512 m = gost_from_bytes(last);
+    h = gost_g(nsum, h, m);
+    G512 bits{};
+    const size_t nb = rem * 8;
+    reinterpret_cast<u8*>(bits.w)[63] = u8(nb);
+    reinterpret_cast<u8*>(bits.w)[62] = u8(nb >> 8);
+    nsum = gost_add(nsum, bits);
+    sigma = gost_add(sigma, m);
+    h = gost_g(zero, h, nsum);
+    h = gost_g(zero, h, sigma);
+    std::vector<u8> out(size_t(out_bits / 8));
+    std::memcpy(out.data(), h.w, out.size());  // the first bytes of the big-endian string
+    return out;
+}
+
 }  // namespace nodexa
