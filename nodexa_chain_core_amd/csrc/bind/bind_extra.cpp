@@ -602,6 +602,8 @@ void bind_extra(py::module_& m) {
             return std::vector<BlockHeader>(b.hs.begin() + std::min(lo, hi), b.hs.begin() + hi);
         }, py::arg("lo") = 0, py::arg("hi") = size_t(-1));
 
+    py::class_<AcceptPrep, std::shared_ptr<AcceptPrep>>(m, "AcceptPrep")
+        .def_readonly("n", &AcceptPrep::n);
     py::class_<HeaderChain, std::shared_ptr<HeaderChain>>(m, "HeaderChain")
         .def("accept_batch",
              [](HeaderChain& c, HeaderBatch& b, int64_t adjusted_time, const py::object& hashes,
@@ -645,6 +647,45 @@ void bind_extra(py::module_& m) {
              },
              py::arg("batch"), py::arg("adjusted_time"), py::arg("hashes") = py::none(), py::arg("bits") = py::none(),
              py::arg("lo") = 0, py::arg("hi") = size_t(-1))
+        .def("prepare_batch",
+             [](const HeaderChain& c, HeaderBatch& b, int64_t adjusted_time, const py::buffer& hashes,
+                const py::buffer& bits) {
+                 // accept_batch's read-only first phase over the whole batch (hashes n x 32 and
+                 // nBits n x u32 are copied): the result commits a prefix later (commit_batch)
+                 {
+                     py::gil_scoped_release rel;
+                     b.materialize();
+                 }
+                 const py::buffer_info hb = hashes.request(), bb = bits.request();
+                 const size_t n = b.hs.size();
+                 if (size_t(hb.size * hb.itemsize) != n * 32) throw std::invalid_argument("hashes: n x 32 bytes");
+                 if (size_t(bb.size * bb.itemsize) != n * 4) throw std::invalid_argument("bits: n x 4 bytes");
+                 py::gil_scoped_release rel;
+                 return std::make_shared<AcceptPrep>(c.prepare_headers(
+                     b.hs.data(), n, adjusted_time, false, reinterpret_cast<const Uint256*>(hb.ptr),
+                     static_cast<const u32*>(bb.ptr)));
+             },
+             py::arg("batch"), py::arg("adjusted_time"), py::arg("hashes"), py::arg("bits"),
+             py::keep_alive<0, 2>())  // the prepared state points into the batch's headers
+        .def("commit_batch",
+             [](HeaderChain& c, AcceptPrep& p, size_t hi) {
+                 // accept headers [0, hi) of a prepare_batch: (accepted, reject reason or None, dos)
+                 std::vector<AcceptResult> r;
+                 {
+                     py::gil_scoped_release rel;
+                     r = c.commit_headers(p, hi);
+                 }
+                 size_t ok = 0;
+                 while (ok < r.size() && r[ok].ok) ++ok;
+                 py::object why = py::none();
+                 int dos = 0;
+                 if (ok < r.size()) {
+                     why = py::str(r[ok].reject);
+                     dos = r[ok].dos;
+                 }
+                 return py::make_tuple(ok, why, dos);
+             },
+             py::arg("prepared"), py::arg("hi"))
         .def("dgw_ancestors",
              [](const HeaderChain& c, const py::bytes& prev) -> py::object {
                  // the DGW series prefix of a batch whose first header builds on `prev`: prev and up

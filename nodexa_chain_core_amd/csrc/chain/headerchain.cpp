@@ -86,6 +86,7 @@ const HeaderIndex* HeaderChain::add_to_index(const BlockHeader& h, const Uint256
         idx.skip = batch && !batch->empty() && skip_h >= b0 ? (*batch)[size_t(skip_h - b0)] : prev->ancestor(skip_h);
     }
     index_.insert(&idx);
+    ++version_;
     return &idx;
 }
 
@@ -321,20 +322,37 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const BlockHeader* hs, siz
                                                       bool check_pow, const Uint256* known_hashes,
                                                       const u32* known_bits) {
     std::lock_guard<std::recursive_mutex> g(mu_);
-    std::vector<AcceptResult> out;
-    out.reserve(n);
-    std::vector<Uint256> hashes;
-    std::vector<u32> expected;
-    std::vector<u8> have(n, 0), have_mtp(n, 0);
-    std::vector<ArithU256> proofs;
-    std::vector<int64_t> mtp;
-    std::vector<AcceptResult> pre;
+    AcceptPrep p = prepare_headers(hs, n, adjusted_time, check_pow, known_hashes, known_bits);
+    return commit_headers(p, n);
+}
+
+AcceptPrep HeaderChain::prepare_headers(const BlockHeader* hs, size_t n, int64_t adjusted_time, bool check_pow,
+                                        const Uint256* known_hashes, const u32* known_bits) const {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    AcceptPrep P;
+    P.hs = hs;
+    P.n = n;
+    P.adjusted_time = adjusted_time;
+    P.check_pow = check_pow;
+    P.version = version_;
+    P.strict_height = strict_kawpow_height;
+    if (known_bits) P.known_bits.assign(known_bits, known_bits + n);
+    std::vector<Uint256>& hashes = P.hashes;
+    std::vector<u32>& expected = P.expected;
+    std::vector<u8>& have = P.have;
+    std::vector<u8>& have_mtp = P.have_mtp;
+    have.assign(n, 0);
+    have_mtp.assign(n, 0);
+    std::vector<ArithU256>& proofs = P.proofs;
+    std::vector<int64_t>& mtp = P.mtp;
+    std::vector<AcceptResult>& pre = P.pre;
     if (n >= kParallelAcceptMin && check_pow) {  // CheckBlockHeader (full PoW) is context-free
         pre.resize(n);
         parallel_for(n, [&](size_t i) { pre[i] = check_header(hs[i], true); });
     }
-    std::vector<u8> ctx, fresh;
-    int base_height = 0;
+    std::vector<u8>& ctx = P.ctx;
+    std::vector<u8>& fresh = P.fresh;
+    int& base_height = P.base_height;
     if (n >= kParallelAcceptMin) {
         if (known_hashes) {
             hashes.assign(known_hashes, known_hashes + n);
@@ -397,6 +415,35 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const BlockHeader* hs, siz
             });
         }
     }
+    return P;
+}
+
+std::vector<AcceptResult> HeaderChain::commit_headers(AcceptPrep& P, size_t hi) {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    hi = std::min(hi, P.n);
+    if (P.version != version_ || P.strict_height != strict_kawpow_height) {
+        // the index (or the height policy) changed since the prepare: prepare the prefix again
+        AcceptPrep again = prepare_headers(P.hs, hi, P.adjusted_time, P.check_pow,
+                                           P.hashes.size() >= hi ? P.hashes.data() : nullptr,
+                                           P.known_bits.size() >= hi ? P.known_bits.data() : nullptr);
+        return commit_headers(again, hi);
+    }
+    const BlockHeader* hs = P.hs;
+    const size_t n = hi;
+    const int64_t adjusted_time = P.adjusted_time;
+    const bool check_pow = P.check_pow;
+    std::vector<Uint256>& hashes = P.hashes;
+    std::vector<u32>& expected = P.expected;
+    std::vector<u8>& have = P.have;
+    std::vector<u8>& have_mtp = P.have_mtp;
+    std::vector<ArithU256>& proofs = P.proofs;
+    std::vector<int64_t>& mtp = P.mtp;
+    std::vector<AcceptResult>& pre = P.pre;
+    std::vector<u8>& ctx = P.ctx;
+    std::vector<u8>& fresh = P.fresh;
+    const int base_height = P.base_height;
+    std::vector<AcceptResult> out;
+    out.reserve(n);
     if (ctx.empty()) {
         for (size_t i = 0; i < n; ++i) {
             out.push_back(accept_header_impl(hs[i], hashes.empty() ? nullptr : &hashes[i], adjusted_time, check_pow,
@@ -456,6 +503,7 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const BlockHeader* hs, siz
                 });
             });
             index_.add_count(m);
+            ++version_;
             active_.insert(active_.end(), batch.begin() + std::ptrdiff_t(s0), batch.end());
             prev = batch.back();
             i += m;
@@ -528,6 +576,7 @@ void HeaderChain::update_active_chain() {
 
 // Re-point the active chain at `best`: only the entries from the fork point up change.
 void HeaderChain::set_active_tip(const HeaderIndex* best) {
+    ++version_;
     active_.resize(size_t(best->height) + 1, nullptr);
     for (const HeaderIndex* p = best; p && active_[size_t(p->height)] != p; p = p->prev)
         active_[size_t(p->height)] = p;
@@ -567,6 +616,7 @@ void HeaderChain::invalidate(const Uint256& hash) {
     const HeaderIndex* e = index_.find(hash);
     if (e == nullptr || e == genesis_) return;
     failed_[e] = true;
+    ++version_;
     update_active_chain();
 }
 
@@ -584,6 +634,7 @@ void HeaderChain::reconsider(const Uint256& hash) {
         const bool related = x->height >= node->height ? walk(x, node->height) == node : walk(node, x->height) == x;
         f = related ? failed_.erase(f) : std::next(f);
     }
+    ++version_;
     update_active_chain();
 }
 

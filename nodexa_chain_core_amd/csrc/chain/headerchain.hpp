@@ -154,6 +154,29 @@ private:
     unsigned shift_ = 64;
 };
 
+// accept_headers in two phases (HeaderChain::prepare_headers / commit_headers): the context-free
+// and read-only per-header work of a batch -- hashes, block proofs, parent MTPs, expected nBits,
+// contextual rules, freshness -- then the serial index insert. The resident batch verify
+// (models/verify.py) prepares while the device is still finishing the PoW verdicts and commits
+// the verified prefix afterwards; the commit redoes everything when the index changed between.
+struct AcceptPrep {
+    const BlockHeader* hs = nullptr;
+    size_t n = 0;
+    int64_t adjusted_time = 0;
+    bool check_pow = false;
+    std::vector<Uint256> hashes;
+    std::vector<u32> expected;
+    std::vector<u8> have, have_mtp;
+    std::vector<ArithU256> proofs;
+    std::vector<int64_t> mtp;
+    std::vector<AcceptResult> pre;
+    std::vector<u8> ctx, fresh;  // empty: the batch takes the header-by-header path
+    int base_height = 0;
+    u64 version = 0;  // the chain's version when prepared
+    bool strict_height = false;
+    std::vector<u32> known_bits;  // the caller's nBits (0 = unknown), kept for a re-prepare
+};
+
 class HeaderChain {
 public:
     HeaderChain(ChainParams params, std::shared_ptr<const PowVerifier> verifier);
@@ -185,6 +208,11 @@ public:
                     std::vector<u32>& bits, size_t& a, int& base_height) const;
     std::vector<AcceptResult> accept_headers(const BlockHeader* hs, size_t n, int64_t adjusted_time, bool check_pow,
                                              const Uint256* known_hashes, const u32* known_bits);
+    // The two phases of accept_headers (AcceptPrep); commit accepts headers [0, hi) of the
+    // prepared ones (a verified prefix), exactly as accept_headers over that prefix would.
+    AcceptPrep prepare_headers(const BlockHeader* hs, size_t n, int64_t adjusted_time, bool check_pow,
+                               const Uint256* known_hashes, const u32* known_bits) const;
+    std::vector<AcceptResult> commit_headers(AcceptPrep& p, size_t hi);
 
     const HeaderIndex* tip() const;
     const HeaderIndex* genesis() const { return genesis_; }
@@ -227,6 +255,7 @@ private:
     std::unordered_map<const HeaderIndex*, bool> failed_;
     std::vector<const HeaderIndex*> active_;
     const HeaderIndex* genesis_ = nullptr;
+    u64 version_ = 0;  // bumped by every change of the index, the failed set or the active chain
 };
 
 // blk?????.dat files: [magic 4][u32 size][block] records, 128 MiB per file.

@@ -8,10 +8,12 @@
 //   kawpow_mixonly_batch (sha256d.hip)  rows -> header hash | mix-only final | boundary | claimed mix
 //   hb_jobs                             -> KawpowVerifyJob + program index per header
 //   kawpow_verify_dag (per epoch range) -> computed mix | final per header (the resident DAG)
-//   hb_verdict                          -> one code + the block hash per header
-//   eq_verify + sha256d_batch + hb_eq_scatter for Equihash-extension headers
-//   dgw_batch                           -> the DarkGravityWave nBits of every header
-// and one device-to-host copy brings back codes, block hashes and nBits together.
+//   hb_verdict                          -> one code per KawPow header
+//   eq_verify + sha256d_batch + hb_eq_scatter for Equihash-extension headers (side stream)
+//   dgw_batch                           -> the DarkGravityWave nBits of every header (side stream)
+// hb_jobs writes the KawPow block hashes, so hashes + nBits are complete once the side stream and
+// hb_jobs are done: an early copy of them lets the host prepare the index insert while the full
+// hashes run, and one final device-to-host copy brings back codes, hashes and nBits together.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -46,6 +48,14 @@ extern "C" __global__ __launch_bounds__(256) void hb_jobs(HeaderBatchParams p) {
     }
     p.jobs[i] = j;
     p.job_program[i] = prog;
+    // a KawPow row's block hash (GetHash: the mix-only final, byte-reversed into uint256 storage
+    // order) is known here already: written now, the early copy of hashes + nBits lets the host
+    // prepare the index insert while the full hashes are still running
+    if (p.kinds[i] == 0) {
+        uint8_t* out_hash = p.out + (size_t)p.n + (size_t)i * 32;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) out_hash[k] = mo[32 + 31 - k];
+    }
 }
 
 // One thread per header: the verdict of a KawPow row from the mix-only pass and the full hash
@@ -57,9 +67,10 @@ extern "C" __global__ __launch_bounds__(256) void hb_verdict(HeaderBatchParams p
     if (t >= p.count) return;
     const uint32_t i = p.first + t;
     const uint8_t* mo = p.mixonly + (size_t)i * 128;
-    uint8_t* out_hash = p.out + (size_t)p.n + (size_t)i * 32;
     if (p.kinds[i] != 0) {
-        p.out[i] = 255;
+        // Equihash rows get their code from hb_eq_scatter (on the side stream, possibly already
+        // done); pre-KawPow rows are decided by the host
+        if (p.kinds[i] != 2) p.out[i] = 255;
         return;
     }
     // CheckBlockHeader's order (src/validation.cpp:11638-11665): below the last checkpoint only the
@@ -87,9 +98,7 @@ extern "C" __global__ __launch_bounds__(256) void hb_verdict(HeaderBatchParams p
         for (int k = 0; k < 8; ++k) same &= full[k] == hb_le32(mo + 96 + 4 * k);
         code = same ? 0 : 1;
     }
-    p.out[i] = code;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) out_hash[k] = mo[32 + 31 - k];
+    p.out[i] = code;  // (the block hash was written by hb_jobs)
 }
 
 // Equihash-extension headers: the eq_verify verdict (0 = valid solution) and the SHA256d block

@@ -364,11 +364,23 @@ def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, wo
         return None
     params = chain.params
     series = chain.dgw_ancestors(batch.header(0).prev)
-    # the header objects the index insert needs are decoded on the host cores while the device
-    # verifies (HeaderBatch.from_bytes defers them); NODEXA_VERIFY_OVERLAP=0 decodes them first
-    if os.environ.get("NODEXA_VERIFY_OVERLAP", "1") == "0":
+    # while the device verifies, the host decodes the header objects the index insert needs
+    # (HeaderBatch.from_bytes defers them) and, once the block hashes and DGW nBits are back (they
+    # come before the full hashes), runs the insert's read-only prepare phase; the commit of the
+    # verified prefix follows the verdicts. NODEXA_VERIFY_OVERLAP=0: decode first, no prepare.
+    overlap_on = os.environ.get("NODEXA_VERIFY_OVERLAP", "1") != "0"
+    if not overlap_on:
         batch.materialize()
-    r = v.run(params, batch, series, plan, world, overlap=batch.materialize)
+    prepared = []
+    no_legacy = not bool((plan["kinds"] == 3).any())
+
+    def overlap(early):
+        batch.materialize()
+        got = early() if overlap_on and no_legacy else None
+        if got is not None:
+            prepared.append(chain.prepare_batch(batch, adjusted_time, got[0], got[1]))
+
+    r = v.run(params, batch, series, plan, world, overlap=overlap)
     t1 = time.perf_counter()
     codes = r["codes"]
     n = len(batch)
@@ -387,7 +399,10 @@ def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, wo
     bad = np.flatnonzero(codes != 0)
     first_bad = int(bad[0]) if len(bad) else n
     t2 = time.perf_counter()
-    accepted, why, _dos = chain.accept_batch(batch, adjusted_time, hashes, r["bits"], 0, first_bad)
+    if prepared:
+        accepted, why, _dos = chain.commit_batch(prepared[0], first_bad)
+    else:
+        accepted, why, _dos = chain.accept_batch(batch, adjusted_time, hashes, r["bits"], 0, first_bad)
     t3 = time.perf_counter()
     reject = {"index": accepted, "reason": why} if why is not None else None
     if reject is None and first_bad < n:

@@ -60,6 +60,10 @@ class ResidentHeaderVerifier:
             self.ev_end = torch.cuda.Event(enable_timing=True)
             self.ev_in, self.ev_jobs = torch.cuda.Event(), torch.cuda.Event()
             self.ev_side = [torch.cuda.Event() for _ in self.side]
+            # the early copy of block hashes + nBits (models/verify.py prepares the index insert
+            # from it while the full hashes run)
+            self.early_stream = torch.cuda.Stream(device=self.dev)
+            self.ev_early = torch.cuda.Event()
         self.cap = 0
         self.in_cap = 0
         self.programs: dict[int, torch.Tensor] = {}
@@ -99,6 +103,7 @@ class ResidentHeaderVerifier:
                 self.out = torch.empty(cap * 37, dtype=torch.uint8, device=self.dev)  # codes | hashes | bits
                 self.gath = torch.empty(cap * 33 * 2 + 64 * 33, dtype=torch.uint8, device=self.dev)
                 self.out_host = torch.empty(cap * 37, dtype=torch.uint8).pin_memory()
+                self.early_host = torch.empty(cap * 36, dtype=torch.uint8).pin_memory()  # hashes | bits
                 self.cap = cap
             if in_bytes > self.in_cap:
                 cap = max(in_bytes, 2 * self.in_cap)
@@ -148,9 +153,12 @@ class ResidentHeaderVerifier:
     def run(self, params, batch, series, plan: dict | None = None, world=None, overlap=None) -> dict:
         """Verify the PoW of every header and compute every header's DGW nBits on the device.
         `series`: (ancestor times bytes, ancestor bits bytes, a, base_height) of the batch's parent
-        (HeaderChain.dgw_ancestors) or None. `overlap`: host work to run while the device works
-        (models/verify.py passes the batch's deferred header decode). Returns codes (n,) u8, hashes
-        (n, 32) u8, bits (n,) u32 as numpy views of the pinned result buffer, plus timings."""
+        (HeaderChain.dgw_ancestors) or None. `overlap(early)`: host work to run while the device
+        works (models/verify.py: the batch's deferred header decode, then the index insert's
+        prepare phase); `early()` waits for the block hashes + DGW nBits only (one rank: they are
+        complete before the full hashes are) and returns them as (n, 32) u8 / (n,) u32 views, or
+        None on a multi-rank world. Returns codes (n,) u8, hashes (n, 32) u8, bits (n,) u32 as
+        numpy views of the pinned result buffer, plus timings."""
         from . import verify as V
 
         t0 = time.perf_counter()
@@ -238,6 +246,8 @@ class ResidentHeaderVerifier:
             s = int(main.cuda_stream)
             self.ev_start.record(main)
             self.din[:cur].copy_(self.in_host[:cur], non_blocking=True)
+            if series is None:
+                self.out[n * 33:n * 37].zero_()  # nBits 0 = the host decides
             self.ev_in.record(main)
             # Equihash solutions + block hashes and the DGW nBits depend only on the upload: a side
             # stream runs them beside the KawPow chain (mix-only -> jobs -> full hashes -> verdicts)
@@ -251,11 +261,21 @@ class ResidentHeaderVerifier:
                 c = _core.dgw_constants(params)
                 h.launch_dgw(self.k_dgw, P("times"), P("bits"), out + n * 33, a, n, series[3], c["dgw_activation_block"],
                              c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], s0)
+            if m:
+                glue(2, 0, 0, s0)  # Equihash codes + block hashes (hb_verdict leaves those rows alone)
             self.ev_side[0].record(side)
             if nr:
                 h.launch_kawpow_mixonly(self.k_mo, P("rows") + lo_r * ROW, nr, ROW, self.mo.data_ptr() + lo_r * 128, s)
-                glue(0, lo_r, nr, s)
-                self.ev_jobs.record(main)
+                glue(0, lo_r, nr, s)  # jobs + the KawPow block hashes
+            self.ev_jobs.record(main)
+            if ws == 1:  # the early copy: hashes + nBits as soon as hb_jobs and the side stream are done
+                es = self.early_stream
+                es.wait_event(self.ev_jobs)
+                es.wait_event(self.ev_side[0])
+                with torch.cuda.stream(es):
+                    self.early_host[:n * 36].copy_(self.out[n:n * 37], non_blocking=True)
+                self.ev_early.record(es)
+            if nr:
                 # one full-hash launch per epoch range, the ranges side by side: each is bound by
                 # its 64 dependent rounds per job, not by width
                 slot_off = np.r_[0, np.cumsum([len(t) for t in slot_tabs])].tolist()
@@ -288,17 +308,20 @@ class ResidentHeaderVerifier:
                     k += 1
                 glue(1, lo_r, nr, s)
             main.wait_event(self.ev_side[0])
-            if m:
-                glue(2, 0, 0, s)  # after the verdicts: it overwrites the Equihash rows' codes
-            if series is None:
-                self.out[n * 33:n * 37].zero_()
             if ws > 1:
                 self._gather(world, n, per, lo_r, hi_r)
             self.out_host[:n * 37].copy_(self.out[:n * 37], non_blocking=True)
             self.ev_end.record(main)
         t_issue = time.perf_counter()
         if overlap is not None:
-            overlap()
+            def early():
+                if ws != 1:
+                    return None
+                self.ev_early.synchronize()
+                e = self.early_host.numpy()
+                return e[:n * 32].reshape(n, 32), e[n * 32:n * 36].view("<u4")
+
+            overlap(early)
         t_overlap = time.perf_counter()
         self.ev_end.synchronize()
         t_done = time.perf_counter()

@@ -288,6 +288,52 @@ def test_copy_into_is_bounded(core):
         core.copy_into(b"read-only target", 0, b"x")
 
 
+def test_prepare_commit_equals_accept(core):
+    """HeaderChain.prepare_batch / commit_batch (the resident verify's two-phase accept): committing a
+    prefix of a prepared batch builds the same chain as accept_batch over that prefix, and a chain
+    changed between the two phases (another header accepted, a block invalidated) is prepared
+    again rather than trusted."""
+    import os
+
+    import numpy as np
+
+    from nodexa_chain_core_amd.models import synthetic
+
+    path = os.path.join(os.path.dirname(__file__), "data", "testnet_mixed_10k.hdr")
+    params, hs = synthetic.load(path)
+    act = params.kawpow_activation_time
+    raw = open(path, "rb").read()
+    adj = hs[-1].time + 3600
+    ref = core.HeaderChain(params)
+    assert ref.accept_batch(core.HeaderBatch.from_bytes(raw, act), adj) == (len(hs), None, 0)
+    n = len(hs)
+    hashes = np.frombuffer(b"".join(ref.at_height(i + 1).hash for i in range(n)), np.uint8).reshape(n, 32).copy()
+    bits = np.array([h.bits for h in hs], dtype="<u4")
+    for hi in (n, 4321, 0):
+        c = core.HeaderChain(params)
+        b = core.HeaderBatch.from_bytes(raw, act)
+        prep = c.prepare_batch(b, adj, hashes, bits)
+        del b  # the prepared state keeps the batch alive
+        assert c.commit_batch(prep, hi) == (hi, None, 0)
+        assert c.height() == hi and c.tip().hash == (ref.at_height(hi).hash if hi else c.genesis().hash)
+    # the chain moves between prepare and commit: the first 10 headers arrive on their own
+    c = core.HeaderChain(params)
+    b = core.HeaderBatch.from_bytes(raw, act)
+    prep = c.prepare_batch(b, adj, hashes, bits)
+    assert c.accept_batch(b, adj, None, None, 0, 10) == (10, None, 0)
+    assert c.commit_batch(prep, 3000) == (3000, None, 0)  # the first 10 are duplicates now
+    assert c.height() == 3000 and c.tip().hash == ref.at_height(3000).hash
+    # a wrong nBits at 2500 (as the device would report it) stops the commit there
+    bad = bits.copy()
+    bad[2500] ^= 1
+    c = core.HeaderChain(params)
+    prep = c.prepare_batch(core.HeaderBatch.from_bytes(raw, act), adj, hashes, bad)
+    acc, why, dos = c.commit_batch(prep, n)
+    assert (acc, why) == (2500, "bad-diffbits") and c.height() == 2500
+    with pytest.raises(ValueError):
+        c.prepare_batch(core.HeaderBatch.from_bytes(raw, act), adj, hashes[:10], bits)
+
+
 def _serial(params, headers, adj, check_pow=False, chain=None):
     c = chain or _core.HeaderChain(params)
     out = []
