@@ -584,6 +584,40 @@ void bind_extra(py::module_& m) {
         .def_property_readonly("eq_ser", [view](const HeaderBatch& b) { return view(b.eq_ser); })
         .def_readonly("eq_ser_len", &HeaderBatch::eq_ser_len)
         .def_readonly("eq_uniform", &HeaderBatch::eq_uniform)
+        .def("kawpow_plan", [](const HeaderBatch& b, u32 epoch_length) -> py::object {
+            // the resident verify's plan in one pass: the (epoch, lo, hi) ranges of the KawPow
+            // rows and every row's nHeight, nTime and nBits (row bytes 76, 68, 72; u32 bytes each);
+            // None when the KawPow rows' epochs are not in ascending order
+            if (epoch_length == 0) throw std::invalid_argument("epoch_length");
+            const size_t n = b.size();
+            std::string heights(n * 4, '\0'), times(n * 4, '\0'), bits(n * 4, '\0');
+            py::list ranges;
+            long long cur = -1;
+            size_t lo = 0, hi = 0;
+            bool ordered = true;
+            for (size_t i = 0; i < n; ++i) {
+                const u8* row = reinterpret_cast<const u8*>(b.rows.data()) + i * kBatchRow;
+                const u32 h = load_le32(row + 76);
+                std::memcpy(&heights[i * 4], row + 76, 4);
+                std::memcpy(&times[i * 4], row + 68, 4);
+                std::memcpy(&bits[i * 4], row + 72, 4);
+                if (b.kinds[i] != 0 || !ordered) continue;
+                const long long e = h / epoch_length;
+                if (e < cur) {
+                    ordered = false;
+                } else if (e != cur) {
+                    if (cur >= 0) ranges.append(py::make_tuple(cur, lo, hi));
+                    cur = e;
+                    lo = i;
+                    hi = i + 1;
+                } else {
+                    hi = i + 1;
+                }
+            }
+            if (!ordered) return py::none();
+            if (cur >= 0) ranges.append(py::make_tuple(cur, lo, hi));
+            return py::make_tuple(ranges, py::bytes(heights), py::bytes(times), py::bytes(bits));
+        }, py::arg("epoch_length"))
         .def("materialize", [](HeaderBatch& b) {
             py::gil_scoped_release rel;
             b.materialize();

@@ -116,20 +116,14 @@ class ResidentHeaderVerifier:
         """Host-side numpy planning (no device work): epoch ranges of the KawPow rows. None when
         the batch is not in height order (the resident path wants contiguous epoch ranges)."""
         n = len(batch)
-        rows = np.frombuffer(batch.rows, dtype=np.uint8).reshape(n, ROW)
-        kinds = np.frombuffer(batch.kinds, dtype=np.uint8)
-        kp = np.flatnonzero(kinds == 0)
-        ranges = []
-        if len(kp):
-            heights = np.ascontiguousarray(rows[kp, 76:80]).view("<u4").ravel()
-            epochs = heights // _core.EPOCH_LENGTH
-            if np.any(np.diff(epochs.astype(np.int64)) < 0):
-                return None
-            for e in np.unique(epochs).tolist():
-                idx = kp[epochs == e]
-                ranges.append((int(e), int(idx[0]), int(idx[-1]) + 1))
-        return {"rows": rows, "kinds": kinds, "ranges": ranges,
-                "heights": np.ascontiguousarray(rows[:, 76:80]).view("<u4").ravel()}
+        got = batch.kawpow_plan(_core.EPOCH_LENGTH)  # one native pass over the rows
+        if got is None:
+            return None
+        ranges, heights, times, bits = got
+        return {"rows": np.frombuffer(batch.rows, dtype=np.uint8).reshape(n, ROW),
+                "kinds": np.frombuffer(batch.kinds, dtype=np.uint8), "ranges": ranges,
+                "heights": np.frombuffer(heights, dtype="<u4"), "times": np.frombuffer(times, dtype="<u4"),
+                "bits": np.frombuffer(bits, dtype="<u4")}
 
     @staticmethod
     def wave_slots(rows_idx: np.ndarray, heights: np.ndarray, lo: int) -> np.ndarray:
@@ -210,8 +204,8 @@ class ResidentHeaderVerifier:
             bits = np.empty(a + n, dtype="<u4")
             times[:a] = np.frombuffer(series[0], dtype="<u4")
             bits[:a] = np.frombuffer(series[1], dtype="<u4")
-            times[a:] = np.ascontiguousarray(rows[:, 68:72]).view("<u4").ravel()
-            bits[a:] = np.ascontiguousarray(rows[:, 72:76]).view("<u4").ravel()
+            times[a:] = plan["times"]
+            bits[a:] = plan["bits"]
             put("times", times)
             put("bits", bits)
         if nslots:

@@ -334,6 +334,34 @@ def test_prepare_commit_equals_accept(core):
         c.prepare_batch(core.HeaderBatch.from_bytes(raw, act), adj, hashes[:10], bits)
 
 
+def test_kawpow_plan_matches_numpy(core):
+    """HeaderBatch.kawpow_plan (the resident verify's plan in one native pass): the KawPow rows'
+    epoch ranges and every row's nHeight / nTime / nBits, None for descending epochs."""
+    import os
+
+    import numpy as np
+
+    from nodexa_chain_core_amd.models import synthetic
+
+    path = os.path.join(os.path.dirname(__file__), "data", "testnet_mixed_10k.hdr")
+    params, hs = synthetic.load(path)
+    act = params.kawpow_activation_time
+    b = core.HeaderBatch.from_bytes(open(path, "rb").read(), act)
+    ranges, heights, times, bits = b.kawpow_plan(core.EPOCH_LENGTH)
+    rows = np.frombuffer(b.rows, np.uint8).reshape(len(b), 128)
+    kinds = np.frombuffer(b.kinds, np.uint8)
+    kp = np.flatnonzero(kinds == 0)
+    ep = np.ascontiguousarray(rows[kp, 76:80]).view("<u4").ravel() // core.EPOCH_LENGTH
+    want = [(int(e), int(kp[ep == e][0]), int(kp[ep == e][-1]) + 1) for e in np.unique(ep).tolist()]
+    assert [tuple(r) for r in ranges] == want and len(want) == 2
+    for col, got in ((76, heights), (68, times), (72, bits)):
+        assert np.array_equal(np.frombuffer(got, "<u4"), np.ascontiguousarray(rows[:, col:col + 4]).view("<u4").ravel())
+    assert np.array_equal(np.frombuffer(times, "<u4"), [h.time for h in hs])
+    # a batch whose KawPow epochs go backwards has no plan
+    back = b"".join(h.serialize(act) for h in list(hs[7600:7610]) + list(hs[100:110]))
+    assert core.HeaderBatch.from_bytes(back, act).kawpow_plan(core.EPOCH_LENGTH) is None
+
+
 def _serial(params, headers, adj, check_pow=False, chain=None):
     c = chain or _core.HeaderChain(params)
     out = []
