@@ -318,6 +318,24 @@ std::vector<AcceptResult> HeaderChain::accept_headers(const std::vector<BlockHea
                           known_bits && known_bits->size() == hs.size() ? known_bits->data() : nullptr);
 }
 
+// out[k] = base + proofs[0] + ... + proofs[k] (mod 2^256): the chain work of a run of headers,
+// in 64-bit limbs with the carries chained (one 256-bit add is four adds, not eight).
+static void chain_work_prefix(const ArithU256& base, const ArithU256* proofs, size_t m, ArithU256* out) {
+    u64 acc[4], p[4];
+    std::memcpy(acc, base.pn, 32);
+    for (size_t k = 0; k < m; ++k) {
+        std::memcpy(p, proofs[k].pn, 32);
+        unsigned __int128 s = (unsigned __int128)acc[0] + p[0];
+        acc[0] = u64(s);
+        s = (unsigned __int128)acc[1] + p[1] + u64(s >> 64);
+        acc[1] = u64(s);
+        s = (unsigned __int128)acc[2] + p[2] + u64(s >> 64);
+        acc[2] = u64(s);
+        acc[3] = acc[3] + p[3] + u64(s >> 64);
+        std::memcpy(out[k].pn, acc, 32);
+    }
+}
+
 std::vector<AcceptResult> HeaderChain::accept_headers(const BlockHeader* hs, size_t n, int64_t adjusted_time,
                                                       bool check_pow, const Uint256* known_hashes,
                                                       const u32* known_bits) {
@@ -481,8 +499,7 @@ std::vector<AcceptResult> HeaderChain::commit_headers(AcceptPrep& P, size_t hi) 
             const size_t s0 = batch.size();
             nodes.resize(m);
             work.resize(m);
-            ArithU256 w = prev->chain_work;
-            for (size_t k = 0; k < m; ++k) work[k] = w += proofs[i + k];
+            chain_work_prefix(prev->chain_work, proofs.data() + i, m, work.data());
             storage_.emplace_n(m, nodes.data(), [&] {
                 batch.insert(batch.end(), nodes.begin(), nodes.end());  // reserved: no reallocation
                 parallel_for(m, [&](size_t k) {
