@@ -559,6 +559,7 @@ void bind_extra(py::module_& m) {
                 PyObject* o = buf.ptr();
                 Py_INCREF(o);
                 keep = std::shared_ptr<const void>(o, [](const void* q) {
+                    if (!Py_IsInitialized()) return;  // interpreter shutdown: leave the reference
                     py::gil_scoped_acquire g;
                     Py_DECREF(reinterpret_cast<PyObject*>(const_cast<void*>(q)));
                 });
