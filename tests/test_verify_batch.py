@@ -266,6 +266,12 @@ def test_header_batch_wire_pack_equals_object_pack(core):
     bad = bytearray(raw[80:80 + 120 * 3])
     with pytest.raises(Exception):
         core.HeaderBatch.from_bytes(bytes(bad[:-1]), act)
+    # a mutable buffer is copied: changing it after the parse changes nothing the batch decodes
+    buf = bytearray(raw)
+    d = core.HeaderBatch.from_bytes(buf, act)
+    buf[:] = bytes(len(buf))
+    assert d.header(1).serialize(act) == objs[1].serialize(act)
+    assert [h.serialize(act) for h in d.headers(5000, 5002)] == [h.serialize(act) for h in objs[5000:5002]]
 
 
 def test_copy_into_is_bounded(core):
