@@ -50,11 +50,16 @@ def _baseline() -> tuple[float | None, str | None]:
             return float(v), "BASELINE.json published.kawpow_mhs"
     except (OSError, ValueError):
         pass
-    try:
-        with open(os.path.join(ROOT, "profiles", "ref_cpu_baseline", "epoch384.json")) as f:
-            return float(json.load(f)["mhs"]), "reference progpow::search, 8-core host, epoch 384 (BASELINE.md)"
-    except (OSError, ValueError, KeyError):
-        return None, None
+    # a copy of profiles/ref_cpu_baseline/epoch384.json inside the package: profiles/ is not sent
+    # to the GPU boxes (.gpurunignore)
+    for path in (os.path.join(ROOT, "nodexa_chain_core_amd", "data", "ref_cpu_baseline_epoch384.json"),
+                 os.path.join(ROOT, "profiles", "ref_cpu_baseline", "epoch384.json")):
+        try:
+            with open(path) as f:
+                return float(json.load(f)["mhs"]), "reference progpow::search, 8-core host, epoch 384 (BASELINE.md)"
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
 
 
 def _verify_headers_bench(log) -> dict | None:

@@ -210,6 +210,35 @@ PYBIND11_MODULE(_hip, m) {
         r["mem_bus_width"] = p.memoryBusWidth;
         return r;
     });
+    // Thin stream-ordered helpers for pipelines issued from Python (ops/header_batch.py): one
+    // pybind call each instead of torch's Python-level stream / event / copy wrappers.
+    m.def("event_create", [](bool timing) {
+        hipEvent_t e;
+        check(hipEventCreateWithFlags(&e, timing ? hipEventDefault : hipEventDisableTiming), "hipEventCreate");
+        return reinterpret_cast<uintptr_t>(e);
+    }, py::arg("timing") = false);
+    m.def("event_destroy", [](uintptr_t e) { check(hipEventDestroy(reinterpret_cast<hipEvent_t>(e)), "hipEventDestroy"); });
+    m.def("event_record", [](uintptr_t e, uintptr_t s) {
+        check(hipEventRecord(reinterpret_cast<hipEvent_t>(e), as_stream(s)), "hipEventRecord");
+    });
+    m.def("stream_wait_event", [](uintptr_t s, uintptr_t e) {
+        check(hipStreamWaitEvent(as_stream(s), reinterpret_cast<hipEvent_t>(e), 0), "hipStreamWaitEvent");
+    });
+    m.def("event_synchronize", [](uintptr_t e) {
+        check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(e)), "hipEventSynchronize");
+    }, py::call_guard<py::gil_scoped_release>());
+    m.def("event_elapsed_ms", [](uintptr_t a, uintptr_t b) {
+        float ms = 0;
+        check(hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(a), reinterpret_cast<hipEvent_t>(b)), "hipEventElapsedTime");
+        return ms;
+    });
+    m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
+        if (n) check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyDefault,
+                                    as_stream(s)), "hipMemcpyAsync");
+    });
+    m.def("memset_async", [](uintptr_t dst, int v, size_t n, uintptr_t s) {
+        if (n) check(hipMemsetAsync(reinterpret_cast<void*>(dst), v, n, as_stream(s)), "hipMemsetAsync");
+    });
     m.def("memcpy_htod", [](uintptr_t dst, uintptr_t src, size_t n) {
         check(hipMemcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyHostToDevice),
               "hipMemcpy(HtoD)");

@@ -56,14 +56,16 @@ class ResidentHeaderVerifier:
         with torch.cuda.device(self.dev):
             self.stream = torch.cuda.Stream(device=self.dev)
             self.side = [torch.cuda.Stream(device=self.dev) for _ in range(3)]  # Equihash + DGW, epoch ranges
-            self.ev_start = torch.cuda.Event(enable_timing=True)
-            self.ev_end = torch.cuda.Event(enable_timing=True)
-            self.ev_in, self.ev_jobs = torch.cuda.Event(), torch.cuda.Event()
-            self.ev_side = [torch.cuda.Event() for _ in self.side]
+            # raw HIP events, recorded / waited through the runtime's one-call helpers (torch's
+            # Python wrappers cost several microseconds per operation on this issue path)
+            h = self.h
+            self.ev_start, self.ev_end = h.event_create(True), h.event_create(True)
+            self.ev_in, self.ev_jobs = h.event_create(), h.event_create()
+            self.ev_side = [h.event_create() for _ in self.side]
             # the early copy of block hashes + nBits (models/verify.py prepares the index insert
             # from it while the full hashes run)
             self.early_stream = torch.cuda.Stream(device=self.dev)
-            self.ev_early = torch.cuda.Event()
+            self.ev_early = h.event_create()
         self.cap = 0
         self.in_cap = 0
         self.programs: dict[int, torch.Tensor] = {}
@@ -238,16 +240,15 @@ class ResidentHeaderVerifier:
         main = self.stream
         with torch.cuda.device(self.dev), torch.cuda.stream(main):
             s = int(main.cuda_stream)
-            self.ev_start.record(main)
-            self.din[:cur].copy_(self.in_host[:cur], non_blocking=True)
+            h.event_record(self.ev_start, s)
+            h.memcpy_async(base, self.in_host.data_ptr(), cur, s)
             if series is None:
-                self.out[n * 33:n * 37].zero_()  # nBits 0 = the host decides
-            self.ev_in.record(main)
+                h.memset_async(out + n * 33, 0, n * 4, s)  # nBits 0 = the host decides
+            h.event_record(self.ev_in, s)
             # Equihash solutions + block hashes and the DGW nBits depend only on the upload: a side
             # stream runs them beside the KawPow chain (mix-only -> jobs -> full hashes -> verdicts)
-            side = self.side[0]
-            side.wait_event(self.ev_in)
-            s0 = int(side.cuda_stream)
+            s0 = int(self.side[0].cuda_stream)
+            h.stream_wait_event(s0, self.ev_in)
             if m:
                 h.launch_equihash_verify(self.k_eq, self.h0, P("eq_msgs"), 112, m, P("eq_sols"), P("eq_verdict"), s0)
                 h.launch_sha256d(self.k_sha, P("eq_ser"), eq_len, eq_len, m, P("eq_hash"), False, s0)
@@ -257,18 +258,17 @@ class ResidentHeaderVerifier:
                              c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], s0)
             if m:
                 glue(2, 0, 0, s0)  # Equihash codes + block hashes (hb_verdict leaves those rows alone)
-            self.ev_side[0].record(side)
+            h.event_record(self.ev_side[0], s0)
             if nr:
                 h.launch_kawpow_mixonly(self.k_mo, P("rows") + lo_r * ROW, nr, ROW, self.mo.data_ptr() + lo_r * 128, s)
                 glue(0, lo_r, nr, s)  # jobs + the KawPow block hashes
-            self.ev_jobs.record(main)
+            h.event_record(self.ev_jobs, s)
             if ws == 1:  # the early copy: hashes + nBits as soon as hb_jobs and the side stream are done
-                es = self.early_stream
-                es.wait_event(self.ev_jobs)
-                es.wait_event(self.ev_side[0])
-                with torch.cuda.stream(es):
-                    self.early_host[:n * 36].copy_(self.out[n:n * 37], non_blocking=True)
-                self.ev_early.record(es)
+                es = int(self.early_stream.cuda_stream)
+                h.stream_wait_event(es, self.ev_jobs)
+                h.stream_wait_event(es, self.ev_side[0])
+                h.memcpy_async(self.early_host.data_ptr(), out + n, n * 36, es)
+                h.event_record(self.ev_early, es)
             if nr:
                 # one full-hash launch per epoch range, the ranges side by side: each is bound by
                 # its 64 dependent rounds per job, not by width
@@ -280,7 +280,7 @@ class ResidentHeaderVerifier:
                         continue
                     st = main if k == 0 else self.side[1 + (k - 1) % (len(self.side) - 1)]
                     if st is not main:
-                        st.wait_event(self.ev_jobs)
+                        h.stream_wait_event(int(st.cuda_stream), self.ev_jobs)
                     ep = V._device_epoch(epoch, self.device)
                     if WAVES:
                         tab = slot_tabs[k]
@@ -297,33 +297,33 @@ class ResidentHeaderVerifier:
                                                    self.full.data_ptr() + lo * 64, int(st.cuda_stream))
                     if st is not main:
                         ev = self.ev_side[1 + (k - 1) % (len(self.side) - 1)]
-                        ev.record(st)
-                        main.wait_event(ev)
+                        h.event_record(ev, int(st.cuda_stream))
+                        h.stream_wait_event(s, ev)
                     k += 1
                 glue(1, lo_r, nr, s)
-            main.wait_event(self.ev_side[0])
+            h.stream_wait_event(s, self.ev_side[0])
             if ws > 1:
                 self._gather(world, n, per, lo_r, hi_r)
-            self.out_host[:n * 37].copy_(self.out[:n * 37], non_blocking=True)
-            self.ev_end.record(main)
+            h.memcpy_async(self.out_host.data_ptr(), out, n * 37, s)
+            h.event_record(self.ev_end, s)
         t_issue = time.perf_counter()
         if overlap is not None:
             def early():
                 if ws != 1:
                     return None
-                self.ev_early.synchronize()
+                h.event_synchronize(self.ev_early)
                 e = self.early_host.numpy()
                 return e[:n * 32].reshape(n, 32), e[n * 32:n * 36].view("<u4")
 
             overlap(early)
         t_overlap = time.perf_counter()
-        self.ev_end.synchronize()
+        h.event_synchronize(self.ev_end)
         t_done = time.perf_counter()
         res = self.out_host.numpy()
         return {"codes": res[:n], "hashes": res[n:n * 33].reshape(n, 32), "bits": res[n * 33:n * 37].view("<u4"),
                 "pack_ms": (t_pack - t0) * 1e3, "issue_ms": (t_issue - t_pack) * 1e3,
                 "overlap_ms": (t_overlap - t_issue) * 1e3, "wait_ms": (t_done - t_overlap) * 1e3,
-                "device_ms": self.ev_start.elapsed_time(self.ev_end)}
+                "device_ms": h.event_elapsed_ms(self.ev_start, self.ev_end)}
 
     def _gather(self, world, n: int, per: int, lo_r: int, hi_r: int) -> None:
         """All ranks' codes and block hashes (33 bytes per row) into every rank's result buffer:
