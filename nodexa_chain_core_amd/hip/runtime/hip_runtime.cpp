@@ -232,10 +232,15 @@ PYBIND11_MODULE(_hip, m) {
         check(hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(a), reinterpret_cast<hipEvent_t>(b)), "hipEventElapsedTime");
         return ms;
     });
-    m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
-        if (n) check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, hipMemcpyDefault,
-                                    as_stream(s)), "hipMemcpyAsync");
-    });
+    // kind: "htod" / "dtoh" / "dtod" (an explicit direction spares the runtime a pointer lookup)
+    m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s, const std::string& kind) {
+        const hipMemcpyKind k = kind == "htod" ? hipMemcpyHostToDevice
+                                : kind == "dtoh" ? hipMemcpyDeviceToHost
+                                : kind == "dtod" ? hipMemcpyDeviceToDevice
+                                                 : throw std::invalid_argument("memcpy_async kind: htod, dtoh or dtod");
+        if (n) check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n, k, as_stream(s)),
+                     "hipMemcpyAsync");
+    }, py::arg("dst"), py::arg("src"), py::arg("n"), py::arg("stream"), py::arg("kind"));
     m.def("memset_async", [](uintptr_t dst, int v, size_t n, uintptr_t s) {
         if (n) check(hipMemsetAsync(reinterpret_cast<void*>(dst), v, n, as_stream(s)), "hipMemsetAsync");
     });

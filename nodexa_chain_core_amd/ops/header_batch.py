@@ -241,7 +241,7 @@ class ResidentHeaderVerifier:
         with torch.cuda.device(self.dev), torch.cuda.stream(main):
             s = int(main.cuda_stream)
             h.event_record(self.ev_start, s)
-            h.memcpy_async(base, self.in_host.data_ptr(), cur, s)
+            h.memcpy_async(base, self.in_host.data_ptr(), cur, s, "htod")
             if series is None:
                 h.memset_async(out + n * 33, 0, n * 4, s)  # nBits 0 = the host decides
             h.event_record(self.ev_in, s)
@@ -267,7 +267,7 @@ class ResidentHeaderVerifier:
                 es = int(self.early_stream.cuda_stream)
                 h.stream_wait_event(es, self.ev_jobs)
                 h.stream_wait_event(es, self.ev_side[0])
-                h.memcpy_async(self.early_host.data_ptr(), out + n, n * 36, es)
+                h.memcpy_async(self.early_host.data_ptr(), out + n, n * 36, es, "dtoh")
                 h.event_record(self.ev_early, es)
             if nr:
                 # one full-hash launch per epoch range, the ranges side by side: each is bound by
@@ -304,7 +304,7 @@ class ResidentHeaderVerifier:
             h.stream_wait_event(s, self.ev_side[0])
             if ws > 1:
                 self._gather(world, n, per, lo_r, hi_r)
-            h.memcpy_async(self.out_host.data_ptr(), out, n * 37, s)
+            h.memcpy_async(self.out_host.data_ptr(), out, n * 37, s, "dtoh")
             h.event_record(self.ev_end, s)
         t_issue = time.perf_counter()
         if overlap is not None:
