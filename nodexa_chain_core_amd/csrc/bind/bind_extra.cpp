@@ -519,6 +519,42 @@ void bind_extra(py::module_& m) {
             std::memcpy(d + o, s + o, std::min(kChunk, len - o));
         }, 1);
     }, py::arg("dst"), py::arg("offset"), py::arg("src"));
+    m.def("copy_into_many", [](const py::buffer& dst, const py::list& parts) {
+        // dst[offset : offset + len(src)] = src for every (offset, src) of `parts`, bounds checked
+        // before anything is written; sources of 256 KiB or more are copied on all cores (the
+        // resident verify stages its whole upload with this one call)
+        const py::buffer_info db = dst.request(true);
+        const size_t dlen = size_t(db.size) * size_t(db.itemsize);
+        char* d = static_cast<char*>(db.ptr);
+        std::vector<py::buffer_info> infos;
+        std::vector<size_t> offs;
+        infos.reserve(parts.size());
+        for (const py::handle& item : parts) {
+            const py::tuple t = item.cast<py::tuple>();
+            if (t.size() != 2) throw std::invalid_argument("copy_into_many: (offset, buffer) pairs");
+            const size_t o = t[0].cast<size_t>();
+            py::buffer_info bi = t[1].cast<py::buffer>().request();
+            const size_t len = size_t(bi.size) * size_t(bi.itemsize);
+            if (o > dlen || len > dlen - o) throw std::out_of_range("copy_into_many: a source does not fit");
+            offs.push_back(o);
+            infos.push_back(std::move(bi));
+        }
+        py::gil_scoped_release rel;
+        constexpr size_t kChunk = 64 << 10;
+        for (size_t k = 0; k < infos.size(); ++k) {
+            const char* src = static_cast<const char*>(infos[k].ptr);
+            const size_t len = size_t(infos[k].size) * size_t(infos[k].itemsize);
+            char* to = d + offs[k];
+            if (len < 4 * kChunk) {
+                if (len) std::memcpy(to, src, len);
+                continue;
+            }
+            parallel_for_each((len + kChunk - 1) / kChunk, [&](size_t c) {
+                const size_t o = c * kChunk;
+                std::memcpy(to + o, src + o, std::min(kChunk, len - o));
+            }, 1);
+        }
+    }, py::arg("dst"), py::arg("parts"));
     m.def("wave_slots", [](const py::buffer& kinds_buf, const py::buffer& heights_buf, size_t lo, size_t hi) {
         // kawpow_verify_waves' slot table for the KawPow rows (kind 0) of [lo, hi): the rows grouped
         // by ProgPoW period (height / 3), 4 slots per wave64 (one 16-lane group each), -1 = idle

@@ -177,13 +177,14 @@ class ResidentHeaderVerifier:
         off = {}
         cur = 0
         # per epoch range of this rank: the wave-uniform slot table (kawpow_verify_waves)
-        slot_tabs = []
+        slot_tabs = []  # int32 bytes per range
         if WAVES:
             for epoch, lo, hi in plan["ranges"]:
                 lo, hi = max(lo, lo_r), min(hi, hi_r)
                 if lo < hi:
-                    slot_tabs.append(np.frombuffer(_core.wave_slots(kinds, plan["heights"], lo, hi), dtype=np.int32))
-        nslots = sum(len(t) for t in slot_tabs)
+                    slot_tabs.append(_core.wave_slots(kinds, plan["heights"], lo, hi))
+        slot_lens = [len(t) // 4 for t in slot_tabs]
+        nslots = sum(slot_lens)
         for name, size in (("rows", n * ROW), ("kinds", n), ("times", (a + n) * 4), ("bits", (a + n) * 4),
                            ("eq_index", m * 4), ("eq_msgs", m * 128), ("eq_sols", m * 1344),
                            ("eq_ser", m * eq_len), ("eq_verdict", m * 4), ("eq_hash", m * 32),
@@ -193,35 +194,24 @@ class ResidentHeaderVerifier:
         self._ensure(n, cur)
         stage = self.in_host.numpy()
 
-        def put(name, arr):
-            o, size = off[name]
-            if size:
-                stage[o:o + size] = np.frombuffer(arr, dtype=np.uint8) if not isinstance(arr, np.ndarray) else \
-                    arr.view(np.uint8).ravel()[:size]
-
-        _core.copy_into(stage, off["rows"][0], batch.rows)  # the 1.3 MB of rows on all cores
-        put("kinds", kinds)
-        if series is not None:
-            times = np.empty(a + n, dtype="<u4")
-            bits = np.empty(a + n, dtype="<u4")
-            times[:a] = np.frombuffer(series[0], dtype="<u4")
-            bits[:a] = np.frombuffer(series[1], dtype="<u4")
-            times[a:] = plan["times"]
-            bits[a:] = plan["bits"]
-            put("times", times)
-            put("bits", bits)
-        if nslots:
-            put("slots", np.concatenate(slot_tabs))
+        # the whole upload staged by one native call: (offset, bytes-like) parts, bounds checked
+        parts = [(off["rows"][0], batch.rows), (off["kinds"][0], batch.kinds)]
+        if series is not None:  # the ancestors' (nTime, nBits), then the batch's own
+            parts += [(off["times"][0], series[0]), (off["times"][0] + 4 * a, plan["times"]),
+                      (off["bits"][0], series[1]), (off["bits"][0] + 4 * a, plan["bits"])]
+        o = off["slots"][0]
+        for t, ln in zip(slot_tabs, slot_lens):
+            parts.append((o, t))
+            o += 4 * ln
         if m == len(eq_index):  # every Equihash header is this rank's: the packed arrays as they are
-            put("eq_index", eq_index)
-            put("eq_msgs", batch.eq_msgs)
-            put("eq_sols", batch.eq_sols)
-            put("eq_ser", batch.eq_ser)
+            parts += [(off["eq_index"][0], batch.eq_index), (off["eq_msgs"][0], batch.eq_msgs),
+                      (off["eq_sols"][0], batch.eq_sols), (off["eq_ser"][0], batch.eq_ser)]
         elif m:
-            put("eq_index", eq_index[mine_eq].astype(np.uint32))
-            put("eq_msgs", np.frombuffer(batch.eq_msgs, np.uint8).reshape(-1, 128)[mine_eq])
-            put("eq_sols", np.frombuffer(batch.eq_sols, np.uint8).reshape(-1, 1344)[mine_eq])
-            put("eq_ser", np.frombuffer(batch.eq_ser, np.uint8).reshape(-1, eq_len)[mine_eq])
+            parts += [(off["eq_index"][0], eq_index[mine_eq].astype(np.uint32)),
+                      (off["eq_msgs"][0], np.ascontiguousarray(np.frombuffer(batch.eq_msgs, np.uint8).reshape(-1, 128)[mine_eq])),
+                      (off["eq_sols"][0], np.ascontiguousarray(np.frombuffer(batch.eq_sols, np.uint8).reshape(-1, 1344)[mine_eq])),
+                      (off["eq_ser"][0], np.ascontiguousarray(np.frombuffer(batch.eq_ser, np.uint8).reshape(-1, eq_len)[mine_eq]))]
+        _core.copy_into_many(stage, parts)
         t_pack = time.perf_counter()
         h = self.h
         base = self.din.data_ptr()
@@ -272,7 +262,7 @@ class ResidentHeaderVerifier:
             if nr:
                 # one full-hash launch per epoch range, the ranges side by side: each is bound by
                 # its 64 dependent rounds per job, not by width
-                slot_off = np.r_[0, np.cumsum([len(t) for t in slot_tabs])].tolist()
+                slot_off = [sum(slot_lens[:j]) for j in range(len(slot_lens))]  # in slots
                 k = 0
                 for epoch, lo, hi in plan["ranges"]:
                     lo, hi = max(lo, lo_r), min(hi, hi_r)
@@ -283,12 +273,11 @@ class ResidentHeaderVerifier:
                         h.stream_wait_event(int(st.cuda_stream), self.ev_jobs)
                     ep = V._device_epoch(epoch, self.device)
                     if WAVES:
-                        tab = slot_tabs[k]
                         h.launch_kawpow_verify_waves(self.k_waves, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(),
                                                      self.jobs.data_ptr() + lo * 48,
                                                      self.program_table(epoch).data_ptr(), _core.EPOCH_LENGTH // 3,
                                                      self.jprog.data_ptr() + lo * 4, hi - lo,
-                                                     P("slots") + slot_off[k] * 4, len(tab),
+                                                     P("slots") + slot_off[k] * 4, slot_lens[k],
                                                      self.full.data_ptr() + lo * 64, int(st.cuda_stream))
                     else:
                         h.launch_kawpow_verify_dag(self.k_dag, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(),

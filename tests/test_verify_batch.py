@@ -292,6 +292,14 @@ def test_copy_into_is_bounded(core):
         core.copy_into(small, 17, b"")
     with pytest.raises(Exception):
         core.copy_into(b"read-only target", 0, b"x")
+    # several parts in one call; nothing is written when any part does not fit
+    big = np.zeros(1 << 21, dtype=np.uint8)
+    core.copy_into_many(big, [(0, src), (1 << 20, b"xyz"), ((1 << 20) + 3, np.array([7, 8], np.uint32))])
+    assert bytes(big[:1 << 20]) == src.tobytes() and bytes(big[(1 << 20):(1 << 20) + 11]) == b"xyz" + bytes([7, 0, 0, 0, 8, 0, 0, 0])
+    clean = np.zeros(16, dtype=np.uint8)
+    with pytest.raises(Exception):
+        core.copy_into_many(clean, [(0, b"ok"), (15, b"too long")])
+    assert not clean.any()
 
 
 def test_prepare_commit_equals_accept(core):
