@@ -86,23 +86,30 @@ def test_discardfee_drops_dust_change(core, node_factory):  # noqa: F811
     fund(c)
     w = node.wallet
     assert w._change_discard_threshold() == (34 + 148) * 10_000 // 1000
-    # selection is largest-first, so size the payments against the largest spendable coin
-    coin = max(round(u["amount"] * 1e8) for u in c.listunspent())
+    # selection is largest-first, so size the payments against the coin the wallet itself picks
+    # for a payment of half the largest listed coin (that one input's value = outputs + fee)
+    top = max(round(u["amount"] * 1e8) for u in c.listunspent())
     from nodexa_chain_core_amd.wallet.wallet import WalletError
 
     for _ in range(8):
         dest = core.address_to_script(c.getnewaddress(), node.params.pubkey_prefix, node.params.script_prefix)
-        tx, fee = w.create_transaction([(dest, coin // 2)])
+        # a fixed 1 sat/B: a signature one byte longer or shorter moves the fee by 1 sat, not by
+        # more than the dust margin (the node's own rate can be thousands of sat/B here)
+        tx, fee = w.create_transaction([(dest, top // 2)], fee_rate=1000)
         assert len(tx.vout) == 2  # ordinary change
+        if len(tx.vin) != 1:
+            continue
+        coin = sum(o.value for o in tx.vout) + fee
         amount = coin - fee - 1000  # would leave 1000 sat of change: dust at the discard rate
         try:
-            tx2, fee2 = w.create_transaction([(dest, amount)])
+            tx2, fee2 = w.create_transaction([(dest, amount)], fee_rate=1000)
         except WalletError:
             # the second signature came out one byte longer than the first (DER length varies with
             # R and S): at this fee rate that byte costs more than the 1000 sat, so no change is
             # left at all; another destination gives other signatures
             continue
-        assert len(tx2.vout) == 1 and fee2 == coin - amount
+        assert len(tx2.vout) == 1 and fee2 == coin - amount, (len(tx2.vin), [o.value for o in tx2.vout], fee2, coin,
+                                                               amount, fee)
         break
     else:
         raise AssertionError("no attempt left dust change to discard")
