@@ -66,10 +66,6 @@ class ResidentHeaderVerifier:
             # from it while the full hashes run)
             self.early_stream = torch.cuda.Stream(device=self.dev)
             self.ev_early = h.event_create()
-            # DGW on a stream of its own, beside the Equihash checks (r4z11 trace: the two in a
-            # row on one stream held the early copy back by ~200 us)
-            self.dgw_stream = torch.cuda.Stream(device=self.dev)
-            self.ev_dgw = h.event_create()
         self.cap = 0
         self.in_cap = 0
         self.programs: dict[int, torch.Tensor] = {}
@@ -246,13 +242,10 @@ class ResidentHeaderVerifier:
             if m:
                 h.launch_equihash_verify(self.k_eq, self.h0, P("eq_msgs"), 112, m, P("eq_sols"), P("eq_verdict"), s0)
                 h.launch_sha256d(self.k_sha, P("eq_ser"), eq_len, eq_len, m, P("eq_hash"), False, s0)
-            sd = int(self.dgw_stream.cuda_stream)
-            h.stream_wait_event(sd, self.ev_in)
             if series is not None:
                 c = _core.dgw_constants(params)
                 h.launch_dgw(self.k_dgw, P("times"), P("bits"), out + n * 33, a, n, series[3], c["dgw_activation_block"],
-                             c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], sd)
-            h.event_record(self.ev_dgw, sd)
+                             c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], s0)
             if m:
                 glue(2, 0, 0, s0)  # Equihash codes + block hashes (hb_verdict leaves those rows alone)
             h.event_record(self.ev_side[0], s0)
@@ -264,7 +257,6 @@ class ResidentHeaderVerifier:
                 es = int(self.early_stream.cuda_stream)
                 h.stream_wait_event(es, self.ev_jobs)
                 h.stream_wait_event(es, self.ev_side[0])
-                h.stream_wait_event(es, self.ev_dgw)
                 h.memcpy_async(self.early_host.data_ptr(), out + n, n * 36, es, "dtoh")
                 h.event_record(self.ev_early, es)
             if nr:
@@ -299,7 +291,6 @@ class ResidentHeaderVerifier:
                     k += 1
                 glue(1, lo_r, nr, s)
             h.stream_wait_event(s, self.ev_side[0])
-            h.stream_wait_event(s, self.ev_dgw)
             if ws > 1:
                 self._gather(world, n, per, lo_r, hi_r)
             h.memcpy_async(self.out_host.data_ptr(), out, n * 37, s, "dtoh")
