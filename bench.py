@@ -323,14 +323,21 @@ def main() -> int:
     sync()
     W.barrier()
     sync()
+    gpu_start = gpu_snapshot(world)
+    end0 = svc.last_end_ms
     t_start = time.perf_counter()
     for _ in range(args.steps):
         svc.step()
     sync()
     W.barrier()
     elapsed = W.all_reduce_max(time.perf_counter() - t_start)
+    gpu_end = gpu_snapshot(world)
     total = batch * ws * args.steps
     mhs = total / elapsed / 1e6
+    # the same windows on the device clock: the end of the last warmup window to the end of the last
+    # timed one (each step takes one window), i.e. the rate without the host's edges; slowest rank
+    dev_span = W.all_reduce_max(max(0.0, (svc.last_end_ms - end0) / 1e3))
+    kernel_mhs = total / dev_span / 1e6 if dev_span > 0 else None
     # stop every rank's loop (stop packet; the queued window is aborted), then drain
     if leader is not None:
         leader.shutdown()
@@ -388,6 +395,10 @@ def main() -> int:
                 "parallelism": f"dp{ws}",
             },
             "loop": "miner/service.MiningService.step (the node's mining loop)",
+            "device_clock_mhs": round(kernel_mhs, 3) if kernel_mhs else None,
+            # rank 0's GPU at the start / end of the timed KawPow steps (amdsmi; empty when absent)
+            "gpu_start": gpu_start,
+            "gpu_end": gpu_end,
             "shares_rehashed": checked,
             "dag_build_s": round(dag_s, 3),
             "equihash_sol_per_s": eq["node_sol_per_s"] if eq else None,
@@ -400,6 +411,15 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     W.shutdown()
     return 0
+
+
+def gpu_snapshot(world) -> dict:
+    """Clocks, power and temperature of this rank's GPU (utils/gpuinfo; {} on CPU or without amdsmi)."""
+    if world.device.type != "cuda":
+        return {}
+    from nodexa_chain_core_amd.utils import gpuinfo
+
+    return gpuinfo.snapshot(world.device.index)
 
 
 def ep_bytes_gib(epoch: int) -> float:

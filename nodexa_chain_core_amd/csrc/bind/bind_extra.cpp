@@ -4,6 +4,8 @@
 #include "../crypto/aes.hpp"
 #include <pybind11/stl.h>
 
+#include <atomic>
+#include <stdexcept>
 #include <thread>
 
 #include "../chain/headerbatch.hpp"
@@ -519,6 +521,23 @@ void bind_extra(py::module_& m) {
             std::memcpy(d + o, s + o, std::min(kChunk, len - o));
         }, 1);
     }, py::arg("dst"), py::arg("offset"), py::arg("src"));
+    m.def("workpool_selftest", [](size_t n, int64_t throw_at) {
+        // test hook: sum of 0..n-1 over the pool; the part holding index `throw_at` (if >= 0)
+        // throws, which must reach the caller as an exception once every part has returned
+        std::atomic<uint64_t> sum{0};
+        {
+            py::gil_scoped_release rel;
+            parallel_for_range(n, [&](size_t lo, size_t hi) {
+                uint64_t s = 0;
+                for (size_t i = lo; i < hi; ++i) {
+                    if (throw_at >= 0 && i == size_t(throw_at)) throw std::runtime_error("workpool_selftest: part failed");
+                    s += i;
+                }
+                sum += s;
+            }, 1);
+        }
+        return uint64_t(sum.load());
+    }, py::arg("n"), py::arg("throw_at") = -1);
     m.def("copy_into_many", [](const py::buffer& dst, const py::list& parts) {
         // dst[offset : offset + len(src)] = src for every (offset, src) of `parts`, bounds checked
         // before anything is written; sources of 256 KiB or more are copied on all cores (the

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -24,10 +25,20 @@ struct Job {
     std::atomic<size_t> pending{0};  // parts not finished yet
     std::mutex mu;
     std::condition_variable done;
+    std::exception_ptr error;  // the first exception a part threw (rethrown on the caller)
+
+    void fail(std::exception_ptr e) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!error) error = e;
+    }
 
     void work() {
         for (size_t p; (p = next.fetch_add(1, std::memory_order_relaxed)) < parts;) {
-            (*fn)(p * step, std::min(n, (p + 1) * step));
+            try {
+                (*fn)(p * step, std::min(n, (p + 1) * step));
+            } catch (...) {
+                fail(std::current_exception());  // the part still counts as finished
+            }
             if (pending.fetch_sub(1, std::memory_order_acq_rel) == 1) {
                 std::lock_guard<std::mutex> g(mu);
                 done.notify_all();
@@ -62,12 +73,22 @@ public:
             ++gen_;
         }
         cv_.notify_all();
-        fn(0, std::min(n, job->step));
+        try {
+            fn(0, std::min(n, job->step));
+        } catch (...) {
+            job->fail(std::current_exception());
+        }
         job->work();  // the caller helps with the parts no worker has claimed yet
-        std::unique_lock<std::mutex> g(job->mu);
-        job->done.wait(g, [&] { return job->pending.load(std::memory_order_acquire) == 0; });
-        std::lock_guard<std::mutex> g2(mu_);
-        job_.reset();
+        {
+            // every part has returned before `fn` (the caller's) can go out of scope
+            std::unique_lock<std::mutex> g(job->mu);
+            job->done.wait(g, [&] { return job->pending.load(std::memory_order_acquire) == 0; });
+        }
+        {
+            std::lock_guard<std::mutex> g2(mu_);
+            job_.reset();
+        }
+        if (job->error) std::rethrow_exception(job->error);
     }
 
 private:

@@ -259,3 +259,88 @@ NX_DEV void eq_reconstruct_body(const uint32_t* refs, const uint32_t* c, uint32_
     }
 }
 
+// Leaf indices of every candidate of a pair-log solver (equihash_cb.hip): node ids at level L are
+// row ids, children(L, id, a, b) gives the two level-(L-1) ids a row was made of, and level-0 ids
+// are leaf indices. Same pruning, canonical order and duplicate check as eq_reconstruct_body.
+template <int BLOCK, class Children>
+NX_DEV void eq_reconstruct_tree(Children children, const uint32_t* c, uint32_t* sb) {
+    __shared__ uint32_t cur[512];
+    __shared__ uint32_t tmp[512];
+    __shared__ int bad;
+    __shared__ uint32_t slot;
+    const uint32_t ncand = min(c[0], (uint32_t)EQ_MAX_CAND);
+    for (uint32_t cand = blockIdx.x; cand < ncand; cand += gridDim.x) {
+        __syncthreads();  // previous iteration done with the LDS arrays
+        if (threadIdx.x == 0) {
+            cur[0] = c[1 + 2 * cand];
+            cur[1] = c[2 + 2 * cand];
+            bad = 0;
+        }
+        __syncthreads();
+        uint32_t width = 2;
+        for (int level = 8; level >= 1; --level) {
+            for (uint32_t t = threadIdx.x; t < width; t += BLOCK) {
+                uint32_t a, b;
+                children(level, cur[t], a, b);
+                tmp[2 * t] = a;
+                tmp[2 * t + 1] = b;
+            }
+            __syncthreads();
+            width *= 2;
+            for (uint32_t t = threadIdx.x; t < width; t += BLOCK) cur[t] = tmp[t];
+            __syncthreads();
+            if (width <= 64) {  // a repeated row at any level means repeated leaves
+                const uint32_t npairs = width * (width - 1) / 2;
+                for (uint32_t q = threadIdx.x; q < npairs; q += BLOCK) {
+                    uint32_t a = 0, rem = q;
+                    while (rem >= width - 1 - a) { rem -= width - 1 - a; ++a; }
+                    if (cur[a] == cur[a + 1 + rem]) bad = 1;
+                }
+                __syncthreads();
+                if (bad) break;
+            }
+        }
+        if (bad) continue;
+        // canonical order: every node's left subtree starts with the smaller index
+        for (uint32_t sz = 1; sz < 512; sz *= 2) {
+            for (uint32_t node = threadIdx.x; node < 512 / (2 * sz); node += BLOCK) {
+                const uint32_t l = node * 2 * sz, r = l + sz;
+                if (cur[l] > cur[r]) {
+                    for (uint32_t k = 0; k < sz; ++k) {
+                        const uint32_t x = cur[l + k];
+                        cur[l + k] = cur[r + k];
+                        cur[r + k] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // full duplicate check on a bitonic-sorted copy
+        for (uint32_t t = threadIdx.x; t < 512; t += BLOCK) tmp[t] = cur[t];
+        __syncthreads();
+        for (uint32_t k = 2; k <= 512; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t t = threadIdx.x; t < 512; t += BLOCK) {
+                    const uint32_t ixj = t ^ j;
+                    if (ixj > t) {
+                        const bool up = (t & k) == 0;
+                        const uint32_t a = tmp[t], b = tmp[ixj];
+                        if ((a > b) == up) {
+                            tmp[t] = b;
+                            tmp[ixj] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t t = threadIdx.x; t < 511; t += BLOCK)
+            if (tmp[t] == tmp[t + 1]) bad = 1;
+        __syncthreads();
+        if (bad) continue;
+        if (threadIdx.x == 0) slot = atomicAdd(&sb[0], 1u);
+        __syncthreads();
+        if (slot < EQ_MAX_SOL)
+            for (uint32_t t = threadIdx.x; t < 512; t += BLOCK) sb[1 + slot * 512 + t] = cur[t];
+    }
+}

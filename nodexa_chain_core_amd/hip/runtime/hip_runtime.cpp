@@ -652,6 +652,55 @@ PYBIND11_MODULE(_hip, m) {
     }, py::arg("ks"), py::arg("h0"), py::arg("msgs"), py::arg("input_len"), py::arg("num_inst"), py::arg("groups"),
        py::arg("hashes"), py::arg("refs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
        py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQP_FINAL_GROUPS);
+    // Coarse-bucket solver (equihash_cb.hip): ks = [eqc_gen, eqc_round1..8, eqc_final,
+    // eqc_reconstruct]; `groups` writers per instance, `seg` rows per segment (the caller sizes the
+    // buffers), a pair log of groups * EQC_COARSE * seg ids per instance and level. Buffers as
+    // documented on EquihashCbDev.
+    m.attr("EQC_COARSE") = EQC_COARSE;
+    m.attr("EQC_STAGE") = EQC_STAGE;
+    m.attr("EQC_ROW_WORDS") = EQC_ROW_WORDS;
+    m.attr("EQC_STAT_PAIRS") = EQC_STAT_PAIRS;
+    m.def("launch_equihash_cb_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
+                                         uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uint32_t groups,
+                                         uint32_t seg, uintptr_t hashes, uintptr_t pairs, uintptr_t counts, uintptr_t cands,
+                                         uintptr_t sols, uintptr_t stats, uintptr_t stream, uint32_t block,
+                                         uint32_t final_groups) {
+        if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash_cb kernels");
+        if (final_groups == 0 || final_groups > EQC_COARSE) throw std::invalid_argument("final_groups: 1..EQC_COARSE");
+        if (block != 1024) throw std::invalid_argument("block: 1024 (the build's EQC_BLOCK)");
+        if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
+        if (input_len > 124 || num_inst == 0 || num_inst > 65535) throw std::invalid_argument("bad equihash geometry");
+        // P a power of two in [16, EQC_COARSE]: every writer owns whole coarse buckets in the rounds,
+        // 2^20 / P digests in gen, and a segment of `seg` rows in every bucket (u16 counts)
+        if (groups < 16 || groups > EQC_COARSE || (groups & (groups - 1))) throw std::invalid_argument("groups: 16..EQC_COARSE, 2^k");
+        if (seg == 0 || seg > 65535) throw std::invalid_argument("seg: 1..65535");
+        EquihashCbDev p{};
+        p.msgs = reinterpret_cast<const uint64_t*>(msgs);
+        for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
+        p.input_len = input_len;
+        p.num_inst = num_inst;
+        p.groups = groups;
+        p.seg = seg;
+        p.pmax = EQC_COARSE * seg;
+        p.hashes = reinterpret_cast<uint32_t*>(hashes);
+        p.pairs = reinterpret_cast<uint32_t*>(pairs);
+        p.counts = reinterpret_cast<uint16_t*>(counts);
+        p.cands = reinterpret_cast<uint32_t*>(cands);
+        p.sols = reinterpret_cast<uint32_t*>(sols);
+        p.stats = reinterpret_cast<uint32_t*>(stats);
+        hipStream_t s = as_stream(stream);
+        const size_t n = num_inst;
+        check(hipMemsetAsync(p.cands, 0, n * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
+        check(hipMemsetAsync(p.sols, 0, n * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
+        check(hipMemsetAsync(p.stats, 0, n * EQP_STATS * 4, s), "memset stats");
+        // counts need no clear: every writer writes its whole row of every level
+        const dim3 grid(groups, num_inst);
+        for (size_t k = 0; k < 9; ++k) ks[k]->launch_bytes(grid, dim3(block), 0, s, &p, sizeof(p));
+        ks[9]->launch_bytes(dim3(final_groups, num_inst), dim3(block), 0, s, &p, sizeof(p));
+        ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
+    }, py::arg("ks"), py::arg("h0"), py::arg("msgs"), py::arg("input_len"), py::arg("num_inst"), py::arg("groups"),
+       py::arg("seg"), py::arg("hashes"), py::arg("pairs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
+       py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQC_COARSE);
     // The 11 kernel launches captured once into a hipGraph (fixed device buffers, so the graph
     // stays valid across batches; only the message words change, in place). Per batch: 3
     // memsets + one hipGraphLaunch instead of 14 stream operations.

@@ -149,6 +149,7 @@ class SlotResult:
     device_ms: float = 0.0
     aborted: int = 0
     algo: int = ALGO_KAWPOW
+    end_ms: float = 0.0  # device clock: the window's end, ms after the device's first window began
 
 
 class DeviceHung(RuntimeError):
@@ -197,6 +198,7 @@ class GpuSearchDevice:
             self.events = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             self.starts = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         self.meta: list[tuple | None] = [None, None]
+        self.anchor = None  # timing event before the first window: SlotResult.end_ms is relative to it
         self.gen_ptr = self.h.host_words_alloc(1)
         self.generation = 0
         self.pending_build: dict[int, object] = {}
@@ -309,6 +311,9 @@ class GpuSearchDevice:
         with torch.cuda.device(self.device), torch.cuda.stream(st):
             ring = self.rings[slot]
             ring[:4].zero_()
+            if self.anchor is None:
+                self.anchor = torch.cuda.Event(enable_timing=True)
+                self.anchor.record(st)
             self.starts[slot].record(st)
             s.launch(work.header_hash, start, count, work.target64(), stream=int(st.cuda_stream),
                      results=ring, gen_word=self.gen_ptr, generation=self.generation)
@@ -333,7 +338,7 @@ class GpuSearchDevice:
         shares = [x for x in shares if _core.hash_le(x.final_hash, work.boundary)]
         hashes = max(0, count - skipped * block)
         return SlotResult(work.job_id, start, count, hashes, shares, self.starts[slot].elapsed_time(ev), skipped,
-                          ALGO_KAWPOW)
+                          ALGO_KAWPOW, self.anchor.elapsed_time(ev))
 
     def abort(self) -> None:
         """Make every queued or running window stale (its remaining workgroups exit at start)."""

@@ -656,6 +656,7 @@ class MiningService:
         self.error: BaseException | None = None
         self.last_step_ms = 0.0
         self.coll_ms = 0.0
+        self.last_end_ms = 0.0  # device clock of the last window this rank took (SlotResult.end_ms)
         self.failures = 0          # consecutive failed windows on this rank
         self.total_failures = 0
         self.dev_alive = True
@@ -729,6 +730,7 @@ class MiningService:
                 res = self.pipe.step(w, start, count)
             if res is not None:
                 self.failures = 0
+                self.last_end_ms = res.end_ms
         except DeviceFault as e:
             self._device_failure(e)
             res = None

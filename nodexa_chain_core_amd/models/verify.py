@@ -346,7 +346,7 @@ def resident_ready(headers, act: int, device: int, mode: str = "auto") -> bool:
         if h.time >= act and not h.is_equihash():
             e = int(h.height) // _core.EPOCH_LENGTH
             epochs[e] = epochs.get(e, 0) + 1
-    return bool(epochs) and all((device, e) in V._epochs or n > V.LIGHT_MAX_JOBS for e, n in epochs.items())
+    return bool(epochs) and all(V.is_resident(device, e) or n > V.LIGHT_MAX_JOBS for e, n in epochs.items())
 
 
 def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, world=None) -> dict | None:
@@ -358,9 +358,17 @@ def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, wo
     from ..ops.header_batch import CODES
 
     t0 = time.perf_counter()
+    # a peer-chosen batch the resident path cannot take whole goes to process_headers, which
+    # rejects the bad header with its DoS score and keeps the valid prefix: an Equihash header whose
+    # solution is not 1344 bytes, or more KawPow epochs than the resident-DAG LRU holds (a DAG an
+    # in-flight range still reads must not be evicted by the next range's build)
+    if len(batch) == 0 or not batch.eq_uniform:
+        return None
+    from ..ops import verify as V
+
     v = resident_verifier(device)
     plan = v.plan(batch)
-    if plan is None or len(batch) == 0:
+    if plan is None or len({r[0] for r in plan["ranges"]}) > V.MAX_RESIDENT_DAGS:
         return None
     params = chain.params
     series = chain.dgw_ancestors(batch.header(0).prev)

@@ -1,15 +1,16 @@
-"""Equihash(200,9) solver on one MI355X (hip/kernels/equihash.hip).
+"""Equihash(200,9) solver on one MI355X.
 
-`EquihashSolver(num_inst)` solves `num_inst` inputs (different nonces) per
-launch sequence — 1 BLAKE2b generation kernel, 8 collision rounds, the final
-40-bit round and the index reconstruction, all enqueued on one stream with no
-host synchronisation in between. Every solution the GPU returns is re-verified
-by the CPU golden verifier (`_core.equihash_verify`) before it is reported.
+`EquihashSolver(num_inst)` solves `num_inst` inputs (different nonces) per launch sequence — 1
+BLAKE2b generation kernel, 8 collision rounds, the final 40-bit round and the index
+reconstruction, all enqueued on one stream with no host synchronisation in between — and checks
+every solution on the device (equihash.hip eq_verify_slots) before it is reported.
 
-Memory per instance, private-slot engine (default): 2 x 4096 x 2048 x 32 B row
-buffers (537 MB of address space, ~67 MB written per level) + 9 levels of
-index refs (151 MB) — 8 instances use ~5.5 GB of the 288 GB HBM3E. The
-global-slot engine needs 2 x 4096 x 768 x 32 B (201 MB) + 113 MB of refs.
+Engines (NODEXA_EQ_ENGINE selects; the default is the measured winner, profiles/README r5):
+  "cb"  coarse destination buckets (equihash_cb.hip): a level's rows stored by 8 digit bits
+        (256 buckets), fine buckets read as slices, back-pointers through a pair log. Memory at
+        16 instances: 2 x 16 x 256 x 16 x 721 x 28 B level buffers (2.6 GB) + the pair log
+        (16 x 9 x 3.0M x 8 B = 3.4 GB) of the 288 GB HBM3E.
+  "ps"  private slot segments in 4096 buckets (equihash_ps.hip): one EA write request per row.
 """
 from __future__ import annotations
 
@@ -23,11 +24,10 @@ from .. import _core
 from ..utils.trace import traced
 from . import runtime
 
-KERNELS = ["eq_gen"] + [f"eq_round{r}" for r in range(1, 9)] + ["eq_final", "eq_reconstruct"]
-PS_KERNELS = ["eqp_gen"] + [f"eqp_round{r}" for r in range(1, 9)] + ["eqp_final", "eqp_reconstruct"]
-# "ps": private slot segments per workgroup, pipelined rounds, 16-byte rows from level 5
-# (equihash_ps.hip; 5.64 ms per 8 solves, profiles/README r2d); "global": one global slot atomic
-# per row (equihash.hip; 6.54 ms). NODEXA_EQ_ENGINE overrides the default.
+ENGINE_KERNELS = {
+    "ps": ("equihash_ps", ["eqp_gen"] + [f"eqp_round{r}" for r in range(1, 9)] + ["eqp_final", "eqp_reconstruct"]),
+    "cb": ("equihash_cb", ["eqc_gen"] + [f"eqc_round{r}" for r in range(1, 9)] + ["eqc_final", "eqc_reconstruct"]),
+}
 DEFAULT_ENGINE = os.environ.get("NODEXA_EQ_ENGINE", "ps")
 
 
@@ -92,51 +92,56 @@ def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | 
 
 
 class EquihashSolver:
-    def __init__(self, num_inst: int = 8, device: int | None = None, banks: int = 8,
-                 code_object: str | None = None, engine: str | None = None, groups: int | None = None,
-                 block: int = 1024, final_groups: int | None = None):
+    def __init__(self, num_inst: int = 8, device: int | None = None, code_object: str | None = None,
+                 engine: str | None = None, groups: int | None = None, block: int = 1024,
+                 final_groups: int | None = None):
         """`code_object`: path of an alternative build of the engine's .hip (tuning sweeps).
-        `engine`: "ps" (private slot segments, `groups` workgroups per instance per round) or
-        "global" (global slot atomics, `banks` counters per bucket)."""
+        `engine`: "cb" or "ps" (module docstring); `groups` writers (workgroups) per instance per
+        round, by default so that groups x instances = 256 (one 1024-thread workgroup per CU)."""
         self.engine = DEFAULT_ENGINE if engine is None else engine
-        if self.engine not in ("ps", "global"):
+        if self.engine not in ENGINE_KERNELS:
             raise ValueError(f"unknown Equihash engine {self.engine!r}")
-        self.banks = int(banks)
-        # ps writers per instance: one 1024-thread workgroup per CU over the whole launch (P x
+        # writers per instance: one 1024-thread workgroup per CU over the whole launch (P x
         # instances = 256: 32 at 8 instances, 16 at the mining window's 16; profiles/README r4k:
         # 8.50 vs 8.65 ms at 16 instances, and 7.48 vs 4.38 ms when P=16 leaves half the CUs idle at 8)
         self.groups = int(groups) if groups else min(256, max(16, 1 << max(0, (256 // max(1, int(num_inst))).bit_length() - 1)))
-        self.block = int(block)  # ps: threads per workgroup, must match the code object's EQP_BLOCK
-        # ps: workgroups per instance of the final round (it writes no level, so any width works):
-        # ~4096 over the launch (256 at 16 instances: -1 % against 1024, r4k)
-        self.final_groups = int(final_groups or os.environ.get("NODEXA_EQP_FINAL_GROUPS", 0) or 0) or \
-            min(1024, max(64, 4096 // max(1, int(num_inst))))
+        self.block = int(block)  # threads per workgroup, must match the code object's EQP_BLOCK / EQC_BLOCK
         runtime.require_gpu()
         self.h = runtime.hip()
+        cb = self.engine == "cb"
+        # final round (writes no level, so any width works): ps ~4096 workgroups over the launch
+        # (256 at 16 instances: -1 % against 1024, r4k); cb one workgroup per coarse bucket at most
+        fg = int(final_groups or os.environ.get("NODEXA_EQP_FINAL_GROUPS", 0) or 0)
+        self.final_groups = fg or (self.h.EQC_COARSE if cb else min(1024, max(64, 4096 // max(1, int(num_inst)))))
         self.num_inst = int(num_inst)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
         self.params = _core.EquihashParams(200, 9)
-        B, C, W, L = self.h.EQ_BUCKETS, self.h.EQ_CAP, self.h.EQ_WORDS, self.h.EQ_LEVELS
+        B, L = self.h.EQ_BUCKETS, self.h.EQ_LEVELS
         ni = self.num_inst
-        ps = self.engine == "ps"
-        module, names = ("equihash_ps", PS_KERNELS) if ps else ("equihash", KERNELS)
+        module, names = ENGINE_KERNELS[self.engine]
         with torch.cuda.device(self.device):
             if code_object is None:
                 self.kernels = [runtime.static_kernel(module, k) for k in names]
             else:
                 co = runtime.load_code_object(code_object)
                 self.kernels = [co.function(k) for k in names]
-            if ps:
-                S, R = self.h.EQP_SLOTS, self.h.EQP_REF_STRIDE
+            if cb:
+                D, Wd = self.h.EQC_COARSE, self.h.EQC_ROW_WORDS
+                # rows per (coarse bucket, writer) segment: mean m = 2^21 / D / P (level sizes run
+                # up to ~4 % above 2^21) + 8 sigma, so an overflow (a host re-solve) stays ~1e-12
+                m = (1 << 21) / D / self.groups
+                self.seg = int(m * 1.04 + 8 * m ** 0.5 + 8)
+                self.pmax = D * self.seg
+                self.hashes = torch.empty(2 * ni * D * self.groups * self.seg * Wd, dtype=torch.int32,
+                                          device=self.device)
+                self.pairs = torch.empty(ni * L * self.groups * self.pmax * 2, dtype=torch.int32, device=self.device)
+                self.counts = torch.empty(ni * L * self.groups * D, dtype=torch.int16, device=self.device)
+            else:
+                S, R, W = self.h.EQP_SLOTS, self.h.EQP_REF_STRIDE, self.h.EQ_WORDS
                 self.hashes = torch.empty(2 * ni * B * S * W, dtype=torch.int32, device=self.device)
                 self.refs = torch.empty(ni * L * B * R, dtype=torch.int32, device=self.device)
                 self.counts = torch.empty(ni * L * self.groups * B, dtype=torch.uint8, device=self.device)
-                self.stats_buf = torch.zeros(ni * self.h.EQP_STATS, dtype=torch.int32, device=self.device)
-            else:
-                self.hashes = torch.empty(2 * ni * B * C * W, dtype=torch.int32, device=self.device)
-                self.refs = torch.empty(ni * L * B * C, dtype=torch.int32, device=self.device)
-                self.counts = torch.empty(ni * (L + 1) * B * self.h.EQ_MAX_BANKS, dtype=torch.int32,
-                                          device=self.device)
+            self.stats_buf = torch.zeros(ni * self.h.EQP_STATS, dtype=torch.int32, device=self.device)
             self.cands = torch.empty(ni * (1 + 2 * self.h.EQ_MAX_CAND), dtype=torch.int32, device=self.device)
             self.sols = torch.empty(ni * (1 + self.h.EQ_MAX_SOL * 512), dtype=torch.int32, device=self.device)
             self.msgs = torch.zeros(ni * 16, dtype=torch.int64, device=self.device)
@@ -144,8 +149,8 @@ class EquihashSolver:
             # back on the stream right after its kernels, so launch i+1 can be
             # queued before the host verifies launch i (GPU and CPU overlap)
             self._landing = [torch.empty(self.sols.numel(), dtype=torch.int32).pin_memory() for _ in range(2)]
-            # per launch: [inst][EQP_STATS] truncation counters (ps) + [inst] candidate counts
-            nstat = ni * self.h.EQP_STATS if ps else 0
+            # per launch: [inst][EQP_STATS] truncation counters + [inst] candidate counts
+            nstat = ni * self.h.EQP_STATS
             self._land_stats = [torch.zeros(nstat + ni, dtype=torch.int32).pin_memory() for _ in range(2)]
             # device-side check of every solution slot (equihash.hip eq_verify_slots) right after the
             # solve: the verdicts ride back with the solutions, so collect() needs no host pass over
@@ -160,11 +165,6 @@ class EquihashSolver:
         self._pending: list[tuple[list[bytes], torch.Tensor, torch.cuda.Event]] = []
         self._next = 0
         self.h0 = blake2b_h0()
-        # hipGraph of the 11 solve kernels (captured on first launch; the 3 state clears stay
-        # stream memsets). Opt-in (NODEXA_EQ_GRAPH=1, global engine) until measured: see
-        # profiles/README r1u
-        self.use_graph = os.environ.get("NODEXA_EQ_GRAPH", "0") == "1" and not ps
-        self._graph = None
         self.input_len = None
 
     def launch(self, inputs: list[bytes], stream: int | None = None) -> None:
@@ -187,14 +187,18 @@ class EquihashSolver:
             stage.copy_(torch.frombuffer(buf, dtype=torch.int64))
             self.msgs.copy_(stage, non_blocking=True)
             s = runtime.current_stream_handle() if stream is None else stream
-            if self.engine == "ps":
+            if self.engine == "cb":
+                self.h.launch_equihash_cb_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
+                                                self.num_inst, self.groups, self.seg, self.hashes.data_ptr(),
+                                                self.pairs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
+                                                self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block,
+                                                self.final_groups)
+            else:
                 self.h.launch_equihash_ps_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
                                                 self.num_inst, self.groups, self.hashes.data_ptr(),
                                                 self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
                                                 self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block,
                                                 self.final_groups)
-            else:
-                self._issue_global(s)
             self.h.launch_equihash_verify_slots(self.verify_kernel, self.h0, self.msgs.data_ptr(), self.input_len,
                                                 self.num_inst, self.sols.data_ptr(), self.verdicts.data_ptr(), s)
             land = self._landing[self._next]
@@ -204,25 +208,19 @@ class EquihashSolver:
             land.copy_(self.sols, non_blocking=True)
             lver.copy_(self.verdicts, non_blocking=True)
             nstat = lstat.numel() - self.num_inst
-            if nstat:
-                lstat[:nstat].copy_(self.stats_buf, non_blocking=True)
+            lstat[:nstat].copy_(self.stats_buf, non_blocking=True)
             lstat[nstat:].copy_(self.cands.view(self.num_inst, -1)[:, 0], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
         self._pending.append((list(inputs), (land, lstat, lver), ev))
 
-    def _issue_global(self, s: int) -> None:
-        args = (self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst, self.hashes.data_ptr(),
-                self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(), self.sols.data_ptr())
-        if self.use_graph and self._graph is None:
-            try:
-                self._graph = self.h.capture_equihash_solve(*args, self.banks)
-            except RuntimeError:
-                self.use_graph = False  # capture unsupported here: plain launches
-        if self._graph is not None:
-            self._graph.launch(s)
-        else:
-            self.h.launch_equihash_solve(*args, s, self.banks)
+    def _lossy(self, st: np.ndarray) -> bool:
+        """Whether one instance's stats row records a loss: segment / staging overflow (slots
+        0-10), or (cb) pair ids beyond a writer's range; slot 11 is a diagnostic maximum."""
+        lost = bool(st[:self.h.EQP_STAT_STAGE + 1].any())
+        if self.engine == "cb":
+            lost |= bool(st[self.h.EQC_STAT_PAIRS])
+        return lost
 
     def collect_arrays(self, inputs: list[bytes] | None = None, verify: str = "device") -> list[np.ndarray]:
         """Solutions of the oldest queued launch (waits only for that launch), one (m, 512) uint32
@@ -245,15 +243,14 @@ class EquihashSolver:
         out = []
         for i in range(self.num_inst):
             truncated = int(st[nstat + i]) > self.h.EQ_MAX_CAND
-            if nstat:
-                truncated |= bool(st[i * self.h.EQP_STATS:i * self.h.EQP_STATS + self.h.EQP_STAT_STAGE + 1].any())
+            truncated |= self._lossy(st[i * self.h.EQP_STATS:(i + 1) * self.h.EQP_STATS])
             if truncated:
                 # a bucket, chain or candidate cap cut something: the device result may miss a
                 # solution, so this instance is solved again on the golden solver (it keeps the
                 # solution set exact by construction)
                 self.fallbacks += 1
-                self.fallback_log.append({"stats": st[i * self.h.EQP_STATS:(i + 1) * self.h.EQP_STATS].tolist()
-                                          if nstat else [], "candidates": int(st[nstat + i])})
+                self.fallback_log.append({"stats": st[i * self.h.EQP_STATS:(i + 1) * self.h.EQP_STATS].tolist(),
+                                          "candidates": int(st[nstat + i])})
                 sols, _ = _core.equihash_solve_cpu(self.params, inputs[i], ms, 0)
                 out.append(np.asarray(sols, dtype=np.uint32).reshape(-1, 512))
                 continue
@@ -286,18 +283,11 @@ class EquihashSolver:
 
     def stats(self) -> dict:
         """Per-level fill of the last solve (instance 0) — overflow diagnostics."""
-        B, L = self.h.EQ_BUCKETS, self.h.EQ_LEVELS
-        if self.engine == "ps":
-            c = self.counts[: L * self.groups * B].view(L, self.groups, B).to(torch.int32).sum(1).cpu()
-            dropped = self.stats_buf[: self.h.EQP_STATS].cpu().tolist()
-            return {"rows_per_level": [int(x) for x in c.sum(1)], "max_fill": [int(x) for x in c.max(1).values],
-                    "cap": self.h.EQP_STAGE, "dropped_per_level": dropped[:L],
-                    "stage_dropped": dropped[self.h.EQP_STAT_STAGE], "largest_bucket": dropped[self.h.EQP_STAT_STAGE_MAX],
-                    "candidates": int(self.cands[0].item())}
-        nb = self.h.EQ_MAX_BANKS
-        per = self.h.EQ_CAP // self.banks
-        c = self.counts[: (L + 1) * B * nb].view(L + 1, B, nb)[:, :, :self.banks].cpu()
-        over = int((c > per).sum())
-        c = c.clamp(max=per).sum(2)
-        return {"rows_per_level": [int(x) for x in c.sum(1)][:L], "max_fill": [int(x) for x in c.max(1).values][:L],
-                "cap": self.h.EQ_CAP, "overflowed_banks": over, "candidates": int(self.cands[0].item())}
+        L = self.h.EQ_LEVELS
+        D = self.h.EQC_COARSE if self.engine == "cb" else self.h.EQ_BUCKETS
+        c = self.counts[: L * self.groups * D].view(L, self.groups, D).to(torch.int32).sum(1).cpu()
+        dropped = self.stats_buf[: self.h.EQP_STATS].cpu().tolist()
+        return {"rows_per_level": [int(x) for x in c.sum(1)], "max_fill": [int(x) for x in c.max(1).values],
+                "cap": self.h.EQC_STAGE if self.engine == "cb" else self.h.EQP_STAGE, "dropped_per_level": dropped[:L],
+                "stage_dropped": dropped[self.h.EQP_STAT_STAGE], "largest_bucket": dropped[self.h.EQP_STAT_STAGE_MAX],
+                "lost_ids": dropped[12], "candidates": int(self.cands[0].item())}

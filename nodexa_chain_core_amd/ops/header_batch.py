@@ -171,7 +171,7 @@ class ResidentHeaderVerifier:
         m = len(mine_eq)
         eq_len = int(batch.eq_ser_len)
         if m and not batch.eq_uniform:
-            raise ValueError("malformed Equihash header in the batch")
+            raise ValueError("malformed Equihash header in the batch")  # process_batch_resident filters these
         # staging layout (one pinned buffer, one H2D copy)
         a = series[2] if series is not None else 0
         off = {}
@@ -227,6 +227,14 @@ class ResidentHeaderVerifier:
                                   self.jprog.data_ptr(), self.full.data_ptr(), out, P("eq_index"), P("eq_verdict"),
                                   P("eq_hash"), n, m, first, count, _core.EPOCH_LENGTH, cp, lim, st)
 
+        # every epoch DAG of the plan resolved (built or pinned in the LRU) before the first launch:
+        # a build inside the issue loop could evict a DAG a side-stream range is still reading
+        epochs_dev = {}
+        for epoch, lo, hi in plan["ranges"]:
+            if max(lo, lo_r) < min(hi, hi_r) and epoch not in epochs_dev:
+                epochs_dev[epoch] = V._device_epoch(epoch, self.device)
+        if len(epochs_dev) > V.MAX_RESIDENT_DAGS:
+            raise ValueError("batch spans more epochs than the resident DAGs")
         main = self.stream
         with torch.cuda.device(self.dev), torch.cuda.stream(main):
             s = int(main.cuda_stream)
@@ -271,7 +279,7 @@ class ResidentHeaderVerifier:
                     st = main if k == 0 else self.side[1 + (k - 1) % (len(self.side) - 1)]
                     if st is not main:
                         h.stream_wait_event(int(st.cuda_stream), self.ev_jobs)
-                    ep = V._device_epoch(epoch, self.device)
+                    ep = epochs_dev[epoch]
                     if WAVES:
                         h.launch_kawpow_verify_waves(self.k_waves, ep.dag.data_ptr(), ep.items2048, ep.l1.data_ptr(),
                                                      self.jobs.data_ptr() + lo * 48,
@@ -291,6 +299,8 @@ class ResidentHeaderVerifier:
                     k += 1
                 glue(1, lo_r, nr, s)
             h.stream_wait_event(s, self.ev_side[0])
+            if ws == 1:  # the early copy reads `out` and lands in early_host: both done before ev_end
+                h.stream_wait_event(s, self.ev_early)
             if ws > 1:
                 self._gather(world, n, per, lo_r, hi_r)
             h.memcpy_async(self.out_host.data_ptr(), out, n * 37, s, "dtoh")

@@ -20,6 +20,7 @@ below LIGHT_MAX_JOBS jobs per epoch.
 from __future__ import annotations
 
 import struct
+import threading
 
 import numpy as np
 import torch
@@ -34,30 +35,40 @@ JOB = struct.Struct("<8IQII")
 JOB_DT = np.dtype([("hh", "<u4", 8), ("nonce", "<u8"), ("bn", "<u4"), ("pad", "<u4")])
 LIGHT_MAX_JOBS = 50_000
 MAX_RESIDENT_DAGS = 4  # per device: <= 4 x ~5 GiB of the 288 GiB HBM
+# the miner thread offers its DAGs (share_epoch) while the P2P thread verifies (_device_epoch):
+# every access to _epochs holds this lock
+_epochs_lock = threading.RLock()
 
 
 def _device_epoch(epoch: int, device: int) -> DeviceEpoch:
     key = (device, epoch)
-    e = _epochs.get(key)
-    if e is None:
-        mine = [k for k in _epochs if k[0] == device]  # LRU: a header batch often spans 2 epochs
-        for k in mine[:max(0, len(mine) - MAX_RESIDENT_DAGS + 1)]:
-            _epochs.pop(k)
-        with torch.cuda.device(device):
-            e = DeviceEpoch(epoch, device=device)
-            e.build()
-            torch.cuda.synchronize()
-        _epochs[key] = e
-    else:
-        _epochs[key] = _epochs.pop(key)  # most recently used last
-    return e
+    with _epochs_lock:
+        e = _epochs.get(key)
+        if e is None:
+            mine = [k for k in list(_epochs) if k[0] == device]  # LRU: a header batch often spans 2 epochs
+            for k in mine[:max(0, len(mine) - MAX_RESIDENT_DAGS + 1)]:
+                _epochs.pop(k)
+            with torch.cuda.device(device):
+                e = DeviceEpoch(epoch, device=device)
+                e.build()
+                torch.cuda.synchronize()
+            _epochs[key] = e
+        else:
+            _epochs[key] = _epochs.pop(key)  # most recently used last
+        return e
+
+
+def is_resident(device: int, epoch: int) -> bool:
+    with _epochs_lock:
+        return (device, epoch) in _epochs
 
 
 def share_epoch(device: int, epoch: int, e: DeviceEpoch) -> None:
     """Offer a DAG built elsewhere on `device` (the miner's, miner/search.GpuSearchDevice) to batch
     verify: a mining node then verifies the current epoch's headers against the DAG it mines on
     instead of building a second 4 GiB copy (read-only on both sides)."""
-    _epochs.setdefault((device, epoch), e)
+    with _epochs_lock:
+        _epochs.setdefault((device, epoch), e)
 
 
 def _light_epoch(epoch: int, device: int) -> DeviceEpoch:
@@ -75,7 +86,8 @@ def _light_epoch(epoch: int, device: int) -> DeviceEpoch:
 def register_resident(epoch_dev: DeviceEpoch) -> None:
     """Let verification reuse a DAG some other component (the miner) keeps resident."""
     if epoch_dev.built and epoch_dev.dag is not None:
-        _epochs[(epoch_dev.device.index, epoch_dev.epoch)] = epoch_dev
+        with _epochs_lock:
+            _epochs[(epoch_dev.device.index, epoch_dev.epoch)] = epoch_dev
 
 
 def _pack_jobs(block_numbers, header_hashes, nonces) -> np.ndarray:
@@ -191,7 +203,7 @@ def gpu_hash_jobs(jobs: np.ndarray, device: int = 0, mode: str = "auto") -> np.n
         idx = np.flatnonzero(epochs == epoch)
         m = mode
         if m == "auto":
-            m = "dag" if (device, epoch) in _epochs or len(idx) > LIGHT_MAX_JOBS else "light"
+            m = "dag" if is_resident(device, epoch) or len(idx) > LIGHT_MAX_JOBS else "light"
         with torch.cuda.device(device):
             if m == "dag":
                 out[idx] = _run_dag(_device_epoch(epoch, device), jobs[idx])

@@ -121,3 +121,25 @@ def test_synthetic_fixture_chain(core, name):
     sample = headers[:40] + headers[7490:7510] + eq
     res = verify_headers(params, sample)
     assert all(r["valid"] for r in res), [r for r in res if not r["valid"]][:3]
+
+
+def test_resident_path_declines_malformed_equihash(core, mixed_chain):
+    """a peer's `headers` batch with one Equihash header whose solution is not 1344 bytes
+    must not reach the resident pipeline (it would raise and drop the peer unscored); the resident
+    entry declines it (None), and process_headers keeps the valid prefix and rejects the bad
+    header as invalid-solution (the DoS-100 rule of net/p2p.on_headers)."""
+    from nodexa_chain_core_amd.models.verify import process_batch_resident, process_headers
+
+    params, headers = mixed_chain
+    act = params.kawpow_activation_time
+    last = headers[-1]
+    bad = core.BlockHeader.deserialize(last.serialize(act), act)
+    bad.solution = bytes(last.solution[:-1])
+    batch_headers = list(headers[:-1]) + [bad]
+    batch = core.HeaderBatch.from_headers(batch_headers, act)
+    assert not batch.eq_uniform
+    chain = core.HeaderChain(params)
+    assert process_batch_resident(chain, batch, last.time + 60, device=0) is None  # no GPU touched
+    res = process_headers(chain, batch_headers, last.time + 60, gpus=None)
+    assert res["accepted"] == len(headers) - 1
+    assert res["reject"]["reason"] == "invalid-solution"

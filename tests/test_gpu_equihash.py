@@ -4,9 +4,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["global", "ps"])
+@pytest.fixture(scope="module", params=["cb", "ps"])
 def solver(gpu, request):
-    """Both engines: global slot atomics (equihash.hip) and private slot segments (equihash_ps.hip)."""
+    """Both engines: coarse buckets + pair log (equihash_cb.hip) and private slot segments
+    (equihash_ps.hip)."""
     import torch
 
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
@@ -31,9 +32,8 @@ def test_gpu_solutions_valid_and_match_cpu(core, solver):
     gpu = solver.solve(inputs)  # every solution already CPU-verified inside collect()
     st = solver.stats()
     assert max(st["max_fill"]) <= st["cap"], st
-    if solver.engine == "ps":
-        assert sum(st["dropped_per_level"]) < 64, st  # segment / staging overflow stays rare
-        assert min(st["rows_per_level"]) > 1_900_000, st
+    assert sum(st["dropped_per_level"]) < 64, st  # segment / staging overflow stays rare
+    assert min(st["rows_per_level"]) > 1_900_000, st
     total_gpu = sum(len(s) for s in gpu)
     total_cpu = 0
     for inp, g in zip(inputs, gpu):
@@ -45,15 +45,16 @@ def test_gpu_solutions_valid_and_match_cpu(core, solver):
     assert total_gpu >= total_cpu - 1  # bucket-capacity drops may lose at most a rare solution
 
 
-def test_ps_solver_exactly_matches_cpu_on_16_inputs(core, gpu):
-    """The default engine is lossless: every device-side cap (segment, staging, chain, candidate)
-    is counted per instance and a counted instance is re-solved on the golden solver, so the
-    solution sets equal the CPU solver's on every input."""
+@pytest.mark.parametrize("engine", ["cb", "ps"])
+def test_solver_exactly_matches_cpu_on_16_inputs(core, gpu, engine):
+    """Both engines are lossless: every device-side cap (segment, staging, chain, candidate, pair
+    id) is counted per instance and a counted instance is re-solved on the golden solver, so the
+    solution sets equal the CPU solver's on every input — and no instance needed that here."""
     import torch
 
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
-    s = EquihashSolver(num_inst=8, device=0, engine="ps")
+    s = EquihashSolver(num_inst=8, device=0, engine=engine)
     p = core.EquihashParams(200, 9)
     inputs = [bytes([0x5A]) * 80 + i.to_bytes(32, "little") for i in range(16)]
     gpu = s.solve(inputs[:8]) + s.solve(inputs[8:])
@@ -63,6 +64,7 @@ def test_ps_solver_exactly_matches_cpu_on_16_inputs(core, gpu):
         assert sorted(map(tuple, g)) == sorted(map(tuple, cpu)), inp[-32:].hex()
         total += len(g)
     assert total > 8
+    assert s.fallbacks == 0, s.fallback_log
     del s
     torch.cuda.empty_cache()
 

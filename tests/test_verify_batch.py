@@ -512,3 +512,15 @@ def test_resident_ready_policy(chain_fixture):
     finally:
         V._epochs.clear()
         V._epochs.update(saved)
+
+
+def test_workpool_exception_reaches_caller():
+    """csrc/util/workpool.cpp: a part that throws (on a worker or on the caller) is rethrown on the
+    caller after every part has returned, and the pool keeps working afterwards."""
+    c = core()
+    n = 100_000
+    assert c.workpool_selftest(n) == n * (n - 1) // 2
+    for bad in (0, n // 2, n - 1):
+        with pytest.raises(RuntimeError, match="part failed"):
+            c.workpool_selftest(n, bad)
+        assert c.workpool_selftest(n) == n * (n - 1) // 2
