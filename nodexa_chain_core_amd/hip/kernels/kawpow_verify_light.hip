@@ -283,6 +283,12 @@ extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(Kawpo
     uint32_t pi = __builtin_amdgcn_readfirstlane(p.job_program[first]);
     pi = pi < p.num_programs ? pi : 0;  // host validates; never index past the table
     const uint32_t* prog = p.programs + (size_t)pi * KV_PROG_WORDS;
+    // the period's 51 op words, loaded once into SGPRs: inside the round loop every op word is a
+    // literal SGPR (the loop below is unrolled), so no op waits on a scalar load -- and the LDS L1
+    // lookups, which share the lgkm counter with scalar loads, no longer wait behind them either
+    uint32_t pw[51];
+#pragma unroll
+    for (int i = 0; i < 51; ++i) pw[i] = __builtin_amdgcn_readfirstlane(prog[i]);
     const KawpowVerifyJob j = p.jobs[jj];
 
     uint32_t st2[8];
@@ -322,16 +328,20 @@ extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(Kawpo
         const uint32_t index = kl_mod(__shfl(mix[0], (int)(r & 15), 16), p.items);
         // lane l merges words ((l^r)%16)*4..+3 of the 2048-bit item: load exactly that slice
         const uint4 d = dag[(size_t)index * 16 + ((lane ^ r) & 15)];
-#pragma unroll 1
+        // opaque per round: the op fields are decoded where they are used (SALU, next to the op)
+        // instead of being hoisted out of the loop into ~150 loop-invariant SGPRs that spill
+#pragma unroll
+        for (int i = 0; i < 51; ++i) asm volatile("" : "+s"(pw[i]));
+#pragma unroll
         for (int i = 0; i < 18; ++i) {
             if (i < 11) {
-                const uint32_t op = __builtin_amdgcn_readfirstlane(prog[i]);
+                const uint32_t op = pw[i];
                 const uint32_t a = kw_get(mix, op);
                 const uint32_t dst = (op >> 8) & 31;
                 kw_set(mix, dst, kl_merge(kw_get(mix, dst), l1[a & 4095u], (op >> 16) & 3, op >> 24));
             }
-            const uint32_t op = __builtin_amdgcn_readfirstlane(prog[11 + i]);
-            const uint32_t mg = __builtin_amdgcn_readfirstlane(prog[29 + i]);
+            const uint32_t op = pw[11 + i];
+            const uint32_t mg = pw[29 + i];
             const uint32_t v = kl_math(kw_get(mix, op), kw_get(mix, op >> 8), (op >> 16) & 15);
             const uint32_t dst = op >> 24;
             kw_set(mix, dst, kl_merge(kw_get(mix, dst), v, mg & 3, mg >> 8));
@@ -339,7 +349,7 @@ extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(Kawpo
         const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint32_t op = __builtin_amdgcn_readfirstlane(prog[47 + i]);
+            const uint32_t op = pw[47 + i];
             kw_set(mix, op, kl_merge(kw_get(mix, op), dw[i], (op >> 8) & 3, op >> 16));
         }
     }

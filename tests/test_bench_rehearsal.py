@@ -18,8 +18,9 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("n", [1, 2])
+@pytest.mark.parametrize("n", [1, 2, 8])
 def test_bench_contract_on_cpu(n):
+    """n = 8: the driver's whole-node launch shape (8 ranks, one JSON line with n_gpus 8)."""
     args = ["bench.py", "--gpus", str(n), "--device", "cpu", "--epoch", "0", "--steps", "2", "--warmup", "1",
             "--batch", "4", "--equihash", "0", "--verify", "0", "--quiet"]
     if n > 1:

@@ -77,8 +77,9 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_gloo_collectives(world):
+    """World 8 = one rank per GPU of an MI355X node: 8-shard DAG gather, record gather of 8 ranks."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

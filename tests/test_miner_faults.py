@@ -41,6 +41,23 @@ def test_gloo_world3_evicts_failing_rank_and_repartitions(tmp_path, core):
     _check_disjoint(tmp_path, 3, rep)
 
 
+def test_gloo_world8_shrinks_to_7(tmp_path, core):
+    """The node's 8-rank shape (one rank per GPU of an MI355X node) with rank 5's device failing
+    every window: the 8 ranks mine from disjoint nonce ranges, rank 5 is evicted, and the other 7
+    re-form the world (8 -> 7) and finish the blocks; every share the node took re-checks on the host."""
+    from nodexa_chain_core_amd.miner.service import EXIT_DEVICE_FAILED
+
+    codes, outs, report = _run_world(tmp_path, 8, blocks=2, timeout_s=6.0,
+                                     rank_env={5: {"NODEXA_MINER_FAILRATE": "1"}})
+    assert codes[5] == EXIT_DEVICE_FAILED, "\n".join(outs)
+    assert all(codes[r] == 0 for r in range(8) if r != 5), (codes, "\n".join(outs))
+    rep = json.load(open(report))
+    assert rep["height"] == 4 and rep["world_size"] == 7 and rep["stats"]["bad_shares"] == 0
+    assert [g["rank"] for g in rep["gpus_first"]] == list(range(8))
+    assert len(rep["gpus_last"]) == 7
+    _check_disjoint(tmp_path, 8, rep)
+
+
 def test_single_rank_all_failing_raises(state):
     from nodexa_chain_core_amd.miner.service import Miner
 
