@@ -85,6 +85,8 @@ class ValidationInterface:
 
 
 DB_FORMATS = ("leveldb", "journal")
+# chainstate/ record: the height at which a reference datadir's assets/ databases were imported
+ASSETS_IMPORT_KEY = b"\x02assets.import"
 
 
 def detect_db_format(datadir: str | None, requested: str | None = None) -> str:
@@ -215,6 +217,7 @@ class ChainState:
         self.block_version_override: int | None = None  # -blockversion (regtest only)
         self.transactions_updated = 0
         self.datadir = datadir
+        self.assets_import_height = -1  # see _import_reference_assets
         self.store = None
         self.start_time = time.time()
         self.index_log: BlockIndexLog | None = None
@@ -921,8 +924,14 @@ class ChainState:
             # asset records live in the same store and are flushed in the same batch as the coins
             if not _core.assets_load_ldb(self.assets, self.coins_db, self._coins_obf) or \
                     self.assets.best_block != self.coins.best_block:
-                log.log_printf("asset records missing or out of step with the UTXO set; replaying from genesis")
-                loaded = False
+                if self._import_reference_assets():
+                    pass  # a reference datadir: its assets/ databases describe the chainstate's block
+                else:
+                    log.log_printf("asset records missing or out of step with the UTXO set; replaying from genesis")
+                    loaded = False
+            raw = self.coins_db.get(ASSETS_IMPORT_KEY) if loaded else None
+            if raw is not None:
+                self.assets_import_height = int.from_bytes(_core.chaindb_xor(raw, self._coins_obf)[:4], "little")
         elif loaded:  # the asset state must describe the same block as the UTXO snapshot
             raw = None
             if os.path.exists(self.assets_path):
@@ -980,6 +989,57 @@ class ChainState:
                 self.coins.compact(self.coins_path, self.coins_log)  # a fresh snapshot restarts the journal
         with self.lock:
             self._activate()
+
+    def _import_reference_assets(self) -> bool:
+        """A reference datadir's asset state: CAssetsDB (`assets/`) and CRestrictedDB
+        (`assets/restricted`), which the reference flushes together with its chainstate
+        (src/validation.cpp FlushStateToDisk), read into this engine's asset records
+        (csrc/store/chaindb.cpp assets_import_reference) and written to chainstate/ in the same
+        batch as 'B', so the node opens without replaying the chain. Blocks the reference
+        connected have no asset undo records of this engine: the import height is kept, and a
+        reorg that would disconnect one of them with asset activity asks for -reindex-chainstate
+        (as the reference does for a missing undo, src/validation.cpp DisconnectBlock)."""
+        if not self.datadir:
+            return False
+        adir = os.path.join(self.datadir, "assets")
+        if not os.path.exists(os.path.join(adir, "CURRENT")):
+            return False
+        tip = self.chain.find(self.coins.best_block)
+        if tip is None:
+            return False
+        rdir = os.path.join(adir, "restricted")
+        adb = _core.LevelDB(adir, create_if_missing=False)
+        rdb = _core.LevelDB(rdir, create_if_missing=False) if os.path.exists(os.path.join(rdir, "CURRENT")) else None
+        try:
+            st = _core.AssetsState()
+            r = _core.assets_import_reference_ldb(st, adb, rdb)
+        finally:
+            adb.close()
+            if rdb is not None:
+                rdb.close()
+        if r["bad"]:
+            log.log_printf(f"assets/: {r['bad']} unreadable record(s); replaying the asset state instead")
+            return False
+        st.best_block = self.coins.best_block
+        st.mark_all_dirty()
+        self.assets = st
+        self.assets_import_height = int(tip.height)
+        self.coins_db.write([(ASSETS_IMPORT_KEY, _core.chaindb_xor(int(tip.height).to_bytes(4, "little"),
+                                                                   self._coins_obf))])
+        _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True, self.assets)
+        log.log_printf(f"assets/: imported {r['assets']} assets, {r['balances']} balances, {r['tags']} tags, "
+                       f"{r['restrictions']} restrictions, {r['global_restrictions']} global restrictions and "
+                       f"{r['verifiers']} verifiers at height {tip.height}")
+        return True
+
+    @staticmethod
+    def _block_has_asset_ops(blk) -> bool:
+        for tx in blk.vtx:
+            for o in tx.vout:
+                if _core.parse_asset_script(o.script_pubkey) is not None or \
+                        _core.parse_null_asset_script(o.script_pubkey) is not None:
+                    return True
+        return False
 
     def _rewind_indexes(self, ix) -> bool:
         """Bring loaded indexes to the UTXO set's block. A flush writes the index records before the
@@ -1066,7 +1126,12 @@ class ChainState:
                 undo = self.undo.read(cur.hash, cur.prev_hash)
                 if blk is None or undo is None:
                     raise RuntimeError(f"cannot disconnect {_core.u256_hex(cur.hash)}: block or undo data missing")
-                aundo = self.asset_undo.read(cur.hash, cur.prev_hash) or b""
+                aundo = self.asset_undo.read(cur.hash, cur.prev_hash)
+                if aundo is None and cur.height <= self.assets_import_height and self._block_has_asset_ops(blk):
+                    # connected by the reference node (assets/ imported): no undo record of this engine
+                    raise RuntimeError(f"cannot disconnect {_core.u256_hex(cur.hash)}: its asset undo data is in "
+                                       "the reference's format; restart with -reindex-chainstate")
+                aundo = aundo or b""
                 if not _core.disconnect_block(blk, undo, self.coins, self.assets, aundo):
                     log.log_printf(f"disconnect of {_core.u256_hex(cur.hash)} found an inconsistent UTXO set")
                 self.indexes.disconnect(blk, cur.height, cur.hash, undo)

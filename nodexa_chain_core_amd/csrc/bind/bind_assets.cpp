@@ -210,6 +210,8 @@ void bind_assets(py::module_& m) {
             return meta_dict(*meta);
         })
         .def("__len__", [](const assets::State& s) { return s.metas().size(); })
+        .def("mark_all_dirty", &assets::State::mark_all_dirty)
+        .def("dirty_count", &assets::State::dirty_count)
         .def("names", [](const assets::State& s) {
             std::vector<std::string> out;
             for (auto& kv : s.metas()) out.push_back(kv.first);

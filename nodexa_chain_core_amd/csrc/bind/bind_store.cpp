@@ -127,6 +127,22 @@ void bind_store(py::module_& m) {
         py::gil_scoped_release rel;
         return chaindb::assets_load(st, db, k);
     });
+    m.def("assets_import_reference_ldb", [](assets::State& st, ldb::DB& assets_db, ldb::DB* restricted_db) {
+        chaindb::RefAssetsLoad r;
+        {
+            py::gil_scoped_release rel;
+            r = chaindb::assets_import_reference(st, assets_db, restricted_db);
+        }
+        py::dict d;
+        d["assets"] = r.metas;
+        d["balances"] = r.balances;
+        d["tags"] = r.tags;
+        d["restrictions"] = r.restrictions;
+        d["global_restrictions"] = r.globals;
+        d["verifiers"] = r.verifiers;
+        d["bad"] = r.bad;
+        return d;
+    }, py::arg("state"), py::arg("assets_db"), py::arg("restricted_db") = nullptr);
     m.def("coin_db_key", [](const py::bytes& txid, u32 n) {
         const std::string s = txid;
         if (s.size() != 32) throw std::invalid_argument("expected a 32-byte txid");

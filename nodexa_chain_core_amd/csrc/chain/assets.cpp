@@ -1081,6 +1081,15 @@ void State::for_each_dirty(
     }
 }
 
+void State::mark_all_dirty() {
+    for (auto& kv : meta_) dirty_.insert({0, {kv.first, ""}});
+    for (auto& kv : bal_) dirty_.insert({1, kv.first});
+    for (auto& k : tags_) dirty_.insert({2, k});
+    for (auto& k : frozen_) dirty_.insert({3, k});
+    for (auto& k : global_) dirty_.insert({4, {k, ""}});
+    for (auto& kv : verifier_) dirty_.insert({5, {kv.first, ""}});
+}
+
 bool State::load_entry(u8 kind, const std::string& a, const std::string& b, const Bytes& value) {
     try {
         Reader r(value);

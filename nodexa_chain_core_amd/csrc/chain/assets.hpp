@@ -184,6 +184,7 @@ public:
     // stored value without marking it changed.
     void for_each_dirty(const std::function<void(u8, const std::string&, const std::string&, const Bytes*)>& f) const;
     void clear_dirty() { dirty_.clear(); }
+    void mark_all_dirty();                      // every entry changed (an imported state's first flush)
     size_t dirty_count() const { return dirty_.size(); }
     bool load_entry(u8 kind, const std::string& a, const std::string& b, const Bytes& value);
     void reset() { *this = State(); }

@@ -1,10 +1,13 @@
 // Chain databases in the reference's key layout: see chaindb.hpp.
 #include "chaindb.hpp"
 
+#include <algorithm>
+#include <cstring>
 #include <random>
 #include <stdexcept>
 
 #include "../chain/primitives.hpp"
+#include "../chain/script.hpp"
 
 namespace nodexa {
 namespace chaindb {
@@ -132,6 +135,135 @@ bool assets_load(assets::State& st, ldb::DB& db, const std::string& obf) {
     st.best_block = Uint256::from_bytes(reinterpret_cast<const u8*>(v.data()));
     st.clear_dirty();
     return ok;
+}
+
+namespace {
+// CDBWrapper keys of the asset databases: a flag char, then one or two serialized strings.
+bool ref_key(const std::string& k, char flag, int nstr, std::string& a, std::string& b) {
+    if (k.empty() || k[0] != flag) return false;
+    try {
+        Reader r(reinterpret_cast<const u8*>(k.data()) + 1, k.size() - 1);
+        const Bytes x = r.var_bytes();
+        a.assign(x.begin(), x.end());
+        if (nstr == 2) {
+            const Bytes y = r.var_bytes();
+            b.assign(y.begin(), y.end());
+        }
+        return r.empty();
+    } catch (const std::exception&) {
+        return false;
+    }
+}
+
+// An address of the reference's records as this engine's 20-byte balance / tag key.
+bool ref_addr20(const std::string& addr, std::string& out) {
+    Bytes payload;
+    if (!base58check_decode(addr, payload) || payload.size() != 21) return false;
+    out.assign(reinterpret_cast<const char*>(payload.data()) + 1, 20);
+    return true;
+}
+
+// ReadWriteAssetHash (src/assets/assettypes.h:59-95): 0x12 + 32 bytes -> "\x12\x20" + 32 bytes,
+// any other tag (the txid notifier) -> the 32 bytes.
+std::string ref_asset_hash(Reader& r) {
+    const u8 tag = r.u8_();
+    const Bytes h = r.var_bytes();
+    std::string out;
+    if (tag == 0x12) out = std::string("\x12\x20", 2);
+    out.append(reinterpret_cast<const char*>(h.data()), std::min<size_t>(h.size(), 32));
+    return out;
+}
+}  // namespace
+
+RefAssetsLoad assets_import_reference(assets::State& st, ldb::DB& adb, ldb::DB* rdb) {
+    RefAssetsLoad out;
+    st.reset();
+    auto value = [](ldb::DB& db, std::string v, const std::string& obf) {
+        xor_obf(v, obf);
+        return v;
+    };
+    const std::string aobf = obfuscation_key(adb, false);
+    // 'A': CDatabasedAssetData = CNewAsset (name, amount, units, reissuable, has_ipfs [, hash]),
+    // nHeight, blockHash
+    adb.scan("A", "B", [&](const std::string& k, const std::string& v0) {
+        std::string name, unused;
+        if (!ref_key(k, 'A', 1, name, unused)) {
+            ++out.bad;
+            return true;
+        }
+        try {
+            const std::string v = value(adb, v0, aobf);
+            Reader r(reinterpret_cast<const u8*>(v.data()), v.size());
+            assets::Meta m;
+            const Bytes n = r.var_bytes();
+            m.name.assign(n.begin(), n.end());
+            m.amount = r.i64_();
+            m.units = int8_t(r.u8_());
+            m.reissuable = int8_t(r.u8_());
+            m.has_ipfs = int8_t(r.u8_());
+            if (m.has_ipfs == 1) m.ipfs = ref_asset_hash(r);
+            m.height = r.i32_();
+            m.block = r.u256();
+            if (m.name != name) throw std::runtime_error("name mismatch");
+            st.set_meta(m);
+            ++out.metas;
+        } catch (const std::exception&) {
+            ++out.bad;
+        }
+        return true;
+    });
+    // 'B': (asset name, address) -> CAmount
+    adb.scan("B", "C", [&](const std::string& k, const std::string& v0) {
+        std::string name, addr, key;
+        const std::string v = value(adb, v0, aobf);
+        if (!ref_key(k, 'B', 2, name, addr) || v.size() != 8 || !ref_addr20(addr, key)) {
+            ++out.bad;
+            return true;
+        }
+        int64_t q;
+        std::memcpy(&q, v.data(), 8);  // little-endian CAmount
+        if (q != 0) st.add_balance(name, reinterpret_cast<const u8*>(key.data()), q);
+        ++out.balances;
+        return true;
+    });
+    if (rdb) {
+        const std::string robf = obfuscation_key(*rdb, false);
+        rdb->scan("G", "H", [&](const std::string& k, const std::string&) {
+            std::string name, unused;
+            if (!ref_key(k, 'G', 1, name, unused)) ++out.bad;
+            else st.set_global(name, true), ++out.globals;
+            return true;
+        });
+        rdb->scan("R", "S", [&](const std::string& k, const std::string&) {
+            std::string addr, name, key;
+            if (!ref_key(k, 'R', 2, addr, name) || !ref_addr20(addr, key)) ++out.bad;
+            else st.set_frozen(name, reinterpret_cast<const u8*>(key.data()), true), ++out.restrictions;
+            return true;
+        });
+        rdb->scan("T", "U", [&](const std::string& k, const std::string&) {
+            std::string addr, tag, key;
+            if (!ref_key(k, 'T', 2, addr, tag) || !ref_addr20(addr, key)) ++out.bad;
+            else st.set_tag(tag, reinterpret_cast<const u8*>(key.data()), true), ++out.tags;
+            return true;
+        });
+        rdb->scan("V", "W", [&](const std::string& k, const std::string& v0) {
+            std::string name, unused;
+            try {
+                const std::string v = value(*rdb, v0, robf);
+                Reader r(reinterpret_cast<const u8*>(v.data()), v.size());
+                const Bytes ver = r.var_bytes();
+                if (!ref_key(k, 'V', 1, name, unused)) throw std::runtime_error("key");
+                st.set_verifier(name, std::string(ver.begin(), ver.end()));
+                ++out.verifiers;
+            } catch (const std::exception&) {
+                ++out.bad;
+            }
+            return true;
+        });
+    }
+    st.clear_journal();  // an imported state has no undo history in this engine
+    st.clear_dirty();
+    return out;
 }
 
 size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sync, assets::State* assets) {

@@ -46,6 +46,17 @@ size_t coins_flush(CoinsView& view, ldb::DB& db, const std::string& obf, bool sy
 bool assets_load(assets::State& st, ldb::DB& db, const std::string& obf);
 std::string coin_key(const OutPoint& o);
 
+// A reference datadir's asset state: CAssetsDB (assets/: 'A' name -> CDatabasedAssetData, 'B'
+// (name, address) -> CAmount; src/assets/assetdb.cpp:17-41) and CRestrictedDB (assets/restricted:
+// 'V' verifier strings, 'T' (address, qualifier) tags, 'R' (address, name) frozen addresses, 'G'
+// global freezes; src/assets/restricteddb.cpp:10-100) read into `st` (replacing its contents;
+// addresses become their 20-byte hashes, as this engine keys them). The reverse indexes ('C',
+// 'Q'), the mempool reissue state ('Z') and the undo records ('U') are not needed for the state.
+struct RefAssetsLoad {
+    size_t metas = 0, balances = 0, tags = 0, restrictions = 0, globals = 0, verifiers = 0, bad = 0;
+};
+RefAssetsLoad assets_import_reference(assets::State& st, ldb::DB& assets_db, ldb::DB* restricted_db);
+
 // CDiskBlockIndex
 struct DiskIndex {
     Uint256 hash;

@@ -56,6 +56,12 @@ constexpr uint32_t CB = EQC_COARSE_BITS, SB = EQC_SLICE_BITS, KB = 20 - CB - SB;
 constexpr uint32_t NCO = EQC_COARSE, NSL = 1u << SB, NKEY = 1u << KB;
 static_assert(KB >= 6 && KB <= 12, "chain key width");
 
+// The slice of a row (payload bits [0, SB)); every row is in slice 0 without slices.
+NX_DEV uint32_t eqc_slice(uint32_t w1) {
+    if constexpr (SB == 0) return 0;
+    else return w1 >> (32 - SB);
+}
+
 // Payload words of a level-L row (bits [20L + CB, 200)).
 constexpr int eqc_payload(int level) { return (200 - 20 * level - (int)CB + 31) / 32; }
 constexpr int eqc_words(int level) { return 1 + eqc_payload(level); }
@@ -110,6 +116,7 @@ NX_DEV void eqc_flush_counts(const EquihashCbDev& p, uint32_t inst, uint32_t grp
 // workgroup's segment of their coarse bucket (word 0 = the leaf index = the level-0 id).
 extern "C" __global__ __launch_bounds__(EQC_BLOCK) void eqc_gen(EquihashCbDev p) {
     __shared__ uint32_t cnt[NCO];
+    if (p.coarse != NCO) return;  // a code object of another geometry than the host sized: no rows
     const uint32_t inst = blockIdx.y, grp = blockIdx.x;
     eqc_clear(cnt);
     __syncthreads();
@@ -200,7 +207,7 @@ NX_DEV uint32_t eqc_stage_slice(const EquihashCbDev& p, uint32_t inst, uint32_t 
         }
 #pragma unroll
         for (int k = 0; k < BATCH; ++k) {
-            const bool keep = valid[k] && (r[k].w[1] >> (32 - SB)) == s;
+            const bool keep = valid[k] && eqc_slice(r[k].w[1]) == s;
             if (__ballot(keep) == 0) continue;  // wave-uniform
             if (!keep) continue;
             const uint32_t idx = eqc_wave_alloc(nstaged);
@@ -232,9 +239,10 @@ NX_DEV void eqc_round_impl(const EquihashCbDev& p) {
     __shared__ uint32_t ids[2][EQC_STAGE];
     __shared__ int head[NKEY];
     __shared__ short nxt[EQC_STAGE];
-    __shared__ uint32_t segc[NP / 64][NCO];  // one prefix copy per producer wave (P <= NCO)
+    __shared__ uint32_t segc[NP / 64][EQC_MAX_P];  // one prefix copy per producer wave
     __shared__ uint32_t nstaged[2];
     __shared__ uint32_t pcount;
+    if (p.coarse != NCO) return;  // geometry mismatch (whole workgroup): nothing staged or emitted
     const uint32_t inst = blockIdx.y, grp = blockIdx.x;
     const uint32_t P = p.groups, G = gridDim.x;
     const bool producer = threadIdx.x < NP;

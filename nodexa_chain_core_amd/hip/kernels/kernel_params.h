@@ -126,10 +126,15 @@ struct EquihashPsDev {
 // bucket 2^EQC_SLICE_BITS times (L2 hits after the first). Back-pointers go through a pair log:
 // row word 0 = the row's id (writer x pmax + the writer's emission count), pairs[level][id] = the
 // ids of the two parent rows (level 0 ids are leaf indices).
-#define EQC_COARSE_BITS 8
+#ifndef EQC_COARSE_BITS
+#define EQC_COARSE_BITS 8   // the shipping geometry; a code object built with other bits is run with
+#endif                      // the matching `coarse` (EquihashCbDev.coarse, ops/equihash.py coarse_bits)
+#ifndef EQC_SLICE_BITS
 #define EQC_SLICE_BITS 2
+#endif
 #define EQC_COARSE (1 << EQC_COARSE_BITS)
-#define EQC_STAGE 2400      // rows of one fine bucket staged in LDS (mean 2048, sigma 45)
+#define EQC_MAX_P 64        // writers per instance (the counts scan keeps one prefix per producer wave)
+#define EQC_STAGE 2560      // rows of one fine bucket staged in LDS (mean 2048-2100; 2472 seen, r5b)
 #define EQC_ROW_WORDS 7     // widest stored row (levels 0-1: id + 6 payload words)
 #define EQC_STAT_PAIRS 12   // stats slot: pair ids beyond a writer's pmax (a loss, like slots 0-10)
 struct EquihashCbDev {
@@ -139,8 +144,8 @@ struct EquihashCbDev {
     uint32_t num_inst;
     uint32_t groups;        // P: writers (workgroups) per instance in gen and rounds 1-8, <= EQC_COARSE
     uint32_t seg;           // rows per (coarse bucket, writer) segment (mean 2^21 / 256 / P; host-sized)
-    uint32_t pmax;          // pair ids per writer and level: EQC_COARSE * seg
-    uint32_t pad;
+    uint32_t pmax;          // pair ids per writer and level: coarse * seg
+    uint32_t coarse;        // coarse buckets per level: must equal the code object's EQC_COARSE
     uint32_t* hashes;       // [2][inst][EQC_COARSE][P][seg] row slots of EQC_ROW_WORDS words (rows at their level's width)
     uint32_t* pairs;        // [inst][LEVELS][P * pmax][2]: parent ids of every row id (levels 1..8)
     uint16_t* counts;       // [inst][LEVELS][P][EQC_COARSE] rows per segment (clamped to seg)

@@ -660,19 +660,22 @@ PYBIND11_MODULE(_hip, m) {
     m.attr("EQC_STAGE") = EQC_STAGE;
     m.attr("EQC_ROW_WORDS") = EQC_ROW_WORDS;
     m.attr("EQC_STAT_PAIRS") = EQC_STAT_PAIRS;
+    m.attr("EQC_MAX_P") = EQC_MAX_P;
     m.def("launch_equihash_cb_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
                                          uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uint32_t groups,
                                          uint32_t seg, uintptr_t hashes, uintptr_t pairs, uintptr_t counts, uintptr_t cands,
                                          uintptr_t sols, uintptr_t stats, uintptr_t stream, uint32_t block,
-                                         uint32_t final_groups) {
+                                         uint32_t final_groups, uint32_t coarse) {
         if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash_cb kernels");
-        if (final_groups == 0 || final_groups > EQC_COARSE) throw std::invalid_argument("final_groups: 1..EQC_COARSE");
+        if (coarse < 64 || coarse > 4096 || (coarse & (coarse - 1))) throw std::invalid_argument("coarse: 64..4096, 2^k");
+        if (final_groups == 0 || final_groups > coarse) throw std::invalid_argument("final_groups: 1..coarse");
         if (block != 1024) throw std::invalid_argument("block: 1024 (the build's EQC_BLOCK)");
         if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
         if (input_len > 124 || num_inst == 0 || num_inst > 65535) throw std::invalid_argument("bad equihash geometry");
         // P a power of two in [16, EQC_COARSE]: every writer owns whole coarse buckets in the rounds,
         // 2^20 / P digests in gen, and a segment of `seg` rows in every bucket (u16 counts)
-        if (groups < 16 || groups > EQC_COARSE || (groups & (groups - 1))) throw std::invalid_argument("groups: 16..EQC_COARSE, 2^k");
+        if (groups < 16 || groups > EQC_MAX_P || groups > coarse || (groups & (groups - 1)))
+            throw std::invalid_argument("groups: 16..EQC_MAX_P, 2^k");
         if (seg == 0 || seg > 65535) throw std::invalid_argument("seg: 1..65535");
         EquihashCbDev p{};
         p.msgs = reinterpret_cast<const uint64_t*>(msgs);
@@ -681,7 +684,8 @@ PYBIND11_MODULE(_hip, m) {
         p.num_inst = num_inst;
         p.groups = groups;
         p.seg = seg;
-        p.pmax = EQC_COARSE * seg;
+        p.pmax = coarse * seg;
+        p.coarse = coarse;
         p.hashes = reinterpret_cast<uint32_t*>(hashes);
         p.pairs = reinterpret_cast<uint32_t*>(pairs);
         p.counts = reinterpret_cast<uint16_t*>(counts);
@@ -700,7 +704,8 @@ PYBIND11_MODULE(_hip, m) {
         ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
     }, py::arg("ks"), py::arg("h0"), py::arg("msgs"), py::arg("input_len"), py::arg("num_inst"), py::arg("groups"),
        py::arg("seg"), py::arg("hashes"), py::arg("pairs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
-       py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQC_COARSE);
+       py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQC_COARSE,
+       py::arg("coarse") = EQC_COARSE);
     // The 11 kernel launches captured once into a hipGraph (fixed device buffers, so the graph
     // stays valid across batches; only the message words change, in place). Per batch: 3
     // memsets + one hipGraphLaunch instead of 14 stream operations.

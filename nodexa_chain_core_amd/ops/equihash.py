@@ -94,7 +94,7 @@ def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | 
 class EquihashSolver:
     def __init__(self, num_inst: int = 8, device: int | None = None, code_object: str | None = None,
                  engine: str | None = None, groups: int | None = None, block: int = 1024,
-                 final_groups: int | None = None):
+                 final_groups: int | None = None, coarse_bits: int | None = None):
         """`code_object`: path of an alternative build of the engine's .hip (tuning sweeps).
         `engine`: "cb" or "ps" (module docstring); `groups` writers (workgroups) per instance per
         round, by default so that groups x instances = 256 (one 1024-thread workgroup per CU)."""
@@ -104,15 +104,18 @@ class EquihashSolver:
         # writers per instance: one 1024-thread workgroup per CU over the whole launch (P x
         # instances = 256: 32 at 8 instances, 16 at the mining window's 16; profiles/README r4k:
         # 8.50 vs 8.65 ms at 16 instances, and 7.48 vs 4.38 ms when P=16 leaves half the CUs idle at 8)
-        self.groups = int(groups) if groups else min(256, max(16, 1 << max(0, (256 // max(1, int(num_inst))).bit_length() - 1)))
-        self.block = int(block)  # threads per workgroup, must match the code object's EQP_BLOCK / EQC_BLOCK
         runtime.require_gpu()
         self.h = runtime.hip()
         cb = self.engine == "cb"
+        cap = self.h.EQC_MAX_P if cb else 256
+        self.groups = int(groups) if groups else min(cap, max(16, 1 << max(0, (256 // max(1, int(num_inst))).bit_length() - 1)))
+        self.block = int(block)  # threads per workgroup, must match the code object's EQP_BLOCK / EQC_BLOCK
+        # cb: coarse buckets per level (the code object's EQC_COARSE_BITS; other bits for sweeps)
+        self.coarse = 1 << int(coarse_bits) if coarse_bits else self.h.EQC_COARSE
         # final round (writes no level, so any width works): ps ~4096 workgroups over the launch
         # (256 at 16 instances: -1 % against 1024, r4k); cb one workgroup per coarse bucket at most
         fg = int(final_groups or os.environ.get("NODEXA_EQP_FINAL_GROUPS", 0) or 0)
-        self.final_groups = fg or (self.h.EQC_COARSE if cb else min(1024, max(64, 4096 // max(1, int(num_inst)))))
+        self.final_groups = fg or (self.coarse if cb else min(1024, max(64, 4096 // max(1, int(num_inst)))))
         self.num_inst = int(num_inst)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
         self.params = _core.EquihashParams(200, 9)
@@ -126,7 +129,7 @@ class EquihashSolver:
                 co = runtime.load_code_object(code_object)
                 self.kernels = [co.function(k) for k in names]
             if cb:
-                D, Wd = self.h.EQC_COARSE, self.h.EQC_ROW_WORDS
+                D, Wd = self.coarse, self.h.EQC_ROW_WORDS
                 # rows per (coarse bucket, writer) segment: mean m = 2^21 / D / P (level sizes run
                 # up to ~4 % above 2^21) + 8 sigma, so an overflow (a host re-solve) stays ~1e-12
                 m = (1 << 21) / D / self.groups
@@ -192,7 +195,7 @@ class EquihashSolver:
                                                 self.num_inst, self.groups, self.seg, self.hashes.data_ptr(),
                                                 self.pairs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
                                                 self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block,
-                                                self.final_groups)
+                                                self.final_groups, self.coarse)
             else:
                 self.h.launch_equihash_ps_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
                                                 self.num_inst, self.groups, self.hashes.data_ptr(),
@@ -284,7 +287,7 @@ class EquihashSolver:
     def stats(self) -> dict:
         """Per-level fill of the last solve (instance 0) — overflow diagnostics."""
         L = self.h.EQ_LEVELS
-        D = self.h.EQC_COARSE if self.engine == "cb" else self.h.EQ_BUCKETS
+        D = self.coarse if self.engine == "cb" else self.h.EQ_BUCKETS
         c = self.counts[: L * self.groups * D].view(L, self.groups, D).to(torch.int32).sum(1).cpu()
         dropped = self.stats_buf[: self.h.EQP_STATS].cpu().tolist()
         return {"rows_per_level": [int(x) for x in c.sum(1)], "max_fill": [int(x) for x in c.max(1).values],

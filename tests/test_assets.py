@@ -2,6 +2,8 @@
 test vectors (src/test/assets/asset_tests.cpp, verifier_string_tests.cpp — the name / expression
 strings and expected answers are used as data), then a regtest node issuing, transferring,
 reissuing, tagging and freezing through the RPCs, with reorg and restart."""
+import os
+
 import pytest
 
 from test_node_rpc import client, node_factory  # noqa: F401 — shared fixtures
@@ -175,6 +177,74 @@ def test_asset_lifecycle_regtest(core, node_factory):  # noqa: F811
     c = client(node)
     assert {n: c.getassetdata(n) for n in c.listassets()} == snapshot
     assert c.checkglobalrestriction("$ROSE")
+    # a reference datadir: the same state as CAssetsDB / CRestrictedDB records (assets/,
+    # assets/restricted) and none of this engine's asset records in chainstate/ -> imported at
+    # start-up (chain/state._import_reference_assets), no replay
+    before = _asset_state_view(node.state)
+    height = node.state.coins_tip().height
+    dd = node.state.datadir
+    node.stop()
+    _write_reference_asset_dbs(core, dd, before)
+    db = core.LevelDB(os.path.join(dd, "chainstate"))
+    db.write([(k, None) for k, _ in db.items(b"\x01", b"\x02")] + [(b"\x02assets.best", None)])
+    db.close()
+    node, _ = node_factory()
+    assert not node.state.rebuilt and node.state.assets_import_height == height
+    assert _asset_state_view(node.state) == before
+    c = client(node)
+    assert {n: c.getassetdata(n) for n in c.listassets()} == snapshot
+    node.stop()
+    node, _ = node_factory()  # the imported state was written in this engine's records
+    assert not node.state.rebuilt and _asset_state_view(node.state) == before
+
+
+def _asset_state_view(state):
+    st = state.assets
+    return {"metas": {n: st.get(n) for n in st.names()}, "balances": sorted(st.balances()),
+            "tags": sorted(st.tags()), "restrictions": sorted(st.restrictions()),
+            "global": sorted(st.global_restrictions()),
+            "verifiers": {n: st.verifier(n) for n in st.names() if st.verifier(n) is not None}}
+
+
+def _write_reference_asset_dbs(core, datadir, view):
+    """The reference's record layout, serialized here from its sources (not through the importer):
+    src/assets/assetdb.cpp:17-41 (CAssetsDB keys), assettypes.h:59-185 (CDatabasedAssetData /
+    CNewAsset / ReadWriteAssetHash), restricteddb.cpp:10-100 (CRestrictedDB keys, int8 1 values)."""
+    import struct
+
+    def cs(n):
+        return bytes([n]) if n < 253 else b"\xfd" + struct.pack("<H", n)
+
+    def s(b):
+        b = b.encode() if isinstance(b, str) else b
+        return cs(len(b)) + b
+
+    def addr(h):
+        return core.base58check_encode(bytes([42]) + h)
+
+    a, r = [], []
+    for name, m in view["metas"].items():
+        v = s(name) + struct.pack("<qbbb", m["amount"], m["units"], m["reissuable"], m["has_ipfs"])
+        if m["has_ipfs"] == 1:
+            ipfs = m["ipfs"]
+            v += (b"\x12" + s(ipfs[2:])) if len(ipfs) == 34 else (b"\x54" + s(ipfs))
+        a.append((b"A" + s(name), v + struct.pack("<i", m["height"]) + m["block"]))
+    for name, h, q in view["balances"]:
+        a.append((b"B" + s(name) + s(addr(h)), struct.pack("<q", q)))
+        a.append((b"C" + s(addr(h)) + s(name), struct.pack("<q", q)))  # the reverse index (not needed)
+    for name, ver in view["verifiers"].items():
+        r.append((b"V" + s(name), s(ver)))
+    for tag, h in view["tags"]:
+        r.append((b"T" + s(addr(h)) + s(tag), b"\x01"))
+        r.append((b"Q" + s(tag) + s(addr(h)), b"\x01"))
+    for name, h in view["restrictions"]:
+        r.append((b"R" + s(addr(h)) + s(name), b"\x01"))
+    for name in view["global"]:
+        r.append((b"G" + s(name), b"\x01"))
+    for sub, recs in (("assets", a), (os.path.join("assets", "restricted"), r)):
+        db = core.LevelDB(os.path.join(datadir, sub))
+        db.write(recs)
+        db.close()
 
 
 def test_asset_consensus_rejections(core, node_factory):  # noqa: F811

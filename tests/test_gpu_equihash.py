@@ -31,7 +31,7 @@ def test_gpu_solutions_valid_and_match_cpu(core, solver):
     inputs = [bytes(80) + i.to_bytes(32, "little") for i in range(4)]
     gpu = solver.solve(inputs)  # every solution already CPU-verified inside collect()
     st = solver.stats()
-    assert max(st["max_fill"]) <= st["cap"], st
+    assert st["stage_dropped"] == 0 and st["largest_bucket"] <= st["cap"], st  # no staged bucket over its cap
     assert sum(st["dropped_per_level"]) < 64, st  # segment / staging overflow stays rare
     assert min(st["rows_per_level"]) > 1_900_000, st
     total_gpu = sum(len(s) for s in gpu)
@@ -64,7 +64,7 @@ def test_solver_exactly_matches_cpu_on_16_inputs(core, gpu, engine):
         assert sorted(map(tuple, g)) == sorted(map(tuple, cpu)), inp[-32:].hex()
         total += len(g)
     assert total > 8
-    assert s.fallbacks == 0, s.fallback_log
+    assert s.fallbacks == 0, str(s.fallback_log)
     del s
     torch.cuda.empty_cache()
 

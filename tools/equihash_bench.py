@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Equihash(200,9) GPU solver timing: device-only time per batch (hip events),
-solutions per solve and host verification cost, for several counter-bank
-settings and compile-time variants of equihash.hip, interleaved in one process.
+solutions per solve and host verification cost, for both engines and compile-time variants of
+their .hip sources, interleaved in one process.
 
-    python tools/equihash_bench.py --banks 8 --variants "" EQ_NO_HALF EQ_DIRECT
-    python tools/equihash_bench.py --compile-only --variants EQ_NO_HALF   # on the build host
+    python tools/equihash_bench.py --inst 16 --engines cb ps --variants "" EQC_BATCH=4
+    python tools/equihash_bench.py --compile-only --engines cb --variants EQC_BATCH=4   # on the build host
 
-Variants are built to .kernel_cache/equihash_<tag>.hsaco (hipcc --genco).
+Engines: "cb[:groups[:block[:final_groups]]]" (equihash_cb.hip) and "ps[:...]" (equihash_ps.hip).
+Variants are built to .kernel_cache/<source>_<tag>.hsaco (hipcc --genco).
 """
 from __future__ import annotations
 
@@ -38,42 +39,38 @@ def variant_object(defines: tuple[str, ...], source: str = "equihash.hip") -> st
     return out
 
 
+SOURCES = {"cb": "equihash_cb.hip", "ps": "equihash_ps.hip"}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--inst", type=int, default=8)
     ap.add_argument("--batches", type=int, default=5)
-    ap.add_argument("--banks", type=int, nargs="*", default=[8])
     ap.add_argument("--variants", nargs="*", default=[""])
     ap.add_argument("--compile-only", action="store_true")
-    ap.add_argument("--engines", nargs="*", default=["global"], help="global and/or ps[:groups]")
+    ap.add_argument("--engines", nargs="*", default=["cb"], help="cb|ps[:groups[:block[:final_groups]]]")
     a = ap.parse_args()
     variants = [tuple(x for x in v.split(",") if x) for v in a.variants]
-    objs = {v: variant_object(v) for v in variants} if "global" in a.engines else {}
-    ps_objs = {v: variant_object(v, "equihash_ps.hip") for v in variants} if any(
-        e.startswith("ps") for e in a.engines) else {}
+    kinds = sorted({e.split(":")[0] for e in a.engines})
+    objs = {(k, v): variant_object(v, SOURCES[k]) for k in kinds for v in variants}
     if a.compile_only:
-        print(json.dumps({",".join(v) or "base": o for v, o in list(objs.items()) + list(ps_objs.items())}))
+        print(json.dumps({f"{k}:{','.join(v) or 'base'}": o for (k, v), o in objs.items()}))
         return 0
     import torch
 
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
-    cfgs = []
-    for e in a.engines:
-        if e == "global":
-            cfgs += [(b, v) for v in variants for b in a.banks]
-        else:  # "ps" or "ps:<groups>": the private-slot engine (variants of equihash_ps.hip)
-            cfgs += [(e, v) for v in variants]
+    cfgs = [(e, v) for e in a.engines for v in variants]
 
     def make(c):
-        if isinstance(c[0], str):
-            f = c[0].split(":")  # ps[:groups[:block[:final_groups]]]
-            g = int(f[1]) if len(f) > 1 else None  # None: the solver's own choice (P x instances = 256)
-            blk = int(f[2]) if len(f) > 2 else 1024
-            fin = int(f[3]) if len(f) > 3 else None
-            return EquihashSolver(num_inst=a.inst, device=0, engine="ps", groups=g, block=blk,
-                                  code_object=ps_objs[c[1]], final_groups=fin)
-        return EquihashSolver(num_inst=a.inst, device=0, engine="global", banks=c[0], code_object=objs[c[1]])
+        f = c[0].split(":")
+        g = int(f[1]) if len(f) > 1 and f[1] else None  # None: the solver's own choice (P x instances = 256)
+        blk = int(f[2]) if len(f) > 2 else 1024
+        fin = int(f[3]) if len(f) > 3 else None
+        # a variant of another cb geometry (EQC_COARSE_BITS=<b>) runs with buffers sized for it
+        cbits = next((int(d.split("=")[1]) for d in c[1] if d.startswith("EQC_COARSE_BITS=")), None)
+        return EquihashSolver(num_inst=a.inst, device=0, engine=f[0], groups=g, block=blk,
+                              code_object=objs[(f[0], c[1])], final_groups=fin, coarse_bits=cbits)
 
     solvers = {c: make(c) for c in cfgs}
     batches = [[os.urandom(112) for _ in range(a.inst)] for _ in range(a.batches + 1)]
@@ -92,14 +89,14 @@ def main() -> int:
             t = time.perf_counter()
             res[c]["sols"] += sum(len(x) for x in s.collect(bt))
             res[c]["verify_s"] += time.perf_counter() - t
-    for (b, v), r in res.items():
+    for (e, v), r in res.items():
         per_batch = sum(r["dev_ms"]) / len(r["dev_ms"])
-        out = {"variant": ",".join(v) or "base", "banks": b, "inst_per_batch": a.inst,
+        out = {"engine": e, "variant": ",".join(v) or "base", "inst_per_batch": a.inst,
                "device_ms_per_batch": round(per_batch, 3), "device_ms_per_solve": round(per_batch / a.inst, 3),
                "sols_per_solve": round(r["sols"] / (a.batches * a.inst), 3),
                "device_sol_per_s": round(r["sols"] / (sum(r["dev_ms"]) / 1e3), 1),
                "host_collect_verify_s_per_batch": round(r["verify_s"] / a.batches, 4),
-               "stats": solvers[(b, v)].stats()}
+               "fallbacks": solvers[(e, v)].fallbacks, "stats": solvers[(e, v)].stats()}
         print(json.dumps(out), flush=True)
     return 0
 
