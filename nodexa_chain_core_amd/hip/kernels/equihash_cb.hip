@@ -1,42 +1,38 @@
 // Equihash(200,9) Wagner solver for gfx950 with coarse destination buckets (new; the reference has
 // no Equihash — SURVEY §0.4 / Appendix D). CPU golden model: csrc/pow/equihash.cpp.
 //
-// What bounds a Wagner round on MI355X is its scattered row stores: every round appends 2^21
-// rows per instance to random buckets, and at 4096 buckets per level each row leaves the L2 as
-// its own partial-line write (1.06-1.18 EA write requests per row, profiles/README r4r/r4l).
-// The private-slot solver (equihash_ps.hip) sits on that floor. This solver keeps fewer lines
-// open instead: a level's rows are stored by the top EQC_COARSE_BITS (8) bits of the digit they
-// collide on next, so a writer appends to 256 segments instead of 4096 and the L2 merges its
-// appends into lines before they go out. The store probe (tools/eq_runs_probe.hip, profiles r5a)
-// in the solver's shape: 0.43-0.54 requests and 0.32-0.44 ms per 33.5M rows at 256 buckets against
-// 1.06-1.18 and 0.71-0.87 ms at 4096.
+// What bounds a Wagner round on MI355X is its scattered row stores: every round appends 2^21 rows
+// per instance to random buckets, and with 4096 destination buckets each row leaves the L2 as its
+// own partial-line write (1.06-1.18 EA write requests per row, profiles/README r4r/r4l); the
+// private-slot solver (equihash_ps.hip) sits on that floor. This solver keeps its collision
+// structure -- 4096 fine buckets of ~512 rows staged in LDS, 8-bit chain sub-digits, 32-bit
+// back-pointers (bucket << 20 | index a << 10 | index b) and the refs table -- but STORES a level's
+// rows by the top EQC_COARSE_BITS (8) bits of their next digit only: a writer appends to 256
+// segments instead of 4096, and the L2 merges its appends into lines before they go out
+// (tools/eq_runs_probe.hip, profiles r5a: 0.43-0.54 requests and 0.32-0.44 ms per 33.5M rows at 256
+// buckets against 1.06-1.18 and 0.71-0.87 ms at 4096). The remaining 4 bucket bits (the slice)
+// travel in the row.
 //
-// The collisions still need the full 20-bit digit. A round's work item is a fine bucket = (coarse
-// bucket, slice): the next EQC_SLICE_BITS (2) digit bits, carried in the row. The workgroup that
-// owns a coarse bucket processes its 4 slices back to back and reads the coarse bucket once per
-// slice, keeping the slice's rows (~2048; the probe: re-reads of a bucket right after the first
-// pass hit the L2). Within a fine bucket rows chain on the remaining 10 digit bits (LDS linked
-// lists, as the private-slot solver's 8-bit sub-digits).
+// So a coarse bucket holds 16 fine buckets. The workgroup that owns it stages them one after
+// another in two phases (profiles r5c: one pass over the coarse bucket per fine bucket costs more
+// than the stores save): phase 1, once per coarse bucket, reads only word 1 of every row (the slice
+// bits) with all of a lane's positions in flight at once and keeps (segment, slice) per position in
+// registers; phase 2, per fine bucket, gives each wave one contiguous range of staging indices for
+// the rows of its positions in that slice (one LDS atomic), parks their (segment, slot) there, and
+// loads those rows spread evenly over the wave's lanes.
 //
-// Back-pointers: a fine bucket of ~2048 staged rows needs 12-bit indices, and (bucket, index a,
-// index b) no longer fits 32 bits. So every emitted row gets an id (its writer x pmax + the
-// writer's emission count, one wave-aggregated LDS atomic), stored as the row's word 0, and the
-// ids of its two parent rows go to a pair log: pairs[level][id] = (parent a, parent b), written
-// coalesced (consecutive ids per wave). Level-0 ids are leaf indices, so reconstruction walks
-// pairs[8] .. pairs[1] from a candidate's two level-8 ids straight to its 512 leaves.
-//
-// Row format (level L): word 0 = id, then the row's bits [20L + 8, 200) big-endian and contiguous
-// (the payload: slice bits [0, 2), chain key [2, 12), next digit's coarse bits [12, 20), ...).
-// Bits [20L, 20L + 8) are the coarse bucket and live in the row's address. Payload words 6, 6, 5,
-// 5, 4, 3, 3, 2, 1 for levels 0..8; rows are stored unpadded (id + payload).
+// Row format (level L): word 0 = back-pointer (level 0: the leaf index), then the row's bits
+// [20L + 8, 200) big-endian and contiguous (payload: slice [0, 4), chain sub-digit [4, 12), the
+// next digit's coarse bits [12, 20), ...). Bits [20L, 20L + 8) are the coarse bucket and live in
+// the row's address. Payload words 6, 6, 5, 5, 4, 3, 3, 2, 1 for levels 0..8.
 //
 // Layouts (num_inst = ni, P writers per instance, seg rows per segment: mean 2^13 / P + 8 sigma):
-//   hashes [2][ni][COARSE][P][seg][words(level)]  (levels alternate between two buffers)
+//   hashes [2][ni][COARSE][P][seg][words(level)]   (levels alternate between two buffers)
 //   counts [ni][LEVELS][P][COARSE] u16
-//   pairs  [ni][LEVELS][P * pmax][2]
-// Every device-side cap (segment slots, staged rows, chain length, candidates, pair ids) is
-// counted in p.stats; the host re-solves an instance with any count on the golden solver, so the
-// solution set is exact either way (ops/equihash.py).
+//   refs   [ni][LEVELS][4096][EQP_REF_STRIDE]       (as equihash_ps.hip: staged order, fine buckets)
+// Every device-side cap (segment slots, positions per lane, staged rows, chain length, candidates)
+// is counted in p.stats; the host re-solves an instance with any count on the golden solver, so
+// the solution set is exact either way (ops/equihash.py).
 #include "equihash_device.hpp"
 
 #ifndef EQC_BLOCK
@@ -48,19 +44,16 @@
 #ifndef EQC_NP
 #define EQC_NP 448  // producer threads of a round workgroup (7 of its 16 waves)
 #endif
-#ifndef EQC_BATCH
-#define EQC_BATCH 6  // rows in flight per producer lane while a coarse bucket streams in
+#ifndef EQC_KMAX
+#define EQC_KMAX 24  // coarse-bucket positions per producer lane: 24 x 448 = 10752 rows (mean 8.2-8.6k)
+#endif
+#ifndef EQC_B2
+#define EQC_B2 4  // kept rows in flight per lane in phase 2 (a slice is ~512 rows: ~0.7 per lane)
 #endif
 
-constexpr uint32_t CB = EQC_COARSE_BITS, SB = EQC_SLICE_BITS, KB = 20 - CB - SB;
-constexpr uint32_t NCO = EQC_COARSE, NSL = 1u << SB, NKEY = 1u << KB;
-static_assert(KB >= 6 && KB <= 12, "chain key width");
-
-// The slice of a row (payload bits [0, SB)); every row is in slice 0 without slices.
-NX_DEV uint32_t eqc_slice(uint32_t w1) {
-    if constexpr (SB == 0) return 0;
-    else return w1 >> (32 - SB);
-}
+constexpr uint32_t CB = EQC_COARSE_BITS, SB = EQ_BUCKET_BITS - CB, KB = 8;
+constexpr uint32_t NCO = EQC_COARSE, NSL = 1u << SB;
+static_assert(CB >= 8 && CB <= 11, "a level-8 payload must fit one word and a slice take 1..4 bits");
 
 // Payload words of a level-L row (bits [20L + CB, 200)).
 constexpr int eqc_payload(int level) { return (200 - 20 * level - (int)CB + 31) / 32; }
@@ -84,17 +77,6 @@ NX_DEV uint32_t* eqc_row(const EquihashCbDev& p, uint32_t inst, uint32_t d, uint
 
 NX_DEV uint32_t eqc_lane() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
-// Wave-aggregated allocation on an LDS counter: one atomic per wave for its active lanes, which
-// get consecutive values in lane order.
-NX_DEV uint32_t eqc_wave_alloc(uint32_t* ctr) {
-    const uint64_t m = __ballot(1);
-    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
-    uint32_t base = 0;
-    if (eqc_lane() == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)leader, 64);
-    return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
 NX_DEV void eqc_clear(uint32_t* cnt) {
     for (uint32_t k = threadIdx.x; k < NCO; k += EQC_BLOCK) cnt[k] = 0;
 }
@@ -113,7 +95,7 @@ NX_DEV void eqc_flush_counts(const EquihashCbDev& p, uint32_t inst, uint32_t grp
 }
 
 // Round 0: BLAKE2b of this workgroup's 2^20 / P digest indices, 2 leaves each, appended to this
-// workgroup's segment of their coarse bucket (word 0 = the leaf index = the level-0 id).
+// workgroup's segment of their coarse bucket (word 0 = the leaf index).
 extern "C" __global__ __launch_bounds__(EQC_BLOCK) void eqc_gen(EquihashCbDev p) {
     __shared__ uint32_t cnt[NCO];
     if (p.coarse != NCO) return;  // a code object of another geometry than the host sized: no rows
@@ -179,69 +161,117 @@ NX_DEV uint32_t eqc_wave_scan(uint32_t P, const uint32_t v[4], uint32_t* segc) {
     return __shfl(x, 63, 64);
 }
 
-// Producer threads stage slice `s` of coarse bucket d of level L: every row of the bucket (its P
-// segments as one list of `total` rows; a row's segment by binary search over the prefix segc) is
-// read, and the rows of the slice are appended to the LDS buffer (payload at stride ST, ids apart)
-// at positions from a wave-aggregated counter. Returns the rows this lane dropped at the cap.
+// Phase 1, once per coarse bucket d: for this lane's positions pt + k * NP (k < KMAX) of the
+// bucket's rows (its P segments as one list of `total` rows), meta = segment << 8 | slice (16 bits
+// per position, two per word), read from word 1 of each row; positions past `total` get slice
+// 0xFF. The segment of increasing positions is found by walking the prefix segc forward.
 template <int L, uint32_t NP>
-NX_DEV uint32_t eqc_stage_slice(const EquihashCbDev& p, uint32_t inst, uint32_t d, uint32_t s, const uint32_t* segc,
-                                uint32_t total, uint32_t* rows, uint32_t* ids, uint32_t* nstaged) {
-    constexpr int BATCH = EQC_BATCH, W = eqc_words(L), PL = eqc_payload(L), ST = eqc_lds_stride(L);
-    const uint32_t P = p.groups, pt = threadIdx.x, wave0 = pt & ~63u;
-    uint32_t dropped = 0;
-#pragma unroll 1
-    for (uint32_t p0 = wave0; p0 < total; p0 += NP * BATCH) {  // wave-uniform loop
-        EqcRow<W> r[BATCH];
-        bool valid[BATCH];
+NX_DEV void eqc_scan_slices(const EquihashCbDev& p, uint32_t inst, uint32_t d, const uint32_t* segc, uint32_t total,
+                            uint32_t (&meta)[(EQC_KMAX + 1) / 2]) {
+    constexpr int K = EQC_KMAX;
+    const uint32_t pt = threadIdx.x, P = p.groups;
+    uint32_t w1[K], seg[K];
+    uint32_t a = 0;
 #pragma unroll
-        for (int k = 0; k < BATCH; ++k) {
-            const uint32_t pos = p0 + (pt - wave0) + k * NP;
-            valid[k] = pos < total;
-            if (!valid[k]) continue;
-            uint32_t a = 0, z = P;  // largest segment whose prefix is <= pos
-            while (z - a > 1) {
-                const uint32_t mid = (a + z) >> 1;
-                if (segc[mid] <= pos) a = mid; else z = mid;
-            }
-            r[k] = *(const EqcRow<W>*)eqc_row<L>(p, inst, d, a, pos - segc[a]);
-        }
-#pragma unroll
-        for (int k = 0; k < BATCH; ++k) {
-            const bool keep = valid[k] && eqc_slice(r[k].w[1]) == s;
-            if (__ballot(keep) == 0) continue;  // wave-uniform
-            if (!keep) continue;
-            const uint32_t idx = eqc_wave_alloc(nstaged);
-            if (idx >= EQC_STAGE) {
-                ++dropped;
-                continue;
-            }
-            ids[idx] = r[k].w[0];
-#pragma unroll
-            for (int q = 0; q < ST; ++q) rows[idx * ST + q] = q < PL ? r[k].w[1 + q] : 0u;
+    for (int k = 0; k < K; ++k) {
+        const uint32_t pos = pt + (uint32_t)k * NP;
+        w1[k] = 0xFFFFFFFFu;
+        seg[k] = a;
+        if (pos < total) {
+            while (a + 1 < P && segc[a + 1] <= pos) ++a;
+            seg[k] = a;
+            w1[k] = eqc_row<L>(p, inst, d, a, pos - segc[a])[1];
         }
     }
-    return dropped;
+#pragma unroll
+    for (int k = 0; k < (K + 1) / 2; ++k) meta[k] = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t pos = pt + (uint32_t)k * NP;
+        const uint32_t sl = pos < total ? w1[k] >> (32 - SB) : 0xFFu;
+        meta[k / 2] |= ((seg[k] << 8) | sl) << (16 * (k & 1));
+    }
+}
+
+// Phase 2: stage fine bucket b = d * NSL + s (slice s of coarse bucket d): the rows of this lane's
+// positions in the slice get staging indices from one contiguous range per wave, the wave parks
+// their (segment, slot) there and loads the range's rows spread evenly over its 64 lanes; payload
+// words to `rows` (stride ST), back-pointers to refs[L][b][index]. Returns the rows dropped at the
+// staging cap.
+template <int L, uint32_t NP>
+NX_DEV uint32_t eqc_stage_slice(const EquihashCbDev& p, uint32_t inst, uint32_t d, uint32_t s, const uint32_t* segc,
+                                const uint32_t (&meta)[(EQC_KMAX + 1) / 2], uint32_t* rows, uint32_t* park,
+                                uint32_t* nstaged) {
+    constexpr int K = EQC_KMAX, B2 = EQC_B2, W = eqc_words(L), PL = eqc_payload(L), ST = eqc_lds_stride(L);
+    const uint32_t pt = threadIdx.x, lane = eqc_lane();
+    uint32_t nk = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) nk += ((meta[k / 2] >> (16 * (k & 1))) & 0xFFu) == s;
+    uint32_t x = nk;  // wave prefix of the kept counts: one range per wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((int)lane >= o) x += y;
+    }
+    const uint32_t wave_tot = __shfl(x, 63, 64);
+    uint32_t base = 0;
+    if (lane == 0 && wave_tot) base = atomicAdd(nstaged, wave_tot);
+    base = __shfl(base, 0, 64);
+    uint32_t at = base + x - nk;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t m = (meta[k / 2] >> (16 * (k & 1))) & 0xFFFFu;
+        if ((m & 0xFFu) == s) {
+            const uint32_t a = m >> 8, pos = pt + (uint32_t)k * NP;
+            if (at < EQP_STAGE) park[at] = (a << 16) | (pos - segc[a]);
+            ++at;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t n = base >= EQP_STAGE ? 0 : min(wave_tot, (uint32_t)EQP_STAGE - base);
+    const uint32_t b = d * NSL + s;
+    uint32_t* refs = p.refs + (((size_t)inst * EQ_LEVELS + L) * EQ_BUCKETS + b) * EQP_REF_STRIDE;
+#pragma unroll 1
+    for (uint32_t t0 = 0; t0 < n; t0 += 64 * B2) {
+        EqcRow<W> r[B2];
+        uint32_t idx[B2];
+#pragma unroll
+        for (int q = 0; q < B2; ++q) {
+            const uint32_t t = t0 + lane + 64u * q;
+            idx[q] = t < n ? base + t : 0xFFFFFFFFu;
+            if (idx[q] == 0xFFFFFFFFu) continue;
+            const uint32_t pk = park[idx[q]];
+            r[q] = *(const EqcRow<W>*)eqc_row<L>(p, inst, d, pk >> 16, pk & 0xFFFFu);
+        }
+#pragma unroll
+        for (int q = 0; q < B2; ++q) {
+            if (idx[q] == 0xFFFFFFFFu) continue;
+            refs[idx[q]] = r[q].w[0];
+#pragma unroll
+            for (int w = 0; w < ST; ++w) rows[idx[q] * ST + w] = w < PL ? r[q].w[1 + w] : 0u;
+        }
+    }
+    return lane == 0 ? wave_tot - n : 0u;
 }
 
 // Round R (1..8): collide level R-1 on digit R-1 fine bucket by fine bucket, write level R.
 // R = 9 is the final round: level-8 rows equal on d_8 and d_9 (40 bits) become candidates.
 //
 // Producer / consumer split as in the private-slot solver: the first EQC_NP threads (7 waves)
-// stage the NEXT fine bucket (a coarse bucket's counts scan, its rows streamed, the slice kept)
-// while the other 9 waves chain and collide the current one and emit rows. Two barriers per fine
-// bucket: after staging (A: rows ready) and after chaining (B: links ready).
+// stage the NEXT fine bucket while the other 9 waves chain and collide the current one and emit
+// rows. Two barriers per fine bucket: after staging (A: rows ready) and after chaining (B: links
+// ready).
 template <int R>
 NX_DEV void eqc_round_impl(const EquihashCbDev& p) {
     constexpr int ST = eqc_lds_stride(R - 1);  // LDS words per staged level-(R-1) row
     constexpr uint32_t NP = EQC_NP, NC = EQC_BLOCK - NP;
     __shared__ uint32_t cnt[NCO];
-    __shared__ __attribute__((aligned(16))) uint32_t rows[2][EQC_STAGE * ST];
-    __shared__ uint32_t ids[2][EQC_STAGE];
-    __shared__ int head[NKEY];
-    __shared__ short nxt[EQC_STAGE];
+    __shared__ __attribute__((aligned(16))) uint32_t rows[2][EQP_STAGE * ST];
+    __shared__ uint32_t park[EQP_STAGE];
+    __shared__ int head[1 << KB];
+    __shared__ short nxt[EQP_STAGE];
     __shared__ uint32_t segc[NP / 64][EQC_MAX_P];  // one prefix copy per producer wave
     __shared__ uint32_t nstaged[2];
-    __shared__ uint32_t pcount;
     if (p.coarse != NCO) return;  // geometry mismatch (whole workgroup): nothing staged or emitted
     const uint32_t inst = blockIdx.y, grp = blockIdx.x;
     const uint32_t P = p.groups, G = gridDim.x;
@@ -249,24 +279,25 @@ NX_DEV void eqc_round_impl(const EquihashCbDev& p) {
     const uint32_t ct = threadIdx.x - NP;
     uint32_t* my_segc = segc[threadIdx.x / 64 % (NP / 64)];
     eqc_clear(cnt);
-    for (uint32_t i = threadIdx.x; i < NKEY; i += EQC_BLOCK) head[i] = -1;
-    if (threadIdx.x == 0) {
-        nstaged[0] = nstaged[1] = 0;
-        pcount = 0;
-    }
+    for (uint32_t i = threadIdx.x; i < (1u << KB); i += EQC_BLOCK) head[i] = -1;
+    if (threadIdx.x == 0) nstaged[0] = nstaged[1] = 0;
     __syncthreads();
-    // work item k of this workgroup: coarse bucket grp + G * (k / NSL), slice k % NSL (the slices
-    // of a coarse bucket back to back, so its re-reads find it in the L2)
+    // work item k of this workgroup: coarse bucket grp + G * (k / NSL), slice k % NSL (a coarse
+    // bucket's fine buckets back to back, so its phase-1 scan serves all of them)
     const uint32_t items = grp < NCO ? ((NCO - 1 - grp) / G + 1) * NSL : 0;
     auto coarse = [&](uint32_t k) { return grp + G * (k / NSL); };
     uint32_t cv[4] = {0, 0, 0, 0};
-    uint32_t total = 0;  // rows of the coarse bucket being staged (producer waves, after the scan)
-    uint32_t dropped = 0, truncated = 0, staged_max = 0, lost_ids = 0;
+    uint32_t meta[(EQC_KMAX + 1) / 2];
+    uint32_t dropped = 0, truncated = 0, staged_max = 0;
     auto stage = [&](uint32_t k, uint32_t buf) {
         const uint32_t d = coarse(k), s = k % NSL;
-        if (s == 0) total = eqc_wave_scan(P, cv, my_segc);  // counts loaded one item ahead
-        dropped += eqc_stage_slice<R - 1, NP>(p, inst, d, s, my_segc, total, rows[buf], ids[buf], &nstaged[buf]);
-        if (s == NSL - 1 && k + 1 < items) eqc_load_counts(p, inst, R - 1, coarse(k + 1), cv);
+        if (s == 0) {
+            const uint32_t total = eqc_wave_scan(P, cv, my_segc);  // counts loaded one bucket ahead
+            if (total > NP * EQC_KMAX && threadIdx.x == 0) dropped += total - NP * EQC_KMAX;
+            eqc_scan_slices<R - 1, NP>(p, inst, d, my_segc, total, meta);
+            if (k + NSL < items) eqc_load_counts(p, inst, R - 1, coarse(k + NSL), cv);
+        }
+        dropped += eqc_stage_slice<R - 1, NP>(p, inst, d, s, my_segc, meta, rows[buf], park, &nstaged[buf]);
     };
     if (producer && items) {  // prologue: stage the first item
         eqc_load_counts(p, inst, R - 1, coarse(0), cv);
@@ -276,13 +307,13 @@ NX_DEV void eqc_round_impl(const EquihashCbDev& p) {
     for (uint32_t k = 0; k < items; ++k, cur ^= 1) {
         __syncthreads();  // A: rows[cur] staged, head reset, previous item's emission done
         const uint32_t got = nstaged[cur];
-        const uint32_t n = min(got, (uint32_t)EQC_STAGE);
+        const uint32_t n = min(got, (uint32_t)EQP_STAGE);
         const uint32_t* rc = rows[cur];
-        const uint32_t* ic = ids[cur];
+        const uint32_t b = coarse(k) * NSL + k % NSL;  // the fine bucket being collided
         if (!producer) {
             for (uint32_t i = ct; i < n; i += NC) {
-                const uint32_t key = (rc[i * ST] >> (32 - SB - KB)) & (NKEY - 1);
-                nxt[i] = (short)atomicExch(&head[key], (int)i);
+                const uint32_t sub = (rc[i * ST] >> (32 - SB - KB)) & ((1u << KB) - 1);
+                nxt[i] = (short)atomicExch(&head[sub], (int)i);
             }
         } else if (threadIdx.x == 0) {
             nstaged[cur ^ 1] = 0;  // every read of it (item k - 1) happened before A
@@ -290,11 +321,11 @@ NX_DEV void eqc_round_impl(const EquihashCbDev& p) {
         }
         __syncthreads();  // B: chain links of the current item complete
         if (producer) {
-            for (uint32_t i = threadIdx.x; i < NKEY; i += NP) head[i] = -1;  // chain building is over
+            for (uint32_t i = threadIdx.x; i < (1u << KB); i += NP) head[i] = -1;  // chain building is over
             if (k + 1 < items) stage(k + 1, cur ^ 1);
-        } else if constexpr (R == 9) {  // final round: equal d_8 and d_9 make a candidate
+        } else if constexpr (R == 9) {  // final round: equal d_8 (chain) and d_9 make a candidate
             for (uint32_t i = ct; i < n; i += NC) {
-                // a level-8 payload is one word: slice, key and d_9 (CB = 8)
+                // a level-8 payload is one word: slice, sub-digit and d_9 (CB = 8)
                 const uint32_t di = rc[i * ST];
                 int j = nxt[i], steps = 0;
                 for (; j >= 0 && steps < EQ_MAX_CHAIN; j = nxt[j], ++steps) {
@@ -302,16 +333,15 @@ NX_DEV void eqc_round_impl(const EquihashCbDev& p) {
                     uint32_t* c = p.cands + (size_t)inst * (1 + 2 * EQ_MAX_CAND);
                     const uint32_t q = atomicAdd(&c[0], 1u);
                     if (q < EQ_MAX_CAND) {
-                        c[1 + 2 * q] = ic[i];
-                        c[2 + 2 * q] = ic[(uint32_t)j];
+                        c[1 + 2 * q] = b * EQP_REF_STRIDE + i;
+                        c[2 + 2 * q] = b * EQP_REF_STRIDE + (uint32_t)j;
                     }
                 }
                 truncated += j >= 0;  // the chain went on past EQ_MAX_CHAIN: pairs not tried
             }
         } else {
             constexpr int WO = eqc_words(R), MO = eqc_payload(R);
-            constexpr uint32_t REST = 0xFFFFFFFFu >> (SB + KB);  // payload bits after slice + key
-            uint2* plog = (uint2*)p.pairs + ((size_t)inst * EQ_LEVELS + R) * (size_t)P * p.pmax;
+            constexpr uint32_t REST = 0xFFFFFFFFu >> (SB + KB);  // payload bits after slice + sub-digit
             for (uint32_t i = ct; i < n; i += NC) {
                 const uint32_t* ra = rc + i * ST;
                 int j = nxt[i], steps = 0;
@@ -327,16 +357,9 @@ NX_DEV void eqc_round_impl(const EquihashCbDev& p) {
                     if (rest == 0) continue;  // identical remainder: only duplicate indices
                     const uint32_t nb = (x[0] >> 12) & (NCO - 1);  // the next digit's coarse bits
                     const uint32_t slot = atomicAdd(&cnt[nb], 1u);
-                    const uint32_t kid = eqc_wave_alloc(&pcount);
-                    if (kid >= p.pmax) {
-                        ++lost_ids;
-                        continue;
-                    }
-                    const uint32_t id = grp * p.pmax + kid;
-                    plog[id] = make_uint2(ic[i], ic[(uint32_t)j]);
                     if (slot < p.seg) {
                         EqcRow<WO> r;
-                        r.w[0] = id;
+                        r.w[0] = (b << 20) | (i << 10) | (uint32_t)j;
 #pragma unroll
                         for (int q = 0; q < WO - 1; ++q)
                             r.w[1 + q] = q < MO ? (x[q] << 20) | (q + 1 < ST ? x[q + 1] >> 12 : 0u) : 0u;
@@ -348,11 +371,10 @@ NX_DEV void eqc_round_impl(const EquihashCbDev& p) {
         }
     }
     __syncthreads();
-    // staging overflow (rows of a fine bucket beyond EQC_STAGE), segment overflow (level-R rows
-    // beyond a segment) and pair ids beyond pmax are counted apart
+    // staging overflow (rows of a fine bucket beyond EQP_STAGE, or of a coarse bucket beyond the
+    // positions the producers scan) and segment overflow (level-R rows beyond a segment) apart
     if (dropped) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_STAGE], dropped);
     if (threadIdx.x == 0 && staged_max) atomicMax(&p.stats[inst * EQP_STATS + EQP_STAT_STAGE_MAX], staged_max);
-    if (lost_ids) atomicAdd(&p.stats[inst * EQP_STATS + EQC_STAT_PAIRS], lost_ids);
     if constexpr (R < 9) eqc_flush_counts(p, inst, grp, R, cnt);
     if (truncated) atomicAdd(&p.stats[inst * EQP_STATS + EQP_STAT_CHAIN], truncated);
 }
@@ -371,17 +393,10 @@ EQC_ROUND_KERNEL(8)
 
 extern "C" __global__ __launch_bounds__(EQC_BLOCK, EQC_MIN_WAVES) void eqc_final(EquihashCbDev p) { eqc_round_impl<9>(p); }
 
-// Leaf indices of every candidate: pairs[8] .. pairs[1] from its two level-8 ids (shared body:
-// equihash_device.hpp, with the pair log as the children lookup).
+// Leaf indices of every candidate (shared body: equihash_device.hpp; refs as equihash_ps.hip).
 extern "C" __global__ __launch_bounds__(256) void eqc_reconstruct(EquihashCbDev p) {
     const uint32_t inst = blockIdx.y;
-    const uint2* plog = (const uint2*)p.pairs + (size_t)inst * EQ_LEVELS * (size_t)p.groups * p.pmax;
-    const size_t level_stride = (size_t)p.groups * p.pmax;
-    eq_reconstruct_tree<256>(
-        [&](int level, uint32_t s, uint32_t& a, uint32_t& b) {
-            const uint2 v = plog[(size_t)level * level_stride + s];
-            a = v.x;
-            b = v.y;
-        },
-        p.cands + (size_t)inst * (1 + 2 * EQ_MAX_CAND), p.sols + (size_t)inst * (1 + EQ_MAX_SOL * 512));
+    eq_reconstruct_body<EQP_REF_STRIDE, 256>(p.refs + (size_t)inst * EQ_LEVELS * EQ_BUCKETS * EQP_REF_STRIDE,
+                                             p.cands + (size_t)inst * (1 + 2 * EQ_MAX_CAND),
+                                             p.sols + (size_t)inst * (1 + EQ_MAX_SOL * 512));
 }

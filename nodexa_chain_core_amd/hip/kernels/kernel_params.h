@@ -118,40 +118,33 @@ struct EquihashPsDev {
     uint32_t* stats;        // [inst][EQP_STATS]: rows dropped per level (segment or staging overflow)
 };
 
-// Coarse-bucket Equihash(200,9) solver (equihash_cb.hip). A level's rows are stored by their
-// digit's top EQC_COARSE_BITS bits only (EQC_COARSE destination buckets instead of 4096), so every
-// writer keeps 16x fewer partially written lines open and the L2 merges its appends (profiles/README
-// r5a: 0.43-0.54 EA write requests per row against 1.06-1.18); a round's work item is a fine bucket
-// = coarse bucket x EQC_SLICE_BITS slice bits read from the row, so consumers read each coarse
-// bucket 2^EQC_SLICE_BITS times (L2 hits after the first). Back-pointers go through a pair log:
-// row word 0 = the row's id (writer x pmax + the writer's emission count), pairs[level][id] = the
-// ids of the two parent rows (level 0 ids are leaf indices).
+// Coarse-bucket Equihash(200,9) solver (equihash_cb.hip): the private-slot solver's 4096 fine
+// buckets, staging, chains and back-pointers, with a level's rows STORED by the top
+// EQC_COARSE_BITS bits of their digit only (EQC_COARSE destination buckets instead of 4096: every
+// writer keeps 16x fewer partially written lines open and the L2 merges its appends; profiles/README
+// r5a: 0.43-0.54 EA write requests per row against 1.06-1.18). The other bucket bits travel in the
+// row; producers stage a coarse bucket's fine buckets in two phases (slice scan, then the rows).
 #ifndef EQC_COARSE_BITS
 #define EQC_COARSE_BITS 8   // the shipping geometry; a code object built with other bits is run with
 #endif                      // the matching `coarse` (EquihashCbDev.coarse, ops/equihash.py coarse_bits)
-#ifndef EQC_SLICE_BITS
-#define EQC_SLICE_BITS 2
-#endif
 #define EQC_COARSE (1 << EQC_COARSE_BITS)
 #define EQC_MAX_P 64        // writers per instance (the counts scan keeps one prefix per producer wave)
-#define EQC_STAGE 2560      // rows of one fine bucket staged in LDS (mean 2048-2100; 2472 seen, r5b)
-#define EQC_ROW_WORDS 7     // widest stored row (levels 0-1: id + 6 payload words)
-#define EQC_STAT_PAIRS 12   // stats slot: pair ids beyond a writer's pmax (a loss, like slots 0-10)
+#define EQC_ROW_WORDS 7     // widest stored row (levels 0-1: back-pointer + 6 payload words)
 struct EquihashCbDev {
     const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashDev)
     uint64_t h0[8];
     uint32_t input_len;
     uint32_t num_inst;
-    uint32_t groups;        // P: writers (workgroups) per instance in gen and rounds 1-8, <= EQC_COARSE
-    uint32_t seg;           // rows per (coarse bucket, writer) segment (mean 2^21 / 256 / P; host-sized)
-    uint32_t pmax;          // pair ids per writer and level: coarse * seg
+    uint32_t groups;        // P: writers (workgroups) per instance in gen and rounds 1-8, <= EQC_MAX_P
+    uint32_t seg;           // rows per (coarse bucket, writer) segment (mean 2^21 / coarse / P; host-sized)
     uint32_t coarse;        // coarse buckets per level: must equal the code object's EQC_COARSE
-    uint32_t* hashes;       // [2][inst][EQC_COARSE][P][seg] row slots of EQC_ROW_WORDS words (rows at their level's width)
-    uint32_t* pairs;        // [inst][LEVELS][P * pmax][2]: parent ids of every row id (levels 1..8)
-    uint16_t* counts;       // [inst][LEVELS][P][EQC_COARSE] rows per segment (clamped to seg)
-    uint32_t* cands;        // [inst][1 + 2*MAX_CAND]: count, then level-8 id pairs
+    uint32_t pad;
+    uint32_t* hashes;       // [2][inst][coarse][P][seg] row slots of EQC_ROW_WORDS words (rows at their level's width)
+    uint32_t* refs;         // [inst][LEVELS][BUCKETS][EQP_REF_STRIDE] in staged order (as EquihashPsDev)
+    uint16_t* counts;       // [inst][LEVELS][P][coarse] rows per segment (clamped to seg)
+    uint32_t* cands;        // [inst][1 + 2*MAX_CAND]: count, then (fine bucket << 10 | index) pairs at level 8
     uint32_t* sols;         // [inst][1 + MAX_SOL*512]
-    uint32_t* stats;        // [inst][EQP_STATS] as the private-slot solver, + EQC_STAT_PAIRS
+    uint32_t* stats;        // [inst][EQP_STATS] as the private-slot solver
 };
 
 // Batch ECDSA verification (secp256k1_verify.hip): one job per signature, limbs little-endian.

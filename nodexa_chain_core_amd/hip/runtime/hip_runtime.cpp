@@ -654,16 +654,14 @@ PYBIND11_MODULE(_hip, m) {
        py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQP_FINAL_GROUPS);
     // Coarse-bucket solver (equihash_cb.hip): ks = [eqc_gen, eqc_round1..8, eqc_final,
     // eqc_reconstruct]; `groups` writers per instance, `seg` rows per segment (the caller sizes the
-    // buffers), a pair log of groups * EQC_COARSE * seg ids per instance and level. Buffers as
-    // documented on EquihashCbDev.
+    // buffers), `coarse` buckets per level (the code object's). Buffers as documented on
+    // EquihashCbDev.
     m.attr("EQC_COARSE") = EQC_COARSE;
-    m.attr("EQC_STAGE") = EQC_STAGE;
     m.attr("EQC_ROW_WORDS") = EQC_ROW_WORDS;
-    m.attr("EQC_STAT_PAIRS") = EQC_STAT_PAIRS;
     m.attr("EQC_MAX_P") = EQC_MAX_P;
     m.def("launch_equihash_cb_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
                                          uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uint32_t groups,
-                                         uint32_t seg, uintptr_t hashes, uintptr_t pairs, uintptr_t counts, uintptr_t cands,
+                                         uint32_t seg, uintptr_t hashes, uintptr_t refs, uintptr_t counts, uintptr_t cands,
                                          uintptr_t sols, uintptr_t stats, uintptr_t stream, uint32_t block,
                                          uint32_t final_groups, uint32_t coarse) {
         if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash_cb kernels");
@@ -684,10 +682,9 @@ PYBIND11_MODULE(_hip, m) {
         p.num_inst = num_inst;
         p.groups = groups;
         p.seg = seg;
-        p.pmax = coarse * seg;
         p.coarse = coarse;
         p.hashes = reinterpret_cast<uint32_t*>(hashes);
-        p.pairs = reinterpret_cast<uint32_t*>(pairs);
+        p.refs = reinterpret_cast<uint32_t*>(refs);
         p.counts = reinterpret_cast<uint16_t*>(counts);
         p.cands = reinterpret_cast<uint32_t*>(cands);
         p.sols = reinterpret_cast<uint32_t*>(sols);
@@ -703,7 +700,7 @@ PYBIND11_MODULE(_hip, m) {
         ks[9]->launch_bytes(dim3(final_groups, num_inst), dim3(block), 0, s, &p, sizeof(p));
         ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
     }, py::arg("ks"), py::arg("h0"), py::arg("msgs"), py::arg("input_len"), py::arg("num_inst"), py::arg("groups"),
-       py::arg("seg"), py::arg("hashes"), py::arg("pairs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
+       py::arg("seg"), py::arg("hashes"), py::arg("refs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
        py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQC_COARSE,
        py::arg("coarse") = EQC_COARSE);
     // The 11 kernel launches captured once into a hipGraph (fixed device buffers, so the graph

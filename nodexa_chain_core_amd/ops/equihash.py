@@ -6,10 +6,10 @@ reconstruction, all enqueued on one stream with no host synchronisation in betwe
 every solution on the device (equihash.hip eq_verify_slots) before it is reported.
 
 Engines (NODEXA_EQ_ENGINE selects; the default is the measured winner, profiles/README r5):
-  "cb"  coarse destination buckets (equihash_cb.hip): a level's rows stored by 8 digit bits
-        (256 buckets), fine buckets read as slices, back-pointers through a pair log. Memory at
-        16 instances: 2 x 16 x 256 x 16 x 721 x 28 B level buffers (2.6 GB) + the pair log
-        (16 x 9 x 3.0M x 8 B = 3.4 GB) of the 288 GB HBM3E.
+  "cb"  coarse destination buckets (equihash_cb.hip): the "ps" collision structure, with a
+        level's rows stored by 8 digit bits (256 buckets, 16 fine buckets each). Memory at 16
+        instances: 2 x 16 x 256 x 16 x 721 x 28 B level buffers (2.6 GB) + refs (2.4 GB) of the
+        288 GB HBM3E.
   "ps"  private slot segments in 4096 buckets (equihash_ps.hip): one EA write request per row.
 """
 from __future__ import annotations
@@ -134,10 +134,9 @@ class EquihashSolver:
                 # up to ~4 % above 2^21) + 8 sigma, so an overflow (a host re-solve) stays ~1e-12
                 m = (1 << 21) / D / self.groups
                 self.seg = int(m * 1.04 + 8 * m ** 0.5 + 8)
-                self.pmax = D * self.seg
                 self.hashes = torch.empty(2 * ni * D * self.groups * self.seg * Wd, dtype=torch.int32,
                                           device=self.device)
-                self.pairs = torch.empty(ni * L * self.groups * self.pmax * 2, dtype=torch.int32, device=self.device)
+                self.refs = torch.empty(ni * L * B * self.h.EQP_REF_STRIDE, dtype=torch.int32, device=self.device)
                 self.counts = torch.empty(ni * L * self.groups * D, dtype=torch.int16, device=self.device)
             else:
                 S, R, W = self.h.EQP_SLOTS, self.h.EQP_REF_STRIDE, self.h.EQ_WORDS
@@ -193,7 +192,7 @@ class EquihashSolver:
             if self.engine == "cb":
                 self.h.launch_equihash_cb_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
                                                 self.num_inst, self.groups, self.seg, self.hashes.data_ptr(),
-                                                self.pairs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
+                                                self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
                                                 self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block,
                                                 self.final_groups, self.coarse)
             else:
@@ -218,12 +217,9 @@ class EquihashSolver:
         self._pending.append((list(inputs), (land, lstat, lver), ev))
 
     def _lossy(self, st: np.ndarray) -> bool:
-        """Whether one instance's stats row records a loss: segment / staging overflow (slots
-        0-10), or (cb) pair ids beyond a writer's range; slot 11 is a diagnostic maximum."""
-        lost = bool(st[:self.h.EQP_STAT_STAGE + 1].any())
-        if self.engine == "cb":
-            lost |= bool(st[self.h.EQC_STAT_PAIRS])
-        return lost
+        """Whether one instance's stats row records a loss: segment / staging overflow or a cut
+        chain (slots 0-10); slot 11 is a diagnostic maximum."""
+        return bool(st[:self.h.EQP_STAT_STAGE + 1].any())
 
     def collect_arrays(self, inputs: list[bytes] | None = None, verify: str = "device") -> list[np.ndarray]:
         """Solutions of the oldest queued launch (waits only for that launch), one (m, 512) uint32
@@ -291,6 +287,6 @@ class EquihashSolver:
         c = self.counts[: L * self.groups * D].view(L, self.groups, D).to(torch.int32).sum(1).cpu()
         dropped = self.stats_buf[: self.h.EQP_STATS].cpu().tolist()
         return {"rows_per_level": [int(x) for x in c.sum(1)], "max_fill": [int(x) for x in c.max(1).values],
-                "cap": self.h.EQC_STAGE if self.engine == "cb" else self.h.EQP_STAGE, "dropped_per_level": dropped[:L],
+                "cap": self.h.EQP_STAGE, "dropped_per_level": dropped[:L],
                 "stage_dropped": dropped[self.h.EQP_STAT_STAGE], "largest_bucket": dropped[self.h.EQP_STAT_STAGE_MAX],
-                "lost_ids": dropped[12], "candidates": int(self.cands[0].item())}
+                "chains_cut": dropped[self.h.EQP_STAT_CHAIN], "candidates": int(self.cands[0].item())}
