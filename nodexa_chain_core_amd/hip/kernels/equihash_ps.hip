@@ -67,17 +67,9 @@
 #define EQP_NP 448  // producer threads of a round workgroup (7 of its 16 waves)
 #endif
 
-// Instance and writer of this workgroup in a (writers x instances) grid. Workgroups are dispatched
-// to the 8 XCDs round-robin by linear id, so blockIdx.y = instance spreads every instance over all
-// XCDs; EQP_XCD_LOCAL (measured variant) takes instance = id mod instances instead, which keeps
-// an instance's writers -- and the rows of its buckets -- on one XCD's L2.
-#ifdef EQP_XCD_LOCAL
-#define EQP_INST_GRP(inst, grp)                                           \
-    const uint32_t eqp_lin_ = blockIdx.x + blockIdx.y * gridDim.x;        \
-    const uint32_t inst = eqp_lin_ % gridDim.y, grp = eqp_lin_ / gridDim.y
-#else
+// Instance and writer of this workgroup in a (writers x instances) grid: blockIdx.y = instance
+// spreads every instance over all 8 XCDs (XCD-local instances measured neutral, profiles/README r4c).
 #define EQP_INST_GRP(inst, grp) const uint32_t inst = blockIdx.y, grp = blockIdx.x
-#endif
 
 // EQP_NO_ROW_STORE (measurement only, results invalid): the row stores compiled out, the rest of
 // each kernel (gathers, chains, slot counters, back-pointer copies) unchanged -- what the rows'

@@ -67,28 +67,13 @@ struct KawpowVerifyJob {
 // ---------------------------------------------------------------- Equihash(200,9)
 #define EQ_BUCKET_BITS 12
 #define EQ_BUCKETS (1 << EQ_BUCKET_BITS)
-#define EQ_CAP 768  // mean fill 512..537 rows/bucket, max observed 647 over 4096 buckets
 #define EQ_WORDS 8
 #define EQ_LEVELS 9
 #define EQ_MAX_CAND 16384  // ~500-1100 final-round collisions per nonce (almost all duplicate trees), 4300-4900
                           // in ~0.2 % of nonces: a 4096 cap sent those to the host re-solve (profiles r3zb)
 #define EQ_RECON_GROUPS 128  // reconstruct workgroups per instance (grid-stride over candidates)
-#define EQ_MAX_BANKS 8
 #define EQ_MAX_SOL 16
 
-struct EquihashDev {
-    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (input bytes, LE); the index is OR-ed in-kernel
-    uint64_t h0[8];         // BLAKE2b state after the parameter block (digest 50, "ZcashPoW" personal)
-    uint32_t input_len;     // bytes of input (<= 124: one compression per digest)
-    uint32_t num_inst;
-    uint32_t banks;         // slot-counter banks per bucket (1,2,4,8): spreads the append atomics
-    uint32_t pad;
-    uint32_t* hashes;       // [2][inst][BUCKETS][CAP][WORDS]
-    uint32_t* refs;         // [inst][LEVELS][BUCKETS][CAP]
-    uint32_t* counts;       // [inst][LEVELS+1][BUCKETS][EQ_MAX_BANKS]
-    uint32_t* cands;        // [inst][1 + 2*MAX_CAND]: count, then (slot_a, slot_b) global slot ids at level 8
-    uint32_t* sols;         // [inst][1 + MAX_SOL*512]: count, then solutions
-};
 
 // Private-slot Equihash(200,9) solver (equihash_ps.hip). Each round runs `groups` (P)
 // workgroups per instance; workgroup w owns a `seg`-row (C) segment of every bucket of the
@@ -104,7 +89,7 @@ struct EquihashDev {
 #define EQP_STAT_STAGE_MAX 11  // largest bucket seen by a round (diagnostic, not a loss)
 #define EQP_FINAL_GROUPS 1024  // final-round workgroups per instance (it writes no level)
 struct EquihashPsDev {
-    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashDev)
+    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (input bytes, LE; the index is OR-ed in-kernel)
     uint64_t h0[8];
     uint32_t input_len;
     uint32_t num_inst;
@@ -116,35 +101,6 @@ struct EquihashPsDev {
     uint32_t* cands;        // [inst][1 + 2*MAX_CAND]: count, then (bucket << 10 | index) pairs at level 8
     uint32_t* sols;         // [inst][1 + MAX_SOL*512]
     uint32_t* stats;        // [inst][EQP_STATS]: rows dropped per level (segment or staging overflow)
-};
-
-// Coarse-bucket Equihash(200,9) solver (equihash_cb.hip): the private-slot solver's 4096 fine
-// buckets, staging, chains and back-pointers, with a level's rows STORED by the top
-// EQC_COARSE_BITS bits of their digit only (EQC_COARSE destination buckets instead of 4096: every
-// writer keeps 16x fewer partially written lines open and the L2 merges its appends; profiles/README
-// r5a: 0.43-0.54 EA write requests per row against 1.06-1.18). The other bucket bits travel in the
-// row; producers stage a coarse bucket's fine buckets in two phases (slice scan, then the rows).
-#ifndef EQC_COARSE_BITS
-#define EQC_COARSE_BITS 8   // the shipping geometry; a code object built with other bits is run with
-#endif                      // the matching `coarse` (EquihashCbDev.coarse, ops/equihash.py coarse_bits)
-#define EQC_COARSE (1 << EQC_COARSE_BITS)
-#define EQC_MAX_P 64        // writers per instance (the counts scan keeps one prefix per producer wave)
-#define EQC_ROW_WORDS 7     // widest stored row (levels 0-1: back-pointer + 6 payload words)
-struct EquihashCbDev {
-    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashDev)
-    uint64_t h0[8];
-    uint32_t input_len;
-    uint32_t num_inst;
-    uint32_t groups;        // P: writers (workgroups) per instance in gen and rounds 1-8, <= EQC_MAX_P
-    uint32_t seg;           // rows per (coarse bucket, writer) segment (mean 2^21 / coarse / P; host-sized)
-    uint32_t coarse;        // coarse buckets per level: must equal the code object's EQC_COARSE
-    uint32_t pad;
-    uint32_t* hashes;       // [2][inst][coarse][P][seg] row slots of EQC_ROW_WORDS words (rows at their level's width)
-    uint32_t* refs;         // [inst][LEVELS][BUCKETS][EQP_REF_STRIDE] in staged order (as EquihashPsDev)
-    uint16_t* counts;       // [inst][LEVELS][P][coarse] rows per segment (clamped to seg)
-    uint32_t* cands;        // [inst][1 + 2*MAX_CAND]: count, then (fine bucket << 10 | index) pairs at level 8
-    uint32_t* sols;         // [inst][1 + MAX_SOL*512]
-    uint32_t* stats;        // [inst][EQP_STATS] as the private-slot solver
 };
 
 // Batch ECDSA verification (secp256k1_verify.hip): one job per signature, limbs little-endian.
@@ -170,7 +126,7 @@ struct SecpVerifyParams {
 // Batch verification of packed Equihash(200,9) solutions (equihash.hip eq_verify).
 #define EQ_SOL_WORDS 336  // 1344 bytes = 512 x 21-bit big-endian indices
 struct EquihashVerifyParams {
-    const uint64_t* msgs;   // [num][16] BLAKE2b message words of each input (as EquihashDev)
+    const uint64_t* msgs;   // [num][16] BLAKE2b message words of each input (as EquihashPsDev)
     uint64_t h0[8];
     uint32_t input_len;
     uint32_t num;
@@ -179,7 +135,7 @@ struct EquihashVerifyParams {
 };
 // The solver's own solution slots, verified on the device (equihash.hip eq_verify_slots).
 struct EquihashSlotVerifyParams {
-    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashDev)
+    const uint64_t* msgs;   // [inst][16] BLAKE2b message words (as EquihashPsDev)
     uint64_t h0[8];
     uint32_t input_len;
     uint32_t num_inst;

@@ -112,66 +112,6 @@ void load_words(const std::string& b, uint32_t out[8]) {
 }  // namespace
 
 
-// ---------------------------------------------------------------- Equihash solve sequence
-EquihashDev make_equihash_params(const std::vector<std::shared_ptr<Kernel>>& ks, const std::vector<uint64_t>& h0,
-                                 uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
-                                 uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols, uint32_t banks) {
-    if (banks == 0 || banks > EQ_MAX_BANKS || (banks & (banks - 1)) || EQ_CAP % banks)
-        throw std::invalid_argument("banks must be a power of two <= EQ_MAX_BANKS dividing EQ_CAP");
-    // ks = [eq_gen, eq_round1..eq_round8, eq_final, eq_reconstruct]
-    if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash kernels");
-    if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
-    if (input_len > 124 || num_inst == 0) throw std::invalid_argument("bad equihash geometry");
-    EquihashDev p{};
-    p.msgs = reinterpret_cast<const uint64_t*>(msgs);
-    for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
-    p.input_len = input_len;
-    p.num_inst = num_inst;
-    p.banks = banks;
-    p.hashes = reinterpret_cast<uint32_t*>(hashes);
-    p.refs = reinterpret_cast<uint32_t*>(refs);
-    p.counts = reinterpret_cast<uint32_t*>(counts);
-    p.cands = reinterpret_cast<uint32_t*>(cands);
-    p.sols = reinterpret_cast<uint32_t*>(sols);
-    return p;
-}
-
-// argv == nullptr: HIP_LAUNCH_PARAM_BUFFER_POINTER launches of &p (direct use). Under stream
-// capture pass argv = {&p} with p owned by the graph: the kernel nodes then take the
-// argument through kernelParams and nothing points into this function's stack.
-void clear_equihash_state(const EquihashDev& p, hipStream_t s) {
-    const uint32_t n = p.num_inst;
-    check(hipMemsetAsync(p.counts, 0, size_t(n) * (EQ_LEVELS + 1) * EQ_BUCKETS * EQ_MAX_BANKS * 4, s), "memset counts");
-    check(hipMemsetAsync(p.cands, 0, size_t(n) * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
-    check(hipMemsetAsync(p.sols, 0, size_t(n) * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
-}
-
-void issue_equihash_solve(const std::vector<std::shared_ptr<Kernel>>& ks, const EquihashDev& p, hipStream_t s,
-                          void** argv = nullptr) {
-    const uint32_t n = p.num_inst;
-    if (!argv) clear_equihash_state(p, s);  // captured graphs hold the kernels only (see LaunchGraph)
-    auto launch = [&](size_t k, dim3 grid) {
-        if (argv) ks[k]->launch_args(grid, dim3(256), 0, s, argv);
-        else ks[k]->launch_bytes(grid, dim3(256), 0, s, &p, sizeof(p));
-    };
-    launch(0, dim3((1u << 20) / 256, n));
-    for (size_t r = 1; r <= 8; ++r) launch(r, dim3(EQ_BUCKETS, n));
-    launch(9, dim3(EQ_BUCKETS, n));
-    launch(10, dim3(EQ_RECON_GROUPS, n));
-}
-
-struct LaunchGraph {
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    size_t num_nodes = 0;
-    EquihashDev params{};  // the launches' parameter block lives as long as the graph
-    void* argv[1] = {&params};
-    ~LaunchGraph() {
-        if (exec) (void)hipGraphExecDestroy(exec);
-        if (graph) (void)hipGraphDestroy(graph);
-    }
-};
-
 PYBIND11_MODULE(_hip, m) {
     m.doc() = "nodexa HIP host runtime: gfx950 code-object loading and typed kernel launchers";
 
@@ -471,12 +411,10 @@ PYBIND11_MODULE(_hip, m) {
 
     // ---- Equihash(200,9): one full Wagner solve for `num_inst` inputs, enqueued on `stream`
     m.attr("EQ_BUCKETS") = EQ_BUCKETS;
-    m.attr("EQ_CAP") = EQ_CAP;
     m.attr("EQ_WORDS") = EQ_WORDS;
     m.attr("EQ_LEVELS") = EQ_LEVELS;
     m.attr("EQ_MAX_CAND") = EQ_MAX_CAND;
     m.attr("EQ_MAX_SOL") = EQ_MAX_SOL;
-    m.attr("EQ_MAX_BANKS") = EQ_MAX_BANKS;
     m.attr("EQ_SOL_WORDS") = EQ_SOL_WORDS;
     // Batch SHA-256d (sha256d.hip): messages of `len` bytes at `stride`, or (merkle=true) one
     // ComputeMerkleRoot level of `len` 32-byte nodes into (len + 1) / 2 nodes.
@@ -595,14 +533,6 @@ PYBIND11_MODULE(_hip, m) {
         p.out = reinterpret_cast<uint32_t*>(out);
         k.launch_bytes(dim3(EQ_MAX_SOL, num_inst), dim3(256), 0, as_stream(stream), &p, sizeof(p));
     });
-    m.def("launch_equihash_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
-                                      uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
-                                      uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols,
-                                      uintptr_t stream, uint32_t banks) {
-        const EquihashDev p = make_equihash_params(ks, h0, msgs, input_len, num_inst, hashes, refs, counts, cands,
-                                                   sols, banks);
-        issue_equihash_solve(ks, p, as_stream(stream));
-    });
     // Private-slot solver (equihash_ps.hip): ks = [eqp_gen, eqp_round1..8, eqp_final,
     // eqp_reconstruct]; `groups` workgroups per instance per round, EQP_SLOTS / groups rows per
     // segment. Buffers as documented on EquihashPsDev.
@@ -652,90 +582,4 @@ PYBIND11_MODULE(_hip, m) {
     }, py::arg("ks"), py::arg("h0"), py::arg("msgs"), py::arg("input_len"), py::arg("num_inst"), py::arg("groups"),
        py::arg("hashes"), py::arg("refs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
        py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQP_FINAL_GROUPS);
-    // Coarse-bucket solver (equihash_cb.hip): ks = [eqc_gen, eqc_round1..8, eqc_final,
-    // eqc_reconstruct]; `groups` writers per instance, `seg` rows per segment (the caller sizes the
-    // buffers), `coarse` buckets per level (the code object's). Buffers as documented on
-    // EquihashCbDev.
-    m.attr("EQC_COARSE") = EQC_COARSE;
-    m.attr("EQC_ROW_WORDS") = EQC_ROW_WORDS;
-    m.attr("EQC_MAX_P") = EQC_MAX_P;
-    m.def("launch_equihash_cb_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
-                                         uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uint32_t groups,
-                                         uint32_t seg, uintptr_t hashes, uintptr_t refs, uintptr_t counts, uintptr_t cands,
-                                         uintptr_t sols, uintptr_t stats, uintptr_t stream, uint32_t block,
-                                         uint32_t final_groups, uint32_t coarse) {
-        if (ks.size() != 11) throw std::invalid_argument("expected 11 equihash_cb kernels");
-        if (coarse < 64 || coarse > 4096 || (coarse & (coarse - 1))) throw std::invalid_argument("coarse: 64..4096, 2^k");
-        if (final_groups == 0 || final_groups > coarse) throw std::invalid_argument("final_groups: 1..coarse");
-        if (block != 1024) throw std::invalid_argument("block: 1024 (the build's EQC_BLOCK)");
-        if (h0.size() != 8) throw std::invalid_argument("h0 must have 8 words");
-        if (input_len > 124 || num_inst == 0 || num_inst > 65535) throw std::invalid_argument("bad equihash geometry");
-        // P a power of two in [16, EQC_COARSE]: every writer owns whole coarse buckets in the rounds,
-        // 2^20 / P digests in gen, and a segment of `seg` rows in every bucket (u16 counts)
-        if (groups < 16 || groups > EQC_MAX_P || groups > coarse || (groups & (groups - 1)))
-            throw std::invalid_argument("groups: 16..EQC_MAX_P, 2^k");
-        if (seg == 0 || seg > 65535) throw std::invalid_argument("seg: 1..65535");
-        EquihashCbDev p{};
-        p.msgs = reinterpret_cast<const uint64_t*>(msgs);
-        for (int i = 0; i < 8; ++i) p.h0[i] = h0[size_t(i)];
-        p.input_len = input_len;
-        p.num_inst = num_inst;
-        p.groups = groups;
-        p.seg = seg;
-        p.coarse = coarse;
-        p.hashes = reinterpret_cast<uint32_t*>(hashes);
-        p.refs = reinterpret_cast<uint32_t*>(refs);
-        p.counts = reinterpret_cast<uint16_t*>(counts);
-        p.cands = reinterpret_cast<uint32_t*>(cands);
-        p.sols = reinterpret_cast<uint32_t*>(sols);
-        p.stats = reinterpret_cast<uint32_t*>(stats);
-        hipStream_t s = as_stream(stream);
-        const size_t n = num_inst;
-        check(hipMemsetAsync(p.cands, 0, n * (1 + 2 * EQ_MAX_CAND) * 4, s), "memset cands");
-        check(hipMemsetAsync(p.sols, 0, n * (1 + EQ_MAX_SOL * 512) * 4, s), "memset sols");
-        check(hipMemsetAsync(p.stats, 0, n * EQP_STATS * 4, s), "memset stats");
-        // counts need no clear: every writer writes its whole row of every level
-        const dim3 grid(groups, num_inst);
-        for (size_t k = 0; k < 9; ++k) ks[k]->launch_bytes(grid, dim3(block), 0, s, &p, sizeof(p));
-        ks[9]->launch_bytes(dim3(final_groups, num_inst), dim3(block), 0, s, &p, sizeof(p));
-        ks[10]->launch_bytes(dim3(EQ_RECON_GROUPS, num_inst), dim3(256), 0, s, &p, sizeof(p));
-    }, py::arg("ks"), py::arg("h0"), py::arg("msgs"), py::arg("input_len"), py::arg("num_inst"), py::arg("groups"),
-       py::arg("seg"), py::arg("hashes"), py::arg("refs"), py::arg("counts"), py::arg("cands"), py::arg("sols"), py::arg("stats"),
-       py::arg("stream"), py::arg("block") = 1024, py::arg("final_groups") = EQC_COARSE,
-       py::arg("coarse") = EQC_COARSE);
-    // The 11 kernel launches captured once into a hipGraph (fixed device buffers, so the graph
-    // stays valid across batches; only the message words change, in place). Per batch: 3
-    // memsets + one hipGraphLaunch instead of 14 stream operations.
-    py::class_<LaunchGraph, std::shared_ptr<LaunchGraph>>(m, "LaunchGraph")
-        .def("launch", [](LaunchGraph& g, uintptr_t stream) {
-            // the counter / candidate / solution clears stay plain stream memsets: captured as
-            // graph memset nodes they did not re-run on replay here (stale counts, invalid rows)
-            clear_equihash_state(g.params, as_stream(stream));
-            check(hipGraphLaunch(g.exec, as_stream(stream)), "hipGraphLaunch");
-        })
-        .def_readonly("num_nodes", &LaunchGraph::num_nodes);
-    m.def("capture_equihash_solve", [](const std::vector<std::shared_ptr<Kernel>>& ks, std::vector<uint64_t> h0,
-                                       uintptr_t msgs, uint32_t input_len, uint32_t num_inst, uintptr_t hashes,
-                                       uintptr_t refs, uintptr_t counts, uintptr_t cands, uintptr_t sols,
-                                       uint32_t banks) {
-        auto g = std::make_shared<LaunchGraph>();
-        g->params = make_equihash_params(ks, h0, msgs, input_len, num_inst, hashes, refs, counts, cands, sols, banks);
-        hipStream_t cs = nullptr;
-        check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate");
-        check(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-        try {
-            issue_equihash_solve(ks, g->params, cs, g->argv);
-        } catch (...) {
-            hipGraph_t broken = nullptr;
-            (void)hipStreamEndCapture(cs, &broken);
-            if (broken) (void)hipGraphDestroy(broken);
-            (void)hipStreamDestroy(cs);
-            throw;
-        }
-        check(hipStreamEndCapture(cs, &g->graph), "hipStreamEndCapture");
-        (void)hipStreamDestroy(cs);
-        check(hipGraphGetNodes(g->graph, nullptr, &g->num_nodes), "hipGraphGetNodes");
-        check(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0), "hipGraphInstantiate");
-        return g;
-    });
 }

@@ -57,21 +57,13 @@ class EquihashGpuDevice:
         self.torch = torch
         self.device = int(device)
         self.num_inst = int(num_inst)
-        # NODEXA_EQ_STREAMS=2: a solver (its own ~8.6 GB of level buffers at 16 instances) and a
-        # stream per slot, so the queued window's kernels could fill the running one's tails.
-        # Measured no gain (profiles/README r4g: 7.5-8.3 vs 8.0-8.1 ms per window; r4z: the two
-        # streams landed on one hardware queue and the loop ran 1 ms per step slower), so one
-        # solver on one stream is the default: the solver keeps both slots' launches in flight
-        two = os.environ.get("NODEXA_EQ_STREAMS", "1") == "2"
+        # one solver on one stream serves both slots (the solver keeps two launches in flight); a
+        # solver + stream per slot measured no gain (profiles/README r4g: 7.5-8.3 vs 8.0-8.1 ms per
+        # window; r4z: the two streams landed on one hardware queue, +1 ms per step) and was removed
         with torch.cuda.device(self.device):
-            self.streams = [torch.cuda.Stream(device=self.device)]
-            self.streams.append(torch.cuda.Stream(device=self.device) if two else self.streams[0])
-            self.solvers = []
-            for k in range(2 if two else 1):
-                with torch.cuda.stream(self.streams[k]):
-                    self.solvers.append(EquihashSolver(num_inst=self.num_inst, device=self.device))
-            if not two:
-                self.solvers.append(self.solvers[0])
+            self.streams = [torch.cuda.Stream(device=self.device)] * 2
+            with torch.cuda.stream(self.streams[0]):
+                self.solvers = [EquihashSolver(num_inst=self.num_inst, device=self.device)] * 2
             self.starts = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             self.ends = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         self.stream = self.streams[0]

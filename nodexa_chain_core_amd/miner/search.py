@@ -28,7 +28,6 @@ of collectives and one failure path serve every era of the chain; `FaultInjectin
 from __future__ import annotations
 
 import hashlib
-import os
 import struct
 import threading
 import time
@@ -186,12 +185,11 @@ class GpuSearchDevice:
         self.dag_build_s: dict[int, float] = {}
         nbytes = self.h.sizeof_results()
         with torch.cuda.device(self.device):
-            # one stream per slot (NODEXA_SEARCH_STREAMS=1: both slots on one): the queued window
-            # starts on the CUs the running one's last workgroups leave idle instead of waiting
-            # for its whole grid to drain (the tail of a 2^25-nonce window is ~0.8 % of it)
+            # one stream per slot: the queued window starts on the CUs the running one's last
+            # workgroups leave idle instead of waiting for its whole grid to drain (the tail of a
+            # 2^25-nonce window is ~0.8 % of it; +0.3 % against one stream, profiles/README r4f)
             self.stream = torch.cuda.Stream(device=self.device)
-            two = os.environ.get("NODEXA_SEARCH_STREAMS", "2") != "1"
-            self.slot_streams = [self.stream, torch.cuda.Stream(device=self.device) if two else self.stream]
+            self.slot_streams = [self.stream, torch.cuda.Stream(device=self.device)]
             self.side = torch.cuda.Stream(device=self.device)  # next-epoch DAG builds
             self.rings = [torch.zeros(nbytes // 4, dtype=torch.int32, device=self.device) for _ in range(2)]
             self.host = [torch.zeros(nbytes // 4, dtype=torch.int32).pin_memory() for _ in range(2)]

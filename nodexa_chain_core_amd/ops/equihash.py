@@ -5,16 +5,17 @@ BLAKE2b generation kernel, 8 collision rounds, the final 40-bit round and the in
 reconstruction, all enqueued on one stream with no host synchronisation in between — and checks
 every solution on the device (equihash.hip eq_verify_slots) before it is reported.
 
-Engines (NODEXA_EQ_ENGINE selects; the default is the measured winner, profiles/README r5):
-  "cb"  coarse destination buckets (equihash_cb.hip): the "ps" collision structure, with a
-        level's rows stored by 8 digit bits (256 buckets, 16 fine buckets each). Memory at 16
-        instances: 2 x 16 x 256 x 16 x 721 x 28 B level buffers (2.6 GB) + refs (2.4 GB) of the
-        288 GB HBM3E.
-  "ps"  private slot segments in 4096 buckets (equihash_ps.hip): one EA write request per row.
+The engine is the private-slot solver (equihash_ps.hip): every workgroup owns a segment of
+every destination bucket, so a row costs one LDS atomic and one store. Two alternatives were
+built, measured and removed: one global atomic per row (equihash.hip until round 5: 6.5 ms per
+8 solves against 4.4) and coarse destination buckets with the fine bucket bits in the row
+(equihash_cb.hip in round 5: fewer EA write requests per row, 0.38-0.77 against 1.0-1.27, but
+9.3-12.7 ms per 16-solve window against 8.5 — the producers' extra staging work cost more than
+the stores saved; profiles/README r5a-r5e). Memory per instance: 2 x 4096 x 2048 x 32 B row
+buffers (537 MB of address space, ~67 MB written per level) + 9 levels of index refs (151 MB).
 """
 from __future__ import annotations
 
-import os
 import struct
 
 import numpy as np
@@ -24,11 +25,7 @@ from .. import _core
 from ..utils.trace import traced
 from . import runtime
 
-ENGINE_KERNELS = {
-    "ps": ("equihash_ps", ["eqp_gen"] + [f"eqp_round{r}" for r in range(1, 9)] + ["eqp_final", "eqp_reconstruct"]),
-    "cb": ("equihash_cb", ["eqc_gen"] + [f"eqc_round{r}" for r in range(1, 9)] + ["eqc_final", "eqc_reconstruct"]),
-}
-DEFAULT_ENGINE = os.environ.get("NODEXA_EQ_ENGINE", "ps")
+KERNELS = ["eqp_gen"] + [f"eqp_round{r}" for r in range(1, 9)] + ["eqp_final", "eqp_reconstruct"]
 
 
 def blake2b_h0(n: int = 200, k: int = 9) -> list[int]:
@@ -93,56 +90,35 @@ def verify_solutions(inputs: list[bytes], solutions: list[bytes], device: int | 
 
 class EquihashSolver:
     def __init__(self, num_inst: int = 8, device: int | None = None, code_object: str | None = None,
-                 engine: str | None = None, groups: int | None = None, block: int = 1024,
-                 final_groups: int | None = None, coarse_bits: int | None = None):
-        """`code_object`: path of an alternative build of the engine's .hip (tuning sweeps).
-        `engine`: "cb" or "ps" (module docstring); `groups` writers (workgroups) per instance per
-        round, by default so that groups x instances = 256 (one 1024-thread workgroup per CU)."""
-        self.engine = DEFAULT_ENGINE if engine is None else engine
-        if self.engine not in ENGINE_KERNELS:
-            raise ValueError(f"unknown Equihash engine {self.engine!r}")
+                 groups: int | None = None, block: int = 1024, final_groups: int | None = None):
+        """`code_object`: path of an alternative build of equihash_ps.hip (tuning sweeps);
+        `groups` writers (workgroups) per instance per round, by default so that groups x
+        instances = 256 (one 1024-thread workgroup per CU)."""
+        runtime.require_gpu()
+        self.h = runtime.hip()
         # writers per instance: one 1024-thread workgroup per CU over the whole launch (P x
         # instances = 256: 32 at 8 instances, 16 at the mining window's 16; profiles/README r4k:
         # 8.50 vs 8.65 ms at 16 instances, and 7.48 vs 4.38 ms when P=16 leaves half the CUs idle at 8)
-        runtime.require_gpu()
-        self.h = runtime.hip()
-        cb = self.engine == "cb"
-        cap = self.h.EQC_MAX_P if cb else 256
-        self.groups = int(groups) if groups else min(cap, max(16, 1 << max(0, (256 // max(1, int(num_inst))).bit_length() - 1)))
-        self.block = int(block)  # threads per workgroup, must match the code object's EQP_BLOCK / EQC_BLOCK
-        # cb: coarse buckets per level (the code object's EQC_COARSE_BITS; other bits for sweeps)
-        self.coarse = 1 << int(coarse_bits) if coarse_bits else self.h.EQC_COARSE
-        # final round (writes no level, so any width works): ps ~4096 workgroups over the launch
-        # (256 at 16 instances: -1 % against 1024, r4k); cb one workgroup per coarse bucket at most
-        fg = int(final_groups or os.environ.get("NODEXA_EQP_FINAL_GROUPS", 0) or 0)
-        self.final_groups = fg or (self.coarse if cb else min(1024, max(64, 4096 // max(1, int(num_inst)))))
+        self.groups = int(groups) if groups else min(256, max(16, 1 << max(0, (256 // max(1, int(num_inst))).bit_length() - 1)))
+        self.block = int(block)  # threads per workgroup, must match the code object's EQP_BLOCK
+        # final round (writes no level, so any width works): ~4096 workgroups over the launch
+        # (256 at 16 instances: -1 % against 1024, r4k)
+        self.final_groups = int(final_groups or 0) or min(1024, max(64, 4096 // max(1, int(num_inst))))
         self.num_inst = int(num_inst)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else int(device))
         self.params = _core.EquihashParams(200, 9)
         B, L = self.h.EQ_BUCKETS, self.h.EQ_LEVELS
         ni = self.num_inst
-        module, names = ENGINE_KERNELS[self.engine]
         with torch.cuda.device(self.device):
             if code_object is None:
-                self.kernels = [runtime.static_kernel(module, k) for k in names]
+                self.kernels = [runtime.static_kernel("equihash_ps", k) for k in KERNELS]
             else:
                 co = runtime.load_code_object(code_object)
-                self.kernels = [co.function(k) for k in names]
-            if cb:
-                D, Wd = self.coarse, self.h.EQC_ROW_WORDS
-                # rows per (coarse bucket, writer) segment: mean m = 2^21 / D / P (level sizes run
-                # up to ~4 % above 2^21) + 8 sigma, so an overflow (a host re-solve) stays ~1e-12
-                m = (1 << 21) / D / self.groups
-                self.seg = int(m * 1.04 + 8 * m ** 0.5 + 8)
-                self.hashes = torch.empty(2 * ni * D * self.groups * self.seg * Wd, dtype=torch.int32,
-                                          device=self.device)
-                self.refs = torch.empty(ni * L * B * self.h.EQP_REF_STRIDE, dtype=torch.int32, device=self.device)
-                self.counts = torch.empty(ni * L * self.groups * D, dtype=torch.int16, device=self.device)
-            else:
-                S, R, W = self.h.EQP_SLOTS, self.h.EQP_REF_STRIDE, self.h.EQ_WORDS
-                self.hashes = torch.empty(2 * ni * B * S * W, dtype=torch.int32, device=self.device)
-                self.refs = torch.empty(ni * L * B * R, dtype=torch.int32, device=self.device)
-                self.counts = torch.empty(ni * L * self.groups * B, dtype=torch.uint8, device=self.device)
+                self.kernels = [co.function(k) for k in KERNELS]
+            S, R, W = self.h.EQP_SLOTS, self.h.EQP_REF_STRIDE, self.h.EQ_WORDS
+            self.hashes = torch.empty(2 * ni * B * S * W, dtype=torch.int32, device=self.device)
+            self.refs = torch.empty(ni * L * B * R, dtype=torch.int32, device=self.device)
+            self.counts = torch.empty(ni * L * self.groups * B, dtype=torch.uint8, device=self.device)
             self.stats_buf = torch.zeros(ni * self.h.EQP_STATS, dtype=torch.int32, device=self.device)
             self.cands = torch.empty(ni * (1 + 2 * self.h.EQ_MAX_CAND), dtype=torch.int32, device=self.device)
             self.sols = torch.empty(ni * (1 + self.h.EQ_MAX_SOL * 512), dtype=torch.int32, device=self.device)
@@ -189,18 +165,10 @@ class EquihashSolver:
             stage.copy_(torch.frombuffer(buf, dtype=torch.int64))
             self.msgs.copy_(stage, non_blocking=True)
             s = runtime.current_stream_handle() if stream is None else stream
-            if self.engine == "cb":
-                self.h.launch_equihash_cb_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
-                                                self.num_inst, self.groups, self.seg, self.hashes.data_ptr(),
-                                                self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
-                                                self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block,
-                                                self.final_groups, self.coarse)
-            else:
-                self.h.launch_equihash_ps_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len,
-                                                self.num_inst, self.groups, self.hashes.data_ptr(),
-                                                self.refs.data_ptr(), self.counts.data_ptr(), self.cands.data_ptr(),
-                                                self.sols.data_ptr(), self.stats_buf.data_ptr(), s, self.block,
-                                                self.final_groups)
+            self.h.launch_equihash_ps_solve(self.kernels, self.h0, self.msgs.data_ptr(), self.input_len, self.num_inst,
+                                            self.groups, self.hashes.data_ptr(), self.refs.data_ptr(),
+                                            self.counts.data_ptr(), self.cands.data_ptr(), self.sols.data_ptr(),
+                                            self.stats_buf.data_ptr(), s, self.block, self.final_groups)
             self.h.launch_equihash_verify_slots(self.verify_kernel, self.h0, self.msgs.data_ptr(), self.input_len,
                                                 self.num_inst, self.sols.data_ptr(), self.verdicts.data_ptr(), s)
             land = self._landing[self._next]
@@ -282,9 +250,8 @@ class EquihashSolver:
 
     def stats(self) -> dict:
         """Per-level fill of the last solve (instance 0) — overflow diagnostics."""
-        L = self.h.EQ_LEVELS
-        D = self.coarse if self.engine == "cb" else self.h.EQ_BUCKETS
-        c = self.counts[: L * self.groups * D].view(L, self.groups, D).to(torch.int32).sum(1).cpu()
+        B, L = self.h.EQ_BUCKETS, self.h.EQ_LEVELS
+        c = self.counts[: L * self.groups * B].view(L, self.groups, B).to(torch.int32).sum(1).cpu()
         dropped = self.stats_buf[: self.h.EQP_STATS].cpu().tolist()
         return {"rows_per_level": [int(x) for x in c.sum(1)], "max_fill": [int(x) for x in c.max(1).values],
                 "cap": self.h.EQP_STAGE, "dropped_per_level": dropped[:L],

@@ -10,7 +10,7 @@ rows in one parallel pass) crosses the PCIe bus twice in total:
   host  -> device  one copy: rows | kinds | DGW ancestor series | Equihash messages, solutions
                    and serialized headers (one pinned staging buffer)
   device           kawpow_mixonly_batch (SHA256d header hash + mix-only final + nBits boundary),
-                   hb_jobs, kawpow_verify_dag per epoch range (resident DAG, per-epoch program
+                   hb_jobs, kawpow_verify_waves per epoch range (resident DAG, per-epoch program
                    table resident too; the ranges side by side on their own streams), hb_verdict;
                    beside that chain eq_verify + sha256d_batch and dgw_batch on a side stream;
                    then hb_eq_scatter — ordered by events, no host synchronisation in between
@@ -22,7 +22,6 @@ compact results are all-gathered device to device (RCCL) before the single copy 
 """
 from __future__ import annotations
 
-import os
 import time
 
 import numpy as np
@@ -35,9 +34,10 @@ _core = core()
 ROW = 128
 CODES = {1: "invalid-mix-hash", 2: "high-hash", 3: "invalid-solution"}
 _ALIGN = 256
-# full hashes with wave-uniform programs (kawpow_verify_waves: mix in VGPRs) instead of the
-# LDS-mix interpreter (kawpow_verify_dag); NODEXA_VERIFY_WAVES=0 selects the latter
-WAVES = os.environ.get("NODEXA_VERIFY_WAVES", "1") != "0"
+# full hashes with wave-uniform programs (kawpow_verify_waves: program in SGPRs, mix in VGPRs);
+# test hook only: False runs the LDS-mix interpreter (kawpow_verify_dag), the bit-exactness oracle
+# of tests/test_gpu_resident_verify.py
+WAVES = True
 
 
 def _al(x: int) -> int:

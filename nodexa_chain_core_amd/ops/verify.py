@@ -122,7 +122,7 @@ def _grouped(jobs: np.ndarray, device):
 def _run_dag(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
     """Resident-DAG batch: one job per 16-lane group, headers of thousands of different periods in
     one dense launch. kawpow_verify_waves (jobs grouped by period four to a wave64, the program
-    wave-uniform, the mix in VGPRs) unless NODEXA_VERIFY_WAVES=0 selects kawpow_verify_dag (each
+    wave-uniform, the mix in VGPRs) unless the test hook header_batch.WAVES selects kawpow_verify_dag (each
     group's program and mix in LDS)."""
     from . import header_batch as HB
 

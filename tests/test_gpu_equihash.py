@@ -4,15 +4,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["cb", "ps"])
-def solver(gpu, request):
-    """Both engines: coarse buckets + pair log (equihash_cb.hip) and private slot segments
-    (equihash_ps.hip)."""
+@pytest.fixture(scope="module")
+def solver(gpu):
+    """The private-slot solver (equihash_ps.hip)."""
     import torch
 
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
-    s = EquihashSolver(num_inst=4, device=0, engine=request.param)
+    s = EquihashSolver(num_inst=4, device=0)
     yield s
     del s
     torch.cuda.empty_cache()
@@ -45,16 +44,15 @@ def test_gpu_solutions_valid_and_match_cpu(core, solver):
     assert total_gpu >= total_cpu - 1  # bucket-capacity drops may lose at most a rare solution
 
 
-@pytest.mark.parametrize("engine", ["cb", "ps"])
-def test_solver_exactly_matches_cpu_on_16_inputs(core, gpu, engine):
-    """Both engines are lossless: every device-side cap (segment, staging, chain, candidate, pair
-    id) is counted per instance and a counted instance is re-solved on the golden solver, so the
-    solution sets equal the CPU solver's on every input — and no instance needed that here."""
+def test_solver_exactly_matches_cpu_on_16_inputs(core, gpu):
+    """The solver is lossless: every device-side cap (segment, staging, chain, candidate) is
+    counted per instance and a counted instance is re-solved on the golden solver, so the solution
+    sets equal the CPU solver's on every input — and no instance needed that here."""
     import torch
 
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
-    s = EquihashSolver(num_inst=8, device=0, engine=engine)
+    s = EquihashSolver(num_inst=8, device=0)
     p = core.EquihashParams(200, 9)
     inputs = [bytes([0x5A]) * 80 + i.to_bytes(32, "little") for i in range(16)]
     gpu = s.solve(inputs[:8]) + s.solve(inputs[8:])

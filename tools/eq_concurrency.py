@@ -34,7 +34,7 @@ def main() -> int:
     base = bytes(range(108))
 
     def run(inst, groups, nsolv, tag):
-        solvers = [EquihashSolver(num_inst=inst, device=0, engine="ps", groups=groups) for _ in range(nsolv)]
+        solvers = [EquihashSolver(num_inst=inst, device=0, groups=groups) for _ in range(nsolv)]
         streams = [torch.cuda.Stream() for _ in range(nsolv)]
         mk = lambda s, i, j: base + struct.pack("<I", (tag << 24) ^ (s << 20) ^ (i << 8) ^ j)  # noqa: E731
         for s, (sv, st) in enumerate(zip(solvers, streams)):  # warm-up

@@ -19,7 +19,7 @@ def main() -> int:
     hdr = BlockHeader(version=0x20000000, prev=_core.sha256d(b"nodexa-bench-prev"),
                       merkle_root=_core.sha256d(b"nodexa-bench-merkle"), time=1_700_000_000,
                       bits=0x1b00ffff, height=384 * 7500 + 123)
-    s = EquihashSolver(num_inst=8, device=0, engine="ps")
+    s = EquihashSolver(num_inst=8, device=0)
     t0 = time.time()
     n = 0
     for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 24):

@@ -25,7 +25,7 @@ def main() -> int:
     from nodexa_chain_core_amd.ops.equihash import EquihashSolver
 
     defines = tuple(x for x in a.variant.split(",") if x)
-    s = EquihashSolver(num_inst=a.inst, engine="ps", code_object=variant_object(defines, "equihash_ps.hip"))
+    s = EquihashSolver(num_inst=a.inst, code_object=variant_object(defines, "equihash_ps.hip"))
     s.hashes.zero_()
     for k in range(a.launches):
         s.launch([bytes([k, j]) * 56 for j in range(a.inst)])

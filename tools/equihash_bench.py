@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Equihash(200,9) GPU solver timing: device-only time per batch (hip events),
-solutions per solve and host verification cost, for both engines and compile-time variants of
-their .hip sources, interleaved in one process.
+solutions per solve and host verification cost, for solver shapes and compile-time variants of
+equihash_ps.hip, interleaved in one process.
 
-    python tools/equihash_bench.py --inst 16 --engines cb ps --variants "" EQC_BATCH=4
-    python tools/equihash_bench.py --compile-only --engines cb --variants EQC_BATCH=4   # on the build host
+    python tools/equihash_bench.py --inst 16 --engines ps ps:32 --variants "" EQP_NP=384
+    python tools/equihash_bench.py --compile-only --variants EQP_NP=384   # on the build host
 
-Engines: "cb[:groups[:block[:final_groups]]]" (equihash_cb.hip) and "ps[:...]" (equihash_ps.hip).
-Variants are built to .kernel_cache/<source>_<tag>.hsaco (hipcc --genco).
+Shapes: "ps[:groups[:block[:final_groups]]]". Variants are built to
+.kernel_cache/equihash_ps_<tag>.hsaco (hipcc --genco).
 """
 from __future__ import annotations
 
@@ -39,7 +39,7 @@ def variant_object(defines: tuple[str, ...], source: str = "equihash.hip") -> st
     return out
 
 
-SOURCES = {"cb": "equihash_cb.hip", "ps": "equihash_ps.hip"}
+SOURCES = {"ps": "equihash_ps.hip"}
 
 
 def main() -> int:
@@ -48,7 +48,7 @@ def main() -> int:
     ap.add_argument("--batches", type=int, default=5)
     ap.add_argument("--variants", nargs="*", default=[""])
     ap.add_argument("--compile-only", action="store_true")
-    ap.add_argument("--engines", nargs="*", default=["cb"], help="cb|ps[:groups[:block[:final_groups]]]")
+    ap.add_argument("--engines", nargs="*", default=["ps"], help="ps[:groups[:block[:final_groups]]]")
     a = ap.parse_args()
     variants = [tuple(x for x in v.split(",") if x) for v in a.variants]
     kinds = sorted({e.split(":")[0] for e in a.engines})
@@ -67,10 +67,8 @@ def main() -> int:
         g = int(f[1]) if len(f) > 1 and f[1] else None  # None: the solver's own choice (P x instances = 256)
         blk = int(f[2]) if len(f) > 2 else 1024
         fin = int(f[3]) if len(f) > 3 else None
-        # a variant of another cb geometry (EQC_COARSE_BITS=<b>) runs with buffers sized for it
-        cbits = next((int(d.split("=")[1]) for d in c[1] if d.startswith("EQC_COARSE_BITS=")), None)
-        return EquihashSolver(num_inst=a.inst, device=0, engine=f[0], groups=g, block=blk,
-                              code_object=objs[(f[0], c[1])], final_groups=fin, coarse_bits=cbits)
+        return EquihashSolver(num_inst=a.inst, device=0, groups=g, block=blk, code_object=objs[(f[0], c[1])],
+                              final_groups=fin)
 
     solvers = {c: make(c) for c in cfgs}
     batches = [[os.urandom(112) for _ in range(a.inst)] for _ in range(a.batches + 1)]
