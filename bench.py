@@ -317,27 +317,29 @@ def main() -> int:
     svc = MiningService(dev, leader, window=max(block, args.batch // block * block))
     batch = svc.window
 
+    gpu_start = gpu_snapshot(world)  # before the warmup: amdsmi's first call is slow, keep it out of the loop
     svc.step()  # the work packet goes out (the loop starts idle)
     for _ in range(args.warmup):
         svc.step()
     sync()
     W.barrier()
     sync()
-    gpu_start = gpu_snapshot(world)
-    end0 = svc.last_end_ms
     t_start = time.perf_counter()
+    ends = []
     for _ in range(args.steps):
         svc.step()
+        ends.append(svc.last_end_ms)
     sync()
     W.barrier()
     elapsed = W.all_reduce_max(time.perf_counter() - t_start)
     gpu_end = gpu_snapshot(world)
     total = batch * ws * args.steps
     mhs = total / elapsed / 1e6
-    # the same windows on the device clock: the end of the last warmup window to the end of the last
-    # timed one (each step takes one window), i.e. the rate without the host's edges; slowest rank
-    dev_span = W.all_reduce_max(max(0.0, (svc.last_end_ms - end0) / 1e3))
-    kernel_mhs = total / dev_span / 1e6 if dev_span > 0 else None
+    # the same windows on the device clock: window ends 2..K of the timed steps (K - 2 windows; the
+    # first interval holds the pipeline's restart from the drained warmup), i.e. the steady-state
+    # rate without the host's edges; slowest rank
+    dev_span = W.all_reduce_max(max(0.0, (ends[-1] - ends[1]) / 1e3)) if args.steps > 2 else 0.0
+    kernel_mhs = batch * ws * (args.steps - 2) / dev_span / 1e6 if dev_span > 0 else None
     # stop every rank's loop (stop packet; the queued window is aborted), then drain
     if leader is not None:
         leader.shutdown()

@@ -268,6 +268,12 @@ typedef uint32_t kw_mix_t __attribute__((ext_vector_type(32)));
 NX_DEV uint32_t kw_get(const kw_mix_t& m, uint32_t i) { return m[i & 31]; }
 NX_DEV void kw_set(kw_mix_t& m, uint32_t i, uint32_t v) { m[i & 31] = v; }
 
+// kl_math / kl_merge with a wave-uniform kind lower to scalar branches. Branch-free VALU selects
+// (every candidate computed, v_cndmask on the kind) were measured slower: 586 against 458 us per
+// launch (profiles/README r5g), so the branches stay.
+#define kw_math kl_math
+#define kw_merge kl_merge
+
 extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(KawpowLightParams p) {
     __shared__ uint32_t l1[4096];
     for (int i = threadIdx.x; i < 4096; i += KL_BLOCK) l1[i] = p.l1[i];
@@ -338,19 +344,19 @@ extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(Kawpo
                 const uint32_t op = pw[i];
                 const uint32_t a = kw_get(mix, op);
                 const uint32_t dst = (op >> 8) & 31;
-                kw_set(mix, dst, kl_merge(kw_get(mix, dst), l1[a & 4095u], (op >> 16) & 3, op >> 24));
+                kw_set(mix, dst, kw_merge(kw_get(mix, dst), l1[a & 4095u], (op >> 16) & 3, op >> 24));
             }
             const uint32_t op = pw[11 + i];
             const uint32_t mg = pw[29 + i];
-            const uint32_t v = kl_math(kw_get(mix, op), kw_get(mix, op >> 8), (op >> 16) & 15);
+            const uint32_t v = kw_math(kw_get(mix, op), kw_get(mix, op >> 8), (op >> 16) & 15);
             const uint32_t dst = op >> 24;
-            kw_set(mix, dst, kl_merge(kw_get(mix, dst), v, mg & 3, mg >> 8));
+            kw_set(mix, dst, kw_merge(kw_get(mix, dst), v, mg & 3, mg >> 8));
         }
         const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t op = pw[47 + i];
-            kw_set(mix, op, kl_merge(kw_get(mix, op), dw[i], (op >> 8) & 3, op >> 16));
+            kw_set(mix, op, kw_merge(kw_get(mix, op), dw[i], (op >> 8) & 3, op >> 16));
         }
     }
     uint32_t lh = 0x811c9dc5u;
