@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "../store/bdb.hpp"
 #include "../store/chaindb.hpp"
 #include "../store/ldb.hpp"
 
@@ -83,6 +84,18 @@ void bind_store(py::module_& m) {
         .def_property_readonly("disk_bytes", &ldb::DB::disk_bytes)
         .def("close", &ldb::DB::close);
     m.def("ldb_destroy", &ldb::destroy);
+    m.def("bdb_read", [](const std::string& path, const std::string& subdb) {
+        bdb::Records recs;
+        {
+            py::gil_scoped_release nogil;
+            recs = bdb::read_btree(path, subdb);
+        }
+        py::list out;
+        for (const auto& [k, v] : recs) out.append(py::make_tuple(py::bytes(k), py::bytes(v)));
+        return out;
+    }, py::arg("path"), py::arg("subdb") = "main",
+       "Key/value records of a Berkeley DB btree file's sub-database (read-only; store/bdb.hpp)");
+    m.def("bdb_databases", &bdb::databases, "Sub-database names of a Berkeley DB btree file");
     m.def("ldb_crc32c", [](const py::bytes& b) {
         const std::string s = b;
         return ldb::crc32c(s.data(), s.size());

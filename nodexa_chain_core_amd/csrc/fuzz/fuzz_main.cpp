@@ -23,6 +23,7 @@
 #include "../crypto/secp256k1.hpp"
 #include "../pow/legacy_algos.hpp"
 #include "../pow/x16r.hpp"
+#include "../store/bdb.hpp"
 
 using namespace nodexa;
 
@@ -149,7 +150,7 @@ void fuzz_der(const Bytes& in) {
 extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     if (size == 0) return 0;
     const Bytes in(data + 1, data + size);
-    switch (data[0] % 13) {
+    switch (data[0] % 14) {
     case 0: fuzz_block(in, kKawpowAlways); break;
     case 1: fuzz_block(in, kKawpowNever); break;
     case 2: fuzz_header(in, kKawpowAlways); break;
@@ -177,6 +178,15 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         const size_t body = in.size() - 7, split = body ? in[6] % (body + 1) : 0;
         (void)lyra2_hash(in.data() + 7, split, in.data() + 7 + split, body - split, in[5], 1 + in[4] % 3,
                          u64(4) << (in[2] % 3), 1 + in[3] % 4, in[6] & 1);
+        break;
+    }
+    case 13: {
+        // a wallet.dat page walk (store/bdb.cpp): malformed pages must be refused, never read
+        // past the buffer, and a tree with cycles must end; the sub-database is "main" or none
+        try {
+            (void)bdb::read_btree_bytes(std::string(in.begin(), in.end()), in.size() & 1 ? "main" : "");
+        } catch (const std::runtime_error&) {
+        }
         break;
     }
     }

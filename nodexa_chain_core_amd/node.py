@@ -180,9 +180,13 @@ class Node:
                 # -bip44 (default on): a new wallet derives from BIP39 words (-mnemonic /
                 # -mnemonicpassphrase; the default wallet only)
                 first = not self.wallets
+                dat = self._reference_wallet_file(name, wpath)
                 w = Wallet(self.state, self.params, wpath, bip44=a.get_bool("bip44", True),
                            mnemonic=(a.get("mnemonic", "") or "") if first else "",
-                           mnemonic_passphrase=(a.get("mnemonicpassphrase", "") or "") if first else "")
+                           mnemonic_passphrase=(a.get("mnemonicpassphrase", "") or "") if first else "",
+                           import_from=dat)
+                if w.import_report is not None:
+                    log.log_printf(f"Imported reference wallet {dat} into {wpath}: {w.import_report}")
                 w.name = name
                 self.wallets[name] = w
                 rescan = hist_path is not None and not os.path.exists(hist_path) and bool(w.keys)
@@ -551,8 +555,24 @@ class Node:
         history, `<name without .json>_txs.json` (wallet.json -> wallet_txs.json)."""
         if not self.datadir:
             return None, None
+        if name.endswith(".dat"):  # -wallet=<name>.dat names a reference wallet: its JSON sits beside it
+            name = name[:-4] + ".json"
         stem = name[:-5] if name.endswith(".json") else name
         return os.path.join(self.datadir, name), os.path.join(self.datadir, stem + "_txs.json")
+
+    def _reference_wallet_file(self, name: str, wpath: str | None) -> str | None:
+        """The reference wallet.dat (Berkeley DB) to import for wallet `name` (wallet/walletdb.py):
+        <datadir>/wallet.dat for the default wallet, <datadir>/<name> for -wallet=<name>.dat; only
+        while no JSON wallet of that name exists."""
+        from .wallet.walletdb import is_bdb_file
+
+        if not self.datadir or wpath is None or os.path.exists(wpath):
+            return None
+        dat = "wallet.dat" if name == DEFAULT_WALLET else name if name.endswith(".dat") else None
+        if dat is None:
+            return None
+        path = os.path.join(self.datadir, dat)
+        return path if is_bdb_file(path) else None
 
     def resolve_wallet(self):
         """GetWalletForJSONRPCRequest + EnsureWalletIsAvailable (src/wallet/rpcwallet.cpp:40-78): the

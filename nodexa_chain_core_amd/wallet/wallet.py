@@ -1,6 +1,6 @@
 """Key wallet (the subset a mining / validating node uses).
 
-Parity (behaviour, not the BerkeleyDB format): CWallet key store and its RPCs in
+Parity (behaviour; a reference wallet.dat is imported once by wallet/walletdb.py): CWallet key store and its RPCs in
 src/wallet/rpcwallet.cpp (getnewaddress, getbalance, listunspent, sendtoaddress, sendmany,
 dumpprivkey / importprivkey, signrawtransaction, getwalletinfo), CKey::Sign + the standard
 signature producers of src/script/sign.cpp for P2PKH, P2PK, P2WPKH and P2SH-P2WPKH outputs, WIF
@@ -127,7 +127,7 @@ def multisig_script(m: int, pubkeys: list[bytes]) -> bytes:
 
 class Wallet:
     def __init__(self, state, params, path: str | None, bip44: bool = True, mnemonic: str = "",
-                 mnemonic_passphrase: str = ""):
+                 mnemonic_passphrase: str = "", import_from: str | None = None):
         self.state = state
         self.params = params
         self.path = path
@@ -158,8 +158,11 @@ class Wallet:
         self._master: bytes | None = None       # the master key while unlocked
         self._relock = None
         self.unlocked_until = 0
+        self.import_report: dict | None = None  # what import_from brought in (walletdb.py)
         if path and os.path.exists(path):
             self._load()
+        elif import_from:
+            self.import_report = self._import_reference(import_from)
         if self.hd is None and not self.keys:  # a new wallet is HD (CWallet::GenerateNewSeed)
             self._init_hd(bip44, mnemonic, mnemonic_passphrase)
 
@@ -213,11 +216,112 @@ class Wallet:
                        "mnemonic_passphrase": hd.get("mnemonic_passphrase"),
                        "mnemonic_crypted": bytes.fromhex(hd["mnemonic_crypted"]) if hd.get("mnemonic_crypted")
                        else None}
+            for f in ("seed_iv", "ref_words_crypted", "ref_pass_crypted"):  # an imported wallet.dat's
+                if hd.get(f) is not None:
+                    self.hd[f] = bytes.fromhex(hd[f])
         for rs in data.get("redeem_scripts", []):
             script = bytes.fromhex(rs)
             self.redeem_scripts[_core.hash160(script)] = script
         for wo in data.get("watch", []):
             self.watch[bytes.fromhex(wo["spk"])] = {"label": wo.get("label", ""), "solvable": wo.get("solvable", False)}
+
+    def _import_reference(self, dat_path: str) -> dict:
+        """A reference wallet.dat (wallet/walletdb.py) as this wallet: keys (plain or encrypted with
+        the reference's master key, which encrypts the same way, CCrypter), labels, key metadata,
+        the keypool, the HD chain with its counters and BIP39 data, redeem scripts and watch-only
+        scripts. Saved as JSON at once; the .dat file is only read."""
+        from .walletdb import read_wallet_dat
+
+        ref = read_wallet_dat(dat_path)
+        report = {"keys": 0, "crypted_keys": 0, "uncompressed_skipped": 0, "labels": 0, "pool": 0,
+                  "scripts": len(ref["cscripts"]), "watch": len(ref["watchs"]), "hd": None,
+                  "encrypted": bool(ref["mkeys"]), "version": ref["version"], "not_imported": ref["skipped"]}
+        if ref["mkeys"]:
+            mk = ref["mkeys"][min(ref["mkeys"])]  # CWallet::Unlock tries each; one is all encryptwallet writes
+            if mk["method"] != 0:
+                raise WalletError(f"wallet.dat master key derivation method {mk['method']} is not supported")
+            self.mkey = {"salt": mk["salt"], "rounds": mk["rounds"], "crypted": mk["crypted"]}
+        pubs: dict[bytes, bytes] = {}  # hash160 -> pub of every imported key
+        for pub, sec in ref["keys"].items():
+            if len(pub) != 33:
+                report["uncompressed_skipped"] += 1
+                continue
+            h = _core.hash160(pub)
+            self.keys[h] = (None if self.mkey is not None else sec, pub)
+            if self.mkey is not None:  # a plain key in an encrypted wallet (written before encryption)
+                raise WalletError("wallet.dat holds unencrypted keys beside a master key")
+            pubs[h] = pub
+            report["keys"] += 1
+        for pub, blob in ref["ckeys"].items():
+            if len(pub) != 33:
+                report["uncompressed_skipped"] += 1
+                continue
+            if self.mkey is None:
+                raise WalletError("wallet.dat holds encrypted keys but no master key")
+            h = _core.hash160(pub)
+            self.keys[h] = (None, pub)
+            self.crypted[h] = blob
+            pubs[h] = pub
+            report["crypted_keys"] += 1
+        for h in pubs:
+            self._p2sh_wpkh[_core.hash160(b"\x00\x14" + h)] = h
+            self.labels.setdefault(h, "")
+            self.created.setdefault(h, 0)
+        for pub, meta in ref["keymeta"].items():
+            h = _core.hash160(pub)
+            if h in pubs:
+                self.created[h] = meta["created"]
+                if meta["hdkeypath"] and meta["hdkeypath"] != "m":
+                    self.hdpath[h] = meta["hdkeypath"]
+        spk_label: dict[bytes, str] = {}
+        for addr, label in ref["names"].items():
+            spk = _core.address_to_script(addr, self.params.pubkey_prefix, self.params.script_prefix)
+            if spk is None:
+                continue
+            spk_label[bytes(spk)] = label
+            if len(spk) == 25 and spk[3:23] in pubs:
+                self.labels[spk[3:23]] = label
+                report["labels"] += 1
+        for idx in sorted(ref["pool"]):
+            h = _core.hash160(ref["pool"][idx]["pub"])
+            if h in pubs and h not in self.pool:
+                self.pool.append(h)
+                report["pool"] += 1
+        for h, script in ref["cscripts"].items():
+            self.redeem_scripts[_core.hash160(script)] = script
+        for script in ref["watchs"]:
+            self.watch[script] = {"label": spk_label.get(script, ""), "solvable": False}
+        hc = ref["hdchain"]
+        if hc is not None and hc["seed_id"] != bytes(20):
+            b39 = ref["bip39"]
+            hd = {"master_id": hc["seed_id"], "next": {"0": hc["external"], "1": hc["internal"]},
+                  "seed": None, "seed_crypted": None, "bip44": hc["bip44"], "mnemonic": None,
+                  "mnemonic_passphrase": None, "mnemonic_crypted": None}
+            if hc["bip44"]:  # the BIP39 seed (g_vchSeed) and words, IV = the word hash
+                if "bip39vchseed" in b39:
+                    hd["seed"] = b39["bip39vchseed"]
+                    hd["mnemonic"] = b39["bip39words"][1].decode() if "bip39words" in b39 else None
+                    hd["mnemonic_passphrase"] = b39.get("bip39passphrase", b"").decode()
+                elif "cbip39vchseed" in b39 and "cbip39words" in b39:
+                    word_hash, words_c = b39["cbip39words"]
+                    hd["seed_crypted"] = b39["cbip39vchseed"]
+                    hd["seed_iv"] = word_hash[:16]
+                    hd["ref_words_crypted"] = words_c
+                    hd["ref_pass_crypted"] = b39.get("cbip39passphrase", b"")
+                else:
+                    raise WalletError("wallet.dat: a BIP44 HD chain without its BIP39 seed")
+            else:  # the 0.15 layout: the seed is the wallet key whose hash160 is the seed id
+                if hc["seed_id"] not in pubs:
+                    raise WalletError("wallet.dat: HD seed key not found")
+                if self.mkey is None:
+                    hd["seed"] = self.keys[hc["seed_id"]][0]
+                else:
+                    hd["seed_crypted"] = self.crypted[hc["seed_id"]]
+                    hd["seed_iv"] = _iv(pubs[hc["seed_id"]])
+            self.hd = hd
+            report["hd"] = {"bip44": hc["bip44"], "external": hc["external"], "internal": hc["internal"]}
+        self._save()
+        return report
 
     def _save(self) -> None:
         if not self.path:
@@ -247,6 +351,9 @@ class Wallet:
                           "mnemonic_passphrase": self.hd.get("mnemonic_passphrase") if plain else None,
                           "mnemonic_crypted": self.hd["mnemonic_crypted"].hex() if self.hd.get("mnemonic_crypted")
                           else None}
+            for f in ("seed_iv", "ref_words_crypted", "ref_pass_crypted"):
+                if self.hd.get(f) is not None:
+                    data["hd"][f] = self.hd[f].hex()
         if self.mkey is not None:
             data["mkey"] = {"salt": self.mkey["salt"].hex(), "rounds": self.mkey["rounds"],
                             "crypted": self.mkey["crypted"].hex()}
@@ -444,7 +551,13 @@ class Wallet:
             for h, (_, pub) in list(self.keys.items()):
                 self.keys[h] = (_core.aes256_cbc_decrypt(master, _iv(pub), self.crypted[h]), pub)
             if self.hd is not None and self.hd.get("seed_crypted"):
-                self.hd["seed"] = _core.aes256_cbc_decrypt(master, _iv(b"hdseed"), self.hd["seed_crypted"])
+                iv = self.hd.get("seed_iv") or _iv(b"hdseed")
+                self.hd["seed"] = _core.aes256_cbc_decrypt(master, iv, self.hd["seed_crypted"])
+            if self.hd is not None and self.hd.get("ref_words_crypted"):  # imported: words, passphrase apart
+                iv = self.hd["seed_iv"]
+                self.hd["mnemonic"] = _core.aes256_cbc_decrypt(master, iv, self.hd["ref_words_crypted"]).decode()
+                pc = self.hd.get("ref_pass_crypted")
+                self.hd["mnemonic_passphrase"] = _core.aes256_cbc_decrypt(master, iv, pc).decode() if pc else ""
             if self.hd is not None and self.hd.get("mnemonic_crypted"):
                 m, pp = json.loads(_core.aes256_cbc_decrypt(master, _iv(b"bip39words"), self.hd["mnemonic_crypted"]))
                 self.hd["mnemonic"], self.hd["mnemonic_passphrase"] = m, pp
@@ -465,7 +578,7 @@ class Wallet:
                 self.keys[h] = (None, pub)
             if self.hd is not None:
                 self.hd["seed"] = None
-                if self.hd.get("mnemonic_crypted"):
+                if self.hd.get("mnemonic_crypted") or self.hd.get("ref_words_crypted"):
                     self.hd["mnemonic"] = self.hd["mnemonic_passphrase"] = None
             self.unlocked_until = 0
 

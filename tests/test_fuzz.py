@@ -4,7 +4,8 @@ deserializes 17 wire / disk types from fuzzer input).
 bin/fuzz_nodexa (csrc/fuzz/fuzz_main.cpp, libFuzzer + ASan + UBSan, host code only) runs a fixed
 number of mutations from a seed corpus of real encodings: the regtest / main genesis blocks in
 both header formats, KawPow testnet headers, a coinbase transaction, standard scripts, asset
-verifier strings, the fee-estimator / asset / index snapshots and a DER signature. A crash, a
+verifier strings, the fee-estimator / asset / index snapshots, a DER signature and a two-page
+Berkeley DB btree (the wallet.dat reader, store/bdb.cpp). A crash, a
 sanitizer report or a broken round-trip invariant fails the run."""
 import os
 import subprocess
@@ -41,7 +42,28 @@ def _seeds(core):
                                        "022046e1f2a3b4c5d6e7f8091a2b3c4d5e6f708192a3b4c5d6e7f8091a2b3c4d5e6f"))
     out.append(b"\x0b" + bytes(80))
     out.append(b"\x0c" + bytes([2, 4, 1, 3, 1, 32, 17]) + bytes(range(40)))
+    out.append(b"\x0d" + _bdb_seed())
     return out
+
+
+def _bdb_seed() -> bytes:
+    """A two-page Berkeley DB btree (512-byte pages): meta page, one leaf with one key/value."""
+    import struct
+
+    ps = 512
+    meta = bytearray(ps)
+    struct.pack_into("<III", meta, 12, 0x053162, 9, ps)
+    meta[25] = 9
+    struct.pack_into("<I", meta, 32, 1)   # last_pgno
+    struct.pack_into("<I", meta, 88, 1)   # root
+    leaf = bytearray(ps)
+    struct.pack_into("<IIIHH", leaf, 8, 1, 0, 0, 2, ps - 16)
+    leaf[24], leaf[25] = 1, 5
+    for i, (off, item) in enumerate(((ps - 8, b"key"), (ps - 16, b"value"))):
+        struct.pack_into("<H", leaf, 26 + 2 * i, off)
+        struct.pack_into("<HB", leaf, off, len(item), 1)
+        leaf[off + 3:off + 3 + len(item)] = item
+    return bytes(meta + leaf)
 
 
 def test_fuzz_native_core(core, tmp_path):
