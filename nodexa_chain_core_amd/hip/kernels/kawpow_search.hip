@@ -249,6 +249,7 @@ NX_DEV void kp_final(const uint32_t st2[8], const uint32_t digest[8], uint32_t o
 // their L1 word from `pf`, which the previous round filled between its program and its DAG merge
 // -- under the wait for its HBM gather instead of on this round's dependency chain.
 #define KP_PF_SLOTS (KP_PF_MAX > 0 ? KP_PF_MAX : 1)
+#define KP_EARLY_SLOTS (KP_EARLY > 0 ? KP_EARLY : 1)
 template <int J>
 NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], uint32_t (&pf)[KP_HASHES][KP_PF_SLOTS], kp_dag_t dag,
                        const FastMod32& items, const uint32_t* l1, uint32_t lane) {
@@ -262,8 +263,22 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], uint32_t (&pf)[KP_HASHES][
     // a third of the round's work waits behind a ~1 us HBM gather instead of hiding it.
     __builtin_amdgcn_sched_barrier(0);
 #endif
+    // KP_EARLY > 0: the first KP_EARLY lookups whose source no earlier op of the round writes are
+    // issued together as the round's first LDS reads (a fence keeps the scheduler from sinking
+    // them back next to their consumers, where each waits out its own LDS latency).
+    uint32_t early[KP_HASHES][KP_EARLY_SLOTS];
 #pragma unroll
-    for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM_PF(l1, mx[k], pf[k]);
+    for (int k = 0; k < KP_HASHES; ++k) {
+        early[k][0] = 0;
+#if KP_EARLY > 0
+        KAWPOW_EARLY(l1, mx[k], early[k]);
+#endif
+    }
+#if KP_EARLY > 0 && defined(KP_EARLY_FENCE)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+    for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM_PF(l1, mx[k], pf[k], early[k]);
 #ifdef KP_SCHED_FENCE
     __builtin_amdgcn_sched_barrier(0);
 #endif
