@@ -244,14 +244,8 @@ NX_DEV void kp_final(const uint32_t st2[8], const uint32_t digest[8], uint32_t o
 // digest words go to `own` of the lane that owns the hash (8 DPP broadcasts).
 // One ProgPoW round with the round index known mod 16 (J): the item index comes
 // from lane J of the row via DPP and the lane's 16-byte slice is lane ^ J.
-// KP_PF_MAX > 0 (cross-round lookahead, csrc/pow/kawpow_codegen.cpp): the first KP_PF_MAX cache
-// ops of the program whose source register is final when the previous round's program ends take
-// their L1 word from `pf`, which the previous round filled between its program and its DAG merge
-// -- under the wait for its HBM gather instead of on this round's dependency chain.
-#define KP_PF_SLOTS (KP_PF_MAX > 0 ? KP_PF_MAX : 1)
-#define KP_EARLY_SLOTS (KP_EARLY > 0 ? KP_EARLY : 1)
 template <int J>
-NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], uint32_t (&pf)[KP_HASHES][KP_PF_SLOTS], kp_dag_t dag,
+NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag,
                        const FastMod32& items, const uint32_t* l1, uint32_t lane) {
     uint4 d[KP_HASHES];
     const uint32_t part = lane ^ (uint32_t)J;
@@ -263,31 +257,10 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], uint32_t (&pf)[KP_HASHES][
     // a third of the round's work waits behind a ~1 us HBM gather instead of hiding it.
     __builtin_amdgcn_sched_barrier(0);
 #endif
-    // KP_EARLY > 0: the first KP_EARLY lookups whose source no earlier op of the round writes are
-    // issued together as the round's first LDS reads (a fence keeps the scheduler from sinking
-    // them back next to their consumers, where each waits out its own LDS latency).
-    uint32_t early[KP_HASHES][KP_EARLY_SLOTS];
 #pragma unroll
-    for (int k = 0; k < KP_HASHES; ++k) {
-        early[k][0] = 0;
-#if KP_EARLY > 0
-        KAWPOW_EARLY(l1, mx[k], early[k]);
-#endif
-    }
-#if KP_EARLY > 0 && defined(KP_EARLY_FENCE)
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-#pragma unroll
-    for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM_PF(l1, mx[k], pf[k], early[k]);
+    for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PROGRAM(l1, mx[k]);
 #ifdef KP_SCHED_FENCE
     __builtin_amdgcn_sched_barrier(0);
-#endif
-#if KP_PF_MAX > 0
-#pragma unroll
-    for (int k = 0; k < KP_HASHES; ++k) KAWPOW_PREFETCH(l1, mx[k], pf[k]);  // the next round's lookahead
-#ifdef KP_SCHED_FENCE
-    __builtin_amdgcn_sched_barrier(0);  // issued before the merge's wait for the gather
-#endif
 #endif
 #pragma unroll
     for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
@@ -309,25 +282,17 @@ NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t
 #pragma unroll
             for (int i = 0; i < 32; ++i) mx[k][i] = rng.next();
         }
-        uint32_t pf[KP_HASHES][KP_PF_SLOTS];
-#pragma unroll
-        for (int k = 0; k < KP_HASHES; ++k) {
-            pf[k][0] = 0;
-#if KP_PF_MAX > 0
-            KAWPOW_PREFETCH(l1, mx[k], pf[k]);  // round 0's lookahead, from the initial mix
-#endif
-        }
         // 64 rounds = 4 x 16 with the round index mod 16 baked into each copy
 #pragma unroll 1
         for (uint32_t rr = 0; rr < 64; rr += 16) {
-            kp_round_c<0>(mx, pf, dag, items, l1, lane);   kp_round_c<1>(mx, pf, dag, items, l1, lane);
-            kp_round_c<2>(mx, pf, dag, items, l1, lane);   kp_round_c<3>(mx, pf, dag, items, l1, lane);
-            kp_round_c<4>(mx, pf, dag, items, l1, lane);   kp_round_c<5>(mx, pf, dag, items, l1, lane);
-            kp_round_c<6>(mx, pf, dag, items, l1, lane);   kp_round_c<7>(mx, pf, dag, items, l1, lane);
-            kp_round_c<8>(mx, pf, dag, items, l1, lane);   kp_round_c<9>(mx, pf, dag, items, l1, lane);
-            kp_round_c<10>(mx, pf, dag, items, l1, lane);  kp_round_c<11>(mx, pf, dag, items, l1, lane);
-            kp_round_c<12>(mx, pf, dag, items, l1, lane);  kp_round_c<13>(mx, pf, dag, items, l1, lane);
-            kp_round_c<14>(mx, pf, dag, items, l1, lane);  kp_round_c<15>(mx, pf, dag, items, l1, lane);
+            kp_round_c<0>(mx, dag, items, l1, lane);   kp_round_c<1>(mx, dag, items, l1, lane);
+            kp_round_c<2>(mx, dag, items, l1, lane);   kp_round_c<3>(mx, dag, items, l1, lane);
+            kp_round_c<4>(mx, dag, items, l1, lane);   kp_round_c<5>(mx, dag, items, l1, lane);
+            kp_round_c<6>(mx, dag, items, l1, lane);   kp_round_c<7>(mx, dag, items, l1, lane);
+            kp_round_c<8>(mx, dag, items, l1, lane);   kp_round_c<9>(mx, dag, items, l1, lane);
+            kp_round_c<10>(mx, dag, items, l1, lane);  kp_round_c<11>(mx, dag, items, l1, lane);
+            kp_round_c<12>(mx, dag, items, l1, lane);  kp_round_c<13>(mx, dag, items, l1, lane);
+            kp_round_c<14>(mx, dag, items, l1, lane);  kp_round_c<15>(mx, dag, items, l1, lane);
         }
 #pragma unroll
         for (int k = 0; k < KP_HASHES; ++k) {

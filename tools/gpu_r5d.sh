@@ -1,4 +1,5 @@
 #!/bin/bash
+# (KP_PF_MAX was removed in round 5 after this A/B: it lost; the code is at commit 65a1eaa)
 # r5d: KawPow cross-round lookahead (KP_PF_MAX: the first N cache ops whose source register is final
 # when the previous round's program ends read the L1 under that round's DAG wait), interleaved A/B,
 # every variant bit-exact over its share windows; the collective-stream dispatch probe while two

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (KP_EARLY was removed after this A/B: it lost; the code is at commit 65a1eaa)
 # r5h: KawPow in-round early issue (KP_EARLY=N: the first N L1 lookups whose source register no
 # earlier op of the round writes are issued together as the round's first LDS reads; the ISA goes
 # from 11 serialized ds_read -> s_waitcnt lgkmcnt(0) pairs to one batch plus the dependent ones),
