@@ -192,6 +192,24 @@ struct KawpowHashParams {
     struct FastMod32 items;
 };
 
+// Classic Ethash hashimoto over the resident DAG (ethash_hashimoto.hip): jobs are (header hash,
+// nonce) pairs (KawpowVerifyJob, block_number unused); out per job: mix[8] then final[8].
+struct EthashHashParams {
+    const void* dag;                  // full dataset (1024-bit pages = pairs of 512-bit items)
+    const struct KawpowVerifyJob* jobs;
+    uint32_t* out;
+    uint32_t* seeds;                  // scratch: n x 16 words (keccak512 seeds, phase 1 -> 2, 3)
+    uint32_t num_jobs;
+    uint32_t max_hits;                // search: capacity of hits[1..]
+    struct FastMod32 pages;           // modulo by the number of 1024-bit pages (full_items)
+    // search mode (jobs == nullptr): job i hashes (header, start_nonce + i); with `hits`, the final
+    // kernel appends i for every final <= boundary (both big-endian byte strings, 8 words each)
+    uint32_t header[8];
+    uint64_t start_nonce;
+    uint32_t boundary[8];
+    uint32_t* hits;                   // [0] = count, [1..max_hits] = job indices
+};
+
 // Batch SHA-256d (sha256d.hip). sha256d_batch: n messages of len bytes, stride bytes apart.
 // sha256d_merkle_level: n output nodes from len 32-byte input nodes (stride unused).
 // Mix-only batch header check (K4 + K6, sha256d.hip: kawpow_mixonly_batch), one lane per header:

@@ -311,6 +311,53 @@ PYBIND11_MODULE(_hip, m) {
         if (grid == 0) return;
         k.launch_bytes(dim3(grid), dim3(block), 0, as_stream(stream), &p, sizeof(p));
     });
+    // Classic Ethash hashimoto (ethash_hashimoto.hip): seed -> mix (per_row jobs per 16-lane row,
+    // 16 rows per block) -> final, in order on one stream; `seeds` holds n x 64 bytes. Search mode
+    // (search_header given, jobs ignored): job i is (header, start_nonce + i); with a boundary, the
+    // final kernel appends every job whose final hash is <= it to `hits` ([0] count, then indices).
+    m.def("launch_ethash_hash_batch", [](const Kernel& k_seed, const Kernel& k_mix, const Kernel& k_final,
+                                         uintptr_t dag, uint32_t full_items, uintptr_t jobs, uint32_t num_jobs,
+                                         uintptr_t out, uintptr_t seeds, uintptr_t stream, uint32_t per_row,
+                                         const std::string& search_header, uint64_t start_nonce,
+                                         const std::string& search_boundary, uintptr_t hits, uint32_t max_hits) {
+        // per_row: the mix kernel's hashes per 16-lane row (EH_HASHES, ops/ethash.EH_HASHES)
+        if (num_jobs == 0) return;
+        if (per_row == 0 || per_row > 16) throw std::invalid_argument("hashes per row in 1..16");
+        for (const Kernel* k : {&k_seed, &k_mix, &k_final})
+            if (k->max_threads < 256) throw std::invalid_argument("ethash hashimoto kernels need 256-thread blocks");
+        EthashHashParams p{};
+        p.dag = reinterpret_cast<const void*>(dag);
+        p.jobs = reinterpret_cast<const KawpowVerifyJob*>(jobs);
+        p.out = reinterpret_cast<uint32_t*>(out);
+        p.seeds = reinterpret_cast<uint32_t*>(seeds);
+        p.num_jobs = num_jobs;
+        p.pages = make_fastmod(full_items);
+        if (!search_header.empty() || !search_boundary.empty()) {
+            if (search_header.size() != 32 || (!search_boundary.empty() && search_boundary.size() != 32))
+                throw std::invalid_argument("search: 32-byte header hash and boundary");
+            if (!search_boundary.empty() && (hits == 0 || max_hits == 0))
+                throw std::invalid_argument("search: a hit buffer");
+            std::memcpy(p.header, search_header.data(), 32);
+            if (!search_boundary.empty()) {
+                std::memcpy(p.boundary, search_boundary.data(), 32);
+                p.hits = reinterpret_cast<uint32_t*>(hits);
+                p.max_hits = max_hits;
+            }
+            p.jobs = nullptr;
+            p.start_nonce = start_nonce;
+        } else if (jobs == 0) {
+            throw std::invalid_argument("jobs, or a search header");
+        }
+        const hipStream_t s = as_stream(stream);
+        const unsigned lanes_grid = (num_jobs + 255) / 256;
+        const unsigned per_block = 16 * per_row;
+        k_seed.launch_bytes(dim3(lanes_grid), dim3(256), 0, s, &p, sizeof(p));
+        k_mix.launch_bytes(dim3((num_jobs + per_block - 1) / per_block), dim3(256), 0, s, &p, sizeof(p));
+        k_final.launch_bytes(dim3(lanes_grid), dim3(256), 0, s, &p, sizeof(p));
+    }, py::arg("k_seed"), py::arg("k_mix"), py::arg("k_final"), py::arg("dag"), py::arg("full_items"), py::arg("jobs"),
+       py::arg("num_jobs"), py::arg("out"), py::arg("seeds"), py::arg("stream"), py::arg("per_row"),
+       py::arg("search_header") = std::string(), py::arg("start_nonce") = 0, py::arg("search_boundary") = std::string(),
+       py::arg("hits") = 0, py::arg("max_hits") = 0);
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
     m.attr("KV_PROG_WORDS") = KV_PROG_WORDS;
     m.def("launch_kawpow_verify_light", [](const Kernel& k, uintptr_t light, uint32_t light_items, uintptr_t l1,

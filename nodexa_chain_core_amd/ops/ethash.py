@@ -21,6 +21,8 @@ from ..utils.trace import traced
 # 512-bit items per launch: keeps a single dispatch well under a second even
 # at epoch 384 while still giving >> 256 CUs x 8 waves of work.
 _DAG_CHUNK = 1 << 22
+# hashes per 16-lane row of ethash_hash_batch (EH_HASHES in hip/kernels/ethash_hashimoto.hip)
+EH_HASHES = 2
 
 
 class DeviceEpoch:
@@ -100,3 +102,75 @@ class DeviceEpoch:
 
     def item512(self, index: int) -> bytes:
         return bytes(self.dag[index * 64:(index + 1) * 64].cpu().numpy().tobytes())
+
+    def hashimoto_batch(self, header_hashes: list[bytes], nonces: list[int], stream: int | None = None
+                        ) -> list[tuple[bytes, bytes]]:
+        """Classic Ethash (final_hash, mix_hash) of each (header hash, nonce) over this resident
+        DAG (hip/kernels/ethash_hashimoto.hip; ethash::hash, src/crypto/ethash/lib/ethash/
+        ethash.cpp:416-440), as `_core.ethash_hash` computes them on the host."""
+        import struct
+
+        if not self.built or self.dag is None:
+            raise RuntimeError("hashimoto_batch needs the built DAG")
+        n = len(nonces)
+        if n != len(header_hashes):
+            raise ValueError("one nonce per header hash")
+        if n == 0:
+            return []
+        job = struct.Struct("<8IQII")
+        buf = bytearray(job.size * n)
+        for i, (hh, nonce) in enumerate(zip(header_hashes, nonces)):
+            if len(hh) != 32:
+                raise ValueError("header hashes are 32 bytes")
+            job.pack_into(buf, i * job.size, *struct.unpack("<8I", hh), int(nonce), 0, 0)
+        h = runtime.hip()
+        ks = [runtime.static_kernel("ethash_hashimoto", f"ethash_{x}_batch") for x in ("seed", "mix", "final")]
+        with torch.cuda.device(self.device):
+            jobs = torch.frombuffer(buf, dtype=torch.uint8).to(self.device)
+            out = torch.empty(n * 16, dtype=torch.int32, device=self.device)
+            seeds = torch.empty(n * 16, dtype=torch.int32, device=self.device)
+            s = runtime.current_stream_handle() if stream is None else stream
+            h.launch_ethash_hash_batch(*ks, self.dag.data_ptr(), self.full_items, jobs.data_ptr(), n, out.data_ptr(),
+                                       seeds.data_ptr(), s, EH_HASHES)
+            raw = out.cpu().numpy().tobytes()
+        return [(raw[i * 64 + 32:i * 64 + 64], raw[i * 64:i * 64 + 32]) for i in range(n)]
+
+    def ethash_search(self, header_hash: bytes, boundary: bytes, start_nonce: int, iterations: int,
+                      window: int = 1 << 22) -> tuple[int, bytes, bytes] | None:
+        """ethash::search (src/crypto/ethash/lib/ethash/ethash.cpp:326-350): the first nonce in
+        [start_nonce, start_nonce + iterations) whose classic Ethash final hash is <= boundary, as
+        (nonce, final_hash, mix_hash), or None. Nonces run on the device in windows of `window`
+        (job i = start + i, no host-side job list); the final kernel appends each hit and the
+        lowest one of the first window that has any is the answer."""
+        if not self.built or self.dag is None:
+            raise RuntimeError("ethash_search needs the built DAG")
+        if len(header_hash) != 32 or len(boundary) != 32:
+            raise ValueError("32-byte header hash and boundary")
+        h = runtime.hip()
+        ks = [runtime.static_kernel("ethash_hashimoto", f"ethash_{x}_batch") for x in ("seed", "mix", "final")]
+        max_hits = 1024
+        with torch.cuda.device(self.device):
+            w = max(1, min(int(window), int(iterations)))
+            out = torch.empty(w * 16, dtype=torch.int32, device=self.device)
+            seeds = torch.empty(w * 16, dtype=torch.int32, device=self.device)
+            hits = torch.zeros(1 + max_hits, dtype=torch.int32, device=self.device)
+            s = runtime.current_stream_handle()
+            done = 0
+            while done < iterations:
+                n = min(w, iterations - done)
+                start = (int(start_nonce) + done) & 0xFFFFFFFFFFFFFFFF
+                hits.zero_()
+                h.launch_ethash_hash_batch(*ks, self.dag.data_ptr(), self.full_items, 0, n, out.data_ptr(),
+                                           seeds.data_ptr(), s, EH_HASHES, bytes(header_hash), start, bytes(boundary),
+                                           hits.data_ptr(), max_hits)
+                got = hits.cpu().numpy().view("<u4")
+                cnt = int(got[0])
+                if cnt:
+                    i = int(got[1:1 + min(cnt, max_hits)].min())
+                    if cnt > max_hits:  # the ring overflowed: the lowest hit may be past it
+                        raw = out[:n * 16].cpu().numpy().tobytes()
+                        i = next(j for j in range(n) if raw[j * 64 + 32:j * 64 + 64] <= boundary)
+                    row = out[i * 16:(i + 1) * 16].cpu().numpy().tobytes()
+                    return (start + i) & 0xFFFFFFFFFFFFFFFF, row[32:], row[:32]
+                done += n
+        return None

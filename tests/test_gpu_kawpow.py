@@ -69,6 +69,33 @@ def test_hash_batch_random_vs_cpu(core, epoch0):
 
 
 @pytest.mark.skipif(os.environ.get("NODEXA_FAST_GPU_TESTS") == "1", reason="multi-epoch DAG builds")
+def test_classic_hashimoto_batch_vs_cpu(core, epoch0):
+    """ethash_hashimoto.hip (classic Ethash over the resident DAG) against the host's ethash_hash
+    for random header hashes and nonces, plus a batch size that leaves a partial last block."""
+    rng = random.Random(11)
+    n = 37
+    hh = [rng.randbytes(32) for _ in range(n)]
+    nonces = [rng.getrandbits(64) for _ in range(n)]
+    nonces[0], hh[0] = 7, bytes(32)
+    got = epoch0.hashimoto_batch(hh, nonces)
+    for h, nonce, (f, m) in zip(hh, nonces, got):
+        assert (f, m) == core.ethash_hash(epoch0.ctx, h, nonce), nonce
+        assert core.ethash_verify(epoch0.ctx, h, m, nonce, f)
+
+
+def test_classic_ethash_search_vs_cpu(core, epoch0):
+    """ethash_search (device-side nonces and boundary check) returns the first nonce the host's
+    sequential ethash_hash loop finds, with its final and mix hashes; a boundary nothing meets in
+    the range returns None."""
+    hh = bytes(range(32))
+    boundary = bytes.fromhex("0f" + "ff" * 31)
+    got = epoch0.ethash_search(hh, boundary, 1000, 200, window=64)  # several windows
+    nonce = next(n for n in range(1000, 1200) if core.ethash_hash(epoch0.ctx, hh, n)[0] <= boundary)
+    f, m = core.ethash_hash(epoch0.ctx, hh, nonce)
+    assert got == (nonce, f, m)
+    assert epoch0.ethash_search(hh, bytes(32), 0, 300) is None
+
+
 def test_vectors_other_epochs(core, gpu):
     import torch
 
