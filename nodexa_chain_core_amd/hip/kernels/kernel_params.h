@@ -210,6 +210,18 @@ struct EthashHashParams {
     uint32_t* hits;                   // [0] = count, [1..max_hits] = job indices
 };
 
+// X16R / X16RV2 chain step on the GPU (x16r.hip): workgroup (x, slot) runs slot `blockIdx.y` over
+// its share of the headers whose step-`step` algorithm is that slot.
+struct X16rStepParams {
+    const uint8_t* headers;     // n x 80 bytes (the legacy header)
+    uint8_t* state;             // n x 64 bytes: the chain value, the final hash in its first 32
+    const uint8_t* v2;          // n flags: X16RV2 (Tiger pre-hash on slots 4, 6, 15)
+    const int32_t* order;       // this step's header indices grouped by slot
+    const int32_t* offsets;     // 17 entries: slot a owns order[offsets[a] .. offsets[a + 1])
+    uint32_t n;
+    uint32_t step;              // 0: hash the 80-byte header, else the 64-byte chain value
+};
+
 // Batch SHA-256d (sha256d.hip). sha256d_batch: n messages of len bytes, stride bytes apart.
 // sha256d_merkle_level: n output nodes from len 32-byte input nodes (stride unused).
 // Mix-only batch header check (K4 + K6, sha256d.hip: kawpow_mixonly_batch), one lane per header:

@@ -358,6 +358,23 @@ PYBIND11_MODULE(_hip, m) {
        py::arg("num_jobs"), py::arg("out"), py::arg("seeds"), py::arg("stream"), py::arg("per_row"),
        py::arg("search_header") = std::string(), py::arg("start_nonce") = 0, py::arg("search_boundary") = std::string(),
        py::arg("hits") = 0, py::arg("max_hits") = 0);
+    // X16R / X16RV2 chain step (x16r.hip): grid (ceil(max_group / 64), 16); group sizes from `offsets`
+    m.def("launch_x16r_step", [](const Kernel& k, uintptr_t headers, uintptr_t state, uintptr_t v2, uintptr_t order,
+                                 uintptr_t offsets, uint32_t n, uint32_t step, uint32_t max_group, uintptr_t stream) {
+        if (n == 0 || max_group == 0) return;
+        if (step > 15) throw std::invalid_argument("X16R has 16 steps");
+        if (max_group > n) throw std::invalid_argument("a slot group larger than the batch");
+        X16rStepParams p{};
+        p.headers = reinterpret_cast<const uint8_t*>(headers);
+        p.state = reinterpret_cast<uint8_t*>(state);
+        p.v2 = reinterpret_cast<const uint8_t*>(v2);
+        p.order = reinterpret_cast<const int32_t*>(order);
+        p.offsets = reinterpret_cast<const int32_t*>(offsets);
+        p.n = n;
+        p.step = step;
+        const unsigned block = unsigned(k.max_threads);
+        k.launch_bytes(dim3((max_group + block - 1) / block, 16), dim3(block), 0, as_stream(stream), &p, sizeof(p));
+    });
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
     m.attr("KV_PROG_WORDS") = KV_PROG_WORDS;
     m.def("launch_kawpow_verify_light", [](const Kernel& k, uintptr_t light, uint32_t light_items, uintptr_t l1,

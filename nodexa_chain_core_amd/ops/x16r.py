@@ -1,0 +1,62 @@
+"""Batch X16R / X16RV2 hashing of legacy (80-byte) headers on the GPU.
+
+Reference: HashX16R / HashX16RV2 (src/hash.h:335-605) hash one header at a time on the CPU, the
+16-step algorithm order taken from hashPrevBlock (GetHashSelection, src/hash.h:320-327). Here a
+whole batch advances one step per launch (hip/kernels/x16r.hip): the host groups the headers of
+each step by the slot they run, once for the batch (numpy over the 16 selection nibbles of every
+header), and the kernel's workgroup (x, slot) runs that slot over its group -- every wave executes
+one primitive. The 16 launches are queued on one stream with the chain values resident on the
+device; one copy brings the 32-byte hashes back.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import runtime
+
+
+def selections(headers: np.ndarray) -> np.ndarray:
+    """(n, 16) slot of each header at each step: nibble 48 + i of hashPrevBlock (header bytes
+    4..35, storage order), as x16r_selection on the host."""
+    prev = headers[:, 4:36]
+    out = np.empty((len(headers), 16), dtype=np.int32)
+    for i in range(16):
+        j = 63 - (48 + i)
+        byte = prev[:, j // 2]
+        out[:, i] = (byte >> 4) if j % 2 == 1 else (byte & 0x0F)
+    return out
+
+
+def x16r_hash_batch(headers: bytes | np.ndarray, v2: bool | np.ndarray = False, device: int = 0) -> np.ndarray:
+    """(n, 32) uint8 X16R (or, per header where `v2`, X16RV2) hashes of n 80-byte headers, in
+    uint256 storage order (as `_core.x16r` / `_core.x16rv2` return them)."""
+    runtime.require_gpu()
+    hdr = np.frombuffer(headers, dtype=np.uint8) if isinstance(headers, (bytes, bytearray)) else np.asarray(headers, np.uint8)
+    hdr = np.array(hdr.reshape(-1, 80), dtype=np.uint8, copy=True)  # writable, contiguous (torch.from_numpy)
+    n = len(hdr)
+    if n == 0:
+        return np.zeros((0, 32), dtype=np.uint8)
+    flags = np.broadcast_to(np.asarray(v2, dtype=np.uint8), (n,)).copy()
+    sel = selections(hdr)
+    order = np.empty((16, n), dtype=np.int32)
+    offsets = np.zeros((16, 17), dtype=np.int32)
+    for s in range(16):
+        order[s] = np.argsort(sel[:, s], kind="stable")
+        offsets[s, 1:] = np.cumsum(np.bincount(sel[:, s], minlength=16))
+    max_group = int(np.diff(offsets, axis=1).max())
+    h = runtime.hip()
+    k = runtime.static_kernel("x16r", "x16r_step")
+    dev = torch.device("cuda", device)
+    with torch.cuda.device(dev):
+        d_hdr = torch.from_numpy(hdr).to(dev, non_blocking=False)
+        d_flags = torch.from_numpy(flags).to(dev)
+        d_order = torch.from_numpy(order).to(dev)
+        d_off = torch.from_numpy(offsets).to(dev)
+        state = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        s = runtime.current_stream_handle()
+        for step in range(16):
+            h.launch_x16r_step(k, d_hdr.data_ptr(), state.data_ptr(), d_flags.data_ptr(),
+                               d_order.data_ptr() + step * n * 4, d_off.data_ptr() + step * 17 * 4, n, step,
+                               max_group, s)
+        return state[:, :32].cpu().numpy()
