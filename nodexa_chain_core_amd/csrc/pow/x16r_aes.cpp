@@ -62,52 +62,65 @@ void aes_round(u8 s[16], const u8* key) {
 }  // namespace
 
 // ================================================================ Groestl-512
-// 8 x 16 byte state (column-major), P1024 / Q1024 with 14 rounds each.
+// 16 columns of 8 bytes (u64, row i in byte i), P1024 / Q1024 with 14 rounds each. SubBytes,
+// ShiftBytes and MixBytes fold into eight 256 x u64 tables: T[k][x] is the column that byte x
+// in row k contributes after the S-box and the circulant circ(2,2,3,4,5,3,5,7), so a round is 8
+// lookups per output column (the tables are derived here from the S-box and GF(2^8)).
 namespace {
 
-void groestl_perm(u8 st[128], bool q) {
+struct GroestlTables {
+    u64 T[8][256];
+    GroestlTables() {
+        static const u8 kMix[8] = {2, 2, 3, 4, 5, 3, 5, 7};
+        const u8* S = aes_sbox();
+        for (int k = 0; k < 8; ++k)
+            for (int x = 0; x < 256; ++x) {
+                u64 v = 0;
+                for (int i = 0; i < 8; ++i) v |= u64(gmul(S[x], kMix[(k - i) & 7])) << (8 * i);
+                T[k][x] = v;
+            }
+    }
+};
+
+const GroestlTables& groestl_tables() {
+    static const GroestlTables t;
+    return t;
+}
+
+void groestl_perm(u64 st[16], bool q) {
     static const int kShiftP[8] = {0, 1, 2, 3, 4, 5, 6, 11};
     static const int kShiftQ[8] = {1, 3, 5, 11, 0, 2, 4, 6};
-    static const u8 kMix[8] = {2, 2, 3, 4, 5, 3, 5, 7};
-    const u8* S = aes_sbox();
+    const GroestlTables& G = groestl_tables();
     const int* sh = q ? kShiftQ : kShiftP;
-    u8 t[128];
+    u64 t[16];
     for (int r = 0; r < 14; ++r) {
-        // AddRoundConstant
+        for (int j = 0; j < 16; ++j)  // AddRoundConstant
+            st[j] ^= q ? ~(u64((j << 4) ^ r) << 56) : u64((j << 4) ^ r);
         for (int j = 0; j < 16; ++j) {
-            if (!q) {
-                st[8 * j] ^= u8((j << 4) ^ r);
-            } else {
-                for (int i = 0; i < 7; ++i) st[8 * j + i] ^= 0xFF;
-                st[8 * j + 7] ^= u8(0xFF ^ (j << 4) ^ r);
-            }
+            u64 v = 0;
+            for (int k = 0; k < 8; ++k) v ^= G.T[k][u8(st[(j + sh[k]) & 15] >> (8 * k))];
+            t[j] = v;
         }
-        // SubBytes + ShiftBytes: row i moves left by sh[i] columns
-        for (int j = 0; j < 16; ++j)
-            for (int i = 0; i < 8; ++i) t[8 * j + i] = S[st[8 * ((j + sh[i]) & 15) + i]];
-        // MixBytes: column times circ(2,2,3,4,5,3,5,7)
-        for (int j = 0; j < 16; ++j)
-            for (int i = 0; i < 8; ++i) {
-                u8 v = 0;
-                for (int k = 0; k < 8; ++k) v ^= gmul(t[8 * j + k], kMix[(k - i) & 7]);
-                st[8 * j + i] = v;
-            }
+        std::memcpy(st, t, sizeof t);
     }
 }
 
-void groestl_compress(u8 h[128], const u8 m[128]) {
-    u8 p[128], q[128];
-    for (int i = 0; i < 128; ++i) { p[i] = h[i] ^ m[i]; q[i] = m[i]; }
+void groestl_compress(u64 h[16], const u8 m[128]) {
+    u64 p[16], q[16];
+    for (int j = 0; j < 16; ++j) {
+        q[j] = load_le64(m + 8 * j);
+        p[j] = h[j] ^ q[j];
+    }
     groestl_perm(p, false);
     groestl_perm(q, true);
-    for (int i = 0; i < 128; ++i) h[i] ^= p[i] ^ q[i];
+    for (int j = 0; j < 16; ++j) h[j] ^= p[j] ^ q[j];
 }
 
 }  // namespace
 
 Hash512 groestl512(const u8* data, size_t n) {
-    u8 h[128] = {0};
-    h[126] = 0x02;  // output size 512, 64-bit big-endian at the end of the IV
+    u64 h[16] = {0};
+    h[15] = u64(0x02) << 48;  // output size 512, 64-bit big-endian at the end of the IV (byte 126)
     u64 blocks = 0;
     for (; n >= 128; n -= 128, data += 128, ++blocks) groestl_compress(h, data);
     u8 buf[256] = {0};
@@ -118,11 +131,11 @@ Hash512 groestl512(const u8* data, size_t n) {
     store_be64(buf + len - 8, blocks);
     groestl_compress(h, buf);
     if (len == 256) groestl_compress(h, buf + 128);
-    u8 x[128];
-    std::memcpy(x, h, 128);
+    u64 x[16];
+    std::memcpy(x, h, sizeof x);
     groestl_perm(x, false);
     Hash512 out;
-    for (int i = 0; i < 64; ++i) out.bytes[i] = x[64 + i] ^ h[64 + i];
+    for (int j = 0; j < 8; ++j) store_le64(out.bytes + 8 * j, x[8 + j] ^ h[8 + j]);
     return out;
 }
 

@@ -6,6 +6,8 @@
 // procedurally (JH: R6 iterated from the fractional bits of sqrt(2)).
 #include "x16r_prims.hpp"
 
+#include <stdexcept>
+
 namespace nodexa {
 
 // ================================================================ JH-512 (42 rounds)
@@ -53,27 +55,123 @@ struct JhConstants {
     }
 };
 
-void jh_e8(u8 H[128]) {
-    static const JhConstants k;
-    auto bit = [&](int i) { return (H[i >> 3] >> (7 - (i & 7))) & 1; };
-    u8 tmp[256], A[256];
-    for (int i = 0; i < 256; ++i)
-        tmp[i] = u8((bit(i) << 3) | (bit(i + 256) << 2) | (bit(i + 512) << 1) | bit(i + 768));
-    for (int i = 0; i < 128; ++i) {
-        A[2 * i] = tmp[i];
-        A[2 * i + 1] = tmp[i + 128];
-    }
-    for (int r = 0; r < 42; ++r) jh_round(A, 256, k.sel[r]);
-    for (int i = 0; i < 128; ++i) {
-        tmp[i] = A[2 * i];
-        tmp[i + 128] = A[2 * i + 1];
-    }
-    std::memset(H, 0, 128);
-    for (int i = 0; i < 256; ++i)
-        for (int b = 0; b < 4; ++b) {
-            const int pos = i + 256 * b;
-            H[pos >> 3] |= u8(((tmp[i] >> (3 - b)) & 1) << (7 - (pos & 7)));
+// Bit-sliced E8 (the JH submission's bitslice form, derived here from the element form above):
+// H is eight 128-bit words x0..x7 (16 bytes each). Element i < 128 of the grouping holds bits i of
+// x0, x2, x4, x6 (its bits 3..0); element i + 128 the same bits of x1, x3, x5, x7; element-form
+// pairs (A[2p], A[2p+1]) are position p of the even and the odd words. Then R8's S-box layer is
+// the 4-bit S-boxes evaluated bitwise (a ten-operation circuit, the round-constant mask picking
+// S1), L is eight word XORs, and P8 becomes, with the element order relabelled every
+// round, a swap of the odd words' positions p <-> p ^ 2^(r mod 7); after 42 rounds the relabelling
+// is the identity again. JhBitslice tracks that relabelling to place each round's constant bits
+// (and the construction is checked: the pairing, the final identity and the S-box circuit against
+// S0 / S1 are asserted).
+// S0 / S1 of four bit planes (m0 = element bit 3 .. m3 = bit 0), the round-constant mask cc
+// choosing S1: ten boolean operations per 64 elements.
+inline void jh_sbox(u64& m0, u64& m1, u64& m2, u64& m3, u64 cc) {
+    m3 = ~m3;
+    m0 ^= ~m2 & cc;
+    const u64 t0 = cc ^ (m0 & m1);
+    m0 ^= m2 & m3;
+    m3 ^= ~m1 & m2;
+    m1 ^= m0 & m2;
+    m2 ^= m0 & ~m3;
+    m0 ^= m1 | m3;
+    m3 ^= m1 & m2;
+    m1 ^= t0 & m0;
+    m2 ^= t0;
+}
+
+struct JhBitslice {
+    u64 c[42][2][2];   // round, word parity (even / odd words), 128-bit mask as (bytes 0-7, 8-15) LE
+    JhBitslice() {
+        static const JhConstants k;
+        int M[2][128];  // element index (element form, start of round r) of word parity g, position p
+        for (int g = 0; g < 2; ++g)
+            for (int p = 0; p < 128; ++p) M[g][p] = 2 * p + g;
+        auto p8 = [](int e) {
+            if (e % 4 == 2) e += 1;
+            else if (e % 4 == 3) e -= 1;
+            int i = e % 2 == 0 ? e / 2 : (e - 1) / 2 + 128;
+            return i >= 128 ? i ^ 1 : i;
+        };
+        for (int r = 0; r < 42; ++r) {
+            for (int g = 0; g < 2; ++g) {
+                c[r][g][0] = c[r][g][1] = 0;
+                for (int p = 0; p < 128; ++p) {
+                    if (g == 0 && (M[0][p] % 2 != 0 || M[1][p] != M[0][p] + 1))
+                        throw std::logic_error("JH bitslice: element pairing broken");
+                    if (k.sel[r][M[g][p]]) c[r][g][p >> 6] |= u64(1) << (8 * ((p >> 3) & 7) + 7 - (p & 7));
+                }
+            }
+            int n[2][128];
+            const int s = 1 << (r % 7);
+            for (int p = 0; p < 128; ++p) {
+                n[0][p] = p8(M[0][p]);
+                n[1][p ^ s] = p8(M[1][p]);
+            }
+            std::memcpy(M, n, sizeof M);
         }
+        for (int g = 0; g < 2; ++g)
+            for (int p = 0; p < 128; ++p)
+                if (M[g][p] != 2 * p + g) throw std::logic_error("JH bitslice: relabelling not the identity");
+        for (int cc = 0; cc < 2; ++cc)  // the bitsliced S-box circuit is S0 / S1 on every input
+            for (int x = 0; x < 16; ++x) {
+                u64 m0 = (x >> 3) & 1, m1 = (x >> 2) & 1, m2 = (x >> 1) & 1, m3 = x & 1;
+                jh_sbox(m0, m1, m2, m3, u64(cc));
+                if (int(((m0 & 1) << 3) | ((m1 & 1) << 2) | ((m2 & 1) << 1) | (m3 & 1)) != kJhS[cc][x])
+                    throw std::logic_error("JH bitslice: S-box circuit");
+            }
+    }
+};
+
+const JhBitslice& jh_bitslice() {
+    static const JhBitslice t;
+    return t;
+}
+
+// Swap positions p <-> p ^ 2^k of a 128-bit word (positions: byte p / 8, bit 7 - p % 8).
+inline void jh_swap(u64 w[2], int k) {
+    static const u64 kMask[6] = {0x5555555555555555ULL, 0x3333333333333333ULL, 0x0F0F0F0F0F0F0F0FULL,
+                                 0x00FF00FF00FF00FFULL, 0x0000FFFF0000FFFFULL, 0x00000000FFFFFFFFULL};
+    if (k == 6) {
+        std::swap(w[0], w[1]);
+        return;
+    }
+    // position bits 0-2 pick the bit in the byte (7 - p % 8: flipping bit k of p flips bit k of
+    // it), bits 3-5 the byte in the u64: either way p ^ 2^k is physical bit ^ 2^k
+    const int sh = 1 << k;
+    const u64 m = kMask[k];
+    for (int h = 0; h < 2; ++h) w[h] = ((w[h] & m) << sh) | ((w[h] >> sh) & m);
+}
+
+void jh_e8(u8 H[128]) {
+    const JhBitslice& B = jh_bitslice();
+    u64 x[8][2];
+    for (int j = 0; j < 8; ++j) {
+        x[j][0] = load_le64(H + 16 * j);
+        x[j][1] = load_le64(H + 16 * j + 8);
+    }
+    for (int r = 0; r < 42; ++r) {
+        for (int g = 0; g < 2; ++g)
+            for (int h = 0; h < 2; ++h) {
+                jh_sbox(x[g][h], x[2 + g][h], x[4 + g][h], x[6 + g][h], B.c[r][g][h]);
+            }
+        for (int h = 0; h < 2; ++h) {  // L: odd words ^= mul2(even words), then even ^= mul2(odd)
+            x[1][h] ^= x[2][h];
+            x[3][h] ^= x[4][h];
+            x[5][h] ^= x[6][h] ^ x[0][h];
+            x[7][h] ^= x[0][h];
+            x[0][h] ^= x[3][h];
+            x[2][h] ^= x[5][h];
+            x[4][h] ^= x[7][h] ^ x[1][h];
+            x[6][h] ^= x[1][h];
+        }
+        for (int j = 1; j < 8; j += 2) jh_swap(x[j], r % 7);
+    }
+    for (int j = 0; j < 8; ++j) {
+        store_le64(H + 16 * j, x[j][0]);
+        store_le64(H + 16 * j + 8, x[j][1]);
+    }
 }
 
 void jh_f8(u8 H[128], const u8 m[64]) {

@@ -7,8 +7,8 @@
 // into 32 x 8 message words; four rounds of eight Feistel steps over four
 // 8-word registers (IF for the first half of a round, MAJ for the second),
 // rotations (r, s) chained per round, lane permutations n -> n ^ c, and a
-// four-step feed-forward of the incoming chaining value. The transform is the
-// direct O(n^2) sum (header-chain verification, not a mining path).
+// four-step feed-forward of the incoming chaining value. The transform is a radix-2 NTT
+// (256 points, 8 stages).
 #include "x16r_prims.hpp"
 
 namespace nodexa {
@@ -57,12 +57,26 @@ struct SimdState {
 
 void simd_compress(u32 state[32], const u8 blk[128], bool last) {
     const SimdTables& T = simd_tables();
+    // y_i = sum_j blk[j] 41^(ij) mod 257 (the 128 bytes zero-extended to 256 points): radix-2
+    // decimation-in-time NTT, bit-reversed input, 8 stages of 128 butterflies
     int q[256];
+    for (int j = 0; j < 256; ++j) {
+        int r = 0;
+        for (int b = 0; b < 8; ++b) r |= ((j >> b) & 1) << (7 - b);
+        q[r] = j < 128 ? int(blk[j]) : 0;
+    }
+    for (int len = 2; len <= 256; len <<= 1) {
+        const int half = len / 2, stride = 256 / len;
+        for (int i = 0; i < 256; i += len)
+            for (int k = 0; k < half; ++k) {
+                const int u = q[i + k], v = q[i + k + half] * T.pw[stride * k] % 257;
+                q[i + k] = (u + v) % 257;
+                q[i + k + half] = (u - v + 257) % 257;
+            }
+    }
     const int* yoff = last ? T.yoff_f : T.yoff_n;
     for (int i = 0; i < 256; ++i) {
-        int acc = yoff[i];
-        for (int j = 0; j < 128; ++j) acc += int(blk[j]) * T.pw[(i * j) & 255];
-        acc %= 257;
+        const int acc = (q[i] + yoff[i]) % 257;
         q[i] = acc <= 128 ? acc : acc - 257;
     }
     // message words: 4 rounds x 8 steps x 8 lanes, from q pairs lifted by 185 / 233

@@ -213,100 +213,99 @@ X16R_FN void aes_round(u8 s[16], const u8* key) {
 }
 
 // ================================================================ Groestl-512 (slot 2)
+// 16 u64 columns (row i in byte i); SubBytes + ShiftBytes + MixBytes as 8 table lookups per column.
 constexpr int kGrShiftP[8] = {0, 1, 2, 3, 4, 5, 6, 11};
 constexpr int kGrShiftQ[8] = {1, 3, 5, 11, 0, 2, 4, 6};
-constexpr u8 kGrMix[8] = {2, 2, 3, 4, 5, 3, 5, 7};
 
-X16R_FN void groestl_perm(u8 st[128], bool q) {
+X16R_FN void groestl_perm(u64 st[16], bool q) {
     const int* sh = q ? kGrShiftQ : kGrShiftP;
-    u8 t[128];
+    u64 t[16];
     for (int r = 0; r < 14; ++r) {
+        for (int j = 0; j < 16; ++j) st[j] ^= q ? ~(u64((j << 4) ^ r) << 56) : u64((j << 4) ^ r);
         for (int j = 0; j < 16; ++j) {
-            if (!q) {
-                st[8 * j] ^= u8((j << 4) ^ r);
-            } else {
-                for (int i = 0; i < 7; ++i) st[8 * j + i] ^= 0xFF;
-                st[8 * j + 7] ^= u8(0xFF ^ (j << 4) ^ r);
-            }
+            u64 v = 0;
+            for (int k = 0; k < 8; ++k) v ^= kX16rGroestlT[256 * k + u8(st[(j + sh[k]) & 15] >> (8 * k))];
+            t[j] = v;
         }
-        for (int j = 0; j < 16; ++j)
-            for (int i = 0; i < 8; ++i) t[8 * j + i] = kX16rAesSbox[st[8 * ((j + sh[i]) & 15) + i]];
-        for (int j = 0; j < 16; ++j)
-            for (int i = 0; i < 8; ++i) {
-                u8 v = 0;
-                for (int k = 0; k < 8; ++k) v ^= gmul(t[8 * j + k], kGrMix[(k - i) & 7]);
-                st[8 * j + i] = v;
-            }
+        for (int j = 0; j < 16; ++j) st[j] = t[j];
     }
 }
 
-X16R_FN void groestl_compress(u8 h[128], const u8 m[128]) {
-    u8 p[128], q[128];
-    for (int i = 0; i < 128; ++i) { p[i] = h[i] ^ m[i]; q[i] = m[i]; }
-    groestl_perm(p, false);
-    groestl_perm(q, true);
-    for (int i = 0; i < 128; ++i) h[i] ^= p[i] ^ q[i];
-}
-
 X16R_FN void groestl512(const u8* data, int n, u8* out) {  // n < 120: one padded block
-    u8 h[128];
-    zero(h, 128);
-    h[126] = 0x02;
     u8 buf[128];
     zero(buf, 128);
     cpy(buf, data, n);
     buf[n] = 0x80;
     stb64(buf + 120, 1);
-    groestl_compress(h, buf);
-    u8 x[128];
-    cpy(x, h, 128);
-    groestl_perm(x, false);
-    for (int i = 0; i < 64; ++i) out[i] = x[64 + i] ^ h[64 + i];
+    u64 h[16], p[16], q[16];
+    for (int j = 0; j < 16; ++j) {
+        h[j] = j == 15 ? (u64(0x02) << 48) : 0;
+        q[j] = ld64(buf + 8 * j);
+        p[j] = h[j] ^ q[j];
+    }
+    groestl_perm(p, false);
+    groestl_perm(q, true);
+    for (int j = 0; j < 16; ++j) {
+        h[j] ^= p[j] ^ q[j];
+        p[j] = h[j];
+    }
+    groestl_perm(p, false);
+    for (int j = 0; j < 8; ++j) st64(out + 8 * j, p[8 + j] ^ h[8 + j]);
 }
 
 // ================================================================ JH-512 (slot 3)
-constexpr u8 kJhS[2][16] = {{9, 0, 4, 11, 13, 12, 3, 15, 1, 10, 2, 6, 7, 5, 8, 14},
-                            {3, 12, 6, 13, 5, 7, 1, 9, 15, 2, 0, 4, 11, 10, 14, 8}};
-X16R_FN u8 jh_mul2(u8 a) { return u8(((a << 1) ^ (a >> 3) ^ ((a >> 2) & 2)) & 0xF); }
-
-X16R_FN void jh_round(u8* x, int r) {  // R8 with the round's selector bits
-    u8 t[256];
-    const u8* sel = kX16rJhSel + 32 * r;
-    for (int i = 0; i < 256; ++i) t[i] = kJhS[(sel[i >> 3] >> (7 - (i & 7))) & 1][x[i]];
-    for (int i = 0; i < 256; i += 2) {
-        t[i + 1] ^= jh_mul2(t[i]);
-        t[i] ^= jh_mul2(t[i + 1]);
-    }
-    for (int i = 0; i < 256; i += 4) swp(t[i + 2], t[i + 3]);
-    for (int i = 0; i < 128; ++i) {
-        x[i] = t[2 * i];
-        x[i + 128] = t[2 * i + 1];
-    }
-    for (int i = 128; i < 256; i += 2) swp(x[i], x[i + 1]);
+// Bit-sliced E8 over eight 128-bit words (csrc/pow/x16r_bitslice.cpp derives the form and the
+// per-round constant masks kX16rJhC from the element-form specification).
+X16R_FN void jh_sbox(u64& m0, u64& m1, u64& m2, u64& m3, u64 cc) {
+    m3 = ~m3;
+    m0 ^= ~m2 & cc;
+    const u64 t0 = cc ^ (m0 & m1);
+    m0 ^= m2 & m3;
+    m3 ^= ~m1 & m2;
+    m1 ^= m0 & m2;
+    m2 ^= m0 & ~m3;
+    m0 ^= m1 | m3;
+    m3 ^= m1 & m2;
+    m1 ^= t0 & m0;
+    m2 ^= t0;
 }
+constexpr u64 kJhSwapMask[6] = {0x5555555555555555ULL, 0x3333333333333333ULL, 0x0F0F0F0F0F0F0F0FULL,
+                                0x00FF00FF00FF00FFULL, 0x0000FFFF0000FFFFULL, 0x00000000FFFFFFFFULL};
 
 X16R_FN void jh_e8(u8 H[128]) {
-    u8 tmp[256], A[256];
-    for (int i = 0; i < 256; ++i) {
-        const int b0 = (H[i >> 3] >> (7 - (i & 7))) & 1, b1 = (H[(i + 256) >> 3] >> (7 - (i & 7))) & 1;
-        const int b2 = (H[(i + 512) >> 3] >> (7 - (i & 7))) & 1, b3 = (H[(i + 768) >> 3] >> (7 - (i & 7))) & 1;
-        tmp[i] = u8((b0 << 3) | (b1 << 2) | (b2 << 1) | b3);
+    u64 x[8][2];
+    for (int j = 0; j < 8; ++j) {
+        x[j][0] = ld64(H + 16 * j);
+        x[j][1] = ld64(H + 16 * j + 8);
     }
-    for (int i = 0; i < 128; ++i) {
-        A[2 * i] = tmp[i];
-        A[2 * i + 1] = tmp[i + 128];
-    }
-    for (int r = 0; r < 42; ++r) jh_round(A, r);
-    for (int i = 0; i < 128; ++i) {
-        tmp[i] = A[2 * i];
-        tmp[i + 128] = A[2 * i + 1];
-    }
-    zero(H, 128);
-    for (int i = 0; i < 256; ++i)
-        for (int b = 0; b < 4; ++b) {
-            const int pos = i + 256 * b;
-            H[pos >> 3] |= u8(((tmp[i] >> (3 - b)) & 1) << (7 - (pos & 7)));
+    for (int r = 0; r < 42; ++r) {
+        for (int g = 0; g < 2; ++g)
+            for (int h = 0; h < 2; ++h) jh_sbox(x[g][h], x[2 + g][h], x[4 + g][h], x[6 + g][h], kX16rJhC[4 * r + 2 * g + h]);
+        for (int h = 0; h < 2; ++h) {
+            x[1][h] ^= x[2][h];
+            x[3][h] ^= x[4][h];
+            x[5][h] ^= x[6][h] ^ x[0][h];
+            x[7][h] ^= x[0][h];
+            x[0][h] ^= x[3][h];
+            x[2][h] ^= x[5][h];
+            x[4][h] ^= x[7][h] ^ x[1][h];
+            x[6][h] ^= x[1][h];
         }
+        const int k = r % 7;
+        for (int j = 1; j < 8; j += 2) {
+            if (k == 6) {
+                swp(x[j][0], x[j][1]);
+            } else {
+                const int sh = 1 << k;
+                const u64 m = kJhSwapMask[k];
+                for (int h = 0; h < 2; ++h) x[j][h] = ((x[j][h] & m) << sh) | ((x[j][h] >> sh) & m);
+            }
+        }
+    }
+    for (int j = 0; j < 8; ++j) {
+        st64(H + 16 * j, x[j][0]);
+        st64(H + 16 * j + 8, x[j][1]);
+    }
 }
 
 X16R_FN void jh_f8(u8 H[128], const u8 m[64]) {
@@ -655,12 +654,24 @@ X16R_FN void simd_step(u32 A[8], u32 B[8], u32 C[8], u32 D[8], const u32 w[8], i
 }
 
 X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last) {
-    int q[256];
+    int q[256];  // 256-point NTT over Z_257 (root 41), radix 2, bit-reversed input
+    for (int j = 0; j < 256; ++j) {
+        int r = 0;
+        for (int b = 0; b < 8; ++b) r |= ((j >> b) & 1) << (7 - b);
+        q[r] = j < 128 ? int(blk[j]) : 0;
+    }
+    for (int len = 2; len <= 256; len <<= 1) {
+        const int half = len / 2, stride = 256 / len;
+        for (int i = 0; i < 256; i += len)
+            for (int k = 0; k < half; ++k) {
+                const int u = q[i + k], v = q[i + k + half] * kX16rSimdPw[stride * k] % 257;
+                q[i + k] = (u + v) % 257;
+                q[i + k + half] = (u - v + 257) % 257;
+            }
+    }
     const int16_t* yoff = last ? kX16rSimdYf : kX16rSimdYn;
     for (int i = 0; i < 256; ++i) {
-        int acc = yoff[i];
-        for (int j = 0; j < 128; ++j) acc += int(blk[j]) * kX16rSimdPw[(i * j) & 255];
-        acc %= 257;
+        const int acc = (q[i] + yoff[i]) % 257;
         q[i] = acc <= 128 ? acc : acc - 257;
     }
     u32 A[8], B[8], C[8], D[8], saved[32];

@@ -358,22 +358,38 @@ PYBIND11_MODULE(_hip, m) {
        py::arg("num_jobs"), py::arg("out"), py::arg("seeds"), py::arg("stream"), py::arg("per_row"),
        py::arg("search_header") = std::string(), py::arg("start_nonce") = 0, py::arg("search_boundary") = std::string(),
        py::arg("hits") = 0, py::arg("max_hits") = 0);
-    // X16R / X16RV2 chain step (x16r.hip): grid (ceil(max_group / 64), 16); group sizes from `offsets`
-    m.def("launch_x16r_step", [](const Kernel& k, uintptr_t headers, uintptr_t state, uintptr_t v2, uintptr_t order,
-                                 uintptr_t offsets, uint32_t n, uint32_t step, uint32_t max_group, uintptr_t stream) {
-        if (n == 0 || max_group == 0) return;
-        if (step > 15) throw std::invalid_argument("X16R has 16 steps");
-        if (max_group > n) throw std::invalid_argument("a slot group larger than the batch");
+    // X16R / X16RV2 (x16r.hip): the 16 chain steps of a batch, each as one launch per slot group that
+    // has headers (x16r_step_<slot>, 64-thread blocks), all queued on `stream` by this one call.
+    // order: 16 x n header indices grouped by slot, offsets: 16 x 17 group bounds (device copies;
+    // offsets_host is the same table for the grid sizes).
+    m.def("launch_x16r_chain", [](const std::vector<const Kernel*>& slots, uintptr_t headers, uintptr_t state,
+                                  uintptr_t v2, uintptr_t order, uintptr_t offsets,
+                                  const std::vector<int32_t>& offsets_host, uint32_t n, uintptr_t stream) {
+        if (n == 0) return;
+        if (slots.size() != 16 || offsets_host.size() != 16 * 17) throw std::invalid_argument("16 slot kernels, 16 x 17 offsets");
+        for (int s = 0; s < 16; ++s)
+            for (int a = 0; a <= 16; ++a) {
+                const int32_t v = offsets_host[size_t(s * 17 + a)];
+                if (v < 0 || uint32_t(v) > n || (a && v < offsets_host[size_t(s * 17 + a - 1)]))
+                    throw std::invalid_argument("X16R offsets out of order");
+            }
         X16rStepParams p{};
         p.headers = reinterpret_cast<const uint8_t*>(headers);
         p.state = reinterpret_cast<uint8_t*>(state);
         p.v2 = reinterpret_cast<const uint8_t*>(v2);
-        p.order = reinterpret_cast<const int32_t*>(order);
-        p.offsets = reinterpret_cast<const int32_t*>(offsets);
         p.n = n;
-        p.step = step;
-        const unsigned block = unsigned(k.max_threads);
-        k.launch_bytes(dim3((max_group + block - 1) / block, 16), dim3(block), 0, as_stream(stream), &p, sizeof(p));
+        const hipStream_t st = as_stream(stream);
+        for (uint32_t s = 0; s < 16; ++s) {
+            p.step = s;
+            p.order = reinterpret_cast<const int32_t*>(order) + size_t(s) * n;
+            p.offsets = reinterpret_cast<const int32_t*>(offsets) + size_t(s) * 17;
+            for (int a = 0; a < 16; ++a) {
+                const uint32_t cnt = uint32_t(offsets_host[size_t(s * 17 + a + 1)] - offsets_host[size_t(s * 17 + a)]);
+                if (cnt == 0) continue;
+                const unsigned block = unsigned(slots[size_t(a)]->max_threads);
+                slots[size_t(a)]->launch_bytes(dim3((cnt + block - 1) / block), dim3(block), 0, st, &p, sizeof(p));
+            }
+        }
     });
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
     m.attr("KV_PROG_WORDS") = KV_PROG_WORDS;

@@ -4,9 +4,9 @@ Reference: HashX16R / HashX16RV2 (src/hash.h:335-605) hash one header at a time 
 16-step algorithm order taken from hashPrevBlock (GetHashSelection, src/hash.h:320-327). Here a
 whole batch advances one step per launch (hip/kernels/x16r.hip): the host groups the headers of
 each step by the slot they run, once for the batch (numpy over the 16 selection nibbles of every
-header), and the kernel's workgroup (x, slot) runs that slot over its group -- every wave executes
-one primitive. The 16 launches are queued on one stream with the chain values resident on the
-device; one copy brings the 32-byte hashes back.
+header), and each (step, slot) group runs that slot's kernel -- every wave executes one primitive.
+All launches (one per non-empty group, up to 256) are queued on one stream by one native call with
+the chain values resident on the device; one copy brings the 32-byte hashes back.
 """
 from __future__ import annotations
 
@@ -44,19 +44,15 @@ def x16r_hash_batch(headers: bytes | np.ndarray, v2: bool | np.ndarray = False, 
     for s in range(16):
         order[s] = np.argsort(sel[:, s], kind="stable")
         offsets[s, 1:] = np.cumsum(np.bincount(sel[:, s], minlength=16))
-    max_group = int(np.diff(offsets, axis=1).max())
     h = runtime.hip()
-    k = runtime.static_kernel("x16r", "x16r_step")
+    ks = [runtime.static_kernel("x16r", f"x16r_step_{a}") for a in range(16)]
     dev = torch.device("cuda", device)
     with torch.cuda.device(dev):
-        d_hdr = torch.from_numpy(hdr).to(dev, non_blocking=False)
+        d_hdr = torch.from_numpy(hdr).to(dev)
         d_flags = torch.from_numpy(flags).to(dev)
         d_order = torch.from_numpy(order).to(dev)
         d_off = torch.from_numpy(offsets).to(dev)
         state = torch.empty((n, 64), dtype=torch.uint8, device=dev)
-        s = runtime.current_stream_handle()
-        for step in range(16):
-            h.launch_x16r_step(k, d_hdr.data_ptr(), state.data_ptr(), d_flags.data_ptr(),
-                               d_order.data_ptr() + step * n * 4, d_off.data_ptr() + step * 17 * 4, n, step,
-                               max_group, s)
+        h.launch_x16r_chain(ks, d_hdr.data_ptr(), state.data_ptr(), d_flags.data_ptr(), d_order.data_ptr(),
+                            d_off.data_ptr(), offsets.reshape(-1).tolist(), n, runtime.current_stream_handle())
         return state[:, :32].cpu().numpy()
