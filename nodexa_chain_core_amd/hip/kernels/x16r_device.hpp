@@ -197,10 +197,10 @@ X16R_FN u8 gmul(u8 a, u8 b) {
     return r;
 }
 // One AES round on a 16-byte column-major block (key may be null).
-X16R_FN void aes_round(u8 s[16], const u8* key) {
+X16R_FN void aes_round(u8 s[16], const u8* key, const u8* sbox = kX16rAesSbox) {
     u8 t[16];
     for (int c = 0; c < 4; ++c)
-        for (int r = 0; r < 4; ++r) t[4 * c + r] = kX16rAesSbox[s[4 * ((c + r) & 3) + r]];
+        for (int r = 0; r < 4; ++r) t[4 * c + r] = sbox[s[4 * ((c + r) & 3) + r]];
     for (int c = 0; c < 4; ++c) {
         const u8 a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
         s[4 * c + 0] = u8(xtime(a0) ^ xtime(a1) ^ a1 ^ a2 ^ a3);
@@ -217,21 +217,21 @@ X16R_FN void aes_round(u8 s[16], const u8* key) {
 constexpr int kGrShiftP[8] = {0, 1, 2, 3, 4, 5, 6, 11};
 constexpr int kGrShiftQ[8] = {1, 3, 5, 11, 0, 2, 4, 6};
 
-X16R_FN void groestl_perm(u64 st[16], bool q) {
+X16R_FN void groestl_perm(u64 st[16], bool q, const u64* T) {
     const int* sh = q ? kGrShiftQ : kGrShiftP;
     u64 t[16];
     for (int r = 0; r < 14; ++r) {
         for (int j = 0; j < 16; ++j) st[j] ^= q ? ~(u64((j << 4) ^ r) << 56) : u64((j << 4) ^ r);
         for (int j = 0; j < 16; ++j) {
             u64 v = 0;
-            for (int k = 0; k < 8; ++k) v ^= kX16rGroestlT[256 * k + u8(st[(j + sh[k]) & 15] >> (8 * k))];
+            for (int k = 0; k < 8; ++k) v ^= T[256 * k + u8(st[(j + sh[k]) & 15] >> (8 * k))];
             t[j] = v;
         }
         for (int j = 0; j < 16; ++j) st[j] = t[j];
     }
 }
 
-X16R_FN void groestl512(const u8* data, int n, u8* out) {  // n < 120: one padded block
+X16R_FN void groestl512(const u8* data, int n, u8* out, const u64* T = kX16rGroestlT) {  // n < 120: one block
     u8 buf[128];
     zero(buf, 128);
     cpy(buf, data, n);
@@ -243,13 +243,13 @@ X16R_FN void groestl512(const u8* data, int n, u8* out) {  // n < 120: one padde
         q[j] = ld64(buf + 8 * j);
         p[j] = h[j] ^ q[j];
     }
-    groestl_perm(p, false);
-    groestl_perm(q, true);
+    groestl_perm(p, false, T);
+    groestl_perm(q, true, T);
     for (int j = 0; j < 16; ++j) {
         h[j] ^= p[j] ^ q[j];
         p[j] = h[j];
     }
-    groestl_perm(p, false);
+    groestl_perm(p, false, T);
     for (int j = 0; j < 8; ++j) st64(out + 8 * j, p[8 + j] ^ h[8 + j]);
 }
 
@@ -545,10 +545,10 @@ X16R_FN void cubehash512(const u8* data, int n, u8* out) {
 }
 
 // ================================================================ SHAvite-3-512 (slot 8)
-X16R_FN void aes_words(u32 x[4]) {
+X16R_FN void aes_words(u32 x[4], const u8* sbox) {
     u8 b[16];
     for (int i = 0; i < 4; ++i) st32(b + 4 * i, x[i]);
-    aes_round(b, nullptr);
+    aes_round(b, nullptr, sbox);
     for (int i = 0; i < 4; ++i) x[i] = ld32(b + 4 * i);
 }
 
@@ -556,25 +556,25 @@ X16R_FN void shavite_inject(u32* rk, int u, const u32 cnt[4], int a, int b, int 
     rk[u] ^= cnt[a]; rk[u + 1] ^= cnt[b]; rk[u + 2] ^= cnt[c]; rk[u + 3] ^= ~cnt[d];
 }
 
-X16R_FN void shavite_F(u32 L[4], const u32 R[4], const u32* rk, int& r_idx) {
+X16R_FN void shavite_F(u32 L[4], const u32 R[4], const u32* rk, int& r_idx, const u8* sbox) {
     u32 x[4];
     for (int k = 0; k < 4; ++k) x[k] = R[k] ^ rk[r_idx++];
-    aes_words(x);
+    aes_words(x, sbox);
     for (int j = 0; j < 3; ++j) {
         for (int k = 0; k < 4; ++k) x[k] ^= rk[r_idx++];
-        aes_words(x);
+        aes_words(x, sbox);
     }
     for (int k = 0; k < 4; ++k) L[k] ^= x[k];
 }
 
-X16R_FN void shavite_c512(u32 h[16], const u8 msg[128], const u32 cnt[4]) {
+X16R_FN void shavite_c512(u32 h[16], const u8 msg[128], const u32 cnt[4], const u8* sbox) {
     u32 rk[448];
     for (int i = 0; i < 32; ++i) rk[i] = ld32(msg + 4 * i);
     int u = 32;
     for (;;) {
         for (int s = 0; s < 8; ++s) {
             u32 x[4] = {rk[u - 31], rk[u - 30], rk[u - 29], rk[u - 32]};
-            aes_words(x);
+            aes_words(x, sbox);
             for (int k = 0; k < 4; ++k) rk[u + k] = x[k] ^ rk[u - 4 + k];
             if (u == 32) shavite_inject(rk, 32, cnt, 0, 1, 2, 3);
             else if (u == 164) shavite_inject(rk, 164, cnt, 3, 2, 1, 0);
@@ -591,8 +591,8 @@ X16R_FN void shavite_c512(u32 h[16], const u8 msg[128], const u32 cnt[4]) {
         for (int k = 0; k < 4; ++k) P[b][k] = h[4 * b + k];
     int r_idx = 0;
     for (int r = 0; r < 14; ++r) {
-        shavite_F(P[0], P[1], rk, r_idx);
-        shavite_F(P[2], P[3], rk, r_idx);
+        shavite_F(P[0], P[1], rk, r_idx, sbox);
+        shavite_F(P[2], P[3], rk, r_idx, sbox);
         u32 t[4];
         for (int k = 0; k < 4; ++k) {
             t[k] = P[3][k];
@@ -610,7 +610,7 @@ constexpr u32 kShaviteIV[16] = {0x72FCCDD8, 0x79CA4727, 0x128A077B, 0x40D55AEC, 
                                 0xB29F5CD1, 0xDF07FBFC, 0x8E45D73D, 0x681AB538, 0xBDE86578, 0xDD577E47,
                                 0xE275EADE, 0x502D9FCD, 0xB9357178, 0x022A4B9A};
 
-X16R_FN void shavite512(const u8* data, int n, u8* out) {  // 0 < n < 110: one padded block
+X16R_FN void shavite512(const u8* data, int n, u8* out, const u8* sbox = kX16rAesSbox) {  // 0 < n < 110
     u32 h[16];
     for (int i = 0; i < 16; ++i) h[i] = kShaviteIV[i];
     const u64 bits = u64(n) * 8;
@@ -622,7 +622,7 @@ X16R_FN void shavite512(const u8* data, int n, u8* out) {  // 0 < n < 110: one p
     for (int i = 0; i < 4; ++i) st32(buf + 110 + 4 * i, total[i]);
     buf[126] = 0x00;
     buf[127] = 0x02;
-    shavite_c512(h, buf, total);
+    shavite_c512(h, buf, total, sbox);
     for (int i = 0; i < 16; ++i) st32(out + 4 * i, h[i]);
 }
 
@@ -637,6 +637,13 @@ constexpr u32 kSimdIV[32] = {
     0xAC506643, 0xA90635A5, 0xE25B878B, 0xAAB7878F, 0x88817F7A, 0x0A02892B, 0x559A7550, 0x598F657E,
     0x7EEF60A1, 0x6B70E3E8, 0x9C1714D1, 0xB958E2A8, 0xAB02675E, 0xED1C014F, 0xCD8D65BB, 0xFDB7A257,
     0x09254899, 0xD699C7BC, 0x9019B6DC, 0x2B9022E4, 0x8FA14956, 0x21BF9BD3, 0xB94D0943, 0x6FFDDC22};
+
+// x mod 257 for 0 <= x <= 2^16 (every use here): 256 = -1 (mod 257), so x = 256 h + l = l - h.
+X16R_FN int mod257(int x) {
+    int r = (x & 255) - (x >> 8);
+    r += r < 0 ? 257 : 0;
+    return r >= 257 ? r - 257 : r;
+}
 
 X16R_FN u32 simd_inner(int lo, int hi, int mm) { return (u32(lo * mm) & 0xFFFFu) + (u32(hi * mm) << 16); }
 
@@ -653,26 +660,29 @@ X16R_FN void simd_step(u32 A[8], u32 B[8], u32 C[8], u32 D[8], const u32 w[8], i
     }
 }
 
-X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last) {
-    int q[256];  // 256-point NTT over Z_257 (root 41), radix 2, bit-reversed input
+// Q(i) is element i of the 256-entry NTT buffer `qb` spaced `qs` apart (the kernel interleaves the
+// buffers of a workgroup's lanes in LDS; the host self-check uses a local array, qs = 1).
+#define Q(i) qb[(i) * qs]
+X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t* qb, int qs) {
+    // 256-point NTT over Z_257 (root 41), radix 2, bit-reversed input
     for (int j = 0; j < 256; ++j) {
         int r = 0;
         for (int b = 0; b < 8; ++b) r |= ((j >> b) & 1) << (7 - b);
-        q[r] = j < 128 ? int(blk[j]) : 0;
+        Q(r) = int16_t(j < 128 ? int(blk[j]) : 0);
     }
     for (int len = 2; len <= 256; len <<= 1) {
         const int half = len / 2, stride = 256 / len;
         for (int i = 0; i < 256; i += len)
             for (int k = 0; k < half; ++k) {
-                const int u = q[i + k], v = q[i + k + half] * kX16rSimdPw[stride * k] % 257;
-                q[i + k] = (u + v) % 257;
-                q[i + k + half] = (u - v + 257) % 257;
+                const int u = Q(i + k), v = mod257(Q(i + k + half) * kX16rSimdPw[stride * k]);
+                Q(i + k) = int16_t(mod257(u + v));
+                Q(i + k + half) = int16_t(mod257(u - v + 257));
             }
     }
     const int16_t* yoff = last ? kX16rSimdYf : kX16rSimdYn;
     for (int i = 0; i < 256; ++i) {
-        const int acc = (q[i] + yoff[i]) % 257;
-        q[i] = acc <= 128 ? acc : acc - 257;
+        const int acc = mod257(Q(i) + yoff[i]);
+        Q(i) = int16_t(acc <= 128 ? acc : acc - 257);
     }
     u32 A[8], B[8], C[8], D[8], saved[32];
     for (int i = 0; i < 32; ++i) saved[i] = state[i];
@@ -682,20 +692,25 @@ X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last) {
         C[i] = state[16 + i] ^ ld32(blk + 64 + 4 * i);
         D[i] = state[24 + i] ^ ld32(blk + 96 + 4 * i);
     }
+    // unrolled: the step's lane permutation n ^ pc and rotations become constants (a runtime
+    // pc would index tA[] through scratch memory on the GPU)
+#pragma unroll
     for (int r = 0; r < 4; ++r)
+#pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int sb = kSimdSb[r][j];
             u32 w[8];
             for (int k = 0; k < 8; ++k) {
                 if (r < 2) {
-                    w[k] = simd_inner(q[16 * sb + 2 * k], q[16 * sb + 2 * k + 1], 185);
+                    w[k] = simd_inner(Q(16 * sb + 2 * k), Q(16 * sb + 2 * k + 1), 185);
                 } else {
                     const int base = 16 * (sb - 8 * r) + 2 * k + (r == 3 ? 1 : 0);
-                    w[k] = simd_inner(q[base], q[base + 128], 233);
+                    w[k] = simd_inner(Q(base), Q(base + 128), 233);
                 }
             }
             simd_step(A, B, C, D, w, j >= 4, kSimdRot[r][j & 3], kSimdRot[r][(j + 1) & 3], kSimdPerm[(j + r) % 7]);
         }
+#pragma unroll
     for (int k = 0; k < 4; ++k)
         simd_step(A, B, C, D, saved + 8 * k, 0, kSimdFf[k][0], kSimdFf[k][1], kSimdPerm[kSimdFf[k][2]]);
     for (int i = 0; i < 8; ++i) {
@@ -705,22 +720,25 @@ X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last) {
         state[24 + i] = D[i];
     }
 }
+#undef Q
 
-X16R_FN void simd512(const u8* data, int n, u8* out) {  // 0 < n < 128
+X16R_FN void simd512(const u8* data, int n, u8* out, int16_t* qb = nullptr, int qs = 1) {  // 0 < n < 128
+    int16_t local[256];
+    if (qb == nullptr) qb = local;
     u32 st[32];
     for (int i = 0; i < 32; ++i) st[i] = kSimdIV[i];
     u8 buf[128];
     zero(buf, 128);
     cpy(buf, data, n);
-    simd_compress(st, buf, false);
+    simd_compress(st, buf, false, qb, qs);
     zero(buf, 128);
     st64(buf, u64(n) * 8);
-    simd_compress(st, buf, true);
+    simd_compress(st, buf, true, qb, qs);
     for (int i = 0; i < 16; ++i) st32(out + 4 * i, st[i]);
 }
 
 // ================================================================ ECHO-512 (slot 10)
-X16R_FN void echo_compress(u8 v[8][16], const u8 m[128], u64 counter_bits) {
+X16R_FN void echo_compress(u8 v[8][16], const u8 m[128], u64 counter_bits, const u8* sbox) {
     u8 w[16][16];
     for (int i = 0; i < 8; ++i) cpy(w[i], v[i], 16);
     for (int i = 0; i < 8; ++i) cpy(w[8 + i], m + 16 * i, 16);
@@ -733,8 +751,8 @@ X16R_FN void echo_compress(u8 v[8][16], const u8 m[128], u64 counter_bits) {
             zero(key, 16);
             st64(key, k);
             ++k;
-            aes_round(w[i], key);
-            aes_round(w[i], salt);
+            aes_round(w[i], key, sbox);
+            aes_round(w[i], salt, sbox);
         }
         u8 t[16][16];
         for (int j = 0; j < 4; ++j)
@@ -752,7 +770,7 @@ X16R_FN void echo_compress(u8 v[8][16], const u8 m[128], u64 counter_bits) {
         for (int b = 0; b < 16; ++b) v[i][b] ^= m[16 * i + b] ^ w[i][b] ^ w[8 + i][b];
 }
 
-X16R_FN void echo512(const u8* data, int n, u8* out) {  // 0 < n < 110: one padded block
+X16R_FN void echo512(const u8* data, int n, u8* out, const u8* sbox = kX16rAesSbox) {  // 0 < n < 110
     u8 v[8][16];
     for (int i = 0; i < 8; ++i) {
         zero(v[i], 16);
@@ -766,7 +784,7 @@ X16R_FN void echo512(const u8* data, int n, u8* out) {  // 0 < n < 110: one padd
     buf[110] = 0x00;
     buf[111] = 0x02;
     st64(buf + 112, bits);
-    echo_compress(v, buf, bits);
+    echo_compress(v, buf, bits, sbox);
     for (int i = 0; i < 4; ++i) cpy(out + 16 * i, v[i], 16);
 }
 
@@ -837,12 +855,12 @@ X16R_FN void hamsi512(const u8* data, int n, u8* out) {
 }
 
 // ================================================================ Fugue-512 (slot 12)
-X16R_FN void fugue_smix(u32& x0, u32& x1, u32& x2, u32& x3) {
+X16R_FN void fugue_smix(u32& x0, u32& x1, u32& x2, u32& x3, const u32* mt) {
     const u32 x[4] = {x0, x1, x2, x3};
     u32 c[4] = {0, 0, 0, 0}, r[4] = {0, 0, 0, 0};
     for (int j = 0; j < 4; ++j)
         for (int k = 0; k < 4; ++k) {
-            const u32 t = kX16rFugueMt[256 * k + ((x[j] >> (24 - 8 * k)) & 0xFF)];
+            const u32 t = mt[256 * k + ((x[j] >> (24 - 8 * k)) & 0xFF)];
             c[j] ^= t;
             if (k != j) r[k] ^= t;
         }
@@ -860,20 +878,20 @@ X16R_FN void fugue_ror(u32 S[36], int n) {
     for (int i = 0; i < 36; ++i) t[(i + n) % 36] = S[i];
     for (int i = 0; i < 36; ++i) S[i] = t[i];
 }
-X16R_FN void fugue_cmix_sub(u32 S[36]) {
+X16R_FN void fugue_cmix_sub(u32 S[36], const u32* mt) {
     fugue_ror(S, 3);
     S[0] ^= S[4]; S[1] ^= S[5]; S[2] ^= S[6];
     S[18] ^= S[4]; S[19] ^= S[5]; S[20] ^= S[6];
-    fugue_smix(S[0], S[1], S[2], S[3]);
+    fugue_smix(S[0], S[1], S[2], S[3], mt);
 }
-X16R_FN void fugue_word(u32 S[36], u32 I) {
+X16R_FN void fugue_word(u32 S[36], u32 I, const u32* mt) {
     S[22] ^= S[0];
     S[0] = I;
     S[8] ^= S[0];
     S[1] ^= S[24];
     S[4] ^= S[27];
     S[7] ^= S[30];
-    for (int k = 0; k < 4; ++k) fugue_cmix_sub(S);
+    for (int k = 0; k < 4; ++k) fugue_cmix_sub(S, mt);
 }
 constexpr u32 kFugueIV[16] = {0x8807a57e, 0xe616af75, 0xc5d3e4db, 0xac9ab027, 0xd915f117, 0xb6eecc54,
                               0x06e8020b, 0x4a92efd1, 0xaac6e2c9, 0xddb21398, 0xcae65838, 0x437f203f,
@@ -881,25 +899,25 @@ constexpr u32 kFugueIV[16] = {0x8807a57e, 0xe616af75, 0xc5d3e4db, 0xac9ab027, 0x
 constexpr int kFugueG[4][4] = {{4, 9, 18, 27}, {4, 10, 18, 27}, {4, 10, 19, 27}, {4, 10, 19, 28}};
 constexpr int kFugueOut[16] = {1, 2, 3, 4, 9, 10, 11, 12, 18, 19, 20, 21, 27, 28, 29, 30};
 
-X16R_FN void fugue512(const u8* data, int n, u8* out) {
+X16R_FN void fugue512(const u8* data, int n, u8* out, const u32* mt = kX16rFugueMt) {
     u32 S[36];
     for (int i = 0; i < 36; ++i) S[i] = 0;
     for (int i = 0; i < 16; ++i) S[20 + i] = kFugueIV[i];
     const u64 bits = u64(n) * 8;
-    for (; n >= 4; n -= 4, data += 4) fugue_word(S, ldb32(data));
+    for (; n >= 4; n -= 4, data += 4) fugue_word(S, ldb32(data), mt);
     if (n) {
         u8 w[4] = {0, 0, 0, 0};
         cpy(w, data, n);
-        fugue_word(S, ldb32(w));
+        fugue_word(S, ldb32(w), mt);
     }
-    fugue_word(S, u32(bits >> 32));
-    fugue_word(S, u32(bits));
-    for (int i = 0; i < 32; ++i) fugue_cmix_sub(S);
+    fugue_word(S, u32(bits >> 32), mt);
+    fugue_word(S, u32(bits), mt);
+    for (int i = 0; i < 32; ++i) fugue_cmix_sub(S, mt);
     for (int i = 0; i < 13; ++i)
         for (int k = 0; k < 4; ++k) {
             for (int j = 0; j < 4; ++j) S[kFugueG[k][j]] ^= S[0];
             fugue_ror(S, k == 3 ? 8 : 9);
-            fugue_smix(S[0], S[1], S[2], S[3]);
+            fugue_smix(S[0], S[1], S[2], S[3], mt);
         }
     for (int j = 0; j < 4; ++j) S[kFugueG[0][j]] ^= S[0];
     for (int i = 0; i < 16; ++i) stb32(out + 4 * i, S[kFugueOut[i]]);
@@ -950,15 +968,15 @@ X16R_FN void shabal512(const u8* data, int n, u8* out) {
 }
 
 // ================================================================ Whirlpool (slot 14)
-X16R_FN void whirl_round(const u64 a[8], const u64 k[8], u64 out[8]) {
+X16R_FN void whirl_round(const u64 a[8], const u64 k[8], u64 out[8], const u64* T) {
     for (int i = 0; i < 8; ++i) {
         u64 v = k[i];
-        for (int j = 0; j < 8; ++j) v ^= kX16rWhirlT[256 * j + u8(a[(i - j) & 7] >> (8 * j))];
+        for (int j = 0; j < 8; ++j) v ^= T[256 * j + u8(a[(i - j) & 7] >> (8 * j))];
         out[i] = v;
     }
 }
 
-X16R_FN void whirl_compress(u64 H[8], const u8 blk[64]) {
+X16R_FN void whirl_compress(u64 H[8], const u8 blk[64], const u64* T) {
     u64 K[8], st[8], m[8], tmp[8];
     for (int i = 0; i < 8; ++i) {
         m[i] = ld64(blk + 8 * i);
@@ -967,27 +985,27 @@ X16R_FN void whirl_compress(u64 H[8], const u8 blk[64]) {
     }
     for (int r = 1; r <= 10; ++r) {
         const u64 c[8] = {kX16rWhirlRc[r], 0, 0, 0, 0, 0, 0, 0};
-        whirl_round(K, c, tmp);
+        whirl_round(K, c, tmp, T);
         for (int i = 0; i < 8; ++i) K[i] = tmp[i];
-        whirl_round(st, K, tmp);
+        whirl_round(st, K, tmp, T);
         for (int i = 0; i < 8; ++i) st[i] = tmp[i];
     }
     for (int i = 0; i < 8; ++i) H[i] ^= st[i] ^ m[i];
 }
 
-X16R_FN void whirlpool512(const u8* data, int n, u8* out) {
+X16R_FN void whirlpool512(const u8* data, int n, u8* out, const u64* T = kX16rWhirlT) {
     u64 H[8];
     for (int i = 0; i < 8; ++i) H[i] = 0;
     const u64 bits = u64(n) * 8;
-    for (; n >= 64; n -= 64, data += 64) whirl_compress(H, data);
+    for (; n >= 64; n -= 64, data += 64) whirl_compress(H, data, T);
     u8 buf[128];
     zero(buf, 128);
     cpy(buf, data, n);
     buf[n] = 0x80;
     const int len = n < 32 ? 64 : 128;
     stb64(buf + len - 8, bits);
-    whirl_compress(H, buf);
-    if (len == 128) whirl_compress(H, buf + 64);
+    whirl_compress(H, buf, T);
+    if (len == 128) whirl_compress(H, buf + 64, T);
     for (int i = 0; i < 8; ++i) st64(out + 8 * i, H[i]);
 }
 
@@ -1039,18 +1057,16 @@ X16R_FN void sha512(const u8* data, int n, u8* out) {  // n < 112: one padded bl
 }
 
 // ================================================================ Tiger-192, zero-padded (X16RV2)
-X16R_FN void tiger_rnd(u64& A, u64& B, u64& C, u64 xv, u64 mul) {
+X16R_FN void tiger_rnd(u64& A, u64& B, u64& C, u64 xv, u64 mul, const u64* T) {
     C ^= xv;
-    A -= kX16rTiger[u8(C)] ^ kX16rTiger[256 + u8(C >> 16)] ^ kX16rTiger[512 + u8(C >> 32)] ^
-         kX16rTiger[768 + u8(C >> 48)];
-    B += kX16rTiger[768 + u8(C >> 8)] ^ kX16rTiger[512 + u8(C >> 24)] ^ kX16rTiger[256 + u8(C >> 40)] ^
-         kX16rTiger[u8(C >> 56)];
+    A -= T[u8(C)] ^ T[256 + u8(C >> 16)] ^ T[512 + u8(C >> 32)] ^ T[768 + u8(C >> 48)];
+    B += T[768 + u8(C >> 8)] ^ T[512 + u8(C >> 24)] ^ T[256 + u8(C >> 40)] ^ T[u8(C >> 56)];
     B *= mul;
 }
-X16R_FN void tiger_pass(u64& A, u64& B, u64& C, const u64 x[8], u64 mul) {
-    tiger_rnd(A, B, C, x[0], mul); tiger_rnd(B, C, A, x[1], mul); tiger_rnd(C, A, B, x[2], mul);
-    tiger_rnd(A, B, C, x[3], mul); tiger_rnd(B, C, A, x[4], mul); tiger_rnd(C, A, B, x[5], mul);
-    tiger_rnd(A, B, C, x[6], mul); tiger_rnd(B, C, A, x[7], mul);
+X16R_FN void tiger_pass(u64& A, u64& B, u64& C, const u64 x[8], u64 mul, const u64* T) {
+    tiger_rnd(A, B, C, x[0], mul, T); tiger_rnd(B, C, A, x[1], mul, T); tiger_rnd(C, A, B, x[2], mul, T);
+    tiger_rnd(A, B, C, x[3], mul, T); tiger_rnd(B, C, A, x[4], mul, T); tiger_rnd(C, A, B, x[5], mul, T);
+    tiger_rnd(A, B, C, x[6], mul, T); tiger_rnd(B, C, A, x[7], mul, T);
 }
 X16R_FN void tiger_schedule(u64 x[8]) {
     x[0] -= x[7] ^ 0xA5A5A5A5A5A5A5A5ULL; x[1] ^= x[0]; x[2] += x[1]; x[3] -= x[2] ^ ((~x[1]) << 19);
@@ -1058,26 +1074,26 @@ X16R_FN void tiger_schedule(u64 x[8]) {
     x[0] += x[7]; x[1] -= x[0] ^ ((~x[7]) << 19); x[2] ^= x[1]; x[3] += x[2];
     x[4] -= x[3] ^ ((~x[2]) >> 23); x[5] ^= x[4]; x[6] += x[5]; x[7] -= x[6] ^ 0x0123456789ABCDEFULL;
 }
-X16R_FN void tiger_compress(const u64 xin[8], u64 st[3]) {
+X16R_FN void tiger_compress(const u64 xin[8], u64 st[3], const u64* T) {
     u64 a = st[0], b = st[1], c = st[2], x[8];
     for (int i = 0; i < 8; ++i) x[i] = xin[i];
-    tiger_pass(a, b, c, x, 5);
+    tiger_pass(a, b, c, x, 5, T);
     tiger_schedule(x);
-    tiger_pass(c, a, b, x, 7);
+    tiger_pass(c, a, b, x, 7, T);
     tiger_schedule(x);
-    tiger_pass(b, c, a, x, 9);
+    tiger_pass(b, c, a, x, 9, T);
     st[0] = a ^ st[0];
     st[1] = b - st[1];
     st[2] = c + st[2];
 }
 
-X16R_FN void tiger192_padded(const u8* data, int n, u8* out) {
+X16R_FN void tiger192_padded(const u8* data, int n, u8* out, const u64* T = kX16rTiger) {
     u64 st[3] = {0x0123456789ABCDEFULL, 0xFEDCBA9876543210ULL, 0xF096A5B4C3B2E187ULL};
     u64 x[8];
     const u64 bits = u64(n) * 8;
     for (; n >= 64; n -= 64, data += 64) {
         for (int i = 0; i < 8; ++i) x[i] = ld64(data + 8 * i);
-        tiger_compress(x, st);
+        tiger_compress(x, st, T);
     }
     u8 buf[128];
     zero(buf, 128);
@@ -1087,7 +1103,7 @@ X16R_FN void tiger192_padded(const u8* data, int n, u8* out) {
     st64(buf + len - 8, bits);
     for (int off = 0; off < len; off += 64) {
         for (int i = 0; i < 8; ++i) x[i] = ld64(buf + off + 8 * i);
-        tiger_compress(x, st);
+        tiger_compress(x, st, T);
     }
     zero(out, 64);
     for (int i = 0; i < 3; ++i) st64(out + 8 * i, st[i]);

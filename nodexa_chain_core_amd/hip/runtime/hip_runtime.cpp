@@ -30,6 +30,33 @@ void check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Side streams of one device for work that fans out and joins (the X16R slot kernels of a chain
+// step run side by side): created on first use, kept for the process; one event per stream.
+struct FanOut {
+    static constexpr int kStreams = 4;
+    hipStream_t streams[kStreams] = {};
+    hipEvent_t done[kStreams] = {};
+    hipEvent_t start = nullptr;
+};
+
+FanOut& fan_out() {
+    static std::mutex mu;
+    static std::unordered_map<int, std::unique_ptr<FanOut>> per_device;
+    int dev = 0;
+    check(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> g(mu);
+    auto& f = per_device[dev];
+    if (!f) {
+        f = std::make_unique<FanOut>();
+        for (int i = 0; i < FanOut::kStreams; ++i) {
+            check(hipStreamCreateWithFlags(&f->streams[i], hipStreamNonBlocking), "hipStreamCreateWithFlags");
+            check(hipEventCreateWithFlags(&f->done[i], hipEventDisableTiming), "hipEventCreateWithFlags");
+        }
+        check(hipEventCreateWithFlags(&f->start, hipEventDisableTiming), "hipEventCreateWithFlags");
+    }
+    return *f;
+}
+
 FastMod32 make_fastmod(uint32_t d) {
     if (d < 2) throw std::invalid_argument("fastmod divisor must be >= 2");
     uint32_t s = 0;
@@ -378,18 +405,33 @@ PYBIND11_MODULE(_hip, m) {
         p.state = reinterpret_cast<uint8_t*>(state);
         p.v2 = reinterpret_cast<const uint8_t*>(v2);
         p.n = n;
+        // the slot groups of a step are independent: they run side by side on the fan-out streams,
+        // and every stream waits for all of them before the next step (each header's next slot
+        // can be any of the 16); the caller's stream waits for the last step
         const hipStream_t st = as_stream(stream);
+        FanOut& f = fan_out();
+        constexpr int S = FanOut::kStreams;
+        check(hipEventRecord(f.start, st), "hipEventRecord");
+        for (int i = 0; i < S; ++i) check(hipStreamWaitEvent(f.streams[i], f.start, 0), "hipStreamWaitEvent");
         for (uint32_t s = 0; s < 16; ++s) {
             p.step = s;
             p.order = reinterpret_cast<const int32_t*>(order) + size_t(s) * n;
             p.offsets = reinterpret_cast<const int32_t*>(offsets) + size_t(s) * 17;
+            int used = 0;
             for (int a = 0; a < 16; ++a) {
                 const uint32_t cnt = uint32_t(offsets_host[size_t(s * 17 + a + 1)] - offsets_host[size_t(s * 17 + a)]);
                 if (cnt == 0) continue;
                 const unsigned block = unsigned(slots[size_t(a)]->max_threads);
-                slots[size_t(a)]->launch_bytes(dim3((cnt + block - 1) / block), dim3(block), 0, st, &p, sizeof(p));
+                slots[size_t(a)]->launch_bytes(dim3((cnt + block - 1) / block), dim3(block), 0, f.streams[used % S], &p,
+                                               sizeof(p));
+                ++used;
             }
+            for (int i = 0; i < S; ++i) check(hipEventRecord(f.done[i], f.streams[i]), "hipEventRecord");
+            for (int i = 0; i < S; ++i)
+                for (int j = 0; j < S; ++j)
+                    if (i != j) check(hipStreamWaitEvent(f.streams[i], f.done[j], 0), "hipStreamWaitEvent");
         }
+        for (int i = 0; i < S; ++i) check(hipStreamWaitEvent(st, f.done[i], 0), "hipStreamWaitEvent");
     });
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
     m.attr("KV_PROG_WORDS") = KV_PROG_WORDS;
