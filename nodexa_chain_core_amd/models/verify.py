@@ -160,7 +160,7 @@ def _verify_native(params, headers, gpus, threads: int, mode: str, rows_fn=None)
     t4 = time.perf_counter()
     legacy = np.flatnonzero(kinds == 3).tolist()
     if legacy:
-        _verify_x16r(params, headers, legacy, out, threads)
+        _verify_x16r(params, headers, legacy, out, threads, gpus)
     LAST_TIMING.update(prepare_s=t1 - t0, kawpow_s=t2 - t1, check_s=t3 - t2, equihash_s=t4 - t3,
                        x16r_s=time.perf_counter() - t4)
     return out
@@ -219,19 +219,38 @@ def _cpu_rows(jobs: np.ndarray, threads: int) -> np.ndarray:
     return np.frombuffer(b"".join(rows), dtype=np.uint8).reshape(len(jobs), 64)
 
 
-def _verify_x16r(params, headers, idxs: list[int], out: list[dict], threads: int) -> None:
-    """Pre-KawPow headers: X16R / X16RV2 by nTime (src/primitives/block.cpp:38-55) on the
-    host cores (the native hash releases the GIL), then CheckProofOfWork."""
-    def one(i):
-        h = headers[i]
-        fn = _core.x16rv2 if h.time >= params.x16rv2_activation_time else _core.x16r
-        return fn(h.legacy80(), h.prev)
+# Legacy-header batches at least this large hash on the GPU (hip/kernels/x16r.hip: 16 rounds of
+# slot-grouped launches, ~1.7 M hashes/s on 65k headers); smaller ones stay on the host cores.
+X16R_GPU_MIN = 512
 
-    with cf.ThreadPoolExecutor(max_workers=threads or (os.cpu_count() or 4)) as ex:
-        for i, hsh in zip(idxs, ex.map(one, idxs)):
-            ok = _core.check_proof_of_work(hsh, headers[i].bits, params)
-            out.set(i, {"valid": bool(ok), "hash": _core.u256_hex(hsh)} if ok else
-                    {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(hsh)}, hsh)
+
+def x16r_hashes(params, legacy80: list[bytes], times: list[int], gpu: int | None) -> list[bytes]:
+    """X16R / X16RV2 (by nTime, src/primitives/block.cpp:38-55) hashes of legacy headers: one
+    batch on `gpu` (ops/x16r) when it is large enough, else the native host hash on all cores
+    (it releases the GIL)."""
+    v2 = [t >= params.x16rv2_activation_time for t in times]
+    if gpu is not None and len(legacy80) >= X16R_GPU_MIN:
+        from ..ops.x16r import x16r_hash_batch
+
+        got = x16r_hash_batch(b"".join(legacy80), v2=np.array(v2), device=gpu)
+        return [bytes(r) for r in got]
+
+    def one(k):
+        fn = _core.x16rv2 if v2[k] else _core.x16r
+        return fn(legacy80[k], legacy80[k][4:36])
+
+    with cf.ThreadPoolExecutor(max_workers=os.cpu_count() or 4) as ex:
+        return list(ex.map(one, range(len(legacy80))))
+
+
+def _verify_x16r(params, headers, idxs: list[int], out: list[dict], threads: int, gpus=None) -> None:
+    """Pre-KawPow headers: X16R / X16RV2 (x16r_hashes), then CheckProofOfWork."""
+    hs = x16r_hashes(params, [headers[i].legacy80() for i in idxs], [headers[i].time for i in idxs],
+                     gpus[0] if gpus else None)
+    for i, hsh in zip(idxs, hs):
+        ok = _core.check_proof_of_work(hsh, headers[i].bits, params)
+        out.set(i, {"valid": bool(ok), "hash": _core.u256_hex(hsh)} if ok else
+                {"valid": False, "reason": "high-hash", "hash": _core.u256_hex(hsh)}, hsh)
 
 
 def _verify_equihash(params, headers, idxs: list[int], out: list[dict], gpus, threads: int) -> None:
@@ -394,13 +413,12 @@ def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, wo
     n = len(batch)
     legacy = np.flatnonzero(codes == 255)
     hashes = r["hashes"]
-    if len(legacy):  # X16R / X16RV2 headers: host cores, then their hashes join the device ones
+    if len(legacy):  # X16R / X16RV2 headers (x16r_hashes: this device or the host cores), joined in
         hs = [batch.header(int(i)) for i in legacy]
         hashes = np.array(hashes)
         codes = np.array(codes)
-        for i, hdr in zip(legacy.tolist(), hs):
-            fn = _core.x16rv2 if hdr.time >= params.x16rv2_activation_time else _core.x16r
-            hsh = fn(hdr.legacy80(), hdr.prev)
+        xs = x16r_hashes(params, [hdr.legacy80() for hdr in hs], [hdr.time for hdr in hs], device)
+        for i, hdr, hsh in zip(legacy.tolist(), hs, xs):
             hashes[i] = np.frombuffer(hsh, np.uint8)
             ok = _core.check_proof_of_work(hsh, hdr.bits, params)
             codes[i] = 0 if ok else 2

@@ -32,3 +32,30 @@ def test_random_batch_mixed_versions_vs_host(core, gpu):
     for i in range(0, n, 7):  # the host chain is the slow side
         fn = core.x16rv2 if v2[i] else core.x16r
         assert bytes(got[i]) == fn(hdrs[i], hdrs[i][4:36]), i
+
+
+def test_verify_headers_legacy_batch_on_gpu_matches_host(core, gpu):
+    """models/verify routes a legacy (pre-KawPow) batch of X16R_GPU_MIN headers or more through the
+    GPU hash: same verdicts and hashes as the host cores, X16R and X16RV2 by nTime."""
+    from nodexa_chain_core_amd.chain.state import make_params
+    from nodexa_chain_core_amd.models import verify as MV
+
+    params = make_params("regtest")
+    # regtest activates KawPow before X16RV2: move X16RV2 inside the legacy era for this batch
+    params.x16rv2_activation_time = params.kawpow_activation_time - 100_000
+    rng = random.Random(5)
+    hs = []
+    for i in range(MV.X16R_GPU_MIN + 40):
+        h = core.BlockHeader()
+        h.version = 0x20000000
+        h.prev = rng.randbytes(32)
+        h.merkle_root = rng.randbytes(32)
+        h.time = params.x16rv2_activation_time + rng.choice([-1000, 1000])  # both versions
+        h.bits = 0x207fffff  # regtest limit: about half of the hashes meet it
+        h.nonce = rng.getrandbits(32)
+        hs.append(h)
+    assert all(h.time < params.kawpow_activation_time for h in hs)
+    gpu_r = MV.verify_headers(params, hs, gpus=[0])
+    cpu_r = MV.verify_headers(params, hs, gpus=None)
+    assert [(r["valid"], r["hash"]) for r in gpu_r] == [(r["valid"], r["hash"]) for r in cpu_r]
+    assert 0 < sum(r["valid"] for r in gpu_r) < len(hs)
