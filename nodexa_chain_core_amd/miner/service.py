@@ -1032,7 +1032,7 @@ def follower_main() -> int:
     watchdog = float(os.environ.get("NODEXA_MINER_WATCHDOG", "120"))
     window = int(os.environ.get("NODEXA_MINER_WINDOW", str(1 << 25)))
     W.init(use_gpu=not cpu, device_index=None if dev_index is None else int(dev_index),
-           timeout_s=int(max(timeout, 10)), elastic=True)
+           timeout_s=max(int(timeout), W.rendezvous_timeout()), elastic=True)
     w = W.get()
     dev = make_rank_device(cpu, w.device.index if not cpu else None, collective_dag=w.collective, window=window,
                            fail_rate=float(os.environ.get("NODEXA_MINER_FAILRATE", "0") or 0),

@@ -390,7 +390,7 @@ class Node:
         self.miner_procs = []
         ranks = max(1, a.get_int("minerranks", 1)) if a.get_bool("minerservice", False) else 1
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)), elastic=True)
+            W.init(use_gpu=not cpu, timeout_s=max(int(timeout), W.rendezvous_timeout()), elastic=True)
         elif cpu and ranks == 1 and not a.get_bool("minerforcecollectives", False):
             pass  # a single host rank: nothing to exchange, no process group
         else:
@@ -409,7 +409,8 @@ class Node:
                 if a.get("gpuintensity"):
                     env["NODEXA_MINER_WINDOW"] = a.get("gpuintensity")
                 self.miner_procs = MS.spawn_followers(gpus, port, cpu=cpu, extra_env=env)
-            W.init(use_gpu=not cpu, timeout_s=int(max(10, timeout)), device_index=None if cpu else gpus[0],
+            W.init(use_gpu=not cpu, timeout_s=max(int(timeout), W.rendezvous_timeout()),
+                   device_index=None if cpu else gpus[0],
                    rank=0, world_size=len(gpus), elastic=True,
                    force_collectives=a.get_bool("minerforcecollectives", False) or None)
         w = W.get()

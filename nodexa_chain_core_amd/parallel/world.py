@@ -46,6 +46,14 @@ class World:
 _WORLD: World | None = None
 
 
+def rendezvous_timeout() -> int:
+    """Timeout of the default group (NODEXA_RENDEZVOUS_TIMEOUT, default 300 s): the start-up
+    rendezvous and full-mesh connect, which must tolerate ranks that start seconds apart (a loaded
+    host, a cold torch import). Failure detection does not use it: the mining loop's collectives run
+    on a group of their own with the collective timeout (miner/service.Comm)."""
+    return int(os.environ.get("NODEXA_RENDEZVOUS_TIMEOUT", "300"))
+
+
 def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | None = None,
          rank: int | None = None, world_size: int | None = None, elastic: bool = False,
          force_collectives: bool | None = None) -> World:

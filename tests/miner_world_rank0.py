@@ -22,7 +22,7 @@ def main(out_path: str) -> int:
 
     _core = core()
     timeout = float(os.environ.get("NODEXA_MINER_COLLECTIVE_TIMEOUT", "30"))
-    W.init(use_gpu=False, timeout_s=int(max(timeout, 10)))
+    W.init(use_gpu=False, timeout_s=max(int(timeout), W.rendezvous_timeout()))
     blocks = int(os.environ.get("NODEXA_TEST_BLOCKS", "2"))
     window = int(os.environ.get("NODEXA_MINER_WINDOW", "8"))
     eq_act = int(time.time()) - 100 if os.environ.get("NODEXA_TEST_EQUIHASH") == "1" else None

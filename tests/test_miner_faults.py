@@ -47,9 +47,9 @@ def test_gloo_world8_shrinks_to_7(tmp_path, core):
     re-form the world (8 -> 7) and finish the blocks; every share the node took re-checks on the host."""
     from nodexa_chain_core_amd.miner.service import EXIT_DEVICE_FAILED
 
-    # the collective timeout also bounds each gloo group's full-mesh connect (8 ranks: 56 pairs);
-    # on a loaded 8-CPU host that took more than 6 s, so this world gets 20 s (the failing rank
-    # exits on its own and its peers see closed sockets at once: nothing here waits a timeout out)
+    # 8 ranks on a loaded 8-CPU host start seconds apart: the default group's rendezvous has its
+    # own generous timeout (world.rendezvous_timeout); the loop's collective timeout only has to
+    # cover the shrunk group's connect (the failing rank exits, its peers see closed sockets)
     codes, outs, report = _run_world(tmp_path, 8, blocks=2, timeout_s=20.0,
                                      rank_env={5: {"NODEXA_MINER_FAILRATE": "1"}})
     assert codes[5] == EXIT_DEVICE_FAILED, "\n".join(outs)
