@@ -59,6 +59,39 @@ void aes_round(u8 s[16], const u8* key) {
         for (int i = 0; i < 16; ++i) s[i] ^= key[i];
 }
 
+// The same round on four little-endian column words through the usual four 256 x u32 tables:
+// T[k][x] is the MixColumns image of S[x] entering at row k (T[0][x] bytes 2S, S, S, 3S).
+struct AesT {
+    u32 T[4][256];
+    AesT() {
+        const u8* S = aes_sbox();
+        for (int x = 0; x < 256; ++x) {
+            const u8 s = S[x], s2 = xtime(s), s3 = u8(s2 ^ s);
+            const u32 v = u32(s2) | (u32(s) << 8) | (u32(s) << 16) | (u32(s3) << 24);
+            for (int k = 0; k < 4; ++k) T[k][x] = k ? rotl32(v, 8 * k) : v;
+        }
+    }
+};
+
+const AesT& aes_t() {
+    static const AesT t;
+    return t;
+}
+
+inline void aes_round_w(u32 x[4], const u32* key, const AesT& A) {
+    const u32 y0 = A.T[0][x[0] & 0xFF] ^ A.T[1][(x[1] >> 8) & 0xFF] ^ A.T[2][(x[2] >> 16) & 0xFF] ^ A.T[3][x[3] >> 24];
+    const u32 y1 = A.T[0][x[1] & 0xFF] ^ A.T[1][(x[2] >> 8) & 0xFF] ^ A.T[2][(x[3] >> 16) & 0xFF] ^ A.T[3][x[0] >> 24];
+    const u32 y2 = A.T[0][x[2] & 0xFF] ^ A.T[1][(x[3] >> 8) & 0xFF] ^ A.T[2][(x[0] >> 16) & 0xFF] ^ A.T[3][x[1] >> 24];
+    const u32 y3 = A.T[0][x[3] & 0xFF] ^ A.T[1][(x[0] >> 8) & 0xFF] ^ A.T[2][(x[1] >> 16) & 0xFF] ^ A.T[3][x[2] >> 24];
+    x[0] = y0 ^ (key ? key[0] : 0);
+    x[1] = y1 ^ (key ? key[1] : 0);
+    x[2] = y2 ^ (key ? key[2] : 0);
+    x[3] = y3 ^ (key ? key[3] : 0);
+}
+
+// xtime on four packed bytes
+inline u32 xtime4(u32 v) { return ((v & 0x7F7F7F7Fu) << 1) ^ (((v >> 7) & 0x01010101u) * 0x1Bu); }
+
 }  // namespace
 
 // ================================================================ Groestl-512
@@ -143,45 +176,45 @@ Hash512 groestl512(const u8* data, size_t n) {
 // 16 x 128-bit words; 1024-bit chaining value, 1024-bit message block, 10 rounds.
 namespace {
 
-void echo_compress(u8 v[8][16], const u8 m[128], u64 counter_bits) {
-    u8 w[16][16];
-    for (int i = 0; i < 8; ++i) std::memcpy(w[i], v[i], 16);
-    for (int i = 0; i < 8; ++i) std::memcpy(w[8 + i], m + 16 * i, 16);
+// 16 words of 128 bits as 4 little-endian column words each; BIG.SubWords is two word rounds,
+// BIG.MixColumns the AES MixColumns applied bytewise across four words (packed four bytes at once).
+void echo_compress(u32 v[8][4], const u8 m[128], u64 counter_bits) {
+    const AesT& A = aes_t();
+    u32 w[16][4];
+    for (int i = 0; i < 8; ++i)
+        for (int c = 0; c < 4; ++c) w[i][c] = v[i][c];
+    for (int i = 0; i < 8; ++i)
+        for (int c = 0; c < 4; ++c) w[8 + i][c] = load_le32(m + 16 * i + 4 * c);
     u64 k = counter_bits;
-    const u8 salt[16] = {0};
     for (int r = 0; r < 10; ++r) {
-        // BIG.SubWords: two AES rounds per word, keys (counter, salt)
         for (int i = 0; i < 16; ++i) {
-            u8 key[16] = {0};
-            store_le64(key, k);
+            const u32 key[4] = {u32(k), u32(k >> 32), 0, 0};
             ++k;
-            aes_round(w[i], key);
-            aes_round(w[i], salt);
+            aes_round_w(w[i], key, A);
+            aes_round_w(w[i], nullptr, A);
         }
-        // BIG.ShiftRows: word (row i, column j) at index 4j + i; row i rotates by i
-        u8 t[16][16];
+        u32 t[16][4];
         for (int j = 0; j < 4; ++j)
             for (int i = 0; i < 4; ++i) std::memcpy(t[4 * j + i], w[4 * ((j + i) & 3) + i], 16);
-        // BIG.MixColumns: AES MixColumns across the 4 words of each column, per byte
         for (int j = 0; j < 4; ++j)
-            for (int b = 0; b < 16; ++b) {
-                const u8 a0 = t[4 * j][b], a1 = t[4 * j + 1][b], a2 = t[4 * j + 2][b], a3 = t[4 * j + 3][b];
-                w[4 * j + 0][b] = u8(xtime(a0) ^ xtime(a1) ^ a1 ^ a2 ^ a3);
-                w[4 * j + 1][b] = u8(a0 ^ xtime(a1) ^ xtime(a2) ^ a2 ^ a3);
-                w[4 * j + 2][b] = u8(a0 ^ a1 ^ xtime(a2) ^ xtime(a3) ^ a3);
-                w[4 * j + 3][b] = u8(xtime(a0) ^ a0 ^ a1 ^ a2 ^ xtime(a3));
+            for (int c = 0; c < 4; ++c) {
+                const u32 a0 = t[4 * j][c], a1 = t[4 * j + 1][c], a2 = t[4 * j + 2][c], a3 = t[4 * j + 3][c];
+                const u32 x0 = xtime4(a0), x1 = xtime4(a1), x2 = xtime4(a2), x3 = xtime4(a3);
+                w[4 * j + 0][c] = x0 ^ x1 ^ a1 ^ a2 ^ a3;
+                w[4 * j + 1][c] = a0 ^ x1 ^ x2 ^ a2 ^ a3;
+                w[4 * j + 2][c] = a0 ^ a1 ^ x2 ^ x3 ^ a3;
+                w[4 * j + 3][c] = x0 ^ a0 ^ a1 ^ a2 ^ x3;
             }
     }
-    // BIG.Final
     for (int i = 0; i < 8; ++i)
-        for (int b = 0; b < 16; ++b) v[i][b] ^= m[16 * i + b] ^ w[i][b] ^ w[8 + i][b];
+        for (int c = 0; c < 4; ++c) v[i][c] ^= load_le32(m + 16 * i + 4 * c) ^ w[i][c] ^ w[8 + i][c];
 }
 
 }  // namespace
 
 Hash512 echo512(const u8* data, size_t n) {
-    u8 v[8][16] = {{0}};
-    for (int i = 0; i < 8; ++i) v[i][1] = 0x02;  // 512, 128-bit little-endian
+    u32 v[8][4] = {{0}};
+    for (int i = 0; i < 8; ++i) v[i][0] = 0x0200;  // 512, 128-bit little-endian
     const u64 total_bits = u64(n) * 8;
     u64 done = 0;
     for (; n >= 128; n -= 128, data += 128) {
@@ -202,7 +235,8 @@ Hash512 echo512(const u8* data, size_t n) {
         echo_compress(v, buf + 128, 0);
     }
     Hash512 out;
-    for (int i = 0; i < 4; ++i) std::memcpy(out.bytes + 16 * i, v[i], 16);
+    for (int i = 0; i < 4; ++i)
+        for (int c = 0; c < 4; ++c) store_le32(out.bytes + 16 * i + 4 * c, v[i][c]);
     return out;
 }
 
@@ -215,12 +249,7 @@ namespace {
 
 u32 le_word(const u8* p) { return load_le32(p); }
 
-void aes_words(u32 x[4]) {  // one keyless AES round on four little-endian column words
-    u8 b[16];
-    for (int i = 0; i < 4; ++i) store_le32(b + 4 * i, x[i]);
-    aes_round(b, nullptr);
-    for (int i = 0; i < 4; ++i) x[i] = le_word(b + 4 * i);
-}
+void aes_words(u32 x[4]) { aes_round_w(x, nullptr, aes_t()); }  // one keyless AES round
 
 void shavite_c512(u32 h[16], const u8 msg[128], const u32 cnt[4]) {
     u32 rk[448];
@@ -352,29 +381,32 @@ void fugue_smix(const FugueTables& T, u32& x0, u32& x1, u32& x2, u32& x3) {
          ((c[1] ^ (r[2] >> 8)) & 0x0000FF00u) | ((c[2] ^ (r[3] >> 8)) & 0x000000FFu);
 }
 
+// The 36 columns as a ring: logical column i is R[(i + off) % 36], so the ROR3 / ROR8 / ROR9
+// rotations are offset updates instead of 36-word moves.
 struct Fugue {
-    u32 S[36];
+    u32 R[36];
+    int off = 0;
     const FugueTables& T;
     explicit Fugue(const FugueTables& t) : T(t) {}
-    void ror(int n) {
-        u32 t[36];
-        for (int i = 0; i < 36; ++i) t[(i + n) % 36] = S[i];
-        std::memcpy(S, t, sizeof S);
+    u32& S(int i) {
+        const int j = i + off;
+        return R[j >= 36 ? j - 36 : j];
     }
-    void smix() { fugue_smix(T, S[0], S[1], S[2], S[3]); }
+    void ror(int n) { off = off >= n ? off - n : off - n + 36; }
+    void smix() { fugue_smix(T, S(0), S(1), S(2), S(3)); }
     void cmix_sub() {
         ror(3);
-        S[0] ^= S[4]; S[1] ^= S[5]; S[2] ^= S[6];
-        S[18] ^= S[4]; S[19] ^= S[5]; S[20] ^= S[6];
+        S(0) ^= S(4); S(1) ^= S(5); S(2) ^= S(6);
+        S(18) ^= S(4); S(19) ^= S(5); S(20) ^= S(6);
         smix();
     }
     void word(u32 I) {
-        S[22] ^= S[0];
-        S[0] = I;
-        S[8] ^= S[0];
-        S[1] ^= S[24];
-        S[4] ^= S[27];
-        S[7] ^= S[30];
+        S(22) ^= S(0);
+        S(0) = I;
+        S(8) ^= S(0);
+        S(1) ^= S(24);
+        S(4) ^= S(27);
+        S(7) ^= S(30);
         for (int k = 0; k < 4; ++k) cmix_sub();
     }
 };
@@ -387,8 +419,8 @@ Hash512 fugue512(const u8* data, size_t n) {
                                 0x06e8020b, 0x4a92efd1, 0xaac6e2c9, 0xddb21398, 0xcae65838, 0x437f203f,
                                 0x25ea78e7, 0x951fddd6, 0xda6ed11d, 0xe13e3567};
     Fugue f(T);
-    std::memset(f.S, 0, sizeof f.S);
-    std::memcpy(f.S + 20, kIV, sizeof kIV);
+    std::memset(f.R, 0, sizeof f.R);
+    std::memcpy(f.R + 20, kIV, sizeof kIV);
     const u64 bits = u64(n) * 8;
     for (; n >= 4; n -= 4, data += 4) f.word(load_be32(data));
     if (n) {
@@ -398,19 +430,18 @@ Hash512 fugue512(const u8* data, size_t n) {
     }
     f.word(u32(bits >> 32));
     f.word(u32(bits));
-    u32* S = f.S;
     for (int i = 0; i < 32; ++i) f.cmix_sub();
     static const int kG[4][4] = {{4, 9, 18, 27}, {4, 10, 18, 27}, {4, 10, 19, 27}, {4, 10, 19, 28}};
     for (int i = 0; i < 13; ++i)
         for (int k = 0; k < 4; ++k) {
-            for (int j = 0; j < 4; ++j) S[kG[k][j]] ^= S[0];
+            for (int j = 0; j < 4; ++j) f.S(kG[k][j]) ^= f.S(0);
             f.ror(k == 3 ? 8 : 9);
             f.smix();
         }
-    for (int j = 0; j < 4; ++j) S[kG[0][j]] ^= S[0];
+    for (int j = 0; j < 4; ++j) f.S(kG[0][j]) ^= f.S(0);
     static const int kOut[16] = {1, 2, 3, 4, 9, 10, 11, 12, 18, 19, 20, 21, 27, 28, 29, 30};
     Hash512 out;
-    for (int i = 0; i < 16; ++i) store_be32(out.bytes + 4 * i, S[kOut[i]]);
+    for (int i = 0; i < 16; ++i) store_be32(out.bytes + 4 * i, f.S(kOut[i]));
     return out;
 }
 

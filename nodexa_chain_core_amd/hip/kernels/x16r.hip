@@ -23,7 +23,7 @@
 // own register allocation (the light ARX slots are not held to the occupancy of the heaviest).
 // The slot's lookup tables copied into LDS once per workgroup (the per-lane byte-indexed lookups
 // would otherwise be 64 scattered global loads per instruction): Groestl's and Whirlpool's 8 x 256
-// u64, Fugue's 4 x 256 u32, the AES S-box of SHAvite-3 and ECHO, and Tiger's 4 x 256 u64 on the
+// u64, Fugue's 4 x 256 u32, the AES round tables (4 x 256 u32) of SHAvite-3 and ECHO, and Tiger's 4 x 256 u64 on the
 // slots X16RV2 pre-hashes with it.
 template <typename T, int N>
 __device__ void x16r_stage(T* dst, const T* src) {
@@ -35,13 +35,13 @@ __device__ void x16r_group(const X16rStepParams& p) {
     constexpr bool kGroestl = A == 2, kWhirl = A == 14, kFugue = A == 12, kAes = A == 8 || A == 10;
     constexpr bool kTiger = A == 4 || A == 6 || A == 15;
     __shared__ uint64_t t64[(kGroestl || kWhirl) ? 2048 : kTiger ? 1024 : 1];
-    __shared__ uint32_t t32[kFugue ? 1024 : kAes ? 64 : 1];
+    __shared__ uint32_t t32[(kFugue || kAes) ? 1024 : 1];
     __shared__ int16_t ntt[A == 9 ? 256 * X16R_BLOCK : 1];  // SIMD: each lane's NTT buffer, lanes interleaved
     if (kGroestl) x16r_stage<uint64_t, 2048>(t64, kX16rGroestlT);
     if (kWhirl) x16r_stage<uint64_t, 2048>(t64, kX16rWhirlT);
     if (kTiger) x16r_stage<uint64_t, 1024>(t64, kX16rTiger);
     if (kFugue) x16r_stage<uint32_t, 1024>(t32, kX16rFugueMt);
-    if (kAes) x16r_stage<uint32_t, 64>(t32, (const uint32_t*)kX16rAesSbox);
+    if (kAes) x16r_stage<uint32_t, 1024>(t32, kX16rAesT);
     if (kGroestl || kWhirl || kTiger || kFugue || kAes) __syncthreads();  // every thread, before any exits
 
     const int32_t lo = p.offsets[A], hi = p.offsets[A + 1];
@@ -60,7 +60,6 @@ __device__ void x16r_group(const X16rStepParams& p) {
         x16rd::st32(in + 16 * w + 12, v.w);
     }
     uint8_t out[64];
-    const uint8_t* sbox = (const uint8_t*)t32;
     if (kTiger && p.v2[i] != 0) {  // X16RV2: Tiger-192 first
         uint8_t t[64];
         x16rd::tiger192_padded(in, len, t, t64);
@@ -74,9 +73,9 @@ __device__ void x16r_group(const X16rStepParams& p) {
     } else if (A == 9) {
         x16rd::simd512(in, len, out, ntt + threadIdx.x, X16R_BLOCK);
     } else if (A == 8) {
-        x16rd::shavite512(in, len, out, sbox);
+        x16rd::shavite512(in, len, out, t32);
     } else if (A == 10) {
-        x16rd::echo512(in, len, out, sbox);
+        x16rd::echo512(in, len, out, t32);
     } else {
         x16rd::single(A, in, len, out);
     }

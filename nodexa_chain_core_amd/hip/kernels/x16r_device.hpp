@@ -185,32 +185,19 @@ X16R_FN void bmw512(const u8* data, int n, u8* out) {  // n < 120: one padded bl
     for (int i = 0; i < 8; ++i) st64(out + 8 * i, H[8 + i]);
 }
 
-// ================================================================ AES round, GF(2^8)
-X16R_FN u8 xtime(u8 a) { return u8((a << 1) ^ ((a & 0x80) ? 0x1B : 0)); }
-X16R_FN u8 gmul(u8 a, u8 b) {
-    u8 r = 0;
-    while (b) {
-        if (b & 1) r ^= a;
-        a = xtime(a);
-        b >>= 1;
-    }
-    return r;
+// ================================================================ AES round
+// The round on four little-endian column words through 4 x 256 u32 tables (kX16rAesT).
+X16R_FN void aes_round_w(u32 x[4], u32 k0, u32 k1, const u32* T) {
+    const u32 y0 = T[x[0] & 0xFF] ^ T[256 + ((x[1] >> 8) & 0xFF)] ^ T[512 + ((x[2] >> 16) & 0xFF)] ^ T[768 + (x[3] >> 24)];
+    const u32 y1 = T[x[1] & 0xFF] ^ T[256 + ((x[2] >> 8) & 0xFF)] ^ T[512 + ((x[3] >> 16) & 0xFF)] ^ T[768 + (x[0] >> 24)];
+    const u32 y2 = T[x[2] & 0xFF] ^ T[256 + ((x[3] >> 8) & 0xFF)] ^ T[512 + ((x[0] >> 16) & 0xFF)] ^ T[768 + (x[1] >> 24)];
+    const u32 y3 = T[x[3] & 0xFF] ^ T[256 + ((x[0] >> 8) & 0xFF)] ^ T[512 + ((x[1] >> 16) & 0xFF)] ^ T[768 + (x[2] >> 24)];
+    x[0] = y0 ^ k0;
+    x[1] = y1 ^ k1;
+    x[2] = y2;
+    x[3] = y3;
 }
-// One AES round on a 16-byte column-major block (key may be null).
-X16R_FN void aes_round(u8 s[16], const u8* key, const u8* sbox = kX16rAesSbox) {
-    u8 t[16];
-    for (int c = 0; c < 4; ++c)
-        for (int r = 0; r < 4; ++r) t[4 * c + r] = sbox[s[4 * ((c + r) & 3) + r]];
-    for (int c = 0; c < 4; ++c) {
-        const u8 a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
-        s[4 * c + 0] = u8(xtime(a0) ^ xtime(a1) ^ a1 ^ a2 ^ a3);
-        s[4 * c + 1] = u8(a0 ^ xtime(a1) ^ xtime(a2) ^ a2 ^ a3);
-        s[4 * c + 2] = u8(a0 ^ a1 ^ xtime(a2) ^ xtime(a3) ^ a3);
-        s[4 * c + 3] = u8(xtime(a0) ^ a0 ^ a1 ^ a2 ^ xtime(a3));
-    }
-    if (key)
-        for (int i = 0; i < 16; ++i) s[i] ^= key[i];
-}
+X16R_FN u32 xtime4(u32 v) { return ((v & 0x7F7F7F7Fu) << 1) ^ (((v >> 7) & 0x01010101u) * 0x1Bu); }
 
 // ================================================================ Groestl-512 (slot 2)
 // 16 u64 columns (row i in byte i); SubBytes + ShiftBytes + MixBytes as 8 table lookups per column.
@@ -545,18 +532,13 @@ X16R_FN void cubehash512(const u8* data, int n, u8* out) {
 }
 
 // ================================================================ SHAvite-3-512 (slot 8)
-X16R_FN void aes_words(u32 x[4], const u8* sbox) {
-    u8 b[16];
-    for (int i = 0; i < 4; ++i) st32(b + 4 * i, x[i]);
-    aes_round(b, nullptr, sbox);
-    for (int i = 0; i < 4; ++i) x[i] = ld32(b + 4 * i);
-}
+X16R_FN void aes_words(u32 x[4], const u32* T) { aes_round_w(x, 0, 0, T); }
 
 X16R_FN void shavite_inject(u32* rk, int u, const u32 cnt[4], int a, int b, int c, int d) {
     rk[u] ^= cnt[a]; rk[u + 1] ^= cnt[b]; rk[u + 2] ^= cnt[c]; rk[u + 3] ^= ~cnt[d];
 }
 
-X16R_FN void shavite_F(u32 L[4], const u32 R[4], const u32* rk, int& r_idx, const u8* sbox) {
+X16R_FN void shavite_F(u32 L[4], const u32 R[4], const u32* rk, int& r_idx, const u32* sbox) {
     u32 x[4];
     for (int k = 0; k < 4; ++k) x[k] = R[k] ^ rk[r_idx++];
     aes_words(x, sbox);
@@ -567,7 +549,7 @@ X16R_FN void shavite_F(u32 L[4], const u32 R[4], const u32* rk, int& r_idx, cons
     for (int k = 0; k < 4; ++k) L[k] ^= x[k];
 }
 
-X16R_FN void shavite_c512(u32 h[16], const u8 msg[128], const u32 cnt[4], const u8* sbox) {
+X16R_FN void shavite_c512(u32 h[16], const u8 msg[128], const u32 cnt[4], const u32* sbox) {
     u32 rk[448];
     for (int i = 0; i < 32; ++i) rk[i] = ld32(msg + 4 * i);
     int u = 32;
@@ -610,7 +592,7 @@ constexpr u32 kShaviteIV[16] = {0x72FCCDD8, 0x79CA4727, 0x128A077B, 0x40D55AEC, 
                                 0xB29F5CD1, 0xDF07FBFC, 0x8E45D73D, 0x681AB538, 0xBDE86578, 0xDD577E47,
                                 0xE275EADE, 0x502D9FCD, 0xB9357178, 0x022A4B9A};
 
-X16R_FN void shavite512(const u8* data, int n, u8* out, const u8* sbox = kX16rAesSbox) {  // 0 < n < 110
+X16R_FN void shavite512(const u8* data, int n, u8* out, const u32* sbox = kX16rAesT) {  // 0 < n < 110
     u32 h[16];
     for (int i = 0; i < 16; ++i) h[i] = kShaviteIV[i];
     const u64 bits = u64(n) * 8;
@@ -738,43 +720,43 @@ X16R_FN void simd512(const u8* data, int n, u8* out, int16_t* qb = nullptr, int 
 }
 
 // ================================================================ ECHO-512 (slot 10)
-X16R_FN void echo_compress(u8 v[8][16], const u8 m[128], u64 counter_bits, const u8* sbox) {
-    u8 w[16][16];
-    for (int i = 0; i < 8; ++i) cpy(w[i], v[i], 16);
-    for (int i = 0; i < 8; ++i) cpy(w[8 + i], m + 16 * i, 16);
+X16R_FN void echo_compress(u32 v[8][4], const u8 m[128], u64 counter_bits, const u32* T) {
+    u32 w[16][4];
+    for (int i = 0; i < 8; ++i)
+        for (int c = 0; c < 4; ++c) {
+            w[i][c] = v[i][c];
+            w[8 + i][c] = ld32(m + 16 * i + 4 * c);
+        }
     u64 k = counter_bits;
-    u8 salt[16];
-    zero(salt, 16);
     for (int r = 0; r < 10; ++r) {
         for (int i = 0; i < 16; ++i) {
-            u8 key[16];
-            zero(key, 16);
-            st64(key, k);
+            aes_round_w(w[i], u32(k), u32(k >> 32), T);
             ++k;
-            aes_round(w[i], key, sbox);
-            aes_round(w[i], salt, sbox);
+            aes_round_w(w[i], 0, 0, T);
         }
-        u8 t[16][16];
+        u32 t[16][4];
         for (int j = 0; j < 4; ++j)
-            for (int i = 0; i < 4; ++i) cpy(t[4 * j + i], w[4 * ((j + i) & 3) + i], 16);
+            for (int i = 0; i < 4; ++i)
+                for (int c = 0; c < 4; ++c) t[4 * j + i][c] = w[4 * ((j + i) & 3) + i][c];
         for (int j = 0; j < 4; ++j)
-            for (int b = 0; b < 16; ++b) {
-                const u8 a0 = t[4 * j][b], a1 = t[4 * j + 1][b], a2 = t[4 * j + 2][b], a3 = t[4 * j + 3][b];
-                w[4 * j + 0][b] = u8(xtime(a0) ^ xtime(a1) ^ a1 ^ a2 ^ a3);
-                w[4 * j + 1][b] = u8(a0 ^ xtime(a1) ^ xtime(a2) ^ a2 ^ a3);
-                w[4 * j + 2][b] = u8(a0 ^ a1 ^ xtime(a2) ^ xtime(a3) ^ a3);
-                w[4 * j + 3][b] = u8(xtime(a0) ^ a0 ^ a1 ^ a2 ^ xtime(a3));
+            for (int c = 0; c < 4; ++c) {
+                const u32 a0 = t[4 * j][c], a1 = t[4 * j + 1][c], a2 = t[4 * j + 2][c], a3 = t[4 * j + 3][c];
+                const u32 x0 = xtime4(a0), x1 = xtime4(a1), x2 = xtime4(a2), x3 = xtime4(a3);
+                w[4 * j + 0][c] = x0 ^ x1 ^ a1 ^ a2 ^ a3;
+                w[4 * j + 1][c] = a0 ^ x1 ^ x2 ^ a2 ^ a3;
+                w[4 * j + 2][c] = a0 ^ a1 ^ x2 ^ x3 ^ a3;
+                w[4 * j + 3][c] = x0 ^ a0 ^ a1 ^ a2 ^ x3;
             }
     }
     for (int i = 0; i < 8; ++i)
-        for (int b = 0; b < 16; ++b) v[i][b] ^= m[16 * i + b] ^ w[i][b] ^ w[8 + i][b];
+        for (int c = 0; c < 4; ++c) v[i][c] ^= ld32(m + 16 * i + 4 * c) ^ w[i][c] ^ w[8 + i][c];
 }
 
-X16R_FN void echo512(const u8* data, int n, u8* out, const u8* sbox = kX16rAesSbox) {  // 0 < n < 110
-    u8 v[8][16];
+X16R_FN void echo512(const u8* data, int n, u8* out, const u32* T = kX16rAesT) {  // 0 < n < 110
+    u32 v[8][4];
     for (int i = 0; i < 8; ++i) {
-        zero(v[i], 16);
-        v[i][1] = 0x02;
+        v[i][0] = 0x0200;  // 512, 128-bit little-endian
+        v[i][1] = v[i][2] = v[i][3] = 0;
     }
     const u64 bits = u64(n) * 8;
     u8 buf[128];
@@ -784,8 +766,9 @@ X16R_FN void echo512(const u8* data, int n, u8* out, const u8* sbox = kX16rAesSb
     buf[110] = 0x00;
     buf[111] = 0x02;
     st64(buf + 112, bits);
-    echo_compress(v, buf, bits, sbox);
-    for (int i = 0; i < 4; ++i) cpy(out + 16 * i, v[i], 16);
+    echo_compress(v, buf, bits, T);
+    for (int i = 0; i < 4; ++i)
+        for (int c = 0; c < 4; ++c) st32(out + 16 * i + 4 * c, v[i][c]);
 }
 
 // ================================================================ Hamsi-512 (slot 11)
@@ -873,25 +856,30 @@ X16R_FN void fugue_smix(u32& x0, u32& x1, u32& x2, u32& x3, const u32* mt) {
     x3 = ((c[3] ^ (r[0] << 24)) & 0xFF000000u) | ((c[0] ^ (r[1] >> 8)) & 0x00FF0000u) |
          ((c[1] ^ (r[2] >> 8)) & 0x0000FF00u) | ((c[2] ^ (r[3] >> 8)) & 0x000000FFu);
 }
-X16R_FN void fugue_ror(u32 S[36], int n) {
-    u32 t[36];
-    for (int i = 0; i < 36; ++i) t[(i + n) % 36] = S[i];
-    for (int i = 0; i < 36; ++i) S[i] = t[i];
+// The 36 columns as a ring: logical column i is R[(i + off) % 36], the RORs move `off`.
+struct FugueRing {
+    u32 R[36];
+    int off;
+};
+X16R_FN u32& fs(FugueRing& f, int i) {
+    const int j = i + f.off;
+    return f.R[j >= 36 ? j - 36 : j];
 }
-X16R_FN void fugue_cmix_sub(u32 S[36], const u32* mt) {
-    fugue_ror(S, 3);
-    S[0] ^= S[4]; S[1] ^= S[5]; S[2] ^= S[6];
-    S[18] ^= S[4]; S[19] ^= S[5]; S[20] ^= S[6];
-    fugue_smix(S[0], S[1], S[2], S[3], mt);
+X16R_FN void fugue_ror(FugueRing& f, int n) { f.off = f.off >= n ? f.off - n : f.off - n + 36; }
+X16R_FN void fugue_cmix_sub(FugueRing& f, const u32* mt) {
+    fugue_ror(f, 3);
+    fs(f, 0) ^= fs(f, 4); fs(f, 1) ^= fs(f, 5); fs(f, 2) ^= fs(f, 6);
+    fs(f, 18) ^= fs(f, 4); fs(f, 19) ^= fs(f, 5); fs(f, 20) ^= fs(f, 6);
+    fugue_smix(fs(f, 0), fs(f, 1), fs(f, 2), fs(f, 3), mt);
 }
-X16R_FN void fugue_word(u32 S[36], u32 I, const u32* mt) {
-    S[22] ^= S[0];
-    S[0] = I;
-    S[8] ^= S[0];
-    S[1] ^= S[24];
-    S[4] ^= S[27];
-    S[7] ^= S[30];
-    for (int k = 0; k < 4; ++k) fugue_cmix_sub(S, mt);
+X16R_FN void fugue_word(FugueRing& f, u32 I, const u32* mt) {
+    fs(f, 22) ^= fs(f, 0);
+    fs(f, 0) = I;
+    fs(f, 8) ^= fs(f, 0);
+    fs(f, 1) ^= fs(f, 24);
+    fs(f, 4) ^= fs(f, 27);
+    fs(f, 7) ^= fs(f, 30);
+    for (int k = 0; k < 4; ++k) fugue_cmix_sub(f, mt);
 }
 constexpr u32 kFugueIV[16] = {0x8807a57e, 0xe616af75, 0xc5d3e4db, 0xac9ab027, 0xd915f117, 0xb6eecc54,
                               0x06e8020b, 0x4a92efd1, 0xaac6e2c9, 0xddb21398, 0xcae65838, 0x437f203f,
@@ -900,27 +888,28 @@ constexpr int kFugueG[4][4] = {{4, 9, 18, 27}, {4, 10, 18, 27}, {4, 10, 19, 27},
 constexpr int kFugueOut[16] = {1, 2, 3, 4, 9, 10, 11, 12, 18, 19, 20, 21, 27, 28, 29, 30};
 
 X16R_FN void fugue512(const u8* data, int n, u8* out, const u32* mt = kX16rFugueMt) {
-    u32 S[36];
-    for (int i = 0; i < 36; ++i) S[i] = 0;
-    for (int i = 0; i < 16; ++i) S[20 + i] = kFugueIV[i];
+    FugueRing f;
+    f.off = 0;
+    for (int i = 0; i < 20; ++i) f.R[i] = 0;
+    for (int i = 0; i < 16; ++i) f.R[20 + i] = kFugueIV[i];
     const u64 bits = u64(n) * 8;
-    for (; n >= 4; n -= 4, data += 4) fugue_word(S, ldb32(data), mt);
+    for (; n >= 4; n -= 4, data += 4) fugue_word(f, ldb32(data), mt);
     if (n) {
         u8 w[4] = {0, 0, 0, 0};
         cpy(w, data, n);
-        fugue_word(S, ldb32(w), mt);
+        fugue_word(f, ldb32(w), mt);
     }
-    fugue_word(S, u32(bits >> 32), mt);
-    fugue_word(S, u32(bits), mt);
-    for (int i = 0; i < 32; ++i) fugue_cmix_sub(S, mt);
+    fugue_word(f, u32(bits >> 32), mt);
+    fugue_word(f, u32(bits), mt);
+    for (int i = 0; i < 32; ++i) fugue_cmix_sub(f, mt);
     for (int i = 0; i < 13; ++i)
         for (int k = 0; k < 4; ++k) {
-            for (int j = 0; j < 4; ++j) S[kFugueG[k][j]] ^= S[0];
-            fugue_ror(S, k == 3 ? 8 : 9);
-            fugue_smix(S[0], S[1], S[2], S[3], mt);
+            for (int j = 0; j < 4; ++j) fs(f, kFugueG[k][j]) ^= fs(f, 0);
+            fugue_ror(f, k == 3 ? 8 : 9);
+            fugue_smix(fs(f, 0), fs(f, 1), fs(f, 2), fs(f, 3), mt);
         }
-    for (int j = 0; j < 4; ++j) S[kFugueG[0][j]] ^= S[0];
-    for (int i = 0; i < 16; ++i) stb32(out + 4 * i, S[kFugueOut[i]]);
+    for (int j = 0; j < 4; ++j) fs(f, kFugueG[0][j]) ^= fs(f, 0);
+    for (int i = 0; i < 16; ++i) stb32(out + 4 * i, fs(f, kFugueOut[i]));
 }
 
 // ================================================================ Shabal-512 (slot 13)
