@@ -37,12 +37,18 @@ __device__ void x16r_group(const X16rStepParams& p) {
     __shared__ uint64_t t64[(kGroestl || kWhirl) ? 2048 : kTiger ? 1024 : 1];
     __shared__ uint32_t t32[(kFugue || kAes) ? 1024 : 1];
     __shared__ int16_t ntt[A == 9 ? 256 * X16R_BLOCK : 1];  // SIMD: each lane's NTT buffer, lanes interleaved
+    __shared__ int16_t simd_t[A == 9 ? 768 : 1];             // SIMD: 41^k mod 257 and the two y offsets
     if (kGroestl) x16r_stage<uint64_t, 2048>(t64, kX16rGroestlT);
     if (kWhirl) x16r_stage<uint64_t, 2048>(t64, kX16rWhirlT);
     if (kTiger) x16r_stage<uint64_t, 1024>(t64, kX16rTiger);
     if (kFugue) x16r_stage<uint32_t, 1024>(t32, kX16rFugueMt);
     if (kAes) x16r_stage<uint32_t, 1024>(t32, kX16rAesT);
-    if (kGroestl || kWhirl || kTiger || kFugue || kAes) __syncthreads();  // every thread, before any exits
+    if (A == 9) {
+        x16r_stage<int16_t, 256>(simd_t, kX16rSimdPw);
+        x16r_stage<int16_t, 256>(simd_t + 256, kX16rSimdYn);
+        x16r_stage<int16_t, 256>(simd_t + 512, kX16rSimdYf);
+    }
+    if (kGroestl || kWhirl || kTiger || kFugue || kAes || A == 9) __syncthreads();  // every thread, before any exits
 
     const int32_t lo = p.offsets[A], hi = p.offsets[A + 1];
     const int32_t k = lo + (int32_t)(blockIdx.x * X16R_BLOCK + threadIdx.x);
@@ -71,7 +77,7 @@ __device__ void x16r_group(const X16rStepParams& p) {
     } else if (kFugue) {
         x16rd::fugue512(in, len, out, t32);
     } else if (A == 9) {
-        x16rd::simd512(in, len, out, ntt + threadIdx.x, X16R_BLOCK);
+        x16rd::simd512(in, len, out, ntt + threadIdx.x, X16R_BLOCK, simd_t, simd_t + 256, simd_t + 512);
     } else if (A == 8) {
         x16rd::shavite512(in, len, out, t32);
     } else if (A == 10) {

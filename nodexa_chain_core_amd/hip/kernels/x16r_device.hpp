@@ -645,7 +645,8 @@ X16R_FN void simd_step(u32 A[8], u32 B[8], u32 C[8], u32 D[8], const u32 w[8], i
 // Q(i) is element i of the 256-entry NTT buffer `qb` spaced `qs` apart (the kernel interleaves the
 // buffers of a workgroup's lanes in LDS; the host self-check uses a local array, qs = 1).
 #define Q(i) qb[(i) * qs]
-X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t* qb, int qs) {
+X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t* qb, int qs, const int16_t* pw,
+                           const int16_t* yn, const int16_t* yf) {
     // 256-point NTT over Z_257 (root 41), radix 2, bit-reversed input
     for (int j = 0; j < 256; ++j) {
         int r = 0;
@@ -656,12 +657,12 @@ X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t*
         const int half = len / 2, stride = 256 / len;
         for (int i = 0; i < 256; i += len)
             for (int k = 0; k < half; ++k) {
-                const int u = Q(i + k), v = mod257(Q(i + k + half) * kX16rSimdPw[stride * k]);
+                const int u = Q(i + k), v = mod257(Q(i + k + half) * pw[stride * k]);
                 Q(i + k) = int16_t(mod257(u + v));
                 Q(i + k + half) = int16_t(mod257(u - v + 257));
             }
     }
-    const int16_t* yoff = last ? kX16rSimdYf : kX16rSimdYn;
+    const int16_t* yoff = last ? yf : yn;
     for (int i = 0; i < 256; ++i) {
         const int acc = mod257(Q(i) + yoff[i]);
         Q(i) = int16_t(acc <= 128 ? acc : acc - 257);
@@ -704,7 +705,8 @@ X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t*
 }
 #undef Q
 
-X16R_FN void simd512(const u8* data, int n, u8* out, int16_t* qb = nullptr, int qs = 1) {  // 0 < n < 128
+X16R_FN void simd512(const u8* data, int n, u8* out, int16_t* qb = nullptr, int qs = 1, const int16_t* pw = kX16rSimdPw,
+                     const int16_t* yn = kX16rSimdYn, const int16_t* yf = kX16rSimdYf) {  // 0 < n < 128
     int16_t local[256];
     if (qb == nullptr) qb = local;
     u32 st[32];
@@ -712,10 +714,10 @@ X16R_FN void simd512(const u8* data, int n, u8* out, int16_t* qb = nullptr, int 
     u8 buf[128];
     zero(buf, 128);
     cpy(buf, data, n);
-    simd_compress(st, buf, false, qb, qs);
+    simd_compress(st, buf, false, qb, qs, pw, yn, yf);
     zero(buf, 128);
     st64(buf, u64(n) * 8);
-    simd_compress(st, buf, true, qb, qs);
+    simd_compress(st, buf, true, qb, qs, pw, yn, yf);
     for (int i = 0; i < 16; ++i) st32(out + 4 * i, st[i]);
 }
 
@@ -856,30 +858,28 @@ X16R_FN void fugue_smix(u32& x0, u32& x1, u32& x2, u32& x3, const u32* mt) {
     x3 = ((c[3] ^ (r[0] << 24)) & 0xFF000000u) | ((c[0] ^ (r[1] >> 8)) & 0x00FF0000u) |
          ((c[1] ^ (r[2] >> 8)) & 0x0000FF00u) | ((c[2] ^ (r[3] >> 8)) & 0x000000FFu);
 }
-// The 36 columns as a ring: logical column i is R[(i + off) % 36], the RORs move `off`.
-struct FugueRing {
-    u32 R[36];
-    int off;
-};
-X16R_FN u32& fs(FugueRing& f, int i) {
-    const int j = i + f.off;
-    return f.R[j >= 36 ? j - 36 : j];
+// Physical rotations (the host keeps the columns as a ring with a moving offset; on the GPU a
+// runtime offset turns every column access into a scratch-memory access, while the unrolled
+// rotations stay in registers: 41 vs 271 us per 16k-header launch, profiles/README r5k).
+X16R_FN void fugue_ror(u32 S[36], int n) {
+    u32 t[36];
+    for (int i = 0; i < 36; ++i) t[(i + n) % 36] = S[i];
+    for (int i = 0; i < 36; ++i) S[i] = t[i];
 }
-X16R_FN void fugue_ror(FugueRing& f, int n) { f.off = f.off >= n ? f.off - n : f.off - n + 36; }
-X16R_FN void fugue_cmix_sub(FugueRing& f, const u32* mt) {
-    fugue_ror(f, 3);
-    fs(f, 0) ^= fs(f, 4); fs(f, 1) ^= fs(f, 5); fs(f, 2) ^= fs(f, 6);
-    fs(f, 18) ^= fs(f, 4); fs(f, 19) ^= fs(f, 5); fs(f, 20) ^= fs(f, 6);
-    fugue_smix(fs(f, 0), fs(f, 1), fs(f, 2), fs(f, 3), mt);
+X16R_FN void fugue_cmix_sub(u32 S[36], const u32* mt) {
+    fugue_ror(S, 3);
+    S[0] ^= S[4]; S[1] ^= S[5]; S[2] ^= S[6];
+    S[18] ^= S[4]; S[19] ^= S[5]; S[20] ^= S[6];
+    fugue_smix(S[0], S[1], S[2], S[3], mt);
 }
-X16R_FN void fugue_word(FugueRing& f, u32 I, const u32* mt) {
-    fs(f, 22) ^= fs(f, 0);
-    fs(f, 0) = I;
-    fs(f, 8) ^= fs(f, 0);
-    fs(f, 1) ^= fs(f, 24);
-    fs(f, 4) ^= fs(f, 27);
-    fs(f, 7) ^= fs(f, 30);
-    for (int k = 0; k < 4; ++k) fugue_cmix_sub(f, mt);
+X16R_FN void fugue_word(u32 S[36], u32 I, const u32* mt) {
+    S[22] ^= S[0];
+    S[0] = I;
+    S[8] ^= S[0];
+    S[1] ^= S[24];
+    S[4] ^= S[27];
+    S[7] ^= S[30];
+    for (int k = 0; k < 4; ++k) fugue_cmix_sub(S, mt);
 }
 constexpr u32 kFugueIV[16] = {0x8807a57e, 0xe616af75, 0xc5d3e4db, 0xac9ab027, 0xd915f117, 0xb6eecc54,
                               0x06e8020b, 0x4a92efd1, 0xaac6e2c9, 0xddb21398, 0xcae65838, 0x437f203f,
@@ -888,28 +888,27 @@ constexpr int kFugueG[4][4] = {{4, 9, 18, 27}, {4, 10, 18, 27}, {4, 10, 19, 27},
 constexpr int kFugueOut[16] = {1, 2, 3, 4, 9, 10, 11, 12, 18, 19, 20, 21, 27, 28, 29, 30};
 
 X16R_FN void fugue512(const u8* data, int n, u8* out, const u32* mt = kX16rFugueMt) {
-    FugueRing f;
-    f.off = 0;
-    for (int i = 0; i < 20; ++i) f.R[i] = 0;
-    for (int i = 0; i < 16; ++i) f.R[20 + i] = kFugueIV[i];
+    u32 S[36];
+    for (int i = 0; i < 36; ++i) S[i] = 0;
+    for (int i = 0; i < 16; ++i) S[20 + i] = kFugueIV[i];
     const u64 bits = u64(n) * 8;
-    for (; n >= 4; n -= 4, data += 4) fugue_word(f, ldb32(data), mt);
+    for (; n >= 4; n -= 4, data += 4) fugue_word(S, ldb32(data), mt);
     if (n) {
         u8 w[4] = {0, 0, 0, 0};
         cpy(w, data, n);
-        fugue_word(f, ldb32(w), mt);
+        fugue_word(S, ldb32(w), mt);
     }
-    fugue_word(f, u32(bits >> 32), mt);
-    fugue_word(f, u32(bits), mt);
-    for (int i = 0; i < 32; ++i) fugue_cmix_sub(f, mt);
+    fugue_word(S, u32(bits >> 32), mt);
+    fugue_word(S, u32(bits), mt);
+    for (int i = 0; i < 32; ++i) fugue_cmix_sub(S, mt);
     for (int i = 0; i < 13; ++i)
         for (int k = 0; k < 4; ++k) {
-            for (int j = 0; j < 4; ++j) fs(f, kFugueG[k][j]) ^= fs(f, 0);
-            fugue_ror(f, k == 3 ? 8 : 9);
-            fugue_smix(fs(f, 0), fs(f, 1), fs(f, 2), fs(f, 3), mt);
+            for (int j = 0; j < 4; ++j) S[kFugueG[k][j]] ^= S[0];
+            fugue_ror(S, k == 3 ? 8 : 9);
+            fugue_smix(S[0], S[1], S[2], S[3], mt);
         }
-    for (int j = 0; j < 4; ++j) fs(f, kFugueG[0][j]) ^= fs(f, 0);
-    for (int i = 0; i < 16; ++i) stb32(out + 4 * i, fs(f, kFugueOut[i]));
+    for (int j = 0; j < 4; ++j) S[kFugueG[0][j]] ^= S[0];
+    for (int i = 0; i < 16; ++i) stb32(out + 4 * i, S[kFugueOut[i]]);
 }
 
 // ================================================================ Shabal-512 (slot 13)
