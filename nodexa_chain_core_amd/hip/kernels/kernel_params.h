@@ -220,6 +220,21 @@ struct X16rStepParams {
     const int32_t* offsets;     // 17 entries: slot a owns order[offsets[a] .. offsets[a + 1])
     uint32_t n;
     uint32_t step;              // 0: hash the 80-byte header, else the 64-byte chain value
+    // search mode (tmpl != nullptr): header i is the 80-byte template with nNonce (bytes 76..79,
+    // little-endian) = start_nonce + i, and v2_all replaces the per-header flags
+    const uint8_t* tmpl;
+    uint32_t start_nonce;
+    uint32_t v2_all;
+};
+
+// x16r_hits: the lowest index i < n whose chain value (a little-endian uint256 in its first 32
+// bytes) is <= target, by atomicMin into *best (the host sets it to 0xffffffff first).
+struct X16rHitParams {
+    const uint8_t* state;       // n x 64 bytes
+    uint32_t* best;
+    uint32_t target[8];         // little-endian words, word 7 most significant
+    uint32_t n;
+    uint32_t pad;
 };
 
 // Batch SHA-256d (sha256d.hip). sha256d_batch: n messages of len bytes, stride bytes apart.

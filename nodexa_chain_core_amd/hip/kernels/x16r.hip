@@ -57,7 +57,8 @@ __device__ void x16r_group(const X16rStepParams& p) {
     if (i >= p.n) return;
     uint8_t in[80];
     const int len = p.step == 0 ? 80 : 64;
-    const uint4* src = (const uint4*)(p.step == 0 ? p.headers + (size_t)i * 80 : p.state + (size_t)i * 64);
+    const bool search = p.tmpl != nullptr;
+    const uint4* src = (const uint4*)(p.step != 0 ? p.state + (size_t)i * 64 : search ? p.tmpl : p.headers + (size_t)i * 80);
     for (int w = 0; w < len / 16; ++w) {
         const uint4 v = src[w];
         x16rd::st32(in + 16 * w, v.x);
@@ -65,8 +66,10 @@ __device__ void x16r_group(const X16rStepParams& p) {
         x16rd::st32(in + 16 * w + 8, v.z);
         x16rd::st32(in + 16 * w + 12, v.w);
     }
+    if (search && p.step == 0) x16rd::st32(in + 76, p.start_nonce + i);
+    const bool v2 = search ? p.v2_all != 0 : p.v2[i] != 0;
     uint8_t out[64];
-    if (kTiger && p.v2[i] != 0) {  // X16RV2: Tiger-192 first
+    if (kTiger && v2) {  // X16RV2: Tiger-192 first
         uint8_t t[64];
         x16rd::tiger192_padded(in, len, t, t64);
         x16rd::single(A, t, 64, out);
@@ -89,6 +92,22 @@ __device__ void x16r_group(const X16rStepParams& p) {
     for (int w = 0; w < 4; ++w)
         dst[w] = make_uint4(x16rd::ld32(out + 16 * w), x16rd::ld32(out + 16 * w + 4), x16rd::ld32(out + 16 * w + 8),
                             x16rd::ld32(out + 16 * w + 12));
+}
+
+extern "C" __global__ __launch_bounds__(256) void x16r_hits(X16rHitParams p) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    const uint4* h = (const uint4*)(p.state + (size_t)i * 64);
+    const uint4 lo = h[0], hi = h[1];
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    bool le = true;
+    for (int k = 7; k >= 0; --k) {
+        if (w[k] != p.target[k]) {
+            le = w[k] < p.target[k];
+            break;
+        }
+    }
+    if (le) atomicMin(p.best, i);
 }
 
 #define X16R_SLOT(A) \

@@ -433,6 +433,40 @@ PYBIND11_MODULE(_hip, m) {
         }
         for (int i = 0; i < S; ++i) check(hipStreamWaitEvent(st, f.done[i], 0), "hipStreamWaitEvent");
     });
+    // X16R / X16RV2 nonce search (x16r.hip, search mode): `count` headers from one 80-byte template
+    // with nNonce = start + i; every header of the window runs the same 16 slots (`slots_of_steps`,
+    // from the template's hashPrevBlock), one launch per step, then x16r_hits keeps the lowest index
+    // whose hash is <= the target. order: `count` identity indices; offsets: 16 x 17 (device).
+    m.def("launch_x16r_search", [](const std::vector<const Kernel*>& slots, const Kernel& hits, uintptr_t tmpl,
+                                   uintptr_t state, uintptr_t order, uintptr_t offsets,
+                                   const std::vector<int>& slots_of_steps, uint32_t start, uint32_t count, bool v2,
+                                   const std::string& target_le, uintptr_t best, uintptr_t stream) {
+        if (count == 0) return;
+        if (slots.size() != 16 || slots_of_steps.size() != 16 || target_le.size() != 32)
+            throw std::invalid_argument("16 slot kernels, 16 steps, 32-byte target");
+        X16rStepParams p{};
+        p.state = reinterpret_cast<uint8_t*>(state);
+        p.tmpl = reinterpret_cast<const uint8_t*>(tmpl);
+        p.start_nonce = start;
+        p.v2_all = v2 ? 1u : 0u;
+        p.n = count;
+        const hipStream_t st = as_stream(stream);
+        for (uint32_t s = 0; s < 16; ++s) {
+            const int a = slots_of_steps[s];
+            if (a < 0 || a > 15) throw std::invalid_argument("slot out of range");
+            p.step = s;
+            p.order = reinterpret_cast<const int32_t*>(order);
+            p.offsets = reinterpret_cast<const int32_t*>(offsets) + size_t(s) * 17;
+            const unsigned block = unsigned(slots[size_t(a)]->max_threads);
+            slots[size_t(a)]->launch_bytes(dim3((count + block - 1) / block), dim3(block), 0, st, &p, sizeof(p));
+        }
+        X16rHitParams h{};
+        h.state = reinterpret_cast<const uint8_t*>(state);
+        h.best = reinterpret_cast<uint32_t*>(best);
+        std::memcpy(h.target, target_le.data(), 32);
+        h.n = count;
+        hits.launch_bytes(dim3((count + 255) / 256), dim3(256), 0, st, &h, sizeof(h));
+    });
     m.def("sizeof_verify_job", [] { return sizeof(KawpowVerifyJob); });
     m.attr("KV_PROG_WORDS") = KV_PROG_WORDS;
     m.def("launch_kawpow_verify_light", [](const Kernel& k, uintptr_t light, uint32_t light_items, uintptr_t l1,

@@ -18,8 +18,9 @@ format and one two-slot device protocol carry every proof of work the chain know
   (le64(nonce) || 24 zero bytes) appended to the 80-byte header prefix; the GPU solves them in one
   launch sequence, verifies every solution on the device and the host keeps the solutions whose
   SHA256d(header) meets the boundary.
-* **X16R / X16RV2** (LegacyHostDevice): templates before the KawPow activation (the default on
-  regtest) scan the 32-bit nNonce on the host cores (csrc/pow/x16r.cpp).
+* **X16R / X16RV2** (LegacyGpuDevice on a GPU rank, LegacyHostDevice otherwise): templates before
+  the KawPow activation (the default on regtest) scan the 32-bit nNonce, 2^20 nonces per GPU
+  window (hip/kernels/x16r.hip, search mode) or 2^16 on the host cores (csrc/pow/x16r.cpp).
 
 `RankDevice` routes each slot to the device of its work packet's algorithm, so one loop, one set
 of collectives and one failure path serve every era of the chain; `FaultInjectingDevice`
@@ -55,6 +56,7 @@ ALGO_NAMES = ("kawpow", "equihash", "x16r", "x16rv2")
 
 EPOCH_PREBUILD_WINDOW = 120  # blocks before an epoch boundary at which the next DAG is prebuilt
 LEGACY_WINDOW = 1 << 16      # nNonce values per host X16R window
+LEGACY_GPU_WINDOW = 1 << 20  # nNonce values per GPU X16R window (~0.6 ms at 1.9 M hashes/s)
 EQ_SOLUTION_PREFIX = b"\xfd\x40\x05"  # CompactSize(1344) in front of the packed solution
 
 
@@ -446,6 +448,38 @@ class LegacyHostDevice:
 
     def close(self) -> None:
         pass
+
+
+class LegacyGpuDevice(LegacyHostDevice):
+    """The same X16R / X16RV2 windows on this rank's GPU (ops/x16r.X16rSearcher: every nonce of a
+    window runs the same 16 slots, one launch per step, the lowest hit kept on the device)."""
+
+    name = "gpu-x16r"
+
+    def __init__(self, device: int = 0, window: int = LEGACY_GPU_WINDOW):
+        super().__init__()
+        self.device = int(device)
+        self._window = int(window)
+        self._searcher = None
+
+    def window_for(self, work: Work, window: int) -> int:
+        return self._window
+
+    def wait(self, slot: int, timeout_s: float | None = None) -> SlotResult:
+        work, start, count, gen = self.meta[slot]
+        self.meta[slot] = None
+        if gen != self.generation:
+            return SlotResult(work.job_id, start, count, 0, [], 0.0, 1, work.algo)
+        count = min(count, (1 << 32) - start)
+        if self._searcher is None:
+            from ..ops.x16r import X16rSearcher
+
+            self._searcher = X16rSearcher(self.device, window=self._window)
+        t0 = time.perf_counter()
+        res, hashes = self._searcher.search(work.header, work.algo == ALGO_X16RV2, work.boundary[::-1], start, count)
+        dt = (time.perf_counter() - t0) * 1e3
+        shares = [LegacyShare(int(res[0]), bytes(res[1]))] if res is not None else []
+        return SlotResult(work.job_id, start, count, int(hashes), shares, dt, 0, work.algo)
 
 
 class RankDevice:

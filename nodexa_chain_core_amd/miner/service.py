@@ -1003,8 +1003,8 @@ def spawn_followers(gpus: list[int], port: int, cpu: bool = False, extra_env: di
 
 def make_rank_device(cpu: bool, device_index: int | None = None, collective_dag: bool = False, window: int = 4096,
                      fail_rate: float = 0.0, drop_rate: float = 0.0, seed: int = 0, eq_window: int = 1):
-    """This rank's RankDevice: GPU KawPow + GPU Equihash (built on first use), or the host
-    equivalents; -gpufailrate / -dropshare wrap it."""
+    """This rank's RankDevice: GPU KawPow + GPU Equihash (built on first use) + GPU X16R, or the
+    host equivalents; -gpufailrate / -dropshare wrap it."""
     from .equihash_search import EquihashCpuDevice
     from .search import CpuSearchDevice, FaultInjectingDevice, RankDevice
 
@@ -1012,11 +1012,11 @@ def make_rank_device(cpu: bool, device_index: int | None = None, collective_dag:
         dev = RankDevice(CpuSearchDevice(max_window=window), EquihashCpuDevice(eq_window))
     else:
         from .equihash_search import EquihashGpuDevice
-        from .search import GpuSearchDevice
+        from .search import GpuSearchDevice, LegacyGpuDevice
 
         idx = int(device_index or 0)
         dev = RankDevice(GpuSearchDevice(idx, collective_dag=collective_dag),
-                         equihash_factory=lambda: EquihashGpuDevice(idx))
+                         equihash_factory=lambda: EquihashGpuDevice(idx), legacy=LegacyGpuDevice(idx))
     if fail_rate or drop_rate:
         dev = FaultInjectingDevice(dev, fail_rate, drop_rate, seed=seed)
     return dev

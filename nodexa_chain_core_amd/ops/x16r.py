@@ -56,3 +56,55 @@ def x16r_hash_batch(headers: bytes | np.ndarray, v2: bool | np.ndarray = False, 
         h.launch_x16r_chain(ks, d_hdr.data_ptr(), state.data_ptr(), d_flags.data_ptr(), d_order.data_ptr(),
                             d_off.data_ptr(), offsets.reshape(-1).tolist(), n, runtime.current_stream_handle())
         return state[:, :32].cpu().numpy()
+
+
+class X16rSearcher:
+    """GPU nonce search of a legacy header (generateBlocks' loop, src/rpc/mining.cpp:141-149, as
+    `_core.x16r_search` does it on the host): every nonce of a window shares hashPrevBlock, so all
+    of them run the same slot at each of the 16 steps -- one launch per step over the whole window
+    -- and x16r_hits keeps the lowest nonce whose hash is <= the target."""
+
+    def __init__(self, device: int = 0, window: int = 1 << 20):
+        runtime.require_gpu()
+        self.device = int(device)
+        self.window = int(window)
+        self.h = runtime.hip()
+        self.slots = [runtime.static_kernel("x16r", f"x16r_step_{a}") for a in range(16)]
+        self.hits = runtime.static_kernel("x16r", "x16r_hits")
+        dev = torch.device("cuda", self.device)
+        with torch.cuda.device(dev):
+            self.state = torch.empty((self.window, 64), dtype=torch.uint8, device=dev)
+            self.order = torch.arange(self.window, dtype=torch.int32, device=dev)
+            self.offsets = torch.zeros((16, 17), dtype=torch.int32, device=dev)
+            self.tmpl = torch.empty(80, dtype=torch.uint8, device=dev)
+            self.best = torch.empty(1, dtype=torch.int32, device=dev)
+        self.dev = dev
+
+    def search(self, header80: bytes, v2: bool, target_le: bytes, start: int, count: int):
+        """((nonce, hash) or None, hashes done): the lowest nonce in [start, start + count) whose
+        X16R / X16RV2 hash (storage order) is <= target_le (little-endian uint256)."""
+        if len(header80) != 80 or len(target_le) != 32:
+            raise ValueError("80-byte header, 32-byte target")
+        start &= 0xFFFFFFFF
+        count = min(int(count), (1 << 32) - start)
+        sel = selections(np.frombuffer(header80, dtype=np.uint8).reshape(1, 80))[0].tolist()
+        offsets = np.zeros((16, 17), dtype=np.int32)
+        done = 0
+        with torch.cuda.device(self.dev):
+            s = runtime.current_stream_handle()
+            self.tmpl.copy_(torch.frombuffer(bytearray(header80), dtype=torch.uint8))
+            while done < count:
+                n = min(self.window, count - done)
+                for k in range(16):
+                    offsets[k, sel[k] + 1:] = n
+                    offsets[k, :sel[k] + 1] = 0
+                self.offsets.copy_(torch.from_numpy(offsets))
+                self.best.fill_(-1)
+                self.h.launch_x16r_search(self.slots, self.hits, self.tmpl.data_ptr(), self.state.data_ptr(),
+                                          self.order.data_ptr(), self.offsets.data_ptr(), sel, start + done, n,
+                                          bool(v2), bytes(target_le), self.best.data_ptr(), s)
+                best = int(self.best.cpu().numpy().view(np.uint32)[0])
+                if best != 0xFFFFFFFF:
+                    return (start + done + best, bytes(self.state[best, :32].cpu().numpy().tobytes())), done + best + 1
+                done += n
+        return None, done

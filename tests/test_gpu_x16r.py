@@ -59,3 +59,41 @@ def test_verify_headers_legacy_batch_on_gpu_matches_host(core, gpu):
     cpu_r = MV.verify_headers(params, hs, gpus=None)
     assert [(r["valid"], r["hash"]) for r in gpu_r] == [(r["valid"], r["hash"]) for r in cpu_r]
     assert 0 < sum(r["valid"] for r in gpu_r) < len(hs)
+
+
+def test_gpu_search_matches_host_search(core, gpu):
+    """X16rSearcher finds the same lowest nonce (and hash) as the host's x16r_search, over windows
+    that end with and without a hit, X16R and X16RV2."""
+    from nodexa_chain_core_amd.ops.x16r import X16rSearcher
+
+    s = X16rSearcher(0, window=4096)
+    rng = random.Random(8)
+    for v2 in (False, True):
+        hdr = rng.randbytes(80)
+        target = (1 << 248).to_bytes(32, "little")  # ~1 in 256 hashes
+        got, hashes = s.search(hdr, v2, target, 1000, 20000)
+        want, _ = core.x16r_search(hdr, v2, target, 1000, 20000)
+        assert got is not None and want is not None
+        assert (got[0], got[1]) == (int(want[0]), bytes(want[1]))
+        assert hashes == got[0] - 1000 + 1
+        none, n = s.search(hdr, v2, bytes(32), 0, 5000)  # nothing meets a zero target
+        assert none is None and n == 5000
+
+
+def test_node_miner_legacy_blocks_on_gpu(core, gpu):
+    """The mining loop's X16R / X16RV2 windows run on the GPU (LegacyGpuDevice) and find blocks
+    the host accepts."""
+    from nodexa_chain_core_amd.miner.search import ALGO_X16R, LegacyGpuDevice, Work
+
+    dev = LegacyGpuDevice(0, window=1 << 14)
+    hdr = bytearray(random.Random(2).randbytes(80))
+    boundary = ((1 << 256) // 64).to_bytes(32, "big")  # ~1 in 64
+    w = Work(header=bytes(hdr), boundary=boundary, height=5, algo=ALGO_X16R)
+    dev.submit(0, w, 0, 1 << 14)
+    r = dev.wait(0)
+    assert r.shares, r
+    sh = r.shares[0]
+    h = bytearray(hdr)
+    h[76:80] = sh.nonce.to_bytes(4, "little")
+    assert core.x16r(bytes(h), bytes(h[4:36])) == sh.block_hash
+    assert int.from_bytes(sh.block_hash, "little") <= int.from_bytes(boundary, "big")

@@ -45,6 +45,17 @@ def main() -> int:
             bad += bytes(got[i]) != (_core.x16rv2 if v2 else _core.x16r)(h, h[4:36])
         res["x16rv2" if v2 else "x16r"] = {"s": round(min(times), 4), "hashes_per_s": round(a.n / min(times)),
                                           "mismatches": bad}
+    # the nonce search (all nonces of a window run the same slots): a zero target scans every nonce
+    from nodexa_chain_core_amd.ops.x16r import X16rSearcher
+
+    srch = X16rSearcher(0, window=1 << 20)
+    hdr = bytes(hdrs[0])
+    srch.search(hdr, False, bytes(32), 0, 1 << 16)
+    for v2 in (False, True):
+        t = time.perf_counter()
+        hit, n = srch.search(hdr, v2, bytes(32), 0, 1 << 22)
+        dt = time.perf_counter() - t
+        res[("x16rv2" if v2 else "x16r") + "_search"] = {"nonces": n, "s": round(dt, 4), "hashes_per_s": round(n / dt)}
     print(json.dumps({"n": a.n, **res}), flush=True)
     return 0 if all(r["mismatches"] == 0 for r in res.values()) else 1
 
