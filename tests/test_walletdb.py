@@ -47,10 +47,15 @@ def _dbt(b: bytes, keep: list):
     return _DBT(ctypes.cast(buf, ctypes.c_void_p), len(b), 0, 0, 0, None, 0)
 
 
-def bdb_write(path: str, records, subdb: bytes = b"main", delete=()) -> None:
-    """A btree file written by libdb itself (DB->open(DB_BTREE, DB_CREATE), DB->put, DB->del)."""
+def bdb_write(path: str, records, subdb: bytes = b"main", delete=(), lorder: int = 0, pagesize: int = 0) -> None:
+    """A btree file written by libdb itself (DB->open(DB_BTREE, DB_CREATE), DB->put, DB->del);
+    `lorder` 4321 writes a big-endian file, `pagesize` overrides the page size."""
     db = ctypes.c_void_p()
     assert LIBDB.db_create(ctypes.byref(db), None, 0) == 0
+    if lorder:
+        assert LIBDB.__db_set_lorder(db, lorder) == 0
+    if pagesize:
+        assert LIBDB.__db_set_pagesize(db, pagesize) == 0
     assert LIBDB.__db_open_pp(db, None, path.encode(), subdb, 1, 1, 0o600) == 0  # DB_BTREE, DB_CREATE
     keep: list = []
     for k, v in records:
@@ -132,6 +137,18 @@ def test_bdb_reader_matches_libdb(core, tmp_path):
     assert dict(core.bdb_read(p, "other")) == other
     with pytest.raises(RuntimeError, match="no sub-database"):
         core.bdb_read(p, "nope")
+
+
+@needs_libdb
+@pytest.mark.parametrize("lorder,pagesize", [(4321, 0), (1234, 512), (4321, 65536)])
+def test_bdb_reader_byte_orders_and_page_sizes(core, tmp_path, lorder, pagesize):
+    """Big-endian files (a wallet.dat written on another host) and the smallest and largest page
+    sizes read back exactly."""
+    rng = random.Random(lorder + pagesize)
+    recs = {rng.randbytes(rng.randint(1, 30)): rng.randbytes(rng.choice([1, 40, 700, 5000])) for _ in range(400)}
+    p = str(tmp_path / "t.dat")
+    bdb_write(p, list(recs.items()), lorder=lorder, pagesize=pagesize)
+    assert dict(core.bdb_read(p, "main")) == recs
 
 
 @needs_libdb
