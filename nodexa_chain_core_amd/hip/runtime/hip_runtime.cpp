@@ -14,6 +14,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -30,32 +31,6 @@ void check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Side streams of one device for work that fans out and joins (the X16R slot kernels of a chain
-// step run side by side): created on first use, kept for the process; one event per stream.
-struct FanOut {
-    static constexpr int kStreams = 4;
-    hipStream_t streams[kStreams] = {};
-    hipEvent_t done[kStreams] = {};
-    hipEvent_t start = nullptr;
-};
-
-FanOut& fan_out() {
-    static std::mutex mu;
-    static std::unordered_map<int, std::unique_ptr<FanOut>> per_device;
-    int dev = 0;
-    check(hipGetDevice(&dev), "hipGetDevice");
-    std::lock_guard<std::mutex> g(mu);
-    auto& f = per_device[dev];
-    if (!f) {
-        f = std::make_unique<FanOut>();
-        for (int i = 0; i < FanOut::kStreams; ++i) {
-            check(hipStreamCreateWithFlags(&f->streams[i], hipStreamNonBlocking), "hipStreamCreateWithFlags");
-            check(hipEventCreateWithFlags(&f->done[i], hipEventDisableTiming), "hipEventCreateWithFlags");
-        }
-        check(hipEventCreateWithFlags(&f->start, hipEventDisableTiming), "hipEventCreateWithFlags");
-    }
-    return *f;
-}
 
 FastMod32 make_fastmod(uint32_t d) {
     if (d < 2) throw std::invalid_argument("fastmod divisor must be >= 2");
@@ -385,53 +360,34 @@ PYBIND11_MODULE(_hip, m) {
        py::arg("num_jobs"), py::arg("out"), py::arg("seeds"), py::arg("stream"), py::arg("per_row"),
        py::arg("search_header") = std::string(), py::arg("start_nonce") = 0, py::arg("search_boundary") = std::string(),
        py::arg("hits") = 0, py::arg("max_hits") = 0);
-    // X16R / X16RV2 (x16r.hip): the 16 chain steps of a batch, each as one launch per slot group that
-    // has headers (x16r_step_<slot>, 64-thread blocks), all queued on `stream` by this one call.
-    // order: 16 x n header indices grouped by slot, offsets: 16 x 17 group bounds (device copies;
-    // offsets_host is the same table for the grid sizes).
-    m.def("launch_x16r_chain", [](const std::vector<const Kernel*>& slots, uintptr_t headers, uintptr_t state,
-                                  uintptr_t v2, uintptr_t order, uintptr_t offsets,
-                                  const std::vector<int32_t>& offsets_host, uint32_t n, uintptr_t stream) {
+    // X16R / X16RV2 (x16r.hip): the 16 chain steps of a batch, each ONE launch with every slot group
+    // of the step (x16r_step_all, grid y = slot). order: 16 x n header indices grouped by slot,
+    // offsets: 16 x 17 group bounds (device copies; offsets_host is the same table, for the grids).
+    m.def("launch_x16r_chain_all", [](const Kernel& k, uintptr_t headers, uintptr_t state, uintptr_t v2,
+                                      uintptr_t order, uintptr_t offsets, const std::vector<int32_t>& offsets_host,
+                                      uint32_t n, uintptr_t stream) {
         if (n == 0) return;
-        if (slots.size() != 16 || offsets_host.size() != 16 * 17) throw std::invalid_argument("16 slot kernels, 16 x 17 offsets");
-        for (int s = 0; s < 16; ++s)
-            for (int a = 0; a <= 16; ++a) {
-                const int32_t v = offsets_host[size_t(s * 17 + a)];
-                if (v < 0 || uint32_t(v) > n || (a && v < offsets_host[size_t(s * 17 + a - 1)]))
-                    throw std::invalid_argument("X16R offsets out of order");
-            }
+        if (offsets_host.size() != 16 * 17) throw std::invalid_argument("16 x 17 offsets");
         X16rStepParams p{};
         p.headers = reinterpret_cast<const uint8_t*>(headers);
         p.state = reinterpret_cast<uint8_t*>(state);
         p.v2 = reinterpret_cast<const uint8_t*>(v2);
         p.n = n;
-        // the slot groups of a step are independent: they run side by side on the fan-out streams,
-        // and every stream waits for all of them before the next step (each header's next slot
-        // can be any of the 16); the caller's stream waits for the last step
         const hipStream_t st = as_stream(stream);
-        FanOut& f = fan_out();
-        constexpr int S = FanOut::kStreams;
-        check(hipEventRecord(f.start, st), "hipEventRecord");
-        for (int i = 0; i < S; ++i) check(hipStreamWaitEvent(f.streams[i], f.start, 0), "hipStreamWaitEvent");
+        const unsigned block = unsigned(k.max_threads);
         for (uint32_t s = 0; s < 16; ++s) {
+            int32_t maxg = 0;
+            for (int a = 0; a < 16; ++a) {
+                const int32_t lo = offsets_host[size_t(s * 17 + a)], hi = offsets_host[size_t(s * 17 + a + 1)];
+                if (lo < 0 || hi < lo || uint32_t(hi) > n) throw std::invalid_argument("X16R offsets out of order");
+                maxg = std::max(maxg, hi - lo);
+            }
+            if (maxg == 0) continue;
             p.step = s;
             p.order = reinterpret_cast<const int32_t*>(order) + size_t(s) * n;
             p.offsets = reinterpret_cast<const int32_t*>(offsets) + size_t(s) * 17;
-            int used = 0;
-            for (int a = 0; a < 16; ++a) {
-                const uint32_t cnt = uint32_t(offsets_host[size_t(s * 17 + a + 1)] - offsets_host[size_t(s * 17 + a)]);
-                if (cnt == 0) continue;
-                const unsigned block = unsigned(slots[size_t(a)]->max_threads);
-                slots[size_t(a)]->launch_bytes(dim3((cnt + block - 1) / block), dim3(block), 0, f.streams[used % S], &p,
-                                               sizeof(p));
-                ++used;
-            }
-            for (int i = 0; i < S; ++i) check(hipEventRecord(f.done[i], f.streams[i]), "hipEventRecord");
-            for (int i = 0; i < S; ++i)
-                for (int j = 0; j < S; ++j)
-                    if (i != j) check(hipStreamWaitEvent(f.streams[i], f.done[j], 0), "hipStreamWaitEvent");
+            k.launch_bytes(dim3((uint32_t(maxg) + block - 1) / block, 16), dim3(block), 0, st, &p, sizeof(p));
         }
-        for (int i = 0; i < S; ++i) check(hipStreamWaitEvent(st, f.done[i], 0), "hipStreamWaitEvent");
     });
     // X16R / X16RV2 nonce search (x16r.hip, search mode): `count` headers from one 80-byte template
     // with nNonce = start + i; every header of the window runs the same 16 slots (`slots_of_steps`,

@@ -57,7 +57,7 @@ def main() -> int:
         dt = time.perf_counter() - t
         res[("x16rv2" if v2 else "x16r") + "_search"] = {"nonces": n, "s": round(dt, 4), "hashes_per_s": round(n / dt)}
     print(json.dumps({"n": a.n, **res}), flush=True)
-    return 0 if all(r["mismatches"] == 0 for r in res.values()) else 1
+    return 0 if all(r.get("mismatches", 0) == 0 for r in res.values()) else 1
 
 
 if __name__ == "__main__":
