@@ -268,11 +268,87 @@ typedef uint32_t kw_mix_t __attribute__((ext_vector_type(32)));
 NX_DEV uint32_t kw_get(const kw_mix_t& m, uint32_t i) { return m[i & 31]; }
 NX_DEV void kw_set(kw_mix_t& m, uint32_t i, uint32_t v) { m[i & 31] = v; }
 
-// kl_math / kl_merge with a wave-uniform kind lower to scalar branches. Branch-free VALU selects
-// (every candidate computed, v_cndmask on the kind) were measured slower: 586 against 458 us per
-// launch (profiles/README r5g), so the branches stay.
-#define kw_math kl_math
-#define kw_merge kl_merge
+// Op dispatch: one shared handler table per kernel, called per op. The op and merge kinds are
+// wave-uniform, but as C++ switches they lower to scalar branch trees (~4 levels for the 11 math
+// kinds, each level a compare, a branch and the structurizer's flow blocks), and those trees were
+// 57 % of the kernel (profiles/README r5o: 711 -> 309 us with the kinds fixed). Branch-free VALU
+// selects cost more than they save (r5g: every candidate computed, 586 against 458 us). Instead the
+// kinds index 64-byte handler slots: `s_swappc_b64` into slot 4 * math + merge (math and the merge
+// of its result fused, one call per op) or 44 + merge (the cache and DAG merges), and the handler
+// returns with `s_setpc_b64`: two jumps per op whatever the kinds, bit-exact, 712 -> 518 us for
+// the 10k fixture's two launches (r5o). tools/check_jump_slots.py checks every slot's first
+// instruction in the built code object (tests/test_kernel_isa.py).
+//
+// Calling convention (registers pinned by the asm constraints, so the compiler moves the mix
+// words in and out around each call): v61 = a, v62 = b (clobbered by the clz handler), v63 = the
+// destination's old value in and the merged value out, v60 = the math result (in: the value of a
+// merge-only slot), s96 = the merge rotation, s[94:95] = the target, s[98:99] = the return address,
+// s97 = scratch. Every asm statement declares SCC clobbered: the dispatch's adds write it, and a
+// compare the compiler had scheduled across the call would otherwise branch on a stale value.
+#define KWM0 "v_add_u32_e32 v60, v61, v62\n"
+#define KWM1 "v_mul_lo_u32 v60, v61, v62\n"
+#define KWM2 "v_mul_hi_u32 v60, v61, v62\n"
+#define KWM3 "v_min_u32_e32 v60, v61, v62\n"
+#define KWM4 "v_sub_u32_e32 v60, 0, v62\n v_alignbit_b32 v60, v61, v61, v60\n"
+#define KWM5 "v_alignbit_b32 v60, v61, v61, v62\n"
+#define KWM6 "v_and_b32_e32 v60, v61, v62\n"
+#define KWM7 "v_or_b32_e32 v60, v61, v62\n"
+#define KWM8 "v_xor_b32_e32 v60, v61, v62\n"
+#define KWM9 "v_ffbh_u32_e32 v60, v61\n v_min_u32_e32 v60, 32, v60\n v_ffbh_u32_e32 v62, v62\n v_min_u32_e32 v62, 32, v62\n v_add_u32_e32 v60, v60, v62\n"
+#define KWM10 "v_bcnt_u32_b32 v60, v61, 0\n v_bcnt_u32_b32 v60, v62, v60\n"
+#define KWG0 "v_lshl_add_u32 v63, v63, 5, v63\n v_add_u32_e32 v63, v63, v60\n"
+#define KWG1 "v_xor_b32_e32 v63, v63, v60\n v_lshl_add_u32 v63, v63, 5, v63\n"
+#define KWG2 "s_sub_u32 s97, 0, s96\n v_alignbit_b32 v63, v63, v63, s97\n v_xor_b32_e32 v63, v63, v60\n"
+#define KWG3 "v_alignbit_b32 v63, v63, v63, s96\n v_xor_b32_e32 v63, v63, v60\n"
+#define KWS(n, body) ".org .Lkwt_tab%=+(" #n ")*64\n" body "s_setpc_b64 s[98:99]\n"
+#define KWS4(m, n0) KWS(n0, KWM##m KWG0) KWS(n0 + 1, KWM##m KWG1) KWS(n0 + 2, KWM##m KWG2) KWS(n0 + 3, KWM##m KWG3)
+
+// the table, jumped over once per wave; returns its address
+NX_DEV void kwt_table(uint32_t& lo, uint32_t& hi) {
+    asm volatile(
+        "s_getpc_b64 s[94:95]\n"
+        ".Lkwt_pc%=:\n"
+        "s_add_u32 %[lo], s94, .Lkwt_tab%=-.Lkwt_pc%=\n"
+        "s_addc_u32 %[hi], s95, 0\n"
+        "s_branch .Lkwt_end%=\n"
+        ".p2align 6\n"
+        ".Lkwt_tab%=:\n"
+        KWS4(0, 0) KWS4(1, 4) KWS4(2, 8) KWS4(3, 12) KWS4(4, 16) KWS4(5, 20) KWS4(6, 24) KWS4(7, 28)
+        KWS4(8, 32) KWS4(9, 36) KWS4(10, 40)
+        KWS(44, KWG0) KWS(45, KWG1) KWS(46, KWG2) KWS(47, KWG3)
+        ".org .Lkwt_tab%=+48*64\n"
+        ".Lkwt_end%=:\n"
+        : [lo] "=s"(lo), [hi] "=s"(hi)
+        :
+        : "s94", "s95", "scc");
+}
+
+// d = merge(d, math(a, b)) through fused slot 4 * min(kind, 10) + merge kind
+NX_DEV uint32_t kwt_op(uint32_t lo, uint32_t hi, uint32_t a, uint32_t b, uint32_t d, uint32_t kind, uint32_t mkind,
+                       uint32_t rot) {
+    const uint32_t off = ((kind < 10u ? kind : 10u) * 4u + (mkind & 3u)) << 6;
+    asm volatile(
+        "s_add_u32 s94, %[lo], %[off]\n"
+        "s_addc_u32 s95, %[hi], 0\n"
+        "s_swappc_b64 s[98:99], s[94:95]\n"
+        : "+{v63}"(d), "+{v62}"(b)
+        : "{v61}"(a), "{s96}"(rot), [lo] "s"(lo), [hi] "s"(hi), [off] "s"(off)
+        : "v60", "s94", "s95", "s97", "s98", "s99", "scc");
+    return d;
+}
+
+// d = merge(d, v) through merge-only slot 44 + merge kind
+NX_DEV uint32_t kwt_merge(uint32_t lo, uint32_t hi, uint32_t d, uint32_t v, uint32_t mkind, uint32_t rot) {
+    const uint32_t off = (44u + (mkind & 3u)) << 6;
+    asm volatile(
+        "s_add_u32 s94, %[lo], %[off]\n"
+        "s_addc_u32 s95, %[hi], 0\n"
+        "s_swappc_b64 s[98:99], s[94:95]\n"
+        : "+{v63}"(d)
+        : "{v60}"(v), "{s96}"(rot), [lo] "s"(lo), [hi] "s"(hi), [off] "s"(off)
+        : "s94", "s95", "s97", "s98", "s99", "scc");
+    return d;
+}
 
 extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(KawpowLightParams p) {
     __shared__ uint32_t l1[4096];
@@ -329,6 +405,8 @@ extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(Kawpo
         }
     }
     const uint4* dag = (const uint4*)p.dag;
+    uint32_t tlo, thi;
+    kwt_table(tlo, thi);
 #pragma unroll 1
     for (uint32_t r = 0; r < 64; ++r) {
         const uint32_t index = kl_mod(__shfl(mix[0], (int)(r & 15), 16), p.items);
@@ -342,21 +420,20 @@ extern "C" __global__ __launch_bounds__(KL_BLOCK) void kawpow_verify_waves(Kawpo
         for (int i = 0; i < 18; ++i) {
             if (i < 11) {
                 const uint32_t op = pw[i];
-                const uint32_t a = kw_get(mix, op);
                 const uint32_t dst = (op >> 8) & 31;
-                kw_set(mix, dst, kw_merge(kw_get(mix, dst), l1[a & 4095u], (op >> 16) & 3, op >> 24));
+                kw_set(mix, dst, kwt_merge(tlo, thi, kw_get(mix, dst), l1[kw_get(mix, op) & 4095u], (op >> 16) & 3, op >> 24));
             }
             const uint32_t op = pw[11 + i];
             const uint32_t mg = pw[29 + i];
-            const uint32_t v = kw_math(kw_get(mix, op), kw_get(mix, op >> 8), (op >> 16) & 15);
             const uint32_t dst = op >> 24;
-            kw_set(mix, dst, kw_merge(kw_get(mix, dst), v, mg & 3, mg >> 8));
+            kw_set(mix, dst, kwt_op(tlo, thi, kw_get(mix, op), kw_get(mix, op >> 8), kw_get(mix, dst), (op >> 16) & 15,
+                                    mg & 3, mg >> 8));
         }
         const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t op = pw[47 + i];
-            kw_set(mix, op, kw_merge(kw_get(mix, op), dw[i], (op >> 8) & 3, op >> 16));
+            kw_set(mix, op, kwt_merge(tlo, thi, kw_get(mix, op), dw[i], (op >> 8) & 3, op >> 16));
         }
     }
     uint32_t lh = 0x811c9dc5u;
