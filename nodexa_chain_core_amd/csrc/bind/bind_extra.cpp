@@ -5,6 +5,8 @@
 #include <pybind11/stl.h>
 
 #include <atomic>
+#include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <thread>
 
@@ -246,6 +248,42 @@ void bind_extra(py::module_& m) {
         return py::bytes(reinterpret_cast<const char*>(h.bytes), 64);
     });
     m.def("x16r_slot_available", &x16r_slot_available);
+    m.def("x16r_groups", [](const py::buffer& headers) {
+        // ops/x16r.x16r_hash_batch's launch tables: for each of the 16 steps, the headers grouped
+        // by the slot they run there (a stable counting sort on the step's hashPrevBlock nibble,
+        // GetHashSelection: nibble 48 + step = header byte 4 + (15 - step) / 2) as int32 bytes
+        // (16 x n), and each step's 17 group offsets
+        const py::buffer_info b = headers.request();
+        const size_t len = size_t(b.size * b.itemsize);
+        if (len % 80) throw std::invalid_argument("x16r_groups: 80-byte headers");
+        const size_t n = len / 80;
+        if (n > size_t(INT32_MAX)) throw std::invalid_argument("x16r_groups: too many headers");
+        const u8* h = static_cast<const u8*>(b.ptr);
+        std::string order(16 * n * 4, '\0');
+        std::vector<int32_t> offsets(16 * 17, 0);
+        {
+            py::gil_scoped_release rel;
+            int32_t* ord = reinterpret_cast<int32_t*>(order.data());
+            parallel_for_each(16, [&](size_t s) {
+                const size_t j = 15 - s, at = 4 + j / 2;
+                const bool high = j & 1;
+                int32_t* off = &offsets[s * 17];
+                for (size_t i = 0; i < n; ++i) {
+                    const u8 v = h[i * 80 + at];
+                    ++off[1 + (high ? v >> 4 : v & 15)];
+                }
+                for (int k = 0; k < 16; ++k) off[k + 1] += off[k];
+                int32_t pos[16];
+                std::memcpy(pos, off, sizeof(pos));
+                int32_t* o = ord + s * n;
+                for (size_t i = 0; i < n; ++i) {
+                    const u8 v = h[i * 80 + at];
+                    o[pos[high ? v >> 4 : v & 15]++] = int32_t(i);
+                }
+            }, 1);
+        }
+        return py::make_tuple(py::bytes(order), offsets);
+    }, py::arg("headers"));
 
     // ------------------------------------------------ HAVAL / Lyra2 (linked by the reference, unused by consensus)
     m.def("haval", [](const py::bytes& data, int passes, int out_bits) {

@@ -202,7 +202,13 @@ class Comm:
                 # drain the two-window pipeline every step (profiles/README r4b)
                 self.stream = torch.cuda.Stream(device=self.w.device, priority=-16)
             if self.group is None:
-                self.group = dist.new_group(ranks=list(range(self.w.world_size)), timeout=self.timeout)
+                # gloo connects the group's full mesh under the group timeout, and ranks reach this
+                # point seconds apart on a loaded host (a DAG build, a cold import): connect under the
+                # rendezvous timeout. Every collective stays bounded by self.timeout (_wait), and a
+                # dead gloo peer fails its pair at once.
+                conn = self.timeout if self.gpu else max(self.timeout,
+                                                         datetime.timedelta(seconds=self.W.rendezvous_timeout()))
+                self.group = dist.new_group(ranks=list(range(self.w.world_size)), timeout=conn)
 
     def abort(self) -> None:
         """Tear down the loop's communicator after a failure: RCCL kernels still waiting for a dead

@@ -3,8 +3,8 @@
 Reference: HashX16R / HashX16RV2 (src/hash.h:335-605) hash one header at a time on the CPU, the
 16-step algorithm order taken from hashPrevBlock (GetHashSelection, src/hash.h:320-327). Here a
 whole batch advances one step per launch (hip/kernels/x16r.hip): the host groups the headers of
-each step by the slot they run, once for the batch (numpy over the 16 selection nibbles of every
-header), and each step is one launch whose workgroup (x, slot) runs that slot over its group --
+each step by the slot they run, once for the batch (`_core.x16r_groups`: a counting sort on each
+step's selection nibble), and each step is one launch whose workgroup (x, slot) runs that slot over its group --
 every wave executes one primitive. (One kernel per slot, a step's 16 groups on 4 fan-out streams,
 measured 1.91 M against 2.27 M hashes/s: the groups are small and latency-bound, and 4 hardware
 queues ran them at most 4 at a time; profiles/README r5k.) The 16 launches are queued by one
@@ -15,6 +15,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from .. import _core
 from . import runtime
 
 
@@ -40,12 +41,11 @@ def x16r_hash_batch(headers: bytes | np.ndarray, v2: bool | np.ndarray = False, 
     if n == 0:
         return np.zeros((0, 32), dtype=np.uint8)
     flags = np.broadcast_to(np.asarray(v2, dtype=np.uint8), (n,)).copy()
-    sel = selections(hdr)
-    order = np.empty((16, n), dtype=np.int32)
-    offsets = np.zeros((16, 17), dtype=np.int32)
-    for s in range(16):
-        order[s] = np.argsort(sel[:, s], kind="stable")
-        offsets[s, 1:] = np.cumsum(np.bincount(sel[:, s], minlength=16))
+    # each step's slot groups: one native counting-sort pass per step (numpy's 16 argsorts took
+    # several ms of host time per batch, as long as the kernels of a 16k batch)
+    order_b, offsets = _core.x16r_groups(hdr)
+    order = np.frombuffer(order_b, dtype=np.int32).reshape(16, n).copy()
+    offsets = np.asarray(offsets, dtype=np.int32).reshape(16, 17)
     h = runtime.hip()
     dev = torch.device("cuda", device)
     with torch.cuda.device(dev):

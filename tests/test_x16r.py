@@ -39,3 +39,26 @@ def test_chains(v2):
         hdr, prev = bytes.fromhex(c["header"]), bytes.fromhex(c["prev"])
         got = (_core.x16rv2 if v2 else _core.x16r)(hdr, prev)
         assert got.hex() == c["x16rv2" if v2 else "x16r"]
+
+
+def test_x16r_groups_matches_selections():
+    """_core.x16r_groups (the GPU batch's launch tables) is a stable grouping of every step's
+    headers by the selection nibble ops/x16r.selections reads."""
+    import numpy as np
+
+    from nodexa_chain_core_amd import _core
+    from nodexa_chain_core_amd.ops.x16r import selections
+
+    rng = np.random.default_rng(4)
+    for n in (1, 7, 1000):
+        hdr = rng.integers(0, 256, size=(n, 80), dtype=np.uint8)
+        order_b, offsets = _core.x16r_groups(hdr)
+        order = np.frombuffer(order_b, dtype=np.int32).reshape(16, n)
+        offsets = np.asarray(offsets).reshape(16, 17)
+        sel = selections(hdr)
+        for s in range(16):
+            assert (order[s] == np.argsort(sel[:, s], kind="stable")).all()
+            assert (offsets[s, 1:] == np.cumsum(np.bincount(sel[:, s], minlength=16))).all()
+            assert offsets[s, 0] == 0
+    with pytest.raises(ValueError):
+        _core.x16r_groups(b"\0" * 79)
