@@ -86,7 +86,25 @@ def main() -> int:
                 for k in ("pack_ms", "issue_ms", "overlap_ms", "wait_ms", "accept_ms", "device_ms"):
                     stages[k].append(r[k])
     v.h = h
-    out = {"runs": a.runs, "median_ms": round(statistics.median(totals) * 1e3, 3),
+    # the host parts of the overlap and accept stages, each on its own (fresh batch / chain)
+    parts = collections.defaultdict(list)
+    for _ in range(a.runs):
+        chain = _core.HeaderChain(params)
+        b = _core.HeaderBatch.from_bytes(raw, act)
+        t = time.perf_counter()
+        b.materialize()
+        parts["materialize_ms"].append((time.perf_counter() - t) * 1e3)
+        r = process_batch_resident(_core.HeaderChain(params), _core.HeaderBatch.from_bytes(raw, act), adjusted, device=0)
+        hashes = v.early_host.numpy()[:len(headers) * 32].copy()
+        bits = v.early_host.numpy()[len(headers) * 32:len(headers) * 36].view("<u4").copy()
+        t = time.perf_counter()
+        prep = chain.prepare_batch(b, adjusted, hashes, bits)
+        parts["prepare_ms"].append((time.perf_counter() - t) * 1e3)
+        t = time.perf_counter()
+        chain.commit_batch(prep, len(headers))
+        parts["commit_ms"].append((time.perf_counter() - t) * 1e3)
+    out_parts = {k: round(statistics.median(x), 3) for k, x in parts.items()}
+    out = {"host_parts_ms": out_parts,"runs": a.runs, "median_ms": round(statistics.median(totals) * 1e3, 3),
            "headers_per_s": round(len(headers) / statistics.median(totals)),
            "stages_ms": {k: round(statistics.median(x), 3) for k, x in stages.items()},
            "runtime_calls_per_run": {k: {"n": c[0] // a.runs, "us": round(c[1] / a.runs * 1e6, 1)}
