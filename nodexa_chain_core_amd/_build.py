@@ -21,6 +21,8 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import contextlib
+import fcntl
 import glob
 import os
 import shutil
@@ -62,6 +64,53 @@ def _newer(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def _fresh(target: str, srcs: list[str]) -> bool:
+    """`target` exists and is newer than every source and header it is built from: nothing to
+    do, whether or not the intermediate objects exist (a gpurun snapshot ships the built .so files
+    but not build/)."""
+    return os.path.exists(target) and not _newer(target, srcs + _headers(CSRC) + _headers(HIPDIR))
+
+
+_LOCK_DEPTH = 0
+
+
+@contextlib.contextmanager
+def _build_lock():
+    """One build at a time across processes: the ranks of a torchrun job (bench.py builds before
+    the process group exists) and pytest workers all call the build; the first one builds, the
+    others wait on the lock and then find everything up to date. Re-entrant within a process."""
+    global _LOCK_DEPTH
+    if _LOCK_DEPTH:
+        _LOCK_DEPTH += 1
+        try:
+            yield
+        finally:
+            _LOCK_DEPTH -= 1
+        return
+    d = os.path.join(PKG, "..", "build")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, ".lock"), "a") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        _LOCK_DEPTH = 1
+        try:
+            yield
+        finally:
+            _LOCK_DEPTH = 0
+            fcntl.flock(f, fcntl.LOCK_UN)
+
+
+def _link(cmd: list[str], out: str) -> None:
+    """Link to a temporary name, then rename over `out`: a process that already mapped the old
+    library keeps its inode, and nobody ever opens a half-written one."""
+    tmp = f"{out}.tmp{os.getpid()}"
+    try:
+        _run(cmd + ["-o", tmp])
+        os.replace(tmp, out)
+    finally:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+
+
 def _headers(root: str) -> list[str]:
     return glob.glob(os.path.join(root, "**", "*.h*"), recursive=True)
 
@@ -98,9 +147,12 @@ def core_sources() -> list[str]:
 
 def build_core(force: bool = False, jobs: int = 8) -> str:
     out = os.path.join(PKG, "_core" + EXT)
-    objs = _compile_all(core_sources(), CXXFLAGS + _pybind_includes(), os.path.join(BUILD, "core"), jobs, force)
-    if force or _newer(out, objs):
-        _run(["g++", "-shared", "-o", out, *objs, "-pthread"])
+    with _build_lock():
+        if not force and _fresh(out, core_sources()):
+            return out
+        objs = _compile_all(core_sources(), CXXFLAGS + _pybind_includes(), os.path.join(BUILD, "core"), jobs, force)
+        if force or _newer(out, objs):
+            _link(["g++", "-shared", *objs, "-pthread"], out)
     return out
 
 
@@ -110,13 +162,16 @@ def build_bench(force: bool = False, jobs: int = 8) -> str:
     out_dir = os.path.join(PKG, "bin")
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.join(out_dir, "bench_nodexa")
-    core_objs = _compile_all(core_sources(), CXXFLAGS + _pybind_includes(), os.path.join(BUILD, "core"), jobs, force)
-    core_objs = [o for o in core_objs if "_bind_" not in os.path.basename(o)]
     bench_srcs = sorted(glob.glob(os.path.join(CSRC, "bench", "*.cpp")))
-    bench_objs = _compile_all(bench_srcs, CXXFLAGS, os.path.join(BUILD, "bench"), jobs, force)
-    objs = core_objs + bench_objs
-    if force or _newer(out, objs):
-        _run(["g++", "-o", out, *objs, "-pthread"])
+    with _build_lock():
+        if not force and _fresh(out, core_sources() + bench_srcs):
+            return out
+        core_objs = _compile_all(core_sources(), CXXFLAGS + _pybind_includes(), os.path.join(BUILD, "core"), jobs, force)
+        core_objs = [o for o in core_objs if "_bind_" not in os.path.basename(o)]
+        bench_objs = _compile_all(bench_srcs, CXXFLAGS, os.path.join(BUILD, "bench"), jobs, force)
+        objs = core_objs + bench_objs
+        if force or _newer(out, objs):
+            _link(["g++", *objs, "-pthread"], out)
     return out
 
 
@@ -169,10 +224,12 @@ def build_hip_runtime(force: bool = False, jobs: int = 8) -> str:
     # The runtime takes host data (light cache, generated program) from _core by
     # pointer/bytes, so it links no core objects: one epoch-context cache per process.
     flags = CXXFLAGS + _pybind_includes() + ["-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include")]
-    objs = _compile_all(srcs, flags, os.path.join(BUILD, "hip"), jobs, force)
-    if force or _newer(out, objs):
-        _run(["g++", "-shared", "-o", out, *objs, "-L" + tlib, "-lamdhip64",
-              "-Wl,-rpath," + tlib, "-pthread"])
+    with _build_lock():
+        if not force and _fresh(out, srcs):
+            return out
+        objs = _compile_all(srcs, flags, os.path.join(BUILD, "hip"), jobs, force)
+        if force or _newer(out, objs):
+            _link(["g++", "-shared", *objs, "-L" + tlib, "-lamdhip64", "-Wl,-rpath," + tlib, "-pthread"], out)
     return out
 
 
@@ -206,18 +263,29 @@ def build_kernels(force: bool = False, jobs: int = 8) -> list[str]:
         outs.append(o)
         if force or _newer(o, [s] + hdrs):
             todo.append((s, o))
-    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        for f in [ex.submit(hipcc_genco, s, o) for s, o in todo]:
+    def one(s: str, o: str) -> None:  # compiled under a temporary name, renamed over the old one
+        tmp = f"{o}.tmp{os.getpid()}"
+        try:
+            hipcc_genco(s, tmp)
+            os.replace(tmp, o)
+        finally:
+            if os.path.exists(tmp):
+                os.remove(tmp)
+
+    with _build_lock(), cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        todo = [(s, o) for s, o in todo if force or _newer(o, [s] + hdrs)]  # another process may have built them
+        for f in [ex.submit(one, s, o) for s, o in todo]:
             f.result()
     return outs
 
 
 def build_all(force: bool = False, jobs: int = 8, with_hip: bool = True) -> None:
-    build_core(force, jobs)
-    build_bench(force, jobs)
-    if with_hip:
-        build_hip_runtime(force, jobs)
-        build_kernels(force, jobs)
+    with _build_lock():
+        build_core(force, jobs)
+        build_bench(force, jobs)
+        if with_hip:
+            build_hip_runtime(force, jobs)
+            build_kernels(force, jobs)
 
 
 def main() -> None:
