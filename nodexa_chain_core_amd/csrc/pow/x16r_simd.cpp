@@ -55,11 +55,11 @@ struct SimdState {
     }
 };
 
-void simd_compress(u32 state[32], const u8 blk[128], bool last) {
+// y_i = sum_j blk[j] 41^(ij) mod 257 (the 128 bytes zero-extended to 256 points): radix-2
+// decimation-in-time NTT, bit-reversed input, 8 stages of 128 butterflies; then the X^255 (and, for
+// the final block, X^253) tweak and the centred lift to [-128, 128]
+void simd_expand(const u8 blk[128], bool last, int q[256]) {
     const SimdTables& T = simd_tables();
-    // y_i = sum_j blk[j] 41^(ij) mod 257 (the 128 bytes zero-extended to 256 points): radix-2
-    // decimation-in-time NTT, bit-reversed input, 8 stages of 128 butterflies
-    int q[256];
     for (int j = 0; j < 256; ++j) {
         int r = 0;
         for (int b = 0; b < 8; ++b) r |= ((j >> b) & 1) << (7 - b);
@@ -79,6 +79,27 @@ void simd_compress(u32 state[32], const u8 blk[128], bool last) {
         const int acc = (q[i] + yoff[i]) % 257;
         q[i] = acc <= 128 ? acc : acc - 257;
     }
+}
+
+// The final block of a 64- or 80-byte message (every X16R input) is its bit length and zeros:
+// its expansion is a constant, computed once (and emitted for the GPU, tools/x16r_gen_tables.cpp).
+struct SimdFinal {
+    int q64[256], q80[256];
+    SimdFinal() {
+        u8 blk[128] = {0};
+        store_le64(blk, 64 * 8);
+        simd_expand(blk, true, q64);
+        store_le64(blk, 80 * 8);
+        simd_expand(blk, true, q80);
+    }
+};
+
+const SimdFinal& simd_final() {
+    static const SimdFinal f;
+    return f;
+}
+
+void simd_rounds(u32 state[32], const u8 blk[128], const int q[256]) {
     // message words: 4 rounds x 8 steps x 8 lanes, from q pairs lifted by 185 / 233
     auto inner = [](int lo, int hi, int mm) { return (u32(lo * mm) & 0xFFFFu) + (u32(hi * mm) << 16); };
     static const int kSb[4][8] = {{4, 6, 0, 2, 7, 5, 3, 1}, {15, 11, 12, 8, 9, 13, 10, 14},
@@ -120,6 +141,12 @@ void simd_compress(u32 state[32], const u8 blk[128], bool last) {
     }
 }
 
+void simd_compress(u32 state[32], const u8 blk[128], bool last) {
+    int q[256];
+    simd_expand(blk, last, q);
+    simd_rounds(state, blk, q);
+}
+
 }  // namespace
 
 Hash512 simd512(const u8* data, size_t n) {
@@ -139,7 +166,10 @@ Hash512 simd512(const u8* data, size_t n) {
         std::memset(buf, 0, sizeof buf);
     }
     store_le64(buf, bits);
-    simd_compress(st, buf, true);
+    if (bits == 64 * 8 || bits == 80 * 8)
+        simd_rounds(st, buf, bits == 64 * 8 ? simd_final().q64 : simd_final().q80);
+    else
+        simd_compress(st, buf, true);
     Hash512 out;
     for (int i = 0; i < 16; ++i) store_le32(out.bytes + 4 * i, st[i]);
     return out;

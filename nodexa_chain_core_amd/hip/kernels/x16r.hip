@@ -122,7 +122,7 @@ extern "C" __global__ __launch_bounds__(256) void x16r_hits(X16rHitParams p) {
 #define X16R_SLOT(A)                                                                         \
     extern "C" __global__ __launch_bounds__(X16R_BLOCK) void x16r_step_##A(X16rStepParams p) {     \
         __shared__ uint64_t lds[x16r_lds_bytes<A>() / 8];                                        \
-        x16r_group<A>(p, lds);                                                                   \
+        [[clang::always_inline]] x16r_group<A>(p, lds);                                          \
     }
 X16R_SLOT(0) X16R_SLOT(1) X16R_SLOT(2) X16R_SLOT(3) X16R_SLOT(4) X16R_SLOT(5) X16R_SLOT(6) X16R_SLOT(7)
 X16R_SLOT(8) X16R_SLOT(9) X16R_SLOT(10) X16R_SLOT(11) X16R_SLOT(12) X16R_SLOT(13) X16R_SLOT(14) X16R_SLOT(15)
@@ -142,7 +142,7 @@ extern "C" __global__ __launch_bounds__(X16R_BLOCK) void x16r_step_all(X16rStepP
         case 6: x16r_group<6>(p, lds); break;
         case 7: x16r_group<7>(p, lds); break;
         case 8: x16r_group<8>(p, lds); break;
-        case 9: x16r_group<9>(p, lds); break;
+        case 9: [[clang::always_inline]] x16r_group<9>(p, lds); break;  // SIMD: too big for the inliner's budget
         case 10: x16r_group<10>(p, lds); break;
         case 11: x16r_group<11>(p, lds); break;
         case 12: x16r_group<12>(p, lds); break;

@@ -642,18 +642,36 @@ X16R_FN void simd_step(u32 A[8], u32 B[8], u32 C[8], u32 D[8], const u32 w[8], i
     }
 }
 
-// Q(i) is element i of the 256-entry NTT buffer `qb` spaced `qs` apart (the kernel interleaves the
-// buffers of a workgroup's lanes in LDS; the host self-check uses a local array, qs = 1).
+// The expanded message: element i of the 256-entry NTT buffer `qb` spaced `qs` apart (the kernel
+// interleaves the buffers of a workgroup's lanes in LDS; the host self-check uses a local array,
+// qs = 1).
+// `n64`: only bytes 0..63 of the block can be nonzero (a 64-byte input's message block). Their
+// bit-reversed positions are the multiples of 4, so the first two butterfly stages only copy each
+// of them over its group of four: the NTT starts at the third stage.
+X16R_FN void simd_expand(const u8 blk[128], bool last, int16_t* qb, int qs, const int16_t* pw, const int16_t* yn,
+                         const int16_t* yf, bool n64 = false) {
 #define Q(i) qb[(i) * qs]
-X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t* qb, int qs, const int16_t* pw,
-                           const int16_t* yn, const int16_t* yf) {
     // 256-point NTT over Z_257 (root 41), radix 2, bit-reversed input
-    for (int j = 0; j < 256; ++j) {
-        int r = 0;
-        for (int b = 0; b < 8; ++b) r |= ((j >> b) & 1) << (7 - b);
-        Q(r) = int16_t(j < 128 ? int(blk[j]) : 0);
+    int len = 2;
+    if (n64) {
+        for (int j = 0; j < 64; ++j) {
+            int r = 0;
+            for (int b = 0; b < 6; ++b) r |= ((j >> b) & 1) << (7 - b);
+            const int16_t v = int16_t(blk[j]);
+            Q(r) = v;
+            Q(r + 1) = v;
+            Q(r + 2) = v;
+            Q(r + 3) = v;
+        }
+        len = 8;
+    } else {
+        for (int j = 0; j < 256; ++j) {
+            int r = 0;
+            for (int b = 0; b < 8; ++b) r |= ((j >> b) & 1) << (7 - b);
+            Q(r) = int16_t(j < 128 ? int(blk[j]) : 0);
+        }
     }
-    for (int len = 2; len <= 256; len <<= 1) {
+    for (; len <= 256; len <<= 1) {
         const int half = len / 2, stride = 256 / len;
         for (int i = 0; i < 256; i += len)
             for (int k = 0; k < half; ++k) {
@@ -667,6 +685,14 @@ X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t*
         const int acc = mod257(Q(i) + yoff[i]);
         Q(i) = int16_t(acc <= 128 ? acc : acc - 257);
     }
+#undef Q
+}
+
+// The four rounds and the feed-forward; q(i) returns expanded-message element i. For the final
+// block of a 64-byte input q reads its constant expansion (kX16rSimdFin64, made by the host,
+// x16r_simd.cpp): with the rounds unrolled every message word is then a literal.
+template <class QF>
+X16R_FN __attribute__((always_inline)) void simd_rounds(u32 state[32], const u8 blk[128], QF q) {
     u32 A[8], B[8], C[8], D[8], saved[32];
     for (int i = 0; i < 32; ++i) saved[i] = state[i];
     for (int i = 0; i < 8; ++i) {
@@ -683,12 +709,13 @@ X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t*
         for (int j = 0; j < 8; ++j) {
             const int sb = kSimdSb[r][j];
             u32 w[8];
+#pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (r < 2) {
-                    w[k] = simd_inner(Q(16 * sb + 2 * k), Q(16 * sb + 2 * k + 1), 185);
+                    w[k] = simd_inner(q(16 * sb + 2 * k), q(16 * sb + 2 * k + 1), 185);
                 } else {
                     const int base = 16 * (sb - 8 * r) + 2 * k + (r == 3 ? 1 : 0);
-                    w[k] = simd_inner(Q(base), Q(base + 128), 233);
+                    w[k] = simd_inner(q(base), q(base + 128), 233);
                 }
             }
             simd_step(A, B, C, D, w, j >= 4, kSimdRot[r][j & 3], kSimdRot[r][(j + 1) & 3], kSimdPerm[(j + r) % 7]);
@@ -703,21 +730,41 @@ X16R_FN void simd_compress(u32 state[32], const u8 blk[128], bool last, int16_t*
         state[24 + i] = D[i];
     }
 }
-#undef Q
 
-X16R_FN void simd512(const u8* data, int n, u8* out, int16_t* qb = nullptr, int qs = 1, const int16_t* pw = kX16rSimdPw,
-                     const int16_t* yn = kX16rSimdYn, const int16_t* yf = kX16rSimdYf) {  // 0 < n < 128
-    int16_t local[256];
-    if (qb == nullptr) qb = local;
+struct SimdQBuf {  // the expansion in the NTT buffer
+    const int16_t* qb;
+    int qs;
+    X16R_FN int operator()(int i) const { return qb[i * qs]; }
+};
+struct SimdQFin64 {  // the constant expansion of a 64-byte input's final block
+    X16R_FN int operator()(int i) const { return kX16rSimdFin64[i]; }
+};
+
+// qb: the lane's NTT buffer (the kernel's LDS, lanes interleaved qs apart; a local array in single())
+X16R_FN __attribute__((always_inline)) void simd512(const u8* data, int n, u8* out, int16_t* qb, int qs = 1,
+                                                    const int16_t* pw = kX16rSimdPw, const int16_t* yn = kX16rSimdYn,
+                                                    const int16_t* yf = kX16rSimdYf) {  // 0 < n < 128
     u32 st[32];
     for (int i = 0; i < 32; ++i) st[i] = kSimdIV[i];
     u8 buf[128];
-    zero(buf, 128);
-    cpy(buf, data, n);
-    simd_compress(st, buf, false, qb, qs, pw, yn, yf);
-    zero(buf, 128);
-    st64(buf, u64(n) * 8);
-    simd_compress(st, buf, true, qb, qs, pw, yn, yf);
+    // the message block, then the final (length) block: one copy of the rounds over the NTT buffer
+    // serves both (the loop is kept rolled); a 64-byte input's final block -- X16R steps 1..15 --
+    // takes the constant expansion instead of a second NTT
+#pragma unroll 1
+    for (int b = 0; b < 2; ++b) {
+        zero(buf, 128);
+        if (b == 0) {
+            cpy(buf, data, n);
+        } else {
+            st64(buf, u64(n) * 8);
+            if (n == 64) {
+                simd_rounds(st, buf, SimdQFin64{});
+                break;
+            }
+        }
+        simd_expand(buf, b == 1, qb, qs, pw, yn, yf, b == 0 && n == 64);
+        simd_rounds(st, buf, SimdQBuf{qb, qs});
+    }
     for (int i = 0; i < 16; ++i) st32(out + 4 * i, st[i]);
 }
 
@@ -1110,7 +1157,11 @@ X16R_FN void single(int algo, const u8* in, int n, u8* out) {
         case 6: luffa512(in, n, out); break;
         case 7: cubehash512(in, n, out); break;
         case 8: shavite512(in, n, out); break;
-        case 9: simd512(in, n, out); break;
+        case 9: {
+            int16_t q[256];
+            simd512(in, n, out, q);
+            break;
+        }
         case 10: echo512(in, n, out); break;
         case 11: hamsi512(in, n, out); break;
         case 12: fugue512(in, n, out); break;
