@@ -645,6 +645,9 @@ X16R_FN void simd_step(u32 A[8], u32 B[8], u32 C[8], u32 D[8], const u32 w[8], i
 // The expanded message: element i of the 256-entry NTT buffer `qb` spaced `qs` apart (the kernel
 // interleaves the buffers of a workgroup's lanes in LDS; the host self-check uses a local array,
 // qs = 1).
+#ifndef SIMD_NTT_BATCH
+#define SIMD_NTT_BATCH 8
+#endif
 // `n64`: only bytes 0..63 of the block can be nonzero (a 64-byte input's message block). Their
 // bit-reversed positions are the multiples of 4, so the first two butterfly stages only copy each
 // of them over its group of four: the NTT starts at the third stage.
@@ -671,14 +674,27 @@ X16R_FN void simd_expand(const u8 blk[128], bool last, int16_t* qb, int qs, cons
             Q(r) = int16_t(j < 128 ? int(blk[j]) : 0);
         }
     }
+    // a stage's 128 butterflies are independent: SIMD_NTT_BATCH of them at a time, every load before
+    // any store, so that many LDS round trips are in flight at once (one lane's NTT is otherwise a
+    // chain of dependent LDS accesses, and a step runs one wave per SIMD: nothing hides them)
     for (; len <= 256; len <<= 1) {
-        const int half = len / 2, stride = 256 / len;
-        for (int i = 0; i < 256; i += len)
-            for (int k = 0; k < half; ++k) {
-                const int u = Q(i + k), v = mod257(Q(i + k + half) * pw[stride * k]);
-                Q(i + k) = int16_t(mod257(u + v));
-                Q(i + k + half) = int16_t(mod257(u - v + 257));
+        const int half = len / 2, lg = __builtin_ctz(unsigned(half)), stride = 256 / len;
+        for (int b0 = 0; b0 < 128; b0 += SIMD_NTT_BATCH) {
+            int lo[SIMD_NTT_BATCH], u[SIMD_NTT_BATCH], v[SIMD_NTT_BATCH];
+#pragma unroll
+            for (int t = 0; t < SIMD_NTT_BATCH; ++t) {
+                const int b = b0 + t, k = b & (half - 1);
+                lo[t] = ((b >> lg) << (lg + 1)) + k;
+                u[t] = Q(lo[t]);
+                v[t] = Q(lo[t] + half) * pw[stride * k];
             }
+#pragma unroll
+            for (int t = 0; t < SIMD_NTT_BATCH; ++t) {
+                const int w = mod257(v[t]);
+                Q(lo[t]) = int16_t(mod257(u[t] + w));
+                Q(lo[t] + half) = int16_t(mod257(u[t] - w + 257));
+            }
+        }
     }
     const int16_t* yoff = last ? yf : yn;
     for (int i = 0; i < 256; ++i) {

@@ -23,19 +23,27 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 14)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--hsaco", default=None, help="an x16r code object to use instead of kernels/x16r.hsaco")
+    ap.add_argument("--slots", nargs="*", type=int, default=list(range(16)))
     a = ap.parse_args()
 
     import numpy as np
     import torch
 
+    from nodexa_chain_core_amd.ops import runtime
     from nodexa_chain_core_amd.ops.x16r import selections, x16r_hash_batch
+
+    if a.hsaco:  # A/B of a variant build: ops/x16r.py looks its kernels up through static_kernel
+        co = runtime.load_code_object(a.hsaco)
+        base_static = runtime.static_kernel
+        runtime.static_kernel = lambda m, n: co.function(n) if m == "x16r" else base_static(m, n)
 
     rng = np.random.default_rng(11)
     base = rng.integers(0, 256, size=(a.n, 80), dtype=np.uint8)
     x16r_hash_batch(base[:256])
     torch.cuda.synchronize()
     out = {}
-    for slot in range(16):
+    for slot in a.slots:
         hdr = base.copy()
         hdr[:, 4:12] = (slot << 4) | slot  # nibbles 48..63 of hashPrevBlock
         assert (selections(hdr[:4]) == slot).all()
@@ -45,7 +53,13 @@ def main() -> int:
             x16r_hash_batch(hdr)
             ts.append(time.perf_counter() - t)
         out[NAMES[slot]] = round(min(ts) / 16 * 1e3, 3)
-    print(json.dumps({"n": a.n, "ms_per_step": out}), flush=True)
+    ts = []
+    for _ in range(a.reps):  # the random batch (every slot mixed)
+        t = time.perf_counter()
+        x16r_hash_batch(base)
+        ts.append(time.perf_counter() - t)
+    print(json.dumps({"n": a.n, "hsaco": a.hsaco, "ms_per_step": out,
+                      "mixed_hashes_per_s": round(a.n / min(ts))}), flush=True)
     return 0
 
 
