@@ -11,6 +11,7 @@
 //   V7  jump-table merges, branch-tree math
 //   V8  jump-table math, branch-tree merges
 //   V9  one shared handler table called per op (math + merge fused): kwt_* of the shipping kernel
+//   V10 V9 + a cache op fused into the math op after it when their registers do not overlap
 #include "kawpow_verify_light.hip"
 
 // kind-indexed handler slots inside one asm block: s_getpc gives the address after itself, the
@@ -82,6 +83,53 @@ NX_DEV uint32_t pj_merge(uint32_t a, uint32_t b, uint32_t kind, uint32_t rot) {
     return d;
 }
 
+
+
+// ---- V10: V9's table plus 176 fused slots (cache merge gc, math m, merge gm) at 48 + 44 gc + 4 m + gm:
+// a cache op and the math op after it in one call when the cache op's destination is none of the
+// math op's registers (else the two V9 calls). Extra registers: v59 = the cache destination's
+// value in and out, v58 = the L1 word, s93 = the cache merge rotation.
+#define KWC0 "v_lshl_add_u32 v59, v59, 5, v59\n v_add_u32_e32 v59, v59, v58\n"
+#define KWC1 "v_xor_b32_e32 v59, v59, v58\n v_lshl_add_u32 v59, v59, 5, v59\n"
+#define KWC2 "s_sub_u32 s97, 0, s93\n v_alignbit_b32 v59, v59, v59, s97\n v_xor_b32_e32 v59, v59, v58\n"
+#define KWC3 "v_alignbit_b32 v59, v59, v59, s93\n v_xor_b32_e32 v59, v59, v58\n"
+#define KWF4(c, m, n0) KWS(n0, KWC##c KWM##m KWG0) KWS(n0 + 1, KWC##c KWM##m KWG1) KWS(n0 + 2, KWC##c KWM##m KWG2) \
+    KWS(n0 + 3, KWC##c KWM##m KWG3)
+#define KWF44(c, n0) KWF4(c, 0, n0) KWF4(c, 1, n0 + 4) KWF4(c, 2, n0 + 8) KWF4(c, 3, n0 + 12) KWF4(c, 4, n0 + 16) \
+    KWF4(c, 5, n0 + 20) KWF4(c, 6, n0 + 24) KWF4(c, 7, n0 + 28) KWF4(c, 8, n0 + 32) KWF4(c, 9, n0 + 36) KWF4(c, 10, n0 + 40)
+
+NX_DEV void kwt2_table(uint32_t& lo, uint32_t& hi) {
+    asm volatile(
+        "s_getpc_b64 s[94:95]\n"
+        ".Lkwt_pc%=:\n"
+        "s_add_u32 %[lo], s94, .Lkwt_tab%=-.Lkwt_pc%=\n"
+        "s_addc_u32 %[hi], s95, 0\n"
+        "s_branch .Lkwt_end%=\n"
+        ".p2align 6\n"
+        ".Lkwt_tab%=:\n"
+        KWS4(0, 0) KWS4(1, 4) KWS4(2, 8) KWS4(3, 12) KWS4(4, 16) KWS4(5, 20) KWS4(6, 24) KWS4(7, 28)
+        KWS4(8, 32) KWS4(9, 36) KWS4(10, 40)
+        KWS(44, KWG0) KWS(45, KWG1) KWS(46, KWG2) KWS(47, KWG3)
+        KWF44(0, 48) KWF44(1, 92) KWF44(2, 136) KWF44(3, 180)
+        ".org .Lkwt_tab%=+224*64\n"
+        ".Lkwt_end%=:\n"
+        : [lo] "=s"(lo), [hi] "=s"(hi)
+        :
+        : "s94", "s95", "scc");
+}
+
+// dc = merge_c(dc, lv); d = merge_m(d, math(a, b)) in one call
+NX_DEV void kwt_fused(uint32_t lo, uint32_t hi, uint32_t a, uint32_t b, uint32_t& d, uint32_t& dc, uint32_t lv,
+                      uint32_t ckind, uint32_t crot, uint32_t kind, uint32_t mkind, uint32_t rot) {
+    const uint32_t off = (48u + (ckind & 3u) * 44u + (kind < 10u ? kind : 10u) * 4u + (mkind & 3u)) << 6;
+    asm volatile(
+        "s_add_u32 s94, %[lo], %[off]\n"
+        "s_addc_u32 s95, %[hi], 0\n"
+        "s_swappc_b64 s[98:99], s[94:95]\n"
+        : "+{v63}"(d), "+{v62}"(b), "+{v59}"(dc)
+        : "{v61}"(a), "{v58}"(lv), "{s96}"(rot), "{s93}"(crot), [lo] "s"(lo), [hi] "s"(hi), [off] "s"(off)
+        : "v60", "s94", "s95", "s97", "s98", "s99", "scc");
+}
 
 template <int V>
 NX_DEV uint32_t pv_merge(uint32_t a, uint32_t b, uint32_t kind, uint32_t rot) {
@@ -166,6 +214,7 @@ NX_DEV void pv_waves(const KawpowLightParams& p) {
     const uint4* dag = (const uint4*)p.dag;
     uint32_t tlo = 0, thi = 0;
     if constexpr (V == 9) kwt_table(tlo, thi);
+    if constexpr (V == 10) kwt2_table(tlo, thi);
 #pragma unroll 1
     for (uint32_t r = 0; r < 64; ++r) {
         const uint32_t index = kl_mod(__shfl(mix[0], (int)(r & 15), 16), p.items);
@@ -174,6 +223,37 @@ NX_DEV void pv_waves(const KawpowLightParams& p) {
         else d = dag[(size_t)index * 16 + ((lane ^ r) & 15)];
 #pragma unroll
         for (int i = 0; i < 51; ++i) asm volatile("" : "+s"(pw[i]));
+        if constexpr (V == 10) {
+#pragma unroll
+            for (int i = 0; i < 18; ++i) {
+                const uint32_t op = pw[11 + i];
+                const uint32_t mg = pw[29 + i];
+                const uint32_t dst = op >> 24;
+                if (i < 11) {
+                    const uint32_t opc = pw[i];
+                    const uint32_t dc = (opc >> 8) & 31;
+                    const uint32_t lv = l1[kw_get(mix, opc) & 4095u];
+                    if (dc != (op & 31) && dc != ((op >> 8) & 31) && dc != (dst & 31)) {
+                        uint32_t d = kw_get(mix, dst), vc = kw_get(mix, dc);
+                        kwt_fused(tlo, thi, kw_get(mix, op), kw_get(mix, op >> 8), d, vc, lv, (opc >> 16) & 3, opc >> 24,
+                                  (op >> 16) & 15, mg & 3, mg >> 8);
+                        kw_set(mix, dc, vc);
+                        kw_set(mix, dst, d);
+                        continue;
+                    }
+                    kw_set(mix, dc, kwt_merge(tlo, thi, kw_get(mix, dc), lv, (opc >> 16) & 3, opc >> 24));
+                }
+                kw_set(mix, dst, kwt_op(tlo, thi, kw_get(mix, op), kw_get(mix, op >> 8), kw_get(mix, dst), (op >> 16) & 15,
+                                        mg & 3, mg >> 8));
+            }
+            const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t op = pw[47 + i];
+                kw_set(mix, op, kwt_merge(tlo, thi, kw_get(mix, op), dw[i], (op >> 8) & 3, op >> 16));
+            }
+            continue;
+        }
         if constexpr (V == 9) {
 #pragma unroll
             for (int i = 0; i < 18; ++i) {
@@ -262,3 +342,4 @@ PV(6)
 PV(7)
 PV(8)
 PV(9)
+PV(10)
