@@ -55,22 +55,36 @@ __device__ __forceinline__ void sha256_compress(uint32_t s[8], uint32_t w[16]) {
     s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
 }
 
-// SHA-256 of len bytes at m (any alignment), padding generated on the fly.
+// SHA-256 of len bytes at m (any alignment), padding generated on the fly. A block that lies
+// inside the message with a dword to spare is read as 17 aligned dwords and realigned in registers
+// (v_alignbyte + byte swap): 17 loads instead of 64 byte loads per block, which matters for the
+// 1487-byte Equihash headers (23 such blocks each) of the resident verify's side stream. The tail
+// blocks (message end, padding, length) keep the byte path, so no load reaches past the message.
 __device__ void sha256_bytes(const uint8_t* m, uint32_t len, uint32_t s[8]) {
     sha256_init(s);
     const uint32_t nblocks = (len + 9 + 63) / 64;
+    const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(m) & 3);
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(m - mis);
     for (uint32_t b = 0; b < nblocks; ++b) {
         uint32_t w[16];
+        if ((b + 1) * 64 + 4 <= len) {
+            uint32_t d[17];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            uint32_t word = 0;
+            for (int k = 0; k < 17; ++k) d[k] = a[b * 16 + k];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t idx = b * 64 + uint32_t(j) * 4 + uint32_t(k);
-                const uint32_t byte = idx < len ? m[idx] : (idx == len ? 0x80u : 0u);
-                word = (word << 8) | byte;
+            for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[j + 1], d[j], mis));
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t idx = b * 64 + uint32_t(j) * 4 + uint32_t(k);
+                    const uint32_t byte = idx < len ? m[idx] : (idx == len ? 0x80u : 0u);
+                    word = (word << 8) | byte;
+                }
+                w[j] = word;
             }
-            w[j] = word;
         }
         if (b == nblocks - 1) {
             w[14] = len >> 29;

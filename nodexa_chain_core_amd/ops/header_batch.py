@@ -63,9 +63,9 @@ class ResidentHeaderVerifier:
             self.ev_in, self.ev_jobs = h.event_create(), h.event_create()
             self.ev_side = [h.event_create() for _ in self.side]
             # the early copy of block hashes + nBits (models/verify.py prepares the index insert
-            # from it while the full hashes run)
-            self.early_stream = torch.cuda.Stream(device=self.dev)
+            # from it while the full hashes run), made at the end of the side stream
             self.ev_early = h.event_create()
+            self.ev_dgw = h.event_create()
         self.cap = 0
         self.in_cap = 0
         self.programs: dict[int, torch.Tensor] = {}
@@ -247,26 +247,27 @@ class ResidentHeaderVerifier:
             # stream runs them beside the KawPow chain (mix-only -> jobs -> full hashes -> verdicts)
             s0 = int(self.side[0].cuda_stream)
             h.stream_wait_event(s0, self.ev_in)
+            if series is not None:
+                # DGW (~120 us, latency-bound per lane) on a stream of its own, beside the Equihash
+                # work: the early copy below needs both
+                sd = int(self.side[-1].cuda_stream)
+                h.stream_wait_event(sd, self.ev_in)
+                c = _core.dgw_constants(params)
+                h.launch_dgw(self.k_dgw, P("times"), P("bits"), out + n * 33, a, n, series[3], c["dgw_activation_block"],
+                             c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], sd)
+                h.event_record(self.ev_dgw, sd)
             if m:
                 h.launch_equihash_verify(self.k_eq, self.h0, P("eq_msgs"), 112, m, P("eq_sols"), P("eq_verdict"), s0)
                 h.launch_sha256d(self.k_sha, P("eq_ser"), eq_len, eq_len, m, P("eq_hash"), False, s0)
-            if series is not None:
-                c = _core.dgw_constants(params)
-                h.launch_dgw(self.k_dgw, P("times"), P("bits"), out + n * 33, a, n, series[3], c["dgw_activation_block"],
-                             c["kawpow_time"], c["equihash_time"], c["limits"], c["compacts"], c["target_timespan"], s0)
             if m:
                 glue(2, 0, 0, s0)  # Equihash codes + block hashes (hb_verdict leaves those rows alone)
+            if series is not None:
+                h.stream_wait_event(s0, self.ev_dgw)  # ev_side[0]: the Equihash work and DGW done
             h.event_record(self.ev_side[0], s0)
             if nr:
                 h.launch_kawpow_mixonly(self.k_mo, P("rows") + lo_r * ROW, nr, ROW, self.mo.data_ptr() + lo_r * 128, s)
                 glue(0, lo_r, nr, s)  # jobs + the KawPow block hashes
             h.event_record(self.ev_jobs, s)
-            if ws == 1:  # the early copy: hashes + nBits as soon as hb_jobs and the side stream are done
-                es = int(self.early_stream.cuda_stream)
-                h.stream_wait_event(es, self.ev_jobs)
-                h.stream_wait_event(es, self.ev_side[0])
-                h.memcpy_async(self.early_host.data_ptr(), out + n, n * 36, es, "dtoh")
-                h.event_record(self.ev_early, es)
             if nr:
                 # one full-hash launch per epoch range, the ranges side by side: each is bound by
                 # its 64 dependent rounds per job, not by width
@@ -298,6 +299,16 @@ class ResidentHeaderVerifier:
                         h.stream_wait_event(s, ev)
                     k += 1
                 glue(1, lo_r, nr, s)
+            if ws == 1:
+                # the early copy: hashes + nBits as soon as hb_jobs and the side stream are done, at
+                # the end of the side stream itself and issued after every full-hash launch. Streams
+                # share the process's 4 hardware queues: a kernel queued behind this copy's event
+                # waits sat out the side stream (the second epoch range's launch started 450 us
+                # late), and a copy queued behind a full-hash launch waited for it (profiles/README
+                # r5z)
+                h.stream_wait_event(s0, self.ev_jobs)
+                h.memcpy_async(self.early_host.data_ptr(), out + n, n * 36, s0, "dtoh")
+                h.event_record(self.ev_early, s0)
             h.stream_wait_event(s, self.ev_side[0])
             if ws == 1:  # the early copy reads `out` and lands in early_host: both done before ev_end
                 h.stream_wait_event(s, self.ev_early)
