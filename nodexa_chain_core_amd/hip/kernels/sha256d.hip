@@ -65,12 +65,23 @@ __device__ void sha256_bytes(const uint8_t* m, uint32_t len, uint32_t s[8]) {
     const uint32_t nblocks = (len + 9 + 63) / 64;
     const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(m) & 3);
     const uint32_t* a = reinterpret_cast<const uint32_t*>(m - mis);
+    // the next in-message block's dwords are loaded before this block is compressed, so the load
+    // latency hides behind the 64 rounds (one lane hashes its message's blocks one after another)
+    uint32_t nxt[17];
+    if (64 + 4 <= len) {
+#pragma unroll
+        for (int k = 0; k < 17; ++k) nxt[k] = a[k];
+    }
     for (uint32_t b = 0; b < nblocks; ++b) {
         uint32_t w[16];
         if ((b + 1) * 64 + 4 <= len) {
             uint32_t d[17];
 #pragma unroll
-            for (int k = 0; k < 17; ++k) d[k] = a[b * 16 + k];
+            for (int k = 0; k < 17; ++k) d[k] = nxt[k];
+            if ((b + 2) * 64 + 4 <= len) {
+#pragma unroll
+                for (int k = 0; k < 17; ++k) nxt[k] = a[(b + 1) * 16 + k];
+            }
 #pragma unroll
             for (int j = 0; j < 16; ++j) w[j] = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[j + 1], d[j], mis));
         } else {
