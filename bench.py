@@ -19,8 +19,10 @@ the committed 10k-header fixture through models/verify.process_headers, PoW + DG
 every header required to be accepted (config 5; per-epoch setup excluded, reported).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
-          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+    (N>1 either way: bench.py starts its N ranks itself, one child process per GPU, or
+     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
+          --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...;
+     a WORLD_SIZE that disagrees with --gpus exits 2)
 
 Timing: W untimed steps, barrier + synchronize, K timed steps, synchronize + barrier, max
 elapsed over ranks. Rank 0 prints ONE JSON line.
@@ -255,6 +257,15 @@ def main() -> int:
     ap.add_argument("--quiet", action="store_true")
     args = ap.parse_args()
 
+    # --gpus N without a launcher: this process becomes rank 0 and starts ranks 1..N-1 itself, as
+    # fresh child processes, before anything here touches a GPU (never an exec of this process)
+    env_ws = os.environ.get("WORLD_SIZE")
+    if env_ws is not None and int(env_ws) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_ws} (launcher and flag disagree)", file=sys.stderr)
+        return 2
+    if env_ws is None and args.gpus > 1:
+        return _run_as_launcher(args)
+
     import torch
 
     from nodexa_chain_core_amd import _build
@@ -272,6 +283,8 @@ def main() -> int:
 
     world = W.init(use_gpu=not cpu, force_collectives=args.collectives or None)
     rank, ws = world.rank, world.world_size
+    if os.environ.get("NODEXA_BENCH_FAIL_RANK") == str(rank):  # test hook: one rank dies, the rest must not hang
+        raise SystemExit(f"rank {rank}: NODEXA_BENCH_FAIL_RANK")
     log = (lambda *a: print(*a, file=sys.stderr, flush=True)) if (rank == 0 and not args.quiet) else (lambda *a: None)
     sync = (lambda: None) if cpu else torch.cuda.synchronize
 
@@ -416,6 +429,64 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     W.shutdown()
     return 0
+
+
+def _run_as_launcher(args) -> int:
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: start ranks 1..N-1 as child
+    processes of this one (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* in their environment; rank r
+    drives GPU r), run rank 0 in a child too, and reap them all. Exit status: the first non-zero
+    child status, else 0. Reference analogue: GenerateClores starting its N miner threads itself
+    (/root/reference/src/miner.cpp:728-759); here they are processes, one per GPU."""
+    import signal
+    import socket
+    import subprocess
+
+    n = args.gpus
+    if args.device == "gpu" and os.environ.get("NODEXA_DIST_BACKEND", "nccl") == "nccl":
+        import torch  # device_count does not initialise the GPU on this image
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but {have} GPU(s) visible; RCCL needs one GPU per rank "
+                  "(NODEXA_DIST_BACKEND=gloo lets ranks share a GPU for rehearsals)", file=sys.stderr)
+            return 2
+    port = os.environ.get("MASTER_PORT")
+    if port is None:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = str(s.getsockname()[1])
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    term_at = None
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    # a failed rank leaves the others blocked in a collective: end them now
+                    for q in pending:
+                        q.send_signal(signal.SIGTERM)
+                    term_at = time.monotonic()
+            if term_at is not None and time.monotonic() - term_at > 30:
+                for q in pending:
+                    q.kill()
+                term_at = None
+            time.sleep(0.05)
+    except BaseException:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        raise
+    return rc
 
 
 def gpu_snapshot(world) -> dict:

@@ -23,12 +23,19 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def test_two_rank_bench_on_one_gpu(gpu):
+@pytest.mark.parametrize("launcher", ["torchrun", "self"])
+def test_two_rank_bench_on_one_gpu(gpu, launcher):
+    """launcher "self": a bare `bench.py --gpus 2` starts its own two ranks (the driver's N-GPU run
+    need not wrap the bench in torchrun)."""
     env = dict(os.environ, NODEXA_DIST_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--batch", str(1 << 23), "--equihash", "2",
-           "--verify", "1", "--check-shares", "4"]
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    pre = [sys.executable]
+    if launcher == "torchrun":
+        pre += ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())]
+    cmd = pre + ["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", str(1 << 23),
+                 "--equihash", "2", "--verify", "1", "--check-shares", "4"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
