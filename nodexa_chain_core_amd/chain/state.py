@@ -47,7 +47,10 @@ from .versionbits import VersionBits
 
 _core = core()
 
-REGTEST_NODEXA_KAWPOW_ACTIVATION = 1524179366 + 1  # genesis + 1: every mined regtest block is KawPow
+# -kawpowactivationtime value that makes every mined regtest block KawPow (genesis time + 1). The
+# regtest default is the reference's own (3582830167, src/chainparams.cpp:566-570: X16RV2 mining);
+# KawPow regtest is an explicit override, never the default
+REGTEST_KAWPOW_FROM_GENESIS = 1524179366 + 1
 
 
 @dataclass
@@ -119,8 +122,6 @@ def make_params(network: str, kawpow_activation_time: int | None = None,
     p = _core.make_chain_params(network)
     if kawpow_activation_time is not None:
         p.kawpow_activation_time = int(kawpow_activation_time)
-    elif network == "regtest":
-        p.kawpow_activation_time = REGTEST_NODEXA_KAWPOW_ACTIVATION
     if equihash_activation_time is not None:
         p.equihash_activation_time = int(equihash_activation_time)
     return p

@@ -7,12 +7,16 @@ RPC server (warm-up until the chain is loaded), start the miner when -gen,
 wait for shutdown; Interrupt/Shutdown (src/init.cpp:172,355).
 
 MI355X specifics: `-gpus=0,1,...` selects the devices the miner and the batch
-verifier use (one DAG per device, built on the GPU); `-kawpowactivationtime`
-overrides the activation (regtest default: genesis+1, so regtest blocks are
-KawPow — the reference's 2083 default would mine X16RV2); `-equihash=<time>`
-enables the Equihash(200,9) extension from that time (off by default).
+verifier use (one DAG per device, built on the GPU); `-kawpowactivationtime=<t>`
+overrides the KawPow activation time. Every network's default is the reference's
+(regtest: 3582830167, src/chainparams.cpp:566-570, so a default regtest node mines
+80-byte X16RV2 headers exactly as clore_blockchaind does);
+`-kawpowactivationtime=1524179367` (genesis + 1) makes every mined regtest block
+KawPow. `-equihash=<time>` enables the Equihash(200,9) extension from that time
+(off by default).
 
     python -m nodexa_chain_core_amd.node -regtest -rpcport=19443 -miningaddress=<addr> [-gpus=0]
+        [-kawpowactivationtime=1524179367]
 """
 from __future__ import annotations
 

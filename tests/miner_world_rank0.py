@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 def main(out_path: str) -> int:
     from nodexa_chain_core_amd import core
-    from nodexa_chain_core_amd.chain.state import ChainState, make_params
+    from nodexa_chain_core_amd.chain.state import REGTEST_KAWPOW_FROM_GENESIS, ChainState, make_params
     from nodexa_chain_core_amd.miner.service import ChainLeader, MiningService, make_rank_device
     from nodexa_chain_core_amd.parallel import world as W
 
@@ -26,7 +26,7 @@ def main(out_path: str) -> int:
     blocks = int(os.environ.get("NODEXA_TEST_BLOCKS", "2"))
     window = int(os.environ.get("NODEXA_MINER_WINDOW", "8"))
     eq_act = int(time.time()) - 100 if os.environ.get("NODEXA_TEST_EQUIHASH") == "1" else None
-    state = ChainState(make_params("regtest", equihash_activation_time=eq_act), None)
+    state = ChainState(make_params("regtest", REGTEST_KAWPOW_FROM_GENESIS, equihash_activation_time=eq_act), None)
     leader = ChainLeader(state, target_bits=int(os.environ.get("NODEXA_TEST_TARGET_BITS", "7")))
     dev = make_rank_device(True, window=window, fail_rate=float(os.environ.get("NODEXA_MINER_FAILRATE", "0")))
     svc = MiningService(dev, leader, window=window, collective_timeout_s=timeout, record_windows=True)

@@ -17,7 +17,7 @@ def test_node_mines_equihash_on_gpu(core, gpu, tmp_path):
 
     addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
     args = ArgsManager()
-    args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+    args.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
                            f"-miningaddress={addr}", "-printtoconsole=0", "-gpus=0",
                            "-equihash=%d" % (int(time.time()) - 100), "-minertargetbits=6"])
     n = Node(args)

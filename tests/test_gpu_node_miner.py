@@ -48,7 +48,7 @@ def test_node_setgenerate_sustains_kernel_rate(core, gpu, tmp_path):
     kernel = _kernel_rate(core, 0)
     addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
     args = ArgsManager()
-    args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+    args.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
                            f"-miningaddress={addr}", "-printtoconsole=0", "-gpus=0", "-minertargetbits=28"])
     n = Node(args)
     n.start()

@@ -162,7 +162,7 @@ def test_p2p_header_sync_takes_the_resident_path(core, gpu, tmp_path):
         d = tmp_path / name
         d.mkdir()
         args = ArgsManager()
-        args.parse_parameters(["-regtest", f"-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+        args.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", f"-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
                                f"-miningaddress={addr}", "-printtoconsole=0", *extra])
         n = Node(args)
         n.start()

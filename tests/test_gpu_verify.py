@@ -60,7 +60,7 @@ def test_node_gpu_mining_and_batch_verify(core, gpu, tmp_path):
 
     addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
     args = ArgsManager()
-    args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+    args.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
                            f"-miningaddress={addr}", "-printtoconsole=0", "-gpus=0", "-gpuintensity=65536"])
     node = Node(args)
     node.start()

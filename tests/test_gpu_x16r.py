@@ -37,11 +37,11 @@ def test_random_batch_mixed_versions_vs_host(core, gpu):
 def test_verify_headers_legacy_batch_on_gpu_matches_host(core, gpu):
     """models/verify routes a legacy (pre-KawPow) batch of X16R_GPU_MIN headers or more through the
     GPU hash: same verdicts and hashes as the host cores, X16R and X16RV2 by nTime."""
-    from nodexa_chain_core_amd.chain.state import make_params
+    from nodexa_chain_core_amd.chain.state import REGTEST_KAWPOW_FROM_GENESIS, make_params
     from nodexa_chain_core_amd.models import verify as MV
 
-    params = make_params("regtest")
-    # regtest activates KawPow before X16RV2: move X16RV2 inside the legacy era for this batch
+    params = make_params("regtest", REGTEST_KAWPOW_FROM_GENESIS)
+    # KawPow-regtest activates KawPow before X16RV2: move X16RV2 inside the legacy era for this batch
     params.x16rv2_activation_time = params.kawpow_activation_time - 100_000
     rng = random.Random(5)
     hs = []

@@ -14,9 +14,9 @@ from test_miner_service import _check_disjoint, _run_world
 
 @pytest.fixture()
 def state(core):
-    from nodexa_chain_core_amd.chain.state import ChainState, make_params
+    from nodexa_chain_core_amd.chain.state import REGTEST_KAWPOW_FROM_GENESIS, ChainState, make_params
 
-    return ChainState(make_params("regtest"), None)
+    return ChainState(make_params("regtest", REGTEST_KAWPOW_FROM_GENESIS), None)
 
 
 def test_gloo_world3_evicts_failing_rank_and_repartitions(tmp_path, core):
@@ -132,7 +132,7 @@ def test_node_metrics_log_and_rest(core, tmp_path):
     metrics.REGISTRY.reset()
     addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
     args = ArgsManager()
-    args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+    args.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
                            f"-miningaddress={addr}", "-printtoconsole=0", "-metricslog=metrics.jsonl",
                            "-metricsinterval=60", "-dagcache=1"])
     n = Node(args)

@@ -22,9 +22,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.fixture()
 def state(core):
-    from nodexa_chain_core_amd.chain.state import ChainState, make_params
+    from nodexa_chain_core_amd.chain.state import REGTEST_KAWPOW_FROM_GENESIS, ChainState, make_params
 
-    return ChainState(make_params("regtest"), None)
+    return ChainState(make_params("regtest", REGTEST_KAWPOW_FROM_GENESIS), None)
 
 
 def test_work_packet_roundtrip():
@@ -252,7 +252,7 @@ def test_node_mines_through_service_with_follower_rank(core, tmp_path):
 
     addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
     args = ArgsManager()
-    args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
+    args.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
                            f"-miningaddress={addr}", "-printtoconsole=0", "-minerservice", "-minerranks=2",
                            "-gpuintensity=8", "-minertargetbits=5", "-minercollectivetimeout=20"])
     n = Node(args)

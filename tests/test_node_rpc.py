@@ -10,6 +10,11 @@ import threading
 import pytest
 
 
+# the engine's override that makes every mined regtest block KawPow (genesis time + 1); without it
+# regtest keeps the reference's activation (3582830167) and mines X16RV2
+KAWPOW_REGTEST = "-kawpowactivationtime=1524179367"
+
+
 @pytest.fixture()
 def node_factory(core, tmp_path):
     from nodexa_chain_core_amd.node import Node
@@ -17,11 +22,14 @@ def node_factory(core, tmp_path):
 
     nodes = []
 
-    def make(extra=()):
+    def make(extra=(), kawpow=True):
+        """kawpow=True: the KawPow-regtest override (every mined block KawPow); False: the
+        reference's default regtest (X16RV2 until 2083)."""
         addr = core.base58check_encode(bytes([42]) + bytes(range(20)))
         args = ArgsManager()
+        flags = [KAWPOW_REGTEST] if kawpow else []
         args.parse_parameters(["-regtest", f"-datadir={tmp_path}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
-                               f"-miningaddress={addr}", "-printtoconsole=0", *extra])
+                               f"-miningaddress={addr}", "-printtoconsole=0", *flags, *extra])
         n = Node(args)
         n.start()
         nodes.append(n)
@@ -197,10 +205,11 @@ def test_cli_main(node_factory, capsys, tmp_path):
 
 
 def test_generate_x16rv2_reference_default(core, node_factory):
-    """BASELINE config 1 with the reference's own regtest params: KawPow activation in
-    2083 (src/chainparams.cpp:566-570), so `generate` hashes 80-byte X16RV2 headers and
-    bumps the 32-bit nNonce (src/rpc/mining.cpp:117-173)."""
-    node, addr = node_factory(["-kawpowactivationtime=3582830167"])
+    """BASELINE config 1 with the reference's own regtest params, which are this engine's default
+    regtest (no flag): KawPow activation in 2083 (src/chainparams.cpp:566-570), so `generate`
+    hashes 80-byte X16RV2 headers and bumps the 32-bit nNonce (src/rpc/mining.cpp:117-173)."""
+    node, addr = node_factory(kawpow=False)
+    assert node.params.kawpow_activation_time == 3582830167
     c = client(node)
     hashes = c.generatetoaddress(2, addr)
     assert c.getblockcount() == 2
@@ -243,3 +252,18 @@ def test_mempool_rpcs_and_rest(core, node_factory):
     raw = c.getrawtransaction(cb, False, hashes[0])
     assert c.decoderawtransaction(raw)["txid"] == cb
     assert c.getrawtransaction(cb, True, hashes[0])["blockhash"] == hashes[0]
+
+
+def test_regtest_kawpow_is_an_override(core, node_factory):
+    """The reference's explicit value and the engine default agree; only the override flag moves the
+    activation, and a KawPow-regtest `generate` makes 120-byte KawPow headers."""
+    from nodexa_chain_core_amd.chain.state import REGTEST_KAWPOW_FROM_GENESIS, make_params
+
+    assert make_params("regtest").kawpow_activation_time == core.make_chain_params("regtest").kawpow_activation_time \
+        == 3582830167
+    assert make_params("regtest", REGTEST_KAWPOW_FROM_GENESIS).kawpow_activation_time == 1524179367
+    node, addr = node_factory()
+    c = client(node)
+    h = c.generatetoaddress(1, addr)[0]
+    raw = bytes.fromhex(c.getblockheader(h, False))
+    assert len(raw) == 120 and core.BlockHeader.deserialize(raw, node.params.kawpow_activation_time).height == 1

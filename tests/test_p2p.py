@@ -59,7 +59,7 @@ def _node(core, tmp_path, name, extra):
     d.mkdir()
     args = ArgsManager()
     args.parse_parameters(["-regtest", f"-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p",
-                           f"-miningaddress={addr}", "-printtoconsole=0", *extra])
+                           f"-miningaddress={addr}", "-printtoconsole=0", "-kawpowactivationtime=1524179367", *extra])
     n = Node(args)
     n.start()
     return n
