@@ -982,7 +982,8 @@ class ChainState:
                 # drop the stale set: every coin record, then the fresh (empty) state's 'B'
                 stale = [(k, None) for k, _ in self.coins_db.items(b"C", b"D")]
                 stale += [(k, None) for k, _ in self.coins_db.items(b"\x01", b"\x02")]  # asset records
-                self.coins_db.write(stale + [(b"H", None)])
+                # a replay rebuilds every block's asset undo: no import height survives it
+                self.coins_db.write(stale + [(b"H", None), (ASSETS_IMPORT_KEY, None)])
                 self.assets.best_block = gh
                 _core.coins_flush_ldb(self.coins, self.coins_db, self._coins_obf, True, self.assets)
                 _core.indexes_purge_ldb(self.index_log.db)  # the indexes are rebuilt by the replay
@@ -999,8 +1000,20 @@ class ChainState:
         batch as 'B', so the node opens without replaying the chain. Blocks the reference
         connected have no asset undo records of this engine: the import height is kept, and a
         reorg that would disconnect one of them with asset activity asks for -reindex-chainstate
-        (as the reference does for a missing undo, src/validation.cpp DisconnectBlock)."""
+        (as the reference does for a missing undo, src/validation.cpp DisconnectBlock).
+
+        Runs at most once per datadir: with an import marker or any engine asset record present it
+        returns False (the caller replays). The reference flushes its coins before its asset
+        databases (src/validation.cpp:10693-10703), so an interrupted reference flush can leave
+        assets/ one flush behind its chainstate; nothing in assets/ records a block to check that
+        against, which is why the import is confined to the first open."""
         if not self.datadir:
+            return False
+        # only the first open of a reference datadir imports: once this engine has written asset
+        # records (or imported once), assets/ is stale — the engine advances the chain without it —
+        # and a later load failure or mismatch must replay from genesis, never re-import
+        if self.coins_db.get(ASSETS_IMPORT_KEY) is not None or self.coins_db.get(b"\x02assets.best") is not None or \
+                next(iter(self.coins_db.items(b"\x01", b"\x02")), None) is not None:
             return False
         adir = os.path.join(self.datadir, "assets")
         if not os.path.exists(os.path.join(adir, "CURRENT")):

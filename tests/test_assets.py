@@ -196,6 +196,19 @@ def test_asset_lifecycle_regtest(core, node_factory):  # noqa: F811
     node.stop()
     node, _ = node_factory()  # the imported state was written in this engine's records
     assert not node.state.rebuilt and _asset_state_view(node.state) == before
+    # after the import the engine owns the asset state: damaged engine records make the node replay
+    # from genesis, never re-import the (now stale) reference assets/ databases
+    node.stop()
+    db = core.LevelDB(os.path.join(dd, "chainstate"))
+    db.write([(k, None) for k, _ in db.items(b"\x01", b"\x02")] + [(b"\x02assets.best", None)])
+    db.close()
+    node, _ = node_factory()
+    assert node.state.rebuilt and node.state.assets_import_height == -1
+    assert _asset_state_view(node.state) == before  # the replay rebuilds the same state
+    node.stop()
+    node, _ = node_factory()  # and is the engine's own from then on: loaded, no import height
+    assert not node.state.rebuilt and node.state.assets_import_height == -1
+    assert _asset_state_view(node.state) == before
 
 
 def _asset_state_view(state):
