@@ -276,6 +276,13 @@ def build_kernels(force: bool = False, jobs: int = 8) -> list[str]:
         todo = [(s, o) for s, o in todo if force or _newer(o, [s] + hdrs)]  # another process may have built them
         for f in [ex.submit(one, s, o) for s, o in todo]:
             f.result()
+        # kawpow_verify_waves jumps into handler slots by computed address: stamp the code object
+        # only after its slot layout checks out (ops/jump_slots.py); the loader refuses it unstamped
+        from .ops import jump_slots
+
+        for o in outs:
+            if os.path.splitext(os.path.basename(o))[0] in jump_slots.STAMPED and not jump_slots.stamp_ok(o):
+                jump_slots.verify_and_stamp(o)
     return outs
 
 

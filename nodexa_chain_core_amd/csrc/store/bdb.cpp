@@ -93,6 +93,9 @@ public:
             item(p, i, 12);
             uint32_t next = u32(p + off + 4);
             const uint32_t total = u32(p + off + 8);
+            // the chain has at most npages_ pages of payload: a length beyond that is damage, and
+            // must not reserve gigabytes before the first page is checked
+            if (uint64_t(total) > uint64_t(npages_) * pagesize_) fail("overflow item longer than the file");
             out.clear();
             out.reserve(total);
             for (size_t hops = 0; out.size() < total; ++hops) {

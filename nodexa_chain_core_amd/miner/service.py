@@ -201,7 +201,7 @@ class Comm:
                 # stream, where they would wait behind the window queued for the next step and
                 # drain the two-window pipeline every step (profiles/README r4b)
                 self.stream = torch.cuda.Stream(device=self.w.device, priority=-16)
-            if self.group is None:
+            if self.W.is_init_group(self.group):
                 # gloo connects the group's full mesh under the group timeout, and ranks reach this
                 # point seconds apart on a loaded host (a DAG build, a cold import): connect under the
                 # rendezvous timeout. Every collective stays bounded by self.timeout (_wait), and a
@@ -1038,7 +1038,7 @@ def follower_main() -> int:
     watchdog = float(os.environ.get("NODEXA_MINER_WATCHDOG", "120"))
     window = int(os.environ.get("NODEXA_MINER_WINDOW", str(1 << 25)))
     W.init(use_gpu=not cpu, device_index=None if dev_index is None else int(dev_index),
-           timeout_s=max(int(timeout), W.rendezvous_timeout()), elastic=True)
+           timeout_s=max(int(timeout), W.rendezvous_timeout()), elastic=True, collective_timeout_s=timeout)
     w = W.get()
     dev = make_rank_device(cpu, w.device.index if not cpu else None, collective_dag=w.collective, window=window,
                            fail_rate=float(os.environ.get("NODEXA_MINER_FAILRATE", "0") or 0),

@@ -188,7 +188,7 @@ class Node:
                 w = Wallet(self.state, self.params, wpath, bip44=a.get_bool("bip44", True),
                            mnemonic=(a.get("mnemonic", "") or "") if first else "",
                            mnemonic_passphrase=(a.get("mnemonicpassphrase", "") or "") if first else "",
-                           import_from=dat)
+                           import_from=dat, keep_uncompressed=a.get_bool("walletkeepuncompressed", False))
                 if w.import_report is not None:
                     log.log_printf(f"Imported reference wallet {dat} into {wpath}: {w.import_report}")
                 w.name = name
@@ -394,7 +394,8 @@ class Node:
         self.miner_procs = []
         ranks = max(1, a.get_int("minerranks", 1)) if a.get_bool("minerservice", False) else 1
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            W.init(use_gpu=not cpu, timeout_s=max(int(timeout), W.rendezvous_timeout()), elastic=True)
+            W.init(use_gpu=not cpu, timeout_s=max(int(timeout), W.rendezvous_timeout()), elastic=True,
+                   collective_timeout_s=timeout)
         elif cpu and ranks == 1 and not a.get_bool("minerforcecollectives", False):
             pass  # a single host rank: nothing to exchange, no process group
         else:
@@ -415,7 +416,7 @@ class Node:
                 self.miner_procs = MS.spawn_followers(gpus, port, cpu=cpu, extra_env=env)
             W.init(use_gpu=not cpu, timeout_s=max(int(timeout), W.rendezvous_timeout()),
                    device_index=None if cpu else gpus[0],
-                   rank=0, world_size=len(gpus), elastic=True,
+                   rank=0, world_size=len(gpus), elastic=True, collective_timeout_s=timeout,
                    force_collectives=a.get_bool("minerforcecollectives", False) or None)
         w = W.get()
         window = a.get_int("gpuintensity", 4096 if cpu else 1 << 25)

@@ -92,4 +92,10 @@ def static_kernel(module: str, name: str):
     path = os.path.join(KERNEL_DIR, module + ".hsaco")
     if not os.path.exists(path):
         raise NativeUnavailable(f"missing {path}; run `python -m nodexa_chain_core_amd._build kernels`")
+    from . import jump_slots
+
+    if module in jump_slots.STAMPED and not jump_slots.stamp_ok(path):
+        # computed jumps into a slot table whose layout was not checked: never load it
+        raise NativeUnavailable(f"{path} has no valid handler-slot stamp (ops/jump_slots.py); rebuild it with "
+                                "`python -m nodexa_chain_core_amd._build kernels`")
     return load_code_object(path).function(name)

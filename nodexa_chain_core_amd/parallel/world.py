@@ -44,24 +44,39 @@ class World:
 
 
 _WORLD: World | None = None
+_INIT_GROUP = None  # the collective-timeout group init() made (None: the default group)
+
+
+def is_init_group(group) -> bool:
+    """`group` is the whole-world collective group of init(), shared by this module's helpers
+    (users that must abort their communicator alone, miner/service.Comm, make their own)."""
+    return group is None or group is _INIT_GROUP
 
 
 def rendezvous_timeout() -> int:
     """Timeout of the default group (NODEXA_RENDEZVOUS_TIMEOUT, default 300 s): the start-up
     rendezvous and full-mesh connect, which must tolerate ranks that start seconds apart (a loaded
-    host, a cold torch import). Failure detection does not use it: the mining loop's collectives run
-    on a group of their own with the collective timeout (miner/service.Comm)."""
+    host, a cold torch import). On RCCL failure detection does not use it: the mining loop's
+    collectives run on a group of their own with the collective timeout (miner/service.Comm), and
+    this module's helpers on the group init(collective_timeout_s=...) makes."""
     return int(os.environ.get("NODEXA_RENDEZVOUS_TIMEOUT", "300"))
 
 
 def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | None = None,
          rank: int | None = None, world_size: int | None = None, elastic: bool = False,
-         force_collectives: bool | None = None) -> World:
+         force_collectives: bool | None = None, collective_timeout_s: float | None = None) -> World:
     """Initialise from RANK/WORLD_SIZE/LOCAL_RANK (torchrun, or the node's spawned miner ranks)
     or single-process; `rank` / `world_size` override the environment. `device_index`: the GPU
     of this rank (default: LOCAL_RANK). `force_collectives` (env NODEXA_FORCE_COLLECTIVES=1):
     make a process group even for one rank, so every collective of the miner, the DAG build and
-    batch verify really runs (one-rank RCCL on a 1-GPU box exercises the 8-GPU code path)."""
+    batch verify really runs (one-rank RCCL on a 1-GPU box exercises the 8-GPU code path).
+
+    `timeout_s` bounds the start-up rendezvous (callers pass rendezvous_timeout(), minutes). With
+    `collective_timeout_s` below it, the collectives of this module (barrier, all_reduce_*, the
+    sharded DAG gather of parallel/dag.py, batch verify) run on a group of their own created with
+    that shorter timeout, so a rank lost mid-collective is detected in collective time, not
+    rendezvous time. RCCL only: a gloo group connects its full mesh under its own timeout, and
+    host rehearsals whose ranks start seconds apart keep the default group."""
     global _WORLD
     rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
     world_size = int(os.environ.get("WORLD_SIZE", "1")) if world_size is None else int(world_size)
@@ -104,7 +119,13 @@ def init(use_gpu: bool | None = None, timeout_s: int = 600, device_index: int | 
             kw["device_id"] = device
         dist.init_process_group(backend=backend, rank=rank, world_size=world_size,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    _WORLD = World(rank, world_size, local_rank, backend, device, None, tuple(range(world_size)))
+    global _INIT_GROUP
+    group = None
+    if backend == "nccl" and collective_timeout_s is not None and collective_timeout_s < timeout_s:
+        group = dist.new_group(ranks=list(range(world_size)),
+                               timeout=datetime.timedelta(seconds=float(collective_timeout_s)))
+    _INIT_GROUP = group
+    _WORLD = World(rank, world_size, local_rank, backend, device, group, tuple(range(world_size)))
     return _WORLD
 
 
@@ -133,10 +154,11 @@ def get() -> World:
 
 
 def shutdown() -> None:
-    global _WORLD
+    global _WORLD, _INIT_GROUP
     if _WORLD is not None and _WORLD.collective and dist.is_initialized():
         dist.destroy_process_group()
     _WORLD = None
+    _INIT_GROUP = None
 
 
 def barrier() -> None:

@@ -127,7 +127,7 @@ def multisig_script(m: int, pubkeys: list[bytes]) -> bytes:
 
 class Wallet:
     def __init__(self, state, params, path: str | None, bip44: bool = True, mnemonic: str = "",
-                 mnemonic_passphrase: str = "", import_from: str | None = None):
+                 mnemonic_passphrase: str = "", import_from: str | None = None, keep_uncompressed: bool = False):
         self.state = state
         self.params = params
         self.path = path
@@ -159,6 +159,10 @@ class Wallet:
         self._relock = None
         self.unlocked_until = 0
         self.import_report: dict | None = None  # what import_from brought in (walletdb.py)
+        # uncompressed keys of an imported wallet.dat (pub -> secret or encrypted blob): this wallet
+        # does not spend with them yet, so they are kept verbatim in the saved file, not dropped
+        self.uncompressed: dict[bytes, dict] = {}
+        self._keep_uncompressed = keep_uncompressed
         if path and os.path.exists(path):
             self._load()
         elif import_from:
@@ -185,9 +189,12 @@ class Wallet:
     @fee_rate.setter
     def fee_rate(self, v: int) -> None:
         self.pay_tx_fee = int(v)
+
     def _load(self) -> None:
         with open(self.path) as f:
             data = json.load(f)
+        for rec in data.get("uncompressed_keys", []):
+            self.uncompressed[bytes.fromhex(rec["pub"])] = {k: bytes.fromhex(v) for k, v in rec.items() if k != "pub"}
         mk = data.get("mkey")
         if mk:
             self.mkey = {"salt": bytes.fromhex(mk["salt"]), "rounds": int(mk["rounds"]),
@@ -242,6 +249,14 @@ class Wallet:
                 raise WalletError(f"wallet.dat master key derivation method {mk['method']} is not supported")
             self.mkey = {"salt": mk["salt"], "rounds": mk["rounds"], "crypted": mk["crypted"]}
         pubs: dict[bytes, bytes] = {}  # hash160 -> pub of every imported key
+        unc = {pub: {"sec": sec} for pub, sec in ref["keys"].items() if len(pub) != 33}
+        unc.update({pub: {"crypted": blob} for pub, blob in ref["ckeys"].items() if len(pub) != 33})
+        if unc and not self._keep_uncompressed:
+            # funds at those keys' addresses would drop out of this wallet: refuse, unless asked
+            raise WalletError(f"wallet.dat holds {len(unc)} uncompressed key(s), which this wallet cannot spend "
+                              "with yet; -walletkeepuncompressed=1 imports the rest and keeps them aside "
+                              "(saved verbatim, not spendable here)")
+        self.uncompressed = unc
         for pub, sec in ref["keys"].items():
             if len(pub) != 33:
                 report["uncompressed_skipped"] += 1
@@ -357,6 +372,9 @@ class Wallet:
         if self.mkey is not None:
             data["mkey"] = {"salt": self.mkey["salt"].hex(), "rounds": self.mkey["rounds"],
                             "crypted": self.mkey["crypted"].hex()}
+        if self.uncompressed:  # kept aside from an imported wallet.dat (not spendable here)
+            data["uncompressed_keys"] = [{"pub": pub.hex(), **{k: v.hex() for k, v in rec.items()}}
+                                         for pub, rec in self.uncompressed.items()]
         tmp = self.path + ".new"
         with open(tmp, "w") as f:
             json.dump(data, f, indent=1)

@@ -335,6 +335,31 @@ def test_import_legacy_hd_wallet(core, tmp_path):
 
 
 @needs_libdb
+def test_import_uncompressed_keys_refused_or_kept_aside(core, tmp_path):
+    """A wallet.dat with an uncompressed key: refused by default (its funds would drop out of the
+    wallet); with keep_uncompressed (-walletkeepuncompressed=1) the rest is imported and the
+    uncompressed key is saved verbatim beside it, surviving a reload."""
+    from nodexa_chain_core_amd.wallet.wallet import Wallet, WalletError
+
+    params = _params()
+    comp, unc = bytes([3]) * 32, bytes([4]) * 32
+    upub = core.secp_pubkey_create(unc, False)
+    uder = bytes([0x30, 0x82, 0x01, 0x13, 0x02, 0x01, 0x01, 0x04, 0x20]) + unc + bytes(141) + b"\xa1\x44\x03\x42\x00" + upub
+    recs = [key_record(core, comp), (rkey("key", vec(upub)), vec(uder) + core.sha256d(upub + uder))]
+    dat = str(tmp_path / "wallet.dat")
+    bdb_write(dat, recs)
+    js = str(tmp_path / "w.json")
+    with pytest.raises(WalletError, match="uncompressed"):
+        Wallet(None, params, js, import_from=dat)
+    assert not os.path.exists(js)
+    w = Wallet(None, params, js, import_from=dat, keep_uncompressed=True)
+    assert w.import_report["keys"] == 1 and w.import_report["uncompressed_skipped"] == 1
+    assert w.uncompressed == {upub: {"sec": unc}}
+    w2 = Wallet(None, params, js)
+    assert w2.uncompressed == {upub: {"sec": unc}} and len(w2.keys) == 1
+
+
+@needs_libdb
 def test_import_rejects_corrupt_key_record(core, tmp_path):
     from nodexa_chain_core_amd.wallet.wallet import Wallet
 
