@@ -132,6 +132,9 @@ def _verify_headers_bench(log) -> dict | None:
                        "issue_ms": r["issue_ms"], "overlap_ms": r["overlap_ms"], "wait_ms": r["wait_ms"],
                        "accept_ms": r["accept_ms"],
                        "dgw_on_gpu": r["dgw_gpu"], "parse_included": True,
+                       "ranks": "split over the ranks, all-gathered" if r.get("sharded") else
+                       ("rank 0, verdict broadcast (batch below NODEXA_VERIFY_SHARD_MIN)" if w.world_size > 1
+                        else "one rank"),
                        "first_run_incl_epoch_setup_s": round(setup, 3)}
     log(f"[bench] verify {n} headers (resident): {n / dt:.0f} headers/s (host {r['host_ms']:.2f} ms, "
         f"{r['host_exposed_ms']:.2f} of it beside no device work, device "

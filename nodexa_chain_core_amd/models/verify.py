@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import os
+import struct
 import time
 
 import numpy as np
@@ -368,12 +369,58 @@ def resident_ready(headers, act: int, device: int, mode: str = "auto") -> bool:
     return bool(epochs) and all(V.is_resident(device, e) or n > V.LIGHT_MAX_JOBS for e, n in epochs.items())
 
 
+def shard_min_headers() -> int:
+    """Smallest batch the resident verify splits over the ranks of a world (NODEXA_VERIFY_SHARD_MIN,
+    default 65536). Below it one rank verifies the whole batch and broadcasts the verdict: a 10k
+    batch costs ~1.4 ms on one MI355X, of which ~0.6 ms is device work already hidden under the host
+    decode + prepare (both spread over the host cores by parallel_for inside the one rank), so a
+    split saves no critical-path time and adds an all-gather (profiles/README r6: 2 ranks sharing a
+    GPU measured 3.0 M headers/s sharded against 7.4 M on one rank)."""
+    return int(os.environ.get("NODEXA_VERIFY_SHARD_MIN", "65536"))
+
+
+_VERDICT = 96  # broadcast packet: accepted u32 | reject index i32 | dos i32 | reason (84 bytes, utf-8)
+
+
+def _broadcast_verdict(world, r: dict | None) -> dict | None:
+    """Rank 0's verdict to every rank of `world` (one 96-byte broadcast): the others' result dict
+    carries the same accepted count and reject, and no timings of their own."""
+    from ..parallel import world as W
+
+    pkt = None
+    if world.rank == 0 and r is None:  # rank 0 could not take the batch: every rank falls back
+        pkt = struct.pack("<Iii84s", 0xFFFFFFFF, -1, 0, b"")
+    elif world.rank == 0:
+        rej = r["reject"] or {}
+        why = (rej.get("reason") or "").encode()[:84]
+        pkt = struct.pack("<Iii84s", r["accepted"], rej.get("index", -1) if rej else -1, r.get("dos", 0), why)
+    raw = W.broadcast_bytes(pkt, _VERDICT)
+    if world.rank == 0:
+        return r
+    acc, idx, dos, why = struct.unpack("<Iii84s", raw)
+    if acc == 0xFFFFFFFF:
+        return None
+    why = why.rstrip(b"\0").decode()
+    return {"accepted": acc, "reject": {"index": idx, "reason": why} if idx >= 0 else None, "dos": dos,
+            "pow_s": 0.0, "context_s": 0.0, "dgw_gpu": True, "resident": True, "sharded": False,
+            "host_ms": 0.0, "host_exposed_ms": 0.0, "overlap_ms": 0.0, "device_ms": 0.0, "pack_ms": 0.0,
+            "issue_ms": 0.0, "wait_ms": 0.0, "accept_ms": 0.0}
+
+
 def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, world=None) -> dict | None:
     """ProcessNewBlockHeaders for a native HeaderBatch with the device-resident pipeline
     (ops/header_batch.py): one upload, PoW + block hashes + DGW nBits of every header on the GPU,
     one download, then the serial index insert on the host (HeaderChain.accept_batch). Pre-KawPow
     (X16R) headers, if any, are hashed on the host cores. Same result as process_headers; None when
-    the batch does not suit the resident path (not in height order), so the caller falls back."""
+    the batch does not suit the resident path (not in height order), so the caller falls back.
+
+    Over a world of N ranks (every rank calls with the same batch): a batch of shard_min_headers()
+    or more has its device work split in contiguous slices and the codes + block hashes all-gathered;
+    a smaller one is verified whole by rank 0 (which commits it to its chain) and the verdict is
+    broadcast, so N GPUs never verify slower than one plus a 96-byte broadcast."""
+    if world is not None and world.collective and world.world_size > 1 and len(batch) < shard_min_headers():
+        r = process_batch_resident(chain, batch, adjusted_time, device, None) if world.rank == 0 else None
+        return _broadcast_verdict(world, r)
     from ..ops.header_batch import CODES
 
     t0 = time.perf_counter()
@@ -433,8 +480,9 @@ def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, wo
     reject = {"index": accepted, "reason": why} if why is not None else None
     if reject is None and first_bad < n:
         reject = {"index": first_bad, "reason": CODES.get(int(codes[first_bad]), "high-hash")}
-    return {"accepted": accepted, "reject": reject, "pow_s": t1 - t0 + (t2 - t1), "context_s": t3 - t2,
+    return {"accepted": accepted, "reject": reject, "dos": _dos, "pow_s": t1 - t0 + (t2 - t1), "context_s": t3 - t2,
             "dgw_gpu": series is not None, "resident": True,
+            "sharded": world is not None and world.collective and world.world_size > 1,
             # host_ms: all host work (the wait for the device excluded); host_exposed_ms: the part
             # the device does not cover (the decode beside it counts only as far as the device ran
             # after the issue)

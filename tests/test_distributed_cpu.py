@@ -43,6 +43,14 @@ def _worker(rank, world, port, q):
         # 2. reductions
         assert W.all_reduce_max(float(rank) + 0.5) == world - 0.5
         assert W.all_reduce_sum_int(rank + 1) == world * (world + 1) // 2
+        # 2b. resident batch verify below the shard threshold: rank 0's verdict broadcast to all
+        from nodexa_chain_core_amd.models.verify import _broadcast_verdict
+
+        v0 = {"accepted": 9990, "reject": {"index": 9990, "reason": "high-hash"}, "dos": 50}
+        got = _broadcast_verdict(w, v0 if rank == 0 else None)
+        assert got["accepted"] == 9990 and got["reject"] == {"index": 9990, "reason": "high-hash"} and got["dos"] == 50
+        got = _broadcast_verdict(w, {"accepted": 10000, "reject": None, "dos": 0} if rank == 0 else None)
+        assert got["accepted"] == 10000 and got["reject"] is None
         # 3. DAG shard all-gather: each rank fills its slice with golden 2048-bit items
         ctx = _core.get_epoch_context(0)
         per_items = 8

@@ -27,7 +27,9 @@ def _free_port() -> int:
 def test_two_rank_bench_on_one_gpu(gpu, launcher):
     """launcher "self": a bare `bench.py --gpus 2` starts its own two ranks (the driver's N-GPU run
     need not wrap the bench in torchrun)."""
-    env = dict(os.environ, NODEXA_DIST_BACKEND="gloo")
+    # torchrun: the resident verify split over the ranks (shard threshold 0); self: the default
+    # policy, where the 10k batch is verified by rank 0 and the verdict broadcast
+    env = dict(os.environ, NODEXA_DIST_BACKEND="gloo", NODEXA_VERIFY_SHARD_MIN="0" if launcher == "torchrun" else "65536")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     pre = [sys.executable]
@@ -48,4 +50,5 @@ def test_two_rank_bench_on_one_gpu(gpu, launcher):
     assert out["equihash_sol_per_s"] > 0
     # the resident verify sliced over the ranks, codes + block hashes all-gathered (header_batch._gather)
     assert out["verify_headers_per_s"] > 0 and out["verify_headers_light_per_s"] > 0
+    assert out["verify_headers"]["resident"]["ranks"].startswith("split" if launcher == "torchrun" else "rank 0")
     assert "over 2 GPU(s)" in r.stderr  # the DAG was built sharded and all-gathered
