@@ -851,6 +851,11 @@ void bind_extra(py::module_& m) {
         .def(py::init([](const ChainParams& p) { return std::make_shared<HeaderChain>(p, std::make_shared<CpuPowVerifier>()); }))
         .def_property_readonly("params", &HeaderChain::params, py::return_value_policy::reference_internal)
         .def("set_kawpow_activation_time", [](HeaderChain& c, u32 t) { c.mutable_params().kawpow_activation_time = t; })
+        .def("add_anchor",
+             [](HeaderChain& c, const std::vector<BlockHeader>& hs, int base_height, const py::int_& base_work) {
+                 return c.add_anchor(hs, base_height, int_to_arith(base_work));
+             },
+             py::arg("headers"), py::arg("base_height"), py::arg("base_work"), py::return_value_policy::reference_internal)
         .def_readwrite("strict_kawpow_height", &HeaderChain::strict_kawpow_height)
         .def_readwrite("max_reorg_depth", &HeaderChain::max_reorg_depth)
         .def("check_header", &HeaderChain::check_header, py::call_guard<py::gil_scoped_release>())

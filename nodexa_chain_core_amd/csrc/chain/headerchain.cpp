@@ -612,6 +612,35 @@ void HeaderChain::consider_new_header(const HeaderIndex* idx) {
     set_active_tip(idx);
 }
 
+const HeaderIndex* HeaderChain::add_anchor(const std::vector<BlockHeader>& hs, int base_height,
+                                           const ArithU256& base_work) {
+    std::lock_guard<std::recursive_mutex> g(mu_);
+    if (hs.empty() || base_height <= 0) throw std::invalid_argument("add_anchor: empty run or height <= 0");
+    const HeaderIndex* prev = nullptr;
+    ArithU256 work = base_work;
+    for (size_t i = 0; i < hs.size(); ++i) {
+        const BlockHeader& h = hs[i];
+        const Uint256 hash = verifier_->block_hash(h, params_);
+        if (prev != nullptr && h.prev != prev->hash) throw std::invalid_argument("add_anchor: headers do not link");
+        if (index_.find(hash) != nullptr) throw std::invalid_argument("add_anchor: header already indexed");
+        HeaderIndex& idx = *storage_.alloc();
+        idx.hash = hash;
+        idx.prev = prev;
+        idx.height = base_height + int(i);
+        idx.time = h.time;
+        idx.bits = h.bits;
+        idx.header = h;
+        work = work + block_proof(h.bits);
+        idx.chain_work = work;
+        idx.skip = prev ? prev->ancestor(skip_height(idx.height)) : nullptr;
+        index_.insert(&idx);
+        prev = &idx;
+    }
+    ++version_;
+    consider_new_header(prev);
+    return prev;
+}
+
 const HeaderIndex* HeaderChain::tip() const {
     std::lock_guard<std::recursive_mutex> g(mu_);
     return active_.empty() ? nullptr : active_.back();

@@ -214,6 +214,14 @@ public:
                                const Uint256* known_hashes, const u32* known_bits) const;
     std::vector<AcceptResult> commit_headers(AcceptPrep& p, size_t hi);
 
+    // A run of stored headers continuing from a point this index does not hold (the state a node
+    // restored from its block-index database at height `base_height` has: LoadBlockIndexDB does
+    // not re-validate stored entries either): hs[0] at `base_height`, each next header's prev the
+    // previous one's hash, chain work `base_work` + the run's proofs. Not checked (trusted, like a
+    // loaded index); enough of them (>= 180) make DarkGravityWave and the median time past of the
+    // headers built on top exact. Returns the last entry (the new tip when it has the most work).
+    const HeaderIndex* add_anchor(const std::vector<BlockHeader>& hs, int base_height, const ArithU256& base_work);
+
     const HeaderIndex* tip() const;
     const HeaderIndex* genesis() const { return genesis_; }
     const HeaderIndex* at_height(int h) const;

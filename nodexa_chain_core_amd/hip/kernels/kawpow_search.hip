@@ -70,7 +70,8 @@
 //   KP_DPP        (always on; accepted for compatibility) rounds unrolled by 16, the item index
 //                 broadcast by DPP row_newbcast
 //   KP_BARRETT    5-op Barrett modulo for the item index
-//   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride), DAG < 4 GiB only
+//   KP_SBUFFER    structured-buffer DAG loads (item index x 256 B stride)
+//   KP_PTR64      (instead of KP_SBUFFER) 64-bit item addresses, one v_mad_u64_u32: DAGs >= 4 GiB
 //   KP_L1X4       L1 replicated 4x in LDS (64 KiB) so an L1 address is one
 //                 16-bit shift: ((x << 2) & 0xffff) reads l1[x % 4096]
 // Digests: each finished hash's 8 digest words go straight to the lane that owns the hash's
@@ -80,6 +81,7 @@
 #ifndef KP_BLOCK
 #define KP_BLOCK NODEXA_KAWPOW_BLOCK
 #endif
+
 #ifdef KP_MIN_WAVES
 #define KP_BOUNDS __launch_bounds__(KP_BLOCK, KP_MIN_WAVES)
 #else
@@ -137,7 +139,8 @@ NX_DEV uint32_t kp_fastmod(uint32_t x, const FastMod32& f) {
 #endif
 }
 
-// DAG item access: structured-buffer loads below 4 GiB, 64-bit pointers above.
+// DAG item access: structured-buffer loads (one V# below 4 GiB, two from 4 GiB up); the 64-bit
+// pointer form is kept for the untuned template.
 #if defined(KP_SBUFFER)
 // Structured-buffer addressing: vindex = item, stride 256 B in the V#, voffset = the lane's
 // 16-byte slice: one buffer_load_dwordx4 idxen offen per round and no address VALU at all
@@ -173,6 +176,40 @@ NX_DEV kp_dag_t kp_dag_handle(const void* dag) { return (const uint4*)dag; }
 NX_DEV uint4 kp_dag_item(kp_dag_t dag, uint32_t index, uint32_t part) {
     return kp_dag_load(dag + (size_t)index * 16 + part);
 }
+#endif
+#if defined(KP_PTR64)
+// DAGs of 4 GiB or more (epochs >= 385): MUBUF offsets are 32-bit, so the item address is a 64-bit
+// VGPR pair: one v_mad_u64_u32 (index * 256 + dag; dag an SGPR pair, 256 in a VGPR: one
+// constant-bus read on gfx9) and one v_or for the lane's 16-byte slice (lane ^ J) * 16, which
+// never carries: dag is 256-byte aligned. Measured at epoch 390 (profiles/r6_dag_over_4g):
+// +1.7 % over the 512-thread pointer form; the plain C pointer form at 768 threads hoists the 16
+// per-round 64-bit slice bases (32 VGPRs) and spills; a second V# for items >= 2^24 costs a second
+// load instruction per round (-9 %: the gather is address-bound); a branch in the round (either
+// V# per wave) spills the mix.
+typedef uint64_t kp_dag_p64;
+NX_DEV kp_dag_p64 kp_dag_handle_p64(const void* dag) { return (uint64_t)dag; }
+typedef __attribute__((address_space(1))) const kp_u32x4 kp_gu32x4;
+template <int J>
+NX_DEV uint4 kp_dag_item_p64(kp_dag_p64 dag, uint32_t index, uint32_t lane16) {
+    uint64_t a, carry;
+    const uint32_t k256 = 256u;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(a), "=s"(carry) : "v"(index), "v"(k256), "s"(dag));
+    const uint32_t lo = (uint32_t)a | (lane16 ^ (uint32_t)(J << 4));
+    kp_gu32x4* ptr = (kp_gu32x4*)((a & 0xffffffff00000000ull) | lo);
+#ifdef KP_NT_DAG
+    const kp_u32x4 v = __builtin_nontemporal_load(ptr);
+#else
+    const kp_u32x4 v = *ptr;
+#endif
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+#define KP_DAG kp_dag_p64
+#define KP_DAG_HANDLE kp_dag_handle_p64
+#define KP_DAG_ITEM_J(dag, index, part, J) kp_dag_item_p64<J>((dag), (index), (part ^ (uint32_t)J) << 4)
+#else
+#define KP_DAG kp_dag_t
+#define KP_DAG_HANDLE kp_dag_handle
+#define KP_DAG_ITEM_J(dag, index, part, J) kp_dag_item((dag), (index), (part))
 #endif
 
 // Broadcast lane j of each 16-lane row: DPP row_newbcast (one VALU op, no LDS
@@ -245,12 +282,12 @@ NX_DEV void kp_final(const uint32_t st2[8], const uint32_t digest[8], uint32_t o
 // One ProgPoW round with the round index known mod 16 (J): the item index comes
 // from lane J of the row via DPP and the lane's 16-byte slice is lane ^ J.
 template <int J>
-NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag,
+NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], const KP_DAG& dag,
                        const FastMod32& items, const uint32_t* l1, uint32_t lane) {
     uint4 d[KP_HASHES];
     const uint32_t part = lane ^ (uint32_t)J;
 #pragma unroll
-    for (int k = 0; k < KP_HASHES; ++k) d[k] = kp_dag_item(dag, kp_fastmod(kp_bcast<J>(mx[k][0]), items), part);
+    for (int k = 0; k < KP_HASHES; ++k) d[k] = KP_DAG_ITEM_J(dag, kp_fastmod(kp_bcast<J>(mx[k][0]), items), part, J);
 #ifdef KP_SCHED_FENCE
     // Keep the round's DAG merge after the whole cache/math program: left alone, the register-
     // pressure scheduler pulls the merge (and its vmcnt wait) into the middle of the program, so
@@ -266,7 +303,7 @@ NX_DEV void kp_round_c(uint32_t (&mx)[KP_HASHES][32], kp_dag_t dag,
     for (int k = 0; k < KP_HASHES; ++k) KAWPOW_DAG_MERGE(d[k], mx[k]);
 }
 
-NX_DEV void kp_group_hashes(kp_dag_t dag, const FastMod32& items, const uint32_t* l1,
+NX_DEV void kp_group_hashes(const KP_DAG& dag, const FastMod32& items, const uint32_t* l1,
                             uint32_t st0, uint32_t st1, uint32_t lane, uint32_t (&own)[8]) {
 #pragma unroll 1
     for (uint32_t h0 = 0; h0 < 16; h0 += KP_HASHES) {
@@ -344,7 +381,7 @@ extern "C" __global__ KP_BOUNDS void kawpow_search(KawpowSearchParams p) {
     {
         uint32_t st2[8];
         kp_seed(p.header, nonce, st2);
-        kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, digest);
+        kp_group_hashes(KP_DAG_HANDLE(p.dag), p.items, l1, st2[0], st2[1], lane, digest);
     }
     uint32_t st2[8], fin[8];
     // recomputed: cheaper than 6 VGPRs held across the mix loop. The nonce goes through an empty
@@ -382,7 +419,7 @@ extern "C" __global__ KP_BOUNDS void kawpow_hash_batch(KawpowHashParams p) {
     const KawpowVerifyJob j = p.jobs[valid ? job : 0];
     uint32_t st2[8], digest[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fin[8];
     kp_seed(j.header, j.nonce, st2);
-    kp_group_hashes(kp_dag_handle(p.dag), p.items, l1, st2[0], st2[1], lane, digest);
+    kp_group_hashes(KP_DAG_HANDLE(p.dag), p.items, l1, st2[0], st2[1], lane, digest);
     kp_final(st2, digest, fin);
     if (valid) {
         uint32_t* o = p.out + (size_t)job * 16;

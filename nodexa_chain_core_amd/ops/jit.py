@@ -98,16 +98,14 @@ DEFAULT_DEFINES: tuple[str, ...] = TUNED_DEFINES if _env is None else tuple(
 
 def defines_for(dag_bytes: int, defines: tuple[str, ...] | None = None) -> tuple[str, ...]:
     """The variant to compile for a DAG of `dag_bytes`: KP_SBUFFER addresses the DAG with 32-bit
-    buffer offsets, so it is dropped for DAGs of 4 GiB or more (epochs >= 385; measured there: the
-    structured form is not bit-exact, the pointer form is), and there the 768-thread form falls
-    back to 512 threads."""
+    buffer offsets, so for DAGs of 4 GiB or more (epochs >= 385; measured there: the structured
+    form is not bit-exact) it becomes KP_PTR64 (64-bit addresses by one v_mad_u64_u32), at the
+    same 768 threads / 6 waves per SIMD: profiles/r6_dag_over_4g, epoch 390, 273.0 MH/s against
+    268.6 for the 512-thread pointer form it replaces and 283.3 for the buffer form at epoch 384 on
+    the same box (1.2 % of that gap is the larger DAG itself: KP_PTR64 at epoch 384 runs 276.4)."""
     d = DEFAULT_DEFINES if defines is None else tuple(defines)
-    if dag_bytes >= 1 << 32:  # 32-bit buffer offsets: 64-bit pointers for DAGs of 4 GiB or more
-        d = tuple(x for x in d if x != "KP_SBUFFER")
-        if "KP_BLOCK=768" in d:
-            # the pointer path needs more VGPRs: at 6 waves/SIMD it spills and loses 4.5 % to the
-            # 512-thread / 4-wave form (profiles/r2n_kawpow768; r4b: 257.7 vs 269.3 MH/s, epoch 390)
-            d = tuple("KP_BLOCK=512" if x == "KP_BLOCK=768" else x for x in d if x != "KP_MIN_WAVES=6")
+    if dag_bytes >= 1 << 32 and "KP_SBUFFER" in d:  # 32-bit buffer offsets: 64-bit addresses
+        d = tuple("KP_PTR64" if x == "KP_SBUFFER" else x for x in d)
     return d
 
 

@@ -161,8 +161,8 @@ def _headline_epoch(core, epoch):
 @pytest.mark.parametrize("epoch", [384, 390])
 def test_shipped_variant_full_hash_at_headline_epochs(core, gpu, epoch):
     """The kernel variant that ships at each DAG size — epoch 384 (4.00 GiB: structured-buffer
-    loads, 768 threads, register digests, scheduling fences) and epoch 390 (4.05 GiB: 64-bit
-    pointer path) — hashes bit-exactly like the host golden model (_core.kawpow_hash, light mode),
+    loads, 768 threads, register digests, scheduling fences) and epoch 390 (4.05 GiB: the same form
+    with 64-bit item addresses, KP_PTR64) — hashes bit-exactly like the host golden model (_core.kawpow_hash, light mode),
     both through hash_batch and through search (every share of a window re-hashed in full)."""
     import torch
 
@@ -173,7 +173,8 @@ def test_shipped_variant_full_hash_at_headline_epochs(core, gpu, epoch):
     height = epoch * core.EPOCH_LENGTH + 123
     s = KawpowSearcher(e, height)
     variant = jit.defines_for(e.dag_bytes)
-    assert ("KP_SBUFFER" in variant) == (epoch == 384)
+    assert ("KP_SBUFFER" in variant) == (epoch == 384) and ("KP_PTR64" in variant) == (epoch == 390)
+    assert "KP_BLOCK=768" in variant and s.block == 768
     rng = random.Random(epoch)
     headers = [rng.randbytes(32) for _ in range(64)]
     nonces = [rng.getrandbits(64) for _ in range(64)]

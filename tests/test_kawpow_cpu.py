@@ -117,20 +117,20 @@ def test_light_cache_disk_cache(core, tmp_path):
 
 
 def test_search_variant_selection_by_dag_size(core):
-    """ops/jit.defines_for: the 32-bit buffer-offset DAG loads (KP_SBUFFER) are used
-    below 4 GiB only (epoch 384 is 4294962304 bytes; epoch 385 is above 2^32)."""
+    """ops/jit.defines_for: the 32-bit buffer-offset DAG loads (KP_SBUFFER) are used below 4 GiB
+    only (epoch 384 is 4294962304 bytes; epoch 385 is above 2^32); above, the 64-bit form
+    (KP_PTR64) keeps the 768-thread / 6-wave tuning."""
     from nodexa_chain_core_amd.ops import jit
 
     below = core.full_dataset_num_items(384) * 128
     above = core.full_dataset_num_items(385) * 128
     assert below < 1 << 32 <= above
-    assert "KP_SBUFFER" in jit.defines_for(below, jit.TUNED_DEFINES)
-    big = jit.defines_for(above, jit.TUNED_DEFINES)
-    assert "KP_SBUFFER" not in big and "KP_DPP" in big
-    # 768-thread register-digest form below 4 GiB, the 512-thread form on the pointer path
     small = jit.defines_for(below, jit.TUNED_DEFINES)
-    assert {"KP_BLOCK=768", "KP_MIN_WAVES=6"} <= set(small)
-    assert "KP_BLOCK=512" in big and "KP_BLOCK=768" not in big and "KP_MIN_WAVES=6" not in big
-    assert "KP_SBUFFER" not in jit.defines_for(above, ("KP_SBUFFER", "KP_DPP"))
+    big = jit.defines_for(above, jit.TUNED_DEFINES)
+    assert "KP_SBUFFER" in small and "KP_PTR64" not in small
+    assert "KP_SBUFFER" not in big and "KP_PTR64" in big and "KP_DPP" in big
+    for d in (small, big):
+        assert {"KP_BLOCK=768", "KP_MIN_WAVES=6", "KP_SCHED_FENCE", "KP_NT_DAG"} <= set(d)
+    assert jit.defines_for(above, ("KP_SBUFFER", "KP_DPP")) == ("KP_PTR64", "KP_DPP")
 
 
