@@ -118,7 +118,8 @@ def _verify_headers_bench(log) -> dict | None:
         W.barrier()
         t0 = time.perf_counter()
         r = resident(chain)
-        W.barrier()
+        # each rank's own time from the common start (a rank that waits for rank 0's verdict or
+        # for the all-gather includes that wait), the slowest rank's is the run's
         runs.append((W.all_reduce_max(time.perf_counter() - t0), r))
         if r["accepted"] != n or warm["accepted"] != n:
             raise SystemExit(f"header verify (resident): accepted {r['accepted']}/{n}, first reject {r['reject']}")
@@ -458,11 +459,26 @@ def _run_as_launcher(args) -> int:
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = str(s.getsockname()[1])
-    procs = []
+    import threading
+
+    procs, pumps = [], []
+
+    def pump(stream, rank):
+        # the one JSON line comes from rank 0's stdout; everything else a rank writes there (gloo's
+        # connect notices, native prints) goes to stderr, so stdout carries exactly that line
+        for line in iter(stream.readline, b""):
+            out = sys.stdout if rank == 0 and line.startswith(b"{") else sys.stderr
+            out.buffer.write(line)
+            out.flush()
+
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                             stdout=subprocess.PIPE)
+        procs.append(p)
+        pumps.append(threading.Thread(target=pump, args=(p.stdout, r), daemon=True))
+        pumps[-1].start()
     rc = 0
     term_at = None
     try:
@@ -489,6 +505,8 @@ def _run_as_launcher(args) -> int:
             if p.poll() is None:
                 p.kill()
         raise
+    for t in pumps:
+        t.join(timeout=10)
     return rc
 
 

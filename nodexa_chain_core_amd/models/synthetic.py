@@ -119,29 +119,68 @@ def _solve_equihash_header(h, params, solver, rng) -> None:
                     return
 
 
+ANCHOR_LEN = 181  # stored headers below a fixture that starts past genesis: DGW reads 180, MTP 11
+
+
+def make_anchor(params, first_height: int, end_time: int, seed: int = 1):
+    """The stored headers a node has below height `first_height` (HeaderChain.add_anchor): ANCHOR_LEN
+    linked KawPow-layout headers at the pow limit, 61 s apart, the last at `end_time`, plus the
+    chain work below them (the pow-limit proof per block). Their proof of work is not checked (a
+    loaded block index is not re-validated), so they are not mined. Returns (headers, base_height,
+    base_work)."""
+    base = first_height - ANCHOR_LEN
+    if base <= 0:
+        raise ValueError("an anchored fixture starts above height ANCHOR_LEN")
+    limit_bits = _core.HeaderChain(params).next_bits(params.genesis.header)  # height 1: the pow limit
+    chain = _core.HeaderChain(params)
+    out, prev = [], bytes(32)
+    for k in range(ANCHOR_LEN):
+        h = _core.BlockHeader()
+        h.version = 0x30000000
+        h.prev = prev
+        h.merkle_root = _core.sha256d(b"nodexa-anchor-%d-%d" % (seed, base + k))
+        h.time = end_time - 61 * (ANCHOR_LEN - 1 - k)
+        h.height = base + k
+        h.bits = limit_bits
+        h.nonce64 = k
+        out.append(h)
+        prev = chain.block_hash(h)
+    target, _, _ = _core.set_compact(limit_bits)
+    work = (1 << 256) // (target + 1)
+    return out, base, work * base
+
+
 def build_chain(n_kawpow: int, n_equihash: int = 0, network: str = "test", backend: str = "cpu", seed: int = 1,
-                device: int = 0, spacing: tuple[int, int] = (21, 101), progress=None):
-    """Mine `n_kawpow` KawPow headers then `n_equihash` Equihash-extension headers on
-    top of `network`'s genesis. Returns (params, headers)."""
+                device: int = 0, spacing: tuple[int, int] = (21, 101), progress=None, first_height: int = 1):
+    """Mine `n_kawpow` KawPow headers then `n_equihash` Equihash-extension headers on top of
+    `network`'s genesis, or (first_height > 1) on top of a make_anchor run ending at
+    first_height - 1 (a node's stored index at that height: the headline-epoch fixture starts at
+    2,880,000, epoch 384). Returns (params, headers); with an anchor, (params, headers, anchor)."""
     rng = random.Random(seed)
     base = synthetic_params(network)
-    times, t = [], int(base.genesis.header.time)
+    t0 = int(base.genesis.header.time) + 61 * (first_height - 1)
+    times, t = [], t0
     for _ in range(n_kawpow + n_equihash):
         t += rng.randint(*spacing)
         times.append(t)
     eq_act = times[n_kawpow] if n_equihash else None
     params = synthetic_params(network, eq_act)
     chain = _core.HeaderChain(params)
+    anchor = None
+    if first_height > 1:
+        anchor = make_anchor(params, first_height, t0, seed)
+        chain.add_anchor(*anchor)
     kp = _GpuKawpow(device) if backend == "gpu" else _CpuKawpow()
     eq = (_GpuEquihash(device) if backend == "gpu" else _CpuEquihash()) if n_equihash else None
     out = []
     for i in range(1, n_kawpow + n_equihash + 1):
+        height = first_height - 1 + i
         h = _core.BlockHeader()
         h.version = 0x30000000 | (_core.EQUIHASH_VERSION_BIT if i > n_kawpow else 0)
         h.prev = chain.tip().hash
-        h.merkle_root = _core.sha256d(b"nodexa-synthetic-%d-%d" % (seed, i))
+        h.merkle_root = _core.sha256d(b"nodexa-synthetic-%d-%d" % (seed, height))
         h.time = times[i - 1]
-        h.height = i
+        h.height = height
         h.bits = chain.next_bits(h)
         if i <= n_kawpow:
             hh = to_progpow(h.kawpow_header_hash())
@@ -149,7 +188,7 @@ def build_chain(n_kawpow: int, n_equihash: int = 0, network: str = "test", backe
             start = rng.getrandbits(40) << 16
             found = None
             while found is None:
-                found, tried = kp(i, hh, boundary, start)
+                found, tried = kp(height, hh, boundary, start)
                 start += tried
             nonce, fin, mix = found
             h.nonce64 = nonce
@@ -158,11 +197,11 @@ def build_chain(n_kawpow: int, n_equihash: int = 0, network: str = "test", backe
             _solve_equihash_header(h, params, eq, rng)
         r = chain.accept_header(h, h.time + 7200, i > n_kawpow)  # Equihash era: full check while mining
         if not r.ok:
-            raise RuntimeError(f"synthetic header {i} rejected: {r.reject}")
+            raise RuntimeError(f"synthetic header {height} rejected: {r.reject}")
         out.append(h)
         if progress and (i % 250 == 0 or (i > n_kawpow and i % 10 == 0)):  # Equihash headers are ~100x slower
             progress(i)
-    return params, out
+    return (params, out) if anchor is None else (params, out, anchor)
 
 
 def build_kawpow_chain(n: int, network: str = "test", backend: str = "cpu", seed: int = 1, device: int = 0,
@@ -170,7 +209,9 @@ def build_kawpow_chain(n: int, network: str = "test", backend: str = "cpu", seed
     return build_chain(n, 0, network, backend, seed, device, spacing, progress)
 
 
-def save(path: str, params, headers) -> None:
+def save(path: str, params, headers, anchor=None) -> None:
+    """`path`: the headers, serialized back to back; `path`.json: parameters; with an anchor
+    (make_anchor), `path`.anchor holds its headers and the json its height and chain work."""
     act = params.kawpow_activation_time
     with open(path, "wb") as f:
         for h in headers:
@@ -178,6 +219,13 @@ def save(path: str, params, headers) -> None:
     meta = {"network": params.network_id, "kawpow_activation_time": int(params.kawpow_activation_time),
             "equihash_activation_time": int(params.equihash_activation_time), "headers": len(headers),
             "equihash_headers": sum(1 for h in headers if h.is_equihash())}
+    if anchor is not None:
+        ahs, base_height, base_work = anchor
+        with open(path + ".anchor", "wb") as f:
+            for h in ahs:
+                f.write(h.serialize(act))
+        meta.update({"first_height": int(headers[0].height), "anchor_height": base_height,
+                     "anchor_headers": len(ahs), "anchor_work": hex(base_work)})
     with open(path + ".json", "w") as f:
         json.dump(meta, f, indent=1)
 
@@ -193,3 +241,24 @@ def load(path: str):
     if len(headers) != meta["headers"]:
         raise ValueError("header count mismatch")
     return params, headers
+
+
+def load_anchor(path: str, params):
+    """The fixture's anchor (make_anchor) as (headers, base_height, base_work), or None."""
+    with open(path + ".json") as f:
+        meta = json.load(f)
+    if "anchor_height" not in meta:
+        return None
+    with open(path + ".anchor", "rb") as f:
+        hs = _core.deserialize_headers(f.read(), params.kawpow_activation_time)
+    if len(hs) != meta["anchor_headers"]:
+        raise ValueError("anchor header count mismatch")
+    return hs, int(meta["anchor_height"]), int(meta["anchor_work"], 16)
+
+
+def new_chain(params, anchor=None):
+    """A HeaderChain for verifying a fixture: genesis, plus the fixture's anchor when it has one."""
+    chain = _core.HeaderChain(params)
+    if anchor is not None:
+        chain.add_anchor(*anchor)
+    return chain

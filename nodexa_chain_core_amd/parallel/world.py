@@ -171,9 +171,10 @@ def barrier() -> None:
 
 
 def broadcast_bytes(payload: bytes | None, size: int, src: int = 0) -> bytes:
-    """Broadcast a fixed-size packet (e.g. the 96-byte work packet) from `src`."""
+    """Broadcast a fixed-size packet (e.g. the 96-byte work packet) from `src`: a device tensor
+    over RCCL, a host tensor over gloo (which would copy a device tensor through the host anyway)."""
     w = get()
-    t = torch.zeros(size, dtype=torch.uint8, device=w.device)
+    t = torch.zeros(size, dtype=torch.uint8, device=w.device if w.backend == "nccl" else "cpu")
     if w.rank == src and payload is not None:
         if len(payload) != size:
             raise ValueError("payload size mismatch")
