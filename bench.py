@@ -38,7 +38,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-VERIFY_FIXTURE = os.path.join(ROOT, "tests", "data", "testnet_mixed_10k.hdr")
+VERIFY_FIXTURE = os.path.join(ROOT, "tests", "data", "testnet_mixed_10k.hdr")  # heights 1-10,000 (epochs 0-1)
+# heights 2,880,000-2,889,999 (epochs 384-385, 4 GiB DAGs, 64 MiB light caches), on a stored-index anchor
+VERIFY_FIXTURE_E384 = os.path.join(ROOT, "tests", "data", "testnet_mixed_e384_10k.hdr")
 
 
 def _baseline() -> tuple[float | None, str | None]:
@@ -64,7 +66,7 @@ def _baseline() -> tuple[float | None, str | None]:
     return None, None
 
 
-def _verify_headers_bench(log) -> dict | None:
+def _verify_headers_bench(log, fixture: str = VERIFY_FIXTURE) -> dict | None:
     """BASELINE config 5: the 10k-header fixture through ProcessNewBlockHeaders' work — parse the
     wire bytes, PoW of every header, DarkGravityWave + contextual rules, index insert — timed end to
     end (parse included). "resident" is the device-resident pipeline (models/verify.
@@ -83,17 +85,21 @@ def _verify_headers_bench(log) -> dict | None:
     from nodexa_chain_core_amd.parallel import world as W
     from nodexa_chain_core_amd.parallel.verify import verify_headers_distributed
 
-    if not os.path.exists(VERIFY_FIXTURE):
+    if not os.path.exists(fixture):
         return None
-    params, headers = synthetic.load(VERIFY_FIXTURE)
-    with open(VERIFY_FIXTURE, "rb") as f:
+    params, headers = synthetic.load(fixture)
+    anchor = synthetic.load_anchor(fixture, params)  # the stored index below a fixture past genesis
+    new_chain = functools.partial(synthetic.new_chain, params, anchor)
+    with open(fixture, "rb") as f:
         raw = f.read()
     act = params.kawpow_activation_time
     adjusted = headers[-1].time + 3600
     n = len(headers)
     w = W.get()
     dev = w.device.index
-    out = {"headers": n, "fixture": os.path.relpath(VERIFY_FIXTURE, ROOT)}
+    epochs = sorted({h.height // _core.EPOCH_LENGTH for h in headers if not h.is_equihash()})
+    out = {"headers": n, "fixture": os.path.relpath(fixture, ROOT), "heights": [headers[0].height, headers[-1].height],
+           "kawpow_epochs": epochs}
 
     # a node's header chain exists before a `headers` message arrives: each run gets a fresh
     # chain made (and, after the run, freed) outside the timed region
@@ -109,12 +115,12 @@ def _verify_headers_bench(log) -> dict | None:
         return r
 
     t0 = time.perf_counter()
-    warm = resident(_core.HeaderChain(params))  # every epoch's DAG and program table
+    warm = resident(new_chain())  # every epoch's DAG and program table
     torch.cuda.synchronize()
     setup = W.all_reduce_max(time.perf_counter() - t0)
     runs = []
     for _ in range(15):  # ~2 ms each: the median of 15 is steady box to box
-        chain = _core.HeaderChain(params)
+        chain = new_chain()
         W.barrier()
         t0 = time.perf_counter()
         r = resident(chain)
@@ -137,16 +143,17 @@ def _verify_headers_bench(log) -> dict | None:
                        ("rank 0, verdict broadcast (batch below NODEXA_VERIFY_SHARD_MIN)" if w.world_size > 1
                         else "one rank"),
                        "first_run_incl_epoch_setup_s": round(setup, 3)}
-    log(f"[bench] verify {n} headers (resident): {n / dt:.0f} headers/s (host {r['host_ms']:.2f} ms, "
-        f"{r['host_exposed_ms']:.2f} of it beside no device work, device "
+    log(f"[bench] verify {n} headers at heights {headers[0].height}-{headers[-1].height} (resident): {n / dt:.0f} "
+        f"headers/s (host {r['host_ms']:.2f} ms, {r['host_exposed_ms']:.2f} of it beside no device work, device "
         f"{r['device_ms']:.2f} ms, accept {r['accept_ms']:.2f} ms)")
     fn = functools.partial(verify_headers_distributed, mode="light")
     dgw_dev = dev if w.device.type == "cuda" else None
-    process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn, dgw_device=dgw_dev)  # light epochs
+    process_headers(new_chain(), headers, adjusted, verify_fn=fn, dgw_device=dgw_dev)  # light epochs
     torch.cuda.synchronize()
+    chain = new_chain()
     W.barrier()
     t0 = time.perf_counter()
-    r = process_headers(_core.HeaderChain(params), headers, adjusted, verify_fn=fn, dgw_device=dgw_dev)
+    r = process_headers(chain, headers, adjusted, verify_fn=fn, dgw_device=dgw_dev)
     torch.cuda.synchronize()
     W.barrier()
     dt = W.all_reduce_max(time.perf_counter() - t0)
@@ -155,7 +162,8 @@ def _verify_headers_bench(log) -> dict | None:
     out["light"] = {"mode": "light, no DAG (a non-mining node syncing a new epoch)", "headers_per_s": round(n / dt, 1),
                     "ms": round(dt * 1e3, 2), "pow_ms": round(r["pow_s"] * 1e3, 2),
                     "context_ms": round(r["context_s"] * 1e3, 2), "dgw_on_gpu": r["dgw_gpu"]}
-    log(f"[bench] verify {n} headers (light, no DAG): {n / dt:.0f} headers/s")
+    log(f"[bench] verify {n} headers at heights {headers[0].height}-{headers[-1].height} (light, no DAG): "
+        f"{n / dt:.0f} headers/s")
     return out
 
 
@@ -390,6 +398,12 @@ def main() -> int:
         eq = _equihash_bench(args, hdr, height, rank, log)
 
     verify = _verify_headers_bench(log) if args.verify and not cpu else None
+    if verify is not None:
+        # the same pipeline at the headline epoch (BASELINE config 5 on a live chain's heights)
+        v384 = _verify_headers_bench(log, VERIFY_FIXTURE_E384)
+        if v384 is not None:
+            verify["resident_e384"], verify["light_e384"] = v384["resident"], v384["light"]
+            verify["e384_fixture"] = {k: v384[k] for k in ("fixture", "heights", "kawpow_epochs", "headers")}
 
     if rank == 0:
         base, base_src = _baseline()
@@ -427,6 +441,11 @@ def main() -> int:
             "verify_headers": verify,
             "verify_headers_per_s": verify["resident"]["headers_per_s"] if verify else None,  # DAG resident (mining node)
             "verify_headers_light_per_s": verify["light"]["headers_per_s"] if verify else None,  # no DAG
+            # the same at heights 2,880,000-2,889,999 (epochs 384-385: 4 GiB DAGs, 64 MiB light caches)
+            "verify_headers_e384_per_s": verify["resident_e384"]["headers_per_s"] if verify and "resident_e384" in verify
+            else None,
+            "verify_headers_light_e384_per_s": verify["light_e384"]["headers_per_s"] if verify and "light_e384" in verify
+            else None,
             "baseline_mhs": base,
             "baseline_source": base_src,
         }

@@ -125,7 +125,7 @@ ANCHOR_LEN = 181  # stored headers below a fixture that starts past genesis: DGW
 def make_anchor(params, first_height: int, end_time: int, seed: int = 1):
     """The stored headers a node has below height `first_height` (HeaderChain.add_anchor): ANCHOR_LEN
     linked KawPow-layout headers at the pow limit, 61 s apart, the last at `end_time`, plus the
-    chain work below them (the pow-limit proof per block). Their proof of work is not checked (a
+    chain work below them (genesis, then the pow-limit proof per block). Their proof of work is not checked (a
     loaded block index is not re-validated), so they are not mined. Returns (headers, base_height,
     base_work)."""
     base = first_height - ANCHOR_LEN
@@ -147,7 +147,8 @@ def make_anchor(params, first_height: int, end_time: int, seed: int = 1):
         prev = chain.block_hash(h)
     target, _, _ = _core.set_compact(limit_bits)
     work = (1 << 256) // (target + 1)
-    return out, base, work * base
+    # genesis' work (testnet genesis is harder than the pow limit) + the pow-limit proof per block
+    return out, base, int(chain.genesis().chain_work) + work * (base - 1)
 
 
 def build_chain(n_kawpow: int, n_equihash: int = 0, network: str = "test", backend: str = "cpu", seed: int = 1,

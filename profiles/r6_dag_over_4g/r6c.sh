@@ -1,0 +1,7 @@
+mkdir -p gpurun_out/r6c
+A="KP_HASHES=1,KP_DPP,KP_BARRETT,KP_L1X4,KP_BLOCK=512,KP_NT_DAG,KP_SCHED_FENCE"
+B="KP_HASHES=1,KP_DPP,KP_BARRETT,KP_PTR64,KP_L1X4,KP_BLOCK=768,KP_MIN_WAVES=6,KP_NT_DAG,KP_SCHED_FENCE"
+C="KP_HASHES=1,KP_DPP,KP_BARRETT,KP_PTR64,KP_PTR64_NOASM,KP_L1X4,KP_BLOCK=768,KP_MIN_WAVES=6,KP_NT_DAG,KP_SCHED_FENCE"
+T="KP_HASHES=1,KP_DPP,KP_BARRETT,KP_SBUFFER,KP_L1X4,KP_BLOCK=768,KP_MIN_WAVES=6,KP_NT_DAG,KP_SCHED_FENCE"
+timeout -k 10 300 python tools/kawpow_sweep.py --epoch 390 --raw --rounds 11 --batch 33554432 --variants "$A" "$B" "$C" --out gpurun_out/r6c/e390.json > gpurun_out/r6c/e390.log 2>&1 && \
+timeout -k 10 300 python tools/kawpow_sweep.py --epoch 384 --raw --rounds 11 --batch 33554432 --variants "$T" "$B" "$C" --out gpurun_out/r6c/e384.json > gpurun_out/r6c/e384.log 2>&1

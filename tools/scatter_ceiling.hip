@@ -6,7 +6,7 @@
 // G = 1 is Equihash's one row per lane; G > 1 shows what a write-combined (bucket-major) layout
 // would get for the same bytes. NT = nontemporal stores.
 //
-//   hipcc --offload-arch=gfx950 -O3 -o scatter_ceiling tools/scatter_ceiling.hip && ./scatter_ceiling
+//   hipcc --offload-arch=gfx950 -O3 -o scatter_ceiling tools/scatter_ceiling.hip && ./scatter_ceiling [a|m|c]
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -185,9 +185,9 @@ static void run(const char* name, uint32_t* buf, size_t bytes, uint64_t lanes) {
         best = ms < best ? ms : best;
     }
     const double rows = double(grid) * 256 * PER;
-    std::printf("{\"variant\":\"%s\",\"row_bytes\":%d,\"run_lanes\":%d,\"nt\":%d,\"ms\":%.3f,\"tb_s\":%.3f,"
-                "\"grows_s\":%.2f}\n",
-                name, S, G, int(NT), best, rows * S / best / 1e9, rows / best / 1e6);
+    std::printf("{\"variant\":\"%s\",\"row_bytes\":%d,\"run_lanes\":%d,\"nt\":%d,\"target_mib\":%zu,\"ms\":%.3f,"
+                "\"tb_s\":%.3f,\"grows_s\":%.2f}\n",
+                name, S, G, int(NT), bytes >> 20, best, rows * S / best / 1e9, rows / best / 1e6);
     std::fflush(stdout);
 }
 
@@ -262,6 +262,24 @@ int main(int argc, char** argv) {
         CHECK(hipFree(buf));
         CHECK(hipFree(gcnt));
         CHECK(hipFree(dropped));
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'c') {
+        // Infinity Cache residency (round 6): the rounds' isolated-row stores into a target that
+        // fits the 256 MB MALL against one that does not. 64M rows per launch at every size, so a
+        // small target is rewritten many times (as a level's live rows would be by the next window)
+        const size_t max_bytes = size_t(4) << 30;
+        uint32_t* buf = nullptr;
+        CHECK(hipMalloc(&buf, max_bytes));
+        CHECK(hipMemset(buf, 0, max_bytes));
+        const uint64_t lanes = 1ull << 22;
+        for (size_t mib : {4096, 1024, 512, 256, 192, 128, 64, 32}) {
+            const size_t bytes = mib << 20;
+            run<16, 1, false>("row16", buf, bytes, lanes);
+            run<24, 1, false>("row24", buf, bytes, lanes);
+            run<32, 1, false>("row32", buf, bytes, lanes);
+        }
+        CHECK(hipFree(buf));
         return 0;
     }
     if (argc > 1 && argv[1][0] == 'm') {  // merge + gather probes only (tools/gpu_r4t.sh)
