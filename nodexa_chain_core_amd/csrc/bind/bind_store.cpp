@@ -96,6 +96,16 @@ void bind_store(py::module_& m) {
     }, py::arg("path"), py::arg("subdb") = "main",
        "Key/value records of a Berkeley DB btree file's sub-database (read-only; store/bdb.hpp)");
     m.def("bdb_databases", &bdb::databases, "Sub-database names of a Berkeley DB btree file");
+    m.def("bdb_write", [](const std::string& path, const py::list& records, const std::string& subdb, uint32_t pagesize) {
+        bdb::Records recs;
+        for (const auto& r : records) {
+            auto t = r.cast<py::tuple>();
+            recs.emplace_back(t[0].cast<std::string>(), t[1].cast<std::string>());
+        }
+        py::gil_scoped_release rel;
+        bdb::write_btree(path, std::move(recs), subdb, pagesize);
+    }, py::arg("path"), py::arg("records"), py::arg("subdb") = "main", py::arg("pagesize") = 4096,
+       "Write (key, value) byte records as a Berkeley DB btree file (sub-database `subdb`; store/bdb.hpp)");
     m.def("ldb_crc32c", [](const py::bytes& b) {
         const std::string s = b;
         return ldb::crc32c(s.data(), s.size());

@@ -594,7 +594,13 @@ void HeaderChain::update_active_chain() {
 // Re-point the active chain at `best`: only the entries from the fork point up change.
 void HeaderChain::set_active_tip(const HeaderIndex* best) {
     ++version_;
-    active_.resize(size_t(best->height) + 1, nullptr);
+    const size_t want = size_t(best->height) + 1;
+    if (want > active_.capacity()) {
+        // headroom for the next 2^20 headers (~35 days of chain): a 10k-header batch at height
+        // 2.88M must not reallocate and copy a 23 MB vector (3 ms, profiles/README r6g)
+        active_.reserve(want + (size_t(1) << 20));
+    }
+    active_.resize(want, nullptr);
     for (const HeaderIndex* p = best; p && active_[size_t(p->height)] != p; p = p->prev)
         active_[size_t(p->height)] = p;
 }

@@ -1,9 +1,12 @@
-// Read-only Berkeley DB btree reader (see bdb.hpp for the page format it walks).
+// Berkeley DB btree reader and writer (see bdb.hpp for the page format).
 #include "bdb.hpp"
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <random>
 #include <stdexcept>
 #include <utility>
 
@@ -182,7 +185,192 @@ std::string slurp(const std::string& path) {
     return std::string(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
 }
 
+// ------------------------------------------------------------------------------ writer
+constexpr uint32_t BTREE_VERSION = 9;  // Berkeley DB 4.8 .. 5.3
+constexpr uint8_t LEAFLEVEL = 1;
+
+struct Writer {
+    uint32_t ps;
+    std::vector<std::string> pages;  // page images, index = pgno
+
+    explicit Writer(uint32_t pagesize) : ps(pagesize) {}
+
+    static void put16(std::string& p, size_t off, uint16_t v) { std::memcpy(&p[off], &v, 2); }
+    static void put32(std::string& p, size_t off, uint32_t v) { std::memcpy(&p[off], &v, 4); }
+
+    uint32_t alloc(uint8_t type, uint8_t level) {
+        const uint32_t pgno = uint32_t(pages.size());
+        std::string p(ps, '\0');
+        put32(p, 0, 0);
+        put32(p, 4, 1);  // LSN {0, 1}: not logged
+        put32(p, 8, pgno);
+        put16(p, 22, uint16_t(ps));  // hf_offset: no items yet
+        p[24] = char(level);
+        p[25] = char(type);
+        pages.push_back(std::move(p));
+        return pgno;
+    }
+
+    // Bytes an item takes on a page (4-byte aligned) plus its index slot.
+    static size_t need(size_t item_bytes) { return ((item_bytes + 3) & ~size_t(3)) + 2; }
+    size_t free_bytes(uint32_t pgno) const {
+        const std::string& p = pages[pgno];
+        uint16_t n, hf;
+        std::memcpy(&n, &p[20], 2);
+        std::memcpy(&hf, &p[22], 2);
+        return size_t(hf) - (PAGE_HDR + 2 * size_t(n));
+    }
+    // Appends an item image (below the previous ones, index slot after the previous slots).
+    void add_item(uint32_t pgno, const std::string& item) {
+        std::string& p = pages[pgno];
+        uint16_t n, hf;
+        std::memcpy(&n, &p[20], 2);
+        std::memcpy(&hf, &p[22], 2);
+        const size_t sz = (item.size() + 3) & ~size_t(3);
+        if (sz + 2 > free_bytes(pgno)) throw std::logic_error("bdb writer: item does not fit");
+        const uint16_t off = uint16_t(hf - sz);
+        std::memcpy(&p[off], item.data(), item.size());
+        put16(p, PAGE_HDR + 2 * size_t(n), off);
+        put16(p, 20, uint16_t(n + 1));
+        put16(p, 22, off);
+    }
+    // A BOVERFLOW item pointing at a fresh chain of overflow pages holding `data`.
+    std::string overflow(const std::string& data) {
+        const size_t cap = ps - PAGE_HDR;
+        uint32_t first = 0, prev = 0;
+        for (size_t at = 0; at < data.size(); at += cap) {
+            const size_t len = std::min(cap, data.size() - at);
+            const uint32_t pg = alloc(P_OVERFLOW, 0);
+            std::string& p = pages[pg];
+            put16(p, 20, 1);  // reference count
+            put16(p, 22, uint16_t(len));  // OV_LEN: payload bytes on this page
+            put32(p, 12, prev);
+            std::memcpy(&p[PAGE_HDR], data.data() + at, len);
+            if (prev) put32(pages[prev], 16, pg);
+            if (!first) first = pg;
+            prev = pg;
+        }
+        std::string it(12, '\0');
+        it[2] = char(B_OVERFLOW);
+        put32(it, 4, first);
+        put32(it, 8, uint32_t(data.size()));
+        return it;
+    }
+    static std::string keydata(const std::string& data) {
+        std::string it(3, '\0');
+        put16(it, 0, uint16_t(data.size()));
+        it[2] = char(B_KEYDATA);
+        return it + data;
+    }
+    void meta(uint32_t pgno, uint32_t root, uint32_t last, uint32_t flags, const std::string& uid) {
+        std::string& p = pages[pgno];
+        std::fill(p.begin() + 12, p.end(), '\0');  // the meta layout reuses the page-header fields
+        put32(p, 12, BTREE_MAGIC);
+        put32(p, 16, BTREE_VERSION);
+        put32(p, 20, ps);
+        p[25] = char(P_BTREEMETA);
+        put32(p, 32, last);
+        put32(p, 48, flags);
+        std::memcpy(&p[52], uid.data(), 20);
+        put32(p, 76, 2);  // minkey
+        put32(p, 88, root);
+    }
+
+    // The btree of sorted `recs`: returns its root page.
+    uint32_t tree(const Records& recs) {
+        // items larger than the overflow size go to overflow pages (B_MINKEY_TO_OVFLSIZE, minkey 2)
+        const size_t ovfl = (ps - PAGE_HDR) / 4 - 8;
+        std::vector<std::pair<uint32_t, std::string>> level;  // (page, first key) of this level
+        uint32_t leaf = alloc(P_LBTREE, LEAFLEVEL);
+        level.emplace_back(leaf, recs.empty() ? std::string() : recs[0].first);
+        for (const auto& [k, v] : recs) {
+            const std::string ki = k.size() > ovfl ? overflow(k) : keydata(k);
+            const std::string vi = v.size() > ovfl ? overflow(v) : keydata(v);
+            if (need(ki.size()) + need(vi.size()) > free_bytes(leaf)) {
+                const uint32_t next = alloc(P_LBTREE, LEAFLEVEL);
+                put32(pages[leaf], 16, next);  // leaf siblings are linked
+                put32(pages[next], 12, leaf);
+                leaf = next;
+                level.emplace_back(leaf, k);
+            }
+            add_item(leaf, ki);
+            add_item(leaf, vi);
+        }
+        // internal levels until one page holds the level
+        for (uint8_t lv = LEAFLEVEL + 1; level.size() > 1; ++lv) {
+            std::vector<std::pair<uint32_t, std::string>> up;
+            uint32_t pg = alloc(P_IBTREE, lv);
+            up.emplace_back(pg, level[0].second);
+            for (size_t i = 0; i < level.size(); ++i) {
+                // BINTERNAL: len, type, unused, child pgno, nrecs, key (empty on a page's first entry)
+                std::string key = pages[pg][20] == 0 && pages[pg][21] == 0 ? std::string() : level[i].second;
+                auto item = [&](const std::string& kk) {
+                    std::string it(12, '\0');
+                    put16(it, 0, uint16_t(kk.size()));
+                    it[2] = char(B_KEYDATA);
+                    put32(it, 4, level[i].first);
+                    return it + kk;
+                };
+                if (key.size() > ovfl) throw std::invalid_argument("bdb writer: key longer than the overflow size");
+                if (need(item(key).size()) > free_bytes(pg)) {
+                    pg = alloc(P_IBTREE, lv);
+                    up.emplace_back(pg, level[i].second);
+                    key.clear();
+                }
+                add_item(pg, item(key));
+            }
+            level.swap(up);
+        }
+        return level[0].first;
+    }
+};
+
 }  // namespace
+
+std::string write_btree_bytes(Records records, const std::string& subdb, uint32_t pagesize, const std::string& uid_in) {
+    if (pagesize < 512 || pagesize > 65536 || (pagesize & (pagesize - 1))) throw std::invalid_argument("bad page size");
+    if (subdb.empty()) throw std::invalid_argument("bdb writer: a sub-database name is required");
+    // __bam_defcmp: bytewise, a prefix sorts first
+    std::sort(records.begin(), records.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (size_t i = 1; i < records.size(); ++i)
+        if (records[i].first == records[i - 1].first) throw std::invalid_argument("bdb writer: duplicate key");
+    std::string uid = uid_in;
+    if (uid.size() != 20) {
+        std::random_device rd;
+        uid.assign(20, '\0');
+        for (auto& c : uid) c = char(rd());
+    }
+    Writer w(pagesize);
+    w.alloc(P_BTREEMETA, 0);                  // 0: master meta
+    const uint32_t mleaf = w.alloc(P_LBTREE, LEAFLEVEL);  // 1: master root leaf
+    w.alloc(P_BTREEMETA, 0);                  // 2: the sub-database's meta
+    const uint32_t root = w.tree(records);
+    std::string pg(4, '\0');
+    const uint32_t be = __builtin_bswap32(2u);  // network byte order (__db_master_update)
+    std::memcpy(&pg[0], &be, 4);
+    w.add_item(mleaf, Writer::keydata(subdb));
+    w.add_item(mleaf, Writer::keydata(pg));
+    const uint32_t last = uint32_t(w.pages.size() - 1);
+    w.meta(0, mleaf, last, BTM_SUBDB, uid);
+    w.meta(2, root, 2, BTM_SUBDB, uid);
+    std::string out;
+    out.reserve(w.pages.size() * size_t(pagesize));
+    for (const auto& p : w.pages) out += p;
+    return out;
+}
+
+void write_btree(const std::string& path, Records records, const std::string& subdb, uint32_t pagesize) {
+    const std::string data = write_btree_bytes(std::move(records), subdb, pagesize);
+    const std::string tmp = path + ".tmp";
+    {
+        std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+        if (!f) throw std::runtime_error("cannot write " + tmp);
+        f.write(data.data(), std::streamsize(data.size()));
+        f.flush();
+        if (!f) throw std::runtime_error("short write to " + tmp);
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot rename " + tmp);
+}
 
 Records read_btree_bytes(std::string data, const std::string& subdb) {
     File f(std::move(data));

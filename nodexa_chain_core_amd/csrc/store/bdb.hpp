@@ -1,4 +1,4 @@
-// Read-only reader of Berkeley DB btree files (the reference's wallet.dat).
+// Reader and writer of Berkeley DB btree files (the reference's wallet.dat).
 //
 // The reference keeps its wallet in a Berkeley DB 4.8 btree file with the records in a
 // sub-database named "main" (src/wallet/db.cpp:235, 436, 536: Db::open(..., "main", DB_BTREE,
@@ -41,6 +41,18 @@ Records read_btree_bytes(std::string data, const std::string& subdb);
 
 // Names of the sub-databases of the file (empty for a file without any).
 std::vector<std::string> databases(const std::string& path);
+
+// A btree file holding `records` (any order; duplicate keys refused) in sub-database `subdb`, in
+// the layout Berkeley DB 4.8-5.3 writes without an environment (version 9, host byte order,
+// LSNs "not logged", no checksums): master meta page, master leaf mapping the name to the
+// sub-database's meta page (network byte order), that meta page, then the tree -- full leaf pages
+// linked left to right, internal levels above them, items over the overflow size on overflow page
+// chains. The file is written to `path`.tmp and renamed over `path`. The reference opens it as a
+// wallet (src/wallet/db.cpp: Db::open(..., "main", DB_BTREE, ...)); libdb's own verifier accepts it
+// (tests/test_walletdb.py).
+void write_btree(const std::string& path, Records records, const std::string& subdb, uint32_t pagesize = 4096);
+std::string write_btree_bytes(Records records, const std::string& subdb, uint32_t pagesize = 4096,
+                              const std::string& uid = std::string());
 
 }  // namespace bdb
 }  // namespace nodexa

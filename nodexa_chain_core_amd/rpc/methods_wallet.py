@@ -454,17 +454,27 @@ def register(table, node) -> None:
         return None
 
     def rpc_backupwallet(p):
-        """backupwallet "destination" """
+        """backupwallet "destination" — a destination ending in ".dat" gets the reference's own
+        format (a Berkeley DB wallet.dat that clore_blockchaind opens: wallet/walletdb.
+        write_wallet_dat; an encrypted wallet whose BIP39 data is not held in that form must be
+        unlocked), any other name a copy of this node's JSON wallet."""
         if not p:
             raise RPCError(RPC_INVALID_PARAMETER, 'backupwallet "destination"')
         w = wallet()
         with w.lock:
             w._save()
-            import shutil
-
             try:
-                shutil.copyfile(w.path, p[0])
-            except OSError as e:
+                if str(p[0]).endswith(".dat"):
+                    from ..wallet.walletdb import write_wallet_dat
+
+                    write_wallet_dat(w, p[0])
+                else:
+                    import shutil
+
+                    shutil.copyfile(w.path, p[0])
+            except WalletError as e:
+                raise RPCError(-13, str(e))
+            except (OSError, RuntimeError) as e:
                 raise RPCError(RPC_WALLET_ERROR, f"Error: Wallet backup failed! {e}")
         return None
 

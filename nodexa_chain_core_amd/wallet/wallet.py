@@ -223,7 +223,7 @@ class Wallet:
                        "mnemonic_passphrase": hd.get("mnemonic_passphrase"),
                        "mnemonic_crypted": bytes.fromhex(hd["mnemonic_crypted"]) if hd.get("mnemonic_crypted")
                        else None}
-            for f in ("seed_iv", "ref_words_crypted", "ref_pass_crypted"):  # an imported wallet.dat's
+            for f in ("seed_iv", "ref_words_crypted", "ref_pass_crypted", "ref_word_hash"):  # an imported wallet.dat's
                 if hd.get(f) is not None:
                     self.hd[f] = bytes.fromhex(hd[f])
         for rs in data.get("redeem_scripts", []):
@@ -321,6 +321,7 @@ class Wallet:
                     word_hash, words_c = b39["cbip39words"]
                     hd["seed_crypted"] = b39["cbip39vchseed"]
                     hd["seed_iv"] = word_hash[:16]
+                    hd["ref_word_hash"] = word_hash  # kept whole: a wallet.dat export writes it back
                     hd["ref_words_crypted"] = words_c
                     hd["ref_pass_crypted"] = b39.get("cbip39passphrase", b"")
                 else:
@@ -366,7 +367,7 @@ class Wallet:
                           "mnemonic_passphrase": self.hd.get("mnemonic_passphrase") if plain else None,
                           "mnemonic_crypted": self.hd["mnemonic_crypted"].hex() if self.hd.get("mnemonic_crypted")
                           else None}
-            for f in ("seed_iv", "ref_words_crypted", "ref_pass_crypted"):
+            for f in ("seed_iv", "ref_words_crypted", "ref_pass_crypted", "ref_word_hash"):
                 if self.hd.get(f) is not None:
                     data["hd"][f] = self.hd[f].hex()
         if self.mkey is not None:

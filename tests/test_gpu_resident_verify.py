@@ -20,18 +20,27 @@ def _load(core, fixture):
     return params, list(headers), raw
 
 
-@pytest.mark.parametrize("fixture", ["testnet_kawpow_10k.hdr", "testnet_mixed_10k.hdr"])
+def _chain(core, params, fixture):
+    """A fresh chain for `fixture`: genesis, plus its stored-index anchor when it starts past genesis
+    (the headline-epoch fixture, heights 2,880,000-2,889,999)."""
+    from nodexa_chain_core_amd.models import synthetic
+
+    return synthetic.new_chain(params, synthetic.load_anchor(os.path.join(DATA, fixture), params))
+
+
+@pytest.mark.parametrize("fixture", ["testnet_kawpow_10k.hdr", "testnet_mixed_10k.hdr", "testnet_mixed_e384_10k.hdr"])
 def test_resident_matches_host_chain(core, gpu, fixture):
+    """Epochs 0-1 and the headline epochs 384-385 (4 GiB DAGs)."""
     from nodexa_chain_core_amd.models.verify import process_batch_resident
 
     params, hs, raw = _load(core, fixture)
     act = params.kawpow_activation_time
     adj = hs[-1].time + 3600
-    ref = core.HeaderChain(params)
+    ref = _chain(core, params, fixture)
     assert all(r.ok for r in ref.accept_headers(hs, adj, False))
     batch = core.HeaderBatch.from_bytes(raw, act)
     for _ in range(2):  # cold (epoch DAGs, program tables) and warm
-        c = core.HeaderChain(params)
+        c = _chain(core, params, fixture)
         r = process_batch_resident(c, batch, adj, device=0)
         assert r["accepted"] == len(hs) and r["reject"] is None, r
         assert c.tip().hash == ref.tip().hash and c.height() == ref.height()
@@ -61,7 +70,8 @@ def _tampered(core, params, hs, i, field):
 @pytest.mark.parametrize("field,fixture,index", [("mix", "testnet_kawpow_10k.hdr", 4321),
                                                  ("nonce", "testnet_kawpow_10k.hdr", 9000),
                                                  ("bits", "testnet_kawpow_10k.hdr", 7000),
-                                                 ("solution", "testnet_mixed_10k.hdr", None)])
+                                                 ("solution", "testnet_mixed_10k.hdr", None),
+                                                 ("mix", "testnet_mixed_e384_10k.hdr", 8100)])
 def test_resident_rejects_like_host(core, gpu, field, fixture, index):
     from nodexa_chain_core_amd.models.verify import process_batch_resident
 
@@ -71,9 +81,9 @@ def test_resident_rejects_like_host(core, gpu, field, fixture, index):
         index = next(i for i in range(len(hs) - 1, 0, -1) if hs[i].is_equihash())
     bad = _tampered(core, params, hs, index, field)
     adj = hs[-1].time + 3600
-    want = core.HeaderChain(params).accept_headers(bad, adj, True)  # host golden PoW
+    want = _chain(core, params, fixture).accept_headers(bad[:index + 1], adj, True)  # host golden PoW
     batch = core.HeaderBatch.from_headers(bad, act)
-    c = core.HeaderChain(params)
+    c = _chain(core, params, fixture)
     r = process_batch_resident(c, batch, adj, device=0)
     assert r["accepted"] == len(want) - 1 == index, (r, want[-1].reject)
     assert r["reject"]["index"] == index and r["reject"]["reason"] == want[-1].reject

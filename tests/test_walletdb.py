@@ -390,3 +390,179 @@ def test_node_imports_reference_wallet_dat(core, node_factory, tmp_path):  # noq
     assert c.validateaddress(a0)["ismine"] is True
     assert c.dumpprivkey(a0) == core.base58check_encode(bytes([114]) + secrets[0] + b"\x01")  # regtest WIF
     assert os.path.exists(d / "wallet.json") and os.path.exists(d / "wallet.dat")
+
+
+# ------------------------------------------------------------------ export (wallet/walletdb.py)
+def _libdb_records(path: str):
+    """Every (key, value) of sub-database "main" read by libdb itself (DB->open + a DB_NEXT cursor),
+    after DB->verify of the whole file."""
+    db = ctypes.c_void_p()
+    assert LIBDB.db_create(ctypes.byref(db), None, 0) == 0
+    assert LIBDB.__db_verify_pp(db, path.encode(), None, None, 0) == 0  # DB->verify closes the handle
+    db = ctypes.c_void_p()
+    assert LIBDB.db_create(ctypes.byref(db), None, 0) == 0
+    assert LIBDB.__db_open_pp(db, None, path.encode(), b"main", 1, 0, 0) == 0  # DB_BTREE
+    dbc = ctypes.c_void_p()
+    assert LIBDB.__db_cursor_pp(db, None, ctypes.byref(dbc), 0) == 0
+    out = []
+    while True:
+        k, v = _DBT(), _DBT()
+        if LIBDB.__dbc_get_pp(dbc, ctypes.byref(k), ctypes.byref(v), 16) != 0:  # DB_NEXT
+            break
+        out.append((ctypes.string_at(k.data, k.size), ctypes.string_at(v.data, v.size)))
+    LIBDB.__db_close_pp(db, 0)
+    return out
+
+
+def test_bdb_writer_pages_and_overflow(core, tmp_path):
+    """The native writer (csrc/store/bdb.cpp) over records that need several leaf pages, an
+    internal level and overflow chains; read back by this reader (and by libdb when present)."""
+    import random
+
+    rng = random.Random(3)
+    recs = {rng.randbytes(rng.randint(1, 60)): rng.randbytes(rng.choice([1, 40, 300, 1500, 9000])) for _ in range(700)}
+    path = str(tmp_path / "w.dat")
+    core.bdb_write(path, list(recs.items()))
+    assert core.bdb_read(path, "main") == sorted(recs.items())
+    assert core.bdb_databases(path) == ["main"]
+    if LIBDB is not None:
+        assert _libdb_records(path) == sorted(recs.items())
+    with pytest.raises(Exception):
+        core.bdb_write(path, [(b"a", b"1"), (b"a", b"2")])  # duplicate key
+
+
+@needs_libdb
+def test_bdb_writer_file_takes_libdb_updates(core, tmp_path):
+    """libdb inserts into a file this writer made (page splits included), and both readers agree."""
+    path = str(tmp_path / "w.dat")
+    base = [(b"k%04d" % i, b"v" * 30) for i in range(200)]
+    core.bdb_write(path, base)
+    more = [(b"m%04d" % i, bytes([i % 256]) * 90) for i in range(300)]
+    bdb_write(path, more)
+    assert core.bdb_read(path, "main") == sorted(base + more) == _libdb_records(path)
+
+
+def _export_reimport(core, params, w, tmp_path, name="out.dat"):
+    from nodexa_chain_core_amd.wallet.walletdb import write_wallet_dat
+    from nodexa_chain_core_amd.wallet.wallet import Wallet
+
+    dat = str(tmp_path / name)
+    n = write_wallet_dat(w, dat)
+    assert n > 0
+    if LIBDB is not None:
+        assert len(_libdb_records(dat)) == n
+    return Wallet(None, params, str(tmp_path / (name + ".json")), import_from=dat), dat
+
+
+def test_export_plain_bip44_wallet_round_trips(core, tmp_path):
+    """A wallet made here (BIP44 / BIP39) written as a reference wallet.dat and imported again:
+    the same keys, labels, words, keypool and the HD chain continuing at the same index."""
+    from nodexa_chain_core_amd.wallet.wallet import Wallet
+    from nodexa_chain_core_amd.wallet.walletdb import read_wallet_dat
+
+    params = _params()
+    w = Wallet(None, params, str(tmp_path / "w.json"))
+    a1 = w.new_address("alice")
+    a2 = w.new_address("")
+    w.keypool_refill(3)
+    w2, dat = _export_reimport(core, params, w, tmp_path)
+    ref = read_wallet_dat(dat)
+    assert ref["version"] == 4040402 and ref["hdchain"]["version"] == 3 and ref["hdchain"]["bip44"]
+    assert ref["hdchain"]["seed_id"] == core.hash160(b"")  # what the reference writes for a BIP39 seed
+    assert len(ref["keys"]) == len(w.keys) and len(ref["pool"]) == len(w.pool) == 3
+    assert ref["names"][a1] == "alice" and ref["purposes"][a1] == "receive"
+    assert w2.mnemonic() == w.mnemonic()
+    assert w2.dump_privkey(a1) == w.dump_privkey(a1) and w2.dump_privkey(a2) == w.dump_privkey(a2)
+    assert w2.labels[core.hash160(core.secp_pubkey_create(w.keys[w.pool[0]][0], True))] == "" and w2.pool == w.pool
+    for _ in range(5):  # pool first, then the chain continues where the exported wallet stands
+        assert w2.new_address("x") == w.new_address("x")
+
+
+def test_export_legacy_hd_wallet_round_trips(core, tmp_path):
+    """-bip44=0 (the 0.15 layout): the seed becomes a wallet key of keypath "s" named by the HD
+    chain, and the chain continues at the same m/0'/0'/i'."""
+    from nodexa_chain_core_amd.wallet.wallet import Wallet
+    from nodexa_chain_core_amd.wallet.walletdb import read_wallet_dat
+
+    params = _params()
+    w = Wallet(None, params, str(tmp_path / "w.json"), bip44=False)
+    a = [w.new_address("l%d" % i) for i in range(3)]
+    w2, dat = _export_reimport(core, params, w, tmp_path)
+    ref = read_wallet_dat(dat)
+    spub = core.secp_pubkey_create(w.hd["seed"], True)
+    assert ref["hdchain"]["version"] == 2 and ref["hdchain"]["seed_id"] == core.hash160(spub)
+    assert ref["keymeta"][spub]["hdkeypath"] == "s"
+    assert [w2.dump_privkey(x) for x in a] == [w.dump_privkey(x) for x in a]
+    assert w2.new_address("y") == w.new_address("y")
+
+
+def test_export_encrypted_wallet_round_trips(core, tmp_path):
+    """An encrypted wallet exports its master key and encrypted secrets as they are and its BIP39
+    data in the reference's form (EncryptBip39: IV = word hash); locked, a wallet made here refuses
+    (its BIP39 data is held in this node's form); the import unlocks with the same passphrase."""
+    from nodexa_chain_core_amd.wallet.wallet import Wallet, WalletError
+    from nodexa_chain_core_amd.wallet.walletdb import read_wallet_dat, write_wallet_dat
+
+    params = _params()
+    w = Wallet(None, params, str(tmp_path / "w.json"))
+    a1 = w.new_address("a")
+    words = w.mnemonic()
+    wif = w.dump_privkey(a1)
+    w.encrypt("pw one")
+    with pytest.raises(WalletError, match="passphrase"):
+        write_wallet_dat(w, str(tmp_path / "locked.dat"))
+    w.unlock("pw one")
+    w2, dat = _export_reimport(core, params, w, tmp_path)
+    ref = read_wallet_dat(dat)
+    assert ref["mkeys"] and not ref["keys"] and len(ref["ckeys"]) == len(w.keys)
+    assert {"cbip39words", "cbip39vchseed"} <= set(ref["bip39"]) and "bip39words" not in ref["bip39"]
+    assert w2.locked
+    w2.unlock("pw one")
+    assert w2.dump_privkey(a1) == wif and w2.mnemonic() == words
+    # once imported, the reference form is kept: the imported wallet exports again while locked
+    w2.lock_wallet()
+    w3, _ = _export_reimport(core, params, w2, tmp_path, "again.dat")
+    w3.unlock("pw one")
+    assert w3.dump_privkey(a1) == wif and w3.mnemonic() == words
+
+
+@needs_libdb
+def test_reference_fixture_survives_import_export(core, tmp_path):
+    """A wallet.dat in the reference's layout (written by libdb) -> import -> export -> import: the
+    keys, labels, pool, scripts and HD chain come through unchanged."""
+    from nodexa_chain_core_amd.wallet import bip39
+    from nodexa_chain_core_amd.wallet.wallet import Wallet
+
+    params = _params()
+    words = bip39.generate(128)
+    recs, secrets, seed = _bip44_wallet_records(core, words, "pp", 3)
+    a0 = _p2pkh_addr(core, params, secrets[0])
+    recs.append((rkey("name", vec(a0.encode())), vec(b"savings")))
+    recs.append(pool_record(1, core.secp_pubkey_create(secrets[2], True)))
+    redeem = b"\x51\x21" + core.secp_pubkey_create(secrets[1], True) + b"\x51\xae"
+    recs.append((rkey("cscript", core.hash160(redeem)), vec(redeem)))
+    dat = str(tmp_path / "wallet.dat")
+    bdb_write(dat, recs)
+    w = Wallet(None, params, str(tmp_path / "w.json"), import_from=dat)
+    w2, _ = _export_reimport(core, params, w, tmp_path)
+    assert w2.mnemonic() == (words, "pp") and w2.dump_privkey(a0) == w.dump_privkey(a0)
+    assert w2.labels[core.hash160(core.secp_pubkey_create(secrets[0], True))] == "savings"
+    assert w2.pool == w.pool and w2.redeem_scripts == w.redeem_scripts
+    assert w2.new_address("z") == w.new_address("z")
+
+
+def test_backupwallet_writes_reference_wallet_dat(core, node_factory, tmp_path):  # noqa: F811
+    """backupwallet to a .dat name: a wallet.dat in the reference's format holding the node's keys."""
+    from nodexa_chain_core_amd.wallet.walletdb import read_wallet_dat
+
+    node, addr = node_factory()
+    c = client(node)
+    a = c.getnewaddress("backup-label")
+    dest = str(tmp_path / "backup.dat")
+    c.backupwallet(dest)
+    ref = read_wallet_dat(dest)
+    assert ref["names"][a] == "backup-label" and ref["hdchain"] is not None
+    w = node.wallets[next(iter(node.wallets))] if hasattr(node, "wallets") else node.wallet
+    assert len(ref["keys"]) == len(w.keys)
+    c.backupwallet(str(tmp_path / "backup.json"))  # any other name: the JSON wallet
+    assert open(tmp_path / "backup.json").read().lstrip().startswith("{")
