@@ -306,9 +306,8 @@ class Node:
             w.reject_long_chains = a.get_bool("walletrejectlongchains", False)
         # Berkeley DB tuning / recovery options of the reference wallet (src/wallet/init.cpp): the
         # wallet here is a JSON file rewritten atomically on every change (older layouts upgraded
-        # on load), so these have nothing to act on; -upnp needs miniupnpc, not built here either
-        for flag in ("dblogsize", "flushwallet", "privdb", "salvagewallet", "upgradewallet", "upnp",
-                     "fuzzmessagestest"):
+        # on load), so these have nothing to act on
+        for flag in ("dblogsize", "flushwallet", "privdb", "salvagewallet", "upgradewallet", "fuzzmessagestest"):
             if a.is_set(flag):
                 log.log_printf(f"-{flag} has no effect in this build")
         # -maxsigcachesize (MiB, src/script/sigcache.cpp InitSignatureCache): bounded by its 32-byte entries
@@ -686,6 +685,12 @@ class Node:
 
             h, pt = parse_host_port(ext, cm.port or self.params.default_port)
             cm.add_local(h, pt, 4)
+        if listen is not None and a.get_bool("upnp", False):  # MapPort(-upnp): net/upnp.py
+            from .net.upnp import PortMapper
+
+            self.upnp = PortMapper(cm.port, add_local=cm.add_local,
+                                   discover_external=a.get_bool("discover", True))
+            self.upnp.start()
         if listen is not None and a.get_bool("listenonion", True):  # StartTorControl (src/init.cpp)
             from .net.torcontrol import DEFAULT_TOR_CONTROL, TorController
 
@@ -777,6 +782,8 @@ class Node:
                 log.log_printf(f"Failed to write fee estimates: {e}")
         if getattr(self, "torcontrol", None) is not None:
             self.torcontrol.stop()  # InterruptTorControl / StopTorControl
+        if getattr(self, "upnp", None) is not None:
+            self.upnp.stop()  # MapPort(false): the mapping is deleted
         if getattr(self, "connman", None) is not None:
             self.connman.stop()
         if self.state is not None:
