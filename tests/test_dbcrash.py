@@ -90,7 +90,7 @@ from nodexa_chain_core_amd.utils.config import ArgsManager
 from nodexa_chain_core_amd.rpc.client import RPCClient
 from nodexa_chain_core_amd import _core
 a = ArgsManager()
-a.parse_parameters(["-regtest", "-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p", "-printtoconsole=0",
+a.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", "-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p", "-printtoconsole=0",
                     "-dbcrashratio={ratio}"])
 n = Node(a)
 n.start()
@@ -142,7 +142,7 @@ from nodexa_chain_core_amd.node import Node
 from nodexa_chain_core_amd.utils.config import ArgsManager
 from nodexa_chain_core_amd.rpc.client import RPCClient
 a = ArgsManager()
-a.parse_parameters(["-regtest", "-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p", "-printtoconsole=0",
+a.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", "-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p", "-printtoconsole=0",
                     "-prune=1", "-addressindex", "-spentindex", "-dbcrashratio={ratio}"])
 n = Node(a)
 n.start()

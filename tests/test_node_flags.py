@@ -299,7 +299,7 @@ from nodexa_chain_core_amd.node import Node
 from nodexa_chain_core_amd.utils.config import ArgsManager
 from nodexa_chain_core_amd import _core
 a = ArgsManager()
-a.parse_parameters(["-regtest", "-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p", "-printtoconsole=0",
+a.parse_parameters(["-regtest", "-kawpowactivationtime=1524179367", "-datadir={d}", "-rpcport=0", "-rpcuser=u", "-rpcpassword=p", "-printtoconsole=0",
                     "-dbcrashratio=1"])
 n = Node(a)
 n.start()
