@@ -20,6 +20,7 @@ from __future__ import annotations
 import os
 import socket
 import threading
+import urllib.error
 import urllib.parse
 import urllib.request
 import xml.etree.ElementTree as ET
@@ -31,6 +32,7 @@ IGD_SEARCH = ("urn:schemas-upnp-org:device:InternetGatewayDevice:1",
               "urn:schemas-upnp-org:device:InternetGatewayDevice:2")
 WAN_SERVICES = ("urn:schemas-upnp-org:service:WANIPConnection:2", "urn:schemas-upnp-org:service:WANIPConnection:1",
                 "urn:schemas-upnp-org:service:WANPPPConnection:1")
+MAX_XML = 256 << 10  # a device description or SOAP reply larger than this is refused (LAN input)
 LOCAL_UPNP = 3  # the reference's address score of a UPnP-discovered address (net.h LOCAL_UPNP)
 REFRESH_S = 20 * 60  # AddPortMapping again every 20 minutes, as the reference
 _SOAP_ENV = ("<?xml version=\"1.0\"?><s:Envelope xmlns:s=\"http://schemas.xmlsoap.org/soap/envelope/\" "
@@ -80,6 +82,13 @@ def discover(timeout: float = 2.0, target: tuple[str, int] | None = None) -> lis
     return found
 
 
+def _bounded(resp) -> bytes:
+    data = resp.read(MAX_XML + 1)
+    if len(data) > MAX_XML:
+        raise UPnPError(f"reply larger than {MAX_XML} bytes")
+    return data
+
+
 def _local(tag: str) -> str:
     return tag.rsplit("}", 1)[-1]
 
@@ -87,7 +96,7 @@ def _local(tag: str) -> str:
 def describe(location: str, timeout: float = 5.0) -> tuple[str, str, str]:
     """UPNP_GetValidIGD for one device: (control URL, service type, LAN address of this host)."""
     with urllib.request.urlopen(location, timeout=timeout) as r:
-        root = ET.fromstring(r.read())
+        root = ET.fromstring(_bounded(r))
     base = next((e.text for e in root.iter() if _local(e.tag) == "URLBase" and e.text), location)
     services = [e for e in root.iter() if _local(e.tag) == "service"]
     for want in WAN_SERVICES:
@@ -110,10 +119,10 @@ def soap(control: str, service: str, action: str, args: dict | None = None, time
         "Content-Type": "text/xml; charset=\"utf-8\"", "SOAPAction": f"\"{service}#{action}\""})
     try:
         with urllib.request.urlopen(req, timeout=timeout) as r:
-            root = ET.fromstring(r.read())
+            root = ET.fromstring(_bounded(r))
     except urllib.error.HTTPError as e:
         try:
-            root = ET.fromstring(e.read())
+            root = ET.fromstring(_bounded(e))
         except ET.ParseError:
             raise UPnPError(f"{action}: HTTP {e.code}", e.code) from e
         code = next((el.text for el in root.iter() if _local(el.tag) == "errorCode"), None)
@@ -157,7 +166,7 @@ class PortMapper:
                 try:
                     self.control, self.service, self.lan = describe(loc)
                     break
-                except (UPnPError, OSError, ET.ParseError) as e:
+                except (UPnPError, OSError, ET.ParseError, ValueError) as e:
                     log.log_printf(f"UPnP: {loc}: {e}")
             if self.control is None:
                 log.log_printf("No valid UPnP IGDs found")
