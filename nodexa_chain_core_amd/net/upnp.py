@@ -24,6 +24,7 @@ import urllib.error
 import urllib.parse
 import urllib.request
 import xml.etree.ElementTree as ET
+from xml.sax.saxutils import escape
 
 from ..utils import log
 
@@ -113,7 +114,7 @@ def describe(location: str, timeout: float = 5.0) -> tuple[str, str, str]:
 
 def soap(control: str, service: str, action: str, args: dict | None = None, timeout: float = 5.0) -> dict:
     """One SOAP action; the response's out-arguments, or UPnPError with the device's errorCode."""
-    inner = "".join(f"<{k}>{v}</{k}>" for k, v in (args or {}).items())
+    inner = "".join(f"<{k}>{escape(str(v))}</{k}>" for k, v in (args or {}).items())
     body = _SOAP_ENV.format(body=f"<u:{action} xmlns:u=\"{service}\">{inner}</u:{action}>").encode()
     req = urllib.request.Request(control, data=body, method="POST", headers={
         "Content-Type": "text/xml; charset=\"utf-8\"", "SOAPAction": f"\"{service}#{action}\""})
