@@ -150,7 +150,7 @@ void fuzz_der(const Bytes& in) {
 extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     if (size == 0) return 0;
     const Bytes in(data + 1, data + size);
-    switch (data[0] % 14) {
+    switch (data[0] % 15) {
     case 0: fuzz_block(in, kKawpowAlways); break;
     case 1: fuzz_block(in, kKawpowNever); break;
     case 2: fuzz_header(in, kKawpowAlways); break;
@@ -186,6 +186,33 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
         try {
             (void)bdb::read_btree_bytes(std::string(in.begin(), in.end()), in.size() & 1 ? "main" : "");
         } catch (const std::runtime_error&) {
+        }
+        break;
+    }
+    case 14: {
+        // the btree writer (wallet.dat export): records cut from the input (1-byte key length,
+        // 2-byte value length) at a page size from the first byte, written and read back exactly
+        bdb::Records recs;
+        std::map<std::string, std::string> want;
+        size_t at = 1;
+        while (at + 3 <= in.size()) {
+            const size_t kl = 1 + in[at] % 64, vl = (size_t(in[at + 1]) << 8 | in[at + 2]) % 6000;
+            at += 3;
+            if (at + kl + vl > in.size()) break;
+            std::string k(reinterpret_cast<const char*>(in.data() + at), kl);
+            std::string v(reinterpret_cast<const char*>(in.data() + at + kl), vl);
+            at += kl + vl;
+            if (want.emplace(k, v).second) recs.emplace_back(k, v);
+        }
+        if (in.empty()) break;
+        const uint32_t ps = 512u << (in[0] % 4);  // 512 .. 4096
+        const std::string file = bdb::write_btree_bytes(recs, "main", ps, std::string(20, '\x5a'));
+        const bdb::Records back = bdb::read_btree_bytes(file, "main");
+        if (back.size() != want.size()) __builtin_trap();
+        size_t i = 0;
+        for (const auto& kv : want) {
+            if (back[i].first != kv.first || back[i].second != kv.second) __builtin_trap();
+            ++i;
         }
         break;
     }

@@ -1,0 +1,129 @@
+// Issue rate of the VALU instructions the KawPow round is made of, on one MI355X (gfx950).
+//
+// Each thread runs 8 independent chains of one instruction (inline asm, so the compiler can
+// neither fuse nor drop it) for ITER iterations; 8 waves per SIMD keep the issue port busy. The
+// printed figure is cycles per wave64 instruction per SIMD at the clock the kernel ran at
+// (s_memtime deltas), so 4.0 = one wave64 op every 4 cycles ("full rate" on a 16-lane SIMD).
+//
+//   hipcc --offload-arch=gfx950 -O3 -o tools/bin/valu_rates tools/valu_rates.hip && tools/bin/valu_rates
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                                           \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+
+constexpr int ITER = 4096;
+constexpr int BLOCK = 512;  // 8 waves: 2 per SIMD per workgroup
+
+#define OP2(name, ins)                                                                      \
+    struct name {                                                                           \
+        static constexpr const char* tag = ins;                                             \
+        __device__ static void run(uint32_t& a, uint32_t b) { asm volatile(ins " %0, %0, %1" : "+v"(a) : "v"(b)); } \
+    };
+#define OP3(name, ins)                                                                      \
+    struct name {                                                                           \
+        static constexpr const char* tag = ins;                                             \
+        __device__ static void run(uint32_t& a, uint32_t b) {                               \
+            asm volatile(ins " %0, %0, %1, %0" : "+v"(a) : "v"(b));                         \
+        }                                                                                   \
+    };
+
+OP2(Add, "v_add_u32")
+OP2(Xor, "v_xor_b32")
+OP2(MulLo, "v_mul_lo_u32")
+OP2(MulHi, "v_mul_hi_u32")
+OP2(Mul24, "v_mul_u32_u24")
+OP2(MulHi24, "v_mul_hi_u32_u24")
+OP2(Min, "v_min_u32")
+OP3(Alignbit, "v_alignbit_b32")
+OP3(LshlAdd, "v_lshl_add_u32")
+OP3(Xad, "v_xad_u32")
+OP3(Mad24, "v_mad_u32_u24")
+
+struct MadU64 {
+    static constexpr const char* tag = "v_mad_u64_u32";
+    __device__ static void run(uint32_t& a, uint32_t b) {
+        uint64_t r;
+        asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b) : "vcc");
+        a = (uint32_t)r ^ (uint32_t)(r >> 32);
+    }
+};
+
+template <class Op>
+__global__ __launch_bounds__(BLOCK) void bench(uint32_t* out, uint64_t* cycles, uint32_t seed) {
+    uint32_t a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = seed + threadIdx.x * 8 + k;
+    const uint32_t b = seed | 1u;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+    for (int i = 0; i < ITER; ++i) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) Op::run(a[k], b);
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x ^= a[k];
+    out[blockIdx.x * BLOCK + threadIdx.x] = x;
+    if (threadIdx.x == 0) cycles[blockIdx.x] = t1 - t0;
+}
+
+template <class Op>
+static void run(uint32_t* out, uint64_t* cyc, int blocks) {
+    bench<Op><<<blocks, BLOCK>>>(out, cyc, 7);  // warm
+    CHECK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    CHECK(hipEventRecord(e0));
+    bench<Op><<<blocks, BLOCK>>>(out, cyc, 9);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    // wave64 instructions issued per SIMD: blocks x 8 waves x ITER x 8 over (CUs x 4 SIMDs)
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    int khz = 0;
+    CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, 0));
+    const double per_simd = double(blocks) * (BLOCK / 64) * ITER * 8 / (double(cus) * 4);
+    const double cycles_at_max = ms * 1e-3 * khz * 1e3;
+    std::printf("{\"op\":\"%s\",\"ms\":%.3f,\"cycles_per_wave_op_at_max_clock\":%.2f}\n", Op::tag, ms,
+                cycles_at_max / per_simd);
+    std::fflush(stdout);
+}
+
+int main() {
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int blocks = cus * 4;  // 4 workgroups of 8 waves per CU: 8 waves per SIMD
+    uint32_t* out = nullptr;
+    uint64_t* cyc = nullptr;
+    CHECK(hipMalloc(&out, size_t(blocks) * BLOCK * 4));
+    CHECK(hipMalloc(&cyc, size_t(blocks) * 8));
+    run<Add>(out, cyc, blocks);
+    run<Xor>(out, cyc, blocks);
+    run<Min>(out, cyc, blocks);
+    run<Alignbit>(out, cyc, blocks);
+    run<LshlAdd>(out, cyc, blocks);
+    run<Xad>(out, cyc, blocks);
+    run<Mul24>(out, cyc, blocks);
+    run<Mad24>(out, cyc, blocks);
+    run<MulHi24>(out, cyc, blocks);
+    run<MulLo>(out, cyc, blocks);
+    run<MulHi>(out, cyc, blocks);
+    run<MadU64>(out, cyc, blocks);
+    CHECK(hipFree(out));
+    CHECK(hipFree(cyc));
+    return 0;
+}
