@@ -98,8 +98,15 @@ static void run(uint32_t* out, uint64_t* cyc, int blocks) {
     CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeClockRate, 0));
     const double per_simd = double(blocks) * (BLOCK / 64) * ITER * 8 / (double(cus) * 4);
     const double cycles_at_max = ms * 1e-3 * khz * 1e3;
-    std::printf("{\"op\":\"%s\",\"ms\":%.3f,\"cycles_per_wave_op_at_max_clock\":%.2f}\n", Op::tag, ms,
-                cycles_at_max / per_simd);
+    // the shader-clock cycles one workgroup measured itself (s_memtime): its 2 waves per SIMD
+    // interleave with the 6 of the other 3 workgroups on that SIMD, so SIMD cycles per wave op =
+    // elapsed / (8 waves x ITER x 8 ops)
+    uint64_t c0 = 0;
+    CHECK(hipMemcpy(&c0, cyc, 8, hipMemcpyDeviceToHost));
+    const double sclk_cycles = double(c0) / (8.0 * ITER * 8);
+    std::printf("{\"op\":\"%s\",\"ms\":%.3f,\"cycles_per_wave_op_at_max_clock\":%.2f,"
+                "\"cycles_per_wave_op_memtime\":%.2f,\"implied_mhz\":%.0f}\n", Op::tag, ms,
+                cycles_at_max / per_simd, sclk_cycles, double(c0) / (ms * 1e3));
     std::fflush(stdout);
 }
 
