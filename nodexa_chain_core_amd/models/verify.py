@@ -388,7 +388,9 @@ def _broadcast_verdict(world, r: dict | None) -> dict | None:
     from ..parallel import world as W
 
     pkt = None
-    if world.rank == 0 and r is None:  # rank 0 could not take the batch: every rank falls back
+    if world.rank == 0 and isinstance(r, BaseException):  # rank 0 failed: every rank raises
+        pkt = struct.pack("<Iii84s", 0xFFFFFFFE, -1, 0, repr(r).encode()[:84])
+    elif world.rank == 0 and r is None:  # rank 0 could not take the batch: every rank falls back
         pkt = struct.pack("<Iii84s", 0xFFFFFFFF, -1, 0, b"")
     elif world.rank == 0:
         rej = r["reject"] or {}
@@ -396,10 +398,14 @@ def _broadcast_verdict(world, r: dict | None) -> dict | None:
         pkt = struct.pack("<Iii84s", r["accepted"], rej.get("index", -1) if rej else -1, r.get("dos", 0), why)
     raw = W.broadcast_bytes(pkt, _VERDICT)
     if world.rank == 0:
+        if isinstance(r, BaseException):
+            raise r
         return r
     acc, idx, dos, why = struct.unpack("<Iii84s", raw)
     if acc == 0xFFFFFFFF:
         return None
+    if acc == 0xFFFFFFFE:
+        raise RuntimeError("batch verify failed on rank 0: " + why.rstrip(b"\0").decode(errors="replace"))
     why = why.rstrip(b"\0").decode()
     return {"accepted": acc, "reject": {"index": idx, "reason": why} if idx >= 0 else None, "dos": dos,
             "pow_s": 0.0, "context_s": 0.0, "dgw_gpu": True, "resident": True, "sharded": False,
@@ -419,7 +425,12 @@ def process_batch_resident(chain, batch, adjusted_time: int, device: int = 0, wo
     a smaller one is verified whole by rank 0 (which commits it to its chain) and the verdict is
     broadcast, so N GPUs never verify slower than one plus a 96-byte broadcast."""
     if world is not None and world.collective and world.world_size > 1 and len(batch) < shard_min_headers():
-        r = process_batch_resident(chain, batch, adjusted_time, device, None) if world.rank == 0 else None
+        r = None
+        if world.rank == 0:
+            try:
+                r = process_batch_resident(chain, batch, adjusted_time, device, None)
+            except Exception as e:  # noqa: BLE001 - the other ranks wait in the broadcast: tell them
+                r = e
         return _broadcast_verdict(world, r)
     from ..ops.header_batch import CODES
 

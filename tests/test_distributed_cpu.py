@@ -51,6 +51,11 @@ def _worker(rank, world, port, q):
         assert got["accepted"] == 9990 and got["reject"] == {"index": 9990, "reason": "high-hash"} and got["dos"] == 50
         got = _broadcast_verdict(w, {"accepted": 10000, "reject": None, "dos": 0} if rank == 0 else None)
         assert got["accepted"] == 10000 and got["reject"] is None
+        try:  # a failure on rank 0 reaches every rank instead of leaving them in the broadcast
+            _broadcast_verdict(w, ValueError("device lost") if rank == 0 else None)
+            raise AssertionError("no exception")
+        except (ValueError, RuntimeError) as e:
+            assert "device lost" in str(e)
         # 3. DAG shard all-gather: each rank fills its slice with golden 2048-bit items
         ctx = _core.get_epoch_context(0)
         per_items = 8
