@@ -10,6 +10,8 @@
 #include <stdexcept>
 #include <utility>
 
+#include <unistd.h>
+
 namespace nodexa {
 namespace bdb {
 namespace {
@@ -362,12 +364,15 @@ std::string write_btree_bytes(Records records, const std::string& subdb, uint32_
 void write_btree(const std::string& path, Records records, const std::string& subdb, uint32_t pagesize) {
     const std::string data = write_btree_bytes(std::move(records), subdb, pagesize);
     const std::string tmp = path + ".tmp";
-    {
-        std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
-        if (!f) throw std::runtime_error("cannot write " + tmp);
-        f.write(data.data(), std::streamsize(data.size()));
-        f.flush();
-        if (!f) throw std::runtime_error("short write to " + tmp);
+    // written in full and synced before it takes the name: a crash leaves the old file or the new one
+    std::FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + tmp);
+    const bool ok = std::fwrite(data.data(), 1, data.size(), f) == data.size() && std::fflush(f) == 0 &&
+                    ::fsync(::fileno(f)) == 0;
+    std::fclose(f);
+    if (!ok) {
+        std::remove(tmp.c_str());
+        throw std::runtime_error("short write to " + tmp);
     }
     if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("cannot rename " + tmp);
 }
