@@ -463,6 +463,7 @@ def _run_as_launcher(args) -> int:
     import signal
     import socket
     import subprocess
+    import threading
 
     n = args.gpus
     if args.device == "gpu" and os.environ.get("NODEXA_DIST_BACKEND", "nccl") == "nccl":
@@ -478,9 +479,12 @@ def _run_as_launcher(args) -> int:
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = str(s.getsockname()[1])
-    import threading
-
     procs, pumps = [], []
+
+    def on_term(signum, _frame):  # a launcher told to stop takes its ranks down with it
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_term)
 
     def pump(stream, rank):
         # the one JSON line comes from rank 0's stdout; everything else a rank writes there (gloo's
@@ -490,17 +494,17 @@ def _run_as_launcher(args) -> int:
             out.buffer.write(line)
             out.flush()
 
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                             stdout=subprocess.PIPE)
-        procs.append(p)
-        pumps.append(threading.Thread(target=pump, args=(p.stdout, r), daemon=True))
-        pumps[-1].start()
     rc = 0
     term_at = None
     try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+            p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                 stdout=subprocess.PIPE)
+            procs.append(p)
+            pumps.append(threading.Thread(target=pump, args=(p.stdout, r), daemon=True))
+            pumps[-1].start()
         pending = list(procs)
         while pending:
             for p in list(pending):

@@ -62,3 +62,34 @@ def test_bench_self_launch_propagates_rank_failure():
     r = subprocess.run([sys.executable] + args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_bench_self_launch_sigterm_takes_ranks_down():
+    """The launcher stopped with SIGTERM (a driver timeout) ends its rank processes too."""
+    import signal
+    import time
+
+    import psutil
+
+    args = ["bench.py", "--gpus", "2", "--device", "cpu", "--epoch", "0", "--steps", "100000", "--warmup", "1",
+            "--batch", "4", "--equihash", "0", "--verify", "0", "--quiet"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.Popen([sys.executable] + args, cwd=ROOT, env=env, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL)
+    try:
+        deadline = time.time() + 120
+        kids = []
+        while time.time() < deadline and len(kids) < 2:
+            kids = psutil.Process(p.pid).children()
+            time.sleep(0.2)
+        assert len(kids) == 2
+        time.sleep(2)
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) != 0
+        gone, alive = psutil.wait_procs(kids, timeout=60)
+        assert not alive
+    finally:
+        if p.poll() is None:
+            p.kill()
