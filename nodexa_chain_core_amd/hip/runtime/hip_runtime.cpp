@@ -240,8 +240,8 @@ PYBIND11_MODULE(_hip, m) {
         args.p.num_items = num_items;
         args.p.light_items = light_items;
         args.lmod = make_fastmod(light_items);
-        const unsigned block = 256;
-        const uint64_t grid = (num_items + block - 1) / block;
+        const unsigned block = 256;  // one item per lane quad (hip/kernels/ethash_dag.hip): 64 per workgroup
+        const uint64_t grid = (num_items + 63) / 64;
         if (grid == 0) return;
         if (grid > 0x7fffffffULL) throw std::invalid_argument("dag build launch too large; split it");
         k.launch_bytes(dim3(unsigned(grid)), dim3(block), 0, as_stream(stream), &args, sizeof(args));
