@@ -94,9 +94,18 @@ def _local(tag: str) -> str:
     return tag.rsplit("}", 1)[-1]
 
 
+def _http_url(url: str) -> str:
+    """A URL an SSDP answer or a device description handed us, refused unless it is plain http
+    (any LAN host can answer an M-SEARCH: no file:, ftp: or other scheme is ever opened)."""
+    u = urllib.parse.urlparse(url)
+    if u.scheme != "http" or not u.hostname:
+        raise UPnPError(f"refusing non-http UPnP URL {url[:120]!r}")
+    return url
+
+
 def describe(location: str, timeout: float = 5.0) -> tuple[str, str, str]:
     """UPNP_GetValidIGD for one device: (control URL, service type, LAN address of this host)."""
-    with urllib.request.urlopen(location, timeout=timeout) as r:
+    with urllib.request.urlopen(_http_url(location), timeout=timeout) as r:
         root = ET.fromstring(_bounded(r))
     base = next((e.text for e in root.iter() if _local(e.tag) == "URLBase" and e.text), location)
     services = [e for e in root.iter() if _local(e.tag) == "service"]
@@ -104,7 +113,7 @@ def describe(location: str, timeout: float = 5.0) -> tuple[str, str, str]:
         for svc in services:
             fields = {_local(c.tag): (c.text or "").strip() for c in svc}
             if fields.get("serviceType") == want and fields.get("controlURL"):
-                control = urllib.parse.urljoin(base, fields["controlURL"])
+                control = _http_url(urllib.parse.urljoin(base, fields["controlURL"]))
                 u = urllib.parse.urlparse(control)
                 with socket.create_connection((u.hostname, u.port or 80), timeout=timeout) as c:
                     lan = c.getsockname()[0]

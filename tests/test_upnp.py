@@ -181,3 +181,32 @@ def test_node_upnp_flag(core, tmp_path, igd):
     finally:
         n.stop()
     assert igd.actions[-1][0] == "DeletePortMapping"
+
+
+def test_non_http_locations_are_refused(tmp_path):
+    """Any LAN host can answer an M-SEARCH: a file: (or other non-http) LOCATION or controlURL is
+    never opened."""
+    from nodexa_chain_core_amd.net import upnp
+
+    f = tmp_path / "desc.xml"
+    f.write_text(DESC)
+    with pytest.raises(upnp.UPnPError, match="non-http"):
+        upnp.describe(f.as_uri())
+    g = FakeIGD()
+    try:
+        bad = DESC.replace("<controlURL>/ctl/IPConn</controlURL>", "<controlURL>file:///etc/passwd</controlURL>")
+        orig = g.http.RequestHandlerClass.do_GET
+
+        def do_get(self):
+            body = bad.encode()
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        g.http.RequestHandlerClass.do_GET = do_get
+        with pytest.raises(upnp.UPnPError, match="non-http"):
+            upnp.describe("http://127.0.0.1:%d/rootDesc.xml" % g.http.server_address[1])
+        g.http.RequestHandlerClass.do_GET = orig
+    finally:
+        g.close()
