@@ -119,11 +119,12 @@ def _grouped(jobs: np.ndarray, device):
     return dj, _programs(periods, device), len(periods), jp
 
 
-def _run_dag(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
+def _run_dag(ep: DeviceEpoch, jobs: np.ndarray):
     """Resident-DAG batch: one job per 16-lane group, headers of thousands of different periods in
     one dense launch. kawpow_verify_waves (jobs grouped by period four to a wave64, the program
     wave-uniform, the mix in VGPRs) unless the test hook header_batch.WAVES selects kawpow_verify_dag (each
-    group's program and mix in LDS)."""
+    group's program and mix in LDS). Like the other _run_*: issued on the current stream, returns
+    the call that waits for it and yields the (m, 64) rows."""
     from . import header_batch as HB
 
     m = len(jobs)
@@ -143,7 +144,7 @@ def _run_dag(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
             runtime.static_kernel("kawpow_verify_light", "kawpow_verify_dag"), ep.dag.data_ptr(), ep.items2048,
             ep.l1.data_ptr(), dj.data_ptr(), progs.data_ptr(), nprog, jp.data_ptr(), m, res.data_ptr(),
             runtime.current_stream_handle())
-    return res.cpu().numpy().view(np.uint8).reshape(m, 64)
+    return lambda: res.cpu().numpy().view(np.uint8).reshape(m, 64)
 
 
 def _run_dag_slabs(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
@@ -171,13 +172,17 @@ def _run_dag_slabs(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
         runtime.static_kernel("kawpow_verify", "kawpow_verify_batch"), ep.dag.data_ptr(), ep.items2048,
         dj.data_ptr(), progs.data_ptr(), slabs.data_ptr(), len(order), res.data_ptr(),
         runtime.current_stream_handle())
-    raw = res.cpu().numpy().view(np.uint8).reshape(len(order), 64)
-    out = np.empty((len(jobs), 64), dtype=np.uint8)
-    out[order[valid]] = raw[valid]
-    return out
+
+    def finish():
+        raw = res.cpu().numpy().view(np.uint8).reshape(len(order), 64)
+        out = np.empty((len(jobs), 64), dtype=np.uint8)
+        out[order[valid]] = raw[valid]
+        return out
+
+    return finish
 
 
-def _run_light(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
+def _run_light(ep: DeviceEpoch, jobs: np.ndarray):
     m = len(jobs)
     dj, progs, nprog, jp = _grouped(jobs, ep.device)
     res = torch.empty(m * 16, dtype=torch.int32, device=ep.device)
@@ -185,7 +190,7 @@ def _run_light(ep: DeviceEpoch, jobs: np.ndarray) -> np.ndarray:
         runtime.static_kernel("kawpow_verify_light", "kawpow_verify_light"), ep.light.data_ptr(),
         int(ep.ctx.light_items), ep.l1.data_ptr(), ep.items2048, dj.data_ptr(), progs.data_ptr(), nprog,
         jp.data_ptr(), m, res.data_ptr(), runtime.current_stream_handle())
-    return res.cpu().numpy().view(np.uint8).reshape(m, 64)
+    return lambda: res.cpu().numpy().view(np.uint8).reshape(m, 64)
 
 
 def gpu_hash_jobs(jobs: np.ndarray, device: int = 0, mode: str = "auto") -> np.ndarray:
@@ -199,19 +204,39 @@ def gpu_hash_jobs(jobs: np.ndarray, device: int = 0, mode: str = "auto") -> np.n
     jobs = np.asarray(jobs, dtype=np.uint8).reshape(-1, JOB.size)
     out = np.empty((len(jobs), 64), dtype=np.uint8)
     epochs = _block_numbers(jobs) // _core.EPOCH_LENGTH
-    for epoch in np.unique(epochs).tolist():
-        idx = np.flatnonzero(epochs == epoch)
-        m = mode
-        if m == "auto":
-            m = "dag" if is_resident(device, epoch) or len(idx) > LIGHT_MAX_JOBS else "light"
-        with torch.cuda.device(device):
-            if m == "dag":
-                out[idx] = _run_dag(_device_epoch(epoch, device), jobs[idx])
-            elif m == "dag-slab":
-                out[idx] = _run_dag_slabs(_device_epoch(epoch, device), jobs[idx])
-            else:
-                out[idx] = _run_light(_light_epoch(epoch, device), jobs[idx])
+    # every epoch group is issued before any is waited for, each on a stream of its own: a launch
+    # is bound by its jobs' 64 dependent rounds (light: 64 x 512 dependent light-cache reads,
+    # ~14 ms at any batch size the GPU holds), so the groups of a batch that spans an epoch
+    # boundary run side by side instead of one after the other
+    pending = []
+    with torch.cuda.device(device):
+        for k, epoch in enumerate(np.unique(epochs).tolist()):
+            idx = np.flatnonzero(epochs == epoch)
+            m = mode
+            if m == "auto":
+                m = "dag" if is_resident(device, epoch) or len(idx) > LIGHT_MAX_JOBS else "light"
+            ep = _light_epoch(epoch, device) if m == "light" else _device_epoch(epoch, device)
+            s = _side_stream(device, k)
+            s.wait_stream(torch.cuda.current_stream(device))  # the epoch's uploads / build
+            with torch.cuda.stream(s):
+                run = _run_dag if m == "dag" else _run_dag_slabs if m == "dag-slab" else _run_light
+                pending.append((idx, s, run(ep, jobs[idx])))
+        for idx, s, finish in pending:
+            with torch.cuda.stream(s):  # the read-back queues behind its own launch
+                out[idx] = finish()
     return out
+
+
+_streams: dict[tuple[int, int], torch.cuda.Stream] = {}
+
+
+def _side_stream(device: int, k: int) -> torch.cuda.Stream:
+    """The k-th (mod 4) verify stream of `device`, made once: epoch groups of one batch."""
+    key = (device, k % 4)
+    s = _streams.get(key)
+    if s is None:
+        s = _streams[key] = torch.cuda.Stream(device=device)
+    return s
 
 
 def gpu_full_hash(block_numbers: list[int], header_hashes: list[bytes], nonces: list[int],
