@@ -230,6 +230,7 @@ class ResidentHeaderVerifier:
         # every epoch DAG of the plan resolved (built or pinned in the LRU) before the first launch:
         # a build inside the issue loop could evict a DAG a side-stream range is still reading
         epochs_dev = {}
+        V.prefetch_contexts({e for e, lo, hi in plan["ranges"] if max(lo, lo_r) < min(hi, hi_r)}, self.device)
         for epoch, lo, hi in plan["ranges"]:
             if max(lo, lo_r) < min(hi, hi_r) and epoch not in epochs_dev:
                 epochs_dev[epoch] = V._device_epoch(epoch, self.device)

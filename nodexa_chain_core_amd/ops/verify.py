@@ -71,6 +71,21 @@ def share_epoch(device: int, epoch: int, e: DeviceEpoch) -> None:
         _epochs.setdefault((device, epoch), e)
 
 
+def prefetch_contexts(epochs, device: int) -> None:
+    """Build the host epoch contexts (light caches: a serial keccak chain per epoch, ~0.5 s at
+    epoch 0 and ~2 s at 384 on one core) of the batch's epochs that this device has neither as a
+    resident DAG nor as a light epoch, in parallel threads (the native build releases the GIL), so
+    a batch that crosses an epoch boundary pays for one build, not two in a row. The native LRU
+    (csrc/pow/ethash.cpp get_epoch_context) then hands them to DeviceEpoch."""
+    with _epochs_lock:
+        need = [int(e) for e in epochs if (device, int(e)) not in _epochs and (device, int(e)) not in _light]
+    if len(need) > 1:
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(min(len(need), 4)) as ex:
+            list(ex.map(_core.get_epoch_context, need[:4]))
+
+
 def _light_epoch(epoch: int, device: int) -> DeviceEpoch:
     key = (device, epoch)
     e = _light.get(key)
@@ -209,6 +224,7 @@ def gpu_hash_jobs(jobs: np.ndarray, device: int = 0, mode: str = "auto") -> np.n
     # ~14 ms at any batch size the GPU holds), so the groups of a batch that spans an epoch
     # boundary run side by side instead of one after the other
     pending = []
+    prefetch_contexts(np.unique(epochs).tolist(), device)
     with torch.cuda.device(device):
         for k, epoch in enumerate(np.unique(epochs).tolist()):
             idx = np.flatnonzero(epochs == epoch)

@@ -134,3 +134,17 @@ def test_search_variant_selection_by_dag_size(core):
     assert jit.defines_for(above, ("KP_SBUFFER", "KP_DPP")) == ("KP_PTR64", "KP_DPP")
 
 
+
+
+def test_prefetch_contexts_builds_in_parallel(core):
+    """ops/verify.prefetch_contexts: the light caches of a batch's new epochs are built side by
+    side (the native build releases the GIL) and land in the native LRU the verify paths read."""
+    import time
+
+    from nodexa_chain_core_amd.ops import verify as V
+
+    V.prefetch_contexts([7, 8], device=0)
+    t = time.perf_counter()
+    a, b = core.get_epoch_context(7), core.get_epoch_context(8)
+    assert time.perf_counter() - t < 0.2  # LRU hits, not two ~1 s builds
+    assert a.light_items > 0 and b.light_items > a.light_items
