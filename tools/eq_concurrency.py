@@ -2,7 +2,8 @@
 """Equihash(200,9) end-to-end Sol/s (wall clock, host verification included, as bench.py times
 it) for instances per batch, workgroups per instance and the number of solvers driven round-robin
 on separate HIP streams from one process (two ranks sharing one GPU measured 4025 Sol/s against
-3657 for one: profiles/r3za_two_rank_rehearsal).
+3657 for one: profiles/r3za_two_rank_rehearsal; 3929 against 3682 in r6u). Solutions are checked
+on the device by default, as the mining loop does.
 
     python tools/eq_concurrency.py --configs 8:32:1 16:32:1 8:32:2
 """
@@ -25,6 +26,9 @@ def main() -> int:
                     help="inst:groups:solvers")
     ap.add_argument("--solves", type=int, default=192, help="solves per config (per measurement)")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--verify", choices=("device", "host"), default="device",
+                    help="device: the eq_verify_slots verdicts (the mining loop's path); host: the C++ "
+                         "verifier as well (~225 us per solution on one core: host-bound)")
     a = ap.parse_args()
 
     import torch
@@ -39,7 +43,8 @@ def main() -> int:
         mk = lambda s, i, j: base + struct.pack("<I", (tag << 24) ^ (s << 20) ^ (i << 8) ^ j)  # noqa: E731
         for s, (sv, st) in enumerate(zip(solvers, streams)):  # warm-up
             with torch.cuda.stream(st):
-                sv.solve([mk(s, 255, j) for j in range(inst)])
+                sv.launch([mk(s, 255, j) for j in range(inst)])
+                sv.collect_arrays(verify=a.verify)
         torch.cuda.synchronize()
         batches = max(2, a.solves // (inst * nsolv))
         found = 0
@@ -49,9 +54,9 @@ def main() -> int:
                 with torch.cuda.stream(st):
                     sv.launch([mk(s, i, j) for j in range(inst)])
                 if i >= 1:
-                    found += sum(len(x) for x in sv.collect())
+                    found += sum(len(x) for x in sv.collect_arrays(verify=a.verify))
         for sv in solvers:
-            found += sum(len(x) for x in sv.collect())
+            found += sum(len(x) for x in sv.collect_arrays(verify=a.verify))
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         solves = batches * inst * nsolv
