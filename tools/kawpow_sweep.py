@@ -27,6 +27,9 @@ def main() -> int:
     ap.add_argument("--out", default=None)
     ap.add_argument("--check-windows", type=int, default=4, help="nonce windows re-hashed per variant")
     ap.add_argument("--raw", action="store_true", help="compile the variants as given (no jit.defines_for)")
+    ap.add_argument("--objects", nargs="*", default=[],
+                    help="name=path: prebuilt code objects of the same period timed as extra variants "
+                         "(e.g. tools/kawpow_e64.py output)")
     a = ap.parse_args()
 
     import torch
@@ -57,6 +60,10 @@ def main() -> int:
     dag_bytes = _core.full_dataset_num_items(a.epoch) * 128
     variants = list(dict.fromkeys(parse(v) if a.raw else jit.defines_for(dag_bytes, parse(v)) for v in a.variants))
     paths = {v: jit.get(period, v) for v in variants}
+    for spec in a.objects:  # prebuilt objects: keyed ("obj:<name>",)
+        name, _, path = spec.partition("=")
+        variants.append(("obj:" + name,))
+        paths[variants[-1]] = os.path.abspath(path)
     torch.cuda.set_device(0)
     ep = DeviceEpoch(a.epoch, device=0)
     ep.build()

@@ -2,10 +2,13 @@
 //
 // Each thread runs 8 independent chains of one instruction (inline asm, so the compiler can
 // neither fuse nor drop it) for ITER iterations; 8 waves per SIMD keep the issue port busy. The
-// printed figure is cycles per wave64 instruction per SIMD at the clock the kernel ran at
-// (s_memtime deltas), so 4.0 = one wave64 op every 4 cycles ("full rate" on a 16-lane SIMD).
+// printed cycles assume the 2.4 GHz maximum clock (s_memtime does not tick with the shader clock);
+// the exact figure is taken under counters: SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs)
+// = wave64 VALU instructions issued per CU per cycle (profiles/r6t_valu_issue: 0.89-0.90 for
+// most ops, 1.17 for v_add / v_xor).
 //
-//   hipcc --offload-arch=gfx950 -O3 -o tools/bin/valu_rates tools/valu_rates.hip && tools/bin/valu_rates
+//   hipcc --offload-arch=gfx950 -O3 -o tools/bin/valu_rates tools/valu_rates.hip
+//   rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- tools/bin/valu_rates
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -48,6 +51,56 @@ OP3(Alignbit, "v_alignbit_b32")
 OP3(LshlAdd, "v_lshl_add_u32")
 OP3(Xad, "v_xad_u32")
 OP3(Mad24, "v_mad_u32_u24")
+OP2(And, "v_and_b32")
+OP2(Or, "v_or_b32")
+OP2(Sub, "v_sub_u32")
+OP2(Lshl, "v_lshlrev_b32")
+OP2(Lshr, "v_lshrrev_b32")
+OP2(Max, "v_max_u32")
+OP3(Add3, "v_add3_u32")
+OP3(Or3, "v_or3_b32")
+OP3(LshlOr, "v_lshl_or_b32")
+OP3(AndOr, "v_and_or_b32")
+OP3(Perm, "v_perm_b32")
+OP3(Bfi, "v_bfi_b32")
+OP2(AddE64, "v_add_u32_e64")
+OP2(XorE64, "v_xor_b32_e64")
+OP2(AndE64, "v_and_b32_e64")
+OP2(SubE64, "v_sub_u32_e64")
+OP2(MinE64, "v_min_u32_e64")
+OP2(Mul24E64, "v_mul_u32_u24_e64")
+OP2(LshlE64, "v_lshlrev_b32_e64")
+struct Bitop3b {
+    static constexpr const char* tag = "v_bitop3_b32 (0x6c)";
+    __device__ static void run(uint32_t& a, uint32_t b) { asm volatile("v_bitop3_b32 %0, %0, %1, %0 bitop3:0x6c" : "+v"(a) : "v"(b)); }
+};
+struct AlignbitImm {
+    static constexpr const char* tag = "v_alignbit_b32 (rotate by an inline constant)";
+    __device__ static void run(uint32_t& a, uint32_t) { asm volatile("v_alignbit_b32 %0, %0, %0, 13" : "+v"(a)); }
+};
+struct AddSgpr {
+    static constexpr const char* tag = "v_add_u32 (SGPR operand)";
+    __device__ static void run(uint32_t& a, uint32_t b) { asm volatile("v_add_u32 %0, %1, %0" : "+v"(a) : "s"(b)); }
+};
+
+struct Bitop3 {
+    static constexpr const char* tag = "v_bitop3_b32 (0x96: 3-way xor)";
+    __device__ static void run(uint32_t& a, uint32_t b) { asm volatile("v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96" : "+v"(a) : "v"(b)); }
+};
+struct Bcnt {
+    static constexpr const char* tag = "v_bcnt_u32_b32";
+    __device__ static void run(uint32_t& a, uint32_t b) { asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(a) : "v"(b)); }
+};
+struct Ffbh {
+    static constexpr const char* tag = "v_ffbh_u32";
+    __device__ static void run(uint32_t& a, uint32_t) { asm volatile("v_ffbh_u32 %0, %0" : "+v"(a)); }
+};
+struct MovDpp {
+    static constexpr const char* tag = "v_mov_b32_dpp row_newbcast:1";
+    __device__ static void run(uint32_t& a, uint32_t) {
+        asm volatile("s_nop 1\n v_mov_b32_dpp %0, %0 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(a));
+    }
+};
 
 struct MadU64 {
     static constexpr const char* tag = "v_mad_u64_u32";
@@ -130,6 +183,33 @@ int main() {
     run<MulLo>(out, cyc, blocks);
     run<MulHi>(out, cyc, blocks);
     run<MadU64>(out, cyc, blocks);
+    run<And>(out, cyc, blocks);
+    run<Or>(out, cyc, blocks);
+    run<Sub>(out, cyc, blocks);
+    run<Lshl>(out, cyc, blocks);
+    run<Lshr>(out, cyc, blocks);
+    run<Max>(out, cyc, blocks);
+    run<Add3>(out, cyc, blocks);
+    run<Or3>(out, cyc, blocks);
+    run<LshlOr>(out, cyc, blocks);
+    run<AndOr>(out, cyc, blocks);
+    run<Perm>(out, cyc, blocks);
+    run<Bfi>(out, cyc, blocks);
+    run<AddE64>(out, cyc, blocks);
+    run<XorE64>(out, cyc, blocks);
+    run<AndE64>(out, cyc, blocks);
+    run<SubE64>(out, cyc, blocks);
+    run<MinE64>(out, cyc, blocks);
+    run<Mul24E64>(out, cyc, blocks);
+    run<LshlE64>(out, cyc, blocks);
+    run<Bitop3b>(out, cyc, blocks);
+    run<AlignbitImm>(out, cyc, blocks);
+    run<AddSgpr>(out, cyc, blocks);
+    run<Add>(out, cyc, blocks);
+    run<Bitop3>(out, cyc, blocks);
+    run<Bcnt>(out, cyc, blocks);
+    run<Ffbh>(out, cyc, blocks);
+    run<MovDpp>(out, cyc, blocks);
     CHECK(hipFree(out));
     CHECK(hipFree(cyc));
     return 0;
