@@ -223,23 +223,32 @@ def gpu_hash_jobs(jobs: np.ndarray, device: int = 0, mode: str = "auto") -> np.n
     # is bound by its jobs' 64 dependent rounds (light: 64 x 512 dependent light-cache reads,
     # ~14 ms at any batch size the GPU holds), so the groups of a batch that spans an epoch
     # boundary run side by side instead of one after the other
-    pending = []
-    prefetch_contexts(np.unique(epochs).tolist(), device)
+    groups = np.unique(epochs).tolist()
+    prefetch_contexts(groups, device)
     with torch.cuda.device(device):
-        for k, epoch in enumerate(np.unique(epochs).tolist()):
-            idx = np.flatnonzero(epochs == epoch)
-            m = mode
-            if m == "auto":
-                m = "dag" if is_resident(device, epoch) or len(idx) > LIGHT_MAX_JOBS else "light"
-            ep = _light_epoch(epoch, device) if m == "light" else _device_epoch(epoch, device)
-            s = _side_stream(device, k)
-            s.wait_stream(torch.cuda.current_stream(device))  # the epoch's uploads / build
-            with torch.cuda.stream(s):
-                run = _run_dag if m == "dag" else _run_dag_slabs if m == "dag-slab" else _run_light
-                pending.append((idx, s, run(ep, jobs[idx])))
-        for idx, s, finish in pending:
-            with torch.cuda.stream(s):  # the read-back queues behind its own launch
-                out[idx] = finish()
+        # at most MAX_RESIDENT_DAGS groups in flight: every epoch of a wave is resolved (DAG built
+        # or light cache uploaded) before its first launch and held until its read-back, so the
+        # LRUs can never evict, and the allocator never reuse, a DAG or light cache that a launch
+        # still in flight reads
+        for lo in range(0, len(groups), MAX_RESIDENT_DAGS):
+            wave = []
+            for epoch in groups[lo:lo + MAX_RESIDENT_DAGS]:
+                idx = np.flatnonzero(epochs == epoch)
+                m = mode
+                if m == "auto":
+                    m = "dag" if is_resident(device, epoch) or len(idx) > LIGHT_MAX_JOBS else "light"
+                wave.append((idx, m, _light_epoch(epoch, device) if m == "light" else _device_epoch(epoch, device)))
+            pending = []
+            for k, (idx, m, ep) in enumerate(wave):
+                s = _side_stream(device, k)
+                s.wait_stream(torch.cuda.current_stream(device))  # the epoch's uploads / build
+                with torch.cuda.stream(s):
+                    run = _run_dag if m == "dag" else _run_dag_slabs if m == "dag-slab" else _run_light
+                    pending.append((idx, s, run(ep, jobs[idx])))
+            for idx, s, finish in pending:
+                with torch.cuda.stream(s):  # the read-back queues behind its own launch
+                    out[idx] = finish()
+            del wave, pending
     return out
 
 

@@ -52,6 +52,23 @@ def test_verify_light_other_epoch_and_mixed_batch(core, gpu):
     assert res[-1] == core.kawpow_hash(ctx4, blocks[-1], headers[-1], nonces[-1])
 
 
+def test_verify_light_batch_over_five_epochs(core, gpu):
+    """One light batch over epochs 0-4: more epoch groups than the in-flight limit
+    (ops/verify.MAX_RESIDENT_DAGS), so the groups run in two waves on the side streams; every row
+    matches the host golden model."""
+    from nodexa_chain_core_amd.ops.verify import MAX_RESIDENT_DAGS, gpu_full_hash
+
+    rng = random.Random(11)
+    blocks = [e * 7500 + rng.randrange(0, 7500) for e in range(5) for _ in range(6)]
+    rng.shuffle(blocks)
+    assert len({b // 7500 for b in blocks}) > MAX_RESIDENT_DAGS
+    headers = [rng.randbytes(32) for _ in blocks]
+    nonces = [rng.getrandbits(64) for _ in blocks]
+    res = gpu_full_hash(blocks, headers, nonces, device=0, mode="light")
+    for i, b in enumerate(blocks):
+        assert res[i] == core.kawpow_hash(core.get_epoch_context(b // 7500), b, headers[i], nonces[i]), i
+
+
 def test_node_gpu_mining_and_batch_verify(core, gpu, tmp_path):
     from nodexa_chain_core_amd.models.verify import verify_headers
     from nodexa_chain_core_amd.node import Node
