@@ -32,11 +32,11 @@ def _sharded_rows(jobs: np.ndarray, mode: str) -> np.ndarray:
         local = gpu_hash_jobs(mine, device=w.device.index, mode=mode) if len(mine) else np.zeros((0, 64), np.uint8)
     else:
         local = _cpu_rows(mine, 0) if len(mine) else np.zeros((0, 64), np.uint8)
+    if not w.collective:  # one rank: its rows are the batch's, no round trip through the device
+        return np.ascontiguousarray(local)[:m]
     buf = torch.zeros((per, 64), dtype=torch.uint8, device=w.device)
     if len(local):
         buf[:len(local)] = torch.from_numpy(np.ascontiguousarray(local)).to(w.device)
-    if not w.collective:
-        return buf.cpu().numpy()[:m]
     out = torch.empty((per * w.world_size, 64), dtype=torch.uint8, device=w.device)
     dist.all_gather_into_tensor(out, buf, group=w.group)
     return out.cpu().numpy()[:m]
