@@ -50,7 +50,8 @@ def main() -> int:
     ap.add_argument("--compile-only", action="store_true")
     ap.add_argument("--engines", nargs="*", default=["ps"], help="ps[:groups[:block[:final_groups]]]")
     a = ap.parse_args()
-    variants = [tuple(x for x in v.split(",") if x) for v in a.variants]
+    # a variant that starts with "-" (an "-mllvm:..." backend option) is passed with a leading space
+    variants = [tuple(x.strip() for x in v.split(",") if x.strip()) for v in a.variants]
     kinds = sorted({e.split(":")[0] for e in a.engines})
     objs = {(k, v): variant_object(v, SOURCES[k]) for k in kinds for v in variants}
     if a.compile_only:
